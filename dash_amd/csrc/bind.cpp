@@ -1,0 +1,271 @@
+// Python bindings of the native core (pybind11).
+#include <pybind11/numpy.h>
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include "layers.h"
+
+namespace py = pybind11;
+using namespace dash;
+
+namespace dash {
+void register_hip_bindings(py::module_& m);  // runtime_hip.cpp / runtime_stub.cpp
+}
+
+namespace {
+
+u128 py_to_u128(py::int_ v) {
+    py::int_ mask64 = py::int_(0xFFFFFFFFFFFFFFFFull);
+    py::object lo = v & mask64;
+    py::object hi = (v >> py::int_(64)) & mask64;
+    return (static_cast<u128>(hi.cast<uint64_t>()) << 64) | lo.cast<uint64_t>();
+}
+py::int_ u128_to_py(u128 x) {
+    py::int_ hi(static_cast<uint64_t>(x >> 64)), lo(static_cast<uint64_t>(x));
+    return py::int_((hi << py::int_(64)) | lo);
+}
+
+Params to_params(const py::dict& d) {
+    Params p;
+    for (auto item : d) {
+        std::string key = py::str(item.first);
+        py::object v = py::reinterpret_borrow<py::object>(item.second);
+        py::array_t<i64, py::array::c_style | py::array::forcecast> a = py::array_t<i64, py::array::c_style | py::array::forcecast>::ensure(v);
+        if (!a) {
+            a = py::array_t<i64, py::array::c_style | py::array::forcecast>(py::array(py::make_tuple(v)));
+        }
+        std::vector<i64> vec(a.data(), a.data() + a.size());
+        p[key] = std::move(vec);
+    }
+    return p;
+}
+
+py::dict from_params(const Params& p) {
+    py::dict d;
+    for (const auto& kv : p) d[py::str(kv.first)] = py::cast(kv.second);
+    return d;
+}
+
+py::array array_view(const Array& a, py::object owner) {
+    std::vector<py::ssize_t> shape(a.shape.begin(), a.shape.end());
+    switch (a.dtype) {
+        case DType::i16: return py::array_t<int16_t>(shape, a.ptr<int16_t>(), owner);
+        case DType::i32: return py::array_t<int32_t>(shape, a.ptr<int32_t>(), owner);
+        case DType::i64: return py::array_t<int64_t>(shape, a.ptr<int64_t>(), owner);
+        case DType::u8: return py::array_t<uint8_t>(shape, a.ptr<uint8_t>(), owner);
+        case DType::u128: {
+            shape.push_back(2);
+            return py::array_t<uint64_t>(shape, a.ptr<uint64_t>(), owner);
+        }
+    }
+    return py::none();
+}
+
+py::list labels_to_py(const CrtLabels& L) {
+    py::list out;
+    for (const auto& x : L) {
+        py::array_t<int16_t> arr({static_cast<py::ssize_t>(x.N), static_cast<py::ssize_t>(x.n)});
+        std::memcpy(arr.mutable_data(), x.c.data(), x.c.size() * sizeof(comp_t));
+        out.append(py::make_tuple(x.p, arr));
+    }
+    return out;
+}
+
+CrtLabels labels_from_py(const py::list& l) {
+    CrtLabels out;
+    for (auto item : l) {
+        py::tuple t = item.cast<py::tuple>();
+        int p = t[0].cast<int>();
+        auto arr = py::array_t<int16_t, py::array::c_style | py::array::forcecast>::ensure(t[1]);
+        DASH_CHECK(arr && arr.ndim() == 2, "labels must be (N, n) int16 arrays");
+        Labels L(p, arr.shape(0));
+        DASH_CHECK(arr.shape(1) == L.n, "label width does not match modulus");
+        std::memcpy(L.c.data(), arr.data(), L.c.size() * sizeof(comp_t));
+        out.push_back(std::move(L));
+    }
+    return out;
+}
+
+std::vector<LayerSpec> specs_from_py(const py::list& l) {
+    std::vector<LayerSpec> out;
+    for (auto item : l) {
+        py::tuple t = item.cast<py::tuple>();
+        LayerSpec s;
+        s.kind = t[0].cast<int>();
+        s.p = to_params(t[1].cast<py::dict>());
+        out.push_back(std::move(s));
+    }
+    return out;
+}
+
+class IntegrityError : public std::exception {};
+
+}  // namespace
+
+PYBIND11_MODULE(_dash_native, m) {
+    m.doc() = "dash_amd native core: labels, AES, garbler, host evaluator, HIP runtime";
+    static py::exception<std::runtime_error> integrity_exc(m, "IntegrityError");
+    py::register_exception_translator([](std::exception_ptr p) {
+        try {
+            if (p) std::rethrow_exception(p);
+        } catch (const std::runtime_error& e) {
+            if (std::string(e.what()).rfind("dash integrity", 0) == 0) {
+                PyErr_SetString(integrity_exc.ptr(), e.what());
+                return;
+            }
+            throw;
+        }
+    });
+
+    m.def("nr_comps", &nr_comps);
+    m.def("first_primes", &first_primes);
+    m.def("mul_inv", [](py::int_ a, i64 b) { return mul_inv(py_to_u128(a), b); });
+    m.def("set_num_threads", &set_default_threads);
+    m.def("get_num_threads", &default_threads);
+    m.def("aes_hash", [](py::int_ x) { return u128_to_py(hash(py_to_u128(x))); }, "fixed-key AES-128 of a 128-bit int");
+    m.def("aes_hash_array", [](py::array_t<uint64_t, py::array::c_style | py::array::forcecast> a) {
+        DASH_CHECK(a.ndim() == 2 && a.shape(1) == 2, "expected (n, 2) uint64 array");
+        py::array_t<uint64_t> out({a.shape(0), static_cast<py::ssize_t>(2)});
+        hash_batch(reinterpret_cast<const u128*>(a.data()), reinterpret_cast<u128*>(out.mutable_data()), a.shape(0));
+        return out;
+    });
+    m.def("aes_encrypt_block", [](py::bytes key, py::bytes block) {
+        std::string k = key, b = block;
+        DASH_CHECK(k.size() == 16 && b.size() == 16, "key and block must be 16 bytes");
+        AesKey ak;
+        aes_expand(reinterpret_cast<const uint8_t*>(k.data()), ak);
+        __m128i x;
+        std::memcpy(&x, b.data(), 16);
+        x = aes_enc_block(x, ak);
+        char out[16];
+        std::memcpy(out, &x, 16);
+        return py::bytes(out, 16);
+    });
+    m.def("aes_round_keys", [](py::bytes key) {
+        std::string k = key;
+        DASH_CHECK(k.size() == 16, "key must be 16 bytes");
+        AesKey ak;
+        aes_expand(reinterpret_cast<const uint8_t*>(k.data()), ak);
+        uint8_t rk[176];
+        aes_round_key_bytes(ak, rk);
+        return py::bytes(reinterpret_cast<char*>(rk), 176);
+    });
+    m.def("compress", [](py::array_t<int16_t, py::array::c_style | py::array::forcecast> a, int p) {
+        const ModInfo& mi = mod_info(p);
+        DASH_CHECK(a.size() == mi.n, "label length mismatch");
+        return u128_to_py(compress(a.data(), mi));
+    });
+    m.def("decompress", [](py::int_ c, int p) {
+        const ModInfo& mi = mod_info(p);
+        py::array_t<int16_t> out(mi.n);
+        decompress(py_to_u128(c), out.mutable_data(), mi);
+        return out;
+    });
+    m.def("gen_approx_lookup", &gen_approx_lookup);
+    m.def("prg_label", [](py::bytes seed, uint64_t stream, uint64_t ctr, int p) {
+        std::string s = seed;
+        DASH_CHECK(s.size() == 16, "seed must be 16 bytes");
+        Prg prg(reinterpret_cast<const uint8_t*>(s.data()));
+        py::array_t<int16_t> out(nr_comps(p));
+        prg.label(stream, ctr, p, nr_comps(p), out.mutable_data());
+        return out;
+    });
+    m.def("kind_name", &kind_name);
+
+    py::class_<GarbledModel, std::shared_ptr<GarbledModel>>(m, "GarbledModel")
+        .def("serialize", [](const GarbledModel& g) { return py::bytes(g.serialize()); })
+        .def_static("deserialize", [](py::bytes b) { return std::make_shared<GarbledModel>(GarbledModel::deserialize(std::string(b))); })
+        .def_property_readonly("crt", [](const GarbledModel& g) { return g.h.crt; })
+        .def_property_readonly("mrs", [](const GarbledModel& g) { return g.h.mrs; })
+        .def_property_readonly("in_dims", [](const GarbledModel& g) { return g.h.in_dims; })
+        .def_property_readonly("out_dims", [](const GarbledModel& g) { return g.h.out_dims; })
+        .def_property_readonly("out_moduli", [](const GarbledModel& g) { return g.h.out_moduli; })
+        .def_property_readonly("max_mod", [](const GarbledModel& g) { return g.h.max_mod; })
+        .def_property_readonly("num_layers", [](const GarbledModel& g) { return g.layers.size(); })
+        .def("table_bytes", &GarbledModel::table_bytes)
+        .def("total_bytes", &GarbledModel::total_bytes)
+        .def("layer_kind", [](const GarbledModel& g, size_t i) { return g.layers.at(i).kind; })
+        .def("layer_params", [](const GarbledModel& g, size_t i) { return from_params(g.layers.at(i).p); })
+        .def("layer_arrays", [](std::shared_ptr<GarbledModel> g, size_t i) {
+            py::dict d;
+            py::object owner = py::cast(g);
+            for (const auto& kv : g->layers.at(i).a) d[py::str(kv.first)] = array_view(kv.second, owner);
+            return d;
+        })
+        .def("consts", [](std::shared_ptr<GarbledModel> g) {
+            py::dict d;
+            py::object owner = py::cast(g);
+            for (const auto& kv : g->consts) d[py::str(kv.first)] = array_view(kv.second, owner);
+            return d;
+        })
+        .def("flip_table_bit", [](GarbledModel& g, size_t layer, const std::string& name, size_t entry, int bit) {
+            // fault injection for integrity tests
+            Array& a = g.layers.at(layer).a.at(name);
+            DASH_CHECK(a.dtype == DType::u128 && entry < a.count(), "bad fault-injection target");
+            a.ptr<u128>()[entry] ^= (static_cast<u128>(1) << bit);
+        });
+
+    py::class_<Decoder, std::shared_ptr<Decoder>>(m, "Decoder")
+        .def("decode", [](const Decoder& d, const py::list& labels) {
+            auto v = d.decode(labels_from_py(labels));
+            return py::array_t<i64>(v.size(), v.data());
+        })
+        .def("decode_residues", [](const Decoder& d, const py::list& labels) {
+            auto v = d.decode_residues(labels_from_py(labels));
+            return py::array_t<i64>({static_cast<py::ssize_t>(d.moduli.size()), static_cast<py::ssize_t>(d.n_out)}, v.data());
+        })
+        .def_property_readonly("moduli", [](const Decoder& d) { return d.moduli; })
+        .def_property_readonly("n_out", [](const Decoder& d) { return d.n_out; })
+        .def("serialize", [](const Decoder& d) { return py::bytes(d.serialize()); })
+        .def_static("deserialize", [](py::bytes b) { return std::make_shared<Decoder>(Decoder::deserialize(std::string(b))); })
+        .def("tables", [](std::shared_ptr<Decoder> d) {
+            py::list l;
+            py::object owner = py::cast(d);
+            for (const auto& a : d->dec) l.append(array_view(a, owner));
+            return l;
+        });
+
+    py::class_<Garbler, std::shared_ptr<Garbler>>(m, "Garbler")
+        .def(py::init([](std::vector<int> crt, std::vector<int> mrs, py::bytes seed, int max_mod) {
+                 return std::make_shared<Garbler>(crt, mrs, std::string(seed), max_mod);
+             }),
+             py::arg("crt"), py::arg("mrs"), py::arg("seed"), py::arg("max_mod") = 0)
+        .def("garble", [](Garbler& g, const py::list& layers, std::vector<i64> in_dims, int nthreads) {
+            auto specs = specs_from_py(layers);
+            GarbleOptions o;
+            o.nthreads = nthreads;
+            GarbledModel gm;
+            {
+                py::gil_scoped_release rel;
+                gm = g.garble(specs, in_dims, o);
+            }
+            return std::make_shared<GarbledModel>(std::move(gm));
+        }, py::arg("layers"), py::arg("in_dims"), py::arg("nthreads") = 0)
+        .def("encode", [](const Garbler& g, py::array_t<i64, py::array::c_style | py::array::forcecast> x) {
+            std::vector<i64> v(x.data(), x.data() + x.size());
+            return labels_to_py(g.encode(v));
+        })
+        .def("decoder", [](const Garbler& g) { return std::make_shared<Decoder>(g.decoder()); })
+        .def_property_readonly("crt_modulus", &Garbler::crt_modulus)
+        .def("offset_label", [](const Garbler& g, int p) {
+            const comp_t* r = g.offsets().get(p);
+            return py::array_t<int16_t>(nr_comps(p), r);
+        })
+        .def("zero_label", [](const Garbler& g, int p) {
+            const comp_t* r = g.zeros().get(p);
+            return py::array_t<int16_t>(nr_comps(p), r);
+        })
+        .def("input_base", [](const Garbler& g) { return labels_to_py(g.input_base()); });
+
+    m.def("cpu_evaluate", [](std::shared_ptr<GarbledModel> gm, const py::list& labels, int nthreads) {
+        CrtLabels in = labels_from_py(labels);
+        CrtLabels out;
+        {
+            py::gil_scoped_release rel;
+            out = cpu_evaluate(*gm, in, nthreads);
+        }
+        return labels_to_py(out);
+    }, py::arg("model"), py::arg("labels"), py::arg("nthreads") = 0);
+
+    dash::register_hip_bindings(m);
+}

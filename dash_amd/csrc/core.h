@@ -1,0 +1,318 @@
+// dash_amd native core: scalar domain, CRT math, label primitives, fixed-key
+// AES hash (AES-NI), AES-CTR label PRG and a small thread pool.
+//
+// Behavioural parity with the reference (UzL-ITS/dash):
+//   * label width n_p = floor(128 / log2 p)         dash/include/garbling/label_tensor.h:1353-1357
+//   * compress C = sum_j L_j p^j (uint128, L_0 LSD)   label_tensor.h:715-724
+//   * H(C) = AES-128_K(LE bytes of C), K = 00..0f     crypto/cpu_aes_engine.h:23-40
+//   * color = component 0, offsets have R[0] = 1      label_tensor.h:1303-1307
+//   * CRT helpers (signed modulo, mul_inv, CRT)      misc/util.h:43-156
+// The implementation is new: chunked Horner/long-division digit codecs,
+// pipelined AES-NI, a deterministic AES-CTR PRG (the reference uses RDRAND,
+// which makes garbling non-reproducible and impossible to mirror on the GPU).
+#pragma once
+
+#include <immintrin.h>
+
+#include <algorithm>
+#include <atomic>
+#include <cmath>
+#include <condition_variable>
+#include <cstdint>
+#include <cstring>
+#include <functional>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <numeric>
+#include <stdexcept>
+#include <string>
+#include <thread>
+#include <vector>
+
+namespace dash {
+
+using u128 = unsigned __int128;
+using i64 = int64_t;
+using u64 = uint64_t;
+using comp_t = int16_t;  // one label component ("crt_val_t" in the reference)
+
+#define DASH_CHECK(cond, msg)                                                 \
+    do {                                                                      \
+        if (!(cond)) throw std::runtime_error(std::string("dash: ") + (msg)); \
+    } while (0)
+
+// ----------------------------------------------------------------------------
+// Scalar / CRT math
+// ----------------------------------------------------------------------------
+inline int nr_comps(i64 p) {
+    // Same floating point formula as the reference so label widths match for
+    // every modulus (including prime powers such as 32).
+    return static_cast<int>(std::floor(128.0 / std::log2(static_cast<double>(p))));
+}
+
+inline i64 pmod(i64 a, i64 p) {
+    i64 r = a % p;
+    return r < 0 ? r + p : r;
+}
+
+// Multiplicative inverse of a mod b (extended Euclid), b < 2^16.
+inline i64 mul_inv(u128 a, i64 b) {
+    if (b == 1) return 1;
+    i64 b0 = b;
+    i64 x0 = 0, x1 = 1;
+    u128 aa = a;
+    u128 bb = static_cast<u128>(b);
+    while (aa > 1) {
+        if (bb == 0) throw std::runtime_error("dash: mul_inv of non-invertible value");
+        i64 q = static_cast<i64>(aa / bb);
+        u128 t = bb;
+        bb = aa % bb;
+        aa = t;
+        i64 tx = x0;
+        x0 = x1 - q * x0;
+        x1 = tx;
+    }
+    if (x1 < 0) x1 += b0;
+    return x1;
+}
+
+std::vector<int> first_primes(int k);
+
+// ----------------------------------------------------------------------------
+// Label digit codecs (compress / decompress)
+// ----------------------------------------------------------------------------
+struct ModInfo {
+    int p = 0;        // modulus
+    int n = 0;        // components per label
+    int chunk = 1;    // digits per 32-bit chunk (p^chunk < 2^32)
+    u64 pchunk = 1;   // p^chunk
+    bool pow2 = false;
+    int bits = 0;     // log2 p when pow2
+};
+
+const ModInfo& mod_info(int p);
+
+// C = sum_j L[j] * p^j  (mod 2^128)
+inline u128 compress(const comp_t* L, const ModInfo& m) {
+    const int n = m.n;
+    if (m.pow2) {
+        u128 C = 0;
+        for (int j = n - 1; j >= 0; --j) C = (C << m.bits) | static_cast<u128>(static_cast<uint16_t>(L[j]));
+        return C;
+    }
+    // Horner over chunks of `chunk` digits evaluated in 64-bit, then folded in
+    // 128-bit: C = C * p^c + chunk_value.
+    u128 C = 0;
+    int j = n - 1;
+    const u64 p = static_cast<u64>(m.p);
+    int first = n % m.chunk;
+    if (first == 0) first = m.chunk;
+    // leading (partial) chunk
+    {
+        u64 v = 0;
+        for (int t = 0; t < first; ++t, --j) v = v * p + static_cast<u64>(static_cast<uint16_t>(L[j]));
+        C = v;
+    }
+    while (j >= 0) {
+        u64 v = 0;
+        for (int t = 0; t < m.chunk; ++t, --j) v = v * p + static_cast<u64>(static_cast<uint16_t>(L[j]));
+        C = C * static_cast<u128>(m.pchunk) + v;
+    }
+    return C;
+}
+
+// Inverse of compress for a valid C (< p^n). For arbitrary C the first n-1
+// digits are the base-p digits and the top digit is reduced mod p.
+inline void decompress(u128 C, comp_t* L, const ModInfo& m) {
+    const int n = m.n;
+    if (m.pow2) {
+        const u128 mask = (static_cast<u128>(1) << m.bits) - 1;
+        for (int j = 0; j < n; ++j) {
+            L[j] = static_cast<comp_t>(static_cast<int>(C & mask));
+            C >>= m.bits;
+        }
+        L[n - 1] = static_cast<comp_t>(static_cast<int>(L[n - 1]) % m.p);
+        return;
+    }
+    const u64 D = m.pchunk;
+    const u64 p = static_cast<u64>(m.p);
+    int j = 0;
+    while (j < n) {
+        // (C, r) = divmod(C, D) with D < 2^32
+        u64 hi = static_cast<u64>(C >> 64), lo = static_cast<u64>(C);
+        u64 qh = hi / D, r = hi % D;
+        u64 x1 = (r << 32) | (lo >> 32);
+        u64 q1 = x1 / D;
+        r = x1 % D;
+        u64 x0 = (r << 32) | (lo & 0xffffffffull);
+        u64 q0 = x0 / D;
+        r = x0 % D;
+        C = (static_cast<u128>(qh) << 64) | (static_cast<u128>(q1) << 32) | q0;
+        int cnt = std::min(m.chunk, n - j);
+        for (int t = 0; t < cnt; ++t, ++j) {
+            L[j] = static_cast<comp_t>(r % p);
+            r /= p;
+        }
+    }
+    // top digit: (floor(C_orig / p^(n-1))) mod p  -- matches the reference's
+    // final `%= modulus` for in-range payloads.
+    (void)C;
+}
+
+// ----------------------------------------------------------------------------
+// Label vector arithmetic (component-wise mod p)
+// ----------------------------------------------------------------------------
+inline void lab_add(comp_t* a, const comp_t* b, int n, int p) {
+    for (int i = 0; i < n; ++i) {
+        int v = a[i] + b[i];
+        a[i] = static_cast<comp_t>(v >= p ? v - p : v);
+    }
+}
+inline void lab_sub(comp_t* a, const comp_t* b, int n, int p) {
+    for (int i = 0; i < n; ++i) {
+        int v = a[i] - b[i];
+        a[i] = static_cast<comp_t>(v < 0 ? v + p : v);
+    }
+}
+// a = a * c mod p  (c any signed integer)
+inline void lab_scale(comp_t* a, i64 c, int n, int p) {
+    i64 cc = pmod(c, p);
+    for (int i = 0; i < n; ++i) a[i] = static_cast<comp_t>((a[i] * cc) % p);
+}
+// a = a + c*b mod p
+inline void lab_axpy(comp_t* a, i64 c, const comp_t* b, int n, int p) {
+    i64 cc = pmod(c, p);
+    for (int i = 0; i < n; ++i) a[i] = static_cast<comp_t>((a[i] + cc * b[i]) % p);
+}
+// out = base + c*off mod p
+inline void lab_affine(comp_t* out, const comp_t* base, i64 c, const comp_t* off, int n, int p) {
+    i64 cc = pmod(c, p);
+    for (int i = 0; i < n; ++i) out[i] = static_cast<comp_t>((base[i] + cc * off[i]) % p);
+}
+
+// ----------------------------------------------------------------------------
+// AES-128 (AES-NI)
+// ----------------------------------------------------------------------------
+struct AesKey {
+    __m128i rk[11];
+};
+void aes_expand(const uint8_t key[16], AesKey& out);
+// Round keys in the byte order a portable/GPU implementation needs (11x16 B).
+void aes_round_key_bytes(const AesKey& k, uint8_t out[176]);
+
+inline __m128i aes_enc_block(__m128i x, const AesKey& k) {
+    x = _mm_xor_si128(x, k.rk[0]);
+    for (int r = 1; r < 10; ++r) x = _mm_aesenc_si128(x, k.rk[r]);
+    return _mm_aesenclast_si128(x, k.rk[10]);
+}
+
+inline __m128i u128_to_m(u128 v) {
+    __m128i r;
+    std::memcpy(&r, &v, 16);
+    return r;
+}
+inline u128 m_to_u128(__m128i v) {
+    u128 r;
+    std::memcpy(&r, &v, 16);
+    return r;
+}
+
+// The fixed-key hash used for every gate (key 00 01 .. 0f).
+const AesKey& fixed_key();
+inline u128 hash(u128 x) { return m_to_u128(aes_enc_block(u128_to_m(x), fixed_key())); }
+void hash_batch(const u128* in, u128* out, size_t n);
+
+// ----------------------------------------------------------------------------
+// Deterministic label PRG: AES-128-CTR keyed with the garbler seed.
+// block(stream, ctr) = AES_k(stream << 64 | ctr); each block yields two
+// 64-bit samples; component = sample mod p (bias <= p / 2^64).
+// ----------------------------------------------------------------------------
+struct Prg {
+    AesKey key;
+    explicit Prg(const uint8_t seed[16]) { aes_expand(seed, key); }
+    Prg() {
+        uint8_t z[16] = {0};
+        aes_expand(z, key);
+    }
+    inline void label(u64 stream, u64& ctr, int p, int n, comp_t* out) const {
+        for (int j = 0; j < n; j += 2) {
+            u128 blk = (static_cast<u128>(stream) << 64) | ctr++;
+            u128 r = m_to_u128(aes_enc_block(u128_to_m(blk), key));
+            u64 lo = static_cast<u64>(r), hi = static_cast<u64>(r >> 64);
+            out[j] = static_cast<comp_t>(lo % static_cast<u64>(p));
+            if (j + 1 < n) out[j + 1] = static_cast<comp_t>(hi % static_cast<u64>(p));
+        }
+    }
+};
+
+// Stream identifiers: distinct (layer, slot, element) triples never collide.
+inline u64 stream_id(u64 layer, u64 slot, u64 elem) {
+    return (layer << 44) ^ (slot << 36) ^ elem;
+}
+constexpr u64 kGlobalLayer = 0xFFFFF;
+
+// ----------------------------------------------------------------------------
+// Thread pool / parallel_for (static chunking, deterministic results)
+// ----------------------------------------------------------------------------
+int default_threads();
+void set_default_threads(int n);
+void parallel_for(i64 n, const std::function<void(i64, i64)>& body, int nthreads = 0);
+
+// ----------------------------------------------------------------------------
+// Typed, 64-byte aligned n-d array (the unit of the GarbledModel format)
+// ----------------------------------------------------------------------------
+enum class DType : uint8_t { i16 = 0, i32 = 1, i64 = 2, u128 = 3, u8 = 4 };
+inline size_t dtype_size(DType d) {
+    switch (d) {
+        case DType::i16: return 2;
+        case DType::i32: return 4;
+        case DType::i64: return 8;
+        case DType::u128: return 16;
+        case DType::u8: return 1;
+    }
+    return 1;
+}
+
+struct Array {
+    DType dtype = DType::u8;
+    std::vector<i64> shape;
+    std::shared_ptr<uint8_t> buf;
+    size_t nbytes = 0;
+
+    Array() = default;
+    Array(DType dt, std::vector<i64> shp) : dtype(dt), shape(std::move(shp)) {
+        size_t cnt = 1;
+        for (auto s : shape) cnt *= static_cast<size_t>(s);
+        nbytes = cnt * dtype_size(dt);
+        size_t alloc = (nbytes + 63) & ~size_t(63);
+        if (alloc == 0) alloc = 64;
+        uint8_t* p = static_cast<uint8_t*>(std::aligned_alloc(64, alloc));
+        if (!p) throw std::bad_alloc();
+        std::memset(p, 0, alloc);
+        buf = std::shared_ptr<uint8_t>(p, [](uint8_t* q) { std::free(q); });
+    }
+    size_t count() const { return nbytes / dtype_size(dtype); }
+    template <typename T>
+    T* ptr() { return reinterpret_cast<T*>(buf.get()); }
+    template <typename T>
+    const T* ptr() const { return reinterpret_cast<const T*>(buf.get()); }
+};
+
+// ----------------------------------------------------------------------------
+// Label tensor: N labels mod p, label-major (the n components of one label are
+// contiguous), element index = flattened semantic index.
+// ----------------------------------------------------------------------------
+struct Labels {
+    int p = 0;
+    int n = 0;
+    i64 N = 0;
+    std::vector<comp_t> c;
+    Labels() = default;
+    Labels(int p_, i64 N_) : p(p_), n(nr_comps(p_)), N(N_), c(static_cast<size_t>(N_) * nr_comps(p_), 0) {}
+    comp_t* at(i64 i) { return c.data() + i * n; }
+    const comp_t* at(i64 i) const { return c.data() + i * n; }
+};
+using CrtLabels = std::vector<Labels>;  // one Labels per residue
+
+}  // namespace dash

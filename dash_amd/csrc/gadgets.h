@@ -1,0 +1,196 @@
+// Garbled gates and gadgets shared by the host garbler and the host (oracle)
+// evaluator. Every gadget is written per *element* (one neuron across all CRT
+// residues) so that the garbler, the CPU evaluator and the HIP kernels all
+// walk exactly the same sequence of gates and table offsets.
+//
+// Reference behaviour reproduced here (semantics, not code):
+//   projection gate           garbling/gates/projection_gate.h:62-102
+//   mini projection           garbling/gates/projection_gate_mini.h:25-56
+//   generalized half gate     garbling/gates/generalized_half_gate.h:51-89
+//   mixed-modulus half gate   garbling/gates/mixed_mod_half_gate.h:56-104
+//   approx-residue lookup     garbling/gadgets/lookup_approx_sign.h:75-101
+//   approximate sign gadget   garbling/gadgets/sign_gadget.h:425-671
+//   rescale gadget            garbling/gadgets/rescale_gadget.h:115-362
+//   base extension gadget     garbling/gadgets/base_extension_gadget.h:70-295
+// Table layouts are element-major (see docs/WIRE_FORMAT.md); the reference's
+// residue-major rescale layout (rescale_gadget.h:152-175) is not reproduced
+// because its own GPU kernel could not read it.
+#pragma once
+
+#include "core.h"
+
+namespace dash {
+
+// ---------------------------------------------------------------------------
+// Offset (R_p) and zero (Z_p) labels for every modulus 2..max_modulus.
+// ---------------------------------------------------------------------------
+struct LabelBank {
+    int max_mod = 0;
+    std::vector<std::vector<comp_t>> lab;  // indexed by modulus
+    const comp_t* get(int p) const {
+        DASH_CHECK(p >= 2 && p <= max_mod && !lab[p].empty(), "label bank has no entry for modulus " + std::to_string(p));
+        return lab[p].data();
+    }
+};
+
+// ---------------------------------------------------------------------------
+// Projection gate
+// ---------------------------------------------------------------------------
+struct ProjScratch {
+    std::vector<comp_t> key, tmp;
+    std::vector<u128> kc, hc, payc;
+    std::vector<int> colors;
+    std::vector<uint8_t> have;
+};
+ProjScratch& proj_scratch();
+
+// table[color(in0 + i*Rin)] = compress(out0 + f(i)*outR) + H(compress(in0 + i*Rin))
+template <class F>
+inline void garble_proj(const comp_t* in0, const comp_t* Rin, const ModInfo& mi, const comp_t* out0,
+                        const comp_t* outR, const ModInfo& mo, F&& f, u128* table) {
+    ProjScratch& s = proj_scratch();
+    const int pin = mi.p, nin = mi.n;
+    s.key.assign(in0, in0 + nin);
+    s.kc.resize(pin);
+    s.hc.resize(pin);
+    s.colors.resize(pin);
+    for (int i = 0; i < pin; ++i) {
+        s.kc[i] = compress(s.key.data(), mi);
+        s.colors[i] = s.key[0];
+        lab_add(s.key.data(), Rin, nin, pin);
+    }
+    hash_batch(s.kc.data(), s.hc.data(), pin);
+    s.payc.resize(mo.p);
+    s.have.assign(mo.p, 0);
+    s.tmp.resize(mo.n);
+    for (int i = 0; i < pin; ++i) {
+        int c = static_cast<int>(pmod(f(i), mo.p));
+        if (!s.have[c]) {
+            lab_affine(s.tmp.data(), out0, c, outR, mo.n, mo.p);
+            s.payc[c] = compress(s.tmp.data(), mo);
+            s.have[c] = 1;
+        }
+        table[s.colors[i]] = s.payc[c] + s.hc[i];
+    }
+}
+
+// Mini projection: 16-bit payloads packed into one table entry.
+template <class F>
+inline void garble_proj_mini(const comp_t* in0, const comp_t* Rin, const ModInfo& mi, F&& f, u128* entry) {
+    ProjScratch& s = proj_scratch();
+    const int pin = mi.p, nin = mi.n;
+    DASH_CHECK(pin <= 8, "mini projection supports input moduli <= 8");
+    s.key.assign(in0, in0 + nin);
+    int16_t* t16 = reinterpret_cast<int16_t*>(entry);
+    for (int i = 0; i < pin; ++i) {
+        u128 h = hash(compress(s.key.data(), mi));
+        int color = s.key[0];
+        t16[color] = static_cast<int16_t>(static_cast<int16_t>(f(i)) + static_cast<int16_t>(static_cast<uint16_t>(h)));
+        lab_add(s.key.data(), Rin, nin, pin);
+    }
+}
+
+inline int color_of(const comp_t* L, int p) { return static_cast<int>(static_cast<uint16_t>(L[0]) % static_cast<unsigned>(p)); }
+
+// out = decompress(T[color(in)] - H(compress(in)))
+inline void eval_proj(const comp_t* in, const ModInfo& mi, const u128* table, const ModInfo& mo, comp_t* out) {
+    u128 h = hash(compress(in, mi));
+    decompress(table[color_of(in, mi.p)] - h, out, mo);
+}
+
+inline int16_t eval_proj_mini(const comp_t* in, const ModInfo& mi, const u128* entry) {
+    u128 h = hash(compress(in, mi));
+    const int16_t* t16 = reinterpret_cast<const int16_t*>(entry);
+    return static_cast<int16_t>(t16[color_of(in, mi.p)] - static_cast<int16_t>(static_cast<uint16_t>(h)));
+}
+
+// ---------------------------------------------------------------------------
+// Approximate sign gadget (per element)
+// ---------------------------------------------------------------------------
+struct SignPlan {
+    std::vector<int> crt, mrs, out_mod;
+    int lower = 0, upper = 1;
+    std::vector<std::vector<int16_t>> lookup;  // [k][v * t + d], d = 0 is most significant
+    std::vector<i64> crt_prefix;
+    i64 sum_crt = 0;
+    i64 n_approx = 0, n_cast = 0, n_sign = 0;  // table entries per element
+    int max_n = 0;                             // largest label width touched
+
+    SignPlan() = default;
+    SignPlan(const std::vector<int>& crt_, const std::vector<int>& mrs_, const std::vector<int>& out, int lo, int up);
+};
+
+std::vector<std::vector<int16_t>> gen_approx_lookup(const std::vector<int>& crt, const std::vector<int>& mrs);
+
+// Garbler: in0[j] = base label of residue j (mod crt[j]); out0[o] receives the
+// output base label for out_mod[o].
+void sign_garble_elem(const SignPlan& P, const LabelBank& R, const LabelBank& Z, const Prg& prg, u64 stream,
+                      const comp_t* const* in0, u128* approx, u128* cast1, u128* cast2, u128* sign,
+                      comp_t* const* out0);
+void sign_eval_elem(const SignPlan& P, const LabelBank& Z, const comp_t* const* in, const u128* approx,
+                    const u128* cast1, const u128* cast2, const u128* sign, comp_t* const* out);
+
+// ---------------------------------------------------------------------------
+// Mixed-modulus half gate x (mod p) * y (mod q), q <= 8. Tables: g[p], e[q+1].
+// ---------------------------------------------------------------------------
+void mixed_mult_garble(const comp_t* x0, const ModInfo& mp, const comp_t* y0, const ModInfo& mq,
+                       const LabelBank& R, const Prg& prg, u64 stream, u64& ctr, u128* g, u128* e, comp_t* out0);
+void mixed_mult_eval(const comp_t* x, const ModInfo& mp, const comp_t* y, const ModInfo& mq, const u128* g,
+                     const u128* e, comp_t* out);
+
+// Generalized half gate x * y, both mod p. Tables g[p], e[p].
+void gen_mult_garble(const comp_t* x0, const comp_t* y0, const ModInfo& mp, const LabelBank& R, const Prg& prg,
+                     u64 stream, u64& ctr, u128* g, u128* e, comp_t* out0);
+void gen_mult_eval(const comp_t* x, const comp_t* y, const ModInfo& mp, const u128* g, const u128* e, comp_t* out);
+
+// ---------------------------------------------------------------------------
+// Base extension (ReDash MRS conversion) per element
+// ---------------------------------------------------------------------------
+struct BEPlan {
+    std::vector<int> moduli;        // output (full) base, length E
+    std::vector<int> extra;         // moduli to (re)derive
+    std::vector<int> extra_idx;     // their indices in `moduli`
+    std::vector<int> swapped;       // moduli order used by the MRS loop
+    std::vector<int> pos_of;        // for every base index i: position in swapped
+    std::vector<std::vector<i64>> inv_partial;  // [i][j] = inv(b_i) mod b_{i+j+1}
+    std::vector<i64> invv;          // per extra modulus
+    int nonext = 0;
+    i64 n_tab = 0;                  // table entries per element
+    BEPlan() = default;
+    BEPlan(const std::vector<int>& moduli, const std::vector<int>& extra);
+};
+// L[j] are labels (mod moduli[j]) of one element, updated in place.
+void be_garble_elem(const BEPlan& P, const LabelBank& R, const Prg& prg, u64 stream, u64& ctr, comp_t* const* L,
+                    u128* tab);
+void be_eval_elem(const BEPlan& P, comp_t* const* L, const u128* tab);
+
+// ---------------------------------------------------------------------------
+// Rescale gadget (one iteration) per element.
+//   legacy: factors = {2}, residue 0 recovered by a sign gadget (out {2}, 1/0)
+//   redash: factors = s (subset of the CRT base), recovered by base extension
+// ---------------------------------------------------------------------------
+struct RescalePlan {
+    std::vector<int> crt;
+    std::vector<int> factors;
+    std::vector<int> factor_idx;
+    bool sign_be = true;
+    i64 n_trans = 0;  // trans-mod entries per element
+    std::vector<std::vector<int>> active;  // per factor: residues processed
+    std::vector<std::vector<i64>> inv;     // per factor, per active residue: inv(s) mod p
+    SignPlan sign;                         // when sign_be
+    BEPlan be;                             // otherwise
+    i64 n_be = 0;
+    i64 sprod = 1;
+    RescalePlan() = default;
+    RescalePlan(const std::vector<int>& crt, const std::vector<int>& mrs, const std::vector<int>& factors, bool sign_be);
+};
+// Garbler: L[j] base labels (mod crt[j]) in/out; up/down are the garbler-side
+// (offset-free) shift base labels.
+void rescale_garble_elem(const RescalePlan& P, const LabelBank& R, const LabelBank& Z, const Prg& prg, u64 stream,
+                         comp_t* const* L, const comp_t* const* up_base, const comp_t* const* down_base, u128* trans,
+                         u128* s_approx, u128* s_cast1, u128* s_cast2, u128* s_sign, u128* be);
+void rescale_eval_elem(const RescalePlan& P, const LabelBank& Z, comp_t* const* L, const comp_t* const* up,
+                       const comp_t* const* down, const u128* trans, const u128* s_approx, const u128* s_cast1,
+                       const u128* s_cast2, const u128* s_sign, const u128* be);
+
+}  // namespace dash

@@ -1,0 +1,129 @@
+// GarbledModel: the single artefact passed from the garbler to the evaluator
+// (offline message), plus the garbler-side secrets and decoder.
+//
+// The reference keeps garbler and evaluator state inside one object
+// (garbling/garbled_circuit_interface.h) and never serializes it; here the
+// two roles are split and the model has a versioned binary format
+// (docs/WIRE_FORMAT.md) so that garbling and evaluation can run in different
+// processes, hosts or devices.
+#pragma once
+
+#include <string>
+
+#include "core.h"
+#include "gadgets.h"
+
+namespace dash {
+
+enum Kind : int {
+    K_DENSE = 0,
+    K_CONV = 1,
+    K_RELU = 2,
+    K_SIGN = 3,
+    K_RESCALE = 4,
+    K_MAXPOOL = 5,
+    K_FLATTEN = 6,
+    K_PROJ = 7,
+    K_MULT = 8,
+    K_MMULT = 9,
+    K_MAX = 10,
+    K_BASEEXT = 11,
+    K_ADD = 12,
+    K_SUMPOOL = 13,
+};
+const char* kind_name(int kind);
+
+using Params = std::map<std::string, std::vector<i64>>;
+
+struct LayerSpec {
+    int kind = 0;
+    Params p;
+};
+
+struct GLayer {
+    int kind = 0;
+    Params p;
+    std::map<std::string, Array> a;
+    i64 param(const std::string& k, i64 dflt = -1) const {
+        auto it = p.find(k);
+        return (it == p.end() || it->second.empty()) ? dflt : it->second[0];
+    }
+    const std::vector<i64>& vec(const std::string& k) const {
+        auto it = p.find(k);
+        DASH_CHECK(it != p.end(), std::string("missing layer param ") + k);
+        return it->second;
+    }
+    const Array& arr(const std::string& k) const {
+        auto it = a.find(k);
+        DASH_CHECK(it != a.end(), std::string("missing layer array ") + k);
+        return it->second;
+    }
+};
+
+struct ModelHeader {
+    int version = 1;
+    std::vector<int> crt, mrs;
+    std::vector<i64> in_dims, out_dims;
+    std::vector<int> out_moduli;  // moduli of the output residues
+    int max_mod = 0;
+};
+
+struct GarbledModel {
+    ModelHeader h;
+    std::map<std::string, Array> consts;  // evaluator-visible constants (Z_p, shift labels)
+    std::vector<GLayer> layers;
+
+    std::string serialize() const;
+    static GarbledModel deserialize(const std::string& blob);
+    size_t table_bytes() const;  // bytes of garbled tables (u128 arrays)
+    size_t total_bytes() const;
+    LabelBank zero_bank() const;
+};
+
+// Held by whoever decodes the outputs (the garbler / client).
+struct Decoder {
+    std::vector<int> moduli;
+    i64 n_out = 0;
+    std::vector<Array> dec;  // per residue: u128 [p][n_out] = H(compress(out0 + v*R))
+    std::vector<i64> decode(const CrtLabels& out) const;
+    std::vector<i64> decode_residues(const CrtLabels& out) const;  // [k][n_out] residues
+    std::string serialize() const;
+    static Decoder deserialize(const std::string& blob);
+};
+
+struct GarbleOptions {
+    int nthreads = 0;
+};
+
+class Garbler {
+   public:
+    Garbler(const std::vector<int>& crt, const std::vector<int>& mrs, const std::string& seed16, int max_mod = 0);
+    GarbledModel garble(const std::vector<LayerSpec>& layers, const std::vector<i64>& in_dims,
+                        const GarbleOptions& opt = {});
+    // Online message #1: encoded inputs x -> W0 + (x mod p) * R
+    CrtLabels encode(const std::vector<i64>& x) const;
+    const Decoder& decoder() const { return dec_; }
+    const std::vector<int>& crt() const { return crt_; }
+    i64 crt_modulus() const { return M_; }
+    // secrets (exposed for tests / the SGX-style split)
+    const LabelBank& offsets() const { return R_; }
+    const LabelBank& zeros() const { return Z_; }
+    const CrtLabels& input_base() const { return in_base_; }
+
+   private:
+    std::vector<int> crt_, mrs_;
+    i64 M_ = 1;
+    int max_mod_ = 0;
+    Prg prg_;
+    LabelBank R_, Z_;
+    CrtLabels in_base_;
+    Decoder dec_;
+};
+
+// Host (oracle) evaluator: bit-exact reference for the HIP evaluator.
+CrtLabels cpu_evaluate(const GarbledModel& m, const CrtLabels& inputs, int nthreads = 0);
+
+// Required moduli (for R/Z banks) given bases.
+int required_max_modulus(const std::vector<int>& crt, const std::vector<int>& mrs, const std::vector<LayerSpec>& layers);
+
+}  // namespace dash

@@ -1,0 +1,181 @@
+// Versioned binary format of GarbledModel and Decoder (docs/WIRE_FORMAT.md).
+// Little-endian, length-prefixed; every array carries dtype + shape.
+#include "model.h"
+
+namespace dash {
+
+namespace {
+constexpr char kModelMagic[8] = {'D', 'A', 'M', 'D', 'G', 'C', '0', '1'};
+constexpr char kDecMagic[8] = {'D', 'A', 'M', 'D', 'D', 'E', 'C', '1'};
+
+struct W {
+    std::string s;
+    void raw(const void* p, size_t n) { s.append(static_cast<const char*>(p), n); }
+    void u32(uint32_t v) { raw(&v, 4); }
+    void i64v(i64 v) { raw(&v, 8); }
+    void str(const std::string& x) {
+        u32(static_cast<uint32_t>(x.size()));
+        raw(x.data(), x.size());
+    }
+    void ivec(const std::vector<i64>& v) {
+        u32(static_cast<uint32_t>(v.size()));
+        for (auto x : v) i64v(x);
+    }
+    void ivec32(const std::vector<int>& v) {
+        u32(static_cast<uint32_t>(v.size()));
+        for (auto x : v) i64v(x);
+    }
+    void arr(const Array& a) {
+        uint8_t dt = static_cast<uint8_t>(a.dtype);
+        raw(&dt, 1);
+        ivec(a.shape);
+        i64v(static_cast<i64>(a.nbytes));
+        raw(a.buf.get(), a.nbytes);
+    }
+};
+
+struct Rd {
+    const std::string& s;
+    size_t off = 0;
+    explicit Rd(const std::string& x) : s(x) {}
+    void raw(void* p, size_t n) {
+        DASH_CHECK(off + n <= s.size(), "truncated blob");
+        std::memcpy(p, s.data() + off, n);
+        off += n;
+    }
+    uint32_t u32() {
+        uint32_t v;
+        raw(&v, 4);
+        return v;
+    }
+    i64 i64v() {
+        i64 v;
+        raw(&v, 8);
+        return v;
+    }
+    std::string str() {
+        uint32_t n = u32();
+        DASH_CHECK(off + n <= s.size(), "truncated blob");
+        std::string r = s.substr(off, n);
+        off += n;
+        return r;
+    }
+    std::vector<i64> ivec() {
+        uint32_t n = u32();
+        std::vector<i64> v(n);
+        for (auto& x : v) x = i64v();
+        return v;
+    }
+    std::vector<int> ivec32() {
+        auto v = ivec();
+        return std::vector<int>(v.begin(), v.end());
+    }
+    Array arr() {
+        uint8_t dt;
+        raw(&dt, 1);
+        DASH_CHECK(dt <= 4, "bad dtype");
+        auto shape = ivec();
+        Array a(static_cast<DType>(dt), shape);
+        i64 nb = i64v();
+        DASH_CHECK(static_cast<size_t>(nb) == a.nbytes, "array size mismatch");
+        raw(a.buf.get(), a.nbytes);
+        return a;
+    }
+};
+}  // namespace
+
+std::string GarbledModel::serialize() const {
+    W w;
+    w.raw(kModelMagic, 8);
+    w.u32(static_cast<uint32_t>(h.version));
+    w.ivec32(h.crt);
+    w.ivec32(h.mrs);
+    w.ivec(h.in_dims);
+    w.ivec(h.out_dims);
+    w.ivec32(h.out_moduli);
+    w.i64v(h.max_mod);
+    w.u32(static_cast<uint32_t>(consts.size()));
+    for (const auto& kv : consts) {
+        w.str(kv.first);
+        w.arr(kv.second);
+    }
+    w.u32(static_cast<uint32_t>(layers.size()));
+    for (const auto& l : layers) {
+        w.u32(static_cast<uint32_t>(l.kind));
+        w.u32(static_cast<uint32_t>(l.p.size()));
+        for (const auto& kv : l.p) {
+            w.str(kv.first);
+            w.ivec(kv.second);
+        }
+        w.u32(static_cast<uint32_t>(l.a.size()));
+        for (const auto& kv : l.a) {
+            w.str(kv.first);
+            w.arr(kv.second);
+        }
+    }
+    return std::move(w.s);
+}
+
+GarbledModel GarbledModel::deserialize(const std::string& blob) {
+    Rd r(blob);
+    char mg[8];
+    r.raw(mg, 8);
+    DASH_CHECK(std::memcmp(mg, kModelMagic, 8) == 0, "not a garbled model blob");
+    GarbledModel m;
+    m.h.version = static_cast<int>(r.u32());
+    DASH_CHECK(m.h.version == 1, "unsupported garbled model version");
+    m.h.crt = r.ivec32();
+    m.h.mrs = r.ivec32();
+    m.h.in_dims = r.ivec();
+    m.h.out_dims = r.ivec();
+    m.h.out_moduli = r.ivec32();
+    m.h.max_mod = static_cast<int>(r.i64v());
+    uint32_t nc = r.u32();
+    for (uint32_t i = 0; i < nc; ++i) {
+        std::string k = r.str();
+        m.consts[k] = r.arr();
+    }
+    uint32_t nl = r.u32();
+    for (uint32_t i = 0; i < nl; ++i) {
+        GLayer g;
+        g.kind = static_cast<int>(r.u32());
+        uint32_t np = r.u32();
+        for (uint32_t q = 0; q < np; ++q) {
+            std::string k = r.str();
+            g.p[k] = r.ivec();
+        }
+        uint32_t na = r.u32();
+        for (uint32_t q = 0; q < na; ++q) {
+            std::string k = r.str();
+            g.a[k] = r.arr();
+        }
+        m.layers.push_back(std::move(g));
+    }
+    DASH_CHECK(r.off == blob.size(), "trailing bytes after garbled model");
+    return m;
+}
+
+std::string Decoder::serialize() const {
+    W w;
+    w.raw(kDecMagic, 8);
+    w.ivec32(moduli);
+    w.i64v(n_out);
+    w.u32(static_cast<uint32_t>(dec.size()));
+    for (const auto& a : dec) w.arr(a);
+    return std::move(w.s);
+}
+
+Decoder Decoder::deserialize(const std::string& blob) {
+    Rd r(blob);
+    char mg[8];
+    r.raw(mg, 8);
+    DASH_CHECK(std::memcmp(mg, kDecMagic, 8) == 0, "not a decoder blob");
+    Decoder d;
+    d.moduli = r.ivec32();
+    d.n_out = r.i64v();
+    uint32_t n = r.u32();
+    for (uint32_t i = 0; i < n; ++i) d.dec.push_back(r.arr());
+    return d;
+}
+
+}  // namespace dash

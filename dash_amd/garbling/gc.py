@@ -1,0 +1,88 @@
+"""High-level garbled-circuit API.
+
+`GarbledCircuit` mirrors the reference's public entry points
+(garbling/garbled_circuit.h:43-109 constructors; garbled_circuit_interface.h:
+garble_inputs :325-343, cpu_evaluate :345-380, decode_outputs :422-467,
+cuda_move/cuda_evaluate/cuda_move_outputs :477-736) on top of the split
+garbler / evaluator roles:
+
+    garbler  = native.Garbler   (secrets: R_p, input base labels, decoder)
+    model    = native.GarbledModel  (offline message, serializable)
+    evaluator = cpu_evaluate / dash_amd.runtime.HipEvaluator
+"""
+from __future__ import annotations
+
+import os
+import time
+from typing import Optional, Sequence, Union
+
+import numpy as np
+
+from ..ir.bases import crt_modulus as _crt_mod
+from ..ir.bases import first_primes, get_mrs_base
+from ..ir.circuit import Circuit
+from ..native import native
+
+Labels = list  # list[(modulus, np.ndarray int16 [N, n_p])]
+
+
+class GarbledCircuit:
+    def __init__(self, circuit: Circuit, crt: Union[int, Sequence[int]], mrs: Union[None, float, Sequence[int]] = None,
+                 max_modulus: int = 0, seed: Optional[bytes] = None, garble_me: bool = True, nthreads: int = 0):
+        self.circuit = circuit
+        self.crt_base = first_primes(crt) if isinstance(crt, int) else [int(p) for p in crt]
+        if mrs is None:
+            self.mrs_base: list[int] = []
+        elif isinstance(mrs, (int, float)) and not isinstance(mrs, bool):
+            self.mrs_base = get_mrs_base(len(self.crt_base), float(mrs))
+        else:
+            self.mrs_base = [int(m) for m in mrs]
+        self.crt_modulus = _crt_mod(self.crt_base)
+        self.seed = seed if seed is not None else os.urandom(16)
+        self.nthreads = nthreads
+        self._n = native()
+        self.garbler = self._n.Garbler(self.crt_base, self.mrs_base, self.seed, int(max_modulus))
+        self.model = None
+        self.decoder = None
+        self.garbling_time_s = 0.0
+        if garble_me:
+            self.garble()
+
+    # -------------------------------------------------------------- offline
+    def garble(self):
+        specs = self.circuit.garble_specs()
+        t = time.perf_counter()
+        self.model = self.garbler.garble(specs, list(self.circuit.input_dims), self.nthreads)
+        self.garbling_time_s = time.perf_counter() - t
+        self.decoder = self.garbler.decoder()
+        return self.model
+
+    # --------------------------------------------------------------- online
+    def garble_inputs(self, x: np.ndarray) -> Labels:
+        x = np.asarray(x, dtype=np.int64).reshape(-1)
+        assert x.size == self.circuit.input_size, "input dimension does not match circuit input dimension"
+        return self.garbler.encode(x)
+
+    def cpu_evaluate(self, labels: Labels, nr_threads: int = 0) -> Labels:
+        return self._n.cpu_evaluate(self.model, labels, nr_threads)
+
+    def decode_outputs(self, labels: Labels) -> np.ndarray:
+        return self.decoder.decode(labels)
+
+    # ------------------------------------------------------------------ HIP
+    def hip_evaluator(self, **kw):
+        from ..runtime import HipEvaluator
+
+        return HipEvaluator([self.model], **kw)
+
+    # -------------------------------------------------------------- helpers
+    @property
+    def table_bytes(self) -> int:
+        return self.model.table_bytes()
+
+    def plain_q_eval(self, x: np.ndarray) -> np.ndarray:
+        return self.circuit.plain_q_eval(x, track=False, crt_modulus=self.crt_modulus)
+
+
+def garble(circuit: Circuit, crt, mrs=None, **kw) -> GarbledCircuit:
+    return GarbledCircuit(circuit, crt, mrs, **kw)

@@ -1,0 +1,146 @@
+"""Circuit container: plaintext / quantized evaluation, accuracy, CRT sizing and
+quantization search. Reference: circuit/circuit.h (C12)."""
+from __future__ import annotations
+
+from typing import Optional, Sequence
+
+import numpy as np
+
+from .bases import crt_modulus, first_primes
+from .layers import Layer
+from .quant import quantize_simple
+
+
+class Circuit:
+    def __init__(self, layers: Sequence[Layer], q_parameter: int = -1):
+        self.layers = list(layers)
+        assert self.layers, "circuit needs at least one layer"
+        self.q_parameter = q_parameter
+        self.input_dims = self.layers[0].in_dims
+        self.output_dims = self.layers[-1].out_dims
+
+    @property
+    def input_size(self) -> int:
+        return self.layers[0].in_size
+
+    @property
+    def output_size(self) -> int:
+        return self.layers[-1].out_size
+
+    def __len__(self):
+        return len(self.layers)
+
+    def __iter__(self):
+        return iter(self.layers)
+
+    # ---------------------------------------------------------------- eval
+    def plain_eval(self, x: np.ndarray, track: bool = True) -> np.ndarray:
+        x = np.asarray(x, dtype=np.float32).reshape(-1)
+        assert x.size == self.input_size, "input size does not match circuit input size"
+        ctx = [x]
+        for layer in self.layers:
+            x = layer.plain_eval(x, track, ctx)
+            ctx.append(x)
+        return x
+
+    def plain_q_eval(self, x: np.ndarray, track: bool = True, crt_modulus: Optional[int] = None) -> np.ndarray:
+        """Quantized evaluation. With `crt_modulus` the CRT-rescale semantics of
+        the garbled circuit are reproduced exactly (see layers.Rescale)."""
+        x = np.asarray(x, dtype=np.int64).reshape(-1)
+        assert x.size == self.input_size, "input size does not match circuit input size"
+        ctx = [x]
+        for layer in self.layers:
+            x = layer.plain_q_eval(x, track, ctx, crt_modulus)
+            ctx.append(x)
+        return x
+
+    def plain_test(self, inputs, labels) -> float:
+        return float(np.mean([int(np.argmax(self.plain_eval(x, False)) == int(l)) for x, l in zip(inputs, labels)]))
+
+    def plain_q_test(self, inputs, labels, crt_modulus: Optional[int] = None) -> float:
+        return float(np.mean([int(np.argmax(self.plain_q_eval(x, False, crt_modulus)) == int(l))
+                              for x, l in zip(inputs, labels)]))
+
+    def compute_q_acc(self, x, q_x, q_constant: float, error_bound: float = 1.0) -> float:
+        out = self.plain_eval(x)
+        rec = self.plain_q_eval(q_x).astype(np.float32) * q_constant
+        rel = np.abs(out - rec) / np.abs(out)
+        return float(np.mean(rel < error_bound))
+
+    # ---------------------------------------------------------- ranges / CRT
+    def reset_ranges(self):
+        for layer in self.layers:
+            layer.reset_ranges()
+
+    def get_min_plain_q_val(self) -> int:
+        return min(l.get_min_plain_q_val() for l in self.layers)
+
+    def get_max_plain_q_val(self) -> int:
+        return max(l.get_max_plain_q_val() for l in self.layers)
+
+    def required_crt_modulus(self) -> int:
+        return 2 * max(abs(self.get_min_plain_q_val()), abs(self.get_max_plain_q_val()))
+
+    def infer_crt_base_size(self, inputs, max_k: int = 11, assert_bound: bool = True) -> int:
+        """Smallest k such that the product of the first k primes covers every
+        tracked intermediate value (circuit.h:159-265)."""
+        if isinstance(inputs, np.ndarray) and inputs.ndim == 1:
+            inputs = [inputs]
+        for x in inputs:
+            self.plain_q_eval(x, True)
+        need = self.required_crt_modulus()
+        k = 0
+        M = 0
+        while M < need:
+            k += 1
+            if k > (max_k if assert_bound else 100):
+                if assert_bound:
+                    raise ValueError("inferred CRT base size too large; optimize the quantization constant")
+                return -1
+            M = crt_modulus(first_primes(k))
+        return max(k, 1)
+
+    def quantize(self, q_const: float):
+        for layer in self.layers:
+            layer.quantize(q_const)
+
+    def get_q_const(self) -> float:
+        for layer in self.layers:
+            if layer.get_q_const() != 0:
+                return layer.get_q_const()
+        return 0.0
+
+    def optimize_quantization(self, target_k: int, inputs, init_q: float = 0.2, init_step: float = 0.01,
+                              final_step: float = 1e-5, nr_samples: int = -1) -> float:
+        """Step search on the SimpleQuant constant until the inferred CRT size
+        equals `target_k` with step <= final_step (circuit.h:273-311)."""
+        step, k, q, last_q = init_step, -1, init_q, init_q
+        self.quantize(q)
+        eps = np.finfo(np.float64).eps
+        samples = inputs if nr_samples < 0 else inputs[:nr_samples]
+        for _ in range(100000):
+            if k == target_k and step <= final_step:
+                break
+            assert q != 0, "q_val cannot be 0"
+            self.reset_ranges()
+            qin = [quantize_simple(x, q) for x in samples]
+            k = self.infer_crt_base_size(qin, assert_bound=False)
+            if k == -1:
+                self.quantize(last_q)
+                return last_q
+            if k > target_k:
+                if abs(last_q - (q + step)) < eps:
+                    step /= 2
+                last_q, q = q, q + step
+            else:
+                if abs(last_q - (q - step)) < eps or abs(q - step) < eps:
+                    step /= 2
+                last_q, q = q, q - step
+            self.quantize(q)
+        return q
+
+    def garble_specs(self) -> list:
+        return [l.garble_spec() for l in self.layers]
+
+    def __repr__(self) -> str:
+        return "Circuit(\n  " + "\n  ".join(repr(l) for l in self.layers) + "\n)"
