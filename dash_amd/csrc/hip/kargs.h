@@ -1,0 +1,103 @@
+// Kernel argument structs shared by the HIP kernels and the host runtime.
+#pragma once
+
+#include <stdint.h>
+
+#include "dev.h"
+
+namespace dash {
+namespace dev {
+
+constexpr int kMaxRes = 16;   // max CRT residues on the GPU path
+constexpr int kMaxMrs = 16;
+constexpr int kMaxOut = 16;
+
+// Residue-major activation description: act[j] -> int16 [B][n_j][N]
+struct Act {
+    int16_t* p[kMaxRes];
+    int64_t N;  // elements per GC
+};
+
+struct CrtInfo {
+    int k;
+    int p[kMaxRes];
+    int n[kMaxRes];
+    int prefix[kMaxRes];
+    int sum;
+};
+
+struct SignArgs {
+    CrtInfo crt;
+    int t;
+    int mrs[kMaxMrs];
+    int nout;
+    int out_mod[kMaxOut];
+    int64_t N;           // elements
+    int B;
+    int64_t n_approx, n_cast, n_sign;  // table entries per element
+    const u128* approx;  // [B][N][n_approx]
+    const u128* cast1;   // [B][N][n_cast]
+    const u128* cast2;
+    const u128* sign;    // [B][N][n_sign]
+    u128* mrsP;          // [B][k][t][N] compressed approx outputs
+    u128* hx;            // [B][k][N] H(compress(x_j)) (ReLU reuse) - may be null
+    uint16_t* colx;      // [B][k][N]
+    u128* outP;          // [B][nout][N] compressed sign outputs
+    u128* hs;            // [B][N] H(compress(sign mod 2)) when relu != 0
+    uint8_t* cs;         // [B][N]
+    const u128* zc;      // [B][zc_stride] compressed zero labels, indexed by modulus
+    const uint16_t* zcol;  // [B][zc_stride] zero-label colors
+    int zc_stride;
+    int relu;            // also produce hs / cs for the ReLU multiply
+};
+
+struct RescaleArgs {
+    CrtInfo crt;
+    int64_t N;
+    int fi, s;
+    int add_up;
+    int active[kMaxRes];   // 1 if residue is processed by this factor
+    int aidx[kMaxRes];     // index among active residues (table offset / s)
+    int inv[kMaxRes];      // s^-1 mod p_j
+    int64_t n_trans, off;  // entries per element, offset of this factor
+    const u128* trans;     // [B][N][n_trans]
+    const u128* h0;
+    const uint16_t* col0;
+    const int16_t* up;     // [B][sum n] per-GC upshift labels (residue-concatenated)
+    const int16_t* zero;   // [B][sum n] zero labels of the CRT moduli
+    int lab_stride;        // sum_j n_j
+    int lab_off[kMaxRes];  // offset of residue j inside up/zero rows
+};
+
+struct BEArgs {
+    int E, nonext;
+    int swapped[kMaxRes];    // moduli in MRS order
+    int src[kMaxRes];        // residue index of position i
+    int inv[kMaxRes][kMaxRes];  // inv_partial[i][j]
+    int nextra;
+    int extra_pos[kMaxRes];  // position (in swapped order) of extra residue x
+    int extra_res[kMaxRes];  // residue index of extra x
+    int invv[kMaxRes];
+    int64_t N, n_tab;
+    const u128* tab;         // [B][N][n_tab]
+    int16_t* work;
+};
+
+struct ProjArgs {
+    int k;
+    int pin[kMaxRes], pout[kMaxRes];
+    const u128* tab[kMaxRes];  // [B][N][pin_j]
+    int64_t N;
+};
+
+struct MultArgs {
+    CrtInfo crt;
+    int64_t No;  // outputs per GC
+    int q;       // 0 = same-modulus multiply, else mixed with modulus q
+    const u128* t;  // [B][No][sum]   (mixed only)
+    const u128* g;  // [B][No][sum]
+    const u128* e;  // same: [B][No][sum]; mixed: [B][No][k][q+1]
+};
+
+}  // namespace dev
+}  // namespace dash

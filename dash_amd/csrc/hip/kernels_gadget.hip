@@ -1,0 +1,460 @@
+// Gadget kernels for gfx950: approximate sign (3 phases), ReLU multiply,
+// rescale (legacy sign-BE and ReDash base extension), projection and
+// multiplication test gates.
+//
+// Work decomposition (vs the reference's one-stream-per-residue launches,
+// sign_gadget.h:737-795, garbled_relu.h:258-294):
+//   phase A  one lane per (GC, residue, element): ONE hash per input label,
+//            reused for all |mrs| approx projections and later for the ReLU
+//            garbler half-gate (the reference hashes the same key |mrs|+1
+//            times); outputs stay compressed (u128).
+//   phase B  one lane per (GC, element): the serial mixed-radix carry chain,
+//            fully in registers, no device malloc (reference uses new[]).
+//   phase C  one lane per (GC, residue, element): ReLU mixed-mod multiply, no
+//            AES at all (hashes come from phases A/B).
+#include "kargs.h"
+#include "launch.h"
+
+namespace dash {
+namespace dev {
+
+#define AES_PROLOGUE(tab, rk)                    \
+    extern __shared__ uint32_t lds_aes[];         \
+    aes_lds_fill(lds_aes, tab);                   \
+    const AesCtx aes = aes_ctx(lds_aes, rk)
+
+// ---------------------------------------------------------------------------
+// Phase A: approximate residues. grid (ceil(N/256), k, B)
+__global__ __launch_bounds__(256) void k_sign_approx(SignArgs a, Act x, const ModC* mc, const uint32_t* te0,
+                                                     const uint32_t* rk) {
+    AES_PROLOGUE(te0, rk);
+    const int j = blockIdx.y, b = blockIdx.z;
+    const int64_t N = a.N;
+    const int64_t e = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (e >= N) return;
+    const int p = a.crt.p[j];
+    const ModC m = mc[p];
+    const int16_t* L = x.p[j] + static_cast<int64_t>(b) * m.n * N + e;
+    const u128 C = compress_cm(L, N, m);
+    const u128 H = aes_encrypt(aes, C);
+    const uint32_t col = static_cast<uint16_t>(L[0]) % static_cast<uint32_t>(p);
+    const int64_t bke = (static_cast<int64_t>(b) * a.crt.k + j) * N + e;
+    if (a.hx) {
+        a.hx[bke] = H;
+        a.colx[bke] = static_cast<uint16_t>(col);
+    }
+    const u128* T = a.approx + (static_cast<int64_t>(b) * N + e) * a.n_approx + static_cast<int64_t>(a.t) * a.crt.prefix[j];
+    u128* out = a.mrsP + (static_cast<int64_t>(b) * a.crt.k + j) * a.t * N + e;
+    for (int d = 0; d < a.t; ++d) out[static_cast<int64_t>(d) * N] = T[d * p + col] - H;
+}
+
+// ---------------------------------------------------------------------------
+// Phase B: mixed-radix carry chain + sign projection. grid (ceil(N/128), 1, B)
+template <int MAXN>
+__global__ __launch_bounds__(128) void k_sign_chain(SignArgs a, const ModC* mc, const uint32_t* te0,
+                                                    const uint32_t* rk) {
+    AES_PROLOGUE(te0, rk);
+    const int b = blockIdx.z;
+    const int64_t N = a.N;
+    const int64_t e = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (e >= N) return;
+    const int k = a.crt.k, t = a.t;
+    const u128* T1 = a.cast1 + (static_cast<int64_t>(b) * N + e) * a.n_cast;
+    const u128* T2 = a.cast2 + (static_cast<int64_t>(b) * N + e) * a.n_cast;
+    const u128* P0 = a.mrsP + static_cast<int64_t>(b) * k * t * N + e;  // + (j*t + d)*N
+    const int mlast = a.mrs[t - 1];
+    u128 carry = a.zc[static_cast<int64_t>(b) * a.zc_stride + mlast];
+    uint32_t ccol = a.zcol[static_cast<int64_t>(b) * a.zc_stride + mlast];
+    int32_t acc[MAXN];
+    int64_t c1 = 0, c2 = 0;
+    for (int d = t - 1; d >= 1; --d) {
+        const int m = a.mrs[d];
+        const int mo = (k + 1) * m;
+        const ModC Mm = mc[m];
+        const ModC Mo = mc[mo];
+#pragma unroll
+        for (int i = 0; i < MAXN; ++i) acc[i] = 0;
+        for (int j = 0; j <= k; ++j) {
+            u128 key;
+            uint32_t col;
+            if (j < k) {
+                key = P0[(static_cast<int64_t>(j) * t + d) * N];
+                col = u128_mod(key, Mm);
+            } else {
+                key = carry;
+                col = ccol;
+            }
+            const u128 H = aes_encrypt(aes, key);
+            const u128 P = T1[c1 + col] - H;
+            c1 += m;
+            DigitStream s;
+            s.init(P);
+#pragma unroll
+            for (int i = 0; i < MAXN; ++i)
+                if (i < static_cast<int>(Mo.n)) acc[i] += static_cast<int32_t>(s.next(Mo));
+        }
+        CompressFwd cf;
+        cf.init();
+#pragma unroll
+        for (int i = 0; i < MAXN; ++i)
+            if (i < static_cast<int>(Mo.n)) cf.push(static_cast<uint32_t>(acc[i]) % mo, Mo);
+        const u128 key2 = cf.finish();
+        const uint32_t col2 = static_cast<uint32_t>(acc[0]) % mo;
+        const u128 H2 = aes_encrypt(aes, key2);
+        carry = T2[c2 + col2] - H2;
+        c2 += mo;
+        ccol = u128_mod(carry, mc[a.mrs[d - 1]]);
+    }
+    // most significant digit: sum = carry + sum_j mrs[j][0]
+    const int m0 = a.mrs[0];
+    const ModC M0 = mc[m0];
+#pragma unroll
+    for (int i = 0; i < MAXN; ++i) acc[i] = 0;
+    for (int j = 0; j <= k; ++j) {
+        const u128 P = j < k ? P0[static_cast<int64_t>(j) * t * N] : carry;
+        DigitStream s;
+        s.init(P);
+#pragma unroll
+        for (int i = 0; i < MAXN; ++i)
+            if (i < static_cast<int>(M0.n)) acc[i] += static_cast<int32_t>(s.next(M0));
+    }
+    CompressFwd cf;
+    cf.init();
+#pragma unroll
+    for (int i = 0; i < MAXN; ++i)
+        if (i < static_cast<int>(M0.n)) cf.push(static_cast<uint32_t>(acc[i]) % m0, M0);
+    const u128 key = cf.finish();
+    const uint32_t col = static_cast<uint32_t>(acc[0]) % m0;
+    const u128 H = aes_encrypt(aes, key);
+    const u128* TS = a.sign + (static_cast<int64_t>(b) * N + e) * a.n_sign;
+    for (int o = 0; o < a.nout; ++o) {
+        const u128 P = TS[o * m0 + col] - H;
+        a.outP[(static_cast<int64_t>(b) * a.nout + o) * N + e] = P;
+        if (a.relu && o == 0) {
+            a.hs[static_cast<int64_t>(b) * N + e] = aes_encrypt(aes, P);
+            a.cs[static_cast<int64_t>(b) * N + e] = static_cast<uint8_t>(static_cast<uint32_t>(P) & 1u);
+        }
+    }
+}
+
+// Decompress compressed outputs into residue activations. grid (ceil(N/256), nres, B)
+__global__ __launch_bounds__(256) void k_unpack(const u128* P, int nres, Act out, CrtInfo mods, const ModC* mc,
+                                                int64_t N) {
+    const int j = blockIdx.y, b = blockIdx.z;
+    const int64_t e = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (e >= N) return;
+    const ModC m = mc[mods.p[j]];
+    DigitStream s;
+    s.init(P[(static_cast<int64_t>(b) * nres + j) * N + e]);
+    int16_t* o = out.p[j] + static_cast<int64_t>(b) * m.n * N + e;
+    for (int i = 0; i < static_cast<int>(m.n); ++i) o[i * N] = static_cast<int16_t>(s.next(m));
+}
+
+// ---------------------------------------------------------------------------
+// Phase C: ReLU = x * sign01(x) via the mixed-modulus half gate.
+// grid (ceil(N/256), k, B)
+__global__ __launch_bounds__(256) void k_relu_mult(SignArgs a, Act x, Act y, const u128* gtab, const u128* etab,
+                                                   const ModC* mc) {
+    const int j = blockIdx.y, b = blockIdx.z;
+    const int64_t N = a.N;
+    const int64_t e = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (e >= N) return;
+    const int k = a.crt.k;
+    const int p = a.crt.p[j];
+    const ModC m = mc[p];
+    const int64_t bke = (static_cast<int64_t>(b) * k + j) * N + e;
+    const u128 Hx = a.hx[bke];
+    const uint32_t colx = a.colx[bke];
+    const u128 HS = a.hs[static_cast<int64_t>(b) * N + e];
+    const uint32_t cS = a.cs[static_cast<int64_t>(b) * N + e];
+    const int64_t be = static_cast<int64_t>(b) * N + e;
+    const u128 G = gtab[be * a.crt.sum + a.crt.prefix[j] + colx] - Hx;
+    const u128* E3 = etab + (be * k + j) * 3;
+    const u128 E = E3[cS] - HS;
+    const u128 mini = E3[2];
+    const int16_t t16 = static_cast<int16_t>(static_cast<uint16_t>(mini >> (16 * cS)));
+    const int16_t ypr16 = static_cast<int16_t>(t16 - static_cast<int16_t>(static_cast<uint16_t>(HS)));
+    int32_t ypr = ypr16 % p;
+    if (ypr < 0) ypr += p;
+    const int16_t* X = x.p[j] + static_cast<int64_t>(b) * m.n * N + e;
+    int16_t* Y = y.p[j] + static_cast<int64_t>(b) * m.n * N + e;
+    DigitStream sg, se;
+    sg.init(G);
+    se.init(E);
+    for (int i = 0; i < static_cast<int>(m.n); ++i) {
+        const int32_t g = static_cast<int32_t>(sg.next(m));
+        const int32_t ev = static_cast<int32_t>(se.next(m));
+        const int32_t xi = X[i * N];
+        int32_t v = (ev + ypr * xi - g) % p;
+        if (v < 0) v += p;
+        Y[i * N] = static_cast<int16_t>(v);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Rescale step 1+2 for one factor: hash the factor residue (optionally after
+// the upshift). grid (ceil(N/256), 1, B)
+__global__ __launch_bounds__(256) void k_rescale_hash(Act x, int fi, int s, const int16_t* up, int up_stride,
+                                                      int add_up, int64_t N, u128* h0, uint16_t* col0,
+                                                      const ModC* mc, const uint32_t* te0, const uint32_t* rk) {
+    AES_PROLOGUE(te0, rk);
+    const int b = blockIdx.z;
+    const int64_t e = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (e >= N) return;
+    const ModC m = mc[s];
+    const int16_t* L = x.p[fi] + static_cast<int64_t>(b) * m.n * N + e;
+    const int16_t* U = up + static_cast<int64_t>(b) * up_stride;
+    // compress of (L + up) mod s, reverse Horner
+    u128 C = 0;
+    uint32_t c0 = 0;
+    for (int i = static_cast<int>(m.n) - 1; i >= 0; --i) {
+        uint32_t d = static_cast<uint16_t>(L[i * N]);
+        if (add_up) {
+            d += static_cast<uint16_t>(U[i]);
+            if (d >= static_cast<uint32_t>(s)) d -= s;
+        }
+        if (m.bits)
+            C = (C << m.bits) | d;
+        else
+            C = C * static_cast<u128>(s) + d;
+        c0 = d;
+    }
+    h0[static_cast<int64_t>(b) * N + e] = aes_encrypt(aes, C);
+    col0[static_cast<int64_t>(b) * N + e] = static_cast<uint16_t>(c0);
+}
+
+
+// grid (ceil(N/256), k, B)
+__global__ __launch_bounds__(256) void k_rescale_update(RescaleArgs a, Act x, const ModC* mc) {
+    const int j = blockIdx.y, b = blockIdx.z;
+    const int64_t N = a.N;
+    const int64_t e = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (e >= N) return;
+    const int p = a.crt.p[j];
+    const ModC m = mc[p];
+    int16_t* L = x.p[j] + static_cast<int64_t>(b) * m.n * N + e;
+    const int16_t* U = a.up + static_cast<int64_t>(b) * a.lab_stride + a.lab_off[j];
+    if (j == a.fi) {
+        const int16_t* Zl = a.zero + static_cast<int64_t>(b) * a.lab_stride + a.lab_off[j];
+        for (int i = 0; i < static_cast<int>(m.n); ++i) L[i * N] = Zl[i];
+        return;
+    }
+    if (!a.active[j]) return;  // residue of an earlier factor (already zero)
+    const int64_t be = static_cast<int64_t>(b) * N + e;
+    const u128 P = a.trans[be * a.n_trans + a.off + static_cast<int64_t>(a.aidx[j]) * a.s + a.col0[be]] - a.h0[be];
+    DigitStream s;
+    s.init(P);
+    const int32_t inv = a.inv[j];
+    for (int i = 0; i < static_cast<int>(m.n); ++i) {
+        int32_t v = L[i * N];
+        if (a.add_up) v += U[i];
+        v -= static_cast<int32_t>(s.next(m));
+        v = (v % p + p) % p;
+        L[i * N] = static_cast<int16_t>((v * inv) % p);
+    }
+}
+
+// Downshift (and, for sign base extension, install the recovered mod-2 residue).
+// grid (ceil(N/256), k, B)
+__global__ __launch_bounds__(256) void k_rescale_post(Act x, CrtInfo crt, int64_t N, const u128* signP,
+                                                      const int16_t* down, int lab_stride, const int* lab_off,
+                                                      const ModC* mc) {
+    const int j = blockIdx.y, b = blockIdx.z;
+    const int64_t e = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (e >= N) return;
+    const int p = crt.p[j];
+    const ModC m = mc[p];
+    int16_t* L = x.p[j] + static_cast<int64_t>(b) * m.n * N + e;
+    const int16_t* D = down + static_cast<int64_t>(b) * lab_stride + lab_off[j];
+    if (j == 0 && signP) {
+        DigitStream s;
+        s.init(signP[static_cast<int64_t>(b) * N + e]);
+        for (int i = 0; i < static_cast<int>(m.n); ++i) {
+            int32_t v = static_cast<int32_t>(s.next(m)) - D[i];
+            L[i * N] = static_cast<int16_t>(v < 0 ? v + p : v);
+        }
+        return;
+    }
+    for (int i = 0; i < static_cast<int>(m.n); ++i) {
+        int32_t v = L[i * N] - D[i];
+        L[i * N] = static_cast<int16_t>(v < 0 ? v + p : v);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// ReDash base extension (MRS conversion). One lane per (GC, element); the
+// working copies live in `work` (component-major, [B][E][128][N]).
+
+__global__ __launch_bounds__(128) void k_base_ext(BEArgs a, Act x, const ModC* mc, const uint32_t* te0,
+                                                  const uint32_t* rk) {
+    AES_PROLOGUE(te0, rk);
+    const int b = blockIdx.z;
+    const int64_t N = a.N;
+    const int64_t e = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (e >= N) return;
+    const int E = a.E;
+    auto W = [&](int pos) { return a.work + ((static_cast<int64_t>(b) * E + pos) * 128) * N + e; };
+    for (int i = 0; i < E; ++i) {
+        const ModC m = mc[a.swapped[i]];
+        const int16_t* src = x.p[a.src[i]] + static_cast<int64_t>(b) * m.n * N + e;
+        int16_t* w = W(i);
+        for (int c = 0; c < static_cast<int>(m.n); ++c) w[c * N] = src[c * N];
+    }
+    const u128* T = a.tab + (static_cast<int64_t>(b) * N + e) * a.n_tab;
+    int64_t off = 0;
+    for (int i = 0; i < a.nonext; ++i) {
+        const ModC mi = mc[a.swapped[i]];
+        const int16_t* li = W(i);
+        const u128 H = aes_encrypt(aes, compress_cm(li, N, mi));
+        const uint32_t col = static_cast<uint16_t>(li[0]);
+        for (int j = 0; j < E - i - 1; ++j) {
+            const int tg = i + j + 1;
+            const int q = a.swapped[tg];
+            const ModC mo = mc[q];
+            const u128 P = T[off + col] - H;
+            off += mi.q;
+            DigitStream s;
+            s.init(P);
+            int16_t* lt = W(tg);
+            const int32_t inv = a.inv[i][j];
+            for (int c = 0; c < static_cast<int>(mo.n); ++c) {
+                int32_t v = lt[c * N] - static_cast<int32_t>(s.next(mo));
+                if (v < 0) v += q;
+                lt[c * N] = static_cast<int16_t>((v * inv) % q);
+            }
+        }
+    }
+    for (int xi = 0; xi < a.nextra; ++xi) {
+        const int r = a.extra_res[xi];
+        const int q = a.swapped[a.extra_pos[xi]];
+        const ModC m = mc[q];
+        const int16_t* w = W(a.extra_pos[xi]);
+        int16_t* dst = x.p[r] + static_cast<int64_t>(b) * m.n * N + e;
+        const int32_t f = a.invv[xi];  // already negated mod q on the host
+        for (int c = 0; c < static_cast<int>(m.n); ++c) dst[c * N] = static_cast<int16_t>((w[c * N] * f) % q);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Generic projection layer (test-only Projection). grid (ceil(N/256), k, B)
+__global__ __launch_bounds__(256) void k_proj(ProjArgs a, Act x, Act y, const ModC* mc, const uint32_t* te0,
+                                              const uint32_t* rk) {
+    AES_PROLOGUE(te0, rk);
+    const int j = blockIdx.y, b = blockIdx.z;
+    const int64_t N = a.N;
+    const int64_t e = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (e >= N) return;
+    const ModC mi = mc[a.pin[j]], mo = mc[a.pout[j]];
+    const int16_t* L = x.p[j] + static_cast<int64_t>(b) * mi.n * N + e;
+    const u128 H = aes_encrypt(aes, compress_cm(L, N, mi));
+    const uint32_t col = static_cast<uint16_t>(L[0]) % mi.q;
+    const u128 P = a.tab[j][(static_cast<int64_t>(b) * N + e) * mi.q + col] - H;
+    DigitStream s;
+    s.init(P);
+    int16_t* O = y.p[j] + static_cast<int64_t>(b) * mo.n * N + e;
+    for (int i = 0; i < static_cast<int>(mo.n); ++i) O[i * N] = static_cast<int16_t>(s.next(mo));
+}
+
+// Generalized half-gate product of pairs (2e, 2e+1), and the mixed-modulus
+// variant (second operand first projected to Z_q). grid (ceil(No/256), k, B)
+__global__ __launch_bounds__(256) void k_mult(MultArgs a, Act x, Act y, const ModC* mc, const uint32_t* te0,
+                                              const uint32_t* rk) {
+    AES_PROLOGUE(te0, rk);
+    const int j = blockIdx.y, b = blockIdx.z;
+    const int64_t No = a.No, Ni = 2 * No;
+    const int64_t o = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (o >= No) return;
+    const int p = a.crt.p[j];
+    const ModC m = mc[p];
+    const int16_t* X = x.p[j] + static_cast<int64_t>(b) * m.n * Ni + 2 * o;
+    const int16_t* Yv = X + 1;
+    const int64_t bo = static_cast<int64_t>(b) * No + o;
+    const u128 Hx = aes_encrypt(aes, compress_cm(X, Ni, m));
+    const uint32_t colx = static_cast<uint16_t>(X[0]) % p;
+    const u128 G = a.g[bo * a.crt.sum + a.crt.prefix[j] + colx] - Hx;
+    u128 E;
+    int32_t ypr;
+    if (a.q == 0) {
+        const u128 Hy = aes_encrypt(aes, compress_cm(Yv, Ni, m));
+        const uint32_t coly = static_cast<uint16_t>(Yv[0]) % p;
+        E = a.e[bo * a.crt.sum + a.crt.prefix[j] + coly] - Hy;
+        ypr = static_cast<int32_t>(coly);
+    } else {
+        const ModC mq = mc[a.q];
+        const u128 Hy = aes_encrypt(aes, compress_cm(Yv, Ni, m));
+        const uint32_t coly = static_cast<uint16_t>(Yv[0]) % p;
+        const u128 Pt = a.t[bo * a.crt.sum + a.crt.prefix[j] + coly] - Hy;  // compressed label mod q
+        const u128 Ht = aes_encrypt(aes, Pt);
+        const uint32_t colt = u128_mod(Pt, mq);
+        const u128* E3 = a.e + (bo * a.crt.k + j) * (a.q + 1);
+        E = E3[colt] - Ht;
+        const int16_t t16 = static_cast<int16_t>(static_cast<uint16_t>(E3[a.q] >> (16 * colt)));
+        ypr = static_cast<int16_t>(t16 - static_cast<int16_t>(static_cast<uint16_t>(Ht)));
+        ypr %= p;
+        if (ypr < 0) ypr += p;
+    }
+    DigitStream sg, se;
+    sg.init(G);
+    se.init(E);
+    int16_t* O = y.p[j] + static_cast<int64_t>(b) * m.n * No + o;
+    for (int i = 0; i < static_cast<int>(m.n); ++i) {
+        const int32_t gv = static_cast<int32_t>(sg.next(m));
+        const int32_t ev = static_cast<int32_t>(se.next(m));
+        int32_t v = (ev + ypr * static_cast<int32_t>(X[i * Ni]) - gv) % p;
+        if (v < 0) v += p;
+        O[i * No] = static_cast<int16_t>(v);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// launchers
+static inline dim3 grid_for(int64_t n, int bs, int y, int z) {
+    return dim3(static_cast<unsigned>((n + bs - 1) / bs), y, z);
+}
+constexpr size_t kAesLds = DASH_AES_LDS_WORDS * sizeof(uint32_t);
+
+void launch_sign_approx(const SignArgs& a, const Act& x, const ModC* mc, const AesGlobals& g, hipStream_t st) {
+    hipLaunchKernelGGL(k_sign_approx, grid_for(a.N, 256, a.crt.k, a.B), dim3(256), kAesLds, st, a, x, mc, g.te0, g.rk);
+}
+void launch_sign_chain(const SignArgs& a, int maxn, const ModC* mc, const AesGlobals& g, hipStream_t st) {
+    dim3 gr = grid_for(a.N, 128, 1, a.B);
+    if (maxn <= 32)
+        hipLaunchKernelGGL(k_sign_chain<32>, gr, dim3(128), kAesLds, st, a, mc, g.te0, g.rk);
+    else
+        hipLaunchKernelGGL(k_sign_chain<64>, gr, dim3(128), kAesLds, st, a, mc, g.te0, g.rk);
+}
+void launch_unpack(const u128* P, int nres, const Act& out, const CrtInfo& mods, const ModC* mc, int64_t N, int B,
+                   hipStream_t st) {
+    hipLaunchKernelGGL(k_unpack, grid_for(N, 256, nres, B), dim3(256), 0, st, P, nres, out, mods, mc, N);
+}
+void launch_relu_mult(const SignArgs& a, const Act& x, const Act& y, const u128* gtab, const u128* etab,
+                      const ModC* mc, hipStream_t st) {
+    hipLaunchKernelGGL(k_relu_mult, grid_for(a.N, 256, a.crt.k, a.B), dim3(256), 0, st, a, x, y, gtab, etab, mc);
+}
+void launch_rescale_hash(const Act& x, int fi, int s, const int16_t* up, int up_stride, int add_up, int64_t N, int B,
+                         u128* h0, uint16_t* col0, const ModC* mc, const AesGlobals& g, hipStream_t st) {
+    hipLaunchKernelGGL(k_rescale_hash, grid_for(N, 256, 1, B), dim3(256), kAesLds, st, x, fi, s, up, up_stride,
+                       add_up, N, h0, col0, mc, g.te0, g.rk);
+}
+void launch_rescale_update(const RescaleArgs& a, const Act& x, int B, const ModC* mc, hipStream_t st) {
+    hipLaunchKernelGGL(k_rescale_update, grid_for(a.N, 256, a.crt.k, B), dim3(256), 0, st, a, x, mc);
+}
+void launch_rescale_post(const Act& x, const CrtInfo& crt, int64_t N, int B, const u128* signP, const int16_t* down,
+                         int lab_stride, const int* lab_off, const ModC* mc, hipStream_t st) {
+    hipLaunchKernelGGL(k_rescale_post, grid_for(N, 256, crt.k, B), dim3(256), 0, st, x, crt, N, signP, down,
+                       lab_stride, lab_off, mc);
+}
+void launch_base_ext(const BEArgs& a, const Act& x, int B, const ModC* mc, const AesGlobals& g, hipStream_t st) {
+    hipLaunchKernelGGL(k_base_ext, grid_for(a.N, 128, 1, B), dim3(128), kAesLds, st, a, x, mc, g.te0, g.rk);
+}
+void launch_proj(const ProjArgs& a, const Act& x, const Act& y, int B, const ModC* mc, const AesGlobals& g,
+                 hipStream_t st) {
+    hipLaunchKernelGGL(k_proj, grid_for(a.N, 256, a.k, B), dim3(256), kAesLds, st, a, x, y, mc, g.te0, g.rk);
+}
+void launch_mult(const MultArgs& a, const Act& x, const Act& y, int B, const ModC* mc, const AesGlobals& g,
+                 hipStream_t st) {
+    hipLaunchKernelGGL(k_mult, grid_for(a.No, 256, a.crt.k, B), dim3(256), kAesLds, st, a, x, y, mc, g.te0, g.rk);
+}
+
+}  // namespace dev
+}  // namespace dash

@@ -1,0 +1,248 @@
+// Garbled linear layers: per-residue modular matrix products on labels.
+//   out = (sum_{w != 0 mod p} w * x  +  (#zero weights) * Z_p  +  bias_label) mod p
+// The (#zero weights) * Z_p term is the exact algebraic form of the
+// reference's per-term "add Z when w == 0 (mod p)" quirk
+// (misc/cuda_util.h:105-106, :239-244, label_tensor.h:806-808).
+//
+// Two conv paths:
+//   * VALU (any p): one lane per output position, weights uniform (SGPR).
+//   * MFMA int8 (p <= 255): implicit GEMM C[F][n] = W[F][K] * im2col(X)[K][n]
+//     on v_mfma_i32_16x16x64_i8 with both operands centered into [-127, 127]
+//     (products mod p are unchanged), int32 accumulation, mod-p epilogue fused
+//     with the zero-count and bias-label adds. n runs over (GC, component,
+//     output position) of one residue, so every residue is one large GEMM.
+#include "launch.h"
+
+namespace dash {
+namespace dev {
+
+struct ZMap {
+    int j[1024];
+    int c[1024];
+};
+
+__device__ __forceinline__ int32_t mod_p(int32_t v, int p) {
+    v %= p;
+    return v < 0 ? v + p : v;
+}
+
+// grid (ceil(O/256), 1, B*sum_n); z -> (b, j, c)
+__global__ __launch_bounds__(256) void k_dense(DenseArgs a, Act x, Act y, const int* zj, const int* zcomp, int sumn) {
+    const int z = blockIdx.z;
+    const int b = z / sumn, r = z % sumn;
+    const int j = zj[r], c = zcomp[r];
+    const int64_t o = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (o >= a.O) return;
+    const int p = a.crt.p[j], n = a.crt.n[j];
+    const int16_t* X = x.p[j] + (static_cast<int64_t>(b) * n + c) * a.K;
+    const int16_t* W = a.w[j];
+    int32_t acc = 0;
+    for (int64_t i = 0; i < a.K; ++i) {
+        const int64_t s = a.src ? a.src[i] : i;
+        acc += static_cast<int32_t>(W[i * a.O + o]) * X[s];
+        if ((i & 1023) == 1023) acc %= p;
+    }
+    const int32_t zc = a.zc[j][o];
+    const int16_t zv = a.zero[static_cast<int64_t>(b) * a.lab_stride + a.lab_off[j] + c];
+    const int16_t bv = a.bias[j][(static_cast<int64_t>(b) * a.O + o) * n + c];
+    y.p[j][(static_cast<int64_t>(b) * n + c) * a.O + o] = static_cast<int16_t>(mod_p(acc % p + zc * zv + bv, p));
+}
+
+// VALU conv: grid (ceil(OH*OW/256), F, B*sum_n)
+__global__ __launch_bounds__(256) void k_conv_valu(ConvArgs a, Act x, Act y, const int* zj, const int* zcomp,
+                                                   int sumn) {
+    const int z = blockIdx.z;
+    const int b = z / sumn, r = z % sumn;
+    const int j = zj[r], c = zcomp[r];
+    const int f = blockIdx.y;
+    const int pos = blockIdx.x * blockDim.x + threadIdx.x;
+    const int npos = a.OH * a.OW;
+    if (pos >= npos) return;
+    const int oy = pos / a.OW, ox = pos % a.OW;
+    const int p = a.crt.p[j], n = a.crt.n[j];
+    const int16_t* X = x.p[j] + (static_cast<int64_t>(b) * n + c) * a.C * a.H * a.W;
+    const int16_t* Wf = a.w[j] + static_cast<int64_t>(f) * a.C * a.kh * a.kw;
+    const int16_t zv = a.zero[static_cast<int64_t>(b) * a.lab_stride + a.lab_off[j] + c];
+    int32_t acc = 0;
+    for (int ci = 0; ci < a.C; ++ci) {
+        for (int dy = 0; dy < a.kh; ++dy) {
+            const int iy = oy * a.sh - a.ph + dy;
+            const bool rowok = iy >= 0 && iy < a.H;
+            for (int dx = 0; dx < a.kw; ++dx) {
+                const int ix = ox * a.sw - a.pw + dx;
+                const int32_t w = Wf[(ci * a.kh + dy) * a.kw + dx];
+                const int32_t v = (rowok && ix >= 0 && ix < a.W) ? X[(ci * a.H + iy) * a.W + ix] : zv;
+                acc += w * v;
+            }
+        }
+        if ((ci & 15) == 15) acc %= p;
+    }
+    const int32_t zc = a.zc[j][f];
+    const int16_t bv = a.bias[j][(static_cast<int64_t>(b) * a.F + f) * n + c];
+    y.p[j][((static_cast<int64_t>(b) * n + c) * a.F + f) * npos + pos] =
+        static_cast<int16_t>(mod_p(acc % p + zc * zv + bv, p));
+}
+
+// ---------------------------------------------------------------------------
+// MFMA implicit-GEMM conv (int8). Block = 256 threads = 4 waves; tile =
+// 64 filters x 64 columns; each wave owns a 16-filter x 64-column slab
+// (4 MFMA 16x16 tiles). Columns index (gc, comp, pos) of residue j.
+// A (weights) and the im2col B tile are staged in LDS per K-chunk of 64.
+typedef int32_t v4i __attribute__((ext_vector_type(4)));
+typedef int64_t v2l __attribute__((ext_vector_type(2)));
+
+__global__ __launch_bounds__(256) void k_conv_mfma(ConvArgs a, Act x, Act y, int j, int64_t ncols) {
+    __shared__ __attribute__((aligned(16))) int8_t As[64 * 64];   // [f][k]
+    __shared__ __attribute__((aligned(16))) int8_t Bs[64 * 64];   // [col][k]
+    const int p = a.crt.p[j], n = a.crt.n[j];
+    const int npos = a.OH * a.OW;
+    const int K = a.C * a.kh * a.kw;
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const int64_t col0 = static_cast<int64_t>(blockIdx.x) * 64;
+    const int f0 = blockIdx.y * 64;
+    const int half = p / 2;
+    // per-thread B-staging coordinates: thread stages column (tid & 63), k-rows (tid>>6)*16 .. +16
+    const int scol = tid & 63, sk0 = (tid >> 6) * 16;
+    const int64_t gcol = col0 + scol;
+    int sb = 0, sc = 0, soy = 0, sox = 0;
+    bool colok = gcol < ncols;
+    if (colok) {
+        const int64_t per_gc = static_cast<int64_t>(n) * npos;
+        sb = static_cast<int>(gcol / per_gc);
+        const int64_t r = gcol % per_gc;
+        sc = static_cast<int>(r / npos);
+        const int pos = static_cast<int>(r % npos);
+        soy = pos / a.OW;
+        sox = pos % a.OW;
+    }
+    const int16_t* X = x.p[j] + (static_cast<int64_t>(sb) * n + sc) * a.C * a.H * a.W;
+    const int16_t zv = colok ? a.zero[static_cast<int64_t>(sb) * a.lab_stride + a.lab_off[j] + sc] : 0;
+    const int8_t* W8 = a.w8[j];
+    v4i acc[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) acc[t] = v4i{0, 0, 0, 0};
+    for (int k0 = 0; k0 < a.Kpad; k0 += 64) {
+        // stage A: 64 filters x 64 k  (16 bytes per thread)
+        {
+            const int fr = tid >> 2, kc = (tid & 3) * 16;
+            const int f = f0 + fr;
+            v4i v = v4i{0, 0, 0, 0};
+            if (f < a.F) v = *reinterpret_cast<const v4i*>(W8 + static_cast<int64_t>(f) * a.Kpad + k0 + kc);
+            *reinterpret_cast<v4i*>(As + fr * 64 + kc) = v;
+        }
+        // stage B: im2col gather, centered int8
+        {
+            int8_t vals[16];
+#pragma unroll
+            for (int t = 0; t < 16; ++t) {
+                const int kk = k0 + sk0 + t;
+                int v = 0;
+                if (colok && kk < K) {
+                    const int ci = kk / (a.kh * a.kw), rr = kk % (a.kh * a.kw), dy = rr / a.kw, dx = rr % a.kw;
+                    const int iy = soy * a.sh - a.ph + dy, ix = sox * a.sw - a.pw + dx;
+                    v = (iy >= 0 && iy < a.H && ix >= 0 && ix < a.W) ? X[(ci * a.H + iy) * a.W + ix] : zv;
+                    if (v > half) v -= p;
+                }
+                vals[t] = static_cast<int8_t>(v);
+            }
+            *reinterpret_cast<v4i*>(Bs + scol * 64 + sk0) = *reinterpret_cast<v4i*>(vals);
+        }
+        __syncthreads();
+        // MFMA: wave owns filters [16*wave, +16), columns 64 (4 tiles of 16)
+        // operand maps (16x16x64 i8): lane l holds A[row l&15][k = 16*(l>>4) .. +16)
+        //                              and B[k = 16*(l>>4) .. +16)[col l&15]
+        const v2l av = *reinterpret_cast<const v2l*>(As + (wave * 16 + (lane & 15)) * 64 + (lane >> 4) * 16);
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            const v2l bv = *reinterpret_cast<const v2l*>(Bs + (t * 16 + (lane & 15)) * 64 + (lane >> 4) * 16);
+            acc[t] = __builtin_amdgcn_mfma_i32_16x16x64_i8(av, bv, acc[t], 0, 0, 0);
+        }
+        __syncthreads();
+    }
+    // epilogue: C/D map col = lane & 15, row = (lane >> 4) * 4 + r
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+        const int64_t col = col0 + t * 16 + (lane & 15);
+        if (col >= ncols) continue;
+        const int64_t per_gc = static_cast<int64_t>(n) * npos;
+        const int b = static_cast<int>(col / per_gc);
+        const int64_t rr = col % per_gc;
+        const int c = static_cast<int>(rr / npos);
+        const int pos = static_cast<int>(rr % npos);
+        const int16_t zvv = a.zero[static_cast<int64_t>(b) * a.lab_stride + a.lab_off[j] + c];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int f = f0 + wave * 16 + (lane >> 4) * 4 + r;
+            if (f >= a.F) continue;
+            const int32_t zc = a.zc[j][f];
+            const int16_t bv = a.bias[j][(static_cast<int64_t>(b) * a.F + f) * n + c];
+            y.p[j][((static_cast<int64_t>(b) * n + c) * a.F + f) * npos + pos] =
+                static_cast<int16_t>(mod_p(acc[t][r] % p + zc * zvv + bv, p));
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+namespace {
+struct ZTab {
+    int* dj = nullptr;
+    int* dc = nullptr;
+    int sumn = 0;
+    CrtInfo key{};
+};
+ZTab& ztab_for(const CrtInfo& crt, hipStream_t st) {
+    static thread_local ZTab t;
+    bool same = t.dj && t.key.k == crt.k;
+    for (int j = 0; same && j < crt.k; ++j) same = t.key.n[j] == crt.n[j];
+    if (!same) {
+        if (t.dj) {
+            (void)hipFree(t.dj);
+            (void)hipFree(t.dc);
+        }
+        int sumn = 0;
+        for (int j = 0; j < crt.k; ++j) sumn += crt.n[j];
+        std::vector<int> hj(sumn), hc(sumn);
+        int q = 0;
+        for (int j = 0; j < crt.k; ++j)
+            for (int c = 0; c < crt.n[j]; ++c, ++q) {
+                hj[q] = j;
+                hc[q] = c;
+            }
+        (void)hipMalloc(&t.dj, sumn * sizeof(int));
+        (void)hipMalloc(&t.dc, sumn * sizeof(int));
+        (void)hipMemcpy(t.dj, hj.data(), sumn * sizeof(int), hipMemcpyHostToDevice);
+        (void)hipMemcpy(t.dc, hc.data(), sumn * sizeof(int), hipMemcpyHostToDevice);
+        t.sumn = sumn;
+        t.key = crt;
+    }
+    (void)st;
+    return t;
+}
+}  // namespace
+
+void launch_dense(const DenseArgs& a, const Act& x, const Act& y, int B, hipStream_t st) {
+    ZTab& z = ztab_for(a.crt, st);
+    dim3 g(static_cast<unsigned>((a.O + 255) / 256), 1, static_cast<unsigned>(B * z.sumn));
+    hipLaunchKernelGGL(k_dense, g, dim3(256), 0, st, a, x, y, z.dj, z.dc, z.sumn);
+}
+
+void launch_conv(const ConvArgs& a, const Act& x, const Act& y, int B, hipStream_t st) {
+    if (a.use_mfma) {
+        for (int j = 0; j < a.crt.k; ++j) {
+            if (!a.w8[j]) continue;
+            const int64_t ncols = static_cast<int64_t>(B) * a.crt.n[j] * a.OH * a.OW;
+            dim3 g(static_cast<unsigned>((ncols + 63) / 64), static_cast<unsigned>((a.F + 63) / 64), 1);
+            hipLaunchKernelGGL(k_conv_mfma, g, dim3(256), 0, st, a, x, y, j, ncols);
+        }
+        // residues without an int8 image (p > 255) fall through to VALU below
+        bool rest = false;
+        for (int j = 0; j < a.crt.k; ++j) rest |= (a.w8[j] == nullptr);
+        if (!rest) return;
+    }
+    ZTab& z = ztab_for(a.crt, st);
+    dim3 g(static_cast<unsigned>((a.OH * a.OW + 255) / 256), static_cast<unsigned>(a.F), static_cast<unsigned>(B * z.sumn));
+    hipLaunchKernelGGL(k_conv_valu, g, dim3(256), 0, st, a, x, y, z.dj, z.dc, z.sumn);
+}
+
+}  // namespace dev
+}  // namespace dash

@@ -1,0 +1,147 @@
+// Free (non-cryptographic) label kernels: gathers, pair differences / sums
+// for the max-pool reduction tree, residual add, window sums, plus small
+// parity-test kernels for the AES and digit codecs.
+#include "launch.h"
+
+namespace dash {
+namespace dev {
+
+// out[b][j][c][o] = in[b][j][c][idx[o]]     grid (ceil(Nout*n_max/256), k, B)
+__global__ __launch_bounds__(256) void k_copy_gather(Act in, int64_t Nin, Act out, int64_t Nout, const int64_t* idx,
+                                                     CrtInfo crt) {
+    const int j = blockIdx.y, b = blockIdx.z;
+    const int n = crt.n[j];
+    const int64_t t = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (t >= Nout * n) return;
+    const int64_t c = t / Nout, o = t % Nout;
+    out.p[j][(static_cast<int64_t>(b) * n + c) * Nout + o] = in.p[j][(static_cast<int64_t>(b) * n + c) * Nin + idx[o]];
+}
+
+// d[..][o*ops+q] = v[..][o*cnt+2q+1] - v[..][o*cnt+2q]
+__global__ __launch_bounds__(256) void k_pair_diff(Act v, int64_t Nv, Act d, int64_t Nout, int ops, int cnt,
+                                                   CrtInfo crt) {
+    const int j = blockIdx.y, b = blockIdx.z;
+    const int n = crt.n[j], p = crt.p[j];
+    const int64_t Nd = Nout * ops;
+    const int64_t t = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (t >= Nd * n) return;
+    const int64_t c = t / Nd, e = t % Nd, o = e / ops, q = e % ops;
+    const int16_t* V = v.p[j] + (static_cast<int64_t>(b) * n + c) * Nv + o * cnt + 2 * q;
+    int32_t x = V[1] - V[0];
+    d.p[j][(static_cast<int64_t>(b) * n + c) * Nd + e] = static_cast<int16_t>(x < 0 ? x + p : x);
+}
+
+// nv[o*cnt1+q] = v[o*cnt+2q] + r[o*ops+q]; odd leftover copied to slot ops
+__global__ __launch_bounds__(256) void k_pair_add(Act v, int64_t Nv, Act r, Act nv, int64_t Nout, int ops, int cnt,
+                                                  int cnt1, CrtInfo crt) {
+    const int j = blockIdx.y, b = blockIdx.z;
+    const int n = crt.n[j], p = crt.p[j];
+    const int64_t Nn = Nout * cnt1, Nr = Nout * ops;
+    const int64_t t = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (t >= Nn * n) return;
+    const int64_t c = t / Nn, e = t % Nn, o = e / cnt1, q = e % cnt1;
+    const int16_t* V = v.p[j] + (static_cast<int64_t>(b) * n + c) * Nv + o * cnt;
+    int16_t val;
+    if (q < ops) {
+        int32_t x = V[2 * q] + r.p[j][(static_cast<int64_t>(b) * n + c) * Nr + o * ops + q];
+        val = static_cast<int16_t>(x >= p ? x - p : x);
+    } else {
+        val = V[cnt - 1];
+    }
+    nv.p[j][(static_cast<int64_t>(b) * n + c) * Nn + e] = val;
+}
+
+__global__ __launch_bounds__(256) void k_add(Act x, Act y, int64_t N, CrtInfo crt) {
+    const int j = blockIdx.y, b = blockIdx.z;
+    const int n = crt.n[j], p = crt.p[j];
+    const int64_t t = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (t >= N * n) return;
+    const int64_t off = static_cast<int64_t>(b) * n * N + t;
+    int32_t v = x.p[j][off] + y.p[j][off];
+    x.p[j][off] = static_cast<int16_t>(v >= p ? v - p : v);
+}
+
+// out[o] = sum_s in[idx[o*K+s]]
+__global__ __launch_bounds__(256) void k_window_sum(Act in, int64_t Nin, Act out, int64_t Nout, const int64_t* idx,
+                                                    int K, CrtInfo crt) {
+    const int j = blockIdx.y, b = blockIdx.z;
+    const int n = crt.n[j], p = crt.p[j];
+    const int64_t t = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (t >= Nout * n) return;
+    const int64_t c = t / Nout, o = t % Nout;
+    const int16_t* I = in.p[j] + (static_cast<int64_t>(b) * n + c) * Nin;
+    int32_t acc = 0;
+    for (int s = 0; s < K; ++s) acc += I[idx[o * K + s]];
+    out.p[j][(static_cast<int64_t>(b) * n + c) * Nout + o] = static_cast<int16_t>(acc % p);
+}
+
+__global__ __launch_bounds__(256) void k_aes_test(const u128* in, u128* out, int64_t n, const uint32_t* te0,
+                                                  const uint32_t* rk) {
+    extern __shared__ uint32_t lds_aes[];
+    aes_lds_fill(lds_aes, te0);
+    const AesCtx aes = aes_ctx(lds_aes, rk);
+    const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (i < n) out[i] = aes_encrypt(aes, in[i]);
+}
+
+// labels: component-major [n][N]; comp[e] = compress, decomp = decompress(comp)
+__global__ __launch_bounds__(256) void k_codec_test(const int16_t* L, int64_t N, int q, const ModC* mc, u128* comp,
+                                                    int16_t* decomp) {
+    const int64_t e = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (e >= N) return;
+    const ModC m = mc[q];
+    const u128 C = compress_cm(L + e, N, m);
+    comp[e] = C;
+    DigitStream s;
+    s.init(C);
+    CompressFwd f;
+    f.init();
+    for (int i = 0; i < static_cast<int>(m.n); ++i) {
+        uint32_t d = s.next(m);
+        decomp[i * N + e] = static_cast<int16_t>(d);
+        f.push(d, m);
+    }
+    // forward compress must agree with reverse Horner
+    if (f.finish() != C) decomp[e] = -1;
+}
+
+static inline dim3 g1(int64_t n, int y, int z) { return dim3(static_cast<unsigned>((n + 255) / 256), y, z); }
+static inline int64_t nmax(const CrtInfo& c) {
+    int m = 0;
+    for (int j = 0; j < c.k; ++j) m = c.n[j] > m ? c.n[j] : m;
+    return m;
+}
+
+void launch_copy_gather(const Act& in, int64_t Nin, const Act& out, int64_t Nout, const int64_t* idx,
+                        const CrtInfo& crt, int B, hipStream_t st) {
+    hipLaunchKernelGGL(k_copy_gather, g1(Nout * nmax(crt), crt.k, B), dim3(256), 0, st, in, Nin, out, Nout, idx, crt);
+}
+void launch_pair_diff(const Act& v, int64_t Nv, const Act& d, int64_t Nout, int ops, int cnt, const CrtInfo& crt,
+                      int B, hipStream_t st) {
+    hipLaunchKernelGGL(k_pair_diff, g1(Nout * ops * nmax(crt), crt.k, B), dim3(256), 0, st, v, Nv, d, Nout, ops, cnt,
+                       crt);
+}
+void launch_pair_add(const Act& v, int64_t Nv, const Act& r, const Act& nv, int64_t Nout, int ops, int cnt, int cnt1,
+                     const CrtInfo& crt, int B, hipStream_t st) {
+    hipLaunchKernelGGL(k_pair_add, g1(Nout * cnt1 * nmax(crt), crt.k, B), dim3(256), 0, st, v, Nv, r, nv, Nout, ops,
+                       cnt, cnt1, crt);
+}
+void launch_add(const Act& x, const Act& y, int64_t N, const CrtInfo& crt, int B, hipStream_t st) {
+    hipLaunchKernelGGL(k_add, g1(N * nmax(crt), crt.k, B), dim3(256), 0, st, x, y, N, crt);
+}
+void launch_window_sum(const Act& in, int64_t Nin, const Act& out, int64_t Nout, const int64_t* idx, int K,
+                       const CrtInfo& crt, int B, hipStream_t st) {
+    hipLaunchKernelGGL(k_window_sum, g1(Nout * nmax(crt), crt.k, B), dim3(256), 0, st, in, Nin, out, Nout, idx, K,
+                       crt);
+}
+void launch_aes_test(const u128* in, u128* out, int64_t n, const AesGlobals& g, hipStream_t st) {
+    hipLaunchKernelGGL(k_aes_test, g1(n, 1, 1), dim3(256), DASH_AES_LDS_WORDS * sizeof(uint32_t), st, in, out, n, g.te0,
+                       g.rk);
+}
+void launch_codec_test(const int16_t* labels, int64_t N, int q, const ModC* mc, u128* comp, int16_t* decomp,
+                       hipStream_t st) {
+    hipLaunchKernelGGL(k_codec_test, g1(N, 1, 1), dim3(256), 0, st, labels, N, q, mc, comp, decomp);
+}
+
+}  // namespace dev
+}  // namespace dash

@@ -1,14 +1,986 @@
-// HIP runtime (placeholder while the evaluator kernels are brought up).
-#include <hip/hip_runtime.h>
+// HIP evaluator runtime: uploads a batch of B garbled models (same circuit,
+// independent garblings) into an HBM arena and evaluates them together, one
+// kernel launch per gadget phase over (GC x residue x element). All launches
+// go to one stream (no per-layer device synchronisation, unlike the
+// reference's cudaDeviceSynchronize after every layer), so the whole forward
+// can be captured into a hipGraph.
+#include <pybind11/numpy.h>
 #include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include <chrono>
+#include <functional>
+
+#include "../layers.h"
+#include "launch.h"
 
 namespace py = pybind11;
+
 namespace dash {
+using namespace dev;
+
+#define HIPCHECK(x)                                                                                      \
+    do {                                                                                                 \
+        hipError_t e_ = (x);                                                                             \
+        if (e_ != hipSuccess)                                                                            \
+            throw std::runtime_error(std::string("HIP error: ") + hipGetErrorString(e_) + " at " + __FILE__ + \
+                                     ":" + std::to_string(__LINE__));                                    \
+    } while (0)
+
+namespace {
+
+// --------------------------------------------------------------- AES tables
+uint8_t gmul(uint8_t a, uint8_t b) {
+    uint8_t r = 0;
+    while (b) {
+        if (b & 1) r ^= a;
+        a = static_cast<uint8_t>((a << 1) ^ ((a & 0x80) ? 0x1b : 0));
+        b >>= 1;
+    }
+    return r;
+}
+std::vector<uint32_t> make_te0() {
+    // S-box from the GF(2^8) inverse and the AES affine map
+    uint8_t sbox[256];
+    for (int x = 0; x < 256; ++x) {
+        uint8_t inv = 0;
+        if (x)
+            for (int y = 1; y < 256; ++y)
+                if (gmul(static_cast<uint8_t>(x), static_cast<uint8_t>(y)) == 1) {
+                    inv = static_cast<uint8_t>(y);
+                    break;
+                }
+        uint8_t s = inv;
+        uint8_t r = s;
+        for (int i = 0; i < 4; ++i) {
+            r = static_cast<uint8_t>((r << 1) | (r >> 7));
+            s ^= r;
+        }
+        sbox[x] = static_cast<uint8_t>(s ^ 0x63);
+    }
+    std::vector<uint32_t> te(256);
+    for (int x = 0; x < 256; ++x) {
+        uint8_t s = sbox[x];
+        te[x] = (static_cast<uint32_t>(gmul(s, 2)) << 24) | (static_cast<uint32_t>(s) << 16) |
+                (static_cast<uint32_t>(s) << 8) | gmul(s, 3);
+    }
+    return te;
+}
+std::vector<uint32_t> fixed_round_key_words() {
+    uint8_t rk[176];
+    aes_round_key_bytes(fixed_key(), rk);
+    std::vector<uint32_t> w(44);
+    for (int i = 0; i < 44; ++i)
+        w[i] = (static_cast<uint32_t>(rk[4 * i]) << 24) | (static_cast<uint32_t>(rk[4 * i + 1]) << 16) |
+               (static_cast<uint32_t>(rk[4 * i + 2]) << 8) | rk[4 * i + 3];
+    return w;
+}
+
+ModC make_modc(int q) {
+    ModC m{};
+    m.q = q;
+    m.n = nr_comps(q);
+    if ((q & (q - 1)) == 0) {
+        int b = 0;
+        while ((1 << b) < q) ++b;
+        m.bits = b;
+        m.c = 1;
+        m.D = q;
+        return m;
+    }
+    uint64_t D = q;
+    int c = 1;
+    while (D * static_cast<uint64_t>(q) < (1ull << 32)) {
+        D *= q;
+        ++c;
+    }
+    m.c = c;
+    m.D = static_cast<uint32_t>(D);
+    m.mD = static_cast<uint64_t>((static_cast<u128>(1) << 64) / D);
+    m.mq = static_cast<uint32_t>((1ull << 32) / static_cast<uint64_t>(q));
+    return m;
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------
+class HipEvaluator {
+   public:
+    HipEvaluator(std::vector<std::shared_ptr<GarbledModel>> models, int device, bool use_mfma)
+        : models_(std::move(models)), mfma_(use_mfma) {
+        DASH_CHECK(!models_.empty(), "HipEvaluator needs at least one garbled model");
+        int ndev = 0;
+        if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0)
+            throw std::runtime_error("dash: no HIP device available for HipEvaluator");
+        dev_ = device;
+        HIPCHECK(hipSetDevice(dev_));
+        const GarbledModel& m0 = *models_[0];
+        for (auto& m : models_) {
+            DASH_CHECK(m->h.crt == m0.h.crt && m->h.mrs == m0.h.mrs && m->layers.size() == m0.layers.size(),
+                       "all models of a batch must garble the same circuit");
+        }
+        B_ = static_cast<int>(models_.size());
+        crt_ = m0.h.crt;
+        k_ = static_cast<int>(crt_.size());
+        DASH_CHECK(k_ <= kMaxRes, "too many CRT residues for the GPU path");
+        build();
+    }
+    ~HipEvaluator() {
+        for (void* p : allocs_) (void)hipFree(p);
+        for (void* p : host_allocs_) (void)hipHostFree(p);
+    }
+
+    int batch() const { return B_; }
+    size_t device_bytes() const { return dev_bytes_; }
+    size_t table_bytes() const { return table_bytes_; }
+
+    void set_inputs(const std::vector<CrtLabels>& in, hipStream_t st) {
+        DASH_CHECK(static_cast<int>(in.size()) == B_, "need one input per garbled model in the batch");
+        for (int j = 0; j < k_; ++j) {
+            const int n = nr_comps(crt_[j]);
+            int16_t* stg = in_stage_[j];
+            for (int b = 0; b < B_; ++b) {
+                const Labels& L = in[b][j];
+                DASH_CHECK(L.p == crt_[j] && L.N == N0_, "input label shape mismatch");
+                for (i64 e = 0; e < N0_; ++e)
+                    for (int c = 0; c < n; ++c) stg[(static_cast<i64>(b) * n + c) * N0_ + e] = L.c[e * n + c];
+            }
+            HIPCHECK(hipMemcpyAsync(bufs_[0].p[j], stg, sizeof(int16_t) * B_ * n * N0_, hipMemcpyHostToDevice, st));
+        }
+    }
+
+    void run(hipStream_t st) {
+        for (size_t i = 0; i < ops_.size(); ++i) {
+            if (profile_) HIPCHECK(hipEventRecord(ev_[i], st));
+            ops_[i](st);
+        }
+        if (profile_) HIPCHECK(hipEventRecord(ev_.back(), st));
+        HIPCHECK(hipGetLastError());
+    }
+
+    std::vector<CrtLabels> get_outputs(hipStream_t st) {
+        std::vector<CrtLabels> out(B_);
+        for (int j = 0; j < k_; ++j) {
+            const int q = out_mod_[j], n = nr_comps(q);
+            HIPCHECK(hipMemcpyAsync(out_stage_[j], final_.p[j], sizeof(int16_t) * B_ * n * Nout_, hipMemcpyDeviceToHost, st));
+        }
+        HIPCHECK(hipStreamSynchronize(st));
+        for (int b = 0; b < B_; ++b)
+            for (int j = 0; j < k_; ++j) {
+                const int q = out_mod_[j];
+                Labels L(q, Nout_);
+                const int n = L.n;
+                for (i64 e = 0; e < Nout_; ++e)
+                    for (int c = 0; c < n; ++c) L.c[e * n + c] = out_stage_[j][(static_cast<i64>(b) * n + c) * Nout_ + e];
+                out[b].push_back(std::move(L));
+            }
+        return out;
+    }
+
+    void set_profile(bool on) {
+        profile_ = on;
+        if (on && ev_.empty()) {
+            ev_.resize(ops_.size() + 1);
+            for (auto& e : ev_) HIPCHECK(hipEventCreate(&e));
+        }
+    }
+    std::vector<std::pair<std::string, double>> op_times() const {
+        std::vector<std::pair<std::string, double>> r;
+        if (!profile_) return r;
+        for (size_t i = 0; i < ops_.size(); ++i) {
+            float ms = 0;
+            (void)hipEventElapsedTime(&ms, ev_[i], ev_[i + 1]);
+            r.emplace_back(op_names_[i], ms);
+        }
+        return r;
+    }
+
+   private:
+    // ------------------------------------------------------------ helpers
+    template <typename T>
+    T* dalloc(size_t count) {
+        void* p = nullptr;
+        size_t bytes = std::max<size_t>(count * sizeof(T), 64);
+        HIPCHECK(hipMalloc(&p, bytes));
+        allocs_.push_back(p);
+        dev_bytes_ += bytes;
+        return static_cast<T*>(p);
+    }
+    template <typename T>
+    T* upload(const T* host, size_t count) {
+        T* d = dalloc<T>(count);
+        HIPCHECK(hipMemcpy(d, host, count * sizeof(T), hipMemcpyHostToDevice));
+        return d;
+    }
+    // one device buffer holding array `name` of layer li of every model
+    const u128* upload_tables(size_t li, const std::string& name) {
+        const Array& a0 = models_[0]->layers[li].arr(name);
+        const size_t nb = a0.nbytes;
+        uint8_t* d = dalloc<uint8_t>(nb * B_);
+        for (int b = 0; b < B_; ++b) {
+            const Array& a = models_[b]->layers[li].arr(name);
+            DASH_CHECK(a.nbytes == nb, "table size mismatch across batch");
+            HIPCHECK(hipMemcpy(d + nb * b, a.buf.get(), nb, hipMemcpyHostToDevice));
+        }
+        table_bytes_ += nb * B_;
+        return reinterpret_cast<const u128*>(d);
+    }
+    const int16_t* upload_i16_rows(size_t li, const std::string& name) {
+        const Array& a0 = models_[0]->layers[li].arr(name);
+        const size_t nb = a0.nbytes;
+        uint8_t* d = dalloc<uint8_t>(nb * B_);
+        for (int b = 0; b < B_; ++b)
+            HIPCHECK(hipMemcpy(d + nb * b, models_[b]->layers[li].arr(name).buf.get(), nb, hipMemcpyHostToDevice));
+        return reinterpret_cast<const int16_t*>(d);
+    }
+    // per-GC concatenated residue labels from model consts ("up.j", "down.s.j", "Z.p")
+    const int16_t* upload_const_rows(const std::function<std::string(int)>& name_of) {
+        std::vector<int16_t> h(static_cast<size_t>(B_) * lab_stride_);
+        for (int b = 0; b < B_; ++b)
+            for (int j = 0; j < k_; ++j) {
+                auto it = models_[b]->consts.find(name_of(j));
+                DASH_CHECK(it != models_[b]->consts.end(), "missing model constant " + name_of(j));
+                std::memcpy(&h[static_cast<size_t>(b) * lab_stride_ + lab_off_[j]], it->second.ptr<int16_t>(),
+                            sizeof(int16_t) * nr_comps(crt_[j]));
+            }
+        return upload(h.data(), h.size());
+    }
+    CrtInfo crt_info(const std::vector<int>& mods) const {
+        CrtInfo c{};
+        c.k = static_cast<int>(mods.size());
+        int s = 0;
+        for (int j = 0; j < c.k; ++j) {
+            c.p[j] = mods[j];
+            c.n[j] = nr_comps(mods[j]);
+            c.prefix[j] = s;
+            s += mods[j];
+        }
+        c.sum = s;
+        return c;
+    }
+    Act act_of(int which) const { return bufs_[which]; }
+    void add_op(const std::string& name, std::function<void(hipStream_t)> f) {
+        ops_.push_back(std::move(f));
+        op_names_.push_back(name);
+    }
+
+    // sign gadget phases over `x` (N elements); results in sign scratch
+    SignArgs make_sign(size_t li, const std::string& pre, const SignPlan& sp, i64 N, int relu) {
+        SignArgs a{};
+        a.crt = crt_info(crt_);
+        a.t = static_cast<int>(sp.mrs.size());
+        DASH_CHECK(a.t <= kMaxMrs, "MRS base too long for the GPU path");
+        for (int d = 0; d < a.t; ++d) a.mrs[d] = sp.mrs[d];
+        a.nout = static_cast<int>(sp.out_mod.size());
+        for (int o = 0; o < a.nout; ++o) a.out_mod[o] = sp.out_mod[o];
+        a.N = N;
+        a.B = B_;
+        a.n_approx = sp.n_approx;
+        a.n_cast = models_[0]->layers[li].arr(pre + "s.cast1").shape[1];
+        a.n_sign = sp.n_sign;
+        a.approx = upload_tables(li, pre + "s.approx");
+        a.cast1 = upload_tables(li, pre + "s.cast1");
+        a.cast2 = upload_tables(li, pre + "s.cast2");
+        a.sign = upload_tables(li, pre + "s.sign");
+        a.mrsP = mrsP_;
+        a.hx = relu ? hx_ : nullptr;
+        a.colx = relu ? colx_ : nullptr;
+        a.outP = outP_;
+        a.hs = hs_;
+        a.cs = cs_;
+        a.zc = zc_;
+        a.zcol = zcol_;
+        a.zc_stride = zstride_;
+        a.relu = relu;
+        int maxn = 0;
+        const int k = k_;
+        for (size_t d = 1; d < sp.mrs.size(); ++d) maxn = std::max(maxn, nr_comps((k + 1) * sp.mrs[d]));
+        maxn = std::max(maxn, nr_comps(sp.mrs[0]));
+        DASH_CHECK(maxn <= 64, "MRS moduli too small for the GPU sign chain (label width > 64)");
+        sign_maxn_ = maxn;
+        return a;
+    }
+
+    void build();
+
+    std::vector<std::shared_ptr<GarbledModel>> models_;
+    bool mfma_;
+    int dev_ = 0, B_ = 1, k_ = 0;
+    std::vector<int> crt_, out_mod_;
+    i64 N0_ = 0, Nout_ = 0;
+    std::vector<void*> allocs_, host_allocs_;
+    size_t dev_bytes_ = 0, table_bytes_ = 0;
+    std::vector<std::function<void(hipStream_t)>> ops_;
+    std::vector<std::string> op_names_;
+    bool profile_ = false;
+    std::vector<hipEvent_t> ev_;
+    Act bufs_[4]{};  // ping-pong activation buffers (+ scratch)
+    Act final_{};
+    std::vector<int16_t*> in_stage_, out_stage_;
+    // constants
+    ModC* mc_ = nullptr;
+    AesGlobals aes_{};
+    int lab_stride_ = 0;
+    int lab_off_[kMaxRes]{};
+    int* d_lab_off_ = nullptr;
+    const int16_t* zero_rows_ = nullptr;
+    const int16_t* up_rows_ = nullptr;
+    const u128* zc_ = nullptr;
+    const uint16_t* zcol_ = nullptr;
+    int zstride_ = 0;
+    // scratch
+    u128 *mrsP_ = nullptr, *hx_ = nullptr, *outP_ = nullptr, *hs_ = nullptr, *h0_ = nullptr;
+    uint16_t *colx_ = nullptr, *col0_ = nullptr;
+    uint8_t* cs_ = nullptr;
+    int16_t* be_work_ = nullptr;
+    int sign_maxn_ = 32;
+    std::vector<std::vector<int16_t*>> saved_;  // residual-add sources
+};
+
+void HipEvaluator::build() {
+    const GarbledModel& m0 = *models_[0];
+    // ---- global constants
+    const int maxmod = m0.h.max_mod;
+    std::vector<ModC> mc(maxmod + 1);
+    for (int q = 2; q <= maxmod; ++q) mc[q] = make_modc(q);
+    mc_ = upload(mc.data(), mc.size());
+    auto te = make_te0();
+    auto rk = fixed_round_key_words();
+    aes_.te0 = upload(te.data(), te.size());
+    aes_.rk = upload(rk.data(), rk.size());
+    for (int j = 0; j < k_; ++j) {
+        lab_off_[j] = lab_stride_;
+        lab_stride_ += nr_comps(crt_[j]);
+    }
+    d_lab_off_ = upload(lab_off_, k_);
+    zero_rows_ = upload_const_rows([&](int j) { return "Z." + std::to_string(crt_[j]); });
+    // compressed zero labels + colors for every modulus (carry init)
+    zstride_ = maxmod + 1;
+    {
+        std::vector<u128> zc(static_cast<size_t>(B_) * zstride_, 0);
+        std::vector<uint16_t> zcol(static_cast<size_t>(B_) * zstride_, 0);
+        for (int b = 0; b < B_; ++b) {
+            LabelBank Z = models_[b]->zero_bank();
+            for (int q = 2; q <= maxmod; ++q) {
+                if (Z.lab[q].empty()) continue;
+                zc[static_cast<size_t>(b) * zstride_ + q] = compress(Z.lab[q].data(), mod_info(q));
+                zcol[static_cast<size_t>(b) * zstride_ + q] = static_cast<uint16_t>(Z.lab[q][0]);
+            }
+        }
+        zc_ = upload(zc.data(), zc.size());
+        zcol_ = upload(zcol.data(), zcol.size());
+    }
+    bool any_rescale = false;
+    for (auto& l : m0.layers) any_rescale |= (l.kind == K_RESCALE);
+    if (any_rescale) up_rows_ = upload_const_rows([&](int j) { return "up." + std::to_string(j); });
+
+    // ---- shape pass: buffer capacities
+    N0_ = 1;
+    for (auto d : m0.h.in_dims) N0_ *= d;
+    i64 maxN = N0_, maxSignN = 1, maxPoolSlots = 1;
+    std::vector<int> widest(k_, 0), mods = crt_;
+    for (int j = 0; j < k_; ++j) widest[j] = nr_comps(crt_[j]);
+    {
+        i64 N = N0_;
+        for (auto& l : m0.layers) {
+            switch (l.kind) {
+                case K_DENSE: N = l.param("out"); break;
+                case K_CONV: N = ConvGeom(l).out_size(); break;
+                case K_RELU: case K_SIGN: case K_RESCALE: maxSignN = std::max(maxSignN, N); break;
+                case K_MAXPOOL: {
+                    PoolGeom G(l.p);
+                    maxPoolSlots = std::max(maxPoolSlots, G.out_size() * G.kh * G.kw);
+                    maxSignN = std::max(maxSignN, G.out_size() * G.kh * G.kw);
+                    N = G.out_size();
+                    break;
+                }
+                case K_MAX:
+                    maxPoolSlots = std::max(maxPoolSlots, N);
+                    maxSignN = std::max(maxSignN, N);
+                    N = 1;
+                    break;
+                case K_SUMPOOL: N = PoolGeom(l.p).out_size(); break;
+                case K_MULT: case K_MMULT: N /= 2; break;
+                case K_PROJ: {
+                    const auto& om = l.vec("out_mod");
+                    for (int j = 0; j < k_; ++j) widest[j] = std::max(widest[j], nr_comps(static_cast<int>(om[j])));
+                    break;
+                }
+                default: break;
+            }
+            maxN = std::max(maxN, N);
+        }
+    }
+    const i64 cap = std::max(maxN, maxPoolSlots);
+    for (int bi = 0; bi < 4; ++bi) {
+        bufs_[bi].N = 0;
+        for (int j = 0; j < k_; ++j) bufs_[bi].p[j] = dalloc<int16_t>(static_cast<size_t>(B_) * widest[j] * cap);
+    }
+    int tmax = std::max<int>(1, static_cast<int>(m0.h.mrs.size()));
+    mrsP_ = dalloc<u128>(static_cast<size_t>(B_) * k_ * tmax * maxSignN);
+    hx_ = dalloc<u128>(static_cast<size_t>(B_) * k_ * maxSignN);
+    colx_ = dalloc<uint16_t>(static_cast<size_t>(B_) * k_ * maxSignN);
+    outP_ = dalloc<u128>(static_cast<size_t>(B_) * k_ * maxSignN);
+    hs_ = dalloc<u128>(static_cast<size_t>(B_) * maxSignN);
+    cs_ = dalloc<uint8_t>(static_cast<size_t>(B_) * maxSignN);
+    h0_ = dalloc<u128>(static_cast<size_t>(B_) * maxN);
+    col0_ = dalloc<uint16_t>(static_cast<size_t>(B_) * maxN);
+    for (int j = 0; j < k_; ++j) {
+        int16_t* p = nullptr;
+        HIPCHECK(hipHostMalloc(reinterpret_cast<void**>(&p), sizeof(int16_t) * B_ * nr_comps(crt_[j]) * N0_));
+        host_allocs_.push_back(p);
+        in_stage_.push_back(p);
+    }
+
+    // ---- plan
+    std::vector<int> keep(m0.layers.size() + 1, 0);
+    for (auto& l : m0.layers)
+        if (l.kind == K_ADD) keep[l.param("src") + 1] = 1;
+    saved_.assign(m0.layers.size() + 1, {});
+    int cur = 0;  // buffer index holding the current activation
+    i64 N = N0_;
+    const CrtInfo crt = crt_info(crt_);
+    auto save_if_needed = [&](size_t slot, int buf, i64 n_el, const std::vector<int>& md) {
+        if (!keep[slot]) return;
+        std::vector<int16_t*> s;
+        for (int j = 0; j < k_; ++j) {
+            const size_t bytes = sizeof(int16_t) * B_ * nr_comps(md[j]) * n_el;
+            int16_t* d = dalloc<int16_t>(bytes / sizeof(int16_t));
+            int16_t* src = bufs_[buf].p[j];
+            add_op("save", [d, src, bytes](hipStream_t st) { HIPCHECK(hipMemcpyAsync(d, src, bytes, hipMemcpyDeviceToDevice, st)); });
+            s.push_back(d);
+        }
+        saved_[slot] = s;
+    };
+    save_if_needed(0, cur, N, mods);
+
+    for (size_t li = 0; li < m0.layers.size(); ++li) {
+        const GLayer& g = m0.layers[li];
+        const int nxt = (cur + 1) % 2;
+        const std::string lname = std::string(kind_name(g.kind)) + "#" + std::to_string(li);
+        switch (g.kind) {
+            case K_FLATTEN:
+                break;
+            case K_DENSE: {
+                DenseArgs a{};
+                a.crt = crt;
+                a.K = g.param("in");
+                a.O = g.param("out");
+                const i64 ch = g.param("channel_tf", 0);
+                const Array& w = g.arr("w");
+                for (int j = 0; j < k_; ++j) {
+                    const int p = crt_[j];
+                    std::vector<int16_t> wt(static_cast<size_t>(a.K * a.O));
+                    std::vector<int32_t> zc(a.O, 0);
+                    for (i64 o = 0; o < a.O; ++o)
+                        for (i64 i = 0; i < a.K; ++i) {
+                            const int v = static_cast<int>(w.ptr<i64>()[o * a.K + i] % p);
+                            wt[i * a.O + o] = static_cast<int16_t>(v);
+                            if (v == 0) ++zc[o];
+                        }
+                    a.w[j] = upload(wt.data(), wt.size());
+                    a.zc[j] = upload(zc.data(), zc.size());
+                    a.bias[j] = upload_i16_rows(li, arr_name("bias.", j, ""));
+                }
+                a.zero = zero_rows_;
+                a.lab_stride = lab_stride_;
+                for (int j = 0; j < k_; ++j) a.lab_off[j] = lab_off_[j];
+                if (ch > 0) {
+                    std::vector<int32_t> src(a.K);
+                    for (i64 i = 0; i < a.K; ++i) src[i] = static_cast<int32_t>(dense_src(i, a.K, ch));
+                    a.src = upload(src.data(), src.size());
+                }
+                Act x = act_of(cur), y = act_of(nxt);
+                x.N = N;
+                y.N = a.O;
+                const int B = B_;
+                add_op(lname, [a, x, y, B](hipStream_t st) { launch_dense(a, x, y, B, st); });
+                N = a.O;
+                cur = nxt;
+                break;
+            }
+            case K_CONV: {
+                ConvGeom G(g);
+                ConvArgs a{};
+                a.crt = crt;
+                a.C = static_cast<int>(G.C); a.H = static_cast<int>(G.H); a.W = static_cast<int>(G.W);
+                a.F = static_cast<int>(G.F); a.kh = static_cast<int>(G.kh); a.kw = static_cast<int>(G.kw);
+                a.sh = static_cast<int>(G.sh); a.sw = static_cast<int>(G.sw);
+                a.ph = static_cast<int>(G.ph); a.pw = static_cast<int>(G.pw);
+                a.OH = static_cast<int>(G.OH); a.OW = static_cast<int>(G.OW);
+                const i64 K = G.K();
+                a.Kpad = static_cast<int>((K + 63) / 64 * 64);
+                a.use_mfma = mfma_ ? 1 : 0;
+                const Array& w = g.arr("w");
+                for (int j = 0; j < k_; ++j) {
+                    const int p = crt_[j];
+                    std::vector<int16_t> wm(static_cast<size_t>(G.F * K));
+                    std::vector<int8_t> w8(static_cast<size_t>(G.F) * a.Kpad, 0);
+                    std::vector<int32_t> zc(G.F, 0);
+                    for (i64 f = 0; f < G.F; ++f)
+                        for (i64 q = 0; q < K; ++q) {
+                            const int v = static_cast<int>(w.ptr<i64>()[f * K + q] % p);
+                            wm[f * K + q] = static_cast<int16_t>(v);
+                            if (v == 0) ++zc[f];
+                            w8[f * a.Kpad + q] = static_cast<int8_t>(v > p / 2 ? v - p : v);
+                        }
+                    a.w[j] = upload(wm.data(), wm.size());
+                    a.w8[j] = (mfma_ && p <= 255) ? upload(w8.data(), w8.size()) : nullptr;
+                    a.zc[j] = upload(zc.data(), zc.size());
+                    a.bias[j] = upload_i16_rows(li, arr_name("bias.", j, ""));
+                }
+                a.zero = zero_rows_;
+                a.lab_stride = lab_stride_;
+                for (int j = 0; j < k_; ++j) a.lab_off[j] = lab_off_[j];
+                Act x = act_of(cur), y = act_of(nxt);
+                const int B = B_;
+                add_op(lname, [a, x, y, B](hipStream_t st) { launch_conv(a, x, y, B, st); });
+                N = G.out_size();
+                cur = nxt;
+                break;
+            }
+            case K_RELU: {
+                SignPlan sp(crt_, m0.h.mrs, {2}, 0, 1);
+                SignArgs a = make_sign(li, "", sp, N, 1);
+                const u128* gt = upload_tables(li, "mm.g");
+                const u128* et = upload_tables(li, "mm.e");
+                Act x = act_of(cur), y = act_of(nxt);
+                const ModC* mc = mc_;
+                const AesGlobals ag = aes_;
+                const int maxn = sign_maxn_;
+                add_op(lname + ".A", [a, x, mc, ag](hipStream_t st) { launch_sign_approx(a, x, mc, ag, st); });
+                add_op(lname + ".B", [a, maxn, mc, ag](hipStream_t st) { launch_sign_chain(a, maxn, mc, ag, st); });
+                add_op(lname + ".C", [a, x, y, gt, et, mc](hipStream_t st) { launch_relu_mult(a, x, y, gt, et, mc, st); });
+                cur = nxt;
+                break;
+            }
+            case K_SIGN: {
+                SignPlan sp(crt_, m0.h.mrs, crt_, -1, 1);
+                SignArgs a = make_sign(li, "", sp, N, 0);
+                Act x = act_of(cur), y = act_of(nxt);
+                const ModC* mc = mc_;
+                const AesGlobals ag = aes_;
+                const int maxn = sign_maxn_;
+                const int B = B_;
+                const u128* outP = outP_;
+                const i64 NN = N;
+                add_op(lname + ".A", [a, x, mc, ag](hipStream_t st) { launch_sign_approx(a, x, mc, ag, st); });
+                add_op(lname + ".B", [a, maxn, mc, ag](hipStream_t st) { launch_sign_chain(a, maxn, mc, ag, st); });
+                add_op(lname + ".unpack", [outP, y, crt, mc, NN, B](hipStream_t st) { launch_unpack(outP, crt.k, y, crt, mc, NN, B, st); });
+                cur = nxt;
+                break;
+            }
+            case K_RESCALE: {
+                const i64 mode = g.param("mode", 0);
+                const i64 iters = g.param("iters");
+                for (i64 it = 0; it < iters; ++it) {
+                    std::vector<int> factors;
+                    if (mode == 0)
+                        factors = {2};
+                    else
+                        for (auto v : g.vec("s")) factors.push_back(static_cast<int>(v));
+                    RescalePlan P(crt_, m0.h.mrs, factors, mode == 0);
+                    const std::string pre = arr_name("it", static_cast<int>(it), ".");
+                    const u128* trans = upload_tables(li, pre + "trans");
+                    Act x = act_of(cur);
+                    const ModC* mc = mc_;
+                    const AesGlobals ag = aes_;
+                    const int B = B_;
+                    const i64 NN = N;
+                    i64 off = 0;
+                    for (size_t f = 0; f < P.factors.size(); ++f) {
+                        const int fi = P.factor_idx[f], s = P.factors[f];
+                        const int add_up = f == 0 ? 1 : 0;
+                        const int16_t* up = up_rows_ + lab_off_[fi];
+                        u128* h0 = h0_;
+                        uint16_t* col0 = col0_;
+                        const int ls = lab_stride_;
+                        add_op(lname + ".hash", [x, fi, s, up, ls, add_up, NN, B, h0, col0, mc, ag](hipStream_t st) {
+                            launch_rescale_hash(x, fi, s, up, ls, add_up, NN, B, h0, col0, mc, ag, st);
+                        });
+                        RescaleArgs ra{};
+                        ra.crt = crt;
+                        ra.N = N;
+                        ra.fi = fi;
+                        ra.s = s;
+                        ra.add_up = add_up;
+                        for (size_t q = 0; q < P.active[f].size(); ++q) {
+                            const int jj = P.active[f][q];
+                            ra.active[jj] = 1;
+                            ra.aidx[jj] = static_cast<int>(q);
+                            ra.inv[jj] = static_cast<int>(P.inv[f][q]);
+                        }
+                        ra.n_trans = P.n_trans;
+                        ra.off = off;
+                        off += static_cast<i64>(P.active[f].size()) * s;
+                        ra.trans = trans;
+                        ra.h0 = h0_;
+                        ra.col0 = col0_;
+                        ra.up = up_rows_;
+                        ra.zero = zero_rows_;
+                        ra.lab_stride = lab_stride_;
+                        for (int j = 0; j < k_; ++j) ra.lab_off[j] = lab_off_[j];
+                        add_op(lname + ".update", [ra, x, B, mc](hipStream_t st) { launch_rescale_update(ra, x, B, mc, st); });
+                    }
+                    const u128* signP = nullptr;
+                    if (P.sign_be) {
+                        SignArgs a = make_sign(li, pre, P.sign, N, 0);
+                        const int maxn = sign_maxn_;
+                        add_op(lname + ".sA", [a, x, mc, ag](hipStream_t st) { launch_sign_approx(a, x, mc, ag, st); });
+                        add_op(lname + ".sB", [a, maxn, mc, ag](hipStream_t st) { launch_sign_chain(a, maxn, mc, ag, st); });
+                        signP = outP_;
+                    } else {
+                        const BEPlan& be = P.be;
+                        BEArgs ba{};
+                        ba.E = static_cast<int>(be.moduli.size());
+                        ba.nonext = be.nonext;
+                        std::vector<int> idx(ba.E);
+                        for (int i = 0; i < ba.E; ++i) idx[be.pos_of[i]] = i;
+                        for (int i = 0; i < ba.E; ++i) {
+                            ba.swapped[i] = be.swapped[i];
+                            ba.src[i] = idx[i];
+                        }
+                        for (int i = 0; i + 1 < ba.E; ++i)
+                            for (size_t jj = 0; jj < be.inv_partial[i].size(); ++jj)
+                                ba.inv[i][jj] = static_cast<int>(be.inv_partial[i][jj]);
+                        ba.nextra = static_cast<int>(be.extra.size());
+                        for (int xi = 0; xi < ba.nextra; ++xi) {
+                            ba.extra_res[xi] = be.extra_idx[xi];
+                            ba.extra_pos[xi] = be.pos_of[be.extra_idx[xi]];
+                            const int q = be.moduli[be.extra_idx[xi]];
+                            ba.invv[xi] = static_cast<int>(pmod(-be.invv[xi], q));
+                        }
+                        ba.N = N;
+                        ba.n_tab = be.n_tab;
+                        ba.tab = upload_tables(li, pre + "be");
+                        if (!be_work_) be_work_ = dalloc<int16_t>(static_cast<size_t>(B_) * k_ * 128 * maxN);
+                        ba.work = be_work_;
+                        add_op(lname + ".be", [ba, x, B, mc, ag](hipStream_t st) { launch_base_ext(ba, x, B, mc, ag, st); });
+                    }
+                    const int16_t* down = upload_const_rows(
+                        [&](int j) { return "down." + std::to_string(P.sprod) + "." + std::to_string(j); });
+                    const int ls = lab_stride_;
+                    const int* loff = d_lab_off_;
+                    add_op(lname + ".post", [x, crt, NN, B, signP, down, ls, loff, mc](hipStream_t st) {
+                        launch_rescale_post(x, crt, NN, B, signP, down, ls, loff, mc, st);
+                    });
+                }
+                break;
+            }
+            case K_MAXPOOL:
+            case K_MAX: {
+                i64 Nout, K;
+                std::vector<i64> idx;
+                if (g.kind == K_MAXPOOL) {
+                    PoolGeom G(g.p);
+                    Nout = G.out_size();
+                    K = G.kh * G.kw;
+                    std::vector<i64> w;
+                    for (i64 o = 0; o < Nout; ++o) {
+                        G.window(o, w);
+                        idx.insert(idx.end(), w.begin(), w.end());
+                    }
+                } else {
+                    Nout = 1;
+                    K = N;
+                    for (i64 i = 0; i < N; ++i) idx.push_back(i);
+                }
+                const int64_t* didx = upload(idx.data(), idx.size());
+                MaxTree T(K);
+                SignPlan sp(crt_, m0.h.mrs, {2}, 0, 1);
+                // buffers: vals in 2/3 ping-pong, diff in nxt-other... use bufs 2,3 for vals; relu out in buf nxt
+                int va = 2, vb = 3;
+                Act xin = act_of(cur), v0 = act_of(va);
+                const int B = B_;
+                const i64 NN = N;
+                add_op(lname + ".gather", [xin, NN, v0, Nout, K, didx, crt, B](hipStream_t st) {
+                    launch_copy_gather(xin, NN, v0, Nout * K, didx, crt, B, st);
+                });
+                // scratch for diffs: reuse buffer `cur` (its content is no longer needed) and relu out in `nxt`
+                for (size_t lv = 0; lv < T.ops.size(); ++lv) {
+                    const int ops = T.ops[lv], cnt = T.cnt[lv], cnt1 = T.cnt[lv + 1];
+                    const std::string pre = arr_name("lv", static_cast<int>(lv), ".");
+                    SignArgs a = make_sign(li, pre, sp, Nout * ops, 1);
+                    const u128* gt = upload_tables(li, pre + "mm.g");
+                    const u128* et = upload_tables(li, pre + "mm.e");
+                    Act V = act_of(va), D = act_of(cur), Rr = act_of(nxt), NV = act_of(vb);
+                    const ModC* mc = mc_;
+                    const AesGlobals ag = aes_;
+                    const int maxn = sign_maxn_;
+                    const i64 Nv = Nout * cnt;
+                    add_op(lname + ".diff", [V, Nv, D, Nout, ops, cnt, crt, B](hipStream_t st) {
+                        launch_pair_diff(V, Nv, D, Nout, ops, cnt, crt, B, st);
+                    });
+                    add_op(lname + ".A", [a, D, mc, ag](hipStream_t st) { launch_sign_approx(a, D, mc, ag, st); });
+                    add_op(lname + ".B", [a, maxn, mc, ag](hipStream_t st) { launch_sign_chain(a, maxn, mc, ag, st); });
+                    add_op(lname + ".C", [a, D, Rr, gt, et, mc](hipStream_t st) { launch_relu_mult(a, D, Rr, gt, et, mc, st); });
+                    add_op(lname + ".add", [V, Nv, Rr, NV, Nout, ops, cnt, cnt1, crt, B](hipStream_t st) {
+                        launch_pair_add(V, Nv, Rr, NV, Nout, ops, cnt, cnt1, crt, B, st);
+                    });
+                    std::swap(va, vb);
+                }
+                // result (cnt == 1) lives in buffer va: copy into nxt
+                std::vector<i64> ident(Nout);
+                for (i64 o = 0; o < Nout; ++o) ident[o] = o;
+                const int64_t* did = upload(ident.data(), ident.size());
+                Act vres = act_of(va), y = act_of(nxt);
+                add_op(lname + ".out", [vres, Nout, y, did, crt, B](hipStream_t st) {
+                    launch_copy_gather(vres, Nout, y, Nout, did, crt, B, st);
+                });
+                N = Nout;
+                cur = nxt;
+                break;
+            }
+            case K_SUMPOOL: {
+                PoolGeom G(g.p);
+                std::vector<i64> idx, w;
+                for (i64 o = 0; o < G.out_size(); ++o) {
+                    G.window(o, w);
+                    idx.insert(idx.end(), w.begin(), w.end());
+                }
+                const int64_t* didx = upload(idx.data(), idx.size());
+                Act x = act_of(cur), y = act_of(nxt);
+                const i64 NN = N, No = G.out_size();
+                const int K = static_cast<int>(G.kh * G.kw);
+                const int B = B_;
+                add_op(lname, [x, NN, y, No, didx, K, crt, B](hipStream_t st) { launch_window_sum(x, NN, y, No, didx, K, crt, B, st); });
+                N = No;
+                cur = nxt;
+                break;
+            }
+            case K_ADD: {
+                const i64 src = g.param("src");
+                const auto& s = saved_[src + 1];
+                DASH_CHECK(!s.empty(), "residual source not saved");
+                Act x = act_of(cur), y{};
+                for (int j = 0; j < k_; ++j) y.p[j] = s[j];
+                const i64 NN = N;
+                const int B = B_;
+                add_op(lname, [x, y, NN, crt, B](hipStream_t st) { launch_add(x, y, NN, crt, B, st); });
+                break;
+            }
+            case K_PROJ: {
+                const auto& inm = g.vec("in_mod");
+                const auto& outm = g.vec("out_mod");
+                ProjArgs a{};
+                a.k = k_;
+                a.N = N;
+                for (int j = 0; j < k_; ++j) {
+                    a.pin[j] = static_cast<int>(inm[j]);
+                    a.pout[j] = static_cast<int>(outm[j]);
+                    a.tab[j] = upload_tables(li, arr_name("t.", j, ""));
+                    mods[j] = a.pout[j];
+                }
+                Act x = act_of(cur), y = act_of(nxt);
+                const ModC* mc = mc_;
+                const AesGlobals ag = aes_;
+                const int B = B_;
+                add_op(lname, [a, x, y, B, mc, ag](hipStream_t st) { launch_proj(a, x, y, B, mc, ag, st); });
+                cur = nxt;
+                break;
+            }
+            case K_MULT:
+            case K_MMULT: {
+                MultArgs a{};
+                a.crt = crt;
+                a.No = N / 2;
+                a.q = g.kind == K_MMULT ? static_cast<int>(g.param("q")) : 0;
+                if (a.q) a.t = upload_tables(li, "t");
+                a.g = upload_tables(li, "g");
+                a.e = upload_tables(li, "e");
+                Act x = act_of(cur), y = act_of(nxt);
+                const ModC* mc = mc_;
+                const AesGlobals ag = aes_;
+                const int B = B_;
+                add_op(lname, [a, x, y, B, mc, ag](hipStream_t st) { launch_mult(a, x, y, B, mc, ag, st); });
+                N = a.No;
+                cur = nxt;
+                break;
+            }
+            case K_BASEEXT: {
+                std::vector<int> ext;
+                for (auto v : g.vec("extra")) ext.push_back(static_cast<int>(v));
+                BEPlan be(crt_, ext);
+                Act x = act_of(cur);
+                const ModC* mc = mc_;
+                const AesGlobals ag = aes_;
+                const int B = B_;
+                for (int xi : be.extra_idx) {
+                    RescaleArgs ra{};
+                    ra.crt = crt;
+                    ra.N = N;
+                    ra.fi = xi;
+                    ra.zero = zero_rows_;
+                    ra.up = zero_rows_;
+                    ra.lab_stride = lab_stride_;
+                    for (int j = 0; j < k_; ++j) ra.lab_off[j] = lab_off_[j];
+                    add_op(lname + ".zero", [ra, x, B, mc](hipStream_t st) { launch_rescale_update(ra, x, B, mc, st); });
+                }
+                BEArgs ba{};
+                ba.E = static_cast<int>(be.moduli.size());
+                ba.nonext = be.nonext;
+                std::vector<int> idx(ba.E);
+                for (int i = 0; i < ba.E; ++i) idx[be.pos_of[i]] = i;
+                for (int i = 0; i < ba.E; ++i) {
+                    ba.swapped[i] = be.swapped[i];
+                    ba.src[i] = idx[i];
+                }
+                for (int i = 0; i + 1 < ba.E; ++i)
+                    for (size_t jj = 0; jj < be.inv_partial[i].size(); ++jj) ba.inv[i][jj] = static_cast<int>(be.inv_partial[i][jj]);
+                ba.nextra = static_cast<int>(be.extra.size());
+                for (int xi = 0; xi < ba.nextra; ++xi) {
+                    ba.extra_res[xi] = be.extra_idx[xi];
+                    ba.extra_pos[xi] = be.pos_of[be.extra_idx[xi]];
+                    ba.invv[xi] = static_cast<int>(pmod(-be.invv[xi], be.moduli[be.extra_idx[xi]]));
+                }
+                ba.N = N;
+                ba.n_tab = be.n_tab;
+                ba.tab = upload_tables(li, "be");
+                if (!be_work_) be_work_ = dalloc<int16_t>(static_cast<size_t>(B_) * k_ * 128 * maxN);
+                ba.work = be_work_;
+                add_op(lname, [ba, x, B, mc, ag](hipStream_t st) { launch_base_ext(ba, x, B, mc, ag, st); });
+                break;
+            }
+            default:
+                throw std::runtime_error(std::string("dash: HIP evaluator cannot run layer kind ") + kind_name(g.kind));
+        }
+        save_if_needed(li + 1, cur, N, mods);
+    }
+    final_ = act_of(cur);
+    Nout_ = N;
+    out_mod_ = mods;
+    for (int j = 0; j < k_; ++j) {
+        int16_t* p = nullptr;
+        HIPCHECK(hipHostMalloc(reinterpret_cast<void**>(&p), sizeof(int16_t) * B_ * nr_comps(mods[j]) * std::max<i64>(Nout_, 1)));
+        host_allocs_.push_back(p);
+        out_stage_.push_back(p);
+    }
+    HIPCHECK(hipDeviceSynchronize());
+}
+
+// ---------------------------------------------------------------------------
+namespace {
+py::list labels_to_py2(const CrtLabels& L) {
+    py::list out;
+    for (const auto& x : L) {
+        py::array_t<int16_t> arr({static_cast<py::ssize_t>(x.N), static_cast<py::ssize_t>(x.n)});
+        std::memcpy(arr.mutable_data(), x.c.data(), x.c.size() * sizeof(comp_t));
+        out.append(py::make_tuple(x.p, arr));
+    }
+    return out;
+}
+CrtLabels labels_from_py2(const py::list& l) {
+    CrtLabels out;
+    for (auto item : l) {
+        py::tuple t = item.cast<py::tuple>();
+        int p = t[0].cast<int>();
+        auto arr = py::array_t<int16_t, py::array::c_style | py::array::forcecast>::ensure(t[1]);
+        DASH_CHECK(arr && arr.ndim() == 2, "labels must be (N, n) int16 arrays");
+        Labels L(p, arr.shape(0));
+        DASH_CHECK(arr.shape(1) == L.n, "label width does not match modulus");
+        std::memcpy(L.c.data(), arr.data(), L.c.size() * sizeof(comp_t));
+        out.push_back(std::move(L));
+    }
+    return out;
+}
+hipStream_t as_stream(uintptr_t s) { return reinterpret_cast<hipStream_t>(s); }
+}  // namespace
+
 void register_hip_bindings(py::module_& m) {
     m.def("hip_device_count", []() {
         int n = 0;
         if (hipGetDeviceCount(&n) != hipSuccess) return 0;
         return n;
     });
+    py::class_<HipEvaluator, std::shared_ptr<HipEvaluator>>(m, "HipEvaluator")
+        .def(py::init([](std::vector<std::shared_ptr<GarbledModel>> models, int device, bool mfma) {
+                 return std::make_shared<HipEvaluator>(std::move(models), device, mfma);
+             }),
+             py::arg("models"), py::arg("device") = 0, py::arg("mfma") = true)
+        .def_property_readonly("batch", &HipEvaluator::batch)
+        .def("device_bytes", &HipEvaluator::device_bytes)
+        .def("table_bytes", &HipEvaluator::table_bytes)
+        .def("set_profile", &HipEvaluator::set_profile)
+        .def("op_times", &HipEvaluator::op_times)
+        .def("set_inputs", [](HipEvaluator& h, const py::list& inputs, uintptr_t stream) {
+            std::vector<CrtLabels> in;
+            for (auto it : inputs) in.push_back(labels_from_py2(it.cast<py::list>()));
+            h.set_inputs(in, as_stream(stream));
+        }, py::arg("inputs"), py::arg("stream") = 0)
+        .def("run", [](HipEvaluator& h, uintptr_t stream) { h.run(as_stream(stream)); }, py::arg("stream") = 0)
+        .def("get_outputs", [](HipEvaluator& h, uintptr_t stream) {
+            auto o = h.get_outputs(as_stream(stream));
+            py::list r;
+            for (auto& x : o) r.append(labels_to_py2(x));
+            return r;
+        }, py::arg("stream") = 0)
+        .def("evaluate", [](HipEvaluator& h, const py::list& inputs, uintptr_t stream) {
+            std::vector<CrtLabels> in;
+            for (auto it : inputs) in.push_back(labels_from_py2(it.cast<py::list>()));
+            std::vector<CrtLabels> o;
+            {
+                py::gil_scoped_release rel;
+                h.set_inputs(in, as_stream(stream));
+                h.run(as_stream(stream));
+                o = h.get_outputs(as_stream(stream));
+            }
+            py::list r;
+            for (auto& x : o) r.append(labels_to_py2(x));
+            return r;
+        }, py::arg("inputs"), py::arg("stream") = 0);
+
+    // parity helpers for tests
+    m.def("hip_aes_hash_array", [](py::array_t<uint64_t, py::array::c_style | py::array::forcecast> a) {
+        DASH_CHECK(a.ndim() == 2 && a.shape(1) == 2, "expected (n,2) uint64");
+        const int64_t n = a.shape(0);
+        auto te = make_te0();
+        auto rk = fixed_round_key_words();
+        uint32_t *dte, *drk;
+        u128 *din, *dout;
+        HIPCHECK(hipMalloc(&dte, 256 * 4));
+        HIPCHECK(hipMalloc(&drk, 44 * 4));
+        HIPCHECK(hipMalloc(&din, n * 16 + 16));
+        HIPCHECK(hipMalloc(&dout, n * 16 + 16));
+        HIPCHECK(hipMemcpy(dte, te.data(), 256 * 4, hipMemcpyHostToDevice));
+        HIPCHECK(hipMemcpy(drk, rk.data(), 44 * 4, hipMemcpyHostToDevice));
+        HIPCHECK(hipMemcpy(din, a.data(), n * 16, hipMemcpyHostToDevice));
+        AesGlobals g{dte, drk};
+        launch_aes_test(din, dout, n, g, nullptr);
+        py::array_t<uint64_t> out({static_cast<py::ssize_t>(n), static_cast<py::ssize_t>(2)});
+        HIPCHECK(hipMemcpy(out.mutable_data(), dout, n * 16, hipMemcpyDeviceToHost));
+        (void)hipFree(dte); (void)hipFree(drk); (void)hipFree(din); (void)hipFree(dout);
+        return out;
+    });
+    m.def("hip_codec", [](py::array_t<int16_t, py::array::c_style | py::array::forcecast> labels, int q) {
+        // labels (N, n) label-major -> (compressed (N,2) u64, decompressed (N, n))
+        DASH_CHECK(labels.ndim() == 2, "expected (N, n)");
+        const int64_t N = labels.shape(0), n = labels.shape(1);
+        DASH_CHECK(n == nr_comps(q), "label width mismatch");
+        std::vector<int16_t> cm(N * n);
+        for (int64_t e = 0; e < N; ++e)
+            for (int64_t c = 0; c < n; ++c) cm[c * N + e] = labels.data()[e * n + c];
+        std::vector<ModC> mc(q + 1);
+        mc[q] = make_modc(q);
+        ModC* dmc;
+        int16_t *dl, *dd;
+        u128* dc;
+        HIPCHECK(hipMalloc(&dmc, sizeof(ModC) * (q + 1)));
+        HIPCHECK(hipMalloc(&dl, N * n * 2));
+        HIPCHECK(hipMalloc(&dd, N * n * 2));
+        HIPCHECK(hipMalloc(&dc, N * 16));
+        HIPCHECK(hipMemcpy(dmc, mc.data(), sizeof(ModC) * (q + 1), hipMemcpyHostToDevice));
+        HIPCHECK(hipMemcpy(dl, cm.data(), N * n * 2, hipMemcpyHostToDevice));
+        launch_codec_test(dl, N, q, dmc, dc, dd, nullptr);
+        py::array_t<uint64_t> comp({static_cast<py::ssize_t>(N), static_cast<py::ssize_t>(2)});
+        HIPCHECK(hipMemcpy(comp.mutable_data(), dc, N * 16, hipMemcpyDeviceToHost));
+        std::vector<int16_t> dec(N * n);
+        HIPCHECK(hipMemcpy(dec.data(), dd, N * n * 2, hipMemcpyDeviceToHost));
+        py::array_t<int16_t> decomp({static_cast<py::ssize_t>(N), static_cast<py::ssize_t>(n)});
+        for (int64_t e = 0; e < N; ++e)
+            for (int64_t c = 0; c < n; ++c) decomp.mutable_data()[e * n + c] = dec[c * N + e];
+        (void)hipFree(dmc); (void)hipFree(dl); (void)hipFree(dd); (void)hipFree(dc);
+        return py::make_tuple(comp, decomp);
+    });
 }
+
 }  // namespace dash

@@ -1,0 +1,85 @@
+"""GPU evaluator front-end (HIP / gfx950).
+
+`HipEvaluator` evaluates a *batch* of garbled models of the same circuit in
+one pass: every kernel launch covers (GC x residue x element), tables of all
+GCs sit in one HBM arena. Input/output labels use the same host format as the
+CPU evaluator: per residue a tuple (modulus, int16 array [N, n_p]).
+
+Replaces the reference's cuda_move / cuda_move_inputs / cuda_evaluate /
+cuda_move_outputs (garbled_circuit_interface.h:477-736).
+"""
+from __future__ import annotations
+
+from typing import Optional, Sequence
+
+from .native import native
+
+
+def _stream_handle(stream) -> int:
+    if stream is None:
+        try:
+            import torch
+
+            if torch.cuda.is_available():
+                return int(torch.cuda.current_stream().cuda_stream)
+        except Exception:
+            pass
+        return 0
+    if isinstance(stream, int):
+        return stream
+    return int(stream.cuda_stream)
+
+
+class HipEvaluator:
+    def __init__(self, models: Sequence, device: int = 0, mfma: bool = True, profile: bool = False):
+        n = native()
+        if n.hip_device_count() == 0:
+            raise RuntimeError("dash_amd: no HIP device visible; HipEvaluator needs an MI355X (gfx950)")
+        self.models = list(models)
+        self._h = n.HipEvaluator(self.models, device, mfma)
+        if profile:
+            self._h.set_profile(True)
+
+    @property
+    def batch(self) -> int:
+        return self._h.batch
+
+    def device_bytes(self) -> int:
+        return self._h.device_bytes()
+
+    def table_bytes(self) -> int:
+        return self._h.table_bytes()
+
+    def evaluate(self, inputs: Sequence, stream=None):
+        """inputs: one label list per model -> list of output label lists."""
+        return self._h.evaluate(list(inputs), _stream_handle(stream))
+
+    def set_inputs(self, inputs: Sequence, stream=None):
+        self._h.set_inputs(list(inputs), _stream_handle(stream))
+
+    def run(self, stream=None):
+        self._h.run(_stream_handle(stream))
+
+    def get_outputs(self, stream=None):
+        return self._h.get_outputs(_stream_handle(stream))
+
+    def set_profile(self, on: bool = True):
+        self._h.set_profile(on)
+
+    def op_times(self):
+        return self._h.op_times()
+
+    def layer_times(self) -> dict:
+        """Per-layer milliseconds of the last run (profile mode)."""
+        out: dict = {}
+        for name, ms in self._h.op_times():
+            layer = name.split("#")[0]
+            out[layer] = out.get(layer, 0.0) + ms
+        return out
+
+
+def hip_available() -> bool:
+    try:
+        return native().hip_device_count() > 0
+    except Exception:
+        return False

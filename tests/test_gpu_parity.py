@@ -1,0 +1,131 @@
+"""HIP evaluator vs host oracle: bit-exact labels for every layer type."""
+import numpy as np
+import pytest
+
+import dash_amd as d
+from dash_amd.garbling import GarbledCircuit
+
+pytestmark = pytest.mark.gpu
+
+
+def _hip(models, mfma=True):
+    from dash_amd.runtime import HipEvaluator
+
+    return HipEvaluator(models, mfma=mfma)
+
+
+def _check(circuit, crt, mrs, xs, mfma=True, seeds=None):
+    gcs = [GarbledCircuit(circuit, crt, mrs, seed=bytes([i + 1]) * 16) for i in range(len(xs))]
+    enc = [g.garble_inputs(x) for g, x in zip(gcs, xs)]
+    cpu = [g.cpu_evaluate(e) for g, e in zip(gcs, enc)]
+    ev = _hip([g.model for g in gcs], mfma=mfma)
+    gpu = ev.evaluate(enc)
+    for c, g in zip(cpu, gpu):
+        assert len(c) == len(g)
+        for (pc, ac), (pg, ag) in zip(c, g):
+            assert pc == pg
+            np.testing.assert_array_equal(ac, ag)
+    outs = [g.decode_outputs(o) for g, o in zip(gcs, gpu)]
+    for g, x, o in zip(gcs, xs, outs):
+        np.testing.assert_array_equal(o, g.plain_q_eval(x))
+    return outs
+
+
+def test_aes_parity(native):
+    rng = np.random.default_rng(0)
+    a = rng.integers(0, 2**63, size=(1000, 2), dtype=np.uint64)
+    np.testing.assert_array_equal(native.hip_aes_hash_array(a), native.aes_hash_array(a))
+
+
+@pytest.mark.parametrize("q", [2, 3, 5, 7, 11, 13, 17, 19, 23, 32, 56, 86, 97, 107, 167, 173])
+def test_codec_parity(native, q):
+    rng = np.random.default_rng(q)
+    n = native.nr_comps(q)
+    L = rng.integers(0, q, size=(500, n)).astype(np.int16)
+    comp, dec = native.hip_codec(L, q)
+    np.testing.assert_array_equal(dec, L)
+    for i in range(0, 500, 97):
+        c = int(comp[i, 0]) | (int(comp[i, 1]) << 64)
+        assert c == native.compress(L[i], q)
+
+
+def test_dense_relu():
+    rng = np.random.default_rng(1)
+    W1 = rng.integers(-8, 9, (20, 30)); b1 = rng.integers(-8, 9, 20)
+    W2 = rng.integers(-8, 9, (5, 20)); b2 = rng.integers(-8, 9, 5)
+    c = d.Circuit([d.Dense.from_quantized(W1, b1), d.Relu((20,)), d.Dense.from_quantized(W2, b2)])
+    xs = [rng.integers(-20, 20, 30) for _ in range(3)]
+    _check(c, 8, 100.0, xs)
+
+
+@pytest.mark.parametrize("mfma", [False, True])
+def test_conv(mfma):
+    rng = np.random.default_rng(2)
+    W = rng.integers(-5, 6, (8, 3, 3, 3)); b = rng.integers(-5, 6, 8)
+    W2 = rng.integers(-5, 6, (4, 8, 2, 2)); b2 = rng.integers(-5, 6, 4)
+    c = d.Circuit([d.Conv2d.from_quantized(W, b, 9, 9, 3, 8, 3, 3, 1, 1, pad_width=1, pad_height=1),
+                   d.Conv2d.from_quantized(W2, b2, 9, 9, 8, 4, 2, 2, 2, 2)])
+    xs = [rng.integers(-5, 6, 3 * 81) for _ in range(2)]
+    _check(c, 9, None, xs, mfma=mfma)
+
+
+def test_sign_edges():
+    vals = [0, 1, -1, 55773217, -55773217, 111546434, -111546435]
+    c = d.Circuit([d.Sign((len(vals),))])
+    _check(c, 9, [76, 7, 7, 7, 7, 7, 5, 5], [vals, vals[::-1]])
+
+
+def test_relu_edges():
+    vals = [0, 1, -1, 7, -7, 14, -15]
+    c = d.Circuit([d.Relu((len(vals),))])
+    _check(c, [2, 3, 5], [26, 6, 3, 2], [vals])
+
+
+def test_rescale_legacy():
+    rng = np.random.default_rng(3)
+    xs = [rng.integers(-100000, 100000, 300) for _ in range(2)]
+    c = d.Circuit([d.Rescale(2, (300,))])
+    _check(c, 9, 100.0, xs)
+
+
+@pytest.mark.parametrize("crt,mrs", [([32, 97, 107], [22, 19, 15, 13]), ([32, 3, 5, 7, 11, 13, 17], [10, 9, 9, 8, 7, 7, 6])])
+def test_rescale_redash(crt, mrs):
+    rng = np.random.default_rng(4)
+    xs = [rng.integers(-100000, 100000, 200) for _ in range(2)]
+    c = d.Circuit([d.Rescale([32], (200,))])
+    _check(c, crt, mrs, xs)
+
+
+def test_maxpool_sumpool_add():
+    rng = np.random.default_rng(5)
+    c = d.Circuit([d.MaxPool2d(6, 6, 2, 2, 2), d.Add((2, 3, 3), 0), d.SumPool2d(3, 3, 2, 3, 3)])
+    xs = [rng.integers(-50, 50, 72) for _ in range(2)]
+    _check(c, 7, 100.0, xs)
+
+
+def test_projection_mult_mixed():
+    c = d.Circuit([d.Projection((4,), [19], [91], lambda v: v), d.Projection((4,), [91], [19], lambda v: v % 19)])
+    _check(c, [19], None, [[0, 1, 5, 18]])
+    c = d.Circuit([d.MultLayer((4,))])
+    _check(c, [19], None, [[2, -4, -1, -2]])
+    c = d.Circuit([d.MixedModMultLayer((4,), smaller_modulus=2)])
+    _check(c, [19], None, [[5, 1, -3, 0]])
+
+
+def test_base_extension():
+    rng = np.random.default_rng(6)
+    c = d.Circuit([d.BaseExtension((20,), [32])])
+    xs = [rng.integers(0, 97 * 107, 20)]
+    gcs = GarbledCircuit(c, [32, 97, 107], [22, 19, 15, 13], seed=bytes(16))
+    enc = gcs.garble_inputs(xs[0])
+    ev = _hip([gcs.model])
+    out = gcs.decode_outputs(ev.evaluate([enc])[0])
+    np.testing.assert_array_equal(out, xs[0])
+
+
+def test_model_a_batch():
+    from dash_amd.models import build_circuit, quantized_inputs
+
+    c = build_circuit("MODEL_A")
+    xs = quantized_inputs("MODEL_A", 3)
+    _check(c, 7, 100.0, xs)
