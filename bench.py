@@ -1,0 +1,193 @@
+#!/usr/bin/env python
+"""Headline benchmark: online garbled inferences/sec for the MiniONN-style
+CIFAR-10 CNN (MODEL_F_MINIONN_POOL_REPL, DASH legacy config: ScaleQuant l=5,
+k=7 CRT base {2..17}, ReLU accuracy 100 % -> MRS {86,7,6,6,5}).
+
+Timed region per step (the reference's GPU model benchmark,
+benchmarks/model_benchmarks/sgx/Enclave/Enclave.cpp:177-183):
+    garble_inputs -> H2D -> evaluate -> D2H -> decode_outputs
+for B independent garbled circuits per GPU (one fresh input per GC per step).
+Offline garbling and the table upload are excluded, as in the reference, and
+reported separately. Data: synthetic CIFAR-shaped normalized images, random
+(PyTorch-default) initialised weights.
+
+Multi-GPU: one process per GPU (torchrun), batch data parallel; every rank
+garbles and evaluates its own GCs; decoded logits are all-gathered over RCCL.
+"""
+from __future__ import annotations
+
+import argparse
+import hashlib
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+BASELINE_INF_PER_S = 1000.0 / 1443.0  # RTX 4090, DASH GPU, MiniONN
+
+
+def log(*a):
+    print(f"[bench {time.strftime('%H:%M:%S')}]", *a, file=sys.stderr, flush=True)
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--batch", type=int, default=int(os.environ.get("DASH_BENCH_BATCH", "8")),
+                    help="garbled circuits evaluated together per GPU")
+    ap.add_argument("--model", default="MODEL_F_MINIONN_POOL_REPL")
+    ap.add_argument("--config", default="DASH", choices=["DASH", "REDASH_OPT", "REDASH_CPM"])
+    ap.add_argument("--no-mfma", action="store_true")
+    ap.add_argument("--profile", action="store_true", help="print per-layer GPU times")
+    ap.add_argument("--threads", type=int, default=0)
+    ap.add_argument("--verify", type=int, default=1)
+    args = ap.parse_args()
+
+    import torch
+
+    from dash_amd.garbling import GarbledCircuit
+    from dash_amd.ir.quant import QuantizationMethod
+    from dash_amd.models import BENCH_CONFIGS, build_circuit, canonical, quantized_inputs
+    from dash_amd.native import native
+    from dash_amd.runtime import HipEvaluator
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = world > 1
+    if dist:
+        import torch.distributed as tdist
+
+        torch.cuda.set_device(local_rank)
+        tdist.init_process_group("nccl")
+    else:
+        torch.cuda.set_device(0)
+    device = torch.cuda.current_device()
+    if args.threads:
+        native().set_num_threads(args.threads)
+
+    model = canonical(args.model)
+    cfg = BENCH_CONFIGS.get(f"{model}/{args.config}") or BENCH_CONFIGS["MODEL_F_MINIONN_POOL_REPL/DASH"]
+    qm, qp = QuantizationMethod(cfg["q_method"]), cfg["q_parameter"]
+    circuit = build_circuit(model, qm, qp, seed=0)  # public model, identical on every rank
+    B = args.batch
+    n_inputs = B * (args.steps + args.warmup)
+    inputs = quantized_inputs(model, n_inputs, qm, qp, seed=1000 + rank)
+
+    # ---------------- offline: garble B circuits, stream them into HBM
+    t_off = time.perf_counter()
+    gcs = []
+    ev = None
+    garble_s = 0.0
+    upload_s = 0.0
+    for b in range(B):
+        seed = hashlib.sha256(f"dash-bench/{rank}/{b}/{os.getpid()}".encode()).digest()[:16]
+        t = time.perf_counter()
+        gc = GarbledCircuit(circuit, cfg["crt"], cfg["mrs"], seed=seed)
+        garble_s += time.perf_counter() - t
+        t = time.perf_counter()
+        if ev is None:
+            ev = HipEvaluator(template=gc.model, batch=B, device=device, mfma=not args.no_mfma,
+                              profile=args.profile)
+        ev.load(b, gc.model)
+        upload_s += time.perf_counter() - t
+        table_gb = gc.table_bytes / 1e9
+        gc.model = None  # host copy no longer needed (tables live in HBM)
+        gcs.append(gc)
+        log(f"rank {rank}: garbled+uploaded GC {b + 1}/{B} ({table_gb:.2f} GB tables)")
+    offline_s = time.perf_counter() - t_off
+
+    stream = torch.cuda.current_stream()
+
+    def step(i: int, verify: bool = False):
+        xs = inputs[i * B:(i + 1) * B]
+        enc = [gc.garble_inputs(x) for gc, x in zip(gcs, xs)]  # online message #1
+        ev.set_inputs(enc, stream)
+        ev.run(stream)
+        outs = ev.get_outputs(stream)  # online message #2 (synchronizes)
+        dec = [gc.decode_outputs(o) for gc, o in zip(gcs, outs)]
+        if verify:
+            for gc, x, y in zip(gcs, xs, dec):
+                ref = gc.plain_q_eval(x)
+                if not np.array_equal(ref, y):
+                    raise RuntimeError(f"garbled output mismatch: {y} vs {ref}")
+        return dec
+
+    verified = False
+    for w in range(args.warmup):
+        step(w, verify=bool(args.verify) and w == 0)
+        verified = verified or bool(args.verify)
+    torch.cuda.synchronize()
+    if dist:
+        tdist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    last = None
+    for s in range(args.steps):
+        last = step(args.warmup + s)
+    torch.cuda.synchronize()
+    if dist:
+        tdist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+
+    if dist:
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        # gather decoded logits of the last step onto every rank (RCCL all-gather over xGMI)
+        logits = torch.tensor(np.stack(last), dtype=torch.int64, device="cuda")
+        gathered = [torch.empty_like(logits) for _ in range(world)]
+        tdist.all_gather(gathered, logits)
+
+    total_inf = world * B * args.steps
+    value = total_inf / elapsed
+    ms_step = 1000.0 * elapsed / args.steps
+    prof = None
+    if args.profile:
+        step(0)
+        prof = {k: round(v, 3) for k, v in ev.layer_times().items()}
+    if rank == 0:
+        out = {
+            "metric": "online garbled inferences/sec (MiniONN CIFAR-10 CNN)",
+            "value": round(value, 3),
+            "unit": "inferences/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_step, 3),
+            "ms_per_inference": round(1000.0 * elapsed / (B * args.steps), 3),
+            "latency_ms_per_batch": round(ms_step, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": round(value / BASELINE_INF_PER_S, 2),
+            "dtype": "int16 labels / int8 MFMA (exact modular arithmetic)",
+            "data": "synthetic CIFAR-10-shaped inputs, random-init weights",
+            "config": {
+                "model": model,
+                "scheme": args.config,
+                "crt_base": cfg["crt"] if isinstance(cfg["crt"], list) else native().first_primes(cfg["crt"]),
+                "mrs": cfg["mrs"],
+                "global_batch": world * B,
+                "gcs_per_gpu": B,
+                "seq_len": None,
+                "input_shape": [3, 32, 32],
+                "parallelism": f"dp{world}",
+            },
+            "offline": {"garble_s_per_gc": round(garble_s / B, 2), "upload_s_per_gc": round(upload_s / B, 2),
+                        "table_gb_per_gc": round(table_gb, 3), "offline_total_s": round(offline_s, 1)},
+            "verified_vs_plaintext": verified,
+        }
+        if prof:
+            out["layer_ms"] = prof
+        print(json.dumps(out), flush=True)
+    if dist:
+        tdist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -106,24 +106,31 @@ ModC make_modc(int q) {
 // ---------------------------------------------------------------------------
 class HipEvaluator {
    public:
-    HipEvaluator(std::vector<std::shared_ptr<GarbledModel>> models, int device, bool use_mfma)
-        : models_(std::move(models)), mfma_(use_mfma) {
-        DASH_CHECK(!models_.empty(), "HipEvaluator needs at least one garbled model");
+    HipEvaluator(std::shared_ptr<GarbledModel> tmpl, int B, int device, bool use_mfma)
+        : tmpl_(std::move(tmpl)), mfma_(use_mfma) {
+        DASH_CHECK(tmpl_ && B >= 1, "HipEvaluator needs a template model and B >= 1");
         int ndev = 0;
         if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0)
             throw std::runtime_error("dash: no HIP device available for HipEvaluator");
         dev_ = device;
         HIPCHECK(hipSetDevice(dev_));
-        const GarbledModel& m0 = *models_[0];
-        for (auto& m : models_) {
-            DASH_CHECK(m->h.crt == m0.h.crt && m->h.mrs == m0.h.mrs && m->layers.size() == m0.layers.size(),
-                       "all models of a batch must garble the same circuit");
-        }
-        B_ = static_cast<int>(models_.size());
-        crt_ = m0.h.crt;
+        B_ = B;
+        crt_ = tmpl_->h.crt;
         k_ = static_cast<int>(crt_.size());
         DASH_CHECK(k_ <= kMaxRes, "too many CRT residues for the GPU path");
+        loaded_.assign(B_, 0);
         build();
+    }
+    // Upload garbled model `m` (same circuit as the template) into batch slot b.
+    void load(int b, const GarbledModel& m) {
+        DASH_CHECK(b >= 0 && b < B_, "batch slot out of range");
+        DASH_CHECK(m.h.crt == tmpl_->h.crt && m.h.mrs == tmpl_->h.mrs && m.layers.size() == tmpl_->layers.size() &&
+                       m.h.in_dims == tmpl_->h.in_dims,
+                   "model does not garble the evaluator's circuit");
+        HIPCHECK(hipSetDevice(dev_));
+        for (auto& f : loaders_) f(b, m);
+        HIPCHECK(hipDeviceSynchronize());
+        loaded_[b] = 1;
     }
     ~HipEvaluator() {
         for (void* p : allocs_) (void)hipFree(p);
@@ -150,6 +157,7 @@ class HipEvaluator {
     }
 
     void run(hipStream_t st) {
+        for (int b = 0; b < B_; ++b) DASH_CHECK(loaded_[b], "batch slot " + std::to_string(b) + " has no garbled model loaded");
         for (size_t i = 0; i < ops_.size(); ++i) {
             if (profile_) HIPCHECK(hipEventRecord(ev_[i], st));
             ops_[i](st);
@@ -212,38 +220,43 @@ class HipEvaluator {
         HIPCHECK(hipMemcpy(d, host, count * sizeof(T), hipMemcpyHostToDevice));
         return d;
     }
-    // one device buffer holding array `name` of layer li of every model
+    // one device buffer holding array `name` of layer li of every GC slot
     const u128* upload_tables(size_t li, const std::string& name) {
-        const Array& a0 = models_[0]->layers[li].arr(name);
-        const size_t nb = a0.nbytes;
+        const size_t nb = tmpl_->layers[li].arr(name).nbytes;
         uint8_t* d = dalloc<uint8_t>(nb * B_);
-        for (int b = 0; b < B_; ++b) {
-            const Array& a = models_[b]->layers[li].arr(name);
+        loaders_.push_back([d, nb, li, name](int b, const GarbledModel& m) {
+            const Array& a = m.layers[li].arr(name);
             DASH_CHECK(a.nbytes == nb, "table size mismatch across batch");
             HIPCHECK(hipMemcpy(d + nb * b, a.buf.get(), nb, hipMemcpyHostToDevice));
-        }
+        });
         table_bytes_ += nb * B_;
         return reinterpret_cast<const u128*>(d);
     }
     const int16_t* upload_i16_rows(size_t li, const std::string& name) {
-        const Array& a0 = models_[0]->layers[li].arr(name);
-        const size_t nb = a0.nbytes;
+        const size_t nb = tmpl_->layers[li].arr(name).nbytes;
         uint8_t* d = dalloc<uint8_t>(nb * B_);
-        for (int b = 0; b < B_; ++b)
-            HIPCHECK(hipMemcpy(d + nb * b, models_[b]->layers[li].arr(name).buf.get(), nb, hipMemcpyHostToDevice));
+        loaders_.push_back([d, nb, li, name](int b, const GarbledModel& m) {
+            HIPCHECK(hipMemcpy(d + nb * b, m.layers[li].arr(name).buf.get(), nb, hipMemcpyHostToDevice));
+        });
         return reinterpret_cast<const int16_t*>(d);
     }
     // per-GC concatenated residue labels from model consts ("up.j", "down.s.j", "Z.p")
     const int16_t* upload_const_rows(const std::function<std::string(int)>& name_of) {
-        std::vector<int16_t> h(static_cast<size_t>(B_) * lab_stride_);
-        for (int b = 0; b < B_; ++b)
-            for (int j = 0; j < k_; ++j) {
-                auto it = models_[b]->consts.find(name_of(j));
-                DASH_CHECK(it != models_[b]->consts.end(), "missing model constant " + name_of(j));
-                std::memcpy(&h[static_cast<size_t>(b) * lab_stride_ + lab_off_[j]], it->second.ptr<int16_t>(),
-                            sizeof(int16_t) * nr_comps(crt_[j]));
+        int16_t* d = dalloc<int16_t>(static_cast<size_t>(B_) * lab_stride_);
+        std::vector<std::string> names;
+        for (int j = 0; j < k_; ++j) names.push_back(name_of(j));
+        const int ls = lab_stride_, k = k_;
+        std::vector<int> off(lab_off_, lab_off_ + k_), crt = crt_;
+        loaders_.push_back([d, names, ls, k, off, crt](int b, const GarbledModel& m) {
+            std::vector<int16_t> h(ls);
+            for (int j = 0; j < k; ++j) {
+                auto it = m.consts.find(names[j]);
+                DASH_CHECK(it != m.consts.end(), "missing model constant " + names[j]);
+                std::memcpy(&h[off[j]], it->second.ptr<int16_t>(), sizeof(int16_t) * nr_comps(crt[j]));
             }
-        return upload(h.data(), h.size());
+            HIPCHECK(hipMemcpy(d + static_cast<size_t>(b) * ls, h.data(), sizeof(int16_t) * ls, hipMemcpyHostToDevice));
+        });
+        return d;
     }
     CrtInfo crt_info(const std::vector<int>& mods) const {
         CrtInfo c{};
@@ -276,7 +289,7 @@ class HipEvaluator {
         a.N = N;
         a.B = B_;
         a.n_approx = sp.n_approx;
-        a.n_cast = models_[0]->layers[li].arr(pre + "s.cast1").shape[1];
+        a.n_cast = tmpl_->layers[li].arr(pre + "s.cast1").shape[1];
         a.n_sign = sp.n_sign;
         a.approx = upload_tables(li, pre + "s.approx");
         a.cast1 = upload_tables(li, pre + "s.cast1");
@@ -303,8 +316,10 @@ class HipEvaluator {
 
     void build();
 
-    std::vector<std::shared_ptr<GarbledModel>> models_;
+    std::shared_ptr<GarbledModel> tmpl_;
     bool mfma_;
+    std::vector<std::function<void(int, const GarbledModel&)>> loaders_;
+    std::vector<int> loaded_;
     int dev_ = 0, B_ = 1, k_ = 0;
     std::vector<int> crt_, out_mod_;
     i64 N0_ = 0, Nout_ = 0;
@@ -338,7 +353,7 @@ class HipEvaluator {
 };
 
 void HipEvaluator::build() {
-    const GarbledModel& m0 = *models_[0];
+    const GarbledModel& m0 = *tmpl_;
     // ---- global constants
     const int maxmod = m0.h.max_mod;
     std::vector<ModC> mc(maxmod + 1);
@@ -357,18 +372,23 @@ void HipEvaluator::build() {
     // compressed zero labels + colors for every modulus (carry init)
     zstride_ = maxmod + 1;
     {
-        std::vector<u128> zc(static_cast<size_t>(B_) * zstride_, 0);
-        std::vector<uint16_t> zcol(static_cast<size_t>(B_) * zstride_, 0);
-        for (int b = 0; b < B_; ++b) {
-            LabelBank Z = models_[b]->zero_bank();
+        u128* dzc = dalloc<u128>(static_cast<size_t>(B_) * zstride_);
+        uint16_t* dzcol = dalloc<uint16_t>(static_cast<size_t>(B_) * zstride_);
+        zc_ = dzc;
+        zcol_ = dzcol;
+        const int zs = zstride_;
+        loaders_.push_back([dzc, dzcol, zs, maxmod](int b, const GarbledModel& m) {
+            std::vector<u128> zc(zs, 0);
+            std::vector<uint16_t> zcol(zs, 0);
+            LabelBank Z = m.zero_bank();
             for (int q = 2; q <= maxmod; ++q) {
                 if (Z.lab[q].empty()) continue;
-                zc[static_cast<size_t>(b) * zstride_ + q] = compress(Z.lab[q].data(), mod_info(q));
-                zcol[static_cast<size_t>(b) * zstride_ + q] = static_cast<uint16_t>(Z.lab[q][0]);
+                zc[q] = compress(Z.lab[q].data(), mod_info(q));
+                zcol[q] = static_cast<uint16_t>(Z.lab[q][0]);
             }
-        }
-        zc_ = upload(zc.data(), zc.size());
-        zcol_ = upload(zcol.data(), zcol.size());
+            HIPCHECK(hipMemcpy(dzc + static_cast<size_t>(b) * zs, zc.data(), sizeof(u128) * zs, hipMemcpyHostToDevice));
+            HIPCHECK(hipMemcpy(dzcol + static_cast<size_t>(b) * zs, zcol.data(), sizeof(uint16_t) * zs, hipMemcpyHostToDevice));
+        });
     }
     bool any_rescale = false;
     for (auto& l : m0.layers) any_rescale |= (l.kind == K_RESCALE);
@@ -893,10 +913,14 @@ void register_hip_bindings(py::module_& m) {
         return n;
     });
     py::class_<HipEvaluator, std::shared_ptr<HipEvaluator>>(m, "HipEvaluator")
-        .def(py::init([](std::vector<std::shared_ptr<GarbledModel>> models, int device, bool mfma) {
-                 return std::make_shared<HipEvaluator>(std::move(models), device, mfma);
+        .def(py::init([](std::shared_ptr<GarbledModel> tmpl, int B, int device, bool mfma) {
+                 return std::make_shared<HipEvaluator>(std::move(tmpl), B, device, mfma);
              }),
-             py::arg("models"), py::arg("device") = 0, py::arg("mfma") = true)
+             py::arg("template"), py::arg("batch"), py::arg("device") = 0, py::arg("mfma") = true)
+        .def("load", [](HipEvaluator& h, int b, std::shared_ptr<GarbledModel> m) {
+            py::gil_scoped_release rel;
+            h.load(b, *m);
+        })
         .def_property_readonly("batch", &HipEvaluator::batch)
         .def("device_bytes", &HipEvaluator::device_bytes)
         .def("table_bytes", &HipEvaluator::table_bytes)

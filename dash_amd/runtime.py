@@ -31,14 +31,28 @@ def _stream_handle(stream) -> int:
 
 
 class HipEvaluator:
-    def __init__(self, models: Sequence, device: int = 0, mfma: bool = True, profile: bool = False):
+    def __init__(self, models: Sequence = (), device: int = 0, mfma: bool = True, profile: bool = False,
+                 template=None, batch: Optional[int] = None):
+        """Either pass all `models` (uploaded immediately), or a `template`
+        model plus a `batch` size and stream models in with `load(b, m)` so
+        that host memory never holds more than one garbled model."""
         n = native()
         if n.hip_device_count() == 0:
             raise RuntimeError("dash_amd: no HIP device visible; HipEvaluator needs an MI355X (gfx950)")
-        self.models = list(models)
-        self._h = n.HipEvaluator(self.models, device, mfma)
+        models = list(models)
+        if template is None:
+            if not models:
+                raise ValueError("need models or a template")
+            template = models[0]
+        B = batch if batch is not None else len(models)
+        self._h = n.HipEvaluator(template, B, device, mfma)
+        for b, m in enumerate(models):
+            self._h.load(b, m)
         if profile:
             self._h.set_profile(True)
+
+    def load(self, b: int, model) -> None:
+        self._h.load(b, model)
 
     @property
     def batch(self) -> int:
