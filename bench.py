@@ -105,8 +105,9 @@ def main() -> None:
 
     def step(i: int, verify: bool = False):
         xs = inputs[i * B:(i + 1) * B]
-        enc = [gc.garble_inputs(x) for gc, x in zip(gcs, xs)]  # online message #1
-        ev.set_inputs(enc, stream)
+        for b, (gc, x) in enumerate(zip(gcs, xs)):  # online message #1 (garbler -> pinned staging)
+            ev.encode_into(b, gc, x)
+        ev.upload_inputs(stream)
         ev.run(stream)
         outs = ev.get_outputs(stream)  # online message #2 (synchronizes)
         dec = [gc.decode_outputs(o) for gc, o in zip(gcs, outs)]

@@ -245,6 +245,23 @@ PYBIND11_MODULE(_dash_native, m) {
             std::vector<i64> v(x.data(), x.data() + x.size());
             return labels_to_py(g.encode(v));
         })
+        .def("encode_cm", [](const Garbler& g, py::array_t<i64, py::array::c_style | py::array::forcecast> x) {
+            // online message #1 in component-major layout: one (n_j, N) int16 array per residue
+            const i64 N = x.size();
+            py::list out;
+            std::vector<py::array_t<int16_t>> arrs;
+            std::vector<comp_t*> dst;
+            for (int p : g.crt()) {
+                arrs.emplace_back(std::vector<py::ssize_t>{nr_comps(p), static_cast<py::ssize_t>(N)});
+                dst.push_back(arrs.back().mutable_data());
+            }
+            {
+                py::gil_scoped_release rel;
+                g.encode_cm(x.data(), N, dst);
+            }
+            for (auto& a : arrs) out.append(a);
+            return out;
+        })
         .def("decoder", [](const Garbler& g) { return std::make_shared<Decoder>(g.decoder()); })
         .def_property_readonly("crt_modulus", &Garbler::crt_modulus)
         .def("offset_label", [](const Garbler& g, int p) {

@@ -174,6 +174,44 @@ CrtLabels Garbler::encode(const std::vector<i64>& x) const {
     return out;
 }
 
+void Garbler::encode_cm(const i64* x, i64 N, const std::vector<comp_t*>& dst, int nthreads) const {
+    DASH_CHECK(!in_base_.empty() && in_base_[0].N == N, "input size does not match the garbled circuit");
+    DASH_CHECK(dst.size() == crt_.size(), "need one destination per residue");
+    const int k = static_cast<int>(crt_.size());
+    // residues of every input once, then per residue a (value x component) LUT of v*R mod p
+    std::vector<std::vector<uint16_t>> res(k, std::vector<uint16_t>(N));
+    for (int j = 0; j < k; ++j)
+        for (i64 e = 0; e < N; ++e) res[j][e] = static_cast<uint16_t>(pmod(x[e], crt_[j]));
+    i64 total = 0;
+    std::vector<i64> start(k + 1, 0);
+    for (int j = 0; j < k; ++j) start[j + 1] = start[j] + nr_comps(crt_[j]);
+    total = start[k];
+    std::vector<std::vector<int16_t>> lut(k);
+    for (int j = 0; j < k; ++j) {
+        const int p = crt_[j], n = nr_comps(p);
+        const comp_t* R = R_.get(p);
+        lut[j].resize(static_cast<size_t>(p) * n);
+        for (int v = 0; v < p; ++v)
+            for (int c = 0; c < n; ++c) lut[j][v * n + c] = static_cast<int16_t>((v * R[c]) % p);
+    }
+    parallel_for(total, [&](i64 r0, i64 r1) {
+        for (i64 r = r0; r < r1; ++r) {
+            int j = 0;
+            while (start[j + 1] <= r) ++j;
+            const int c = static_cast<int>(r - start[j]);
+            const int p = crt_[j], n = nr_comps(p);
+            const Labels& W0 = in_base_[j];
+            const int16_t* L = lut[j].data();
+            comp_t* out = dst[j] + static_cast<i64>(c) * N;
+            const uint16_t* rv = res[j].data();
+            for (i64 e = 0; e < N; ++e) {
+                int v = W0.c[e * n + c] + L[rv[e] * n + c];
+                out[e] = static_cast<comp_t>(v >= p ? v - p : v);
+            }
+        }
+    }, nthreads);
+}
+
 GarbledModel Garbler::garble(const std::vector<LayerSpec>& layers, const std::vector<i64>& in_dims,
                              const GarbleOptions& opt) {
     const int nt = opt.nthreads;

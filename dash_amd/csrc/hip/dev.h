@@ -214,6 +214,45 @@ __device__ __forceinline__ u128 aes_encrypt(const AesCtx& a, u128 in) {
            ((static_cast<uint64_t>(bswap32(o1)) << 32) | bswap32(o0));
 }
 
+
+// Two independent blocks with interleaved rounds: doubles the LDS-read ILP of
+// a latency-bound lane (the serial sign chain) at no extra instructions.
+__device__ __forceinline__ void aes_encrypt2(const AesCtx& a, u128 inA, u128 inB, u128& outA, u128& outB) {
+    const uint32_t* rk = a.rk;
+    uint32_t a0 = bswap32(static_cast<uint32_t>(inA)) ^ rk[0], a1 = bswap32(static_cast<uint32_t>(inA >> 32)) ^ rk[1];
+    uint32_t a2 = bswap32(static_cast<uint32_t>(inA >> 64)) ^ rk[2], a3 = bswap32(static_cast<uint32_t>(inA >> 96)) ^ rk[3];
+    uint32_t b0 = bswap32(static_cast<uint32_t>(inB)) ^ rk[0], b1 = bswap32(static_cast<uint32_t>(inB >> 32)) ^ rk[1];
+    uint32_t b2 = bswap32(static_cast<uint32_t>(inB >> 64)) ^ rk[2], b3 = bswap32(static_cast<uint32_t>(inB >> 96)) ^ rk[3];
+#define DASH_AES_COL(s0, s1, s2, s3, r)                                                              \
+    (te(a, (s0) >> 24) ^ ror32(te(a, ((s1) >> 16) & 0xff), 8) ^ ror32(te(a, ((s2) >> 8) & 0xff), 16) ^ \
+     ror32(te(a, (s3)&0xff), 24) ^ rk[r])
+#pragma unroll
+    for (int r = 1; r < 10; ++r) {
+        uint32_t ta0 = DASH_AES_COL(a0, a1, a2, a3, 4 * r + 0);
+        uint32_t tb0 = DASH_AES_COL(b0, b1, b2, b3, 4 * r + 0);
+        uint32_t ta1 = DASH_AES_COL(a1, a2, a3, a0, 4 * r + 1);
+        uint32_t tb1 = DASH_AES_COL(b1, b2, b3, b0, 4 * r + 1);
+        uint32_t ta2 = DASH_AES_COL(a2, a3, a0, a1, 4 * r + 2);
+        uint32_t tb2 = DASH_AES_COL(b2, b3, b0, b1, 4 * r + 2);
+        uint32_t ta3 = DASH_AES_COL(a3, a0, a1, a2, 4 * r + 3);
+        uint32_t tb3 = DASH_AES_COL(b3, b0, b1, b2, 4 * r + 3);
+        a0 = ta0; a1 = ta1; a2 = ta2; a3 = ta3;
+        b0 = tb0; b1 = tb1; b2 = tb2; b3 = tb3;
+    }
+#undef DASH_AES_COL
+    auto S = [&](uint32_t x) { return (te(a, x) >> 8) & 0xffu; };
+    auto last = [&](uint32_t s0, uint32_t s1, uint32_t s2, uint32_t s3) -> u128 {
+        uint32_t o0 = (S(s0 >> 24) << 24) ^ (S((s1 >> 16) & 0xff) << 16) ^ (S((s2 >> 8) & 0xff) << 8) ^ S(s3 & 0xff) ^ rk[40];
+        uint32_t o1 = (S(s1 >> 24) << 24) ^ (S((s2 >> 16) & 0xff) << 16) ^ (S((s3 >> 8) & 0xff) << 8) ^ S(s0 & 0xff) ^ rk[41];
+        uint32_t o2 = (S(s2 >> 24) << 24) ^ (S((s3 >> 16) & 0xff) << 16) ^ (S((s0 >> 8) & 0xff) << 8) ^ S(s1 & 0xff) ^ rk[42];
+        uint32_t o3 = (S(s3 >> 24) << 24) ^ (S((s0 >> 16) & 0xff) << 16) ^ (S((s1 >> 8) & 0xff) << 8) ^ S(s2 & 0xff) ^ rk[43];
+        return (static_cast<u128>((static_cast<uint64_t>(bswap32(o3)) << 32) | bswap32(o2)) << 64) |
+               ((static_cast<uint64_t>(bswap32(o1)) << 32) | bswap32(o0));
+    };
+    outA = last(a0, a1, a2, a3);
+    outB = last(b0, b1, b2, b3);
+}
+
 // Global tables: Te0 (256 words) and the fixed-key round keys (44 words).
 struct AesGlobals {
     const uint32_t* te0;

@@ -35,17 +35,25 @@ __global__ __launch_bounds__(256) void k_sign_approx(SignArgs a, Act x, const Mo
     const int p = a.crt.p[j];
     const ModC m = mc[p];
     const int16_t* L = x.p[j] + static_cast<int64_t>(b) * m.n * N + e;
+    const uint32_t col = static_cast<uint16_t>(L[0]) % static_cast<uint32_t>(p);
+    const u128* T = a.approx + (static_cast<int64_t>(b) * N + e) * a.n_approx + static_cast<int64_t>(a.t) * a.crt.prefix[j];
+    // issue the table gathers first: their HBM latency hides under the AES
+    u128 ent[8];
+#pragma unroll
+    for (int d = 0; d < 8; ++d)
+        if (d < a.t) ent[d] = T[d * p + col];
     const u128 C = compress_cm(L, N, m);
     const u128 H = aes_encrypt(aes, C);
-    const uint32_t col = static_cast<uint16_t>(L[0]) % static_cast<uint32_t>(p);
     const int64_t bke = (static_cast<int64_t>(b) * a.crt.k + j) * N + e;
     if (a.hx) {
         a.hx[bke] = H;
         a.colx[bke] = static_cast<uint16_t>(col);
     }
-    const u128* T = a.approx + (static_cast<int64_t>(b) * N + e) * a.n_approx + static_cast<int64_t>(a.t) * a.crt.prefix[j];
     u128* out = a.mrsP + (static_cast<int64_t>(b) * a.crt.k + j) * a.t * N + e;
-    for (int d = 0; d < a.t; ++d) out[static_cast<int64_t>(d) * N] = T[d * p + col] - H;
+#pragma unroll
+    for (int d = 0; d < 8; ++d)
+        if (d < a.t) out[static_cast<int64_t>(d) * N] = ent[d] - H;
+    for (int d = 8; d < a.t; ++d) out[static_cast<int64_t>(d) * N] = T[d * p + col] - H;
 }
 
 // ---------------------------------------------------------------------------
@@ -74,24 +82,44 @@ __global__ __launch_bounds__(128) void k_sign_chain(SignArgs a, const ModC* mc, 
         const ModC Mo = mc[mo];
 #pragma unroll
         for (int i = 0; i < MAXN; ++i) acc[i] = 0;
-        for (int j = 0; j <= k; ++j) {
-            u128 key;
-            uint32_t col;
+        for (int j = 0; j <= k; j += 2) {
+            const bool two = j + 1 <= k;
+            u128 keyA, keyB = 0;
+            uint32_t colA, colB = 0;
             if (j < k) {
-                key = P0[(static_cast<int64_t>(j) * t + d) * N];
-                col = u128_mod(key, Mm);
+                keyA = P0[(static_cast<int64_t>(j) * t + d) * N];
+                colA = u128_mod(keyA, Mm);
             } else {
-                key = carry;
-                col = ccol;
+                keyA = carry;
+                colA = ccol;
             }
-            const u128 H = aes_encrypt(aes, key);
-            const u128 P = T1[c1 + col] - H;
-            c1 += m;
-            DigitStream s;
-            s.init(P);
+            if (two) {
+                if (j + 1 < k) {
+                    keyB = P0[(static_cast<int64_t>(j + 1) * t + d) * N];
+                    colB = u128_mod(keyB, Mm);
+                } else {
+                    keyB = carry;
+                    colB = ccol;
+                }
+            }
+            // gathers before the AES so the HBM latency overlaps it
+            const u128 TA = T1[c1 + colA];
+            const u128 TB = two ? T1[c1 + m + colB] : static_cast<u128>(0);
+            u128 HA, HB;
+            if (two)
+                aes_encrypt2(aes, keyA, keyB, HA, HB);
+            else
+                HA = aes_encrypt(aes, keyA);
+            c1 += two ? 2 * m : m;
+            DigitStream sa, sb;
+            sa.init(TA - HA);
+            sb.init(TB - HB);
 #pragma unroll
             for (int i = 0; i < MAXN; ++i)
-                if (i < static_cast<int>(Mo.n)) acc[i] += static_cast<int32_t>(s.next(Mo));
+                if (i < static_cast<int>(Mo.n)) {
+                    acc[i] += static_cast<int32_t>(sa.next(Mo));
+                    if (two) acc[i] += static_cast<int32_t>(sb.next(Mo));
+                }
         }
         CompressFwd cf;
         cf.init();
@@ -100,8 +128,9 @@ __global__ __launch_bounds__(128) void k_sign_chain(SignArgs a, const ModC* mc, 
             if (i < static_cast<int>(Mo.n)) cf.push(static_cast<uint32_t>(acc[i]) % mo, Mo);
         const u128 key2 = cf.finish();
         const uint32_t col2 = static_cast<uint32_t>(acc[0]) % mo;
+        const u128 T2e = T2[c2 + col2];
         const u128 H2 = aes_encrypt(aes, key2);
-        carry = T2[c2 + col2] - H2;
+        carry = T2e - H2;
         c2 += mo;
         ccol = u128_mod(carry, mc[a.mrs[d - 1]]);
     }
@@ -125,10 +154,11 @@ __global__ __launch_bounds__(128) void k_sign_chain(SignArgs a, const ModC* mc, 
         if (i < static_cast<int>(M0.n)) cf.push(static_cast<uint32_t>(acc[i]) % m0, M0);
     const u128 key = cf.finish();
     const uint32_t col = static_cast<uint32_t>(acc[0]) % m0;
-    const u128 H = aes_encrypt(aes, key);
     const u128* TS = a.sign + (static_cast<int64_t>(b) * N + e) * a.n_sign;
+    const u128 TS0 = TS[col];
+    const u128 H = aes_encrypt(aes, key);
     for (int o = 0; o < a.nout; ++o) {
-        const u128 P = TS[o * m0 + col] - H;
+        const u128 P = (o == 0 ? TS0 : TS[o * m0 + col]) - H;
         a.outP[(static_cast<int64_t>(b) * a.nout + o) * N + e] = P;
         if (a.relu && o == 0) {
             a.hs[static_cast<int64_t>(b) * N + e] = aes_encrypt(aes, P);
@@ -279,6 +309,95 @@ __global__ __launch_bounds__(256) void k_rescale_post(Act x, CrtInfo crt, int64_
         int32_t v = L[i * N] - D[i];
         L[i * N] = static_cast<int16_t>(v < 0 ? v + p : v);
     }
+}
+
+
+// ---------------------------------------------------------------------------
+// Legacy (DASH) rescale, fused per iteration:
+//   hash   : residue-0 key from the previous iteration's sign payload bits
+//            (mod-2 labels: +/- is XOR, so no decompress at all)
+//   update : L_j = (L_j + delta_j - proj(L_0)) * 2^-1 streamed digit by digit,
+//            compressed on the fly and hashed -> approx projections of the
+//            next sign gadget (phase A) in the same pass.
+// The downshift of iteration i and the upshift of i+1 collapse into one
+// delta = up - down; only the last iteration writes a downshifted result.
+__global__ __launch_bounds__(256) void k_rescale_hash_sign(const u128* signP, const u128* du, int64_t N, u128* h0,
+                                                           uint16_t* col0, const uint32_t* te0, const uint32_t* rk) {
+    AES_PROLOGUE(te0, rk);
+    const int b = blockIdx.z;
+    const int64_t e = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (e >= N) return;
+    const u128 C = signP[static_cast<int64_t>(b) * N + e] ^ du[b];
+    h0[static_cast<int64_t>(b) * N + e] = aes_encrypt(aes, C);
+    col0[static_cast<int64_t>(b) * N + e] = static_cast<uint16_t>(static_cast<uint32_t>(C) & 1u);
+}
+
+// grid (ceil(N/256), k, B)
+__global__ __launch_bounds__(256) void k_rescale_update_approx(RescaleArgs r, SignArgs a, Act x, const int16_t* delta,
+                                                               const u128* zh, const ModC* mc, const uint32_t* te0,
+                                                               const uint32_t* rk) {
+    AES_PROLOGUE(te0, rk);
+    const int j = blockIdx.y, b = blockIdx.z;
+    const int64_t N = r.N;
+    const int64_t e = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (e >= N) return;
+    const int p = r.crt.p[j];
+    const ModC m = mc[p];
+    const int64_t be = static_cast<int64_t>(b) * N + e;
+    const u128* TA = a.approx + be * a.n_approx + static_cast<int64_t>(a.t) * a.crt.prefix[j];
+    u128 H;
+    uint32_t col;
+    u128 ent[8];
+    if (j == r.fi) {
+        // factor residue is the zero label: constant key per GC
+        H = zh[static_cast<int64_t>(b) * a.zc_stride + p];
+        col = a.zcol[static_cast<int64_t>(b) * a.zc_stride + p];
+#pragma unroll
+        for (int d = 0; d < 8; ++d)
+            if (d < a.t) ent[d] = TA[d * p + col];
+    } else {
+        const u128 Tt = r.trans[be * r.n_trans + static_cast<int64_t>(r.aidx[j]) * r.s + r.col0[be]];
+        const u128 P = Tt - r.h0[be];
+        int16_t* L = x.p[j] + static_cast<int64_t>(b) * m.n * N + e;
+        const int16_t* Dl = delta + static_cast<int64_t>(b) * r.lab_stride + r.lab_off[j];
+        DigitStream s;
+        s.init(P);
+        CompressFwd cf;
+        cf.init();
+        const int32_t inv = r.inv[j];
+        col = 0;
+        for (int i = 0; i < static_cast<int>(m.n); ++i) {
+            int32_t v = L[i * N] + Dl[i] - static_cast<int32_t>(s.next(m));
+            v %= p;
+            if (v < 0) v += p;
+            v = (v * inv) % p;
+            L[i * N] = static_cast<int16_t>(v);
+            cf.push(static_cast<uint32_t>(v), m);
+            if (i == 0) {
+                col = static_cast<uint32_t>(v);
+#pragma unroll
+                for (int d = 0; d < 8; ++d)
+                    if (d < a.t) ent[d] = TA[d * p + col];
+            }
+        }
+        H = aes_encrypt(aes, cf.finish());
+    }
+    u128* out = a.mrsP + (static_cast<int64_t>(b) * a.crt.k + j) * a.t * N + e;
+#pragma unroll
+    for (int d = 0; d < 8; ++d)
+        if (d < a.t) out[static_cast<int64_t>(d) * N] = ent[d] - H;
+    for (int d = 8; d < a.t; ++d) out[static_cast<int64_t>(d) * N] = TA[d * p + col] - H;
+}
+
+void launch_rescale_hash_sign(const u128* signP, const u128* du, int64_t N, int B, u128* h0, uint16_t* col0,
+                              const AesGlobals& g, hipStream_t st) {
+    hipLaunchKernelGGL(k_rescale_hash_sign, dim3(static_cast<unsigned>((N + 255) / 256), 1, B), dim3(256),
+                       DASH_AES_LDS_WORDS * sizeof(uint32_t), st, signP, du, N, h0, col0, g.te0, g.rk);
+}
+void launch_rescale_update_approx(const RescaleArgs& r, const SignArgs& a, const Act& x, const int16_t* delta,
+                                  const u128* zh, int B, const ModC* mc, const AesGlobals& g, hipStream_t st) {
+    hipLaunchKernelGGL(k_rescale_update_approx, dim3(static_cast<unsigned>((r.N + 255) / 256), r.crt.k, B), dim3(256),
+                       DASH_AES_LDS_WORDS * sizeof(uint32_t), st, r, a, x, delta, zh, mc, g.te0, g.rk);
 }
 
 // ---------------------------------------------------------------------------

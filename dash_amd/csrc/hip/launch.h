@@ -20,6 +20,10 @@ void launch_rescale_hash(const Act& x, int fi, int s, const int16_t* up, int up_
 void launch_rescale_update(const RescaleArgs& a, const Act& x, int B, const ModC* mc, hipStream_t st);
 void launch_rescale_post(const Act& x, const CrtInfo& crt, int64_t N, int B, const u128* signP, const int16_t* down,
                          int lab_stride, const int* lab_off, const ModC* mc, hipStream_t st);
+void launch_rescale_hash_sign(const u128* signP, const u128* du, int64_t N, int B, u128* h0, uint16_t* col0,
+                              const AesGlobals& g, hipStream_t st);
+void launch_rescale_update_approx(const RescaleArgs& r, const SignArgs& a, const Act& x, const int16_t* delta,
+                                  const u128* zh, int B, const ModC* mc, const AesGlobals& g, hipStream_t st);
 void launch_base_ext(const BEArgs& a, const Act& x, int B, const ModC* mc, const AesGlobals& g, hipStream_t st);
 void launch_proj(const ProjArgs& a, const Act& x, const Act& y, int B, const ModC* mc, const AesGlobals& g,
                  hipStream_t st);

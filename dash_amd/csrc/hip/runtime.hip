@@ -156,6 +156,20 @@ class HipEvaluator {
         }
     }
 
+    // pinned staging slots for GC b (one component-major block per residue)
+    std::vector<int16_t*> input_slot(int b) const {
+        DASH_CHECK(b >= 0 && b < B_, "batch slot out of range");
+        std::vector<int16_t*> v;
+        for (int j = 0; j < k_; ++j) v.push_back(in_stage_[j] + static_cast<i64>(b) * nr_comps(crt_[j]) * N0_);
+        return v;
+    }
+    i64 input_size() const { return N0_; }
+    void upload_inputs(hipStream_t st) {
+        for (int j = 0; j < k_; ++j)
+            HIPCHECK(hipMemcpyAsync(bufs_[0].p[j], in_stage_[j], sizeof(int16_t) * B_ * nr_comps(crt_[j]) * N0_,
+                                    hipMemcpyHostToDevice, st));
+    }
+
     void run(hipStream_t st) {
         for (int b = 0; b < B_; ++b) DASH_CHECK(loaded_[b], "batch slot " + std::to_string(b) + " has no garbled model loaded");
         for (size_t i = 0; i < ops_.size(); ++i) {
@@ -315,6 +329,7 @@ class HipEvaluator {
     }
 
     void build();
+    void plan_rescale_legacy(size_t li, i64 iters, i64 N, const CrtInfo& crt, const std::string& lname);
 
     std::shared_ptr<GarbledModel> tmpl_;
     bool mfma_;
@@ -331,6 +346,7 @@ class HipEvaluator {
     std::vector<hipEvent_t> ev_;
     Act bufs_[4]{};  // ping-pong activation buffers (+ scratch)
     Act final_{};
+    Act cur_act_{};
     std::vector<int16_t*> in_stage_, out_stage_;
     // constants
     ModC* mc_ = nullptr;
@@ -341,6 +357,7 @@ class HipEvaluator {
     const int16_t* zero_rows_ = nullptr;
     const int16_t* up_rows_ = nullptr;
     const u128* zc_ = nullptr;
+    const u128* zh_ = nullptr;
     const uint16_t* zcol_ = nullptr;
     int zstride_ = 0;
     // scratch
@@ -373,20 +390,24 @@ void HipEvaluator::build() {
     zstride_ = maxmod + 1;
     {
         u128* dzc = dalloc<u128>(static_cast<size_t>(B_) * zstride_);
+        u128* dzh = dalloc<u128>(static_cast<size_t>(B_) * zstride_);
         uint16_t* dzcol = dalloc<uint16_t>(static_cast<size_t>(B_) * zstride_);
         zc_ = dzc;
+        zh_ = dzh;
         zcol_ = dzcol;
         const int zs = zstride_;
-        loaders_.push_back([dzc, dzcol, zs, maxmod](int b, const GarbledModel& m) {
-            std::vector<u128> zc(zs, 0);
+        loaders_.push_back([dzc, dzh, dzcol, zs, maxmod](int b, const GarbledModel& m) {
+            std::vector<u128> zc(zs, 0), zh(zs, 0);
             std::vector<uint16_t> zcol(zs, 0);
             LabelBank Z = m.zero_bank();
             for (int q = 2; q <= maxmod; ++q) {
                 if (Z.lab[q].empty()) continue;
                 zc[q] = compress(Z.lab[q].data(), mod_info(q));
+                zh[q] = hash(zc[q]);
                 zcol[q] = static_cast<uint16_t>(Z.lab[q][0]);
             }
             HIPCHECK(hipMemcpy(dzc + static_cast<size_t>(b) * zs, zc.data(), sizeof(u128) * zs, hipMemcpyHostToDevice));
+            HIPCHECK(hipMemcpy(dzh + static_cast<size_t>(b) * zs, zh.data(), sizeof(u128) * zs, hipMemcpyHostToDevice));
             HIPCHECK(hipMemcpy(dzcol + static_cast<size_t>(b) * zs, zcol.data(), sizeof(uint16_t) * zs, hipMemcpyHostToDevice));
         });
     }
@@ -478,6 +499,7 @@ void HipEvaluator::build() {
         const GLayer& g = m0.layers[li];
         const int nxt = (cur + 1) % 2;
         const std::string lname = std::string(kind_name(g.kind)) + "#" + std::to_string(li);
+        cur_act_ = act_of(cur);
         switch (g.kind) {
             case K_FLATTEN:
                 break;
@@ -593,6 +615,10 @@ void HipEvaluator::build() {
             case K_RESCALE: {
                 const i64 mode = g.param("mode", 0);
                 const i64 iters = g.param("iters");
+                if (mode == 0) {
+                    plan_rescale_legacy(li, iters, N, crt, lname);
+                    break;
+                }
                 for (i64 it = 0; it < iters; ++it) {
                     std::vector<int> factors;
                     if (mode == 0)
@@ -878,6 +904,95 @@ void HipEvaluator::build() {
     HIPCHECK(hipDeviceSynchronize());
 }
 
+void HipEvaluator::plan_rescale_legacy(size_t li, i64 iters, i64 N, const CrtInfo& crt, const std::string& lname) {
+    const GarbledModel& m0 = *tmpl_;
+    Act x = act_of(0);
+    // the current activation buffer is whatever `cur` is; callers keep the
+    // in-place convention: rescale always operates on the current buffer
+    x = cur_act_;
+    const ModC* mc = mc_;
+    const AesGlobals ag = aes_;
+    const int B = B_;
+    const int ls = lab_stride_;
+    DASH_CHECK(crt_[0] == 2, "legacy rescale needs crt[0] == 2");
+    // per-GC constants: delta = up - down (all residues), du = bits(up0) ^ bits(down0)
+    const int16_t* delta = nullptr;
+    const u128* du = nullptr;
+    {
+        int16_t* dd = dalloc<int16_t>(static_cast<size_t>(B_) * lab_stride_);
+        u128* ddu = dalloc<u128>(B_);
+        const int k = k_;
+        std::vector<int> off(lab_off_, lab_off_ + k_), crtv = crt_;
+        loaders_.push_back([dd, ddu, ls, k, off, crtv](int b, const GarbledModel& m) {
+            std::vector<int16_t> h(ls);
+            u128 pk = 0;
+            for (int j = 0; j < k; ++j) {
+                const int p = crtv[j], n = nr_comps(p);
+                const int16_t* up = m.consts.at("up." + std::to_string(j)).ptr<int16_t>();
+                const int16_t* dn = m.consts.at("down.2." + std::to_string(j)).ptr<int16_t>();
+                for (int c = 0; c < n; ++c) h[off[j] + c] = static_cast<int16_t>(pmod(up[c] - dn[c], p));
+                if (j == 0)
+                    for (int c = 0; c < n; ++c) pk |= static_cast<u128>((up[c] ^ dn[c]) & 1) << c;
+            }
+            HIPCHECK(hipMemcpy(dd + static_cast<size_t>(b) * ls, h.data(), sizeof(int16_t) * ls, hipMemcpyHostToDevice));
+            HIPCHECK(hipMemcpy(ddu + b, &pk, sizeof(u128), hipMemcpyHostToDevice));
+        });
+        delta = dd;
+        du = ddu;
+    }
+    const int16_t* down = upload_const_rows([&](int j) { return "down.2." + std::to_string(j); });
+    for (i64 it = 0; it < iters; ++it) {
+        RescalePlan P(crt_, m0.h.mrs, {2}, true);
+        const std::string pre = arr_name("it", static_cast<int>(it), ".");
+        const u128* trans = upload_tables(li, pre + "trans");
+        SignArgs sa = make_sign(li, pre, P.sign, N, 0);
+        const int maxn = sign_maxn_;
+        u128* h0 = h0_;
+        uint16_t* col0 = col0_;
+        if (it == 0) {
+            const int16_t* up = up_rows_ + lab_off_[0];
+            add_op(lname + ".hash", [x, up, ls, N, B, h0, col0, mc, ag](hipStream_t st) {
+                launch_rescale_hash(x, 0, 2, up, ls, 1, N, B, h0, col0, mc, ag, st);
+            });
+        } else {
+            const u128* sp = outP_;
+            add_op(lname + ".hash", [sp, du, N, B, h0, col0, ag](hipStream_t st) {
+                launch_rescale_hash_sign(sp, du, N, B, h0, col0, ag, st);
+            });
+        }
+        RescaleArgs ra{};
+        ra.crt = crt;
+        ra.N = N;
+        ra.fi = 0;
+        ra.s = 2;
+        ra.add_up = 1;
+        for (size_t q = 0; q < P.active[0].size(); ++q) {
+            const int jj = P.active[0][q];
+            ra.active[jj] = 1;
+            ra.aidx[jj] = static_cast<int>(q);
+            ra.inv[jj] = static_cast<int>(P.inv[0][q]);
+        }
+        ra.n_trans = P.n_trans;
+        ra.off = 0;
+        ra.trans = trans;
+        ra.h0 = h0_;
+        ra.col0 = col0_;
+        ra.lab_stride = lab_stride_;
+        for (int j = 0; j < k_; ++j) ra.lab_off[j] = lab_off_[j];
+        const int16_t* dl = it == 0 ? up_rows_ : delta;
+        const u128* zh = zh_;
+        add_op(lname + ".upd+A", [ra, sa, x, dl, zh, B, mc, ag](hipStream_t st) {
+            launch_rescale_update_approx(ra, sa, x, dl, zh, B, mc, ag, st);
+        });
+        add_op(lname + ".B", [sa, maxn, mc, ag](hipStream_t st) { launch_sign_chain(sa, maxn, mc, ag, st); });
+    }
+    const u128* signP = outP_;
+    const int* loff = d_lab_off_;
+    add_op(lname + ".post", [x, crt, N, B, signP, down, ls, loff, mc](hipStream_t st) {
+        launch_rescale_post(x, crt, N, B, signP, down, ls, loff, mc, st);
+    });
+}
+
 // ---------------------------------------------------------------------------
 namespace {
 py::list labels_to_py2(const CrtLabels& L) {
@@ -907,6 +1022,17 @@ hipStream_t as_stream(uintptr_t s) { return reinterpret_cast<hipStream_t>(s); }
 }  // namespace
 
 void register_hip_bindings(py::module_& m) {
+    // in-process two-party fast path: the garbler encodes straight into the
+    // evaluator's pinned staging slot (the bytes are exactly online message #1)
+    m.def("encode_into", [](const Garbler& g, py::array_t<i64, py::array::c_style | py::array::forcecast> x,
+                            HipEvaluator& h, int b) {
+        auto slot = h.input_slot(b);
+        DASH_CHECK(x.size() == h.input_size(), "input size mismatch");
+        const i64* xp = x.data();
+        const i64 N = x.size();
+        py::gil_scoped_release rel;
+        g.encode_cm(xp, N, slot);
+    });
     m.def("hip_device_count", []() {
         int n = 0;
         if (hipGetDeviceCount(&n) != hipSuccess) return 0;
@@ -932,6 +1058,15 @@ void register_hip_bindings(py::module_& m) {
             h.set_inputs(in, as_stream(stream));
         }, py::arg("inputs"), py::arg("stream") = 0)
         .def("run", [](HipEvaluator& h, uintptr_t stream) { h.run(as_stream(stream)); }, py::arg("stream") = 0)
+        .def("set_input_cm", [](HipEvaluator& h, int b, const py::list& arrs) {
+            auto slot = h.input_slot(b);
+            DASH_CHECK(static_cast<size_t>(py::len(arrs)) == slot.size(), "one array per residue expected");
+            for (size_t j = 0; j < slot.size(); ++j) {
+                auto a = py::array_t<int16_t, py::array::c_style | py::array::forcecast>::ensure(arrs[j]);
+                std::memcpy(slot[j], a.data(), a.size() * sizeof(int16_t));
+            }
+        })
+        .def("upload_inputs", [](HipEvaluator& h, uintptr_t stream) { h.upload_inputs(as_stream(stream)); }, py::arg("stream") = 0)
         .def("get_outputs", [](HipEvaluator& h, uintptr_t stream) {
             auto o = h.get_outputs(as_stream(stream));
             py::list r;

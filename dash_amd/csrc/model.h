@@ -102,6 +102,8 @@ class Garbler {
                         const GarbleOptions& opt = {});
     // Online message #1: encoded inputs x -> W0 + (x mod p) * R
     CrtLabels encode(const std::vector<i64>& x) const;
+    // Same message, component-major per residue: dst[j][c * N + e]
+    void encode_cm(const i64* x, i64 N, const std::vector<comp_t*>& dst, int nthreads = 0) const;
     const Decoder& decoder() const { return dec_; }
     const std::vector<int>& crt() const { return crt_; }
     i64 crt_modulus() const { return M_; }

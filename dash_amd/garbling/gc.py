@@ -63,6 +63,12 @@ class GarbledCircuit:
         assert x.size == self.circuit.input_size, "input dimension does not match circuit input dimension"
         return self.garbler.encode(x)
 
+    def garble_inputs_cm(self, x: np.ndarray) -> list:
+        """Online message #1 in the GPU wire layout: per residue an int16 (n_p, N) array."""
+        x = np.asarray(x, dtype=np.int64).reshape(-1)
+        assert x.size == self.circuit.input_size, "input dimension does not match circuit input dimension"
+        return self.garbler.encode_cm(x)
+
     def cpu_evaluate(self, labels: Labels, nr_threads: int = 0) -> Labels:
         return self._n.cpu_evaluate(self.model, labels, nr_threads)
 

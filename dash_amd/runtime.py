@@ -71,6 +71,20 @@ class HipEvaluator:
     def set_inputs(self, inputs: Sequence, stream=None):
         self._h.set_inputs(list(inputs), _stream_handle(stream))
 
+    def set_input_cm(self, b: int, arrays) -> None:
+        """Stage component-major input labels (GarbledCircuit.garble_inputs_cm) for slot b."""
+        self._h.set_input_cm(b, list(arrays))
+
+    def encode_into(self, b: int, gc, x) -> None:
+        """In-process fast path: garbler `gc` encodes x straight into the pinned staging slot b."""
+        import numpy as np
+
+        native().encode_into(gc.garbler, np.asarray(x, dtype=np.int64).reshape(-1), self._h, b)
+
+    def upload_inputs(self, stream=None) -> None:
+        """H2D of every staged slot (async on `stream`)."""
+        self._h.upload_inputs(_stream_handle(stream))
+
     def run(self, stream=None):
         self._h.run(_stream_handle(stream))
 

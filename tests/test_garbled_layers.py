@@ -1,0 +1,239 @@
+"""End-to-end garbling tests (garble -> encode -> host evaluate -> decode vs the
+plaintext reference), ported from the reference's gtest suite
+(dash/test/test_dense.h, test_conv2d.h, test_sign.h, test_relu.h,
+test_rescale.h, test_maxpool2d.h, test_projection.h, test_mult.h,
+test_mixed_mod_mult.h) plus cases the reference never ran."""
+import numpy as np
+import pytest
+
+import dash_amd as d
+from dash_amd.garbling import GarbledCircuit
+
+SEED = bytes(range(16))
+
+
+def run(circuit, crt, mrs, x, seed=SEED, threads=0):
+    gc = GarbledCircuit(circuit, crt, mrs, seed=seed, nthreads=threads)
+    return gc.decode_outputs(gc.cpu_evaluate(gc.garble_inputs(x))), gc
+
+
+# ---------------------------------------------------------------- dense
+DENSE_PARAMS = [
+    (np.array([[1]]), np.array([0]), [5]),
+    (np.array([[2, 3]]), np.array([1]), [4, -3]),
+    (np.array([[1, 0], [0, 1]]), np.array([0, 0]), [7, -9]),
+    (np.array([[1, -1, 2], [0, 0, 0]]), np.array([5, -5]), [3, 4, 5]),
+    (np.array([[-3, 2], [4, -1], [0, 7]]), np.array([1, 2, 3]), [-2, 6]),
+]
+
+
+@pytest.mark.parametrize("W,b,x", DENSE_PARAMS)
+def test_single_dense(W, b, x):
+    c = d.Circuit([d.Dense.from_quantized(W, b)])
+    out, _ = run(c, 8, None, x)
+    np.testing.assert_array_equal(out, W @ np.array(x) + b)
+
+
+def test_dense_random_100_50_and_two_layers():
+    rng = np.random.default_rng(0)
+    W1 = rng.integers(-20, 21, (50, 100)); b1 = rng.integers(-20, 21, 50)
+    W2 = rng.integers(-20, 21, (10, 50)); b2 = rng.integers(-20, 21, 10)
+    x = rng.integers(-20, 21, 100)
+    c = d.Circuit([d.Dense.from_quantized(W1, b1), d.Dense.from_quantized(W2, b2)])
+    out, _ = run(c, 8, None, x)
+    np.testing.assert_array_equal(out, W2 @ (W1 @ x + b1) + b2)
+
+
+def test_dense_channel_tf():
+    rng = np.random.default_rng(1)
+    W = rng.integers(-5, 6, (4, 12)); b = rng.integers(-5, 6, 4)
+    x = rng.integers(-5, 6, 12)
+    dn = d.Dense.from_quantized(W, b, channel_tf=3)
+    out, gc = run(d.Circuit([dn]), 8, None, x)
+    np.testing.assert_array_equal(out, gc.plain_q_eval(x))
+
+
+# ----------------------------------------------------------------- conv
+def naive_conv(x, W, b, C, H, Wd, s=(1, 1), p=(0, 0)):
+    F, _, kh, kw = W.shape
+    xp = np.pad(x.reshape(C, H, Wd), ((0, 0), (p[0], p[0]), (p[1], p[1])))
+    OH = (H + 2 * p[0] - kh) // s[0] + 1
+    OW = (Wd + 2 * p[1] - kw) // s[1] + 1
+    out = np.zeros((F, OH, OW), np.int64)
+    for f in range(F):
+        for y in range(OH):
+            for xx in range(OW):
+                out[f, y, xx] = np.sum(W[f] * xp[:, y * s[0]:y * s[0] + kh, xx * s[1]:xx * s[1] + kw]) + b[f]
+    return out.reshape(-1)
+
+
+CONV_PARAMS = [  # (C, H, W, F, kh, kw, sh, sw, ph, pw)
+    (1, 3, 3, 1, 1, 1, 1, 1, 0, 0),   # identity
+    (1, 4, 4, 1, 2, 2, 1, 1, 0, 0),   # 2x2
+    (3, 5, 5, 1, 3, 3, 1, 1, 0, 0),   # multi channel
+    (2, 5, 5, 4, 3, 3, 1, 1, 0, 0),   # multi filter
+    (2, 6, 6, 3, 2, 2, 2, 2, 0, 0),   # stride 2
+    (2, 6, 7, 3, 2, 3, 1, 2, 0, 0),   # non-square kernel (reference bug §2.7 #2)
+    (3, 5, 5, 2, 3, 3, 1, 1, 1, 1),   # same padding
+]
+
+
+@pytest.mark.parametrize("p", CONV_PARAMS)
+def test_conv(p):
+    C, H, W_, F, kh, kw, sh, sw, ph, pw = p
+    rng = np.random.default_rng(sum(p))
+    W = rng.integers(-6, 7, (F, C, kh, kw)); b = rng.integers(-6, 7, F)
+    x = rng.integers(-8, 9, C * H * W_)
+    conv = d.Conv2d.from_quantized(W, b, W_, H, C, F, kw, kh, sw, sh, pad_width=pw, pad_height=ph)
+    out, _ = run(d.Circuit([conv]), 8, None, x)
+    np.testing.assert_array_equal(out, naive_conv(x, W, b, C, H, W_, (sh, sw), (ph, pw)))
+
+
+def test_two_conv_random():
+    rng = np.random.default_rng(3)
+    W1 = rng.integers(-3, 4, (4, 3, 4, 4)); b1 = rng.integers(-3, 4, 4)
+    W2 = rng.integers(-3, 4, (2, 4, 3, 3)); b2 = rng.integers(-3, 4, 2)
+    c1 = d.Conv2d.from_quantized(W1, b1, 16, 16, 3, 4, 4, 4, 2, 2)
+    c2 = d.Conv2d.from_quantized(W2, b2, 7, 7, 4, 2, 3, 3)
+    x = rng.integers(-4, 5, 3 * 16 * 16)
+    out, gc = run(d.Circuit([c1, c2]), 8, None, x)
+    np.testing.assert_array_equal(out, gc.plain_q_eval(x))
+
+
+# ------------------------------------------------------ sign / relu edges
+SIGN_PARAMS = [
+    ([2, 3, 5], [26, 6, 3, 2], [0, 1, -1, 7, -7, 14, -15]),
+    (9, [76, 7, 7, 7, 7, 7, 5, 5], [0, 1, -1, 7, -7, 55773217, -55773217, 111546434, -111546435]),
+]
+
+
+@pytest.mark.parametrize("crt,mrs,vals", SIGN_PARAMS)
+def test_sign(crt, mrs, vals):
+    out, _ = run(d.Circuit([d.Sign((len(vals),))]), crt, mrs, vals)
+    np.testing.assert_array_equal(out, np.where(np.array(vals) >= 0, 1, -1))
+
+
+@pytest.mark.parametrize("crt,mrs,vals", SIGN_PARAMS)
+def test_relu(crt, mrs, vals):
+    out, _ = run(d.Circuit([d.Relu((len(vals),))]), crt, mrs, vals)
+    np.testing.assert_array_equal(out, np.maximum(vals, 0))
+
+
+@pytest.mark.parametrize("k,acc", [(4, 100.0), (5, 100.0), (6, 100.0), (7, 100.0), (8, 100.0), (9, 100.0), (7, 99.99)])
+def test_relu_mrs_table(k, acc):
+    from dash_amd.ir.bases import crt_modulus, first_primes
+
+    M = crt_modulus(first_primes(k))
+    rng = np.random.default_rng(k)
+    vals = rng.integers(-M // 2, M // 2, 40)
+    out, _ = run(d.Circuit([d.Relu((40,))]), k, acc, vals)
+    if acc == 100.0:
+        np.testing.assert_array_equal(out, np.maximum(vals, 0))
+    else:  # approximate: wrong only very close to 0 / M/2
+        assert np.mean(out == np.maximum(vals, 0)) > 0.9
+
+
+# -------------------------------------------------------------- rescale
+RESCALE_VALS = [0, 1, -1, 7, -7, 14, -15, 55773217, -55773217, 111546434, -111546435]
+
+
+def test_rescale_legacy_reference_case():
+    c = d.Circuit([d.Rescale(2, (len(RESCALE_VALS),))])
+    out, _ = run(c, 9, 100.0, RESCALE_VALS)
+    expected = -((-np.array(RESCALE_VALS)) // 4)  # ceil(ceil(x/2)/2)
+    np.testing.assert_array_equal(out, expected)
+
+
+@pytest.mark.parametrize("crt,mrs,s", [([32, 97, 107], [22, 19, 15, 13], [32]),
+                                       ([32, 167, 173], [26, 25, 21, 13], [32]),
+                                       ([2, 3, 5, 7, 11, 13, 17], [86, 7, 6, 6, 5], [2, 3]),
+                                       ([32, 3, 5, 7, 11, 13, 17], [10, 9, 9, 8, 7, 7, 6], [32])])
+def test_rescale_redash(crt, mrs, s):
+    rng = np.random.default_rng(len(crt))
+    x = rng.integers(-100000, 100000, 64)
+    c = d.Circuit([d.Rescale(s, (64,))])
+    out, gc = run(c, crt, mrs, x)
+    np.testing.assert_array_equal(out, c.plain_q_eval(x, False, gc.crt_modulus))
+
+
+def test_base_extension():
+    rng = np.random.default_rng(9)
+    x = rng.integers(0, 97 * 107, 30)
+    out, _ = run(d.Circuit([d.BaseExtension((30,), [32])]), [32, 97, 107], [22, 19, 15, 13], x)
+    np.testing.assert_array_equal(out, x)
+
+
+# -------------------------------------------------------------- pooling
+@pytest.mark.parametrize("C,H,W,k,s", [(1, 2, 2, 2, 2), (2, 4, 4, 2, 2), (1, 3, 3, 1, 1), (3, 6, 6, 3, 3), (2, 5, 5, 2, 1)])
+def test_maxpool(C, H, W, k, s):
+    rng = np.random.default_rng(C * H + k)
+    x = rng.integers(-1000, 1000, C * H * W)
+    mp = d.MaxPool2d(W, H, C, k, k, s, s)
+    out, _ = run(d.Circuit([mp]), 7, 100.0, x)
+    np.testing.assert_array_equal(out, mp.plain_q_eval(x))
+
+
+def test_max_and_sumpool_and_residual():
+    x = [5, -3, 12, 7]
+    out, _ = run(d.Circuit([d.Max((4,))]), 6, 100.0, x)
+    assert out[0] == 12
+    rng = np.random.default_rng(4)
+    x = rng.integers(-30, 30, 2 * 4 * 4)
+    c = d.Circuit([d.SumPool2d(4, 4, 2, 2, 2), d.Add((2, 2, 2), 0), d.Relu((2, 2, 2))])
+    out, gc = run(c, 7, 100.0, x)
+    np.testing.assert_array_equal(out, gc.plain_q_eval(x))
+
+
+# --------------------------------------------------------- gate layers
+def test_projection_up_and_down():
+    c = d.Circuit([d.Projection((3,), [19], [91], lambda v: v), d.Projection((3,), [91], [19], lambda v: v % 19)])
+    gc = GarbledCircuit(c, [19], None, seed=SEED)
+    res = gc.decoder.decode_residues(gc.cpu_evaluate(gc.garble_inputs([0, 5, 18])))
+    np.testing.assert_array_equal(res[0], [0, 5, 18])
+    c = d.Circuit([d.Projection((3,), [19], [10], lambda v: v % 10), d.Projection((3,), [10], [19], lambda v: v)])
+    gc = GarbledCircuit(c, [19], None, seed=SEED)
+    res = gc.decoder.decode_residues(gc.cpu_evaluate(gc.garble_inputs([3, 9, 12])))
+    np.testing.assert_array_equal(res[0], [3, 9, 2])
+
+
+MULT = [[0, 0], [0, 2], [0, -2], [2, 1], [2, 2], [2, 4], [-2, 1], [-2, 2], [-2, 4], [-1, -1], [-1, -2], [-1, -4]]
+
+
+@pytest.mark.parametrize("v", MULT)
+def test_mult(v):
+    out, _ = run(d.Circuit([d.MultLayer((2,))]), [19], None, v)
+    assert out[0] == v[0] * v[1]
+
+
+def test_mult_multi_residue():
+    out, _ = run(d.Circuit([d.MultLayer((4,))]), 5, None, [23, -45, -7, 9])
+    np.testing.assert_array_equal(out, [23 * -45, -63])
+
+
+@pytest.mark.parametrize("v", [[5, 1], [5, 0], [-3, 1], [0, 1], [8, 1]])
+def test_mixed_mod_mult(v):
+    out, _ = run(d.Circuit([d.MixedModMultLayer((2,), smaller_modulus=2)]), [19], None, v)
+    assert out[0] == v[0] * v[1]
+
+
+def test_sign_dense_model_e():
+    rng = np.random.default_rng(11)
+    W1 = rng.integers(-3, 4, (10, 20)); b1 = rng.integers(-3, 4, 10)
+    W2 = rng.integers(-3, 4, (4, 10)); b2 = rng.integers(-3, 4, 4)
+    c = d.Circuit([d.Dense.from_quantized(W1, b1), d.Sign((10,)), d.Dense.from_quantized(W2, b2)])
+    x = rng.integers(-5, 6, 20)
+    out, gc = run(c, 5, 100.0, x)
+    np.testing.assert_array_equal(out, gc.plain_q_eval(x))
+
+
+def test_encode_cm_matches_encode():
+    from dash_amd.models import build_circuit, quantized_inputs
+
+    c = build_circuit("MODEL_A")
+    x = quantized_inputs("MODEL_A", 1)[0]
+    gc = GarbledCircuit(c, 7, 100.0, seed=SEED)
+    lab = gc.garble_inputs(x)
+    cm = gc.garble_inputs_cm(x)
+    assert len(cm) == len(lab)
+    for (p, a), b in zip(lab, cm):
+        np.testing.assert_array_equal(a.T, b)

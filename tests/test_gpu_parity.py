@@ -130,3 +130,25 @@ def test_model_a_batch():
     c = build_circuit("MODEL_A")
     xs = quantized_inputs("MODEL_A", 3)
     _check(c, 7, 100.0, xs)
+
+
+def test_staged_input_paths():
+    """encode_into / set_input_cm + upload_inputs == the label-list path."""
+    from dash_amd.models import build_circuit, quantized_inputs
+
+    c = build_circuit("MODEL_A")
+    xs = quantized_inputs("MODEL_A", 2)
+    gcs = [GarbledCircuit(c, 7, 100.0, seed=bytes([i + 9]) * 16) for i in range(2)]
+    ev = _hip([g.model for g in gcs])
+    ref = ev.evaluate([g.garble_inputs(x) for g, x in zip(gcs, xs)])
+    ev.encode_into(0, gcs[0], xs[0])
+    ev.set_input_cm(1, gcs[1].garble_inputs_cm(xs[1]))
+    ev.upload_inputs()
+    ev.run()
+    got = ev.get_outputs()
+    for r, g in zip(ref, got):
+        for (pr, ar), (pg, ag) in zip(r, g):
+            assert pr == pg
+            np.testing.assert_array_equal(ar, ag)
+    for g, x, o in zip(gcs, xs, got):
+        np.testing.assert_array_equal(g.decode_outputs(o), g.plain_q_eval(x))
