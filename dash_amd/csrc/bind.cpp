@@ -3,7 +3,9 @@
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
+#include "dataloader.h"
 #include "layers.h"
+#include "onnx.h"
 
 namespace py = pybind11;
 using namespace dash;
@@ -283,6 +285,85 @@ PYBIND11_MODULE(_dash_native, m) {
         }
         return labels_to_py(out);
     }, py::arg("model"), py::arg("labels"), py::arg("nthreads") = 0);
+
+    // ---------------------------------------------------------------- ONNX
+    m.def("onnx_parse", [](py::bytes blob) {
+        onnx::Model mdl;
+        {
+            std::string s = blob;
+            py::gil_scoped_release rel;
+            mdl = onnx::parse_model(s);
+        }
+        auto tensor = [](const onnx::Tensor& t) {
+            py::dict d;
+            d["name"] = t.name;
+            d["data_type"] = t.data_type;
+            d["dims"] = t.dims;
+            std::vector<py::ssize_t> shape(t.dims.begin(), t.dims.end());
+            py::array_t<float> v(static_cast<py::ssize_t>(t.values.size()));
+            if (!t.values.empty()) std::memcpy(v.mutable_data(), t.values.data(), t.values.size() * sizeof(float));
+            d["values"] = v;
+            d["ivalues"] = t.ivalues;
+            return d;
+        };
+        py::dict out;
+        out["ir_version"] = mdl.ir_version;
+        out["opset"] = mdl.opset;
+        out["producer_name"] = mdl.producer_name;
+        out["producer_version"] = mdl.producer_version;
+        py::list nodes;
+        for (const auto& n : mdl.graph.nodes) {
+            py::dict nd;
+            nd["name"] = n.name;
+            nd["op_type"] = n.op_type;
+            nd["inputs"] = n.inputs;
+            nd["outputs"] = n.outputs;
+            py::dict attrs;
+            for (const auto& a : n.attributes) {
+                if (!a.ints.empty()) attrs[py::str(a.name)] = a.ints;
+                else if (!a.floats.empty()) attrs[py::str(a.name)] = a.floats;
+                else if (a.t) attrs[py::str(a.name)] = tensor(*a.t);
+                else if (a.has_i) attrs[py::str(a.name)] = a.i;
+                else if (a.has_f) attrs[py::str(a.name)] = a.f;
+                else attrs[py::str(a.name)] = py::bytes(a.s);
+            }
+            nd["attrs"] = attrs;
+            nodes.append(nd);
+        }
+        out["nodes"] = nodes;
+        py::list inits;
+        for (const auto& t : mdl.graph.initializers) inits.append(tensor(t));
+        out["initializers"] = inits;
+        auto vis = [](const std::vector<onnx::ValueInfo>& v) {
+            py::list l;
+            for (const auto& vi : v) {
+                py::dict d;
+                d["name"] = vi.name;
+                d["elem_type"] = vi.elem_type;
+                d["dims"] = vi.dims;
+                l.append(d);
+            }
+            return l;
+        };
+        out["inputs"] = vis(mdl.graph.inputs);
+        out["outputs"] = vis(mdl.graph.outputs);
+        return out;
+    });
+
+    // ------------------------------------------------------------ datasets
+    auto dataset_to_py = [](const Dataset& d) {
+        auto split = [](const ImageSet& s) {
+            py::array_t<uint8_t> x({static_cast<py::ssize_t>(s.n), static_cast<py::ssize_t>(s.c),
+                                    static_cast<py::ssize_t>(s.h), static_cast<py::ssize_t>(s.w)});
+            if (!s.pixels.empty()) std::memcpy(x.mutable_data(), s.pixels.data(), s.pixels.size());
+            py::array_t<uint8_t> y(static_cast<py::ssize_t>(s.labels.size()));
+            if (!s.labels.empty()) std::memcpy(y.mutable_data(), s.labels.data(), s.labels.size());
+            return py::make_tuple(x, y);
+        };
+        return py::make_tuple(split(d.train), split(d.test));
+    };
+    m.def("load_mnist", [dataset_to_py](const std::string& dir) { return dataset_to_py(load_mnist(dir)); });
+    m.def("load_cifar10", [dataset_to_py](const std::string& dir) { return dataset_to_py(load_cifar10(dir)); });
 
     dash::register_hip_bindings(m);
 }

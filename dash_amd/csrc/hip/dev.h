@@ -170,108 +170,149 @@ __device__ __forceinline__ uint32_t u128_mod(u128 P, const ModC& m) {
 }
 
 // ---------------------------------------------------------------------------
-// AES-128 (fixed key)
+// AES-128 (fixed key 00..0f), T-table form tuned for CDNA4.
+//
+// LDS image (64 KiB): 256 rows of 256 B; row x holds Te0[x] in words 0..31
+// and Te2[x] = ror16(Te0[x]) in words 32..63 (32 copies each). Lane l reads
+// copy (l mod 32), so a ds_read_b32 from 32 lanes hits 32 distinct banks
+// (bank = (addr/4) mod 32) whatever the indices: conflict-free.
+// The byte offset of a lookup, (byte_i(s) << 8) | (4 * (lane mod 32)), is a
+// single v_perm_b32; Te2 sits at +128 B (instruction offset field). With
+// Te1 = ror8(Te0) and Te3 = ror8(Te2) one AES column costs
+//   4 perm + 4 ds_read + xor3 + alignbit + xor3
+// (the round key is folded into the rotated xor3 as rol8(rk)): ~7 VALU per
+// column vs ~16 for a byte-extract/shift/add/rotate formulation.
+// The round keys of the fixed key are compile-time constants (the key is part
+// of the scheme, crypto/cpu_aes_engine.h:23-24), so they become literals.
+#define DASH_AES_LDS_BYTES 65536
+#define DASH_AES_LDS_WORDS (DASH_AES_LDS_BYTES / 4)
+
+__device__ constexpr uint32_t kAesRk[44] = {
+    0x00010203u, 0x04050607u, 0x08090a0bu, 0x0c0d0e0fu, 0xd6aa74fdu, 0xd2af72fau, 0xdaa678f1u, 0xd6ab76feu,
+    0xb692cf0bu, 0x643dbdf1u, 0xbe9bc500u, 0x6830b3feu, 0xb6ff744eu, 0xd2c2c9bfu, 0x6c590cbfu, 0x0469bf41u,
+    0x47f7f7bcu, 0x95353e03u, 0xf96c32bcu, 0xfd058dfdu, 0x3caaa3e8u, 0xa99f9debu, 0x50f3af57u, 0xadf622aau,
+    0x5e390f7du, 0xf7a69296u, 0xa7553dc1u, 0x0aa31f6bu, 0x14f9701au, 0xe35fe28cu, 0x440adf4du, 0x4ea9c026u,
+    0x47438735u, 0xa41c65b9u, 0xe016baf4u, 0xaebf7ad2u, 0x549932d1u, 0xf0855768u, 0x1093ed9cu, 0xbe2c974eu,
+    0x13111d7fu, 0xe3944a17u, 0xf307a78bu, 0x4d2b30c5u};
+
 struct AesCtx {
-    const uint32_t* T;   // LDS: 256 entries x 32 copies
-    const uint32_t* rk;  // 44 round key words (big-endian column words)
-    uint32_t lane32;
+    const char* T;  // LDS image base
+    uint32_t lo;    // 4 * (lane mod 32)
 };
 
 __device__ __forceinline__ uint32_t ror32(uint32_t x, int r) { return (x >> r) | (x << (32 - r)); }
+__device__ __forceinline__ uint32_t rol32c(uint32_t x, int r) { return (x << r) | (x >> (32 - r)); }
 __device__ __forceinline__ uint32_t bswap32(uint32_t x) { return __builtin_bswap32(x); }
 
-__device__ __forceinline__ uint32_t te(const AesCtx& a, uint32_t idx) { return a.T[(idx << 5) | a.lane32]; }
+// byte offset of row byte_I(s), lane copy: D = {0, 0, s.byte[I], lo.byte[0]}
+template <int I>
+__device__ __forceinline__ uint32_t aes_off(uint32_t s, uint32_t lo) {
+    return __builtin_amdgcn_perm(s, lo, 0x0c0c0000u | ((4u + I) << 8));
+}
+template <int I>
+__device__ __forceinline__ uint32_t aes_t0(const AesCtx& a, uint32_t s) {
+    return *reinterpret_cast<const uint32_t*>(a.T + aes_off<I>(s, a.lo));
+}
+template <int I>
+__device__ __forceinline__ uint32_t aes_t2(const AesCtx& a, uint32_t s) {
+    return *reinterpret_cast<const uint32_t*>(a.T + aes_off<I>(s, a.lo) + 128);
+}
+// three-input XOR in one VALU op (v_bitop3_b32, truth table 0x96)
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+    uint32_t d;
+    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(d) : "v"(a), "v"(b), "v"(c));
+    return d;
+}
+// one output column of a middle round: Te0[s0.b3]^Te1[s1.b2]^Te2[s2.b1]^Te3[s3.b0]^rk
+__device__ __forceinline__ uint32_t aes_col(const AesCtx& a, uint32_t s0, uint32_t s1, uint32_t s2, uint32_t s3,
+                                            uint32_t rk) {
+    const uint32_t u = xor3(aes_t0<2>(a, s1), aes_t2<0>(a, s3), rol32c(rk, 8));
+    return xor3(aes_t0<3>(a, s0), aes_t2<1>(a, s2), ror32(u, 8));
+}
+// final round column: S-box bytes sit at Te2.b3, Te0.b2, Te0.b1, Te2.b0
+__device__ __forceinline__ uint32_t aes_last(const AesCtx& a, uint32_t s0, uint32_t s1, uint32_t s2, uint32_t s3,
+                                             uint32_t rk) {
+    const uint32_t x1 = __builtin_amdgcn_perm(aes_t2<3>(a, s0), aes_t0<2>(a, s1), 0x07020c0cu);
+    const uint32_t x2 = __builtin_amdgcn_perm(aes_t0<1>(a, s2), aes_t2<0>(a, s3), 0x0c0c0500u);
+    return xor3(x1, x2, rk);
+}
 
 __device__ __forceinline__ u128 aes_encrypt(const AesCtx& a, u128 in) {
-    const uint32_t* rk = a.rk;
-    uint32_t s0 = bswap32(static_cast<uint32_t>(in)) ^ rk[0];
-    uint32_t s1 = bswap32(static_cast<uint32_t>(in >> 32)) ^ rk[1];
-    uint32_t s2 = bswap32(static_cast<uint32_t>(in >> 64)) ^ rk[2];
-    uint32_t s3 = bswap32(static_cast<uint32_t>(in >> 96)) ^ rk[3];
-    uint32_t t0, t1, t2, t3;
+    uint32_t s0 = bswap32(static_cast<uint32_t>(in)) ^ kAesRk[0];
+    uint32_t s1 = bswap32(static_cast<uint32_t>(in >> 32)) ^ kAesRk[1];
+    uint32_t s2 = bswap32(static_cast<uint32_t>(in >> 64)) ^ kAesRk[2];
+    uint32_t s3 = bswap32(static_cast<uint32_t>(in >> 96)) ^ kAesRk[3];
 #pragma unroll
     for (int r = 1; r < 10; ++r) {
-        t0 = te(a, s0 >> 24) ^ ror32(te(a, (s1 >> 16) & 0xff), 8) ^ ror32(te(a, (s2 >> 8) & 0xff), 16) ^
-             ror32(te(a, s3 & 0xff), 24) ^ rk[4 * r + 0];
-        t1 = te(a, s1 >> 24) ^ ror32(te(a, (s2 >> 16) & 0xff), 8) ^ ror32(te(a, (s3 >> 8) & 0xff), 16) ^
-             ror32(te(a, s0 & 0xff), 24) ^ rk[4 * r + 1];
-        t2 = te(a, s2 >> 24) ^ ror32(te(a, (s3 >> 16) & 0xff), 8) ^ ror32(te(a, (s0 >> 8) & 0xff), 16) ^
-             ror32(te(a, s1 & 0xff), 24) ^ rk[4 * r + 2];
-        t3 = te(a, s3 >> 24) ^ ror32(te(a, (s0 >> 16) & 0xff), 8) ^ ror32(te(a, (s1 >> 8) & 0xff), 16) ^
-             ror32(te(a, s2 & 0xff), 24) ^ rk[4 * r + 3];
+        const uint32_t t0 = aes_col(a, s0, s1, s2, s3, kAesRk[4 * r + 0]);
+        const uint32_t t1 = aes_col(a, s1, s2, s3, s0, kAesRk[4 * r + 1]);
+        const uint32_t t2 = aes_col(a, s2, s3, s0, s1, kAesRk[4 * r + 2]);
+        const uint32_t t3 = aes_col(a, s3, s0, s1, s2, kAesRk[4 * r + 3]);
         s0 = t0;
         s1 = t1;
         s2 = t2;
         s3 = t3;
     }
-    // final round: S-box = byte 2 of Te0 (Te0[x] = 2s | s | s | 3s)
-    auto S = [&](uint32_t x) { return (te(a, x) >> 8) & 0xffu; };
-    uint32_t o0 = (S(s0 >> 24) << 24) ^ (S((s1 >> 16) & 0xff) << 16) ^ (S((s2 >> 8) & 0xff) << 8) ^ S(s3 & 0xff) ^ rk[40];
-    uint32_t o1 = (S(s1 >> 24) << 24) ^ (S((s2 >> 16) & 0xff) << 16) ^ (S((s3 >> 8) & 0xff) << 8) ^ S(s0 & 0xff) ^ rk[41];
-    uint32_t o2 = (S(s2 >> 24) << 24) ^ (S((s3 >> 16) & 0xff) << 16) ^ (S((s0 >> 8) & 0xff) << 8) ^ S(s1 & 0xff) ^ rk[42];
-    uint32_t o3 = (S(s3 >> 24) << 24) ^ (S((s0 >> 16) & 0xff) << 16) ^ (S((s1 >> 8) & 0xff) << 8) ^ S(s2 & 0xff) ^ rk[43];
+    const uint32_t o0 = aes_last(a, s0, s1, s2, s3, kAesRk[40]);
+    const uint32_t o1 = aes_last(a, s1, s2, s3, s0, kAesRk[41]);
+    const uint32_t o2 = aes_last(a, s2, s3, s0, s1, kAesRk[42]);
+    const uint32_t o3 = aes_last(a, s3, s0, s1, s2, kAesRk[43]);
     return (static_cast<u128>((static_cast<uint64_t>(bswap32(o3)) << 32) | bswap32(o2)) << 64) |
            ((static_cast<uint64_t>(bswap32(o1)) << 32) | bswap32(o0));
 }
 
-
 // Two independent blocks with interleaved rounds: doubles the LDS-read ILP of
-// a latency-bound lane (the serial sign chain) at no extra instructions.
+// a latency-bound lane (the serial sign chain).
 __device__ __forceinline__ void aes_encrypt2(const AesCtx& a, u128 inA, u128 inB, u128& outA, u128& outB) {
-    const uint32_t* rk = a.rk;
-    uint32_t a0 = bswap32(static_cast<uint32_t>(inA)) ^ rk[0], a1 = bswap32(static_cast<uint32_t>(inA >> 32)) ^ rk[1];
-    uint32_t a2 = bswap32(static_cast<uint32_t>(inA >> 64)) ^ rk[2], a3 = bswap32(static_cast<uint32_t>(inA >> 96)) ^ rk[3];
-    uint32_t b0 = bswap32(static_cast<uint32_t>(inB)) ^ rk[0], b1 = bswap32(static_cast<uint32_t>(inB >> 32)) ^ rk[1];
-    uint32_t b2 = bswap32(static_cast<uint32_t>(inB >> 64)) ^ rk[2], b3 = bswap32(static_cast<uint32_t>(inB >> 96)) ^ rk[3];
-#define DASH_AES_COL(s0, s1, s2, s3, r)                                                              \
-    (te(a, (s0) >> 24) ^ ror32(te(a, ((s1) >> 16) & 0xff), 8) ^ ror32(te(a, ((s2) >> 8) & 0xff), 16) ^ \
-     ror32(te(a, (s3)&0xff), 24) ^ rk[r])
+    uint32_t a0 = bswap32(static_cast<uint32_t>(inA)) ^ kAesRk[0], a1 = bswap32(static_cast<uint32_t>(inA >> 32)) ^ kAesRk[1];
+    uint32_t a2 = bswap32(static_cast<uint32_t>(inA >> 64)) ^ kAesRk[2], a3 = bswap32(static_cast<uint32_t>(inA >> 96)) ^ kAesRk[3];
+    uint32_t b0 = bswap32(static_cast<uint32_t>(inB)) ^ kAesRk[0], b1 = bswap32(static_cast<uint32_t>(inB >> 32)) ^ kAesRk[1];
+    uint32_t b2 = bswap32(static_cast<uint32_t>(inB >> 64)) ^ kAesRk[2], b3 = bswap32(static_cast<uint32_t>(inB >> 96)) ^ kAesRk[3];
 #pragma unroll
     for (int r = 1; r < 10; ++r) {
-        uint32_t ta0 = DASH_AES_COL(a0, a1, a2, a3, 4 * r + 0);
-        uint32_t tb0 = DASH_AES_COL(b0, b1, b2, b3, 4 * r + 0);
-        uint32_t ta1 = DASH_AES_COL(a1, a2, a3, a0, 4 * r + 1);
-        uint32_t tb1 = DASH_AES_COL(b1, b2, b3, b0, 4 * r + 1);
-        uint32_t ta2 = DASH_AES_COL(a2, a3, a0, a1, 4 * r + 2);
-        uint32_t tb2 = DASH_AES_COL(b2, b3, b0, b1, 4 * r + 2);
-        uint32_t ta3 = DASH_AES_COL(a3, a0, a1, a2, 4 * r + 3);
-        uint32_t tb3 = DASH_AES_COL(b3, b0, b1, b2, 4 * r + 3);
+        const uint32_t ta0 = aes_col(a, a0, a1, a2, a3, kAesRk[4 * r + 0]);
+        const uint32_t tb0 = aes_col(a, b0, b1, b2, b3, kAesRk[4 * r + 0]);
+        const uint32_t ta1 = aes_col(a, a1, a2, a3, a0, kAesRk[4 * r + 1]);
+        const uint32_t tb1 = aes_col(a, b1, b2, b3, b0, kAesRk[4 * r + 1]);
+        const uint32_t ta2 = aes_col(a, a2, a3, a0, a1, kAesRk[4 * r + 2]);
+        const uint32_t tb2 = aes_col(a, b2, b3, b0, b1, kAesRk[4 * r + 2]);
+        const uint32_t ta3 = aes_col(a, a3, a0, a1, a2, kAesRk[4 * r + 3]);
+        const uint32_t tb3 = aes_col(a, b3, b0, b1, b2, kAesRk[4 * r + 3]);
         a0 = ta0; a1 = ta1; a2 = ta2; a3 = ta3;
         b0 = tb0; b1 = tb1; b2 = tb2; b3 = tb3;
     }
-#undef DASH_AES_COL
-    auto S = [&](uint32_t x) { return (te(a, x) >> 8) & 0xffu; };
-    auto last = [&](uint32_t s0, uint32_t s1, uint32_t s2, uint32_t s3) -> u128 {
-        uint32_t o0 = (S(s0 >> 24) << 24) ^ (S((s1 >> 16) & 0xff) << 16) ^ (S((s2 >> 8) & 0xff) << 8) ^ S(s3 & 0xff) ^ rk[40];
-        uint32_t o1 = (S(s1 >> 24) << 24) ^ (S((s2 >> 16) & 0xff) << 16) ^ (S((s3 >> 8) & 0xff) << 8) ^ S(s0 & 0xff) ^ rk[41];
-        uint32_t o2 = (S(s2 >> 24) << 24) ^ (S((s3 >> 16) & 0xff) << 16) ^ (S((s0 >> 8) & 0xff) << 8) ^ S(s1 & 0xff) ^ rk[42];
-        uint32_t o3 = (S(s3 >> 24) << 24) ^ (S((s0 >> 16) & 0xff) << 16) ^ (S((s1 >> 8) & 0xff) << 8) ^ S(s2 & 0xff) ^ rk[43];
+    auto fin = [&](uint32_t s0, uint32_t s1, uint32_t s2, uint32_t s3) -> u128 {
+        const uint32_t o0 = aes_last(a, s0, s1, s2, s3, kAesRk[40]);
+        const uint32_t o1 = aes_last(a, s1, s2, s3, s0, kAesRk[41]);
+        const uint32_t o2 = aes_last(a, s2, s3, s0, s1, kAesRk[42]);
+        const uint32_t o3 = aes_last(a, s3, s0, s1, s2, kAesRk[43]);
         return (static_cast<u128>((static_cast<uint64_t>(bswap32(o3)) << 32) | bswap32(o2)) << 64) |
                ((static_cast<uint64_t>(bswap32(o1)) << 32) | bswap32(o0));
     };
-    outA = last(a0, a1, a2, a3);
-    outB = last(b0, b1, b2, b3);
+    outA = fin(a0, a1, a2, a3);
+    outB = fin(b0, b1, b2, b3);
 }
 
-// Global tables: Te0 (256 words) and the fixed-key round keys (44 words).
+// Global tables: Te0 (256 words); rk kept for the launch ABI (round keys are literals).
 struct AesGlobals {
     const uint32_t* te0;
     const uint32_t* rk;
 };
 
-#define DASH_AES_LDS_WORDS (256 * 32)
-// Fill the replicated LDS table; all threads of the block participate.
+// Fill the LDS image; all threads of the block participate.
 __device__ __forceinline__ void aes_lds_fill(uint32_t* lds, const uint32_t* te0) {
-    for (int i = threadIdx.x + threadIdx.y * blockDim.x; i < DASH_AES_LDS_WORDS; i += blockDim.x * blockDim.y)
-        lds[i] = te0[i >> 5];
+    const int nt = blockDim.x * blockDim.y;
+    for (int i = threadIdx.x + threadIdx.y * blockDim.x; i < DASH_AES_LDS_WORDS; i += nt) {
+        const uint32_t v = te0[i >> 6];
+        lds[i] = (i & 32) ? ror32(v, 16) : v;
+    }
     __syncthreads();
 }
 
-__device__ __forceinline__ AesCtx aes_ctx(const uint32_t* lds, const uint32_t* rk) {
+__device__ __forceinline__ AesCtx aes_ctx(const uint32_t* lds, const uint32_t* /*rk*/) {
     AesCtx a;
-    a.T = lds;
-    a.rk = rk;
-    a.lane32 = threadIdx.x & 31;
+    a.T = reinterpret_cast<const char*>(lds);
+    a.lo = (__lane_id() & 31u) << 2;
     return a;
 }
 

@@ -18,20 +18,41 @@
 namespace dash {
 namespace dev {
 
+constexpr size_t kAesLds = 0;  // AES image is static LDS
+
+// AES kernels stride over their elements so the 64 KiB LDS image is filled
+// once per resident block instead of once per 512 elements: about two
+// resident blocks per CU (LDS bound), x4 for tail balance.
+static int aes_block_cap() {
+    static int cap = [] {
+        int dev = 0, cus = 256;
+        if (hipGetDevice(&dev) == hipSuccess) hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+        return 8 * cus;
+    }();
+    return cap;
+}
+static inline dim3 grid_aes(int64_t n, int bs, int y, int z) {
+    int64_t nx = (n + bs - 1) / bs;
+    const int64_t capx = std::max<int64_t>(1, aes_block_cap() / (static_cast<int64_t>(y) * z));
+    return dim3(static_cast<unsigned>(std::min(nx, capx)), y, z);
+}
+
+// static (not dynamic) LDS: its address is a link-time constant, so the
+// table base folds into the ds_read offset field
 #define AES_PROLOGUE(tab, rk)                    \
-    extern __shared__ uint32_t lds_aes[];         \
+    __shared__ uint32_t lds_aes[DASH_AES_LDS_WORDS]; \
     aes_lds_fill(lds_aes, tab);                   \
     const AesCtx aes = aes_ctx(lds_aes, rk)
 
 // ---------------------------------------------------------------------------
 // Phase A: approximate residues. grid (ceil(N/256), k, B)
-__global__ __launch_bounds__(256) void k_sign_approx(SignArgs a, Act x, const ModC* mc, const uint32_t* te0,
+__global__ __launch_bounds__(512) void k_sign_approx(SignArgs a, Act x, const ModC* mc, const uint32_t* te0,
                                                      const uint32_t* rk) {
     AES_PROLOGUE(te0, rk);
     const int j = blockIdx.y, b = blockIdx.z;
     const int64_t N = a.N;
-    const int64_t e = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-    if (e >= N) return;
+    for (int64_t e = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; e < N;
+         e += static_cast<int64_t>(gridDim.x) * blockDim.x) {
     const int p = a.crt.p[j];
     const ModC m = mc[p];
     const int16_t* L = x.p[j] + static_cast<int64_t>(b) * m.n * N + e;
@@ -54,18 +75,19 @@ __global__ __launch_bounds__(256) void k_sign_approx(SignArgs a, Act x, const Mo
     for (int d = 0; d < 8; ++d)
         if (d < a.t) out[static_cast<int64_t>(d) * N] = ent[d] - H;
     for (int d = 8; d < a.t; ++d) out[static_cast<int64_t>(d) * N] = T[d * p + col] - H;
+    }
 }
 
 // ---------------------------------------------------------------------------
 // Phase B: mixed-radix carry chain + sign projection. grid (ceil(N/128), 1, B)
 template <int MAXN>
-__global__ __launch_bounds__(128) void k_sign_chain(SignArgs a, const ModC* mc, const uint32_t* te0,
+__global__ __launch_bounds__(512) void k_sign_chain(SignArgs a, const ModC* mc, const uint32_t* te0,
                                                     const uint32_t* rk) {
     AES_PROLOGUE(te0, rk);
     const int b = blockIdx.z;
     const int64_t N = a.N;
-    const int64_t e = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-    if (e >= N) return;
+    for (int64_t e = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; e < N;
+         e += static_cast<int64_t>(gridDim.x) * blockDim.x) {
     const int k = a.crt.k, t = a.t;
     const u128* T1 = a.cast1 + (static_cast<int64_t>(b) * N + e) * a.n_cast;
     const u128* T2 = a.cast2 + (static_cast<int64_t>(b) * N + e) * a.n_cast;
@@ -165,6 +187,7 @@ __global__ __launch_bounds__(128) void k_sign_chain(SignArgs a, const ModC* mc, 
             a.cs[static_cast<int64_t>(b) * N + e] = static_cast<uint8_t>(static_cast<uint32_t>(P) & 1u);
         }
     }
+    }
 }
 
 // Decompress compressed outputs into residue activations. grid (ceil(N/256), nres, B)
@@ -224,13 +247,13 @@ __global__ __launch_bounds__(256) void k_relu_mult(SignArgs a, Act x, Act y, con
 // ---------------------------------------------------------------------------
 // Rescale step 1+2 for one factor: hash the factor residue (optionally after
 // the upshift). grid (ceil(N/256), 1, B)
-__global__ __launch_bounds__(256) void k_rescale_hash(Act x, int fi, int s, const int16_t* up, int up_stride,
+__global__ __launch_bounds__(512) void k_rescale_hash(Act x, int fi, int s, const int16_t* up, int up_stride,
                                                       int add_up, int64_t N, u128* h0, uint16_t* col0,
                                                       const ModC* mc, const uint32_t* te0, const uint32_t* rk) {
     AES_PROLOGUE(te0, rk);
     const int b = blockIdx.z;
-    const int64_t e = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-    if (e >= N) return;
+    for (int64_t e = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; e < N;
+         e += static_cast<int64_t>(gridDim.x) * blockDim.x) {
     const ModC m = mc[s];
     const int16_t* L = x.p[fi] + static_cast<int64_t>(b) * m.n * N + e;
     const int16_t* U = up + static_cast<int64_t>(b) * up_stride;
@@ -251,6 +274,7 @@ __global__ __launch_bounds__(256) void k_rescale_hash(Act x, int fi, int s, cons
     }
     h0[static_cast<int64_t>(b) * N + e] = aes_encrypt(aes, C);
     col0[static_cast<int64_t>(b) * N + e] = static_cast<uint16_t>(c0);
+    }
 }
 
 
@@ -321,26 +345,27 @@ __global__ __launch_bounds__(256) void k_rescale_post(Act x, CrtInfo crt, int64_
 //            next sign gadget (phase A) in the same pass.
 // The downshift of iteration i and the upshift of i+1 collapse into one
 // delta = up - down; only the last iteration writes a downshifted result.
-__global__ __launch_bounds__(256) void k_rescale_hash_sign(const u128* signP, const u128* du, int64_t N, u128* h0,
+__global__ __launch_bounds__(512) void k_rescale_hash_sign(const u128* signP, const u128* du, int64_t N, u128* h0,
                                                            uint16_t* col0, const uint32_t* te0, const uint32_t* rk) {
     AES_PROLOGUE(te0, rk);
     const int b = blockIdx.z;
-    const int64_t e = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-    if (e >= N) return;
+    for (int64_t e = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; e < N;
+         e += static_cast<int64_t>(gridDim.x) * blockDim.x) {
     const u128 C = signP[static_cast<int64_t>(b) * N + e] ^ du[b];
     h0[static_cast<int64_t>(b) * N + e] = aes_encrypt(aes, C);
     col0[static_cast<int64_t>(b) * N + e] = static_cast<uint16_t>(static_cast<uint32_t>(C) & 1u);
+    }
 }
 
 // grid (ceil(N/256), k, B)
-__global__ __launch_bounds__(256) void k_rescale_update_approx(RescaleArgs r, SignArgs a, Act x, const int16_t* delta,
+__global__ __launch_bounds__(512) void k_rescale_update_approx(RescaleArgs r, SignArgs a, Act x, const int16_t* delta,
                                                                const u128* zh, const ModC* mc, const uint32_t* te0,
                                                                const uint32_t* rk) {
     AES_PROLOGUE(te0, rk);
     const int j = blockIdx.y, b = blockIdx.z;
     const int64_t N = r.N;
-    const int64_t e = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-    if (e >= N) return;
+    for (int64_t e = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; e < N;
+         e += static_cast<int64_t>(gridDim.x) * blockDim.x) {
     const int p = r.crt.p[j];
     const ModC m = mc[p];
     const int64_t be = static_cast<int64_t>(b) * N + e;
@@ -387,30 +412,29 @@ __global__ __launch_bounds__(256) void k_rescale_update_approx(RescaleArgs r, Si
     for (int d = 0; d < 8; ++d)
         if (d < a.t) out[static_cast<int64_t>(d) * N] = ent[d] - H;
     for (int d = 8; d < a.t; ++d) out[static_cast<int64_t>(d) * N] = TA[d * p + col] - H;
+    }
 }
 
 void launch_rescale_hash_sign(const u128* signP, const u128* du, int64_t N, int B, u128* h0, uint16_t* col0,
                               const AesGlobals& g, hipStream_t st) {
-    hipLaunchKernelGGL(k_rescale_hash_sign, dim3(static_cast<unsigned>((N + 255) / 256), 1, B), dim3(256),
-                       DASH_AES_LDS_WORDS * sizeof(uint32_t), st, signP, du, N, h0, col0, g.te0, g.rk);
+    hipLaunchKernelGGL(k_rescale_hash_sign, grid_aes(N, 512, 1, B), dim3(512), kAesLds, st, signP, du, N, h0, col0, g.te0, g.rk);
 }
 void launch_rescale_update_approx(const RescaleArgs& r, const SignArgs& a, const Act& x, const int16_t* delta,
                                   const u128* zh, int B, const ModC* mc, const AesGlobals& g, hipStream_t st) {
-    hipLaunchKernelGGL(k_rescale_update_approx, dim3(static_cast<unsigned>((r.N + 255) / 256), r.crt.k, B), dim3(256),
-                       DASH_AES_LDS_WORDS * sizeof(uint32_t), st, r, a, x, delta, zh, mc, g.te0, g.rk);
+    hipLaunchKernelGGL(k_rescale_update_approx, grid_aes(r.N, 512, r.crt.k, B), dim3(512), kAesLds, st, r, a, x, delta, zh, mc, g.te0, g.rk);
 }
 
 // ---------------------------------------------------------------------------
 // ReDash base extension (MRS conversion). One lane per (GC, element); the
 // working copies live in `work` (component-major, [B][E][128][N]).
 
-__global__ __launch_bounds__(128) void k_base_ext(BEArgs a, Act x, const ModC* mc, const uint32_t* te0,
+__global__ __launch_bounds__(256) void k_base_ext(BEArgs a, Act x, const ModC* mc, const uint32_t* te0,
                                                   const uint32_t* rk) {
     AES_PROLOGUE(te0, rk);
     const int b = blockIdx.z;
     const int64_t N = a.N;
-    const int64_t e = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-    if (e >= N) return;
+    for (int64_t e = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; e < N;
+         e += static_cast<int64_t>(gridDim.x) * blockDim.x) {
     const int E = a.E;
     auto W = [&](int pos) { return a.work + ((static_cast<int64_t>(b) * E + pos) * 128) * N + e; };
     for (int i = 0; i < E; ++i) {
@@ -452,17 +476,18 @@ __global__ __launch_bounds__(128) void k_base_ext(BEArgs a, Act x, const ModC* m
         const int32_t f = a.invv[xi];  // already negated mod q on the host
         for (int c = 0; c < static_cast<int>(m.n); ++c) dst[c * N] = static_cast<int16_t>((w[c * N] * f) % q);
     }
+    }
 }
 
 // ---------------------------------------------------------------------------
 // Generic projection layer (test-only Projection). grid (ceil(N/256), k, B)
-__global__ __launch_bounds__(256) void k_proj(ProjArgs a, Act x, Act y, const ModC* mc, const uint32_t* te0,
+__global__ __launch_bounds__(512) void k_proj(ProjArgs a, Act x, Act y, const ModC* mc, const uint32_t* te0,
                                               const uint32_t* rk) {
     AES_PROLOGUE(te0, rk);
     const int j = blockIdx.y, b = blockIdx.z;
     const int64_t N = a.N;
-    const int64_t e = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-    if (e >= N) return;
+    for (int64_t e = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; e < N;
+         e += static_cast<int64_t>(gridDim.x) * blockDim.x) {
     const ModC mi = mc[a.pin[j]], mo = mc[a.pout[j]];
     const int16_t* L = x.p[j] + static_cast<int64_t>(b) * mi.n * N + e;
     const u128 H = aes_encrypt(aes, compress_cm(L, N, mi));
@@ -472,17 +497,18 @@ __global__ __launch_bounds__(256) void k_proj(ProjArgs a, Act x, Act y, const Mo
     s.init(P);
     int16_t* O = y.p[j] + static_cast<int64_t>(b) * mo.n * N + e;
     for (int i = 0; i < static_cast<int>(mo.n); ++i) O[i * N] = static_cast<int16_t>(s.next(mo));
+    }
 }
 
 // Generalized half-gate product of pairs (2e, 2e+1), and the mixed-modulus
 // variant (second operand first projected to Z_q). grid (ceil(No/256), k, B)
-__global__ __launch_bounds__(256) void k_mult(MultArgs a, Act x, Act y, const ModC* mc, const uint32_t* te0,
+__global__ __launch_bounds__(512) void k_mult(MultArgs a, Act x, Act y, const ModC* mc, const uint32_t* te0,
                                               const uint32_t* rk) {
     AES_PROLOGUE(te0, rk);
     const int j = blockIdx.y, b = blockIdx.z;
     const int64_t No = a.No, Ni = 2 * No;
-    const int64_t o = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-    if (o >= No) return;
+    for (int64_t o = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; o < No;
+         o += static_cast<int64_t>(gridDim.x) * blockDim.x) {
     const int p = a.crt.p[j];
     const ModC m = mc[p];
     const int16_t* X = x.p[j] + static_cast<int64_t>(b) * m.n * Ni + 2 * o;
@@ -523,6 +549,7 @@ __global__ __launch_bounds__(256) void k_mult(MultArgs a, Act x, Act y, const Mo
         if (v < 0) v += p;
         O[i * No] = static_cast<int16_t>(v);
     }
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -530,17 +557,17 @@ __global__ __launch_bounds__(256) void k_mult(MultArgs a, Act x, Act y, const Mo
 static inline dim3 grid_for(int64_t n, int bs, int y, int z) {
     return dim3(static_cast<unsigned>((n + bs - 1) / bs), y, z);
 }
-constexpr size_t kAesLds = DASH_AES_LDS_WORDS * sizeof(uint32_t);
+
 
 void launch_sign_approx(const SignArgs& a, const Act& x, const ModC* mc, const AesGlobals& g, hipStream_t st) {
-    hipLaunchKernelGGL(k_sign_approx, grid_for(a.N, 256, a.crt.k, a.B), dim3(256), kAesLds, st, a, x, mc, g.te0, g.rk);
+    hipLaunchKernelGGL(k_sign_approx, grid_aes(a.N, 512, a.crt.k, a.B), dim3(512), kAesLds, st, a, x, mc, g.te0, g.rk);
 }
 void launch_sign_chain(const SignArgs& a, int maxn, const ModC* mc, const AesGlobals& g, hipStream_t st) {
-    dim3 gr = grid_for(a.N, 128, 1, a.B);
+    dim3 gr = grid_aes(a.N, 512, 1, a.B);
     if (maxn <= 32)
-        hipLaunchKernelGGL(k_sign_chain<32>, gr, dim3(128), kAesLds, st, a, mc, g.te0, g.rk);
+        hipLaunchKernelGGL(k_sign_chain<32>, gr, dim3(512), kAesLds, st, a, mc, g.te0, g.rk);
     else
-        hipLaunchKernelGGL(k_sign_chain<64>, gr, dim3(128), kAesLds, st, a, mc, g.te0, g.rk);
+        hipLaunchKernelGGL(k_sign_chain<64>, gr, dim3(512), kAesLds, st, a, mc, g.te0, g.rk);
 }
 void launch_unpack(const u128* P, int nres, const Act& out, const CrtInfo& mods, const ModC* mc, int64_t N, int B,
                    hipStream_t st) {
@@ -552,7 +579,7 @@ void launch_relu_mult(const SignArgs& a, const Act& x, const Act& y, const u128*
 }
 void launch_rescale_hash(const Act& x, int fi, int s, const int16_t* up, int up_stride, int add_up, int64_t N, int B,
                          u128* h0, uint16_t* col0, const ModC* mc, const AesGlobals& g, hipStream_t st) {
-    hipLaunchKernelGGL(k_rescale_hash, grid_for(N, 256, 1, B), dim3(256), kAesLds, st, x, fi, s, up, up_stride,
+    hipLaunchKernelGGL(k_rescale_hash, grid_aes(N, 512, 1, B), dim3(512), kAesLds, st, x, fi, s, up, up_stride,
                        add_up, N, h0, col0, mc, g.te0, g.rk);
 }
 void launch_rescale_update(const RescaleArgs& a, const Act& x, int B, const ModC* mc, hipStream_t st) {
@@ -564,15 +591,15 @@ void launch_rescale_post(const Act& x, const CrtInfo& crt, int64_t N, int B, con
                        lab_stride, lab_off, mc);
 }
 void launch_base_ext(const BEArgs& a, const Act& x, int B, const ModC* mc, const AesGlobals& g, hipStream_t st) {
-    hipLaunchKernelGGL(k_base_ext, grid_for(a.N, 128, 1, B), dim3(128), kAesLds, st, a, x, mc, g.te0, g.rk);
+    hipLaunchKernelGGL(k_base_ext, grid_aes(a.N, 256, 1, B), dim3(256), kAesLds, st, a, x, mc, g.te0, g.rk);
 }
 void launch_proj(const ProjArgs& a, const Act& x, const Act& y, int B, const ModC* mc, const AesGlobals& g,
                  hipStream_t st) {
-    hipLaunchKernelGGL(k_proj, grid_for(a.N, 256, a.k, B), dim3(256), kAesLds, st, a, x, y, mc, g.te0, g.rk);
+    hipLaunchKernelGGL(k_proj, grid_aes(a.N, 512, a.k, B), dim3(512), kAesLds, st, a, x, y, mc, g.te0, g.rk);
 }
 void launch_mult(const MultArgs& a, const Act& x, const Act& y, int B, const ModC* mc, const AesGlobals& g,
                  hipStream_t st) {
-    hipLaunchKernelGGL(k_mult, grid_for(a.No, 256, a.crt.k, B), dim3(256), kAesLds, st, a, x, y, mc, g.te0, g.rk);
+    hipLaunchKernelGGL(k_mult, grid_aes(a.No, 512, a.crt.k, B), dim3(512), kAesLds, st, a, x, y, mc, g.te0, g.rk);
 }
 
 }  // namespace dev

@@ -75,13 +75,25 @@ __global__ __launch_bounds__(256) void k_window_sum(Act in, int64_t Nin, Act out
     out.p[j][(static_cast<int64_t>(b) * n + c) * Nout + o] = static_cast<int16_t>(acc % p);
 }
 
-__global__ __launch_bounds__(256) void k_aes_test(const u128* in, u128* out, int64_t n, const uint32_t* te0,
+__global__ __launch_bounds__(512) void k_aes_test(const u128* in, u128* out, int64_t n, const uint32_t* te0,
                                                   const uint32_t* rk) {
-    extern __shared__ uint32_t lds_aes[];
+    __shared__ uint32_t lds_aes[DASH_AES_LDS_WORDS];
     aes_lds_fill(lds_aes, te0);
     const AesCtx aes = aes_ctx(lds_aes, rk);
+    for (int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < n;
+         i += static_cast<int64_t>(gridDim.x) * blockDim.x)
+        out[i] = aes_encrypt(aes, in[i]);
+}
+
+// Throughput probe: every lane runs `iters` x 2 chained encryptions.
+__global__ __launch_bounds__(512) void k_aes_bench(u128* out, int iters, const uint32_t* te0) {
+    __shared__ uint32_t lds_aes[DASH_AES_LDS_WORDS];
+    aes_lds_fill(lds_aes, te0);
+    const AesCtx aes = aes_ctx(lds_aes, nullptr);
     const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-    if (i < n) out[i] = aes_encrypt(aes, in[i]);
+    u128 x = static_cast<u128>(i), y = ~static_cast<u128>(i);
+    for (int it = 0; it < iters; ++it) aes_encrypt2(aes, x, y, x, y);
+    out[i] = x ^ y;
 }
 
 // labels: component-major [n][N]; comp[e] = compress, decomp = decompress(comp)
@@ -135,8 +147,11 @@ void launch_window_sum(const Act& in, int64_t Nin, const Act& out, int64_t Nout,
                        crt);
 }
 void launch_aes_test(const u128* in, u128* out, int64_t n, const AesGlobals& g, hipStream_t st) {
-    hipLaunchKernelGGL(k_aes_test, g1(n, 1, 1), dim3(256), DASH_AES_LDS_WORDS * sizeof(uint32_t), st, in, out, n, g.te0,
-                       g.rk);
+    const unsigned nb = static_cast<unsigned>(std::min<int64_t>((n + 511) / 512, 2048));
+    hipLaunchKernelGGL(k_aes_test, dim3(nb), dim3(512), 0, st, in, out, n, g.te0, g.rk);
+}
+void launch_aes_bench(u128* out, int blocks, int iters, const AesGlobals& g, hipStream_t st) {
+    hipLaunchKernelGGL(k_aes_bench, dim3(blocks), dim3(512), 0, st, out, iters, g.te0);
 }
 void launch_codec_test(const int16_t* labels, int64_t N, int q, const ModC* mc, u128* comp, int16_t* decomp,
                        hipStream_t st) {

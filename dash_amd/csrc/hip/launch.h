@@ -40,6 +40,7 @@ void launch_pair_add(const Act& v, int64_t Nv, const Act& r, const Act& nv, int6
 void launch_add(const Act& x, const Act& y, int64_t N, const CrtInfo& crt, int B, hipStream_t st);
 void launch_window_sum(const Act& in, int64_t Nin, const Act& out, int64_t Nout, const int64_t* idx, int K,
                        const CrtInfo& crt, int B, hipStream_t st);
+void launch_aes_bench(u128* out, int blocks, int iters, const AesGlobals& g, hipStream_t st);
 void launch_aes_test(const u128* in, u128* out, int64_t n, const AesGlobals& g, hipStream_t st);
 void launch_codec_test(const int16_t* labels, int64_t N, int q, const ModC* mc, u128* comp, int16_t* decomp,
                        hipStream_t st);

@@ -1110,6 +1110,30 @@ void register_hip_bindings(py::module_& m) {
         (void)hipFree(dte); (void)hipFree(drk); (void)hipFree(din); (void)hipFree(dout);
         return out;
     });
+    m.def("hip_aes_bench", [](int blocks, int iters) {
+        // returns (ms, AES blocks per second)
+        auto te = make_te0();
+        uint32_t* dte;
+        u128* dout;
+        HIPCHECK(hipMalloc(&dte, 256 * 4));
+        HIPCHECK(hipMalloc(&dout, static_cast<size_t>(blocks) * 512 * 16));
+        HIPCHECK(hipMemcpy(dte, te.data(), 256 * 4, hipMemcpyHostToDevice));
+        AesGlobals g{dte, nullptr};
+        launch_aes_bench(dout, blocks, 4, g, nullptr);  // warm-up
+        hipEvent_t e0, e1;
+        HIPCHECK(hipEventCreate(&e0));
+        HIPCHECK(hipEventCreate(&e1));
+        HIPCHECK(hipEventRecord(e0, nullptr));
+        launch_aes_bench(dout, blocks, iters, g, nullptr);
+        HIPCHECK(hipEventRecord(e1, nullptr));
+        HIPCHECK(hipEventSynchronize(e1));
+        float ms = 0;
+        HIPCHECK(hipEventElapsedTime(&ms, e0, e1));
+        (void)hipEventDestroy(e0); (void)hipEventDestroy(e1);
+        (void)hipFree(dte); (void)hipFree(dout);
+        const double n = 2.0 * iters * blocks * 512.0;
+        return py::make_tuple(ms, n / (ms * 1e-3));
+    });
     m.def("hip_codec", [](py::array_t<int16_t, py::array::c_style | py::array::forcecast> labels, int q) {
         // labels (N, n) label-major -> (compressed (N,2) u64, decompressed (N, n))
         DASH_CHECK(labels.ndim() == 2, "expected (N, n)");
