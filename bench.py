@@ -105,12 +105,13 @@ def main() -> None:
 
     def step(i: int, verify: bool = False):
         xs = inputs[i * B:(i + 1) * B]
-        for b, (gc, x) in enumerate(zip(gcs, xs)):  # online message #1 (garbler -> pinned staging)
-            ev.encode_into(b, gc, x)
-        ev.upload_inputs(stream)
+        # online message #1 in wire form (16-B compressed labels) -> pinned staging -> H2D -> GPU unpack
+        for b, (gc, x) in enumerate(zip(gcs, xs)):
+            ev.encode_compressed_into(b, gc, x)
+        ev.upload_inputs_compressed(stream)
         ev.run(stream)
-        outs = ev.get_outputs(stream)  # online message #2 (synchronizes)
-        dec = [gc.decode_outputs(o) for gc, o in zip(gcs, outs)]
+        ev.fetch_outputs(stream)  # online message #2 (synchronizes)
+        dec = [ev.decode(b, gc) for b, gc in enumerate(gcs)]
         if verify:
             for gc, x, y in zip(gcs, xs, dec):
                 ref = gc.plain_q_eval(x)

@@ -100,6 +100,19 @@ std::vector<LayerSpec> specs_from_py(const py::list& l) {
     return out;
 }
 
+py::array_t<uint64_t> u128_array(const u128* src, py::ssize_t k, py::ssize_t n) {
+    py::array_t<uint64_t> out({k, n, static_cast<py::ssize_t>(2)});
+    if (k * n) std::memcpy(out.mutable_data(), src, sizeof(u128) * k * n);
+    return out;
+}
+
+const u128* u128_data(const py::array_t<uint64_t, py::array::c_style | py::array::forcecast>& a, py::ssize_t k,
+                      py::ssize_t n) {
+    DASH_CHECK(a.ndim() == 3 && a.shape(0) == k && a.shape(1) == n && a.shape(2) == 2,
+               "compressed labels must be a (k, N, 2) uint64 array");
+    return reinterpret_cast<const u128*>(a.data());
+}
+
 class IntegrityError : public std::exception {};
 
 }  // namespace
@@ -216,6 +229,15 @@ PYBIND11_MODULE(_dash_native, m) {
             auto v = d.decode_residues(labels_from_py(labels));
             return py::array_t<i64>({static_cast<py::ssize_t>(d.moduli.size()), static_cast<py::ssize_t>(d.n_out)}, v.data());
         })
+        .def("decode_compressed", [](const Decoder& d, py::array_t<uint64_t, py::array::c_style | py::array::forcecast> c) {
+            return d.decode_compressed(u128_data(c, d.moduli.size(), d.n_out));
+        })
+        .def("decode_residues_compressed", [](const Decoder& d, py::array_t<uint64_t, py::array::c_style | py::array::forcecast> c) {
+            auto r = d.decode_residues_compressed(u128_data(c, d.moduli.size(), d.n_out));
+            py::array_t<i64> out({static_cast<py::ssize_t>(d.moduli.size()), static_cast<py::ssize_t>(d.n_out)});
+            std::memcpy(out.mutable_data(), r.data(), r.size() * sizeof(i64));
+            return out;
+        })
         .def_property_readonly("moduli", [](const Decoder& d) { return d.moduli; })
         .def_property_readonly("n_out", [](const Decoder& d) { return d.n_out; })
         .def("serialize", [](const Decoder& d) { return py::bytes(d.serialize()); })
@@ -264,6 +286,15 @@ PYBIND11_MODULE(_dash_native, m) {
             for (auto& a : arrs) out.append(a);
             return out;
         })
+        .def("encode_compressed", [](const Garbler& g, py::array_t<i64, py::array::c_style | py::array::forcecast> x) {
+            const i64 N = x.size();
+            std::vector<u128> buf(g.crt().size() * N);
+            {
+                py::gil_scoped_release rel;
+                g.encode_compressed(x.data(), N, buf.data());
+            }
+            return u128_array(buf.data(), g.crt().size(), N);
+        })
         .def("decoder", [](const Garbler& g) { return std::make_shared<Decoder>(g.decoder()); })
         .def_property_readonly("crt_modulus", &Garbler::crt_modulus)
         .def("offset_label", [](const Garbler& g, int p) {
@@ -276,6 +307,18 @@ PYBIND11_MODULE(_dash_native, m) {
         })
         .def("input_base", [](const Garbler& g) { return labels_to_py(g.input_base()); });
 
+    m.def("compress_labels", [](const py::list& labels) {
+        CrtLabels L = labels_from_py(labels);
+        auto c = compress_labels(L);
+        return u128_array(c.data(), L.size(), L.empty() ? 0 : L[0].N);
+    });
+    m.def("decompress_labels", [](py::array_t<uint64_t, py::array::c_style | py::array::forcecast> c,
+                                  const std::vector<int>& moduli) {
+        DASH_CHECK(c.ndim() == 3, "compressed labels must be (k, N, 2)");
+        const i64 N = c.shape(1);
+        CrtLabels L = decompress_labels(u128_data(c, moduli.size(), N), moduli, N);
+        return labels_to_py(L);
+    });
     m.def("cpu_evaluate", [](std::shared_ptr<GarbledModel> gm, const py::list& labels, int nthreads) {
         CrtLabels in = labels_from_py(labels);
         CrtLabels out;

@@ -423,17 +423,18 @@ CrtLabels cpu_evaluate(const GarbledModel& m, const CrtLabels& inputs, int nt) {
 }
 
 // ---------------------------------------------------------------------------
-std::vector<i64> Decoder::decode_residues(const CrtLabels& out) const {
-    const int k = static_cast<int>(moduli.size());
-    DASH_CHECK(static_cast<int>(out.size()) == k, "decode: residue count mismatch");
+namespace {
+// h(j, e) -> hash of output label e of residue j
+template <class HashOf>
+std::vector<i64> decode_with(const Decoder& d, HashOf&& hash_of) {
+    const int k = static_cast<int>(d.moduli.size());
+    const i64 n_out = d.n_out;
     std::vector<i64> res(static_cast<size_t>(k) * n_out, -1);
     for (int j = 0; j < k; ++j) {
-        const int q = moduli[j];
-        const ModInfo& mq = mod_info(q);
-        DASH_CHECK(out[j].N == n_out && out[j].p == q, "decode: output label shape mismatch");
-        const u128* D = dec[j].ptr<u128>();
+        const int q = d.moduli[j];
+        const u128* D = d.dec[j].ptr<u128>();
         for (i64 e = 0; e < n_out; ++e) {
-            const u128 h = hash(compress(out[j].at(e), mq));
+            const u128 h = hash_of(j, e);
             i64 found = -1;
             for (int v = 0; v < q; ++v)
                 if (D[static_cast<i64>(v) * n_out + e] == h) {
@@ -449,8 +450,7 @@ std::vector<i64> Decoder::decode_residues(const CrtLabels& out) const {
     return res;
 }
 
-std::vector<i64> Decoder::decode(const CrtLabels& out) const {
-    const std::vector<i64> r = decode_residues(out);
+std::vector<i64> crt_combine(const std::vector<int>& moduli, i64 n_out, const std::vector<i64>& r) {
     const int k = static_cast<int>(moduli.size());
     u128 M = 1;
     for (int q : moduli) M *= static_cast<u128>(q);
@@ -461,7 +461,6 @@ std::vector<i64> Decoder::decode(const CrtLabels& out) const {
             const u128 q = static_cast<u128>(moduli[j]);
             const u128 P = M / q;
             const u128 inv = static_cast<u128>(mul_inv(P % q, static_cast<i64>(q)));
-            // term = r * inv mod q, then * P (< M)
             const u128 t = (static_cast<u128>(r[static_cast<size_t>(j) * n_out + e]) * inv) % q;
             sum = (sum + t * P) % M;
         }
@@ -470,6 +469,27 @@ std::vector<i64> Decoder::decode(const CrtLabels& out) const {
         val[e] = v;
     }
     return val;
+}
+}  // namespace
+
+std::vector<i64> Decoder::decode_residues(const CrtLabels& out) const {
+    const int k = static_cast<int>(moduli.size());
+    DASH_CHECK(static_cast<int>(out.size()) == k, "decode: residue count mismatch");
+    for (int j = 0; j < k; ++j)
+        DASH_CHECK(out[j].N == n_out && out[j].p == moduli[j], "decode: output label shape mismatch");
+    return decode_with(*this, [&](int j, i64 e) { return hash(compress(out[j].at(e), mod_info(moduli[j]))); });
+}
+
+std::vector<i64> Decoder::decode_residues_compressed(const u128* C) const {
+    return decode_with(*this, [&](int j, i64 e) { return hash(C[static_cast<i64>(j) * n_out + e]); });
+}
+
+std::vector<i64> Decoder::decode_compressed(const u128* C) const {
+    return crt_combine(moduli, n_out, decode_residues_compressed(C));
+}
+
+std::vector<i64> Decoder::decode(const CrtLabels& out) const {
+    return crt_combine(moduli, n_out, decode_residues(out));
 }
 
 }  // namespace dash

@@ -212,6 +212,55 @@ void Garbler::encode_cm(const i64* x, i64 N, const std::vector<comp_t*>& dst, in
     }, nthreads);
 }
 
+void Garbler::encode_compressed(const i64* x, i64 N, u128* dst, int nthreads) const {
+    DASH_CHECK(!in_base_.empty() && in_base_[0].N == N, "input size does not match the garbled circuit");
+    const int k = static_cast<int>(crt_.size());
+    parallel_for(static_cast<i64>(k) * N, [&](i64 r0, i64 r1) {
+        comp_t buf[128];
+        for (i64 r = r0; r < r1; ++r) {
+            const int j = static_cast<int>(r / N);
+            const i64 e = r % N;
+            const int p = crt_[j];
+            const ModInfo& mi = mod_info(p);
+            const comp_t* W0 = in_base_[j].at(e);
+            const comp_t* R = R_.get(p);
+            const i64 v = pmod(x[e], p);
+            for (int c = 0; c < mi.n; ++c) buf[c] = static_cast<comp_t>((W0[c] + v * R[c]) % p);
+            dst[r] = compress(buf, mi);
+        }
+    }, nthreads);
+}
+
+std::vector<u128> compress_labels(const CrtLabels& L, int nthreads) {
+    const int k = static_cast<int>(L.size());
+    const i64 N = k ? L[0].N : 0;
+    std::vector<u128> out(static_cast<size_t>(k) * N);
+    parallel_for(static_cast<i64>(k) * N, [&](i64 r0, i64 r1) {
+        for (i64 r = r0; r < r1; ++r) {
+            const int j = static_cast<int>(r / N);
+            out[r] = compress(L[j].at(r % N), mod_info(L[j].p));
+        }
+    }, nthreads);
+    return out;
+}
+
+CrtLabels decompress_labels(const u128* C, const std::vector<int>& moduli, i64 N, int nthreads) {
+    CrtLabels out;
+    for (int p : moduli) out.emplace_back(p, N);
+    const int k = static_cast<int>(moduli.size());
+    parallel_for(static_cast<i64>(k) * N, [&](i64 r0, i64 r1) {
+        for (i64 r = r0; r < r1; ++r) {
+            const int j = static_cast<int>(r / N);
+            const ModInfo& mi = mod_info(moduli[j]);
+            comp_t* o = out[j].at(r % N);
+            decompress(C[r], o, mi);
+            for (int c = 0; c < mi.n; ++c)
+                DASH_CHECK(o[c] >= 0 && o[c] < mi.p, "dash integrity: malformed compressed label");
+        }
+    }, nthreads);
+    return out;
+}
+
 GarbledModel Garbler::garble(const std::vector<LayerSpec>& layers, const std::vector<i64>& in_dims,
                              const GarbleOptions& opt) {
     const int nt = opt.nthreads;

@@ -49,7 +49,9 @@ struct SignArgs {
     const uint16_t* zcol;  // [B][zc_stride] zero-label colors
     int zc_stride;
     int relu;            // also produce hs / cs for the ReLU multiply
+    int16_t* csum;       // [B][t][kCsumComps][N] per-digit sums of the k cast labels (phase B1)
 };
+constexpr int kCsumComps = 64;
 
 struct RescaleArgs {
     CrtInfo crt;

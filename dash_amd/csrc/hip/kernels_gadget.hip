@@ -46,7 +46,7 @@ static inline dim3 grid_aes(int64_t n, int bs, int y, int z) {
 
 // ---------------------------------------------------------------------------
 // Phase A: approximate residues. grid (ceil(N/256), k, B)
-__global__ __launch_bounds__(512) void k_sign_approx(SignArgs a, Act x, const ModC* mc, const uint32_t* te0,
+__global__ __launch_bounds__(512, 2) void k_sign_approx(SignArgs a, Act x, const ModC* mc, const uint32_t* te0,
                                                      const uint32_t* rk) {
     AES_PROLOGUE(te0, rk);
     const int j = blockIdx.y, b = blockIdx.z;
@@ -79,114 +79,152 @@ __global__ __launch_bounds__(512) void k_sign_approx(SignArgs a, Act x, const Mo
 }
 
 // ---------------------------------------------------------------------------
-// Phase B: mixed-radix carry chain + sign projection. grid (ceil(N/128), 1, B)
+// Phase B1: per MRS digit d >= 1, the sum over residues j of the casts
+// Z_{m_d} -> Z_{(k+1) m_d} of the approx labels; for d = 0 the plain sum of
+// the approx labels mod m_0. None of this depends on the carry, so it runs
+// fully parallel over (GC, digit, element), with paired AES.
+// grid (x, t, B): blockIdx.y = t-1 is digit 0, otherwise digit y+1.
 template <int MAXN>
-__global__ __launch_bounds__(512) void k_sign_chain(SignArgs a, const ModC* mc, const uint32_t* te0,
+__global__ __launch_bounds__(512, 2) void k_sign_castsum(SignArgs a, const ModC* mc, const uint32_t* te0,
+                                                      const uint32_t* rk) {
+    AES_PROLOGUE(te0, rk);
+    const int b = blockIdx.z;
+    const int k = a.crt.k, t = a.t;
+    const int d = (static_cast<int>(blockIdx.y) == t - 1) ? 0 : static_cast<int>(blockIdx.y) + 1;
+    const int64_t N = a.N;
+    const int m = a.mrs[d];
+    const int mo = d ? (k + 1) * m : m;
+    const ModC Mm = mc[m];
+    const ModC Mo = mc[mo];
+    int64_t c1 = 0;
+    for (int dd = t - 1; dd > d; --dd) c1 += static_cast<int64_t>(k + 1) * a.mrs[dd];
+    for (int64_t e = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; e < N;
+         e += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+        const u128* P0 = a.mrsP + static_cast<int64_t>(b) * k * t * N + e;
+        int32_t acc[MAXN];
+#pragma unroll
+        for (int i = 0; i < MAXN; ++i) acc[i] = 0;
+        if (d == 0) {
+            for (int j = 0; j < k; ++j) {
+                DigitStream s0;
+                s0.init(P0[static_cast<int64_t>(j) * t * N]);
+#pragma unroll
+                for (int i = 0; i < MAXN; ++i)
+                    if (i < static_cast<int>(Mo.n)) acc[i] += static_cast<int32_t>(s0.next(Mo));
+            }
+        } else {
+            const u128* T1 = a.cast1 + (static_cast<int64_t>(b) * N + e) * a.n_cast + c1;
+            for (int j = 0; j < k; j += 2) {
+                const bool two = j + 1 < k;
+                const u128 keyA = P0[(static_cast<int64_t>(j) * t + d) * N];
+                const u128 keyB = two ? P0[(static_cast<int64_t>(j + 1) * t + d) * N] : static_cast<u128>(0);
+                const uint32_t colA = u128_mod(keyA, Mm);
+                const uint32_t colB = two ? u128_mod(keyB, Mm) : 0u;
+                const u128 TA = T1[static_cast<int64_t>(j) * m + colA];
+                const u128 TB = two ? T1[static_cast<int64_t>(j + 1) * m + colB] : static_cast<u128>(0);
+                u128 HA, HB = 0;
+                if (two)
+                    aes_encrypt2(aes, keyA, keyB, HA, HB);
+                else
+                    HA = aes_encrypt(aes, keyA);
+                DigitStream sa, sb;
+                sa.init(TA - HA);
+                sb.init(TB - HB);
+#pragma unroll
+                for (int i = 0; i < MAXN; ++i)
+                    if (i < static_cast<int>(Mo.n)) {
+                        acc[i] += static_cast<int32_t>(sa.next(Mo));
+                        if (two) acc[i] += static_cast<int32_t>(sb.next(Mo));
+                    }
+            }
+        }
+        int16_t* S = a.csum + ((static_cast<int64_t>(b) * t + d) * kCsumComps) * N + e;
+#pragma unroll
+        for (int i = 0; i < MAXN; ++i)
+            if (i < static_cast<int>(Mo.n)) S[i * N] = static_cast<int16_t>(acc[i] % mo);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Phase B2: the serial mixed-radix carry chain + sign projection. Per digit
+// only the carry's cast and the sum's cast2 projection remain on the
+// critical path (2 AES + 2 gathers). grid (x, 1, B)
+template <int MAXN>
+__global__ __launch_bounds__(512, 2) void k_sign_chain(SignArgs a, const ModC* mc, const uint32_t* te0,
                                                     const uint32_t* rk) {
     AES_PROLOGUE(te0, rk);
     const int b = blockIdx.z;
     const int64_t N = a.N;
+    const int k = a.crt.k, t = a.t;
     for (int64_t e = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; e < N;
          e += static_cast<int64_t>(gridDim.x) * blockDim.x) {
-    const int k = a.crt.k, t = a.t;
-    const u128* T1 = a.cast1 + (static_cast<int64_t>(b) * N + e) * a.n_cast;
-    const u128* T2 = a.cast2 + (static_cast<int64_t>(b) * N + e) * a.n_cast;
-    const u128* P0 = a.mrsP + static_cast<int64_t>(b) * k * t * N + e;  // + (j*t + d)*N
-    const int mlast = a.mrs[t - 1];
-    u128 carry = a.zc[static_cast<int64_t>(b) * a.zc_stride + mlast];
-    uint32_t ccol = a.zcol[static_cast<int64_t>(b) * a.zc_stride + mlast];
-    int32_t acc[MAXN];
-    int64_t c1 = 0, c2 = 0;
-    for (int d = t - 1; d >= 1; --d) {
-        const int m = a.mrs[d];
-        const int mo = (k + 1) * m;
-        const ModC Mm = mc[m];
-        const ModC Mo = mc[mo];
+        const u128* T1 = a.cast1 + (static_cast<int64_t>(b) * N + e) * a.n_cast;
+        const u128* T2 = a.cast2 + (static_cast<int64_t>(b) * N + e) * a.n_cast;
+        const int16_t* S = a.csum + static_cast<int64_t>(b) * t * kCsumComps * N + e;
+        const int mlast = a.mrs[t - 1];
+        u128 carry = a.zc[static_cast<int64_t>(b) * a.zc_stride + mlast];
+        uint32_t ccol = a.zcol[static_cast<int64_t>(b) * a.zc_stride + mlast];
+        int64_t c1 = 0, c2 = 0;
+        int32_t acc[MAXN];
+        for (int d = t - 1; d >= 1; --d) {
+            const int m = a.mrs[d];
+            const int mo = (k + 1) * m;
+            const ModC Mo = mc[mo];
+            const u128 TA = T1[c1 + static_cast<int64_t>(k) * m + ccol];
+            const int16_t* Sd = S + static_cast<int64_t>(d) * kCsumComps * N;
 #pragma unroll
-        for (int i = 0; i < MAXN; ++i) acc[i] = 0;
-        for (int j = 0; j <= k; j += 2) {
-            const bool two = j + 1 <= k;
-            u128 keyA, keyB = 0;
-            uint32_t colA, colB = 0;
-            if (j < k) {
-                keyA = P0[(static_cast<int64_t>(j) * t + d) * N];
-                colA = u128_mod(keyA, Mm);
-            } else {
-                keyA = carry;
-                colA = ccol;
-            }
-            if (two) {
-                if (j + 1 < k) {
-                    keyB = P0[(static_cast<int64_t>(j + 1) * t + d) * N];
-                    colB = u128_mod(keyB, Mm);
-                } else {
-                    keyB = carry;
-                    colB = ccol;
-                }
-            }
-            // gathers before the AES so the HBM latency overlaps it
-            const u128 TA = T1[c1 + colA];
-            const u128 TB = two ? T1[c1 + m + colB] : static_cast<u128>(0);
-            u128 HA, HB;
-            if (two)
-                aes_encrypt2(aes, keyA, keyB, HA, HB);
-            else
-                HA = aes_encrypt(aes, keyA);
-            c1 += two ? 2 * m : m;
-            DigitStream sa, sb;
+            for (int i = 0; i < MAXN; ++i)
+                if (i < static_cast<int>(Mo.n)) acc[i] = Sd[i * N];
+            const u128 HA = aes_encrypt(aes, carry);
+            c1 += static_cast<int64_t>(k + 1) * m;
+            DigitStream sa;
             sa.init(TA - HA);
-            sb.init(TB - HB);
+            CompressFwd cf;
+            cf.init();
+            uint32_t col2 = 0;
 #pragma unroll
             for (int i = 0; i < MAXN; ++i)
                 if (i < static_cast<int>(Mo.n)) {
-                    acc[i] += static_cast<int32_t>(sa.next(Mo));
-                    if (two) acc[i] += static_cast<int32_t>(sb.next(Mo));
+                    uint32_t v = static_cast<uint32_t>(acc[i]) + sa.next(Mo);
+                    if (v >= static_cast<uint32_t>(mo)) v -= mo;
+                    if (i == 0) col2 = v;
+                    cf.push(v, Mo);
                 }
+            const u128 key2 = cf.finish();
+            const u128 T2e = T2[c2 + col2];
+            const u128 H2 = aes_encrypt(aes, key2);
+            carry = T2e - H2;
+            c2 += mo;
+            ccol = u128_mod(carry, mc[a.mrs[d - 1]]);
         }
+        // most significant digit: sum = carry + sum_j mrs[j][0] (the latter from phase B1)
+        const int m0 = a.mrs[0];
+        const ModC M0 = mc[m0];
+        DigitStream sc;
+        sc.init(carry);
         CompressFwd cf;
         cf.init();
+        uint32_t col = 0;
 #pragma unroll
         for (int i = 0; i < MAXN; ++i)
-            if (i < static_cast<int>(Mo.n)) cf.push(static_cast<uint32_t>(acc[i]) % mo, Mo);
-        const u128 key2 = cf.finish();
-        const uint32_t col2 = static_cast<uint32_t>(acc[0]) % mo;
-        const u128 T2e = T2[c2 + col2];
-        const u128 H2 = aes_encrypt(aes, key2);
-        carry = T2e - H2;
-        c2 += mo;
-        ccol = u128_mod(carry, mc[a.mrs[d - 1]]);
-    }
-    // most significant digit: sum = carry + sum_j mrs[j][0]
-    const int m0 = a.mrs[0];
-    const ModC M0 = mc[m0];
-#pragma unroll
-    for (int i = 0; i < MAXN; ++i) acc[i] = 0;
-    for (int j = 0; j <= k; ++j) {
-        const u128 P = j < k ? P0[static_cast<int64_t>(j) * t * N] : carry;
-        DigitStream s;
-        s.init(P);
-#pragma unroll
-        for (int i = 0; i < MAXN; ++i)
-            if (i < static_cast<int>(M0.n)) acc[i] += static_cast<int32_t>(s.next(M0));
-    }
-    CompressFwd cf;
-    cf.init();
-#pragma unroll
-    for (int i = 0; i < MAXN; ++i)
-        if (i < static_cast<int>(M0.n)) cf.push(static_cast<uint32_t>(acc[i]) % m0, M0);
-    const u128 key = cf.finish();
-    const uint32_t col = static_cast<uint32_t>(acc[0]) % m0;
-    const u128* TS = a.sign + (static_cast<int64_t>(b) * N + e) * a.n_sign;
-    const u128 TS0 = TS[col];
-    const u128 H = aes_encrypt(aes, key);
-    for (int o = 0; o < a.nout; ++o) {
-        const u128 P = (o == 0 ? TS0 : TS[o * m0 + col]) - H;
-        a.outP[(static_cast<int64_t>(b) * a.nout + o) * N + e] = P;
-        if (a.relu && o == 0) {
-            a.hs[static_cast<int64_t>(b) * N + e] = aes_encrypt(aes, P);
-            a.cs[static_cast<int64_t>(b) * N + e] = static_cast<uint8_t>(static_cast<uint32_t>(P) & 1u);
+            if (i < static_cast<int>(M0.n)) {
+                uint32_t v = static_cast<uint32_t>(S[i * N]) + sc.next(M0);
+                if (v >= static_cast<uint32_t>(m0)) v -= m0;
+                if (i == 0) col = v;
+                cf.push(v, M0);
+            }
+        const u128 key = cf.finish();
+        const u128* TS = a.sign + (static_cast<int64_t>(b) * N + e) * a.n_sign;
+        const u128 TS0 = TS[col];
+        const u128 H = aes_encrypt(aes, key);
+        for (int o = 0; o < a.nout; ++o) {
+            const u128 P = (o == 0 ? TS0 : TS[o * m0 + col]) - H;
+            a.outP[(static_cast<int64_t>(b) * a.nout + o) * N + e] = P;
+            if (a.relu && o == 0) {
+                a.hs[static_cast<int64_t>(b) * N + e] = aes_encrypt(aes, P);
+                a.cs[static_cast<int64_t>(b) * N + e] = static_cast<uint8_t>(static_cast<uint32_t>(P) & 1u);
+            }
         }
-    }
     }
 }
 
@@ -247,7 +285,7 @@ __global__ __launch_bounds__(256) void k_relu_mult(SignArgs a, Act x, Act y, con
 // ---------------------------------------------------------------------------
 // Rescale step 1+2 for one factor: hash the factor residue (optionally after
 // the upshift). grid (ceil(N/256), 1, B)
-__global__ __launch_bounds__(512) void k_rescale_hash(Act x, int fi, int s, const int16_t* up, int up_stride,
+__global__ __launch_bounds__(512, 2) void k_rescale_hash(Act x, int fi, int s, const int16_t* up, int up_stride,
                                                       int add_up, int64_t N, u128* h0, uint16_t* col0,
                                                       const ModC* mc, const uint32_t* te0, const uint32_t* rk) {
     AES_PROLOGUE(te0, rk);
@@ -345,7 +383,7 @@ __global__ __launch_bounds__(256) void k_rescale_post(Act x, CrtInfo crt, int64_
 //            next sign gadget (phase A) in the same pass.
 // The downshift of iteration i and the upshift of i+1 collapse into one
 // delta = up - down; only the last iteration writes a downshifted result.
-__global__ __launch_bounds__(512) void k_rescale_hash_sign(const u128* signP, const u128* du, int64_t N, u128* h0,
+__global__ __launch_bounds__(512, 2) void k_rescale_hash_sign(const u128* signP, const u128* du, int64_t N, u128* h0,
                                                            uint16_t* col0, const uint32_t* te0, const uint32_t* rk) {
     AES_PROLOGUE(te0, rk);
     const int b = blockIdx.z;
@@ -358,7 +396,7 @@ __global__ __launch_bounds__(512) void k_rescale_hash_sign(const u128* signP, co
 }
 
 // grid (ceil(N/256), k, B)
-__global__ __launch_bounds__(512) void k_rescale_update_approx(RescaleArgs r, SignArgs a, Act x, const int16_t* delta,
+__global__ __launch_bounds__(512, 2) void k_rescale_update_approx(RescaleArgs r, SignArgs a, Act x, const int16_t* delta,
                                                                const u128* zh, const ModC* mc, const uint32_t* te0,
                                                                const uint32_t* rk) {
     AES_PROLOGUE(te0, rk);
@@ -481,7 +519,7 @@ __global__ __launch_bounds__(256) void k_base_ext(BEArgs a, Act x, const ModC* m
 
 // ---------------------------------------------------------------------------
 // Generic projection layer (test-only Projection). grid (ceil(N/256), k, B)
-__global__ __launch_bounds__(512) void k_proj(ProjArgs a, Act x, Act y, const ModC* mc, const uint32_t* te0,
+__global__ __launch_bounds__(512, 2) void k_proj(ProjArgs a, Act x, Act y, const ModC* mc, const uint32_t* te0,
                                               const uint32_t* rk) {
     AES_PROLOGUE(te0, rk);
     const int j = blockIdx.y, b = blockIdx.z;
@@ -502,7 +540,7 @@ __global__ __launch_bounds__(512) void k_proj(ProjArgs a, Act x, Act y, const Mo
 
 // Generalized half-gate product of pairs (2e, 2e+1), and the mixed-modulus
 // variant (second operand first projected to Z_q). grid (ceil(No/256), k, B)
-__global__ __launch_bounds__(512) void k_mult(MultArgs a, Act x, Act y, const ModC* mc, const uint32_t* te0,
+__global__ __launch_bounds__(512, 2) void k_mult(MultArgs a, Act x, Act y, const ModC* mc, const uint32_t* te0,
                                               const uint32_t* rk) {
     AES_PROLOGUE(te0, rk);
     const int j = blockIdx.y, b = blockIdx.z;
@@ -563,11 +601,15 @@ void launch_sign_approx(const SignArgs& a, const Act& x, const ModC* mc, const A
     hipLaunchKernelGGL(k_sign_approx, grid_aes(a.N, 512, a.crt.k, a.B), dim3(512), kAesLds, st, a, x, mc, g.te0, g.rk);
 }
 void launch_sign_chain(const SignArgs& a, int maxn, const ModC* mc, const AesGlobals& g, hipStream_t st) {
-    dim3 gr = grid_aes(a.N, 512, 1, a.B);
-    if (maxn <= 32)
+    const dim3 gs = grid_aes(a.N, 512, a.t, a.B);
+    const dim3 gr = grid_aes(a.N, 512, 1, a.B);
+    if (maxn <= 32) {
+        hipLaunchKernelGGL(k_sign_castsum<32>, gs, dim3(512), kAesLds, st, a, mc, g.te0, g.rk);
         hipLaunchKernelGGL(k_sign_chain<32>, gr, dim3(512), kAesLds, st, a, mc, g.te0, g.rk);
-    else
+    } else {
+        hipLaunchKernelGGL(k_sign_castsum<64>, gs, dim3(512), kAesLds, st, a, mc, g.te0, g.rk);
         hipLaunchKernelGGL(k_sign_chain<64>, gr, dim3(512), kAesLds, st, a, mc, g.te0, g.rk);
+    }
 }
 void launch_unpack(const u128* P, int nres, const Act& out, const CrtInfo& mods, const ModC* mc, int64_t N, int B,
                    hipStream_t st) {

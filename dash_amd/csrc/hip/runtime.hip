@@ -164,6 +164,46 @@ class HipEvaluator {
         return v;
     }
     i64 input_size() const { return N0_; }
+    // compressed staging (online message #1 in wire form): [B][k][N0] u128
+    u128* input_slot_compressed(int b) {
+        DASH_CHECK(b >= 0 && b < B_, "batch slot out of range");
+        if (!in_comp_stage_) {
+            const size_t bytes = sizeof(u128) * B_ * k_ * N0_;
+            HIPCHECK(hipHostMalloc(reinterpret_cast<void**>(&in_comp_stage_), bytes));
+            host_allocs_.push_back(in_comp_stage_);
+            HIPCHECK(hipMalloc(reinterpret_cast<void**>(&in_comp_dev_), bytes));
+            allocs_.push_back(in_comp_dev_);
+            dev_bytes_ += bytes;
+        }
+        return in_comp_stage_ + static_cast<i64>(b) * k_ * N0_;
+    }
+    void upload_inputs_compressed(hipStream_t st) {
+        DASH_CHECK(in_comp_stage_ != nullptr, "no compressed inputs staged");
+        HIPCHECK(hipMemcpyAsync(in_comp_dev_, in_comp_stage_, sizeof(u128) * B_ * k_ * N0_, hipMemcpyHostToDevice, st));
+        launch_unpack(in_comp_dev_, k_, bufs_[0], crt_info(crt_), mc_, N0_, B_, st);
+    }
+    // output labels of slot b, compressed on the host: [k][Nout]
+    std::vector<u128> outputs_compressed(int b) const {
+        std::vector<u128> r(static_cast<size_t>(k_) * Nout_);
+        for (int j = 0; j < k_; ++j) {
+            const ModInfo& mi = mod_info(out_mod_[j]);
+            comp_t buf[128];
+            for (i64 e = 0; e < Nout_; ++e) {
+                for (int c = 0; c < mi.n; ++c) buf[c] = out_stage_[j][(static_cast<i64>(b) * mi.n + c) * Nout_ + e];
+                r[static_cast<size_t>(j) * Nout_ + e] = compress(buf, mi);
+            }
+        }
+        return r;
+    }
+    void fetch_outputs(hipStream_t st) {
+        for (int j = 0; j < k_; ++j) {
+            const int n = nr_comps(out_mod_[j]);
+            HIPCHECK(hipMemcpyAsync(out_stage_[j], final_.p[j], sizeof(int16_t) * B_ * n * Nout_, hipMemcpyDeviceToHost, st));
+        }
+        HIPCHECK(hipStreamSynchronize(st));
+    }
+    int crt_size() const { return k_; }
+    i64 output_size() const { return Nout_; }
     void upload_inputs(hipStream_t st) {
         for (int j = 0; j < k_; ++j)
             HIPCHECK(hipMemcpyAsync(bufs_[0].p[j], in_stage_[j], sizeof(int16_t) * B_ * nr_comps(crt_[j]) * N0_,
@@ -319,6 +359,7 @@ class HipEvaluator {
         a.zcol = zcol_;
         a.zc_stride = zstride_;
         a.relu = relu;
+        a.csum = csum_;
         int maxn = 0;
         const int k = k_;
         for (size_t d = 1; d < sp.mrs.size(); ++d) maxn = std::max(maxn, nr_comps((k + 1) * sp.mrs[d]));
@@ -348,6 +389,8 @@ class HipEvaluator {
     Act final_{};
     Act cur_act_{};
     std::vector<int16_t*> in_stage_, out_stage_;
+    u128* in_comp_stage_ = nullptr;
+    u128* in_comp_dev_ = nullptr;
     // constants
     ModC* mc_ = nullptr;
     AesGlobals aes_{};
@@ -364,6 +407,7 @@ class HipEvaluator {
     u128 *mrsP_ = nullptr, *hx_ = nullptr, *outP_ = nullptr, *hs_ = nullptr, *h0_ = nullptr;
     uint16_t *colx_ = nullptr, *col0_ = nullptr;
     uint8_t* cs_ = nullptr;
+    int16_t* csum_ = nullptr;
     int16_t* be_work_ = nullptr;
     int sign_maxn_ = 32;
     std::vector<std::vector<int16_t*>> saved_;  // residual-add sources
@@ -460,6 +504,7 @@ void HipEvaluator::build() {
     int tmax = std::max<int>(1, static_cast<int>(m0.h.mrs.size()));
     mrsP_ = dalloc<u128>(static_cast<size_t>(B_) * k_ * tmax * maxSignN);
     hx_ = dalloc<u128>(static_cast<size_t>(B_) * k_ * maxSignN);
+    csum_ = dalloc<int16_t>(static_cast<size_t>(B_) * tmax * kCsumComps * maxSignN);
     colx_ = dalloc<uint16_t>(static_cast<size_t>(B_) * k_ * maxSignN);
     outP_ = dalloc<u128>(static_cast<size_t>(B_) * k_ * maxSignN);
     hs_ = dalloc<u128>(static_cast<size_t>(B_) * maxSignN);
@@ -1022,6 +1067,15 @@ hipStream_t as_stream(uintptr_t s) { return reinterpret_cast<hipStream_t>(s); }
 }  // namespace
 
 void register_hip_bindings(py::module_& m) {
+    m.def("encode_compressed_into", [](const Garbler& g, py::array_t<i64, py::array::c_style | py::array::forcecast> x,
+                                       HipEvaluator& h, int b) {
+        DASH_CHECK(x.size() == h.input_size(), "input size mismatch");
+        u128* dst = h.input_slot_compressed(b);
+        const i64* xp = x.data();
+        const i64 N = x.size();
+        py::gil_scoped_release rel;
+        g.encode_compressed(xp, N, dst);
+    });
     // in-process two-party fast path: the garbler encodes straight into the
     // evaluator's pinned staging slot (the bytes are exactly online message #1)
     m.def("encode_into", [](const Garbler& g, py::array_t<i64, py::array::c_style | py::array::forcecast> x,
@@ -1067,6 +1121,26 @@ void register_hip_bindings(py::module_& m) {
             }
         })
         .def("upload_inputs", [](HipEvaluator& h, uintptr_t stream) { h.upload_inputs(as_stream(stream)); }, py::arg("stream") = 0)
+        .def("set_input_compressed", [](HipEvaluator& h, int b, py::array_t<uint64_t, py::array::c_style | py::array::forcecast> c) {
+            DASH_CHECK(c.ndim() == 3 && c.shape(0) == h.crt_size() && c.shape(1) == h.input_size() && c.shape(2) == 2,
+                       "compressed inputs must be (k, N, 2) uint64");
+            std::memcpy(h.input_slot_compressed(b), c.data(), sizeof(u128) * h.crt_size() * h.input_size());
+        })
+        .def("upload_inputs_compressed", [](HipEvaluator& h, uintptr_t stream) { h.upload_inputs_compressed(as_stream(stream)); },
+             py::arg("stream") = 0)
+        .def("fetch_outputs", [](HipEvaluator& h, uintptr_t stream) { h.fetch_outputs(as_stream(stream)); }, py::arg("stream") = 0)
+        .def("outputs_compressed", [](const HipEvaluator& h, int b) {
+            auto r = h.outputs_compressed(b);
+            py::array_t<uint64_t> out({static_cast<py::ssize_t>(h.crt_size()), static_cast<py::ssize_t>(h.output_size()),
+                                       static_cast<py::ssize_t>(2)});
+            std::memcpy(out.mutable_data(), r.data(), r.size() * sizeof(u128));
+            return out;
+        })
+        .def("decode_into", [](const HipEvaluator& h, int b, const Decoder& d) {
+            // online message #2 (compressed) decoded by the garbler, no Python round trip
+            auto r = h.outputs_compressed(b);
+            return d.decode_compressed(r.data());
+        })
         .def("get_outputs", [](HipEvaluator& h, uintptr_t stream) {
             auto o = h.get_outputs(as_stream(stream));
             py::list r;

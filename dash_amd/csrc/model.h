@@ -87,6 +87,9 @@ struct Decoder {
     std::vector<Array> dec;  // per residue: u128 [p][n_out] = H(compress(out0 + v*R))
     std::vector<i64> decode(const CrtLabels& out) const;
     std::vector<i64> decode_residues(const CrtLabels& out) const;  // [k][n_out] residues
+    // same, from compressed output labels C[j * n_out + e] (wire form of online message #2)
+    std::vector<i64> decode_residues_compressed(const u128* C) const;
+    std::vector<i64> decode_compressed(const u128* C) const;
     std::string serialize() const;
     static Decoder deserialize(const std::string& blob);
 };
@@ -102,6 +105,8 @@ class Garbler {
                         const GarbleOptions& opt = {});
     // Online message #1: encoded inputs x -> W0 + (x mod p) * R
     CrtLabels encode(const std::vector<i64>& x) const;
+    // Same message compressed (16 B per label, the reference's wire size): dst[j * N + e]
+    void encode_compressed(const i64* x, i64 N, u128* dst, int nthreads = 0) const;
     // Same message, component-major per residue: dst[j][c * N + e]
     void encode_cm(const i64* x, i64 N, const std::vector<comp_t*>& dst, int nthreads = 0) const;
     const Decoder& decoder() const { return dec_; }
@@ -124,6 +129,10 @@ class Garbler {
 
 // Host (oracle) evaluator: bit-exact reference for the HIP evaluator.
 CrtLabels cpu_evaluate(const GarbledModel& m, const CrtLabels& inputs, int nthreads = 0);
+
+// Wire-form helpers: compressed labels [k][N] <-> CrtLabels
+std::vector<u128> compress_labels(const CrtLabels& L, int nthreads = 0);
+CrtLabels decompress_labels(const u128* C, const std::vector<int>& moduli, i64 N, int nthreads = 0);
 
 // Required moduli (for R/Z banks) given bases.
 int required_max_modulus(const std::vector<int>& crt, const std::vector<int>& mrs, const std::vector<LayerSpec>& layers);

@@ -69,6 +69,16 @@ class GarbledCircuit:
         assert x.size == self.circuit.input_size, "input dimension does not match circuit input dimension"
         return self.garbler.encode_cm(x)
 
+    def garble_inputs_compressed(self, x: np.ndarray) -> np.ndarray:
+        """Online message #1 in wire form: (k, N, 2) uint64, one 16-B compressed label per residue."""
+        x = np.asarray(x, dtype=np.int64).reshape(-1)
+        assert x.size == self.circuit.input_size, "input dimension does not match circuit input dimension"
+        return self.garbler.encode_compressed(x)
+
+    def decode_compressed(self, labels: np.ndarray) -> np.ndarray:
+        """Decode online message #2 in wire form ((k, n_out, 2) uint64)."""
+        return np.asarray(self.decoder.decode_compressed(labels), dtype=np.int64)
+
     def cpu_evaluate(self, labels: Labels, nr_threads: int = 0) -> Labels:
         return self._n.cpu_evaluate(self.model, labels, nr_threads)
 

@@ -1,0 +1,208 @@
+"""Garbler/evaluator protocol over a `Channel`.
+
+Messages (tags):
+  HELO  client -> server  JSON {"version", "batch"};   server -> client JSON {"backend", "device"}
+  MODL  client -> server  flags = slot, payload = GarbledModel.serialize()      (offline)
+  INPT  client -> server  flags = n, payload = n x (k, N, 2) uint64 compressed input labels   (online #1)
+  OUTP  server -> client  payload = n x (k, n_out, 2) uint64 compressed output labels          (online #2)
+  BYE_  either side
+  ERR!  server -> client  UTF-8 error text
+
+A garbled model is single use (reusing its labels on a second input would
+leak the offsets R_p): the server drops every slot after one
+INPT round and refuses a second round on the same slots. The online traffic
+per inference is exactly input_size*k*16 B + n_out*k*16 B plus framing, the
+"single online round" of the reference's communication model
+(benchmarks/evaluation.ipynb:895-950).
+"""
+from __future__ import annotations
+
+import json
+import time
+from typing import Optional, Sequence
+
+import numpy as np
+
+from ..native import native
+from .channel import Channel, ChannelClosed, connect
+
+VERSION = 1
+
+
+class EvaluatorServer:
+    """Evaluator party: receives garbled models, evaluates online rounds on
+    the CPU oracle (`backend="cpu"`) or the HIP evaluator (`backend="hip"`)."""
+
+    def __init__(self, backend: str = "cpu", device: int = 0, nthreads: int = 0, tamper: bool = False):
+        assert backend in ("cpu", "hip")
+        self.backend, self.device, self.nthreads = backend, device, nthreads
+        self.tamper = tamper  # fault injection: flip one output bit (tests)
+        self._reset()
+
+    def _reset(self):
+        self.models: dict = {}
+        self.ev = None
+        self.batch = 1
+        self.rounds = 0
+
+    def serve(self, ch: Channel) -> None:
+        n = native()
+        try:
+            while True:
+                try:
+                    tag, flags, buf = ch.recv()
+                except ChannelClosed:
+                    return
+                try:
+                    if tag == b"HELO":
+                        hello = json.loads(buf.decode())
+                        if hello.get("version") != VERSION:
+                            raise ValueError(f"protocol version {hello.get('version')} != {VERSION}")
+                        self._reset()
+                        self.batch = int(hello.get("batch", 1))
+                        ch.send(b"HELO", json.dumps({"backend": self.backend, "device": self.device}).encode())
+                    elif tag == b"MODL":
+                        slot = flags
+                        if not 0 <= slot < self.batch:
+                            raise ValueError(f"slot {slot} out of range")
+                        m = n.GarbledModel.deserialize(bytes(buf))
+                        del buf
+                        if self.backend == "hip":
+                            from ..runtime import HipEvaluator
+
+                            if self.ev is None:
+                                self.ev = HipEvaluator(template=m, batch=self.batch, device=self.device)
+                            self.ev.load(slot, m)
+                            self.models[slot] = True
+                        else:
+                            self.models[slot] = m
+                        ch.send(b"ACK_")
+                    elif tag == b"INPT":
+                        ch.send(b"OUTP", self._round(flags, buf))
+                    elif tag == b"BYE_":
+                        return
+                    else:
+                        raise ValueError(f"unknown message {tag!r}")
+                except (ValueError, RuntimeError) as e:
+                    ch.send(b"ERR!", str(e).encode())
+        finally:
+            ch.close()
+
+    def _round(self, nb: int, buf: bytearray) -> bytes:
+        n = native()
+        if nb != self.batch or len(self.models) != self.batch:
+            raise ValueError(f"online round needs all {self.batch} slots garbled (have {sorted(self.models)})")
+        raw = np.frombuffer(buf, dtype=np.uint64)
+        per = raw.size // nb
+        outs = []
+        if self.backend == "hip":
+            ev = self.ev
+            k = ev._h.crt_size()
+            N = ev._h.input_size()
+            assert per == k * N * 2, "input size mismatch"
+            for b in range(nb):
+                ev.set_input_compressed(b, raw[b * per:(b + 1) * per].reshape(k, N, 2))
+            ev.upload_inputs_compressed()
+            ev.run()
+            ev.fetch_outputs()
+            outs = [ev.outputs_compressed(b) for b in range(nb)]
+        else:
+            for b in range(nb):
+                m = self.models[b]
+                k = len(m.crt)
+                N = int(np.prod(m.in_dims))
+                assert per == k * N * 2, "input size mismatch"
+                labels = n.decompress_labels(raw[b * per:(b + 1) * per].reshape(k, N, 2), list(m.crt))
+                out = n.cpu_evaluate(m, labels, self.nthreads)
+                outs.append(n.compress_labels(out))
+        self.models.clear()  # single use
+        self.rounds += 1
+        payload = np.concatenate([o.reshape(-1) for o in outs])
+        if self.tamper:
+            payload = payload.copy()
+            payload[0] ^= np.uint64(1)
+        return payload.tobytes()
+
+
+def serve_once(sock, backend: str = "cpu", device: int = 0, tamper: bool = False) -> None:
+    """Accept one client on a listening socket and serve it to completion."""
+    conn, _ = sock.accept()
+    EvaluatorServer(backend, device, tamper=tamper).serve(Channel(conn))
+
+
+class GarblerClient:
+    """Garbler party: owns the circuit, garbles fresh GCs (offline), encodes
+    inputs and decodes outputs (online)."""
+
+    def __init__(self, host: str, port: int, circuit, crt, mrs=None, batch: int = 1, max_modulus: int = 0,
+                 seed: Optional[bytes] = None, timeout: float = 600.0):
+        self.circuit, self.crt, self.mrs = circuit, crt, mrs
+        self.batch, self.max_modulus = batch, max_modulus
+        self._seed = seed
+        self._ctr = 0
+        self.ch = connect(host, port, timeout=timeout)
+        self.ch.send(b"HELO", json.dumps({"version": VERSION, "batch": batch}).encode())
+        _, _, buf = self.ch.recv(b"HELO")
+        self.server_info = json.loads(buf.decode())
+        self.gcs: list = []
+        self.stats = {"offline_bytes": 0, "online_bytes": 0, "garble_s": 0.0, "offline_s": 0.0, "online_s": []}
+
+    def _next_seed(self) -> Optional[bytes]:
+        if self._seed is None:
+            return None
+        import hashlib
+
+        self._ctr += 1
+        return hashlib.sha256(self._seed + self._ctr.to_bytes(8, "little")).digest()[:16]
+
+    def offline(self) -> None:
+        """Garble `batch` fresh circuits and ship them (offline phase)."""
+        from ..garbling import GarbledCircuit
+
+        t0 = time.perf_counter()
+        sent0 = self.ch.bytes_sent
+        self.gcs = []
+        for b in range(self.batch):
+            t = time.perf_counter()
+            gc = GarbledCircuit(self.circuit, self.crt, self.mrs, max_modulus=self.max_modulus, seed=self._next_seed())
+            self.stats["garble_s"] += time.perf_counter() - t
+            self.ch.send(b"MODL", gc.model.serialize(), flags=b)
+            self.ch.recv(b"ACK_")
+            gc.model = None  # the garbler keeps only encoder + decoder secrets
+            self.gcs.append(gc)
+        self.stats["offline_bytes"] += self.ch.bytes_sent - sent0
+        self.stats["offline_s"] += time.perf_counter() - t0
+
+    def infer(self, xs: Sequence) -> list:
+        """One online round for `batch` inputs -> decoded outputs."""
+        if len(self.gcs) != self.batch:
+            raise RuntimeError("no fresh garbled circuits: call offline() first (GCs are single use)")
+        assert len(xs) == self.batch
+        t0 = time.perf_counter()
+        b0, r0 = self.ch.bytes_sent, self.ch.bytes_recv
+        msg = np.concatenate([gc.garble_inputs_compressed(x).reshape(-1) for gc, x in zip(self.gcs, xs)])
+        self.ch.send(b"INPT", msg, flags=self.batch)
+        _, _, buf = self.ch.recv(b"OUTP")
+        raw = np.frombuffer(buf, dtype=np.uint64)
+        per = raw.size // self.batch
+        outs = []
+        for b, gc in enumerate(self.gcs):
+            k = len(gc.decoder.moduli)
+            outs.append(gc.decode_compressed(raw[b * per:(b + 1) * per].reshape(k, -1, 2)))
+        self.gcs = []
+        self.stats["online_bytes"] += (self.ch.bytes_sent - b0) + (self.ch.bytes_recv - r0)
+        self.stats["online_s"].append(time.perf_counter() - t0)
+        return outs
+
+    def close(self) -> None:
+        try:
+            self.ch.send(b"BYE_")
+        except OSError:
+            pass
+        self.ch.close()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()

@@ -81,6 +81,32 @@ class HipEvaluator:
 
         native().encode_into(gc.garbler, np.asarray(x, dtype=np.int64).reshape(-1), self._h, b)
 
+    def set_input_compressed(self, b: int, labels) -> None:
+        """Stage compressed input labels ((k, N, 2) uint64, GarbledCircuit.garble_inputs_compressed)."""
+        self._h.set_input_compressed(b, labels)
+
+    def encode_compressed_into(self, b: int, gc, x) -> None:
+        """In-process fast path, wire form: the garbler writes 16-B compressed labels into slot b."""
+        import numpy as np
+
+        native().encode_compressed_into(gc.garbler, np.asarray(x, dtype=np.int64).reshape(-1), self._h, b)
+
+    def upload_inputs_compressed(self, stream=None) -> None:
+        """H2D of the compressed slots and on-GPU decompression into the input activations."""
+        self._h.upload_inputs_compressed(_stream_handle(stream))
+
+    def fetch_outputs(self, stream=None) -> None:
+        """D2H of every slot's output labels (synchronizes `stream`)."""
+        self._h.fetch_outputs(_stream_handle(stream))
+
+    def outputs_compressed(self, b: int):
+        """Online message #2 of slot b in wire form: (k, n_out, 2) uint64 (after fetch_outputs)."""
+        return self._h.outputs_compressed(b)
+
+    def decode(self, b: int, gc):
+        """Decode slot b's fetched outputs with the garbler's decoder (IntegrityError on tampering)."""
+        return self._h.decode_into(b, gc.decoder)
+
     def upload_inputs(self, stream=None) -> None:
         """H2D of every staged slot (async on `stream`)."""
         self._h.upload_inputs(_stream_handle(stream))

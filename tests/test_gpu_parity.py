@@ -152,3 +152,28 @@ def test_staged_input_paths():
             np.testing.assert_array_equal(ar, ag)
     for g, x, o in zip(gcs, xs, got):
         np.testing.assert_array_equal(g.decode_outputs(o), g.plain_q_eval(x))
+
+
+def test_compressed_wire_paths():
+    """Compressed online messages (16 B per label) through the HIP evaluator."""
+    from dash_amd.models import build_circuit, quantized_inputs
+
+    c = build_circuit("MODEL_A")
+    xs = quantized_inputs("MODEL_A", 3)
+    gcs = [GarbledCircuit(c, 7, 100.0, seed=bytes([i + 20]) * 16) for i in range(3)]
+    ev = _hip([g.model for g in gcs])
+    ev.encode_compressed_into(0, gcs[0], xs[0])
+    for b in (1, 2):
+        ev.set_input_compressed(b, gcs[b].garble_inputs_compressed(xs[b]))
+    ev.upload_inputs_compressed()
+    ev.run()
+    ev.fetch_outputs()
+    for b, (g, x) in enumerate(zip(gcs, xs)):
+        ref = g.plain_q_eval(x)
+        np.testing.assert_array_equal(ev.decode(b, g), ref)
+        np.testing.assert_array_equal(g.decode_compressed(ev.outputs_compressed(b)), ref)
+    # a tampered output label must not decode
+    bad = ev.outputs_compressed(0).copy()
+    bad[0, 0, 0] ^= 1
+    with pytest.raises(d.IntegrityError):
+        gcs[0].decode_compressed(bad)
