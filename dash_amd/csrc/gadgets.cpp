@@ -116,7 +116,7 @@ void sign_garble_elem(const SignPlan& P, const LabelBank& R, const LabelBank& Z,
             const ModInfo& mo = mod_info(P.mrs[d]);
             garble_proj(in0[j], R.get(mi.p), mi, mrs_lab + static_cast<size_t>(W) * (j * t + d), R.get(mo.p), mo,
                         [&](int v) { return static_cast<i64>(lut[static_cast<size_t>(v) * t + d]); },
-                        approx + t * P.crt_prefix[j] + static_cast<i64>(d) * mi.p);
+                        approx + t * P.crt_prefix[j] + d, t);
         }
     }
     // Step 2: mixed-radix addition from the least significant digit
@@ -175,8 +175,8 @@ void sign_eval_elem(const SignPlan& P, const LabelBank& Z, const comp_t* const* 
     for (int j = 0; j < k; ++j) {
         const ModInfo& mi = mod_info(P.crt[j]);
         for (int d = 0; d < t; ++d)
-            eval_proj(in[j], mi, approx + t * P.crt_prefix[j] + static_cast<i64>(d) * mi.p, mod_info(P.mrs[d]),
-                      mrs_lab + static_cast<size_t>(W) * (j * t + d));
+            eval_proj(in[j], mi, approx + t * P.crt_prefix[j] + d, mod_info(P.mrs[d]),
+                      mrs_lab + static_cast<size_t>(W) * (j * t + d), t);
     }
     {
         const int m_last = P.mrs[t - 1];

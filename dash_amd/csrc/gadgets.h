@@ -47,7 +47,7 @@ ProjScratch& proj_scratch();
 // table[color(in0 + i*Rin)] = compress(out0 + f(i)*outR) + H(compress(in0 + i*Rin))
 template <class F>
 inline void garble_proj(const comp_t* in0, const comp_t* Rin, const ModInfo& mi, const comp_t* out0,
-                        const comp_t* outR, const ModInfo& mo, F&& f, u128* table) {
+                        const comp_t* outR, const ModInfo& mo, F&& f, u128* table, int stride = 1) {
     ProjScratch& s = proj_scratch();
     const int pin = mi.p, nin = mi.n;
     s.key.assign(in0, in0 + nin);
@@ -70,7 +70,7 @@ inline void garble_proj(const comp_t* in0, const comp_t* Rin, const ModInfo& mi,
             s.payc[c] = compress(s.tmp.data(), mo);
             s.have[c] = 1;
         }
-        table[s.colors[i]] = s.payc[c] + s.hc[i];
+        table[static_cast<i64>(s.colors[i]) * stride] = s.payc[c] + s.hc[i];
     }
 }
 
@@ -92,10 +92,11 @@ inline void garble_proj_mini(const comp_t* in0, const comp_t* Rin, const ModInfo
 
 inline int color_of(const comp_t* L, int p) { return static_cast<int>(static_cast<uint16_t>(L[0]) % static_cast<unsigned>(p)); }
 
-// out = decompress(T[color(in)] - H(compress(in)))
-inline void eval_proj(const comp_t* in, const ModInfo& mi, const u128* table, const ModInfo& mo, comp_t* out) {
+// out = decompress(T[color(in) * stride] - H(compress(in)))
+inline void eval_proj(const comp_t* in, const ModInfo& mi, const u128* table, const ModInfo& mo, comp_t* out,
+                      int stride = 1) {
     u128 h = hash(compress(in, mi));
-    decompress(table[color_of(in, mi.p)] - h, out, mo);
+    decompress(table[static_cast<i64>(color_of(in, mi.p)) * stride] - h, out, mo);
 }
 
 inline int16_t eval_proj_mini(const comp_t* in, const ModInfo& mi, const u128* entry) {

@@ -46,7 +46,7 @@ static inline dim3 grid_aes(int64_t n, int bs, int y, int z) {
 
 // ---------------------------------------------------------------------------
 // Phase A: approximate residues. grid (ceil(N/256), k, B)
-__global__ __launch_bounds__(512, 2) void k_sign_approx(SignArgs a, Act x, const ModC* mc, const uint32_t* te0,
+__global__ __launch_bounds__(512, 4) void k_sign_approx(SignArgs a, Act x, const ModC* mc, const uint32_t* te0,
                                                      const uint32_t* rk) {
     AES_PROLOGUE(te0, rk);
     const int j = blockIdx.y, b = blockIdx.z;
@@ -62,7 +62,7 @@ __global__ __launch_bounds__(512, 2) void k_sign_approx(SignArgs a, Act x, const
     u128 ent[8];
 #pragma unroll
     for (int d = 0; d < 8; ++d)
-        if (d < a.t) ent[d] = T[d * p + col];
+        if (d < a.t) ent[d] = T[col * a.t + d];
     const u128 C = compress_cm(L, N, m);
     const u128 H = aes_encrypt(aes, C);
     const int64_t bke = (static_cast<int64_t>(b) * a.crt.k + j) * N + e;
@@ -74,7 +74,7 @@ __global__ __launch_bounds__(512, 2) void k_sign_approx(SignArgs a, Act x, const
 #pragma unroll
     for (int d = 0; d < 8; ++d)
         if (d < a.t) out[static_cast<int64_t>(d) * N] = ent[d] - H;
-    for (int d = 8; d < a.t; ++d) out[static_cast<int64_t>(d) * N] = T[d * p + col] - H;
+    for (int d = 8; d < a.t; ++d) out[static_cast<int64_t>(d) * N] = T[col * a.t + d] - H;
     }
 }
 
@@ -85,7 +85,7 @@ __global__ __launch_bounds__(512, 2) void k_sign_approx(SignArgs a, Act x, const
 // fully parallel over (GC, digit, element), with paired AES.
 // grid (x, t, B): blockIdx.y = t-1 is digit 0, otherwise digit y+1.
 template <int MAXN>
-__global__ __launch_bounds__(512, 2) void k_sign_castsum(SignArgs a, const ModC* mc, const uint32_t* te0,
+__global__ __launch_bounds__(512, 4) void k_sign_castsum(SignArgs a, const ModC* mc, const uint32_t* te0,
                                                       const uint32_t* rk) {
     AES_PROLOGUE(te0, rk);
     const int b = blockIdx.z;
@@ -150,7 +150,7 @@ __global__ __launch_bounds__(512, 2) void k_sign_castsum(SignArgs a, const ModC*
 // only the carry's cast and the sum's cast2 projection remain on the
 // critical path (2 AES + 2 gathers). grid (x, 1, B)
 template <int MAXN>
-__global__ __launch_bounds__(512, 2) void k_sign_chain(SignArgs a, const ModC* mc, const uint32_t* te0,
+__global__ __launch_bounds__(512, 4) void k_sign_chain(SignArgs a, const ModC* mc, const uint32_t* te0,
                                                     const uint32_t* rk) {
     AES_PROLOGUE(te0, rk);
     const int b = blockIdx.z;
@@ -285,7 +285,7 @@ __global__ __launch_bounds__(256) void k_relu_mult(SignArgs a, Act x, Act y, con
 // ---------------------------------------------------------------------------
 // Rescale step 1+2 for one factor: hash the factor residue (optionally after
 // the upshift). grid (ceil(N/256), 1, B)
-__global__ __launch_bounds__(512, 2) void k_rescale_hash(Act x, int fi, int s, const int16_t* up, int up_stride,
+__global__ __launch_bounds__(512, 4) void k_rescale_hash(Act x, int fi, int s, const int16_t* up, int up_stride,
                                                       int add_up, int64_t N, u128* h0, uint16_t* col0,
                                                       const ModC* mc, const uint32_t* te0, const uint32_t* rk) {
     AES_PROLOGUE(te0, rk);
@@ -383,7 +383,7 @@ __global__ __launch_bounds__(256) void k_rescale_post(Act x, CrtInfo crt, int64_
 //            next sign gadget (phase A) in the same pass.
 // The downshift of iteration i and the upshift of i+1 collapse into one
 // delta = up - down; only the last iteration writes a downshifted result.
-__global__ __launch_bounds__(512, 2) void k_rescale_hash_sign(const u128* signP, const u128* du, int64_t N, u128* h0,
+__global__ __launch_bounds__(512, 4) void k_rescale_hash_sign(const u128* signP, const u128* du, int64_t N, u128* h0,
                                                            uint16_t* col0, const uint32_t* te0, const uint32_t* rk) {
     AES_PROLOGUE(te0, rk);
     const int b = blockIdx.z;
@@ -396,7 +396,7 @@ __global__ __launch_bounds__(512, 2) void k_rescale_hash_sign(const u128* signP,
 }
 
 // grid (ceil(N/256), k, B)
-__global__ __launch_bounds__(512, 2) void k_rescale_update_approx(RescaleArgs r, SignArgs a, Act x, const int16_t* delta,
+__global__ __launch_bounds__(512, 4) void k_rescale_update_approx(RescaleArgs r, SignArgs a, Act x, const int16_t* delta,
                                                                const u128* zh, const ModC* mc, const uint32_t* te0,
                                                                const uint32_t* rk) {
     AES_PROLOGUE(te0, rk);
@@ -417,7 +417,7 @@ __global__ __launch_bounds__(512, 2) void k_rescale_update_approx(RescaleArgs r,
         col = a.zcol[static_cast<int64_t>(b) * a.zc_stride + p];
 #pragma unroll
         for (int d = 0; d < 8; ++d)
-            if (d < a.t) ent[d] = TA[d * p + col];
+            if (d < a.t) ent[d] = TA[col * a.t + d];
     } else {
         const u128 Tt = r.trans[be * r.n_trans + static_cast<int64_t>(r.aidx[j]) * r.s + r.col0[be]];
         const u128 P = Tt - r.h0[be];
@@ -440,7 +440,7 @@ __global__ __launch_bounds__(512, 2) void k_rescale_update_approx(RescaleArgs r,
                 col = static_cast<uint32_t>(v);
 #pragma unroll
                 for (int d = 0; d < 8; ++d)
-                    if (d < a.t) ent[d] = TA[d * p + col];
+                    if (d < a.t) ent[d] = TA[col * a.t + d];
             }
         }
         H = aes_encrypt(aes, cf.finish());
@@ -449,7 +449,7 @@ __global__ __launch_bounds__(512, 2) void k_rescale_update_approx(RescaleArgs r,
 #pragma unroll
     for (int d = 0; d < 8; ++d)
         if (d < a.t) out[static_cast<int64_t>(d) * N] = ent[d] - H;
-    for (int d = 8; d < a.t; ++d) out[static_cast<int64_t>(d) * N] = TA[d * p + col] - H;
+    for (int d = 8; d < a.t; ++d) out[static_cast<int64_t>(d) * N] = TA[col * a.t + d] - H;
     }
 }
 
@@ -519,7 +519,7 @@ __global__ __launch_bounds__(256) void k_base_ext(BEArgs a, Act x, const ModC* m
 
 // ---------------------------------------------------------------------------
 // Generic projection layer (test-only Projection). grid (ceil(N/256), k, B)
-__global__ __launch_bounds__(512, 2) void k_proj(ProjArgs a, Act x, Act y, const ModC* mc, const uint32_t* te0,
+__global__ __launch_bounds__(512, 4) void k_proj(ProjArgs a, Act x, Act y, const ModC* mc, const uint32_t* te0,
                                               const uint32_t* rk) {
     AES_PROLOGUE(te0, rk);
     const int j = blockIdx.y, b = blockIdx.z;
@@ -540,7 +540,7 @@ __global__ __launch_bounds__(512, 2) void k_proj(ProjArgs a, Act x, Act y, const
 
 // Generalized half-gate product of pairs (2e, 2e+1), and the mixed-modulus
 // variant (second operand first projected to Z_q). grid (ceil(No/256), k, B)
-__global__ __launch_bounds__(512, 2) void k_mult(MultArgs a, Act x, Act y, const ModC* mc, const uint32_t* te0,
+__global__ __launch_bounds__(512, 4) void k_mult(MultArgs a, Act x, Act y, const ModC* mc, const uint32_t* te0,
                                               const uint32_t* rk) {
     AES_PROLOGUE(te0, rk);
     const int j = blockIdx.y, b = blockIdx.z;
@@ -603,7 +603,10 @@ void launch_sign_approx(const SignArgs& a, const Act& x, const ModC* mc, const A
 void launch_sign_chain(const SignArgs& a, int maxn, const ModC* mc, const AesGlobals& g, hipStream_t st) {
     const dim3 gs = grid_aes(a.N, 512, a.t, a.B);
     const dim3 gr = grid_aes(a.N, 512, 1, a.B);
-    if (maxn <= 32) {
+    if (maxn <= 24) {
+        hipLaunchKernelGGL(k_sign_castsum<24>, gs, dim3(512), kAesLds, st, a, mc, g.te0, g.rk);
+        hipLaunchKernelGGL(k_sign_chain<24>, gr, dim3(512), kAesLds, st, a, mc, g.te0, g.rk);
+    } else if (maxn <= 32) {
         hipLaunchKernelGGL(k_sign_castsum<32>, gs, dim3(512), kAesLds, st, a, mc, g.te0, g.rk);
         hipLaunchKernelGGL(k_sign_chain<32>, gr, dim3(512), kAesLds, st, a, mc, g.te0, g.rk);
     } else {

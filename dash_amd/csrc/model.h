@@ -61,7 +61,7 @@ struct GLayer {
 };
 
 struct ModelHeader {
-    int version = 1;
+    int version = 2;  // 2: approx tables interleaved [color][digit]
     std::vector<int> crt, mrs;
     std::vector<i64> in_dims, out_dims;
     std::vector<int> out_moduli;  // moduli of the output residues

@@ -123,7 +123,7 @@ GarbledModel GarbledModel::deserialize(const std::string& blob) {
     DASH_CHECK(std::memcmp(mg, kModelMagic, 8) == 0, "not a garbled model blob");
     GarbledModel m;
     m.h.version = static_cast<int>(r.u32());
-    DASH_CHECK(m.h.version == 1, "unsupported garbled model version");
+    DASH_CHECK(m.h.version == 2, "unsupported garbled model version (expected 2)");
     m.h.crt = r.ivec32();
     m.h.mrs = r.ivec32();
     m.h.in_dims = r.ivec();

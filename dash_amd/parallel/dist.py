@@ -1,0 +1,183 @@
+"""Batch data parallelism over GPUs (one process per GPU, RCCL over xGMI).
+
+The reference is single-device (DP over inferences is "No").
+Garbled inference has no cross-inference dependency, so the natural MI355X
+scale-out is batch DP: every rank garbles and evaluates its own single-use
+GCs with all tables resident in its own HBM, and the only collectives are
+
+* a broadcast of the public model from rank 0 (weights are public to the
+  evaluator in the DASH setting), and
+* one all-gather of decoded logits per batch (10 int64 per inference),
+
+both tiny, so scaling is bound by per-GPU throughput, not by xGMI.
+Backend: ``nccl`` (= RCCL on ROCm) when a GPU is present, ``gloo`` otherwise
+(CPU tests, world_size > 1 on one host).
+"""
+from __future__ import annotations
+
+import os
+from dataclasses import dataclass
+from typing import Optional, Sequence
+
+import numpy as np
+
+
+@dataclass
+class DistContext:
+    rank: int = 0
+    world: int = 1
+    local_rank: int = 0
+    backend: str = "none"
+    device: Optional[int] = None
+
+    @property
+    def distributed(self) -> bool:
+        return self.world > 1
+
+    @property
+    def is_main(self) -> bool:
+        return self.rank == 0
+
+
+def init_distributed(backend: Optional[str] = None, use_gpu: Optional[bool] = None) -> DistContext:
+    """Initialise torch.distributed from the torchrun environment (RANK,
+    WORLD_SIZE, LOCAL_RANK, MASTER_ADDR/PORT). Single process -> no-op."""
+    import torch
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if use_gpu is None:
+        use_gpu = torch.cuda.is_available()
+    dev = None
+    if use_gpu:
+        torch.cuda.set_device(local)
+        dev = local
+    if world <= 1:
+        return DistContext(rank, 1, local, "none", dev)
+    import torch.distributed as dist
+
+    if backend is None:
+        backend = "nccl" if use_gpu else "gloo"
+    if not dist.is_initialized():
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group(backend)
+    return DistContext(dist.get_rank(), dist.get_world_size(), local, backend, dev)
+
+
+def shutdown(ctx: DistContext) -> None:
+    if ctx.distributed:
+        import torch.distributed as dist
+
+        if dist.is_initialized():
+            dist.destroy_process_group()
+
+
+def broadcast_object(ctx: DistContext, obj=None, src: int = 0):
+    """Broadcast a picklable object (e.g. the public Circuit) from `src`.
+    Objects only ever come from ranks of the same job, never from files."""
+    if not ctx.distributed:
+        return obj
+    import torch.distributed as dist
+
+    box = [obj if ctx.rank == src else None]
+    dist.broadcast_object_list(box, src=src)
+    return box[0]
+
+
+def _tensor_device(ctx: DistContext):
+    import torch
+
+    return torch.device("cuda", ctx.device) if ctx.backend == "nccl" else torch.device("cpu")
+
+
+def all_gather_array(ctx: DistContext, a: np.ndarray) -> np.ndarray:
+    """All-gather equally shaped int64 arrays -> stacked [world, ...]."""
+    a = np.ascontiguousarray(a, dtype=np.int64)
+    if not ctx.distributed:
+        return a[None]
+    import torch
+    import torch.distributed as dist
+
+    t = torch.from_numpy(a).to(_tensor_device(ctx))
+    out = [torch.empty_like(t) for _ in range(ctx.world)]
+    dist.all_gather(out, t)
+    return np.stack([o.cpu().numpy() for o in out])
+
+
+def all_reduce_max(ctx: DistContext, v: float) -> float:
+    if not ctx.distributed:
+        return float(v)
+    import torch
+    import torch.distributed as dist
+
+    t = torch.tensor([float(v)], dtype=torch.float64, device=_tensor_device(ctx))
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def barrier(ctx: DistContext) -> None:
+    if ctx.distributed:
+        import torch.distributed as dist
+
+        if ctx.backend == "nccl":
+            dist.barrier(device_ids=[ctx.device])
+        else:
+            dist.barrier()
+
+
+def shard(n: int, ctx: DistContext) -> range:
+    """Contiguous shard of n items for this rank (sizes differ by at most 1)."""
+    base, rem = divmod(n, ctx.world)
+    start = ctx.rank * base + min(ctx.rank, rem)
+    return range(start, start + base + (1 if ctx.rank < rem else 0))
+
+
+class BatchDataParallel:
+    """Data-parallel garbled inference: each rank owns `per_rank` fresh GCs per
+    round and evaluates them on its GPU (`backend="hip"`) or on the CPU
+    oracle (`backend="cpu"`); outputs are all-gathered in global order.
+
+    Every round garbles new circuits (GCs are single use)."""
+
+    def __init__(self, ctx: DistContext, circuit, crt, mrs=None, per_rank: int = 1, backend: str = "hip",
+                 max_modulus: int = 0, seed: Optional[bytes] = None):
+        self.ctx, self.circuit, self.crt, self.mrs = ctx, circuit, crt, mrs
+        self.per_rank, self.backend, self.max_modulus = per_rank, backend, max_modulus
+        self.seed = seed
+        self.round = 0
+        self.ev = None
+
+    def _seed(self, b: int) -> Optional[bytes]:
+        if self.seed is None:
+            return None
+        import hashlib
+
+        return hashlib.sha256(self.seed + f"/{self.ctx.rank}/{self.round}/{b}".encode()).digest()[:16]
+
+    def infer(self, inputs: Sequence) -> np.ndarray:
+        """inputs: exactly world * per_rank quantized inputs (global batch) -> [global, n_out]."""
+        from ..garbling import GarbledCircuit
+
+        ctx = self.ctx
+        assert len(inputs) == ctx.world * self.per_rank, "global batch must be world * per_rank"
+        mine = inputs[ctx.rank * self.per_rank:(ctx.rank + 1) * self.per_rank]
+        gcs = [GarbledCircuit(self.circuit, self.crt, self.mrs, max_modulus=self.max_modulus, seed=self._seed(b))
+               for b in range(self.per_rank)]
+        self.round += 1
+        if self.backend == "hip":
+            from ..runtime import HipEvaluator
+
+            if self.ev is None:
+                self.ev = HipEvaluator(template=gcs[0].model, batch=self.per_rank, device=ctx.device or 0)
+            for b, gc in enumerate(gcs):
+                self.ev.load(b, gc.model)
+                gc.model = None
+                self.ev.encode_compressed_into(b, gc, mine[b])
+            self.ev.upload_inputs_compressed()
+            self.ev.run()
+            self.ev.fetch_outputs()
+            outs = np.stack([self.ev.decode(b, gc) for b, gc in enumerate(gcs)])
+        else:
+            outs = np.stack([gc.decode_outputs(gc.cpu_evaluate(gc.garble_inputs(x))) for gc, x in zip(gcs, mine)])
+        return all_gather_array(ctx, outs).reshape(ctx.world * self.per_rank, -1)

@@ -1,0 +1,58 @@
+"""Batch-DP over torch.distributed with the gloo backend, world_size 2 (CPU).
+The same code path runs with nccl (RCCL) on GPUs (bench.py, --gpus N)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.multiprocessing as tmp
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, q):
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
+                      MASTER_PORT=str(port))
+    from dash_amd.garbling import GarbledCircuit
+    from dash_amd.models import build_circuit, quantized_inputs
+    from dash_amd.parallel import BatchDataParallel, broadcast_object, init_distributed, shard, shutdown
+
+    ctx = init_distributed(use_gpu=False)
+    circuit = broadcast_object(ctx, build_circuit("MODEL_A") if ctx.rank == 0 else None)
+    xs = broadcast_object(ctx, quantized_inputs("MODEL_A", world * 2) if ctx.rank == 0 else None)
+    dp = BatchDataParallel(ctx, circuit, 7, 100.0, per_rank=2, backend="cpu", seed=b"dp-test")
+    out = dp.infer(xs)
+    ref = np.stack([GarbledCircuit(circuit, 7, 100.0, seed=bytes(16), garble_me=False).plain_q_eval(x) for x in xs])
+    q.put((rank, bool(np.array_equal(out, ref)), list(shard(5, ctx))))
+    shutdown(ctx)
+
+
+@pytest.mark.parametrize("world", [2])
+def test_batch_dp_gloo(world):
+    ctx = tmp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=300) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert all(ok for _, ok, _ in res)
+    # shards of 5 items over 2 ranks: [0,1,2] and [3,4]
+    assert res[0][2] == [0, 1, 2] and res[1][2] == [3, 4]
+
+
+def test_single_process_context():
+    from dash_amd.parallel import all_gather_array, init_distributed
+
+    ctx = init_distributed(use_gpu=False)
+    assert ctx.world == 1 and not ctx.distributed
+    np.testing.assert_array_equal(all_gather_array(ctx, np.arange(3)), [[0, 1, 2]])
