@@ -265,6 +265,7 @@ PYBIND11_MODULE(_dash_native, m) {
             }
             return std::make_shared<GarbledModel>(std::move(gm));
         }, py::arg("layers"), py::arg("in_dims"), py::arg("nthreads") = 0)
+        .def("layer_ms", [](const Garbler& g) { return g.layer_ms(); })
         .def("encode", [](const Garbler& g, py::array_t<i64, py::array::c_style | py::array::forcecast> x) {
             std::vector<i64> v(x.data(), x.data() + x.size());
             return labels_to_py(g.encode(v));
@@ -327,6 +328,16 @@ PYBIND11_MODULE(_dash_native, m) {
             out = cpu_evaluate(*gm, in, nthreads);
         }
         return labels_to_py(out);
+    }, py::arg("model"), py::arg("labels"), py::arg("nthreads") = 0);
+    m.def("cpu_evaluate_timed", [](std::shared_ptr<GarbledModel> gm, const py::list& labels, int nthreads) {
+        CrtLabels in = labels_from_py(labels);
+        CrtLabels out;
+        std::vector<double> ms;
+        {
+            py::gil_scoped_release rel;
+            out = cpu_evaluate(*gm, in, nthreads, &ms);
+        }
+        return py::make_tuple(labels_to_py(out), ms);
     }, py::arg("model"), py::arg("labels"), py::arg("nthreads") = 0);
 
     // ---------------------------------------------------------------- ONNX

@@ -1,6 +1,10 @@
 // dash_amd native core implementation (see core.h).
 #include "core.h"
 
+#include <pthread.h>
+#include <sched.h>
+#include <sys/mman.h>
+
 #include <wmmintrin.h>
 
 namespace dash {
@@ -54,6 +58,28 @@ const ModTable& mod_table() {
     return t;
 }
 }  // namespace
+
+void* big_alloc(size_t bytes, bool* zeroed) {
+    if (bytes >= kBigAlloc) {
+        void* p = mmap(nullptr, bytes, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+        if (p == MAP_FAILED) throw std::bad_alloc();
+        madvise(p, bytes, MADV_HUGEPAGE);
+        if (zeroed) *zeroed = true;
+        return p;
+    }
+    void* p = std::aligned_alloc(64, (bytes + 63) & ~size_t(63));
+    if (!p) throw std::bad_alloc();
+    if (zeroed) *zeroed = false;
+    return p;
+}
+
+void big_free(void* p, size_t bytes) {
+    if (!p) return;
+    if (bytes >= kBigAlloc)
+        munmap(p, bytes);
+    else
+        std::free(p);
+}
 
 const ModInfo& mod_info(int p) {
     DASH_CHECK(p >= 2 && p < kMaxMod, "modulus out of supported range [2, 4096)");
@@ -121,7 +147,36 @@ namespace {
 class Pool {
    public:
     explicit Pool(int n) : nthreads_(n) {
-        for (int i = 1; i < n; ++i) workers_.emplace_back([this, i] { loop(i); });
+        const int base = std::max(0, sched_getcpu());  // the caller (thread 0) keeps its CPU
+        for (int i = 1; i < n; ++i)
+            workers_.emplace_back([this, i, base] {
+                spread(base + i);
+                loop(i);
+            });
+    }
+    // Move worker i onto the i-th allowed CPU once, then restore the full mask.
+    // Some VM guests (observed: firecracker microVMs) never load-balance new
+    // threads away from their parent's CPU, so an unpinned pool ran all its
+    // workers on one core. The mask is restored, so the OS may still migrate.
+    static void spread(int i) {
+        cpu_set_t all;
+        CPU_ZERO(&all);
+        if (sched_getaffinity(0, sizeof(all), &all) != 0) return;
+        const int cnt = CPU_COUNT(&all);
+        if (cnt <= 1) return;
+        int want = i % cnt, seen = 0, cpu = -1;  // i counts allowed CPUs from the caller's
+        for (int c = 0; c < CPU_SETSIZE; ++c)
+            if (CPU_ISSET(c, &all) && seen++ == want) {
+                cpu = c;
+                break;
+            }
+        if (cpu < 0) return;
+        cpu_set_t one;
+        CPU_ZERO(&one);
+        CPU_SET(cpu, &one);
+        if (pthread_setaffinity_np(pthread_self(), sizeof(one), &one) != 0) return;
+        sched_yield();
+        pthread_setaffinity_np(pthread_self(), sizeof(all), &all);
     }
     ~Pool() {
         {

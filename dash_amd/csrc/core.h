@@ -274,6 +274,28 @@ inline size_t dtype_size(DType d) {
     return 1;
 }
 
+// Large host buffers: anonymous mmap (already zero) advised to use 2 MiB
+// transparent huge pages. In a VM every 4 KiB first-touch fault is an exit
+// that serializes the worker threads; huge pages cut the faults 512x so the
+// garbler and the host evaluator scale with threads.
+void* big_alloc(size_t bytes, bool* zeroed);
+void big_free(void* p, size_t bytes);
+constexpr size_t kBigAlloc = size_t(1) << 20;
+
+template <class T>
+struct BigAllocator {
+    using value_type = T;
+    BigAllocator() = default;
+    template <class U>
+    BigAllocator(const BigAllocator<U>&) {}
+    T* allocate(size_t n) { return static_cast<T*>(big_alloc(n * sizeof(T), nullptr)); }
+    void deallocate(T* p, size_t n) { big_free(p, n * sizeof(T)); }
+    template <class U>
+    bool operator==(const BigAllocator<U>&) const { return true; }
+    template <class U>
+    bool operator!=(const BigAllocator<U>&) const { return false; }
+};
+
 struct Array {
     DType dtype = DType::u8;
     std::vector<i64> shape;
@@ -287,10 +309,10 @@ struct Array {
         nbytes = cnt * dtype_size(dt);
         size_t alloc = (nbytes + 63) & ~size_t(63);
         if (alloc == 0) alloc = 64;
-        uint8_t* p = static_cast<uint8_t*>(std::aligned_alloc(64, alloc));
-        if (!p) throw std::bad_alloc();
-        std::memset(p, 0, alloc);
-        buf = std::shared_ptr<uint8_t>(p, [](uint8_t* q) { std::free(q); });
+        bool zeroed = false;
+        uint8_t* p = static_cast<uint8_t*>(big_alloc(alloc, &zeroed));
+        if (!zeroed) std::memset(p, 0, alloc);
+        buf = std::shared_ptr<uint8_t>(p, [alloc](uint8_t* q) { big_free(q, alloc); });
     }
     size_t count() const { return nbytes / dtype_size(dtype); }
     template <typename T>
@@ -307,7 +329,7 @@ struct Labels {
     int p = 0;
     int n = 0;
     i64 N = 0;
-    std::vector<comp_t> c;
+    std::vector<comp_t, BigAllocator<comp_t>> c;
     Labels() = default;
     Labels(int p_, i64 N_) : p(p_), n(nr_comps(p_)), N(N_), c(static_cast<size_t>(N_) * nr_comps(p_), 0) {}
     comp_t* at(i64 i) { return c.data() + i * n; }

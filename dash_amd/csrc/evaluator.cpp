@@ -1,5 +1,6 @@
 // Host (oracle) evaluator and decoder. Bit-exact with the HIP evaluator; the
 // CPU path of the reference (gci.h:345-380 + every GarbledX::cpu_evaluate).
+#include <chrono>
 #include "layers.h"
 
 namespace dash {
@@ -36,29 +37,30 @@ size_t GarbledModel::total_bytes() const {
 
 namespace {
 
+struct ReluTabs {
+    const Array *ap, *c1, *c2, *sg, *ga, *ea;
+    ReluTabs(const GLayer& g, const std::string& pre)
+        : ap(&g.arr(pre + "s.approx")), c1(&g.arr(pre + "s.cast1")), c2(&g.arr(pre + "s.cast2")),
+          sg(&g.arr(pre + "s.sign")), ga(&g.arr(pre + "mm.g")), ea(&g.arr(pre + "mm.e")) {}
+};
+
 void relu_eval_elem(const SignPlan& sp, const LabelBank& Z, const std::vector<int>& crt,
-                    const std::vector<i64>& prefix, const comp_t* const* x, const GLayer& g, const std::string& pre,
-                    i64 e, comp_t* const* out) {
+                    const std::vector<i64>& prefix, const comp_t* const* x, const ReluTabs& T, i64 e,
+                    comp_t* const* out) {
     const int k = static_cast<int>(crt.size());
-    const Array& ap = g.arr(pre + "s.approx");
-    const Array& c1 = g.arr(pre + "s.cast1");
-    const Array& c2 = g.arr(pre + "s.cast2");
-    const Array& sg = g.arr(pre + "s.sign");
-    const Array& ga = g.arr(pre + "mm.g");
-    const Array& ea = g.arr(pre + "mm.e");
     comp_t sig[128];
     comp_t* outs[1] = {sig};
-    sign_eval_elem(sp, Z, x, ap.ptr<u128>() + e * ap.shape[1], c1.ptr<u128>() + e * c1.shape[1],
-                   c2.ptr<u128>() + e * c2.shape[1], sg.ptr<u128>() + e * sg.shape[1], outs);
+    sign_eval_elem(sp, Z, x, T.ap->ptr<u128>() + e * T.ap->shape[1], T.c1->ptr<u128>() + e * T.c1->shape[1],
+                   T.c2->ptr<u128>() + e * T.c2->shape[1], T.sg->ptr<u128>() + e * T.sg->shape[1], outs);
     const ModInfo& m2 = mod_info(2);
     for (int j = 0; j < k; ++j)
-        mixed_mult_eval(x[j], mod_info(crt[j]), sig, m2, ga.ptr<u128>() + e * ga.shape[1] + prefix[j],
-                        ea.ptr<u128>() + (e * k + j) * 3, out[j]);
+        mixed_mult_eval(x[j], mod_info(crt[j]), sig, m2, T.ga->ptr<u128>() + e * T.ga->shape[1] + prefix[j],
+                        T.ea->ptr<u128>() + (e * k + j) * 3, out[j]);
 }
 
 }  // namespace
 
-CrtLabels cpu_evaluate(const GarbledModel& m, const CrtLabels& inputs, int nt) {
+CrtLabels cpu_evaluate(const GarbledModel& m, const CrtLabels& inputs, int nt, std::vector<double>* layer_ms) {
     const std::vector<int>& crt = m.h.crt;
     const int k = static_cast<int>(crt.size());
     DASH_CHECK(static_cast<int>(inputs.size()) == k, "input residue count mismatch");
@@ -82,7 +84,9 @@ CrtLabels cpu_evaluate(const GarbledModel& m, const CrtLabels& inputs, int nt) {
         return it->second.ptr<comp_t>();
     };
 
+    if (layer_ms) layer_ms->assign(m.layers.size(), 0.0);
     for (size_t li = 0; li < m.layers.size(); ++li) {
+        const auto t_layer = std::chrono::steady_clock::now();
         const GLayer& g = m.layers[li];
         const i64 Nin = cur[0].N;
         switch (g.kind) {
@@ -175,6 +179,7 @@ CrtLabels cpu_evaluate(const GarbledModel& m, const CrtLabels& inputs, int nt) {
             }
             case K_RELU: {
                 SignPlan sp(crt, m.h.mrs, {2}, 0, 1);
+                const ReluTabs T(g, "");
                 CrtLabels nxt;
                 for (int j = 0; j < k; ++j) nxt.emplace_back(crt[j], Nin);
                 parallel_for(Nin, [&](i64 b0, i64 b1) {
@@ -185,7 +190,7 @@ CrtLabels cpu_evaluate(const GarbledModel& m, const CrtLabels& inputs, int nt) {
                             x[j] = cur[j].at(e);
                             y[j] = nxt[j].at(e);
                         }
-                        relu_eval_elem(sp, Z, crt, prefix, x.data(), g, "", e, y.data());
+                        relu_eval_elem(sp, Z, crt, prefix, x.data(), T, e, y.data());
                     }
                 }, nt);
                 cur = std::move(nxt);
@@ -289,6 +294,7 @@ CrtLabels cpu_evaluate(const GarbledModel& m, const CrtLabels& inputs, int nt) {
                     const std::string pre = arr_name("lv", static_cast<int>(lv), ".");
                     std::vector<Labels> nv;
                     for (int j = 0; j < k; ++j) nv.emplace_back(crt[j], Nout * cnt1);
+                    const ReluTabs T(g, pre);
                     parallel_for(Nout * ops, [&](i64 b0, i64 b1) {
                         std::vector<std::vector<comp_t>> diff(k);
                         std::vector<const comp_t*> x(k);
@@ -303,7 +309,7 @@ CrtLabels cpu_evaluate(const GarbledModel& m, const CrtLabels& inputs, int nt) {
                                 x[j] = diff[j].data();
                                 y[j] = nv[j].at(o * cnt1 + q);
                             }
-                            relu_eval_elem(sp, Z, crt, prefix, x.data(), g, pre, e, y.data());
+                            relu_eval_elem(sp, Z, crt, prefix, x.data(), T, e, y.data());
                             for (int j = 0; j < k; ++j) lab_add(y[j], vals[j].at(o * cnt + 2 * q), vals[j].n, vals[j].p);
                         }
                     }, nt);
@@ -418,6 +424,8 @@ CrtLabels cpu_evaluate(const GarbledModel& m, const CrtLabels& inputs, int nt) {
                 throw std::runtime_error("dash: cannot evaluate layer kind " + std::to_string(g.kind));
         }
         if (keep[li + 1]) saved[li + 1] = cur;
+        if (layer_ms)
+            (*layer_ms)[li] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_layer).count();
     }
     return cur;
 }

@@ -8,6 +8,8 @@
 // decoding information of garbled_circuit_interface.h:386-415. Work is
 // parallel over elements with per-element PRG streams, so the result does not
 // depend on the thread count.
+#include <chrono>
+
 #include "layers.h"
 
 namespace dash {
@@ -354,7 +356,9 @@ GarbledModel Garbler::garble(const std::vector<LayerSpec>& layers, const std::ve
         sum_crt += crt_[j];
     }
 
+    layer_ms_.assign(layers.size(), 0.0);
     for (size_t li = 0; li < layers.size(); ++li) {
+        const auto t_layer = std::chrono::steady_clock::now();
         const LayerSpec& spec = layers[li];
         const u64 L = li + 1;
         GLayer g;
@@ -793,6 +797,7 @@ GarbledModel Garbler::garble(const std::vector<LayerSpec>& layers, const std::ve
         }
         if (keep[li + 1]) saved[li + 1] = cur;
         m.layers.push_back(std::move(g));
+        layer_ms_[li] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_layer).count();
     }
 
     // Decoding information (reference gci.h:386-415)

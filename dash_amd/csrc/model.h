@@ -116,6 +116,8 @@ class Garbler {
     const LabelBank& offsets() const { return R_; }
     const LabelBank& zeros() const { return Z_; }
     const CrtLabels& input_base() const { return in_base_; }
+    // per-layer wall time of the last garble() (reference: BENCHMARK timers, garbled_circuit.h:111-116)
+    const std::vector<double>& layer_ms() const { return layer_ms_; }
 
    private:
     std::vector<int> crt_, mrs_;
@@ -125,10 +127,12 @@ class Garbler {
     LabelBank R_, Z_;
     CrtLabels in_base_;
     Decoder dec_;
+    std::vector<double> layer_ms_;
 };
 
 // Host (oracle) evaluator: bit-exact reference for the HIP evaluator.
-CrtLabels cpu_evaluate(const GarbledModel& m, const CrtLabels& inputs, int nthreads = 0);
+CrtLabels cpu_evaluate(const GarbledModel& m, const CrtLabels& inputs, int nthreads = 0,
+                       std::vector<double>* layer_ms = nullptr);
 
 // Wire-form helpers: compressed labels [k][N] <-> CrtLabels
 std::vector<u128> compress_labels(const CrtLabels& L, int nthreads = 0);

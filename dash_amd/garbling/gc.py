@@ -79,6 +79,15 @@ class GarbledCircuit:
         """Decode online message #2 in wire form ((k, n_out, 2) uint64)."""
         return np.asarray(self.decoder.decode_compressed(labels), dtype=np.int64)
 
+    def garbling_layer_ms(self) -> list:
+        """Per-layer garbling wall time (ms) of the last garble()."""
+        return list(self.garbler.layer_ms())
+
+    def cpu_evaluate_timed(self, labels: Labels, nr_threads: int = 0):
+        """(output labels, per-layer evaluation ms) — the reference's BENCHMARK timers."""
+        out, ms = self._n.cpu_evaluate_timed(self.model, labels, nr_threads)
+        return out, list(ms)
+
     def cpu_evaluate(self, labels: Labels, nr_threads: int = 0) -> Labels:
         return self._n.cpu_evaluate(self.model, labels, nr_threads)
 

@@ -64,8 +64,9 @@ class Circuit:
     def compute_q_acc(self, x, q_x, q_constant: float, error_bound: float = 1.0) -> float:
         out = self.plain_eval(x)
         rec = self.plain_q_eval(q_x).astype(np.float32) * q_constant
-        rel = np.abs(out - rec) / np.abs(out)
-        return float(np.mean(rel < error_bound))
+        with np.errstate(divide="ignore", invalid="ignore"):
+            rel = np.abs(out - rec) / np.abs(out)
+        return float(np.mean(np.where(np.isfinite(rel), rel, np.where(out == rec, 0.0, np.inf)) < error_bound))
 
     # ---------------------------------------------------------- ranges / CRT
     def reset_ranges(self):
