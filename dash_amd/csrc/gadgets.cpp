@@ -7,6 +7,10 @@ ProjScratch& proj_scratch() {
     thread_local ProjScratch s;
     return s;
 }
+ProjKeys& proj_keys_scratch() {
+    thread_local ProjKeys k;
+    return k;
+}
 
 namespace {
 struct LabelScratch {
@@ -109,14 +113,16 @@ void sign_garble_elem(const SignPlan& P, const LabelBank& R, const LabelBank& Z,
     for (int j = 0; j < k; ++j)
         for (int d = 0; d < t; ++d) draw(prg, stream, ctr, P.mrs[d], mrs_lab + static_cast<size_t>(W) * (j * t + d));
     // Step 1: approximate residues in mixed radix
+    ProjKeys& K = proj_keys_scratch();
     for (int j = 0; j < k; ++j) {
         const ModInfo& mi = mod_info(P.crt[j]);
         const auto& lut = P.lookup[j];
+        proj_keys(in0[j], R.get(mi.p), mi, K);
         for (int d = 0; d < t; ++d) {
             const ModInfo& mo = mod_info(P.mrs[d]);
-            garble_proj(in0[j], R.get(mi.p), mi, mrs_lab + static_cast<size_t>(W) * (j * t + d), R.get(mo.p), mo,
-                        [&](int v) { return static_cast<i64>(lut[static_cast<size_t>(v) * t + d]); },
-                        approx + t * P.crt_prefix[j] + d, t);
+            garble_proj_keys(K, mrs_lab + static_cast<size_t>(W) * (j * t + d), R.get(mo.p), mo,
+                             [&](int v) { return static_cast<i64>(lut[static_cast<size_t>(v) * t + d]); },
+                             approx + t * P.crt_prefix[j] + d, t);
         }
     }
     // Step 2: mixed-radix addition from the least significant digit

@@ -44,22 +44,34 @@ struct ProjScratch {
 };
 ProjScratch& proj_scratch();
 
-// table[color(in0 + i*Rin)] = compress(out0 + f(i)*outR) + H(compress(in0 + i*Rin))
-template <class F>
-inline void garble_proj(const comp_t* in0, const comp_t* Rin, const ModInfo& mi, const comp_t* out0,
-                        const comp_t* outR, const ModInfo& mo, F&& f, u128* table, int stride = 1) {
-    ProjScratch& s = proj_scratch();
+// Colors and hashes of the p keys in0 + i*Rin of one input label; shared by
+// every projection of that label (the approx step projects one residue label
+// into all t MRS digits: one key schedule instead of t).
+struct ProjKeys {
+    std::vector<comp_t> key;
+    std::vector<u128> kc, hc;
+    std::vector<int> colors;
+};
+inline void proj_keys(const comp_t* in0, const comp_t* Rin, const ModInfo& mi, ProjKeys& K) {
     const int pin = mi.p, nin = mi.n;
-    s.key.assign(in0, in0 + nin);
-    s.kc.resize(pin);
-    s.hc.resize(pin);
-    s.colors.resize(pin);
+    K.key.assign(in0, in0 + nin);
+    K.kc.resize(pin);
+    K.hc.resize(pin);
+    K.colors.resize(pin);
     for (int i = 0; i < pin; ++i) {
-        s.kc[i] = compress(s.key.data(), mi);
-        s.colors[i] = s.key[0];
-        lab_add(s.key.data(), Rin, nin, pin);
+        K.kc[i] = compress(K.key.data(), mi);
+        K.colors[i] = K.key[0];
+        lab_add(K.key.data(), Rin, nin, pin);
     }
-    hash_batch(s.kc.data(), s.hc.data(), pin);
+    hash_batch(K.kc.data(), K.hc.data(), pin);
+}
+
+// table[color(in0 + i*Rin) * stride] = compress(out0 + f(i)*outR) + H(compress(in0 + i*Rin))
+template <class F>
+inline void garble_proj_keys(const ProjKeys& K, const comp_t* out0, const comp_t* outR, const ModInfo& mo, F&& f,
+                             u128* table, int stride = 1) {
+    ProjScratch& s = proj_scratch();
+    const int pin = static_cast<int>(K.hc.size());
     s.payc.resize(mo.p);
     s.have.assign(mo.p, 0);
     s.tmp.resize(mo.n);
@@ -70,11 +82,20 @@ inline void garble_proj(const comp_t* in0, const comp_t* Rin, const ModInfo& mi,
             s.payc[c] = compress(s.tmp.data(), mo);
             s.have[c] = 1;
         }
-        table[static_cast<i64>(s.colors[i]) * stride] = s.payc[c] + s.hc[i];
+        table[static_cast<i64>(K.colors[i]) * stride] = s.payc[c] + K.hc[i];
     }
 }
 
-// Mini projection: 16-bit payloads packed into one table entry.
+ProjKeys& proj_keys_scratch();
+
+template <class F>
+inline void garble_proj(const comp_t* in0, const comp_t* Rin, const ModInfo& mi, const comp_t* out0,
+                        const comp_t* outR, const ModInfo& mo, F&& f, u128* table, int stride = 1) {
+    ProjKeys& K = proj_keys_scratch();
+    proj_keys(in0, Rin, mi, K);
+    garble_proj_keys(K, out0, outR, mo, std::forward<F>(f), table, stride);
+}
+
 template <class F>
 inline void garble_proj_mini(const comp_t* in0, const comp_t* Rin, const ModInfo& mi, F&& f, u128* entry) {
     ProjScratch& s = proj_scratch();
