@@ -37,8 +37,11 @@ def main() -> None:
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--batch", type=int, default=int(os.environ.get("DASH_BENCH_BATCH", "8")),
+    ap.add_argument("--batch", type=int, default=int(os.environ.get("DASH_BENCH_BATCH", "16")),
                     help="garbled circuits evaluated together per GPU")
+    ap.add_argument("--streams", type=int, default=int(os.environ.get("DASH_BENCH_STREAMS", "2")),
+                    help="independent GC groups per GPU, each on its own HIP stream (overlap latency- and "
+                         "bandwidth-bound phases)")
     ap.add_argument("--model", default="MODEL_F_MINIONN_POOL_REPL")
     ap.add_argument("--config", default="DASH", choices=["DASH", "REDASH_OPT", "REDASH_CPM"])
     ap.add_argument("--no-mfma", action="store_true")
@@ -80,8 +83,11 @@ def main() -> None:
 
     # ---------------- offline: garble B circuits, stream them into HBM
     t_off = time.perf_counter()
+    G = max(1, min(args.streams, B))
+    assert B % G == 0, "--batch must be a multiple of --streams"
+    per = B // G
     gcs = []
-    ev = None
+    evs = [None] * G
     garble_s = 0.0
     upload_s = 0.0
     for b in range(B):
@@ -90,10 +96,11 @@ def main() -> None:
         gc = GarbledCircuit(circuit, cfg["crt"], cfg["mrs"], seed=seed)
         garble_s += time.perf_counter() - t
         t = time.perf_counter()
-        if ev is None:
-            ev = HipEvaluator(template=gc.model, batch=B, device=device, mfma=not args.no_mfma,
-                              profile=args.profile)
-        ev.load(b, gc.model)
+        g = b // per
+        if evs[g] is None:
+            evs[g] = HipEvaluator(template=gc.model, batch=per, device=device, mfma=not args.no_mfma,
+                                  profile=args.profile)
+        evs[g].load(b % per, gc.model)
         upload_s += time.perf_counter() - t
         table_gb = gc.table_bytes / 1e9
         gc.model = None  # host copy no longer needed (tables live in HBM)
@@ -101,17 +108,21 @@ def main() -> None:
         log(f"rank {rank}: garbled+uploaded GC {b + 1}/{B} ({table_gb:.2f} GB tables)")
     offline_s = time.perf_counter() - t_off
 
-    stream = torch.cuda.current_stream()
+    streams = [torch.cuda.current_stream()] + [torch.cuda.Stream() for _ in range(G - 1)]
 
     def step(i: int, verify: bool = False):
         xs = inputs[i * B:(i + 1) * B]
-        # online message #1 in wire form (16-B compressed labels) -> pinned staging -> H2D -> GPU unpack
-        for b, (gc, x) in enumerate(zip(gcs, xs)):
-            ev.encode_compressed_into(b, gc, x)
-        ev.upload_inputs_compressed(stream)
-        ev.run(stream)
-        ev.fetch_outputs(stream)  # online message #2 (synchronizes)
-        dec = [ev.decode(b, gc) for b, gc in enumerate(gcs)]
+        # online message #1 in wire form (16-B compressed labels) -> pinned staging -> H2D -> GPU unpack;
+        # the G groups run concurrently on their own streams
+        for g, (ev, st) in enumerate(zip(evs, streams)):
+            for b in range(per):
+                ev.encode_compressed_into(b, gcs[g * per + b], xs[g * per + b])
+            ev.upload_inputs_compressed(st)
+            ev.run(st)
+        dec = []
+        for g, (ev, st) in enumerate(zip(evs, streams)):
+            ev.fetch_outputs(st)  # online message #2 (synchronizes this group's stream)
+            dec += [ev.decode(b, gcs[g * per + b]) for b in range(per)]
         if verify:
             for gc, x, y in zip(gcs, xs, dec):
                 ref = gc.plain_q_eval(x)
@@ -152,7 +163,7 @@ def main() -> None:
     prof = None
     if args.profile:
         step(0)
-        prof = {k: round(v, 3) for k, v in ev.layer_times().items()}
+        prof = {k: round(v, 3) for k, v in evs[0].layer_times().items()}
     if rank == 0:
         out = {
             "metric": "online garbled inferences/sec (MiniONN CIFAR-10 CNN)",
@@ -176,6 +187,7 @@ def main() -> None:
                 "mrs": cfg["mrs"],
                 "global_batch": world * B,
                 "gcs_per_gpu": B,
+                "streams": G,
                 "seq_len": None,
                 "input_shape": [3, 32, 32],
                 "parallelism": f"dp{world}",

@@ -603,10 +603,7 @@ void launch_sign_approx(const SignArgs& a, const Act& x, const ModC* mc, const A
 void launch_sign_chain(const SignArgs& a, int maxn, const ModC* mc, const AesGlobals& g, hipStream_t st) {
     const dim3 gs = grid_aes(a.N, 512, a.t, a.B);
     const dim3 gr = grid_aes(a.N, 512, 1, a.B);
-    if (maxn <= 24) {
-        hipLaunchKernelGGL(k_sign_castsum<24>, gs, dim3(512), kAesLds, st, a, mc, g.te0, g.rk);
-        hipLaunchKernelGGL(k_sign_chain<24>, gr, dim3(512), kAesLds, st, a, mc, g.te0, g.rk);
-    } else if (maxn <= 32) {
+    if (maxn <= 32) {
         hipLaunchKernelGGL(k_sign_castsum<32>, gs, dim3(512), kAesLds, st, a, mc, g.te0, g.rk);
         hipLaunchKernelGGL(k_sign_chain<32>, gr, dim3(512), kAesLds, st, a, mc, g.te0, g.rk);
     } else {
