@@ -39,7 +39,7 @@ def main() -> None:
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--batch", type=int, default=int(os.environ.get("DASH_BENCH_BATCH", "16")),
                     help="garbled circuits evaluated together per GPU")
-    ap.add_argument("--streams", type=int, default=int(os.environ.get("DASH_BENCH_STREAMS", "2")),
+    ap.add_argument("--streams", type=int, default=int(os.environ.get("DASH_BENCH_STREAMS", "4")),
                     help="independent GC groups per GPU, each on its own HIP stream (overlap latency- and "
                          "bandwidth-bound phases)")
     ap.add_argument("--model", default="MODEL_F_MINIONN_POOL_REPL")
