@@ -1,5 +1,6 @@
 """Trusted-garbler process split (reference SGX flow, C40/C41), CPU evaluator."""
 import numpy as np
+import pytest
 
 from dash_amd.garbling import GarbledCircuit
 from dash_amd.models import build_circuit, quantized_inputs
@@ -14,3 +15,4 @@ def test_enclave_ann_infer_cpu():
         assert enc.last_stats["online_bytes"] > 0
     ref = GarbledCircuit(c, 7, 100.0, garble_me=False)
     np.testing.assert_array_equal(out, np.stack([ref.plain_q_eval(x) for x in xs]))
+

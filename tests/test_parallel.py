@@ -56,3 +56,19 @@ def test_single_process_context():
     ctx = init_distributed(use_gpu=False)
     assert ctx.world == 1 and not ctx.distributed
     np.testing.assert_array_equal(all_gather_array(ctx, np.arange(3)), [[0, 1, 2]])
+
+
+@pytest.mark.gpu
+def test_batch_dp_hip_single_rank():
+    from dash_amd.garbling import GarbledCircuit
+    from dash_amd.models import build_circuit, quantized_inputs
+    from dash_amd.parallel import BatchDataParallel, init_distributed
+
+    ctx = init_distributed(use_gpu=True)
+    c = build_circuit("MODEL_A")
+    xs = quantized_inputs("MODEL_A", 3)
+    dp = BatchDataParallel(ctx, c, 7, 100.0, per_rank=3, backend="hip")
+    for _ in range(2):  # fresh GCs every round, evaluator reused
+        out = dp.infer(xs)
+        ref = GarbledCircuit(c, 7, 100.0, garble_me=False)
+        np.testing.assert_array_equal(out, np.stack([ref.plain_q_eval(x) for x in xs]))

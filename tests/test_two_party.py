@@ -86,3 +86,32 @@ def test_two_party_rejects_incomplete_batch():
         cl.close()
     finally:
         p.join(timeout=60)
+
+
+@pytest.mark.gpu
+def test_two_party_hip_server_in_thread():
+    """HIP evaluator party; both parties in one process (no process spawn on the GPU box)."""
+    import threading
+
+    from dash_amd.net.channel import Channel
+    from dash_amd.net.protocol import EvaluatorServer
+
+    c = build_circuit("MODEL_A")
+    xs = quantized_inputs("MODEL_A", 4)
+    s = listen("127.0.0.1", 0)
+    port = s.getsockname()[1]
+
+    def serve():
+        conn, _ = s.accept()
+        EvaluatorServer("hip").serve(Channel(conn))
+
+    th = threading.Thread(target=serve, daemon=True)
+    th.start()
+    with GarblerClient("127.0.0.1", port, c, 7, 100.0, batch=2) as cl:
+        for r in range(2):
+            cl.offline()
+            outs = cl.infer(xs[2 * r:2 * r + 2])
+            for x, y in zip(xs[2 * r:2 * r + 2], outs):
+                np.testing.assert_array_equal(y, _plain(c, x))
+    th.join(timeout=60)
+    s.close()
