@@ -108,7 +108,7 @@ def main() -> None:
         log(f"rank {rank}: garbled+uploaded GC {b + 1}/{B} ({table_gb:.2f} GB tables)")
     offline_s = time.perf_counter() - t_off
 
-    streams = [torch.cuda.current_stream()] + [torch.cuda.Stream() for _ in range(G - 1)]
+    streams = [torch.cuda.Stream() for _ in range(G)]  # non-default streams: the evaluators replay hipGraphs
 
     def step(i: int, verify: bool = False):
         xs = inputs[i * B:(i + 1) * B]

@@ -182,6 +182,115 @@ __global__ __launch_bounds__(256) void k_conv_mfma(ConvArgs a, Act x, Act y, int
     }
 }
 
+
+// ---------------------------------------------------------------------------
+// LDS-image MFMA conv. One block = one (GC, label component) image of one
+// residue and a band of output rows, 64 filters (4 waves x 16). The input
+// band is staged once in LDS as centered int8 in channel-last order
+// [row][x][ci] (x stride Cpad+16 bytes: conflict-free ds_read_b128 for 16
+// consecutive output columns), padding positions hold the zero label's
+// component. The im2col operand is then a plain 16-byte LDS read per lane
+// for every (dy, dx, 64-channel chunk): no index arithmetic in the K loop.
+// All residues of a layer run in one launch.
+__global__ __launch_bounds__(256) void k_conv_img(ConvArgs a, Act x, Act y, int B) {
+    extern __shared__ __attribute__((aligned(16))) int8_t img[];
+    const int band = static_cast<int>(blockIdx.x % static_cast<unsigned>(a.nbands));
+    const int64_t gimg = blockIdx.x / static_cast<unsigned>(a.nbands);
+    int j = 0;
+    while (j + 1 < a.crt.k && gimg >= a.img_off[j + 1]) ++j;
+    if (!a.w8r[j]) return;  // residue handled by the VALU kernel (p > 255)
+    const int n = a.crt.n[j], p = a.crt.p[j], half = p / 2;
+    const int64_t r0 = gimg - a.img_off[j];
+    const int b = static_cast<int>(r0 / n), c = static_cast<int>(r0 % n);
+    const int f0 = blockIdx.y * 64;
+    const int oy0 = band * a.band;
+    const int oy1 = min(a.OH, oy0 + a.band);
+    const int iy0 = oy0 * a.sh - a.ph;
+    const int in_rows = (oy1 - oy0 - 1) * a.sh + a.kh;
+    const int S = a.Cpad + 16, Wp = a.W + 2 * a.pw;
+    const int HW = a.H * a.W;
+    const int16_t* X = x.p[j] + (static_cast<int64_t>(b) * n + c) * a.C * HW;
+    const int16_t zv = a.zero[static_cast<int64_t>(b) * a.lab_stride + a.lab_off[j] + c];
+    const int zc8 = zv > half ? zv - p : zv;
+    const int tid = threadIdx.x;
+    // stage the band: 4 channels per thread -> one dword; consecutive threads walk x (coalesced)
+    const int c4n = a.Cpad / 4;
+    const int items = in_rows * Wp * c4n;
+    for (int it = tid; it < items; it += 256) {
+        const int xq = it % Wp;
+        const int t2 = it / Wp;
+        const int yq = t2 % in_rows;
+        const int c4 = t2 / in_rows;
+        const int iy = iy0 + yq, ix = xq - a.pw;
+        const bool inside = iy >= 0 && iy < a.H && ix >= 0 && ix < a.W;
+        uint32_t packed = 0;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int ci = c4 * 4 + q;
+            int v = 0;
+            if (ci < a.C) {
+                if (inside) {
+                    v = X[static_cast<int64_t>(ci) * HW + iy * a.W + ix];
+                    if (v > half) v -= p;
+                } else {
+                    v = zc8;
+                }
+            }
+            packed |= (static_cast<uint32_t>(v) & 0xffu) << (8 * q);
+        }
+        *reinterpret_cast<uint32_t*>(img + (yq * Wp + xq) * S + c4 * 4) = packed;
+    }
+    __syncthreads();
+    const int wave = tid >> 6, lane = tid & 63;
+    const int fw = f0 + wave * 16;
+    if (fw >= a.F) return;  // wave-uniform; no barrier follows
+    const int ncol = (oy1 - oy0) * a.OW;
+    const int KK = a.kh * a.kw, CC = a.Cpad / 64;
+    const int8_t* Wr = a.w8r[j] + static_cast<int64_t>(fw + (lane & 15)) * (KK * a.Cpad) + (lane >> 4) * 16;
+    const int npos = a.OH * a.OW;
+    const int32_t* zcp = a.zc[j];
+    const int16_t* bias = a.bias[j];
+    int16_t* Y = y.p[j] + (static_cast<int64_t>(b) * n + c) * a.F * npos;
+    for (int col0 = 0; col0 < ncol; col0 += 64) {
+        v4i acc[4];
+        int base[4];
+        bool ok[4];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            acc[t] = v4i{0, 0, 0, 0};
+            const int col = col0 + t * 16 + (lane & 15);
+            ok[t] = col < ncol;
+            const int oyl = ok[t] ? col / a.OW : 0, ox = ok[t] ? col % a.OW : 0;
+            base[t] = ((oyl * a.sh) * Wp + ox * a.sw) * S + (lane >> 4) * 16;
+        }
+        for (int dy = 0; dy < a.kh; ++dy)
+            for (int dx = 0; dx < a.kw; ++dx)
+                for (int cc = 0; cc < CC; ++cc) {
+                    const v2l av = *reinterpret_cast<const v2l*>(Wr + (dy * a.kw + dx) * a.Cpad + cc * 64);
+                    const int off = (dy * Wp + dx) * S + cc * 64;
+#pragma unroll
+                    for (int t = 0; t < 4; ++t) {
+                        const v2l bv = ok[t] ? *reinterpret_cast<const v2l*>(img + base[t] + off) : v2l{0, 0};
+                        acc[t] = __builtin_amdgcn_mfma_i32_16x16x64_i8(av, bv, acc[t], 0, 0, 0);
+                    }
+                }
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            if (!ok[t]) continue;
+            const int col = col0 + t * 16 + (lane & 15);
+            const int pos = (oy0 + col / a.OW) * a.OW + col % a.OW;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int f = fw + (lane >> 4) * 4 + r;
+                if (f >= a.F) continue;
+                const int16_t bv = bias[(static_cast<int64_t>(b) * a.F + f) * n + c];
+                Y[static_cast<int64_t>(f) * npos + pos] =
+                    static_cast<int16_t>(mod_p(acc[t][r] % p + zcp[f] * zv + bv, p));
+            }
+        }
+    }
+}
+
 // ---------------------------------------------------------------------------
 namespace {
 struct ZTab {
@@ -227,7 +336,16 @@ void launch_dense(const DenseArgs& a, const Act& x, const Act& y, int B, hipStre
 }
 
 void launch_conv(const ConvArgs& a, const Act& x, const Act& y, int B, hipStream_t st) {
-    if (a.use_mfma) {
+    if (a.use_mfma && a.nbands > 0) {
+        const int64_t nimg = a.img_off[a.crt.k];
+        const int in_rows = (min(a.band, a.OH) - 1) * a.sh + a.kh;
+        const size_t lds = static_cast<size_t>(in_rows) * (a.W + 2 * a.pw) * (a.Cpad + 16);
+        dim3 g(static_cast<unsigned>(nimg * a.nbands), static_cast<unsigned>((a.F + 63) / 64), 1);
+        hipLaunchKernelGGL(k_conv_img, g, dim3(256), lds, st, a, x, y, B);
+        bool rest = false;
+        for (int j = 0; j < a.crt.k; ++j) rest |= (a.w8r[j] == nullptr);
+        if (!rest) return;
+    } else if (a.use_mfma) {
         for (int j = 0; j < a.crt.k; ++j) {
             if (!a.w8[j]) continue;
             const int64_t ncols = static_cast<int64_t>(B) * a.crt.n[j] * a.OH * a.OW;

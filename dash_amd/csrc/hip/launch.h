@@ -71,6 +71,10 @@ struct ConvArgs {
     int lab_stride;
     int lab_off[kMaxRes];
     int use_mfma;
+    // LDS-image MFMA path (k_conv_img): weights [F16][kh][kw][Cpad] centered int8
+    const int8_t* w8r[kMaxRes];
+    int Cpad = 0, band = 0, nbands = 0;
+    int64_t img_off[kMaxRes + 1];  // first image index of residue j: B * sum_{i<j} n_i
 };
 void launch_conv(const ConvArgs& a, const Act& x, const Act& y, int B, hipStream_t st);
 

@@ -133,6 +133,7 @@ class HipEvaluator {
         loaded_[b] = 1;
     }
     ~HipEvaluator() {
+        if (gexec_) (void)hipGraphExecDestroy(gexec_);
         for (void* p : allocs_) (void)hipFree(p);
         for (void* p : host_allocs_) (void)hipHostFree(p);
     }
@@ -210,15 +211,36 @@ class HipEvaluator {
                                     hipMemcpyHostToDevice, st));
     }
 
+    // The op list is static (all device pointers fixed at build time), so
+    // after one eager run (lazy one-time allocations) it is captured into a
+    // hipGraph and replayed: one launch per evaluation instead of ~200.
     void run(hipStream_t st) {
         for (int b = 0; b < B_; ++b) DASH_CHECK(loaded_[b], "batch slot " + std::to_string(b) + " has no garbled model loaded");
-        for (size_t i = 0; i < ops_.size(); ++i) {
-            if (profile_) HIPCHECK(hipEventRecord(ev_[i], st));
-            ops_[i](st);
+        if (profile_ || !use_graph_ || runs_ == 0 || st == nullptr) {
+            for (size_t i = 0; i < ops_.size(); ++i) {
+                if (profile_) HIPCHECK(hipEventRecord(ev_[i], st));
+                ops_[i](st);
+            }
+            if (profile_) HIPCHECK(hipEventRecord(ev_.back(), st));
+            HIPCHECK(hipGetLastError());
+            ++runs_;
+            return;
         }
-        if (profile_) HIPCHECK(hipEventRecord(ev_.back(), st));
-        HIPCHECK(hipGetLastError());
+        if (!gexec_ || gstream_ != st) {
+            if (gexec_) HIPCHECK(hipGraphExecDestroy(gexec_));
+            gexec_ = nullptr;
+            hipGraph_t graph = nullptr;
+            HIPCHECK(hipStreamBeginCapture(st, hipStreamCaptureModeRelaxed));
+            for (auto& op : ops_) op(st);
+            HIPCHECK(hipStreamEndCapture(st, &graph));
+            HIPCHECK(hipGraphInstantiate(&gexec_, graph, nullptr, nullptr, 0));
+            HIPCHECK(hipGraphDestroy(graph));
+            gstream_ = st;
+        }
+        HIPCHECK(hipGraphLaunch(gexec_, st));
+        ++runs_;
     }
+    void set_graph(bool on) { use_graph_ = on; }
 
     std::vector<CrtLabels> get_outputs(hipStream_t st) {
         std::vector<CrtLabels> out(B_);
@@ -390,6 +412,13 @@ class HipEvaluator {
     Act cur_act_{};
     std::vector<int16_t*> in_stage_, out_stage_;
     u128* in_comp_stage_ = nullptr;
+    bool use_graph_ = [] {
+        const char* e = std::getenv("DASH_HIP_GRAPH");
+        return !(e && e[0] == '0');
+    }();
+    hipGraphExec_t gexec_ = nullptr;
+    hipStream_t gstream_ = nullptr;
+    long runs_ = 0;
     u128* in_comp_dev_ = nullptr;
     // constants
     ModC* mc_ = nullptr;
@@ -598,6 +627,20 @@ void HipEvaluator::build() {
                 const i64 K = G.K();
                 a.Kpad = static_cast<int>((K + 63) / 64 * 64);
                 a.use_mfma = mfma_ ? 1 : 0;
+                // LDS-image kernel geometry: 64-channel chunks, row bands that fit 64 KiB of LDS
+                a.Cpad = static_cast<int>((G.C + 63) / 64 * 64);
+                {
+                    const i64 row_bytes = (G.W + 2 * G.pw) * (a.Cpad + 16);
+                    i64 band = G.OH;
+                    while (band > 1 && ((band - 1) * G.sh + G.kh) * row_bytes > 65536) --band;
+                    if (((band - 1) * G.sh + G.kh) * row_bytes <= 65536 && mfma_) {
+                        a.band = static_cast<int>(band);
+                        a.nbands = static_cast<int>((G.OH + band - 1) / band);
+                    }
+                }
+                a.img_off[0] = 0;
+                for (int j = 0; j < k_; ++j) a.img_off[j + 1] = a.img_off[j] + static_cast<i64>(B_) * crt.n[j];
+                const i64 F16 = (G.F + 15) / 16 * 16;
                 const Array& w = g.arr("w");
                 for (int j = 0; j < k_; ++j) {
                     const int p = crt_[j];
@@ -613,6 +656,19 @@ void HipEvaluator::build() {
                         }
                     a.w[j] = upload(wm.data(), wm.size());
                     a.w8[j] = (mfma_ && p <= 255) ? upload(w8.data(), w8.size()) : nullptr;
+                    if (a.nbands > 0 && p <= 255) {
+                        // [F16][kh][kw][Cpad] centered int8 (im2col order ci*kh*kw + dy*kw + dx -> (dy, dx, ci))
+                        std::vector<int8_t> w8r(static_cast<size_t>(F16) * G.kh * G.kw * a.Cpad, 0);
+                        for (i64 f = 0; f < G.F; ++f)
+                            for (i64 ci = 0; ci < G.C; ++ci)
+                                for (i64 dy = 0; dy < G.kh; ++dy)
+                                    for (i64 dx = 0; dx < G.kw; ++dx)
+                                        w8r[((f * G.kh + dy) * G.kw + dx) * a.Cpad + ci] =
+                                            w8[f * a.Kpad + (ci * G.kh + dy) * G.kw + dx];
+                        a.w8r[j] = upload(w8r.data(), w8r.size());
+                    } else {
+                        a.w8r[j] = nullptr;
+                    }
                     a.zc[j] = upload(zc.data(), zc.size());
                     a.bias[j] = upload_i16_rows(li, arr_name("bias.", j, ""));
                 }
@@ -1129,6 +1185,10 @@ void register_hip_bindings(py::module_& m) {
         .def("upload_inputs_compressed", [](HipEvaluator& h, uintptr_t stream) { h.upload_inputs_compressed(as_stream(stream)); },
              py::arg("stream") = 0)
         .def("fetch_outputs", [](HipEvaluator& h, uintptr_t stream) { h.fetch_outputs(as_stream(stream)); }, py::arg("stream") = 0)
+        .def("crt_size", &HipEvaluator::crt_size)
+        .def("set_graph", &HipEvaluator::set_graph)
+        .def("input_size", &HipEvaluator::input_size)
+        .def("output_size", &HipEvaluator::output_size)
         .def("outputs_compressed", [](const HipEvaluator& h, int b) {
             auto r = h.outputs_compressed(b);
             py::array_t<uint64_t> out({static_cast<py::ssize_t>(h.crt_size()), static_cast<py::ssize_t>(h.output_size()),

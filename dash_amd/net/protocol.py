@@ -83,8 +83,8 @@ class EvaluatorServer:
                         return
                     else:
                         raise ValueError(f"unknown message {tag!r}")
-                except (ValueError, RuntimeError) as e:
-                    ch.send(b"ERR!", str(e).encode())
+                except Exception as e:  # report every failure to the peer, keep serving
+                    ch.send(b"ERR!", f"{type(e).__name__}: {e}".encode())
         finally:
             ch.close()
 

@@ -177,3 +177,25 @@ def test_compressed_wire_paths():
     bad[0, 0, 0] ^= 1
     with pytest.raises(d.IntegrityError):
         gcs[0].decode_compressed(bad)
+
+
+def test_graph_replay_matches_eager():
+    """Runs 2+ replay the captured hipGraph; results must equal the eager run."""
+    import torch
+
+    from dash_amd.models import build_circuit, quantized_inputs
+    from dash_amd.ir.quant import QuantizationMethod as Q
+
+    c = build_circuit("MODEL_B_POOL_REPL", Q.ScaleQuant, 3, seed=4)
+    xs = quantized_inputs("MODEL_B_POOL_REPL", 6, Q.ScaleQuant, 3)
+    gcs = [GarbledCircuit(c, 8, 100.0, seed=bytes([i + 40]) * 16) for i in range(2)]
+    ev = _hip([g.model for g in gcs])
+    st = torch.cuda.Stream()
+    for r in range(3):
+        for b, g in enumerate(gcs):
+            ev.encode_compressed_into(b, g, xs[2 * r + b])
+        ev.upload_inputs_compressed(st)
+        ev.run(st)
+        ev.fetch_outputs(st)
+        for b, g in enumerate(gcs):
+            np.testing.assert_array_equal(ev.decode(b, g), g.plain_q_eval(xs[2 * r + b]))
