@@ -72,8 +72,10 @@ CrtLabels cpu_evaluate(const GarbledModel& m, const CrtLabels& inputs, int nt, s
         sum_crt += crt[j];
     }
     std::vector<int> keep(m.layers.size() + 1, 0);
-    for (const auto& l : m.layers)
+    for (const auto& l : m.layers) {
         if (l.kind == K_ADD) keep[l.param("src") + 1] = 1;
+        if (l.p.count("in_src")) keep[l.param("in_src") + 1] = 1;
+    }
     std::vector<CrtLabels> saved(m.layers.size() + 1);
 
     CrtLabels cur = inputs;
@@ -88,6 +90,7 @@ CrtLabels cpu_evaluate(const GarbledModel& m, const CrtLabels& inputs, int nt, s
     for (size_t li = 0; li < m.layers.size(); ++li) {
         const auto t_layer = std::chrono::steady_clock::now();
         const GLayer& g = m.layers[li];
+        if (g.p.count("in_src")) cur = saved[g.param("in_src") + 1];
         const i64 Nin = cur[0].N;
         switch (g.kind) {
             case K_FLATTEN:

@@ -340,15 +340,25 @@ GarbledModel Garbler::garble(const std::vector<LayerSpec>& layers, const std::ve
     };
 
     // which layer outputs are referenced by residual adds
+    // (and by layers that read an earlier output, param "in_src": projection shortcuts)
     std::vector<int> keep(layers.size() + 1, 0);
-    for (const auto& l : layers)
+    for (const auto& l : layers) {
         if (l.kind == K_ADD) keep[param1(l.p, "src") + 1] = 1;
+        auto it = l.p.find("in_src");
+        if (it != l.p.end() && !it->second.empty()) keep[it->second[0] + 1] = 1;
+    }
     std::vector<CrtLabels> saved(layers.size() + 1);
+    std::vector<std::vector<int>> saved_mod(layers.size() + 1);
+    std::vector<std::vector<i64>> saved_dims(layers.size() + 1);
 
     CrtLabels cur = in_base_;
     std::vector<int> cur_mod = crt_;
     std::vector<i64> dims = in_dims;
-    if (keep[0]) saved[0] = cur;
+    if (keep[0]) {
+        saved[0] = cur;
+        saved_mod[0] = cur_mod;
+        saved_dims[0] = dims;
+    }
     std::vector<i64> prefix(k);
     i64 sum_crt = 0;
     for (int j = 0; j < k; ++j) {
@@ -361,6 +371,16 @@ GarbledModel Garbler::garble(const std::vector<LayerSpec>& layers, const std::ve
         const auto t_layer = std::chrono::steady_clock::now();
         const LayerSpec& spec = layers[li];
         const u64 L = li + 1;
+        {
+            auto it = spec.p.find("in_src");
+            if (it != spec.p.end() && !it->second.empty()) {
+                const i64 s = it->second[0];
+                DASH_CHECK(s >= -1 && s < static_cast<i64>(li), "in_src must name an earlier layer");
+                cur = saved[s + 1];
+                cur_mod = saved_mod[s + 1];
+                dims = saved_dims[s + 1];
+            }
+        }
         GLayer g;
         g.kind = spec.kind;
         // copy scalar/list params except the large weight arrays (stored as arrays)
@@ -795,7 +815,11 @@ GarbledModel Garbler::garble(const std::vector<LayerSpec>& layers, const std::ve
             default:
                 throw std::runtime_error(std::string("dash: cannot garble layer kind ") + std::to_string(spec.kind));
         }
-        if (keep[li + 1]) saved[li + 1] = cur;
+        if (keep[li + 1]) {
+            saved[li + 1] = cur;
+            saved_mod[li + 1] = cur_mod;
+            saved_dims[li + 1] = dims;
+        }
         m.layers.push_back(std::move(g));
         layer_ms_[li] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_layer).count();
     }

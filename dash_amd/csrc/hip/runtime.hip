@@ -496,7 +496,10 @@ void HipEvaluator::build() {
     for (int j = 0; j < k_; ++j) widest[j] = nr_comps(crt_[j]);
     {
         i64 N = N0_;
+        std::vector<i64> outN(m0.layers.size() + 1, N0_);
+        size_t li0 = 0;
         for (auto& l : m0.layers) {
+            if (l.p.count("in_src")) N = outN[l.param("in_src") + 1];
             switch (l.kind) {
                 case K_DENSE: N = l.param("out"); break;
                 case K_CONV: N = ConvGeom(l).out_size(); break;
@@ -523,6 +526,7 @@ void HipEvaluator::build() {
                 default: break;
             }
             maxN = std::max(maxN, N);
+            outN[++li0] = N;
         }
     }
     const i64 cap = std::max(maxN, maxPoolSlots);
@@ -549,9 +553,13 @@ void HipEvaluator::build() {
 
     // ---- plan
     std::vector<int> keep(m0.layers.size() + 1, 0);
-    for (auto& l : m0.layers)
+    for (auto& l : m0.layers) {
         if (l.kind == K_ADD) keep[l.param("src") + 1] = 1;
+        if (l.p.count("in_src")) keep[l.param("in_src") + 1] = 1;
+    }
     saved_.assign(m0.layers.size() + 1, {});
+    std::vector<i64> saved_n(m0.layers.size() + 1, 0);
+    std::vector<std::vector<int>> saved_mods(m0.layers.size() + 1);
     int cur = 0;  // buffer index holding the current activation
     i64 N = N0_;
     const CrtInfo crt = crt_info(crt_);
@@ -566,6 +574,8 @@ void HipEvaluator::build() {
             s.push_back(d);
         }
         saved_[slot] = s;
+        saved_n[slot] = n_el;
+        saved_mods[slot] = md;
     };
     save_if_needed(0, cur, N, mods);
 
@@ -573,6 +583,22 @@ void HipEvaluator::build() {
         const GLayer& g = m0.layers[li];
         const int nxt = (cur + 1) % 2;
         const std::string lname = std::string(kind_name(g.kind)) + "#" + std::to_string(li);
+        if (g.p.count("in_src")) {
+            // layer reads an earlier output (projection shortcut): restore it into the current buffer
+            const i64 src = g.param("in_src");
+            const auto& sv = saved_[src + 1];
+            DASH_CHECK(!sv.empty(), "in_src source not saved");
+            N = saved_n[src + 1];
+            mods = saved_mods[src + 1];
+            for (int j = 0; j < k_; ++j) {
+                const size_t bytes = sizeof(int16_t) * B_ * nr_comps(mods[j]) * N;
+                int16_t* d = bufs_[cur].p[j];
+                const int16_t* sp = sv[j];
+                add_op("restore", [d, sp, bytes](hipStream_t st) {
+                    HIPCHECK(hipMemcpyAsync(d, sp, bytes, hipMemcpyDeviceToDevice, st));
+                });
+            }
+        }
         cur_act_ = act_of(cur);
         switch (g.kind) {
             case K_FLATTEN:

@@ -39,7 +39,8 @@ class Circuit:
         assert x.size == self.input_size, "input size does not match circuit input size"
         ctx = [x]
         for layer in self.layers:
-            x = layer.plain_eval(x, track, ctx)
+            src = getattr(layer, "in_src", None)
+            x = layer.plain_eval(ctx[src + 1] if src is not None else x, track, ctx)
             ctx.append(x)
         return x
 
@@ -50,7 +51,8 @@ class Circuit:
         assert x.size == self.input_size, "input size does not match circuit input size"
         ctx = [x]
         for layer in self.layers:
-            x = layer.plain_q_eval(x, track, ctx, crt_modulus)
+            src = getattr(layer, "in_src", None)
+            x = layer.plain_q_eval(ctx[src + 1] if src is not None else x, track, ctx, crt_modulus)
             ctx.append(x)
         return x
 
@@ -141,7 +143,13 @@ class Circuit:
         return q
 
     def garble_specs(self) -> list:
-        return [l.garble_spec() for l in self.layers]
+        specs = []
+        for l in self.layers:
+            kind, params = l.garble_spec()
+            if getattr(l, "in_src", None) is not None:
+                params = dict(params, in_src=int(l.in_src))
+            specs.append((kind, params))
+        return specs
 
     def __repr__(self) -> str:
         return "Circuit(\n  " + "\n  ".join(repr(l) for l in self.layers) + "\n)"

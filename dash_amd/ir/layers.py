@@ -47,6 +47,10 @@ class Layer:
     kind: int = -1
     name: str = "layer"
 
+    # index of the layer whose output this layer reads (-1 = circuit input);
+    # None = the previous layer (sequential). Used for projection shortcuts.
+    in_src = None
+
     def __init__(self, in_dims: Sequence[int], out_dims: Sequence[int]):
         self.in_dims = tuple(int(d) for d in in_dims)
         self.out_dims = tuple(int(d) for d in out_dims)

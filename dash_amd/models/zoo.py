@@ -143,11 +143,11 @@ def build_circuit(name: str, q_method: QuantizationMethod = QuantizationMethod.S
             layers.append(Relu(d1))
             d2 = conv(cout, 3, 1, 1, cout, d1[1], d1[2])
             if stride != 1 or cin != cout:
-                # projection shortcut: 1x1 conv on the block input, then add the main path
+                # projection shortcut: 1x1 conv reading the block input (in_src), then add the main path
                 main_last = len(layers) - 1
+                sc = len(layers)
                 conv(cout, 1, stride, 0, cin, dims[1], dims[2])
-                # the shortcut conv consumed the main path as input in a sequential IR, so the
-                # shortcut here is applied to the main path output; see docs/MODELS.md
+                layers[sc].in_src = src
                 layers.append(Add(d2, main_last))
             else:
                 layers.append(Add(d2, src))

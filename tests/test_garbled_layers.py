@@ -237,3 +237,41 @@ def test_encode_cm_matches_encode():
     assert len(cm) == len(lab)
     for (p, a), b in zip(lab, cm):
         np.testing.assert_array_equal(a.T, b)
+
+
+def _shortcut_block(seed=0):
+    """conv -> relu -> [main: strided conv, relu, conv] + [shortcut: 1x1 strided conv on the block input] -> relu"""
+    from dash_amd.ir.circuit import Circuit
+    from dash_amd.ir.layers import Add, Conv2d, Relu
+
+    rng = np.random.default_rng(seed)
+    c0 = Conv2d(rng.integers(-3, 4, (4, 2, 3, 3)), rng.integers(-5, 5, 4), 6, 6, 2, 4, 3, 3, 1, 1, pad_width=1,
+                pad_height=1, q_const=1.0)
+    ca = Conv2d(rng.integers(-3, 4, (8, 4, 3, 3)), rng.integers(-5, 5, 8), 6, 6, 4, 8, 3, 3, 2, 2, pad_width=1,
+                pad_height=1, q_const=1.0)
+    cb = Conv2d(rng.integers(-3, 4, (8, 8, 3, 3)), rng.integers(-5, 5, 8), 3, 3, 8, 8, 3, 3, 1, 1, pad_width=1,
+                pad_height=1, q_const=1.0)
+    cs = Conv2d(rng.integers(-3, 4, (8, 4, 1, 1)), rng.integers(-5, 5, 8), 6, 6, 4, 8, 1, 1, 2, 2, q_const=1.0)
+    cs.in_src = 1  # reads the block input (output of layer 1)
+    c = Circuit([c0, Relu(c0.out_dims), ca, Relu(ca.out_dims), cb, cs, Add(cb.out_dims, 4), Relu(cb.out_dims)])
+    xs = [rng.integers(-4, 5, c.input_size) for _ in range(3)]
+    return c, xs
+
+
+def test_projection_shortcut_in_src():
+    c, xs = _shortcut_block()
+    k = c.infer_crt_base_size(xs)
+    for x in xs:
+        out, _ = run(c, k, 100.0, x)
+        ref = GarbledCircuit(c, k, 100.0, garble_me=False).plain_q_eval(x)
+        np.testing.assert_array_equal(out, ref)
+
+
+def test_resnet18_zoo_has_projection_shortcuts():
+    from dash_amd.models import build_circuit
+
+    c = build_circuit("RESNET18")
+    srcs = [l.in_src for l in c.layers if l.in_src is not None]
+    assert len(srcs) == 3  # stages 2-4 change width / stride
+    specs = c.garble_specs()
+    assert sum("in_src" in p for _, p in specs) == 3

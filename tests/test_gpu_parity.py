@@ -199,3 +199,11 @@ def test_graph_replay_matches_eager():
         ev.fetch_outputs(st)
         for b, g in enumerate(gcs):
             np.testing.assert_array_equal(ev.decode(b, g), g.plain_q_eval(xs[2 * r + b]))
+
+
+def test_projection_shortcut_in_src():
+    from tests.test_garbled_layers import _shortcut_block
+
+    c, xs = _shortcut_block()
+    k = c.infer_crt_base_size(xs)
+    _check(c, k, 100.0, xs)
