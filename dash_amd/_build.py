@@ -112,7 +112,8 @@ def build(jobs: int | None = None, debug: bool = False, clean: bool = False, ver
     if tasks or not out.exists() or out.stat().st_mtime < newest:
         tmp = out.with_suffix(".tmp.so")
         link = [str(ROCM / "bin" / "hipcc"), "-shared", "-fPIC", f"--offload-arch={ARCH}", *map(str, objs), "-o",
-                str(tmp), f"-L{ROCM / 'lib'}", "-lamdhip64", "-lpthread"]
+                str(tmp), f"-L{ROCM / 'lib'}", f"-Wl,-rpath,{ROCM / 'lib'}", "-lamdhip64",
+                "-lrocprofiler-sdk-roctx", "-lpthread"]
         if verbose:
             print(" ".join(link), flush=True)
         r = subprocess.run(link, capture_output=True, text=True)

@@ -14,6 +14,8 @@
 #include "../layers.h"
 #include "launch.h"
 
+#include <rocprofiler-sdk-roctx/roctx.h>
+
 namespace py = pybind11;
 
 namespace dash {
@@ -217,9 +219,16 @@ class HipEvaluator {
     void run(hipStream_t st) {
         for (int b = 0; b < B_; ++b) DASH_CHECK(loaded_[b], "batch slot " + std::to_string(b) + " has no garbled model loaded");
         if (profile_ || !use_graph_ || runs_ == 0 || st == nullptr) {
+            // roctx ranges per op (layer / gadget phase) for rocprofv3 --marker-trace (DASH_ROCTX=1)
+            static const bool markers = [] {
+                const char* e = std::getenv("DASH_ROCTX");
+                return e && e[0] == '1';
+            }();
             for (size_t i = 0; i < ops_.size(); ++i) {
                 if (profile_) HIPCHECK(hipEventRecord(ev_[i], st));
+                if (markers) roctxRangePushA(op_names_[i].c_str());
                 ops_[i](st);
+                if (markers) roctxRangePop();
             }
             if (profile_) HIPCHECK(hipEventRecord(ev_.back(), st));
             HIPCHECK(hipGetLastError());
@@ -659,7 +668,11 @@ void HipEvaluator::build() {
                     const i64 row_bytes = (G.W + 2 * G.pw) * (a.Cpad + 16);
                     i64 band = G.OH;
                     while (band > 1 && ((band - 1) * G.sh + G.kh) * row_bytes > 65536) --band;
-                    if (((band - 1) * G.sh + G.kh) * row_bytes <= 65536 && mfma_) {
+                    static const bool img_ok = [] {
+                        const char* e = std::getenv("DASH_CONV_IMG");
+                        return !(e && e[0] == '0');
+                    }();
+                    if (((band - 1) * G.sh + G.kh) * row_bytes <= 65536 && mfma_ && img_ok) {
                         a.band = static_cast<int>(band);
                         a.nbands = static_cast<int>((G.OH + band - 1) / band);
                     }
