@@ -37,7 +37,7 @@ def main() -> None:
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--batch", type=int, default=int(os.environ.get("DASH_BENCH_BATCH", "16")),
+    ap.add_argument("--batch", type=int, default=int(os.environ.get("DASH_BENCH_BATCH", "24")),
                     help="garbled circuits evaluated together per GPU")
     ap.add_argument("--streams", type=int, default=int(os.environ.get("DASH_BENCH_STREAMS", "4")),
                     help="independent GC groups per GPU, each on its own HIP stream (overlap latency- and "
@@ -58,17 +58,15 @@ def main() -> None:
     from dash_amd.native import native
     from dash_amd.runtime import HipEvaluator
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    dist = world > 1
-    if dist:
-        import torch.distributed as tdist
+    from dash_amd.parallel import all_gather_array, all_reduce_max, barrier, init_distributed, shutdown
 
-        torch.cuda.set_device(local_rank)
-        tdist.init_process_group("nccl")
-    else:
-        torch.cuda.set_device(0)
+    # one process per GPU (torchrun); backend nccl (= RCCL over xGMI). DASH_DIST_BACKEND=gloo and a
+    # device count smaller than the world size are only for rehearsing the multi-rank path on one GPU.
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    if int(os.environ.get("WORLD_SIZE", "1")) > 1 and torch.cuda.device_count() < int(os.environ["WORLD_SIZE"]):
+        os.environ["LOCAL_RANK"] = str(int(os.environ.get("LOCAL_RANK", "0")) % max(1, torch.cuda.device_count()))
+    ctx = init_distributed(backend=os.environ.get("DASH_DIST_BACKEND") or None, use_gpu=True)
+    world, rank, dist = ctx.world, ctx.rank, ctx.distributed
     device = torch.cuda.current_device()
     if args.threads:
         native().set_num_threads(args.threads)
@@ -108,7 +106,13 @@ def main() -> None:
         log(f"rank {rank}: garbled+uploaded GC {b + 1}/{B} ({table_gb:.2f} GB tables)")
     offline_s = time.perf_counter() - t_off
 
-    streams = [torch.cuda.Stream() for _ in range(G)]  # non-default streams: the evaluators replay hipGraphs
+    # group 0 on the current stream, the others on torch pool streams (measured best on MI355X:
+    # 313 inf/s at B=24 vs 295 with one dedicated non-blocking HIP stream per group, which runs all
+    # groups fully concurrently and over-subscribes caches); DASH_BENCH_TORCH_STREAMS=0 -> dedicated
+    if os.environ.get("DASH_BENCH_TORCH_STREAMS", "1") == "1":
+        streams = [torch.cuda.current_stream()] + [torch.cuda.Stream() for _ in range(G - 1)]
+    else:
+        streams = [native().hip_stream_create(0) for _ in range(G)]
 
     def step(i: int, verify: bool = False):
         xs = inputs[i * B:(i + 1) * B]
@@ -135,27 +139,21 @@ def main() -> None:
         step(w, verify=bool(args.verify) and w == 0)
         verified = verified or bool(args.verify)
     torch.cuda.synchronize()
-    if dist:
-        tdist.barrier()
+    barrier(ctx)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     last = None
     for s in range(args.steps):
         last = step(args.warmup + s)
     torch.cuda.synchronize()
-    if dist:
-        tdist.barrier()
+    barrier(ctx)
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
 
-    if dist:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-        tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
-        elapsed = float(t.item())
-        # gather decoded logits of the last step onto every rank (RCCL all-gather over xGMI)
-        logits = torch.tensor(np.stack(last), dtype=torch.int64, device="cuda")
-        gathered = [torch.empty_like(logits) for _ in range(world)]
-        tdist.all_gather(gathered, logits)
+    elapsed = all_reduce_max(ctx, elapsed)  # slowest rank defines the step time
+    # decoded logits of the last step onto every rank (RCCL all-gather over xGMI)
+    gathered = all_gather_array(ctx, np.stack(last))
+    assert gathered.shape[0] == world
 
     total_inf = world * B * args.steps
     value = total_inf / elapsed
@@ -199,8 +197,7 @@ def main() -> None:
         if prof:
             out["layer_ms"] = prof
         print(json.dumps(out), flush=True)
-    if dist:
-        tdist.destroy_process_group()
+    shutdown(ctx)
 
 
 if __name__ == "__main__":

@@ -213,32 +213,42 @@ __global__ __launch_bounds__(256) void k_conv_img(ConvArgs a, Act x, Act y, int 
     const int16_t zv = a.zero[static_cast<int64_t>(b) * a.lab_stride + a.lab_off[j] + c];
     const int zc8 = zv > half ? zv - p : zv;
     const int tid = threadIdx.x;
-    // stage the band: 4 channels per thread -> one dword; consecutive threads walk x (coalesced)
+    // stage the band: each item is a 4-channel x 4-column block transposed in
+    // registers into 4 dwords (channel-last); consecutive threads walk x.
     const int c4n = a.Cpad / 4;
-    const int items = in_rows * Wp * c4n;
+    const int WQ = (Wp + 3) / 4;
+    const int items = in_rows * WQ * c4n;
     for (int it = tid; it < items; it += 256) {
-        const int xq = it % Wp;
-        const int t2 = it / Wp;
+        const int xq = it % WQ;
+        const int t2 = it / WQ;
         const int yq = t2 % in_rows;
         const int c4 = t2 / in_rows;
-        const int iy = iy0 + yq, ix = xq - a.pw;
-        const bool inside = iy >= 0 && iy < a.H && ix >= 0 && ix < a.W;
-        uint32_t packed = 0;
+        const int iy = iy0 + yq;
+        const bool rowin = iy >= 0 && iy < a.H;
+        uint32_t packed[4] = {0u, 0u, 0u, 0u};
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
             const int ci = c4 * 4 + q;
-            int v = 0;
-            if (ci < a.C) {
-                if (inside) {
-                    v = X[static_cast<int64_t>(ci) * HW + iy * a.W + ix];
+            if (ci >= a.C) continue;
+            const int16_t* row = X + static_cast<int64_t>(ci) * HW + static_cast<int64_t>(iy) * a.W;
+#pragma unroll
+            for (int t = 0; t < 4; ++t) {
+                const int ix = xq * 4 + t - a.pw;
+                int v;
+                if (rowin && ix >= 0 && ix < a.W) {
+                    v = row[ix];
                     if (v > half) v -= p;
                 } else {
                     v = zc8;
                 }
+                packed[t] |= (static_cast<uint32_t>(v) & 0xffu) << (8 * q);
             }
-            packed |= (static_cast<uint32_t>(v) & 0xffu) << (8 * q);
         }
-        *reinterpret_cast<uint32_t*>(img + (yq * Wp + xq) * S + c4 * 4) = packed;
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            const int xx = xq * 4 + t;
+            if (xx < Wp) *reinterpret_cast<uint32_t*>(img + (yq * Wp + xx) * S + c4 * 4) = packed[t];
+        }
     }
     __syncthreads();
     const int wave = tid >> 6, lane = tid & 63;

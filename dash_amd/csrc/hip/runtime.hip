@@ -1182,6 +1182,15 @@ void register_hip_bindings(py::module_& m) {
         py::gil_scoped_release rel;
         g.encode_cm(xp, N, slot);
     });
+    // Dedicated non-blocking HIP streams (each new stream is mapped to the next
+    // hardware queue), for running independent GC groups concurrently.
+    m.def("hip_stream_create", [](int priority) {
+        hipStream_t st = nullptr;
+        HIPCHECK(hipStreamCreateWithPriority(&st, hipStreamNonBlocking, priority));
+        return reinterpret_cast<uintptr_t>(st);
+    }, py::arg("priority") = 0);
+    m.def("hip_stream_destroy", [](uintptr_t st) { HIPCHECK(hipStreamDestroy(reinterpret_cast<hipStream_t>(st))); });
+    m.def("hip_stream_sync", [](uintptr_t st) { HIPCHECK(hipStreamSynchronize(reinterpret_cast<hipStream_t>(st))); });
     m.def("hip_device_count", []() {
         int n = 0;
         if (hipGetDeviceCount(&n) != hipSuccess) return 0;

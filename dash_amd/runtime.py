@@ -132,6 +132,11 @@ class HipEvaluator:
         return out
 
 
+def hip_stream(priority: int = 0) -> int:
+    """A dedicated non-blocking HIP stream (handle usable wherever a stream is accepted)."""
+    return native().hip_stream_create(priority)
+
+
 def hip_available() -> bool:
     try:
         return native().hip_device_count() > 0
