@@ -164,7 +164,8 @@ def main() -> None:
         prof = {k: round(v, 3) for k, v in evs[0].layer_times().items()}
     if rank == 0:
         out = {
-            "metric": "online garbled inferences/sec (MiniONN CIFAR-10 CNN)",
+            "metric": ("online garbled inferences/sec (MiniONN CIFAR-10 CNN)" if model == "MODEL_F_MINIONN_POOL_REPL"
+                       else f"online garbled inferences/sec ({model})"),
             "value": round(value, 3),
             "unit": "inferences/s",
             "n_gpus": world,

@@ -26,7 +26,8 @@ ROCM = Path(os.environ.get("ROCM_PATH", "/opt/rocm"))
 ARCH = os.environ.get("DASH_GPU_ARCH", "gfx950")
 
 HOST_SOURCES = ["core.cpp", "gadgets.cpp", "garbler.cpp", "evaluator.cpp", "serialize.cpp", "onnx.cpp", "dataloader.cpp", "bind.cpp"]
-HIP_SOURCES = ["hip/runtime.hip", "hip/kernels_label.hip", "hip/kernels_gemm.hip", "hip/kernels_gadget.hip"]
+HIP_SOURCES = ["hip/runtime.hip", "hip/kernels_label.hip", "hip/kernels_gemm.hip", "hip/kernels_gadget.hip",
+               "hip/garble_gpu.hip"]
 
 
 def ext_suffix() -> str:

@@ -254,17 +254,18 @@ PYBIND11_MODULE(_dash_native, m) {
                  return std::make_shared<Garbler>(crt, mrs, std::string(seed), max_mod);
              }),
              py::arg("crt"), py::arg("mrs"), py::arg("seed"), py::arg("max_mod") = 0)
-        .def("garble", [](Garbler& g, const py::list& layers, std::vector<i64> in_dims, int nthreads) {
+        .def("garble", [](Garbler& g, const py::list& layers, std::vector<i64> in_dims, int nthreads, int device) {
             auto specs = specs_from_py(layers);
             GarbleOptions o;
             o.nthreads = nthreads;
+            o.device = device;
             GarbledModel gm;
             {
                 py::gil_scoped_release rel;
                 gm = g.garble(specs, in_dims, o);
             }
             return std::make_shared<GarbledModel>(std::move(gm));
-        }, py::arg("layers"), py::arg("in_dims"), py::arg("nthreads") = 0)
+        }, py::arg("layers"), py::arg("in_dims"), py::arg("nthreads") = 0, py::arg("device") = -1)
         .def("layer_ms", [](const Garbler& g) { return g.layer_ms(); })
         .def("encode", [](const Garbler& g, py::array_t<i64, py::array::c_style | py::array::forcecast> x) {
             std::vector<i64> v(x.data(), x.data() + x.size());

@@ -11,6 +11,7 @@
 #include <chrono>
 
 #include "layers.h"
+#include "hip/gpu_garbler.h"
 
 namespace dash {
 
@@ -157,6 +158,7 @@ Garbler::Garbler(const std::vector<int>& crt, const std::vector<int>& mrs, const
     DASH_CHECK(!crt_.empty(), "empty CRT base");
     DASH_CHECK(seed16.size() == 16, "garbler seed must be 16 bytes");
     prg_ = Prg(reinterpret_cast<const uint8_t*>(seed16.data()));
+    seed_ = seed16;
     for (int p : crt_) M_ *= p;
     max_mod_ = max_mod;
 }
@@ -291,6 +293,9 @@ GarbledModel Garbler::garble(const std::vector<LayerSpec>& layers, const std::ve
         std::memcpy(z.ptr<comp_t>(), Z_.lab[p].data(), sizeof(comp_t) * n);
         m.consts["Z." + std::to_string(p)] = z;
     }
+
+    std::unique_ptr<GpuGarbler> gpu;
+    if (opt.device >= 0) gpu.reset(new GpuGarbler(crt_, mrs_, seed_, R_, Z_, opt.device));
 
     // Input base labels
     i64 N = 1;
@@ -503,7 +508,9 @@ GarbledModel Garbler::garble(const std::vector<LayerSpec>& layers, const std::ve
                 ReluTables t = make_relu_tables(sp, Nin, sum_crt, k);
                 CrtLabels nxt;
                 for (int j = 0; j < k; ++j) nxt.emplace_back(crt_[j], Nin);
-                parallel_for(Nin, [&](i64 b0, i64 b1) {
+                if (gpu) {
+                    gpu->sign_layer(L, sp, cur, t.approx, t.cast1, t.cast2, t.sign, nxt, &crt_, &prefix, &t.g, &t.e);
+                } else parallel_for(Nin, [&](i64 b0, i64 b1) {
                     std::vector<const comp_t*> x(k);
                     std::vector<comp_t*> y(k);
                     for (i64 e = b0; e < b1; ++e) {
@@ -526,7 +533,9 @@ GarbledModel Garbler::garble(const std::vector<LayerSpec>& layers, const std::ve
                     c2(DType::u128, {Nin, std::max<i64>(sp.n_cast, 1)}), sg(DType::u128, {Nin, sp.n_sign});
                 CrtLabels nxt;
                 for (int j = 0; j < k; ++j) nxt.emplace_back(crt_[j], Nin);
-                parallel_for(Nin, [&](i64 b0, i64 b1) {
+                if (gpu) {
+                    gpu->sign_layer(L, sp, cur, ap, c1, c2, sg, nxt, nullptr, nullptr, nullptr, nullptr);
+                } else parallel_for(Nin, [&](i64 b0, i64 b1) {
                     std::vector<const comp_t*> x(k);
                     std::vector<comp_t*> y(k);
                     for (i64 e = b0; e < b1; ++e) {
@@ -578,7 +587,9 @@ GarbledModel Garbler::garble(const std::vector<LayerSpec>& layers, const std::ve
                     } else {
                         be = Array(DType::u128, {Nin, P.n_be});
                     }
-                    parallel_for(Nin, [&](i64 b0, i64 b1) {
+                    if (gpu && P.sign_be) {
+                        gpu->rescale_legacy_iter(L, static_cast<int>(it), P, cur, up_base, dn, tr, ap, c1, c2, sg);
+                    } else parallel_for(Nin, [&](i64 b0, i64 b1) {
                         std::vector<comp_t*> Lp(k);
                         for (i64 e = b0; e < b1; ++e) {
                             for (int j = 0; j < k; ++j) Lp[j] = cur[j].at(e);

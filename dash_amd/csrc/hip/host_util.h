@@ -1,0 +1,114 @@
+// Host-side helpers shared by the HIP translation units: error checking,
+// AES T-table / round-key images and modulus constants for the device codecs.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "../core.h"
+#include "dev.h"
+
+namespace dash {
+
+#define HIPCHECK(x)                                                                                      \
+    do {                                                                                                 \
+        hipError_t e_ = (x);                                                                             \
+        if (e_ != hipSuccess)                                                                            \
+            throw std::runtime_error(std::string("HIP error: ") + hipGetErrorString(e_) + " at " + __FILE__ + \
+                                     ":" + std::to_string(__LINE__));                                    \
+    } while (0)
+
+namespace hostutil {
+
+// --------------------------------------------------------------- AES tables
+inline uint8_t gmul(uint8_t a, uint8_t b) {
+    uint8_t r = 0;
+    while (b) {
+        if (b & 1) r ^= a;
+        a = static_cast<uint8_t>((a << 1) ^ ((a & 0x80) ? 0x1b : 0));
+        b >>= 1;
+    }
+    return r;
+}
+inline std::vector<uint32_t> make_te0() {
+    // S-box from the GF(2^8) inverse and the AES affine map
+    uint8_t sbox[256];
+    for (int x = 0; x < 256; ++x) {
+        uint8_t inv = 0;
+        if (x)
+            for (int y = 1; y < 256; ++y)
+                if (gmul(static_cast<uint8_t>(x), static_cast<uint8_t>(y)) == 1) {
+                    inv = static_cast<uint8_t>(y);
+                    break;
+                }
+        uint8_t s = inv;
+        uint8_t r = s;
+        for (int i = 0; i < 4; ++i) {
+            r = static_cast<uint8_t>((r << 1) | (r >> 7));
+            s ^= r;
+        }
+        sbox[x] = static_cast<uint8_t>(s ^ 0x63);
+    }
+    std::vector<uint32_t> te(256);
+    for (int x = 0; x < 256; ++x) {
+        uint8_t s = sbox[x];
+        te[x] = (static_cast<uint32_t>(gmul(s, 2)) << 24) | (static_cast<uint32_t>(s) << 16) |
+                (static_cast<uint32_t>(s) << 8) | gmul(s, 3);
+    }
+    return te;
+}
+inline std::vector<uint32_t> fixed_round_key_words() {
+    uint8_t rk[176];
+    aes_round_key_bytes(fixed_key(), rk);
+    std::vector<uint32_t> w(44);
+    for (int i = 0; i < 44; ++i)
+        w[i] = (static_cast<uint32_t>(rk[4 * i]) << 24) | (static_cast<uint32_t>(rk[4 * i + 1]) << 16) |
+               (static_cast<uint32_t>(rk[4 * i + 2]) << 8) | rk[4 * i + 3];
+    return w;
+}
+
+inline dev::ModC make_modc(int q) {
+    dev::ModC m{};
+    m.q = q;
+    m.n = nr_comps(q);
+    if ((q & (q - 1)) == 0) {
+        int b = 0;
+        while ((1 << b) < q) ++b;
+        m.bits = b;
+        m.c = 1;
+        m.D = q;
+        return m;
+    }
+    uint64_t D = q;
+    int c = 1;
+    while (D * static_cast<uint64_t>(q) < (1ull << 32)) {
+        D *= q;
+        ++c;
+    }
+    m.c = c;
+    m.D = static_cast<uint32_t>(D);
+    m.mD = static_cast<uint64_t>((static_cast<u128>(1) << 64) / D);
+    m.mq = static_cast<uint32_t>((1ull << 32) / static_cast<uint64_t>(q));
+    return m;
+}
+
+}  // namespace
+
+
+// AES-128 round keys of an arbitrary key as big-endian column words (device layout)
+inline std::vector<uint32_t> round_key_words(const uint8_t key16[16]) {
+    AesKey k;
+    aes_expand(key16, k);
+    uint8_t rk[176];
+    aes_round_key_bytes(k, rk);
+    std::vector<uint32_t> w(44);
+    for (int i = 0; i < 44; ++i)
+        w[i] = (static_cast<uint32_t>(rk[4 * i]) << 24) | (static_cast<uint32_t>(rk[4 * i + 1]) << 16) |
+               (static_cast<uint32_t>(rk[4 * i + 2]) << 8) | rk[4 * i + 3];
+    return w;
+}
+
+}  // namespace dash

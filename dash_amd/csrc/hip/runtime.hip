@@ -12,6 +12,7 @@
 #include <functional>
 
 #include "../layers.h"
+#include "host_util.h"
 #include "launch.h"
 
 #include <rocprofiler-sdk-roctx/roctx.h>
@@ -21,89 +22,7 @@ namespace py = pybind11;
 namespace dash {
 using namespace dev;
 
-#define HIPCHECK(x)                                                                                      \
-    do {                                                                                                 \
-        hipError_t e_ = (x);                                                                             \
-        if (e_ != hipSuccess)                                                                            \
-            throw std::runtime_error(std::string("HIP error: ") + hipGetErrorString(e_) + " at " + __FILE__ + \
-                                     ":" + std::to_string(__LINE__));                                    \
-    } while (0)
-
-namespace {
-
-// --------------------------------------------------------------- AES tables
-uint8_t gmul(uint8_t a, uint8_t b) {
-    uint8_t r = 0;
-    while (b) {
-        if (b & 1) r ^= a;
-        a = static_cast<uint8_t>((a << 1) ^ ((a & 0x80) ? 0x1b : 0));
-        b >>= 1;
-    }
-    return r;
-}
-std::vector<uint32_t> make_te0() {
-    // S-box from the GF(2^8) inverse and the AES affine map
-    uint8_t sbox[256];
-    for (int x = 0; x < 256; ++x) {
-        uint8_t inv = 0;
-        if (x)
-            for (int y = 1; y < 256; ++y)
-                if (gmul(static_cast<uint8_t>(x), static_cast<uint8_t>(y)) == 1) {
-                    inv = static_cast<uint8_t>(y);
-                    break;
-                }
-        uint8_t s = inv;
-        uint8_t r = s;
-        for (int i = 0; i < 4; ++i) {
-            r = static_cast<uint8_t>((r << 1) | (r >> 7));
-            s ^= r;
-        }
-        sbox[x] = static_cast<uint8_t>(s ^ 0x63);
-    }
-    std::vector<uint32_t> te(256);
-    for (int x = 0; x < 256; ++x) {
-        uint8_t s = sbox[x];
-        te[x] = (static_cast<uint32_t>(gmul(s, 2)) << 24) | (static_cast<uint32_t>(s) << 16) |
-                (static_cast<uint32_t>(s) << 8) | gmul(s, 3);
-    }
-    return te;
-}
-std::vector<uint32_t> fixed_round_key_words() {
-    uint8_t rk[176];
-    aes_round_key_bytes(fixed_key(), rk);
-    std::vector<uint32_t> w(44);
-    for (int i = 0; i < 44; ++i)
-        w[i] = (static_cast<uint32_t>(rk[4 * i]) << 24) | (static_cast<uint32_t>(rk[4 * i + 1]) << 16) |
-               (static_cast<uint32_t>(rk[4 * i + 2]) << 8) | rk[4 * i + 3];
-    return w;
-}
-
-ModC make_modc(int q) {
-    ModC m{};
-    m.q = q;
-    m.n = nr_comps(q);
-    if ((q & (q - 1)) == 0) {
-        int b = 0;
-        while ((1 << b) < q) ++b;
-        m.bits = b;
-        m.c = 1;
-        m.D = q;
-        return m;
-    }
-    uint64_t D = q;
-    int c = 1;
-    while (D * static_cast<uint64_t>(q) < (1ull << 32)) {
-        D *= q;
-        ++c;
-    }
-    m.c = c;
-    m.D = static_cast<uint32_t>(D);
-    m.mD = static_cast<uint64_t>((static_cast<u128>(1) << 64) / D);
-    m.mq = static_cast<uint32_t>((1ull << 32) / static_cast<uint64_t>(q));
-    return m;
-}
-
-}  // namespace
+using namespace hostutil;
 
 // ---------------------------------------------------------------------------
 class HipEvaluator {

@@ -96,6 +96,7 @@ struct Decoder {
 
 struct GarbleOptions {
     int nthreads = 0;
+    int device = -1;  // >= 0: garble ReLU / Sign / legacy rescale layers on this GPU
 };
 
 class Garbler {
@@ -124,6 +125,7 @@ class Garbler {
     i64 M_ = 1;
     int max_mod_ = 0;
     Prg prg_;
+    std::string seed_;
     LabelBank R_, Z_;
     CrtLabels in_base_;
     Decoder dec_;

@@ -28,7 +28,8 @@ Labels = list  # list[(modulus, np.ndarray int16 [N, n_p])]
 
 class GarbledCircuit:
     def __init__(self, circuit: Circuit, crt: Union[int, Sequence[int]], mrs: Union[None, float, Sequence[int]] = None,
-                 max_modulus: int = 0, seed: Optional[bytes] = None, garble_me: bool = True, nthreads: int = 0):
+                 max_modulus: int = 0, seed: Optional[bytes] = None, garble_me: bool = True, nthreads: int = 0,
+                 device: Optional[int] = None):
         self.circuit = circuit
         self.crt_base = first_primes(crt) if isinstance(crt, int) else [int(p) for p in crt]
         if mrs is None:
@@ -40,6 +41,8 @@ class GarbledCircuit:
         self.crt_modulus = _crt_mod(self.crt_base)
         self.seed = seed if seed is not None else os.urandom(16)
         self.nthreads = nthreads
+        # device: garble the ReLU / Sign / legacy-rescale layers on this GPU (bit-identical to the CPU garbler)
+        self.device = -1 if device is None else int(device)
         self._n = native()
         self.garbler = self._n.Garbler(self.crt_base, self.mrs_base, self.seed, int(max_modulus))
         self.model = None
@@ -52,7 +55,7 @@ class GarbledCircuit:
     def garble(self):
         specs = self.circuit.garble_specs()
         t = time.perf_counter()
-        self.model = self.garbler.garble(specs, list(self.circuit.input_dims), self.nthreads)
+        self.model = self.garbler.garble(specs, list(self.circuit.input_dims), self.nthreads, self.device)
         self.garbling_time_s = time.perf_counter() - t
         self.decoder = self.garbler.decoder()
         return self.model

@@ -1,0 +1,47 @@
+#!/usr/bin/env python
+"""Offline-phase timing: garble one GC on the host vs with the GPU sign-gadget garbler.
+
+  python scripts/garble_bench.py --model MODEL_F_MINIONN_POOL_REPL --reps 2
+Prints one JSON line per mode with seconds per GC and per-layer milliseconds, and checks
+that the device-garbled model is byte-identical to the host-garbled one.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+from dash_amd.garbling import GarbledCircuit  # noqa: E402
+from dash_amd.ir.quant import QuantizationMethod as Q  # noqa: E402
+from dash_amd.models import build_circuit  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--model", default="MODEL_F_MINIONN_POOL_REPL")
+    ap.add_argument("--k", type=int, default=7)
+    ap.add_argument("--l", type=int, default=5)
+    ap.add_argument("--reps", type=int, default=2)
+    ap.add_argument("--device", type=int, default=0)
+    args = ap.parse_args()
+    c = build_circuit(args.model, Q.ScaleQuant, args.l, seed=0)
+    seed = bytes(range(16))
+    blobs = {}
+    for mode, dev in (("gpu", args.device), ("cpu", None)):
+        times = []
+        gc = None
+        for _ in range(args.reps):
+            t = time.perf_counter()
+            gc = GarbledCircuit(c, args.k, 100.0, seed=seed, device=dev)
+            times.append(time.perf_counter() - t)
+        blobs[mode] = gc.model.serialize()
+        print(json.dumps({"mode": mode, "model": args.model, "s_per_gc": round(min(times), 3),
+                          "layer_ms": [round(x, 1) for x in gc.garbling_layer_ms()]}), flush=True)
+    print(json.dumps({"identical": blobs["gpu"] == blobs["cpu"]}), flush=True)
+    assert blobs["gpu"] == blobs["cpu"]
+
+
+if __name__ == "__main__":
+    main()

@@ -207,3 +207,29 @@ def test_projection_shortcut_in_src():
     c, xs = _shortcut_block()
     k = c.infer_crt_base_size(xs)
     _check(c, k, 100.0, xs)
+
+
+@pytest.mark.parametrize("name", ["relu", "sign", "rescale", "model_b", "minionn_head"])
+def test_gpu_garbler_bit_identical(name):
+    """GPU garbler (ReLU / Sign / legacy rescale on the device) == CPU garbler, byte for byte."""
+    from dash_amd.ir.circuit import Circuit
+    from dash_amd.ir.layers import Relu, Rescale, Sign
+    from dash_amd.ir.quant import QuantizationMethod as Q
+    from dash_amd.models import build_circuit
+
+    if name == "relu":
+        c, k = Circuit([Relu((300,))]), 8
+    elif name == "sign":
+        c, k = Circuit([Sign((300,))]), 7
+    elif name == "rescale":
+        c, k = Circuit([Rescale(2, (300,))]), 7
+    elif name == "model_b":
+        c, k = build_circuit("MODEL_B_POOL_REPL", Q.ScaleQuant, 3, seed=1), 8
+    else:
+        full = build_circuit("MODEL_F_MINIONN_POOL_REPL", Q.ScaleQuant, 5, seed=0)
+        c, k = Circuit(full.layers[:3]), 7  # conv, rescale(l=5), relu at full size
+    seed = bytes(range(16))
+    cpu = GarbledCircuit(c, k, 100.0, seed=seed)
+    gpu = GarbledCircuit(c, k, 100.0, seed=seed, device=0)
+    assert gpu.model.serialize() == cpu.model.serialize()
+    assert gpu.decoder.serialize() == cpu.decoder.serialize()

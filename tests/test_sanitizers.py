@@ -18,7 +18,8 @@ SOURCES = [str(CSRC / f) for f in ("core.cpp", "gadgets.cpp", "garbler.cpp", "ev
 @pytest.mark.skipif(CXX is None, reason="clang++ not available")
 def test_host_sanitizers(tmp_path):
     common = ["-std=c++17", "-O1", "-g", "-fno-omit-frame-pointer", "-maes", "-msse4.2", "-mavx2", "-mpclmul",
-              f"-I{CSRC}", str(ROOT / "tests" / "native" / "sanitize_main.cpp"), *SOURCES, "-lpthread"]
+              f"-I{CSRC}", str(ROOT / "tests" / "native" / "sanitize_main.cpp"),
+              str(ROOT / "tests" / "native" / "gpu_garbler_stub.cpp"), *SOURCES, "-lpthread"]
     builds = {"asan": ["-fsanitize=address,undefined", "-fno-sanitize-recover=undefined"],
               "tsan": ["-fsanitize=thread"]}
     procs = {k: subprocess.Popen([CXX, *flags, *common, "-o", str(tmp_path / k)], stdout=subprocess.PIPE,
