@@ -48,6 +48,9 @@ def main() -> None:
     ap.add_argument("--profile", action="store_true", help="print per-layer GPU times")
     ap.add_argument("--threads", type=int, default=0)
     ap.add_argument("--verify", type=int, default=1)
+    ap.add_argument("--garble-device", type=int, default=int(os.environ.get("DASH_BENCH_GARBLE_DEVICE", "1")),
+                    help="garble the sign-gadget layers on this rank's GPU (byte-identical to the host garbler; "
+                         "keeps the offline phase off the shared host CPUs when 8 ranks garble at once)")
     args = ap.parse_args()
 
     import torch
@@ -91,7 +94,7 @@ def main() -> None:
     for b in range(B):
         seed = hashlib.sha256(f"dash-bench/{rank}/{b}/{os.getpid()}".encode()).digest()[:16]
         t = time.perf_counter()
-        gc = GarbledCircuit(circuit, cfg["crt"], cfg["mrs"], seed=seed)
+        gc = GarbledCircuit(circuit, cfg["crt"], cfg["mrs"], seed=seed, device=device if args.garble_device else None)
         garble_s += time.perf_counter() - t
         t = time.perf_counter()
         g = b // per
@@ -158,10 +161,11 @@ def main() -> None:
     total_inf = world * B * args.steps
     value = total_inf / elapsed
     ms_step = 1000.0 * elapsed / args.steps
-    prof = None
+    prof = op_ms = None
     if args.profile:
         step(0)
         prof = {k: round(v, 3) for k, v in evs[0].layer_times().items()}
+        op_ms = [[n, round(v, 4)] for n, v in evs[0].op_times()]
     if rank == 0:
         out = {
             "metric": ("online garbled inferences/sec (MiniONN CIFAR-10 CNN)" if model == "MODEL_F_MINIONN_POOL_REPL"
@@ -197,6 +201,7 @@ def main() -> None:
         }
         if prof:
             out["layer_ms"] = prof
+            out["op_ms"] = op_ms
         print(json.dumps(out), flush=True)
     shutdown(ctx)
 

@@ -137,26 +137,43 @@ struct CompressFwd {
     }
 };
 
-// compress of a label stored component-major: L[i * stride] (reverse Horner)
+// Label columns are component-major (stride N). A component loop whose
+// iteration waits for its own load pays one HBM round trip per component
+// (the compiler does not hoist loads across a runtime-trip-count loop, nor
+// past a store to the same column): stage kChunk loads first, then consume.
+constexpr int kChunk = 16;
+
+// dst[c * stride] = f(c, src[c * stride]) for c < n, kChunk loads per round
+// trip (dst may alias src; f is called in component order)
+template <class F>
+__device__ __forceinline__ void col_map(const int16_t* src, int16_t* dst, long stride, int n, F&& f) {
+    for (int i0 = 0; i0 < n; i0 += kChunk) {
+        int16_t v[kChunk];
+#pragma unroll
+        for (int u = 0; u < kChunk; ++u)
+            if (i0 + u < n) v[u] = src[static_cast<long>(i0 + u) * stride];
+#pragma unroll
+        for (int u = 0; u < kChunk; ++u)
+            if (i0 + u < n) dst[static_cast<long>(i0 + u) * stride] = f(i0 + u, v[u]);
+    }
+}
+
+// compress of a label stored component-major: L[i * stride], streamed from
+// the least significant component, kChunk loads in flight per round trip
 __device__ __forceinline__ u128 compress_cm(const int16_t* L, long stride, const ModC& m) {
     const int n = m.n;
-    if (m.bits) {
-        u128 C = 0;
-        for (int i = n - 1; i >= 0; --i) C = (C << m.bits) | static_cast<u128>(static_cast<uint16_t>(L[i * stride]));
-        return C;
+    CompressFwd cf;
+    cf.init();
+    for (int i0 = 0; i0 < n; i0 += kChunk) {
+        uint16_t v[kChunk];
+#pragma unroll
+        for (int u = 0; u < kChunk; ++u)
+            if (i0 + u < n) v[u] = static_cast<uint16_t>(L[static_cast<long>(i0 + u) * stride]);
+#pragma unroll
+        for (int u = 0; u < kChunk; ++u)
+            if (i0 + u < n) cf.push(v[u], m);
     }
-    int first = n % m.c;
-    if (first == 0) first = m.c;
-    int i = n - 1;
-    uint32_t v = 0;
-    for (int t = 0; t < first; ++t, --i) v = v * m.q + static_cast<uint16_t>(L[i * stride]);
-    u128 C = v;
-    while (i >= 0) {
-        v = 0;
-        for (int t = 0; t < static_cast<int>(m.c); ++t, --i) v = v * m.q + static_cast<uint16_t>(L[i * stride]);
-        C = C * static_cast<u128>(m.D) + v;
-    }
-    return C;
+    return cf.finish();
 }
 
 // P mod q (color of a compressed label)

@@ -45,7 +45,52 @@ static inline dim3 grid_aes(int64_t n, int bs, int y, int z) {
     const AesCtx aes = aes_ctx(lds_aes, rk)
 
 // ---------------------------------------------------------------------------
-// Phase A: approximate residues. grid (ceil(N/256), k, B)
+// Phase A tail: the casts Z_{m_d} -> Z_{(k+1) m_d} of residue j's approx
+// labels for every digit d >= 1. They do not depend on the carry, so they run
+// here, in the lane that just produced the approx labels (still in registers):
+// all cast gathers are issued before the paired AES. mrsP[b][j][d] receives
+// the approx label for d = 0 and its cast for d >= 1 (phase B1 only sums).
+// P[d] = approx label of digit d for d < TM; digits >= TM (t > TM) are
+// recomputed from the approx row TA at color `col` (key H).
+template <int TM>
+__device__ __forceinline__ void approx_casts_out(const AesCtx& aes, const SignArgs& a, const ModC* mc, int j, int b,
+                                                 int64_t e, const u128 (&P)[TM], const u128* TA, uint32_t col, u128 H) {
+    const int64_t N = a.N;
+    const int t = a.t;
+    const u128* T1 = a.cast1 + (static_cast<int64_t>(b) * N + e) * a.n_cast;
+    u128* out = a.mrsP + (static_cast<int64_t>(b) * a.crt.k + j) * t * N + e;
+    out[0] = P[0];
+    u128 tt[TM];
+#pragma unroll
+    for (int d = 1; d < TM; ++d)
+        if (d < t) {
+            const int m = a.mrs[d];
+            tt[d] = T1[a.c1off[d] + static_cast<int64_t>(j) * m + u128_mod(P[d], mc[m])];
+        }
+#pragma unroll
+    for (int d = 1; d < TM; d += 2) {
+        if (d < t) {
+            const bool two = (d + 1 < TM) && (d + 1 < t);
+            const u128 PB = (d + 1 < TM) ? P[(d + 1 < TM) ? d + 1 : d] : static_cast<u128>(0);
+            u128 HA, HB = 0;
+            if (two)
+                aes_encrypt2(aes, P[d], PB, HA, HB);
+            else
+                HA = aes_encrypt(aes, P[d]);
+            out[static_cast<int64_t>(d) * N] = tt[d] - HA;
+            if (two) out[static_cast<int64_t>(d + 1) * N] = tt[(d + 1 < TM) ? d + 1 : d] - HB;
+        }
+    }
+    for (int d = TM; d < t; ++d) {
+        const int m = a.mrs[d];
+        const u128 Pd = TA[col * t + d] - H;
+        const u128 Td = T1[a.c1off[d] + static_cast<int64_t>(j) * m + u128_mod(Pd, mc[m])];
+        out[static_cast<int64_t>(d) * N] = Td - aes_encrypt(aes, Pd);
+    }
+}
+
+// Phase A: approximate residues + their casts. grid (x, k, B)
+template <int TM>
 __global__ __launch_bounds__(512, 4) void k_sign_approx(SignArgs a, Act x, const ModC* mc, const uint32_t* te0,
                                                      const uint32_t* rk) {
     AES_PROLOGUE(te0, rk);
@@ -53,96 +98,64 @@ __global__ __launch_bounds__(512, 4) void k_sign_approx(SignArgs a, Act x, const
     const int64_t N = a.N;
     for (int64_t e = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; e < N;
          e += static_cast<int64_t>(gridDim.x) * blockDim.x) {
-    const int p = a.crt.p[j];
-    const ModC m = mc[p];
-    const int16_t* L = x.p[j] + static_cast<int64_t>(b) * m.n * N + e;
-    const uint32_t col = static_cast<uint16_t>(L[0]) % static_cast<uint32_t>(p);
-    const u128* T = a.approx + (static_cast<int64_t>(b) * N + e) * a.n_approx + static_cast<int64_t>(a.t) * a.crt.prefix[j];
-    // issue the table gathers first: their HBM latency hides under the AES
-    u128 ent[8];
+        const int p = a.crt.p[j];
+        const ModC m = mc[p];
+        const int16_t* L = x.p[j] + static_cast<int64_t>(b) * m.n * N + e;
+        const uint32_t col = static_cast<uint16_t>(L[0]) % static_cast<uint32_t>(p);
+        const u128* T =
+            a.approx + (static_cast<int64_t>(b) * N + e) * a.n_approx + static_cast<int64_t>(a.t) * a.crt.prefix[j];
+        // issue the table gathers first: their HBM latency hides under the AES
+        u128 P[TM];
 #pragma unroll
-    for (int d = 0; d < 8; ++d)
-        if (d < a.t) ent[d] = T[col * a.t + d];
-    const u128 C = compress_cm(L, N, m);
-    const u128 H = aes_encrypt(aes, C);
-    const int64_t bke = (static_cast<int64_t>(b) * a.crt.k + j) * N + e;
-    if (a.hx) {
-        a.hx[bke] = H;
-        a.colx[bke] = static_cast<uint16_t>(col);
-    }
-    u128* out = a.mrsP + (static_cast<int64_t>(b) * a.crt.k + j) * a.t * N + e;
+        for (int d = 0; d < TM; ++d)
+            if (d < a.t) P[d] = T[col * a.t + d];
+        const u128 C = compress_cm(L, N, m);
+        const u128 H = aes_encrypt(aes, C);
+        const int64_t bke = (static_cast<int64_t>(b) * a.crt.k + j) * N + e;
+        if (a.hx) {
+            a.hx[bke] = H;
+            a.colx[bke] = static_cast<uint16_t>(col);
+        }
 #pragma unroll
-    for (int d = 0; d < 8; ++d)
-        if (d < a.t) out[static_cast<int64_t>(d) * N] = ent[d] - H;
-    for (int d = 8; d < a.t; ++d) out[static_cast<int64_t>(d) * N] = T[col * a.t + d] - H;
+        for (int d = 0; d < TM; ++d)
+            if (d < a.t) P[d] -= H;
+        approx_casts_out<TM>(aes, a, mc, j, b, e, P, T, col, H);
     }
 }
 
 // ---------------------------------------------------------------------------
-// Phase B1: per MRS digit d >= 1, the sum over residues j of the casts
-// Z_{m_d} -> Z_{(k+1) m_d} of the approx labels; for d = 0 the plain sum of
-// the approx labels mod m_0. None of this depends on the carry, so it runs
-// fully parallel over (GC, digit, element), with paired AES.
-// grid (x, t, B): blockIdx.y = t-1 is digit 0, otherwise digit y+1.
+// Phase B1: per MRS digit, the component-wise sum over residues j of the
+// phase-A outputs (casts mod (k+1) m_d for d >= 1, approx labels mod m_0 for
+// d = 0). No AES and no LDS, so it runs at full occupancy.
+// grid (ceil(N/256), t, B): blockIdx.y = t-1 is digit 0, otherwise digit y+1.
 template <int MAXN>
-__global__ __launch_bounds__(512, 4) void k_sign_castsum(SignArgs a, const ModC* mc, const uint32_t* te0,
-                                                      const uint32_t* rk) {
-    AES_PROLOGUE(te0, rk);
+__global__ __launch_bounds__(256) void k_sign_castsum(SignArgs a, const ModC* mc) {
     const int b = blockIdx.z;
     const int k = a.crt.k, t = a.t;
     const int d = (static_cast<int>(blockIdx.y) == t - 1) ? 0 : static_cast<int>(blockIdx.y) + 1;
     const int64_t N = a.N;
+    const int64_t e = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (e >= N) return;
     const int m = a.mrs[d];
     const int mo = d ? (k + 1) * m : m;
-    const ModC Mm = mc[m];
     const ModC Mo = mc[mo];
-    int64_t c1 = 0;
-    for (int dd = t - 1; dd > d; --dd) c1 += static_cast<int64_t>(k + 1) * a.mrs[dd];
-    for (int64_t e = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; e < N;
-         e += static_cast<int64_t>(gridDim.x) * blockDim.x) {
-        const u128* P0 = a.mrsP + static_cast<int64_t>(b) * k * t * N + e;
-        int32_t acc[MAXN];
+    const u128* P0 = a.mrsP + (static_cast<int64_t>(b) * k * t + d) * N + e;
+    int32_t acc[MAXN];
 #pragma unroll
-        for (int i = 0; i < MAXN; ++i) acc[i] = 0;
-        if (d == 0) {
-            for (int j = 0; j < k; ++j) {
-                DigitStream s0;
-                s0.init(P0[static_cast<int64_t>(j) * t * N]);
-#pragma unroll
-                for (int i = 0; i < MAXN; ++i)
-                    if (i < static_cast<int>(Mo.n)) acc[i] += static_cast<int32_t>(s0.next(Mo));
-            }
-        } else {
-            const u128* T1 = a.cast1 + (static_cast<int64_t>(b) * N + e) * a.n_cast + c1;
-            for (int j = 0; j < k; j += 2) {
-                const bool two = j + 1 < k;
-                const u128 keyA = P0[(static_cast<int64_t>(j) * t + d) * N];
-                const u128 keyB = two ? P0[(static_cast<int64_t>(j + 1) * t + d) * N] : static_cast<u128>(0);
-                const uint32_t colA = u128_mod(keyA, Mm);
-                const uint32_t colB = two ? u128_mod(keyB, Mm) : 0u;
-                const u128 TA = T1[static_cast<int64_t>(j) * m + colA];
-                const u128 TB = two ? T1[static_cast<int64_t>(j + 1) * m + colB] : static_cast<u128>(0);
-                u128 HA, HB = 0;
-                if (two)
-                    aes_encrypt2(aes, keyA, keyB, HA, HB);
-                else
-                    HA = aes_encrypt(aes, keyA);
-                DigitStream sa, sb;
-                sa.init(TA - HA);
-                sb.init(TB - HB);
-#pragma unroll
-                for (int i = 0; i < MAXN; ++i)
-                    if (i < static_cast<int>(Mo.n)) {
-                        acc[i] += static_cast<int32_t>(sa.next(Mo));
-                        if (two) acc[i] += static_cast<int32_t>(sb.next(Mo));
-                    }
-            }
-        }
-        int16_t* S = a.csum + ((static_cast<int64_t>(b) * t + d) * kCsumComps) * N + e;
+    for (int i = 0; i < MAXN; ++i) acc[i] = 0;
+    u128 nk = P0[0];
+    for (int j = 0; j < k; ++j) {
+        DigitStream s;
+        s.init(nk);
+        if (j + 1 < k) nk = P0[static_cast<int64_t>(j + 1) * t * N];
 #pragma unroll
         for (int i = 0; i < MAXN; ++i)
-            if (i < static_cast<int>(Mo.n)) S[i * N] = static_cast<int16_t>(acc[i] % mo);
+            if (i < static_cast<int>(Mo.n)) acc[i] += static_cast<int32_t>(s.next(Mo));
     }
+    int16_t* S = a.csum + ((static_cast<int64_t>(b) * t + d) * kCsumComps) * N + e;
+#pragma unroll
+    for (int i = 0; i < MAXN; ++i)
+        if (i < static_cast<int>(Mo.n)) S[i * N] = static_cast<int16_t>(acc[i] % mo);
 }
 
 // ---------------------------------------------------------------------------
@@ -272,13 +285,21 @@ __global__ __launch_bounds__(256) void k_relu_mult(SignArgs a, Act x, Act y, con
     DigitStream sg, se;
     sg.init(G);
     se.init(E);
-    for (int i = 0; i < static_cast<int>(m.n); ++i) {
-        const int32_t g = static_cast<int32_t>(sg.next(m));
-        const int32_t ev = static_cast<int32_t>(se.next(m));
-        const int32_t xi = X[i * N];
-        int32_t v = (ev + ypr * xi - g) % p;
-        if (v < 0) v += p;
-        Y[i * N] = static_cast<int16_t>(v);
+    const int n = static_cast<int>(m.n);
+    for (int i0 = 0; i0 < n; i0 += kChunk) {
+        int16_t xv[kChunk];
+#pragma unroll
+        for (int u = 0; u < kChunk; ++u)
+            if (i0 + u < n) xv[u] = X[(i0 + u) * N];
+#pragma unroll
+        for (int u = 0; u < kChunk; ++u)
+            if (i0 + u < n) {
+                const int32_t g = static_cast<int32_t>(sg.next(m));
+                const int32_t ev = static_cast<int32_t>(se.next(m));
+                int32_t v = (ev + ypr * xv[u] - g) % p;
+                if (v < 0) v += p;
+                Y[(i0 + u) * N] = static_cast<int16_t>(v);
+            }
     }
 }
 
@@ -295,22 +316,29 @@ __global__ __launch_bounds__(512, 4) void k_rescale_hash(Act x, int fi, int s, c
     const ModC m = mc[s];
     const int16_t* L = x.p[fi] + static_cast<int64_t>(b) * m.n * N + e;
     const int16_t* U = up + static_cast<int64_t>(b) * up_stride;
-    // compress of (L + up) mod s, reverse Horner
-    u128 C = 0;
+    // compress of (L + up) mod s, streamed from the least significant component
+    CompressFwd cf;
+    cf.init();
     uint32_t c0 = 0;
-    for (int i = static_cast<int>(m.n) - 1; i >= 0; --i) {
-        uint32_t d = static_cast<uint16_t>(L[i * N]);
-        if (add_up) {
-            d += static_cast<uint16_t>(U[i]);
-            if (d >= static_cast<uint32_t>(s)) d -= s;
-        }
-        if (m.bits)
-            C = (C << m.bits) | d;
-        else
-            C = C * static_cast<u128>(s) + d;
-        c0 = d;
+    const int n = static_cast<int>(m.n);
+    for (int i0 = 0; i0 < n; i0 += kChunk) {
+        uint16_t lv[kChunk];
+#pragma unroll
+        for (int u = 0; u < kChunk; ++u)
+            if (i0 + u < n) lv[u] = static_cast<uint16_t>(L[(i0 + u) * N]);
+#pragma unroll
+        for (int u = 0; u < kChunk; ++u)
+            if (i0 + u < n) {
+                uint32_t d = lv[u];
+                if (add_up) {
+                    d += static_cast<uint16_t>(U[i0 + u]);
+                    if (d >= static_cast<uint32_t>(s)) d -= s;
+                }
+                if (i0 + u == 0) c0 = d;
+                cf.push(d, m);
+            }
     }
-    h0[static_cast<int64_t>(b) * N + e] = aes_encrypt(aes, C);
+    h0[static_cast<int64_t>(b) * N + e] = aes_encrypt(aes, cf.finish());
     col0[static_cast<int64_t>(b) * N + e] = static_cast<uint16_t>(c0);
     }
 }
@@ -337,12 +365,21 @@ __global__ __launch_bounds__(256) void k_rescale_update(RescaleArgs a, Act x, co
     DigitStream s;
     s.init(P);
     const int32_t inv = a.inv[j];
-    for (int i = 0; i < static_cast<int>(m.n); ++i) {
-        int32_t v = L[i * N];
-        if (a.add_up) v += U[i];
-        v -= static_cast<int32_t>(s.next(m));
-        v = (v % p + p) % p;
-        L[i * N] = static_cast<int16_t>((v * inv) % p);
+    const int n = static_cast<int>(m.n);
+    for (int i0 = 0; i0 < n; i0 += kChunk) {
+        int16_t lv[kChunk];
+#pragma unroll
+        for (int u = 0; u < kChunk; ++u)
+            if (i0 + u < n) lv[u] = L[(i0 + u) * N];
+#pragma unroll
+        for (int u = 0; u < kChunk; ++u)
+            if (i0 + u < n) {
+                int32_t v = lv[u];
+                if (a.add_up) v += U[i0 + u];
+                v -= static_cast<int32_t>(s.next(m));
+                v = (v % p + p) % p;
+                L[(i0 + u) * N] = static_cast<int16_t>((v * inv) % p);
+            }
     }
 }
 
@@ -358,18 +395,30 @@ __global__ __launch_bounds__(256) void k_rescale_post(Act x, CrtInfo crt, int64_
     const ModC m = mc[p];
     int16_t* L = x.p[j] + static_cast<int64_t>(b) * m.n * N + e;
     const int16_t* D = down + static_cast<int64_t>(b) * lab_stride + lab_off[j];
+    const int n = static_cast<int>(m.n);
     if (j == 0 && signP) {
         DigitStream s;
         s.init(signP[static_cast<int64_t>(b) * N + e]);
-        for (int i = 0; i < static_cast<int>(m.n); ++i) {
+        for (int i = 0; i < n; ++i) {
             int32_t v = static_cast<int32_t>(s.next(m)) - D[i];
             L[i * N] = static_cast<int16_t>(v < 0 ? v + p : v);
         }
         return;
     }
-    for (int i = 0; i < static_cast<int>(m.n); ++i) {
-        int32_t v = L[i * N] - D[i];
-        L[i * N] = static_cast<int16_t>(v < 0 ? v + p : v);
+    for (int i0 = 0; i0 < n; i0 += kChunk) {
+        int16_t lv[kChunk], dv[kChunk];
+#pragma unroll
+        for (int u = 0; u < kChunk; ++u)
+            if (i0 + u < n) {
+                lv[u] = L[(i0 + u) * N];
+                dv[u] = D[i0 + u];
+            }
+#pragma unroll
+        for (int u = 0; u < kChunk; ++u)
+            if (i0 + u < n) {
+                const int32_t v = lv[u] - dv[u];
+                L[(i0 + u) * N] = static_cast<int16_t>(v < 0 ? v + p : v);
+            }
     }
 }
 
@@ -395,7 +444,9 @@ __global__ __launch_bounds__(512, 4) void k_rescale_hash_sign(const u128* signP,
     }
 }
 
-// grid (ceil(N/256), k, B)
+// grid (ceil(N/256), k, B); half-size load chunks (the t approx entries stay live)
+constexpr int kChunkUA = kChunk / 4;
+template <int TM>
 __global__ __launch_bounds__(512, 4) void k_rescale_update_approx(RescaleArgs r, SignArgs a, Act x, const int16_t* delta,
                                                                const u128* zh, const ModC* mc, const uint32_t* te0,
                                                                const uint32_t* rk) {
@@ -410,13 +461,13 @@ __global__ __launch_bounds__(512, 4) void k_rescale_update_approx(RescaleArgs r,
     const u128* TA = a.approx + be * a.n_approx + static_cast<int64_t>(a.t) * a.crt.prefix[j];
     u128 H;
     uint32_t col;
-    u128 ent[8];
+    u128 ent[TM];
     if (j == r.fi) {
         // factor residue is the zero label: constant key per GC
         H = zh[static_cast<int64_t>(b) * a.zc_stride + p];
         col = a.zcol[static_cast<int64_t>(b) * a.zc_stride + p];
 #pragma unroll
-        for (int d = 0; d < 8; ++d)
+        for (int d = 0; d < TM; ++d)
             if (d < a.t) ent[d] = TA[col * a.t + d];
     } else {
         const u128 Tt = r.trans[be * r.n_trans + static_cast<int64_t>(r.aidx[j]) * r.s + r.col0[be]];
@@ -429,29 +480,42 @@ __global__ __launch_bounds__(512, 4) void k_rescale_update_approx(RescaleArgs r,
         cf.init();
         const int32_t inv = r.inv[j];
         col = 0;
-        for (int i = 0; i < static_cast<int>(m.n); ++i) {
-            int32_t v = L[i * N] + Dl[i] - static_cast<int32_t>(s.next(m));
-            v %= p;
-            if (v < 0) v += p;
-            v = (v * inv) % p;
-            L[i * N] = static_cast<int16_t>(v);
-            cf.push(static_cast<uint32_t>(v), m);
-            if (i == 0) {
-                col = static_cast<uint32_t>(v);
+        const int n = static_cast<int>(m.n);
+        for (int i0 = 0; i0 < n; i0 += kChunkUA) {
+            int16_t lv[kChunkUA], dv[kChunkUA];
 #pragma unroll
-                for (int d = 0; d < 8; ++d)
-                    if (d < a.t) ent[d] = TA[col * a.t + d];
-            }
+            for (int u = 0; u < kChunkUA; ++u)
+                if (i0 + u < n) {
+                    lv[u] = L[(i0 + u) * N];
+                    dv[u] = Dl[i0 + u];
+                }
+#pragma unroll
+            for (int u = 0; u < kChunkUA; ++u)
+                if (i0 + u < n) {
+                    int32_t v = lv[u] + dv[u] - static_cast<int32_t>(s.next(m));
+                    v %= p;
+                    if (v < 0) v += p;
+                    v = (v * inv) % p;
+                    L[(i0 + u) * N] = static_cast<int16_t>(v);
+                    cf.push(static_cast<uint32_t>(v), m);
+                    if (i0 + u == 0) {
+                        col = static_cast<uint32_t>(v);
+#pragma unroll
+                        for (int d = 0; d < TM; ++d)
+                            if (d < a.t) ent[d] = TA[col * a.t + d];
+                    }
+                }
         }
         H = aes_encrypt(aes, cf.finish());
     }
-    u128* out = a.mrsP + (static_cast<int64_t>(b) * a.crt.k + j) * a.t * N + e;
 #pragma unroll
-    for (int d = 0; d < 8; ++d)
-        if (d < a.t) out[static_cast<int64_t>(d) * N] = ent[d] - H;
-    for (int d = 8; d < a.t; ++d) out[static_cast<int64_t>(d) * N] = TA[col * a.t + d] - H;
+    for (int d = 0; d < TM; ++d)
+        if (d < a.t) ent[d] -= H;
+    approx_casts_out<TM>(aes, a, mc, j, b, e, ent, TA, col, H);
     }
 }
+
+
 
 void launch_rescale_hash_sign(const u128* signP, const u128* du, int64_t N, int B, u128* h0, uint16_t* col0,
                               const AesGlobals& g, hipStream_t st) {
@@ -459,7 +523,12 @@ void launch_rescale_hash_sign(const u128* signP, const u128* du, int64_t N, int 
 }
 void launch_rescale_update_approx(const RescaleArgs& r, const SignArgs& a, const Act& x, const int16_t* delta,
                                   const u128* zh, int B, const ModC* mc, const AesGlobals& g, hipStream_t st) {
-    hipLaunchKernelGGL(k_rescale_update_approx, grid_aes(r.N, 512, r.crt.k, B), dim3(512), kAesLds, st, r, a, x, delta, zh, mc, g.te0, g.rk);
+    if (a.t <= 5)
+        hipLaunchKernelGGL(k_rescale_update_approx<5>, grid_aes(r.N, 512, r.crt.k, B), dim3(512), kAesLds, st, r, a, x,
+                           delta, zh, mc, g.te0, g.rk);
+    else
+        hipLaunchKernelGGL(k_rescale_update_approx<8>, grid_aes(r.N, 512, r.crt.k, B), dim3(512), kAesLds, st, r, a, x,
+                           delta, zh, mc, g.te0, g.rk);
 }
 
 // ---------------------------------------------------------------------------
@@ -479,7 +548,7 @@ __global__ __launch_bounds__(256) void k_base_ext(BEArgs a, Act x, const ModC* m
         const ModC m = mc[a.swapped[i]];
         const int16_t* src = x.p[a.src[i]] + static_cast<int64_t>(b) * m.n * N + e;
         int16_t* w = W(i);
-        for (int c = 0; c < static_cast<int>(m.n); ++c) w[c * N] = src[c * N];
+        col_map(src, w, N, static_cast<int>(m.n), [](int, int16_t v) { return v; });
     }
     const u128* T = a.tab + (static_cast<int64_t>(b) * N + e) * a.n_tab;
     int64_t off = 0;
@@ -498,11 +567,11 @@ __global__ __launch_bounds__(256) void k_base_ext(BEArgs a, Act x, const ModC* m
             s.init(P);
             int16_t* lt = W(tg);
             const int32_t inv = a.inv[i][j];
-            for (int c = 0; c < static_cast<int>(mo.n); ++c) {
-                int32_t v = lt[c * N] - static_cast<int32_t>(s.next(mo));
+            col_map(lt, lt, N, static_cast<int>(mo.n), [&](int, int16_t x) {
+                int32_t v = x - static_cast<int32_t>(s.next(mo));
                 if (v < 0) v += q;
-                lt[c * N] = static_cast<int16_t>((v * inv) % q);
-            }
+                return static_cast<int16_t>((v * inv) % q);
+            });
         }
     }
     for (int xi = 0; xi < a.nextra; ++xi) {
@@ -512,7 +581,7 @@ __global__ __launch_bounds__(256) void k_base_ext(BEArgs a, Act x, const ModC* m
         const int16_t* w = W(a.extra_pos[xi]);
         int16_t* dst = x.p[r] + static_cast<int64_t>(b) * m.n * N + e;
         const int32_t f = a.invv[xi];  // already negated mod q on the host
-        for (int c = 0; c < static_cast<int>(m.n); ++c) dst[c * N] = static_cast<int16_t>((w[c * N] * f) % q);
+        col_map(w, dst, N, static_cast<int>(m.n), [&](int, int16_t v) { return static_cast<int16_t>((v * f) % q); });
     }
     }
 }
@@ -580,12 +649,21 @@ __global__ __launch_bounds__(512, 4) void k_mult(MultArgs a, Act x, Act y, const
     sg.init(G);
     se.init(E);
     int16_t* O = y.p[j] + static_cast<int64_t>(b) * m.n * No + o;
-    for (int i = 0; i < static_cast<int>(m.n); ++i) {
-        const int32_t gv = static_cast<int32_t>(sg.next(m));
-        const int32_t ev = static_cast<int32_t>(se.next(m));
-        int32_t v = (ev + ypr * static_cast<int32_t>(X[i * Ni]) - gv) % p;
-        if (v < 0) v += p;
-        O[i * No] = static_cast<int16_t>(v);
+    const int n = static_cast<int>(m.n);
+    for (int i0 = 0; i0 < n; i0 += kChunk) {
+        int16_t xv[kChunk];
+#pragma unroll
+        for (int u = 0; u < kChunk; ++u)
+            if (i0 + u < n) xv[u] = X[(i0 + u) * Ni];
+#pragma unroll
+        for (int u = 0; u < kChunk; ++u)
+            if (i0 + u < n) {
+                const int32_t gv = static_cast<int32_t>(sg.next(m));
+                const int32_t ev = static_cast<int32_t>(se.next(m));
+                int32_t v = (ev + ypr * static_cast<int32_t>(xv[u]) - gv) % p;
+                if (v < 0) v += p;
+                O[(i0 + u) * No] = static_cast<int16_t>(v);
+            }
     }
     }
 }
@@ -598,16 +676,24 @@ static inline dim3 grid_for(int64_t n, int bs, int y, int z) {
 
 
 void launch_sign_approx(const SignArgs& a, const Act& x, const ModC* mc, const AesGlobals& g, hipStream_t st) {
-    hipLaunchKernelGGL(k_sign_approx, grid_aes(a.N, 512, a.crt.k, a.B), dim3(512), kAesLds, st, a, x, mc, g.te0, g.rk);
+    if (a.t <= 5)
+        hipLaunchKernelGGL(k_sign_approx<5>, grid_aes(a.N, 512, a.crt.k, a.B), dim3(512), kAesLds, st, a, x, mc, g.te0,
+                           g.rk);
+    else
+        hipLaunchKernelGGL(k_sign_approx<8>, grid_aes(a.N, 512, a.crt.k, a.B), dim3(512), kAesLds, st, a, x, mc, g.te0,
+                           g.rk);
 }
 void launch_sign_chain(const SignArgs& a, int maxn, const ModC* mc, const AesGlobals& g, hipStream_t st) {
-    const dim3 gs = grid_aes(a.N, 512, a.t, a.B);
+    const dim3 gs = grid_for(a.N, 256, a.t, a.B);
     const dim3 gr = grid_aes(a.N, 512, 1, a.B);
-    if (maxn <= 32) {
-        hipLaunchKernelGGL(k_sign_castsum<32>, gs, dim3(512), kAesLds, st, a, mc, g.te0, g.rk);
+    if (maxn <= 24) {  // k = 7 DASH configs (cast outputs mod 8 m_d: <= 22 components)
+        hipLaunchKernelGGL(k_sign_castsum<24>, gs, dim3(256), 0, st, a, mc);
+        hipLaunchKernelGGL(k_sign_chain<24>, gr, dim3(512), kAesLds, st, a, mc, g.te0, g.rk);
+    } else if (maxn <= 32) {
+        hipLaunchKernelGGL(k_sign_castsum<32>, gs, dim3(256), 0, st, a, mc);
         hipLaunchKernelGGL(k_sign_chain<32>, gr, dim3(512), kAesLds, st, a, mc, g.te0, g.rk);
     } else {
-        hipLaunchKernelGGL(k_sign_castsum<64>, gs, dim3(512), kAesLds, st, a, mc, g.te0, g.rk);
+        hipLaunchKernelGGL(k_sign_castsum<64>, gs, dim3(256), 0, st, a, mc);
         hipLaunchKernelGGL(k_sign_chain<64>, gr, dim3(512), kAesLds, st, a, mc, g.te0, g.rk);
     }
 }

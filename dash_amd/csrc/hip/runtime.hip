@@ -310,6 +310,14 @@ class HipEvaluator {
         a.zc_stride = zstride_;
         a.relu = relu;
         a.csum = csum_;
+        {
+            int64_t c1 = 0;
+            for (int d = a.t - 1; d >= 1; --d) {
+                a.c1off[d] = c1;
+                c1 += static_cast<int64_t>(k_ + 1) * a.mrs[d];
+            }
+            DASH_CHECK(c1 == a.n_cast, "cast1 row size does not match the MRS base");
+        }
         int maxn = 0;
         const int k = k_;
         for (size_t d = 1; d < sp.mrs.size(); ++d) maxn = std::max(maxn, nr_comps((k + 1) * sp.mrs[d]));

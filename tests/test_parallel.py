@@ -33,7 +33,7 @@ def _worker(rank, world, port, q):
     shutdown(ctx)
 
 
-@pytest.mark.parametrize("world", [2])
+@pytest.mark.parametrize("world", [2, 4])
 def test_batch_dp_gloo(world):
     ctx = tmp.get_context("spawn")
     q = ctx.Queue()
@@ -46,8 +46,10 @@ def test_batch_dp_gloo(world):
         p.join(timeout=60)
         assert p.exitcode == 0
     assert all(ok for _, ok, _ in res)
-    # shards of 5 items over 2 ranks: [0,1,2] and [3,4]
-    assert res[0][2] == [0, 1, 2] and res[1][2] == [3, 4]
+    # contiguous balanced shards of 5 items: the first 5 % world ranks get one extra
+    sizes = [len(r[2]) for r in res]
+    assert sum(sizes) == 5 and max(sizes) - min(sizes) <= 1
+    assert [i for r in res for i in r[2]] == list(range(5))
 
 
 def test_single_process_context():
