@@ -59,6 +59,24 @@ __device__ __forceinline__ uint32_t div32_q(uint32_t x, uint32_t q, uint32_t mq,
     return d;
 }
 
+// x mod q for 0 <= x < 2^32: reciprocal multiply + one correction. The
+// compiler's `%` by a runtime divisor is a ~25-op v_rcp_iflag sequence (and a
+// 64-bit `%` several times that); this is 4-5 ops, a mask for powers of two
+// (m.bits is uniform per launch).
+__device__ __forceinline__ uint32_t modq(uint32_t x, const ModC& m) {
+    if (m.bits) return x & (m.q - 1);
+    uint32_t r;
+    div32_q(x, m.q, m.mq, r);
+    return r;
+}
+
+// x mod q for a 64-bit x (q < 2^16): (hi mod q) * (2^32 mod q) + lo mod q
+__device__ __forceinline__ uint32_t modq64(uint64_t x, const ModC& m) {
+    const uint32_t h = modq(static_cast<uint32_t>(x >> 32), m), l = modq(static_cast<uint32_t>(x), m);
+    const uint32_t t = modq(0xffffffffu, m) + 1u;  // 2^32 mod q, or q itself
+    return modq(h * t + l, m);
+}
+
 // (Q, r) = divmod(Q, D)
 __device__ __forceinline__ uint32_t divmod128(u128& Q, uint32_t D, uint64_t mD) {
     uint32_t l3 = static_cast<uint32_t>(Q >> 96), l2 = static_cast<uint32_t>(Q >> 64);

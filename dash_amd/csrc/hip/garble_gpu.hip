@@ -99,13 +99,14 @@ __device__ __forceinline__ u128 aes_keyed(const AesCtx& a, u128 in, const uint32
 }
 
 // Prg::label (core.h): two components per AES-CTR block
-__device__ __forceinline__ void prg_label(const AesCtx& a, const uint32_t* rk, uint64_t stream, uint64_t ctr, int p,
-                                          int n, int16_t* out) {
+__device__ __forceinline__ void prg_label(const AesCtx& a, const uint32_t* rk, uint64_t stream, uint64_t ctr,
+                                          const ModC& m, int16_t* out) {
+    const int n = static_cast<int>(m.n);
     for (int j = 0; j < n; j += 2) {
         const u128 blk = (static_cast<u128>(stream) << 64) | (ctr + static_cast<uint64_t>(j >> 1));
         const u128 r = aes_keyed(a, blk, rk);
-        out[j] = static_cast<int16_t>(static_cast<uint64_t>(r) % static_cast<uint64_t>(p));
-        if (j + 1 < n) out[j + 1] = static_cast<int16_t>(static_cast<uint64_t>(r >> 64) % static_cast<uint64_t>(p));
+        out[j] = static_cast<int16_t>(modq64(static_cast<uint64_t>(r), m));
+        if (j + 1 < n) out[j + 1] = static_cast<int16_t>(modq64(static_cast<uint64_t>(r >> 64), m));
     }
 }
 
@@ -135,8 +136,7 @@ __global__ __launch_bounds__(256) void k_draw(Ctx c, Gadget g) {
         const int64_t e = i / g.ndraws;
         const Draw d = g.draws[i % g.ndraws];
         int16_t* out = g.S + (e * g.nslots + d.slot) * kW;
-        prg_label(aes, c.rk, stream_of(g.layer, g.sslot, static_cast<uint64_t>(e), g.mask), d.ctr, d.q,
-                  static_cast<int>(c.mc[d.q].n), out);
+        prg_label(aes, c.rk, stream_of(g.layer, g.sslot, static_cast<uint64_t>(e), g.mask), d.ctr, c.mc[d.q], out);
     }
 }
 
@@ -162,13 +162,14 @@ __global__ __launch_bounds__(256) void k_sign_derive(Ctx c, Gadget g, SignSlots 
     for (int q = 0; q + 1 < t; ++q) {
         const int d = t - 1 - q;
         const int mo = (k + 1) * s.mrs[d];
-        const int n = static_cast<int>(c.mc[mo].n);
+        const ModC Mo = c.mc[mo];
+        const int n = static_cast<int>(Mo.n);
         int16_t* dst = S + (s.sum2_slot0 + q) * kW;
         const int16_t* b0 = S + (s.bases_slot0 + q * s.stride_q) * kW;
         for (int i = 0; i < n; ++i) {
             int v = 0;
             for (int j = 0; j <= k; ++j) v += b0[j * kW + i];
-            dst[i] = static_cast<int16_t>(v % mo);
+            dst[i] = static_cast<int16_t>(modq(static_cast<uint32_t>(v), Mo));
         }
     }
     const int m0 = s.mrs[0];
@@ -178,7 +179,7 @@ __global__ __launch_bounds__(256) void k_sign_derive(Ctx c, Gadget g, SignSlots 
     for (int i = 0; i < n0; ++i) {
         int v = carry[i];
         for (int j = 0; j < k; ++j) v += S[(s.mrs_slot0 + j * t) * kW + i];
-        sum[i] = static_cast<int16_t>(v % m0);
+        sum[i] = static_cast<int16_t>(modq(static_cast<uint32_t>(v), c.mc[m0]));
     }
 }
 
@@ -208,7 +209,7 @@ __global__ __launch_bounds__(256) void k_project(Ctx c, Gadget g, In in, Tables 
         kc.init();
         uint32_t color = 0;
         for (int q = 0; q < static_cast<int>(mi.n); ++q) {
-            const uint32_t v = static_cast<uint32_t>(inl[q] + i * Rin[q]) % static_cast<uint32_t>(P.pin);
+            const uint32_t v = modq(static_cast<uint32_t>(inl[q] + i * Rin[q]), mi);
             if (q == 0) color = v;
             kc.push(v, mi);
         }
@@ -239,8 +240,8 @@ __global__ __launch_bounds__(256) void k_project(Ctx c, Gadget g, In in, Tables 
         CompressFwd pc;
         pc.init();
         for (int q = 0; q < static_cast<int>(mo.n); ++q) {
-            const uint32_t v = static_cast<uint32_t>((ol[q] + cm * oR[q]) % P.pout);
-            pc.push(v, mo);
+            // ol, cm, oR in [0, pout): < pout^2 + pout, 32-bit reduction
+            pc.push(modq(static_cast<uint32_t>(ol[q]) + static_cast<uint32_t>(cm) * static_cast<uint32_t>(oR[q]), mo), mo);
         }
         tb.t[P.table][e * tb.row[P.table] + P.off + static_cast<int64_t>(color) * P.stride] = pc.finish() + H;
     }
@@ -329,7 +330,7 @@ __global__ __launch_bounds__(256) void k_rescale_pre(Ctx c, RsArgs a, Tables tb,
         for (int j = 1; j < a.k; ++j) {
             const int p = a.crt[j];
             const ModC mj = c.mc[p];
-            prg_label(aes, c.rk, stream, ctr, p, static_cast<int>(mj.n), out0);
+            prg_label(aes, c.rk, stream, ctr, mj, out0);
             ctr += (mj.n + 1) / 2;
             const int16_t* Rp = c.R + static_cast<int64_t>(p) * kW;
             for (int i = 0; i < 2; ++i) {
@@ -344,14 +345,15 @@ __global__ __launch_bounds__(256) void k_rescale_pre(Ctx c, RsArgs a, Tables tb,
                 const u128 H = aes_encrypt(aes, kc.finish());
                 CompressFwd pc;
                 pc.init();
-                for (int q = 0; q < static_cast<int>(mj.n); ++q) pc.push(static_cast<uint32_t>((out0[q] + i * Rp[q]) % p), mj);
+                for (int q = 0; q < static_cast<int>(mj.n); ++q)
+                    pc.push(modq(static_cast<uint32_t>(out0[q] + i * Rp[q]), mj), mj);
                 tb.t[6][e * tb.row[6] + (j - 1) * 2 + color] = pc.finish() + H;
             }
             int16_t* L = a.L[j] + e * mj.n;
             for (int q = 0; q < static_cast<int>(mj.n); ++q) {
                 int v = L[q] - out0[q];
                 if (v < 0) v += p;
-                L[q] = static_cast<int16_t>((v * a.inv[j]) % p);
+                L[q] = static_cast<int16_t>(modq(static_cast<uint32_t>(v * a.inv[j]), mj));
             }
         }
         int16_t* Lz = a.L[0] + e * m2.n;

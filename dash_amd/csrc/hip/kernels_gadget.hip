@@ -155,7 +155,7 @@ __global__ __launch_bounds__(256) void k_sign_castsum(SignArgs a, const ModC* mc
     int16_t* S = a.csum + ((static_cast<int64_t>(b) * t + d) * kCsumComps) * N + e;
 #pragma unroll
     for (int i = 0; i < MAXN; ++i)
-        if (i < static_cast<int>(Mo.n)) S[i * N] = static_cast<int16_t>(acc[i] % mo);
+        if (i < static_cast<int>(Mo.n)) S[i * N] = static_cast<int16_t>(modq(static_cast<uint32_t>(acc[i]), Mo));
 }
 
 // ---------------------------------------------------------------------------
@@ -278,8 +278,7 @@ __global__ __launch_bounds__(256) void k_relu_mult(SignArgs a, Act x, Act y, con
     const u128 mini = E3[2];
     const int16_t t16 = static_cast<int16_t>(static_cast<uint16_t>(mini >> (16 * cS)));
     const int16_t ypr16 = static_cast<int16_t>(t16 - static_cast<int16_t>(static_cast<uint16_t>(HS)));
-    int32_t ypr = ypr16 % p;
-    if (ypr < 0) ypr += p;
+    const uint32_t ypr = modq(static_cast<uint32_t>(static_cast<int32_t>(ypr16) + (p << 15)), m);  // p*2^15 > |ypr16|
     const int16_t* X = x.p[j] + static_cast<int64_t>(b) * m.n * N + e;
     int16_t* Y = y.p[j] + static_cast<int64_t>(b) * m.n * N + e;
     DigitStream sg, se;
@@ -294,11 +293,11 @@ __global__ __launch_bounds__(256) void k_relu_mult(SignArgs a, Act x, Act y, con
 #pragma unroll
         for (int u = 0; u < kChunk; ++u)
             if (i0 + u < n) {
-                const int32_t g = static_cast<int32_t>(sg.next(m));
-                const int32_t ev = static_cast<int32_t>(se.next(m));
-                int32_t v = (ev + ypr * xv[u] - g) % p;
-                if (v < 0) v += p;
-                Y[(i0 + u) * N] = static_cast<int16_t>(v);
+                const uint32_t g = sg.next(m);
+                const uint32_t ev = se.next(m);
+                // all terms in [0, p): ev + ypr * x + (p - g) < p^2 + 2p
+                Y[(i0 + u) * N] = static_cast<int16_t>(
+                    modq(ev + ypr * static_cast<uint32_t>(static_cast<uint16_t>(xv[u])) + static_cast<uint32_t>(p) - g, m));
             }
     }
 }
@@ -374,11 +373,9 @@ __global__ __launch_bounds__(256) void k_rescale_update(RescaleArgs a, Act x, co
 #pragma unroll
         for (int u = 0; u < kChunk; ++u)
             if (i0 + u < n) {
-                int32_t v = lv[u];
-                if (a.add_up) v += U[i0 + u];
-                v -= static_cast<int32_t>(s.next(m));
-                v = (v % p + p) % p;
-                L[(i0 + u) * N] = static_cast<int16_t>((v * inv) % p);
+                uint32_t v = static_cast<uint32_t>(lv[u]) + static_cast<uint32_t>(p) - s.next(m);  // [1, 2p)
+                if (a.add_up) v += static_cast<uint32_t>(U[i0 + u]);
+                L[(i0 + u) * N] = static_cast<int16_t>(modq(v * static_cast<uint32_t>(inv), m));
             }
     }
 }
@@ -492,12 +489,11 @@ __global__ __launch_bounds__(512, 4) void k_rescale_update_approx(RescaleArgs r,
 #pragma unroll
             for (int u = 0; u < kChunkUA; ++u)
                 if (i0 + u < n) {
-                    int32_t v = lv[u] + dv[u] - static_cast<int32_t>(s.next(m));
-                    v %= p;
-                    if (v < 0) v += p;
-                    v = (v * inv) % p;
+                    // lv, dv, digit in [0, p): the sum is in [1, 3p), (sum * inv) mod p in one reduction
+                    const uint32_t v = modq((static_cast<uint32_t>(lv[u]) + static_cast<uint32_t>(dv[u]) +
+                                             static_cast<uint32_t>(p) - s.next(m)) * static_cast<uint32_t>(inv), m);
                     L[(i0 + u) * N] = static_cast<int16_t>(v);
-                    cf.push(static_cast<uint32_t>(v), m);
+                    cf.push(v, m);
                     if (i0 + u == 0) {
                         col = static_cast<uint32_t>(v);
 #pragma unroll
@@ -570,7 +566,7 @@ __global__ __launch_bounds__(256) void k_base_ext(BEArgs a, Act x, const ModC* m
             col_map(lt, lt, N, static_cast<int>(mo.n), [&](int, int16_t x) {
                 int32_t v = x - static_cast<int32_t>(s.next(mo));
                 if (v < 0) v += q;
-                return static_cast<int16_t>((v * inv) % q);
+                return static_cast<int16_t>(modq(static_cast<uint32_t>(v * inv), mo));
             });
         }
     }
@@ -581,7 +577,7 @@ __global__ __launch_bounds__(256) void k_base_ext(BEArgs a, Act x, const ModC* m
         const int16_t* w = W(a.extra_pos[xi]);
         int16_t* dst = x.p[r] + static_cast<int64_t>(b) * m.n * N + e;
         const int32_t f = a.invv[xi];  // already negated mod q on the host
-        col_map(w, dst, N, static_cast<int>(m.n), [&](int, int16_t v) { return static_cast<int16_t>((v * f) % q); });
+        col_map(w, dst, N, static_cast<int>(m.n), [&](int, int16_t v) { return static_cast<int16_t>(modq(static_cast<uint32_t>(v * f), m)); });
     }
     }
 }
@@ -686,6 +682,8 @@ void launch_sign_approx(const SignArgs& a, const Act& x, const ModC* mc, const A
 void launch_sign_chain(const SignArgs& a, int maxn, const ModC* mc, const AesGlobals& g, hipStream_t st) {
     const dim3 gs = grid_for(a.N, 256, a.t, a.B);
     const dim3 gr = grid_aes(a.N, 512, 1, a.B);
+    // (measured: folding the castsum pass into the chain lanes is slower, 334 vs 356 inf/s on
+    // MiniONN B=24: the chain is latency bound and the castsum's t-fold lane parallelism wins)
     if (maxn <= 24) {  // k = 7 DASH configs (cast outputs mod 8 m_d: <= 22 components)
         hipLaunchKernelGGL(k_sign_castsum<24>, gs, dim3(256), 0, st, a, mc);
         hipLaunchKernelGGL(k_sign_chain<24>, gr, dim3(512), kAesLds, st, a, mc, g.te0, g.rk);
