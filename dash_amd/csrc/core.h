@@ -297,28 +297,74 @@ struct BigAllocator {
 };
 
 struct Array {
+    // Device-resident payload: the GPU garbler leaves its tables in HBM so the
+    // evaluator on the same node copies them device-to-device (no PCIe round
+    // trip). The host copy is fetched on first host access (serialize, CPU
+    // evaluator, numpy), once, thread-safely, and shared by every copy.
+    struct Device {
+        std::shared_ptr<void> p;  // device buffer (deleter frees it)
+        int device = -1;
+        std::function<void(void* host, const void* dev, size_t n)> fetch;
+        std::once_flag once;
+        std::shared_ptr<uint8_t> host;
+    };
+
     DType dtype = DType::u8;
     std::vector<i64> shape;
     std::shared_ptr<uint8_t> buf;
     size_t nbytes = 0;
+    std::shared_ptr<Device> dev;
 
     Array() = default;
     Array(DType dt, std::vector<i64> shp) : dtype(dt), shape(std::move(shp)) {
+        nbytes = shape_bytes();
+        buf = host_alloc(nbytes);
+    }
+    // an array whose bytes live in a device buffer (no host storage until first host access)
+    static Array on_device(DType dt, std::vector<i64> shp, std::shared_ptr<Device> d) {
+        Array a;
+        a.dtype = dt;
+        a.shape = std::move(shp);
+        a.nbytes = a.shape_bytes();
+        a.dev = std::move(d);
+        return a;
+    }
+    bool device_resident() const { return dev && dev->p; }
+    const void* device_ptr() const { return device_resident() ? dev->p.get() : nullptr; }
+    size_t count() const { return nbytes / dtype_size(dtype); }
+    template <typename T>
+    T* ptr() {
+        return reinterpret_cast<T*>(host_bytes());
+    }
+    template <typename T>
+    const T* ptr() const {
+        return reinterpret_cast<const T*>(host_bytes());
+    }
+    uint8_t* host_bytes() const {
+        if (!device_resident()) return buf.get();
+        Device* d = dev.get();
+        const size_t n = nbytes;
+        std::call_once(d->once, [d, n] {
+            d->host = host_alloc(n);
+            d->fetch(d->host.get(), d->p.get(), n);
+        });
+        return d->host.get();
+    }
+
+   private:
+    size_t shape_bytes() const {
         size_t cnt = 1;
         for (auto s : shape) cnt *= static_cast<size_t>(s);
-        nbytes = cnt * dtype_size(dt);
+        return cnt * dtype_size(dtype);
+    }
+    static std::shared_ptr<uint8_t> host_alloc(size_t nbytes) {
         size_t alloc = (nbytes + 63) & ~size_t(63);
         if (alloc == 0) alloc = 64;
         bool zeroed = false;
         uint8_t* p = static_cast<uint8_t*>(big_alloc(alloc, &zeroed));
         if (!zeroed) std::memset(p, 0, alloc);
-        buf = std::shared_ptr<uint8_t>(p, [alloc](uint8_t* q) { big_free(q, alloc); });
+        return std::shared_ptr<uint8_t>(p, [alloc](uint8_t* q) { big_free(q, alloc); });
     }
-    size_t count() const { return nbytes / dtype_size(dtype); }
-    template <typename T>
-    T* ptr() { return reinterpret_cast<T*>(buf.get()); }
-    template <typename T>
-    const T* ptr() const { return reinterpret_cast<const T*>(buf.get()); }
 };
 
 // ----------------------------------------------------------------------------

@@ -489,6 +489,7 @@ struct GpuGarbler::Impl {
     int max_mod = 0;
     std::vector<int> crt;
     int k = 0;
+    int device = 0;
     ~Impl() {
         for (void* p : owned) (void)hipFree(p);
     }
@@ -499,6 +500,7 @@ GpuGarbler::GpuGarbler(const std::vector<int>& crt, const std::vector<int>& mrs,
     : impl_(new Impl) {
     HIPCHECK(hipSetDevice(device));
     Impl& I = *impl_;
+    I.device = device;
     I.crt = crt;
     I.k = static_cast<int>(crt.size());
     I.max_mod = R.max_mod;
@@ -571,9 +573,19 @@ struct DevTable {
         HIPCHECK(hipMalloc(reinterpret_cast<void**>(&p), std::max<size_t>(16, bytes)));
         HIPCHECK(hipMemset(p, 0, std::max<size_t>(16, bytes)));
     }
-    void to_host(Array& a) const {
+    // hand the buffer to `a` as a device-resident array (kept in HBM; the
+    // evaluator on this node copies it device-to-device)
+    void to_array(Array& a, int device) {
         DASH_CHECK(a.nbytes == bytes, "gpu garbler: table size mismatch");
-        HIPCHECK(hipMemcpy(a.ptr<uint8_t>(), p, bytes, hipMemcpyDeviceToHost));
+        auto d = std::make_shared<Array::Device>();
+        d->p = std::shared_ptr<void>(p, [](void* x) { (void)hipFree(x); });
+        p = nullptr;
+        d->device = device;
+        d->fetch = [device](void* h, const void* dv, size_t n) {
+            HIPCHECK(hipSetDevice(device));
+            HIPCHECK(hipMemcpy(h, dv, n, hipMemcpyDeviceToHost));
+        };
+        a = Array::on_device(a.dtype, a.shape, std::move(d));
     }
 };
 
@@ -693,8 +705,8 @@ void GpuGarbler::sign_layer(uint64_t layer, const SignPlan& sp, const CrtLabels&
         HIPCHECK(hipGetLastError());
         HIPCHECK(hipDeviceSynchronize());
         download_labels(dout, out);
-        tG.to_host(*mmg);
-        tE.to_host(*mme);
+        tG.to_array(*mmg, I.device);
+        tE.to_array(*mme, I.device);
     } else {
         HIPCHECK(hipDeviceSynchronize());
         // sign layer outputs: out0[o] slots (one per CRT residue) -> label-major host labels
@@ -706,10 +718,10 @@ void GpuGarbler::sign_layer(uint64_t layer, const SignPlan& sp, const CrtLabels&
                 std::memcpy(out[o].at(e), hs.data() + (e * L.nslots + L.out_slot0 + o) * gg::kW, n * sizeof(int16_t));
         }
     }
-    tA.to_host(ap);
-    t1.to_host(c1);
-    t2.to_host(c2);
-    tS.to_host(sg);
+    tA.to_array(ap, I.device);
+    t1.to_array(c1, I.device);
+    t2.to_array(c2, I.device);
+    tS.to_array(sg, I.device);
     for (void* p : tmp) (void)hipFree(p);
 }
 
@@ -775,11 +787,11 @@ void GpuGarbler::rescale_legacy_iter(uint64_t layer, int it, const RescalePlan& 
     HIPCHECK(hipGetLastError());
     HIPCHECK(hipDeviceSynchronize());
     download_labels(dL, cur);
-    tT.to_host(tr);
-    tA.to_host(ap);
-    t1.to_host(c1);
-    t2.to_host(c2);
-    tS.to_host(sg);
+    tT.to_array(tr, I.device);
+    tA.to_array(ap, I.device);
+    t1.to_array(c1, I.device);
+    t2.to_array(c2, I.device);
+    tS.to_array(sg, I.device);
     for (void* p : tmp) (void)hipFree(p);
 }
 

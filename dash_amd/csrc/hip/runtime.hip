@@ -224,6 +224,14 @@ class HipEvaluator {
         HIPCHECK(hipMemcpy(d, host, count * sizeof(T), hipMemcpyHostToDevice));
         return d;
     }
+    // a model array into device memory: device-to-device (or peer) when the GPU
+    // garbler left it in HBM and nobody has fetched (and possibly edited) a host copy
+    static void copy_in(uint8_t* dst, const Array& a) {
+        if (a.device_resident() && !a.dev->host)
+            HIPCHECK(hipMemcpy(dst, a.device_ptr(), a.nbytes, hipMemcpyDefault));
+        else
+            HIPCHECK(hipMemcpy(dst, a.ptr<uint8_t>(), a.nbytes, hipMemcpyHostToDevice));
+    }
     // one device buffer holding array `name` of layer li of every GC slot
     const u128* upload_tables(size_t li, const std::string& name) {
         const size_t nb = tmpl_->layers[li].arr(name).nbytes;
@@ -231,7 +239,7 @@ class HipEvaluator {
         loaders_.push_back([d, nb, li, name](int b, const GarbledModel& m) {
             const Array& a = m.layers[li].arr(name);
             DASH_CHECK(a.nbytes == nb, "table size mismatch across batch");
-            HIPCHECK(hipMemcpy(d + nb * b, a.buf.get(), nb, hipMemcpyHostToDevice));
+            copy_in(d + nb * b, a);
         });
         table_bytes_ += nb * B_;
         return reinterpret_cast<const u128*>(d);
@@ -240,7 +248,7 @@ class HipEvaluator {
         const size_t nb = tmpl_->layers[li].arr(name).nbytes;
         uint8_t* d = dalloc<uint8_t>(nb * B_);
         loaders_.push_back([d, nb, li, name](int b, const GarbledModel& m) {
-            HIPCHECK(hipMemcpy(d + nb * b, m.layers[li].arr(name).buf.get(), nb, hipMemcpyHostToDevice));
+            copy_in(d + nb * b, m.layers[li].arr(name));
         });
         return reinterpret_cast<const int16_t*>(d);
     }

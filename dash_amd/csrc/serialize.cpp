@@ -30,7 +30,7 @@ struct W {
         raw(&dt, 1);
         ivec(a.shape);
         i64v(static_cast<i64>(a.nbytes));
-        raw(a.buf.get(), a.nbytes);
+        raw(a.ptr<uint8_t>(), a.nbytes);
     }
 };
 
@@ -78,7 +78,7 @@ struct Rd {
         Array a(static_cast<DType>(dt), shape);
         i64 nb = i64v();
         DASH_CHECK(static_cast<size_t>(nb) == a.nbytes, "array size mismatch");
-        raw(a.buf.get(), a.nbytes);
+        raw(a.ptr<uint8_t>(), a.nbytes);
         return a;
     }
 };
