@@ -108,6 +108,7 @@ def main() -> None:
         gcs.append(gc)
         log(f"rank {rank}: garbled+uploaded GC {b + 1}/{B} ({table_gb:.2f} GB tables)")
     offline_s = time.perf_counter() - t_off
+    free_b, total_b = torch.cuda.mem_get_info(device)
 
     # group 0 on the current stream, the others on torch pool streams (measured best on MI355X:
     # 313 inf/s at B=24 vs 295 with one dedicated non-blocking HIP stream per group, which runs all
@@ -197,6 +198,7 @@ def main() -> None:
             },
             "offline": {"garble_s_per_gc": round(garble_s / B, 2), "upload_s_per_gc": round(upload_s / B, 2),
                         "table_gb_per_gc": round(table_gb, 3), "offline_total_s": round(offline_s, 1)},
+            "hbm_gb": {"used": round((total_b - free_b) / 1e9, 1), "total": round(total_b / 1e9, 1)},
             "verified_vs_plaintext": verified,
         }
         if prof:

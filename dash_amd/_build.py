@@ -21,7 +21,7 @@ from pathlib import Path
 
 PKG = Path(__file__).resolve().parent
 CSRC = PKG / "csrc"
-BUILD = PKG.parent / "build" / "native"
+BUILD = Path(os.environ.get("DASH_BUILD_DIR", str(PKG.parent / "build" / "native")))
 ROCM = Path(os.environ.get("ROCM_PATH", "/opt/rocm"))
 ARCH = os.environ.get("DASH_GPU_ARCH", "gfx950")
 
@@ -56,8 +56,9 @@ def _host_cmd(src: Path, obj: Path, debug: bool) -> list[str]:
 def _hip_cmd(src: Path, obj: Path, debug: bool) -> list[str]:
     hipcc = str(ROCM / "bin" / "hipcc")
     opt = ["-O1", "-g"] if debug else ["-O3"]
+    extra = os.environ.get("DASH_HIP_FLAGS", "").split()  # e.g. -DDASH_AES_BLOCK=512 for A/B builds
     return [hipcc, "-std=c++17", "-fPIC", "-fvisibility=hidden", f"--offload-arch={ARCH}", "-maes", "-msse4.2",
-            *opt, "-Wno-unused-result", *_includes(), "-c", "-x", "hip", str(src), "-o", str(obj)]
+            *opt, "-Wno-unused-result", *extra, *_includes(), "-c", "-x", "hip", str(src), "-o", str(obj)]
 
 
 def _deps_newer(obj: Path, src: Path) -> bool:

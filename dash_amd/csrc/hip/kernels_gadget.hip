@@ -20,14 +20,26 @@ namespace dev {
 
 constexpr size_t kAesLds = 0;  // AES image is static LDS
 
-// AES kernels stride over their elements so the 64 KiB LDS image is filled
-// once per resident block instead of once per 512 elements: about two
-// resident blocks per CU (LDS bound), x4 for tail balance.
+// AES kernels hold a 64 KiB LDS image per block, so at most two blocks fit a
+// CU. Measured on MiniONN B=24 x 4 streams (inf/s): 512 threads / 64 VGPRs 354,
+// 1024 threads (2x the resident waves) 347, 512 threads / 128 VGPRs 345: the
+// concurrent stream groups already fill the CUs, finer blocks pack better.
+#ifndef DASH_AES_BLOCK
+#define DASH_AES_BLOCK 512
+#endif
+constexpr int kAesBlock = DASH_AES_BLOCK;
+#ifndef DASH_AES_MINBLOCKS
+#define DASH_AES_MINBLOCKS (2048 / DASH_AES_BLOCK)
+#endif
+constexpr int kAesMinBlocks = DASH_AES_MINBLOCKS;  // sets the VGPR budget (2048/block -> 64 VGPRs)
+
+// AES kernels stride over their elements so the LDS image is filled once per
+// resident block: two resident blocks per CU, x4 for tail balance.
 static int aes_block_cap() {
     static int cap = [] {
         int dev = 0, cus = 256;
         if (hipGetDevice(&dev) == hipSuccess) hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-        return 8 * cus;
+        return 8 * cus * 512 / kAesBlock;
     }();
     return cap;
 }
@@ -91,7 +103,7 @@ __device__ __forceinline__ void approx_casts_out(const AesCtx& aes, const SignAr
 
 // Phase A: approximate residues + their casts. grid (x, k, B)
 template <int TM>
-__global__ __launch_bounds__(512, 4) void k_sign_approx(SignArgs a, Act x, const ModC* mc, const uint32_t* te0,
+__global__ __launch_bounds__(kAesBlock, kAesMinBlocks) void k_sign_approx(SignArgs a, Act x, const ModC* mc, const uint32_t* te0,
                                                      const uint32_t* rk) {
     AES_PROLOGUE(te0, rk);
     const int j = blockIdx.y, b = blockIdx.z;
@@ -163,7 +175,7 @@ __global__ __launch_bounds__(256) void k_sign_castsum(SignArgs a, const ModC* mc
 // only the carry's cast and the sum's cast2 projection remain on the
 // critical path (2 AES + 2 gathers). grid (x, 1, B)
 template <int MAXN>
-__global__ __launch_bounds__(512, 4) void k_sign_chain(SignArgs a, const ModC* mc, const uint32_t* te0,
+__global__ __launch_bounds__(kAesBlock, kAesMinBlocks) void k_sign_chain(SignArgs a, const ModC* mc, const uint32_t* te0,
                                                     const uint32_t* rk) {
     AES_PROLOGUE(te0, rk);
     const int b = blockIdx.z;
@@ -305,7 +317,7 @@ __global__ __launch_bounds__(256) void k_relu_mult(SignArgs a, Act x, Act y, con
 // ---------------------------------------------------------------------------
 // Rescale step 1+2 for one factor: hash the factor residue (optionally after
 // the upshift). grid (ceil(N/256), 1, B)
-__global__ __launch_bounds__(512, 4) void k_rescale_hash(Act x, int fi, int s, const int16_t* up, int up_stride,
+__global__ __launch_bounds__(kAesBlock, kAesMinBlocks) void k_rescale_hash(Act x, int fi, int s, const int16_t* up, int up_stride,
                                                       int add_up, int64_t N, u128* h0, uint16_t* col0,
                                                       const ModC* mc, const uint32_t* te0, const uint32_t* rk) {
     AES_PROLOGUE(te0, rk);
@@ -429,7 +441,7 @@ __global__ __launch_bounds__(256) void k_rescale_post(Act x, CrtInfo crt, int64_
 //            next sign gadget (phase A) in the same pass.
 // The downshift of iteration i and the upshift of i+1 collapse into one
 // delta = up - down; only the last iteration writes a downshifted result.
-__global__ __launch_bounds__(512, 4) void k_rescale_hash_sign(const u128* signP, const u128* du, int64_t N, u128* h0,
+__global__ __launch_bounds__(kAesBlock, kAesMinBlocks) void k_rescale_hash_sign(const u128* signP, const u128* du, int64_t N, u128* h0,
                                                            uint16_t* col0, const uint32_t* te0, const uint32_t* rk) {
     AES_PROLOGUE(te0, rk);
     const int b = blockIdx.z;
@@ -444,7 +456,7 @@ __global__ __launch_bounds__(512, 4) void k_rescale_hash_sign(const u128* signP,
 // grid (ceil(N/256), k, B); half-size load chunks (the t approx entries stay live)
 constexpr int kChunkUA = kChunk / 4;
 template <int TM>
-__global__ __launch_bounds__(512, 4) void k_rescale_update_approx(RescaleArgs r, SignArgs a, Act x, const int16_t* delta,
+__global__ __launch_bounds__(kAesBlock, kAesMinBlocks) void k_rescale_update_approx(RescaleArgs r, SignArgs a, Act x, const int16_t* delta,
                                                                const u128* zh, const ModC* mc, const uint32_t* te0,
                                                                const uint32_t* rk) {
     AES_PROLOGUE(te0, rk);
@@ -515,15 +527,15 @@ __global__ __launch_bounds__(512, 4) void k_rescale_update_approx(RescaleArgs r,
 
 void launch_rescale_hash_sign(const u128* signP, const u128* du, int64_t N, int B, u128* h0, uint16_t* col0,
                               const AesGlobals& g, hipStream_t st) {
-    hipLaunchKernelGGL(k_rescale_hash_sign, grid_aes(N, 512, 1, B), dim3(512), kAesLds, st, signP, du, N, h0, col0, g.te0, g.rk);
+    hipLaunchKernelGGL(k_rescale_hash_sign, grid_aes(N, kAesBlock, 1, B), dim3(kAesBlock), kAesLds, st, signP, du, N, h0, col0, g.te0, g.rk);
 }
 void launch_rescale_update_approx(const RescaleArgs& r, const SignArgs& a, const Act& x, const int16_t* delta,
                                   const u128* zh, int B, const ModC* mc, const AesGlobals& g, hipStream_t st) {
     if (a.t <= 5)
-        hipLaunchKernelGGL(k_rescale_update_approx<5>, grid_aes(r.N, 512, r.crt.k, B), dim3(512), kAesLds, st, r, a, x,
+        hipLaunchKernelGGL(k_rescale_update_approx<5>, grid_aes(r.N, kAesBlock, r.crt.k, B), dim3(kAesBlock), kAesLds, st, r, a, x,
                            delta, zh, mc, g.te0, g.rk);
     else
-        hipLaunchKernelGGL(k_rescale_update_approx<8>, grid_aes(r.N, 512, r.crt.k, B), dim3(512), kAesLds, st, r, a, x,
+        hipLaunchKernelGGL(k_rescale_update_approx<8>, grid_aes(r.N, kAesBlock, r.crt.k, B), dim3(kAesBlock), kAesLds, st, r, a, x,
                            delta, zh, mc, g.te0, g.rk);
 }
 
@@ -584,7 +596,7 @@ __global__ __launch_bounds__(256) void k_base_ext(BEArgs a, Act x, const ModC* m
 
 // ---------------------------------------------------------------------------
 // Generic projection layer (test-only Projection). grid (ceil(N/256), k, B)
-__global__ __launch_bounds__(512, 4) void k_proj(ProjArgs a, Act x, Act y, const ModC* mc, const uint32_t* te0,
+__global__ __launch_bounds__(kAesBlock, kAesMinBlocks) void k_proj(ProjArgs a, Act x, Act y, const ModC* mc, const uint32_t* te0,
                                               const uint32_t* rk) {
     AES_PROLOGUE(te0, rk);
     const int j = blockIdx.y, b = blockIdx.z;
@@ -605,7 +617,7 @@ __global__ __launch_bounds__(512, 4) void k_proj(ProjArgs a, Act x, Act y, const
 
 // Generalized half-gate product of pairs (2e, 2e+1), and the mixed-modulus
 // variant (second operand first projected to Z_q). grid (ceil(No/256), k, B)
-__global__ __launch_bounds__(512, 4) void k_mult(MultArgs a, Act x, Act y, const ModC* mc, const uint32_t* te0,
+__global__ __launch_bounds__(kAesBlock, kAesMinBlocks) void k_mult(MultArgs a, Act x, Act y, const ModC* mc, const uint32_t* te0,
                                               const uint32_t* rk) {
     AES_PROLOGUE(te0, rk);
     const int j = blockIdx.y, b = blockIdx.z;
@@ -673,26 +685,26 @@ static inline dim3 grid_for(int64_t n, int bs, int y, int z) {
 
 void launch_sign_approx(const SignArgs& a, const Act& x, const ModC* mc, const AesGlobals& g, hipStream_t st) {
     if (a.t <= 5)
-        hipLaunchKernelGGL(k_sign_approx<5>, grid_aes(a.N, 512, a.crt.k, a.B), dim3(512), kAesLds, st, a, x, mc, g.te0,
+        hipLaunchKernelGGL(k_sign_approx<5>, grid_aes(a.N, kAesBlock, a.crt.k, a.B), dim3(kAesBlock), kAesLds, st, a, x, mc, g.te0,
                            g.rk);
     else
-        hipLaunchKernelGGL(k_sign_approx<8>, grid_aes(a.N, 512, a.crt.k, a.B), dim3(512), kAesLds, st, a, x, mc, g.te0,
+        hipLaunchKernelGGL(k_sign_approx<8>, grid_aes(a.N, kAesBlock, a.crt.k, a.B), dim3(kAesBlock), kAesLds, st, a, x, mc, g.te0,
                            g.rk);
 }
 void launch_sign_chain(const SignArgs& a, int maxn, const ModC* mc, const AesGlobals& g, hipStream_t st) {
     const dim3 gs = grid_for(a.N, 256, a.t, a.B);
-    const dim3 gr = grid_aes(a.N, 512, 1, a.B);
+    const dim3 gr = grid_aes(a.N, kAesBlock, 1, a.B);
     // (measured: folding the castsum pass into the chain lanes is slower, 334 vs 356 inf/s on
     // MiniONN B=24: the chain is latency bound and the castsum's t-fold lane parallelism wins)
     if (maxn <= 24) {  // k = 7 DASH configs (cast outputs mod 8 m_d: <= 22 components)
         hipLaunchKernelGGL(k_sign_castsum<24>, gs, dim3(256), 0, st, a, mc);
-        hipLaunchKernelGGL(k_sign_chain<24>, gr, dim3(512), kAesLds, st, a, mc, g.te0, g.rk);
+        hipLaunchKernelGGL(k_sign_chain<24>, gr, dim3(kAesBlock), kAesLds, st, a, mc, g.te0, g.rk);
     } else if (maxn <= 32) {
         hipLaunchKernelGGL(k_sign_castsum<32>, gs, dim3(256), 0, st, a, mc);
-        hipLaunchKernelGGL(k_sign_chain<32>, gr, dim3(512), kAesLds, st, a, mc, g.te0, g.rk);
+        hipLaunchKernelGGL(k_sign_chain<32>, gr, dim3(kAesBlock), kAesLds, st, a, mc, g.te0, g.rk);
     } else {
         hipLaunchKernelGGL(k_sign_castsum<64>, gs, dim3(256), 0, st, a, mc);
-        hipLaunchKernelGGL(k_sign_chain<64>, gr, dim3(512), kAesLds, st, a, mc, g.te0, g.rk);
+        hipLaunchKernelGGL(k_sign_chain<64>, gr, dim3(kAesBlock), kAesLds, st, a, mc, g.te0, g.rk);
     }
 }
 void launch_unpack(const u128* P, int nres, const Act& out, const CrtInfo& mods, const ModC* mc, int64_t N, int B,
@@ -705,7 +717,7 @@ void launch_relu_mult(const SignArgs& a, const Act& x, const Act& y, const u128*
 }
 void launch_rescale_hash(const Act& x, int fi, int s, const int16_t* up, int up_stride, int add_up, int64_t N, int B,
                          u128* h0, uint16_t* col0, const ModC* mc, const AesGlobals& g, hipStream_t st) {
-    hipLaunchKernelGGL(k_rescale_hash, grid_aes(N, 512, 1, B), dim3(512), kAesLds, st, x, fi, s, up, up_stride,
+    hipLaunchKernelGGL(k_rescale_hash, grid_aes(N, kAesBlock, 1, B), dim3(kAesBlock), kAesLds, st, x, fi, s, up, up_stride,
                        add_up, N, h0, col0, mc, g.te0, g.rk);
 }
 void launch_rescale_update(const RescaleArgs& a, const Act& x, int B, const ModC* mc, hipStream_t st) {
@@ -721,11 +733,11 @@ void launch_base_ext(const BEArgs& a, const Act& x, int B, const ModC* mc, const
 }
 void launch_proj(const ProjArgs& a, const Act& x, const Act& y, int B, const ModC* mc, const AesGlobals& g,
                  hipStream_t st) {
-    hipLaunchKernelGGL(k_proj, grid_aes(a.N, 512, a.k, B), dim3(512), kAesLds, st, a, x, y, mc, g.te0, g.rk);
+    hipLaunchKernelGGL(k_proj, grid_aes(a.N, kAesBlock, a.k, B), dim3(kAesBlock), kAesLds, st, a, x, y, mc, g.te0, g.rk);
 }
 void launch_mult(const MultArgs& a, const Act& x, const Act& y, int B, const ModC* mc, const AesGlobals& g,
                  hipStream_t st) {
-    hipLaunchKernelGGL(k_mult, grid_aes(a.No, 512, a.crt.k, B), dim3(512), kAesLds, st, a, x, y, mc, g.te0, g.rk);
+    hipLaunchKernelGGL(k_mult, grid_aes(a.No, kAesBlock, a.crt.k, B), dim3(kAesBlock), kAesLds, st, a, x, y, mc, g.te0, g.rk);
 }
 
 }  // namespace dev
