@@ -453,10 +453,20 @@ __global__ __launch_bounds__(kAesBlock, kAesMinBlocks) void k_rescale_hash_sign(
     }
 }
 
-// grid (ceil(N/256), k, B); half-size load chunks (the t approx entries stay live)
-constexpr int kChunkUA = kChunk / 4;
+// grid (x, k, B). Each component chunk is one dependent HBM round trip (the
+// in-place stores keep the next chunk's loads behind them), so the chunk size
+// sets the round trips per label; the t approx entries stay live across the
+// loop, so larger chunks need the 128-VGPR budget (free here: the 64 KiB AES
+// image already limits a CU to 16 waves).
+#ifndef DASH_UA_CHUNK
+#define DASH_UA_CHUNK 4
+#endif
+#ifndef DASH_UA_MINBLOCKS
+#define DASH_UA_MINBLOCKS kAesMinBlocks
+#endif
+constexpr int kChunkUA = DASH_UA_CHUNK;
 template <int TM>
-__global__ __launch_bounds__(kAesBlock, kAesMinBlocks) void k_rescale_update_approx(RescaleArgs r, SignArgs a, Act x, const int16_t* delta,
+__global__ __launch_bounds__(kAesBlock, DASH_UA_MINBLOCKS) void k_rescale_update_approx(RescaleArgs r, SignArgs a, Act x, const int16_t* delta,
                                                                const u128* zh, const ModC* mc, const uint32_t* te0,
                                                                const uint32_t* rk) {
     AES_PROLOGUE(te0, rk);
