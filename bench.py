@@ -108,6 +108,7 @@ def main() -> None:
         gcs.append(gc)
         log(f"rank {rank}: garbled+uploaded GC {b + 1}/{B} ({table_gb:.2f} GB tables)")
     offline_s = time.perf_counter() - t_off
+    native().gpu_table_cache_trim()  # the garbler's recycled table blocks are no longer needed
     free_b, total_b = torch.cuda.mem_get_info(device)
 
     # group 0 on the current stream, the others on torch pool streams (measured best on MI355X:

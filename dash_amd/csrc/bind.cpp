@@ -4,6 +4,7 @@
 #include <pybind11/stl.h>
 
 #include "dataloader.h"
+#include "hip/gpu_garbler.h"
 #include "layers.h"
 #include "onnx.h"
 
@@ -133,6 +134,8 @@ PYBIND11_MODULE(_dash_native, m) {
     });
 
     m.def("nr_comps", &nr_comps);
+    m.def("gpu_table_cache_trim", &gpu_table_cache_trim, "release the GPU garbler's cached table blocks");
+    m.def("gpu_table_cache_bytes", &gpu_table_cache_bytes);
     m.def("first_primes", &first_primes);
     m.def("mul_inv", [](py::int_ a, i64 b) { return mul_inv(py_to_u128(a), b); });
     m.def("set_num_threads", &set_default_threads);

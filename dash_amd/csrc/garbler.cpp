@@ -1,3 +1,5 @@
+#include <cstdio>
+#include <cstdlib>
 // Host garbler: turns a quantized layer list into a GarbledModel.
 //
 // Layer-level behaviour follows the reference garbled layers
@@ -296,6 +298,9 @@ GarbledModel Garbler::garble(const std::vector<LayerSpec>& layers, const std::ve
 
     std::unique_ptr<GpuGarbler> gpu;
     if (opt.device >= 0) gpu.reset(new GpuGarbler(crt_, mrs_, seed_, R_, Z_, opt.device));
+    // which copy of `cur` is current: GPU layers read and write the device copy,
+    // host layers the host copy; a copy is refreshed only when the other side changed it
+    bool host_ok = true, dev_ok = false;
 
     // Input base labels
     i64 N = 1;
@@ -382,6 +387,8 @@ GarbledModel Garbler::garble(const std::vector<LayerSpec>& layers, const std::ve
                 const i64 s = it->second[0];
                 DASH_CHECK(s >= -1 && s < static_cast<i64>(li), "in_src must name an earlier layer");
                 cur = saved[s + 1];
+                host_ok = true;
+                dev_ok = false;
                 cur_mod = saved_mod[s + 1];
                 dims = saved_dims[s + 1];
             }
@@ -398,6 +405,16 @@ GarbledModel Garbler::garble(const std::vector<LayerSpec>& layers, const std::ve
             return true;
         };
 
+        const bool on_gpu = gpu && (spec.kind == K_CONV || spec.kind == K_RELU || spec.kind == K_SIGN ||
+                                    (spec.kind == K_RESCALE && param1(spec.p, "mode", 0) == 0 && crt_[0] == 2));
+        const bool passthru = spec.kind == K_FLATTEN;
+        if (on_gpu && !dev_ok) {
+            gpu->to_device(cur);
+            dev_ok = true;
+        } else if (!on_gpu && !passthru && !host_ok) {
+            gpu->to_host(cur);
+            host_ok = true;
+        }
         switch (spec.kind) {
             case K_FLATTEN: {
                 dims = {Nin};
@@ -469,6 +486,16 @@ GarbledModel Garbler::garble(const std::vector<LayerSpec>& layers, const std::ve
                     for (i64 f = 0; f < G.F; ++f)
                         lab_affine(bias.ptr<comp_t>() + f * mi.n, Zp, pmod(pmod(b[f], M_), p), R_.get(p), mi.n, p);
                     g.a[arr_name("bias.", j, "")] = bias;
+                }
+                if (gpu) {
+                    gpu->conv(G, std::vector<i64>(wa.ptr<i64>(), wa.ptr<i64>() + wa.count()), cur);
+                    dims = {G.F, G.OH, G.OW};
+                    break;
+                }
+                for (int j = 0; j < k; ++j) {
+                    const int p = crt_[j];
+                    const ModInfo& mi = mod_info(p);
+                    const comp_t* Zp = Z_.get(p);
                     Labels O(p, G.out_size());
                     const Labels& I = cur[j];
                     parallel_for(G.out_size(), [&](i64 b0, i64 b1) {
@@ -507,10 +534,13 @@ GarbledModel Garbler::garble(const std::vector<LayerSpec>& layers, const std::ve
                 SignPlan sp(crt_, mrs_, {2}, 0, 1);
                 ReluTables t = make_relu_tables(sp, Nin, sum_crt, k);
                 CrtLabels nxt;
-                for (int j = 0; j < k; ++j) nxt.emplace_back(crt_[j], Nin);
                 if (gpu) {
-                    gpu->sign_layer(L, sp, cur, t.approx, t.cast1, t.cast2, t.sign, nxt, &crt_, &prefix, &t.g, &t.e);
-                } else parallel_for(Nin, [&](i64 b0, i64 b1) {
+                    gpu->sign_layer(L, sp, cur, t.approx, t.cast1, t.cast2, t.sign, &crt_, &prefix, &t.g, &t.e);
+                    put_relu_tables(g, "", t);
+                    break;
+                }
+                for (int j = 0; j < k; ++j) nxt.emplace_back(crt_[j], Nin);
+                parallel_for(Nin, [&](i64 b0, i64 b1) {
                     std::vector<const comp_t*> x(k);
                     std::vector<comp_t*> y(k);
                     for (i64 e = b0; e < b1; ++e) {
@@ -532,10 +562,12 @@ GarbledModel Garbler::garble(const std::vector<LayerSpec>& layers, const std::ve
                 Array ap(DType::u128, {Nin, sp.n_approx}), c1(DType::u128, {Nin, std::max<i64>(sp.n_cast, 1)}),
                     c2(DType::u128, {Nin, std::max<i64>(sp.n_cast, 1)}), sg(DType::u128, {Nin, sp.n_sign});
                 CrtLabels nxt;
-                for (int j = 0; j < k; ++j) nxt.emplace_back(crt_[j], Nin);
                 if (gpu) {
-                    gpu->sign_layer(L, sp, cur, ap, c1, c2, sg, nxt, nullptr, nullptr, nullptr, nullptr);
-                } else parallel_for(Nin, [&](i64 b0, i64 b1) {
+                    gpu->sign_layer(L, sp, cur, ap, c1, c2, sg, nullptr, nullptr, nullptr, nullptr);
+                } else {
+                    for (int j = 0; j < k; ++j) nxt.emplace_back(crt_[j], Nin);
+                }
+                if (!gpu) parallel_for(Nin, [&](i64 b0, i64 b1) {
                     std::vector<const comp_t*> x(k);
                     std::vector<comp_t*> y(k);
                     for (i64 e = b0; e < b1; ++e) {
@@ -552,7 +584,7 @@ GarbledModel Garbler::garble(const std::vector<LayerSpec>& layers, const std::ve
                 g.a["s.cast1"] = c1;
                 g.a["s.cast2"] = c2;
                 g.a["s.sign"] = sg;
-                cur = std::move(nxt);
+                if (!gpu) cur = std::move(nxt);
                 break;
             }
             case K_RESCALE: {
@@ -587,7 +619,8 @@ GarbledModel Garbler::garble(const std::vector<LayerSpec>& layers, const std::ve
                     } else {
                         be = Array(DType::u128, {Nin, P.n_be});
                     }
-                    if (gpu && P.sign_be) {
+                    if (on_gpu) {
+                        DASH_CHECK(P.sign_be, "gpu garbler: legacy rescale plan without sign base extension");
                         gpu->rescale_legacy_iter(L, static_cast<int>(it), P, cur, up_base, dn, tr, ap, c1, c2, sg);
                     } else parallel_for(Nin, [&](i64 b0, i64 b1) {
                         std::vector<comp_t*> Lp(k);
@@ -826,7 +859,13 @@ GarbledModel Garbler::garble(const std::vector<LayerSpec>& layers, const std::ve
             default:
                 throw std::runtime_error(std::string("dash: cannot garble layer kind ") + std::to_string(spec.kind));
         }
+        if (on_gpu) host_ok = false;
+        else if (!passthru) dev_ok = false;
         if (keep[li + 1]) {
+            if (!host_ok) {
+                gpu->to_host(cur);
+                host_ok = true;
+            }
             saved[li + 1] = cur;
             saved_mod[li + 1] = cur_mod;
             saved_dims[li + 1] = dims;
@@ -835,6 +874,7 @@ GarbledModel Garbler::garble(const std::vector<LayerSpec>& layers, const std::ve
         layer_ms_[li] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_layer).count();
     }
 
+    if (!host_ok) gpu->to_host(cur);
     // Decoding information (reference gci.h:386-415)
     dec_ = Decoder();
     dec_.moduli = cur_mod;

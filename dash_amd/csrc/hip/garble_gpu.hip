@@ -16,7 +16,13 @@
 
 #include <algorithm>
 #include <cstring>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <map>
 #include <memory>
+#include <mutex>
+#include <string>
 
 #include "../layers.h"
 #include "dev.h"
@@ -120,23 +126,57 @@ struct Gadget {
     const Proj* projs;
     int nprojs;
     int64_t entries;  // per element
+    int nblk;         // AES-CTR blocks drawn per element (sum over draws)
     uint64_t layer, sslot, mask;  // PRG stream of this gadget: stream_of(layer, sslot, e, mask)
     int16_t* S;       // scratch [N][nslots][kW]
     int64_t N;
 };
 
-// one thread per (element, draw)
-__global__ __launch_bounds__(256) void k_draw(Ctx c, Gadget g) {
+// Stage a gadget's small descriptor array (draws / projections) in LDS so the
+// per-thread binary search costs LDS, not dependent global round trips.
+constexpr int kMaxDesc = 224;  // 224 x 72-B Proj + the 64 KiB AES image <= 80 KiB: 2 WGs/CU
+constexpr int kGB = 512;        // threads per block of the AES-bound garbling kernels
+template <class T>
+__device__ __forceinline__ void lds_stage(T* dst, const T* src, int n) {
+    const int words = n * static_cast<int>(sizeof(T) / 4);
+    const uint32_t* s = reinterpret_cast<const uint32_t*>(src);
+    uint32_t* d = reinterpret_cast<uint32_t*>(dst);
+    for (int i = threadIdx.x; i < words; i += blockDim.x) d[i] = s[i];
+}
+
+// one thread per (element, AES-CTR block): each block yields two label
+// components of one draw (Prg::label order), so neighbouring lanes write
+// neighbouring components and every lane does exactly one AES.
+__global__ __launch_bounds__(kGB) void k_draw(Ctx c, Gadget g) {
     __shared__ uint32_t lds_aes[DASH_AES_LDS_WORDS];
+    __shared__ Draw sd[kMaxDesc];
+    lds_stage(sd, g.draws, g.ndraws);
     aes_lds_fill(lds_aes, c.te0);
     const AesCtx aes = aes_ctx(lds_aes, nullptr);
-    const int64_t total = g.N * g.ndraws;
+    const int64_t total = g.N * g.nblk;
     for (int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < total;
          i += static_cast<int64_t>(gridDim.x) * blockDim.x) {
-        const int64_t e = i / g.ndraws;
-        const Draw d = g.draws[i % g.ndraws];
-        int16_t* out = g.S + (e * g.nslots + d.slot) * kW;
-        prg_label(aes, c.rk, stream_of(g.layer, g.sslot, static_cast<uint64_t>(e), g.mask), d.ctr, c.mc[d.q], out);
+        const int64_t e = i / g.nblk;
+        const int b = static_cast<int>(i - e * g.nblk);
+        int lo = 0, hi = g.ndraws - 1;
+        while (lo < hi) {  // last draw with ctr <= b
+            const int mid = (lo + hi + 1) >> 1;
+            if (sd[mid].ctr <= b) lo = mid;
+            else hi = mid - 1;
+        }
+        const Draw d = sd[lo];
+        const ModC m = c.mc[d.q];
+        const int j = 2 * (b - d.ctr);
+        const uint64_t stream = stream_of(g.layer, g.sslot, static_cast<uint64_t>(e), g.mask);
+        const u128 r = aes_keyed(aes, (static_cast<u128>(stream) << 64) | static_cast<uint64_t>(b), c.rk);
+        const uint32_t v0 = modq64(static_cast<uint64_t>(r), m);
+        int16_t* out = g.S + (e * g.nslots + d.slot) * kW + j;
+        if (j + 1 < static_cast<int>(m.n)) {
+            const uint32_t v1 = modq64(static_cast<uint64_t>(r >> 64), m);
+            *reinterpret_cast<uint32_t*>(out) = v0 | (v1 << 16);
+        } else {
+            out[0] = static_cast<int16_t>(v0);
+        }
     }
 }
 
@@ -183,37 +223,75 @@ __global__ __launch_bounds__(256) void k_sign_derive(Ctx c, Gadget g, SignSlots 
     }
 }
 
+// Label rows are contiguous int16 runs (label-major inputs, kW-wide slots).
+// Loading one component per loop iteration would make every component a
+// dependent memory round trip; stage kPC components of both operands first.
+constexpr int kPC = 16;
+
+// key = x + i*R (mod m), compressed from the least significant digit
+__device__ __forceinline__ u128 proj_key(const int16_t* x, const int16_t* R, int i, const ModC& m, uint32_t& color) {
+    CompressFwd kc;
+    kc.init();
+    const int n = static_cast<int>(m.n);
+    for (int q0 = 0; q0 < n; q0 += kPC) {
+        int16_t xa[kPC], ra[kPC];
+#pragma unroll
+        for (int u = 0; u < kPC; ++u) {
+            xa[u] = q0 + u < n ? x[q0 + u] : int16_t(0);
+            ra[u] = q0 + u < n ? R[q0 + u] : int16_t(0);
+        }
+#pragma unroll
+        for (int u = 0; u < kPC; ++u)
+            if (q0 + u < n) kc.push(modq(static_cast<uint32_t>(xa[u] + i * ra[u]), m), m);
+    }
+    color = modq(static_cast<uint32_t>(x[0] + i * R[0]), m);
+    return kc.finish();
+}
+
+// payload = o + f*R (mod m), o, f, R in [0, m)
+__device__ __forceinline__ u128 proj_payload(const int16_t* o, const int16_t* R, uint32_t f, const ModC& m) {
+    CompressFwd pc;
+    pc.init();
+    const int n = static_cast<int>(m.n);
+    for (int q0 = 0; q0 < n; q0 += kPC) {
+        int16_t oa[kPC], ra[kPC];
+#pragma unroll
+        for (int u = 0; u < kPC; ++u) {
+            oa[u] = q0 + u < n ? o[q0 + u] : int16_t(0);
+            ra[u] = q0 + u < n ? R[q0 + u] : int16_t(0);
+        }
+#pragma unroll
+        for (int u = 0; u < kPC; ++u)
+            if (q0 + u < n)
+                pc.push(modq(static_cast<uint32_t>(oa[u]) + f * static_cast<uint32_t>(ra[u]), m), m);
+    }
+    return pc.finish();
+}
+
 // one thread per (element, table entry)
-__global__ __launch_bounds__(256) void k_project(Ctx c, Gadget g, In in, Tables tb) {
+__global__ __launch_bounds__(kGB) void k_project(Ctx c, Gadget g, In in, Tables tb) {
     __shared__ uint32_t lds_aes[DASH_AES_LDS_WORDS];
+    __shared__ Proj sp[kMaxDesc];
+    lds_stage(sp, g.projs, g.nprojs);
     aes_lds_fill(lds_aes, c.te0);
     const AesCtx aes = aes_ctx(lds_aes, nullptr);
     const int64_t total = g.N * g.entries;
     for (int64_t gi = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; gi < total;
          gi += static_cast<int64_t>(gridDim.x) * blockDim.x) {
         const int64_t e = gi / g.entries;
-        const int64_t r = gi % g.entries;
+        const int64_t r = gi - e * g.entries;
         int lo = 0, hi = g.nprojs - 1;
         while (lo < hi) {  // last projection with first <= r
             const int mid = (lo + hi + 1) >> 1;
-            if (g.projs[mid].first <= r) lo = mid;
+            if (sp[mid].first <= r) lo = mid;
             else hi = mid - 1;
         }
-        const Proj P = g.projs[lo];
+        const Proj& P = sp[lo];
         const int i = static_cast<int>(r - P.first);
         const ModC mi = c.mc[P.pin], mo = c.mc[P.pout];
         const int16_t* inl = label_ref(c, g, in, e, P.in_kind, P.in_idx, P.pin);
-        const int16_t* Rin = c.R + static_cast<int64_t>(P.pin) * kW;
-        // key = in + i*Rin (mod pin), compressed streaming from the least significant digit
-        CompressFwd kc;
-        kc.init();
-        uint32_t color = 0;
-        for (int q = 0; q < static_cast<int>(mi.n); ++q) {
-            const uint32_t v = modq(static_cast<uint32_t>(inl[q] + i * Rin[q]), mi);
-            if (q == 0) color = v;
-            kc.push(v, mi);
-        }
-        const u128 H = aes_encrypt(aes, kc.finish());
+        uint32_t color;
+        const u128 H = aes_encrypt(aes, proj_key(inl, c.R + static_cast<int64_t>(P.pin) * kW, i, mi, color));
         // function value
         int64_t f;
         switch (P.fn) {
@@ -237,13 +315,8 @@ __global__ __launch_bounds__(256) void k_project(Ctx c, Gadget g, In in, Tables 
         const int16_t* ol = g.S + (e * g.nslots + P.out_slot) * kW;
         const int16_t* oR = P.outr_kind == R_BANK ? c.R + static_cast<int64_t>(P.pout) * kW
                                                   : label_ref(c, g, in, e, S_INPUT, P.outr_idx, 0);
-        CompressFwd pc;
-        pc.init();
-        for (int q = 0; q < static_cast<int>(mo.n); ++q) {
-            // ol, cm, oR in [0, pout): < pout^2 + pout, 32-bit reduction
-            pc.push(modq(static_cast<uint32_t>(ol[q]) + static_cast<uint32_t>(cm) * static_cast<uint32_t>(oR[q]), mo), mo);
-        }
-        tb.t[P.table][e * tb.row[P.table] + P.off + static_cast<int64_t>(color) * P.stride] = pc.finish() + H;
+        const u128 pay = proj_payload(ol, oR, static_cast<uint32_t>(cm), mo);
+        tb.t[P.table][e * tb.row[P.table] + P.off + static_cast<int64_t>(color) * P.stride] = pay + H;
     }
 }
 
@@ -302,77 +375,162 @@ struct RsArgs {
     int k;
     int crt[kMaxRes];
     int inv[kMaxRes];
+    int ctr[kMaxRes];          // first trans-label AES-CTR block of residue j
     int16_t* L[kMaxRes];       // [N][n_j], updated in place
     const int16_t* up;         // [k][kW]
     const int16_t* down;       // [k][kW]
     uint64_t layer, sslot;     // trans stream = stream_of(layer, sslot, e, 0)
 };
 
-__global__ __launch_bounds__(256) void k_rescale_pre(Ctx c, RsArgs a, Tables tb, int64_t N) {
+// One thread per (element, residue j >= 1): the trans projection of the
+// mod-2 residue into residue j plus the in-place update of L_j. The trans
+// output label is drawn one AES-CTR block (two components) at a time and
+// consumed at once (no per-thread label array, no scratch). L_0 is not
+// written here: the sign gadget reads Z_2 for residue 0 directly (In with a
+// zero element stride) and k_rescale_post_g overwrites L_0 afterwards.
+__global__ __launch_bounds__(kGB) void k_rescale_pre(Ctx c, RsArgs a, Tables tb, int64_t N) {
     __shared__ uint32_t lds_aes[DASH_AES_LDS_WORDS];
     aes_lds_fill(lds_aes, c.te0);
     const AesCtx aes = aes_ctx(lds_aes, nullptr);
-    for (int64_t e = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; e < N;
-         e += static_cast<int64_t>(gridDim.x) * blockDim.x) {
-        for (int j = 0; j < a.k; ++j) {
-            const int p = a.crt[j], n = static_cast<int>(c.mc[p].n);
-            int16_t* L = a.L[j] + e * n;
-            for (int q = 0; q < n; ++q) {
-                int v = L[q] + a.up[j * kW + q];
-                L[q] = static_cast<int16_t>(v >= p ? v - p : v);
+    const int km = a.k - 1;
+    const ModC m2 = c.mc[2];
+    const int16_t* R2 = c.R + 2 * kW;
+    for (int64_t gi = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; gi < N * km;
+         gi += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+        const int64_t e = gi / km;
+        const int j = 1 + static_cast<int>(gi - e * km);
+        const int p = a.crt[j];
+        const ModC mj = c.mc[p];
+        const int n = static_cast<int>(mj.n);
+        // keys of the two trans rows: (L_0 + up_0) + i*R_2 over GF(2)
+        const int16_t* L0 = a.L[0] + e * m2.n;
+        CompressFwd k0, k1;
+        k0.init();
+        k1.init();
+        for (int q0 = 0; q0 < static_cast<int>(m2.n); q0 += kPC) {
+            int16_t la[kPC], ua[kPC], ra[kPC];
+#pragma unroll
+            for (int u = 0; u < kPC; ++u) {
+                la[u] = L0[q0 + u];  // m2.n = 128 is a multiple of kPC
+                ua[u] = a.up[q0 + u];
+                ra[u] = R2[q0 + u];
+            }
+#pragma unroll
+            for (int u = 0; u < kPC; ++u) {
+                const uint32_t v = static_cast<uint32_t>(la[u] + ua[u]) & 1u;
+                k0.push(v, m2);
+                k1.push((v + static_cast<uint32_t>(ra[u])) & 1u, m2);
             }
         }
+        const uint32_t color0 = static_cast<uint32_t>(L0[0] + a.up[0]) & 1u;
+        const u128 H0 = aes_encrypt(aes, k0.finish());
+        const u128 H1 = aes_encrypt(aes, k1.finish());
         const uint64_t stream = stream_of(a.layer, a.sslot, static_cast<uint64_t>(e), 0);
-        uint64_t ctr = 0;
-        int16_t out0[kW];
-        const int16_t* L0 = a.L[0] + e * c.mc[2].n;
-        const ModC m2 = c.mc[2];
-        for (int j = 1; j < a.k; ++j) {
-            const int p = a.crt[j];
-            const ModC mj = c.mc[p];
-            prg_label(aes, c.rk, stream, ctr, mj, out0);
-            ctr += (mj.n + 1) / 2;
-            const int16_t* Rp = c.R + static_cast<int64_t>(p) * kW;
-            for (int i = 0; i < 2; ++i) {
-                CompressFwd kc;
-                kc.init();
-                uint32_t color = 0;
-                for (int q = 0; q < static_cast<int>(m2.n); ++q) {
-                    const uint32_t v = static_cast<uint32_t>(L0[q] + i * c.R[2 * kW + q]) & 1u;
-                    if (q == 0) color = v;
-                    kc.push(v, m2);
-                }
-                const u128 H = aes_encrypt(aes, kc.finish());
-                CompressFwd pc;
-                pc.init();
-                for (int q = 0; q < static_cast<int>(mj.n); ++q)
-                    pc.push(modq(static_cast<uint32_t>(out0[q] + i * Rp[q]), mj), mj);
-                tb.t[6][e * tb.row[6] + (j - 1) * 2 + color] = pc.finish() + H;
-            }
-            int16_t* L = a.L[j] + e * mj.n;
-            for (int q = 0; q < static_cast<int>(mj.n); ++q) {
-                int v = L[q] - out0[q];
+        const int16_t* Rp = c.R + static_cast<int64_t>(p) * kW;
+        const int16_t* upj = a.up + j * kW;
+        int16_t* L = a.L[j] + e * n;
+        CompressFwd p0, p1;
+        p0.init();
+        p1.init();
+        for (int q = 0; q < n; q += 2) {
+            const u128 r = aes_keyed(aes, (static_cast<u128>(stream) << 64) | static_cast<uint64_t>(a.ctr[j] + (q >> 1)),
+                                     c.rk);
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                if (q + h >= n) break;
+                const uint32_t o = modq64(static_cast<uint64_t>(h ? r >> 64 : r), mj);
+                p0.push(o, mj);
+                p1.push(modq(o + static_cast<uint32_t>(Rp[q + h]), mj), mj);
+                int v = L[q + h] + upj[q + h];
+                if (v >= p) v -= p;
+                v -= static_cast<int>(o);
                 if (v < 0) v += p;
-                L[q] = static_cast<int16_t>(modq(static_cast<uint32_t>(v * a.inv[j]), mj));
+                L[q + h] = static_cast<int16_t>(modq(static_cast<uint32_t>(v * a.inv[j]), mj));
             }
         }
-        int16_t* Lz = a.L[0] + e * m2.n;
-        for (int q = 0; q < static_cast<int>(m2.n); ++q) Lz[q] = c.Z[2 * kW + q];
+        u128* row = tb.t[6] + e * tb.row[6] + (j - 1) * 2;
+        const uint32_t color1 = static_cast<uint32_t>(L0[0] + a.up[0] + R2[0]) & 1u;
+        row[color0] = p0.finish() + H0;
+        row[color1] = p1.finish() + H1;
     }
 }
 
-// After the sign gadget: L_0 = sign output; L -= down.
+// After the sign gadget: L_0 = sign output; L -= down. Elementwise over
+// (residue j = blockIdx.y, element-component e*n_j + q).
 __global__ __launch_bounds__(256) void k_rescale_post_g(Ctx c, RsArgs a, Gadget g, int sig_slot) {
-    const int64_t e = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-    if (e >= g.N) return;
-    const int16_t* sig = g.S + (e * g.nslots + sig_slot) * kW;
-    for (int j = 0; j < a.k; ++j) {
-        const int p = a.crt[j], n = static_cast<int>(c.mc[p].n);
-        int16_t* L = a.L[j] + e * n;
-        for (int q = 0; q < n; ++q) {
-            int v = (j == 0 ? sig[q] : L[q]) - a.down[j * kW + q];
-            L[q] = static_cast<int16_t>(v < 0 ? v + p : v);
+    const int j = blockIdx.y;
+    const int p = a.crt[j], n = static_cast<int>(c.mc[p].n);
+    const int16_t* dn = a.down + j * kW;
+    int16_t* L = a.L[j];
+    for (int64_t x = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; x < g.N * n;
+         x += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+        const int64_t e = x / n;
+        const int q = static_cast<int>(x - e * n);
+        int v = (j == 0 ? g.S[(e * g.nslots + sig_slot) * kW + q] : L[x]) - dn[q];
+        L[x] = static_cast<int16_t>(v < 0 ? v + p : v);
+    }
+}
+
+// Conv base labels (garbler side of the free linear layer, garbler.cpp K_CONV):
+// y[o][c] = (sum_{k: w[f][k] != 0} w[f][k] * x_k[c] + zc[f] * Z[c]) mod p with
+// x_k the input label under tap k (Z for padding taps). One thread per
+// (output position, component); kFT filters per thread so every input
+// component load feeds kFT MACs. Weights are laid out [f-chunk][K][kFT] and
+// indexed uniformly across the block, so they arrive as scalar loads.
+constexpr int kFT = 16;
+struct ConvG {
+    int C, H, W, F, kh, kw, sh, sw, ph, pw, OH, OW, K, n, p;
+};
+__global__ __launch_bounds__(256) void k_conv_garble(ConvG g, const int16_t* __restrict__ X, int16_t* __restrict__ Y,
+                                                     const int32_t* __restrict__ w, const int32_t* __restrict__ zc,
+                                                     const int16_t* __restrict__ Zp) {
+    const int f0 = blockIdx.y * kFT;
+    const int npos = g.OH * g.OW;
+    const int64_t t = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (t >= static_cast<int64_t>(npos) * g.n) return;
+    const int pos = static_cast<int>(t / g.n), c = static_cast<int>(t - static_cast<int64_t>(pos) * g.n);
+    const int oy = pos / g.OW, ox = pos - oy * g.OW;
+    const int32_t* wc = w + static_cast<int64_t>(blockIdx.y) * g.K * kFT;
+    const int zv = Zp[c];
+    uint32_t acc[kFT];
+#pragma unroll
+    for (int f = 0; f < kFT; ++f) acc[f] = 0;
+    int k = 0;
+    for (int ci = 0; ci < g.C; ++ci)
+        for (int dy = 0; dy < g.kh; ++dy) {
+            const int iy = oy * g.sh - g.ph + dy;
+            for (int dx = 0; dx < g.kw; ++dx, ++k) {
+                const int ix = ox * g.sw - g.pw + dx;
+                const bool in = iy >= 0 && iy < g.H && ix >= 0 && ix < g.W;
+                const uint32_t xv = static_cast<uint32_t>(
+                    in ? X[(static_cast<int64_t>(ci * g.H + iy) * g.W + ix) * g.n + c] : zv);
+                const int32_t* wk = wc + k * kFT;
+#pragma unroll
+                for (int f = 0; f < kFT; ++f) acc[f] += static_cast<uint32_t>(wk[f]) * xv;
+            }
         }
+#pragma unroll
+    for (int f = 0; f < kFT; ++f) {
+        if (f0 + f >= g.F) break;
+        const uint32_t v = (acc[f] + static_cast<uint32_t>(zc[f0 + f]) * static_cast<uint32_t>(zv)) % static_cast<uint32_t>(g.p);
+        Y[(static_cast<int64_t>(f0 + f) * npos + pos) * g.n + c] = static_cast<int16_t>(v);
+    }
+}
+
+// Sign layer outputs: slot out_slot0 + o of every element -> label-major out[o]
+struct GatherArgs {
+    int16_t* out[kMaxRes];
+    int n[kMaxRes];
+    int k, slot0;
+};
+__global__ __launch_bounds__(256) void k_gather_slots(Gadget g, GatherArgs a) {
+    const int o = blockIdx.y;
+    const int n = a.n[o];
+    for (int64_t x = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; x < g.N * n;
+         x += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+        const int64_t e = x / n;
+        const int q = static_cast<int>(x - e * n);
+        a.out[o][x] = g.S[(e * g.nslots + a.slot0 + o) * kW + q];
     }
 }
 
@@ -483,15 +641,228 @@ T* dput(const T* h, size_t n, std::vector<void*>& owned) {
 
 }  // namespace gg
 
+
+// DASH_GG_TRACE=1: per-call phase timings on stderr (upload / alloc / kernels / download)
+struct PhaseTrace {
+    bool on = std::getenv("DASH_GG_TRACE") != nullptr;
+    const char* what;
+    std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now(), t = t0;
+    std::string line;
+    explicit PhaseTrace(const char* w) : what(w) {}
+    void mark(const char* phase) {
+        if (!on) return;
+        const auto n = std::chrono::steady_clock::now();
+        line += std::string(" ") + phase + "=" + std::to_string(std::chrono::duration<double, std::milli>(n - t).count());
+        t = n;
+    }
+    ~PhaseTrace() {
+        if (on) std::fprintf(stderr, "[gg] %s%s\n", what, line.c_str());
+    }
+};
+
+// ------------------------------------------------------- table block cache
+namespace {
+struct BlockCache {
+    std::mutex m;
+    std::multimap<std::pair<int, size_t>, void*> free;
+    size_t cached = 0;
+    size_t cap = static_cast<size_t>(std::getenv("DASH_GG_CACHE_GB") ? std::atof(std::getenv("DASH_GG_CACHE_GB")) * 1e9
+                                                                      : 16e9);
+};
+BlockCache& block_cache() {
+    static BlockCache* c = new BlockCache();  // leaked: deleters may run during static destruction
+    return *c;
+}
+
+void* cache_get(int device, size_t bytes) {
+    BlockCache& c = block_cache();
+    {
+        std::lock_guard<std::mutex> g(c.m);
+        auto it = c.free.find({device, bytes});
+        if (it != c.free.end()) {
+            void* p = it->second;
+            c.free.erase(it);
+            c.cached -= bytes;
+            return p;
+        }
+    }
+    void* p = nullptr;
+    HIPCHECK(hipMalloc(&p, bytes));
+    return p;
+}
+
+void cache_put(int device, void* p, size_t bytes) {
+    if (!p) return;
+    BlockCache& c = block_cache();
+    {
+        std::lock_guard<std::mutex> g(c.m);
+        if (c.cached + bytes <= c.cap) {
+            c.free.emplace(std::make_pair(device, bytes), p);
+            c.cached += bytes;
+            return;
+        }
+    }
+    (void)hipFree(p);
+}
+}  // namespace
+
+void gpu_table_cache_trim() {
+    BlockCache& c = block_cache();
+    std::lock_guard<std::mutex> g(c.m);
+    for (auto& kv : c.free) (void)hipFree(kv.second);
+    c.free.clear();
+    c.cached = 0;
+}
+
+size_t gpu_table_cache_bytes() {
+    BlockCache& c = block_cache();
+    std::lock_guard<std::mutex> g(c.m);
+    return c.cached;
+}
+
+namespace {
+inline unsigned blocks_for(int64_t n, int bs, int cap = 65536) {
+    return static_cast<unsigned>(std::max<int64_t>(1, std::min<int64_t>((n + bs - 1) / bs, cap)));
+}
+
+// a cached device block with RAII return to the cache
+struct DevBlock {
+    void* p = nullptr;
+    size_t bytes = 0;
+    int device = 0;
+    DevBlock() = default;
+    DevBlock(const DevBlock&) = delete;
+    DevBlock& operator=(const DevBlock&) = delete;
+    DevBlock(DevBlock&& o) noexcept { *this = std::move(o); }
+    DevBlock& operator=(DevBlock&& o) noexcept {
+        release();
+        p = o.p;
+        bytes = o.bytes;
+        device = o.device;
+        o.p = nullptr;
+        return *this;
+    }
+    ~DevBlock() { release(); }
+    void alloc(int dev, size_t b) {
+        release();
+        device = dev;
+        bytes = std::max<size_t>(16, b);
+        p = cache_get(dev, bytes);
+    }
+    void release() {
+        if (p) cache_put(device, p, bytes);
+        p = nullptr;
+    }
+    template <class T>
+    T* as() const {
+        return static_cast<T*>(p);
+    }
+};
+
+struct DevTable {
+    DevBlock b;
+    int64_t row = 0;
+    void alloc(int device, int64_t N, int64_t r) {
+        row = r;
+        b.alloc(device, static_cast<size_t>(N) * r * sizeof(u128));
+        HIPCHECK(hipMemsetAsync(b.p, 0, b.bytes, nullptr));
+    }
+    u128* p() const { return b.as<u128>(); }
+    // hand the buffer to `a` as a device-resident array (kept in HBM; the
+    // evaluator on this node copies it device-to-device). Its deleter returns
+    // the block to the cache.
+    void to_array(Array& a, int device) {
+        DASH_CHECK(a.nbytes <= b.bytes && (a.nbytes == static_cast<size_t>(b.bytes) || a.nbytes < 16),
+                   "gpu garbler: table size mismatch");
+        auto d = std::make_shared<Array::Device>();
+        const size_t bytes = b.bytes;
+        d->p = std::shared_ptr<void>(b.p, [device, bytes](void* x) { cache_put(device, x, bytes); });
+        b.p = nullptr;
+        d->device = device;
+        d->fetch = [device](void* h, const void* dv, size_t n) {
+            HIPCHECK(hipSetDevice(device));
+            HIPCHECK(hipMemcpy(h, dv, n, hipMemcpyDeviceToHost));
+        };
+        a = Array::on_device(a.dtype, a.shape, std::move(d));
+    }
+};
+
+// AES-CTR blocks per element: draws are laid out back to back in counter order
+int draw_blocks(const std::vector<gg::Draw>& d) {
+    if (d.empty()) return 0;
+    return d.back().ctr + (nr_comps(d.back().q) + 1) / 2;
+}
+
+void check_desc(const gg::Gadget& g) {
+    DASH_CHECK(g.ndraws <= gg::kMaxDesc && g.nprojs <= gg::kMaxDesc,
+               "gpu garbler: gadget descriptor exceeds the LDS-staged limit");
+}
+
+// run the three sign-gadget passes for N elements with input labels `in`
+void run_sign(const gg::Ctx& c, const gg::SignLayout& L, gg::Gadget& g, const gg::In& in, const gg::Tables& tb,
+              std::vector<void*>& tmp) {
+    g.draws = gg::dput(L.draws.data(), L.draws.size(), tmp);
+    g.ndraws = static_cast<int>(L.draws.size());
+    g.projs = gg::dput(L.projs.data(), L.projs.size(), tmp);
+    g.nprojs = static_cast<int>(L.projs.size());
+    g.entries = L.entries;
+    g.nblk = draw_blocks(L.draws);
+    check_desc(g);
+    hipLaunchKernelGGL(gg::k_draw, dim3(blocks_for(g.N * g.nblk, gg::kGB, 8192)), dim3(gg::kGB), 0, nullptr, c, g);
+    hipLaunchKernelGGL(gg::k_sign_derive, dim3(blocks_for(g.N, 256)), dim3(256), 0, nullptr, c, g, L.ss);
+    hipLaunchKernelGGL(gg::k_project, dim3(blocks_for(g.N * g.entries, gg::kGB, 16384)), dim3(gg::kGB), 0, nullptr, c,
+                       g, in, tb);
+    HIPCHECK(hipGetLastError());
+}
+
+// host labels whose authoritative copy is on the device: shape only
+void set_stale(CrtLabels& cur, const std::vector<int>& mods, int64_t N) {
+    cur.assign(mods.size(), Labels());
+    for (size_t j = 0; j < mods.size(); ++j) {
+        cur[j].p = mods[j];
+        cur[j].n = nr_comps(mods[j]);
+        cur[j].N = N;
+    }
+}
+}  // namespace
+
 struct GpuGarbler::Impl {
     gg::Ctx c{};
     std::vector<void*> owned;
+    // grow-only gadget scratch (label slots) reused by every layer
+    int16_t* S = nullptr;
+    size_t S_bytes = 0;
+    // device cur: per residue label-major [N][n_j]
+    std::vector<DevBlock> cur;
+    std::vector<int> cur_mod;
+    int64_t cur_N = 0;
     int max_mod = 0;
     std::vector<int> crt;
     int k = 0;
     int device = 0;
+    int16_t* scratch(size_t bytes) {
+        if (bytes > S_bytes) {
+            if (S) (void)hipFree(S);
+            HIPCHECK(hipMalloc(reinterpret_cast<void**>(&S), bytes));
+            S_bytes = bytes;
+        }
+        return S;
+    }
+    std::vector<DevBlock> alloc_labels(const std::vector<int>& mods, int64_t N) {
+        std::vector<DevBlock> v(mods.size());
+        for (size_t j = 0; j < mods.size(); ++j)
+            v[j].alloc(device, static_cast<size_t>(N) * nr_comps(mods[j]) * sizeof(int16_t));
+        return v;
+    }
+    void check_cur(const CrtLabels& host) const {
+        DASH_CHECK(host.size() == cur.size() && !host.empty() && host[0].N == cur_N,
+                   "gpu garbler: device labels out of sync with the host garbler");
+        for (size_t j = 0; j < host.size(); ++j) DASH_CHECK(host[j].p == cur_mod[j], "gpu garbler: modulus mismatch");
+    }
     ~Impl() {
+        cur.clear();
         for (void* p : owned) (void)hipFree(p);
+        if (S) (void)hipFree(S);
     }
 };
 
@@ -530,116 +901,115 @@ GpuGarbler::GpuGarbler(const std::vector<int>& crt, const std::vector<int>& mrs,
     }
 }
 
-GpuGarbler::~GpuGarbler() = default;
-
-namespace {
-inline unsigned blocks_for(int64_t n, int bs, int cap = 65536) {
-    return static_cast<unsigned>(std::max<int64_t>(1, std::min<int64_t>((n + bs - 1) / bs, cap)));
+GpuGarbler::~GpuGarbler() {
+    if (impl_) (void)hipSetDevice(impl_->device);
 }
 
-struct DevLabels {
-    std::vector<int16_t*> p;
-    std::vector<void*> owned;
-    ~DevLabels() {
-        for (void* q : owned) (void)hipFree(q);
-    }
-};
-
-void upload_labels(const CrtLabels& L, DevLabels& d) {
-    for (const auto& l : L) {
-        int16_t* x = nullptr;
-        HIPCHECK(hipMalloc(reinterpret_cast<void**>(&x), std::max<size_t>(1, l.c.size()) * sizeof(int16_t)));
-        HIPCHECK(hipMemcpy(x, l.c.data(), l.c.size() * sizeof(int16_t), hipMemcpyHostToDevice));
-        d.p.push_back(x);
-        d.owned.push_back(x);
-    }
-}
-
-void download_labels(const DevLabels& d, CrtLabels& L) {
-    for (size_t j = 0; j < L.size(); ++j)
-        HIPCHECK(hipMemcpy(L[j].c.data(), d.p[j], L[j].c.size() * sizeof(int16_t), hipMemcpyDeviceToHost));
-}
-
-struct DevTable {
-    u128* p = nullptr;
-    int64_t row = 0;
-    size_t bytes = 0;
-    ~DevTable() {
-        if (p) (void)hipFree(p);
-    }
-    void alloc(int64_t N, int64_t r) {
-        row = r;
-        bytes = static_cast<size_t>(N) * r * sizeof(u128);
-        HIPCHECK(hipMalloc(reinterpret_cast<void**>(&p), std::max<size_t>(16, bytes)));
-        HIPCHECK(hipMemset(p, 0, std::max<size_t>(16, bytes)));
-    }
-    // hand the buffer to `a` as a device-resident array (kept in HBM; the
-    // evaluator on this node copies it device-to-device)
-    void to_array(Array& a, int device) {
-        DASH_CHECK(a.nbytes == bytes, "gpu garbler: table size mismatch");
-        auto d = std::make_shared<Array::Device>();
-        d->p = std::shared_ptr<void>(p, [](void* x) { (void)hipFree(x); });
-        p = nullptr;
-        d->device = device;
-        d->fetch = [device](void* h, const void* dv, size_t n) {
-            HIPCHECK(hipSetDevice(device));
-            HIPCHECK(hipMemcpy(h, dv, n, hipMemcpyDeviceToHost));
-        };
-        a = Array::on_device(a.dtype, a.shape, std::move(d));
-    }
-};
-
-// run the three sign-gadget passes for N elements with input labels `in`
-void run_sign(const gg::Ctx& c, const gg::SignLayout& L, gg::Gadget& g, const gg::In& in, const gg::Tables& tb,
-              std::vector<void*>& tmp) {
-    g.draws = gg::dput(L.draws.data(), L.draws.size(), tmp);
-    g.ndraws = static_cast<int>(L.draws.size());
-    g.projs = gg::dput(L.projs.data(), L.projs.size(), tmp);
-    g.nprojs = static_cast<int>(L.projs.size());
-    g.entries = L.entries;
-    hipLaunchKernelGGL(gg::k_draw, dim3(blocks_for(g.N * g.ndraws, 256, 8192)), dim3(256), 0, nullptr, c, g);
-    hipLaunchKernelGGL(gg::k_sign_derive, dim3(blocks_for(g.N, 256)), dim3(256), 0, nullptr, c, g, L.ss);
-    hipLaunchKernelGGL(gg::k_project, dim3(blocks_for(g.N * g.entries, 256, 16384)), dim3(256), 0, nullptr, c, g, in,
-                       tb);
-    HIPCHECK(hipGetLastError());
-}
-}  // namespace
-
-void GpuGarbler::sign_layer(uint64_t layer, const SignPlan& sp, const CrtLabels& cur, Array& ap, Array& c1, Array& c2,
-                            Array& sg, CrtLabels& out, const std::vector<int>* relu_crt, const std::vector<i64>* prefix,
-                            Array* mmg, Array* mme) {
+void GpuGarbler::to_device(const CrtLabels& cur) {
     Impl& I = *impl_;
-    const int64_t N = cur[0].N;
+    HIPCHECK(hipSetDevice(I.device));
+    DASH_CHECK(!cur.empty(), "gpu garbler: no labels");
+    I.cur_mod.clear();
+    for (const auto& l : cur) I.cur_mod.push_back(l.p);
+    I.cur_N = cur[0].N;
+    I.cur = I.alloc_labels(I.cur_mod, I.cur_N);
+    for (size_t j = 0; j < cur.size(); ++j) {
+        DASH_CHECK(cur[j].c.size() == static_cast<size_t>(cur[j].N) * cur[j].n, "gpu garbler: host labels are stale");
+        HIPCHECK(hipMemcpy(I.cur[j].p, cur[j].c.data(), cur[j].c.size() * sizeof(int16_t), hipMemcpyHostToDevice));
+    }
+}
+
+void GpuGarbler::to_host(CrtLabels& cur) {
+    Impl& I = *impl_;
+    HIPCHECK(hipSetDevice(I.device));
+    I.check_cur(cur);
+    HIPCHECK(hipDeviceSynchronize());
+    for (size_t j = 0; j < cur.size(); ++j) {
+        cur[j].c.resize(static_cast<size_t>(cur[j].N) * cur[j].n);
+        HIPCHECK(hipMemcpy(cur[j].c.data(), I.cur[j].p, cur[j].c.size() * sizeof(int16_t), hipMemcpyDeviceToHost));
+    }
+}
+
+void GpuGarbler::conv(const ConvGeom& G, const std::vector<i64>& w, CrtLabels& cur) {
+    Impl& I = *impl_;
+    HIPCHECK(hipSetDevice(I.device));
+    I.check_cur(cur);
+    PhaseTrace tr_("conv");
+    const int K = static_cast<int>(G.K());
+    const int F = static_cast<int>(G.F);
+    const int nch = (F + gg::kFT - 1) / gg::kFT;
+    DASH_CHECK(static_cast<i64>(w.size()) == G.F * G.K(), "gpu garbler: conv weight shape");
+    DASH_CHECK(G.C * G.H * G.W == I.cur_N, "gpu garbler: conv input size mismatch");
+    std::vector<int> mods = I.cur_mod;
+    std::vector<DevBlock> out = I.alloc_labels(mods, G.out_size());
+    std::vector<void*> tmp;
+    for (size_t j = 0; j < mods.size(); ++j) {
+        const int p = mods[j];
+        std::vector<int32_t> wp(static_cast<size_t>(nch) * K * gg::kFT, 0), zc(static_cast<size_t>(nch) * gg::kFT, 0);
+        for (int f = 0; f < F; ++f) {
+            int z = 1;
+            for (int kk = 0; kk < K; ++kk) {
+                const int v = static_cast<int>(w[static_cast<size_t>(f) * K + kk] % p);
+                if (v == 0) ++z;
+                wp[(static_cast<size_t>(f / gg::kFT) * K + kk) * gg::kFT + f % gg::kFT] = v;
+            }
+            zc[f] = z;
+        }
+        gg::ConvG g{static_cast<int>(G.C), static_cast<int>(G.H), static_cast<int>(G.W), F, static_cast<int>(G.kh),
+                    static_cast<int>(G.kw), static_cast<int>(G.sh), static_cast<int>(G.sw), static_cast<int>(G.ph),
+                    static_cast<int>(G.pw), static_cast<int>(G.OH), static_cast<int>(G.OW), K, nr_comps(p), p};
+        const int32_t* dw = gg::dput(wp.data(), wp.size(), tmp);
+        const int32_t* dz = gg::dput(zc.data(), zc.size(), tmp);
+        const int64_t threads = G.OH * G.OW * static_cast<int64_t>(g.n);
+        DASH_CHECK((threads + 255) / 256 < (int64_t(1) << 31), "gpu garbler: conv grid too large");
+        hipLaunchKernelGGL(gg::k_conv_garble, dim3(static_cast<unsigned>((threads + 255) / 256), nch), dim3(256), 0,
+                           nullptr, g, I.cur[j].as<int16_t>(), out[j].as<int16_t>(), dw, dz,
+                           I.c.Z + static_cast<int64_t>(p) * gg::kW);
+    }
+    HIPCHECK(hipGetLastError());
+    HIPCHECK(hipDeviceSynchronize());
+    tr_.mark("kernels");
+    for (void* p : tmp) (void)hipFree(p);
+    I.cur = std::move(out);
+    I.cur_N = G.out_size();
+    set_stale(cur, mods, I.cur_N);
+}
+
+void GpuGarbler::sign_layer(uint64_t layer, const SignPlan& sp, CrtLabels& cur, Array& ap, Array& c1, Array& c2,
+                            Array& sg, const std::vector<int>* relu_crt, const std::vector<i64>* prefix, Array* mmg,
+                            Array* mme) {
+    Impl& I = *impl_;
+    HIPCHECK(hipSetDevice(I.device));
+    I.check_cur(cur);
+    PhaseTrace tr_(relu_crt ? "relu" : "sign");
+    const int64_t N = I.cur_N;
     const int k = I.k;
     std::vector<void*> tmp;
-    DevLabels din;
-    upload_labels(cur, din);
     const bool relu = relu_crt != nullptr;
     // relu: 2 slots per residue for the mixed-mult output labels sk03/sk04
     gg::SignLayout L = gg::sign_layout(sp, relu ? 2 * k : 0);
     int sk0 = L.nslots - (relu ? 2 * k : 0);
-    int16_t* S = nullptr;
-    HIPCHECK(hipMalloc(reinterpret_cast<void**>(&S), static_cast<size_t>(N) * L.nslots * gg::kW * sizeof(int16_t)));
-    tmp.push_back(S);
+    int16_t* S = I.scratch(static_cast<size_t>(N) * L.nslots * gg::kW * sizeof(int16_t));
     DevTable tA, t1, t2, tS, tG, tE;
-    tA.alloc(N, ap.shape[1]);
-    t1.alloc(N, c1.shape[1]);
-    t2.alloc(N, c2.shape[1]);
-    tS.alloc(N, sg.shape[1]);
+    tA.alloc(I.device, N, ap.shape[1]);
+    t1.alloc(I.device, N, c1.shape[1]);
+    t2.alloc(I.device, N, c2.shape[1]);
+    tS.alloc(I.device, N, sg.shape[1]);
     gg::Tables tb{};
-    tb.t[0] = tA.p; tb.row[0] = tA.row;
-    tb.t[1] = t1.p; tb.row[1] = t1.row;
-    tb.t[2] = t2.p; tb.row[2] = t2.row;
-    tb.t[3] = tS.p; tb.row[3] = tS.row;
+    tb.t[0] = tA.p(); tb.row[0] = tA.row;
+    tb.t[1] = t1.p(); tb.row[1] = t1.row;
+    tb.t[2] = t2.p(); tb.row[2] = t2.row;
+    tb.t[3] = tS.p(); tb.row[3] = tS.row;
     if (relu) {
-        tG.alloc(N, mmg->shape[1]);
-        tE.alloc(N, static_cast<int64_t>(k) * 3);
-        tb.t[4] = tG.p; tb.row[4] = tG.row;
-        tb.t[5] = tE.p; tb.row[5] = tE.row;
+        tG.alloc(I.device, N, mmg->shape[1]);
+        tE.alloc(I.device, N, static_cast<int64_t>(k) * 3);
+        tb.t[4] = tG.p(); tb.row[4] = tG.row;
+        tb.t[5] = tE.p(); tb.row[5] = tE.row;
     }
+    tr_.mark("alloc");
     gg::In in{};
     for (int j = 0; j < k; ++j) {
-        in.p[j] = din.p[j];
+        in.p[j] = I.cur[j].as<int16_t>();
         in.n[j] = nr_comps(I.crt[j]);
     }
     gg::Gadget g{};
@@ -650,7 +1020,8 @@ void GpuGarbler::sign_layer(uint64_t layer, const SignPlan& sp, const CrtLabels&
     g.N = N;
     g.nslots = L.nslots;
     run_sign(I.c, L, g, in, tb, tmp);
-    DevLabels dout;
+    std::vector<int> omods = relu ? I.crt : sp.out_mod;
+    std::vector<DevBlock> out = I.alloc_labels(omods, N);
     if (relu) {
         // mixed-mult draws (stream slot 2, counters run over the residues) and the g/e projections
         std::vector<gg::Draw> dr;
@@ -685,44 +1056,43 @@ void GpuGarbler::sign_layer(uint64_t layer, const SignPlan& sp, const CrtLabels&
         gm.projs = gg::dput(pr.data(), pr.size(), tmp);
         gm.nprojs = static_cast<int>(pr.size());
         gm.entries = first;
-        hipLaunchKernelGGL(gg::k_draw, dim3(blocks_for(N * gm.ndraws, 256, 8192)), dim3(256), 0, nullptr, I.c, gm);
-        hipLaunchKernelGGL(gg::k_project, dim3(blocks_for(N * gm.entries, 256, 16384)), dim3(256), 0, nullptr, I.c, gm,
-                           in, tb);
+        gm.nblk = draw_blocks(dr);
+        check_desc(gm);
+        hipLaunchKernelGGL(gg::k_draw, dim3(blocks_for(N * gm.nblk, gg::kGB, 8192)), dim3(gg::kGB), 0, nullptr, I.c, gm);
+        hipLaunchKernelGGL(gg::k_project, dim3(blocks_for(N * gm.entries, gg::kGB, 16384)), dim3(gg::kGB), 0, nullptr,
+                           I.c, gm, in, tb);
         gg::MiniArgs ma{};
         ma.k = k;
         for (int j = 0; j < k; ++j) ma.crt[j] = I.crt[j];
         ma.sig_slot = L.out_slot0;
         ma.sk_slot0 = sk0;
-        for (int j = 0; j < k; ++j) {
-            int16_t* x = nullptr;
-            HIPCHECK(hipMalloc(reinterpret_cast<void**>(&x), out[j].c.size() * sizeof(int16_t)));
-            dout.p.push_back(x);
-            dout.owned.push_back(x);
-            ma.out[j] = x;
-        }
+        for (int j = 0; j < k; ++j) ma.out[j] = out[j].as<int16_t>();
         hipLaunchKernelGGL(gg::k_relu_finish, dim3(blocks_for(N * k, 256, 8192)), dim3(256), 0, nullptr, I.c, gm, in,
                            tb, ma);
-        HIPCHECK(hipGetLastError());
-        HIPCHECK(hipDeviceSynchronize());
-        download_labels(dout, out);
         tG.to_array(*mmg, I.device);
         tE.to_array(*mme, I.device);
     } else {
-        HIPCHECK(hipDeviceSynchronize());
-        // sign layer outputs: out0[o] slots (one per CRT residue) -> label-major host labels
-        std::vector<int16_t> hs(static_cast<size_t>(N) * L.nslots * gg::kW);
-        HIPCHECK(hipMemcpy(hs.data(), S, hs.size() * sizeof(int16_t), hipMemcpyDeviceToHost));
-        for (int o = 0; o < k; ++o) {
-            const int n = out[o].n;
-            for (int64_t e = 0; e < N; ++e)
-                std::memcpy(out[o].at(e), hs.data() + (e * L.nslots + L.out_slot0 + o) * gg::kW, n * sizeof(int16_t));
+        // sign layer outputs: out0[o] slots (one per output residue) -> label-major device labels
+        gg::GatherArgs ga{};
+        ga.k = static_cast<int>(omods.size());
+        ga.slot0 = L.out_slot0;
+        for (int o = 0; o < ga.k; ++o) {
+            ga.out[o] = out[o].as<int16_t>();
+            ga.n[o] = nr_comps(omods[o]);
         }
+        hipLaunchKernelGGL(gg::k_gather_slots, dim3(blocks_for(N * 128, 256, 4096), ga.k), dim3(256), 0, nullptr, g, ga);
     }
+    HIPCHECK(hipGetLastError());
+    HIPCHECK(hipDeviceSynchronize());
+    tr_.mark("kernels");
     tA.to_array(ap, I.device);
     t1.to_array(c1, I.device);
     t2.to_array(c2, I.device);
     tS.to_array(sg, I.device);
     for (void* p : tmp) (void)hipFree(p);
+    I.cur = std::move(out);
+    I.cur_mod = omods;
+    set_stale(cur, omods, N);
 }
 
 void GpuGarbler::rescale_legacy_iter(uint64_t layer, int it, const RescalePlan& P, CrtLabels& cur,
@@ -730,11 +1100,12 @@ void GpuGarbler::rescale_legacy_iter(uint64_t layer, int it, const RescalePlan& 
                                      const std::vector<std::vector<comp_t>>& down, Array& tr, Array& ap, Array& c1,
                                      Array& c2, Array& sg) {
     Impl& I = *impl_;
-    const int64_t N = cur[0].N;
+    HIPCHECK(hipSetDevice(I.device));
+    I.check_cur(cur);
+    PhaseTrace tr_("rescale_iter");
+    const int64_t N = I.cur_N;
     const int k = I.k;
     std::vector<void*> tmp;
-    DevLabels dL;
-    upload_labels(cur, dL);
     std::vector<int16_t> hup(k * gg::kW, 0), hdn(k * gg::kW, 0);
     for (int j = 0; j < k; ++j) {
         std::copy(up[j].begin(), up[j].end(), hup.begin() + j * gg::kW);
@@ -744,7 +1115,7 @@ void GpuGarbler::rescale_legacy_iter(uint64_t layer, int it, const RescalePlan& 
     ra.k = k;
     for (int j = 0; j < k; ++j) {
         ra.crt[j] = I.crt[j];
-        ra.L[j] = dL.p[j];
+        ra.L[j] = I.cur[j].as<int16_t>();
         ra.inv[j] = 0;
     }
     // inverses of 2 for the active residues (plan order = residues 1..k-1)
@@ -754,27 +1125,34 @@ void GpuGarbler::rescale_legacy_iter(uint64_t layer, int it, const RescalePlan& 
     ra.layer = layer;
     ra.sslot = 10 + it;
     DevTable tT, tA, t1, t2, tS;
-    tT.alloc(N, tr.shape[1]);
-    tA.alloc(N, ap.shape[1]);
-    t1.alloc(N, c1.shape[1]);
-    t2.alloc(N, c2.shape[1]);
-    tS.alloc(N, sg.shape[1]);
+    tT.alloc(I.device, N, tr.shape[1]);
+    tA.alloc(I.device, N, ap.shape[1]);
+    t1.alloc(I.device, N, c1.shape[1]);
+    t2.alloc(I.device, N, c2.shape[1]);
+    tS.alloc(I.device, N, sg.shape[1]);
     gg::Tables tb{};
-    tb.t[0] = tA.p; tb.row[0] = tA.row;
-    tb.t[1] = t1.p; tb.row[1] = t1.row;
-    tb.t[2] = t2.p; tb.row[2] = t2.row;
-    tb.t[3] = tS.p; tb.row[3] = tS.row;
-    tb.t[6] = tT.p; tb.row[6] = tT.row;
-    hipLaunchKernelGGL(gg::k_rescale_pre, dim3(blocks_for(N, 256, 4096)), dim3(256), 0, nullptr, I.c, ra, tb, N);
+    tb.t[0] = tA.p(); tb.row[0] = tA.row;
+    tb.t[1] = t1.p(); tb.row[1] = t1.row;
+    tb.t[2] = t2.p(); tb.row[2] = t2.row;
+    tb.t[3] = tS.p(); tb.row[3] = tS.row;
+    tb.t[6] = tT.p(); tb.row[6] = tT.row;
+    tr_.mark("alloc");
+    for (int j = 1, ctr = 0; j < k; ++j) {
+        ra.ctr[j] = ctr;
+        ctr += (nr_comps(I.crt[j]) + 1) / 2;
+    }
+    hipLaunchKernelGGL(gg::k_rescale_pre, dim3(blocks_for(N * (k - 1), gg::kGB, 8192)), dim3(gg::kGB), 0, nullptr, I.c,
+                       ra, tb, N);
     gg::SignLayout L = gg::sign_layout(P.sign, 0);
-    int16_t* S = nullptr;
-    HIPCHECK(hipMalloc(reinterpret_cast<void**>(&S), static_cast<size_t>(N) * L.nslots * gg::kW * sizeof(int16_t)));
-    tmp.push_back(S);
+    int16_t* S = I.scratch(static_cast<size_t>(N) * L.nslots * gg::kW * sizeof(int16_t));
     gg::In in{};
     for (int j = 0; j < k; ++j) {
-        in.p[j] = dL.p[j];
+        in.p[j] = I.cur[j].as<int16_t>();
         in.n[j] = nr_comps(I.crt[j]);
     }
+    DASH_CHECK(I.crt[0] == 2, "gpu garbler: legacy rescale needs residue 0 = 2");
+    in.p[0] = I.c.Z + 2 * gg::kW;  // residue 0 is Z_2 for every element (zero stride)
+    in.n[0] = 0;
     gg::Gadget g{};
     g.layer = layer;
     g.sslot = 10 + it;
@@ -783,16 +1161,18 @@ void GpuGarbler::rescale_legacy_iter(uint64_t layer, int it, const RescalePlan& 
     g.N = N;
     g.nslots = L.nslots;
     run_sign(I.c, L, g, in, tb, tmp);
-    hipLaunchKernelGGL(gg::k_rescale_post_g, dim3(blocks_for(N, 256)), dim3(256), 0, nullptr, I.c, ra, g, L.out_slot0);
+    hipLaunchKernelGGL(gg::k_rescale_post_g, dim3(blocks_for(N * 128, 256, 4096), k), dim3(256), 0, nullptr, I.c, ra,
+                       g, L.out_slot0);
     HIPCHECK(hipGetLastError());
     HIPCHECK(hipDeviceSynchronize());
-    download_labels(dL, cur);
+    tr_.mark("kernels");
     tT.to_array(tr, I.device);
     tA.to_array(ap, I.device);
     t1.to_array(c1, I.device);
     t2.to_array(c2, I.device);
     tS.to_array(sg, I.device);
     for (void* p : tmp) (void)hipFree(p);
+    set_stale(cur, I.cur_mod, N);
 }
 
 }  // namespace dash

@@ -1,5 +1,12 @@
-// GPU garbler for the sign-gadget layers (see garble_gpu.hip). Plain C++
-// interface so the host garbler (garbler.cpp) can dispatch to it.
+// GPU garbler (see garble_gpu.hip). Plain C++ interface so the host garbler
+// (garbler.cpp) can dispatch to it.
+//
+// The garbler's current base labels live on the device between GPU layers
+// ("device cur"): the host garbler calls to_device() before a GPU layer when
+// its host copy is newer and to_host() before a host layer when the device
+// copy is newer, so a run of GPU layers (conv -> rescale -> ReLU -> conv ...)
+// never moves labels over PCIe. GPU layers leave the host `cur` stale: they
+// only set its shape (p, n, N) and clear its storage.
 #pragma once
 
 #include <memory>
@@ -7,6 +14,7 @@
 #include <vector>
 
 #include "../gadgets.h"
+#include "../layers.h"
 
 namespace dash {
 
@@ -15,11 +23,15 @@ class GpuGarbler {
     GpuGarbler(const std::vector<int>& crt, const std::vector<int>& mrs, const std::string& seed16, const LabelBank& R,
                const LabelBank& Z, int device);
     ~GpuGarbler();
-    // ReLU (relu_crt/prefix/mmg/mme set) or Sign layer: tables + next base labels
-    void sign_layer(uint64_t layer, const SignPlan& sp, const CrtLabels& cur, Array& ap, Array& c1, Array& c2,
-                    Array& sg, CrtLabels& out, const std::vector<int>* relu_crt, const std::vector<i64>* prefix,
-                    Array* mmg, Array* mme);
-    // one DASH legacy rescale iteration (sign base extension); cur updated in place
+    void to_device(const CrtLabels& cur);
+    void to_host(CrtLabels& cur);
+    // conv base labels: y = sum_{w != 0 mod p} w*x + (1 + #zero weights)*Z_p (padding reads Z_p);
+    // w are the weights reduced mod M ([F][C][kh][kw])
+    void conv(const ConvGeom& G, const std::vector<i64>& w, CrtLabels& cur);
+    // ReLU (relu_crt/prefix/mmg/mme set) or Sign layer: tables; device cur -> next base labels
+    void sign_layer(uint64_t layer, const SignPlan& sp, CrtLabels& cur, Array& ap, Array& c1, Array& c2, Array& sg,
+                    const std::vector<int>* relu_crt, const std::vector<i64>* prefix, Array* mmg, Array* mme);
+    // one DASH legacy rescale iteration (sign base extension) on the device cur, in place
     void rescale_legacy_iter(uint64_t layer, int it, const RescalePlan& P, CrtLabels& cur,
                              const std::vector<std::vector<comp_t>>& up, const std::vector<std::vector<comp_t>>& down,
                              Array& tr, Array& ap, Array& c1, Array& c2, Array& sg);
@@ -28,5 +40,12 @@ class GpuGarbler {
     struct Impl;
     std::unique_ptr<Impl> impl_;
 };
+
+// Device blocks of garbled tables freed by their owners return to a small
+// per-process cache (exact-size reuse: every GC of one model has the same
+// table sizes), so back-to-back garbling skips the driver's allocate-and-clear
+// of fresh HBM. Bounded by DASH_GG_CACHE_GB (default 16); trim releases it.
+void gpu_table_cache_trim();
+size_t gpu_table_cache_bytes();
 
 }  // namespace dash

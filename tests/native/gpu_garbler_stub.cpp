@@ -8,16 +8,27 @@ namespace dash {
 
 struct GpuGarbler::Impl {};
 
+[[noreturn]] static void no_gpu() { throw std::runtime_error("GPU garbler not linked into the host-only build"); }
+
 GpuGarbler::GpuGarbler(const std::vector<int>&, const std::vector<int>&, const std::string&, const LabelBank&,
                        const LabelBank&, int) {
-    throw std::runtime_error("GPU garbler not linked into the host-only build");
+    no_gpu();
 }
 GpuGarbler::~GpuGarbler() = default;
-void GpuGarbler::sign_layer(uint64_t, const SignPlan&, const CrtLabels&, Array&, Array&, Array&, Array&, CrtLabels&,
-                            const std::vector<int>*, const std::vector<i64>*, Array*, Array*) {}
+void GpuGarbler::to_device(const CrtLabels&) { no_gpu(); }
+void GpuGarbler::to_host(CrtLabels&) { no_gpu(); }
+void GpuGarbler::conv(const ConvGeom&, const std::vector<i64>&, CrtLabels&) { no_gpu(); }
+void GpuGarbler::sign_layer(uint64_t, const SignPlan&, CrtLabels&, Array&, Array&, Array&, Array&,
+                            const std::vector<int>*, const std::vector<i64>*, Array*, Array*) {
+    no_gpu();
+}
 void GpuGarbler::rescale_legacy_iter(uint64_t, int, const RescalePlan&, CrtLabels&,
                                      const std::vector<std::vector<comp_t>>&,
                                      const std::vector<std::vector<comp_t>>&, Array&, Array&, Array&, Array&,
-                                     Array&) {}
+                                     Array&) {
+    no_gpu();
+}
+void gpu_table_cache_trim() {}
+size_t gpu_table_cache_bytes() { return 0; }
 
 }  // namespace dash
