@@ -10,6 +10,7 @@
 
 #include <chrono>
 #include <functional>
+#include <thread>
 
 #include "../layers.h"
 #include "host_util.h"
@@ -1126,6 +1127,22 @@ void register_hip_bindings(py::module_& m) {
     }, py::arg("priority") = 0);
     m.def("hip_stream_destroy", [](uintptr_t st) { HIPCHECK(hipStreamDestroy(reinterpret_cast<hipStream_t>(st))); });
     m.def("hip_stream_sync", [](uintptr_t st) { HIPCHECK(hipStreamSynchronize(reinterpret_cast<hipStream_t>(st))); });
+    // Watchdog primitive: wait for a stream with a deadline instead of an
+    // unbounded hipStreamSynchronize (which a hung kernel never returns from).
+    // Polls hipStreamQuery with the GIL released; true = drained, false = the
+    // deadline passed with work still queued. Errors raised by the stream throw.
+    m.def("hip_stream_wait", [](uintptr_t st, double timeout_s) {
+        py::gil_scoped_release rel;
+        const auto t0 = std::chrono::steady_clock::now();
+        for (int spin = 0;; ++spin) {
+            const hipError_t e = hipStreamQuery(reinterpret_cast<hipStream_t>(st));
+            if (e == hipSuccess) return true;
+            if (e != hipErrorNotReady) HIPCHECK(e);
+            const double dt = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+            if (timeout_s >= 0 && dt > timeout_s) return false;
+            if (spin > 64) std::this_thread::sleep_for(std::chrono::microseconds(spin > 4096 ? 1000 : 50));
+        }
+    }, py::arg("stream"), py::arg("timeout_s"));
     m.def("hip_device_count", []() {
         int n = 0;
         if (hipGetDeviceCount(&n) != hipSuccess) return 0;

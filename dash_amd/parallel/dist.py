@@ -39,9 +39,16 @@ class DistContext:
         return self.rank == 0
 
 
-def init_distributed(backend: Optional[str] = None, use_gpu: Optional[bool] = None) -> DistContext:
+def init_distributed(backend: Optional[str] = None, use_gpu: Optional[bool] = None,
+                     timeout_s: Optional[float] = None) -> DistContext:
     """Initialise torch.distributed from the torchrun environment (RANK,
-    WORLD_SIZE, LOCAL_RANK, MASTER_ADDR/PORT). Single process -> no-op."""
+    WORLD_SIZE, LOCAL_RANK, MASTER_ADDR/PORT). Single process -> no-op.
+
+    Failure detection (the reference has none): collectives time
+    out after ``timeout_s`` (default ``DASH_DIST_TIMEOUT_S`` or 600 s) instead
+    of hanging forever, and RCCL async error handling tears the process group
+    down on a timed-out or failed collective so the rank exits and the
+    launcher (torchrun elastic) can restart it."""
     import torch
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -60,8 +67,13 @@ def init_distributed(backend: Optional[str] = None, use_gpu: Optional[bool] = No
     if backend is None:
         backend = "nccl" if use_gpu else "gloo"
     if not dist.is_initialized():
+        import datetime
+
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group(backend)
+        os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
+        if timeout_s is None:
+            timeout_s = float(os.environ.get("DASH_DIST_TIMEOUT_S", "600"))
+        dist.init_process_group(backend, timeout=datetime.timedelta(seconds=timeout_s))
     return DistContext(dist.get_rank(), dist.get_world_size(), local, backend, dev)
 
 

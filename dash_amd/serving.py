@@ -1,0 +1,369 @@
+"""Production serving engine: pipelined offline/online phases, watchdogs and
+discard-and-re-garble recovery.
+
+The reference has no serving loop, no health checks and no recovery
+(SURVEY §5.3): its only failure detector is the decoding integrity check
+(`garbled_circuit_interface.h:431-453`, which prints and asserts), and every
+benchmark garbles one GC, evaluates it and throws it away
+(`benchmarks/model_benchmarks/non_sgx/main.cpp:27-92`). This module turns the
+same primitives into a long-running service on one MI355X:
+
+* **GC slot pool.** A GC is single use (re-evaluating it with another input
+  leaks the global offsets R_p), so the service keeps ``groups`` HIP evaluators
+  of ``slots_per_group`` slots each; a slot holds one fresh garbled model whose
+  tables live in HBM. After a group has served one batch its slots are stale.
+* **Offline/online pipeline.** A background garbler thread re-garbles stale
+  groups (on the GPU garbler or the host garbler) and streams them into their
+  HBM slots while the online path evaluates the other groups, so in steady
+  state the online latency never waits for garbling unless the pool drains.
+* **Watchdog.** Every online evaluation waits on its stream with a deadline
+  (native ``hip_stream_wait``: hipStreamQuery polling with the GIL released)
+  instead of an unbounded synchronize; a hung step raises ``WatchdogTimeout``
+  and marks the service unhealthy (a hung GPU cannot be recovered in-process:
+  the supervisor — torchrun elastic or the operator — restarts the rank).
+  ``Watchdog`` additionally guards arbitrary host sections (e.g. collectives).
+* **Recovery.** A decode integrity failure (``IntegrityError``: a corrupted
+  table, label or message) discards the GC and resubmits the input on a fresh
+  GC, up to ``max_retries`` times; failures and retries are counted.
+* **Metrics.** Latency percentiles, throughput, retries, integrity failures and
+  timeouts as one JSON-serialisable dict (``stats()``).
+
+Backends: ``"hip"`` (MI355X, batched HIP evaluator) and ``"cpu"`` (the native
+host evaluator, used by the CPU tests).
+"""
+from __future__ import annotations
+
+import hashlib
+import os
+import queue
+import threading
+import time
+from contextlib import contextmanager
+from dataclasses import dataclass, field
+from typing import Callable, List, Optional, Sequence
+
+import numpy as np
+
+from .native import native
+
+
+class WatchdogTimeout(RuntimeError):
+    """A guarded section (GPU step, collective) exceeded its deadline."""
+
+
+class Watchdog:
+    """Deadline monitor for host-side sections.
+
+    ``with wd.guard("allgather", 30): ...`` registers a deadline; a monitor
+    thread calls ``on_timeout(name, elapsed_s)`` once if the section is still
+    running after its deadline. The default handler records the event; pass
+    ``abort_exit_code`` to terminate the process instead (the only way out of a
+    call blocked inside the driver; ``os._exit`` does not exec, so it is safe
+    after GPU initialisation)."""
+
+    def __init__(self, on_timeout: Optional[Callable[[str, float], None]] = None, poll_s: float = 0.05,
+                 abort_exit_code: Optional[int] = None):
+        self.events: List[tuple] = []
+        self._on_timeout = on_timeout
+        self._abort = abort_exit_code
+        self._poll = poll_s
+        self._lock = threading.Lock()
+        self._active: dict = {}
+        self._next = 0
+        self._stop = threading.Event()
+        self._thread = threading.Thread(target=self._run, name="dash-watchdog", daemon=True)
+        self._thread.start()
+
+    def _run(self) -> None:
+        while not self._stop.wait(self._poll):
+            now = time.monotonic()
+            fired = []
+            with self._lock:
+                for key, (name, t0, deadline) in list(self._active.items()):
+                    if now > deadline:
+                        fired.append((name, now - t0))
+                        del self._active[key]
+            for name, dt in fired:
+                self.events.append((name, dt))
+                if self._on_timeout is not None:
+                    self._on_timeout(name, dt)
+                if self._abort is not None:
+                    os._exit(self._abort)
+
+    @contextmanager
+    def guard(self, name: str, timeout_s: float):
+        with self._lock:
+            key = self._next
+            self._next += 1
+            t0 = time.monotonic()
+            self._active[key] = (name, t0, t0 + timeout_s)
+        try:
+            yield
+        finally:
+            with self._lock:
+                fired = key not in self._active
+                self._active.pop(key, None)
+        if fired:
+            raise WatchdogTimeout(f"{name} exceeded its {timeout_s:.3g} s deadline")
+
+    def close(self) -> None:
+        self._stop.set()
+        self._thread.join(timeout=1.0)
+
+
+def wait_stream(stream, timeout_s: float, what: str = "GPU step") -> None:
+    """Bounded wait for a HIP stream (handle, torch stream or None = current)."""
+    from .runtime import _stream_handle
+
+    if not native().hip_stream_wait(_stream_handle(stream), float(timeout_s)):
+        raise WatchdogTimeout(f"{what} still running after {timeout_s:.3g} s (GPU hang?)")
+
+
+@dataclass
+class ServiceStats:
+    inferences: int = 0
+    batches: int = 0
+    retries: int = 0
+    integrity_failures: int = 0
+    timeouts: int = 0
+    gcs_garbled: int = 0
+    garble_s: float = 0.0
+    pool_waits_s: float = 0.0
+    latencies_ms: List[float] = field(default_factory=list)
+    t_start: float = field(default_factory=time.perf_counter)
+
+    def as_dict(self) -> dict:
+        lat = np.asarray(self.latencies_ms, dtype=np.float64)
+        wall = time.perf_counter() - self.t_start
+
+        def pct(q):
+            return round(float(np.percentile(lat, q)), 3) if lat.size else None
+
+        return {
+            "inferences": self.inferences, "batches": self.batches, "retries": self.retries,
+            "integrity_failures": self.integrity_failures, "timeouts": self.timeouts,
+            "gcs_garbled": self.gcs_garbled, "garble_s_per_gc": round(self.garble_s / max(1, self.gcs_garbled), 4),
+            "pool_wait_s": round(self.pool_waits_s, 3),
+            "batch_latency_ms": {"p50": pct(50), "p90": pct(90), "p99": pct(99), "max": pct(100)},
+            "inferences_per_s_wall": round(self.inferences / wall, 3) if wall > 0 else None,
+        }
+
+
+class _Group:
+    """One evaluator (``slots`` GC slots) plus the garbler-side state of its GCs."""
+
+    def __init__(self, idx: int, slots: int):
+        self.idx = idx
+        self.slots = slots
+        self.ev = None          # HipEvaluator (hip backend)
+        self.gcs: list = [None] * slots
+        self.ready = threading.Event()
+        self.stream = None
+
+
+class InferenceService:
+    """Long-running garbled-inference service on one GPU (or the host).
+
+    ``infer(xs)`` takes any number of quantized inputs and returns their
+    decoded logits ``[len(xs), n_out]`` in order; each input is evaluated on a
+    fresh GC. ``fault_hook(global_index, attempt) -> bool`` (tests / chaos
+    runs) corrupts that attempt's output message before decoding, which the
+    integrity check must catch and the service must recover from."""
+
+    def __init__(self, circuit, crt, mrs=None, *, max_modulus: int = 0, slots_per_group: int = 4, groups: int = 2,
+                 backend: str = "hip", device: int = 0, garble_device: Optional[bool] = None, max_retries: int = 2,
+                 step_timeout_s: float = 120.0, seed: Optional[bytes] = None, prefetch: bool = True,
+                 fault_hook: Optional[Callable[[int, int], bool]] = None, nthreads: int = 0):
+        if backend not in ("hip", "cpu"):
+            raise ValueError("backend must be 'hip' or 'cpu'")
+        if backend == "hip" and native().hip_device_count() == 0:
+            raise RuntimeError("InferenceService(backend='hip') needs a visible MI355X")
+        self.circuit, self.crt, self.mrs, self.max_modulus = circuit, crt, mrs, max_modulus
+        self.backend, self.device = backend, device
+        self.garble_device = (backend == "hip") if garble_device is None else bool(garble_device)
+        self.max_retries, self.step_timeout_s = max_retries, step_timeout_s
+        self.fault_hook = fault_hook
+        self.nthreads = nthreads
+        self._seed = seed if seed is not None else os.urandom(16)
+        self._ctr = 0
+        self.stats = ServiceStats()
+        self.healthy = True
+        self.groups = [_Group(g, slots_per_group) for g in range(groups)]
+        self._next_group = 0
+        self._err: Optional[BaseException] = None
+        self._q: "queue.Queue[Optional[_Group]]" = queue.Queue()
+        if backend == "hip":
+            import torch
+
+            torch.cuda.set_device(device)
+            self._streams = [native().hip_stream_create(0) for _ in range(groups)]
+            for g, st in zip(self.groups, self._streams):
+                g.stream = st
+        # fill the pool once synchronously (first GC also sizes the evaluators), then refill in the background
+        for g in self.groups:
+            self._refill(g)
+        self._worker = None
+        if prefetch:
+            self._worker = threading.Thread(target=self._garbler_loop, name="dash-garbler", daemon=True)
+            self._worker.start()
+
+    # ------------------------------------------------------------ offline
+    def _new_gc(self):
+        from .garbling import GarbledCircuit
+
+        seed = hashlib.sha256(self._seed + self._ctr.to_bytes(8, "little")).digest()[:16]
+        self._ctr += 1
+        t = time.perf_counter()
+        gc = GarbledCircuit(self.circuit, self.crt, self.mrs, max_modulus=self.max_modulus, seed=seed,
+                            nthreads=self.nthreads, device=self.device if self.garble_device else None)
+        self.stats.garble_s += time.perf_counter() - t
+        self.stats.gcs_garbled += 1
+        return gc
+
+    def _refill(self, g: _Group) -> None:
+        for b in range(g.slots):
+            gc = self._new_gc()
+            if self.backend == "hip":
+                from .runtime import HipEvaluator
+
+                if g.ev is None:
+                    g.ev = HipEvaluator(template=gc.model, batch=g.slots, device=self.device)
+                g.ev.load(b, gc.model)
+                gc.model = None  # tables live in HBM now
+            g.gcs[b] = gc
+        if self.backend == "hip" and self.garble_device:
+            native().gpu_table_cache_trim()
+        g.ready.set()
+
+    def _garbler_loop(self) -> None:
+        while True:
+            g = self._q.get()
+            if g is None:
+                return
+            try:
+                self._refill(g)
+            except BaseException as e:  # surfaced by the next infer()
+                self._err = e
+                g.ready.set()
+                return
+
+    def _take_group(self) -> _Group:
+        g = self.groups[self._next_group]
+        self._next_group = (self._next_group + 1) % len(self.groups)
+        if not g.ready.is_set():
+            if self._worker is None:
+                self._refill(g)
+            else:
+                t = time.perf_counter()
+                g.ready.wait()
+                self.stats.pool_waits_s += time.perf_counter() - t
+        if self._err is not None:
+            raise RuntimeError("background garbler failed") from self._err
+        return g
+
+    def _release(self, g: _Group) -> None:
+        g.gcs = [None] * g.slots
+        g.ready.clear()
+        if self._worker is not None:
+            self._q.put(g)
+
+    # ------------------------------------------------------------- online
+    def _run_group(self, g: _Group, xs: Sequence[np.ndarray], idx: Sequence[int], attempt: int):
+        """Evaluate len(xs) <= slots inputs on group g. Returns per-input logits or None on integrity failure."""
+        from . import IntegrityError
+
+        out: list = [None] * len(xs)
+        t = time.perf_counter()
+        if self.backend == "hip":
+            ev = g.ev
+            for b in range(g.slots):  # unused slots evaluate a dummy input (their GCs are discarded anyway)
+                ev.encode_compressed_into(b, g.gcs[b], xs[b] if b < len(xs) else xs[0])
+            ev.upload_inputs_compressed(g.stream)
+            ev.run(g.stream)
+            try:
+                wait_stream(g.stream, self.step_timeout_s, f"group {g.idx} evaluation")
+            except WatchdogTimeout:
+                self.stats.timeouts += 1
+                self.healthy = False
+                raise
+            ev.fetch_outputs(g.stream)
+            for b in range(len(xs)):
+                msg = np.array(ev.outputs_compressed(b), copy=True)
+                if self.fault_hook is not None and self.fault_hook(idx[b], attempt):
+                    msg[0, 0, 0] ^= np.uint64(1) << np.uint64(9)
+                try:
+                    out[b] = np.asarray(g.gcs[b].decode_compressed(msg))
+                except IntegrityError:
+                    self.stats.integrity_failures += 1
+        else:
+            for b, x in enumerate(xs):
+                gc = g.gcs[b]
+                labels = gc.cpu_evaluate(gc.garble_inputs(x), self.nthreads)
+                if self.fault_hook is not None and self.fault_hook(idx[b], attempt):
+                    p, arr = labels[0]
+                    arr = np.array(arr, copy=True)
+                    arr.flat[0] = (int(arr.flat[0]) + 1) % int(p)
+                    labels = [(p, arr)] + list(labels[1:])
+                try:
+                    out[b] = np.asarray(gc.decode_outputs(labels))
+                except IntegrityError:
+                    self.stats.integrity_failures += 1
+        self.stats.latencies_ms.append(1000.0 * (time.perf_counter() - t))
+        self.stats.batches += 1
+        return out
+
+    def infer(self, xs: Sequence[np.ndarray]) -> np.ndarray:
+        if not self.healthy:
+            raise RuntimeError("service is unhealthy (a GPU step timed out); restart the rank")
+        xs = [np.asarray(x, dtype=np.int64).reshape(-1) for x in xs]
+        results: list = [None] * len(xs)
+        pending = list(range(len(xs)))
+        attempt = 0
+        while pending:
+            if attempt > self.max_retries:
+                from . import IntegrityError
+
+                raise IntegrityError(f"inputs {pending} failed the integrity check {attempt} times")
+            failed = []
+            for s in range(0, len(pending), self.groups[0].slots):
+                chunk = pending[s:s + self.groups[0].slots]
+                g = self._take_group()
+                try:
+                    out = self._run_group(g, [xs[i] for i in chunk], chunk, attempt)
+                finally:
+                    self._release(g)  # single use: every GC of the group is discarded, then re-garbled
+                for i, y in zip(chunk, out):
+                    if y is None:
+                        failed.append(i)
+                    else:
+                        results[i] = y
+                        self.stats.inferences += 1
+            if failed:
+                self.stats.retries += len(failed)
+            pending = failed
+            attempt += 1
+        return np.stack(results)
+
+    def close(self) -> None:
+        if self._worker is not None:
+            while True:  # drop pending refills: the pool is going away
+                try:
+                    self._q.get_nowait()
+                except queue.Empty:
+                    break
+            self._q.put(None)
+            self._worker.join()
+            self._worker = None
+        for g in self.groups:
+            g.ev = None
+            g.gcs = [None] * g.slots
+        if self.backend == "hip":
+            for st in self._streams:
+                native().hip_stream_destroy(st)
+            self._streams = []
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
