@@ -159,6 +159,7 @@ class _Group:
         self.gcs: list = [None] * slots
         self.ready = threading.Event()
         self.stream = None
+        self.runs = 0           # evaluations so far (run 2 captures the hipGraph)
 
 
 class InferenceService:
@@ -191,6 +192,9 @@ class InferenceService:
         self.groups = [_Group(g, slots_per_group) for g in range(groups)]
         self._next_group = 0
         self._err: Optional[BaseException] = None
+        # hipGraph capture (a group's 2nd run) must not overlap the garbler thread's device-wide syncs and
+        # allocations, which would invalidate the capture; replays and eager runs need no lock
+        self._capture_lock = threading.Lock()
         self._q: "queue.Queue[Optional[_Group]]" = queue.Queue()
         if backend == "hip":
             import torch
@@ -222,18 +226,19 @@ class InferenceService:
 
     def _refill(self, g: _Group) -> None:
         for b in range(g.slots):
-            gc = self._new_gc()
             if self.backend == "hip":
                 from .runtime import HipEvaluator
 
-                if g.ev is None:
-                    g.ev = HipEvaluator(template=gc.model, batch=g.slots, device=self.device)
-                g.ev.load(b, gc.model)
+                with self._capture_lock:  # GPU garbling + upload: device-wide syncs and allocations
+                    gc = self._new_gc()
+                    if g.ev is None:
+                        g.ev = HipEvaluator(template=gc.model, batch=g.slots, device=self.device)
+                    g.ev.load(b, gc.model)
                 gc.model = None  # tables live in HBM now
+            else:
+                gc = self._new_gc()
             g.gcs[b] = gc
-        if self.backend == "hip" and self.garble_device:
-            native().gpu_table_cache_trim()
-        g.ready.set()
+        g.ready.set()  # the GPU garbler's recycled table blocks stay cached for the next refill
 
     def _garbler_loop(self) -> None:
         while True:
@@ -279,7 +284,12 @@ class InferenceService:
             for b in range(g.slots):  # unused slots evaluate a dummy input (their GCs are discarded anyway)
                 ev.encode_compressed_into(b, g.gcs[b], xs[b] if b < len(xs) else xs[0])
             ev.upload_inputs_compressed(g.stream)
-            ev.run(g.stream)
+            if g.runs == 1:
+                with self._capture_lock:
+                    ev.run(g.stream)
+            else:
+                ev.run(g.stream)
+            g.runs += 1
             try:
                 wait_stream(g.stream, self.step_timeout_s, f"group {g.idx} evaluation")
             except WatchdogTimeout:
@@ -358,6 +368,8 @@ class InferenceService:
             g.ev = None
             g.gcs = [None] * g.slots
         if self.backend == "hip":
+            if self.garble_device:
+                native().gpu_table_cache_trim()
             for st in self._streams:
                 native().hip_stream_destroy(st)
             self._streams = []
