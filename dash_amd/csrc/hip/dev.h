@@ -123,20 +123,31 @@ struct DigitStream {
 __device__ __forceinline__ uint32_t reduce_top(uint32_t d, const ModC& m) { return d % m.q; }
 
 // Streaming forward compress: push digits from least significant upwards.
+// Power-of-two moduli pack digits into a 32-bit word first and place whole
+// words into the u128 (one variable 128-bit shift per word, not per digit:
+// a mod-2 label has 128 digits).
 struct CompressFwd {
     u128 C, PW;
-    uint32_t v, pt, cnt;
+    uint32_t v, pt, cnt, bp, sh;
     __device__ __forceinline__ void init() {
         C = 0;
         PW = 1;
         v = 0;
         pt = 1;
         cnt = 0;
+        bp = 0;
+        sh = 0;
     }
     __device__ __forceinline__ void push(uint32_t d, const ModC& m) {
         if (m.bits) {
-            C |= static_cast<u128>(d) << (m.bits * cnt);
-            ++cnt;
+            v |= d << bp;
+            bp += m.bits;
+            if (bp + m.bits > 32) {
+                C |= static_cast<u128>(v) << sh;
+                sh += bp;
+                v = 0;
+                bp = 0;
+            }
             return;
         }
         v += d * pt;
@@ -150,7 +161,8 @@ struct CompressFwd {
         }
     }
     __device__ __forceinline__ u128 finish() {
-        if (cnt && v) C += PW * static_cast<u128>(v);
+        if (bp) C |= static_cast<u128>(v) << sh;  // bits path (bp stays 0 otherwise)
+        else if (cnt && v) C += PW * static_cast<u128>(v);
         return C;
     }
 };

@@ -224,26 +224,54 @@ __global__ __launch_bounds__(256) void k_sign_derive(Ctx c, Gadget g, SignSlots 
 }
 
 // Label rows are contiguous int16 runs (label-major inputs, kW-wide slots).
-// Loading one component per loop iteration would make every component a
-// dependent memory round trip; stage kPC components of both operands first.
-constexpr int kPC = 16;
+// In the element-tiled k_project the 64 lanes of a wave read 64 different
+// rows, so every load instruction costs up to 64 L1 tag lookups: rows are read
+// 8 components (16 B) per load (global_load_dwordx4; gfx950 allows the 2-byte
+// aligned addresses of packed input rows), never past the row end (the tail
+// is read per component), two chunks in flight per step.
+constexpr int kPC = 16;  // components staged per step by the per-component loaders
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+struct __attribute__((packed, aligned(2))) Row8 {
+    u32x4 v;
+};
+__device__ __forceinline__ u32x4 ld_row8(const int16_t* p) {
+    Row8 t;
+    __builtin_memcpy(&t, p, 16);
+    return t.v;
+}
+__device__ __forceinline__ uint32_t lane16(const u32x4& v, int u) {  // component u (0..7), zero-extended
+    const uint32_t w = v[u >> 1];
+    return (u & 1) ? (w >> 16) : (w & 0xffffu);
+}
+
+// digits (a_c + f * b_c) mod m of two label rows a, b (components in [0, m)), pushed into cf
+__device__ __forceinline__ void push_row(CompressFwd& cf, const int16_t* a, const int16_t* b, uint32_t f,
+                                         const ModC& m) {
+    const int n = static_cast<int>(m.n);
+    int q0 = 0;
+    for (; q0 + 16 <= n; q0 += 16) {
+        const u32x4 a0 = ld_row8(a + q0), a1 = ld_row8(a + q0 + 8);
+        const u32x4 b0 = ld_row8(b + q0), b1 = ld_row8(b + q0 + 8);
+#pragma unroll
+        for (int u = 0; u < 8; ++u) cf.push(modq(lane16(a0, u) + f * lane16(b0, u), m), m);
+#pragma unroll
+        for (int u = 0; u < 8; ++u) cf.push(modq(lane16(a1, u) + f * lane16(b1, u), m), m);
+    }
+    if (q0 + 8 <= n) {
+        const u32x4 a0 = ld_row8(a + q0), b0 = ld_row8(b + q0);
+#pragma unroll
+        for (int u = 0; u < 8; ++u) cf.push(modq(lane16(a0, u) + f * lane16(b0, u), m), m);
+        q0 += 8;
+    }
+    for (; q0 < n; ++q0)
+        cf.push(modq(static_cast<uint32_t>(static_cast<uint16_t>(a[q0])) + f * static_cast<uint16_t>(b[q0]), m), m);
+}
 
 // key = x + i*R (mod m), compressed from the least significant digit
 __device__ __forceinline__ u128 proj_key(const int16_t* x, const int16_t* R, int i, const ModC& m, uint32_t& color) {
     CompressFwd kc;
     kc.init();
-    const int n = static_cast<int>(m.n);
-    for (int q0 = 0; q0 < n; q0 += kPC) {
-        int16_t xa[kPC], ra[kPC];
-#pragma unroll
-        for (int u = 0; u < kPC; ++u) {
-            xa[u] = q0 + u < n ? x[q0 + u] : int16_t(0);
-            ra[u] = q0 + u < n ? R[q0 + u] : int16_t(0);
-        }
-#pragma unroll
-        for (int u = 0; u < kPC; ++u)
-            if (q0 + u < n) kc.push(modq(static_cast<uint32_t>(xa[u] + i * ra[u]), m), m);
-    }
+    push_row(kc, x, R, static_cast<uint32_t>(i), m);
     color = modq(static_cast<uint32_t>(x[0] + i * R[0]), m);
     return kc.finish();
 }
@@ -252,43 +280,93 @@ __device__ __forceinline__ u128 proj_key(const int16_t* x, const int16_t* R, int
 __device__ __forceinline__ u128 proj_payload(const int16_t* o, const int16_t* R, uint32_t f, const ModC& m) {
     CompressFwd pc;
     pc.init();
-    const int n = static_cast<int>(m.n);
-    for (int q0 = 0; q0 < n; q0 += kPC) {
-        int16_t oa[kPC], ra[kPC];
-#pragma unroll
-        for (int u = 0; u < kPC; ++u) {
-            oa[u] = q0 + u < n ? o[q0 + u] : int16_t(0);
-            ra[u] = q0 + u < n ? R[q0 + u] : int16_t(0);
-        }
-#pragma unroll
-        for (int u = 0; u < kPC; ++u)
-            if (q0 + u < n)
-                pc.push(modq(static_cast<uint32_t>(oa[u]) + f * static_cast<uint32_t>(ra[u]), m), m);
-    }
+    push_row(pc, o, R, f, m);
     return pc.finish();
 }
 
-// one thread per (element, table entry)
-__global__ __launch_bounds__(kGB) void k_project(Ctx c, Gadget g, In in, Tables tb) {
+// one thread per (element, table entry). Element-tiled order: the 64 lanes of
+// a wavefront are 64 elements of one tile, all on the SAME table entry r, so
+// the projection descriptor, i, the label widths (loop trip counts), the
+// moduli and the function are wave-uniform. They are moved to SGPRs
+// explicitly (readfirstlane): the digit loops then branch on scalar
+// conditions instead of exec masks, and the compressor's running power of the
+// modulus (PW, pt, digit counters) is scalar work issued beside the vector
+// digits. Consecutive waves walk the entries of the same 64 elements, so their
+// label rows stay cached.
+constexpr int kTile = 64;
+#ifndef DASH_GG_PB
+#define DASH_GG_PB 512
+#endif
+constexpr int kPB = DASH_GG_PB;  // threads per k_project block (A/B knob)
+
+__device__ __forceinline__ int rfl(int x) { return __builtin_amdgcn_readfirstlane(x); }
+__device__ __forceinline__ uint32_t rflu(uint32_t x) {
+    return static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(x)));
+}
+__device__ __forceinline__ int64_t rfl64(int64_t x) {
+    const uint64_t u = static_cast<uint64_t>(x);
+    const uint64_t lo = rflu(static_cast<uint32_t>(u)), hi = rflu(static_cast<uint32_t>(u >> 32));
+    return static_cast<int64_t>(lo | (hi << 32));
+}
+__device__ __forceinline__ ModC rfl_modc(const ModC& m) {
+    ModC r;
+    r.q = rflu(m.q);
+    r.n = rflu(m.n);
+    r.c = rflu(m.c);
+    r.D = rflu(m.D);
+    r.mD = static_cast<uint64_t>(rfl64(static_cast<int64_t>(m.mD)));
+    r.mq = rflu(m.mq);
+    r.bits = rflu(m.bits);
+    return r;
+}
+__device__ __forceinline__ Proj rfl_proj(const Proj& p) {
+    Proj r;
+    r.in_kind = rfl(p.in_kind);
+    r.in_idx = rfl(p.in_idx);
+    r.pin = rfl(p.pin);
+    r.out_slot = rfl(p.out_slot);
+    r.pout = rfl(p.pout);
+    r.fn = rfl(p.fn);
+    r.a0 = rfl(p.a0);
+    r.a1 = rfl(p.a1);
+    r.a2 = rfl(p.a2);
+    r.outr_kind = rfl(p.outr_kind);
+    r.outr_idx = rfl(p.outr_idx);
+    r.table = rfl(p.table);
+    r.stride = rfl(p.stride);
+    r.off = rfl64(p.off);
+    r.first = rfl64(p.first);
+    return r;
+}
+
+__global__ __launch_bounds__(kPB) void k_project(Ctx c, Gadget g, In in, Tables tb) {
     __shared__ uint32_t lds_aes[DASH_AES_LDS_WORDS];
     __shared__ Proj sp[kMaxDesc];
     lds_stage(sp, g.projs, g.nprojs);
     aes_lds_fill(lds_aes, c.te0);
     const AesCtx aes = aes_ctx(lds_aes, nullptr);
-    const int64_t total = g.N * g.entries;
-    for (int64_t gi = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; gi < total;
-         gi += static_cast<int64_t>(gridDim.x) * blockDim.x) {
-        const int64_t e = gi / g.entries;
-        const int64_t r = gi - e * g.entries;
+    const int64_t N = g.N;
+    const int64_t tiles = (N + kTile - 1) / kTile;
+    const int64_t nw = tiles * g.entries;  // wave work items (tile, entry)
+    const int lane = static_cast<int>(threadIdx.x) & (kTile - 1);
+    const int64_t wpb = kPB / kTile;
+    const int64_t w0 = static_cast<int64_t>(blockIdx.x) * wpb + rfl(static_cast<int>(threadIdx.x) / kTile);
+    const int64_t wstep = static_cast<int64_t>(gridDim.x) * wpb;
+    for (int64_t w = w0; w < nw; w += wstep) {
+        const int64_t tile = w / g.entries;
+        const int64_t r = w - tile * g.entries;
         int lo = 0, hi = g.nprojs - 1;
-        while (lo < hi) {  // last projection with first <= r
+        while (lo < hi) {  // last projection with first <= r (uniform search)
             const int mid = (lo + hi + 1) >> 1;
-            if (sp[mid].first <= r) lo = mid;
+            if (rfl64(sp[mid].first) <= r) lo = mid;
             else hi = mid - 1;
         }
-        const Proj& P = sp[lo];
+        const Proj P = rfl_proj(sp[lo]);
         const int i = static_cast<int>(r - P.first);
-        const ModC mi = c.mc[P.pin], mo = c.mc[P.pout];
+        const ModC mi = rfl_modc(c.mc[P.pin]), mo = rfl_modc(c.mc[P.pout]);
+        // the last tile's spare lanes recompute element N-1 (uniform control flow) and skip the store
+        const int64_t e_raw = tile * kTile + lane;
+        const int64_t e = e_raw < N ? e_raw : N - 1;
         const int16_t* inl = label_ref(c, g, in, e, P.in_kind, P.in_idx, P.pin);
         uint32_t color;
         const u128 H = aes_encrypt(aes, proj_key(inl, c.R + static_cast<int64_t>(P.pin) * kW, i, mi, color));
@@ -316,7 +394,7 @@ __global__ __launch_bounds__(kGB) void k_project(Ctx c, Gadget g, In in, Tables 
         const int16_t* oR = P.outr_kind == R_BANK ? c.R + static_cast<int64_t>(P.pout) * kW
                                                   : label_ref(c, g, in, e, S_INPUT, P.outr_idx, 0);
         const u128 pay = proj_payload(ol, oR, static_cast<uint32_t>(cm), mo);
-        tb.t[P.table][e * tb.row[P.table] + P.off + static_cast<int64_t>(color) * P.stride] = pay + H;
+        if (e_raw < N) tb.t[P.table][e * tb.row[P.table] + P.off + static_cast<int64_t>(color) * P.stride] = pay + H;
     }
 }
 
@@ -810,7 +888,7 @@ void run_sign(const gg::Ctx& c, const gg::SignLayout& L, gg::Gadget& g, const gg
     check_desc(g);
     hipLaunchKernelGGL(gg::k_draw, dim3(blocks_for(g.N * g.nblk, gg::kGB, 8192)), dim3(gg::kGB), 0, nullptr, c, g);
     hipLaunchKernelGGL(gg::k_sign_derive, dim3(blocks_for(g.N, 256)), dim3(256), 0, nullptr, c, g, L.ss);
-    hipLaunchKernelGGL(gg::k_project, dim3(blocks_for(g.N * g.entries, gg::kGB, 16384)), dim3(gg::kGB), 0, nullptr, c,
+    hipLaunchKernelGGL(gg::k_project, dim3(blocks_for((g.N + 63) / 64 * 64 * g.entries, gg::kPB, 16384)), dim3(gg::kPB), 0, nullptr, c,
                        g, in, tb);
     HIPCHECK(hipGetLastError());
 }
@@ -1059,7 +1137,7 @@ void GpuGarbler::sign_layer(uint64_t layer, const SignPlan& sp, CrtLabels& cur, 
         gm.nblk = draw_blocks(dr);
         check_desc(gm);
         hipLaunchKernelGGL(gg::k_draw, dim3(blocks_for(N * gm.nblk, gg::kGB, 8192)), dim3(gg::kGB), 0, nullptr, I.c, gm);
-        hipLaunchKernelGGL(gg::k_project, dim3(blocks_for(N * gm.entries, gg::kGB, 16384)), dim3(gg::kGB), 0, nullptr,
+        hipLaunchKernelGGL(gg::k_project, dim3(blocks_for((N + 63) / 64 * 64 * gm.entries, gg::kPB, 16384)), dim3(gg::kPB), 0, nullptr,
                            I.c, gm, in, tb);
         gg::MiniArgs ma{};
         ma.k = k;
