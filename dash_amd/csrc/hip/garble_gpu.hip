@@ -194,6 +194,30 @@ struct SignSlots {
     int sum2_slot0, sum_slot, bases_slot0, newc_slot0, mrs_slot0, stride_q;  // stride_q = k + 2
 };
 
+// One thread per element; slot rows are kW-aligned (256 B), so components
+// move 8 at a time (16-B loads/stores; lanes read rows of different elements,
+// and per-component loads were L1 tag-rate bound). Rows are kW wide, so the
+// 8-wide tail past n stays inside the row and is never stored.
+typedef uint32_t u32x4a __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ u32x4a ld8a(const int16_t* p) { return *reinterpret_cast<const u32x4a*>(p); }
+__device__ __forceinline__ void add8(uint32_t (&acc)[8], const u32x4a& v) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        acc[2 * u] += v[u] & 0xffffu;
+        acc[2 * u + 1] += v[u] >> 16;
+    }
+}
+__device__ __forceinline__ void st8a(int16_t* p, const uint32_t (&acc)[8], const ModC& m, int valid) {
+    if (valid >= 8) {
+        u32x4a o;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) o[u] = modq(acc[2 * u], m) | (modq(acc[2 * u + 1], m) << 16);
+        *reinterpret_cast<u32x4a*>(p) = o;
+    } else {
+        for (int u = 0; u < valid; ++u) p[u] = static_cast<int16_t>(modq(acc[u], m));
+    }
+}
+
 __global__ __launch_bounds__(256) void k_sign_derive(Ctx c, Gadget g, SignSlots s) {
     const int64_t e = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
     if (e >= g.N) return;
@@ -206,20 +230,22 @@ __global__ __launch_bounds__(256) void k_sign_derive(Ctx c, Gadget g, SignSlots 
         const int n = static_cast<int>(Mo.n);
         int16_t* dst = S + (s.sum2_slot0 + q) * kW;
         const int16_t* b0 = S + (s.bases_slot0 + q * s.stride_q) * kW;
-        for (int i = 0; i < n; ++i) {
-            int v = 0;
-            for (int j = 0; j <= k; ++j) v += b0[j * kW + i];
-            dst[i] = static_cast<int16_t>(modq(static_cast<uint32_t>(v), Mo));
+        for (int i0 = 0; i0 < n; i0 += 8) {
+            uint32_t acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+            for (int j = 0; j <= k; ++j) add8(acc, ld8a(b0 + j * kW + i0));
+            st8a(dst + i0, acc, Mo, n - i0);
         }
     }
     const int m0 = s.mrs[0];
-    const int n0 = static_cast<int>(c.mc[m0].n);
+    const ModC M0 = c.mc[m0];
+    const int n0 = static_cast<int>(M0.n);
     const int16_t* carry = t >= 2 ? S + (s.newc_slot0 + (t - 2) * s.stride_q) * kW : c.Z + static_cast<int64_t>(m0) * kW;
     int16_t* sum = S + s.sum_slot * kW;
-    for (int i = 0; i < n0; ++i) {
-        int v = carry[i];
-        for (int j = 0; j < k; ++j) v += S[(s.mrs_slot0 + j * t) * kW + i];
-        sum[i] = static_cast<int16_t>(modq(static_cast<uint32_t>(v), c.mc[m0]));
+    for (int i0 = 0; i0 < n0; i0 += 8) {
+        uint32_t acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        add8(acc, ld8a(carry + i0));
+        for (int j = 0; j < k; ++j) add8(acc, ld8a(S + (s.mrs_slot0 + j * t) * kW + i0));
+        st8a(sum + i0, acc, M0, n0 - i0);
     }
 }
 
@@ -485,19 +511,17 @@ __global__ __launch_bounds__(kGB) void k_rescale_pre(Ctx c, RsArgs a, Tables tb,
         CompressFwd k0, k1;
         k0.init();
         k1.init();
-        for (int q0 = 0; q0 < static_cast<int>(m2.n); q0 += kPC) {
-            int16_t la[kPC], ua[kPC], ra[kPC];
+        // mod-2 rows are 128 components = 256 B (aligned): 16-B loads, the XORs done 8 lanes at a time
+        for (int q0 = 0; q0 < static_cast<int>(m2.n); q0 += 8) {
+            const u32x4a la = ld8a(L0 + q0), ua = ld8a(a.up + q0), ra = ld8a(R2 + q0);
 #pragma unroll
-            for (int u = 0; u < kPC; ++u) {
-                la[u] = L0[q0 + u];  // m2.n = 128 is a multiple of kPC
-                ua[u] = a.up[q0 + u];
-                ra[u] = R2[q0 + u];
-            }
-#pragma unroll
-            for (int u = 0; u < kPC; ++u) {
-                const uint32_t v = static_cast<uint32_t>(la[u] + ua[u]) & 1u;
-                k0.push(v, m2);
-                k1.push((v + static_cast<uint32_t>(ra[u])) & 1u, m2);
+            for (int u = 0; u < 4; ++u) {
+                const uint32_t v = (la[u] + ua[u]) & 0x00010001u;  // per 16-bit half: (l + u) & 1
+                const uint32_t w = (v + ra[u]) & 0x00010001u;
+                k0.push(v & 1u, m2);
+                k0.push(v >> 16, m2);
+                k1.push(w & 1u, m2);
+                k1.push(w >> 16, m2);
             }
         }
         const uint32_t color0 = static_cast<uint32_t>(L0[0] + a.up[0]) & 1u;
