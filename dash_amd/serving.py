@@ -11,7 +11,9 @@ same primitives into a long-running service on one MI355X:
 * **GC slot pool.** A GC is single use (re-evaluating it with another input
   leaks the global offsets R_p), so the service keeps ``groups`` HIP evaluators
   of ``slots_per_group`` slots each; a slot holds one fresh garbled model whose
-  tables live in HBM. After a group has served one batch its slots are stale.
+  tables live in HBM. The slots that received an input in a batch are spent
+  and re-garbled; slots a short batch left unused keep their GC (never encoded,
+  so nothing about it was revealed). Failed inputs join the next batch.
 * **Offline/online pipeline.** A background garbler thread re-garbles stale
   groups (on the GPU garbler or the host garbler) and streams them into their
   HBM slots while the online path evaluates the other groups, so in steady
@@ -226,6 +228,8 @@ class InferenceService:
 
     def _refill(self, g: _Group) -> None:
         for b in range(g.slots):
+            if g.gcs[b] is not None:  # never encoded: still fresh
+                continue
             if self.backend == "hip":
                 from .runtime import HipEvaluator
 
@@ -266,14 +270,17 @@ class InferenceService:
             raise RuntimeError("background garbler failed") from self._err
         return g
 
-    def _release(self, g: _Group) -> None:
-        g.gcs = [None] * g.slots
+    def _release(self, g: _Group, used: int) -> None:
+        # only the slots that received an input are spent; an unused slot was never encoded for its GC (its
+        # staging still holds labels of an older, unrelated GC), so its GC stays valid for the next batch
+        for b in range(used):
+            g.gcs[b] = None
         g.ready.clear()
         if self._worker is not None:
             self._q.put(g)
 
     # ------------------------------------------------------------- online
-    def _run_group(self, g: _Group, xs: Sequence[np.ndarray], idx: Sequence[int], attempt: int):
+    def _run_group(self, g: _Group, xs: Sequence[np.ndarray], idx: Sequence[int], attempts: Sequence[int]):
         """Evaluate len(xs) <= slots inputs on group g. Returns per-input logits or None on integrity failure."""
         from . import IntegrityError
 
@@ -281,8 +288,8 @@ class InferenceService:
         t = time.perf_counter()
         if self.backend == "hip":
             ev = g.ev
-            for b in range(g.slots):  # unused slots evaluate a dummy input (their GCs are discarded anyway)
-                ev.encode_compressed_into(b, g.gcs[b], xs[b] if b < len(xs) else xs[0])
+            for b in range(len(xs)):  # unused slots are not encoded (see _release)
+                ev.encode_compressed_into(b, g.gcs[b], xs[b])
             ev.upload_inputs_compressed(g.stream)
             if g.runs == 1:
                 with self._capture_lock:
@@ -299,7 +306,7 @@ class InferenceService:
             ev.fetch_outputs(g.stream)
             for b in range(len(xs)):
                 msg = np.array(ev.outputs_compressed(b), copy=True)
-                if self.fault_hook is not None and self.fault_hook(idx[b], attempt):
+                if self.fault_hook is not None and self.fault_hook(idx[b], attempts[b]):
                     msg[0, 0, 0] ^= np.uint64(1) << np.uint64(9)
                 try:
                     out[b] = np.asarray(g.gcs[b].decode_compressed(msg))
@@ -309,7 +316,7 @@ class InferenceService:
             for b, x in enumerate(xs):
                 gc = g.gcs[b]
                 labels = gc.cpu_evaluate(gc.garble_inputs(x), self.nthreads)
-                if self.fault_hook is not None and self.fault_hook(idx[b], attempt):
+                if self.fault_hook is not None and self.fault_hook(idx[b], attempts[b]):
                     p, arr = labels[0]
                     arr = np.array(arr, copy=True)
                     arr.flat[0] = (int(arr.flat[0]) + 1) % int(p)
@@ -323,35 +330,32 @@ class InferenceService:
         return out
 
     def infer(self, xs: Sequence[np.ndarray]) -> np.ndarray:
+        from collections import deque
+
+        from . import IntegrityError
+
         if not self.healthy:
             raise RuntimeError("service is unhealthy (a GPU step timed out); restart the rank")
         xs = [np.asarray(x, dtype=np.int64).reshape(-1) for x in xs]
         results: list = [None] * len(xs)
-        pending = list(range(len(xs)))
-        attempt = 0
+        pending = deque((i, 0) for i in range(len(xs)))  # (input, attempt); retries join later batches
+        slots = self.groups[0].slots
         while pending:
-            if attempt > self.max_retries:
-                from . import IntegrityError
-
-                raise IntegrityError(f"inputs {pending} failed the integrity check {attempt} times")
-            failed = []
-            for s in range(0, len(pending), self.groups[0].slots):
-                chunk = pending[s:s + self.groups[0].slots]
-                g = self._take_group()
-                try:
-                    out = self._run_group(g, [xs[i] for i in chunk], chunk, attempt)
-                finally:
-                    self._release(g)  # single use: every GC of the group is discarded, then re-garbled
-                for i, y in zip(chunk, out):
-                    if y is None:
-                        failed.append(i)
-                    else:
-                        results[i] = y
-                        self.stats.inferences += 1
-            if failed:
-                self.stats.retries += len(failed)
-            pending = failed
-            attempt += 1
+            batch = [pending.popleft() for _ in range(min(slots, len(pending)))]
+            g = self._take_group()
+            try:
+                out = self._run_group(g, [xs[i] for i, _ in batch], [i for i, _ in batch], [a for _, a in batch])
+            finally:
+                self._release(g, len(batch))  # single use: the GCs that saw an input are discarded, then re-garbled
+            for (i, a), y in zip(batch, out):
+                if y is not None:
+                    results[i] = y
+                    self.stats.inferences += 1
+                elif a + 1 > self.max_retries:
+                    raise IntegrityError(f"input {i} failed the integrity check {a + 1} times")
+                else:
+                    self.stats.retries += 1
+                    pending.append((i, a + 1))
         return np.stack(results)
 
     def close(self) -> None:
