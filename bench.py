@@ -37,7 +37,7 @@ def main() -> None:
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--batch", type=int, default=int(os.environ.get("DASH_BENCH_BATCH", "24")),
+    ap.add_argument("--batch", type=int, default=int(os.environ.get("DASH_BENCH_BATCH", "28")),
                     help="garbled circuits evaluated together per GPU")
     ap.add_argument("--streams", type=int, default=int(os.environ.get("DASH_BENCH_STREAMS", "4")),
                     help="independent GC groups per GPU, each on its own HIP stream (overlap latency- and "

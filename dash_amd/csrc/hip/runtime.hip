@@ -42,12 +42,18 @@ class HipEvaluator {
         DASH_CHECK(k_ <= kMaxRes, "too many CRT residues for the GPU path");
         loaded_.assign(B_, 0);
         build();
+        // Keep only what load() checks: holding the template model would pin
+        // its garbled tables (10 GB per MiniONN GC, device-resident when the
+        // GPU garbler made them) for the evaluator's lifetime.
+        tmpl_h_ = tmpl_->h;
+        tmpl_nlayers_ = tmpl_->layers.size();
+        tmpl_.reset();
     }
     // Upload garbled model `m` (same circuit as the template) into batch slot b.
     void load(int b, const GarbledModel& m) {
         DASH_CHECK(b >= 0 && b < B_, "batch slot out of range");
-        DASH_CHECK(m.h.crt == tmpl_->h.crt && m.h.mrs == tmpl_->h.mrs && m.layers.size() == tmpl_->layers.size() &&
-                       m.h.in_dims == tmpl_->h.in_dims,
+        DASH_CHECK(m.h.crt == tmpl_h_.crt && m.h.mrs == tmpl_h_.mrs && m.layers.size() == tmpl_nlayers_ &&
+                       m.h.in_dims == tmpl_h_.in_dims,
                    "model does not garble the evaluator's circuit");
         HIPCHECK(hipSetDevice(dev_));
         for (auto& f : loaders_) f(b, m);
@@ -339,7 +345,9 @@ class HipEvaluator {
     void build();
     void plan_rescale_legacy(size_t li, i64 iters, i64 N, const CrtInfo& crt, const std::string& lname);
 
-    std::shared_ptr<GarbledModel> tmpl_;
+    std::shared_ptr<GarbledModel> tmpl_;  // build() only
+    ModelHeader tmpl_h_;
+    size_t tmpl_nlayers_ = 0;
     bool mfma_;
     std::vector<std::function<void(int, const GarbledModel&)>> loaders_;
     std::vector<int> loaded_;
