@@ -6,6 +6,8 @@
   python -m dash_amd garble  --out model.dgc [--decoder-out dec.bin] [...model flags]
   python -m dash_amd serve   --port P [--backend hip|cpu]          (evaluator party)
   python -m dash_amd client  --host H --port P [...model flags]    (garbler party)
+  python -m dash_amd run-service [...model flags] [--batch B --groups G --max-retries R --step-timeout-s T]
+                             (serving engine: GC pool re-garbled in the background, recovery, watchdog)
   python -m dash_amd export-onnx --model M --out m.onnx
 """
 from __future__ import annotations
@@ -105,6 +107,28 @@ def cmd_infer(args):
         print(f"accuracy: {np.mean(np.array(preds) == np.array(labels)):.4f}")
 
 
+def cmd_run_service(args):
+    import json
+
+    from .config import DashConfig
+    from .serving import InferenceService
+
+    cfg = DashConfig.from_args(args)
+    circuit, _, xq, labels, (crt, mrs, mm) = _circuit_and_inputs(cfg)
+    with InferenceService(circuit, crt, mrs, max_modulus=mm, slots_per_group=max(1, cfg.batch), groups=cfg.groups,
+                          backend=cfg.backend, device=cfg.device, garble_device=cfg.garble_device,
+                          max_retries=cfg.max_retries, step_timeout_s=cfg.step_timeout_s, seed=cfg.seed_bytes(),
+                          nthreads=cfg.nthreads) as svc:
+        ys = svc.infer(xq)
+        stats = svc.stats.as_dict()
+    preds = [int(np.argmax(y)) for y in ys]
+    for i, p in enumerate(preds):
+        print(f"input {i}: pred {p}")
+    if labels is not None:
+        print(f"accuracy: {np.mean(np.array(preds) == np.array(labels)):.4f}")
+    print(json.dumps(stats))
+
+
 def cmd_garble(args):
     from .config import DashConfig
     from .garbling import GarbledCircuit
@@ -171,7 +195,7 @@ def main(argv=None):
     ap = argparse.ArgumentParser(prog="python -m dash_amd")
     sub = ap.add_subparsers(dest="cmd", required=True)
     sub.add_parser("info")
-    for name in ("infer", "garble", "client"):
+    for name in ("infer", "garble", "client", "run-service"):
         p = sub.add_parser(name)
         DashConfig.add_arguments(p)
         if name == "garble":
@@ -188,7 +212,7 @@ def main(argv=None):
     p.add_argument("--out", required=True)
     args = ap.parse_args(argv)
     {"info": cmd_info, "infer": cmd_infer, "garble": cmd_garble, "serve": cmd_serve, "client": cmd_client,
-     "export-onnx": cmd_export}[args.cmd](args)
+     "export-onnx": cmd_export, "run-service": cmd_run_service}[args.cmd](args)
 
 
 if __name__ == "__main__":

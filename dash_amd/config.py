@@ -57,6 +57,11 @@ class DashConfig:
     nthreads: int = 0
     mfma: bool = True
     profile: bool = False
+    # serving (dash_amd.serving.InferenceService)
+    groups: int = 2                           # evaluator groups in the GC slot pool (each `batch` slots)
+    garble_device: Optional[bool] = None      # GPU garbler (default: on with the hip backend)
+    max_retries: int = 2                      # re-garble + resubmit attempts after an IntegrityError
+    step_timeout_s: float = 120.0             # watchdog deadline of one GPU evaluation
     # data
     dataset: Optional[str] = None             # mnist | cifar10 (None: synthetic)
     data_dir: Optional[str] = None

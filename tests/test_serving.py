@@ -142,3 +142,15 @@ def test_hip_stream_wait_bounded():
         assert native().hip_stream_wait(st, 5.0)  # idle stream drains immediately
     finally:
         native().hip_stream_destroy(st)
+
+
+def test_cli_run_service(capsys):
+    from dash_amd.__main__ import main
+
+    main(["run-service", "--model", "MODEL_A", "--scheme", "SIMPLE", "--backend", "cpu", "--batch", "2",
+          "--groups", "2", "--inputs", "3", "--seed", "00" * 16])
+    out = capsys.readouterr().out
+    import json
+
+    stats = json.loads(out.strip().splitlines()[-1])
+    assert stats["inferences"] == 3 and stats["integrity_failures"] == 0
