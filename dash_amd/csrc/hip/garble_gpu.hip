@@ -130,6 +130,7 @@ struct Gadget {
     uint64_t layer, sslot, mask;  // PRG stream of this gadget: stream_of(layer, sslot, e, mask)
     int16_t* S;       // scratch [N][nslots][kW]
     int64_t N;
+    int mrs[kMaxMrs]; // MRS base of the sign gadget (per-digit output moduli of the fanned-out approx projections)
 };
 
 // Stage a gadget's small descriptor array (draws / projections) in LDS so the
@@ -396,10 +397,25 @@ __global__ __launch_bounds__(kPB) void k_project(Ctx c, Gadget g, In in, Tables 
         const int16_t* inl = label_ref(c, g, in, e, P.in_kind, P.in_idx, P.pin);
         uint32_t color;
         const u128 H = aes_encrypt(aes, proj_key(inl, c.R + static_cast<int64_t>(P.pin) * kW, i, mi, color));
+        if (P.fn == F_LUT) {
+            // approx fan-out: digit d's entry at off + color*t + d, payload mrs0_slot + d + lut[j][i][d] * R_{m_d}
+            const int t = P.stride;
+            u128* row = tb.t[P.table] + e * tb.row[P.table] + P.off + static_cast<int64_t>(color) * t;
+            for (int d = 0; d < t; ++d) {
+                const int pout = rfl(g.mrs[d]);
+                const ModC md = rfl_modc(c.mc[pout]);
+                int64_t f = c.lut[c.lut_off[P.a0] + i * t + d];
+                int64_t cm = f % pout;
+                if (cm < 0) cm += pout;
+                const int16_t* ol = g.S + (e * g.nslots + P.out_slot + d) * kW;
+                const u128 pay = proj_payload(ol, c.R + static_cast<int64_t>(pout) * kW, static_cast<uint32_t>(cm), md);
+                if (e_raw < N) row[d] = pay + H;
+            }
+            continue;
+        }
         // function value
         int64_t f;
         switch (P.fn) {
-            case F_LUT: f = c.lut[c.lut_off[P.a0] + i * P.a2 + P.a1]; break;  // a0 = j, a1 = d, a2 = t
             case F_DIV: f = i / P.a0; break;
             case F_SIGN: f = i < P.a0 ? P.a2 : P.a1; break;  // a0 = half, a1 = lower, a2 = upper
             case F_MULR: {
@@ -689,10 +705,11 @@ SignLayout sign_layout(const SignPlan& P, int extra_slots) {
         first += p.pin;
         L.projs.push_back(p);
     };
+    // approx: ONE projection per residue j fanned out over the t digits (same input key and hash for all
+    // digits; per digit d: output slot mrs0 + j*t + d, modulus mrs[d], table offset + d), see k_project
     for (int j = 0; j < k; ++j)
-        for (int d = 0; d < t; ++d)
-            add(Proj{S_INPUT, j, P.crt[j], mrs0 + j * t + d, P.mrs[d], F_LUT, j, d, t, R_BANK, 0, 0, t,
-                     t * P.crt_prefix[j] + d, 0});
+        add(Proj{S_INPUT, j, P.crt[j], mrs0 + j * t, P.mrs[0], F_LUT, j, 0, t, R_BANK, 0, 0, t,
+                 t * P.crt_prefix[j], 0});
     int64_t c1 = 0, c2 = 0;
     for (int q = 0; q + 1 < t; ++q) {
         const int d = t - 1 - q;
@@ -909,6 +926,7 @@ void run_sign(const gg::Ctx& c, const gg::SignLayout& L, gg::Gadget& g, const gg
     g.nprojs = static_cast<int>(L.projs.size());
     g.entries = L.entries;
     g.nblk = draw_blocks(L.draws);
+    for (int d = 0; d < L.ss.t; ++d) g.mrs[d] = L.ss.mrs[d];
     check_desc(g);
     hipLaunchKernelGGL(gg::k_draw, dim3(blocks_for(g.N * g.nblk, gg::kGB, 8192)), dim3(gg::kGB), 0, nullptr, c, g);
     hipLaunchKernelGGL(gg::k_sign_derive, dim3(blocks_for(g.N, 256)), dim3(256), 0, nullptr, c, g, L.ss);
