@@ -284,6 +284,16 @@ __device__ __forceinline__ uint32_t aes_last(const AesCtx& a, uint32_t s0, uint3
     return xor3(x1, x2, rk);
 }
 
+#ifdef DASH_FAKE_AES
+// A/B experiment only (bound analysis): a cheap stand-in mixing function in place of AES.
+__device__ __forceinline__ u128 aes_encrypt(const AesCtx&, u128 in) {
+    return (in ^ (in >> 61)) * static_cast<u128>(0x9e3779b97f4a7c15ull);
+}
+__device__ __forceinline__ void aes_encrypt2(const AesCtx& a, u128 inA, u128 inB, u128& outA, u128& outB) {
+    outA = aes_encrypt(a, inA);
+    outB = aes_encrypt(a, inB);
+}
+#else
 __device__ __forceinline__ u128 aes_encrypt(const AesCtx& a, u128 in) {
     uint32_t s0 = bswap32(static_cast<uint32_t>(in)) ^ kAesRk[0];
     uint32_t s1 = bswap32(static_cast<uint32_t>(in >> 32)) ^ kAesRk[1];
@@ -339,6 +349,7 @@ __device__ __forceinline__ void aes_encrypt2(const AesCtx& a, u128 inA, u128 inB
     outA = fin(a0, a1, a2, a3);
     outB = fin(b0, b1, b2, b3);
 }
+#endif  // DASH_FAKE_AES
 
 // Global tables: Te0 (256 words); rk kept for the launch ABI (round keys are literals).
 struct AesGlobals {
