@@ -91,11 +91,22 @@ def main() -> None:
     evs = [None] * G
     garble_s = 0.0
     upload_s = 0.0
-    for b in range(B):
+    free0 = torch.cuda.mem_get_info(device)[0]
+    b = 0
+    while b < B:
         seed = hashlib.sha256(f"dash-bench/{rank}/{b}/{os.getpid()}".encode()).digest()[:16]
         t = time.perf_counter()
         gc = GarbledCircuit(circuit, cfg["crt"], cfg["mrs"], seed=seed, device=device if args.garble_device else None)
         garble_s += time.perf_counter() - t
+        if b == 0:
+            # HBM guard: all B GCs' tables stay resident (plus ~3 % evaluator scratch and one GC in flight in the
+            # garbler); shrink B to a multiple of the stream groups if this device cannot hold them
+            fit = int((free0 - gc.table_bytes - 2.5e9) // (1.027 * gc.table_bytes))
+            log(f"rank {rank}: {free0 / 1e9:.1f} GB HBM free, {gc.table_bytes / 1e9:.2f} GB tables per GC: fits {fit}")
+            if fit < B:
+                B = max(G, fit - fit % G)
+                per = B // G
+                log(f"rank {rank}: HBM holds {fit} GCs of {gc.table_bytes / 1e9:.2f} GB: batch reduced to {B}")
         t = time.perf_counter()
         g = b // per
         if evs[g] is None:
@@ -107,6 +118,7 @@ def main() -> None:
         gc.model = None  # host copy no longer needed (tables live in HBM)
         gcs.append(gc)
         log(f"rank {rank}: garbled+uploaded GC {b + 1}/{B} ({table_gb:.2f} GB tables)")
+        b += 1
     offline_s = time.perf_counter() - t_off
     native().gpu_table_cache_trim()  # the garbler's recycled table blocks are no longer needed
     free_b, total_b = torch.cuda.mem_get_info(device)
