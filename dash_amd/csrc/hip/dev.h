@@ -359,10 +359,15 @@ struct AesGlobals {
 
 // Fill the LDS image; all threads of the block participate.
 __device__ __forceinline__ void aes_lds_fill(uint32_t* lds, const uint32_t* te0) {
+    // 16-B LDS stores: the 4 words of an aligned quad share the table entry
+    // (i >> 6) and the rotation (i & 32), so every block's 64 KiB image costs
+    // a quarter of the loads and LDS writes of a word-wise fill
     const int nt = blockDim.x * blockDim.y;
-    for (int i = threadIdx.x + threadIdx.y * blockDim.x; i < DASH_AES_LDS_WORDS; i += nt) {
+    for (int i4 = threadIdx.x + threadIdx.y * blockDim.x; i4 < DASH_AES_LDS_WORDS / 4; i4 += nt) {
+        const int i = 4 * i4;
         const uint32_t v = te0[i >> 6];
-        lds[i] = (i & 32) ? ror32(v, 16) : v;
+        const uint32_t w = (i & 32) ? ror32(v, 16) : v;
+        reinterpret_cast<uint4*>(lds)[i4] = make_uint4(w, w, w, w);
     }
     __syncthreads();
 }

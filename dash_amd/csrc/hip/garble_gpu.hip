@@ -149,7 +149,7 @@ __device__ __forceinline__ void lds_stage(T* dst, const T* src, int n) {
 // components of one draw (Prg::label order), so neighbouring lanes write
 // neighbouring components and every lane does exactly one AES.
 __global__ __launch_bounds__(kGB) void k_draw(Ctx c, Gadget g) {
-    __shared__ uint32_t lds_aes[DASH_AES_LDS_WORDS];
+    __shared__ __attribute__((aligned(16))) uint32_t lds_aes[DASH_AES_LDS_WORDS];
     __shared__ Draw sd[kMaxDesc];
     lds_stage(sd, g.draws, g.ndraws);
     aes_lds_fill(lds_aes, c.te0);
@@ -367,7 +367,7 @@ __device__ __forceinline__ Proj rfl_proj(const Proj& p) {
 }
 
 __global__ __launch_bounds__(kPB) void k_project(Ctx c, Gadget g, In in, Tables tb) {
-    __shared__ uint32_t lds_aes[DASH_AES_LDS_WORDS];
+    __shared__ __attribute__((aligned(16))) uint32_t lds_aes[DASH_AES_LDS_WORDS];
     __shared__ Proj sp[kMaxDesc];
     lds_stage(sp, g.projs, g.nprojs);
     aes_lds_fill(lds_aes, c.te0);
@@ -450,7 +450,7 @@ struct MiniArgs {
 };
 
 __global__ __launch_bounds__(256) void k_relu_finish(Ctx c, Gadget g, In in, Tables tb, MiniArgs m) {
-    __shared__ uint32_t lds_aes[DASH_AES_LDS_WORDS];
+    __shared__ __attribute__((aligned(16))) uint32_t lds_aes[DASH_AES_LDS_WORDS];
     aes_lds_fill(lds_aes, c.te0);
     const AesCtx aes = aes_ctx(lds_aes, nullptr);
     const int64_t total = g.N * m.k;
@@ -509,7 +509,7 @@ struct RsArgs {
 // written here: the sign gadget reads Z_2 for residue 0 directly (In with a
 // zero element stride) and k_rescale_post_g overwrites L_0 afterwards.
 __global__ __launch_bounds__(kGB) void k_rescale_pre(Ctx c, RsArgs a, Tables tb, int64_t N) {
-    __shared__ uint32_t lds_aes[DASH_AES_LDS_WORDS];
+    __shared__ __attribute__((aligned(16))) uint32_t lds_aes[DASH_AES_LDS_WORDS];
     aes_lds_fill(lds_aes, c.te0);
     const AesCtx aes = aes_ctx(lds_aes, nullptr);
     const int km = a.k - 1;

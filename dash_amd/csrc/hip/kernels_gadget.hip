@@ -52,7 +52,7 @@ static inline dim3 grid_aes(int64_t n, int bs, int y, int z) {
 // static (not dynamic) LDS: its address is a link-time constant, so the
 // table base folds into the ds_read offset field
 #define AES_PROLOGUE(tab, rk)                    \
-    __shared__ uint32_t lds_aes[DASH_AES_LDS_WORDS]; \
+    __shared__ __attribute__((aligned(16))) uint32_t lds_aes[DASH_AES_LDS_WORDS]; \
     aes_lds_fill(lds_aes, tab);                   \
     const AesCtx aes = aes_ctx(lds_aes, rk)
 

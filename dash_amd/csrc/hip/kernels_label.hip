@@ -77,7 +77,7 @@ __global__ __launch_bounds__(256) void k_window_sum(Act in, int64_t Nin, Act out
 
 __global__ __launch_bounds__(512) void k_aes_test(const u128* in, u128* out, int64_t n, const uint32_t* te0,
                                                   const uint32_t* rk) {
-    __shared__ uint32_t lds_aes[DASH_AES_LDS_WORDS];
+    __shared__ __attribute__((aligned(16))) uint32_t lds_aes[DASH_AES_LDS_WORDS];
     aes_lds_fill(lds_aes, te0);
     const AesCtx aes = aes_ctx(lds_aes, rk);
     for (int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < n;
@@ -87,7 +87,7 @@ __global__ __launch_bounds__(512) void k_aes_test(const u128* in, u128* out, int
 
 // Throughput probe: every lane runs `iters` x 2 chained encryptions.
 __global__ __launch_bounds__(512) void k_aes_bench(u128* out, int iters, const uint32_t* te0) {
-    __shared__ uint32_t lds_aes[DASH_AES_LDS_WORDS];
+    __shared__ __attribute__((aligned(16))) uint32_t lds_aes[DASH_AES_LDS_WORDS];
     aes_lds_fill(lds_aes, te0);
     const AesCtx aes = aes_ctx(lds_aes, nullptr);
     const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
