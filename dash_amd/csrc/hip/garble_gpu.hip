@@ -20,6 +20,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <map>
+#include <tuple>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -758,6 +759,40 @@ T* dput(const T* h, size_t n, std::vector<void*>& owned) {
     return d;
 }
 
+// Structure-only device constants (gadget descriptors, public conv weights):
+// identical for every GC of a model, so they are uploaded once per process and
+// reused. A fresh hipMalloc + hipMemcpy + hipFree per gadget made every layer
+// drain the GPU queue before the host could prepare the next one.
+struct ConstCache {
+    std::mutex m;
+    std::map<std::tuple<int, uint64_t, size_t>, std::pair<std::string, void*>> map;
+};
+inline ConstCache& const_cache() {
+    static ConstCache* c = new ConstCache();  // leaked: lives as long as the process
+    return *c;
+}
+template <class T>
+const T* dconst(const T* h, size_t n) {
+    const size_t bytes = n * sizeof(T);
+    const char* b = reinterpret_cast<const char*>(h);
+    uint64_t x = 1469598103934665603ull;  // FNV-1a
+    for (size_t i = 0; i < bytes; ++i) x = (x ^ static_cast<uint8_t>(b[i])) * 1099511628211ull;
+    int dev = 0;
+    HIPCHECK(hipGetDevice(&dev));
+    ConstCache& c = const_cache();
+    std::lock_guard<std::mutex> g(c.m);
+    auto key = std::make_tuple(dev, x, bytes);
+    auto it = c.map.find(key);
+    if (it != c.map.end() && it->second.first.compare(0, std::string::npos, b, bytes) == 0)
+        return static_cast<const T*>(it->second.second);
+    void* d = nullptr;
+    HIPCHECK(hipMalloc(&d, std::max<size_t>(1, bytes)));
+    if (bytes) HIPCHECK(hipMemcpy(d, h, bytes, hipMemcpyHostToDevice));
+    if (it != c.map.end()) return static_cast<const T*>(d);  // hash collision: keep the first entry, leak this one
+    c.map.emplace(key, std::make_pair(std::string(b, bytes), d));
+    return static_cast<const T*>(d);
+}
+
 }  // namespace gg
 
 
@@ -920,9 +955,9 @@ void check_desc(const gg::Gadget& g) {
 // run the three sign-gadget passes for N elements with input labels `in`
 void run_sign(const gg::Ctx& c, const gg::SignLayout& L, gg::Gadget& g, const gg::In& in, const gg::Tables& tb,
               std::vector<void*>& tmp) {
-    g.draws = gg::dput(L.draws.data(), L.draws.size(), tmp);
+    g.draws = gg::dconst(L.draws.data(), L.draws.size());
     g.ndraws = static_cast<int>(L.draws.size());
-    g.projs = gg::dput(L.projs.data(), L.projs.size(), tmp);
+    g.projs = gg::dconst(L.projs.data(), L.projs.size());
     g.nprojs = static_cast<int>(L.projs.size());
     g.entries = L.entries;
     g.nblk = draw_blocks(L.draws);
@@ -946,6 +981,20 @@ void set_stale(CrtLabels& cur, const std::vector<int>& mods, int64_t N) {
 }
 }  // namespace
 
+namespace gg {
+// End of a layer's launches. Everything of a GC runs in order on the null
+// stream, so the next layer (and block reuse through the table cache) needs no
+// host-device sync: the host prepares layer i+1 while the GPU runs layer i.
+// Only temporary device allocations force a drain before they are freed;
+// DASH_GG_SYNC=1 restores per-layer syncs (exact per-layer garbling timers).
+inline void end_layer(std::vector<void*>& tmp) {
+    static const bool sync = std::getenv("DASH_GG_SYNC") != nullptr;
+    if (sync || !tmp.empty()) HIPCHECK(hipDeviceSynchronize());
+    for (void* p : tmp) (void)hipFree(p);
+    tmp.clear();
+}
+}  // namespace gg
+
 struct GpuGarbler::Impl {
     gg::Ctx c{};
     std::vector<void*> owned;
@@ -960,6 +1009,29 @@ struct GpuGarbler::Impl {
     std::vector<int> crt;
     int k = 0;
     int device = 0;
+    // per-GC small uploads (up/down shift labels): pinned staging + device ring, copied asynchronously on the
+    // garbling stream (no queue drain); one garble() uses far less than the ring, which restarts per GpuGarbler
+    static constexpr size_t kRing = 8u << 20;
+    char* ring_h = nullptr;
+    char* ring_d = nullptr;
+    size_t ring_off = 0;
+    template <class T>
+    const T* stage(const T* h, size_t n) {
+        const size_t bytes = (n * sizeof(T) + 255) / 256 * 256;
+        if (!ring_h) {
+            HIPCHECK(hipHostMalloc(reinterpret_cast<void**>(&ring_h), kRing));
+            HIPCHECK(hipMalloc(reinterpret_cast<void**>(&ring_d), kRing));
+        }
+        if (ring_off + bytes > kRing) {  // wrap: earlier copies must have landed before their staging is reused
+            HIPCHECK(hipStreamSynchronize(nullptr));
+            ring_off = 0;
+        }
+        std::memcpy(ring_h + ring_off, h, n * sizeof(T));
+        HIPCHECK(hipMemcpyAsync(ring_d + ring_off, ring_h + ring_off, n * sizeof(T), hipMemcpyHostToDevice, nullptr));
+        const T* d = reinterpret_cast<const T*>(ring_d + ring_off);
+        ring_off += bytes;
+        return d;
+    }
     int16_t* scratch(size_t bytes) {
         if (bytes > S_bytes) {
             if (S) (void)hipFree(S);
@@ -980,9 +1052,12 @@ struct GpuGarbler::Impl {
         for (size_t j = 0; j < host.size(); ++j) DASH_CHECK(host[j].p == cur_mod[j], "gpu garbler: modulus mismatch");
     }
     ~Impl() {
+        (void)hipDeviceSynchronize();  // garble() returns with every table written
         cur.clear();
         for (void* p : owned) (void)hipFree(p);
         if (S) (void)hipFree(S);
+        if (ring_h) (void)hipHostFree(ring_h);
+        if (ring_d) (void)hipFree(ring_d);
     }
 };
 
@@ -1078,8 +1153,8 @@ void GpuGarbler::conv(const ConvGeom& G, const std::vector<i64>& w, CrtLabels& c
         gg::ConvG g{static_cast<int>(G.C), static_cast<int>(G.H), static_cast<int>(G.W), F, static_cast<int>(G.kh),
                     static_cast<int>(G.kw), static_cast<int>(G.sh), static_cast<int>(G.sw), static_cast<int>(G.ph),
                     static_cast<int>(G.pw), static_cast<int>(G.OH), static_cast<int>(G.OW), K, nr_comps(p), p};
-        const int32_t* dw = gg::dput(wp.data(), wp.size(), tmp);
-        const int32_t* dz = gg::dput(zc.data(), zc.size(), tmp);
+        const int32_t* dw = gg::dconst(wp.data(), wp.size());
+        const int32_t* dz = gg::dconst(zc.data(), zc.size());
         const int64_t threads = G.OH * G.OW * static_cast<int64_t>(g.n);
         DASH_CHECK((threads + 255) / 256 < (int64_t(1) << 31), "gpu garbler: conv grid too large");
         hipLaunchKernelGGL(gg::k_conv_garble, dim3(static_cast<unsigned>((threads + 255) / 256), nch), dim3(256), 0,
@@ -1087,9 +1162,8 @@ void GpuGarbler::conv(const ConvGeom& G, const std::vector<i64>& w, CrtLabels& c
                            I.c.Z + static_cast<int64_t>(p) * gg::kW);
     }
     HIPCHECK(hipGetLastError());
-    HIPCHECK(hipDeviceSynchronize());
+    gg::end_layer(tmp);
     tr_.mark("kernels");
-    for (void* p : tmp) (void)hipFree(p);
     I.cur = std::move(out);
     I.cur_N = G.out_size();
     set_stale(cur, mods, I.cur_N);
@@ -1171,9 +1245,9 @@ void GpuGarbler::sign_layer(uint64_t layer, const SignPlan& sp, CrtLabels& cur, 
         // the e table row is [k][3]: projection entries land at j*3 + color
         gg::Gadget gm = g;
         gm.sslot = 2;
-        gm.draws = gg::dput(dr.data(), dr.size(), tmp);
+        gm.draws = gg::dconst(dr.data(), dr.size());
         gm.ndraws = static_cast<int>(dr.size());
-        gm.projs = gg::dput(pr.data(), pr.size(), tmp);
+        gm.projs = gg::dconst(pr.data(), pr.size());
         gm.nprojs = static_cast<int>(pr.size());
         gm.entries = first;
         gm.nblk = draw_blocks(dr);
@@ -1203,13 +1277,12 @@ void GpuGarbler::sign_layer(uint64_t layer, const SignPlan& sp, CrtLabels& cur, 
         hipLaunchKernelGGL(gg::k_gather_slots, dim3(blocks_for(N * 128, 256, 4096), ga.k), dim3(256), 0, nullptr, g, ga);
     }
     HIPCHECK(hipGetLastError());
-    HIPCHECK(hipDeviceSynchronize());
+    gg::end_layer(tmp);
     tr_.mark("kernels");
     tA.to_array(ap, I.device);
     t1.to_array(c1, I.device);
     t2.to_array(c2, I.device);
     tS.to_array(sg, I.device);
-    for (void* p : tmp) (void)hipFree(p);
     I.cur = std::move(out);
     I.cur_mod = omods;
     set_stale(cur, omods, N);
@@ -1240,8 +1313,8 @@ void GpuGarbler::rescale_legacy_iter(uint64_t layer, int it, const RescalePlan& 
     }
     // inverses of 2 for the active residues (plan order = residues 1..k-1)
     for (size_t a = 0; a < P.active[0].size(); ++a) ra.inv[P.active[0][a]] = static_cast<int>(P.inv[0][a]);
-    ra.up = gg::dput(hup.data(), hup.size(), tmp);
-    ra.down = gg::dput(hdn.data(), hdn.size(), tmp);
+    ra.up = I.stage(hup.data(), hup.size());
+    ra.down = I.stage(hdn.data(), hdn.size());
     ra.layer = layer;
     ra.sslot = 10 + it;
     DevTable tT, tA, t1, t2, tS;
@@ -1284,14 +1357,13 @@ void GpuGarbler::rescale_legacy_iter(uint64_t layer, int it, const RescalePlan& 
     hipLaunchKernelGGL(gg::k_rescale_post_g, dim3(blocks_for(N * 128, 256, 4096), k), dim3(256), 0, nullptr, I.c, ra,
                        g, L.out_slot0);
     HIPCHECK(hipGetLastError());
-    HIPCHECK(hipDeviceSynchronize());
+    gg::end_layer(tmp);
     tr_.mark("kernels");
     tT.to_array(tr, I.device);
     tA.to_array(ap, I.device);
     t1.to_array(c1, I.device);
     t2.to_array(c2, I.device);
     tS.to_array(sg, I.device);
-    for (void* p : tmp) (void)hipFree(p);
     set_stale(cur, I.cur_mod, N);
 }
 
