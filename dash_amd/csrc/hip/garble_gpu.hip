@@ -625,7 +625,8 @@ __global__ __launch_bounds__(256) void k_conv_garble(ConvG g, const int16_t* __r
                     in ? X[(static_cast<int64_t>(ci * g.H + iy) * g.W + ix) * g.n + c] : zv);
                 const int32_t* wk = wc + k * kFT;
 #pragma unroll
-                for (int f = 0; f < kFT; ++f) acc[f] += static_cast<uint32_t>(wk[f]) * xv;
+                // w, x < p < 2^24: full-rate v_mad_u32_u24 (a 32-bit product is a quarter-rate v_mul_lo_u32)
+                for (int f = 0; f < kFT; ++f) acc[f] = __umul24(static_cast<uint32_t>(wk[f]), xv) + acc[f];
             }
         }
 #pragma unroll
