@@ -82,6 +82,15 @@ def test_relu_edges():
     _check(c, [2, 3, 5], [26, 6, 3, 2], [vals])
 
 
+@pytest.mark.parametrize("layer", ["relu", "sign"])
+def test_single_digit_mrs(layer):
+    """ReLU/Sign accuracy 99 % with k = 8 selects a one-digit MRS base ([126]): no casts, no carry chain."""
+    rng = np.random.default_rng(5)
+    xs = [rng.integers(-1000, 1000, 64) for _ in range(2)]
+    c = d.Circuit([d.Relu((64,)) if layer == "relu" else d.Sign((64,))])
+    _check(c, 8, 99.0, xs, plain=False)  # approximate (99 %): GPU == host labels bit for bit
+
+
 def test_rescale_legacy():
     rng = np.random.default_rng(3)
     xs = [rng.integers(-100000, 100000, 300) for _ in range(2)]
