@@ -221,6 +221,17 @@ void Garbler::encode_cm(const i64* x, i64 N, const std::vector<comp_t*>& dst, in
 void Garbler::encode_compressed(const i64* x, i64 N, u128* dst, int nthreads) const {
     DASH_CHECK(!in_base_.empty() && in_base_[0].N == N, "input size does not match the garbled circuit");
     const int k = static_cast<int>(crt_.size());
+    // online message #1 is on the timed path: per residue a (value x component) table of v*R mod p turns
+    // every component into one add and one conditional subtract (a runtime-divisor 64-bit % per
+    // component was most of the cost: 1.7 ms per MiniONN input on 8 threads)
+    std::vector<std::vector<int16_t>> lut(k);
+    for (int j = 0; j < k; ++j) {
+        const int p = crt_[j], n = nr_comps(p);
+        const comp_t* R = R_.get(p);
+        lut[j].resize(static_cast<size_t>(p) * n);
+        for (int v = 0; v < p; ++v)
+            for (int c = 0; c < n; ++c) lut[j][static_cast<size_t>(v) * n + c] = static_cast<int16_t>((v * R[c]) % p);
+    }
     parallel_for(static_cast<i64>(k) * N, [&](i64 r0, i64 r1) {
         comp_t buf[128];
         for (i64 r = r0; r < r1; ++r) {
@@ -229,9 +240,11 @@ void Garbler::encode_compressed(const i64* x, i64 N, u128* dst, int nthreads) co
             const int p = crt_[j];
             const ModInfo& mi = mod_info(p);
             const comp_t* W0 = in_base_[j].at(e);
-            const comp_t* R = R_.get(p);
-            const i64 v = pmod(x[e], p);
-            for (int c = 0; c < mi.n; ++c) buf[c] = static_cast<comp_t>((W0[c] + v * R[c]) % p);
+            const int16_t* L = lut[j].data() + static_cast<size_t>(pmod(x[e], p)) * mi.n;
+            for (int c = 0; c < mi.n; ++c) {
+                const int v = W0[c] + L[c];
+                buf[c] = static_cast<comp_t>(v >= p ? v - p : v);
+            }
             dst[r] = compress(buf, mi);
         }
     }, nthreads);

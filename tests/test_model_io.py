@@ -101,3 +101,13 @@ def test_cli_infer_and_garble(tmp_path, capsys):
     blob = (tmp_path / "a.dgc").read_bytes()
     assert blob[:8] == b"DAMDGC01"
     assert (tmp_path / "a.dec").read_bytes()[:8] == b"DAMDDEC1"
+
+
+def test_compressed_encoding_matches_label_encoding(small):
+    """Online message #1 in wire form == compress(label-form encoding), every residue and element."""
+    c, xs = small
+    gc = GarbledCircuit(c, 8, 100.0, seed=b"w" * 16)
+    for x in xs:
+        wire = np.asarray(gc.garble_inputs_compressed(x))
+        ref = np.asarray(native().compress_labels(gc.garble_inputs(x))).reshape(wire.shape)
+        np.testing.assert_array_equal(wire, ref)
