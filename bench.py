@@ -8,7 +8,13 @@ benchmarks/model_benchmarks/sgx/Enclave/Enclave.cpp:177-183):
     garble_inputs -> H2D -> evaluate -> D2H -> decode_outputs
 for B independent garbled circuits per GPU (one fresh input per GC per step).
 Offline garbling and the table upload are excluded, as in the reference, and
-reported separately. Data: synthetic CIFAR-shaped normalized images, random
+reported separately. The B GCs are garbled once and re-encoded every step: with
+garbling and upload outside the timed region, a step's work (encode, H2D,
+evaluate, D2H, decode for B inferences) is the same as on fresh GCs
+(benchmarks/serving.py measures the fresh-GC-per-inference service instead).
+Groups are encoded and launched one after the other: the staggered starts
+measured faster (375 inf/s) than encoding the next step ahead and launching
+all groups at once (360). Data: synthetic CIFAR-shaped normalized images, random
 (PyTorch-default) initialised weights.
 
 Multi-GPU: one process per GPU (torchrun), batch data parallel; every rank
