@@ -99,31 +99,62 @@ def main() -> None:
     upload_s = 0.0
     free0 = torch.cuda.mem_get_info(device)[0]
     b = 0
-    while b < B:
+    def offline_one(b: int):
+        """Garble GC b (on this rank's GPU) and stream it into its evaluator slot."""
+        nonlocal B, per, garble_s, upload_s
         seed = hashlib.sha256(f"dash-bench/{rank}/{b}/{os.getpid()}".encode()).digest()[:16]
         t = time.perf_counter()
         gc = GarbledCircuit(circuit, cfg["crt"], cfg["mrs"], seed=seed, device=device if args.garble_device else None)
         garble_s += time.perf_counter() - t
         if b == 0:
-            # HBM guard: all B GCs' tables stay resident (plus ~3 % evaluator scratch and one GC in flight in the
-            # garbler); shrink B to a multiple of the stream groups if this device cannot hold them
-            fit = int((free0 - gc.table_bytes - 2.5e9) // (1.027 * gc.table_bytes))
-            log(f"rank {rank}: {free0 / 1e9:.1f} GB HBM free, {gc.table_bytes / 1e9:.2f} GB tables per GC: fits {fit}")
+            # HBM guard: every GC's tables stay resident. Size B from the first group's real device footprint
+            # (tables + evaluator scratch, per GC) plus one GC in flight in the garbler; shrink B to a multiple of
+            # the stream groups if this device cannot hold it.
+            evs[0] = HipEvaluator(template=gc.model, batch=per, device=device, mfma=not args.no_mfma,
+                                  profile=args.profile)
+            per_gc = evs[0].device_bytes() / per
+            fit = int((free0 - gc.table_bytes - 2.5e9) // per_gc)
+            log(f"rank {rank}: {free0 / 1e9:.1f} GB HBM free, {per_gc / 1e9:.2f} GB per GC "
+                f"({gc.table_bytes / 1e9:.2f} GB tables): fits {fit}")
             if fit < B:
                 B = max(G, fit - fit % G)
                 per = B // G
-                log(f"rank {rank}: HBM holds {fit} GCs of {gc.table_bytes / 1e9:.2f} GB: batch reduced to {B}")
+                log(f"rank {rank}: batch reduced to {B}")
+                evs[0] = None
+                evs[0] = HipEvaluator(template=gc.model, batch=per, device=device, mfma=not args.no_mfma,
+                                      profile=args.profile)
         t = time.perf_counter()
         g = b // per
         if evs[g] is None:
+            native().gpu_table_cache_trim()  # the new group's table arena needs the garbler's cached blocks
             evs[g] = HipEvaluator(template=gc.model, batch=per, device=device, mfma=not args.no_mfma,
                                   profile=args.profile)
         evs[g].load(b % per, gc.model)
         upload_s += time.perf_counter() - t
-        table_gb = gc.table_bytes / 1e9
+        tgb = gc.table_bytes / 1e9
         gc.model = None  # host copy no longer needed (tables live in HBM)
         gcs.append(gc)
-        log(f"rank {rank}: garbled+uploaded GC {b + 1}/{B} ({table_gb:.2f} GB tables)")
+        log(f"rank {rank}: garbled+uploaded GC {b + 1}/{B} ({tgb:.2f} GB tables)")
+        return tgb
+
+    b = 0
+    table_gb = 0.0
+    while b < B:
+        try:
+            table_gb = offline_one(b)
+        except RuntimeError as e:
+            # HBM ran out before the estimate said it would (allocator fragmentation near full memory): keep the
+            # complete groups only
+            if "out of memory" not in str(e) or b < per:
+                raise
+            G = b // per
+            B = G * per
+            del evs[G:]
+            del gcs[B:]
+            native().gpu_table_cache_trim()
+            native().hip_clear_last_error()  # the handled OOM must not resurface in the next launch check
+            log(f"rank {rank}: out of HBM at GC {b + 1}: continuing with {G} groups, batch {B}")
+            break
         b += 1
     offline_s = time.perf_counter() - t_off
     native().gpu_table_cache_trim()  # the garbler's recycled table blocks are no longer needed

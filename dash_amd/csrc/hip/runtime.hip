@@ -1152,6 +1152,9 @@ void register_hip_bindings(py::module_& m) {
             if (spin > 64) std::this_thread::sleep_for(std::chrono::microseconds(spin > 4096 ? 1000 : 50));
         }
     }, py::arg("stream"), py::arg("timeout_s"));
+    // Reset the thread's sticky last-error (e.g. after a handled out-of-memory), so a later
+    // hipGetLastError() launch check does not report it again. Returns the cleared code.
+    m.def("hip_clear_last_error", []() { return static_cast<int>(hipGetLastError()); });
     m.def("hip_device_count", []() {
         int n = 0;
         if (hipGetDeviceCount(&n) != hipSuccess) return 0;
