@@ -218,12 +218,59 @@ void Garbler::encode_cm(const i64* x, i64 N, const std::vector<comp_t*>& dst, in
     }, nthreads);
 }
 
+// Builds the input codebook on first use (bounded to 256 MiB; larger inputs use the per-label path).
+const Garbler::InputCodebook* Garbler::input_codebook() const {
+    InputCodebook& cb = *codebook_;
+    std::lock_guard<std::mutex> g(cb.m);
+    if (cb.built) return cb.tab.empty() ? nullptr : &cb;
+    cb.built = true;
+    if (in_base_.empty()) return nullptr;
+    const int k = static_cast<int>(crt_.size());
+    const i64 N = in_base_[0].N;
+    i64 total = 0;
+    cb.off.assign(k + 1, 0);
+    for (int j = 0; j < k; ++j) cb.off[j + 1] = cb.off[j] + N * crt_[j];
+    total = cb.off[k];
+    if (static_cast<size_t>(total) * sizeof(u128) > (size_t(256) << 20)) return nullptr;
+    cb.tab.resize(total);
+    parallel_for(static_cast<i64>(k) * N, [&](i64 r0, i64 r1) {
+        comp_t buf[128];
+        for (i64 r = r0; r < r1; ++r) {
+            const int j = static_cast<int>(r / N);
+            const i64 e = r % N;
+            const int p = crt_[j];
+            const ModInfo& mi = mod_info(p);
+            const comp_t* W0 = in_base_[j].at(e);
+            const comp_t* R = R_.get(p);
+            for (int c = 0; c < mi.n; ++c) buf[c] = W0[c];
+            u128* out = cb.tab.data() + cb.off[j] + e * p;
+            for (int v = 0; v < p; ++v) {  // W0 + v*R, stepping v by adding R
+                out[v] = compress(buf, mi);
+                for (int c = 0; c < mi.n; ++c) {
+                    const int t = buf[c] + R[c];
+                    buf[c] = static_cast<comp_t>(t >= p ? t - p : t);
+                }
+            }
+        }
+    });
+    return &cb;
+}
+
 void Garbler::encode_compressed(const i64* x, i64 N, u128* dst, int nthreads) const {
     DASH_CHECK(!in_base_.empty() && in_base_[0].N == N, "input size does not match the garbled circuit");
     const int k = static_cast<int>(crt_.size());
-    // online message #1 is on the timed path: per residue a (value x component) table of v*R mod p turns
-    // every component into one add and one conditional subtract (a runtime-divisor 64-bit % per
-    // component was most of the cost: 1.7 ms per MiniONN input on 8 threads)
+    if (const InputCodebook* cb = input_codebook()) {
+        // online message #1 = one codebook lookup per label
+        for (int j = 0; j < k; ++j) {
+            const int p = crt_[j];
+            const u128* T = cb->tab.data() + cb->off[j];
+            u128* d = dst + static_cast<i64>(j) * N;
+            for (i64 e = 0; e < N; ++e) d[e] = T[e * p + pmod(x[e], p)];
+        }
+        return;
+    }
+    // per residue a (value x component) table of v*R mod p: one add and one conditional subtract per
+    // component (a runtime-divisor 64-bit % per component was most of the cost)
     std::vector<std::vector<int16_t>> lut(k);
     for (int j = 0; j < k; ++j) {
         const int p = crt_[j], n = nr_comps(p);
@@ -319,6 +366,7 @@ GarbledModel Garbler::garble(const std::vector<LayerSpec>& layers, const std::ve
     i64 N = 1;
     for (auto d : in_dims) N *= d;
     in_base_.clear();
+    codebook_ = std::make_shared<InputCodebook>();  // a new garbling invalidates the input codebook
     for (int j = 0; j < k; ++j) {
         Labels L(crt_[j], N);
         parallel_for(N, [&](i64 b, i64 e_) {

@@ -8,6 +8,8 @@
 // processes, hosts or devices.
 #pragma once
 
+#include <memory>
+#include <mutex>
 #include <string>
 
 #include "core.h"
@@ -130,6 +132,16 @@ class Garbler {
     CrtLabels in_base_;
     Decoder dec_;
     std::vector<double> layer_ms_;
+    // Input codebook: the compressed label of every (residue j, input element e, value v mod p_j), built
+    // once per GC (offline, on first use) so online message #1 is a table lookup per label.
+    struct InputCodebook {
+        std::mutex m;
+        bool built = false;
+        std::vector<u128> tab;  // residue j at off[j]: [N][p_j]
+        std::vector<i64> off;
+    };
+    std::shared_ptr<InputCodebook> codebook_ = std::make_shared<InputCodebook>();
+    const InputCodebook* input_codebook() const;
 };
 
 // Host (oracle) evaluator: bit-exact reference for the HIP evaluator.
