@@ -114,6 +114,10 @@ def cmd_run_service(args):
     from .serving import InferenceService
 
     cfg = DashConfig.from_args(args)
+    if cfg.seed_bytes() is not None and not cfg.insecure_fixed_seed:
+        # a fixed seed replays the same GC sequence (labels, offsets) on every restart, with new inputs
+        raise SystemExit("run-service: --seed makes every restart reuse the same garbled circuits; "
+                         "pass --insecure-fixed-seed to allow it (tests only)")
     circuit, _, xq, labels, (crt, mrs, mm) = _circuit_and_inputs(cfg)
     with InferenceService(circuit, crt, mrs, max_modulus=mm, slots_per_group=max(1, cfg.batch), groups=cfg.groups,
                           backend=cfg.backend, device=cfg.device, garble_device=cfg.garble_device,

@@ -48,6 +48,7 @@ class DashConfig:
     mrs: Union[float, list, None] = None      # ReLU accuracy (table lookup) or explicit MRS base
     max_modulus: int = 0
     seed: Optional[str] = None                # hex seed for reproducible garbling (tests only)
+    insecure_fixed_seed: bool = False         # allow `seed` in the serving engine (reuses labels across restarts)
     # execution
     backend: str = "hip"                      # hip | cpu
     garbler: str = "host"                     # host (in-process) | remote (dash_amd.net)
@@ -89,7 +90,18 @@ class DashConfig:
         return qm, qp, crt, mrs, (self.max_modulus or mm)
 
     def seed_bytes(self) -> Optional[bytes]:
-        return bytes.fromhex(self.seed) if self.seed else None
+        """The 16-byte garbling seed, or None (fresh randomness).
+
+        CLI values are JSON-decoded, so an all-digit hex seed arrives as an
+        int: coerce to text and left-pad to 32 hex digits."""
+        if self.seed is None or self.seed == "":
+            return None
+        text = str(self.seed).strip().lower()
+        if text.startswith("0x"):
+            text = text[2:]
+        if len(text) > 32:
+            raise ValueError("seed must be at most 16 bytes (32 hex digits)")
+        return bytes.fromhex(text.zfill(32))
 
     # --------------------------------------------------------------- I/O
     def to_dict(self) -> dict:

@@ -486,7 +486,12 @@ void HipEvaluator::build() {
     const i64 cap = std::max(maxN, maxPoolSlots);
     for (int bi = 0; bi < 4; ++bi) {
         bufs_[bi].N = 0;
-        for (int j = 0; j < k_; ++j) bufs_[bi].p[j] = dalloc<int16_t>(static_cast<size_t>(B_) * widest[j] * cap);
+        for (int j = 0; j < k_; ++j) {
+            const size_t count = static_cast<size_t>(B_) * widest[j] * cap;
+            bufs_[bi].p[j] = dalloc<int16_t>(count);
+            // defined contents before any input is staged (serving primes the hipGraph with an unencoded run)
+            HIPCHECK(hipMemset(bufs_[bi].p[j], 0, count * sizeof(int16_t)));
+        }
     }
     int tmax = std::max<int>(1, static_cast<int>(m0.h.mrs.size()));
     mrsP_ = dalloc<u128>(static_cast<size_t>(B_) * k_ * tmax * maxSignN);

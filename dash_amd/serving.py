@@ -42,7 +42,8 @@ import threading
 import time
 from contextlib import contextmanager
 from dataclasses import dataclass, field
-from typing import Callable, List, Optional, Sequence
+from collections import deque
+from typing import Callable, Deque, List, Optional, Sequence
 
 import numpy as np
 
@@ -121,6 +122,10 @@ def wait_stream(stream, timeout_s: float, what: str = "GPU step") -> None:
         raise WatchdogTimeout(f"{what} still running after {timeout_s:.3g} s (GPU hang?)")
 
 
+#: batch latencies kept for the percentiles (a long-running service must not grow without bound)
+LATENCY_WINDOW = 4096
+
+
 @dataclass
 class ServiceStats:
     inferences: int = 0
@@ -131,7 +136,7 @@ class ServiceStats:
     gcs_garbled: int = 0
     garble_s: float = 0.0
     pool_waits_s: float = 0.0
-    latencies_ms: List[float] = field(default_factory=list)
+    latencies_ms: Deque[float] = field(default_factory=lambda: deque(maxlen=LATENCY_WINDOW))
     t_start: float = field(default_factory=time.perf_counter)
 
     def as_dict(self) -> dict:
@@ -146,6 +151,7 @@ class ServiceStats:
             "integrity_failures": self.integrity_failures, "timeouts": self.timeouts,
             "gcs_garbled": self.gcs_garbled, "garble_s_per_gc": round(self.garble_s / max(1, self.gcs_garbled), 4),
             "pool_wait_s": round(self.pool_waits_s, 3),
+            # percentiles over the last LATENCY_WINDOW batches
             "batch_latency_ms": {"p50": pct(50), "p90": pct(90), "p99": pct(99), "max": pct(100)},
             "inferences_per_s_wall": round(self.inferences / wall, 3) if wall > 0 else None,
         }
@@ -171,7 +177,11 @@ class InferenceService:
     decoded logits ``[len(xs), n_out]`` in order; each input is evaluated on a
     fresh GC. ``fault_hook(global_index, attempt) -> bool`` (tests / chaos
     runs) corrupts that attempt's output message before decoding, which the
-    integrity check must catch and the service must recover from."""
+    integrity check must catch and the service must recover from.
+
+    Thread safety: ``infer`` may be called from several request threads; calls
+    are serialized by an internal lock (one batch at a time reaches the GPU
+    groups, whose slot state is not shared across callers)."""
 
     def __init__(self, circuit, crt, mrs=None, *, max_modulus: int = 0, slots_per_group: int = 4, groups: int = 2,
                  backend: str = "hip", device: int = 0, garble_device: Optional[bool] = None, max_retries: int = 2,
@@ -197,6 +207,7 @@ class InferenceService:
         # hipGraph capture (a group's 2nd run) must not overlap the garbler thread's device-wide syncs and
         # allocations, which would invalidate the capture; replays and eager runs need no lock
         self._capture_lock = threading.Lock()
+        self._infer_lock = threading.Lock()
         self._q: "queue.Queue[Optional[_Group]]" = queue.Queue()
         if backend == "hip":
             import torch
@@ -208,6 +219,8 @@ class InferenceService:
         # fill the pool once synchronously (first GC also sizes the evaluators), then refill in the background
         for g in self.groups:
             self._refill(g)
+        if backend == "hip":
+            self._prime_graphs()
         self._worker = None
         if prefetch:
             self._worker = threading.Thread(target=self._garbler_loop, name="dash-garbler", daemon=True)
@@ -225,6 +238,20 @@ class InferenceService:
         self.stats.garble_s += time.perf_counter() - t
         self.stats.gcs_garbled += 1
         return gc
+
+    def _prime_graphs(self) -> None:
+        """Capture every group's hipGraph now, before the background garbler starts.
+
+        A group's first run is eager and its second run captures the graph; the
+        capture must not overlap the garbler thread's device-wide syncs and
+        allocations. Doing both runs here (no input is encoded, so no GC is
+        spent: the activations hold zeros) means the online path never takes
+        the capture lock, and a refill never stalls an online step."""
+        for g in self.groups:
+            for _ in range(2):
+                g.ev.run(g.stream)
+            g.runs = 2
+            wait_stream(g.stream, self.step_timeout_s, f"group {g.idx} graph capture")
 
     def _refill(self, g: _Group) -> None:
         for b in range(g.slots):
@@ -247,13 +274,15 @@ class InferenceService:
     def _garbler_loop(self) -> None:
         while True:
             g = self._q.get()
-            if g is None:
+            if g is None or not self.healthy:
                 return
             try:
                 self._refill(g)
             except BaseException as e:  # surfaced by the next infer()
                 self._err = e
-                g.ready.set()
+                self.healthy = False
+                for other in self.groups:  # wake every waiter: none of them will be refilled
+                    other.ready.set()
                 return
 
     def _take_group(self) -> _Group:
@@ -264,7 +293,9 @@ class InferenceService:
                 self._refill(g)
             else:
                 t = time.perf_counter()
-                g.ready.wait()
+                while not g.ready.wait(0.5):  # re-check for a dead garbler thread
+                    if self._err is not None:
+                        break
                 self.stats.pool_waits_s += time.perf_counter() - t
         if self._err is not None:
             raise RuntimeError("background garbler failed") from self._err
@@ -276,7 +307,9 @@ class InferenceService:
         for b in range(used):
             g.gcs[b] = None
         g.ready.clear()
-        if self._worker is not None:
+        # an unhealthy service (hung GPU step or dead garbler) never refills: the refill would block on the
+        # hung kernel (device-wide syncs in the GPU garbler and in HipEvaluator.load)
+        if self._worker is not None and self.healthy:
             self._q.put(g)
 
     # ------------------------------------------------------------- online
@@ -291,11 +324,7 @@ class InferenceService:
             for b in range(len(xs)):  # unused slots are not encoded (see _release)
                 ev.encode_compressed_into(b, g.gcs[b], xs[b])
             ev.upload_inputs_compressed(g.stream)
-            if g.runs == 1:
-                with self._capture_lock:
-                    ev.run(g.stream)
-            else:
-                ev.run(g.stream)
+            ev.run(g.stream)  # graph replay: captured in _prime_graphs
             g.runs += 1
             try:
                 wait_stream(g.stream, self.step_timeout_s, f"group {g.idx} evaluation")
@@ -330,10 +359,14 @@ class InferenceService:
         return out
 
     def infer(self, xs: Sequence[np.ndarray]) -> np.ndarray:
-        from collections import deque
+        with self._infer_lock:
+            return self._infer(xs)
 
+    def _infer(self, xs: Sequence[np.ndarray]) -> np.ndarray:
         from . import IntegrityError
 
+        if self._err is not None:
+            raise RuntimeError("background garbler failed; restart the rank") from self._err
         if not self.healthy:
             raise RuntimeError("service is unhealthy (a GPU step timed out); restart the rank")
         xs = [np.asarray(x, dtype=np.int64).reshape(-1) for x in xs]
@@ -358,7 +391,13 @@ class InferenceService:
                     pending.append((i, a + 1))
         return np.stack(results)
 
-    def close(self) -> None:
+    def close(self, join_timeout_s: float = 30.0) -> None:
+        """Stop the garbler thread and free the GPU state.
+
+        An unhealthy service (a hung GPU step) only drops its references to the
+        pool: freeing device memory or destroying streams would block on the
+        hung kernel. The garbler thread is a daemon, so the process can still
+        exit (non-zero) and the supervisor restarts the rank."""
         if self._worker is not None:
             while True:  # drop pending refills: the pool is going away
                 try:
@@ -366,8 +405,12 @@ class InferenceService:
                 except queue.Empty:
                     break
             self._q.put(None)
-            self._worker.join()
+            self._worker.join(timeout=join_timeout_s if self.healthy else 1.0)
             self._worker = None
+        if not self.healthy:
+            self._abandoned = (self.groups, getattr(self, "_streams", []))  # never freed, see above
+            self.groups, self._streams = [], []
+            return
         for g in self.groups:
             g.ev = None
             g.gcs = [None] * g.slots

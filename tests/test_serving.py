@@ -148,9 +148,88 @@ def test_cli_run_service(capsys):
     from dash_amd.__main__ import main
 
     main(["run-service", "--model", "MODEL_A", "--scheme", "SIMPLE", "--backend", "cpu", "--batch", "2",
-          "--groups", "2", "--inputs", "3", "--seed", "00" * 16])
+          "--groups", "2", "--inputs", "3", "--seed", "00" * 16, "--insecure-fixed-seed"])
     out = capsys.readouterr().out
     import json
 
     stats = json.loads(out.strip().splitlines()[-1])
     assert stats["inferences"] == 3 and stats["integrity_failures"] == 0
+
+
+def test_cli_run_service_refuses_fixed_seed():
+    from dash_amd.__main__ import main
+
+    with pytest.raises(SystemExit):
+        main(["run-service", "--model", "MODEL_A", "--scheme", "SIMPLE", "--backend", "cpu", "--inputs", "1",
+              "--seed", "11" * 16])
+
+
+def test_seed_bytes_accepts_json_decoded_digits():
+    from dash_amd.config import DashConfig, _parse_value
+
+    assert DashConfig(seed=_parse_value("11" * 16)).seed_bytes() == bytes([0x11]) * 16
+    assert DashConfig(seed=_parse_value("0a" * 16)).seed_bytes() == bytes([0x0A]) * 16
+    assert DashConfig(seed=7).seed_bytes() == bytes(15) + b"\x07"
+    assert DashConfig(seed=None).seed_bytes() is None
+
+
+def test_latency_history_is_bounded():
+    from dash_amd.serving import LATENCY_WINDOW, ServiceStats
+
+    st = ServiceStats()
+    for i in range(LATENCY_WINDOW + 100):
+        st.latencies_ms.append(float(i))
+    assert len(st.latencies_ms) == LATENCY_WINDOW
+    assert st.as_dict()["batch_latency_ms"]["max"] == float(LATENCY_WINDOW + 99)
+
+
+def test_timeout_is_not_requeued_and_close_returns(small, monkeypatch):
+    """A hung GPU step (faked: _run_group raises WatchdogTimeout) marks the service unhealthy; the hung group
+    is not handed to the garbler (whose refill would block on the hung kernel) and close() returns."""
+    import threading
+
+    c, xs = small
+    svc = InferenceService(c, 8, 100.0, backend="cpu", slots_per_group=2, groups=2, seed=b"t" * 16)
+    hang = threading.Event()
+    refills = []
+
+    def hung_refill(g):  # stands in for a refill stuck in hipDeviceSynchronize
+        refills.append(g.idx)
+        hang.wait()
+
+    def timed_out(g, *a, **k):
+        svc.stats.timeouts += 1
+        svc.healthy = False
+        raise WatchdogTimeout("faked GPU hang")
+
+    monkeypatch.setattr(svc, "_refill", hung_refill)
+    monkeypatch.setattr(svc, "_run_group", timed_out)
+    with pytest.raises(WatchdogTimeout):
+        svc.infer(xs[:2])
+    with pytest.raises(RuntimeError, match="unhealthy"):
+        svc.infer(xs[:2])
+    t = time.time()
+    svc.close()
+    assert time.time() - t < 10
+    assert refills == []  # never re-queued
+    hang.set()
+
+
+def test_garbler_failure_wakes_every_waiter(small, monkeypatch):
+    """A dead background garbler fails every later infer() promptly instead of blocking on a group that
+    will never be refilled."""
+    c, xs = small
+    svc = InferenceService(c, 8, 100.0, backend="cpu", slots_per_group=1, groups=3, seed=b"w" * 16)
+
+    def boom():
+        raise OSError("garbler died")
+
+    monkeypatch.setattr(svc, "_new_gc", boom)
+    t = time.time()
+    with pytest.raises(RuntimeError):
+        svc.infer(xs[:6])  # 6 batches of 1 over 3 groups: needs refills
+    with pytest.raises(RuntimeError):
+        svc.infer(xs[:1])
+    assert not svc.healthy
+    assert time.time() - t < 30
+    svc.close()
