@@ -43,8 +43,12 @@ def main() -> None:
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--batch", type=int, default=int(os.environ.get("DASH_BENCH_BATCH", "28")),
-                    help="garbled circuits evaluated together per GPU")
+    ap.add_argument("--batch", type=int, default=int(os.environ.get("DASH_BENCH_BATCH", "0")),
+                    help="garbled circuits evaluated together per GPU (0: as many as HBM holds, a multiple of "
+                         "--streams)")
+    ap.add_argument("--sign", default=os.environ.get("DASH_BENCH_SIGN", "fused"), choices=["fused", "reference"],
+                    help="sign-gadget construction: casts folded into the approx/carry projections (fused) or the "
+                         "reference's explicit cast gates; both compute the same function")
     ap.add_argument("--streams", type=int, default=int(os.environ.get("DASH_BENCH_STREAMS", "4")),
                     help="independent GC groups per GPU, each on its own HIP stream (overlap latency- and "
                          "bandwidth-bound phases)")
@@ -84,13 +88,12 @@ def main() -> None:
     cfg = BENCH_CONFIGS.get(f"{model}/{args.config}") or BENCH_CONFIGS["MODEL_F_MINIONN_POOL_REPL/DASH"]
     qm, qp = QuantizationMethod(cfg["q_method"]), cfg["q_parameter"]
     circuit = build_circuit(model, qm, qp, seed=0)  # public model, identical on every rank
-    B = args.batch
-    n_inputs = B * (args.steps + args.warmup)
-    inputs = quantized_inputs(model, n_inputs, qm, qp, seed=1000 + rank)
+    B = args.batch if args.batch > 0 else 256  # auto: upper bound, sized from HBM after the first GC
+    G = max(1, min(args.streams, B))
+    B -= B % G
 
     # ---------------- offline: garble B circuits, stream them into HBM
     t_off = time.perf_counter()
-    G = max(1, min(args.streams, B))
     assert B % G == 0, "--batch must be a multiple of --streams"
     per = B // G
     gcs = []
@@ -104,25 +107,26 @@ def main() -> None:
         nonlocal B, per, garble_s, upload_s
         seed = hashlib.sha256(f"dash-bench/{rank}/{b}/{os.getpid()}".encode()).digest()[:16]
         t = time.perf_counter()
-        gc = GarbledCircuit(circuit, cfg["crt"], cfg["mrs"], seed=seed, device=device if args.garble_device else None)
+        gc = GarbledCircuit(circuit, cfg["crt"], cfg["mrs"], seed=seed, device=device if args.garble_device else None,
+                            fused_sign=args.sign == "fused")
         garble_s += time.perf_counter() - t
         if b == 0:
-            # HBM guard: every GC's tables stay resident. Size B from the first group's real device footprint
-            # (tables + evaluator scratch, per GC) plus one GC in flight in the garbler; shrink B to a multiple of
-            # the stream groups if this device cannot hold it.
-            evs[0] = HipEvaluator(template=gc.model, batch=per, device=device, mfma=not args.no_mfma,
-                                  profile=args.profile)
-            per_gc = evs[0].device_bytes() / per
+            # HBM guard: every GC's tables stay resident. Size B from the real device footprint of one GC
+            # (tables + evaluator scratch) plus one GC in flight in the garbler; --batch 0 fills HBM, an explicit
+            # batch shrinks to a multiple of the stream groups if this device cannot hold it.
+            probe = HipEvaluator(template=gc.model, batch=1, device=device, mfma=not args.no_mfma)
+            per_gc = probe.device_bytes() * 1.01
+            del probe
             fit = int((free0 - gc.table_bytes - 2.5e9) // per_gc)
             log(f"rank {rank}: {free0 / 1e9:.1f} GB HBM free, {per_gc / 1e9:.2f} GB per GC "
                 f"({gc.table_bytes / 1e9:.2f} GB tables): fits {fit}")
             if fit < B:
                 B = max(G, fit - fit % G)
-                per = B // G
-                log(f"rank {rank}: batch reduced to {B}")
-                evs[0] = None
-                evs[0] = HipEvaluator(template=gc.model, batch=per, device=device, mfma=not args.no_mfma,
-                                      profile=args.profile)
+                log(f"rank {rank}: batch {'sized' if args.batch <= 0 else 'reduced'} to {B}")
+            B = int(-all_reduce_max(ctx, -float(B)))  # every rank evaluates the same number of GCs
+            per = B // G
+            evs[0] = HipEvaluator(template=gc.model, batch=per, device=device, mfma=not args.no_mfma,
+                                  profile=args.profile)
         t = time.perf_counter()
         g = b // per
         if evs[g] is None:
@@ -159,6 +163,8 @@ def main() -> None:
     offline_s = time.perf_counter() - t_off
     native().gpu_table_cache_trim()  # the garbler's recycled table blocks are no longer needed
     free_b, total_b = torch.cuda.mem_get_info(device)
+    n_inputs = B * (args.steps + args.warmup)
+    inputs = quantized_inputs(model, n_inputs, qm, qp, seed=1000 + rank)
 
     # group 0 on the current stream, the others on torch pool streams (measured best on MI355X:
     # 313 inf/s at B=24 vs 295 with one dedicated non-blocking HIP stream per group, which runs all
@@ -242,6 +248,7 @@ def main() -> None:
                 "global_batch": world * B,
                 "gcs_per_gpu": B,
                 "streams": G,
+                "sign_construction": args.sign,
                 "seq_len": None,
                 "input_shape": [3, 32, 32],
                 "parallelism": f"dp{world}",

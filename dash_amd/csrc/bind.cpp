@@ -199,6 +199,7 @@ PYBIND11_MODULE(_dash_native, m) {
         .def_property_readonly("out_dims", [](const GarbledModel& g) { return g.h.out_dims; })
         .def_property_readonly("out_moduli", [](const GarbledModel& g) { return g.h.out_moduli; })
         .def_property_readonly("max_mod", [](const GarbledModel& g) { return g.h.max_mod; })
+        .def_property_readonly("sign_fused", [](const GarbledModel& g) { return g.h.sign_fused != 0; })
         .def_property_readonly("num_layers", [](const GarbledModel& g) { return g.layers.size(); })
         .def("table_bytes", &GarbledModel::table_bytes)
         .def("total_bytes", &GarbledModel::total_bytes)
@@ -257,18 +258,21 @@ PYBIND11_MODULE(_dash_native, m) {
                  return std::make_shared<Garbler>(crt, mrs, std::string(seed), max_mod);
              }),
              py::arg("crt"), py::arg("mrs"), py::arg("seed"), py::arg("max_mod") = 0)
-        .def("garble", [](Garbler& g, const py::list& layers, std::vector<i64> in_dims, int nthreads, int device) {
+        .def("garble", [](Garbler& g, const py::list& layers, std::vector<i64> in_dims, int nthreads, int device,
+                          bool fused_sign) {
             auto specs = specs_from_py(layers);
             GarbleOptions o;
             o.nthreads = nthreads;
             o.device = device;
+            o.fused_sign = fused_sign;
             GarbledModel gm;
             {
                 py::gil_scoped_release rel;
                 gm = g.garble(specs, in_dims, o);
             }
             return std::make_shared<GarbledModel>(std::move(gm));
-        }, py::arg("layers"), py::arg("in_dims"), py::arg("nthreads") = 0, py::arg("device") = -1)
+        }, py::arg("layers"), py::arg("in_dims"), py::arg("nthreads") = 0, py::arg("device") = -1,
+           py::arg("fused_sign") = true)
         .def("layer_ms", [](const Garbler& g) { return g.layer_ms(); })
         .def("encode", [](const Garbler& g, py::array_t<i64, py::array::c_style | py::array::forcecast> x) {
             std::vector<i64> v(x.data(), x.data() + x.size());

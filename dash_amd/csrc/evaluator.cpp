@@ -40,7 +40,8 @@ namespace {
 struct ReluTabs {
     const Array *ap, *c1, *c2, *sg, *ga, *ea;
     ReluTabs(const GLayer& g, const std::string& pre)
-        : ap(&g.arr(pre + "s.approx")), c1(&g.arr(pre + "s.cast1")), c2(&g.arr(pre + "s.cast2")),
+        : ap(&g.arr(pre + "s.approx")), c1(g.a.count(pre + "s.cast1") ? &g.arr(pre + "s.cast1") : nullptr),
+          c2(&g.arr(pre + "s.cast2")),
           sg(&g.arr(pre + "s.sign")), ga(&g.arr(pre + "mm.g")), ea(&g.arr(pre + "mm.e")) {}
 };
 
@@ -50,7 +51,8 @@ void relu_eval_elem(const SignPlan& sp, const LabelBank& Z, const std::vector<in
     const int k = static_cast<int>(crt.size());
     comp_t sig[128];
     comp_t* outs[1] = {sig};
-    sign_eval_elem(sp, Z, x, T.ap->ptr<u128>() + e * T.ap->shape[1], T.c1->ptr<u128>() + e * T.c1->shape[1],
+    sign_eval_elem(sp, Z, x, T.ap->ptr<u128>() + e * T.ap->shape[1],
+                   T.c1 ? T.c1->ptr<u128>() + e * T.c1->shape[1] : nullptr,
                    T.c2->ptr<u128>() + e * T.c2->shape[1], T.sg->ptr<u128>() + e * T.sg->shape[1], outs);
     const ModInfo& m2 = mod_info(2);
     for (int j = 0; j < k; ++j)
@@ -65,6 +67,7 @@ CrtLabels cpu_evaluate(const GarbledModel& m, const CrtLabels& inputs, int nt, s
     const int k = static_cast<int>(crt.size());
     DASH_CHECK(static_cast<int>(inputs.size()) == k, "input residue count mismatch");
     const LabelBank Z = m.zero_bank();
+    const bool fused = m.h.sign_fused != 0;
     std::vector<i64> prefix(k);
     i64 sum_crt = 0;
     for (int j = 0; j < k; ++j) {
@@ -181,7 +184,7 @@ CrtLabels cpu_evaluate(const GarbledModel& m, const CrtLabels& inputs, int nt, s
                 break;
             }
             case K_RELU: {
-                SignPlan sp(crt, m.h.mrs, {2}, 0, 1);
+                SignPlan sp(crt, m.h.mrs, {2}, 0, 1, fused);
                 const ReluTabs T(g, "");
                 CrtLabels nxt;
                 for (int j = 0; j < k; ++j) nxt.emplace_back(crt[j], Nin);
@@ -200,9 +203,9 @@ CrtLabels cpu_evaluate(const GarbledModel& m, const CrtLabels& inputs, int nt, s
                 break;
             }
             case K_SIGN: {
-                SignPlan sp(crt, m.h.mrs, crt, -1, 1);
+                SignPlan sp(crt, m.h.mrs, crt, -1, 1, fused);
                 const Array& ap = g.arr("s.approx");
-                const Array& c1 = g.arr("s.cast1");
+                const Array* c1 = sp.has_cast1() ? &g.arr("s.cast1") : nullptr;
                 const Array& c2 = g.arr("s.cast2");
                 const Array& sg = g.arr("s.sign");
                 CrtLabels nxt;
@@ -215,7 +218,8 @@ CrtLabels cpu_evaluate(const GarbledModel& m, const CrtLabels& inputs, int nt, s
                             x[j] = cur[j].at(e);
                             y[j] = nxt[j].at(e);
                         }
-                        sign_eval_elem(sp, Z, x.data(), ap.ptr<u128>() + e * ap.shape[1], c1.ptr<u128>() + e * c1.shape[1],
+                        sign_eval_elem(sp, Z, x.data(), ap.ptr<u128>() + e * ap.shape[1],
+                                       c1 ? c1->ptr<u128>() + e * c1->shape[1] : nullptr,
                                        c2.ptr<u128>() + e * c2.shape[1], sg.ptr<u128>() + e * sg.shape[1], y.data());
                     }
                 }, nt);
@@ -227,11 +231,11 @@ CrtLabels cpu_evaluate(const GarbledModel& m, const CrtLabels& inputs, int nt, s
                 const i64 iters = g.param("iters");
                 std::vector<RescalePlan> plans;
                 if (mode == 0) {
-                    for (i64 i = 0; i < iters; ++i) plans.emplace_back(crt, m.h.mrs, std::vector<int>{2}, true);
+                    for (i64 i = 0; i < iters; ++i) plans.emplace_back(crt, m.h.mrs, std::vector<int>{2}, true, fused);
                 } else {
                     std::vector<int> s;
                     for (auto v : g.vec("s")) s.push_back(static_cast<int>(v));
-                    plans.emplace_back(crt, m.h.mrs, s, false);
+                    plans.emplace_back(crt, m.h.mrs, s, false, fused);
                 }
                 std::vector<const comp_t*> up(k), dn(k);
                 for (int j = 0; j < k; ++j) up[j] = get_const("up." + std::to_string(j));
@@ -244,7 +248,7 @@ CrtLabels cpu_evaluate(const GarbledModel& m, const CrtLabels& inputs, int nt, s
                     const Array* ap = nullptr, *c1 = nullptr, *c2 = nullptr, *sg = nullptr, *be = nullptr;
                     if (P.sign_be) {
                         ap = &g.arr(pre + "s.approx");
-                        c1 = &g.arr(pre + "s.cast1");
+                        c1 = P.sign.has_cast1() ? &g.arr(pre + "s.cast1") : nullptr;
                         c2 = &g.arr(pre + "s.cast2");
                         sg = &g.arr(pre + "s.sign");
                     } else {
@@ -256,7 +260,8 @@ CrtLabels cpu_evaluate(const GarbledModel& m, const CrtLabels& inputs, int nt, s
                             for (int j = 0; j < k; ++j) Lp[j] = cur[j].at(e);
                             if (P.sign_be)
                                 rescale_eval_elem(P, Z, Lp.data(), up.data(), dn.data(), tr.ptr<u128>() + e * P.n_trans,
-                                                  ap->ptr<u128>() + e * ap->shape[1], c1->ptr<u128>() + e * c1->shape[1],
+                                                  ap->ptr<u128>() + e * ap->shape[1],
+                                                  c1 ? c1->ptr<u128>() + e * c1->shape[1] : nullptr,
                                                   c2->ptr<u128>() + e * c2->shape[1], sg->ptr<u128>() + e * sg->shape[1],
                                                   nullptr);
                             else
@@ -284,7 +289,7 @@ CrtLabels cpu_evaluate(const GarbledModel& m, const CrtLabels& inputs, int nt, s
                     for (i64 i = 0; i < Nin; ++i) win[0].push_back(i);
                 }
                 MaxTree T(K);
-                SignPlan sp(crt, m.h.mrs, {2}, 0, 1);
+                SignPlan sp(crt, m.h.mrs, {2}, 0, 1, fused);
                 std::vector<Labels> vals;
                 for (int j = 0; j < k; ++j) {
                     Labels V(crt[j], Nout * K);

@@ -74,8 +74,8 @@ std::vector<std::vector<int16_t>> gen_approx_lookup(const std::vector<int>& crt,
 }
 
 SignPlan::SignPlan(const std::vector<int>& crt_, const std::vector<int>& mrs_, const std::vector<int>& out, int lo,
-                   int up)
-    : crt(crt_), mrs(mrs_), out_mod(out), lower(lo), upper(up) {
+                   int up, bool fused_)
+    : crt(crt_), mrs(mrs_), out_mod(out), lower(lo), upper(up), fused(fused_) {
     DASH_CHECK(!mrs.empty(), "sign gadget needs a non-empty MRS base");
     DASH_CHECK(mrs[0] % 2 == 0, "sign gadget needs an even most-significant MRS modulus");
     lookup = gen_approx_lookup(crt, mrs);
@@ -97,9 +97,108 @@ SignPlan::SignPlan(const std::vector<int>& crt_, const std::vector<int>& mrs_, c
     for (int o : out) max_n = std::max(max_n, nr_comps(o));
 }
 
+namespace {
+// Fused construction (SignPlan::fused, see gadgets.h). PRG draw order: the
+// k*t digit labels (residue-major, modulus digit_mod(d)), then per digit
+// d = t-1..1 the carry label (modulus carry_mod(d)), then the outputs.
+void sign_garble_fused(const SignPlan& P, const LabelBank& R, const Prg& prg, u64 stream, const comp_t* const* in0,
+                       u128* approx, u128* cast2, u128* sign, comp_t* const* out0) {
+    const int k = static_cast<int>(P.crt.size()), t = static_cast<int>(P.mrs.size());
+    const int W = P.max_n;
+    comp_t* base = sign_scratch().get(static_cast<size_t>(W) * (k * t + 3));
+    comp_t* dig = base;                                    // [k*t][W]
+    comp_t* carry = dig + static_cast<size_t>(W) * k * t;  // carry into the current digit
+    comp_t* sum = carry + W;
+    comp_t* newc = sum + W;
+    u64 ctr = 0;
+    for (int j = 0; j < k; ++j)
+        for (int d = 0; d < t; ++d) draw(prg, stream, ctr, P.digit_mod(d), dig + static_cast<size_t>(W) * (j * t + d));
+    ProjKeys& K = proj_keys_scratch();
+    for (int j = 0; j < k; ++j) {
+        const ModInfo& mi = mod_info(P.crt[j]);
+        const auto& lut = P.lookup[j];
+        proj_keys(in0[j], R.get(mi.p), mi, K);
+        for (int d = 0; d < t; ++d) {
+            const ModInfo& mo = mod_info(P.digit_mod(d));
+            garble_proj_keys(K, dig + static_cast<size_t>(W) * (j * t + d), R.get(mo.p), mo,
+                             [&](int v) { return static_cast<i64>(lut[static_cast<size_t>(v) * t + d]); },
+                             approx + t * P.crt_prefix[j] + d, t);
+        }
+    }
+    bool have_carry = false;
+    i64 c2 = 0;
+    for (int d = t - 1; d >= 1; --d) {
+        const int m = P.mrs[d], mprev = P.mrs[d - 1];
+        const ModInfo& mo = mod_info(P.digit_mod(d));
+        if (have_carry) std::memcpy(sum, carry, sizeof(comp_t) * mo.n);
+        else std::memcpy(sum, dig + static_cast<size_t>(W) * d, sizeof(comp_t) * mo.n);
+        for (int j = have_carry ? 0 : 1; j < k; ++j) lab_add(sum, dig + static_cast<size_t>(W) * (j * t + d), mo.n, mo.p);
+        const ModInfo& mn = mod_info(P.carry_mod(d));
+        draw(prg, stream, ctr, mn.p, newc);
+        garble_proj(sum, R.get(mo.p), mo, newc, R.get(mn.p), mn,
+                    [m, mprev](int v) { return static_cast<i64>((v / m) % mprev); }, cast2 + c2);
+        c2 += mo.p;
+        std::memcpy(carry, newc, sizeof(comp_t) * mn.n);
+        have_carry = true;
+    }
+    const ModInfo& m0 = mod_info(P.mrs[0]);
+    if (have_carry) std::memcpy(sum, carry, sizeof(comp_t) * m0.n);
+    else std::memcpy(sum, dig, sizeof(comp_t) * m0.n);
+    for (int j = have_carry ? 0 : 1; j < k; ++j) lab_add(sum, dig + static_cast<size_t>(W) * (j * t), m0.n, m0.p);
+    const int half = P.mrs[0] / 2;
+    for (size_t o = 0; o < P.out_mod.size(); ++o) {
+        const ModInfo& mo = mod_info(P.out_mod[o]);
+        draw(prg, stream, ctr, mo.p, out0[o]);
+        const int lo = P.lower, up = P.upper;
+        garble_proj(sum, R.get(m0.p), m0, out0[o], R.get(mo.p), mo,
+                    [half, lo, up](int v) { return static_cast<i64>(v < half ? up : lo); }, sign + o * m0.p);
+    }
+}
+
+void sign_eval_fused(const SignPlan& P, const comp_t* const* in, const u128* approx, const u128* cast2,
+                     const u128* sign, comp_t* const* out) {
+    const int k = static_cast<int>(P.crt.size()), t = static_cast<int>(P.mrs.size());
+    const int W = P.max_n;
+    comp_t* base = sign_scratch().get(static_cast<size_t>(W) * (k * t + 3));
+    comp_t* dig = base;
+    comp_t* carry = dig + static_cast<size_t>(W) * k * t;
+    comp_t* sum = carry + W;
+    comp_t* newc = sum + W;
+    for (int j = 0; j < k; ++j) {
+        const ModInfo& mi = mod_info(P.crt[j]);
+        for (int d = 0; d < t; ++d)
+            eval_proj(in[j], mi, approx + t * P.crt_prefix[j] + d, mod_info(P.digit_mod(d)),
+                      dig + static_cast<size_t>(W) * (j * t + d), t);
+    }
+    bool have_carry = false;
+    i64 c2 = 0;
+    for (int d = t - 1; d >= 1; --d) {
+        const ModInfo& mo = mod_info(P.digit_mod(d));
+        if (have_carry) std::memcpy(sum, carry, sizeof(comp_t) * mo.n);
+        else std::memcpy(sum, dig + static_cast<size_t>(W) * d, sizeof(comp_t) * mo.n);
+        for (int j = have_carry ? 0 : 1; j < k; ++j) lab_add(sum, dig + static_cast<size_t>(W) * (j * t + d), mo.n, mo.p);
+        const ModInfo& mn = mod_info(P.carry_mod(d));
+        eval_proj(sum, mo, cast2 + c2, mn, newc);
+        c2 += mo.p;
+        std::memcpy(carry, newc, sizeof(comp_t) * mn.n);
+        have_carry = true;
+    }
+    const ModInfo& m0 = mod_info(P.mrs[0]);
+    if (have_carry) std::memcpy(sum, carry, sizeof(comp_t) * m0.n);
+    else std::memcpy(sum, dig, sizeof(comp_t) * m0.n);
+    for (int j = have_carry ? 0 : 1; j < k; ++j) lab_add(sum, dig + static_cast<size_t>(W) * (j * t), m0.n, m0.p);
+    for (size_t o = 0; o < P.out_mod.size(); ++o)
+        eval_proj(sum, m0, sign + o * m0.p, mod_info(P.out_mod[o]), out[o]);
+}
+}  // namespace
+
 void sign_garble_elem(const SignPlan& P, const LabelBank& R, const LabelBank& Z, const Prg& prg, u64 stream,
                       const comp_t* const* in0, u128* approx, u128* cast1, u128* cast2, u128* sign,
                       comp_t* const* out0) {
+    if (P.fused) {
+        sign_garble_fused(P, R, prg, stream, in0, approx, cast2, sign, out0);
+        return;
+    }
     const int k = static_cast<int>(P.crt.size()), t = static_cast<int>(P.mrs.size());
     const int W = P.max_n;
     comp_t* base = sign_scratch().get(static_cast<size_t>(W) * (k * t + (k + 1) + 4));
@@ -169,6 +268,10 @@ void sign_garble_elem(const SignPlan& P, const LabelBank& R, const LabelBank& Z,
 
 void sign_eval_elem(const SignPlan& P, const LabelBank& Z, const comp_t* const* in, const u128* approx,
                     const u128* cast1, const u128* cast2, const u128* sign, comp_t* const* out) {
+    if (P.fused) {
+        sign_eval_fused(P, in, approx, cast2, sign, out);
+        return;
+    }
     const int k = static_cast<int>(P.crt.size()), t = static_cast<int>(P.mrs.size());
     const int W = P.max_n;
     comp_t* base = sign_scratch().get(static_cast<size_t>(W) * (k * t + (k + 1) + 4));
@@ -360,7 +463,7 @@ void be_eval_elem(const BEPlan& P, comp_t* const* L, const u128* tab) {
 
 // ---------------------------------------------------------------------------
 RescalePlan::RescalePlan(const std::vector<int>& crt_, const std::vector<int>& mrs, const std::vector<int>& f,
-                         bool sbe)
+                         bool sbe, bool fused_sign)
     : crt(crt_), factors(f), sign_be(sbe) {
     const int k = static_cast<int>(crt.size());
     std::vector<int> ignored;
@@ -385,7 +488,7 @@ RescalePlan::RescalePlan(const std::vector<int>& crt_, const std::vector<int>& m
     if (sign_be) {
         DASH_CHECK(factors.size() == 1 && factors[0] == 2 && crt[0] == 2,
                    "sign base extension rescale needs factors {2} and crt[0] == 2");
-        sign = SignPlan(crt, mrs, {2}, 1, 0);
+        sign = SignPlan(crt, mrs, {2}, 1, 0, fused_sign);
     } else {
         be = BEPlan(crt, factors);
         n_be = be.n_tab;

@@ -129,17 +129,39 @@ inline int16_t eval_proj_mini(const comp_t* in, const ModInfo& mi, const u128* e
 // ---------------------------------------------------------------------------
 // Approximate sign gadget (per element)
 // ---------------------------------------------------------------------------
+//
+// Two constructions of the same function (SignPlan::fused):
+//  * reference (fused = false): per digit d >= 1 every residue's approx label
+//    (mod m_d) and the carry (mod m_d) are cast to Z_{(k+1) m_d} by identity
+//    projections before the sum (sign_gadget.h:456-546): k + 1 casts per digit;
+//  * fused (fused = true): the casts are folded into the projections that
+//    produce their inputs. The approx projection of residue j writes digit d
+//    directly as a label mod (k+1) m_d (value lut[j][v][d] < m_d), and the
+//    carry projection of digit d writes (floor(s / m_d) mod m_{d-1}) directly
+//    mod (k+1) m_{d-1} (mod m_0 for the last carry). The least significant
+//    digit has no carry-in (the reference adds a cast of the zero label).
+//    Every wire carries the same value as in the reference construction, so
+//    the gadget computes the same function; it uses k (t-1) + (t-1) fewer
+//    projections per element (k = 7, t = 5: 44 -> 12 hashes and table reads
+//    on the evaluator side; the cast1 table disappears).
 struct SignPlan {
     std::vector<int> crt, mrs, out_mod;
     int lower = 0, upper = 1;
+    bool fused = false;
     std::vector<std::vector<int16_t>> lookup;  // [k][v * t + d], d = 0 is most significant
     std::vector<i64> crt_prefix;
     i64 sum_crt = 0;
-    i64 n_approx = 0, n_cast = 0, n_sign = 0;  // table entries per element
+    i64 n_approx = 0, n_cast = 0, n_sign = 0;  // table entries per element (n_cast: cast2; cast1 too unless fused)
     int max_n = 0;                             // largest label width touched
 
     SignPlan() = default;
-    SignPlan(const std::vector<int>& crt_, const std::vector<int>& mrs_, const std::vector<int>& out, int lo, int up);
+    SignPlan(const std::vector<int>& crt_, const std::vector<int>& mrs_, const std::vector<int>& out, int lo, int up,
+             bool fused = false);
+    // modulus of residue j's approx output for digit d (and of the digit-d sums)
+    int digit_mod(int d) const { return (fused && d >= 1) ? static_cast<int>(crt.size() + 1) * mrs[d] : mrs[d]; }
+    // modulus of the carry produced by digit d >= 1 (consumed by digit d - 1)
+    int carry_mod(int d) const { return fused ? ((d - 1 >= 1) ? static_cast<int>(crt.size() + 1) * mrs[d - 1] : mrs[0]) : mrs[d - 1]; }
+    bool has_cast1() const { return !fused; }
 };
 
 std::vector<std::vector<int16_t>> gen_approx_lookup(const std::vector<int>& crt, const std::vector<int>& mrs);
@@ -204,7 +226,8 @@ struct RescalePlan {
     i64 n_be = 0;
     i64 sprod = 1;
     RescalePlan() = default;
-    RescalePlan(const std::vector<int>& crt, const std::vector<int>& mrs, const std::vector<int>& factors, bool sign_be);
+    RescalePlan(const std::vector<int>& crt, const std::vector<int>& mrs, const std::vector<int>& factors, bool sign_be,
+                bool fused_sign = false);
 };
 // Garbler: L[j] base labels (mod crt[j]) in/out; up/down are the garbler-side
 // (offset-free) shift base labels.

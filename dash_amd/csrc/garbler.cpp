@@ -116,7 +116,7 @@ struct ReluTables {
 ReluTables make_relu_tables(const SignPlan& sp, i64 N, i64 sum_crt, int k) {
     ReluTables t;
     t.approx = Array(DType::u128, {N, sp.n_approx});
-    t.cast1 = Array(DType::u128, {N, std::max<i64>(sp.n_cast, 1)});
+    if (sp.has_cast1()) t.cast1 = Array(DType::u128, {N, std::max<i64>(sp.n_cast, 1)});
     t.cast2 = Array(DType::u128, {N, std::max<i64>(sp.n_cast, 1)});
     t.sign = Array(DType::u128, {N, sp.n_sign});
     t.g = Array(DType::u128, {N, sum_crt});
@@ -126,7 +126,7 @@ ReluTables make_relu_tables(const SignPlan& sp, i64 N, i64 sum_crt, int k) {
 
 void put_relu_tables(GLayer& g, const std::string& pre, ReluTables& t) {
     g.a[pre + "s.approx"] = t.approx;
-    g.a[pre + "s.cast1"] = t.cast1;
+    if (t.cast1.nbytes) g.a[pre + "s.cast1"] = t.cast1;
     g.a[pre + "s.cast2"] = t.cast2;
     g.a[pre + "s.sign"] = t.sign;
     g.a[pre + "mm.g"] = t.g;
@@ -141,7 +141,8 @@ void relu_garble_elem(const SignPlan& sp, const LabelBank& R, const LabelBank& Z
     comp_t sig[128];
     comp_t* outs[1] = {sig};
     sign_garble_elem(sp, R, Z, prg, s_stream, x0, t.approx.ptr<u128>() + e * sp.n_approx,
-                     t.cast1.ptr<u128>() + e * t.cast1.shape[1], t.cast2.ptr<u128>() + e * t.cast2.shape[1],
+                     sp.has_cast1() ? t.cast1.ptr<u128>() + e * t.cast1.shape[1] : nullptr,
+                     t.cast2.ptr<u128>() + e * t.cast2.shape[1],
                      t.sign.ptr<u128>() + e * sp.n_sign, outs);
     u64 ctr = 0;
     const ModInfo& m2 = mod_info(2);
@@ -334,6 +335,8 @@ GarbledModel Garbler::garble(const std::vector<LayerSpec>& layers, const std::ve
     const int need = required_max_modulus(crt_, mrs_, layers);
     max_mod_ = std::max(max_mod_, need);
     GarbledModel m;
+    const bool fused = opt.fused_sign;
+    m.h.sign_fused = fused ? 1 : 0;
     m.h.crt = crt_;
     m.h.mrs = mrs_;
     m.h.in_dims = in_dims;
@@ -592,7 +595,7 @@ GarbledModel Garbler::garble(const std::vector<LayerSpec>& layers, const std::ve
             }
             case K_RELU: {
                 DASH_CHECK(is_crt(), "relu needs CRT-base labels");
-                SignPlan sp(crt_, mrs_, {2}, 0, 1);
+                SignPlan sp(crt_, mrs_, {2}, 0, 1, fused);
                 ReluTables t = make_relu_tables(sp, Nin, sum_crt, k);
                 CrtLabels nxt;
                 if (gpu) {
@@ -619,9 +622,10 @@ GarbledModel Garbler::garble(const std::vector<LayerSpec>& layers, const std::ve
             }
             case K_SIGN: {
                 DASH_CHECK(is_crt(), "sign needs CRT-base labels");
-                SignPlan sp(crt_, mrs_, crt_, -1, 1);
-                Array ap(DType::u128, {Nin, sp.n_approx}), c1(DType::u128, {Nin, std::max<i64>(sp.n_cast, 1)}),
-                    c2(DType::u128, {Nin, std::max<i64>(sp.n_cast, 1)}), sg(DType::u128, {Nin, sp.n_sign});
+                SignPlan sp(crt_, mrs_, crt_, -1, 1, fused);
+                Array ap(DType::u128, {Nin, sp.n_approx}), c1, c2(DType::u128, {Nin, std::max<i64>(sp.n_cast, 1)}),
+                    sg(DType::u128, {Nin, sp.n_sign});
+                if (sp.has_cast1()) c1 = Array(DType::u128, {Nin, std::max<i64>(sp.n_cast, 1)});
                 CrtLabels nxt;
                 if (gpu) {
                     gpu->sign_layer(L, sp, cur, ap, c1, c2, sg, nullptr, nullptr, nullptr, nullptr);
@@ -637,12 +641,13 @@ GarbledModel Garbler::garble(const std::vector<LayerSpec>& layers, const std::ve
                             y[j] = nxt[j].at(e);
                         }
                         sign_garble_elem(sp, R_, Z_, prg_, stream_id(L, 1, e), x.data(),
-                                         ap.ptr<u128>() + e * sp.n_approx, c1.ptr<u128>() + e * c1.shape[1],
+                                         ap.ptr<u128>() + e * sp.n_approx,
+                                         sp.has_cast1() ? c1.ptr<u128>() + e * c1.shape[1] : nullptr,
                                          c2.ptr<u128>() + e * c2.shape[1], sg.ptr<u128>() + e * sp.n_sign, y.data());
                     }
                 }, nt);
                 g.a["s.approx"] = ap;
-                g.a["s.cast1"] = c1;
+                if (sp.has_cast1()) g.a["s.cast1"] = c1;
                 g.a["s.cast2"] = c2;
                 g.a["s.sign"] = sg;
                 if (!gpu) cur = std::move(nxt);
@@ -655,11 +660,11 @@ GarbledModel Garbler::garble(const std::vector<LayerSpec>& layers, const std::ve
                 if (mode == 0) {
                     const i64 l = param1(spec.p, "l");
                     DASH_CHECK(l >= 1, "legacy rescale needs l >= 1");
-                    for (i64 i = 0; i < l; ++i) plans.emplace_back(crt_, mrs_, std::vector<int>{2}, true);
+                    for (i64 i = 0; i < l; ++i) plans.emplace_back(crt_, mrs_, std::vector<int>{2}, true, fused);
                 } else {
                     std::vector<int> s;
                     for (auto v : paramv(spec.p, "s")) s.push_back(static_cast<int>(v));
-                    plans.emplace_back(crt_, mrs_, s, false);
+                    plans.emplace_back(crt_, mrs_, s, false, fused);
                 }
                 get_up();
                 std::vector<const comp_t*> upp(k);
@@ -674,7 +679,7 @@ GarbledModel Garbler::garble(const std::vector<LayerSpec>& layers, const std::ve
                     Array ap, c1, c2, sg, be;
                     if (P.sign_be) {
                         ap = Array(DType::u128, {Nin, P.sign.n_approx});
-                        c1 = Array(DType::u128, {Nin, std::max<i64>(P.sign.n_cast, 1)});
+                        if (P.sign.has_cast1()) c1 = Array(DType::u128, {Nin, std::max<i64>(P.sign.n_cast, 1)});
                         c2 = Array(DType::u128, {Nin, std::max<i64>(P.sign.n_cast, 1)});
                         sg = Array(DType::u128, {Nin, P.sign.n_sign});
                     } else {
@@ -690,7 +695,8 @@ GarbledModel Garbler::garble(const std::vector<LayerSpec>& layers, const std::ve
                             if (P.sign_be) {
                                 rescale_garble_elem(P, R_, Z_, prg_, stream_id(L, 10 + it, e), Lp.data(), upp.data(),
                                                     dnp.data(), tr.ptr<u128>() + e * P.n_trans,
-                                                    ap.ptr<u128>() + e * ap.shape[1], c1.ptr<u128>() + e * c1.shape[1],
+                                                    ap.ptr<u128>() + e * ap.shape[1],
+                                                    P.sign.has_cast1() ? c1.ptr<u128>() + e * c1.shape[1] : nullptr,
                                                     c2.ptr<u128>() + e * c2.shape[1], sg.ptr<u128>() + e * sg.shape[1],
                                                     nullptr);
                             } else {
@@ -703,7 +709,7 @@ GarbledModel Garbler::garble(const std::vector<LayerSpec>& layers, const std::ve
                     g.a[pre + "trans"] = tr;
                     if (P.sign_be) {
                         g.a[pre + "s.approx"] = ap;
-                        g.a[pre + "s.cast1"] = c1;
+                        if (P.sign.has_cast1()) g.a[pre + "s.cast1"] = c1;
                         g.a[pre + "s.cast2"] = c2;
                         g.a[pre + "s.sign"] = sg;
                     } else {
@@ -735,7 +741,7 @@ GarbledModel Garbler::garble(const std::vector<LayerSpec>& layers, const std::ve
                     dims = {1};
                 }
                 MaxTree T(K);
-                SignPlan sp(crt_, mrs_, {2}, 0, 1);
+                SignPlan sp(crt_, mrs_, {2}, 0, 1, fused);
                 // value slots: vals[j] holds Nout x cnt labels (slot-major per output)
                 std::vector<Labels> vals;
                 for (int j = 0; j < k; ++j) {

@@ -42,7 +42,7 @@ constexpr int kW = 128;  // label slot width (max components)
 // label reference kinds
 enum Src : int { S_INPUT = 0, S_SLOT = 1, S_ZERO = 2 };
 // projection functions
-enum Fn : int { F_IDENT = 0, F_LUT = 1, F_DIV = 2, F_SIGN = 3, F_MULR = 4, F_NEGR = 5 };
+enum Fn : int { F_IDENT = 0, F_LUT = 1, F_DIV = 2, F_SIGN = 3, F_MULR = 4, F_NEGR = 5, F_DIVMOD = 6 };
 // output offset kinds
 enum OutR : int { R_BANK = 0, R_INPUT = 1 };
 
@@ -193,7 +193,9 @@ __device__ __forceinline__ const int16_t* label_ref(const Ctx& c, const Gadget& 
 struct SignSlots {
     int k, t;
     int mrs[kMaxMrs];
-    int sum2_slot0, sum_slot, bases_slot0, newc_slot0, mrs_slot0, stride_q;  // stride_q = k + 2
+    int sum2_slot0, sum_slot, bases_slot0, newc_slot0, mrs_slot0, stride_q;  // stride_q = k + 2 (fused: 1)
+    int fused;              // SignPlan::fused: digit sums read the approx outputs + the previous carry directly
+    int dmod[kMaxMrs];      // fused: modulus of digit d's labels (SignPlan::digit_mod)
 };
 
 // One thread per element; slot rows are kW-aligned (256 B), so components
@@ -225,6 +227,23 @@ __global__ __launch_bounds__(256) void k_sign_derive(Ctx c, Gadget g, SignSlots 
     if (e >= g.N) return;
     int16_t* S = g.S + e * g.nslots * kW;
     const int k = s.k, t = s.t;
+    if (s.fused) {
+        // digit q (d = t-1-q): sum_j approx[j][d] (+ carry of the previous digit, none for q = 0);
+        // MSD: sum_j approx[j][0] + last carry (none when t = 1)
+        for (int q = 0; q <= t - 1; ++q) {
+            const int d = t - 1 - q;
+            const ModC Mo = c.mc[s.dmod[d]];
+            const int n = static_cast<int>(Mo.n);
+            int16_t* dst = S + (d == 0 ? s.sum_slot : s.sum2_slot0 + q) * kW;
+            for (int i0 = 0; i0 < n; i0 += 8) {
+                uint32_t acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+                if (q > 0) add8(acc, ld8a(S + (s.newc_slot0 + q - 1) * kW + i0));
+                for (int j = 0; j < k; ++j) add8(acc, ld8a(S + (s.mrs_slot0 + j * t + d) * kW + i0));
+                st8a(dst + i0, acc, Mo, n - i0);
+            }
+        }
+        return;
+    }
     for (int q = 0; q + 1 < t; ++q) {
         const int d = t - 1 - q;
         const int mo = (k + 1) * s.mrs[d];
@@ -418,6 +437,7 @@ __global__ __launch_bounds__(kPB) void k_project(Ctx c, Gadget g, In in, Tables 
         int64_t f;
         switch (P.fn) {
             case F_DIV: f = i / P.a0; break;
+            case F_DIVMOD: f = (i / P.a0) % P.a1; break;
             case F_SIGN: f = i < P.a0 ? P.a2 : P.a1; break;  // a0 = half, a1 = lower, a2 = upper
             case F_MULR: {
                 const int16_t* x = label_ref(c, g, in, e, S_INPUT, P.a0, 0);
@@ -658,14 +678,76 @@ __global__ __launch_bounds__(256) void k_gather_slots(Gadget g, GatherArgs a) {
 struct SignLayout {
     std::vector<Draw> draws;
     std::vector<Proj> projs;
+    int fan[kMaxMrs] = {};  // output modulus of the approx fan-out per digit
     SignSlots ss{};
     int nslots = 0;
     int out_slot0 = 0;
     int64_t entries = 0;
 };
 
+// Fused construction (gadgets.cpp sign_garble_fused): digit labels, carries, outputs.
+SignLayout sign_layout_fused(const SignPlan& P, int extra_slots) {
+    SignLayout L;
+    const int k = static_cast<int>(P.crt.size()), t = static_cast<int>(P.mrs.size());
+    int slot = 0, ctr = 0;
+    auto draw = [&](int q) {
+        L.draws.push_back({slot, q, ctr});
+        ctr += (nr_comps(q) + 1) / 2;
+        return slot++;
+    };
+    const int dig0 = slot;
+    for (int j = 0; j < k; ++j)
+        for (int d = 0; d < t; ++d) draw(P.digit_mod(d));
+    const int newc0 = slot;
+    for (int q = 0; q + 1 < t; ++q) draw(P.carry_mod(t - 1 - q));
+    L.out_slot0 = slot;
+    for (int o : P.out_mod) draw(o);
+    const int sum2_0 = slot;
+    slot += std::max(0, t - 1);
+    const int sum_slot = slot++;
+    L.nslots = slot + extra_slots;
+    L.ss.k = k;
+    L.ss.t = t;
+    L.ss.fused = 1;
+    for (int d = 0; d < t; ++d) {
+        L.ss.mrs[d] = P.mrs[d];
+        L.ss.dmod[d] = P.digit_mod(d);
+        L.fan[d] = P.digit_mod(d);
+    }
+    L.ss.sum2_slot0 = sum2_0;
+    L.ss.sum_slot = sum_slot;
+    L.ss.bases_slot0 = 0;
+    L.ss.newc_slot0 = newc0;
+    L.ss.mrs_slot0 = dig0;
+    L.ss.stride_q = 1;
+    int64_t first = 0;
+    auto add = [&](Proj p) {
+        p.first = first;
+        first += p.pin;
+        L.projs.push_back(p);
+    };
+    for (int j = 0; j < k; ++j)
+        add(Proj{S_INPUT, j, P.crt[j], dig0 + j * t, P.mrs[0], F_LUT, j, 0, t, R_BANK, 0, 0, t,
+                 t * P.crt_prefix[j], 0});
+    int64_t c2 = 0;
+    for (int q = 0; q + 1 < t; ++q) {
+        const int d = t - 1 - q;
+        const int mo = P.digit_mod(d);
+        add(Proj{S_SLOT, sum2_0 + q, mo, newc0 + q, P.carry_mod(d), F_DIVMOD, P.mrs[d], P.mrs[d - 1], 0, R_BANK, 0,
+                 2, 1, c2, 0});
+        c2 += mo;
+    }
+    const int m0 = P.mrs[0];
+    for (size_t o = 0; o < P.out_mod.size(); ++o)
+        add(Proj{S_SLOT, sum_slot, m0, L.out_slot0 + static_cast<int>(o), P.out_mod[o], F_SIGN, m0 / 2, P.lower,
+                 P.upper, R_BANK, 0, 3, 1, static_cast<int64_t>(o) * m0, 0});
+    L.entries = first;
+    return L;
+}
+
 // Mirrors sign_garble_elem: draw order = PRG counter order.
 SignLayout sign_layout(const SignPlan& P, int extra_slots) {
+    if (P.fused) return sign_layout_fused(P, extra_slots);
     SignLayout L;
     const int k = static_cast<int>(P.crt.size()), t = static_cast<int>(P.mrs.size());
     int slot = 0, ctr = 0;
@@ -693,7 +775,11 @@ SignLayout sign_layout(const SignPlan& P, int extra_slots) {
     L.nslots = slot + extra_slots;
     L.ss.k = k;
     L.ss.t = t;
-    for (int d = 0; d < t; ++d) L.ss.mrs[d] = P.mrs[d];
+    for (int d = 0; d < t; ++d) {
+        L.ss.mrs[d] = P.mrs[d];
+        L.ss.dmod[d] = P.mrs[d];
+        L.fan[d] = P.mrs[d];
+    }
     L.ss.sum2_slot0 = sum2_0;
     L.ss.sum_slot = sum_slot;
     L.ss.bases_slot0 = bases0;
@@ -962,7 +1048,7 @@ void run_sign(const gg::Ctx& c, const gg::SignLayout& L, gg::Gadget& g, const gg
     g.nprojs = static_cast<int>(L.projs.size());
     g.entries = L.entries;
     g.nblk = draw_blocks(L.draws);
-    for (int d = 0; d < L.ss.t; ++d) g.mrs[d] = L.ss.mrs[d];
+    for (int d = 0; d < L.ss.t; ++d) g.mrs[d] = L.fan[d];
     check_desc(g);
     hipLaunchKernelGGL(gg::k_draw, dim3(blocks_for(g.N * g.nblk, gg::kGB, 8192)), dim3(gg::kGB), 0, nullptr, c, g);
     hipLaunchKernelGGL(gg::k_sign_derive, dim3(blocks_for(g.N, 256)), dim3(256), 0, nullptr, c, g, L.ss);
@@ -1187,7 +1273,7 @@ void GpuGarbler::sign_layer(uint64_t layer, const SignPlan& sp, CrtLabels& cur, 
     int16_t* S = I.scratch(static_cast<size_t>(N) * L.nslots * gg::kW * sizeof(int16_t));
     DevTable tA, t1, t2, tS, tG, tE;
     tA.alloc(I.device, N, ap.shape[1]);
-    t1.alloc(I.device, N, c1.shape[1]);
+    if (sp.has_cast1()) t1.alloc(I.device, N, c1.shape[1]);
     t2.alloc(I.device, N, c2.shape[1]);
     tS.alloc(I.device, N, sg.shape[1]);
     gg::Tables tb{};
@@ -1281,7 +1367,7 @@ void GpuGarbler::sign_layer(uint64_t layer, const SignPlan& sp, CrtLabels& cur, 
     gg::end_layer(tmp);
     tr_.mark("kernels");
     tA.to_array(ap, I.device);
-    t1.to_array(c1, I.device);
+    if (sp.has_cast1()) t1.to_array(c1, I.device);
     t2.to_array(c2, I.device);
     tS.to_array(sg, I.device);
     I.cur = std::move(out);
@@ -1321,7 +1407,7 @@ void GpuGarbler::rescale_legacy_iter(uint64_t layer, int it, const RescalePlan& 
     DevTable tT, tA, t1, t2, tS;
     tT.alloc(I.device, N, tr.shape[1]);
     tA.alloc(I.device, N, ap.shape[1]);
-    t1.alloc(I.device, N, c1.shape[1]);
+    if (P.sign.has_cast1()) t1.alloc(I.device, N, c1.shape[1]);
     t2.alloc(I.device, N, c2.shape[1]);
     tS.alloc(I.device, N, sg.shape[1]);
     gg::Tables tb{};
@@ -1362,7 +1448,7 @@ void GpuGarbler::rescale_legacy_iter(uint64_t layer, int it, const RescalePlan& 
     tr_.mark("kernels");
     tT.to_array(tr, I.device);
     tA.to_array(ap, I.device);
-    t1.to_array(c1, I.device);
+    if (P.sign.has_cast1()) t1.to_array(c1, I.device);
     t2.to_array(c2, I.device);
     tS.to_array(sg, I.device);
     set_stale(cur, I.cur_mod, N);

@@ -51,6 +51,7 @@ struct SignArgs {
     int relu;            // also produce hs / cs for the ReLU multiply
     int16_t* csum;       // [B][t][kCsumComps][N] per-digit sums of the k cast labels (phase B1)
     int64_t c1off[kMaxMrs];  // offset of digit d's block ((k+1) m_d entries) in a cast1 row
+    int fused;           // SignPlan::fused: approx outputs are already cast, carries come out cast (no cast1)
 };
 constexpr int kCsumComps = 64;
 

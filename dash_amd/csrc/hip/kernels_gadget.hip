@@ -69,8 +69,16 @@ __device__ __forceinline__ void approx_casts_out(const AesCtx& aes, const SignAr
                                                  int64_t e, const u128 (&P)[TM], const u128* TA, uint32_t col, u128 H) {
     const int64_t N = a.N;
     const int t = a.t;
-    const u128* T1 = a.cast1 + (static_cast<int64_t>(b) * N + e) * a.n_cast;
     u128* out = a.mrsP + (static_cast<int64_t>(b) * a.crt.k + j) * t * N + e;
+    if (a.fused) {
+        // fused construction: the approx row already holds every digit in its summation modulus
+#pragma unroll
+        for (int d = 0; d < TM; ++d)
+            if (d < t) out[static_cast<int64_t>(d) * N] = P[d];
+        for (int d = TM; d < t; ++d) out[static_cast<int64_t>(d) * N] = TA[col * t + d] - H;
+        return;
+    }
+    const u128* T1 = a.cast1 + (static_cast<int64_t>(b) * N + e) * a.n_cast;
     out[0] = P[0];
     u128 tt[TM];
 #pragma unroll
@@ -235,6 +243,88 @@ __global__ __launch_bounds__(kAesBlock, kAesMinBlocks) void k_sign_chain(SignArg
             if (i < static_cast<int>(M0.n)) {
                 uint32_t v = static_cast<uint32_t>(S[i * N]) + sc.next(M0);
                 if (v >= static_cast<uint32_t>(m0)) v -= m0;
+                if (i == 0) col = v;
+                cf.push(v, M0);
+            }
+        const u128 key = cf.finish();
+        const u128* TS = a.sign + (static_cast<int64_t>(b) * N + e) * a.n_sign;
+        const u128 TS0 = TS[col];
+        const u128 H = aes_encrypt(aes, key);
+        for (int o = 0; o < a.nout; ++o) {
+            const u128 P = (o == 0 ? TS0 : TS[o * m0 + col]) - H;
+            a.outP[(static_cast<int64_t>(b) * a.nout + o) * N + e] = P;
+            if (a.relu && o == 0) {
+                a.hs[static_cast<int64_t>(b) * N + e] = aes_encrypt(aes, P);
+                a.cs[static_cast<int64_t>(b) * N + e] = static_cast<uint8_t>(static_cast<uint32_t>(P) & 1u);
+            }
+        }
+    }
+}
+
+// Phase B2 of the fused construction (SignPlan::fused): the carry leaves each
+// carry projection already in the next digit's summation modulus, so a digit
+// costs ONE dependent gather + ONE AES on the critical path (the reference
+// construction: two of each). The least significant digit has no carry-in.
+// grid (x, 1, B)
+template <int MAXN>
+__global__ __launch_bounds__(kAesBlock, kAesMinBlocks) void k_sign_chain_fused(SignArgs a, const ModC* mc,
+                                                                               const uint32_t* te0, const uint32_t* rk) {
+    AES_PROLOGUE(te0, rk);
+    const int b = blockIdx.z;
+    const int64_t N = a.N;
+    const int k = a.crt.k, t = a.t;
+    for (int64_t e = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; e < N;
+         e += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+        const u128* T2 = a.cast2 + (static_cast<int64_t>(b) * N + e) * a.n_cast;
+        const int16_t* S = a.csum + static_cast<int64_t>(b) * t * kCsumComps * N + e;
+        u128 carry = 0;
+        int64_t c2 = 0;
+        int32_t acc[MAXN];
+        for (int d = t - 1; d >= 1; --d) {
+            const int mo = (k + 1) * a.mrs[d];
+            const ModC Mo = mc[mo];
+            const int16_t* Sd = S + static_cast<int64_t>(d) * kCsumComps * N;
+#pragma unroll
+            for (int i = 0; i < MAXN; ++i)
+                if (i < static_cast<int>(Mo.n)) acc[i] = Sd[i * N];
+            const bool have = d < t - 1;
+            DigitStream sa;
+            sa.init(carry);
+            CompressFwd cf;
+            cf.init();
+            uint32_t col2 = 0;
+#pragma unroll
+            for (int i = 0; i < MAXN; ++i)
+                if (i < static_cast<int>(Mo.n)) {
+                    uint32_t v = static_cast<uint32_t>(acc[i]);
+                    if (have) {
+                        v += sa.next(Mo);
+                        if (v >= static_cast<uint32_t>(mo)) v -= mo;
+                    }
+                    if (i == 0) col2 = v;
+                    cf.push(v, Mo);
+                }
+            const u128 key2 = cf.finish();
+            const u128 T2e = T2[c2 + col2];
+            carry = T2e - aes_encrypt(aes, key2);
+            c2 += mo;
+        }
+        const int m0 = a.mrs[0];
+        const ModC M0 = mc[m0];
+        const bool have = t >= 2;
+        DigitStream sc;
+        sc.init(carry);
+        CompressFwd cf;
+        cf.init();
+        uint32_t col = 0;
+#pragma unroll
+        for (int i = 0; i < MAXN; ++i)
+            if (i < static_cast<int>(M0.n)) {
+                uint32_t v = static_cast<uint32_t>(S[i * N]);
+                if (have) {
+                    v += sc.next(M0);
+                    if (v >= static_cast<uint32_t>(m0)) v -= m0;
+                }
                 if (i == 0) col = v;
                 cf.push(v, M0);
             }
@@ -708,13 +798,22 @@ void launch_sign_chain(const SignArgs& a, int maxn, const ModC* mc, const AesGlo
     // MiniONN B=24: the chain is latency bound and the castsum's t-fold lane parallelism wins)
     if (maxn <= 24) {  // k = 7 DASH configs (cast outputs mod 8 m_d: <= 22 components)
         hipLaunchKernelGGL(k_sign_castsum<24>, gs, dim3(256), 0, st, a, mc);
-        hipLaunchKernelGGL(k_sign_chain<24>, gr, dim3(kAesBlock), kAesLds, st, a, mc, g.te0, g.rk);
+        if (a.fused)
+            hipLaunchKernelGGL(k_sign_chain_fused<24>, gr, dim3(kAesBlock), kAesLds, st, a, mc, g.te0, g.rk);
+        else
+            hipLaunchKernelGGL(k_sign_chain<24>, gr, dim3(kAesBlock), kAesLds, st, a, mc, g.te0, g.rk);
     } else if (maxn <= 32) {
         hipLaunchKernelGGL(k_sign_castsum<32>, gs, dim3(256), 0, st, a, mc);
-        hipLaunchKernelGGL(k_sign_chain<32>, gr, dim3(kAesBlock), kAesLds, st, a, mc, g.te0, g.rk);
+        if (a.fused)
+            hipLaunchKernelGGL(k_sign_chain_fused<32>, gr, dim3(kAesBlock), kAesLds, st, a, mc, g.te0, g.rk);
+        else
+            hipLaunchKernelGGL(k_sign_chain<32>, gr, dim3(kAesBlock), kAesLds, st, a, mc, g.te0, g.rk);
     } else {
         hipLaunchKernelGGL(k_sign_castsum<64>, gs, dim3(256), 0, st, a, mc);
-        hipLaunchKernelGGL(k_sign_chain<64>, gr, dim3(kAesBlock), kAesLds, st, a, mc, g.te0, g.rk);
+        if (a.fused)
+            hipLaunchKernelGGL(k_sign_chain_fused<64>, gr, dim3(kAesBlock), kAesLds, st, a, mc, g.te0, g.rk);
+        else
+            hipLaunchKernelGGL(k_sign_chain<64>, gr, dim3(kAesBlock), kAesLds, st, a, mc, g.te0, g.rk);
     }
 }
 void launch_unpack(const u128* P, int nres, const Act& out, const CrtInfo& mods, const ModC* mc, int64_t N, int B,

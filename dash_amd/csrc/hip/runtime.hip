@@ -308,10 +308,11 @@ class HipEvaluator {
         a.N = N;
         a.B = B_;
         a.n_approx = sp.n_approx;
-        a.n_cast = tmpl_->layers[li].arr(pre + "s.cast1").shape[1];
+        a.fused = sp.fused ? 1 : 0;
+        a.n_cast = tmpl_->layers[li].arr(pre + "s.cast2").shape[1];
         a.n_sign = sp.n_sign;
         a.approx = upload_tables(li, pre + "s.approx");
-        a.cast1 = upload_tables(li, pre + "s.cast1");
+        a.cast1 = sp.has_cast1() ? upload_tables(li, pre + "s.cast1") : nullptr;
         a.cast2 = upload_tables(li, pre + "s.cast2");
         a.sign = upload_tables(li, pre + "s.sign");
         a.mrsP = mrsP_;
@@ -332,7 +333,7 @@ class HipEvaluator {
                 c1 += static_cast<int64_t>(k_ + 1) * a.mrs[d];
             }
             // a one-digit MRS base (t = 1) has no casts: the garbler stores a 1-entry placeholder row
-            DASH_CHECK(c1 == a.n_cast || (c1 == 0 && a.n_cast <= 1), "cast1 row size does not match the MRS base");
+            DASH_CHECK(c1 == a.n_cast || (c1 == 0 && a.n_cast <= 1), "cast row size does not match the MRS base");
         }
         int maxn = 0;
         const int k = k_;
@@ -672,7 +673,7 @@ void HipEvaluator::build() {
                 break;
             }
             case K_RELU: {
-                SignPlan sp(crt_, m0.h.mrs, {2}, 0, 1);
+                SignPlan sp(crt_, m0.h.mrs, {2}, 0, 1, m0.h.sign_fused != 0);
                 SignArgs a = make_sign(li, "", sp, N, 1);
                 const u128* gt = upload_tables(li, "mm.g");
                 const u128* et = upload_tables(li, "mm.e");
@@ -687,7 +688,7 @@ void HipEvaluator::build() {
                 break;
             }
             case K_SIGN: {
-                SignPlan sp(crt_, m0.h.mrs, crt_, -1, 1);
+                SignPlan sp(crt_, m0.h.mrs, crt_, -1, 1, m0.h.sign_fused != 0);
                 SignArgs a = make_sign(li, "", sp, N, 0);
                 Act x = act_of(cur), y = act_of(nxt);
                 const ModC* mc = mc_;
@@ -715,7 +716,7 @@ void HipEvaluator::build() {
                         factors = {2};
                     else
                         for (auto v : g.vec("s")) factors.push_back(static_cast<int>(v));
-                    RescalePlan P(crt_, m0.h.mrs, factors, mode == 0);
+                    RescalePlan P(crt_, m0.h.mrs, factors, mode == 0, m0.h.sign_fused != 0);
                     const std::string pre = arr_name("it", static_cast<int>(it), ".");
                     const u128* trans = upload_tables(li, pre + "trans");
                     Act x = act_of(cur);
@@ -823,7 +824,7 @@ void HipEvaluator::build() {
                 }
                 const int64_t* didx = upload(idx.data(), idx.size());
                 MaxTree T(K);
-                SignPlan sp(crt_, m0.h.mrs, {2}, 0, 1);
+                SignPlan sp(crt_, m0.h.mrs, {2}, 0, 1, m0.h.sign_fused != 0);
                 // buffers: vals in 2/3 ping-pong, diff in nxt-other... use bufs 2,3 for vals; relu out in buf nxt
                 int va = 2, vb = 3;
                 Act xin = act_of(cur), v0 = act_of(va);
@@ -1032,7 +1033,7 @@ void HipEvaluator::plan_rescale_legacy(size_t li, i64 iters, i64 N, const CrtInf
     }
     const int16_t* down = upload_const_rows([&](int j) { return "down.2." + std::to_string(j); });
     for (i64 it = 0; it < iters; ++it) {
-        RescalePlan P(crt_, m0.h.mrs, {2}, true);
+        RescalePlan P(crt_, m0.h.mrs, {2}, true, m0.h.sign_fused != 0);
         const std::string pre = arr_name("it", static_cast<int>(it), ".");
         const u128* trans = upload_tables(li, pre + "trans");
         SignArgs sa = make_sign(li, pre, P.sign, N, 0);

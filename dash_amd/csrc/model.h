@@ -63,7 +63,8 @@ struct GLayer {
 };
 
 struct ModelHeader {
-    int version = 2;  // 2: approx tables interleaved [color][digit]
+    int version = 3;  // 2: approx tables interleaved [color][digit]; 3: + sign construction flag
+    int sign_fused = 0;  // 1: sign gadgets use the fused-cast construction (SignPlan::fused)
     std::vector<int> crt, mrs;
     std::vector<i64> in_dims, out_dims;
     std::vector<int> out_moduli;  // moduli of the output residues
@@ -99,6 +100,7 @@ struct Decoder {
 struct GarbleOptions {
     int nthreads = 0;
     int device = -1;  // >= 0: garble ReLU / Sign / legacy rescale layers on this GPU
+    bool fused_sign = true;  // sign gadget construction (gadgets.h SignPlan::fused); false: reference casts
 };
 
 class Garbler {

@@ -87,7 +87,8 @@ struct Rd {
 std::string GarbledModel::serialize() const {
     W w;
     w.raw(kModelMagic, 8);
-    w.u32(static_cast<uint32_t>(h.version));
+    w.u32(3u);
+    w.u32(static_cast<uint32_t>(h.sign_fused));
     w.ivec32(h.crt);
     w.ivec32(h.mrs);
     w.ivec(h.in_dims);
@@ -123,7 +124,10 @@ GarbledModel GarbledModel::deserialize(const std::string& blob) {
     DASH_CHECK(std::memcmp(mg, kModelMagic, 8) == 0, "not a garbled model blob");
     GarbledModel m;
     m.h.version = static_cast<int>(r.u32());
-    DASH_CHECK(m.h.version == 2, "unsupported garbled model version (expected 2)");
+    DASH_CHECK(m.h.version == 2 || m.h.version == 3, "unsupported garbled model version (expected 2 or 3)");
+    m.h.sign_fused = m.h.version >= 3 ? static_cast<int>(r.u32()) : 0;
+    DASH_CHECK(m.h.sign_fused == 0 || m.h.sign_fused == 1, "bad sign construction flag");
+    m.h.version = 3;
     m.h.crt = r.ivec32();
     m.h.mrs = r.ivec32();
     m.h.in_dims = r.ivec();

@@ -29,7 +29,10 @@ Labels = list  # list[(modulus, np.ndarray int16 [N, n_p])]
 class GarbledCircuit:
     def __init__(self, circuit: Circuit, crt: Union[int, Sequence[int]], mrs: Union[None, float, Sequence[int]] = None,
                  max_modulus: int = 0, seed: Optional[bytes] = None, garble_me: bool = True, nthreads: int = 0,
-                 device: Optional[int] = None):
+                 device: Optional[int] = None, fused_sign: bool = True):
+        """fused_sign: sign-gadget construction. True (default): the MRS casts are folded into the approx and
+        carry projections (same function, 3.7x fewer gates per sign; gadgets.h SignPlan::fused). False: the
+        reference construction with explicit identity casts (sign_gadget.h:456-546)."""
         self.circuit = circuit
         self.crt_base = first_primes(crt) if isinstance(crt, int) else [int(p) for p in crt]
         if mrs is None:
@@ -43,6 +46,7 @@ class GarbledCircuit:
         self.nthreads = nthreads
         # device: garble the ReLU / Sign / legacy-rescale layers on this GPU (bit-identical to the CPU garbler)
         self.device = -1 if device is None else int(device)
+        self.fused_sign = bool(fused_sign)
         self._n = native()
         self.garbler = self._n.Garbler(self.crt_base, self.mrs_base, self.seed, int(max_modulus))
         self.model = None
@@ -55,7 +59,8 @@ class GarbledCircuit:
     def garble(self):
         specs = self.circuit.garble_specs()
         t = time.perf_counter()
-        self.model = self.garbler.garble(specs, list(self.circuit.input_dims), self.nthreads, self.device)
+        self.model = self.garbler.garble(specs, list(self.circuit.input_dims), self.nthreads, self.device,
+                                         self.fused_sign)
         self.garbling_time_s = time.perf_counter() - t
         self.decoder = self.garbler.decoder()
         return self.model

@@ -12,8 +12,9 @@ from dash_amd.garbling import GarbledCircuit
 SEED = bytes(range(16))
 
 
-def run(circuit, crt, mrs, x, seed=SEED, threads=0):
-    gc = GarbledCircuit(circuit, crt, mrs, seed=seed, nthreads=threads)
+def run(circuit, crt, mrs, x, seed=SEED, threads=0, fused=True):
+    gc = GarbledCircuit(circuit, crt, mrs, seed=seed, nthreads=threads, fused_sign=fused)
+    assert gc.model.sign_fused == fused
     return gc.decode_outputs(gc.cpu_evaluate(gc.garble_inputs(x))), gc
 
 
@@ -107,26 +108,33 @@ SIGN_PARAMS = [
 ]
 
 
+# both sign constructions: fused casts (default) and the reference's explicit casts
+FUSED = pytest.mark.parametrize("fused", [True, False], ids=["fused", "refcasts"])
+
+
+@FUSED
 @pytest.mark.parametrize("crt,mrs,vals", SIGN_PARAMS)
-def test_sign(crt, mrs, vals):
-    out, _ = run(d.Circuit([d.Sign((len(vals),))]), crt, mrs, vals)
+def test_sign(crt, mrs, vals, fused):
+    out, _ = run(d.Circuit([d.Sign((len(vals),))]), crt, mrs, vals, fused=fused)
     np.testing.assert_array_equal(out, np.where(np.array(vals) >= 0, 1, -1))
 
 
+@FUSED
 @pytest.mark.parametrize("crt,mrs,vals", SIGN_PARAMS)
-def test_relu(crt, mrs, vals):
-    out, _ = run(d.Circuit([d.Relu((len(vals),))]), crt, mrs, vals)
+def test_relu(crt, mrs, vals, fused):
+    out, _ = run(d.Circuit([d.Relu((len(vals),))]), crt, mrs, vals, fused=fused)
     np.testing.assert_array_equal(out, np.maximum(vals, 0))
 
 
 @pytest.mark.parametrize("k,acc", [(4, 100.0), (5, 100.0), (6, 100.0), (7, 100.0), (8, 100.0), (9, 100.0), (7, 99.99)])
-def test_relu_mrs_table(k, acc):
+@FUSED
+def test_relu_mrs_table(k, acc, fused):
     from dash_amd.ir.bases import crt_modulus, first_primes
 
     M = crt_modulus(first_primes(k))
     rng = np.random.default_rng(k)
     vals = rng.integers(-M // 2, M // 2, 40)
-    out, _ = run(d.Circuit([d.Relu((40,))]), k, acc, vals)
+    out, _ = run(d.Circuit([d.Relu((40,))]), k, acc, vals, fused=fused)
     if acc == 100.0:
         np.testing.assert_array_equal(out, np.maximum(vals, 0))
     else:  # approximate: wrong only very close to 0 / M/2
@@ -137,9 +145,10 @@ def test_relu_mrs_table(k, acc):
 RESCALE_VALS = [0, 1, -1, 7, -7, 14, -15, 55773217, -55773217, 111546434, -111546435]
 
 
-def test_rescale_legacy_reference_case():
+@FUSED
+def test_rescale_legacy_reference_case(fused):
     c = d.Circuit([d.Rescale(2, (len(RESCALE_VALS),))])
-    out, _ = run(c, 9, 100.0, RESCALE_VALS)
+    out, _ = run(c, 9, 100.0, RESCALE_VALS, fused=fused)
     expected = -((-np.array(RESCALE_VALS)) // 4)  # ceil(ceil(x/2)/2)
     np.testing.assert_array_equal(out, expected)
 
@@ -165,11 +174,12 @@ def test_base_extension():
 
 # -------------------------------------------------------------- pooling
 @pytest.mark.parametrize("C,H,W,k,s", [(1, 2, 2, 2, 2), (2, 4, 4, 2, 2), (1, 3, 3, 1, 1), (3, 6, 6, 3, 3), (2, 5, 5, 2, 1)])
-def test_maxpool(C, H, W, k, s):
+@FUSED
+def test_maxpool(C, H, W, k, s, fused):
     rng = np.random.default_rng(C * H + k)
     x = rng.integers(-1000, 1000, C * H * W)
     mp = d.MaxPool2d(W, H, C, k, k, s, s)
-    out, _ = run(d.Circuit([mp]), 7, 100.0, x)
+    out, _ = run(d.Circuit([mp]), 7, 100.0, x, fused=fused)
     np.testing.assert_array_equal(out, mp.plain_q_eval(x))
 
 
@@ -275,3 +285,18 @@ def test_resnet18_zoo_has_projection_shortcuts():
     assert len(srcs) == 3  # stages 2-4 change width / stride
     specs = c.garble_specs()
     assert sum("in_src" in p for _, p in specs) == 3
+
+
+def test_fused_sign_drops_cast_tables_and_roundtrips():
+    """The fused construction stores no cast1 tables (k (t-1) + (t-1) fewer projections per sign gadget) and
+    survives serialization with its construction flag."""
+    vals = [0, 1, -1, 7, -7, 14, -15]
+    c = d.Circuit([d.Relu((len(vals),))])
+    gf = GarbledCircuit(c, [2, 3, 5], [26, 6, 3, 2], seed=SEED, fused_sign=True)
+    gr = GarbledCircuit(c, [2, 3, 5], [26, 6, 3, 2], seed=SEED, fused_sign=False)
+    assert "s.cast1" not in gf.model.layer_arrays(0) and "s.cast1" in gr.model.layer_arrays(0)
+    assert gf.model.table_bytes() < gr.model.table_bytes()
+    m2 = type(gf.model).deserialize(gf.model.serialize())
+    assert m2.sign_fused
+    gf.model = m2
+    np.testing.assert_array_equal(gf.decode_outputs(gf.cpu_evaluate(gf.garble_inputs(vals))), np.maximum(vals, 0))

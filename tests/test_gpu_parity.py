@@ -14,8 +14,11 @@ def _hip(models, mfma=True):
     return HipEvaluator(models, mfma=mfma)
 
 
-def _check(circuit, crt, mrs, xs, mfma=True, plain=True):
-    gcs = [GarbledCircuit(circuit, crt, mrs, seed=bytes([i + 1]) * 16) for i in range(len(xs))]
+FUSED = pytest.mark.parametrize("fused", [True, False], ids=["fused", "refcasts"])
+
+
+def _check(circuit, crt, mrs, xs, mfma=True, plain=True, fused=True):
+    gcs = [GarbledCircuit(circuit, crt, mrs, seed=bytes([i + 1]) * 16, fused_sign=fused) for i in range(len(xs))]
     enc = [g.garble_inputs(x) for g, x in zip(gcs, xs)]
     cpu = [g.cpu_evaluate(e) for g, e in zip(gcs, enc)]
     ev = _hip([g.model for g in gcs], mfma=mfma)
@@ -70,32 +73,36 @@ def test_conv(mfma):
     _check(c, 9, None, xs, mfma=mfma)
 
 
-def test_sign_edges():
+@FUSED
+def test_sign_edges(fused):
     vals = [0, 1, -1, 55773217, -55773217, 111546434, -111546435]
     c = d.Circuit([d.Sign((len(vals),))])
-    _check(c, 9, [76, 7, 7, 7, 7, 7, 5, 5], [vals, vals[::-1]])
+    _check(c, 9, [76, 7, 7, 7, 7, 7, 5, 5], [vals, vals[::-1]], fused=fused)
 
 
-def test_relu_edges():
+@FUSED
+def test_relu_edges(fused):
     vals = [0, 1, -1, 7, -7, 14, -15]
     c = d.Circuit([d.Relu((len(vals),))])
-    _check(c, [2, 3, 5], [26, 6, 3, 2], [vals])
+    _check(c, [2, 3, 5], [26, 6, 3, 2], [vals], fused=fused)
 
 
+@FUSED
 @pytest.mark.parametrize("layer", ["relu", "sign"])
-def test_single_digit_mrs(layer):
+def test_single_digit_mrs(layer, fused):
     """ReLU/Sign accuracy 99 % with k = 8 selects a one-digit MRS base ([126]): no casts, no carry chain."""
     rng = np.random.default_rng(5)
     xs = [rng.integers(-1000, 1000, 64) for _ in range(2)]
     c = d.Circuit([d.Relu((64,)) if layer == "relu" else d.Sign((64,))])
-    _check(c, 8, 99.0, xs, plain=False)  # approximate (99 %): GPU == host labels bit for bit
+    _check(c, 8, 99.0, xs, plain=False, fused=fused)  # approximate (99 %): GPU == host labels bit for bit
 
 
-def test_rescale_legacy():
+@FUSED
+def test_rescale_legacy(fused):
     rng = np.random.default_rng(3)
     xs = [rng.integers(-100000, 100000, 300) for _ in range(2)]
     c = d.Circuit([d.Rescale(2, (300,))])
-    _check(c, 9, 100.0, xs)
+    _check(c, 9, 100.0, xs, fused=fused)
 
 
 @pytest.mark.parametrize("crt,mrs", [([32, 97, 107], [22, 19, 15, 13]), ([32, 3, 5, 7, 11, 13, 17], [10, 9, 9, 8, 7, 7, 6])])
@@ -106,11 +113,12 @@ def test_rescale_redash(crt, mrs):
     _check(c, crt, mrs, xs)
 
 
-def test_maxpool_sumpool_add():
+@FUSED
+def test_maxpool_sumpool_add(fused):
     rng = np.random.default_rng(5)
     c = d.Circuit([d.MaxPool2d(6, 6, 2, 2, 2), d.Add((2, 3, 3), 0), d.SumPool2d(3, 3, 2, 3, 3)])
     xs = [rng.integers(-50, 50, 72) for _ in range(2)]
-    _check(c, 7, 100.0, xs)
+    _check(c, 7, 100.0, xs, fused=fused)
 
 
 def test_projection_mult_mixed():
@@ -218,8 +226,9 @@ def test_projection_shortcut_in_src():
     _check(c, k, 100.0, xs)
 
 
+@FUSED
 @pytest.mark.parametrize("name", ["relu", "sign", "rescale", "model_b", "minionn_head"])
-def test_gpu_garbler_bit_identical(name):
+def test_gpu_garbler_bit_identical(name, fused):
     """GPU garbler (ReLU / Sign / legacy rescale on the device) == CPU garbler, byte for byte."""
     from dash_amd.ir.circuit import Circuit
     from dash_amd.ir.layers import Relu, Rescale, Sign
@@ -238,7 +247,7 @@ def test_gpu_garbler_bit_identical(name):
         full = build_circuit("MODEL_F_MINIONN_POOL_REPL", Q.ScaleQuant, 5, seed=0)
         c, k = Circuit(full.layers[:3]), 7  # conv, rescale(l=5), relu at full size
     seed = bytes(range(16))
-    cpu = GarbledCircuit(c, k, 100.0, seed=seed)
-    gpu = GarbledCircuit(c, k, 100.0, seed=seed, device=0)
+    cpu = GarbledCircuit(c, k, 100.0, seed=seed, fused_sign=fused)
+    gpu = GarbledCircuit(c, k, 100.0, seed=seed, device=0, fused_sign=fused)
     assert gpu.model.serialize() == cpu.model.serialize()
     assert gpu.decoder.serialize() == cpu.decoder.serialize()
