@@ -228,6 +228,20 @@ CrtLabels cpu_evaluate(const GarbledModel& m, const CrtLabels& inputs, int nt, s
             }
             case K_RESCALE: {
                 const i64 mode = g.param("mode", 0);
+                if (mode == 2) {  // mixed-radix construction of the legacy function
+                    const RescaleMrsPlan P(crt, static_cast<int>(g.param("l")));
+                    const Array& tab = g.arr("mrs");
+                    DASH_CHECK(tab.shape[1] == P.n_tab, "mixed-radix rescale table shape");
+                    parallel_for(Nin, [&](i64 b0, i64 b1) {
+                        std::vector<comp_t*> Lp(k);
+                        for (i64 e = b0; e < b1; ++e) {
+                            for (int j = 0; j < k; ++j) Lp[j] = cur[j].at(e);
+                            rescale_mrs_eval_elem(P, Lp.data(), tab.ptr<u128>() + e * P.n_tab);
+                        }
+                    }, nt);
+                    break;
+                }
+                DASH_CHECK(mode == 0 || mode == 1, "unknown rescale mode " + std::to_string(mode));
                 const i64 iters = g.param("iters");
                 std::vector<RescalePlan> plans;
                 if (mode == 0) {

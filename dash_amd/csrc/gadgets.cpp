@@ -562,4 +562,143 @@ void rescale_eval_elem(const RescalePlan& P, const LabelBank& Z, comp_t* const* 
     for (int j = 0; j < k; ++j) lab_sub(L[j], down[j], nr_comps(P.crt[j]), P.crt[j]);
 }
 
+// ---------------------------------------------------------------------------
+// Single-shot mixed-radix rescale (gadgets.h RescaleMrsPlan)
+RescaleMrsPlan::RescaleMrsPlan(const std::vector<int>& crt_, int l_) : crt(crt_), l(l_) {
+    const int kk = k();
+    DASH_CHECK(kk >= 2 && crt[0] == 2, "mixed-radix rescale needs CRT residue 0 = 2");
+    DASH_CHECK(l >= 1 && l <= 14, "mixed-radix rescale: 1 <= l <= 14");
+    for (int j = 1; j < kk; ++j) DASH_CHECK(crt[j] % 2 == 1, "mixed-radix rescale: residues 1.. must be odd");
+    S = i64(1) << l;
+    T = 2 * S;
+    M = 1;
+    for (int p : crt) M *= p;
+    const i64 h = M / 2;
+    U = h + pmod(S - 1 - h % S, S);
+    q = (U - (S - 1)) / S;
+    B.assign(kk, 1);
+    Binv.assign(kk, 1);
+    Sinv.assign(kk, 0);
+    for (int i = 1; i < kk; ++i) B[i] = B[i - 1] * crt[i - 1];
+    for (int i = 0; i < kk; ++i) Binv[i] = mul_inv(static_cast<u128>(B[i] % crt[i]), crt[i]);
+    for (int j = 1; j < kk; ++j) Sinv[j] = mul_inv(static_cast<u128>(S % crt[j]), crt[j]);
+    dig_off.assign(kk, 0);
+    i64 off = 0;
+    for (int i = 0; i < kk; ++i) {
+        dig_off[i] = off;
+        off += static_cast<i64>(crt[i]) * targets(i);
+    }
+    fin_off = off;
+    n_tab = off + T * kk;
+}
+
+i64 RescaleMrsPlan::digit_fn(int i, int t, i64 v) const {
+    const i64 pi = crt[i];
+    const i64 a = pmod((v + U % pi) * Binv[i], pi);  // digit a_i of x_u
+    const i64 m = target_mod(i, t);
+    return pmod(a * (B[i] % m), m);
+}
+
+i64 RescaleMrsPlan::final_fn(int j, i64 v) const {
+    if (j == 0) return pmod(v / S - q, 2);
+    const i64 p = crt[j];
+    return pmod((pmod(U, p) - v % S) * Sinv[j] - q, p);
+}
+
+void rescale_mrs_garble_elem(const RescaleMrsPlan& P, const LabelBank& R, const Prg& prg, u64 stream,
+                             comp_t* const* L, u128* tab) {
+    const int k = P.k();
+    constexpr int W = 128;
+    // draws, PRG counter order: digit i's target labels (t = 0..k-1-i), then the k final output labels
+    int nd = 0;
+    for (int i = 0; i < k; ++i) nd += P.targets(i);
+    comp_t* buf = rescale_scratch().get(static_cast<size_t>(W) * (nd + k + k + 1));
+    std::vector<comp_t*> dig(nd), fin(k), key(k);
+    u64 ctr = 0;
+    int s = 0;
+    for (int i = 0; i < k; ++i)
+        for (int t = 0; t < P.targets(i); ++t, ++s) {
+            dig[s] = buf + static_cast<size_t>(W) * s;
+            draw(prg, stream, ctr, P.target_mod(i, t), dig[s]);
+        }
+    for (int j = 0; j < k; ++j) {
+        fin[j] = buf + static_cast<size_t>(W) * (nd + j);
+        draw(prg, stream, ctr, P.crt[j], fin[j]);
+    }
+    comp_t* acc = buf + static_cast<size_t>(W) * (nd + 2 * k);
+    const ModInfo& mT = mod_info(static_cast<int>(P.T));
+    std::fill(acc, acc + mT.n, comp_t(0));
+    // key base labels: K_i = L_i - sum_{l<i} P_{l,i}; r = sum_i P_{i,T}
+    for (int j = 0; j < k; ++j) {
+        key[j] = buf + static_cast<size_t>(W) * (nd + k + j);
+        std::memcpy(key[j], L[j], sizeof(comp_t) * nr_comps(P.crt[j]));
+    }
+    s = 0;
+    for (int i = 0; i < k; ++i)
+        for (int t = 0; t < P.targets(i); ++t, ++s) {
+            if (t == k - 1 - i) lab_add(acc, dig[s], mT.n, mT.p);
+            else lab_sub(key[i + 1 + t], dig[s], nr_comps(P.crt[i + 1 + t]), P.crt[i + 1 + t]);
+        }
+    ProjKeys& K = proj_keys_scratch();
+    s = 0;
+    for (int i = 0; i < k; ++i) {
+        const ModInfo& mi = mod_info(P.crt[i]);
+        proj_keys(key[i], R.get(mi.p), mi, K);
+        const int nt = P.targets(i);
+        for (int t = 0; t < nt; ++t, ++s) {
+            const ModInfo& mo = mod_info(P.target_mod(i, t));
+            garble_proj_keys(K, dig[s], R.get(mo.p), mo, [&](int v) { return P.digit_fn(i, t, v); },
+                             tab + P.dig_off[i] + t, nt);
+        }
+    }
+    proj_keys(acc, R.get(mT.p), mT, K);
+    for (int j = 0; j < k; ++j) {
+        const ModInfo& mo = mod_info(P.crt[j]);
+        garble_proj_keys(K, fin[j], R.get(mo.p), mo, [&](int v) { return P.final_fn(j, v); }, tab + P.fin_off + j, k);
+    }
+    // output base labels: Y_j = S^-1 L_j + fin_j (j >= 1), Y_0 = fin_0
+    std::memcpy(L[0], fin[0], sizeof(comp_t) * nr_comps(2));
+    for (int j = 1; j < k; ++j) {
+        const int p = P.crt[j], n = nr_comps(p);
+        lab_scale(L[j], P.Sinv[j], n, p);
+        lab_add(L[j], fin[j], n, p);
+    }
+}
+
+void rescale_mrs_eval_elem(const RescaleMrsPlan& P, comp_t* const* L, const u128* tab) {
+    const int k = P.k();
+    constexpr int W = 128;
+    comp_t* buf = rescale_scratch().get(static_cast<size_t>(W) * (k + 2));
+    std::vector<comp_t*> key(k);
+    for (int j = 0; j < k; ++j) {
+        key[j] = buf + static_cast<size_t>(W) * j;
+        std::memcpy(key[j], L[j], sizeof(comp_t) * nr_comps(P.crt[j]));
+    }
+    const ModInfo& mT = mod_info(static_cast<int>(P.T));
+    comp_t* acc = buf + static_cast<size_t>(W) * k;
+    comp_t* pr = buf + static_cast<size_t>(W) * (k + 1);
+    std::fill(acc, acc + mT.n, comp_t(0));
+    for (int i = 0; i < k; ++i) {
+        const ModInfo& mi = mod_info(P.crt[i]);
+        const u128 h = hash(compress(key[i], mi));
+        const int nt = P.targets(i);
+        const u128* row = tab + P.dig_off[i] + static_cast<i64>(color_of(key[i], mi.p)) * nt;
+        for (int t = 0; t < nt; ++t) {
+            const ModInfo& mo = mod_info(P.target_mod(i, t));
+            decompress(row[t] - h, pr, mo);
+            if (t == nt - 1) lab_add(acc, pr, mo.n, mo.p);
+            else lab_sub(key[i + 1 + t], pr, mo.n, mo.p);
+        }
+    }
+    const u128 h = hash(compress(acc, mT));
+    const u128* row = tab + P.fin_off + static_cast<i64>(color_of(acc, mT.p)) * k;
+    decompress(row[0] - h, L[0], mod_info(2));
+    for (int j = 1; j < k; ++j) {
+        const ModInfo& mo = mod_info(P.crt[j]);
+        decompress(row[j] - h, pr, mo);
+        lab_scale(L[j], P.Sinv[j], mo.n, mo.p);
+        lab_add(L[j], pr, mo.n, mo.p);
+    }
+}
+
 }  // namespace dash

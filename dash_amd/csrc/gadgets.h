@@ -238,4 +238,53 @@ void rescale_eval_elem(const RescalePlan& P, const LabelBank& Z, comp_t* const* 
                        const comp_t* const* down, const u128* trans, const u128* s_approx, const u128* s_cast1,
                        const u128* s_cast2, const u128* s_sign, const u128* be);
 
+// ---------------------------------------------------------------------------
+// Single-shot mixed-radix rescale (the DASH legacy function, new construction)
+//
+// The legacy gadget divides by S = 2^l with l iterations of "subtract the
+// mod-2 residue, halve, recover residue 0 with a sign gadget" (rescale_gadget.h
+// :115-242, each iteration a full approximate sign gadget). Composed, the l
+// iterations compute y = ceil(x / S) (Rescale._apply). Here the same y comes
+// from one exact mixed-radix conversion:
+//   x_u = (x + U) mod M with U = S - 1 + S q, U >= M/2 (U ~ M/2)
+//   MRS digits a_i of x_u over the CRT base (crt[0] = 2, ascending order):
+//     digit i: key K_i = L_i - sum_{l<i} P_{l,i}, a_i = (v_i + U) B_i^-1 mod p_i
+//     its table row fans out P_{i,j} = a_i B_i mod p_j to every later residue j
+//     and P_{i,T} = a_i B_i mod T (T = 2S) to a power-of-two label
+//   r = sum_i P_{i,T} = x_u mod 2S (free additions)
+//   final row (T entries): residue j >= 1: Y_j = S^-1 L_j + [(U - r mod S) S^-1 - q]
+//                          residue 0:      Y_0 = [(floor(r / S) - q) mod 2]
+// so y = floor(x_u / S) - q = ceil(x / S) for every x in [-M/2, M/2 - (U - M/2)):
+// only the top U - M/2 < S values of the signed range wrap (they differ from
+// the legacy gadget). k + 1 hashes and table reads per element on the
+// evaluator instead of l sign gadgets (l = 5, k = 7: 8 instead of ~60), and
+// sum_i p_i (k - i) + T k table entries instead of l (2 (k - 1) + sign).
+// Table (one row per element): digit i at dig_off[i], [color][k - i] entries
+// (targets: residues i+1..k-1, then T); final rows at fin_off, [color][k]
+// (targets: residues 0..k-1).
+struct RescaleMrsPlan {
+    std::vector<int> crt;
+    int l = 0;
+    i64 S = 1, T = 2, M = 1, U = 0, q = 0;
+    std::vector<i64> B;       // B[i] = prod_{m<i} crt[m]
+    std::vector<i64> Binv;    // B[i]^-1 mod crt[i]
+    std::vector<i64> Sinv;    // S^-1 mod crt[j] (j >= 1)
+    std::vector<i64> dig_off; // table offset of digit i's rows
+    i64 fin_off = 0, n_tab = 0;
+    RescaleMrsPlan() = default;
+    RescaleMrsPlan(const std::vector<int>& crt, int l);
+    int k() const { return static_cast<int>(crt.size()); }
+    int targets(int i) const { return k() - i; }
+    // modulus of target t of digit i (residue i + 1 + t, the last one T)
+    int target_mod(int i, int t) const { return t == k() - 1 - i ? static_cast<int>(T) : crt[i + 1 + t]; }
+    // payload value of digit i, target t, for key value v (a_i B_i reduced mod the target modulus)
+    i64 digit_fn(int i, int t, i64 v) const;
+    // payload value of final target j for key value v = x_u mod T
+    i64 final_fn(int j, i64 v) const;
+};
+// L[j] (one element's labels mod crt[j]) are replaced by the rescaled labels.
+void rescale_mrs_garble_elem(const RescaleMrsPlan& P, const LabelBank& R, const Prg& prg, u64 stream,
+                             comp_t* const* L, u128* tab);
+void rescale_mrs_eval_elem(const RescaleMrsPlan& P, comp_t* const* L, const u128* tab);
+
 }  // namespace dash

@@ -88,7 +88,8 @@ MaxTree::MaxTree(i64 K) {
     }
 }
 
-int required_max_modulus(const std::vector<int>& crt, const std::vector<int>& mrs, const std::vector<LayerSpec>& layers) {
+int required_max_modulus(const std::vector<int>& crt, const std::vector<int>& mrs, const std::vector<LayerSpec>& layers,
+                         bool rescale_mrs) {
     int mx = 2;
     for (int p : crt) mx = std::max(mx, p);
     const int k = static_cast<int>(crt.size());
@@ -102,6 +103,8 @@ int required_max_modulus(const std::vector<int>& crt, const std::vector<int>& mr
             for (auto v : paramv(l.p, "in_mod")) mx = std::max<int>(mx, static_cast<int>(v));
         }
         if (l.kind == K_MMULT) mx = std::max<int>(mx, static_cast<int>(param1(l.p, "q")));
+        if (rescale_mrs && l.kind == K_RESCALE && param1(l.p, "mode", 0) == 0)
+            mx = std::max<int>(mx, 2 << static_cast<int>(param1(l.p, "l")));  // the x_u mod 2^(l+1) label
     }
     return mx;
 }
@@ -332,7 +335,7 @@ GarbledModel Garbler::garble(const std::vector<LayerSpec>& layers, const std::ve
                              const GarbleOptions& opt) {
     const int nt = opt.nthreads;
     const int k = static_cast<int>(crt_.size());
-    const int need = required_max_modulus(crt_, mrs_, layers);
+    const int need = required_max_modulus(crt_, mrs_, layers, opt.rescale_mrs);
     max_mod_ = std::max(max_mod_, need);
     GarbledModel m;
     const bool fused = opt.fused_sign;
@@ -469,8 +472,11 @@ GarbledModel Garbler::garble(const std::vector<LayerSpec>& layers, const std::ve
             return true;
         };
 
+        // legacy rescale as one mixed-radix gadget (RescaleMrsPlan)
+        const bool mrs_rescale = opt.rescale_mrs && spec.kind == K_RESCALE && param1(spec.p, "mode", 0) == 0;
         const bool on_gpu = gpu && (spec.kind == K_CONV || spec.kind == K_RELU || spec.kind == K_SIGN ||
-                                    (spec.kind == K_RESCALE && param1(spec.p, "mode", 0) == 0 && crt_[0] == 2));
+                                    (spec.kind == K_RESCALE && param1(spec.p, "mode", 0) == 0 && crt_[0] == 2 &&
+                                     !mrs_rescale));
         const bool passthru = spec.kind == K_FLATTEN;
         if (on_gpu && !dev_ok) {
             gpu->to_device(cur);
@@ -656,6 +662,23 @@ GarbledModel Garbler::garble(const std::vector<LayerSpec>& layers, const std::ve
             case K_RESCALE: {
                 DASH_CHECK(is_crt(), "rescale needs CRT-base labels");
                 const i64 mode = param1(spec.p, "mode", 0);
+                if (mrs_rescale) {
+                    const RescaleMrsPlan P(crt_, static_cast<int>(param1(spec.p, "l")));
+                    Array tab(DType::u128, {Nin, P.n_tab});
+                    parallel_for(Nin, [&](i64 b0, i64 b1) {
+                        std::vector<comp_t*> Lp(k);
+                        for (i64 e = b0; e < b1; ++e) {
+                            for (int j = 0; j < k; ++j) Lp[j] = cur[j].at(e);
+                            rescale_mrs_garble_elem(P, R_, prg_, stream_id(L, 30, e), Lp.data(),
+                                                    tab.ptr<u128>() + e * P.n_tab);
+                        }
+                    }, nt);
+                    g.a["mrs"] = tab;
+                    g.p["mode"] = {2};
+                    g.p["iters"] = {1};
+                    g.p["sprod"] = {P.S};
+                    break;
+                }
                 std::vector<RescalePlan> plans;
                 if (mode == 0) {
                     const i64 l = param1(spec.p, "l");

@@ -231,8 +231,15 @@ __device__ __forceinline__ uint32_t u128_mod(u128 P, const ModC& m) {
 // column vs ~16 for a byte-extract/shift/add/rotate formulation.
 // The round keys of the fixed key are compile-time constants (the key is part
 // of the scheme, crypto/cpu_aes_engine.h:23-24), so they become literals.
-#define DASH_AES_LDS_BYTES 65536
+// DASH_AES_COPIES < 32 shrinks the image (2 KiB per copy) at the price of
+// (32 / copies)-way bank conflicts: more resident blocks per CU (A/B knob).
+#ifndef DASH_AES_COPIES
+#define DASH_AES_COPIES 32
+#endif
+#define DASH_AES_LDS_BYTES (2048 * DASH_AES_COPIES)
 #define DASH_AES_LDS_WORDS (DASH_AES_LDS_BYTES / 4)
+constexpr uint32_t kAesRow = 8 * DASH_AES_COPIES;  // bytes per table row: Te0 copies, then Te2 copies
+constexpr uint32_t kAesT2 = 4 * DASH_AES_COPIES;   // offset of the Te2 copies inside a row
 
 __device__ constexpr uint32_t kAesRk[44] = {
     0x00010203u, 0x04050607u, 0x08090a0bu, 0x0c0d0e0fu, 0xd6aa74fdu, 0xd2af72fau, 0xdaa678f1u, 0xd6ab76feu,
@@ -254,7 +261,11 @@ __device__ __forceinline__ uint32_t bswap32(uint32_t x) { return __builtin_bswap
 // byte offset of row byte_I(s), lane copy: D = {0, 0, s.byte[I], lo.byte[0]}
 template <int I>
 __device__ __forceinline__ uint32_t aes_off(uint32_t s, uint32_t lo) {
+#if DASH_AES_COPIES == 32
     return __builtin_amdgcn_perm(s, lo, 0x0c0c0000u | ((4u + I) << 8));
+#else
+    return (((s >> (8 * I)) & 0xffu) * kAesRow) | lo;
+#endif
 }
 template <int I>
 __device__ __forceinline__ uint32_t aes_t0(const AesCtx& a, uint32_t s) {
@@ -262,7 +273,7 @@ __device__ __forceinline__ uint32_t aes_t0(const AesCtx& a, uint32_t s) {
 }
 template <int I>
 __device__ __forceinline__ uint32_t aes_t2(const AesCtx& a, uint32_t s) {
-    return *reinterpret_cast<const uint32_t*>(a.T + aes_off<I>(s, a.lo) + 128);
+    return *reinterpret_cast<const uint32_t*>(a.T + aes_off<I>(s, a.lo) + kAesT2);
 }
 // three-input XOR in one VALU op (v_bitop3_b32, truth table 0x96)
 __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
@@ -365,8 +376,8 @@ __device__ __forceinline__ void aes_lds_fill(uint32_t* lds, const uint32_t* te0)
     const int nt = blockDim.x * blockDim.y;
     for (int i4 = threadIdx.x + threadIdx.y * blockDim.x; i4 < DASH_AES_LDS_WORDS / 4; i4 += nt) {
         const int i = 4 * i4;
-        const uint32_t v = te0[i >> 6];
-        const uint32_t w = (i & 32) ? ror32(v, 16) : v;
+        const uint32_t v = te0[i / (2 * DASH_AES_COPIES)];
+        const uint32_t w = (i % (2 * DASH_AES_COPIES) >= DASH_AES_COPIES) ? ror32(v, 16) : v;
         reinterpret_cast<uint4*>(lds)[i4] = make_uint4(w, w, w, w);
     }
     __syncthreads();
@@ -375,7 +386,7 @@ __device__ __forceinline__ void aes_lds_fill(uint32_t* lds, const uint32_t* te0)
 __device__ __forceinline__ AesCtx aes_ctx(const uint32_t* lds, const uint32_t* /*rk*/) {
     AesCtx a;
     a.T = reinterpret_cast<const char*>(lds);
-    a.lo = (__lane_id() & 31u) << 2;
+    a.lo = (__lane_id() % DASH_AES_COPIES) << 2;
     return a;
 }
 

@@ -29,6 +29,7 @@
 #include "dev.h"
 #include "gpu_garbler.h"
 #include "kargs.h"
+#include "launch.h"
 #include "host_util.h"
 
 namespace dash {
@@ -57,6 +58,14 @@ struct Proj {
     int table, stride;           // table id, entry stride
     int64_t off;                 // entry offset inside the element's table row
     int64_t first;               // first global entry index of this projection
+    int pay1;                    // 1 + payload bank row of f-index 0 (F_SIGN, F_DIV, F_DIVMOD); 0: computed inline
+};
+
+// A projection whose function takes few distinct values (sign: 2, carry: k+1)
+// has few distinct payloads o + f*R: they are computed once per element into a
+// payload bank (row-major [row][N], coalesced) instead of once per table entry.
+struct PayDesc {
+    int out_slot, pout, f;  // payload = slot label + f * R_pout (f already reduced mod pout)
 };
 
 struct Tables {
@@ -130,6 +139,7 @@ struct Gadget {
     int nblk;         // AES-CTR blocks drawn per element (sum over draws)
     uint64_t layer, sslot, mask;  // PRG stream of this gadget: stream_of(layer, sslot, e, mask)
     int16_t* S;       // scratch [N][nslots][kW]
+    u128* PB;         // payload bank [row][N] (PayDesc rows)
     int64_t N;
     int mrs[kMaxMrs]; // MRS base of the sign gadget (per-digit output moduli of the fanned-out approx projections)
 };
@@ -383,6 +393,7 @@ __device__ __forceinline__ Proj rfl_proj(const Proj& p) {
     r.stride = rfl(p.stride);
     r.off = rfl64(p.off);
     r.first = rfl64(p.first);
+    r.pay1 = rfl(p.pay1);
     return r;
 }
 
@@ -433,6 +444,13 @@ __global__ __launch_bounds__(kPB) void k_project(Ctx c, Gadget g, In in, Tables 
             }
             continue;
         }
+        if (P.pay1 > 0) {
+            // few distinct payloads: precomputed per element by k_payloads
+            const int idx = P.fn == F_SIGN ? (i < P.a0 ? 1 : 0) : i / P.a0;  // F_SIGN: 0 lower / 1 upper; F_DIV(MOD): i / m
+            const u128 pay = g.PB[static_cast<int64_t>(P.pay1 - 1 + idx) * N + e];
+            if (e_raw < N) tb.t[P.table][e * tb.row[P.table] + P.off + static_cast<int64_t>(color) * P.stride] = pay + H;
+            continue;
+        }
         // function value
         int64_t f;
         switch (P.fn) {
@@ -461,6 +479,19 @@ __global__ __launch_bounds__(kPB) void k_project(Ctx c, Gadget g, In in, Tables 
     }
 }
 
+// Payload bank: one thread per (row, element), rows = PayDesc entries.
+__global__ __launch_bounds__(256) void k_payloads(Ctx c, Gadget g, const PayDesc* pd, int npd) {
+    const int64_t total = g.N * npd;
+    for (int64_t x = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; x < total;
+         x += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+        const int r = static_cast<int>(x / g.N);
+        const int64_t e = x - static_cast<int64_t>(r) * g.N;
+        const PayDesc d = pd[r];
+        const int16_t* ol = g.S + (e * g.nslots + d.out_slot) * kW;
+        g.PB[x] = proj_payload(ol, c.R + static_cast<int64_t>(d.pout) * kW, static_cast<uint32_t>(d.f), c.mc[d.pout]);
+    }
+}
+
 // ReLU mixed-mod half gates beyond the g/e projections: mini gate payloads
 // (16-bit, e[q]) and the output base labels out0[j] = sk04 - sk03.
 struct MiniArgs {
@@ -470,10 +501,7 @@ struct MiniArgs {
     int16_t* out[kMaxRes];   // next base labels [N][n_j]
 };
 
-__global__ __launch_bounds__(256) void k_relu_finish(Ctx c, Gadget g, In in, Tables tb, MiniArgs m) {
-    __shared__ __attribute__((aligned(16))) uint32_t lds_aes[DASH_AES_LDS_WORDS];
-    aes_lds_fill(lds_aes, c.te0);
-    const AesCtx aes = aes_ctx(lds_aes, nullptr);
+__global__ __launch_bounds__(256) void k_relu_finish(Ctx c, Gadget g, In in, Tables tb, MiniArgs m, const u128* hk) {
     const int64_t total = g.N * m.k;
     for (int64_t gi = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; gi < total;
          gi += static_cast<int64_t>(gridDim.x) * blockDim.x) {
@@ -482,21 +510,13 @@ __global__ __launch_bounds__(256) void k_relu_finish(Ctx c, Gadget g, In in, Tab
         const int p = m.crt[j];
         const int16_t* x = in.p[j] + e * in.n[j];
         const int16_t* sig = g.S + (e * g.nslots + m.sig_slot) * kW;
-        const ModC m2 = c.mc[2];
         const int16_t* R2 = c.R + 2 * kW;
         const int r = x[0];
-        // mini gate y -> (y + r) mod p, 16-bit payload at t16[color] of entry e[k][2]
+        // mini gate y -> (y + r) mod p, 16-bit payload at t16[color] of entry e[k][2]; key hashes: k_bin_keys
         int16_t* t16 = reinterpret_cast<int16_t*>(tb.t[5] + (e * m.k + j) * 3 + 2);
         for (int i = 0; i < 2; ++i) {
-            CompressFwd kc;
-            kc.init();
-            uint32_t color = 0;
-            for (int q = 0; q < static_cast<int>(m2.n); ++q) {
-                const uint32_t v = static_cast<uint32_t>(sig[q] + i * R2[q]) & 1u;
-                if (q == 0) color = v;
-                kc.push(v, m2);
-            }
-            const u128 H = aes_encrypt(aes, kc.finish());
+            const uint32_t color = static_cast<uint32_t>(sig[0] + i * R2[0]) & 1u;
+            const u128 H = hk[i * g.N + e];
             const int fv = (i + r) % p;
             t16[color] = static_cast<int16_t>(static_cast<int16_t>(fv) + static_cast<int16_t>(static_cast<uint16_t>(H)));
         }
@@ -523,13 +543,59 @@ struct RsArgs {
     uint64_t layer, sslot;     // trans stream = stream_of(layer, sslot, e, 0)
 };
 
+// 8 mod-2 components (0/1 in the low bit of each 16-bit half) -> 8 bits
+__device__ __forceinline__ uint32_t bits8(const u32x4a& v) {
+    uint32_t b = 0;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) b |= ((v[u] & 1u) | ((v[u] >> 15) & 2u)) << (2 * u);
+    return b;
+}
+
+// Keys x + i*R_2 (i = 0, 1) of a mod-2 label x = row(e) [+ add], hashed once
+// per element (hk[i][N]). Both users need the same two hashes for all k
+// residues: the legacy rescale's trans projections of L_0 + up_0 and the ReLU
+// mini gates of the sign output. A mod-2 label compresses to its component
+// bits, so the key is a bit pack and key 1 is key 0 XOR the bits of R_2.
+__global__ __launch_bounds__(kGB) void k_bin_keys(Ctx c, const int16_t* rows, int64_t stride, const int16_t* add,
+                                                  u128* hk, int64_t N) {
+    __shared__ __attribute__((aligned(16))) uint32_t lds_aes[DASH_AES_LDS_WORDS];
+    aes_lds_fill(lds_aes, c.te0);
+    const AesCtx aes = aes_ctx(lds_aes, nullptr);
+    const int16_t* R2 = c.R + 2 * kW;
+    for (int64_t e = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; e < N;
+         e += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+        const int16_t* L0 = rows + e * stride;
+        uint32_t k0[4] = {0, 0, 0, 0}, r[4] = {0, 0, 0, 0};
+#pragma unroll
+        for (int q0 = 0; q0 < 128; q0 += 8) {
+            const u32x4a la = ld8a(L0 + q0), ra = ld8a(R2 + q0);
+            u32x4a s = la;
+            if (add) {
+                const u32x4a ua = ld8a(add + q0);
+#pragma unroll
+                for (int u = 0; u < 4; ++u) s[u] = la[u] + ua[u];  // halves <= 2: no carry between them
+            }
+            k0[q0 >> 5] |= bits8(s) << (q0 & 31);
+            r[q0 >> 5] |= bits8(ra) << (q0 & 31);
+        }
+        const u128 key0 = (static_cast<u128>((static_cast<uint64_t>(k0[3]) << 32) | k0[2]) << 64) |
+                          ((static_cast<uint64_t>(k0[1]) << 32) | k0[0]);
+        const u128 rb = (static_cast<u128>((static_cast<uint64_t>(r[3]) << 32) | r[2]) << 64) |
+                        ((static_cast<uint64_t>(r[1]) << 32) | r[0]);
+        u128 h0, h1;
+        aes_encrypt2(aes, key0, key0 ^ rb, h0, h1);
+        hk[e] = h0;
+        hk[N + e] = h1;
+    }
+}
+
 // One thread per (element, residue j >= 1): the trans projection of the
 // mod-2 residue into residue j plus the in-place update of L_j. The trans
 // output label is drawn one AES-CTR block (two components) at a time and
 // consumed at once (no per-thread label array, no scratch). L_0 is not
 // written here: the sign gadget reads Z_2 for residue 0 directly (In with a
 // zero element stride) and k_rescale_post_g overwrites L_0 afterwards.
-__global__ __launch_bounds__(kGB) void k_rescale_pre(Ctx c, RsArgs a, Tables tb, int64_t N) {
+__global__ __launch_bounds__(kGB) void k_rescale_pre(Ctx c, RsArgs a, Tables tb, const u128* hk, int64_t N) {
     __shared__ __attribute__((aligned(16))) uint32_t lds_aes[DASH_AES_LDS_WORDS];
     aes_lds_fill(lds_aes, c.te0);
     const AesCtx aes = aes_ctx(lds_aes, nullptr);
@@ -543,27 +609,10 @@ __global__ __launch_bounds__(kGB) void k_rescale_pre(Ctx c, RsArgs a, Tables tb,
         const int p = a.crt[j];
         const ModC mj = c.mc[p];
         const int n = static_cast<int>(mj.n);
-        // keys of the two trans rows: (L_0 + up_0) + i*R_2 over GF(2)
+        // hashes of the two trans rows' keys (L_0 + up_0) + i*R_2: k_rescale_keys
         const int16_t* L0 = a.L[0] + e * m2.n;
-        CompressFwd k0, k1;
-        k0.init();
-        k1.init();
-        // mod-2 rows are 128 components = 256 B (aligned): 16-B loads, the XORs done 8 lanes at a time
-        for (int q0 = 0; q0 < static_cast<int>(m2.n); q0 += 8) {
-            const u32x4a la = ld8a(L0 + q0), ua = ld8a(a.up + q0), ra = ld8a(R2 + q0);
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                const uint32_t v = (la[u] + ua[u]) & 0x00010001u;  // per 16-bit half: (l + u) & 1
-                const uint32_t w = (v + ra[u]) & 0x00010001u;
-                k0.push(v & 1u, m2);
-                k0.push(v >> 16, m2);
-                k1.push(w & 1u, m2);
-                k1.push(w >> 16, m2);
-            }
-        }
         const uint32_t color0 = static_cast<uint32_t>(L0[0] + a.up[0]) & 1u;
-        const u128 H0 = aes_encrypt(aes, k0.finish());
-        const u128 H1 = aes_encrypt(aes, k1.finish());
+        const u128 H0 = hk[e], H1 = hk[N + e];
         const uint64_t stream = stream_of(a.layer, a.sslot, static_cast<uint64_t>(e), 0);
         const int16_t* Rp = c.R + static_cast<int64_t>(p) * kW;
         const int16_t* upj = a.up + j * kW;
@@ -678,12 +727,29 @@ __global__ __launch_bounds__(256) void k_gather_slots(Gadget g, GatherArgs a) {
 struct SignLayout {
     std::vector<Draw> draws;
     std::vector<Proj> projs;
+    std::vector<PayDesc> pays;
     int fan[kMaxMrs] = {};  // output modulus of the approx fan-out per digit
     SignSlots ss{};
     int nslots = 0;
     int out_slot0 = 0;
     int64_t entries = 0;
 };
+
+// Route projection p's payloads through the payload bank: row idx < nidx holds
+// out_slot + f(idx) * R_pout.
+template <class F>
+Proj banked(SignLayout& L, Proj p, int nidx, F&& f) {
+    p.pay1 = static_cast<int>(L.pays.size()) + 1;
+    for (int idx = 0; idx < nidx; ++idx) {
+        int64_t cm = static_cast<int64_t>(f(idx)) % p.pout;
+        if (cm < 0) cm += p.pout;
+        L.pays.push_back(PayDesc{p.out_slot, p.pout, static_cast<int>(cm)});
+    }
+    return p;
+}
+inline Proj banked_sign(SignLayout& L, const Proj& p) {  // F_SIGN: row 0 = lower (a1), row 1 = upper (a2)
+    return banked(L, p, 2, [&](int idx) { return idx ? p.a2 : p.a1; });
+}
 
 // Fused construction (gadgets.cpp sign_garble_fused): digit labels, carries, outputs.
 SignLayout sign_layout_fused(const SignPlan& P, int extra_slots) {
@@ -733,14 +799,15 @@ SignLayout sign_layout_fused(const SignPlan& P, int extra_slots) {
     for (int q = 0; q + 1 < t; ++q) {
         const int d = t - 1 - q;
         const int mo = P.digit_mod(d);
-        add(Proj{S_SLOT, sum2_0 + q, mo, newc0 + q, P.carry_mod(d), F_DIVMOD, P.mrs[d], P.mrs[d - 1], 0, R_BANK, 0,
-                 2, 1, c2, 0});
+        const Proj cp{S_SLOT, sum2_0 + q, mo, newc0 + q, P.carry_mod(d), F_DIVMOD, P.mrs[d], P.mrs[d - 1], 0, R_BANK, 0,
+                      2, 1, c2, 0};
+        add(banked(L, cp, (mo + cp.a0 - 1) / cp.a0, [&](int idx) { return idx % cp.a1; }));
         c2 += mo;
     }
     const int m0 = P.mrs[0];
     for (size_t o = 0; o < P.out_mod.size(); ++o)
-        add(Proj{S_SLOT, sum_slot, m0, L.out_slot0 + static_cast<int>(o), P.out_mod[o], F_SIGN, m0 / 2, P.lower,
-                 P.upper, R_BANK, 0, 3, 1, static_cast<int64_t>(o) * m0, 0});
+        add(banked_sign(L, Proj{S_SLOT, sum_slot, m0, L.out_slot0 + static_cast<int>(o), P.out_mod[o], F_SIGN, m0 / 2,
+                                P.lower, P.upper, R_BANK, 0, 3, 1, static_cast<int64_t>(o) * m0, 0}));
     L.entries = first;
     return L;
 }
@@ -825,14 +892,15 @@ SignLayout sign_layout(const SignPlan& P, int extra_slots) {
             c1 += m;
             add(p);
         }
-        add(Proj{S_SLOT, sum2_0 + q, mo, bases0 + q * stride_q + (k + 1), P.mrs[d - 1], F_DIV, m, 0, 0, R_BANK, 0, 2, 1,
-                 c2, 0});
+        add(banked(L, Proj{S_SLOT, sum2_0 + q, mo, bases0 + q * stride_q + (k + 1), P.mrs[d - 1], F_DIV, m, 0, 0, R_BANK,
+                           0, 2, 1, c2, 0},
+                   (mo + m - 1) / m, [](int idx) { return idx; }));
         c2 += mo;
     }
     const int m0 = P.mrs[0];
     for (size_t o = 0; o < P.out_mod.size(); ++o)
-        add(Proj{S_SLOT, sum_slot, m0, L.out_slot0 + static_cast<int>(o), P.out_mod[o], F_SIGN, m0 / 2, P.lower,
-                 P.upper, R_BANK, 0, 3, 1, static_cast<int64_t>(o) * m0, 0});
+        add(banked_sign(L, Proj{S_SLOT, sum_slot, m0, L.out_slot0 + static_cast<int>(o), P.out_mod[o], F_SIGN, m0 / 2,
+                                P.lower, P.upper, R_BANK, 0, 3, 1, static_cast<int64_t>(o) * m0, 0}));
     L.entries = first;
     return L;
 }
@@ -1003,10 +1071,13 @@ struct DevBlock {
 struct DevTable {
     DevBlock b;
     int64_t row = 0;
-    void alloc(int device, int64_t N, int64_t r) {
+    // zero: only for tables whose entries are not all written by the kernels (the ReLU e table's
+    // mini entry fills 2 of its 8 int16 slots); every other table is fully covered, since the
+    // colors of a projection's p keys are a permutation of Z_p (R[0] = 1)
+    void alloc(int device, int64_t N, int64_t r, bool zero = false) {
         row = r;
         b.alloc(device, static_cast<size_t>(N) * r * sizeof(u128));
-        HIPCHECK(hipMemsetAsync(b.p, 0, b.bytes, nullptr));
+        if (zero) HIPCHECK(hipMemsetAsync(b.p, 0, b.bytes, nullptr));
     }
     u128* p() const { return b.as<u128>(); }
     // hand the buffer to `a` as a device-resident array (kept in HBM; the
@@ -1052,6 +1123,12 @@ void run_sign(const gg::Ctx& c, const gg::SignLayout& L, gg::Gadget& g, const gg
     check_desc(g);
     hipLaunchKernelGGL(gg::k_draw, dim3(blocks_for(g.N * g.nblk, gg::kGB, 8192)), dim3(gg::kGB), 0, nullptr, c, g);
     hipLaunchKernelGGL(gg::k_sign_derive, dim3(blocks_for(g.N, 256)), dim3(256), 0, nullptr, c, g, L.ss);
+    if (!L.pays.empty()) {
+        DASH_CHECK(g.PB != nullptr, "gpu garbler: payload bank not allocated");
+        const gg::PayDesc* pd = gg::dconst(L.pays.data(), L.pays.size());
+        const int npd = static_cast<int>(L.pays.size());
+        hipLaunchKernelGGL(gg::k_payloads, dim3(blocks_for(g.N * npd, 256, 16384)), dim3(256), 0, nullptr, c, g, pd, npd);
+    }
     hipLaunchKernelGGL(gg::k_project, dim3(blocks_for((g.N + 63) / 64 * 64 * g.entries, gg::kPB, 16384)), dim3(gg::kPB), 0, nullptr, c,
                        g, in, tb);
     HIPCHECK(hipGetLastError());
@@ -1127,6 +1204,18 @@ struct GpuGarbler::Impl {
         }
         return S;
     }
+    // grow-only payload bank (k_payloads), same lifetime rules as S
+    u128* PB = nullptr;
+    size_t PB_bytes = 0;
+    u128* pbank(size_t rows, int64_t N) {
+        const size_t bytes = std::max<size_t>(16, rows * static_cast<size_t>(N) * sizeof(u128));
+        if (bytes > PB_bytes) {
+            if (PB) (void)hipFree(PB);
+            HIPCHECK(hipMalloc(reinterpret_cast<void**>(&PB), bytes));
+            PB_bytes = bytes;
+        }
+        return PB;
+    }
     std::vector<DevBlock> alloc_labels(const std::vector<int>& mods, int64_t N) {
         std::vector<DevBlock> v(mods.size());
         for (size_t j = 0; j < mods.size(); ++j)
@@ -1143,6 +1232,7 @@ struct GpuGarbler::Impl {
         cur.clear();
         for (void* p : owned) (void)hipFree(p);
         if (S) (void)hipFree(S);
+        if (PB) (void)hipFree(PB);
         if (ring_h) (void)hipHostFree(ring_h);
         if (ring_d) (void)hipFree(ring_d);
     }
@@ -1212,6 +1302,13 @@ void GpuGarbler::to_host(CrtLabels& cur) {
     }
 }
 
+// Conv base labels = the evaluator's garbled conv applied to the zero labels:
+// y = W x + (#zero weights + 1) Z (the +1 is the bias label's Z_p, the bias
+// itself being public). The labels are transposed to the evaluator's
+// component-major layout and run through the same int8 MFMA implicit-GEMM
+// kernel (launch_conv: k_conv_img, one launch for all residues); public
+// weights, zero counts and the all-zero bias rows are cached per process.
+// DASH_GG_CONV=valu selects the label-major VALU kernel (A/B).
 void GpuGarbler::conv(const ConvGeom& G, const std::vector<i64>& w, CrtLabels& cur) {
     Impl& I = *impl_;
     HIPCHECK(hipSetDevice(I.device));
@@ -1219,40 +1316,116 @@ void GpuGarbler::conv(const ConvGeom& G, const std::vector<i64>& w, CrtLabels& c
     PhaseTrace tr_("conv");
     const int K = static_cast<int>(G.K());
     const int F = static_cast<int>(G.F);
-    const int nch = (F + gg::kFT - 1) / gg::kFT;
     DASH_CHECK(static_cast<i64>(w.size()) == G.F * G.K(), "gpu garbler: conv weight shape");
     DASH_CHECK(G.C * G.H * G.W == I.cur_N, "gpu garbler: conv input size mismatch");
+    DASH_CHECK(static_cast<int>(I.cur_mod.size()) <= kMaxRes, "gpu garbler: too many residues");
     std::vector<int> mods = I.cur_mod;
-    std::vector<DevBlock> out = I.alloc_labels(mods, G.out_size());
+    const int64_t Nin = I.cur_N, Nout = G.out_size();
+    std::vector<DevBlock> out = I.alloc_labels(mods, Nout);
     std::vector<void*> tmp;
-    for (size_t j = 0; j < mods.size(); ++j) {
-        const int p = mods[j];
-        std::vector<int32_t> wp(static_cast<size_t>(nch) * K * gg::kFT, 0), zc(static_cast<size_t>(nch) * gg::kFT, 0);
-        for (int f = 0; f < F; ++f) {
-            int z = 1;
-            for (int kk = 0; kk < K; ++kk) {
-                const int v = static_cast<int>(w[static_cast<size_t>(f) * K + kk] % p);
-                if (v == 0) ++z;
-                wp[(static_cast<size_t>(f / gg::kFT) * K + kk) * gg::kFT + f % gg::kFT] = v;
+    static const bool valu = [] {
+        const char* e = std::getenv("DASH_GG_CONV");
+        return e && std::string(e) == "valu";
+    }();
+    if (valu) {
+        const int nch = (F + gg::kFT - 1) / gg::kFT;
+        for (size_t j = 0; j < mods.size(); ++j) {
+            const int p = mods[j];
+            std::vector<int32_t> wp(static_cast<size_t>(nch) * K * gg::kFT, 0), zc(static_cast<size_t>(nch) * gg::kFT, 0);
+            for (int f = 0; f < F; ++f) {
+                int z = 1;
+                for (int kk = 0; kk < K; ++kk) {
+                    const int v = static_cast<int>(w[static_cast<size_t>(f) * K + kk] % p);
+                    if (v == 0) ++z;
+                    wp[(static_cast<size_t>(f / gg::kFT) * K + kk) * gg::kFT + f % gg::kFT] = v;
+                }
+                zc[f] = z;
             }
-            zc[f] = z;
+            gg::ConvG g{static_cast<int>(G.C), static_cast<int>(G.H), static_cast<int>(G.W), F, static_cast<int>(G.kh),
+                        static_cast<int>(G.kw), static_cast<int>(G.sh), static_cast<int>(G.sw), static_cast<int>(G.ph),
+                        static_cast<int>(G.pw), static_cast<int>(G.OH), static_cast<int>(G.OW), K, nr_comps(p), p};
+            const int32_t* dw = gg::dconst(wp.data(), wp.size());
+            const int32_t* dz = gg::dconst(zc.data(), zc.size());
+            const int64_t threads = G.OH * G.OW * static_cast<int64_t>(g.n);
+            DASH_CHECK((threads + 255) / 256 < (int64_t(1) << 31), "gpu garbler: conv grid too large");
+            hipLaunchKernelGGL(gg::k_conv_garble, dim3(static_cast<unsigned>((threads + 255) / 256), nch), dim3(256), 0,
+                               nullptr, g, I.cur[j].as<int16_t>(), out[j].as<int16_t>(), dw, dz,
+                               I.c.Z + static_cast<int64_t>(p) * gg::kW);
         }
-        gg::ConvG g{static_cast<int>(G.C), static_cast<int>(G.H), static_cast<int>(G.W), F, static_cast<int>(G.kh),
-                    static_cast<int>(G.kw), static_cast<int>(G.sh), static_cast<int>(G.sw), static_cast<int>(G.ph),
-                    static_cast<int>(G.pw), static_cast<int>(G.OH), static_cast<int>(G.OW), K, nr_comps(p), p};
-        const int32_t* dw = gg::dconst(wp.data(), wp.size());
-        const int32_t* dz = gg::dconst(zc.data(), zc.size());
-        const int64_t threads = G.OH * G.OW * static_cast<int64_t>(g.n);
-        DASH_CHECK((threads + 255) / 256 < (int64_t(1) << 31), "gpu garbler: conv grid too large");
-        hipLaunchKernelGGL(gg::k_conv_garble, dim3(static_cast<unsigned>((threads + 255) / 256), nch), dim3(256), 0,
-                           nullptr, g, I.cur[j].as<int16_t>(), out[j].as<int16_t>(), dw, dz,
-                           I.c.Z + static_cast<int64_t>(p) * gg::kW);
+    } else {
+        dev::ConvArgs a{};
+        a.crt.k = static_cast<int>(mods.size());
+        for (int j = 0; j < a.crt.k; ++j) {
+            a.crt.p[j] = mods[j];
+            a.crt.n[j] = nr_comps(mods[j]);
+            a.crt.prefix[j] = a.crt.sum;
+            a.crt.sum += mods[j];
+        }
+        a.C = static_cast<int>(G.C); a.H = static_cast<int>(G.H); a.W = static_cast<int>(G.W);
+        a.F = F; a.kh = static_cast<int>(G.kh); a.kw = static_cast<int>(G.kw);
+        a.sh = static_cast<int>(G.sh); a.sw = static_cast<int>(G.sw);
+        a.ph = static_cast<int>(G.ph); a.pw = static_cast<int>(G.pw);
+        a.OH = static_cast<int>(G.OH); a.OW = static_cast<int>(G.OW);
+        a.Kpad = (K + 63) / 64 * 64;
+        a.use_mfma = 1;
+        dev::conv_img_geometry(a);
+        a.zero = I.c.Z;  // one GC: zero label component c of residue j at Z[p_j * kW + c]
+        a.lab_stride = 0;
+        a.img_off[0] = 0;
+        const int F16 = (F + 15) / 16 * 16;
+        for (int j = 0; j < a.crt.k; ++j) {
+            const int p = mods[j], n = a.crt.n[j];
+            a.lab_off[j] = p * gg::kW;
+            a.img_off[j + 1] = a.img_off[j] + n;
+            std::vector<int16_t> wm(static_cast<size_t>(F) * K);
+            std::vector<int8_t> w8(static_cast<size_t>(F) * a.Kpad, 0);
+            std::vector<int32_t> zc(F, 1);
+            for (int f = 0; f < F; ++f)
+                for (int q = 0; q < K; ++q) {
+                    const int v = static_cast<int>(w[static_cast<size_t>(f) * K + q] % p);
+                    wm[static_cast<size_t>(f) * K + q] = static_cast<int16_t>(v);
+                    if (v == 0) ++zc[f];
+                    w8[static_cast<size_t>(f) * a.Kpad + q] = static_cast<int8_t>(v > p / 2 ? v - p : v);
+                }
+            a.w[j] = gg::dconst(wm.data(), wm.size());
+            a.zc[j] = gg::dconst(zc.data(), zc.size());
+            std::vector<int16_t> zb(static_cast<size_t>(F) * n, 0);
+            a.bias[j] = gg::dconst(zb.data(), zb.size());
+            a.w8[j] = nullptr;
+            a.w8r[j] = nullptr;
+            if (p <= 255 && a.nbands > 0) {
+                std::vector<int8_t> w8r(static_cast<size_t>(F16) * G.kh * G.kw * a.Cpad, 0);
+                for (int f = 0; f < F; ++f)
+                    for (int ci = 0; ci < a.C; ++ci)
+                        for (int dy = 0; dy < a.kh; ++dy)
+                            for (int dx = 0; dx < a.kw; ++dx)
+                                w8r[((static_cast<size_t>(f) * a.kh + dy) * a.kw + dx) * a.Cpad + ci] =
+                                    w8[static_cast<size_t>(f) * a.Kpad + (ci * a.kh + dy) * a.kw + dx];
+                a.w8r[j] = gg::dconst(w8r.data(), w8r.size());
+            } else if (p <= 255) {
+                a.w8[j] = gg::dconst(w8.data(), w8.size());
+            }
+        }
+        // label-major [N][n] <-> component-major [n][N] around the evaluator kernel
+        std::vector<DevBlock> xin = I.alloc_labels(mods, Nin), yout = I.alloc_labels(mods, Nout);
+        dev::Act x{}, y{};
+        x.N = Nin;
+        y.N = Nout;
+        for (int j = 0; j < a.crt.k; ++j) {
+            dev::launch_transpose16(I.cur[j].as<int16_t>(), xin[j].as<int16_t>(), Nin, a.crt.n[j], nullptr);
+            x.p[j] = xin[j].as<int16_t>();
+            y.p[j] = yout[j].as<int16_t>();
+        }
+        dev::launch_conv(a, x, y, 1, nullptr);
+        for (int j = 0; j < a.crt.k; ++j)
+            dev::launch_transpose16(yout[j].as<int16_t>(), out[j].as<int16_t>(), a.crt.n[j], Nout, nullptr);
+        // xin / yout return to the block cache; later users are ordered behind these kernels on the null stream
     }
     HIPCHECK(hipGetLastError());
     gg::end_layer(tmp);
     tr_.mark("kernels");
     I.cur = std::move(out);
-    I.cur_N = G.out_size();
+    I.cur_N = Nout;
     set_stale(cur, mods, I.cur_N);
 }
 
@@ -1283,7 +1456,7 @@ void GpuGarbler::sign_layer(uint64_t layer, const SignPlan& sp, CrtLabels& cur, 
     tb.t[3] = tS.p(); tb.row[3] = tS.row;
     if (relu) {
         tG.alloc(I.device, N, mmg->shape[1]);
-        tE.alloc(I.device, N, static_cast<int64_t>(k) * 3);
+        tE.alloc(I.device, N, static_cast<int64_t>(k) * 3, true);
         tb.t[4] = tG.p(); tb.row[4] = tG.row;
         tb.t[5] = tE.p(); tb.row[5] = tE.row;
     }
@@ -1298,6 +1471,7 @@ void GpuGarbler::sign_layer(uint64_t layer, const SignPlan& sp, CrtLabels& cur, 
     g.sslot = 1;
     g.mask = 0;
     g.S = S;
+    g.PB = I.pbank(std::max<size_t>(2, L.pays.size()), N);
     g.N = N;
     g.nslots = L.nslots;
     run_sign(I.c, L, g, in, tb, tmp);
@@ -1348,8 +1522,13 @@ void GpuGarbler::sign_layer(uint64_t layer, const SignPlan& sp, CrtLabels& cur, 
         ma.sig_slot = L.out_slot0;
         ma.sk_slot0 = sk0;
         for (int j = 0; j < k; ++j) ma.out[j] = out[j].as<int16_t>();
+        // the sign gadget's payload bank (>= 2 rows, its readers are done: same stream) now holds the two
+        // mini-gate key hashes of the sign output
+        hipLaunchKernelGGL(gg::k_bin_keys, dim3(blocks_for(N, gg::kGB, 8192)), dim3(gg::kGB), 0, nullptr, I.c,
+                           S + static_cast<int64_t>(L.out_slot0) * gg::kW, static_cast<int64_t>(L.nslots) * gg::kW,
+                           static_cast<const int16_t*>(nullptr), g.PB, N);
         hipLaunchKernelGGL(gg::k_relu_finish, dim3(blocks_for(N * k, 256, 8192)), dim3(256), 0, nullptr, I.c, gm, in,
-                           tb, ma);
+                           tb, ma, static_cast<const u128*>(g.PB));
         tG.to_array(*mmg, I.device);
         tE.to_array(*mme, I.device);
     } else {
@@ -1421,9 +1600,14 @@ void GpuGarbler::rescale_legacy_iter(uint64_t layer, int it, const RescalePlan& 
         ra.ctr[j] = ctr;
         ctr += (nr_comps(I.crt[j]) + 1) / 2;
     }
-    hipLaunchKernelGGL(gg::k_rescale_pre, dim3(blocks_for(N * (k - 1), gg::kGB, 8192)), dim3(gg::kGB), 0, nullptr, I.c,
-                       ra, tb, N);
     gg::SignLayout L = gg::sign_layout(P.sign, 0);
+    // the payload bank is sized once for both users: rows 0-1 hold the trans key hashes until the sign gadget's
+    // k_payloads (later on the same stream) overwrites them
+    u128* PB = I.pbank(std::max<size_t>(2, L.pays.size()), N);
+    hipLaunchKernelGGL(gg::k_bin_keys, dim3(blocks_for(N, gg::kGB, 8192)), dim3(gg::kGB), 0, nullptr, I.c, ra.L[0],
+                       int64_t(128), ra.up, PB, N);
+    hipLaunchKernelGGL(gg::k_rescale_pre, dim3(blocks_for(N * (k - 1), gg::kGB, 8192)), dim3(gg::kGB), 0, nullptr, I.c,
+                       ra, tb, PB, N);
     int16_t* S = I.scratch(static_cast<size_t>(N) * L.nslots * gg::kW * sizeof(int16_t));
     gg::In in{};
     for (int j = 0; j < k; ++j) {
@@ -1438,6 +1622,7 @@ void GpuGarbler::rescale_legacy_iter(uint64_t layer, int it, const RescalePlan& 
     g.sslot = 10 + it;
     g.mask = 1ull << 43;  // nested sign stream (rescale_garble_elem)
     g.S = S;
+    g.PB = I.pbank(std::max<size_t>(2, L.pays.size()), N);
     g.N = N;
     g.nslots = L.nslots;
     run_sign(I.c, L, g, in, tb, tmp);

@@ -34,12 +34,14 @@ constexpr int kAesBlock = DASH_AES_BLOCK;
 constexpr int kAesMinBlocks = DASH_AES_MINBLOCKS;  // sets the VGPR budget (2048/block -> 64 VGPRs)
 
 // AES kernels stride over their elements so the LDS image is filled once per
-// resident block: two resident blocks per CU, x4 for tail balance.
+// resident block: resident blocks per CU (LDS image / VGPR bound), x4 for tail
+// balance (64 KiB image: 2 per CU).
 static int aes_block_cap() {
     static int cap = [] {
         int dev = 0, cus = 256;
         if (hipGetDevice(&dev) == hipSuccess) hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-        return 8 * cus * 512 / kAesBlock;
+        const int resident = std::max(1, std::min(kAesMinBlocks * kAesBlock / 512, 160 * 1024 / DASH_AES_LDS_BYTES));
+        return 4 * resident * cus * 512 / kAesBlock;
     }();
     return cap;
 }

@@ -146,6 +146,28 @@ void launch_window_sum(const Act& in, int64_t Nin, const Act& out, int64_t Nout,
     hipLaunchKernelGGL(k_window_sum, g1(Nout * nmax(crt), crt.k, B), dim3(256), 0, st, in, Nin, out, Nout, idx, K,
                        crt);
 }
+// out[c][r] = in[r][c]: 64x64 tiles through LDS (row pitch 65: conflict-free
+// column reads), both global sides coalesced. grid (ceil(cols/64), ceil(rows/64))
+__global__ __launch_bounds__(256) void k_transpose16(const int16_t* __restrict__ in, int16_t* __restrict__ out,
+                                                     int64_t rows, int64_t cols) {
+    __shared__ int16_t t[64][65];
+    const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+    const int64_t c0 = static_cast<int64_t>(blockIdx.x) * 64, r0 = static_cast<int64_t>(blockIdx.y) * 64;
+    for (int y = ty; y < 64; y += 4) {
+        const int64_t r = r0 + y, c = c0 + tx;
+        if (r < rows && c < cols) t[y][tx] = in[r * cols + c];
+    }
+    __syncthreads();
+    for (int y = ty; y < 64; y += 4) {
+        const int64_t c = c0 + y, r = r0 + tx;
+        if (r < rows && c < cols) out[c * rows + r] = t[tx][y];
+    }
+}
+void launch_transpose16(const int16_t* in, int16_t* out, int64_t rows, int64_t cols, hipStream_t st) {
+    hipLaunchKernelGGL(k_transpose16, dim3(static_cast<unsigned>((cols + 63) / 64), static_cast<unsigned>((rows + 63) / 64)),
+                       dim3(256), 0, st, in, out, rows, cols);
+}
+
 void launch_aes_test(const u128* in, u128* out, int64_t n, const AesGlobals& g, hipStream_t st) {
     const unsigned nb = static_cast<unsigned>(std::min<int64_t>((n + 511) / 512, 2048));
     hipLaunchKernelGGL(k_aes_test, dim3(nb), dim3(512), 0, st, in, out, n, g.te0, g.rk);

@@ -78,5 +78,25 @@ struct ConvArgs {
 };
 void launch_conv(const ConvArgs& a, const Act& x, const Act& y, int B, hipStream_t st);
 
+// k_conv_img geometry: 64-channel chunks (Cpad) and the tallest band of output
+// rows whose input rows fit the 64 KiB LDS image; nbands = 0 if none fits
+// (launch_conv then uses the im2col MFMA kernel).
+inline void conv_img_geometry(ConvArgs& a) {
+    a.Cpad = (a.C + 63) / 64 * 64;
+    const int64_t row_bytes = static_cast<int64_t>(a.W + 2 * a.pw) * (a.Cpad + 16);
+    int band = a.OH;
+    while (band > 1 && ((band - 1) * a.sh + a.kh) * row_bytes > 65536) --band;
+    if (((band - 1) * a.sh + a.kh) * row_bytes <= 65536) {
+        a.band = band;
+        a.nbands = (a.OH + band - 1) / band;
+    } else {
+        a.band = 0;
+        a.nbands = 0;
+    }
+}
+
+// int16 matrix transpose out[c][r] = in[r][c] (label-major <-> component-major), kernels_label.hip
+void launch_transpose16(const int16_t* in, int16_t* out, int64_t rows, int64_t cols, hipStream_t st);
+
 }  // namespace dev
 }  // namespace dash

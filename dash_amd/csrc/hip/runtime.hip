@@ -614,19 +614,13 @@ void HipEvaluator::build() {
                 a.Kpad = static_cast<int>((K + 63) / 64 * 64);
                 a.use_mfma = mfma_ ? 1 : 0;
                 // LDS-image kernel geometry: 64-channel chunks, row bands that fit 64 KiB of LDS
-                a.Cpad = static_cast<int>((G.C + 63) / 64 * 64);
                 {
-                    const i64 row_bytes = (G.W + 2 * G.pw) * (a.Cpad + 16);
-                    i64 band = G.OH;
-                    while (band > 1 && ((band - 1) * G.sh + G.kh) * row_bytes > 65536) --band;
                     static const bool img_ok = [] {
                         const char* e = std::getenv("DASH_CONV_IMG");
                         return !(e && e[0] == '0');
                     }();
-                    if (((band - 1) * G.sh + G.kh) * row_bytes <= 65536 && mfma_ && img_ok) {
-                        a.band = static_cast<int>(band);
-                        a.nbands = static_cast<int>((G.OH + band - 1) / band);
-                    }
+                    conv_img_geometry(a);
+                    if (!(mfma_ && img_ok)) a.band = a.nbands = 0;
                 }
                 a.img_off[0] = 0;
                 for (int j = 0; j < k_; ++j) a.img_off[j + 1] = a.img_off[j] + static_cast<i64>(B_) * crt.n[j];

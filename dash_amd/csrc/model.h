@@ -101,6 +101,7 @@ struct GarbleOptions {
     int nthreads = 0;
     int device = -1;  // >= 0: garble ReLU / Sign / legacy rescale layers on this GPU
     bool fused_sign = true;  // sign gadget construction (gadgets.h SignPlan::fused); false: reference casts
+    bool rescale_mrs = false;  // legacy (l-halving) rescale as one mixed-radix gadget (gadgets.h RescaleMrsPlan)
 };
 
 class Garbler {

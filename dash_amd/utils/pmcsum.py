@@ -16,17 +16,19 @@ from collections import defaultdict
 def load(paths):
     agg = defaultdict(lambda: defaultdict(float))
     times = defaultdict(dict)
+    cpass = defaultdict(dict)  # kernel -> counter -> pass (file) it was collected in
     for p in paths:
         with open(p) as f:
             for r in csv.DictReader(f):
                 k = re.sub(r"\(.*", "", r["Kernel_Name"]).replace("void ", "")
                 agg[k][r["Counter_Name"]] += float(r["Counter_Value"])
+                cpass[k][r["Counter_Name"]] = p
                 times[k][(p, r["Dispatch_Id"])] = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6
-    return agg, times
+    return agg, times, cpass
 
 
 def main(paths):
-    agg, times = load(paths)
+    agg, times, cpass = load(paths)
     rows = []
     for k, c in agg.items():
         # time per pass: counters of different passes come from different dispatches
@@ -44,15 +46,15 @@ def main(paths):
         if c.get("SQ_WAVES"):
             d["valu_insts/wave"] = c.get("SQ_INSTS_VALU", 0) / c["SQ_WAVES"]
             d["vmem_rd/wave"] = c.get("SQ_INSTS_VMEM_RD", 0) / c["SQ_WAVES"]
-        if "FETCH_SIZE" in c and ms_by_pass:
-            p2 = [p for p in ms_by_pass if any(x == p for x, _ in times[k])]
-            fms = ms_by_pass[p2[-1]] if p2 else ms
-            d["fetch_GB"] = c["FETCH_SIZE"] * 1024 / 1e9
-            d["fetch_TB/s"] = d["fetch_GB"] / max(fms, 1e-9)
+        for ctr, name in (("FETCH_SIZE", "fetch"), ("WRITE_SIZE", "write")):
+            if ctr in c and ms_by_pass:
+                pms = ms_by_pass.get(cpass[k][ctr], ms)  # time of the pass that collected this counter
+                d[f"{name}_GB"] = c[ctr] * 1024 / 1e9
+                d[f"{name}_TB/s"] = d[f"{name}_GB"] / max(pms, 1e-9)
         rows.append(d)
     rows.sort(key=lambda r: -r["ms"])
     cols = ["kernel", "ms", "dispatch", "valu%", "active%", "wait%", "stall%", "valu_insts/wave", "vmem_rd/wave",
-            "fetch_GB", "fetch_TB/s"]
+            "fetch_GB", "fetch_TB/s", "write_GB", "write_TB/s"]
     print(" ".join(f"{c:>14s}" if c != "kernel" else f"{c:40s}" for c in cols))
     for r in rows[:25]:
         out = []

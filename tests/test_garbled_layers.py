@@ -300,3 +300,64 @@ def test_fused_sign_drops_cast_tables_and_roundtrips():
     assert m2.sign_fused
     gf.model = m2
     np.testing.assert_array_equal(gf.decode_outputs(gf.cpu_evaluate(gf.garble_inputs(vals))), np.maximum(vals, 0))
+
+
+# ------------------------------------------- mixed-radix rescale (construction of the legacy function)
+def _mrs_shift(M, S):
+    """(U, q) of gadgets.h RescaleMrsPlan: x_u = (x + U) mod M, y = floor(x_u / S) - q."""
+    h = M // 2
+    U = h + (S - 1 - h % S) % S
+    return U, (U - (S - 1)) // S
+
+
+@pytest.mark.parametrize("k,l", [(7, 5), (7, 1), (8, 3), (9, 2), (4, 4)])
+def test_rescale_mrs_equals_legacy_function(k, l):
+    """ceil(x / 2^l) on the whole signed range except the top U - M/2 values (which wrap)."""
+    c0 = d.Circuit([d.Rescale(l, (1,))])
+    M = GarbledCircuit(c0, k, 100.0, seed=SEED, garble_me=False).crt_modulus
+    S = 1 << l
+    U, q = _mrs_shift(M, S)
+    top = M // 2 - (U - M // 2)  # first wrapping value
+    rng = np.random.default_rng(k * 100 + l)
+    vals = [v for v in RESCALE_VALS if -M // 2 <= v < top]
+    vals += [-M // 2, -M // 2 + 1, top - 1, top - 2, 0, S, -S, S - 1, 1 - S]
+    vals += list(rng.integers(-M // 2, top, 48))
+    x = np.array(vals, dtype=np.int64)
+    c = d.Circuit([d.Rescale(l, (len(x),))])
+    gc = GarbledCircuit(c, k, 100.0, seed=SEED, rescale="mrs")
+    out = gc.decode_outputs(gc.cpu_evaluate(gc.garble_inputs(x)))
+    np.testing.assert_array_equal(out, -((-x) // S))
+    # == the legacy gadget's plaintext semantics (l halvings) on this domain
+    np.testing.assert_array_equal(out, c.plain_q_eval(x, False, M))
+    # the wrapping top values follow floor(((x + U) mod M) / S) - q
+    xt = np.arange(top, M // 2, dtype=np.int64)
+    if xt.size:
+        ct = d.Circuit([d.Rescale(l, (xt.size,))])
+        gt = GarbledCircuit(ct, k, 100.0, seed=SEED, rescale="mrs")
+        ot = gt.decode_outputs(gt.cpu_evaluate(gt.garble_inputs(xt)))
+        exp = ((xt + U) % M) // S - q
+        exp = np.where(exp >= M // 2, exp - M, exp)
+        np.testing.assert_array_equal(ot, exp)
+
+
+def test_rescale_mrs_tables_and_model():
+    """One table per rescale layer (no sign gadget), far smaller than the legacy l iterations; a conv ->
+    rescale -> relu -> dense model garbled with it decodes to the plaintext quantized output."""
+    from dash_amd.ir.quant import QuantizationMethod as Q
+    from dash_amd.models import build_circuit, quantized_inputs
+
+    c = build_circuit("MODEL_B_POOL_REPL", Q.ScaleQuant, 3, seed=1)
+    xs = quantized_inputs("MODEL_B_POOL_REPL", 3, Q.ScaleQuant, 3, seed=5)
+    new = GarbledCircuit(c, 8, 100.0, seed=SEED, rescale="mrs")
+    old = GarbledCircuit(c, 8, 100.0, seed=SEED)
+    assert new.table_bytes < old.table_bytes / 2
+    for x in xs:
+        y = new.decode_outputs(new.cpu_evaluate(new.garble_inputs(x)))
+        np.testing.assert_array_equal(y, new.plain_q_eval(x))
+    from dash_amd.native import native
+
+    blob = new.model.serialize()
+    m2 = native().GarbledModel.deserialize(blob)
+    assert m2.serialize() == blob
+    y = new.decode_outputs(native().cpu_evaluate(m2, new.garble_inputs(xs[0]), 0))
+    np.testing.assert_array_equal(y, new.plain_q_eval(xs[0]))
