@@ -156,6 +156,7 @@ std::vector<u128> compress_labels(const CrtLabels& L, int nthreads = 0);
 CrtLabels decompress_labels(const u128* C, const std::vector<int>& moduli, i64 N, int nthreads = 0);
 
 // Required moduli (for R/Z banks) given bases.
-int required_max_modulus(const std::vector<int>& crt, const std::vector<int>& mrs, const std::vector<LayerSpec>& layers);
+int required_max_modulus(const std::vector<int>& crt, const std::vector<int>& mrs, const std::vector<LayerSpec>& layers,
+                         bool rescale_mrs = false);
 
 }  // namespace dash

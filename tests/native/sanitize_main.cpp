@@ -24,8 +24,8 @@ int main() {
     int fails = 0;
     const std::string seed(16, 'z');
     std::mt19937 rng(7);
-    // dense 16 -> 8, relu, rescale (legacy l = 1), sign
-    {
+    // dense 16 -> 8, relu, rescale (legacy l = 1: sign-gadget and mixed-radix constructions), sign
+    for (int mrs_rescale = 0; mrs_rescale < 2; ++mrs_rescale) {
         const i64 I = 16, O = 8;
         std::vector<i64> W(I * O), b(O), x(I);
         for (auto& v : W) v = static_cast<i64>(rng() % 7) - 3;
@@ -44,9 +44,10 @@ int main() {
         L[3].kind = K_SIGN;
         const std::vector<int> crt = first_primes(8);
         const std::vector<int> mrs = {102, 7, 7, 6, 6, 6};
-        Garbler g(crt, mrs, seed, required_max_modulus(crt, mrs, L));
+        Garbler g(crt, mrs, seed, required_max_modulus(crt, mrs, L, mrs_rescale != 0));
         GarbleOptions opt;
         opt.nthreads = 8;
+        opt.rescale_mrs = mrs_rescale != 0;
         GarbledModel m = g.garble(L, {I}, opt);
         CrtLabels in = g.encode(x);
         CrtLabels out = cpu_evaluate(m, in, 8);
@@ -58,7 +59,8 @@ int main() {
             acc = (acc + 1) / 2;  // legacy rescale rounds up (ceil(x / 2) for x >= 0)
             want[o] = acc >= 0 ? 1 : -1;
         }
-        fails += check("dense+relu+rescale+sign", g.decoder().decode(out), want);
+        fails += check(mrs_rescale ? "dense+relu+rescale(mrs)+sign" : "dense+relu+rescale+sign", g.decoder().decode(out),
+                       want);
     }
     // conv 2x6x6 -> 3x6x6 (3x3, pad 1), maxpool 2x2, ReDash rescale by the first modulus
     {

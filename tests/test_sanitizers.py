@@ -34,4 +34,4 @@ def test_host_sanitizers(tmp_path):
         log = r.stdout + r.stderr
         assert r.returncode == 0, f"{k} run failed:\n{log[-4000:]}"
         assert "runtime error" not in log and "ThreadSanitizer" not in log and "AddressSanitizer" not in log, log
-        assert log.count(" ok") == 2
+        assert log.count(" ok") == 3
