@@ -49,6 +49,9 @@ def main() -> None:
     ap.add_argument("--sign", default=os.environ.get("DASH_BENCH_SIGN", "fused"), choices=["fused", "reference"],
                     help="sign-gadget construction: casts folded into the approx/carry projections (fused) or the "
                          "reference's explicit cast gates; both compute the same function")
+    ap.add_argument("--rescale", default=os.environ.get("DASH_BENCH_RESCALE", "legacy"), choices=["mrs", "legacy"],
+                    help="construction of the DASH rescale ceil(x/2^l): one exact mixed-radix conversion (mrs) or the "
+                         "reference's l sign-gadget halvings (legacy); same function on the signed range")
     ap.add_argument("--streams", type=int, default=int(os.environ.get("DASH_BENCH_STREAMS", "4")),
                     help="independent GC groups per GPU, each on its own HIP stream (overlap latency- and "
                          "bandwidth-bound phases)")
@@ -108,7 +111,7 @@ def main() -> None:
         seed = hashlib.sha256(f"dash-bench/{rank}/{b}/{os.getpid()}".encode()).digest()[:16]
         t = time.perf_counter()
         gc = GarbledCircuit(circuit, cfg["crt"], cfg["mrs"], seed=seed, device=device if args.garble_device else None,
-                            fused_sign=args.sign == "fused")
+                            fused_sign=args.sign == "fused", rescale=args.rescale)
         garble_s += time.perf_counter() - t
         if b == 0:
             # HBM guard: every GC's tables stay resident. Size B from the real device footprint of one GC
@@ -249,6 +252,7 @@ def main() -> None:
                 "gcs_per_gpu": B,
                 "streams": G,
                 "sign_construction": args.sign,
+                "rescale_construction": args.rescale,
                 "seq_len": None,
                 "input_shape": [3, 32, 32],
                 "parallelism": f"dp{world}",

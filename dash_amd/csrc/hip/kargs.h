@@ -73,6 +73,19 @@ struct RescaleArgs {
     int lab_off[kMaxRes];  // offset of residue j inside up/zero rows
 };
 
+// Single-shot mixed-radix rescale (gadgets.h RescaleMrsPlan)
+struct MrsArgs {
+    CrtInfo crt;
+    int T;                         // 2^(l+1): modulus of the x_u mod 2S label (power of two)
+    int64_t N, n_tab;
+    const u128* tab;               // [B][N][n_tab]
+    int64_t dig_off[kMaxRes];      // digit i rows: [color][k - i]
+    int64_t fin_off;               // final rows: [color][k]
+    int sinv[kMaxRes];             // S^-1 mod p_j (j >= 1)
+    u128 hmask;                    // top bit of every log2(T)-bit field (packed mod-T additions)
+    u128* pf;                      // [B][k][N] final payloads (chain -> output kernel)
+};
+
 struct BEArgs {
     int E, nonext;
     int swapped[kMaxRes];    // moduli in MRS order

@@ -12,6 +12,9 @@
 //            fully in registers, no device malloc (reference uses new[]).
 //   phase C  one lane per (GC, residue, element): ReLU mixed-mod multiply, no
 //            AES at all (hashes come from phases A/B).
+#include <cstdio>
+#include <cstdlib>
+
 #include "kargs.h"
 #include "launch.h"
 
@@ -639,6 +642,126 @@ void launch_rescale_update_approx(const RescaleArgs& r, const SignArgs& a, const
     else
         hipLaunchKernelGGL(k_rescale_update_approx<8>, grid_aes(r.N, kAesBlock, r.crt.k, B), dim3(kAesBlock), kAesLds, st, r, a, x,
                            delta, zh, mc, g.te0, g.rk);
+}
+
+// ---------------------------------------------------------------------------
+// Single-shot mixed-radix rescale (gadgets.h RescaleMrsPlan): the serial part
+// runs one lane per (GC, element), K (the CRT size) is a template parameter so
+// the payload matrix P[l][j] (digit l -> later residue j) lives in registers
+// with static indices. Digit i's key is residue i's label minus the payloads
+// of the earlier digits, streamed from HBM, compressed and hashed; its row
+// ([color][K - i] contiguous entries) is gathered while the AES runs. The
+// power-of-two label r = x_u mod 2S is accumulated packed (per-field adds, no
+// decompress), its hash selects the final row; the K final payloads go to
+// a.pf for the elementwise output kernel.
+__device__ __forceinline__ u128 add_packed(u128 a, u128 b, u128 hmask) {
+    return ((a & ~hmask) + (b & ~hmask)) ^ ((a ^ b) & hmask);
+}
+
+template <int K>
+__global__ __launch_bounds__(kAesBlock, DASH_UA_MINBLOCKS) void k_rescale_mrs_chain(MrsArgs a, Act x, const ModC* mc,
+                                                                                  const uint32_t* te0,
+                                                                                  const uint32_t* rk) {
+    AES_PROLOGUE(te0, rk);
+    const int b = blockIdx.z;
+    const int64_t N = a.N;
+    for (int64_t e = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; e < N;
+         e += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+        const u128* row0 = a.tab + (static_cast<int64_t>(b) * N + e) * a.n_tab;
+        u128 P[K][K];  // P[l][j], l < j: payload of digit l for residue j (hash removed)
+        u128 acc = 0;
+#pragma unroll
+        for (int i = 0; i < K; ++i) {
+            const ModC m = mc[a.crt.p[i]];
+            const int n = static_cast<int>(m.n);
+            const int16_t* L = x.p[i] + static_cast<int64_t>(b) * n * N + e;
+            DigitStream ds[K > 1 ? K - 1 : 1];
+#pragma unroll
+            for (int l = 0; l < i; ++l) ds[l].init(P[l][i]);
+            CompressFwd cf;
+            cf.init();
+            uint32_t col = 0;
+            for (int c0 = 0; c0 < n; c0 += kChunk) {
+                uint16_t v[kChunk];
+#pragma unroll
+                for (int u = 0; u < kChunk; ++u)
+                    if (c0 + u < n) v[u] = static_cast<uint16_t>(L[static_cast<int64_t>(c0 + u) * N]);
+#pragma unroll
+                for (int u = 0; u < kChunk; ++u)
+                    if (c0 + u < n) {
+                        uint32_t d = v[u];
+#pragma unroll
+                        for (int l = 0; l < i; ++l) {
+                            const uint32_t s = ds[l].next(m);
+                            d = d >= s ? d - s : d + m.q - s;
+                        }
+                        if (c0 + u == 0) col = d;
+                        cf.push(d, m);
+                    }
+            }
+            const u128* row = row0 + a.dig_off[i] + static_cast<int64_t>(col) * (K - i);
+            u128 E[K];
+#pragma unroll
+            for (int t = 0; t < K - i; ++t) E[t] = row[t];
+            const u128 H = aes_encrypt(aes, cf.finish());
+#pragma unroll
+            for (int t = 0; t + 1 < K - i; ++t) P[i][i + 1 + t] = E[t] - H;
+            acc = add_packed(acc, E[K - 1 - i] - H, a.hmask);
+        }
+        const uint32_t col = static_cast<uint32_t>(acc) & static_cast<uint32_t>(a.T - 1);
+        const u128* row = row0 + a.fin_off + static_cast<int64_t>(col) * K;
+        u128 F[K];
+#pragma unroll
+        for (int j = 0; j < K; ++j) F[j] = row[j];
+        const u128 H = aes_encrypt(aes, acc);
+#pragma unroll
+        for (int j = 0; j < K; ++j) a.pf[(static_cast<int64_t>(b) * K + j) * N + e] = F[j] - H;
+    }
+}
+
+// Output: Y_0 = pf_0 (mod 2), Y_j = S^-1 L_j + pf_j (mod p_j), in place. grid (ceil(N/256), k, B)
+__global__ __launch_bounds__(256) void k_rescale_mrs_out(MrsArgs a, Act x, const ModC* mc) {
+    const int j = blockIdx.y, b = blockIdx.z;
+    const int64_t N = a.N;
+    const int64_t e = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (e >= N) return;
+    const int k = a.crt.k;
+    const ModC m = mc[a.crt.p[j]];
+    const int n = static_cast<int>(m.n);
+    int16_t* L = x.p[j] + static_cast<int64_t>(b) * n * N + e;
+    DigitStream s;
+    s.init(a.pf[(static_cast<int64_t>(b) * k + j) * N + e]);
+    if (j == 0) {
+        for (int c = 0; c < n; ++c) L[static_cast<int64_t>(c) * N] = static_cast<int16_t>(s.next(m));
+        return;
+    }
+    const uint32_t inv = static_cast<uint32_t>(a.sinv[j]);
+    const uint32_t q = m.q;
+    for (int c0 = 0; c0 < n; c0 += kChunk) {
+        uint16_t v[kChunk];
+#pragma unroll
+        for (int u = 0; u < kChunk; ++u)
+            if (c0 + u < n) v[u] = static_cast<uint16_t>(L[static_cast<int64_t>(c0 + u) * N]);
+#pragma unroll
+        for (int u = 0; u < kChunk; ++u)
+            if (c0 + u < n)
+                L[static_cast<int64_t>(c0 + u) * N] = static_cast<int16_t>(modq(v[u] * inv + s.next(m), m));  // < p^2 + p
+        (void)q;
+    }
+}
+
+void launch_rescale_mrs(const MrsArgs& a, const Act& x, int B, const ModC* mc, const AesGlobals& g, hipStream_t st) {
+    const dim3 gc = grid_aes(a.N, kAesBlock, 1, B);
+    switch (a.crt.k) {
+#define DASH_MRS_K(KK) \
+        case KK: hipLaunchKernelGGL(k_rescale_mrs_chain<KK>, gc, dim3(kAesBlock), kAesLds, st, a, x, mc, g.te0, g.rk); break;
+        DASH_MRS_K(2) DASH_MRS_K(3) DASH_MRS_K(4) DASH_MRS_K(5) DASH_MRS_K(6) DASH_MRS_K(7) DASH_MRS_K(8)
+        DASH_MRS_K(9) DASH_MRS_K(10) DASH_MRS_K(11) DASH_MRS_K(12)
+#undef DASH_MRS_K
+        default: std::fprintf(stderr, "dash: mixed-radix rescale supports 2..12 CRT residues\n"); std::abort();
+    }
+    hipLaunchKernelGGL(k_rescale_mrs_out, dim3(static_cast<unsigned>((a.N + 255) / 256), a.crt.k, B), dim3(256), 0, st, a,
+                       x, mc);
 }
 
 // ---------------------------------------------------------------------------

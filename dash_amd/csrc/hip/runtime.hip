@@ -440,7 +440,7 @@ void HipEvaluator::build() {
         });
     }
     bool any_rescale = false;
-    for (auto& l : m0.layers) any_rescale |= (l.kind == K_RESCALE);
+    for (auto& l : m0.layers) any_rescale |= (l.kind == K_RESCALE && l.param("mode", 0) != 2);  // mode 2: no shift labels
     if (any_rescale) up_rows_ = upload_const_rows([&](int j) { return "up." + std::to_string(j); });
 
     // ---- shape pass: buffer capacities
@@ -700,6 +700,31 @@ void HipEvaluator::build() {
             case K_RESCALE: {
                 const i64 mode = g.param("mode", 0);
                 const i64 iters = g.param("iters");
+                if (mode == 2) {  // mixed-radix construction of the legacy function (gadgets.h RescaleMrsPlan)
+                    const RescaleMrsPlan P(crt_, static_cast<int>(g.param("l")));
+                    DASH_CHECK(P.T <= m0.h.max_mod, "model lacks the mod-2^(l+1) label constants");
+                    MrsArgs a{};
+                    a.crt = crt;
+                    a.T = static_cast<int>(P.T);
+                    a.N = N;
+                    a.n_tab = P.n_tab;
+                    a.tab = upload_tables(li, "mrs");
+                    for (int i = 0; i < k_; ++i) {
+                        a.dig_off[i] = P.dig_off[i];
+                        a.sinv[i] = static_cast<int>(P.Sinv[i]);
+                    }
+                    a.fin_off = P.fin_off;
+                    const int bits = P.l + 1, nf = nr_comps(static_cast<int>(P.T));
+                    a.hmask = 0;
+                    for (int f = 0; f < nf; ++f) a.hmask |= static_cast<u128>(1) << (bits * f + bits - 1);
+                    a.pf = outP_;  // [B][k][N] <= the sign outputs' scratch
+                    Act x = act_of(cur);
+                    const ModC* mc = mc_;
+                    const AesGlobals ag = aes_;
+                    const int B = B_;
+                    add_op(lname + ".mrs", [a, x, B, mc, ag](hipStream_t st) { launch_rescale_mrs(a, x, B, mc, ag, st); });
+                    break;
+                }
                 if (mode == 0) {
                     plan_rescale_legacy(li, iters, N, crt, lname);
                     break;

@@ -17,8 +17,9 @@ def _hip(models, mfma=True):
 FUSED = pytest.mark.parametrize("fused", [True, False], ids=["fused", "refcasts"])
 
 
-def _check(circuit, crt, mrs, xs, mfma=True, plain=True, fused=True):
-    gcs = [GarbledCircuit(circuit, crt, mrs, seed=bytes([i + 1]) * 16, fused_sign=fused) for i in range(len(xs))]
+def _check(circuit, crt, mrs, xs, mfma=True, plain=True, fused=True, rescale="legacy"):
+    gcs = [GarbledCircuit(circuit, crt, mrs, seed=bytes([i + 1]) * 16, fused_sign=fused, rescale=rescale)
+           for i in range(len(xs))]
     enc = [g.garble_inputs(x) for g, x in zip(gcs, xs)]
     cpu = [g.cpu_evaluate(e) for g, e in zip(gcs, enc)]
     ev = _hip([g.model for g in gcs], mfma=mfma)
@@ -103,6 +104,27 @@ def test_rescale_legacy(fused):
     xs = [rng.integers(-100000, 100000, 300) for _ in range(2)]
     c = d.Circuit([d.Rescale(2, (300,))])
     _check(c, 9, 100.0, xs, fused=fused)
+
+
+@pytest.mark.parametrize("k,l", [(7, 5), (9, 2), (4, 1), (11, 3)])
+def test_rescale_mrs(k, l):
+    """Single-shot mixed-radix rescale (chain + output kernels) == host oracle, bit for bit."""
+    rng = np.random.default_rng(k + l)
+    c = d.Circuit([d.Rescale(l, (300,))])
+    h = GarbledCircuit(c, k, 100.0, garble_me=False).crt_modulus // 2
+    xs = [rng.integers(-h, h - (1 << l), 300) for _ in range(2)]
+    _check(c, k, 100.0, xs, rescale="mrs")
+
+
+def test_minionn_head_mrs_rescale():
+    """MiniONN conv -> rescale(l=5) -> relu at full size with the mixed-radix rescale."""
+    from dash_amd.ir.quant import QuantizationMethod as Q
+    from dash_amd.models import build_circuit, quantized_inputs
+
+    full = build_circuit("MODEL_F_MINIONN_POOL_REPL", Q.ScaleQuant, 5, seed=0)
+    c = d.Circuit(full.layers[:3])
+    xs = quantized_inputs("MODEL_F_MINIONN_POOL_REPL", 2, Q.ScaleQuant, 5, seed=3)
+    _check(c, 7, 100.0, xs, rescale="mrs")
 
 
 @pytest.mark.parametrize("crt,mrs", [([32, 97, 107], [22, 19, 15, 13]), ([32, 3, 5, 7, 11, 13, 17], [10, 9, 9, 8, 7, 7, 6])])
