@@ -49,7 +49,7 @@ def main() -> None:
     ap.add_argument("--sign", default=os.environ.get("DASH_BENCH_SIGN", "fused"), choices=["fused", "reference"],
                     help="sign-gadget construction: casts folded into the approx/carry projections (fused) or the "
                          "reference's explicit cast gates; both compute the same function")
-    ap.add_argument("--rescale", default=os.environ.get("DASH_BENCH_RESCALE", "legacy"), choices=["mrs", "legacy"],
+    ap.add_argument("--rescale", default=os.environ.get("DASH_BENCH_RESCALE", "mrs"), choices=["mrs", "legacy"],
                     help="construction of the DASH rescale ceil(x/2^l): one exact mixed-radix conversion (mrs) or the "
                          "reference's l sign-gadget halvings (legacy); same function on the signed range")
     ap.add_argument("--streams", type=int, default=int(os.environ.get("DASH_BENCH_STREAMS", "4")),

@@ -475,8 +475,7 @@ GarbledModel Garbler::garble(const std::vector<LayerSpec>& layers, const std::ve
         // legacy rescale as one mixed-radix gadget (RescaleMrsPlan)
         const bool mrs_rescale = opt.rescale_mrs && spec.kind == K_RESCALE && param1(spec.p, "mode", 0) == 0;
         const bool on_gpu = gpu && (spec.kind == K_CONV || spec.kind == K_RELU || spec.kind == K_SIGN ||
-                                    (spec.kind == K_RESCALE && param1(spec.p, "mode", 0) == 0 && crt_[0] == 2 &&
-                                     !mrs_rescale));
+                                    (spec.kind == K_RESCALE && param1(spec.p, "mode", 0) == 0 && crt_[0] == 2));
         const bool passthru = spec.kind == K_FLATTEN;
         if (on_gpu && !dev_ok) {
             gpu->to_device(cur);
@@ -665,7 +664,8 @@ GarbledModel Garbler::garble(const std::vector<LayerSpec>& layers, const std::ve
                 if (mrs_rescale) {
                     const RescaleMrsPlan P(crt_, static_cast<int>(param1(spec.p, "l")));
                     Array tab(DType::u128, {Nin, P.n_tab});
-                    parallel_for(Nin, [&](i64 b0, i64 b1) {
+                    if (on_gpu) gpu->rescale_mrs(L, P, cur, tab);
+                    else parallel_for(Nin, [&](i64 b0, i64 b1) {
                         std::vector<comp_t*> Lp(k);
                         for (i64 e = b0; e < b1; ++e) {
                             for (int j = 0; j < k; ++j) Lp[j] = cur[j].at(e);

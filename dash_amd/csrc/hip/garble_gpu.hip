@@ -43,7 +43,7 @@ constexpr int kW = 128;  // label slot width (max components)
 // label reference kinds
 enum Src : int { S_INPUT = 0, S_SLOT = 1, S_ZERO = 2 };
 // projection functions
-enum Fn : int { F_IDENT = 0, F_LUT = 1, F_DIV = 2, F_SIGN = 3, F_MULR = 4, F_NEGR = 5, F_DIVMOD = 6 };
+enum Fn : int { F_IDENT = 0, F_LUT = 1, F_DIV = 2, F_SIGN = 3, F_MULR = 4, F_NEGR = 5, F_DIVMOD = 6, F_FAN = 7 };
 // output offset kinds
 enum OutR : int { R_BANK = 0, R_INPUT = 1 };
 
@@ -142,6 +142,8 @@ struct Gadget {
     u128* PB;         // payload bank [row][N] (PayDesc rows)
     int64_t N;
     int mrs[kMaxMrs]; // MRS base of the sign gadget (per-digit output moduli of the fanned-out approx projections)
+    const int16_t* flut;  // F_FAN: payload values [a0 + i * stride + target] (reduced mod the target modulus)
+    const int* fan;       // F_FAN: target moduli [a1 + target]
 };
 
 // Stage a gadget's small descriptor array (draws / projections) in LDS so the
@@ -444,6 +446,20 @@ __global__ __launch_bounds__(kPB) void k_project(Ctx c, Gadget g, In in, Tables 
             }
             continue;
         }
+        if (P.fn == F_FAN) {
+            // generic fan-out: target d writes slot out_slot + d, modulus fan[a1 + d], value flut[a0 + i * t + d]
+            const int t = P.stride;
+            u128* row = tb.t[P.table] + e * tb.row[P.table] + P.off + static_cast<int64_t>(color) * t;
+            for (int d = 0; d < t; ++d) {
+                const int pout = rfl(g.fan[P.a1 + d]);
+                const ModC md = rfl_modc(c.mc[pout]);
+                const uint32_t cm = static_cast<uint32_t>(rfl(g.flut[P.a0 + i * t + d]));
+                const int16_t* ol = g.S + (e * g.nslots + P.out_slot + d) * kW;
+                const u128 pay = proj_payload(ol, c.R + static_cast<int64_t>(pout) * kW, cm, md);
+                if (e_raw < N) row[d] = pay + H;
+            }
+            continue;
+        }
         if (P.pay1 > 0) {
             // few distinct payloads: precomputed per element by k_payloads
             const int idx = P.fn == F_SIGN ? (i < P.a0 ? 1 : 0) : i / P.a0;  // F_SIGN: 0 lower / 1 upper; F_DIV(MOD): i / m
@@ -476,6 +492,53 @@ __global__ __launch_bounds__(kPB) void k_project(Ctx c, Gadget g, In in, Tables 
                                                   : label_ref(c, g, in, e, S_INPUT, P.outr_idx, 0);
         const u128 pay = proj_payload(ol, oR, static_cast<uint32_t>(cm), mo);
         if (e_raw < N) tb.t[P.table][e * tb.row[P.table] + P.off + static_cast<int64_t>(color) * P.stride] = pay + H;
+    }
+}
+
+// Mixed-radix rescale (gadgets.h RescaleMrsPlan), garbler side of the free
+// operations, one thread per element: key base labels K_i = L_i - sum_{l<i}
+// P_{l,i}, the mod-T accumulator r = sum_i P_{i,T}, then the output base labels
+// (in place) Y_0 = F_0, Y_j = S^-1 L_j + F_j.
+struct MrsG {
+    int k, T;
+    int crt[kMaxRes], sinv[kMaxRes];
+    int dig0[kMaxRes];  // slot of digit i's first target label (targets: residues i+1..k-1, then T)
+    int key0, acc, fin0;
+    int16_t* L[kMaxRes];  // label-major [N][n_j], updated in place
+};
+__global__ __launch_bounds__(256) void k_mrs_derive(Ctx c, Gadget g, MrsG a) {
+    const int64_t e = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (e >= g.N) return;
+    int16_t* S = g.S + e * g.nslots * kW;
+    const int k = a.k;
+    for (int j = 0; j < k; ++j) {
+        const int p = a.crt[j], n = static_cast<int>(c.mc[p].n);
+        const int16_t* Lj = a.L[j] + e * n;
+        int16_t* K = S + (a.key0 + j) * kW;
+        for (int q = 0; q < n; ++q) {
+            int v = Lj[q];
+            for (int l = 0; l < j; ++l) {
+                v -= S[(a.dig0[l] + (j - l - 1)) * kW + q];
+                if (v < 0) v += p;
+            }
+            K[q] = static_cast<int16_t>(v);
+        }
+    }
+    {
+        const int nT = static_cast<int>(c.mc[a.T].n);
+        int16_t* A = S + a.acc * kW;
+        for (int q = 0; q < nT; ++q) {
+            int v = 0;
+            for (int l = 0; l < k; ++l) v += S[(a.dig0[l] + (k - 1 - l)) * kW + q];
+            A[q] = static_cast<int16_t>(v & (a.T - 1));
+        }
+    }
+    for (int j = 0; j < k; ++j) {
+        const int p = a.crt[j], n = static_cast<int>(c.mc[p].n);
+        int16_t* Lj = a.L[j] + e * n;
+        const int16_t* F = S + (a.fin0 + j) * kW;
+        for (int q = 0; q < n; ++q)
+            Lj[q] = j == 0 ? F[q] : static_cast<int16_t>((Lj[q] * a.sinv[j] + F[q]) % p);
     }
 }
 
@@ -1636,6 +1699,108 @@ void GpuGarbler::rescale_legacy_iter(uint64_t layer, int it, const RescalePlan& 
     if (P.sign.has_cast1()) t1.to_array(c1, I.device);
     t2.to_array(c2, I.device);
     tS.to_array(sg, I.device);
+    set_stale(cur, I.cur_mod, N);
+}
+
+// Mixed-radix rescale: draw (digit-target labels, then the k final labels, in
+// rescale_mrs_garble_elem's PRG order) -> derive keys / outputs -> fan-out
+// projections (one per digit, one final).
+void GpuGarbler::rescale_mrs(uint64_t layer, const RescaleMrsPlan& P, CrtLabels& cur, Array& tab) {
+    Impl& I = *impl_;
+    HIPCHECK(hipSetDevice(I.device));
+    I.check_cur(cur);
+    PhaseTrace tr_("rescale_mrs");
+    const int64_t N = I.cur_N;
+    const int k = I.k;
+    DASH_CHECK(P.k() == k && static_cast<int>(P.T) <= I.max_mod, "gpu garbler: mixed-radix rescale plan mismatch");
+    std::vector<gg::Draw> dr;
+    std::vector<gg::Proj> pr;
+    std::vector<int> fan;
+    std::vector<int16_t> flut;
+    gg::MrsG a{};
+    a.k = k;
+    a.T = static_cast<int>(P.T);
+    int slot = 0, ctr = 0;
+    for (int i = 0; i < k; ++i) {
+        a.dig0[i] = slot;
+        for (int t = 0; t < P.targets(i); ++t) {
+            const int q = P.target_mod(i, t);
+            dr.push_back({slot++, q, ctr});
+            ctr += (nr_comps(q) + 1) / 2;
+        }
+    }
+    a.fin0 = slot;
+    for (int j = 0; j < k; ++j) {
+        dr.push_back({slot++, P.crt[j], ctr});
+        ctr += (nr_comps(P.crt[j]) + 1) / 2;
+    }
+    a.key0 = slot;
+    slot += k;
+    a.acc = slot++;
+    const int nslots = slot;
+    int64_t first = 0;
+    for (int i = 0; i < k; ++i) {
+        const int nt = P.targets(i);
+        const int a0 = static_cast<int>(flut.size()), a1 = static_cast<int>(fan.size());
+        for (int v = 0; v < P.crt[i]; ++v)
+            for (int t = 0; t < nt; ++t) flut.push_back(static_cast<int16_t>(P.digit_fn(i, t, v)));
+        for (int t = 0; t < nt; ++t) fan.push_back(P.target_mod(i, t));
+        gg::Proj p{};
+        p.in_kind = gg::S_SLOT; p.in_idx = a.key0 + i; p.pin = P.crt[i];
+        p.out_slot = a.dig0[i]; p.pout = P.target_mod(i, 0); p.fn = gg::F_FAN; p.a0 = a0; p.a1 = a1;
+        p.outr_kind = gg::R_BANK; p.table = 0; p.stride = nt; p.off = P.dig_off[i]; p.first = first;
+        first += P.crt[i];
+        pr.push_back(p);
+    }
+    {
+        const int a0 = static_cast<int>(flut.size()), a1 = static_cast<int>(fan.size());
+        for (int v = 0; v < P.T; ++v)
+            for (int j = 0; j < k; ++j) flut.push_back(static_cast<int16_t>(P.final_fn(j, v)));
+        for (int j = 0; j < k; ++j) fan.push_back(P.crt[j]);
+        gg::Proj p{};
+        p.in_kind = gg::S_SLOT; p.in_idx = a.acc; p.pin = static_cast<int>(P.T);
+        p.out_slot = a.fin0; p.pout = P.crt[0]; p.fn = gg::F_FAN; p.a0 = a0; p.a1 = a1;
+        p.outr_kind = gg::R_BANK; p.table = 0; p.stride = k; p.off = P.fin_off; p.first = first;
+        first += P.T;
+        pr.push_back(p);
+    }
+    for (int j = 0; j < k; ++j) {
+        a.crt[j] = P.crt[j];
+        a.sinv[j] = static_cast<int>(P.Sinv[j]);
+        a.L[j] = I.cur[j].as<int16_t>();
+    }
+    DevTable tT;
+    tT.alloc(I.device, N, P.n_tab);
+    gg::Tables tb{};
+    tb.t[0] = tT.p();
+    tb.row[0] = tT.row;
+    gg::Gadget g{};
+    g.layer = layer;
+    g.sslot = 30;
+    g.mask = 0;
+    g.S = I.scratch(static_cast<size_t>(N) * nslots * gg::kW * sizeof(int16_t));
+    g.PB = nullptr;
+    g.N = N;
+    g.nslots = nslots;
+    g.draws = gg::dconst(dr.data(), dr.size());
+    g.ndraws = static_cast<int>(dr.size());
+    g.projs = gg::dconst(pr.data(), pr.size());
+    g.nprojs = static_cast<int>(pr.size());
+    g.entries = first;
+    g.nblk = draw_blocks(dr);
+    g.flut = gg::dconst(flut.data(), flut.size());
+    g.fan = gg::dconst(fan.data(), fan.size());
+    check_desc(g);
+    gg::In in{};
+    std::vector<void*> tmp;
+    hipLaunchKernelGGL(gg::k_draw, dim3(blocks_for(N * g.nblk, gg::kGB, 8192)), dim3(gg::kGB), 0, nullptr, I.c, g);
+    hipLaunchKernelGGL(gg::k_mrs_derive, dim3(blocks_for(N, 256)), dim3(256), 0, nullptr, I.c, g, a);
+    hipLaunchKernelGGL(gg::k_project, dim3(blocks_for((N + 63) / 64 * 64 * g.entries, gg::kPB, 16384)), dim3(gg::kPB), 0,
+                       nullptr, I.c, g, in, tb);
+    HIPCHECK(hipGetLastError());
+    gg::end_layer(tmp);
+    tr_.mark("kernels");
+    tT.to_array(tab, I.device);
     set_stale(cur, I.cur_mod, N);
 }
 

@@ -36,6 +36,9 @@ class GpuGarbler {
                              const std::vector<std::vector<comp_t>>& up, const std::vector<std::vector<comp_t>>& down,
                              Array& tr, Array& ap, Array& c1, Array& c2, Array& sg);
 
+    // legacy rescale as one mixed-radix gadget (gadgets.h RescaleMrsPlan) on the device cur, in place
+    void rescale_mrs(uint64_t layer, const RescaleMrsPlan& P, CrtLabels& cur, Array& tab);
+
    private:
     struct Impl;
     std::unique_ptr<Impl> impl_;

@@ -273,3 +273,23 @@ def test_gpu_garbler_bit_identical(name, fused):
     gpu = GarbledCircuit(c, k, 100.0, seed=seed, device=0, fused_sign=fused)
     assert gpu.model.serialize() == cpu.model.serialize()
     assert gpu.decoder.serialize() == cpu.decoder.serialize()
+
+
+@pytest.mark.parametrize("name", ["rescale", "minionn_head"])
+def test_gpu_garbler_bit_identical_mrs_rescale(name):
+    """GPU garbler of the mixed-radix rescale == host garbler, byte for byte."""
+    from dash_amd.ir.circuit import Circuit
+    from dash_amd.ir.layers import Rescale
+    from dash_amd.ir.quant import QuantizationMethod as Q
+    from dash_amd.models import build_circuit
+
+    if name == "rescale":
+        c, k = Circuit([Rescale(5, (300,))]), 7
+    else:
+        full = build_circuit("MODEL_F_MINIONN_POOL_REPL", Q.ScaleQuant, 5, seed=0)
+        c, k = Circuit(full.layers[:4]), 7  # conv, rescale(l=5), relu, conv
+    seed = bytes(range(16))
+    cpu = GarbledCircuit(c, k, 100.0, seed=seed, rescale="mrs")
+    gpu = GarbledCircuit(c, k, 100.0, seed=seed, device=0, rescale="mrs")
+    assert gpu.model.serialize() == cpu.model.serialize()
+    assert gpu.decoder.serialize() == cpu.decoder.serialize()
