@@ -84,6 +84,7 @@ struct MrsArgs {
     int sinv[kMaxRes];             // S^-1 mod p_j (j >= 1)
     u128 hmask;                    // top bit of every log2(T)-bit field (packed mod-T additions)
     u128* pf;                      // [B][k][N] final payloads (chain -> output kernel)
+    u128* ps;                      // [B][k(k-1)/2][N] digit payloads for later residues (chain scratch)
 };
 
 struct BEArgs {

@@ -658,6 +658,17 @@ __device__ __forceinline__ u128 add_packed(u128 a, u128 b, u128 hmask) {
     return ((a & ~hmask) + (b & ~hmask)) ^ ((a ^ b) & hmask);
 }
 
+// Digit i's key streams residue i's label in chunks of kMrsChunk components,
+// the next chunk's loads issued before the current one is consumed. The
+// payloads P_{l,j} of digit l for later residues j go to a per-lane scratch
+// (a.ps, [B][pair][N], coalesced) and are read back when digit j starts:
+// holding them in registers (up to K(K-1)/2 u128) spilled.
+constexpr int kMrsChunk = 8;
+template <int K>
+__device__ __forceinline__ constexpr int mrs_pair(int l, int j) {  // l < j < K
+    return l * (2 * K - l - 1) / 2 + (j - l - 1);
+}
+
 template <int K>
 __global__ __launch_bounds__(kAesBlock, DASH_UA_MINBLOCKS) void k_rescale_mrs_chain(MrsArgs a, Act x, const ModC* mc,
                                                                                   const uint32_t* te0,
@@ -665,10 +676,11 @@ __global__ __launch_bounds__(kAesBlock, DASH_UA_MINBLOCKS) void k_rescale_mrs_ch
     AES_PROLOGUE(te0, rk);
     const int b = blockIdx.z;
     const int64_t N = a.N;
+    constexpr int NP = K * (K - 1) / 2 > 0 ? K * (K - 1) / 2 : 1;
     for (int64_t e = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; e < N;
          e += static_cast<int64_t>(gridDim.x) * blockDim.x) {
         const u128* row0 = a.tab + (static_cast<int64_t>(b) * N + e) * a.n_tab;
-        u128 P[K][K];  // P[l][j], l < j: payload of digit l for residue j (hash removed)
+        u128* PS = a.ps + static_cast<int64_t>(b) * NP * N + e;
         u128 acc = 0;
 #pragma unroll
         for (int i = 0; i < K; ++i) {
@@ -677,19 +689,22 @@ __global__ __launch_bounds__(kAesBlock, DASH_UA_MINBLOCKS) void k_rescale_mrs_ch
             const int16_t* L = x.p[i] + static_cast<int64_t>(b) * n * N + e;
             DigitStream ds[K > 1 ? K - 1 : 1];
 #pragma unroll
-            for (int l = 0; l < i; ++l) ds[l].init(P[l][i]);
+            for (int l = 0; l < i; ++l) ds[l].init(PS[static_cast<int64_t>(mrs_pair<K>(l, i)) * N]);
             CompressFwd cf;
             cf.init();
             uint32_t col = 0;
-            for (int c0 = 0; c0 < n; c0 += kChunk) {
-                uint16_t v[kChunk];
+            uint16_t cur[kMrsChunk], nxt[kMrsChunk];
 #pragma unroll
-                for (int u = 0; u < kChunk; ++u)
-                    if (c0 + u < n) v[u] = static_cast<uint16_t>(L[static_cast<int64_t>(c0 + u) * N]);
+            for (int u = 0; u < kMrsChunk; ++u)
+                if (u < n) cur[u] = static_cast<uint16_t>(L[static_cast<int64_t>(u) * N]);
+            for (int c0 = 0; c0 < n; c0 += kMrsChunk) {
 #pragma unroll
-                for (int u = 0; u < kChunk; ++u)
+                for (int u = 0; u < kMrsChunk; ++u)
+                    if (c0 + kMrsChunk + u < n) nxt[u] = static_cast<uint16_t>(L[static_cast<int64_t>(c0 + kMrsChunk + u) * N]);
+#pragma unroll
+                for (int u = 0; u < kMrsChunk; ++u)
                     if (c0 + u < n) {
-                        uint32_t d = v[u];
+                        uint32_t d = cur[u];
 #pragma unroll
                         for (int l = 0; l < i; ++l) {
                             const uint32_t s = ds[l].next(m);
@@ -698,6 +713,8 @@ __global__ __launch_bounds__(kAesBlock, DASH_UA_MINBLOCKS) void k_rescale_mrs_ch
                         if (c0 + u == 0) col = d;
                         cf.push(d, m);
                     }
+#pragma unroll
+                for (int u = 0; u < kMrsChunk; ++u) cur[u] = nxt[u];
             }
             const u128* row = row0 + a.dig_off[i] + static_cast<int64_t>(col) * (K - i);
             u128 E[K];
@@ -705,7 +722,7 @@ __global__ __launch_bounds__(kAesBlock, DASH_UA_MINBLOCKS) void k_rescale_mrs_ch
             for (int t = 0; t < K - i; ++t) E[t] = row[t];
             const u128 H = aes_encrypt(aes, cf.finish());
 #pragma unroll
-            for (int t = 0; t + 1 < K - i; ++t) P[i][i + 1 + t] = E[t] - H;
+            for (int t = 0; t + 1 < K - i; ++t) PS[static_cast<int64_t>(mrs_pair<K>(i, i + 1 + t)) * N] = E[t] - H;
             acc = add_packed(acc, E[K - 1 - i] - H, a.hmask);
         }
         const uint32_t col = static_cast<uint32_t>(acc) & static_cast<uint32_t>(a.T - 1);

@@ -383,6 +383,8 @@ class HipEvaluator {
     int* d_lab_off_ = nullptr;
     const int16_t* zero_rows_ = nullptr;
     const int16_t* up_rows_ = nullptr;
+    u128* mrs_ps_ = nullptr;  // mixed-radix rescale chain scratch (allocated by the first such layer)
+    i64 maxSignN_ = 0;
     const u128* zc_ = nullptr;
     const u128* zh_ = nullptr;
     const uint16_t* zcol_ = nullptr;
@@ -500,6 +502,7 @@ void HipEvaluator::build() {
     csum_ = dalloc<int16_t>(static_cast<size_t>(B_) * tmax * kCsumComps * maxSignN);
     colx_ = dalloc<uint16_t>(static_cast<size_t>(B_) * k_ * maxSignN);
     outP_ = dalloc<u128>(static_cast<size_t>(B_) * k_ * maxSignN);
+    maxSignN_ = maxSignN;
     hs_ = dalloc<u128>(static_cast<size_t>(B_) * maxSignN);
     cs_ = dalloc<uint8_t>(static_cast<size_t>(B_) * maxSignN);
     h0_ = dalloc<u128>(static_cast<size_t>(B_) * maxN);
@@ -718,6 +721,8 @@ void HipEvaluator::build() {
                     a.hmask = 0;
                     for (int f = 0; f < nf; ++f) a.hmask |= static_cast<u128>(1) << (bits * f + bits - 1);
                     a.pf = outP_;  // [B][k][N] <= the sign outputs' scratch
+                    if (!mrs_ps_) mrs_ps_ = dalloc<u128>(static_cast<size_t>(B_) * std::max(1, k_ * (k_ - 1) / 2) * maxSignN_);
+                    a.ps = mrs_ps_;
                     Act x = act_of(cur);
                     const ModC* mc = mc_;
                     const AesGlobals ag = aes_;
