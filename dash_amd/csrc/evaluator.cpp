@@ -184,6 +184,28 @@ CrtLabels cpu_evaluate(const GarbledModel& m, const CrtLabels& inputs, int nt, s
                 break;
             }
             case K_RELU: {
+                if (g.param("smode", 0) == 1) {  // exact mixed-radix sign (SignMrsPlan)
+                    const SignMrsPlan sp(crt);
+                    const Array& tab = g.arr("mrs");
+                    const Array& tg = g.arr("mm.g");
+                    const Array& te = g.arr("mm.e");
+                    CrtLabels nxt;
+                    for (int j = 0; j < k; ++j) nxt.emplace_back(crt[j], Nin);
+                    parallel_for(Nin, [&](i64 b0, i64 b1) {
+                        std::vector<const comp_t*> x(k);
+                        comp_t sig[128];
+                        const ModInfo& m2 = mod_info(2);
+                        for (i64 e = b0; e < b1; ++e) {
+                            for (int j = 0; j < k; ++j) x[j] = cur[j].at(e);
+                            sign_mrs_eval_elem(sp, x.data(), tab.ptr<u128>() + e * tab.shape[1], sig);
+                            for (int j = 0; j < k; ++j)
+                                mixed_mult_eval(x[j], mod_info(crt[j]), sig, m2, tg.ptr<u128>() + e * tg.shape[1] + prefix[j],
+                                                te.ptr<u128>() + (e * k + j) * 3, nxt[j].at(e));
+                        }
+                    }, nt);
+                    cur = std::move(nxt);
+                    break;
+                }
                 SignPlan sp(crt, m.h.mrs, {2}, 0, 1, fused);
                 const ReluTabs T(g, "");
                 CrtLabels nxt;

@@ -701,4 +701,104 @@ void rescale_mrs_eval_elem(const RescaleMrsPlan& P, comp_t* const* L, const u128
     }
 }
 
+// ---------------------------------------------------------------------------
+// Exact sign by mixed-radix conversion (gadgets.h SignMrsPlan)
+SignMrsPlan::SignMrsPlan(const std::vector<int>& crt_) : crt(crt_) {
+    const int kk = k();
+    DASH_CHECK(kk >= 2 && crt[0] == 2, "mixed-radix sign needs CRT residue 0 = 2");
+    for (int j = 1; j < kk; ++j) DASH_CHECK(crt[j] % 2 == 1, "mixed-radix sign: residues 1.. must be odd");
+    for (int p : crt) M *= p;
+    U = M / 2;
+    ord.clear();
+    for (int j = 1; j < kk; ++j) ord.push_back(j);
+    ord.push_back(0);
+    B.assign(kk, 1);
+    Binv.assign(kk, 1);
+    for (int i = 1; i < kk; ++i) B[i] = B[i - 1] * crt[ord[i - 1]];
+    for (int i = 0; i < kk; ++i) Binv[i] = mul_inv(static_cast<u128>(B[i] % crt[ord[i]]), crt[ord[i]]);
+    dig_off.assign(kk - 1, 0);
+    i64 off = 0;
+    for (int i = 0; i + 1 < kk; ++i) {
+        dig_off[i] = off;
+        off += static_cast<i64>(crt[ord[i]]) * targets(i);
+    }
+    n_tab = off;
+}
+
+i64 SignMrsPlan::digit_fn(int i, int t, i64 v) const {
+    const i64 pi = crt[ord[i]];
+    const i64 a = pmod((v + U % pi) * Binv[i], pi);
+    const int r = target_res(i, t);
+    const i64 m = crt[r];
+    i64 val = a * (B[i] % m);
+    if (i == 0 && r == ord[k() - 1]) val -= U % m;  // residue 0's key then carries a_{k-1} itself
+    return pmod(val, m);
+}
+
+void sign_mrs_garble_elem(const SignMrsPlan& P, const LabelBank& R, const Prg& prg, u64 stream,
+                          const comp_t* const* x0, u128* tab, comp_t* sig0) {
+    const int k = P.k();
+    constexpr int W = 128;
+    int nd = 0;
+    for (int i = 0; i + 1 < k; ++i) nd += P.targets(i);
+    comp_t* buf = sign_scratch().get(static_cast<size_t>(W) * (nd + k));
+    std::vector<comp_t*> dig(std::max(nd, 1)), key(k);
+    u64 ctr = 0;
+    int s = 0;
+    for (int i = 0; i + 1 < k; ++i)
+        for (int t = 0; t < P.targets(i); ++t, ++s) {
+            dig[s] = buf + static_cast<size_t>(W) * s;
+            draw(prg, stream, ctr, P.crt[P.target_res(i, t)], dig[s]);
+        }
+    for (int j = 0; j < k; ++j) {
+        key[j] = buf + static_cast<size_t>(W) * (nd + j);
+        std::memcpy(key[j], x0[j], sizeof(comp_t) * nr_comps(P.crt[j]));
+    }
+    s = 0;
+    for (int i = 0; i + 1 < k; ++i)
+        for (int t = 0; t < P.targets(i); ++t, ++s) {
+            const int r = P.target_res(i, t);
+            lab_sub(key[r], dig[s], nr_comps(P.crt[r]), P.crt[r]);
+        }
+    ProjKeys& K = proj_keys_scratch();
+    s = 0;
+    for (int i = 0; i + 1 < k; ++i) {
+        const ModInfo& mi = mod_info(P.crt[P.ord[i]]);
+        proj_keys(key[P.ord[i]], R.get(mi.p), mi, K);
+        const int nt = P.targets(i);
+        for (int t = 0; t < nt; ++t, ++s) {
+            const ModInfo& mo = mod_info(P.crt[P.target_res(i, t)]);
+            garble_proj_keys(K, dig[s], R.get(mo.p), mo, [&](int v) { return P.digit_fn(i, t, v); },
+                             tab + P.dig_off[i] + t, nt);
+        }
+    }
+    std::memcpy(sig0, key[P.ord[k - 1]], sizeof(comp_t) * nr_comps(2));
+}
+
+void sign_mrs_eval_elem(const SignMrsPlan& P, const comp_t* const* x, const u128* tab, comp_t* sig) {
+    const int k = P.k();
+    constexpr int W = 128;
+    comp_t* buf = sign_scratch().get(static_cast<size_t>(W) * (k + 1));
+    std::vector<comp_t*> key(k);
+    for (int j = 0; j < k; ++j) {
+        key[j] = buf + static_cast<size_t>(W) * j;
+        std::memcpy(key[j], x[j], sizeof(comp_t) * nr_comps(P.crt[j]));
+    }
+    comp_t* pr = buf + static_cast<size_t>(W) * k;
+    for (int i = 0; i + 1 < k; ++i) {
+        const int r0 = P.ord[i];
+        const ModInfo& mi = mod_info(P.crt[r0]);
+        const u128 h = hash(compress(key[r0], mi));
+        const int nt = P.targets(i);
+        const u128* row = tab + P.dig_off[i] + static_cast<i64>(color_of(key[r0], mi.p)) * nt;
+        for (int t = 0; t < nt; ++t) {
+            const int r = P.target_res(i, t);
+            const ModInfo& mo = mod_info(P.crt[r]);
+            decompress(row[t] - h, pr, mo);
+            lab_sub(key[r], pr, mo.n, mo.p);
+        }
+    }
+    std::memcpy(sig, key[P.ord[k - 1]], sizeof(comp_t) * nr_comps(2));
+}
+
 }  // namespace dash

@@ -287,4 +287,36 @@ void rescale_mrs_garble_elem(const RescaleMrsPlan& P, const LabelBank& R, const 
                              comp_t* const* L, u128* tab);
 void rescale_mrs_eval_elem(const RescaleMrsPlan& P, comp_t* const* L, const u128* tab);
 
+// ---------------------------------------------------------------------------
+// Exact sign by mixed-radix conversion (a construction of the ReLU/Sign
+// gadget's sign; the reference approximates it, sign_gadget.h:425-581)
+//
+// With residue 0 = 2 converted LAST, x_u = x + M/2 = sum_i a_i B_i and the
+// last digit's weight is B_{k-1} = M/2, so a_{k-1} = [x_u >= M/2] = [x >= 0]
+// exactly. Positions 0..k-2 convert residues 1..k-1 (ascending); digit i's
+// table row fans its value a_i B_i out to the later residues (the constant
+// -M/2 is folded into digit 0's payload for residue 0), and residue 0's key
+// after the k-1 subtractions IS the sign label (mod 2) - no table of its own.
+// k-1 hashes on the critical path; sum_{i<k-1} p_{i+1} (k-1-i) table entries
+// (k = 7: 147 instead of the approximate gadget's 568) and exact for every x.
+// Rows: position i at dig_off[i], [color][k-1-i] (targets: positions i+1..k-1).
+struct SignMrsPlan {
+    std::vector<int> crt;
+    std::vector<int> ord;      // position -> residue: 1, 2, ..., k-1, 0
+    i64 M = 1, U = 0;
+    std::vector<i64> B, Binv;  // per position: product of the earlier positions' moduli; its inverse mod p
+    std::vector<i64> dig_off;
+    i64 n_tab = 0;
+    SignMrsPlan() = default;
+    explicit SignMrsPlan(const std::vector<int>& crt);
+    int k() const { return static_cast<int>(crt.size()); }
+    int targets(int i) const { return k() - 1 - i; }
+    int target_res(int i, int t) const { return ord[i + 1 + t]; }
+    i64 digit_fn(int i, int t, i64 v) const;
+};
+// sign01 base label (mod 2) of one element with residue base labels x0; tables at tab
+void sign_mrs_garble_elem(const SignMrsPlan& P, const LabelBank& R, const Prg& prg, u64 stream,
+                          const comp_t* const* x0, u128* tab, comp_t* sig0);
+void sign_mrs_eval_elem(const SignMrsPlan& P, const comp_t* const* x, const u128* tab, comp_t* sig);
+
 }  // namespace dash

@@ -474,6 +474,7 @@ GarbledModel Garbler::garble(const std::vector<LayerSpec>& layers, const std::ve
 
         // legacy rescale as one mixed-radix gadget (RescaleMrsPlan)
         const bool mrs_rescale = opt.rescale_mrs && spec.kind == K_RESCALE && param1(spec.p, "mode", 0) == 0;
+        const bool relu_mrs = opt.relu_mrs && spec.kind == K_RELU;
         const bool on_gpu = gpu && (spec.kind == K_CONV || spec.kind == K_RELU || spec.kind == K_SIGN ||
                                     (spec.kind == K_RESCALE && param1(spec.p, "mode", 0) == 0 && crt_[0] == 2));
         const bool passthru = spec.kind == K_FLATTEN;
@@ -600,6 +601,38 @@ GarbledModel Garbler::garble(const std::vector<LayerSpec>& layers, const std::ve
             }
             case K_RELU: {
                 DASH_CHECK(is_crt(), "relu needs CRT-base labels");
+                if (relu_mrs) {
+                    const SignMrsPlan sp(crt_);
+                    Array tab(DType::u128, {Nin, std::max<i64>(sp.n_tab, 1)});
+                    Array tg(DType::u128, {Nin, sum_crt}), te(DType::u128, {Nin, static_cast<i64>(k), 3});
+                    if (on_gpu) {
+                        gpu->relu_mrs(L, sp, cur, tab, &crt_, &prefix, tg, te);
+                    } else {
+                        CrtLabels nxt;
+                        for (int j = 0; j < k; ++j) nxt.emplace_back(crt_[j], Nin);
+                        parallel_for(Nin, [&](i64 b0, i64 b1) {
+                            std::vector<const comp_t*> x(k);
+                            comp_t sig[128];
+                            const ModInfo& m2 = mod_info(2);
+                            for (i64 e = b0; e < b1; ++e) {
+                                for (int j = 0; j < k; ++j) x[j] = cur[j].at(e);
+                                sign_mrs_garble_elem(sp, R_, prg_, stream_id(L, 1, e), x.data(),
+                                                     tab.ptr<u128>() + e * tab.shape[1], sig);
+                                u64 ctr = 0;
+                                for (int j = 0; j < k; ++j)
+                                    mixed_mult_garble(x[j], mod_info(crt_[j]), sig, m2, R_, prg_, stream_id(L, 2, e), ctr,
+                                                      tg.ptr<u128>() + e * sum_crt + prefix[j],
+                                                      te.ptr<u128>() + (e * k + j) * 3, nxt[j].at(e));
+                            }
+                        }, nt);
+                        cur = std::move(nxt);
+                    }
+                    g.a["mrs"] = tab;
+                    g.a["mm.g"] = tg;
+                    g.a["mm.e"] = te;
+                    g.p["smode"] = {1};
+                    break;
+                }
                 SignPlan sp(crt_, mrs_, {2}, 0, 1, fused);
                 ReluTables t = make_relu_tables(sp, Nin, sum_crt, k);
                 CrtLabels nxt;

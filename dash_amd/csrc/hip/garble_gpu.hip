@@ -542,6 +542,34 @@ __global__ __launch_bounds__(256) void k_mrs_derive(Ctx c, Gadget g, MrsG a) {
     }
 }
 
+// Mixed-radix sign (gadgets.h SignMrsPlan): key base labels
+// K_r = x_r - sum of the digit-target labels aimed at residue r (slot lists).
+struct MrsSG {
+    int k;
+    int crt[kMaxRes];
+    int nsub[kMaxRes];
+    int sub[kMaxRes][kMaxRes];  // slots subtracted from residue r's key
+    int key0;                   // key slot of residue r = key0 + r
+};
+__global__ __launch_bounds__(256) void k_mrs_sign_derive(Ctx c, Gadget g, In in, MrsSG a) {
+    const int64_t e = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (e >= g.N) return;
+    int16_t* S = g.S + e * g.nslots * kW;
+    for (int r = 0; r < a.k; ++r) {
+        const int p = a.crt[r], n = in.n[r];
+        const int16_t* x = in.p[r] + e * n;
+        int16_t* K = S + (a.key0 + r) * kW;
+        for (int q = 0; q < n; ++q) {
+            int v = x[q];
+            for (int u = 0; u < a.nsub[r]; ++u) {
+                v -= S[a.sub[r][u] * kW + q];
+                if (v < 0) v += p;
+            }
+            K[q] = static_cast<int16_t>(v);
+        }
+    }
+}
+
 // Payload bank: one thread per (row, element), rows = PayDesc entries.
 __global__ __launch_bounds__(256) void k_payloads(Ctx c, Gadget g, const PayDesc* pd, int npd) {
     const int64_t total = g.N * npd;
@@ -1700,6 +1728,153 @@ void GpuGarbler::rescale_legacy_iter(uint64_t layer, int it, const RescalePlan& 
     t2.to_array(c2, I.device);
     tS.to_array(sg, I.device);
     set_stale(cur, I.cur_mod, N);
+}
+
+// ReLU with the mixed-radix sign: draw the digit-target labels (sign_mrs_garble_elem order) -> keys ->
+// fan-out projections; residue 0's key slot is the sign label; then the mixed-modulus half gates exactly as
+// in sign_layer's ReLU branch.
+void GpuGarbler::relu_mrs(uint64_t layer, const SignMrsPlan& P, CrtLabels& cur, Array& tab,
+                          const std::vector<int>* relu_crt, const std::vector<i64>* prefix, Array& mmg, Array& mme) {
+    Impl& I = *impl_;
+    HIPCHECK(hipSetDevice(I.device));
+    I.check_cur(cur);
+    PhaseTrace tr_("relu_mrs");
+    (void)relu_crt;
+    const int64_t N = I.cur_N;
+    const int k = I.k;
+    DASH_CHECK(P.k() == k, "gpu garbler: mixed-radix sign plan mismatch");
+    std::vector<gg::Draw> dr;
+    std::vector<gg::Proj> pr;
+    std::vector<int> fan;
+    std::vector<int16_t> flut;
+    gg::MrsSG a{};
+    a.k = k;
+    int slot = 0, ctr = 0;
+    std::vector<int> dig0(k, 0);
+    for (int i = 0; i + 1 < k; ++i) {
+        dig0[i] = slot;
+        for (int t = 0; t < P.targets(i); ++t) {
+            const int r = P.target_res(i, t);
+            a.sub[r][a.nsub[r]++] = slot;
+            dr.push_back({slot++, P.crt[r], ctr});
+            ctr += (nr_comps(P.crt[r]) + 1) / 2;
+        }
+    }
+    a.key0 = slot;
+    slot += k;
+    const int sig_slot = a.key0 + P.ord[k - 1];
+    const int sk0 = slot;
+    slot += 2 * k;
+    const int nslots = slot;
+    int64_t first = 0;
+    for (int i = 0; i + 1 < k; ++i) {
+        const int nt = P.targets(i), r0 = P.ord[i];
+        const int a0 = static_cast<int>(flut.size()), a1 = static_cast<int>(fan.size());
+        for (int v = 0; v < P.crt[r0]; ++v)
+            for (int t = 0; t < nt; ++t) flut.push_back(static_cast<int16_t>(P.digit_fn(i, t, v)));
+        for (int t = 0; t < nt; ++t) fan.push_back(P.crt[P.target_res(i, t)]);
+        gg::Proj p{};
+        p.in_kind = gg::S_SLOT; p.in_idx = a.key0 + r0; p.pin = P.crt[r0];
+        p.out_slot = dig0[i]; p.pout = P.crt[P.target_res(i, 0)]; p.fn = gg::F_FAN; p.a0 = a0; p.a1 = a1;
+        p.outr_kind = gg::R_BANK; p.table = 0; p.stride = nt; p.off = P.dig_off[i]; p.first = first;
+        first += P.crt[r0];
+        pr.push_back(p);
+    }
+    for (int j = 0; j < k; ++j) a.crt[j] = P.crt[j];
+    DevTable tT, tG, tE;
+    tT.alloc(I.device, N, tab.shape[1]);
+    tG.alloc(I.device, N, mmg.shape[1]);
+    tE.alloc(I.device, N, static_cast<int64_t>(k) * 3, true);
+    gg::Tables tb{};
+    tb.t[0] = tT.p(); tb.row[0] = tT.row;
+    tb.t[4] = tG.p(); tb.row[4] = tG.row;
+    tb.t[5] = tE.p(); tb.row[5] = tE.row;
+    gg::In in{};
+    for (int j = 0; j < k; ++j) {
+        in.p[j] = I.cur[j].as<int16_t>();
+        in.n[j] = nr_comps(I.crt[j]);
+    }
+    gg::Gadget g{};
+    g.layer = layer;
+    g.sslot = 1;
+    g.mask = 0;
+    g.S = I.scratch(static_cast<size_t>(N) * nslots * gg::kW * sizeof(int16_t));
+    g.PB = I.pbank(2, N);
+    g.N = N;
+    g.nslots = nslots;
+    g.draws = gg::dconst(dr.data(), dr.size());
+    g.ndraws = static_cast<int>(dr.size());
+    g.projs = gg::dconst(pr.data(), pr.size());
+    g.nprojs = static_cast<int>(pr.size());
+    g.entries = first;
+    g.nblk = draw_blocks(dr);
+    g.flut = gg::dconst(flut.data(), flut.size());
+    g.fan = gg::dconst(fan.data(), fan.size());
+    check_desc(g);
+    std::vector<void*> tmp;
+    hipLaunchKernelGGL(gg::k_draw, dim3(blocks_for(N * g.nblk, gg::kGB, 8192)), dim3(gg::kGB), 0, nullptr, I.c, g);
+    hipLaunchKernelGGL(gg::k_mrs_sign_derive, dim3(blocks_for(N, 256)), dim3(256), 0, nullptr, I.c, g, in, a);
+    hipLaunchKernelGGL(gg::k_project, dim3(blocks_for((N + 63) / 64 * 64 * g.entries, gg::kPB, 16384)), dim3(gg::kPB), 0,
+                       nullptr, I.c, g, in, tb);
+    // mixed-modulus half gates (as sign_layer's ReLU branch, sign label = residue 0's key slot)
+    std::vector<DevBlock> out = I.alloc_labels(I.crt, N);
+    {
+        std::vector<gg::Draw> dm;
+        std::vector<gg::Proj> pm;
+        int c2 = 0;
+        int64_t f2 = 0;
+        for (int j = 0; j < k; ++j) {
+            const int p = I.crt[j], n = nr_comps(p);
+            dm.push_back({sk0 + 2 * j, p, c2});
+            c2 += (n + 1) / 2;
+            dm.push_back({sk0 + 2 * j + 1, p, c2});
+            c2 += (n + 1) / 2;
+        }
+        for (int j = 0; j < k; ++j) {
+            const int p = I.crt[j];
+            gg::Proj q{gg::S_INPUT, j, p, sk0 + 2 * j, p, gg::F_MULR, j, 0, 0, gg::R_BANK, 0, 4, 1, (*prefix)[j], f2};
+            f2 += p;
+            pm.push_back(q);
+        }
+        for (int j = 0; j < k; ++j) {
+            const int p = I.crt[j];
+            gg::Proj q{gg::S_SLOT, sig_slot, 2, sk0 + 2 * j + 1, p, gg::F_NEGR, j, 0, 0, gg::R_INPUT, j, 5, 1,
+                       static_cast<int64_t>(j) * 3, f2};
+            f2 += 2;
+            pm.push_back(q);
+        }
+        gg::Gadget gm = g;
+        gm.sslot = 2;
+        gm.draws = gg::dconst(dm.data(), dm.size());
+        gm.ndraws = static_cast<int>(dm.size());
+        gm.projs = gg::dconst(pm.data(), pm.size());
+        gm.nprojs = static_cast<int>(pm.size());
+        gm.entries = f2;
+        gm.nblk = draw_blocks(dm);
+        check_desc(gm);
+        hipLaunchKernelGGL(gg::k_draw, dim3(blocks_for(N * gm.nblk, gg::kGB, 8192)), dim3(gg::kGB), 0, nullptr, I.c, gm);
+        hipLaunchKernelGGL(gg::k_project, dim3(blocks_for((N + 63) / 64 * 64 * gm.entries, gg::kPB, 16384)),
+                           dim3(gg::kPB), 0, nullptr, I.c, gm, in, tb);
+        gg::MiniArgs ma{};
+        ma.k = k;
+        for (int j = 0; j < k; ++j) ma.crt[j] = I.crt[j];
+        ma.sig_slot = sig_slot;
+        ma.sk_slot0 = sk0;
+        for (int j = 0; j < k; ++j) ma.out[j] = out[j].as<int16_t>();
+        hipLaunchKernelGGL(gg::k_bin_keys, dim3(blocks_for(N, gg::kGB, 8192)), dim3(gg::kGB), 0, nullptr, I.c,
+                           g.S + static_cast<int64_t>(sig_slot) * gg::kW, static_cast<int64_t>(nslots) * gg::kW,
+                           static_cast<const int16_t*>(nullptr), g.PB, N);
+        hipLaunchKernelGGL(gg::k_relu_finish, dim3(blocks_for(N * k, 256, 8192)), dim3(256), 0, nullptr, I.c, gm, in,
+                           tb, ma, static_cast<const u128*>(g.PB));
+    }
+    HIPCHECK(hipGetLastError());
+    gg::end_layer(tmp);
+    tr_.mark("kernels");
+    tT.to_array(tab, I.device);
+    tG.to_array(mmg, I.device);
+    tE.to_array(mme, I.device);
+    I.cur = std::move(out);
+    set_stale(cur, I.crt, N);
 }
 
 // Mixed-radix rescale: draw (digit-target labels, then the k final labels, in

@@ -39,6 +39,10 @@ class GpuGarbler {
     // legacy rescale as one mixed-radix gadget (gadgets.h RescaleMrsPlan) on the device cur, in place
     void rescale_mrs(uint64_t layer, const RescaleMrsPlan& P, CrtLabels& cur, Array& tab);
 
+    // ReLU with the exact mixed-radix sign (gadgets.h SignMrsPlan) + mixed-modulus half gates; device cur -> next
+    void relu_mrs(uint64_t layer, const SignMrsPlan& P, CrtLabels& cur, Array& tab, const std::vector<int>* relu_crt,
+                  const std::vector<i64>* prefix, Array& mmg, Array& mme);
+
    private:
     struct Impl;
     std::unique_ptr<Impl> impl_;

@@ -102,6 +102,7 @@ struct GarbleOptions {
     int device = -1;  // >= 0: garble ReLU / Sign / legacy rescale layers on this GPU
     bool fused_sign = true;  // sign gadget construction (gadgets.h SignPlan::fused); false: reference casts
     bool rescale_mrs = false;  // legacy (l-halving) rescale as one mixed-radix gadget (gadgets.h RescaleMrsPlan)
+    bool relu_mrs = false;     // ReLU sign by exact mixed-radix conversion (gadgets.h SignMrsPlan)
 };
 
 class Garbler {

@@ -29,7 +29,8 @@ Labels = list  # list[(modulus, np.ndarray int16 [N, n_p])]
 class GarbledCircuit:
     def __init__(self, circuit: Circuit, crt: Union[int, Sequence[int]], mrs: Union[None, float, Sequence[int]] = None,
                  max_modulus: int = 0, seed: Optional[bytes] = None, garble_me: bool = True, nthreads: int = 0,
-                 device: Optional[int] = None, fused_sign: bool = True, rescale: str = "legacy"):
+                 device: Optional[int] = None, fused_sign: bool = True, rescale: str = "legacy",
+                 relu: str = "approx"):
         """fused_sign: sign-gadget construction. True (default): the MRS casts are folded into the approx and
         carry projections (same function, 3.7x fewer gates per sign; gadgets.h SignPlan::fused). False: the
         reference construction with explicit identity casts (sign_gadget.h:456-546).
@@ -37,7 +38,11 @@ class GarbledCircuit:
         rescale: construction of the DASH legacy rescale (divide by 2^l, Rescale(l)). "legacy": l iterations of
         the reference's sign-base-extension gadget (rescale_gadget.h:115-242). "mrs": one exact mixed-radix
         conversion computing the same ceil(x / 2^l) (gadgets.h RescaleMrsPlan; k + 1 hashes per element instead
-        of l sign gadgets); it differs only on the top U - M/2 < 2^l values of the signed range, which wrap."""
+        of l sign gadgets); it differs only on the top U - M/2 < 2^l values of the signed range, which wrap.
+
+        relu: sign of the ReLU gadget. "approx": the reference's approximate sign gadget (construction per
+        fused_sign). "mrs": exact mixed-radix sign with the mod-2 residue converted last (gadgets.h SignMrsPlan;
+        k - 1 hashes, 147 instead of 568 table entries per element at k = 7, exact for every x)."""
         self.circuit = circuit
         self.crt_base = first_primes(crt) if isinstance(crt, int) else [int(p) for p in crt]
         if mrs is None:
@@ -55,6 +60,9 @@ class GarbledCircuit:
         if rescale not in ("legacy", "mrs"):
             raise ValueError(f"rescale construction must be 'legacy' or 'mrs', got {rescale!r}")
         self.rescale = rescale
+        if relu not in ("approx", "mrs"):
+            raise ValueError(f"relu construction must be 'approx' or 'mrs', got {relu!r}")
+        self.relu = relu
         self._n = native()
         self.garbler = self._n.Garbler(self.crt_base, self.mrs_base, self.seed, int(max_modulus))
         self.model = None
@@ -68,7 +76,7 @@ class GarbledCircuit:
         specs = self.circuit.garble_specs()
         t = time.perf_counter()
         self.model = self.garbler.garble(specs, list(self.circuit.input_dims), self.nthreads, self.device,
-                                         self.fused_sign, self.rescale == "mrs")
+                                         self.fused_sign, self.rescale == "mrs", self.relu == "mrs")
         self.garbling_time_s = time.perf_counter() - t
         self.decoder = self.garbler.decoder()
         return self.model

@@ -361,3 +361,34 @@ def test_rescale_mrs_tables_and_model():
     assert m2.serialize() == blob
     y = new.decode_outputs(native().cpu_evaluate(m2, new.garble_inputs(xs[0]), 0))
     np.testing.assert_array_equal(y, new.plain_q_eval(xs[0]))
+
+
+# ---------------------------------------------- exact mixed-radix sign for the ReLU
+@pytest.mark.parametrize("k", [2, 3, 4, 7, 9])
+def test_relu_mrs_sign_exact(k):
+    """ReLU with the exact mixed-radix sign: max(x, 0) on the whole signed range, edges included."""
+    c0 = d.Circuit([d.Relu((1,))])
+    M = GarbledCircuit(c0, k, None, seed=SEED, garble_me=False).crt_modulus
+    h = M // 2
+    rng = np.random.default_rng(k)
+    vals = [0, 1, -1, h - 1, -h, -h + 1, h - 2, 2, -2] + list(rng.integers(-h, h, 40))
+    x = np.array(vals, dtype=np.int64)
+    c = d.Circuit([d.Relu((len(x),))])
+    gc = GarbledCircuit(c, k, None, seed=SEED, relu="mrs")  # no approximate-sign MRS base needed
+    out = gc.decode_outputs(gc.cpu_evaluate(gc.garble_inputs(x)))
+    np.testing.assert_array_equal(out, np.maximum(x, 0))
+
+
+def test_relu_mrs_tables_and_model():
+    """MODEL_B with both mixed-radix constructions decodes to the plaintext output; ReLU tables shrink."""
+    from dash_amd.ir.quant import QuantizationMethod as Q
+    from dash_amd.models import build_circuit, quantized_inputs
+
+    c = build_circuit("MODEL_B_POOL_REPL", Q.ScaleQuant, 3, seed=1)
+    xs = quantized_inputs("MODEL_B_POOL_REPL", 3, Q.ScaleQuant, 3, seed=6)
+    both = GarbledCircuit(c, 8, 100.0, seed=SEED, rescale="mrs", relu="mrs")
+    resc = GarbledCircuit(c, 8, 100.0, seed=SEED, rescale="mrs")
+    assert both.table_bytes < resc.table_bytes
+    for x in xs:
+        y = both.decode_outputs(both.cpu_evaluate(both.garble_inputs(x)))
+        np.testing.assert_array_equal(y, both.plain_q_eval(x))
