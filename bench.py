@@ -52,6 +52,9 @@ def main() -> None:
     ap.add_argument("--rescale", default=os.environ.get("DASH_BENCH_RESCALE", "mrs"), choices=["mrs", "legacy"],
                     help="construction of the DASH rescale ceil(x/2^l): one exact mixed-radix conversion (mrs) or the "
                          "reference's l sign-gadget halvings (legacy); same function on the signed range")
+    ap.add_argument("--relu", default=os.environ.get("DASH_BENCH_RELU", "approx"), choices=["mrs", "approx"],
+                    help="sign of the ReLU: exact mixed-radix conversion (mrs) or the reference's approximate sign "
+                         "gadget at 100 %% accuracy (approx)")
     ap.add_argument("--streams", type=int, default=int(os.environ.get("DASH_BENCH_STREAMS", "4")),
                     help="independent GC groups per GPU, each on its own HIP stream (overlap latency- and "
                          "bandwidth-bound phases)")
@@ -111,7 +114,7 @@ def main() -> None:
         seed = hashlib.sha256(f"dash-bench/{rank}/{b}/{os.getpid()}".encode()).digest()[:16]
         t = time.perf_counter()
         gc = GarbledCircuit(circuit, cfg["crt"], cfg["mrs"], seed=seed, device=device if args.garble_device else None,
-                            fused_sign=args.sign == "fused", rescale=args.rescale)
+                            fused_sign=args.sign == "fused", rescale=args.rescale, relu=args.relu)
         garble_s += time.perf_counter() - t
         if b == 0:
             # HBM guard: every GC's tables stay resident. Size B from the real device footprint of one GC
@@ -253,6 +256,7 @@ def main() -> None:
                 "streams": G,
                 "sign_construction": args.sign,
                 "rescale_construction": args.rescale,
+                "relu_construction": args.relu,
                 "seq_len": None,
                 "input_shape": [3, 32, 32],
                 "parallelism": f"dp{world}",

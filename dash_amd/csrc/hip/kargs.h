@@ -84,7 +84,11 @@ struct MrsArgs {
     int sinv[kMaxRes];             // S^-1 mod p_j (j >= 1)
     u128 hmask;                    // top bit of every log2(T)-bit field (packed mod-T additions)
     u128* pf;                      // [B][k][N] final payloads (chain -> output kernel)
-    u128* ps;                      // [B][k(k-1)/2][N] digit payloads for later residues (chain scratch)
+    u128* ps;                      // [B][k(k-1)/2][N] digit payloads for later positions (chain scratch)
+    int mode;                      // 0: rescale (position i = residue i, T accumulator, final row -> pf)
+                                   // 1: sign (position i = residue (i + 1) mod k; the last key is sign01 -> hs, cs)
+    u128* hs;                      // mode 1: [B][N] hash of the sign label
+    uint8_t* cs;                   // mode 1: [B][N] its color
 };
 
 struct BEArgs {

@@ -669,10 +669,13 @@ __device__ __forceinline__ constexpr int mrs_pair(int l, int j) {  // l < j < K
     return l * (2 * K - l - 1) / 2 + (j - l - 1);
 }
 
-template <int K>
-__global__ __launch_bounds__(kAesBlock, DASH_UA_MINBLOCKS) void k_rescale_mrs_chain(MrsArgs a, Act x, const ModC* mc,
-                                                                                  const uint32_t* te0,
-                                                                                  const uint32_t* rk) {
+// MODE 1 (exact sign, gadgets.h SignMrsPlan): positions convert residues
+// 1..K-1, the last position is residue 0 (mod 2): its key is the bit pack of
+// L_0 XOR the K-1 payloads aimed at it (mod-2 subtraction), i.e. the sign
+// label itself; only its hash and color are produced (the ReLU multiply).
+template <int K, int MODE>
+__global__ __launch_bounds__(kAesBlock, DASH_UA_MINBLOCKS) void k_mrs_chain(MrsArgs a, Act x, const ModC* mc,
+                                                                          const uint32_t* te0, const uint32_t* rk) {
     AES_PROLOGUE(te0, rk);
     const int b = blockIdx.z;
     const int64_t N = a.N;
@@ -684,9 +687,20 @@ __global__ __launch_bounds__(kAesBlock, DASH_UA_MINBLOCKS) void k_rescale_mrs_ch
         u128 acc = 0;
 #pragma unroll
         for (int i = 0; i < K; ++i) {
-            const ModC m = mc[a.crt.p[i]];
+            const int r = MODE == 1 ? (i + 1) % K : i;  // residue converted at position i
+            const ModC m = mc[a.crt.p[r]];
             const int n = static_cast<int>(m.n);
-            const int16_t* L = x.p[i] + static_cast<int64_t>(b) * n * N + e;
+            const int16_t* L = x.p[r] + static_cast<int64_t>(b) * n * N + e;
+            if (MODE == 1 && i == K - 1) {
+                // residue 0 (mod 2): compress = bit pack, subtraction = XOR
+                u128 key = compress_cm(L, N, m);
+#pragma unroll
+                for (int l = 0; l < K - 1; ++l) key ^= PS[static_cast<int64_t>(mrs_pair<K>(l, K - 1)) * N];
+                const u128 H = aes_encrypt(aes, key);
+                a.hs[static_cast<int64_t>(b) * N + e] = H;
+                a.cs[static_cast<int64_t>(b) * N + e] = static_cast<uint8_t>(static_cast<uint32_t>(key) & 1u);
+                break;
+            }
             DigitStream ds[K > 1 ? K - 1 : 1];
 #pragma unroll
             for (int l = 0; l < i; ++l) ds[l].init(PS[static_cast<int64_t>(mrs_pair<K>(l, i)) * N]);
@@ -716,15 +730,18 @@ __global__ __launch_bounds__(kAesBlock, DASH_UA_MINBLOCKS) void k_rescale_mrs_ch
 #pragma unroll
                 for (int u = 0; u < kMrsChunk; ++u) cur[u] = nxt[u];
             }
-            const u128* row = row0 + a.dig_off[i] + static_cast<int64_t>(col) * (K - i);
+            constexpr int kExtra = MODE == 0 ? 1 : 0;        // rescale rows end with the T target
+            const int nt = K - 1 - i + kExtra;
+            const u128* row = row0 + a.dig_off[i] + static_cast<int64_t>(col) * nt;
             u128 E[K];
 #pragma unroll
-            for (int t = 0; t < K - i; ++t) E[t] = row[t];
+            for (int t = 0; t < nt; ++t) E[t] = row[t];
             const u128 H = aes_encrypt(aes, cf.finish());
 #pragma unroll
-            for (int t = 0; t + 1 < K - i; ++t) PS[static_cast<int64_t>(mrs_pair<K>(i, i + 1 + t)) * N] = E[t] - H;
-            acc = add_packed(acc, E[K - 1 - i] - H, a.hmask);
+            for (int t = 0; t < K - 1 - i; ++t) PS[static_cast<int64_t>(mrs_pair<K>(i, i + 1 + t)) * N] = E[t] - H;
+            if (MODE == 0) acc = add_packed(acc, E[K - 1 - i] - H, a.hmask);
         }
+        if (MODE == 1) continue;
         const uint32_t col = static_cast<uint32_t>(acc) & static_cast<uint32_t>(a.T - 1);
         const u128* row = row0 + a.fin_off + static_cast<int64_t>(col) * K;
         u128 F[K];
@@ -767,11 +784,44 @@ __global__ __launch_bounds__(256) void k_rescale_mrs_out(MrsArgs a, Act x, const
     }
 }
 
+// hx[b][j][e] = H(compress(x_j)), colx = color: the ReLU multiply's garbler half gates (exact-sign path;
+// the approximate path gets them from k_sign_approx). grid (x, k, B)
+__global__ __launch_bounds__(kAesBlock, kAesMinBlocks) void k_label_hash(Act x, CrtInfo crt, int64_t N, u128* hx,
+                                                                        uint16_t* colx, const ModC* mc,
+                                                                        const uint32_t* te0, const uint32_t* rk) {
+    AES_PROLOGUE(te0, rk);
+    const int j = blockIdx.y, b = blockIdx.z;
+    for (int64_t e = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; e < N;
+         e += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+        const ModC m = mc[crt.p[j]];
+        const int16_t* L = x.p[j] + static_cast<int64_t>(b) * m.n * N + e;
+        const int64_t bke = (static_cast<int64_t>(b) * crt.k + j) * N + e;
+        colx[bke] = static_cast<uint16_t>(static_cast<uint16_t>(L[0]) % m.q);
+        hx[bke] = aes_encrypt(aes, compress_cm(L, N, m));
+    }
+}
+
+void launch_relu_mrs(const MrsArgs& a, const SignArgs& sa, const Act& x, const Act& y, const u128* gtab,
+                     const u128* etab, int B, const ModC* mc, const AesGlobals& g, hipStream_t st) {
+    hipLaunchKernelGGL(k_label_hash, grid_aes(a.N, kAesBlock, a.crt.k, B), dim3(kAesBlock), kAesLds, st, x, a.crt, a.N,
+                       sa.hx, sa.colx, mc, g.te0, g.rk);
+    const dim3 gc = grid_aes(a.N, kAesBlock, 1, B);
+    switch (a.crt.k) {
+#define DASH_MRS_K(KK) \
+        case KK: hipLaunchKernelGGL((k_mrs_chain<KK, 1>), gc, dim3(kAesBlock), kAesLds, st, a, x, mc, g.te0, g.rk); break;
+        DASH_MRS_K(2) DASH_MRS_K(3) DASH_MRS_K(4) DASH_MRS_K(5) DASH_MRS_K(6) DASH_MRS_K(7) DASH_MRS_K(8)
+        DASH_MRS_K(9) DASH_MRS_K(10) DASH_MRS_K(11) DASH_MRS_K(12)
+#undef DASH_MRS_K
+        default: std::fprintf(stderr, "dash: mixed-radix sign supports 2..12 CRT residues\n"); std::abort();
+    }
+    launch_relu_mult(sa, x, y, gtab, etab, mc, st);
+}
+
 void launch_rescale_mrs(const MrsArgs& a, const Act& x, int B, const ModC* mc, const AesGlobals& g, hipStream_t st) {
     const dim3 gc = grid_aes(a.N, kAesBlock, 1, B);
     switch (a.crt.k) {
 #define DASH_MRS_K(KK) \
-        case KK: hipLaunchKernelGGL(k_rescale_mrs_chain<KK>, gc, dim3(kAesBlock), kAesLds, st, a, x, mc, g.te0, g.rk); break;
+        case KK: hipLaunchKernelGGL((k_mrs_chain<KK, 0>), gc, dim3(kAesBlock), kAesLds, st, a, x, mc, g.te0, g.rk); break;
         DASH_MRS_K(2) DASH_MRS_K(3) DASH_MRS_K(4) DASH_MRS_K(5) DASH_MRS_K(6) DASH_MRS_K(7) DASH_MRS_K(8)
         DASH_MRS_K(9) DASH_MRS_K(10) DASH_MRS_K(11) DASH_MRS_K(12)
 #undef DASH_MRS_K

@@ -670,6 +670,39 @@ void HipEvaluator::build() {
                 break;
             }
             case K_RELU: {
+                if (g.param("smode", 0) == 1) {  // exact mixed-radix sign (gadgets.h SignMrsPlan)
+                    const SignMrsPlan P(crt_);
+                    MrsArgs a{};
+                    a.crt = crt;
+                    a.N = N;
+                    a.n_tab = g.arr("mrs").shape[1];
+                    a.tab = upload_tables(li, "mrs");
+                    for (int i = 0; i + 1 < k_; ++i) a.dig_off[i] = P.dig_off[i];
+                    if (!mrs_ps_) mrs_ps_ = dalloc<u128>(static_cast<size_t>(B_) * std::max(1, k_ * (k_ - 1) / 2) * maxSignN_);
+                    a.ps = mrs_ps_;
+                    a.mode = 1;
+                    a.hs = hs_;
+                    a.cs = cs_;
+                    SignArgs sa{};
+                    sa.crt = crt;
+                    sa.N = N;
+                    sa.B = B_;
+                    sa.hx = hx_;
+                    sa.colx = colx_;
+                    sa.hs = hs_;
+                    sa.cs = cs_;
+                    const u128* gt = upload_tables(li, "mm.g");
+                    const u128* et = upload_tables(li, "mm.e");
+                    Act x = act_of(cur), y = act_of(nxt);
+                    const ModC* mc = mc_;
+                    const AesGlobals ag = aes_;
+                    const int B = B_;
+                    add_op(lname + ".mrs", [a, sa, x, y, gt, et, B, mc, ag](hipStream_t st) {
+                        launch_relu_mrs(a, sa, x, y, gt, et, B, mc, ag, st);
+                    });
+                    cur = nxt;
+                    break;
+                }
                 SignPlan sp(crt_, m0.h.mrs, {2}, 0, 1, m0.h.sign_fused != 0);
                 SignArgs a = make_sign(li, "", sp, N, 1);
                 const u128* gt = upload_tables(li, "mm.g");

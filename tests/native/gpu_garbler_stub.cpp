@@ -28,6 +28,11 @@ void GpuGarbler::rescale_legacy_iter(uint64_t, int, const RescalePlan&, CrtLabel
                                      Array&) {
     no_gpu();
 }
+void GpuGarbler::rescale_mrs(uint64_t, const RescaleMrsPlan&, CrtLabels&, Array&) { no_gpu(); }
+void GpuGarbler::relu_mrs(uint64_t, const SignMrsPlan&, CrtLabels&, Array&, const std::vector<int>*,
+                          const std::vector<i64>*, Array&, Array&) {
+    no_gpu();
+}
 void gpu_table_cache_trim() {}
 size_t gpu_table_cache_bytes() { return 0; }
 

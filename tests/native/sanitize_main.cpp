@@ -48,6 +48,7 @@ int main() {
         GarbleOptions opt;
         opt.nthreads = 8;
         opt.rescale_mrs = mrs_rescale != 0;
+        opt.relu_mrs = mrs_rescale != 0;  // and the exact mixed-radix sign
         GarbledModel m = g.garble(L, {I}, opt);
         CrtLabels in = g.encode(x);
         CrtLabels out = cpu_evaluate(m, in, 8);

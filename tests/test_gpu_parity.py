@@ -17,8 +17,8 @@ def _hip(models, mfma=True):
 FUSED = pytest.mark.parametrize("fused", [True, False], ids=["fused", "refcasts"])
 
 
-def _check(circuit, crt, mrs, xs, mfma=True, plain=True, fused=True, rescale="legacy"):
-    gcs = [GarbledCircuit(circuit, crt, mrs, seed=bytes([i + 1]) * 16, fused_sign=fused, rescale=rescale)
+def _check(circuit, crt, mrs, xs, mfma=True, plain=True, fused=True, rescale="legacy", relu="approx"):
+    gcs = [GarbledCircuit(circuit, crt, mrs, seed=bytes([i + 1]) * 16, fused_sign=fused, rescale=rescale, relu=relu)
            for i in range(len(xs))]
     enc = [g.garble_inputs(x) for g, x in zip(gcs, xs)]
     cpu = [g.cpu_evaluate(e) for g, e in zip(gcs, enc)]
@@ -116,15 +116,27 @@ def test_rescale_mrs(k, l):
     _check(c, k, 100.0, xs, rescale="mrs")
 
 
-def test_minionn_head_mrs_rescale():
-    """MiniONN conv -> rescale(l=5) -> relu at full size with the mixed-radix rescale."""
+@pytest.mark.parametrize("relu", ["approx", "mrs"])
+def test_minionn_head_mrs_rescale(relu):
+    """MiniONN conv -> rescale(l=5) -> relu at full size with the mixed-radix rescale (and sign)."""
     from dash_amd.ir.quant import QuantizationMethod as Q
     from dash_amd.models import build_circuit, quantized_inputs
 
     full = build_circuit("MODEL_F_MINIONN_POOL_REPL", Q.ScaleQuant, 5, seed=0)
     c = d.Circuit(full.layers[:3])
     xs = quantized_inputs("MODEL_F_MINIONN_POOL_REPL", 2, Q.ScaleQuant, 5, seed=3)
-    _check(c, 7, 100.0, xs, rescale="mrs")
+    _check(c, 7, 100.0, xs, rescale="mrs", relu=relu)
+
+
+@pytest.mark.parametrize("k", [2, 3, 7, 9])
+def test_relu_mrs_sign(k):
+    """Exact mixed-radix-sign ReLU (label hash + chain + mixed multiply kernels) == host oracle, edges included."""
+    c0 = d.Circuit([d.Relu((1,))])
+    h = GarbledCircuit(c0, k, None, garble_me=False).crt_modulus // 2
+    rng = np.random.default_rng(k)
+    vals = np.array([0, 1, -1, h - 1, -h, -h + 1, 2, -2] + list(rng.integers(-h, h, 120)), dtype=np.int64)
+    c = d.Circuit([d.Relu((len(vals),))])
+    _check(c, k, None, [vals, vals[::-1].copy()], relu="mrs")
 
 
 @pytest.mark.parametrize("crt,mrs", [([32, 97, 107], [22, 19, 15, 13]), ([32, 3, 5, 7, 11, 13, 17], [10, 9, 9, 8, 7, 7, 6])])
@@ -291,5 +303,25 @@ def test_gpu_garbler_bit_identical_mrs_rescale(name):
     seed = bytes(range(16))
     cpu = GarbledCircuit(c, k, 100.0, seed=seed, rescale="mrs")
     gpu = GarbledCircuit(c, k, 100.0, seed=seed, device=0, rescale="mrs")
+    assert gpu.model.serialize() == cpu.model.serialize()
+    assert gpu.decoder.serialize() == cpu.decoder.serialize()
+
+
+@pytest.mark.parametrize("name", ["relu", "minionn_head"])
+def test_gpu_garbler_bit_identical_mrs_relu(name):
+    """GPU garbler of the mixed-radix-sign ReLU == host garbler, byte for byte."""
+    from dash_amd.ir.circuit import Circuit
+    from dash_amd.ir.layers import Relu
+    from dash_amd.ir.quant import QuantizationMethod as Q
+    from dash_amd.models import build_circuit
+
+    if name == "relu":
+        c, k = Circuit([Relu((300,))]), 7
+    else:
+        full = build_circuit("MODEL_F_MINIONN_POOL_REPL", Q.ScaleQuant, 5, seed=0)
+        c, k = Circuit(full.layers[:5]), 7  # conv, rescale, relu, conv, rescale
+    seed = bytes(range(16))
+    cpu = GarbledCircuit(c, k, 100.0, seed=seed, rescale="mrs", relu="mrs")
+    gpu = GarbledCircuit(c, k, 100.0, seed=seed, device=0, rescale="mrs", relu="mrs")
     assert gpu.model.serialize() == cpu.model.serialize()
     assert gpu.decoder.serialize() == cpu.decoder.serialize()
