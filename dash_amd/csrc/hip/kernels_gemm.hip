@@ -11,6 +11,8 @@
 //     (products mod p are unchanged), int32 accumulation, mod-p epilogue fused
 //     with the zero-count and bias-label adds. n runs over (GC, component,
 //     output position) of one residue, so every residue is one large GEMM.
+#include <cstdlib>
+
 #include "launch.h"
 
 namespace dash {
@@ -302,6 +304,178 @@ __global__ __launch_bounds__(256) void k_conv_img(ConvArgs a, Act x, Act y, int 
 }
 
 // ---------------------------------------------------------------------------
+// k_conv_img2: k_conv_img with
+//  * the wave's A operand (16 filters x all K steps) loaded once into VGPRs
+//    (KS <= kConvAReg k-steps of 64), instead of one 16-B global load per MFMA;
+//  * the band staged with 16-B global loads (8 columns of one channel row),
+//    transposed to channel-last dwords in registers;
+//  * a reciprocal mod p epilogue (one reduction instead of two runtime `%`).
+constexpr int kConvAReg = 9;
+typedef uint32_t u32x4c __attribute__((ext_vector_type(4)));
+struct __attribute__((packed, aligned(2))) Row8c {
+    u32x4c v;
+};
+__device__ __forceinline__ uint32_t modq_conv(uint32_t x, uint32_t q, uint32_t mq) {
+    uint32_t d = __umulhi(x, mq);
+    uint32_t r = x - d * q;
+    return r >= q ? r - q : r;
+}
+
+template <bool AREG>
+__global__ __launch_bounds__(256) void k_conv_img2(ConvArgs a, Act x, Act y, int B) {
+    extern __shared__ __attribute__((aligned(16))) int8_t img[];
+    const int band = static_cast<int>(blockIdx.x % static_cast<unsigned>(a.nbands));
+    const int64_t gimg = blockIdx.x / static_cast<unsigned>(a.nbands);
+    int j = 0;
+    while (j + 1 < a.crt.k && gimg >= a.img_off[j + 1]) ++j;
+    if (!a.w8r[j]) return;  // residue handled by the VALU kernel (p > 255)
+    const int n = a.crt.n[j], p = a.crt.p[j], half = p / 2;
+    const int64_t r0 = gimg - a.img_off[j];
+    const int b = static_cast<int>(r0 / n), c = static_cast<int>(r0 % n);
+    const int f0 = blockIdx.y * 64;
+    const int oy0 = band * a.band;
+    const int oy1 = min(a.OH, oy0 + a.band);
+    const int iy0 = oy0 * a.sh - a.ph;
+    const int in_rows = (oy1 - oy0 - 1) * a.sh + a.kh;
+    const int S = a.Cpad + 16, Wp = a.W + 2 * a.pw;
+    const int HW = a.H * a.W;
+    const int16_t* X = x.p[j] + (static_cast<int64_t>(b) * n + c) * a.C * HW;
+    const int16_t zv = a.zero[static_cast<int64_t>(b) * a.lab_stride + a.lab_off[j] + c];
+    const int zc8 = zv > half ? zv - p : zv;
+    const int tid = threadIdx.x;
+    const int wave = tid >> 6, lane = tid & 63;
+    const int fw = f0 + wave * 16;
+    const int KK = a.kh * a.kw, CC = a.Cpad / 64, KS = KK * CC;
+    const int8_t* Wr = a.w8r[j] + static_cast<int64_t>(fw + (lane & 15)) * (KK * a.Cpad) + (lane >> 4) * 16;
+    // A operand into VGPRs while the band is staged (padded filter rows exist up to F16)
+    v2l av[AREG ? kConvAReg : 1];
+    if (AREG) {
+#pragma unroll
+        for (int s = 0; s < kConvAReg; ++s)
+            if (s < KS && fw < a.F) {
+                const int kk = s / CC, cc = s - kk * CC;
+                av[s] = *reinterpret_cast<const v2l*>(Wr + kk * a.Cpad + cc * 64);
+            }
+    }
+    // stage the band: item = (8 columns, 4 channels, row); 4 x 16-B loads -> 8 channel-last dwords
+    const int c4n = a.Cpad / 4;
+    const int WO = (Wp + 7) / 8;
+    const int items = in_rows * WO * c4n;
+    for (int it = tid; it < items; it += 256) {
+        const int xo = it % WO;
+        const int t2 = it / WO;
+        const int yq = t2 % in_rows;
+        const int c4 = t2 / in_rows;
+        const int iy = iy0 + yq;
+        const bool rowin = iy >= 0 && iy < a.H;
+        const int ix0 = xo * 8 - a.pw;
+        const bool full = rowin && ix0 >= 0 && ix0 + 8 <= a.W;
+        uint32_t packed[8] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int ci = c4 * 4 + q;
+            if (ci >= a.C) continue;
+            const int16_t* row = X + static_cast<int64_t>(ci) * HW + static_cast<int64_t>(iy) * a.W;
+            int v[8];
+            if (full) {
+                Row8c t;
+                __builtin_memcpy(&t, row + ix0, 16);
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    v[2 * u] = static_cast<int>(t.v[u] & 0xffffu);
+                    v[2 * u + 1] = static_cast<int>(t.v[u] >> 16);
+                }
+#pragma unroll
+                for (int u = 0; u < 8; ++u)
+                    if (v[u] > half) v[u] -= p;
+            } else {
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    const int ix = ix0 + u;
+                    if (rowin && ix >= 0 && ix < a.W) {
+                        int w = row[ix];
+                        v[u] = w > half ? w - p : w;
+                    } else {
+                        v[u] = zc8;
+                    }
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < 8; ++u) packed[u] |= (static_cast<uint32_t>(v[u]) & 0xffu) << (8 * q);
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const int xx = xo * 8 + u;
+            if (xx < Wp) *reinterpret_cast<uint32_t*>(img + (yq * Wp + xx) * S + c4 * 4) = packed[u];
+        }
+    }
+    __syncthreads();
+    if (fw >= a.F) return;  // wave-uniform; no barrier follows
+    const int ncol = (oy1 - oy0) * a.OW;
+    const int npos = a.OH * a.OW;
+    const int32_t* zcp = a.zc[j];
+    const int16_t* bias = a.bias[j];
+    int16_t* Y = y.p[j] + (static_cast<int64_t>(b) * n + c) * a.F * npos;
+    const uint32_t mq = a.mq[j];
+    // centered operands: |acc| <= Kpad * half^2; off is a multiple of p above that bound (acc + off >= 0, < 2^31)
+    const uint32_t off = static_cast<uint32_t>(p) * (static_cast<uint32_t>(a.Kpad * half * half) / static_cast<uint32_t>(p) + 1);
+    for (int col0 = 0; col0 < ncol; col0 += 64) {
+        v4i acc[4];
+        int base[4];
+        bool ok[4];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            acc[t] = v4i{0, 0, 0, 0};
+            const int col = col0 + t * 16 + (lane & 15);
+            ok[t] = col < ncol;
+            const int oyl = ok[t] ? col / a.OW : 0, ox = ok[t] ? col % a.OW : 0;
+            base[t] = ((oyl * a.sh) * Wp + ox * a.sw) * S + (lane >> 4) * 16;
+        }
+        if (AREG) {
+#pragma unroll
+            for (int s = 0; s < kConvAReg; ++s)
+                if (s < KS) {
+                    const int kk = s / CC, cc = s - kk * CC;
+                    const int dy = kk / a.kw, dx = kk - dy * a.kw;
+                    const int offs = (dy * Wp + dx) * S + cc * 64;
+#pragma unroll
+                    for (int t = 0; t < 4; ++t) {
+                        const v2l bv = ok[t] ? *reinterpret_cast<const v2l*>(img + base[t] + offs) : v2l{0, 0};
+                        acc[t] = __builtin_amdgcn_mfma_i32_16x16x64_i8(av[s], bv, acc[t], 0, 0, 0);
+                    }
+                }
+        } else {
+            for (int dy = 0; dy < a.kh; ++dy)
+                for (int dx = 0; dx < a.kw; ++dx)
+                    for (int cc = 0; cc < CC; ++cc) {
+                        const v2l av1 = *reinterpret_cast<const v2l*>(Wr + (dy * a.kw + dx) * a.Cpad + cc * 64);
+                        const int offs = (dy * Wp + dx) * S + cc * 64;
+#pragma unroll
+                        for (int t = 0; t < 4; ++t) {
+                            const v2l bv = ok[t] ? *reinterpret_cast<const v2l*>(img + base[t] + offs) : v2l{0, 0};
+                            acc[t] = __builtin_amdgcn_mfma_i32_16x16x64_i8(av1, bv, acc[t], 0, 0, 0);
+                        }
+                    }
+        }
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            if (!ok[t]) continue;
+            const int col = col0 + t * 16 + (lane & 15);
+            const int pos = (oy0 + col / a.OW) * a.OW + col % a.OW;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int f = fw + (lane >> 4) * 4 + r;
+                if (f >= a.F) continue;
+                const uint32_t bv = static_cast<uint16_t>(bias[(static_cast<int64_t>(b) * a.F + f) * n + c]);
+                const uint32_t v = static_cast<uint32_t>(acc[t][r] + static_cast<int32_t>(off)) +
+                                   static_cast<uint32_t>(zcp[f]) * static_cast<uint32_t>(zv) + bv;
+                Y[static_cast<int64_t>(f) * npos + pos] = static_cast<int16_t>(modq_conv(v, static_cast<uint32_t>(p), mq));
+            }
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
 namespace {
 struct ZTab {
     int* dj = nullptr;
@@ -351,7 +525,17 @@ void launch_conv(const ConvArgs& a, const Act& x, const Act& y, int B, hipStream
         const int in_rows = (min(a.band, a.OH) - 1) * a.sh + a.kh;
         const size_t lds = static_cast<size_t>(in_rows) * (a.W + 2 * a.pw) * (a.Cpad + 16);
         dim3 g(static_cast<unsigned>(nimg * a.nbands), static_cast<unsigned>((a.F + 63) / 64), 1);
-        hipLaunchKernelGGL(k_conv_img, g, dim3(256), lds, st, a, x, y, B);
+        static const int ver = [] {
+            const char* e = std::getenv("DASH_CONV_IMG_VER");
+            return e ? std::atoi(e) : 2;
+        }();
+        const int KS = a.kh * a.kw * (a.Cpad / 64);
+        if (ver == 1)
+            hipLaunchKernelGGL(k_conv_img, g, dim3(256), lds, st, a, x, y, B);
+        else if (KS <= kConvAReg)
+            hipLaunchKernelGGL(k_conv_img2<true>, g, dim3(256), lds, st, a, x, y, B);
+        else
+            hipLaunchKernelGGL(k_conv_img2<false>, g, dim3(256), lds, st, a, x, y, B);
         bool rest = false;
         for (int j = 0; j < a.crt.k; ++j) rest |= (a.w8r[j] == nullptr);
         if (!rest) return;

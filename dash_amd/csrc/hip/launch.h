@@ -78,6 +78,7 @@ struct ConvArgs {
     const int8_t* w8r[kMaxRes];
     int Cpad = 0, band = 0, nbands = 0;
     int64_t img_off[kMaxRes + 1];  // first image index of residue j: B * sum_{i<j} n_i
+    uint32_t mq[kMaxRes];          // floor(2^32 / p_j): reciprocal for the epilogue's mod p (conv_img_geometry)
 };
 void launch_conv(const ConvArgs& a, const Act& x, const Act& y, int B, hipStream_t st);
 
@@ -89,6 +90,7 @@ inline void conv_img_geometry(ConvArgs& a) {
     const int64_t row_bytes = static_cast<int64_t>(a.W + 2 * a.pw) * (a.Cpad + 16);
     int band = a.OH;
     while (band > 1 && ((band - 1) * a.sh + a.kh) * row_bytes > 65536) --band;
+    for (int j = 0; j < a.crt.k; ++j) a.mq[j] = static_cast<uint32_t>(0x100000000ull / static_cast<uint32_t>(a.crt.p[j]));
     if (((band - 1) * a.sh + a.kh) * row_bytes <= 65536) {
         a.band = band;
         a.nbands = (a.OH + band - 1) / band;
