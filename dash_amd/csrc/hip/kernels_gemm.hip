@@ -306,11 +306,10 @@ __global__ __launch_bounds__(256) void k_conv_img(ConvArgs a, Act x, Act y, int 
 // ---------------------------------------------------------------------------
 // k_conv_img2: k_conv_img with
 //  * the wave's A operand (16 filters x all K steps) loaded once into VGPRs
-//    (KS <= kConvAReg k-steps of 64), instead of one 16-B global load per MFMA;
+//    (layers with 1, 4 or 9 k-steps of 64), instead of one 16-B global load per MFMA;
 //  * the band staged with 16-B global loads (8 columns of one channel row),
 //    transposed to channel-last dwords in registers;
 //  * a reciprocal mod p epilogue (one reduction instead of two runtime `%`).
-constexpr int kConvAReg = 9;
 typedef uint32_t u32x4c __attribute__((ext_vector_type(4)));
 struct __attribute__((packed, aligned(2))) Row8c {
     u32x4c v;
@@ -321,8 +320,12 @@ __device__ __forceinline__ uint32_t modq_conv(uint32_t x, uint32_t q, uint32_t m
     return r >= q ? r - q : r;
 }
 
-template <bool AREG>
+// KSC > 0: the layer has exactly KSC k-steps of 64 (taps x channel chunks), A is held in VGPRs and the
+// k-step loop is fully unrolled without branches (runtime-bounded steps made the compiler shuttle the
+// accumulators between AGPRs and VGPRs around every MFMA group); KSC = 0: generic streamed-A path.
+template <int KSC>
 __global__ __launch_bounds__(256) void k_conv_img2(ConvArgs a, Act x, Act y, int B) {
+    constexpr bool AREG = KSC > 0;
     extern __shared__ __attribute__((aligned(16))) int8_t img[];
     const int band = static_cast<int>(blockIdx.x % static_cast<unsigned>(a.nbands));
     const int64_t gimg = blockIdx.x / static_cast<unsigned>(a.nbands);
@@ -337,7 +340,7 @@ __global__ __launch_bounds__(256) void k_conv_img2(ConvArgs a, Act x, Act y, int
     const int oy1 = min(a.OH, oy0 + a.band);
     const int iy0 = oy0 * a.sh - a.ph;
     const int in_rows = (oy1 - oy0 - 1) * a.sh + a.kh;
-    const int S = a.Cpad + 16, Wp = a.W + 2 * a.pw;
+    const int S = a.ldsS, R = a.ldsR, Wp = a.W + 2 * a.pw;
     const int HW = a.H * a.W;
     const int16_t* X = x.p[j] + (static_cast<int64_t>(b) * n + c) * a.C * HW;
     const int16_t zv = a.zero[static_cast<int64_t>(b) * a.lab_stride + a.lab_off[j] + c];
@@ -348,66 +351,77 @@ __global__ __launch_bounds__(256) void k_conv_img2(ConvArgs a, Act x, Act y, int
     const int KK = a.kh * a.kw, CC = a.Cpad / 64, KS = KK * CC;
     const int8_t* Wr = a.w8r[j] + static_cast<int64_t>(fw + (lane & 15)) * (KK * a.Cpad) + (lane >> 4) * 16;
     // A operand into VGPRs while the band is staged (padded filter rows exist up to F16)
-    v2l av[AREG ? kConvAReg : 1];
-    if (AREG) {
+    v2l av[AREG ? KSC : 1];
+    if (AREG && fw < a.F) {
 #pragma unroll
-        for (int s = 0; s < kConvAReg; ++s)
-            if (s < KS && fw < a.F) {
-                const int kk = s / CC, cc = s - kk * CC;
-                av[s] = *reinterpret_cast<const v2l*>(Wr + kk * a.Cpad + cc * 64);
-            }
+        for (int s = 0; s < (AREG ? KSC : 1); ++s) {
+            const int kk = s / CC, cc = s - kk * CC;
+            av[s] = *reinterpret_cast<const v2l*>(Wr + kk * a.Cpad + cc * 64);
+        }
     }
-    // stage the band: item = (8 columns, 4 channels, row); 4 x 16-B loads -> 8 channel-last dwords
+    // stage the band: item = (4 channels, 8 columns, row), channel groups fastest across lanes (the
+    // channel-last dword stores of a lane group then cover consecutive banks); 4 x 16-B loads -> 8 dwords.
+    // Two items per round: both items' loads are issued before either is packed (half the round trips).
     const int c4n = a.Cpad / 4;
     const int WO = (Wp + 7) / 8;
     const int items = in_rows * WO * c4n;
-    for (int it = tid; it < items; it += 256) {
-        const int xo = it % WO;
-        const int t2 = it / WO;
-        const int yq = t2 % in_rows;
-        const int c4 = t2 / in_rows;
+    auto load_item = [&](int it, int (&v)[4][8], int& yq, int& xo, int& c4) {
+        c4 = it % c4n;
+        const int t2 = it / c4n;
+        xo = t2 % WO;
+        yq = t2 / WO;
         const int iy = iy0 + yq;
         const bool rowin = iy >= 0 && iy < a.H;
         const int ix0 = xo * 8 - a.pw;
         const bool full = rowin && ix0 >= 0 && ix0 + 8 <= a.W;
-        uint32_t packed[8] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
             const int ci = c4 * 4 + q;
-            if (ci >= a.C) continue;
             const int16_t* row = X + static_cast<int64_t>(ci) * HW + static_cast<int64_t>(iy) * a.W;
-            int v[8];
-            if (full) {
-                Row8c t;
-                __builtin_memcpy(&t, row + ix0, 16);
+            if (ci >= a.C) {
+#pragma unroll
+                for (int u = 0; u < 8; ++u) v[q][u] = 0;
+            } else if (full) {
+                // one 16-B load of 8 int16 (2-B aligned: global loads take unaligned addresses on gfx950;
+                // a packed-struct memcpy compiled to 8 ushort loads)
+                const u32x4c t = *reinterpret_cast<const u32x4c*>(row + ix0);
 #pragma unroll
                 for (int u = 0; u < 4; ++u) {
-                    v[2 * u] = static_cast<int>(t.v[u] & 0xffffu);
-                    v[2 * u + 1] = static_cast<int>(t.v[u] >> 16);
+                    v[q][2 * u] = static_cast<int>(t[u] & 0xffffu);
+                    v[q][2 * u + 1] = static_cast<int>(t[u] >> 16);
                 }
-#pragma unroll
-                for (int u = 0; u < 8; ++u)
-                    if (v[u] > half) v[u] -= p;
             } else {
 #pragma unroll
                 for (int u = 0; u < 8; ++u) {
                     const int ix = ix0 + u;
-                    if (rowin && ix >= 0 && ix < a.W) {
-                        int w = row[ix];
-                        v[u] = w > half ? w - p : w;
-                    } else {
-                        v[u] = zc8;
-                    }
+                    v[q][u] = (rowin && ix >= 0 && ix < a.W) ? row[ix] : -1;  // -1: padding (zero label)
                 }
             }
-#pragma unroll
-            for (int u = 0; u < 8; ++u) packed[u] |= (static_cast<uint32_t>(v[u]) & 0xffu) << (8 * q);
         }
+    };
+    auto store_item = [&](const int (&v)[4][8], int yq, int xo, int c4) {
+        uint32_t packed[8] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                int w = v[q][u];
+                w = w < 0 ? zc8 : (w > half ? w - p : w);
+                packed[u] |= (static_cast<uint32_t>(w) & 0xffu) << (8 * q);
+            }
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
             const int xx = xo * 8 + u;
-            if (xx < Wp) *reinterpret_cast<uint32_t*>(img + (yq * Wp + xx) * S + c4 * 4) = packed[u];
+            if (xx < Wp) *reinterpret_cast<uint32_t*>(img + yq * R + xx * S + c4 * 4) = packed[u];
         }
+    };
+    for (int it = tid; it < items; it += 512) {
+        int va[4][8], vb[4][8], ya, xa, ca, yb = 0, xb = 0, cb = 0;
+        load_item(it, va, ya, xa, ca);
+        const bool two = it + 256 < items;
+        if (two) load_item(it + 256, vb, yb, xb, cb);
+        store_item(va, ya, xa, ca);
+        if (two) store_item(vb, yb, xb, cb);
     }
     __syncthreads();
     if (fw >= a.F) return;  // wave-uniform; no barrier follows
@@ -417,8 +431,28 @@ __global__ __launch_bounds__(256) void k_conv_img2(ConvArgs a, Act x, Act y, int
     const int16_t* bias = a.bias[j];
     int16_t* Y = y.p[j] + (static_cast<int64_t>(b) * n + c) * a.F * npos;
     const uint32_t mq = a.mq[j];
+    // tap offsets of the A-in-VGPR path, once per block (the k-step loop then only adds)
+    int toff[AREG ? KSC : 1];
+    if (AREG) {
+#pragma unroll
+        for (int s = 0; s < (AREG ? KSC : 1); ++s) {
+            const int kk = s / CC, cc = s - kk * CC;
+            const int dy = kk / a.kw, dx = kk - dy * a.kw;
+            toff[s] = dy * R + dx * S + cc * 64;
+        }
+    }
     // centered operands: |acc| <= Kpad * half^2; off is a multiple of p above that bound (acc + off >= 0, < 2^31)
     const uint32_t off = static_cast<uint32_t>(p) * (static_cast<uint32_t>(a.Kpad * half * half) / static_cast<uint32_t>(p) + 1);
+    // per-lane epilogue constants of its 4 filter rows, loaded once (a dependent global load per output
+    // inside the column loop cost a round trip per 64-column chunk)
+    uint32_t addc[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+        const int f = fw + (lane >> 4) * 4 + r;
+        addc[r] = f < a.F ? off + static_cast<uint32_t>(zcp[f]) * static_cast<uint32_t>(zv) +
+                                static_cast<uint16_t>(bias[(static_cast<int64_t>(b) * a.F + f) * n + c])
+                          : 0u;
+    }
     for (int col0 = 0; col0 < ncol; col0 += 64) {
         v4i acc[4];
         int base[4];
@@ -428,31 +462,29 @@ __global__ __launch_bounds__(256) void k_conv_img2(ConvArgs a, Act x, Act y, int
             acc[t] = v4i{0, 0, 0, 0};
             const int col = col0 + t * 16 + (lane & 15);
             ok[t] = col < ncol;
-            const int oyl = ok[t] ? col / a.OW : 0, ox = ok[t] ? col % a.OW : 0;
-            base[t] = ((oyl * a.sh) * Wp + ox * a.sw) * S + (lane >> 4) * 16;
+            // columns past the band read column 0's operands (valid LDS); their results are never stored
+            const int cl = ok[t] ? col : 0;
+            const int oyl = cl / a.OW, ox = cl - oyl * a.OW;
+            base[t] = (oyl * a.sh) * R + (ox * a.sw) * S + (lane >> 4) * 16;
         }
         if (AREG) {
 #pragma unroll
-            for (int s = 0; s < kConvAReg; ++s)
-                if (s < KS) {
-                    const int kk = s / CC, cc = s - kk * CC;
-                    const int dy = kk / a.kw, dx = kk - dy * a.kw;
-                    const int offs = (dy * Wp + dx) * S + cc * 64;
+            for (int s = 0; s < (AREG ? KSC : 1); ++s) {
 #pragma unroll
-                    for (int t = 0; t < 4; ++t) {
-                        const v2l bv = ok[t] ? *reinterpret_cast<const v2l*>(img + base[t] + offs) : v2l{0, 0};
-                        acc[t] = __builtin_amdgcn_mfma_i32_16x16x64_i8(av[s], bv, acc[t], 0, 0, 0);
-                    }
+                for (int t = 0; t < 4; ++t) {
+                    const v2l bv = *reinterpret_cast<const v2l*>(img + base[t] + toff[s]);
+                    acc[t] = __builtin_amdgcn_mfma_i32_16x16x64_i8(av[s], bv, acc[t], 0, 0, 0);
                 }
+            }
         } else {
             for (int dy = 0; dy < a.kh; ++dy)
                 for (int dx = 0; dx < a.kw; ++dx)
                     for (int cc = 0; cc < CC; ++cc) {
                         const v2l av1 = *reinterpret_cast<const v2l*>(Wr + (dy * a.kw + dx) * a.Cpad + cc * 64);
-                        const int offs = (dy * Wp + dx) * S + cc * 64;
+                        const int offs = dy * R + dx * S + cc * 64;
 #pragma unroll
                         for (int t = 0; t < 4; ++t) {
-                            const v2l bv = ok[t] ? *reinterpret_cast<const v2l*>(img + base[t] + offs) : v2l{0, 0};
+                            const v2l bv = *reinterpret_cast<const v2l*>(img + base[t] + offs);
                             acc[t] = __builtin_amdgcn_mfma_i32_16x16x64_i8(av1, bv, acc[t], 0, 0, 0);
                         }
                     }
@@ -466,9 +498,7 @@ __global__ __launch_bounds__(256) void k_conv_img2(ConvArgs a, Act x, Act y, int
             for (int r = 0; r < 4; ++r) {
                 const int f = fw + (lane >> 4) * 4 + r;
                 if (f >= a.F) continue;
-                const uint32_t bv = static_cast<uint16_t>(bias[(static_cast<int64_t>(b) * a.F + f) * n + c]);
-                const uint32_t v = static_cast<uint32_t>(acc[t][r] + static_cast<int32_t>(off)) +
-                                   static_cast<uint32_t>(zcp[f]) * static_cast<uint32_t>(zv) + bv;
+                const uint32_t v = static_cast<uint32_t>(acc[t][r]) + addc[r];
                 Y[static_cast<int64_t>(f) * npos + pos] = static_cast<int16_t>(modq_conv(v, static_cast<uint32_t>(p), mq));
             }
         }
@@ -523,19 +553,23 @@ void launch_conv(const ConvArgs& a, const Act& x, const Act& y, int B, hipStream
     if (a.use_mfma && a.nbands > 0) {
         const int64_t nimg = a.img_off[a.crt.k];
         const int in_rows = (min(a.band, a.OH) - 1) * a.sh + a.kh;
-        const size_t lds = static_cast<size_t>(in_rows) * (a.W + 2 * a.pw) * (a.Cpad + 16);
+        const size_t lds = static_cast<size_t>(in_rows) * a.ldsR;
         dim3 g(static_cast<unsigned>(nimg * a.nbands), static_cast<unsigned>((a.F + 63) / 64), 1);
         static const int ver = [] {
             const char* e = std::getenv("DASH_CONV_IMG_VER");
             return e ? std::atoi(e) : 2;
         }();
         const int KS = a.kh * a.kw * (a.Cpad / 64);
-        if (ver == 1)
-            hipLaunchKernelGGL(k_conv_img, g, dim3(256), lds, st, a, x, y, B);
-        else if (KS <= kConvAReg)
-            hipLaunchKernelGGL(k_conv_img2<true>, g, dim3(256), lds, st, a, x, y, B);
+        if (ver == 1 && a.ldsS == a.Cpad + 16 && a.ldsR == (a.W + 2 * a.pw) * a.ldsS)
+            hipLaunchKernelGGL(k_conv_img, g, dim3(256), lds, st, a, x, y, B);  // A/B: its fixed layout only
+        else if (KS == 9)
+            hipLaunchKernelGGL(k_conv_img2<9>, g, dim3(256), lds, st, a, x, y, B);
+        else if (KS == 4)
+            hipLaunchKernelGGL(k_conv_img2<4>, g, dim3(256), lds, st, a, x, y, B);
+        else if (KS == 1)
+            hipLaunchKernelGGL(k_conv_img2<1>, g, dim3(256), lds, st, a, x, y, B);
         else
-            hipLaunchKernelGGL(k_conv_img2<false>, g, dim3(256), lds, st, a, x, y, B);
+            hipLaunchKernelGGL(k_conv_img2<0>, g, dim3(256), lds, st, a, x, y, B);
         bool rest = false;
         for (int j = 0; j < a.crt.k; ++j) rest |= (a.w8r[j] == nullptr);
         if (!rest) return;

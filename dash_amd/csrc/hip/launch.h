@@ -3,6 +3,9 @@
 
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+#include <cstdlib>
+
 #include "kargs.h"
 
 namespace dash {
@@ -79,24 +82,84 @@ struct ConvArgs {
     int Cpad = 0, band = 0, nbands = 0;
     int64_t img_off[kMaxRes + 1];  // first image index of residue j: B * sum_{i<j} n_i
     uint32_t mq[kMaxRes];          // floor(2^32 / p_j): reciprocal for the epilogue's mod p (conv_img_geometry)
+    int ldsS = 0, ldsR = 0;        // LDS image: bytes per position and per input row (conv_img_geometry)
 };
 void launch_conv(const ConvArgs& a, const Act& x, const Act& y, int B, hipStream_t st);
 
-// k_conv_img geometry: 64-channel chunks (Cpad) and the tallest band of output
-// rows whose input rows fit the 64 KiB LDS image; nbands = 0 if none fits
-// (launch_conv then uses the im2col MFMA kernel).
+// k_conv_img geometry: 64-channel chunks (Cpad), the LDS image's position
+// stride S and row stride R, and the tallest band of output rows whose input
+// rows fit 64 KiB; nbands = 0 if none fits (launch_conv then uses the im2col
+// MFMA kernel). S and R are chosen per layer by simulating the MFMA
+// B-operand ds_read_b128 of the first 64 output columns over all taps under
+// gfx950's banking (64 dword banks, 4 lane groups of 16:
+// {0-3,12-15,20-27}, {4-11,16-19,28-31} and the same +32): 4 LDS cycles per
+// read is conflict-free. The image is stored channel-last with the staging
+// lanes walking channels fastest (ds_write_b32 conflict-free for any S, R).
+inline int conv_lds_read_cycles(const ConvArgs& a, int S, int R) {
+    static const int G[4][16] = {{0, 1, 2, 3, 12, 13, 14, 15, 20, 21, 22, 23, 24, 25, 26, 27},
+                                 {4, 5, 6, 7, 8, 9, 10, 11, 16, 17, 18, 19, 28, 29, 30, 31},
+                                 {32, 33, 34, 35, 44, 45, 46, 47, 52, 53, 54, 55, 56, 57, 58, 59},
+                                 {36, 37, 38, 39, 40, 41, 42, 43, 48, 49, 50, 51, 60, 61, 62, 63}};
+    int total = 0;
+    for (int t = 0; t < 4; ++t)
+        for (int dy = 0; dy < a.kh; ++dy)
+            for (int dx = 0; dx < a.kw; ++dx)
+                for (int g = 0; g < 4; ++g) {
+                    int addr[16];
+                    for (int i = 0; i < 16; ++i) {
+                        const int l = G[g][i];
+                        const int col = t * 16 + (l & 15), oy = col / a.OW, ox = col % a.OW;
+                        addr[i] = ((oy * a.sh + dy) * R + (ox * a.sw + dx) * S + (l >> 4) * 16) / 4;
+                    }
+                    int worst = 1;
+                    for (int bk = 0; bk < 64; ++bk) {  // distinct dwords per bank
+                        int seen[64], ns = 0;
+                        for (int i = 0; i < 16; ++i)
+                            for (int d = 0; d < 4; ++d) {
+                                const int dw = addr[i] + d;
+                                if (dw % 64 != bk) continue;
+                                bool dup = false;
+                                for (int q = 0; q < ns; ++q) dup |= seen[q] == dw;
+                                if (!dup) seen[ns++] = dw;
+                            }
+                        worst = ns > worst ? ns : worst;
+                    }
+                    total += worst;
+                }
+    return total;
+}
+
 inline void conv_img_geometry(ConvArgs& a) {
     a.Cpad = (a.C + 63) / 64 * 64;
-    const int64_t row_bytes = static_cast<int64_t>(a.W + 2 * a.pw) * (a.Cpad + 16);
-    int band = a.OH;
-    while (band > 1 && ((band - 1) * a.sh + a.kh) * row_bytes > 65536) --band;
     for (int j = 0; j < a.crt.k; ++j) a.mq[j] = static_cast<uint32_t>(0x100000000ull / static_cast<uint32_t>(a.crt.p[j]));
-    if (((band - 1) * a.sh + a.kh) * row_bytes <= 65536) {
-        a.band = band;
-        a.nbands = (a.OH + band - 1) / band;
-    } else {
-        a.band = 0;
-        a.nbands = 0;
+    const int Wp = a.W + 2 * a.pw;
+    // LDS budget per block (A/B knob DASH_CONV_LDS_KB, default 40: measured 64 KiB 21.0, 40 KiB 16.3, 32 KiB 17.9 ms of conv per MiniONN step at 102 GCs): smaller bands leave room for more
+    // resident blocks, so one block's staging overlaps another's MFMAs
+    static const int64_t budget = [] {
+        const char* e = std::getenv("DASH_CONV_LDS_KB");
+        const int64_t kb = e ? std::atoll(e) : 40;
+        return std::max<int64_t>(8, std::min<int64_t>(64, kb)) * 1024;
+    }();
+    long best_cyc = -1, best_lds = 0;
+    a.band = a.nbands = 0;
+    for (int extra : {16, 32, 48, 80}) {
+        const int S = a.Cpad + extra;
+        for (int rpad = 0; rpad < 256; rpad += 16) {
+            const int R = Wp * S + rpad;
+            int band = a.OH;
+            while (band > 1 && static_cast<int64_t>((band - 1) * a.sh + a.kh) * R > budget) --band;
+            const int64_t lds = static_cast<int64_t>((band - 1) * a.sh + a.kh) * R;
+            if (lds > budget) continue;
+            const long cyc = conv_lds_read_cycles(a, S, R);
+            if (best_cyc < 0 || cyc < best_cyc || (cyc == best_cyc && lds < best_lds)) {
+                best_cyc = cyc;
+                best_lds = lds;
+                a.ldsS = S;
+                a.ldsR = R;
+                a.band = band;
+                a.nbands = (a.OH + band - 1) / band;
+            }
+        }
     }
 }
 
