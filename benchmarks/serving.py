@@ -31,6 +31,8 @@ def main() -> None:
     ap.add_argument("--requests", type=int, default=8, help="online batches to serve")
     ap.add_argument("--faults", type=float, default=0.0)
     ap.add_argument("--timeout", type=float, default=120.0)
+    ap.add_argument("--rescale", default="mrs", choices=["mrs", "legacy"])
+    ap.add_argument("--relu", default="approx", choices=["mrs", "approx"])
     args = ap.parse_args()
 
     from dash_amd.ir.quant import QuantizationMethod
@@ -47,7 +49,8 @@ def main() -> None:
     hook = (lambda i, a: a == 0 and rng.random() < args.faults) if args.faults > 0 else None
     t0 = time.perf_counter()
     svc = InferenceService(circuit, cfg["crt"], cfg["mrs"], backend=args.backend, slots_per_group=args.slots,
-                           groups=args.groups, fault_hook=hook, step_timeout_s=args.timeout)
+                           groups=args.groups, fault_hook=hook, step_timeout_s=args.timeout, rescale=args.rescale,
+                           relu=args.relu)
     fill_s = time.perf_counter() - t0
     svc.stats.t_start = time.perf_counter()
     from dash_amd.ir.bases import crt_modulus, first_primes
@@ -65,6 +68,7 @@ def main() -> None:
     svc.close()
     print(json.dumps({
         "metric": f"served garbled inferences/s incl. garbling ({model})", "backend": args.backend,
+        "rescale": args.rescale, "relu": args.relu,
         "slots": args.slots, "groups": args.groups, "pool_fill_s": round(fill_s, 2),
         "online_only_inf_per_s": round(st["inferences"] / (online_ms / 1000.0), 2) if online_ms else None,
         **st, "ok": ok}), flush=True)

@@ -506,39 +506,87 @@ struct MrsG {
     int key0, acc, fin0;
     int16_t* L[kMaxRes];  // label-major [N][n_j], updated in place
 };
+// 8 components per step: slot rows are kW-aligned (16-B loads/stores), the
+// label-major input rows [N][n_j] are read 16 B at a time at 2-B alignment
+// (unaligned global loads) except the row tail, which goes per component so
+// the last element never reads past its array.
+__device__ __forceinline__ void unpack8(const u32x4a& v, uint32_t (&d)[8]) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        d[2 * u] = v[u] & 0xffffu;
+        d[2 * u + 1] = v[u] >> 16;
+    }
+}
+__device__ __forceinline__ u32x4a pack8(const uint32_t (&d)[8]) {
+    u32x4a v;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) v[u] = d[2 * u] | (d[2 * u + 1] << 16);
+    return v;
+}
+
 __global__ __launch_bounds__(256) void k_mrs_derive(Ctx c, Gadget g, MrsG a) {
     const int64_t e = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
     if (e >= g.N) return;
     int16_t* S = g.S + e * g.nslots * kW;
     const int k = a.k;
     for (int j = 0; j < k; ++j) {
-        const int p = a.crt[j], n = static_cast<int>(c.mc[p].n);
-        const int16_t* Lj = a.L[j] + e * n;
+        const int p = a.crt[j];
+        const ModC m = c.mc[p];
+        const int n = static_cast<int>(m.n);
+        int16_t* Lj = a.L[j] + e * n;
         int16_t* K = S + (a.key0 + j) * kW;
-        for (int q = 0; q < n; ++q) {
-            int v = Lj[q];
-            for (int l = 0; l < j; ++l) {
-                v -= S[(a.dig0[l] + (j - l - 1)) * kW + q];
-                if (v < 0) v += p;
+        const int16_t* F = S + (a.fin0 + j) * kW;
+        for (int q0 = 0; q0 < n; q0 += 8) {
+            const int cnt = n - q0 < 8 ? n - q0 : 8;
+            uint32_t x[8];
+            if (cnt == 8) {
+                unpack8(*reinterpret_cast<const u32x4a*>(Lj + q0), x);
+            } else {
+#pragma unroll
+                for (int u = 0; u < 8; ++u) x[u] = u < cnt ? static_cast<uint16_t>(Lj[q0 + u]) : 0u;
             }
-            K[q] = static_cast<int16_t>(v);
+            // key: L_j - sum of the digit payload labels aimed at residue j
+            uint32_t kv[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) kv[u] = x[u] + static_cast<uint32_t>(p) * static_cast<uint32_t>(j);
+            for (int l = 0; l < j; ++l) {
+                uint32_t sv[8];
+                unpack8(ld8a(S + (a.dig0[l] + (j - l - 1)) * kW + q0), sv);
+#pragma unroll
+                for (int u = 0; u < 8; ++u) kv[u] -= sv[u];
+            }
+#pragma unroll
+            for (int u = 0; u < 8; ++u) kv[u] = modq(kv[u], m);
+            *reinterpret_cast<u32x4a*>(K + q0) = pack8(kv);  // slot rows are kW wide: the tail stays inside
+            // output base label (in place): Y_0 = F_0, Y_j = S^-1 L_j + F_j
+            uint32_t fv[8], y[8];
+            unpack8(ld8a(F + q0), fv);
+#pragma unroll
+            for (int u = 0; u < 8; ++u) y[u] = j == 0 ? fv[u] : modq(x[u] * static_cast<uint32_t>(a.sinv[j]) + fv[u], m);
+            if (cnt == 8) {
+                *reinterpret_cast<u32x4a*>(Lj + q0) = pack8(y);
+            } else {
+#pragma unroll
+                for (int u = 0; u < 8; ++u)
+                    if (u < cnt) Lj[q0 + u] = static_cast<int16_t>(y[u]);
+            }
         }
     }
     {
         const int nT = static_cast<int>(c.mc[a.T].n);
         int16_t* A = S + a.acc * kW;
-        for (int q = 0; q < nT; ++q) {
-            int v = 0;
-            for (int l = 0; l < k; ++l) v += S[(a.dig0[l] + (k - 1 - l)) * kW + q];
-            A[q] = static_cast<int16_t>(v & (a.T - 1));
+        for (int q0 = 0; q0 < nT; q0 += 8) {
+            uint32_t av[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+            for (int l = 0; l < k; ++l) {
+                uint32_t sv[8];
+                unpack8(ld8a(S + (a.dig0[l] + (k - 1 - l)) * kW + q0), sv);
+#pragma unroll
+                for (int u = 0; u < 8; ++u) av[u] += sv[u];
+            }
+#pragma unroll
+            for (int u = 0; u < 8; ++u) av[u] &= static_cast<uint32_t>(a.T - 1);
+            *reinterpret_cast<u32x4a*>(A + q0) = pack8(av);
         }
-    }
-    for (int j = 0; j < k; ++j) {
-        const int p = a.crt[j], n = static_cast<int>(c.mc[p].n);
-        int16_t* Lj = a.L[j] + e * n;
-        const int16_t* F = S + (a.fin0 + j) * kW;
-        for (int q = 0; q < n; ++q)
-            Lj[q] = j == 0 ? F[q] : static_cast<int16_t>((Lj[q] * a.sinv[j] + F[q]) % p);
     }
 }
 

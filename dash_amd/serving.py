@@ -186,7 +186,8 @@ class InferenceService:
     def __init__(self, circuit, crt, mrs=None, *, max_modulus: int = 0, slots_per_group: int = 4, groups: int = 2,
                  backend: str = "hip", device: int = 0, garble_device: Optional[bool] = None, max_retries: int = 2,
                  step_timeout_s: float = 120.0, seed: Optional[bytes] = None, prefetch: bool = True,
-                 fault_hook: Optional[Callable[[int, int], bool]] = None, nthreads: int = 0):
+                 fault_hook: Optional[Callable[[int, int], bool]] = None, nthreads: int = 0,
+                 rescale: str = "mrs", relu: str = "approx", fused_sign: bool = True):
         if backend not in ("hip", "cpu"):
             raise ValueError("backend must be 'hip' or 'cpu'")
         if backend == "hip" and native().hip_device_count() == 0:
@@ -197,6 +198,8 @@ class InferenceService:
         self.max_retries, self.step_timeout_s = max_retries, step_timeout_s
         self.fault_hook = fault_hook
         self.nthreads = nthreads
+        # gadget constructions (GarbledCircuit): the serving default is the fastest measured one
+        self.gc_kw = dict(rescale=rescale, relu=relu, fused_sign=fused_sign)
         self._seed = seed if seed is not None else os.urandom(16)
         self._ctr = 0
         self.stats = ServiceStats()
@@ -234,7 +237,7 @@ class InferenceService:
         self._ctr += 1
         t = time.perf_counter()
         gc = GarbledCircuit(self.circuit, self.crt, self.mrs, max_modulus=self.max_modulus, seed=seed,
-                            nthreads=self.nthreads, device=self.device if self.garble_device else None)
+                            nthreads=self.nthreads, device=self.device if self.garble_device else None, **self.gc_kw)
         self.stats.garble_s += time.perf_counter() - t
         self.stats.gcs_garbled += 1
         return gc
