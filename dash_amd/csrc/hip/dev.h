@@ -175,8 +175,8 @@ constexpr int kChunk = 16;
 
 // dst[c * stride] = f(c, src[c * stride]) for c < n, kChunk loads per round
 // trip (dst may alias src; f is called in component order)
-template <class F>
-__device__ __forceinline__ void col_map(const int16_t* src, int16_t* dst, long stride, int n, F&& f) {
+template <class T, class U, class F>
+__device__ __forceinline__ void col_map(const T* src, U* dst, long stride, int n, F&& f) {
     for (int i0 = 0; i0 < n; i0 += kChunk) {
         int16_t v[kChunk];
 #pragma unroll
@@ -190,7 +190,8 @@ __device__ __forceinline__ void col_map(const int16_t* src, int16_t* dst, long s
 
 // compress of a label stored component-major: L[i * stride], streamed from
 // the least significant component, kChunk loads in flight per round trip
-__device__ __forceinline__ u128 compress_cm(const int16_t* L, long stride, const ModC& m) {
+template <class T>
+__device__ __forceinline__ u128 compress_cm(const T* L, long stride, const ModC& m) {
     const int n = m.n;
     CompressFwd cf;
     cf.init();

@@ -1545,19 +1545,22 @@ void GpuGarbler::conv(const ConvGeom& G, const std::vector<i64>& w, CrtLabels& c
                 a.w8[j] = gg::dconst(w8.data(), w8.size());
             }
         }
-        // label-major [N][n] <-> component-major [n][N] around the evaluator kernel
-        std::vector<DevBlock> xin = I.alloc_labels(mods, Nin), yout = I.alloc_labels(mods, Nout);
+        // label-major int16 [N][n] <-> the evaluator's component-major byte activations [n][N]
+        std::vector<DevBlock> xin(mods.size()), yout(mods.size());
         dev::Act x{}, y{};
         x.N = Nin;
         y.N = Nout;
         for (int j = 0; j < a.crt.k; ++j) {
-            dev::launch_transpose16(I.cur[j].as<int16_t>(), xin[j].as<int16_t>(), Nin, a.crt.n[j], nullptr);
-            x.p[j] = xin[j].as<int16_t>();
-            y.p[j] = yout[j].as<int16_t>();
+            DASH_CHECK(mods[j] <= dev::kActMaxModulus, "gpu garbler: conv residue modulus above 255");
+            xin[j].alloc(I.device, static_cast<size_t>(Nin) * a.crt.n[j]);
+            yout[j].alloc(I.device, static_cast<size_t>(Nout) * a.crt.n[j]);
+            dev::launch_transpose_to_act(I.cur[j].as<int16_t>(), xin[j].as<dev::act_t>(), Nin, a.crt.n[j], nullptr);
+            x.p[j] = xin[j].as<dev::act_t>();
+            y.p[j] = yout[j].as<dev::act_t>();
         }
         dev::launch_conv(a, x, y, 1, nullptr);
         for (int j = 0; j < a.crt.k; ++j)
-            dev::launch_transpose16(yout[j].as<int16_t>(), out[j].as<int16_t>(), a.crt.n[j], Nout, nullptr);
+            dev::launch_transpose_from_act(yout[j].as<dev::act_t>(), out[j].as<int16_t>(), a.crt.n[j], Nout, nullptr);
         // xin / yout return to the block cache; later users are ordered behind these kernels on the null stream
     }
     HIPCHECK(hipGetLastError());

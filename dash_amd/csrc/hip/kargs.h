@@ -12,9 +12,16 @@ constexpr int kMaxRes = 16;   // max CRT residues on the GPU path
 constexpr int kMaxMrs = 16;
 constexpr int kMaxOut = 16;
 
-// Residue-major activation description: act[j] -> int16 [B][n_j][N]
+// Label components of activations are stored as bytes: every modulus of the
+// GPU path is < 256 (CRT primes, ReDash bases <= 173, power-of-two moduli <=
+// 128), so each streaming kernel moves half the bytes of int16 labels. Tables,
+// constant labels and the host format stay int16.
+typedef uint8_t act_t;
+constexpr int kActMaxModulus = 255;
+
+// Residue-major activation description: act[j] -> act_t [B][n_j][N]
 struct Act {
-    int16_t* p[kMaxRes];
+    act_t* p[kMaxRes];
     int64_t N;  // elements per GC
 };
 

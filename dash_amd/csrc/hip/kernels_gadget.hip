@@ -125,7 +125,7 @@ __global__ __launch_bounds__(kAesBlock, kAesMinBlocks) void k_sign_approx(SignAr
          e += static_cast<int64_t>(gridDim.x) * blockDim.x) {
         const int p = a.crt.p[j];
         const ModC m = mc[p];
-        const int16_t* L = x.p[j] + static_cast<int64_t>(b) * m.n * N + e;
+        const act_t* L = x.p[j] + static_cast<int64_t>(b) * m.n * N + e;
         const uint32_t col = static_cast<uint16_t>(L[0]) % static_cast<uint32_t>(p);
         const u128* T =
             a.approx + (static_cast<int64_t>(b) * N + e) * a.n_approx + static_cast<int64_t>(a.t) * a.crt.prefix[j];
@@ -357,8 +357,8 @@ __global__ __launch_bounds__(256) void k_unpack(const u128* P, int nres, Act out
     const ModC m = mc[mods.p[j]];
     DigitStream s;
     s.init(P[(static_cast<int64_t>(b) * nres + j) * N + e]);
-    int16_t* o = out.p[j] + static_cast<int64_t>(b) * m.n * N + e;
-    for (int i = 0; i < static_cast<int>(m.n); ++i) o[i * N] = static_cast<int16_t>(s.next(m));
+    act_t* o = out.p[j] + static_cast<int64_t>(b) * m.n * N + e;
+    for (int i = 0; i < static_cast<int>(m.n); ++i) o[i * N] = static_cast<act_t>(s.next(m));
 }
 
 // ---------------------------------------------------------------------------
@@ -386,8 +386,8 @@ __global__ __launch_bounds__(256) void k_relu_mult(SignArgs a, Act x, Act y, con
     const int16_t t16 = static_cast<int16_t>(static_cast<uint16_t>(mini >> (16 * cS)));
     const int16_t ypr16 = static_cast<int16_t>(t16 - static_cast<int16_t>(static_cast<uint16_t>(HS)));
     const uint32_t ypr = modq(static_cast<uint32_t>(static_cast<int32_t>(ypr16) + (p << 15)), m);  // p*2^15 > |ypr16|
-    const int16_t* X = x.p[j] + static_cast<int64_t>(b) * m.n * N + e;
-    int16_t* Y = y.p[j] + static_cast<int64_t>(b) * m.n * N + e;
+    const act_t* X = x.p[j] + static_cast<int64_t>(b) * m.n * N + e;
+    act_t* Y = y.p[j] + static_cast<int64_t>(b) * m.n * N + e;
     DigitStream sg, se;
     sg.init(G);
     se.init(E);
@@ -403,7 +403,7 @@ __global__ __launch_bounds__(256) void k_relu_mult(SignArgs a, Act x, Act y, con
                 const uint32_t g = sg.next(m);
                 const uint32_t ev = se.next(m);
                 // all terms in [0, p): ev + ypr * x + (p - g) < p^2 + 2p
-                Y[(i0 + u) * N] = static_cast<int16_t>(
+                Y[(i0 + u) * N] = static_cast<act_t>(
                     modq(ev + ypr * static_cast<uint32_t>(static_cast<uint16_t>(xv[u])) + static_cast<uint32_t>(p) - g, m));
             }
     }
@@ -420,7 +420,7 @@ __global__ __launch_bounds__(kAesBlock, kAesMinBlocks) void k_rescale_hash(Act x
     for (int64_t e = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; e < N;
          e += static_cast<int64_t>(gridDim.x) * blockDim.x) {
     const ModC m = mc[s];
-    const int16_t* L = x.p[fi] + static_cast<int64_t>(b) * m.n * N + e;
+    const act_t* L = x.p[fi] + static_cast<int64_t>(b) * m.n * N + e;
     const int16_t* U = up + static_cast<int64_t>(b) * up_stride;
     // compress of (L + up) mod s, streamed from the least significant component
     CompressFwd cf;
@@ -458,7 +458,7 @@ __global__ __launch_bounds__(256) void k_rescale_update(RescaleArgs a, Act x, co
     if (e >= N) return;
     const int p = a.crt.p[j];
     const ModC m = mc[p];
-    int16_t* L = x.p[j] + static_cast<int64_t>(b) * m.n * N + e;
+    act_t* L = x.p[j] + static_cast<int64_t>(b) * m.n * N + e;
     const int16_t* U = a.up + static_cast<int64_t>(b) * a.lab_stride + a.lab_off[j];
     if (j == a.fi) {
         const int16_t* Zl = a.zero + static_cast<int64_t>(b) * a.lab_stride + a.lab_off[j];
@@ -482,7 +482,7 @@ __global__ __launch_bounds__(256) void k_rescale_update(RescaleArgs a, Act x, co
             if (i0 + u < n) {
                 uint32_t v = static_cast<uint32_t>(lv[u]) + static_cast<uint32_t>(p) - s.next(m);  // [1, 2p)
                 if (a.add_up) v += static_cast<uint32_t>(U[i0 + u]);
-                L[(i0 + u) * N] = static_cast<int16_t>(modq(v * static_cast<uint32_t>(inv), m));
+                L[(i0 + u) * N] = static_cast<act_t>(modq(v * static_cast<uint32_t>(inv), m));
             }
     }
 }
@@ -497,7 +497,7 @@ __global__ __launch_bounds__(256) void k_rescale_post(Act x, CrtInfo crt, int64_
     if (e >= N) return;
     const int p = crt.p[j];
     const ModC m = mc[p];
-    int16_t* L = x.p[j] + static_cast<int64_t>(b) * m.n * N + e;
+    act_t* L = x.p[j] + static_cast<int64_t>(b) * m.n * N + e;
     const int16_t* D = down + static_cast<int64_t>(b) * lab_stride + lab_off[j];
     const int n = static_cast<int>(m.n);
     if (j == 0 && signP) {
@@ -505,7 +505,7 @@ __global__ __launch_bounds__(256) void k_rescale_post(Act x, CrtInfo crt, int64_
         s.init(signP[static_cast<int64_t>(b) * N + e]);
         for (int i = 0; i < n; ++i) {
             int32_t v = static_cast<int32_t>(s.next(m)) - D[i];
-            L[i * N] = static_cast<int16_t>(v < 0 ? v + p : v);
+            L[i * N] = static_cast<act_t>(v < 0 ? v + p : v);
         }
         return;
     }
@@ -521,7 +521,7 @@ __global__ __launch_bounds__(256) void k_rescale_post(Act x, CrtInfo crt, int64_
         for (int u = 0; u < kChunk; ++u)
             if (i0 + u < n) {
                 const int32_t v = lv[u] - dv[u];
-                L[(i0 + u) * N] = static_cast<int16_t>(v < 0 ? v + p : v);
+                L[(i0 + u) * N] = static_cast<act_t>(v < 0 ? v + p : v);
             }
     }
 }
@@ -586,7 +586,7 @@ __global__ __launch_bounds__(kAesBlock, DASH_UA_MINBLOCKS) void k_rescale_update
     } else {
         const u128 Tt = r.trans[be * r.n_trans + static_cast<int64_t>(r.aidx[j]) * r.s + r.col0[be]];
         const u128 P = Tt - r.h0[be];
-        int16_t* L = x.p[j] + static_cast<int64_t>(b) * m.n * N + e;
+        act_t* L = x.p[j] + static_cast<int64_t>(b) * m.n * N + e;
         const int16_t* Dl = delta + static_cast<int64_t>(b) * r.lab_stride + r.lab_off[j];
         DigitStream s;
         s.init(P);
@@ -609,7 +609,7 @@ __global__ __launch_bounds__(kAesBlock, DASH_UA_MINBLOCKS) void k_rescale_update
                     // lv, dv, digit in [0, p): the sum is in [1, 3p), (sum * inv) mod p in one reduction
                     const uint32_t v = modq((static_cast<uint32_t>(lv[u]) + static_cast<uint32_t>(dv[u]) +
                                              static_cast<uint32_t>(p) - s.next(m)) * static_cast<uint32_t>(inv), m);
-                    L[(i0 + u) * N] = static_cast<int16_t>(v);
+                    L[(i0 + u) * N] = static_cast<act_t>(v);
                     cf.push(v, m);
                     if (i0 + u == 0) {
                         col = static_cast<uint32_t>(v);
@@ -690,7 +690,7 @@ __global__ __launch_bounds__(kAesBlock, DASH_UA_MINBLOCKS) void k_mrs_chain(MrsA
             const int r = MODE == 1 ? (i + 1) % K : i;  // residue converted at position i
             const ModC m = mc[a.crt.p[r]];
             const int n = static_cast<int>(m.n);
-            const int16_t* L = x.p[r] + static_cast<int64_t>(b) * n * N + e;
+            const act_t* L = x.p[r] + static_cast<int64_t>(b) * n * N + e;
             if (MODE == 1 && i == K - 1) {
                 // residue 0 (mod 2): compress = bit pack, subtraction = XOR
                 u128 key = compress_cm(L, N, m);
@@ -762,11 +762,11 @@ __global__ __launch_bounds__(256) void k_rescale_mrs_out(MrsArgs a, Act x, const
     const int k = a.crt.k;
     const ModC m = mc[a.crt.p[j]];
     const int n = static_cast<int>(m.n);
-    int16_t* L = x.p[j] + static_cast<int64_t>(b) * n * N + e;
+    act_t* L = x.p[j] + static_cast<int64_t>(b) * n * N + e;
     DigitStream s;
     s.init(a.pf[(static_cast<int64_t>(b) * k + j) * N + e]);
     if (j == 0) {
-        for (int c = 0; c < n; ++c) L[static_cast<int64_t>(c) * N] = static_cast<int16_t>(s.next(m));
+        for (int c = 0; c < n; ++c) L[static_cast<int64_t>(c) * N] = static_cast<act_t>(s.next(m));
         return;
     }
     const uint32_t inv = static_cast<uint32_t>(a.sinv[j]);
@@ -779,7 +779,7 @@ __global__ __launch_bounds__(256) void k_rescale_mrs_out(MrsArgs a, Act x, const
 #pragma unroll
         for (int u = 0; u < kChunk; ++u)
             if (c0 + u < n)
-                L[static_cast<int64_t>(c0 + u) * N] = static_cast<int16_t>(modq(v[u] * inv + s.next(m), m));  // < p^2 + p
+                L[static_cast<int64_t>(c0 + u) * N] = static_cast<act_t>(modq(v[u] * inv + s.next(m), m));  // < p^2 + p
         (void)q;
     }
 }
@@ -794,7 +794,7 @@ __global__ __launch_bounds__(kAesBlock, kAesMinBlocks) void k_label_hash(Act x, 
     for (int64_t e = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; e < N;
          e += static_cast<int64_t>(gridDim.x) * blockDim.x) {
         const ModC m = mc[crt.p[j]];
-        const int16_t* L = x.p[j] + static_cast<int64_t>(b) * m.n * N + e;
+        const act_t* L = x.p[j] + static_cast<int64_t>(b) * m.n * N + e;
         const int64_t bke = (static_cast<int64_t>(b) * crt.k + j) * N + e;
         colx[bke] = static_cast<uint16_t>(static_cast<uint16_t>(L[0]) % m.q);
         hx[bke] = aes_encrypt(aes, compress_cm(L, N, m));
@@ -846,7 +846,7 @@ __global__ __launch_bounds__(256) void k_base_ext(BEArgs a, Act x, const ModC* m
     auto W = [&](int pos) { return a.work + ((static_cast<int64_t>(b) * E + pos) * 128) * N + e; };
     for (int i = 0; i < E; ++i) {
         const ModC m = mc[a.swapped[i]];
-        const int16_t* src = x.p[a.src[i]] + static_cast<int64_t>(b) * m.n * N + e;
+        const act_t* src = x.p[a.src[i]] + static_cast<int64_t>(b) * m.n * N + e;
         int16_t* w = W(i);
         col_map(src, w, N, static_cast<int>(m.n), [](int, int16_t v) { return v; });
     }
@@ -879,7 +879,7 @@ __global__ __launch_bounds__(256) void k_base_ext(BEArgs a, Act x, const ModC* m
         const int q = a.swapped[a.extra_pos[xi]];
         const ModC m = mc[q];
         const int16_t* w = W(a.extra_pos[xi]);
-        int16_t* dst = x.p[r] + static_cast<int64_t>(b) * m.n * N + e;
+        act_t* dst = x.p[r] + static_cast<int64_t>(b) * m.n * N + e;
         const int32_t f = a.invv[xi];  // already negated mod q on the host
         col_map(w, dst, N, static_cast<int>(m.n), [&](int, int16_t v) { return static_cast<int16_t>(modq(static_cast<uint32_t>(v * f), m)); });
     }
@@ -896,14 +896,14 @@ __global__ __launch_bounds__(kAesBlock, kAesMinBlocks) void k_proj(ProjArgs a, A
     for (int64_t e = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; e < N;
          e += static_cast<int64_t>(gridDim.x) * blockDim.x) {
     const ModC mi = mc[a.pin[j]], mo = mc[a.pout[j]];
-    const int16_t* L = x.p[j] + static_cast<int64_t>(b) * mi.n * N + e;
+    const act_t* L = x.p[j] + static_cast<int64_t>(b) * mi.n * N + e;
     const u128 H = aes_encrypt(aes, compress_cm(L, N, mi));
     const uint32_t col = static_cast<uint16_t>(L[0]) % mi.q;
     const u128 P = a.tab[j][(static_cast<int64_t>(b) * N + e) * mi.q + col] - H;
     DigitStream s;
     s.init(P);
-    int16_t* O = y.p[j] + static_cast<int64_t>(b) * mo.n * N + e;
-    for (int i = 0; i < static_cast<int>(mo.n); ++i) O[i * N] = static_cast<int16_t>(s.next(mo));
+    act_t* O = y.p[j] + static_cast<int64_t>(b) * mo.n * N + e;
+    for (int i = 0; i < static_cast<int>(mo.n); ++i) O[i * N] = static_cast<act_t>(s.next(mo));
     }
 }
 
@@ -918,8 +918,8 @@ __global__ __launch_bounds__(kAesBlock, kAesMinBlocks) void k_mult(MultArgs a, A
          o += static_cast<int64_t>(gridDim.x) * blockDim.x) {
     const int p = a.crt.p[j];
     const ModC m = mc[p];
-    const int16_t* X = x.p[j] + static_cast<int64_t>(b) * m.n * Ni + 2 * o;
-    const int16_t* Yv = X + 1;
+    const act_t* X = x.p[j] + static_cast<int64_t>(b) * m.n * Ni + 2 * o;
+    const act_t* Yv = X + 1;
     const int64_t bo = static_cast<int64_t>(b) * No + o;
     const u128 Hx = aes_encrypt(aes, compress_cm(X, Ni, m));
     const uint32_t colx = static_cast<uint16_t>(X[0]) % p;
@@ -948,7 +948,7 @@ __global__ __launch_bounds__(kAesBlock, kAesMinBlocks) void k_mult(MultArgs a, A
     DigitStream sg, se;
     sg.init(G);
     se.init(E);
-    int16_t* O = y.p[j] + static_cast<int64_t>(b) * m.n * No + o;
+    act_t* O = y.p[j] + static_cast<int64_t>(b) * m.n * No + o;
     const int n = static_cast<int>(m.n);
     for (int i0 = 0; i0 < n; i0 += kChunk) {
         int16_t xv[kChunk];
@@ -962,7 +962,7 @@ __global__ __launch_bounds__(kAesBlock, kAesMinBlocks) void k_mult(MultArgs a, A
                 const int32_t ev = static_cast<int32_t>(se.next(m));
                 int32_t v = (ev + ypr * static_cast<int32_t>(xv[u]) - gv) % p;
                 if (v < 0) v += p;
-                O[(i0 + u) * No] = static_cast<int16_t>(v);
+                O[(i0 + u) * No] = static_cast<act_t>(v);
             }
     }
     }

@@ -36,7 +36,7 @@ __global__ __launch_bounds__(256) void k_dense(DenseArgs a, Act x, Act y, const 
     const int64_t o = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
     if (o >= a.O) return;
     const int p = a.crt.p[j], n = a.crt.n[j];
-    const int16_t* X = x.p[j] + (static_cast<int64_t>(b) * n + c) * a.K;
+    const act_t* X = x.p[j] + (static_cast<int64_t>(b) * n + c) * a.K;
     const int16_t* W = a.w[j];
     int32_t acc = 0;
     for (int64_t i = 0; i < a.K; ++i) {
@@ -47,7 +47,7 @@ __global__ __launch_bounds__(256) void k_dense(DenseArgs a, Act x, Act y, const 
     const int32_t zc = a.zc[j][o];
     const int16_t zv = a.zero[static_cast<int64_t>(b) * a.lab_stride + a.lab_off[j] + c];
     const int16_t bv = a.bias[j][(static_cast<int64_t>(b) * a.O + o) * n + c];
-    y.p[j][(static_cast<int64_t>(b) * n + c) * a.O + o] = static_cast<int16_t>(mod_p(acc % p + zc * zv + bv, p));
+    y.p[j][(static_cast<int64_t>(b) * n + c) * a.O + o] = static_cast<act_t>(mod_p(acc % p + zc * zv + bv, p));
 }
 
 // VALU conv: grid (ceil(OH*OW/256), F, B*sum_n)
@@ -62,7 +62,7 @@ __global__ __launch_bounds__(256) void k_conv_valu(ConvArgs a, Act x, Act y, con
     if (pos >= npos) return;
     const int oy = pos / a.OW, ox = pos % a.OW;
     const int p = a.crt.p[j], n = a.crt.n[j];
-    const int16_t* X = x.p[j] + (static_cast<int64_t>(b) * n + c) * a.C * a.H * a.W;
+    const act_t* X = x.p[j] + (static_cast<int64_t>(b) * n + c) * a.C * a.H * a.W;
     const int16_t* Wf = a.w[j] + static_cast<int64_t>(f) * a.C * a.kh * a.kw;
     const int16_t zv = a.zero[static_cast<int64_t>(b) * a.lab_stride + a.lab_off[j] + c];
     int32_t acc = 0;
@@ -82,7 +82,7 @@ __global__ __launch_bounds__(256) void k_conv_valu(ConvArgs a, Act x, Act y, con
     const int32_t zc = a.zc[j][f];
     const int16_t bv = a.bias[j][(static_cast<int64_t>(b) * a.F + f) * n + c];
     y.p[j][((static_cast<int64_t>(b) * n + c) * a.F + f) * npos + pos] =
-        static_cast<int16_t>(mod_p(acc % p + zc * zv + bv, p));
+        static_cast<act_t>(mod_p(acc % p + zc * zv + bv, p));
 }
 
 // ---------------------------------------------------------------------------
@@ -117,7 +117,7 @@ __global__ __launch_bounds__(256) void k_conv_mfma(ConvArgs a, Act x, Act y, int
         soy = pos / a.OW;
         sox = pos % a.OW;
     }
-    const int16_t* X = x.p[j] + (static_cast<int64_t>(sb) * n + sc) * a.C * a.H * a.W;
+    const act_t* X = x.p[j] + (static_cast<int64_t>(sb) * n + sc) * a.C * a.H * a.W;
     const int16_t zv = colok ? a.zero[static_cast<int64_t>(sb) * a.lab_stride + a.lab_off[j] + sc] : 0;
     const int8_t* W8 = a.w8[j];
     v4i acc[4];
@@ -179,7 +179,7 @@ __global__ __launch_bounds__(256) void k_conv_mfma(ConvArgs a, Act x, Act y, int
             const int32_t zc = a.zc[j][f];
             const int16_t bv = a.bias[j][(static_cast<int64_t>(b) * a.F + f) * n + c];
             y.p[j][((static_cast<int64_t>(b) * n + c) * a.F + f) * npos + pos] =
-                static_cast<int16_t>(mod_p(acc[t][r] % p + zc * zvv + bv, p));
+                static_cast<act_t>(mod_p(acc[t][r] % p + zc * zvv + bv, p));
         }
     }
 }
@@ -211,7 +211,7 @@ __global__ __launch_bounds__(256) void k_conv_img(ConvArgs a, Act x, Act y, int 
     const int in_rows = (oy1 - oy0 - 1) * a.sh + a.kh;
     const int S = a.Cpad + 16, Wp = a.W + 2 * a.pw;
     const int HW = a.H * a.W;
-    const int16_t* X = x.p[j] + (static_cast<int64_t>(b) * n + c) * a.C * HW;
+    const act_t* X = x.p[j] + (static_cast<int64_t>(b) * n + c) * a.C * HW;
     const int16_t zv = a.zero[static_cast<int64_t>(b) * a.lab_stride + a.lab_off[j] + c];
     const int zc8 = zv > half ? zv - p : zv;
     const int tid = threadIdx.x;
@@ -232,7 +232,7 @@ __global__ __launch_bounds__(256) void k_conv_img(ConvArgs a, Act x, Act y, int 
         for (int q = 0; q < 4; ++q) {
             const int ci = c4 * 4 + q;
             if (ci >= a.C) continue;
-            const int16_t* row = X + static_cast<int64_t>(ci) * HW + static_cast<int64_t>(iy) * a.W;
+            const act_t* row = X + static_cast<int64_t>(ci) * HW + static_cast<int64_t>(iy) * a.W;
 #pragma unroll
             for (int t = 0; t < 4; ++t) {
                 const int ix = xq * 4 + t - a.pw;
@@ -262,7 +262,7 @@ __global__ __launch_bounds__(256) void k_conv_img(ConvArgs a, Act x, Act y, int 
     const int npos = a.OH * a.OW;
     const int32_t* zcp = a.zc[j];
     const int16_t* bias = a.bias[j];
-    int16_t* Y = y.p[j] + (static_cast<int64_t>(b) * n + c) * a.F * npos;
+    act_t* Y = y.p[j] + (static_cast<int64_t>(b) * n + c) * a.F * npos;
     for (int col0 = 0; col0 < ncol; col0 += 64) {
         v4i acc[4];
         int base[4];
@@ -297,7 +297,7 @@ __global__ __launch_bounds__(256) void k_conv_img(ConvArgs a, Act x, Act y, int 
                 if (f >= a.F) continue;
                 const int16_t bv = bias[(static_cast<int64_t>(b) * a.F + f) * n + c];
                 Y[static_cast<int64_t>(f) * npos + pos] =
-                    static_cast<int16_t>(mod_p(acc[t][r] % p + zcp[f] * zv + bv, p));
+                    static_cast<act_t>(mod_p(acc[t][r] % p + zcp[f] * zv + bv, p));
             }
         }
     }
@@ -342,7 +342,7 @@ __global__ __launch_bounds__(256) void k_conv_img2(ConvArgs a, Act x, Act y, int
     const int in_rows = (oy1 - oy0 - 1) * a.sh + a.kh;
     const int S = a.ldsS, R = a.ldsR, Wp = a.W + 2 * a.pw;
     const int HW = a.H * a.W;
-    const int16_t* X = x.p[j] + (static_cast<int64_t>(b) * n + c) * a.C * HW;
+    const act_t* X = x.p[j] + (static_cast<int64_t>(b) * n + c) * a.C * HW;
     const int16_t zv = a.zero[static_cast<int64_t>(b) * a.lab_stride + a.lab_off[j] + c];
     const int zc8 = zv > half ? zv - p : zv;
     const int tid = threadIdx.x;
@@ -377,19 +377,16 @@ __global__ __launch_bounds__(256) void k_conv_img2(ConvArgs a, Act x, Act y, int
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
             const int ci = c4 * 4 + q;
-            const int16_t* row = X + static_cast<int64_t>(ci) * HW + static_cast<int64_t>(iy) * a.W;
+            const act_t* row = X + static_cast<int64_t>(ci) * HW + static_cast<int64_t>(iy) * a.W;
             if (ci >= a.C) {
 #pragma unroll
                 for (int u = 0; u < 8; ++u) v[q][u] = 0;
             } else if (full) {
-                // one 16-B load of 8 int16 (2-B aligned: global loads take unaligned addresses on gfx950;
-                // a packed-struct memcpy compiled to 8 ushort loads)
-                const u32x4c t = *reinterpret_cast<const u32x4c*>(row + ix0);
+                // one 8-B load of 8 byte components (unaligned: global loads take any address on gfx950)
+                typedef uint32_t u32x2c __attribute__((ext_vector_type(2)));
+                const u32x2c t = *reinterpret_cast<const u32x2c*>(row + ix0);
 #pragma unroll
-                for (int u = 0; u < 4; ++u) {
-                    v[q][2 * u] = static_cast<int>(t[u] & 0xffffu);
-                    v[q][2 * u + 1] = static_cast<int>(t[u] >> 16);
-                }
+                for (int u = 0; u < 8; ++u) v[q][u] = static_cast<int>((t[u >> 2] >> (8 * (u & 3))) & 0xffu);
             } else {
 #pragma unroll
                 for (int u = 0; u < 8; ++u) {
@@ -429,7 +426,7 @@ __global__ __launch_bounds__(256) void k_conv_img2(ConvArgs a, Act x, Act y, int
     const int npos = a.OH * a.OW;
     const int32_t* zcp = a.zc[j];
     const int16_t* bias = a.bias[j];
-    int16_t* Y = y.p[j] + (static_cast<int64_t>(b) * n + c) * a.F * npos;
+    act_t* Y = y.p[j] + (static_cast<int64_t>(b) * n + c) * a.F * npos;
     const uint32_t mq = a.mq[j];
     // tap offsets of the A-in-VGPR path, once per block (the k-step loop then only adds)
     int toff[AREG ? KSC : 1];
@@ -499,7 +496,7 @@ __global__ __launch_bounds__(256) void k_conv_img2(ConvArgs a, Act x, Act y, int
                 const int f = fw + (lane >> 4) * 4 + r;
                 if (f >= a.F) continue;
                 const uint32_t v = static_cast<uint32_t>(acc[t][r]) + addc[r];
-                Y[static_cast<int64_t>(f) * npos + pos] = static_cast<int16_t>(modq_conv(v, static_cast<uint32_t>(p), mq));
+                Y[static_cast<int64_t>(f) * npos + pos] = static_cast<act_t>(modq_conv(v, static_cast<uint32_t>(p), mq));
             }
         }
     }

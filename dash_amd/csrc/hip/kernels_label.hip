@@ -1,6 +1,8 @@
 // Free (non-cryptographic) label kernels: gathers, pair differences / sums
 // for the max-pool reduction tree, residual add, window sums, plus small
 // parity-test kernels for the AES and digit codecs.
+#include <algorithm>
+
 #include "launch.h"
 
 namespace dash {
@@ -26,9 +28,9 @@ __global__ __launch_bounds__(256) void k_pair_diff(Act v, int64_t Nv, Act d, int
     const int64_t t = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
     if (t >= Nd * n) return;
     const int64_t c = t / Nd, e = t % Nd, o = e / ops, q = e % ops;
-    const int16_t* V = v.p[j] + (static_cast<int64_t>(b) * n + c) * Nv + o * cnt + 2 * q;
+    const act_t* V = v.p[j] + (static_cast<int64_t>(b) * n + c) * Nv + o * cnt + 2 * q;
     int32_t x = V[1] - V[0];
-    d.p[j][(static_cast<int64_t>(b) * n + c) * Nd + e] = static_cast<int16_t>(x < 0 ? x + p : x);
+    d.p[j][(static_cast<int64_t>(b) * n + c) * Nd + e] = static_cast<act_t>(x < 0 ? x + p : x);
 }
 
 // nv[o*cnt1+q] = v[o*cnt+2q] + r[o*ops+q]; odd leftover copied to slot ops
@@ -40,11 +42,11 @@ __global__ __launch_bounds__(256) void k_pair_add(Act v, int64_t Nv, Act r, Act 
     const int64_t t = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
     if (t >= Nn * n) return;
     const int64_t c = t / Nn, e = t % Nn, o = e / cnt1, q = e % cnt1;
-    const int16_t* V = v.p[j] + (static_cast<int64_t>(b) * n + c) * Nv + o * cnt;
-    int16_t val;
+    const act_t* V = v.p[j] + (static_cast<int64_t>(b) * n + c) * Nv + o * cnt;
+    act_t val;
     if (q < ops) {
         int32_t x = V[2 * q] + r.p[j][(static_cast<int64_t>(b) * n + c) * Nr + o * ops + q];
-        val = static_cast<int16_t>(x >= p ? x - p : x);
+        val = static_cast<act_t>(x >= p ? x - p : x);
     } else {
         val = V[cnt - 1];
     }
@@ -58,7 +60,7 @@ __global__ __launch_bounds__(256) void k_add(Act x, Act y, int64_t N, CrtInfo cr
     if (t >= N * n) return;
     const int64_t off = static_cast<int64_t>(b) * n * N + t;
     int32_t v = x.p[j][off] + y.p[j][off];
-    x.p[j][off] = static_cast<int16_t>(v >= p ? v - p : v);
+    x.p[j][off] = static_cast<act_t>(v >= p ? v - p : v);
 }
 
 // out[o] = sum_s in[idx[o*K+s]]
@@ -69,10 +71,10 @@ __global__ __launch_bounds__(256) void k_window_sum(Act in, int64_t Nin, Act out
     const int64_t t = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
     if (t >= Nout * n) return;
     const int64_t c = t / Nout, o = t % Nout;
-    const int16_t* I = in.p[j] + (static_cast<int64_t>(b) * n + c) * Nin;
+    const act_t* I = in.p[j] + (static_cast<int64_t>(b) * n + c) * Nin;
     int32_t acc = 0;
     for (int s = 0; s < K; ++s) acc += I[idx[o * K + s]];
-    out.p[j][(static_cast<int64_t>(b) * n + c) * Nout + o] = static_cast<int16_t>(acc % p);
+    out.p[j][(static_cast<int64_t>(b) * n + c) * Nout + o] = static_cast<act_t>(acc % p);
 }
 
 __global__ __launch_bounds__(512) void k_aes_test(const u128* in, u128* out, int64_t n, const uint32_t* te0,
@@ -147,25 +149,46 @@ void launch_window_sum(const Act& in, int64_t Nin, const Act& out, int64_t Nout,
                        crt);
 }
 // out[c][r] = in[r][c]: 64x64 tiles through LDS (row pitch 65: conflict-free
-// column reads), both global sides coalesced. grid (ceil(cols/64), ceil(rows/64))
-__global__ __launch_bounds__(256) void k_transpose16(const int16_t* __restrict__ in, int16_t* __restrict__ out,
-                                                     int64_t rows, int64_t cols) {
+// column reads), both global sides coalesced; element types may differ (label
+// components < 256: int16 host layout <-> byte activations).
+// grid (ceil(cols/64), ceil(rows/64))
+template <class Tin, class Tout>
+__global__ __launch_bounds__(256) void k_transpose(const Tin* __restrict__ in, Tout* __restrict__ out, int64_t rows,
+                                                   int64_t cols) {
     __shared__ int16_t t[64][65];
     const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
     const int64_t c0 = static_cast<int64_t>(blockIdx.x) * 64, r0 = static_cast<int64_t>(blockIdx.y) * 64;
     for (int y = ty; y < 64; y += 4) {
         const int64_t r = r0 + y, c = c0 + tx;
-        if (r < rows && c < cols) t[y][tx] = in[r * cols + c];
+        if (r < rows && c < cols) t[y][tx] = static_cast<int16_t>(in[r * cols + c]);
     }
     __syncthreads();
     for (int y = ty; y < 64; y += 4) {
         const int64_t c = c0 + y, r = r0 + tx;
-        if (r < rows && c < cols) out[c * rows + r] = t[tx][y];
+        if (r < rows && c < cols) out[c * rows + r] = static_cast<Tout>(t[tx][y]);
     }
 }
+__global__ __launch_bounds__(256) void k_narrow(const int16_t* __restrict__ in, act_t* __restrict__ out, int64_t n) {
+    for (int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < n;
+         i += static_cast<int64_t>(gridDim.x) * blockDim.x)
+        out[i] = static_cast<act_t>(in[i]);
+}
+void launch_narrow(const int16_t* in, act_t* out, int64_t n, hipStream_t st) {
+    const unsigned nb = static_cast<unsigned>(std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, 16384)));
+    hipLaunchKernelGGL(k_narrow, dim3(nb), dim3(256), 0, st, in, out, n);
+}
+
+static inline dim3 grid_tr(int64_t rows, int64_t cols) {
+    return dim3(static_cast<unsigned>((cols + 63) / 64), static_cast<unsigned>((rows + 63) / 64));
+}
 void launch_transpose16(const int16_t* in, int16_t* out, int64_t rows, int64_t cols, hipStream_t st) {
-    hipLaunchKernelGGL(k_transpose16, dim3(static_cast<unsigned>((cols + 63) / 64), static_cast<unsigned>((rows + 63) / 64)),
-                       dim3(256), 0, st, in, out, rows, cols);
+    hipLaunchKernelGGL((k_transpose<int16_t, int16_t>), grid_tr(rows, cols), dim3(256), 0, st, in, out, rows, cols);
+}
+void launch_transpose_to_act(const int16_t* in, act_t* out, int64_t rows, int64_t cols, hipStream_t st) {
+    hipLaunchKernelGGL((k_transpose<int16_t, act_t>), grid_tr(rows, cols), dim3(256), 0, st, in, out, rows, cols);
+}
+void launch_transpose_from_act(const act_t* in, int16_t* out, int64_t rows, int64_t cols, hipStream_t st) {
+    hipLaunchKernelGGL((k_transpose<act_t, int16_t>), grid_tr(rows, cols), dim3(256), 0, st, in, out, rows, cols);
 }
 
 void launch_aes_test(const u128* in, u128* out, int64_t n, const AesGlobals& g, hipStream_t st) {

@@ -187,6 +187,9 @@ inline void conv_img_geometry(ConvArgs& a) {
 
 // int16 matrix transpose out[c][r] = in[r][c] (label-major <-> component-major), kernels_label.hip
 void launch_transpose16(const int16_t* in, int16_t* out, int64_t rows, int64_t cols, hipStream_t st);
+void launch_narrow(const int16_t* in, act_t* out, int64_t n, hipStream_t st);  // int16 labels -> byte activations
+void launch_transpose_to_act(const int16_t* in, act_t* out, int64_t rows, int64_t cols, hipStream_t st);
+void launch_transpose_from_act(const act_t* in, int16_t* out, int64_t rows, int64_t cols, hipStream_t st);
 
 }  // namespace dev
 }  // namespace dash

@@ -39,6 +39,9 @@ class HipEvaluator {
         B_ = B;
         crt_ = tmpl_->h.crt;
         k_ = static_cast<int>(crt_.size());
+        for (int p : crt_)
+            DASH_CHECK(p <= kActMaxModulus, "HIP evaluator: CRT modulus " + std::to_string(p) +
+                                                " > 255 (activations are stored as bytes); use the host evaluator");
         DASH_CHECK(k_ <= kMaxRes, "too many CRT residues for the GPU path");
         loaded_.assign(B_, 0);
         build();
@@ -81,8 +84,8 @@ class HipEvaluator {
                 for (i64 e = 0; e < N0_; ++e)
                     for (int c = 0; c < n; ++c) stg[(static_cast<i64>(b) * n + c) * N0_ + e] = L.c[e * n + c];
             }
-            HIPCHECK(hipMemcpyAsync(bufs_[0].p[j], stg, sizeof(int16_t) * B_ * n * N0_, hipMemcpyHostToDevice, st));
         }
+        upload_inputs(st);
     }
 
     // pinned staging slots for GC b (one component-major block per residue)
@@ -127,16 +130,20 @@ class HipEvaluator {
     void fetch_outputs(hipStream_t st) {
         for (int j = 0; j < k_; ++j) {
             const int n = nr_comps(out_mod_[j]);
-            HIPCHECK(hipMemcpyAsync(out_stage_[j], final_.p[j], sizeof(int16_t) * B_ * n * Nout_, hipMemcpyDeviceToHost, st));
+            HIPCHECK(hipMemcpyAsync(out_stage_[j], final_.p[j], sizeof(act_t) * B_ * n * Nout_, hipMemcpyDeviceToHost, st));
         }
         HIPCHECK(hipStreamSynchronize(st));
     }
     int crt_size() const { return k_; }
     i64 output_size() const { return Nout_; }
+    // int16 host staging (the host label format) -> device int16 scratch -> byte activations
     void upload_inputs(hipStream_t st) {
-        for (int j = 0; j < k_; ++j)
-            HIPCHECK(hipMemcpyAsync(bufs_[0].p[j], in_stage_[j], sizeof(int16_t) * B_ * nr_comps(crt_[j]) * N0_,
-                                    hipMemcpyHostToDevice, st));
+        for (int j = 0; j < k_; ++j) {
+            const i64 count = static_cast<i64>(B_) * nr_comps(crt_[j]) * N0_;
+            if (!in16_dev_[j]) in16_dev_[j] = dalloc<int16_t>(static_cast<size_t>(count));
+            HIPCHECK(hipMemcpyAsync(in16_dev_[j], in_stage_[j], sizeof(int16_t) * count, hipMemcpyHostToDevice, st));
+            launch_narrow(in16_dev_[j], bufs_[0].p[j], count, st);
+        }
     }
 
     // The op list is static (all device pointers fixed at build time), so
@@ -181,7 +188,7 @@ class HipEvaluator {
         std::vector<CrtLabels> out(B_);
         for (int j = 0; j < k_; ++j) {
             const int q = out_mod_[j], n = nr_comps(q);
-            HIPCHECK(hipMemcpyAsync(out_stage_[j], final_.p[j], sizeof(int16_t) * B_ * n * Nout_, hipMemcpyDeviceToHost, st));
+            HIPCHECK(hipMemcpyAsync(out_stage_[j], final_.p[j], sizeof(act_t) * B_ * n * Nout_, hipMemcpyDeviceToHost, st));
         }
         HIPCHECK(hipStreamSynchronize(st));
         for (int b = 0; b < B_; ++b)
@@ -365,7 +372,9 @@ class HipEvaluator {
     Act bufs_[4]{};  // ping-pong activation buffers (+ scratch)
     Act final_{};
     Act cur_act_{};
-    std::vector<int16_t*> in_stage_, out_stage_;
+    std::vector<int16_t*> in_stage_;
+    std::vector<act_t*> out_stage_;
+    int16_t* in16_dev_[kMaxRes] = {};  // device int16 copy of the host-encoded inputs (uncompressed input path)
     u128* in_comp_stage_ = nullptr;
     bool use_graph_ = [] {
         const char* e = std::getenv("DASH_HIP_GRAPH");
@@ -396,7 +405,7 @@ class HipEvaluator {
     int16_t* csum_ = nullptr;
     int16_t* be_work_ = nullptr;
     int sign_maxn_ = 32;
-    std::vector<std::vector<int16_t*>> saved_;  // residual-add sources
+    std::vector<std::vector<act_t*>> saved_;  // residual-add sources
 };
 
 void HipEvaluator::build() {
@@ -491,9 +500,9 @@ void HipEvaluator::build() {
         bufs_[bi].N = 0;
         for (int j = 0; j < k_; ++j) {
             const size_t count = static_cast<size_t>(B_) * widest[j] * cap;
-            bufs_[bi].p[j] = dalloc<int16_t>(count);
+            bufs_[bi].p[j] = dalloc<act_t>(count);
             // defined contents before any input is staged (serving primes the hipGraph with an unencoded run)
-            HIPCHECK(hipMemset(bufs_[bi].p[j], 0, count * sizeof(int16_t)));
+            HIPCHECK(hipMemset(bufs_[bi].p[j], 0, count * sizeof(act_t)));
         }
     }
     int tmax = std::max<int>(1, static_cast<int>(m0.h.mrs.size()));
@@ -528,11 +537,11 @@ void HipEvaluator::build() {
     const CrtInfo crt = crt_info(crt_);
     auto save_if_needed = [&](size_t slot, int buf, i64 n_el, const std::vector<int>& md) {
         if (!keep[slot]) return;
-        std::vector<int16_t*> s;
+        std::vector<act_t*> s;
         for (int j = 0; j < k_; ++j) {
-            const size_t bytes = sizeof(int16_t) * B_ * nr_comps(md[j]) * n_el;
-            int16_t* d = dalloc<int16_t>(bytes / sizeof(int16_t));
-            int16_t* src = bufs_[buf].p[j];
+            const size_t bytes = sizeof(act_t) * B_ * nr_comps(md[j]) * n_el;
+            act_t* d = dalloc<act_t>(bytes / sizeof(act_t));
+            act_t* src = bufs_[buf].p[j];
             add_op("save", [d, src, bytes](hipStream_t st) { HIPCHECK(hipMemcpyAsync(d, src, bytes, hipMemcpyDeviceToDevice, st)); });
             s.push_back(d);
         }
@@ -554,9 +563,9 @@ void HipEvaluator::build() {
             N = saved_n[src + 1];
             mods = saved_mods[src + 1];
             for (int j = 0; j < k_; ++j) {
-                const size_t bytes = sizeof(int16_t) * B_ * nr_comps(mods[j]) * N;
-                int16_t* d = bufs_[cur].p[j];
-                const int16_t* sp = sv[j];
+                const size_t bytes = sizeof(act_t) * B_ * nr_comps(mods[j]) * N;
+                act_t* d = bufs_[cur].p[j];
+                const act_t* sp = sv[j];
                 add_op("restore", [d, sp, bytes](hipStream_t st) {
                     HIPCHECK(hipMemcpyAsync(d, sp, bytes, hipMemcpyDeviceToDevice, st));
                 });
@@ -1044,8 +1053,8 @@ void HipEvaluator::build() {
     Nout_ = N;
     out_mod_ = mods;
     for (int j = 0; j < k_; ++j) {
-        int16_t* p = nullptr;
-        HIPCHECK(hipHostMalloc(reinterpret_cast<void**>(&p), sizeof(int16_t) * B_ * nr_comps(mods[j]) * std::max<i64>(Nout_, 1)));
+        act_t* p = nullptr;
+        HIPCHECK(hipHostMalloc(reinterpret_cast<void**>(&p), sizeof(act_t) * B_ * nr_comps(mods[j]) * std::max<i64>(Nout_, 1)));
         host_allocs_.push_back(p);
         out_stage_.push_back(p);
     }
