@@ -75,7 +75,10 @@ def cmd_infer(args):
     B = max(1, cfg.batch if cfg.backend == "hip" else 1)
     for s in range(0, len(xq), B):
         chunk = xq[s:s + B]
-        gcs = [GarbledCircuit(circuit, crt, mrs, max_modulus=mm, nthreads=cfg.nthreads) for _ in chunk]
+        gcs = [GarbledCircuit(circuit, crt, mrs, max_modulus=mm, nthreads=cfg.nthreads,
+                              device=cfg.device if (cfg.garble_device if cfg.garble_device is not None
+                                                     else cfg.backend == "hip") else None,
+                              **cfg.gc_kwargs()) for _ in chunk]
         t = time.perf_counter()
         if cfg.backend == "hip":
             from .runtime import HipEvaluator
@@ -122,7 +125,7 @@ def cmd_run_service(args):
     with InferenceService(circuit, crt, mrs, max_modulus=mm, slots_per_group=max(1, cfg.batch), groups=cfg.groups,
                           backend=cfg.backend, device=cfg.device, garble_device=cfg.garble_device,
                           max_retries=cfg.max_retries, step_timeout_s=cfg.step_timeout_s, seed=cfg.seed_bytes(),
-                          nthreads=cfg.nthreads) as svc:
+                          nthreads=cfg.nthreads, **cfg.gc_kwargs()) as svc:
         ys = svc.infer(xq)
         stats = svc.stats.as_dict()
     preds = [int(np.argmax(y)) for y in ys]
@@ -139,7 +142,8 @@ def cmd_garble(args):
 
     cfg = DashConfig.from_args(args)
     circuit, _, _, _, (crt, mrs, mm) = _circuit_and_inputs(cfg)
-    gc = GarbledCircuit(circuit, crt, mrs, max_modulus=mm, seed=cfg.seed_bytes(), nthreads=cfg.nthreads)
+    gc = GarbledCircuit(circuit, crt, mrs, max_modulus=mm, seed=cfg.seed_bytes(), nthreads=cfg.nthreads,
+                        **cfg.gc_kwargs())
     with open(args.out, "wb") as f:
         f.write(gc.model.serialize())
     if args.decoder_out:
