@@ -244,7 +244,7 @@ def main() -> None:
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": round(value / BASELINE_INF_PER_S, 2),
-            "dtype": "int16 labels / int8 MFMA (exact modular arithmetic)",
+            "dtype": "uint8 label components / int8 MFMA (exact modular arithmetic)",
             "data": "synthetic CIFAR-10-shaped inputs, random-init weights",
             "config": {
                 "model": model,

@@ -103,6 +103,12 @@ struct DigitStream {
         left = 0;
     }
     __device__ __forceinline__ uint32_t next(const ModC& m) {
+#ifdef DASH_FAKE_DECOMP
+        // A/B bound analysis only (wrong digits, in range): a 3-op stand-in for the long division
+        const uint32_t f = min(static_cast<uint32_t>(Q) & 15u, m.q - 1);
+        Q = (Q >> 4) | (Q << 124);
+        return f;
+#endif
         if (m.bits) {
             uint32_t d = static_cast<uint32_t>(Q) & (m.q - 1);
             Q >>= m.bits;
@@ -139,6 +145,10 @@ struct CompressFwd {
         sh = 0;
     }
     __device__ __forceinline__ void push(uint32_t d, const ModC& m) {
+#ifdef DASH_FAKE_COMP
+        v = (v << 1) ^ d;  // A/B bound analysis only
+        return;
+#endif
         if (m.bits) {
             v |= d << bp;
             bp += m.bits;
@@ -161,6 +171,9 @@ struct CompressFwd {
         }
     }
     __device__ __forceinline__ u128 finish() {
+#ifdef DASH_FAKE_COMP
+        return static_cast<u128>(v);
+#endif
         if (bp) C |= static_cast<u128>(v) << sh;  // bits path (bp stays 0 otherwise)
         else if (cnt && v) C += PW * static_cast<u128>(v);
         return C;
@@ -171,7 +184,10 @@ struct CompressFwd {
 // iteration waits for its own load pays one HBM round trip per component
 // (the compiler does not hoist loads across a runtime-trip-count loop, nor
 // past a store to the same column): stage kChunk loads first, then consume.
-constexpr int kChunk = 16;
+#ifndef DASH_KCHUNK
+#define DASH_KCHUNK 16
+#endif
+constexpr int kChunk = DASH_KCHUNK;
 
 // dst[c * stride] = f(c, src[c * stride]) for c < n, kChunk loads per round
 // trip (dst may alias src; f is called in component order)
@@ -235,7 +251,7 @@ __device__ __forceinline__ uint32_t u128_mod(u128 P, const ModC& m) {
 // DASH_AES_COPIES < 32 shrinks the image (2 KiB per copy) at the price of
 // (32 / copies)-way bank conflicts: more resident blocks per CU (A/B knob).
 #ifndef DASH_AES_COPIES
-#define DASH_AES_COPIES 32
+#define DASH_AES_COPIES 16
 #endif
 #define DASH_AES_LDS_BYTES (2048 * DASH_AES_COPIES)
 #define DASH_AES_LDS_WORDS (DASH_AES_LDS_BYTES / 4)

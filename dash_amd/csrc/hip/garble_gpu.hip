@@ -148,7 +148,7 @@ struct Gadget {
 
 // Stage a gadget's small descriptor array (draws / projections) in LDS so the
 // per-thread binary search costs LDS, not dependent global round trips.
-constexpr int kMaxDesc = 224;  // 224 x 72-B Proj + the 64 KiB AES image <= 80 KiB: 2 WGs/CU
+constexpr int kMaxDesc = 224;  // 224 x 72-B Proj (16 KiB) beside the AES image (dev.h)
 constexpr int kGB = 512;        // threads per block of the AES-bound garbling kernels
 template <class T>
 __device__ __forceinline__ void lds_stage(T* dst, const T* src, int n) {

@@ -23,28 +23,38 @@ namespace dev {
 
 constexpr size_t kAesLds = 0;  // AES image is static LDS
 
-// AES kernels hold a 64 KiB LDS image per block, so at most two blocks fit a
-// CU. Measured on MiniONN B=24 x 4 streams (inf/s): 512 threads / 64 VGPRs 354,
-// 1024 threads (2x the resident waves) 347, 512 threads / 128 VGPRs 345: the
-// concurrent stream groups already fill the CUs, finer blocks pack better.
+// AES kernels hold the LDS image (dev.h: 32 KiB at 16 copies) per block; the
+// second launch bound is the minimum number of waves per SIMD, so it sets the
+// register budget: 4 -> 128 VGPRs, 6 -> 80, 8 -> 64. Measured on MiniONN,
+// 24 GCs, one stream (ms per step, scripts/ab_online.py): 64 KiB image at 4
+// waves/SIMD 20.9; 32 KiB image at 6 waves/SIMD 19.7 (the mixed-radix chain
+// 7.4 -> 6.9 ms, approx phase 4.5 -> 4.1); at 8 waves/SIMD the chain spills
+// (9.3 ms) while the approx phase gains again (4.0), so that kernel has its
+// own bound. The 2-way bank conflicts of 16 copies cost less than the extra
+// resident waves buy: these kernels wait on HBM, AES is ~3 % of their time.
 #ifndef DASH_AES_BLOCK
 #define DASH_AES_BLOCK 512
 #endif
 constexpr int kAesBlock = DASH_AES_BLOCK;
 #ifndef DASH_AES_MINBLOCKS
-#define DASH_AES_MINBLOCKS (2048 / DASH_AES_BLOCK)
+#define DASH_AES_MINBLOCKS 6
 #endif
-constexpr int kAesMinBlocks = DASH_AES_MINBLOCKS;  // sets the VGPR budget (2048/block -> 64 VGPRs)
+constexpr int kAesMinBlocks = DASH_AES_MINBLOCKS;  // minimum waves per SIMD (register budget)
+#ifndef DASH_SA_MINBLOCKS
+#define DASH_SA_MINBLOCKS 8
+#endif
+constexpr int kSignApproxMinWaves = DASH_SA_MINBLOCKS;
 
 // AES kernels stride over their elements so the LDS image is filled once per
-// resident block: resident blocks per CU (LDS image / VGPR bound), x4 for tail
-// balance (64 KiB image: 2 per CU).
+// resident block: resident blocks per CU (register budget: waves per SIMD x 4
+// SIMDs x 64 lanes / block size; LDS: 160 KiB / image), x4 for tail balance.
 static int aes_block_cap() {
     static int cap = [] {
         int dev = 0, cus = 256;
         if (hipGetDevice(&dev) == hipSuccess) hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-        const int resident = std::max(1, std::min(kAesMinBlocks * kAesBlock / 512, 160 * 1024 / DASH_AES_LDS_BYTES));
-        return 4 * resident * cus * 512 / kAesBlock;
+        const int waves = std::max(kAesMinBlocks, kSignApproxMinWaves);
+        const int resident = std::max(1, std::min(waves * 256 / kAesBlock, 160 * 1024 / DASH_AES_LDS_BYTES));
+        return 4 * resident * cus;
     }();
     return cap;
 }
@@ -116,7 +126,7 @@ __device__ __forceinline__ void approx_casts_out(const AesCtx& aes, const SignAr
 
 // Phase A: approximate residues + their casts. grid (x, k, B)
 template <int TM>
-__global__ __launch_bounds__(kAesBlock, kAesMinBlocks) void k_sign_approx(SignArgs a, Act x, const ModC* mc, const uint32_t* te0,
+__global__ __launch_bounds__(kAesBlock, kSignApproxMinWaves) void k_sign_approx(SignArgs a, Act x, const ModC* mc, const uint32_t* te0,
                                                      const uint32_t* rk) {
     AES_PROLOGUE(te0, rk);
     const int j = blockIdx.y, b = blockIdx.z;
@@ -392,20 +402,27 @@ __global__ __launch_bounds__(256) void k_relu_mult(SignArgs a, Act x, Act y, con
     sg.init(G);
     se.init(E);
     const int n = static_cast<int>(m.n);
+    // the next chunk's loads go out before this chunk's stores: vmcnt retires in issue order, so a
+    // load issued after a store would also wait for that store
+    uint16_t cur[kChunk], nxt[kChunk];
+#pragma unroll
+    for (int u = 0; u < kChunk; ++u)
+        if (u < n) cur[u] = X[static_cast<int64_t>(u) * N];
     for (int i0 = 0; i0 < n; i0 += kChunk) {
-        int16_t xv[kChunk];
 #pragma unroll
         for (int u = 0; u < kChunk; ++u)
-            if (i0 + u < n) xv[u] = X[(i0 + u) * N];
+            if (i0 + kChunk + u < n) nxt[u] = X[static_cast<int64_t>(i0 + kChunk + u) * N];
 #pragma unroll
         for (int u = 0; u < kChunk; ++u)
             if (i0 + u < n) {
                 const uint32_t g = sg.next(m);
                 const uint32_t ev = se.next(m);
                 // all terms in [0, p): ev + ypr * x + (p - g) < p^2 + 2p
-                Y[(i0 + u) * N] = static_cast<act_t>(
-                    modq(ev + ypr * static_cast<uint32_t>(static_cast<uint16_t>(xv[u])) + static_cast<uint32_t>(p) - g, m));
+                Y[static_cast<int64_t>(i0 + u) * N] =
+                    static_cast<act_t>(modq(ev + ypr * static_cast<uint32_t>(cur[u]) + static_cast<uint32_t>(p) - g, m));
             }
+#pragma unroll
+        for (int u = 0; u < kChunk; ++u) cur[u] = nxt[u];
     }
 }
 
@@ -663,7 +680,10 @@ __device__ __forceinline__ u128 add_packed(u128 a, u128 b, u128 hmask) {
 // payloads P_{l,j} of digit l for later residues j go to a per-lane scratch
 // (a.ps, [B][pair][N], coalesced) and are read back when digit j starts:
 // holding them in registers (up to K(K-1)/2 u128) spilled.
-constexpr int kMrsChunk = 8;
+#ifndef DASH_MRS_CHUNK
+#define DASH_MRS_CHUNK 8
+#endif
+constexpr int kMrsChunk = DASH_MRS_CHUNK;
 template <int K>
 __device__ __forceinline__ constexpr int mrs_pair(int l, int j) {  // l < j < K
     return l * (2 * K - l - 1) / 2 + (j - l - 1);
@@ -770,17 +790,20 @@ __global__ __launch_bounds__(256) void k_rescale_mrs_out(MrsArgs a, Act x, const
         return;
     }
     const uint32_t inv = static_cast<uint32_t>(a.sinv[j]);
-    const uint32_t q = m.q;
+    uint16_t cur[kChunk], nxt[kChunk];  // loads of chunk c+1 before the stores of chunk c (as k_relu_mult)
+#pragma unroll
+    for (int u = 0; u < kChunk; ++u)
+        if (u < n) cur[u] = L[static_cast<int64_t>(u) * N];
     for (int c0 = 0; c0 < n; c0 += kChunk) {
-        uint16_t v[kChunk];
 #pragma unroll
         for (int u = 0; u < kChunk; ++u)
-            if (c0 + u < n) v[u] = static_cast<uint16_t>(L[static_cast<int64_t>(c0 + u) * N]);
+            if (c0 + kChunk + u < n) nxt[u] = L[static_cast<int64_t>(c0 + kChunk + u) * N];
 #pragma unroll
         for (int u = 0; u < kChunk; ++u)
             if (c0 + u < n)
-                L[static_cast<int64_t>(c0 + u) * N] = static_cast<act_t>(modq(v[u] * inv + s.next(m), m));  // < p^2 + p
-        (void)q;
+                L[static_cast<int64_t>(c0 + u) * N] = static_cast<act_t>(modq(cur[u] * inv + s.next(m), m));  // < p^2 + p
+#pragma unroll
+        for (int u = 0; u < kChunk; ++u) cur[u] = nxt[u];
     }
 }
 
