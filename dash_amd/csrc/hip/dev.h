@@ -31,15 +31,18 @@ struct ModC {
     uint64_t mD;     // floor(2^64 / D)
     uint32_t mq;     // floor(2^32 / q)
     uint32_t bits;   // log2 q if power of two, else 0
+    uint32_t dm;     // digit magic: floor(r / q) = mulhi(r, dm) >> ds for r < D (host_util.h make_modc)
+    uint32_t ds;
 };
 
 __device__ __forceinline__ uint64_t mulhi64(uint64_t a, uint64_t b) { return __umul64hi(a, b); }
 
 // floor(x / D), x < D * 2^32 (so the quotient fits 32 bits)
 __device__ __forceinline__ uint32_t div64_32(uint64_t x, uint32_t D, uint64_t mD, uint32_t& rem) {
+    // mD = floor(2^64 / D) underestimates x / D by less than 2, so one correction (a select, no loop)
     uint64_t q = mulhi64(x, mD);
     uint64_t r = x - q * D;
-    while (r >= D) {
+    if (r >= D) {
         r -= D;
         ++q;
     }
@@ -93,6 +96,12 @@ __device__ __forceinline__ uint32_t divmod128(u128& Q, uint32_t D, uint64_t mD) 
     return r;
 }
 
+#ifndef DASH_DIGIT_MAGIC
+#define DASH_DIGIT_MAGIC 1
+#endif
+#ifndef DASH_CHUNK_BITS
+#define DASH_CHUNK_BITS 31  // D = q^c <= 2^DASH_CHUNK_BITS (31 for the digit magic)
+#endif
 // Streaming decompress: digits of P in base q, least significant first.
 struct DigitStream {
     u128 Q;
@@ -118,8 +127,16 @@ struct DigitStream {
             r = divmod128(Q, m.D, m.mD);
             left = m.c;
         }
+        // r < D <= 2^31: exact quotient by multiply-high + shift; the digit (< q < 2^24) from the low
+        // 24 bits of r - quot * q, so the product can be the full-rate 24-bit multiply
+#if DASH_DIGIT_MAGIC
+        const uint32_t quot = __umulhi(r, m.dm) >> m.ds;
+        const uint32_t d = (r - __umul24(quot, m.q)) & 0xFFFFFFu;
+        r = quot;
+#else
         uint32_t d;
         r = div32_q(r, m.q, m.mq, d);
+#endif
         --left;
         return d;
     }
@@ -206,18 +223,18 @@ __device__ __forceinline__ void col_map(const T* src, U* dst, long stride, int n
 
 // compress of a label stored component-major: L[i * stride], streamed from
 // the least significant component, kChunk loads in flight per round trip
-template <class T>
+template <int CH = kChunk, class T>
 __device__ __forceinline__ u128 compress_cm(const T* L, long stride, const ModC& m) {
     const int n = m.n;
     CompressFwd cf;
     cf.init();
-    for (int i0 = 0; i0 < n; i0 += kChunk) {
-        uint16_t v[kChunk];
+    for (int i0 = 0; i0 < n; i0 += CH) {
+        uint16_t v[CH];
 #pragma unroll
-        for (int u = 0; u < kChunk; ++u)
+        for (int u = 0; u < CH; ++u)
             if (i0 + u < n) v[u] = static_cast<uint16_t>(L[static_cast<long>(i0 + u) * stride]);
 #pragma unroll
-        for (int u = 0; u < kChunk; ++u)
+        for (int u = 0; u < CH; ++u)
             if (i0 + u < n) cf.push(v[u], m);
     }
     return cf.finish();

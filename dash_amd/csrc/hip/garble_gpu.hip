@@ -376,6 +376,8 @@ __device__ __forceinline__ ModC rfl_modc(const ModC& m) {
     r.mD = static_cast<uint64_t>(rfl64(static_cast<int64_t>(m.mD)));
     r.mq = rflu(m.mq);
     r.bits = rflu(m.bits);
+    r.dm = rflu(m.dm);
+    r.ds = rflu(m.ds);
     return r;
 }
 __device__ __forceinline__ Proj rfl_proj(const Proj& p) {

@@ -4,6 +4,8 @@
 
 #include <hip/hip_runtime.h>
 
+#include <cstdio>
+#include <cstdlib>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -82,9 +84,12 @@ inline dev::ModC make_modc(int q) {
         m.D = q;
         return m;
     }
+    // chunks of c digits with D = q^c <= 2^31, so that floor(r / q) for r < D is one multiply-high and a
+    // shift: with s = ceil(log2 q) - 1 and dm = ceil(2^(32+s) / q) < 2^32, the error e = dm*q - 2^(32+s) < q
+    // gives r*e < D*q <= 2^31 * 2^(s+1) = 2^(32+s), hence floor(r*dm / 2^(32+s)) = floor(r / q)
     uint64_t D = q;
     int c = 1;
-    while (D * static_cast<uint64_t>(q) < (1ull << 32)) {
+    while (D * static_cast<uint64_t>(q) <= (1ull << DASH_CHUNK_BITS)) {
         D *= q;
         ++c;
     }
@@ -92,6 +97,15 @@ inline dev::ModC make_modc(int q) {
     m.D = static_cast<uint32_t>(D);
     m.mD = static_cast<uint64_t>((static_cast<u128>(1) << 64) / D);
     m.mq = static_cast<uint32_t>((1ull << 32) / static_cast<uint64_t>(q));
+    int s = 0;
+    while ((1 << (s + 1)) < q) ++s;  // 2^s < q <= 2^(s+1)
+    const uint64_t two = 1ull << (32 + s);
+    m.dm = static_cast<uint32_t>((two + q - 1) / q);
+    m.ds = static_cast<uint32_t>(s);
+    if (DASH_DIGIT_MAGIC && (static_cast<u128>(D) * (static_cast<uint64_t>(m.dm) * q - two) > two || q >= (1 << 24))) {
+        std::fprintf(stderr, "dash: no 32-bit digit magic for modulus %d\n", q);
+        std::abort();
+    }
     return m;
 }
 

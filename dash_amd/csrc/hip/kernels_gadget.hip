@@ -29,9 +29,10 @@ constexpr size_t kAesLds = 0;  // AES image is static LDS
 // 24 GCs, one stream (ms per step, scripts/ab_online.py): 64 KiB image at 4
 // waves/SIMD 20.9; 32 KiB image at 6 waves/SIMD 19.7 (the mixed-radix chain
 // 7.4 -> 6.9 ms, approx phase 4.5 -> 4.1); at 8 waves/SIMD the chain spills
-// (9.3 ms) while the approx phase gains again (4.0), so that kernel has its
-// own bound. The 2-way bank conflicts of 16 copies cost less than the extra
-// resident waves buy: these kernels wait on HBM, AES is ~3 % of their time.
+// (9.3 ms). The approx phase has its own knob (8 waves: 4.0-4.3 ms, within the
+// box-to-box noise of 6) and the chain its own (DASH_UA_MINBLOCKS, 4 waves).
+// The 2-way bank conflicts of 16 copies cost less than the extra resident
+// waves buy: these kernels wait on HBM, AES is ~3 % of their time.
 #ifndef DASH_AES_BLOCK
 #define DASH_AES_BLOCK 512
 #endif
@@ -41,9 +42,13 @@ constexpr int kAesBlock = DASH_AES_BLOCK;
 #endif
 constexpr int kAesMinBlocks = DASH_AES_MINBLOCKS;  // minimum waves per SIMD (register budget)
 #ifndef DASH_SA_MINBLOCKS
-#define DASH_SA_MINBLOCKS 8
+#define DASH_SA_MINBLOCKS 6
 #endif
 constexpr int kSignApproxMinWaves = DASH_SA_MINBLOCKS;
+#ifndef DASH_SA_CHUNK
+#define DASH_SA_CHUNK 16
+#endif
+constexpr int kSignApproxChunk = DASH_SA_CHUNK;  // label loads in flight per lane in the approx phase
 
 // AES kernels stride over their elements so the LDS image is filled once per
 // resident block: resident blocks per CU (register budget: waves per SIMD x 4
@@ -144,7 +149,7 @@ __global__ __launch_bounds__(kAesBlock, kSignApproxMinWaves) void k_sign_approx(
 #pragma unroll
         for (int d = 0; d < TM; ++d)
             if (d < a.t) P[d] = T[col * a.t + d];
-        const u128 C = compress_cm(L, N, m);
+        const u128 C = compress_cm<kSignApproxChunk>(L, N, m);
         const u128 H = aes_encrypt(aes, C);
         const int64_t bke = (static_cast<int64_t>(b) * a.crt.k + j) * N + e;
         if (a.hx) {
@@ -573,8 +578,10 @@ __global__ __launch_bounds__(kAesBlock, kAesMinBlocks) void k_rescale_hash_sign(
 #ifndef DASH_UA_CHUNK
 #define DASH_UA_CHUNK 4
 #endif
+// the mixed-radix chain keeps K-1 digit streams live: at 6 waves/SIMD (80 VGPRs) it spills 240 B per
+// lane; 4 waves/SIMD with 128 VGPRs measured faster (6.36 vs 7.04 ms per 24-GC MiniONN step)
 #ifndef DASH_UA_MINBLOCKS
-#define DASH_UA_MINBLOCKS kAesMinBlocks
+#define DASH_UA_MINBLOCKS 4
 #endif
 constexpr int kChunkUA = DASH_UA_CHUNK;
 template <int TM>
