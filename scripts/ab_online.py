@@ -21,6 +21,7 @@ def main():
     ap.add_argument("--batch", type=int, default=24)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--relu", default="approx")
+    ap.add_argument("--detail", action="store_true", help="also print every op's time")
     args = ap.parse_args()
     sys.path.insert(0, os.path.abspath(args.root))
     import torch
@@ -63,6 +64,8 @@ def main():
         k = op.rsplit(".", 1)[-1] if "." in op else re.sub(r"[0-9_#:]+", "", op)
         kinds[k] = round(kinds.get(k, 0.0) + t_ms, 3)
     print(json.dumps({"root": args.root, "batch": B, "ms_per_step": round(ms, 3), "ops": kinds}))
+    if args.detail:
+        print(json.dumps([(op, round(t_ms, 4)) for op, t_ms in ev.op_times()]))
 
 
 if __name__ == "__main__":

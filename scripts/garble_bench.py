@@ -26,6 +26,7 @@ def main():
     ap.add_argument("--reps", type=int, default=2)
     ap.add_argument("--device", type=int, default=0)
     ap.add_argument("--gpu-only", action="store_true", help="skip the host garbler (profiling)")
+    ap.add_argument("--rescale", default="mrs", help="rescale construction (mrs | legacy)")
     args = ap.parse_args()
     c = build_circuit(args.model, Q.ScaleQuant, args.l, seed=0)
     seed = bytes(range(16))
@@ -36,7 +37,7 @@ def main():
         gc = None
         for _ in range(args.reps):
             t = time.perf_counter()
-            gc = GarbledCircuit(c, args.k, 100.0, seed=seed, device=dev)
+            gc = GarbledCircuit(c, args.k, 100.0, seed=seed, device=dev, rescale=args.rescale)
             times.append(time.perf_counter() - t)
         blobs[mode] = gc.model.serialize()
         print(json.dumps({"mode": mode, "model": args.model, "s_per_gc": round(min(times), 3),
