@@ -53,21 +53,36 @@ constexpr int kSignApproxChunk = DASH_SA_CHUNK;  // label loads in flight per la
 // AES kernels stride over their elements so the LDS image is filled once per
 // resident block: resident blocks per CU (register budget: waves per SIMD x 4
 // SIMDs x 64 lanes / block size; LDS: 160 KiB / image), x4 for tail balance.
-static int aes_block_cap() {
-    static int cap = [] {
-        int dev = 0, cus = 256;
-        if (hipGetDevice(&dev) == hipSuccess) hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-        const int waves = std::max(kAesMinBlocks, kSignApproxMinWaves);
-        const int resident = std::max(1, std::min(waves * 256 / kAesBlock, 160 * 1024 / DASH_AES_LDS_BYTES));
-        return 4 * resident * cus;
+static int num_cus() {
+    static int cus = [] {
+        int dev = 0, n = 256;
+        if (hipGetDevice(&dev) == hipSuccess) hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
+        return n;
     }();
-    return cap;
+    return cus;
+}
+static int aes_block_cap(int bs) {
+    const int waves = std::max(kAesMinBlocks, kSignApproxMinWaves);
+    const int resident = std::max(1, std::min(waves * 256 / bs, 160 * 1024 / DASH_AES_LDS_BYTES));
+    return 4 * resident * num_cus();
 }
 static inline dim3 grid_aes(int64_t n, int bs, int y, int z) {
     int64_t nx = (n + bs - 1) / bs;
-    const int64_t capx = std::max<int64_t>(1, aes_block_cap() / (static_cast<int64_t>(y) * z));
+    const int64_t capx = std::max<int64_t>(1, aes_block_cap(bs) / (static_cast<int64_t>(y) * z));
     return dim3(static_cast<unsigned>(std::min(nx, capx)), y, z);
 }
+// Block size of an AES kernel over n x y x z lanes: kAesBlock when the launch
+// fills every CU at that size, else halved (down to one wave) until it does.
+// Small launches (batch-1 latency, the late small layers) then spread over all
+// CUs with few waves per SIMD, and their lanes are serial chains: a wave that
+// has its SIMD to itself finishes sooner.
+static inline int aes_bs(int64_t n, int y, int z) {
+    const int64_t lanes = n * y * z;
+    int bs = kAesBlock;
+    while (bs > 64 && lanes < static_cast<int64_t>(bs) * num_cus()) bs >>= 1;
+    return bs;
+}
+#define AES_LAUNCH(n, y, z) grid_aes((n), aes_bs((n), (y), (z)), (y), (z)), dim3(aes_bs((n), (y), (z)))
 
 // static (not dynamic) LDS: its address is a link-time constant, so the
 // table base folds into the ds_read offset field
@@ -656,15 +671,15 @@ __global__ __launch_bounds__(kAesBlock, DASH_UA_MINBLOCKS) void k_rescale_update
 
 void launch_rescale_hash_sign(const u128* signP, const u128* du, int64_t N, int B, u128* h0, uint16_t* col0,
                               const AesGlobals& g, hipStream_t st) {
-    hipLaunchKernelGGL(k_rescale_hash_sign, grid_aes(N, kAesBlock, 1, B), dim3(kAesBlock), kAesLds, st, signP, du, N, h0, col0, g.te0, g.rk);
+    hipLaunchKernelGGL(k_rescale_hash_sign, AES_LAUNCH(N, 1, B), kAesLds, st, signP, du, N, h0, col0, g.te0, g.rk);
 }
 void launch_rescale_update_approx(const RescaleArgs& r, const SignArgs& a, const Act& x, const int16_t* delta,
                                   const u128* zh, int B, const ModC* mc, const AesGlobals& g, hipStream_t st) {
     if (a.t <= 5)
-        hipLaunchKernelGGL(k_rescale_update_approx<5>, grid_aes(r.N, kAesBlock, r.crt.k, B), dim3(kAesBlock), kAesLds, st, r, a, x,
+        hipLaunchKernelGGL(k_rescale_update_approx<5>, AES_LAUNCH(r.N, r.crt.k, B), kAesLds, st, r, a, x,
                            delta, zh, mc, g.te0, g.rk);
     else
-        hipLaunchKernelGGL(k_rescale_update_approx<8>, grid_aes(r.N, kAesBlock, r.crt.k, B), dim3(kAesBlock), kAesLds, st, r, a, x,
+        hipLaunchKernelGGL(k_rescale_update_approx<8>, AES_LAUNCH(r.N, r.crt.k, B), kAesLds, st, r, a, x,
                            delta, zh, mc, g.te0, g.rk);
 }
 
@@ -833,12 +848,12 @@ __global__ __launch_bounds__(kAesBlock, kAesMinBlocks) void k_label_hash(Act x, 
 
 void launch_relu_mrs(const MrsArgs& a, const SignArgs& sa, const Act& x, const Act& y, const u128* gtab,
                      const u128* etab, int B, const ModC* mc, const AesGlobals& g, hipStream_t st) {
-    hipLaunchKernelGGL(k_label_hash, grid_aes(a.N, kAesBlock, a.crt.k, B), dim3(kAesBlock), kAesLds, st, x, a.crt, a.N,
+    hipLaunchKernelGGL(k_label_hash, AES_LAUNCH(a.N, a.crt.k, B), kAesLds, st, x, a.crt, a.N,
                        sa.hx, sa.colx, mc, g.te0, g.rk);
-    const dim3 gc = grid_aes(a.N, kAesBlock, 1, B);
+    const dim3 gc = grid_aes(a.N, aes_bs(a.N, 1, B), 1, B), bc(aes_bs(a.N, 1, B));
     switch (a.crt.k) {
 #define DASH_MRS_K(KK) \
-        case KK: hipLaunchKernelGGL((k_mrs_chain<KK, 1>), gc, dim3(kAesBlock), kAesLds, st, a, x, mc, g.te0, g.rk); break;
+        case KK: hipLaunchKernelGGL((k_mrs_chain<KK, 1>), gc, bc, kAesLds, st, a, x, mc, g.te0, g.rk); break;
         DASH_MRS_K(2) DASH_MRS_K(3) DASH_MRS_K(4) DASH_MRS_K(5) DASH_MRS_K(6) DASH_MRS_K(7) DASH_MRS_K(8)
         DASH_MRS_K(9) DASH_MRS_K(10) DASH_MRS_K(11) DASH_MRS_K(12)
 #undef DASH_MRS_K
@@ -848,10 +863,10 @@ void launch_relu_mrs(const MrsArgs& a, const SignArgs& sa, const Act& x, const A
 }
 
 void launch_rescale_mrs(const MrsArgs& a, const Act& x, int B, const ModC* mc, const AesGlobals& g, hipStream_t st) {
-    const dim3 gc = grid_aes(a.N, kAesBlock, 1, B);
+    const dim3 gc = grid_aes(a.N, aes_bs(a.N, 1, B), 1, B), bc(aes_bs(a.N, 1, B));
     switch (a.crt.k) {
 #define DASH_MRS_K(KK) \
-        case KK: hipLaunchKernelGGL((k_mrs_chain<KK, 0>), gc, dim3(kAesBlock), kAesLds, st, a, x, mc, g.te0, g.rk); break;
+        case KK: hipLaunchKernelGGL((k_mrs_chain<KK, 0>), gc, bc, kAesLds, st, a, x, mc, g.te0, g.rk); break;
         DASH_MRS_K(2) DASH_MRS_K(3) DASH_MRS_K(4) DASH_MRS_K(5) DASH_MRS_K(6) DASH_MRS_K(7) DASH_MRS_K(8)
         DASH_MRS_K(9) DASH_MRS_K(10) DASH_MRS_K(11) DASH_MRS_K(12)
 #undef DASH_MRS_K
@@ -1007,35 +1022,35 @@ static inline dim3 grid_for(int64_t n, int bs, int y, int z) {
 
 void launch_sign_approx(const SignArgs& a, const Act& x, const ModC* mc, const AesGlobals& g, hipStream_t st) {
     if (a.t <= 5)
-        hipLaunchKernelGGL(k_sign_approx<5>, grid_aes(a.N, kAesBlock, a.crt.k, a.B), dim3(kAesBlock), kAesLds, st, a, x, mc, g.te0,
+        hipLaunchKernelGGL(k_sign_approx<5>, AES_LAUNCH(a.N, a.crt.k, a.B), kAesLds, st, a, x, mc, g.te0,
                            g.rk);
     else
-        hipLaunchKernelGGL(k_sign_approx<8>, grid_aes(a.N, kAesBlock, a.crt.k, a.B), dim3(kAesBlock), kAesLds, st, a, x, mc, g.te0,
+        hipLaunchKernelGGL(k_sign_approx<8>, AES_LAUNCH(a.N, a.crt.k, a.B), kAesLds, st, a, x, mc, g.te0,
                            g.rk);
 }
 void launch_sign_chain(const SignArgs& a, int maxn, const ModC* mc, const AesGlobals& g, hipStream_t st) {
     const dim3 gs = grid_for(a.N, 256, a.t, a.B);
-    const dim3 gr = grid_aes(a.N, kAesBlock, 1, a.B);
+    const dim3 gr = grid_aes(a.N, aes_bs(a.N, 1, a.B), 1, a.B), br(aes_bs(a.N, 1, a.B));
     // (measured: folding the castsum pass into the chain lanes is slower, 334 vs 356 inf/s on
     // MiniONN B=24: the chain is latency bound and the castsum's t-fold lane parallelism wins)
     if (maxn <= 24) {  // k = 7 DASH configs (cast outputs mod 8 m_d: <= 22 components)
         hipLaunchKernelGGL(k_sign_castsum<24>, gs, dim3(256), 0, st, a, mc);
         if (a.fused)
-            hipLaunchKernelGGL(k_sign_chain_fused<24>, gr, dim3(kAesBlock), kAesLds, st, a, mc, g.te0, g.rk);
+            hipLaunchKernelGGL(k_sign_chain_fused<24>, gr, br, kAesLds, st, a, mc, g.te0, g.rk);
         else
-            hipLaunchKernelGGL(k_sign_chain<24>, gr, dim3(kAesBlock), kAesLds, st, a, mc, g.te0, g.rk);
+            hipLaunchKernelGGL(k_sign_chain<24>, gr, br, kAesLds, st, a, mc, g.te0, g.rk);
     } else if (maxn <= 32) {
         hipLaunchKernelGGL(k_sign_castsum<32>, gs, dim3(256), 0, st, a, mc);
         if (a.fused)
-            hipLaunchKernelGGL(k_sign_chain_fused<32>, gr, dim3(kAesBlock), kAesLds, st, a, mc, g.te0, g.rk);
+            hipLaunchKernelGGL(k_sign_chain_fused<32>, gr, br, kAesLds, st, a, mc, g.te0, g.rk);
         else
-            hipLaunchKernelGGL(k_sign_chain<32>, gr, dim3(kAesBlock), kAesLds, st, a, mc, g.te0, g.rk);
+            hipLaunchKernelGGL(k_sign_chain<32>, gr, br, kAesLds, st, a, mc, g.te0, g.rk);
     } else {
         hipLaunchKernelGGL(k_sign_castsum<64>, gs, dim3(256), 0, st, a, mc);
         if (a.fused)
-            hipLaunchKernelGGL(k_sign_chain_fused<64>, gr, dim3(kAesBlock), kAesLds, st, a, mc, g.te0, g.rk);
+            hipLaunchKernelGGL(k_sign_chain_fused<64>, gr, br, kAesLds, st, a, mc, g.te0, g.rk);
         else
-            hipLaunchKernelGGL(k_sign_chain<64>, gr, dim3(kAesBlock), kAesLds, st, a, mc, g.te0, g.rk);
+            hipLaunchKernelGGL(k_sign_chain<64>, gr, br, kAesLds, st, a, mc, g.te0, g.rk);
     }
 }
 void launch_unpack(const u128* P, int nres, const Act& out, const CrtInfo& mods, const ModC* mc, int64_t N, int B,
@@ -1048,7 +1063,7 @@ void launch_relu_mult(const SignArgs& a, const Act& x, const Act& y, const u128*
 }
 void launch_rescale_hash(const Act& x, int fi, int s, const int16_t* up, int up_stride, int add_up, int64_t N, int B,
                          u128* h0, uint16_t* col0, const ModC* mc, const AesGlobals& g, hipStream_t st) {
-    hipLaunchKernelGGL(k_rescale_hash, grid_aes(N, kAesBlock, 1, B), dim3(kAesBlock), kAesLds, st, x, fi, s, up, up_stride,
+    hipLaunchKernelGGL(k_rescale_hash, AES_LAUNCH(N, 1, B), kAesLds, st, x, fi, s, up, up_stride,
                        add_up, N, h0, col0, mc, g.te0, g.rk);
 }
 void launch_rescale_update(const RescaleArgs& a, const Act& x, int B, const ModC* mc, hipStream_t st) {
@@ -1064,11 +1079,11 @@ void launch_base_ext(const BEArgs& a, const Act& x, int B, const ModC* mc, const
 }
 void launch_proj(const ProjArgs& a, const Act& x, const Act& y, int B, const ModC* mc, const AesGlobals& g,
                  hipStream_t st) {
-    hipLaunchKernelGGL(k_proj, grid_aes(a.N, kAesBlock, a.k, B), dim3(kAesBlock), kAesLds, st, a, x, y, mc, g.te0, g.rk);
+    hipLaunchKernelGGL(k_proj, AES_LAUNCH(a.N, a.k, B), kAesLds, st, a, x, y, mc, g.te0, g.rk);
 }
 void launch_mult(const MultArgs& a, const Act& x, const Act& y, int B, const ModC* mc, const AesGlobals& g,
                  hipStream_t st) {
-    hipLaunchKernelGGL(k_mult, grid_aes(a.No, kAesBlock, a.crt.k, B), dim3(kAesBlock), kAesLds, st, a, x, y, mc, g.te0, g.rk);
+    hipLaunchKernelGGL(k_mult, AES_LAUNCH(a.No, a.crt.k, B), kAesLds, st, a, x, y, mc, g.te0, g.rk);
 }
 
 }  // namespace dev
