@@ -315,8 +315,10 @@ struct __attribute__((packed, aligned(2))) Row8c {
     u32x4c v;
 };
 __device__ __forceinline__ uint32_t modq_conv(uint32_t x, uint32_t q, uint32_t mq) {
-    uint32_t d = __umulhi(x, mq);
-    uint32_t r = x - d * q;
+    // d = floor(x / q) or one less; the remainder (< 2q < 2^24) from the low 24 bits of x - d * q, so the
+    // product can be the full-rate 24-bit multiply
+    const uint32_t d = __umulhi(x, mq);
+    const uint32_t r = (x - __umul24(d, q)) & 0xffffffu;
     return r >= q ? r - q : r;
 }
 
@@ -360,12 +362,25 @@ __global__ __launch_bounds__(256) void k_conv_img2(ConvArgs a, Act x, Act y, int
         }
     }
     // stage the band: item = (4 channels, 8 columns, row), channel groups fastest across lanes (the
-    // channel-last dword stores of a lane group then cover consecutive banks); 4 x 16-B loads -> 8 dwords.
-    // Two items per round: both items' loads are issued before either is packed (half the round trips).
+    // channel-last dword stores of a lane group then cover consecutive banks); 4 x 8-B loads -> 8 dwords.
+    // Two items per round: both items' loads are issued before either is stored (half the round trips).
+    // Operands: for p < 128 the residues themselves (0..p-1 are valid int8, no conversion); otherwise
+    // centered into (-p/2, p/2], four bytes at a time (SWAR). The 4 x 4 byte transposes to channel-last
+    // dwords are v_perm_b32 pairs. Items that touch the padding or the image edge go byte by byte.
+    const bool rawx = p < 128;
+    const uint32_t padb = static_cast<uint32_t>(rawx ? zv : zc8) & 0xffu;
+    const uint32_t ck = static_cast<uint32_t>(127 - half) * 0x01010101u;       // b > half <=> bit 7 of b + ck
+    const uint32_t csub = static_cast<uint32_t>(256 - p) * 0x01010101u;         // b - p as a byte (b < p)
+    auto center4 = [&](uint32_t b) -> uint32_t {
+        const uint32_t hi = (b + ck) & 0x80808080u;
+        const uint32_t msk = (hi - (hi >> 7)) | hi;  // 0xff in the bytes above half
+        return ((b + csub) & msk) | (b & ~msk);
+    };
     const int c4n = a.Cpad / 4;
     const int WO = (Wp + 7) / 8;
     const int items = in_rows * WO * c4n;
-    auto load_item = [&](int it, int (&v)[4][8], int& yq, int& xo, int& c4) {
+    // raw[q][h]: channel c4*4+q, columns xo*8 + 4h .. +3 (byte t = column 4h + t), final operand bytes
+    auto load_item = [&](int it, uint32_t (&raw)[4][2], int& yq, int& xo, int& c4) {
         c4 = it % c4n;
         const int t2 = it / c4n;
         xo = t2 % WO;
@@ -379,41 +394,48 @@ __global__ __launch_bounds__(256) void k_conv_img2(ConvArgs a, Act x, Act y, int
             const int ci = c4 * 4 + q;
             const act_t* row = X + static_cast<int64_t>(ci) * HW + static_cast<int64_t>(iy) * a.W;
             if (ci >= a.C) {
-#pragma unroll
-                for (int u = 0; u < 8; ++u) v[q][u] = 0;
+                raw[q][0] = raw[q][1] = 0u;
             } else if (full) {
                 // one 8-B load of 8 byte components (unaligned: global loads take any address on gfx950)
                 typedef uint32_t u32x2c __attribute__((ext_vector_type(2)));
                 const u32x2c t = *reinterpret_cast<const u32x2c*>(row + ix0);
-#pragma unroll
-                for (int u = 0; u < 8; ++u) v[q][u] = static_cast<int>((t[u >> 2] >> (8 * (u & 3))) & 0xffu);
+                raw[q][0] = rawx ? t[0] : center4(t[0]);
+                raw[q][1] = rawx ? t[1] : center4(t[1]);
             } else {
+                raw[q][0] = raw[q][1] = 0u;
 #pragma unroll
                 for (int u = 0; u < 8; ++u) {
                     const int ix = ix0 + u;
-                    v[q][u] = (rowin && ix >= 0 && ix < a.W) ? row[ix] : -1;  // -1: padding (zero label)
+                    uint32_t v = padb;
+                    if (rowin && ix >= 0 && ix < a.W) {
+                        const int w = row[ix];
+                        v = static_cast<uint32_t>(rawx ? w : (w > half ? w - p : w)) & 0xffu;
+                    }
+                    raw[q][u >> 2] |= v << (8 * (u & 3));
                 }
             }
         }
     };
-    auto store_item = [&](const int (&v)[4][8], int yq, int xo, int c4) {
-        uint32_t packed[8] = {0u, 0u, 0u, 0u, 0u, 0u, 0u, 0u};
+    auto store_item = [&](const uint32_t (&raw)[4][2], int yq, int xo, int c4) {
 #pragma unroll
-        for (int q = 0; q < 4; ++q)
+        for (int h = 0; h < 2; ++h) {
+            // [A0 B0 A1 B1], [A2 B2 A3 B3], same for C D; then column t = [A_t B_t C_t D_t]
+            const uint32_t ab0 = __builtin_amdgcn_perm(raw[1][h], raw[0][h], 0x05010400u);
+            const uint32_t ab1 = __builtin_amdgcn_perm(raw[1][h], raw[0][h], 0x07030602u);
+            const uint32_t cd0 = __builtin_amdgcn_perm(raw[3][h], raw[2][h], 0x05010400u);
+            const uint32_t cd1 = __builtin_amdgcn_perm(raw[3][h], raw[2][h], 0x07030602u);
+            const uint32_t col[4] = {__builtin_amdgcn_perm(cd0, ab0, 0x05040100u), __builtin_amdgcn_perm(cd0, ab0, 0x07060302u),
+                                     __builtin_amdgcn_perm(cd1, ab1, 0x05040100u), __builtin_amdgcn_perm(cd1, ab1, 0x07060302u)};
 #pragma unroll
-            for (int u = 0; u < 8; ++u) {
-                int w = v[q][u];
-                w = w < 0 ? zc8 : (w > half ? w - p : w);
-                packed[u] |= (static_cast<uint32_t>(w) & 0xffu) << (8 * q);
+            for (int t = 0; t < 4; ++t) {
+                const int xx = xo * 8 + 4 * h + t;
+                if (xx < Wp) *reinterpret_cast<uint32_t*>(img + yq * R + xx * S + c4 * 4) = col[t];
             }
-#pragma unroll
-        for (int u = 0; u < 8; ++u) {
-            const int xx = xo * 8 + u;
-            if (xx < Wp) *reinterpret_cast<uint32_t*>(img + yq * R + xx * S + c4 * 4) = packed[u];
         }
     };
     for (int it = tid; it < items; it += 512) {
-        int va[4][8], vb[4][8], ya, xa, ca, yb = 0, xb = 0, cb = 0;
+        uint32_t va[4][2], vb[4][2];
+        int ya, xa, ca, yb = 0, xb = 0, cb = 0;
         load_item(it, va, ya, xa, ca);
         const bool two = it + 256 < items;
         if (two) load_item(it + 256, vb, yb, xb, cb);
@@ -438,8 +460,13 @@ __global__ __launch_bounds__(256) void k_conv_img2(ConvArgs a, Act x, Act y, int
             toff[s] = dy * R + dx * S + cc * 64;
         }
     }
-    // centered operands: |acc| <= Kpad * half^2; off is a multiple of p above that bound (acc + off >= 0, < 2^31)
-    const uint32_t off = static_cast<uint32_t>(p) * (static_cast<uint32_t>(a.Kpad * half * half) / static_cast<uint32_t>(p) + 1);
+    // |acc| <= Kpad * half * max|x| (weights centered; x centered, or raw residues < p for p < 128);
+    // off is a multiple of p above that bound (acc + off >= 0, < 2^31)
+    const uint32_t xmax = static_cast<uint32_t>(rawx ? p - 1 : half);
+    const uint32_t off =
+        static_cast<uint32_t>(p) * (static_cast<uint32_t>(a.Kpad * half) * xmax / static_cast<uint32_t>(p) + 1);
+    // col -> (output row in band, column): multiply-high by ceil(2^32 / OW) is exact for col < 2^23
+    const uint32_t owm = a.OW > 1 ? 0xffffffffu / static_cast<uint32_t>(a.OW) + 1u : 0u;
     // per-lane epilogue constants of its 4 filter rows, loaded once (a dependent global load per output
     // inside the column loop cost a round trip per 64-column chunk)
     uint32_t addc[4];
@@ -461,7 +488,8 @@ __global__ __launch_bounds__(256) void k_conv_img2(ConvArgs a, Act x, Act y, int
             ok[t] = col < ncol;
             // columns past the band read column 0's operands (valid LDS); their results are never stored
             const int cl = ok[t] ? col : 0;
-            const int oyl = cl / a.OW, ox = cl - oyl * a.OW;
+            const int oyl = a.OW > 1 ? static_cast<int>(__umulhi(static_cast<uint32_t>(cl), owm)) : cl;
+            const int ox = cl - oyl * a.OW;
             base[t] = (oyl * a.sh) * R + (ox * a.sw) * S + (lane >> 4) * 16;
         }
         if (AREG) {
@@ -489,8 +517,7 @@ __global__ __launch_bounds__(256) void k_conv_img2(ConvArgs a, Act x, Act y, int
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
             if (!ok[t]) continue;
-            const int col = col0 + t * 16 + (lane & 15);
-            const int pos = (oy0 + col / a.OW) * a.OW + col % a.OW;
+            const int pos = oy0 * a.OW + col0 + t * 16 + (lane & 15);  // band rows are whole output rows
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
                 const int f = fw + (lane >> 4) * 4 + r;
