@@ -52,9 +52,10 @@ def main() -> None:
     ap.add_argument("--rescale", default=os.environ.get("DASH_BENCH_RESCALE", "mrs"), choices=["mrs", "legacy"],
                     help="construction of the DASH rescale ceil(x/2^l): one exact mixed-radix conversion (mrs) or the "
                          "reference's l sign-gadget halvings (legacy); same function on the signed range")
-    ap.add_argument("--relu", default=os.environ.get("DASH_BENCH_RELU", "approx"), choices=["mrs", "approx"],
-                    help="sign of the ReLU: exact mixed-radix conversion (mrs) or the reference's approximate sign "
-                         "gadget at 100 %% accuracy (approx)")
+    ap.add_argument("--relu", default=os.environ.get("DASH_BENCH_RELU", "joint"), choices=["mrs", "approx", "joint"],
+                    help="sign of the ReLU: taken from the preceding mixed-radix rescale's conversion where a ReLU "
+                         "follows a rescale, else the approximate gadget (joint); exact mixed-radix conversion "
+                         "(mrs); or the reference's approximate sign gadget at 100 %% accuracy (approx)")
     ap.add_argument("--streams", type=int, default=int(os.environ.get("DASH_BENCH_STREAMS", "4")),
                     help="independent GC groups per GPU, each on its own HIP stream (overlap latency- and "
                          "bandwidth-bound phases)")

@@ -259,7 +259,7 @@ PYBIND11_MODULE(_dash_native, m) {
              }),
              py::arg("crt"), py::arg("mrs"), py::arg("seed"), py::arg("max_mod") = 0)
         .def("garble", [](Garbler& g, const py::list& layers, std::vector<i64> in_dims, int nthreads, int device,
-                          bool fused_sign, bool rescale_mrs, bool relu_mrs) {
+                          bool fused_sign, bool rescale_mrs, bool relu_mrs, bool relu_joint) {
             auto specs = specs_from_py(layers);
             GarbleOptions o;
             o.nthreads = nthreads;
@@ -267,6 +267,7 @@ PYBIND11_MODULE(_dash_native, m) {
             o.fused_sign = fused_sign;
             o.rescale_mrs = rescale_mrs;
             o.relu_mrs = relu_mrs;
+            o.relu_joint = relu_joint;
             GarbledModel gm;
             {
                 py::gil_scoped_release rel;
@@ -275,7 +276,7 @@ PYBIND11_MODULE(_dash_native, m) {
             return std::make_shared<GarbledModel>(std::move(gm));
         }, py::arg("layers"), py::arg("in_dims"), py::arg("nthreads") = 0, py::arg("device") = -1,
            py::arg("fused_sign") = true, py::arg("rescale_mrs") = false,
-           py::arg("relu_mrs") = false)
+           py::arg("relu_mrs") = false, py::arg("relu_joint") = false)
         .def("layer_ms", [](const Garbler& g) { return g.layer_ms(); })
         .def("encode", [](const Garbler& g, py::array_t<i64, py::array::c_style | py::array::forcecast> x) {
             std::vector<i64> v(x.data(), x.data() + x.size());

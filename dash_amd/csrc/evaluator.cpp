@@ -90,6 +90,7 @@ CrtLabels cpu_evaluate(const GarbledModel& m, const CrtLabels& inputs, int nt, s
     };
 
     if (layer_ms) layer_ms->assign(m.layers.size(), 0.0);
+    Labels sig_joint;  // sign labels a mixed-radix rescale with sign_out leaves for the next ReLU
     for (size_t li = 0; li < m.layers.size(); ++li) {
         const auto t_layer = std::chrono::steady_clock::now();
         const GLayer& g = m.layers[li];
@@ -184,6 +185,24 @@ CrtLabels cpu_evaluate(const GarbledModel& m, const CrtLabels& inputs, int nt, s
                 break;
             }
             case K_RELU: {
+                if (g.param("smode", 0) == 2) {  // sign from the preceding rescale (RescaleMrsPlan::sign_last)
+                    DASH_CHECK(sig_joint.N == Nin, "joint ReLU without a preceding sign-producing rescale");
+                    const Array& tg = g.arr("mm.g");
+                    const Array& te = g.arr("mm.e");
+                    CrtLabels nxt;
+                    for (int j = 0; j < k; ++j) nxt.emplace_back(crt[j], Nin);
+                    parallel_for(Nin, [&](i64 b0, i64 b1) {
+                        const ModInfo& m2 = mod_info(2);
+                        for (i64 e = b0; e < b1; ++e)
+                            for (int j = 0; j < k; ++j)
+                                mixed_mult_eval(cur[j].at(e), mod_info(crt[j]), sig_joint.at(e), m2,
+                                                tg.ptr<u128>() + e * tg.shape[1] + prefix[j],
+                                                te.ptr<u128>() + (e * k + j) * 3, nxt[j].at(e));
+                    }, nt);
+                    cur = std::move(nxt);
+                    sig_joint = Labels();
+                    break;
+                }
                 if (g.param("smode", 0) == 1) {  // exact mixed-radix sign (SignMrsPlan)
                     const SignMrsPlan sp(crt);
                     const Array& tab = g.arr("mrs");
@@ -251,14 +270,17 @@ CrtLabels cpu_evaluate(const GarbledModel& m, const CrtLabels& inputs, int nt, s
             case K_RESCALE: {
                 const i64 mode = g.param("mode", 0);
                 if (mode == 2) {  // mixed-radix construction of the legacy function
-                    const RescaleMrsPlan P(crt, static_cast<int>(g.param("l")));
+                    const bool so = g.param("sign_out", 0) == 1;
+                    const RescaleMrsPlan P(crt, static_cast<int>(g.param("l")), so);
                     const Array& tab = g.arr("mrs");
                     DASH_CHECK(tab.shape[1] == P.n_tab, "mixed-radix rescale table shape");
+                    if (so) sig_joint = Labels(2, Nin);
                     parallel_for(Nin, [&](i64 b0, i64 b1) {
                         std::vector<comp_t*> Lp(k);
                         for (i64 e = b0; e < b1; ++e) {
                             for (int j = 0; j < k; ++j) Lp[j] = cur[j].at(e);
-                            rescale_mrs_eval_elem(P, Lp.data(), tab.ptr<u128>() + e * P.n_tab);
+                            rescale_mrs_eval_elem(P, Lp.data(), tab.ptr<u128>() + e * P.n_tab,
+                                                  so ? sig_joint.at(e) : nullptr);
                         }
                     }, nt);
                     break;

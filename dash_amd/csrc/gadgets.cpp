@@ -564,7 +564,8 @@ void rescale_eval_elem(const RescalePlan& P, const LabelBank& Z, comp_t* const* 
 
 // ---------------------------------------------------------------------------
 // Single-shot mixed-radix rescale (gadgets.h RescaleMrsPlan)
-RescaleMrsPlan::RescaleMrsPlan(const std::vector<int>& crt_, int l_) : crt(crt_), l(l_) {
+RescaleMrsPlan::RescaleMrsPlan(const std::vector<int>& crt_, int l_, bool sign_last_)
+    : crt(crt_), l(l_), sign_last(sign_last_) {
     const int kk = k();
     DASH_CHECK(kk >= 2 && crt[0] == 2, "mixed-radix rescale needs CRT residue 0 = 2");
     DASH_CHECK(l >= 1 && l <= 14, "mixed-radix rescale: 1 <= l <= 14");
@@ -576,27 +577,37 @@ RescaleMrsPlan::RescaleMrsPlan(const std::vector<int>& crt_, int l_) : crt(crt_)
     const i64 h = M / 2;
     U = h + pmod(S - 1 - h % S, S);
     q = (U - (S - 1)) / S;
+    ord.clear();
+    if (sign_last) {
+        for (int j = 1; j < kk; ++j) ord.push_back(j);
+        ord.push_back(0);
+    } else {
+        for (int j = 0; j < kk; ++j) ord.push_back(j);
+    }
     B.assign(kk, 1);
     Binv.assign(kk, 1);
     Sinv.assign(kk, 0);
-    for (int i = 1; i < kk; ++i) B[i] = B[i - 1] * crt[i - 1];
-    for (int i = 0; i < kk; ++i) Binv[i] = mul_inv(static_cast<u128>(B[i] % crt[i]), crt[i]);
+    for (int i = 1; i < kk; ++i) B[i] = B[i - 1] * crt[ord[i - 1]];
+    for (int i = 0; i < kk; ++i) Binv[i] = mul_inv(static_cast<u128>(B[i] % crt[ord[i]]), crt[ord[i]]);
     for (int j = 1; j < kk; ++j) Sinv[j] = mul_inv(static_cast<u128>(S % crt[j]), crt[j]);
     dig_off.assign(kk, 0);
     i64 off = 0;
     for (int i = 0; i < kk; ++i) {
         dig_off[i] = off;
-        off += static_cast<i64>(crt[i]) * targets(i);
+        off += static_cast<i64>(crt[ord[i]]) * targets(i);
     }
     fin_off = off;
     n_tab = off + T * kk;
 }
 
 i64 RescaleMrsPlan::digit_fn(int i, int t, i64 v) const {
-    const i64 pi = crt[i];
-    const i64 a = pmod((v + U % pi) * Binv[i], pi);  // digit a_i of x_u
+    const i64 pi = crt[ord[i]];
+    // digit a_i of x_u; with sign_last the mod-2 key already carries a_{k-1} (U folded in below)
+    const i64 a = sign_last && i == k() - 1 ? pmod(v, pi) : pmod((v + U % pi) * Binv[i], pi);
     const i64 m = target_mod(i, t);
-    return pmod(a * (B[i] % m), m);
+    i64 val = a * (B[i] % m);
+    if (sign_last && i == 0 && t < k() - 1 && target_res(i, t) == 0) val -= U % m;
+    return pmod(val, m);
 }
 
 i64 RescaleMrsPlan::final_fn(int j, i64 v) const {
@@ -606,7 +617,7 @@ i64 RescaleMrsPlan::final_fn(int j, i64 v) const {
 }
 
 void rescale_mrs_garble_elem(const RescaleMrsPlan& P, const LabelBank& R, const Prg& prg, u64 stream,
-                             comp_t* const* L, u128* tab) {
+                             comp_t* const* L, u128* tab, comp_t* sig) {
     const int k = P.k();
     constexpr int W = 128;
     // draws, PRG counter order: digit i's target labels (t = 0..k-1-i), then the k final output labels
@@ -628,7 +639,7 @@ void rescale_mrs_garble_elem(const RescaleMrsPlan& P, const LabelBank& R, const 
     comp_t* acc = buf + static_cast<size_t>(W) * (nd + 2 * k);
     const ModInfo& mT = mod_info(static_cast<int>(P.T));
     std::fill(acc, acc + mT.n, comp_t(0));
-    // key base labels: K_i = L_i - sum_{l<i} P_{l,i}; r = sum_i P_{i,T}
+    // key base labels: K_i = L_i - sum_{l<i} P_{l,i} (by residue); r = sum_i P_{i,T}
     for (int j = 0; j < k; ++j) {
         key[j] = buf + static_cast<size_t>(W) * (nd + k + j);
         std::memcpy(key[j], L[j], sizeof(comp_t) * nr_comps(P.crt[j]));
@@ -636,14 +647,19 @@ void rescale_mrs_garble_elem(const RescaleMrsPlan& P, const LabelBank& R, const 
     s = 0;
     for (int i = 0; i < k; ++i)
         for (int t = 0; t < P.targets(i); ++t, ++s) {
-            if (t == k - 1 - i) lab_add(acc, dig[s], mT.n, mT.p);
-            else lab_sub(key[i + 1 + t], dig[s], nr_comps(P.crt[i + 1 + t]), P.crt[i + 1 + t]);
+            if (t == k - 1 - i) {
+                lab_add(acc, dig[s], mT.n, mT.p);
+            } else {
+                const int r = P.target_res(i, t);
+                lab_sub(key[r], dig[s], nr_comps(P.crt[r]), P.crt[r]);
+            }
         }
+    if (P.sign_last && sig) std::memcpy(sig, key[0], sizeof(comp_t) * nr_comps(2));
     ProjKeys& K = proj_keys_scratch();
     s = 0;
     for (int i = 0; i < k; ++i) {
-        const ModInfo& mi = mod_info(P.crt[i]);
-        proj_keys(key[i], R.get(mi.p), mi, K);
+        const ModInfo& mi = mod_info(P.crt[P.ord[i]]);
+        proj_keys(key[P.ord[i]], R.get(mi.p), mi, K);
         const int nt = P.targets(i);
         for (int t = 0; t < nt; ++t, ++s) {
             const ModInfo& mo = mod_info(P.target_mod(i, t));
@@ -665,7 +681,7 @@ void rescale_mrs_garble_elem(const RescaleMrsPlan& P, const LabelBank& R, const 
     }
 }
 
-void rescale_mrs_eval_elem(const RescaleMrsPlan& P, comp_t* const* L, const u128* tab) {
+void rescale_mrs_eval_elem(const RescaleMrsPlan& P, comp_t* const* L, const u128* tab, comp_t* sig) {
     const int k = P.k();
     constexpr int W = 128;
     comp_t* buf = rescale_scratch().get(static_cast<size_t>(W) * (k + 2));
@@ -679,17 +695,19 @@ void rescale_mrs_eval_elem(const RescaleMrsPlan& P, comp_t* const* L, const u128
     comp_t* pr = buf + static_cast<size_t>(W) * (k + 1);
     std::fill(acc, acc + mT.n, comp_t(0));
     for (int i = 0; i < k; ++i) {
-        const ModInfo& mi = mod_info(P.crt[i]);
-        const u128 h = hash(compress(key[i], mi));
+        const int r0 = P.ord[i];
+        const ModInfo& mi = mod_info(P.crt[r0]);
+        const u128 h = hash(compress(key[r0], mi));
         const int nt = P.targets(i);
-        const u128* row = tab + P.dig_off[i] + static_cast<i64>(color_of(key[i], mi.p)) * nt;
+        const u128* row = tab + P.dig_off[i] + static_cast<i64>(color_of(key[r0], mi.p)) * nt;
         for (int t = 0; t < nt; ++t) {
             const ModInfo& mo = mod_info(P.target_mod(i, t));
             decompress(row[t] - h, pr, mo);
             if (t == nt - 1) lab_add(acc, pr, mo.n, mo.p);
-            else lab_sub(key[i + 1 + t], pr, mo.n, mo.p);
+            else lab_sub(key[P.target_res(i, t)], pr, mo.n, mo.p);
         }
     }
+    if (P.sign_last && sig) std::memcpy(sig, key[0], sizeof(comp_t) * nr_comps(2));
     const u128 h = hash(compress(acc, mT));
     const u128* row = tab + P.fin_off + static_cast<i64>(color_of(acc, mT.p)) * k;
     decompress(row[0] - h, L[0], mod_info(2));

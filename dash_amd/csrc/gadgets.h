@@ -260,32 +260,47 @@ void rescale_eval_elem(const RescalePlan& P, const LabelBank& Z, comp_t* const* 
 // evaluator instead of l sign gadgets (l = 5, k = 7: 8 instead of ~60), and
 // sum_i p_i (k - i) + T k table entries instead of l (2 (k - 1) + sign).
 // Table (one row per element): digit i at dig_off[i], [color][k - i] entries
-// (targets: residues i+1..k-1, then T); final rows at fin_off, [color][k]
-// (targets: residues 0..k-1).
+// (targets: the residues of positions i+1..k-1, then T); final rows at
+// fin_off, [color][k] (targets: residues 0..k-1).
+//
+// sign_last (the joint rescale + ReLU sign): positions convert residues
+// 1..k-1 and residue 0 (mod 2) LAST, as SignMrsPlan. Its digit a_{k-1} has
+// weight B_{k-1} = M/2, so a_{k-1} = [x_u >= M/2] = [x >= M/2 - U] with
+// M/2 - U in (-S, 0]; with U mod 2 folded into digit 0's payload for residue
+// 0, residue 0's key after the k-1 subtractions IS the label of a_{k-1}. For
+// the ReLU that follows, relu(y) = y * a_{k-1} with y = ceil(x / S): y >= 1
+// means x >= 1 (sign 1), y <= -1 means x <= -S (sign 0), and y = 0 gives 0
+// either way, so the rescale's conversion replaces the ReLU's sign gadget.
+// The last position's row has one target (T) and takes a_{k-1} as is.
 struct RescaleMrsPlan {
     std::vector<int> crt;
     int l = 0;
+    bool sign_last = false;
     i64 S = 1, T = 2, M = 1, U = 0, q = 0;
-    std::vector<i64> B;       // B[i] = prod_{m<i} crt[m]
-    std::vector<i64> Binv;    // B[i]^-1 mod crt[i]
+    std::vector<int> ord;     // position -> residue (identity, or 1..k-1, 0 with sign_last)
+    std::vector<i64> B;       // B[i] = prod_{m<i} crt[ord[m]]
+    std::vector<i64> Binv;    // B[i]^-1 mod crt[ord[i]]
     std::vector<i64> Sinv;    // S^-1 mod crt[j] (j >= 1)
     std::vector<i64> dig_off; // table offset of digit i's rows
     i64 fin_off = 0, n_tab = 0;
     RescaleMrsPlan() = default;
-    RescaleMrsPlan(const std::vector<int>& crt, int l);
+    RescaleMrsPlan(const std::vector<int>& crt, int l, bool sign_last = false);
     int k() const { return static_cast<int>(crt.size()); }
     int targets(int i) const { return k() - i; }
-    // modulus of target t of digit i (residue i + 1 + t, the last one T)
-    int target_mod(int i, int t) const { return t == k() - 1 - i ? static_cast<int>(T) : crt[i + 1 + t]; }
+    // residue of target t < k-1-i of digit i (position i + 1 + t)
+    int target_res(int i, int t) const { return ord[i + 1 + t]; }
+    // modulus of target t of digit i (residue of position i + 1 + t, the last one T)
+    int target_mod(int i, int t) const { return t == k() - 1 - i ? static_cast<int>(T) : crt[ord[i + 1 + t]]; }
     // payload value of digit i, target t, for key value v (a_i B_i reduced mod the target modulus)
     i64 digit_fn(int i, int t, i64 v) const;
     // payload value of final target j for key value v = x_u mod T
     i64 final_fn(int j, i64 v) const;
 };
-// L[j] (one element's labels mod crt[j]) are replaced by the rescaled labels.
+// L[j] (one element's labels mod crt[j]) are replaced by the rescaled labels;
+// with sign_last, sig (nullable) receives the mod-2 label of a_{k-1}.
 void rescale_mrs_garble_elem(const RescaleMrsPlan& P, const LabelBank& R, const Prg& prg, u64 stream,
-                             comp_t* const* L, u128* tab);
-void rescale_mrs_eval_elem(const RescaleMrsPlan& P, comp_t* const* L, const u128* tab);
+                             comp_t* const* L, u128* tab, comp_t* sig = nullptr);
+void rescale_mrs_eval_elem(const RescaleMrsPlan& P, comp_t* const* L, const u128* tab, comp_t* sig = nullptr);
 
 // ---------------------------------------------------------------------------
 // Exact sign by mixed-radix conversion (a construction of the ReLU/Sign

@@ -444,10 +444,15 @@ GarbledModel Garbler::garble(const std::vector<LayerSpec>& layers, const std::ve
     }
 
     layer_ms_.assign(layers.size(), 0.0);
+    // joint rescale + ReLU sign: the rescale leaves the sign base labels here (host) or in the GPU garbler
+    bool sig_next = false;
+    Labels sig_host;
     for (size_t li = 0; li < layers.size(); ++li) {
         const auto t_layer = std::chrono::steady_clock::now();
         const LayerSpec& spec = layers[li];
         const u64 L = li + 1;
+        const bool sig_in = sig_next;  // the previous layer (a mixed-radix rescale) produced this ReLU's sign
+        sig_next = false;
         {
             auto it = spec.p.find("in_src");
             if (it != spec.p.end() && !it->second.empty()) {
@@ -475,6 +480,8 @@ GarbledModel Garbler::garble(const std::vector<LayerSpec>& layers, const std::ve
         // legacy rescale as one mixed-radix gadget (RescaleMrsPlan)
         const bool mrs_rescale = opt.rescale_mrs && spec.kind == K_RESCALE && param1(spec.p, "mode", 0) == 0;
         const bool relu_mrs = opt.relu_mrs && spec.kind == K_RELU;
+        const bool joint_out = mrs_rescale && opt.relu_joint && li + 1 < layers.size() &&
+                               layers[li + 1].kind == K_RELU && param1(layers[li + 1].p, "in_src", -2) == -2;
         const bool on_gpu = gpu && (spec.kind == K_CONV || spec.kind == K_RELU || spec.kind == K_SIGN ||
                                     (spec.kind == K_RESCALE && param1(spec.p, "mode", 0) == 0 && crt_[0] == 2));
         const bool passthru = spec.kind == K_FLATTEN;
@@ -601,6 +608,32 @@ GarbledModel Garbler::garble(const std::vector<LayerSpec>& layers, const std::ve
             }
             case K_RELU: {
                 DASH_CHECK(is_crt(), "relu needs CRT-base labels");
+                if (sig_in) {
+                    // sign from the preceding rescale (RescaleMrsPlan::sign_last): mixed-modulus half gates only
+                    Array tg(DType::u128, {Nin, sum_crt}), te(DType::u128, {Nin, static_cast<i64>(k), 3});
+                    if (on_gpu) {
+                        gpu->relu_mult(L, cur, &prefix, tg, te);
+                    } else {
+                        DASH_CHECK(sig_host.N == Nin, "joint ReLU: sign labels missing");
+                        CrtLabels nxt;
+                        for (int j = 0; j < k; ++j) nxt.emplace_back(crt_[j], Nin);
+                        parallel_for(Nin, [&](i64 b0, i64 b1) {
+                            const ModInfo& m2 = mod_info(2);
+                            for (i64 e = b0; e < b1; ++e) {
+                                u64 ctr = 0;
+                                for (int j = 0; j < k; ++j)
+                                    mixed_mult_garble(cur[j].at(e), mod_info(crt_[j]), sig_host.at(e), m2, R_, prg_,
+                                                      stream_id(L, 2, e), ctr, tg.ptr<u128>() + e * sum_crt + prefix[j],
+                                                      te.ptr<u128>() + (e * k + j) * 3, nxt[j].at(e));
+                            }
+                        }, nt);
+                        cur = std::move(nxt);
+                    }
+                    g.a["mm.g"] = tg;
+                    g.a["mm.e"] = te;
+                    g.p["smode"] = {2};
+                    break;
+                }
                 if (relu_mrs) {
                     const SignMrsPlan sp(crt_);
                     Array tab(DType::u128, {Nin, std::max<i64>(sp.n_tab, 1)});
@@ -695,19 +728,25 @@ GarbledModel Garbler::garble(const std::vector<LayerSpec>& layers, const std::ve
                 DASH_CHECK(is_crt(), "rescale needs CRT-base labels");
                 const i64 mode = param1(spec.p, "mode", 0);
                 if (mrs_rescale) {
-                    const RescaleMrsPlan P(crt_, static_cast<int>(param1(spec.p, "l")));
+                    const RescaleMrsPlan P(crt_, static_cast<int>(param1(spec.p, "l")), joint_out);
                     Array tab(DType::u128, {Nin, P.n_tab});
+                    if (joint_out && !on_gpu) sig_host = Labels(2, Nin);
                     if (on_gpu) gpu->rescale_mrs(L, P, cur, tab);
                     else parallel_for(Nin, [&](i64 b0, i64 b1) {
                         std::vector<comp_t*> Lp(k);
                         for (i64 e = b0; e < b1; ++e) {
                             for (int j = 0; j < k; ++j) Lp[j] = cur[j].at(e);
                             rescale_mrs_garble_elem(P, R_, prg_, stream_id(L, 30, e), Lp.data(),
-                                                    tab.ptr<u128>() + e * P.n_tab);
+                                                    tab.ptr<u128>() + e * P.n_tab,
+                                                    joint_out ? sig_host.at(e) : nullptr);
                         }
                     }, nt);
                     g.a["mrs"] = tab;
                     g.p["mode"] = {2};
+                    if (joint_out) {
+                        g.p["sign_out"] = {1};
+                        sig_next = true;
+                    }
                     g.p["iters"] = {1};
                     g.p["sprod"] = {P.S};
                     break;

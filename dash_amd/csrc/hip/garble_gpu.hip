@@ -504,7 +504,9 @@ __global__ __launch_bounds__(kPB) void k_project(Ctx c, Gadget g, In in, Tables 
 struct MrsG {
     int k, T;
     int crt[kMaxRes], sinv[kMaxRes];
-    int dig0[kMaxRes];  // slot of digit i's first target label (targets: residues i+1..k-1, then T)
+    int nsub[kMaxRes];
+    int sub[kMaxRes][kMaxRes];  // digit-target slots subtracted from residue j's key
+    int tslot[kMaxRes];         // slot of digit i's T target
     int key0, acc, fin0;
     int16_t* L[kMaxRes];  // label-major [N][n_j], updated in place
 };
@@ -550,10 +552,10 @@ __global__ __launch_bounds__(256) void k_mrs_derive(Ctx c, Gadget g, MrsG a) {
             // key: L_j - sum of the digit payload labels aimed at residue j
             uint32_t kv[8];
 #pragma unroll
-            for (int u = 0; u < 8; ++u) kv[u] = x[u] + static_cast<uint32_t>(p) * static_cast<uint32_t>(j);
-            for (int l = 0; l < j; ++l) {
+            for (int u = 0; u < 8; ++u) kv[u] = x[u] + static_cast<uint32_t>(p) * static_cast<uint32_t>(a.nsub[j]);
+            for (int l = 0; l < a.nsub[j]; ++l) {
                 uint32_t sv[8];
-                unpack8(ld8a(S + (a.dig0[l] + (j - l - 1)) * kW + q0), sv);
+                unpack8(ld8a(S + a.sub[j][l] * kW + q0), sv);
 #pragma unroll
                 for (int u = 0; u < 8; ++u) kv[u] -= sv[u];
             }
@@ -581,7 +583,7 @@ __global__ __launch_bounds__(256) void k_mrs_derive(Ctx c, Gadget g, MrsG a) {
             uint32_t av[8] = {0, 0, 0, 0, 0, 0, 0, 0};
             for (int l = 0; l < k; ++l) {
                 uint32_t sv[8];
-                unpack8(ld8a(S + (a.dig0[l] + (k - 1 - l)) * kW + q0), sv);
+                unpack8(ld8a(S + a.tslot[l] * kW + q0), sv);
 #pragma unroll
                 for (int u = 0; u < 8; ++u) av[u] += sv[u];
             }
@@ -1314,6 +1316,9 @@ struct GpuGarbler::Impl {
     std::vector<int> crt;
     int k = 0;
     int device = 0;
+    // sign base labels a sign_last mixed-radix rescale leaves for the next ReLU ([N][kW], relu_mult)
+    DevBlock sig;
+    int64_t sig_N = 0;
     // per-GC small uploads (up/down shift labels): pinned staging + device ring, copied asynchronously on the
     // garbling stream (no queue drain); one garble() uses far less than the ring, which restarts per GpuGarbler
     static constexpr size_t kRing = 8u << 20;
@@ -1783,6 +1788,65 @@ void GpuGarbler::rescale_legacy_iter(uint64_t layer, int it, const RescalePlan& 
     set_stale(cur, I.cur_mod, N);
 }
 
+// ReLU mixed-modulus half gates out_j = x_j * sig (relu_garble_elem's mixed_mult_garble order): draws of the
+// sk03/sk04 labels (slots sk0 + 2j, + 1) on PRG stream 2 of g.layer, the g (F_MULR) and e (F_NEGR) projections
+// into tables 4 / 5, the mini payloads and output base labels. g.S holds the sign label at sig_slot.
+static std::vector<DevBlock> relu_mult_gates(GpuGarbler::Impl& I, const gg::Gadget& g, const gg::In& in,
+                                             gg::Tables& tb, int sig_slot, int sk0, const std::vector<i64>& prefix) {
+    const int64_t N = g.N;
+    const int k = I.k;
+    std::vector<DevBlock> out = I.alloc_labels(I.crt, N);
+    std::vector<gg::Draw> dm;
+    std::vector<gg::Proj> pm;
+    int c2 = 0;
+    int64_t f2 = 0;
+    for (int j = 0; j < k; ++j) {
+        const int p = I.crt[j], n = nr_comps(p);
+        dm.push_back({sk0 + 2 * j, p, c2});
+        c2 += (n + 1) / 2;
+        dm.push_back({sk0 + 2 * j + 1, p, c2});
+        c2 += (n + 1) / 2;
+    }
+    for (int j = 0; j < k; ++j) {
+        const int p = I.crt[j];
+        gg::Proj q{gg::S_INPUT, j, p, sk0 + 2 * j, p, gg::F_MULR, j, 0, 0, gg::R_BANK, 0, 4, 1, prefix[j], f2};
+        f2 += p;
+        pm.push_back(q);
+    }
+    for (int j = 0; j < k; ++j) {
+        const int p = I.crt[j];
+        gg::Proj q{gg::S_SLOT, sig_slot, 2, sk0 + 2 * j + 1, p, gg::F_NEGR, j, 0, 0, gg::R_INPUT, j, 5, 1,
+                   static_cast<int64_t>(j) * 3, f2};
+        f2 += 2;
+        pm.push_back(q);
+    }
+    gg::Gadget gm = g;
+    gm.sslot = 2;
+    gm.PB = I.pbank(2, N);
+    gm.draws = gg::dconst(dm.data(), dm.size());
+    gm.ndraws = static_cast<int>(dm.size());
+    gm.projs = gg::dconst(pm.data(), pm.size());
+    gm.nprojs = static_cast<int>(pm.size());
+    gm.entries = f2;
+    gm.nblk = draw_blocks(dm);
+    check_desc(gm);
+    hipLaunchKernelGGL(gg::k_draw, dim3(blocks_for(N * gm.nblk, gg::kGB, 8192)), dim3(gg::kGB), 0, nullptr, I.c, gm);
+    hipLaunchKernelGGL(gg::k_project, dim3(blocks_for((N + 63) / 64 * 64 * gm.entries, gg::kPB, 16384)),
+                       dim3(gg::kPB), 0, nullptr, I.c, gm, in, tb);
+    gg::MiniArgs ma{};
+    ma.k = k;
+    for (int j = 0; j < k; ++j) ma.crt[j] = I.crt[j];
+    ma.sig_slot = sig_slot;
+    ma.sk_slot0 = sk0;
+    for (int j = 0; j < k; ++j) ma.out[j] = out[j].as<int16_t>();
+    hipLaunchKernelGGL(gg::k_bin_keys, dim3(blocks_for(N, gg::kGB, 8192)), dim3(gg::kGB), 0, nullptr, I.c,
+                       g.S + static_cast<int64_t>(sig_slot) * gg::kW, static_cast<int64_t>(g.nslots) * gg::kW,
+                       static_cast<const int16_t*>(nullptr), gm.PB, N);
+    hipLaunchKernelGGL(gg::k_relu_finish, dim3(blocks_for(N * k, 256, 8192)), dim3(256), 0, nullptr, I.c, gm, in,
+                       tb, ma, static_cast<const u128*>(gm.PB));
+    return out;
+}
+
 // ReLU with the mixed-radix sign: draw the digit-target labels (sign_mrs_garble_elem order) -> keys ->
 // fan-out projections; residue 0's key slot is the sign label; then the mixed-modulus half gates exactly as
 // in sign_layer's ReLU branch.
@@ -1870,56 +1934,7 @@ void GpuGarbler::relu_mrs(uint64_t layer, const SignMrsPlan& P, CrtLabels& cur, 
     hipLaunchKernelGGL(gg::k_project, dim3(blocks_for((N + 63) / 64 * 64 * g.entries, gg::kPB, 16384)), dim3(gg::kPB), 0,
                        nullptr, I.c, g, in, tb);
     // mixed-modulus half gates (as sign_layer's ReLU branch, sign label = residue 0's key slot)
-    std::vector<DevBlock> out = I.alloc_labels(I.crt, N);
-    {
-        std::vector<gg::Draw> dm;
-        std::vector<gg::Proj> pm;
-        int c2 = 0;
-        int64_t f2 = 0;
-        for (int j = 0; j < k; ++j) {
-            const int p = I.crt[j], n = nr_comps(p);
-            dm.push_back({sk0 + 2 * j, p, c2});
-            c2 += (n + 1) / 2;
-            dm.push_back({sk0 + 2 * j + 1, p, c2});
-            c2 += (n + 1) / 2;
-        }
-        for (int j = 0; j < k; ++j) {
-            const int p = I.crt[j];
-            gg::Proj q{gg::S_INPUT, j, p, sk0 + 2 * j, p, gg::F_MULR, j, 0, 0, gg::R_BANK, 0, 4, 1, (*prefix)[j], f2};
-            f2 += p;
-            pm.push_back(q);
-        }
-        for (int j = 0; j < k; ++j) {
-            const int p = I.crt[j];
-            gg::Proj q{gg::S_SLOT, sig_slot, 2, sk0 + 2 * j + 1, p, gg::F_NEGR, j, 0, 0, gg::R_INPUT, j, 5, 1,
-                       static_cast<int64_t>(j) * 3, f2};
-            f2 += 2;
-            pm.push_back(q);
-        }
-        gg::Gadget gm = g;
-        gm.sslot = 2;
-        gm.draws = gg::dconst(dm.data(), dm.size());
-        gm.ndraws = static_cast<int>(dm.size());
-        gm.projs = gg::dconst(pm.data(), pm.size());
-        gm.nprojs = static_cast<int>(pm.size());
-        gm.entries = f2;
-        gm.nblk = draw_blocks(dm);
-        check_desc(gm);
-        hipLaunchKernelGGL(gg::k_draw, dim3(blocks_for(N * gm.nblk, gg::kGB, 8192)), dim3(gg::kGB), 0, nullptr, I.c, gm);
-        hipLaunchKernelGGL(gg::k_project, dim3(blocks_for((N + 63) / 64 * 64 * gm.entries, gg::kPB, 16384)),
-                           dim3(gg::kPB), 0, nullptr, I.c, gm, in, tb);
-        gg::MiniArgs ma{};
-        ma.k = k;
-        for (int j = 0; j < k; ++j) ma.crt[j] = I.crt[j];
-        ma.sig_slot = sig_slot;
-        ma.sk_slot0 = sk0;
-        for (int j = 0; j < k; ++j) ma.out[j] = out[j].as<int16_t>();
-        hipLaunchKernelGGL(gg::k_bin_keys, dim3(blocks_for(N, gg::kGB, 8192)), dim3(gg::kGB), 0, nullptr, I.c,
-                           g.S + static_cast<int64_t>(sig_slot) * gg::kW, static_cast<int64_t>(nslots) * gg::kW,
-                           static_cast<const int16_t*>(nullptr), g.PB, N);
-        hipLaunchKernelGGL(gg::k_relu_finish, dim3(blocks_for(N * k, 256, 8192)), dim3(256), 0, nullptr, I.c, gm, in,
-                           tb, ma, static_cast<const u128*>(g.PB));
-    }
+    std::vector<DevBlock> out = relu_mult_gates(I, g, in, tb, sig_slot, sk0, *prefix);
     HIPCHECK(hipGetLastError());
     gg::end_layer(tmp);
     tr_.mark("kernels");
@@ -1949,10 +1964,17 @@ void GpuGarbler::rescale_mrs(uint64_t layer, const RescaleMrsPlan& P, CrtLabels&
     a.k = k;
     a.T = static_cast<int>(P.T);
     int slot = 0, ctr = 0;
+    std::vector<int> dig0(k, 0);
     for (int i = 0; i < k; ++i) {
-        a.dig0[i] = slot;
+        dig0[i] = slot;
         for (int t = 0; t < P.targets(i); ++t) {
             const int q = P.target_mod(i, t);
+            if (t == k - 1 - i) {
+                a.tslot[i] = slot;
+            } else {
+                const int r = P.target_res(i, t);
+                a.sub[r][a.nsub[r]++] = slot;
+            }
             dr.push_back({slot++, q, ctr});
             ctr += (nr_comps(q) + 1) / 2;
         }
@@ -1968,16 +1990,16 @@ void GpuGarbler::rescale_mrs(uint64_t layer, const RescaleMrsPlan& P, CrtLabels&
     const int nslots = slot;
     int64_t first = 0;
     for (int i = 0; i < k; ++i) {
-        const int nt = P.targets(i);
+        const int nt = P.targets(i), r0 = P.ord[i];
         const int a0 = static_cast<int>(flut.size()), a1 = static_cast<int>(fan.size());
-        for (int v = 0; v < P.crt[i]; ++v)
+        for (int v = 0; v < P.crt[r0]; ++v)
             for (int t = 0; t < nt; ++t) flut.push_back(static_cast<int16_t>(P.digit_fn(i, t, v)));
         for (int t = 0; t < nt; ++t) fan.push_back(P.target_mod(i, t));
         gg::Proj p{};
-        p.in_kind = gg::S_SLOT; p.in_idx = a.key0 + i; p.pin = P.crt[i];
-        p.out_slot = a.dig0[i]; p.pout = P.target_mod(i, 0); p.fn = gg::F_FAN; p.a0 = a0; p.a1 = a1;
+        p.in_kind = gg::S_SLOT; p.in_idx = a.key0 + r0; p.pin = P.crt[r0];
+        p.out_slot = dig0[i]; p.pout = P.target_mod(i, 0); p.fn = gg::F_FAN; p.a0 = a0; p.a1 = a1;
         p.outr_kind = gg::R_BANK; p.table = 0; p.stride = nt; p.off = P.dig_off[i]; p.first = first;
-        first += P.crt[i];
+        first += P.crt[r0];
         pr.push_back(p);
     }
     {
@@ -2025,11 +2047,64 @@ void GpuGarbler::rescale_mrs(uint64_t layer, const RescaleMrsPlan& P, CrtLabels&
     hipLaunchKernelGGL(gg::k_mrs_derive, dim3(blocks_for(N, 256)), dim3(256), 0, nullptr, I.c, g, a);
     hipLaunchKernelGGL(gg::k_project, dim3(blocks_for((N + 63) / 64 * 64 * g.entries, gg::kPB, 16384)), dim3(gg::kPB), 0,
                        nullptr, I.c, g, in, tb);
+    if (P.sign_last) {
+        // residue 0's key slot is the sign label of the ReLU that follows (relu_mult)
+        I.sig.alloc(I.device, static_cast<size_t>(N) * gg::kW * sizeof(int16_t));
+        I.sig_N = N;
+        HIPCHECK(hipMemcpy2DAsync(I.sig.p, gg::kW * sizeof(int16_t), g.S + static_cast<int64_t>(a.key0) * gg::kW,
+                                  static_cast<size_t>(nslots) * gg::kW * sizeof(int16_t), gg::kW * sizeof(int16_t),
+                                  static_cast<size_t>(N), hipMemcpyDeviceToDevice, nullptr));
+    }
     HIPCHECK(hipGetLastError());
     gg::end_layer(tmp);
     tr_.mark("kernels");
     tT.to_array(tab, I.device);
     set_stale(cur, I.cur_mod, N);
+}
+
+// ReLU whose sign came out of the preceding mixed-radix rescale (RescaleMrsPlan::sign_last, I.sig): the
+// mixed-modulus half gates only; device cur -> next base labels.
+void GpuGarbler::relu_mult(uint64_t layer, CrtLabels& cur, const std::vector<i64>* prefix, Array& mmg, Array& mme) {
+    Impl& I = *impl_;
+    HIPCHECK(hipSetDevice(I.device));
+    I.check_cur(cur);
+    PhaseTrace tr_("relu_mult");
+    const int64_t N = I.cur_N;
+    const int k = I.k;
+    DASH_CHECK(I.sig.p && I.sig_N == N, "gpu garbler: joint ReLU without a preceding sign-producing rescale");
+    const int sig_slot = 0, sk0 = 1, nslots = 1 + 2 * k;
+    DevTable tG, tE;
+    tG.alloc(I.device, N, mmg.shape[1]);
+    tE.alloc(I.device, N, static_cast<int64_t>(k) * 3, true);
+    gg::Tables tb{};
+    tb.t[4] = tG.p(); tb.row[4] = tG.row;
+    tb.t[5] = tE.p(); tb.row[5] = tE.row;
+    gg::In in{};
+    for (int j = 0; j < k; ++j) {
+        in.p[j] = I.cur[j].as<int16_t>();
+        in.n[j] = nr_comps(I.crt[j]);
+    }
+    gg::Gadget g{};
+    g.layer = layer;
+    g.sslot = 2;
+    g.mask = 0;
+    g.S = I.scratch(static_cast<size_t>(N) * nslots * gg::kW * sizeof(int16_t));
+    g.N = N;
+    g.nslots = nslots;
+    HIPCHECK(hipMemcpy2DAsync(g.S + static_cast<int64_t>(sig_slot) * gg::kW, static_cast<size_t>(nslots) * gg::kW *
+                              sizeof(int16_t), I.sig.p, gg::kW * sizeof(int16_t), gg::kW * sizeof(int16_t),
+                              static_cast<size_t>(N), hipMemcpyDeviceToDevice, nullptr));
+    std::vector<DevBlock> out = relu_mult_gates(I, g, in, tb, sig_slot, sk0, *prefix);
+    HIPCHECK(hipGetLastError());
+    std::vector<void*> tmp;
+    gg::end_layer(tmp);
+    tr_.mark("kernels");
+    tG.to_array(mmg, I.device);
+    tE.to_array(mme, I.device);
+    I.cur = std::move(out);
+    I.sig = DevBlock();
+    I.sig_N = 0;
+    set_stale(cur, I.crt, N);
 }
 
 }  // namespace dash

@@ -43,8 +43,13 @@ class GpuGarbler {
     void relu_mrs(uint64_t layer, const SignMrsPlan& P, CrtLabels& cur, Array& tab, const std::vector<int>* relu_crt,
                   const std::vector<i64>* prefix, Array& mmg, Array& mme);
 
-   private:
+    // ReLU whose sign labels the preceding rescale_mrs (P.sign_last) left on the device: mixed-modulus half
+    // gates only; device cur -> next
+    void relu_mult(uint64_t layer, CrtLabels& cur, const std::vector<i64>* prefix, Array& mmg, Array& mme);
+
     struct Impl;
+
+   private:
     std::unique_ptr<Impl> impl_;
 };
 

@@ -94,8 +94,11 @@ struct MrsArgs {
     u128* ps;                      // [B][k(k-1)/2][N] digit payloads for later positions (chain scratch)
     int mode;                      // 0: rescale (position i = residue i, T accumulator, final row -> pf)
                                    // 1: sign (position i = residue (i + 1) mod k; the last key is sign01 -> hs, cs)
-    u128* hs;                      // mode 1: [B][N] hash of the sign label
-    uint8_t* cs;                   // mode 1: [B][N] its color
+                                   // 2: rescale in mode 1's order, the mod-2 key is also the next ReLU's sign
+    u128* hs;                      // modes 1, 2: [B][N] hash of the sign label
+    uint8_t* cs;                   // modes 1, 2: [B][N] its color
+    u128* hx;                      // mode 2: [B][k][N] H(compress(Y_j)) of the outputs (the next ReLU's keys)
+    uint16_t* colx;                // mode 2: [B][k][N] their colors
 };
 
 struct BEArgs {

@@ -715,6 +715,9 @@ __device__ __forceinline__ constexpr int mrs_pair(int l, int j) {  // l < j < K
 // 1..K-1, the last position is residue 0 (mod 2): its key is the bit pack of
 // L_0 XOR the K-1 payloads aimed at it (mod-2 subtraction), i.e. the sign
 // label itself; only its hash and color are produced (the ReLU multiply).
+// MODE 2 (joint rescale + ReLU sign, RescaleMrsPlan::sign_last): MODE 1's
+// order with MODE 0's T target on every row (the mod-2 position's row has only
+// that one) and final row; the mod-2 key's hash and color go to hs / cs.
 template <int K, int MODE>
 __global__ __launch_bounds__(kAesBlock, DASH_UA_MINBLOCKS) void k_mrs_chain(MrsArgs a, Act x, const ModC* mc,
                                                                           const uint32_t* te0, const uint32_t* rk) {
@@ -729,18 +732,22 @@ __global__ __launch_bounds__(kAesBlock, DASH_UA_MINBLOCKS) void k_mrs_chain(MrsA
         u128 acc = 0;
 #pragma unroll
         for (int i = 0; i < K; ++i) {
-            const int r = MODE == 1 ? (i + 1) % K : i;  // residue converted at position i
+            const int r = MODE >= 1 ? (i + 1) % K : i;  // residue converted at position i
             const ModC m = mc[a.crt.p[r]];
             const int n = static_cast<int>(m.n);
             const act_t* L = x.p[r] + static_cast<int64_t>(b) * n * N + e;
-            if (MODE == 1 && i == K - 1) {
+            if (MODE >= 1 && i == K - 1) {
                 // residue 0 (mod 2): compress = bit pack, subtraction = XOR
                 u128 key = compress_cm(L, N, m);
 #pragma unroll
                 for (int l = 0; l < K - 1; ++l) key ^= PS[static_cast<int64_t>(mrs_pair<K>(l, K - 1)) * N];
+                const uint32_t c = static_cast<uint32_t>(key) & 1u;
+                u128 E = 0;
+                if (MODE == 2) E = row0[a.dig_off[K - 1] + c];  // the sign digit's T payload row (one entry)
                 const u128 H = aes_encrypt(aes, key);
                 a.hs[static_cast<int64_t>(b) * N + e] = H;
-                a.cs[static_cast<int64_t>(b) * N + e] = static_cast<uint8_t>(static_cast<uint32_t>(key) & 1u);
+                a.cs[static_cast<int64_t>(b) * N + e] = static_cast<uint8_t>(c);
+                if (MODE == 2) acc = add_packed(acc, E - H, a.hmask);
                 break;
             }
             DigitStream ds[K > 1 ? K - 1 : 1];
@@ -772,7 +779,7 @@ __global__ __launch_bounds__(kAesBlock, DASH_UA_MINBLOCKS) void k_mrs_chain(MrsA
 #pragma unroll
                 for (int u = 0; u < kMrsChunk; ++u) cur[u] = nxt[u];
             }
-            constexpr int kExtra = MODE == 0 ? 1 : 0;        // rescale rows end with the T target
+            constexpr int kExtra = MODE == 1 ? 0 : 1;        // rescale rows end with the T target
             const int nt = K - 1 - i + kExtra;
             const u128* row = row0 + a.dig_off[i] + static_cast<int64_t>(col) * nt;
             u128 E[K];
@@ -781,7 +788,7 @@ __global__ __launch_bounds__(kAesBlock, DASH_UA_MINBLOCKS) void k_mrs_chain(MrsA
             const u128 H = aes_encrypt(aes, cf.finish());
 #pragma unroll
             for (int t = 0; t < K - 1 - i; ++t) PS[static_cast<int64_t>(mrs_pair<K>(i, i + 1 + t)) * N] = E[t] - H;
-            if (MODE == 0) acc = add_packed(acc, E[K - 1 - i] - H, a.hmask);
+            if (MODE != 1) acc = add_packed(acc, E[K - 1 - i] - H, a.hmask);
         }
         if (MODE == 1) continue;
         const uint32_t col = static_cast<uint32_t>(acc) & static_cast<uint32_t>(a.T - 1);
@@ -829,6 +836,64 @@ __global__ __launch_bounds__(256) void k_rescale_mrs_out(MrsArgs a, Act x, const
     }
 }
 
+// Joint rescale + ReLU (MODE 2): the output kernel also produces the next ReLU's garbler half-gate keys
+// hx[b][j][e] = H(compress(Y_j)), colx = color (k_label_hash's job) from the components it writes, so the
+// rescaled labels are not read back. Residue 0's output is the decompressed payload, its compress the payload.
+__global__ __launch_bounds__(kAesBlock, kAesMinBlocks) void k_rescale_mrs_out_hash(MrsArgs a, Act x, const ModC* mc,
+                                                                                  const uint32_t* te0,
+                                                                                  const uint32_t* rk) {
+    AES_PROLOGUE(te0, rk);
+    const int j = blockIdx.y, b = blockIdx.z;
+    const int64_t N = a.N;
+    const int k = a.crt.k;
+    const ModC m = mc[a.crt.p[j]];
+    const int n = static_cast<int>(m.n);
+    for (int64_t e = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; e < N;
+         e += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+        act_t* L = x.p[j] + static_cast<int64_t>(b) * n * N + e;
+        const int64_t bke = (static_cast<int64_t>(b) * k + j) * N + e;
+        const u128 P = a.pf[bke];
+        DigitStream s;
+        s.init(P);
+        if (j == 0) {
+            uint32_t c0 = 0;
+            for (int c = 0; c < n; ++c) {
+                const uint32_t v = s.next(m);
+                if (c == 0) c0 = v;
+                L[static_cast<int64_t>(c) * N] = static_cast<act_t>(v);
+            }
+            a.colx[bke] = static_cast<uint16_t>(c0);
+            a.hx[bke] = aes_encrypt(aes, P);
+            continue;
+        }
+        const uint32_t inv = static_cast<uint32_t>(a.sinv[j]);
+        CompressFwd cf;
+        cf.init();
+        uint32_t c0 = 0;
+        uint16_t cur[kChunk], nxt[kChunk];
+#pragma unroll
+        for (int u = 0; u < kChunk; ++u)
+            if (u < n) cur[u] = L[static_cast<int64_t>(u) * N];
+        for (int q0 = 0; q0 < n; q0 += kChunk) {
+#pragma unroll
+            for (int u = 0; u < kChunk; ++u)
+                if (q0 + kChunk + u < n) nxt[u] = L[static_cast<int64_t>(q0 + kChunk + u) * N];
+#pragma unroll
+            for (int u = 0; u < kChunk; ++u)
+                if (q0 + u < n) {
+                    const uint32_t v = modq(cur[u] * inv + s.next(m), m);  // < p^2 + p
+                    if (q0 + u == 0) c0 = v;
+                    L[static_cast<int64_t>(q0 + u) * N] = static_cast<act_t>(v);
+                    cf.push(v, m);
+                }
+#pragma unroll
+            for (int u = 0; u < kChunk; ++u) cur[u] = nxt[u];
+        }
+        a.colx[bke] = static_cast<uint16_t>(c0);
+        a.hx[bke] = aes_encrypt(aes, cf.finish());
+    }
+}
+
 // hx[b][j][e] = H(compress(x_j)), colx = color: the ReLU multiply's garbler half gates (exact-sign path;
 // the approximate path gets them from k_sign_approx). grid (x, k, B)
 __global__ __launch_bounds__(kAesBlock, kAesMinBlocks) void k_label_hash(Act x, CrtInfo crt, int64_t N, u128* hx,
@@ -862,18 +927,33 @@ void launch_relu_mrs(const MrsArgs& a, const SignArgs& sa, const Act& x, const A
     launch_relu_mult(sa, x, y, gtab, etab, mc, st);
 }
 
+// ReLU after a sign-producing rescale: the rescale wrote the sign's hash / color (chain MODE 2) and the
+// half-gate keys of x (k_rescale_mrs_out_hash); only the mixed-modulus multiply is left
+void launch_relu_joint(const SignArgs& sa, const Act& x, const Act& y, const u128* gtab, const u128* etab, int B,
+                       const ModC* mc, const AesGlobals& g, hipStream_t st) {
+    (void)B;
+    (void)g;
+    launch_relu_mult(sa, x, y, gtab, etab, mc, st);
+}
+
 void launch_rescale_mrs(const MrsArgs& a, const Act& x, int B, const ModC* mc, const AesGlobals& g, hipStream_t st) {
     const dim3 gc = grid_aes(a.N, aes_bs(a.N, 1, B), 1, B), bc(aes_bs(a.N, 1, B));
     switch (a.crt.k) {
 #define DASH_MRS_K(KK) \
-        case KK: hipLaunchKernelGGL((k_mrs_chain<KK, 0>), gc, bc, kAesLds, st, a, x, mc, g.te0, g.rk); break;
+        case KK: \
+            if (a.mode == 2) hipLaunchKernelGGL((k_mrs_chain<KK, 2>), gc, bc, kAesLds, st, a, x, mc, g.te0, g.rk); \
+            else hipLaunchKernelGGL((k_mrs_chain<KK, 0>), gc, bc, kAesLds, st, a, x, mc, g.te0, g.rk); \
+            break;
         DASH_MRS_K(2) DASH_MRS_K(3) DASH_MRS_K(4) DASH_MRS_K(5) DASH_MRS_K(6) DASH_MRS_K(7) DASH_MRS_K(8)
         DASH_MRS_K(9) DASH_MRS_K(10) DASH_MRS_K(11) DASH_MRS_K(12)
 #undef DASH_MRS_K
         default: std::fprintf(stderr, "dash: mixed-radix rescale supports 2..12 CRT residues\n"); std::abort();
     }
-    hipLaunchKernelGGL(k_rescale_mrs_out, dim3(static_cast<unsigned>((a.N + 255) / 256), a.crt.k, B), dim3(256), 0, st, a,
-                       x, mc);
+    if (a.mode == 2)
+        hipLaunchKernelGGL(k_rescale_mrs_out_hash, AES_LAUNCH(a.N, a.crt.k, B), kAesLds, st, a, x, mc, g.te0, g.rk);
+    else
+        hipLaunchKernelGGL(k_rescale_mrs_out, dim3(static_cast<unsigned>((a.N + 255) / 256), a.crt.k, B), dim3(256), 0,
+                           st, a, x, mc);
 }
 
 // ---------------------------------------------------------------------------

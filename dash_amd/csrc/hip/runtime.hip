@@ -679,6 +679,30 @@ void HipEvaluator::build() {
                 break;
             }
             case K_RELU: {
+                if (g.param("smode", 0) == 2) {  // sign from the preceding rescale (RescaleMrsPlan::sign_last)
+                    DASH_CHECK(li > 0 && m0.layers[li - 1].kind == K_RESCALE &&
+                                   m0.layers[li - 1].param("sign_out", 0) == 1,
+                               "joint ReLU must follow a sign-producing rescale");
+                    SignArgs sa{};
+                    sa.crt = crt;
+                    sa.N = N;
+                    sa.B = B_;
+                    sa.hx = hx_;
+                    sa.colx = colx_;
+                    sa.hs = hs_;
+                    sa.cs = cs_;
+                    const u128* gt = upload_tables(li, "mm.g");
+                    const u128* et = upload_tables(li, "mm.e");
+                    Act x = act_of(cur), y = act_of(nxt);
+                    const ModC* mc = mc_;
+                    const AesGlobals ag = aes_;
+                    const int B = B_;
+                    add_op(lname + ".C", [sa, x, y, gt, et, B, mc, ag](hipStream_t st) {
+                        launch_relu_joint(sa, x, y, gt, et, B, mc, ag, st);
+                    });
+                    cur = nxt;
+                    break;
+                }
                 if (g.param("smode", 0) == 1) {  // exact mixed-radix sign (gadgets.h SignMrsPlan)
                     const SignMrsPlan P(crt_);
                     MrsArgs a{};
@@ -746,7 +770,8 @@ void HipEvaluator::build() {
                 const i64 mode = g.param("mode", 0);
                 const i64 iters = g.param("iters");
                 if (mode == 2) {  // mixed-radix construction of the legacy function (gadgets.h RescaleMrsPlan)
-                    const RescaleMrsPlan P(crt_, static_cast<int>(g.param("l")));
+                    const bool so = g.param("sign_out", 0) == 1;  // joint: the next ReLU's sign -> hs_, cs_
+                    const RescaleMrsPlan P(crt_, static_cast<int>(g.param("l")), so);
                     DASH_CHECK(P.T <= m0.h.max_mod, "model lacks the mod-2^(l+1) label constants");
                     MrsArgs a{};
                     a.crt = crt;
@@ -765,6 +790,11 @@ void HipEvaluator::build() {
                     a.pf = outP_;  // [B][k][N] <= the sign outputs' scratch
                     if (!mrs_ps_) mrs_ps_ = dalloc<u128>(static_cast<size_t>(B_) * std::max(1, k_ * (k_ - 1) / 2) * maxSignN_);
                     a.ps = mrs_ps_;
+                    a.mode = so ? 2 : 0;
+                    a.hs = hs_;
+                    a.cs = cs_;
+                    a.hx = hx_;
+                    a.colx = colx_;
                     Act x = act_of(cur);
                     const ModC* mc = mc_;
                     const AesGlobals ag = aes_;

@@ -103,6 +103,9 @@ struct GarbleOptions {
     bool fused_sign = true;  // sign gadget construction (gadgets.h SignPlan::fused); false: reference casts
     bool rescale_mrs = false;  // legacy (l-halving) rescale as one mixed-radix gadget (gadgets.h RescaleMrsPlan)
     bool relu_mrs = false;     // ReLU sign by exact mixed-radix conversion (gadgets.h SignMrsPlan)
+    // A ReLU right after a mixed-radix rescale takes its sign from that rescale's conversion
+    // (gadgets.h RescaleMrsPlan::sign_last); other ReLUs use relu_mrs / the approximate gadget.
+    bool relu_joint = false;
 };
 
 class Garbler {

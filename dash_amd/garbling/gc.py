@@ -42,7 +42,10 @@ class GarbledCircuit:
 
         relu: sign of the ReLU gadget. "approx": the reference's approximate sign gadget (construction per
         fused_sign). "mrs": exact mixed-radix sign with the mod-2 residue converted last (gadgets.h SignMrsPlan;
-        k - 1 hashes, 147 instead of 568 table entries per element at k = 7, exact for every x)."""
+        k - 1 hashes, 147 instead of 568 table entries per element at k = 7, exact for every x). "joint": a ReLU
+        that directly follows a mixed-radix rescale takes its sign from that rescale's conversion (residue 2
+        converted last: its digit is the sign; gadgets.h RescaleMrsPlan::sign_last), so it costs only the
+        mixed-modulus half gates; other ReLUs use the approximate gadget. Needs rescale="mrs" to have effect."""
         self.circuit = circuit
         self.crt_base = first_primes(crt) if isinstance(crt, int) else [int(p) for p in crt]
         if mrs is None:
@@ -60,8 +63,8 @@ class GarbledCircuit:
         if rescale not in ("legacy", "mrs"):
             raise ValueError(f"rescale construction must be 'legacy' or 'mrs', got {rescale!r}")
         self.rescale = rescale
-        if relu not in ("approx", "mrs"):
-            raise ValueError(f"relu construction must be 'approx' or 'mrs', got {relu!r}")
+        if relu not in ("approx", "mrs", "joint"):
+            raise ValueError(f"relu construction must be 'approx', 'mrs' or 'joint', got {relu!r}")
         self.relu = relu
         self._n = native()
         self.garbler = self._n.Garbler(self.crt_base, self.mrs_base, self.seed, int(max_modulus))
@@ -76,7 +79,8 @@ class GarbledCircuit:
         specs = self.circuit.garble_specs()
         t = time.perf_counter()
         self.model = self.garbler.garble(specs, list(self.circuit.input_dims), self.nthreads, self.device,
-                                         self.fused_sign, self.rescale == "mrs", self.relu == "mrs")
+                                         self.fused_sign, self.rescale == "mrs", self.relu == "mrs",
+                                         self.relu == "joint")
         self.garbling_time_s = time.perf_counter() - t
         self.decoder = self.garbler.decoder()
         return self.model

@@ -33,6 +33,7 @@ void GpuGarbler::relu_mrs(uint64_t, const SignMrsPlan&, CrtLabels&, Array&, cons
                           const std::vector<i64>*, Array&, Array&) {
     no_gpu();
 }
+void GpuGarbler::relu_mult(uint64_t, CrtLabels&, const std::vector<i64>*, Array&, Array&) { no_gpu(); }
 void gpu_table_cache_trim() {}
 size_t gpu_table_cache_bytes() { return 0; }
 

@@ -392,3 +392,51 @@ def test_relu_mrs_tables_and_model():
     for x in xs:
         y = both.decode_outputs(both.cpu_evaluate(both.garble_inputs(x)))
         np.testing.assert_array_equal(y, both.plain_q_eval(x))
+
+
+# -------------------------------- joint rescale + ReLU: the rescale's conversion yields the ReLU's sign
+@pytest.mark.parametrize("k,l", [(7, 5), (7, 1), (8, 3), (4, 4), (2, 1)])
+def test_rescale_relu_joint_exact(k, l):
+    """relu(ceil(x / 2^l)) with the sign taken from the rescale's mixed-radix digit of residue 2 (converted
+    last): exact on the rescale's domain, values around 0 (where the sign threshold sits) included."""
+    mrs = 100.0 if k >= 4 else None
+    c0 = d.Circuit([d.Rescale(l, (1,))])
+    M = GarbledCircuit(c0, k, mrs, seed=SEED, garble_me=False).crt_modulus
+    S = 1 << l
+    U, q = _mrs_shift(M, S)
+    top = M // 2 - (U - M // 2)
+    rng = np.random.default_rng(k * 31 + l)
+    vals = [-M // 2, -M // 2 + 1, top - 1, top - 2, 0, 1, -1, 2, S, -S, S - 1, 1 - S, S + 1, -S - 1]
+    vals += list(range(-2 * S - 2, 2 * S + 3))
+    vals += list(rng.integers(-M // 2, top, 48))
+    x = np.array([v for v in vals if -M // 2 <= v < top], dtype=np.int64)
+    n = len(x)
+    c = d.Circuit([d.Rescale(l, (n,)), d.Relu((n,))])
+    gc = GarbledCircuit(c, k, mrs, seed=SEED, rescale="mrs", relu="joint")
+    assert list(gc.model.layer_params(1)["smode"]) == [2]
+    assert list(gc.model.layer_params(0)["sign_out"]) == [1]
+    out = gc.decode_outputs(gc.cpu_evaluate(gc.garble_inputs(x)))
+    np.testing.assert_array_equal(out, np.maximum(-((-x) // S), 0))
+
+
+def test_rescale_relu_joint_model():
+    """MODEL_B with joint rescale + ReLU decodes to the plaintext output; the joint ReLUs carry only the
+    mixed-modulus half-gate tables, and the model survives serialization."""
+    from dash_amd.ir.quant import QuantizationMethod as Q
+    from dash_amd.models import build_circuit, quantized_inputs
+    from dash_amd.native import native
+
+    c = build_circuit("MODEL_B_POOL_REPL", Q.ScaleQuant, 3, seed=1)
+    xs = quantized_inputs("MODEL_B_POOL_REPL", 3, Q.ScaleQuant, 3, seed=7)
+    joint = GarbledCircuit(c, 8, 100.0, seed=SEED, rescale="mrs", relu="joint")
+    resc = GarbledCircuit(c, 8, 100.0, seed=SEED, rescale="mrs")
+    assert joint.table_bytes < resc.table_bytes
+    nj = sum(1 for i in range(joint.model.num_layers) if list(joint.model.layer_params(i).get("smode", [])) == [2])
+    assert nj >= 1
+    for x in xs:
+        y = joint.decode_outputs(joint.cpu_evaluate(joint.garble_inputs(x)))
+        np.testing.assert_array_equal(y, joint.plain_q_eval(x))
+    blob = joint.model.serialize()
+    m2 = native().GarbledModel.deserialize(blob)
+    y = joint.decode_outputs(native().cpu_evaluate(m2, joint.garble_inputs(xs[0]), 0))
+    np.testing.assert_array_equal(y, joint.plain_q_eval(xs[0]))

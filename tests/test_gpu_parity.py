@@ -116,7 +116,7 @@ def test_rescale_mrs(k, l):
     _check(c, k, 100.0, xs, rescale="mrs")
 
 
-@pytest.mark.parametrize("relu", ["approx", "mrs"])
+@pytest.mark.parametrize("relu", ["approx", "mrs", "joint"])
 def test_minionn_head_mrs_rescale(relu):
     """MiniONN conv -> rescale(l=5) -> relu at full size with the mixed-radix rescale (and sign)."""
     from dash_amd.ir.quant import QuantizationMethod as Q
@@ -323,5 +323,40 @@ def test_gpu_garbler_bit_identical_mrs_relu(name):
     seed = bytes(range(16))
     cpu = GarbledCircuit(c, k, 100.0, seed=seed, rescale="mrs", relu="mrs")
     gpu = GarbledCircuit(c, k, 100.0, seed=seed, device=0, rescale="mrs", relu="mrs")
+    assert gpu.model.serialize() == cpu.model.serialize()
+    assert gpu.decoder.serialize() == cpu.decoder.serialize()
+
+
+@pytest.mark.parametrize("k,l", [(7, 5), (8, 3), (2, 1)])
+def test_rescale_relu_joint(k, l):
+    """Joint rescale + ReLU (chain mode 2 writes the sign hash/color, label hash + mixed multiply) == host
+    oracle == relu(ceil(x / 2^l)), values around the sign threshold included."""
+    mrs = 100.0 if k >= 4 else None
+    c0 = d.Circuit([d.Relu((1,))])
+    M = GarbledCircuit(c0, k, mrs, garble_me=False).crt_modulus
+    S, h = 1 << l, M // 2
+    rng = np.random.default_rng(k + l)
+    vals = list(range(-2 * S - 2, 2 * S + 3)) + [-h, -h + 1] + list(rng.integers(-h, h - S, 100))
+    x = np.array([v for v in vals if -h <= v < h - S], dtype=np.int64)  # the rescale's non-wrapping domain
+    c = d.Circuit([d.Rescale(l, (len(x),)), d.Relu((len(x),))])
+    outs = _check(c, k, mrs, [x, x[::-1].copy()], rescale="mrs", relu="joint")
+    np.testing.assert_array_equal(outs[0], np.maximum(-((-x) // S), 0))
+
+
+@pytest.mark.parametrize("name", ["pair", "minionn_head"])
+def test_gpu_garbler_bit_identical_joint_relu(name):
+    """GPU garbler of the joint rescale + ReLU (sign_last rescale, relu_mult) == host garbler, byte for byte."""
+    from dash_amd.ir.circuit import Circuit
+    from dash_amd.ir.quant import QuantizationMethod as Q
+    from dash_amd.models import build_circuit
+
+    if name == "pair":
+        c, k = d.Circuit([d.Rescale(3, (300,)), d.Relu((300,))]), 7
+    else:
+        full = build_circuit("MODEL_F_MINIONN_POOL_REPL", Q.ScaleQuant, 5, seed=0)
+        c, k = Circuit(full.layers[:7]), 7  # conv, rescale, relu, conv, rescale, relu, conv
+    seed = bytes(range(16))
+    cpu = GarbledCircuit(c, k, 100.0, seed=seed, rescale="mrs", relu="joint")
+    gpu = GarbledCircuit(c, k, 100.0, seed=seed, device=0, rescale="mrs", relu="joint")
     assert gpu.model.serialize() == cpu.model.serialize()
     assert gpu.decoder.serialize() == cpu.decoder.serialize()
