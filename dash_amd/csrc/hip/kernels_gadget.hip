@@ -894,6 +894,110 @@ __global__ __launch_bounds__(kAesBlock, kAesMinBlocks) void k_rescale_mrs_out_ha
     }
 }
 
+// Joint rescale + ReLU, both outputs in one pass per (element, residue): Y_j (the rescaled label, written in
+// place), its hash -> the garbler half gate G = g[color(Y_j)] - H(Y_j) (gathered as soon as the first
+// component is known), then relu_j = E + ypr * Y_j - G (k_relu_mult's arithmetic) streamed into y while Y_j
+// is read back from the lines this lane just wrote. The sign's hash / color come from chain MODE 2.
+__global__ __launch_bounds__(kAesBlock, kAesMinBlocks) void k_rescale_relu_out(MrsArgs a, SignArgs sa, Act x, Act y,
+                                                                              const u128* gtab, const u128* etab,
+                                                                              const ModC* mc, const uint32_t* te0,
+                                                                              const uint32_t* rk) {
+    AES_PROLOGUE(te0, rk);
+    const int j = blockIdx.y, b = blockIdx.z;
+    const int64_t N = a.N;
+    const int k = a.crt.k;
+    const int p = a.crt.p[j];
+    const ModC m = mc[p];
+    const int n = static_cast<int>(m.n);
+    const uint32_t inv = static_cast<uint32_t>(a.sinv[j]);
+    for (int64_t e = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; e < N;
+         e += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+        const int64_t be = static_cast<int64_t>(b) * N + e;
+        const int64_t bke = (static_cast<int64_t>(b) * k + j) * N + e;
+        act_t* L = x.p[j] + static_cast<int64_t>(b) * n * N + e;
+        act_t* Y = y.p[j] + static_cast<int64_t>(b) * n * N + e;
+        const u128 HS = a.hs[be];
+        const uint32_t cS = a.cs[be];
+        const u128* E3 = etab + (be * k + j) * 3;
+        const u128 Eraw = E3[cS];
+        const u128 mini = E3[2];
+        const u128* grow = gtab + be * sa.crt.sum + sa.crt.prefix[j];
+        const u128 P = a.pf[bke];
+        DigitStream s;
+        s.init(P);
+        u128 key, Graw;
+        if (j == 0) {
+            // Y_0 = decompress(P), compress(Y_0) = P
+            uint32_t c0 = 0;
+            for (int c = 0; c < n; ++c) {
+                const uint32_t v = s.next(m);
+                if (c == 0) {
+                    c0 = v;
+                    Graw = grow[c0];
+                }
+                L[static_cast<int64_t>(c) * N] = static_cast<act_t>(v);
+            }
+            key = P;
+        } else {
+            CompressFwd cf;
+            cf.init();
+            uint16_t cur[kChunk], nxt[kChunk];
+#pragma unroll
+            for (int u = 0; u < kChunk; ++u)
+                if (u < n) cur[u] = L[static_cast<int64_t>(u) * N];
+            for (int q0 = 0; q0 < n; q0 += kChunk) {
+#pragma unroll
+                for (int u = 0; u < kChunk; ++u)
+                    if (q0 + kChunk + u < n) nxt[u] = L[static_cast<int64_t>(q0 + kChunk + u) * N];
+#pragma unroll
+                for (int u = 0; u < kChunk; ++u)
+                    if (q0 + u < n) {
+                        const uint32_t v = modq(cur[u] * inv + s.next(m), m);  // < p^2 + p
+                        if (q0 + u == 0) Graw = grow[v];
+                        L[static_cast<int64_t>(q0 + u) * N] = static_cast<act_t>(v);
+                        cf.push(v, m);
+                    }
+#pragma unroll
+                for (int u = 0; u < kChunk; ++u) cur[u] = nxt[u];
+            }
+            key = cf.finish();
+        }
+        const u128 G = Graw - aes_encrypt(aes, key);
+        const u128 E = Eraw - HS;
+        const int16_t t16 = static_cast<int16_t>(static_cast<uint16_t>(mini >> (16 * cS)));
+        const int16_t ypr16 = static_cast<int16_t>(t16 - static_cast<int16_t>(static_cast<uint16_t>(HS)));
+        const uint32_t ypr = modq(static_cast<uint32_t>(static_cast<int32_t>(ypr16) + (p << 15)), m);
+        DigitStream sg, se;
+        sg.init(G);
+        se.init(E);
+        uint16_t cur[kChunk], nxt[kChunk];
+#pragma unroll
+        for (int u = 0; u < kChunk; ++u)
+            if (u < n) cur[u] = L[static_cast<int64_t>(u) * N];
+        for (int i0 = 0; i0 < n; i0 += kChunk) {
+#pragma unroll
+            for (int u = 0; u < kChunk; ++u)
+                if (i0 + kChunk + u < n) nxt[u] = L[static_cast<int64_t>(i0 + kChunk + u) * N];
+#pragma unroll
+            for (int u = 0; u < kChunk; ++u)
+                if (i0 + u < n) {
+                    const uint32_t g = sg.next(m);
+                    const uint32_t ev = se.next(m);
+                    Y[static_cast<int64_t>(i0 + u) * N] =
+                        static_cast<act_t>(modq(ev + ypr * static_cast<uint32_t>(cur[u]) + static_cast<uint32_t>(p) - g, m));
+                }
+#pragma unroll
+            for (int u = 0; u < kChunk; ++u) cur[u] = nxt[u];
+        }
+    }
+}
+
+void launch_rescale_relu_out(const MrsArgs& a, const SignArgs& sa, const Act& x, const Act& y, const u128* gtab,
+                             const u128* etab, int B, const ModC* mc, const AesGlobals& g, hipStream_t st) {
+    hipLaunchKernelGGL(k_rescale_relu_out, AES_LAUNCH(a.N, a.crt.k, B), kAesLds, st, a, sa, x, y, gtab, etab, mc,
+                       g.te0, g.rk);
+}
+
 // hx[b][j][e] = H(compress(x_j)), colx = color: the ReLU multiply's garbler half gates (exact-sign path;
 // the approximate path gets them from k_sign_approx). grid (x, k, B)
 __global__ __launch_bounds__(kAesBlock, kAesMinBlocks) void k_label_hash(Act x, CrtInfo crt, int64_t N, u128* hx,
@@ -936,7 +1040,8 @@ void launch_relu_joint(const SignArgs& sa, const Act& x, const Act& y, const u12
     launch_relu_mult(sa, x, y, gtab, etab, mc, st);
 }
 
-void launch_rescale_mrs(const MrsArgs& a, const Act& x, int B, const ModC* mc, const AesGlobals& g, hipStream_t st) {
+void launch_rescale_mrs(const MrsArgs& a, const Act& x, int B, const ModC* mc, const AesGlobals& g, hipStream_t st,
+                        bool chain_only) {
     const dim3 gc = grid_aes(a.N, aes_bs(a.N, 1, B), 1, B), bc(aes_bs(a.N, 1, B));
     switch (a.crt.k) {
 #define DASH_MRS_K(KK) \
@@ -949,6 +1054,7 @@ void launch_rescale_mrs(const MrsArgs& a, const Act& x, int B, const ModC* mc, c
 #undef DASH_MRS_K
         default: std::fprintf(stderr, "dash: mixed-radix rescale supports 2..12 CRT residues\n"); std::abort();
     }
+    if (chain_only) return;  // the joint ReLU's k_rescale_relu_out writes the outputs
     if (a.mode == 2)
         hipLaunchKernelGGL(k_rescale_mrs_out_hash, AES_LAUNCH(a.N, a.crt.k, B), kAesLds, st, a, x, mc, g.te0, g.rk);
     else

@@ -30,7 +30,10 @@ void launch_rescale_hash_sign(const u128* signP, const u128* du, int64_t N, int 
                               const AesGlobals& g, hipStream_t st);
 void launch_rescale_update_approx(const RescaleArgs& r, const SignArgs& a, const Act& x, const int16_t* delta,
                                   const u128* zh, int B, const ModC* mc, const AesGlobals& g, hipStream_t st);
-void launch_rescale_mrs(const MrsArgs& a, const Act& x, int B, const ModC* mc, const AesGlobals& g, hipStream_t st);
+void launch_rescale_mrs(const MrsArgs& a, const Act& x, int B, const ModC* mc, const AesGlobals& g, hipStream_t st,
+                        bool chain_only = false);
+void launch_rescale_relu_out(const MrsArgs& a, const SignArgs& sa, const Act& x, const Act& y, const u128* gtab,
+                             const u128* etab, int B, const ModC* mc, const AesGlobals& g, hipStream_t st);
 void launch_relu_joint(const SignArgs& sa, const Act& x, const Act& y, const u128* gtab, const u128* etab, int B,
                        const ModC* mc, const AesGlobals& g, hipStream_t st);
 void launch_relu_mrs(const MrsArgs& a, const SignArgs& sa, const Act& x, const Act& y, const u128* gtab,

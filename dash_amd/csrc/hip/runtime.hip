@@ -394,6 +394,9 @@ class HipEvaluator {
     const int16_t* up_rows_ = nullptr;
     u128* mrs_ps_ = nullptr;  // mixed-radix rescale chain scratch (allocated by the first such layer)
     i64 maxSignN_ = 0;
+    // planner: a sign-producing rescale whose outputs the next (joint) ReLU's op writes
+    bool joint_pending_ = false;
+    MrsArgs joint_a_{};
     const u128* zc_ = nullptr;
     const u128* zh_ = nullptr;
     const uint16_t* zcol_ = nullptr;
@@ -697,9 +700,17 @@ void HipEvaluator::build() {
                     const ModC* mc = mc_;
                     const AesGlobals ag = aes_;
                     const int B = B_;
-                    add_op(lname + ".C", [sa, x, y, gt, et, B, mc, ag](hipStream_t st) {
-                        launch_relu_joint(sa, x, y, gt, et, B, mc, ag, st);
-                    });
+                    if (joint_pending_) {
+                        const MrsArgs ma = joint_a_;
+                        joint_pending_ = false;
+                        add_op(lname + ".C", [ma, sa, x, y, gt, et, B, mc, ag](hipStream_t st) {
+                            launch_rescale_relu_out(ma, sa, x, y, gt, et, B, mc, ag, st);
+                        });
+                    } else {
+                        add_op(lname + ".C", [sa, x, y, gt, et, B, mc, ag](hipStream_t st) {
+                            launch_relu_joint(sa, x, y, gt, et, B, mc, ag, st);
+                        });
+                    }
                     cur = nxt;
                     break;
                 }
@@ -799,7 +810,26 @@ void HipEvaluator::build() {
                     const ModC* mc = mc_;
                     const AesGlobals ag = aes_;
                     const int B = B_;
-                    add_op(lname + ".mrs", [a, x, B, mc, ag](hipStream_t st) { launch_rescale_mrs(a, x, B, mc, ag, st); });
+                    // joint ReLU next and this output not kept for a later layer: the ReLU's op can write both
+                    // outputs in one pass (k_rescale_relu_out), here only the chain runs. Measured (MiniONN):
+                    // faster at batch 1 (2.81 vs 2.98 ms per step), slower at batch 24 (15.9 vs 15.1 ms: the
+                    // hash -> second pass dependency per lane), so only small batches take it;
+                    // DASH_JOINT_FUSE=0/1 forces it off/on.
+                    static const int fuse_env = [] {
+                        const char* e = std::getenv("DASH_JOINT_FUSE");
+                        return e ? std::atoi(e) : -1;
+                    }();
+                    const bool fuse = fuse_env >= 0 ? fuse_env == 1 : B_ <= 2;
+                    const bool defer = fuse && so && li + 1 < m0.layers.size() && m0.layers[li + 1].kind == K_RELU &&
+                                       m0.layers[li + 1].param("smode", 0) == 2 && !keep[li + 1] &&
+                                       !m0.layers[li + 1].p.count("in_src");
+                    if (defer) {
+                        joint_a_ = a;
+                        joint_pending_ = true;
+                    }
+                    add_op(lname + ".mrs", [a, x, B, mc, ag, defer](hipStream_t st) {
+                        launch_rescale_mrs(a, x, B, mc, ag, st, defer);
+                    });
                     break;
                 }
                 if (mode == 0) {

@@ -327,10 +327,12 @@ def test_gpu_garbler_bit_identical_mrs_relu(name):
     assert gpu.decoder.serialize() == cpu.decoder.serialize()
 
 
+@pytest.mark.parametrize("nb", [2, 3], ids=["b2_one_pass", "b3_two_kernels"])
 @pytest.mark.parametrize("k,l", [(7, 5), (8, 3), (2, 1)])
-def test_rescale_relu_joint(k, l):
-    """Joint rescale + ReLU (chain mode 2 writes the sign hash/color, label hash + mixed multiply) == host
-    oracle == relu(ceil(x / 2^l)), values around the sign threshold included."""
+def test_rescale_relu_joint(k, l, nb):
+    """Joint rescale + ReLU (chain mode 2 writes the sign hash/color; batch <= 2: k_rescale_relu_out, else
+    k_rescale_mrs_out_hash + k_relu_mult) == host oracle == relu(ceil(x / 2^l)), values around the sign
+    threshold included."""
     mrs = 100.0 if k >= 4 else None
     c0 = d.Circuit([d.Relu((1,))])
     M = GarbledCircuit(c0, k, mrs, garble_me=False).crt_modulus
@@ -339,7 +341,8 @@ def test_rescale_relu_joint(k, l):
     vals = list(range(-2 * S - 2, 2 * S + 3)) + [-h, -h + 1] + list(rng.integers(-h, h - S, 100))
     x = np.array([v for v in vals if -h <= v < h - S], dtype=np.int64)  # the rescale's non-wrapping domain
     c = d.Circuit([d.Rescale(l, (len(x),)), d.Relu((len(x),))])
-    outs = _check(c, k, mrs, [x, x[::-1].copy()], rescale="mrs", relu="joint")
+    xs = [x, x[::-1].copy(), np.roll(x, 7)][:nb]
+    outs = _check(c, k, mrs, xs, rescale="mrs", relu="joint")
     np.testing.assert_array_equal(outs[0], np.maximum(-((-x) // S), 0))
 
 
