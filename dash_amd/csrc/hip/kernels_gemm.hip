@@ -328,6 +328,9 @@ __device__ __forceinline__ uint32_t modq_conv(uint32_t x, uint32_t q, uint32_t m
 #ifndef DASH_CONV_ITEMS
 #define DASH_CONV_ITEMS 2
 #endif
+#ifndef DASH_CONV_CLAMP
+#define DASH_CONV_CLAMP 1  // edge items of the band staging as clamped 8-B loads (0: byte-wise, A/B)
+#endif
 template <int KSC>
 __global__ __launch_bounds__(256) void k_conv_img2(ConvArgs a, Act x, Act y, int B) {
     constexpr bool AREG = KSC > 0;
@@ -434,6 +437,25 @@ __global__ __launch_bounds__(256) void k_conv_img2(ConvArgs a, Act x, Act y, int
 #endif
                 raw[q][0] = rawx ? t[0] : center4(t[0]);
                 raw[q][1] = rawx ? t[1] : center4(t[1]);
+            } else if (DASH_CONV_CLAMP && a.W >= 8) {
+                // edge item: one 8-B load clamped into the row, the 8 columns shifted into place and the
+                // out-of-image bytes replaced by the padding byte (branch-free; the byte-wise loop below cost
+                // 8 dependent loads per channel and diverged from the wave's full items)
+                const int s0 = min(max(ix0, 0), a.W - 8);
+                const int sh = ix0 - s0;  // > 0: right edge, < 0: left padding
+                uint64_t t = 0;
+                if (rowin && sh > -8 && sh < 8) t = *reinterpret_cast<const uint64_t*>(row + s0);
+                t = sh >= 8 || sh <= -8 ? 0ull : (sh >= 0 ? t >> (8 * sh) : t << (-8 * sh));
+                const int lo = max(0, -ix0), hi = min(8, a.W - ix0);  // valid bytes [lo, hi)
+                uint64_t msk = 0;
+                if (rowin && hi > lo)
+                    msk = (hi >= 8 ? ~0ull : (1ull << (8 * hi)) - 1ull) & ~((1ull << (8 * lo)) - 1ull);
+                const uint32_t t0 = static_cast<uint32_t>(t), t1 = static_cast<uint32_t>(t >> 32);
+                const uint64_t c = (static_cast<uint64_t>(rawx ? t1 : center4(t1)) << 32) | (rawx ? t0 : center4(t0));
+                const uint64_t padr = static_cast<uint64_t>(padb) * 0x0101010101010101ull;
+                const uint64_t v = (c & msk) | (padr & ~msk);
+                raw[q][0] = static_cast<uint32_t>(v);
+                raw[q][1] = static_cast<uint32_t>(v >> 32);
             } else {
                 raw[q][0] = raw[q][1] = 0u;
 #pragma unroll
