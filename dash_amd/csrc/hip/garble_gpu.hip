@@ -1514,11 +1514,14 @@ void GpuGarbler::conv(const ConvGeom& G, const std::vector<i64>& w, CrtLabels& c
         a.OH = static_cast<int>(G.OH); a.OW = static_cast<int>(G.OW);
         a.Kpad = (K + 63) / 64 * 64;
         a.use_mfma = 1;
+        int max_p = 0;
+        for (int j = 0; j < a.crt.k; ++j) max_p = std::max(max_p, mods[j]);
+        dev::conv_unroll_taps(a, max_p);
         dev::conv_img_geometry(a);
+        DASH_CHECK(!a.ur || a.nbands > 0, "gpu garbler: tap-unrolled conv without an LDS band");
         a.zero = I.c.Z;  // one GC: zero label component c of residue j at Z[p_j * kW + c]
         a.lab_stride = 0;
         a.img_off[0] = 0;
-        const int F16 = (F + 15) / 16 * 16;
         for (int j = 0; j < a.crt.k; ++j) {
             const int p = mods[j], n = a.crt.n[j];
             a.lab_off[j] = p * gg::kW;
@@ -1540,13 +1543,7 @@ void GpuGarbler::conv(const ConvGeom& G, const std::vector<i64>& w, CrtLabels& c
             a.w8[j] = nullptr;
             a.w8r[j] = nullptr;
             if (p <= 255 && a.nbands > 0) {
-                std::vector<int8_t> w8r(static_cast<size_t>(F16) * G.kh * G.kw * a.Cpad, 0);
-                for (int f = 0; f < F; ++f)
-                    for (int ci = 0; ci < a.C; ++ci)
-                        for (int dy = 0; dy < a.kh; ++dy)
-                            for (int dx = 0; dx < a.kw; ++dx)
-                                w8r[((static_cast<size_t>(f) * a.kh + dy) * a.kw + dx) * a.Cpad + ci] =
-                                    w8[static_cast<size_t>(f) * a.Kpad + (ci * a.kh + dy) * a.kw + dx];
+                const std::vector<int8_t> w8r = dev::conv_w8r(a, w8, F);
                 a.w8r[j] = gg::dconst(w8r.data(), w8r.size());
             } else if (p <= 255) {
                 a.w8[j] = gg::dconst(w8.data(), w8.size());

@@ -331,7 +331,9 @@ __device__ __forceinline__ uint32_t modq_conv(uint32_t x, uint32_t q, uint32_t m
 #ifndef DASH_CONV_CLAMP
 #define DASH_CONV_CLAMP 1  // edge items of the band staging as clamped 8-B loads (0: byte-wise, A/B)
 #endif
-template <int KSC>
+// UR: tap-unrolled band (ConvArgs::ur), a separate instantiation so the channel-chunked staging keeps its
+// registers and code
+template <int KSC, bool UR>
 __global__ __launch_bounds__(256) void k_conv_img2(ConvArgs a, Act x, Act y, int B) {
     constexpr bool AREG = KSC > 0;
     extern __shared__ __attribute__((aligned(16))) int8_t img[];
@@ -349,8 +351,9 @@ __global__ __launch_bounds__(256) void k_conv_img2(ConvArgs a, Act x, Act y, int
     const int iy0 = oy0 * a.sh - a.ph;
     const int in_rows = (oy1 - oy0 - 1) * a.sh + a.kh;
     const int S = a.ldsS, R = a.ldsR, Wp = a.W + 2 * a.pw;
-    const int HW = a.H * a.W;
-    const act_t* X = x.p[j] + (static_cast<int64_t>(b) * n + c) * a.C * HW;
+    // the layer's input image (the unrolled view's a.C/H/W describe the staged band, not the input)
+    const int HW = UR ? a.uH * a.uW : a.H * a.W;
+    const act_t* X = x.p[j] + (static_cast<int64_t>(b) * n + c) * (UR ? a.uC : a.C) * HW;
     const int16_t zv = a.zero[static_cast<int64_t>(b) * a.lab_stride + a.lab_off[j] + c];
     const int zc8 = zv > half ? zv - p : zv;
     const int tid = threadIdx.x;
@@ -412,11 +415,63 @@ __global__ __launch_bounds__(256) void k_conv_img2(ConvArgs a, Act x, Act y, int
     // runtime divisions cost ~25 VALU each, 4 per item)
     const uint32_t mc4 = c4n > 1 ? 0xffffffffu / static_cast<uint32_t>(c4n) + 1u : 0u;
     const uint32_t mwo = WO > 1 ? 0xffffffffu / static_cast<uint32_t>(WO) + 1u : 0u;
+    // 8 operand bytes of one channel row (tap-unrolled staging): columns ix0 .. ix0 + 7 of `row` (width Wr)
+    auto fetch8 = [&](const act_t* row, bool rowin, int ix0, int Wr, uint32_t (&o)[2]) {
+        if (Wr >= 8) {
+            const int s0 = min(max(ix0, 0), Wr - 8);
+            const int sh = ix0 - s0;  // > 0: right edge, < 0: left padding
+            uint64_t t = 0;
+            if (rowin && sh > -8 && sh < 8) t = *reinterpret_cast<const uint64_t*>(row + s0);
+            t = sh >= 8 || sh <= -8 ? 0ull : (sh >= 0 ? t >> (8 * sh) : t << (-8 * sh));
+            const int lo = max(0, -ix0), hi = min(8, Wr - ix0);  // valid bytes [lo, hi)
+            uint64_t msk = 0;
+            if (rowin && hi > lo)
+                msk = (hi >= 8 ? ~0ull : (1ull << (8 * hi)) - 1ull) & ~((1ull << (8 * lo)) - 1ull);
+            const uint32_t t0 = static_cast<uint32_t>(t), t1 = static_cast<uint32_t>(t >> 32);
+            const uint64_t c = (static_cast<uint64_t>(rawx ? t1 : center4(t1)) << 32) | (rawx ? t0 : center4(t0));
+            const uint64_t padr = static_cast<uint64_t>(padb) * 0x0101010101010101ull;
+            const uint64_t v = (c & msk) | (padr & ~msk);
+            o[0] = static_cast<uint32_t>(v);
+            o[1] = static_cast<uint32_t>(v >> 32);
+        } else {
+            o[0] = o[1] = 0u;
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const int ix = ix0 + u;
+                uint32_t v = padb;
+                if (rowin && ix >= 0 && ix < Wr) {
+                    const int w = row[ix];
+                    v = static_cast<uint32_t>(rawx ? w : (w > half ? w - p : w)) & 0xffu;
+                }
+                o[u >> 2] |= v << (8 * (u & 3));
+            }
+        }
+    };
     auto load_item = [&](int it, uint32_t (&raw)[4][2], int& yq, int& xo, int& c4) {
         const int t2 = c4n > 1 ? static_cast<int>(__umulhi(static_cast<uint32_t>(it), mc4)) : it;
         c4 = it - t2 * c4n;
         yq = WO > 1 ? static_cast<int>(__umulhi(static_cast<uint32_t>(t2), mwo)) : t2;
         xo = t2 - yq * WO;
+        if constexpr (UR) {
+            // tap-unrolled band: channel cq of output position (row iy0 + yq, column xo * 8 + u) is input
+            // channel ci at (row * sh - ph + dy, column - pw + dx), cq = (dy * kw + dx) * C + ci (unit column
+            // stride: 8 consecutive input columns)
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int cq = c4 * 4 + q;
+                if (cq >= a.C) {
+                    raw[q][0] = raw[q][1] = 0u;
+                    continue;
+                }
+                const int tap = cq / a.uC, ci = cq - tap * a.uC;
+                const int dy = tap / a.ukw, dx = tap - dy * a.ukw;
+                const int iy = (iy0 + yq) * a.ush - a.uph + dy;
+                const bool rowin = iy >= 0 && iy < a.uH;
+                const act_t* row = X + static_cast<int64_t>(ci) * HW + static_cast<int64_t>(iy) * a.uW;
+                fetch8(row, rowin, xo * 8 - a.upw + dx, a.uW, raw[q]);
+            }
+            return;
+        }
         const int iy = iy0 + yq;
         const bool rowin = iy >= 0 && iy < a.H;
         const int ix0 = xo * 8 - a.pw;
@@ -642,14 +697,18 @@ void launch_conv(const ConvArgs& a, const Act& x, const Act& y, int B, hipStream
         const int KS = a.kh * a.kw * (a.Cpad / 64);
         if (ver == 1 && a.ldsS == a.Cpad + 16 && a.ldsR == (a.W + 2 * a.pw) * a.ldsS)
             hipLaunchKernelGGL(k_conv_img, g, dim3(256), lds, st, a, x, y, B);  // A/B: its fixed layout only
+        else if (a.ur && KS == 1)
+            hipLaunchKernelGGL((k_conv_img2<1, true>), g, dim3(256), lds, st, a, x, y, B);
+        else if (a.ur)
+            hipLaunchKernelGGL((k_conv_img2<0, true>), g, dim3(256), lds, st, a, x, y, B);
         else if (KS == 9)
-            hipLaunchKernelGGL(k_conv_img2<9>, g, dim3(256), lds, st, a, x, y, B);
+            hipLaunchKernelGGL((k_conv_img2<9, false>), g, dim3(256), lds, st, a, x, y, B);
         else if (KS == 4)
-            hipLaunchKernelGGL(k_conv_img2<4>, g, dim3(256), lds, st, a, x, y, B);
+            hipLaunchKernelGGL((k_conv_img2<4, false>), g, dim3(256), lds, st, a, x, y, B);
         else if (KS == 1)
-            hipLaunchKernelGGL(k_conv_img2<1>, g, dim3(256), lds, st, a, x, y, B);
+            hipLaunchKernelGGL((k_conv_img2<1, false>), g, dim3(256), lds, st, a, x, y, B);
         else
-            hipLaunchKernelGGL(k_conv_img2<0>, g, dim3(256), lds, st, a, x, y, B);
+            hipLaunchKernelGGL((k_conv_img2<0, false>), g, dim3(256), lds, st, a, x, y, B);
         bool rest = false;
         for (int j = 0; j < a.crt.k; ++j) rest |= (a.w8r[j] == nullptr);
         if (!rest) return;

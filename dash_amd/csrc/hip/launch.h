@@ -91,6 +91,11 @@ struct ConvArgs {
     int64_t img_off[kMaxRes + 1];  // first image index of residue j: B * sum_{i<j} n_i
     uint32_t mq[kMaxRes];          // floor(2^32 / p_j): reciprocal for the epilogue's mod p (conv_img_geometry)
     int ldsS = 0, ldsR = 0;        // LDS image: bytes per position and per input row (conv_img_geometry)
+    // tap-unrolled image (conv_unroll_taps): the band is staged per OUTPUT position with the C*kh*kw patch
+    // bytes as its channels, the MFMA phase then runs a 1x1 conv (one k-step instead of kh*kw for C << 64).
+    // u* hold the layer's own geometry for the staging; the fields above describe the unrolled view.
+    int ur = 0;
+    int uC = 0, uH = 0, uW = 0, ukh = 0, ukw = 0, ush = 0, usw = 0, uph = 0, upw = 0;
 };
 void launch_conv(const ConvArgs& a, const Act& x, const Act& y, int B, hipStream_t st);
 
@@ -188,6 +193,43 @@ inline void conv_img_geometry(ConvArgs& a) {
     }
     std::lock_guard<std::mutex> lk(mu);
     memo[key] = ConvGeomPick{a.ldsS, a.ldsR, a.band, a.nbands};
+}
+
+// Switch a layer to the tap-unrolled image when that cuts the MFMA k-steps (few input channels, e.g. the
+// RGB first layer: 3x3x3 = 27 patch bytes in one 64-wide k-step instead of 9 steps of 3 real channels each)
+// and every residue takes the int8 MFMA path. Unit column stride only (the staging's 8-column loads).
+// Call before conv_img_geometry; the caller lays out w8r with conv_w8r.
+inline void conv_unroll_taps(ConvArgs& a, int max_p) {
+    const int K = a.C * a.kh * a.kw;
+    const int steps = a.kh * a.kw * ((a.C + 63) / 64), usteps = (K + 63) / 64;
+    const bool ok = [] {
+        const char* e = std::getenv("DASH_CONV_UNROLL");
+        return !(e && e[0] == '0');
+    }();
+    if (!ok || a.ur || a.sw != 1 || max_p > 255 || usteps >= steps || a.uW != 0) return;
+    a.ur = 1;
+    a.uC = a.C; a.uH = a.H; a.uW = a.W; a.ukh = a.kh; a.ukw = a.kw;
+    a.ush = a.sh; a.usw = a.sw; a.uph = a.ph; a.upw = a.pw;
+    a.C = K; a.H = a.OH; a.W = a.OW;
+    a.kh = a.kw = a.sh = a.sw = 1;
+    a.ph = a.pw = 0;
+}
+
+// MFMA weight image [F16][kh][kw][Cpad] from the centered im2col weights w8 [F][Kpad] (order ci*kh*kw + dy*kw
+// + dx); tap-unrolled layers: [F16][Cpad] with patch channel (dy*kw + dx)*C + ci (the staging's order)
+inline std::vector<int8_t> conv_w8r(const ConvArgs& a, const std::vector<int8_t>& w8, int F) {
+    const int F16 = (F + 15) / 16 * 16;
+    const int C = a.ur ? a.uC : a.C, kh = a.ur ? a.ukh : a.kh, kw = a.ur ? a.ukw : a.kw;
+    std::vector<int8_t> r(static_cast<size_t>(F16) * a.kh * a.kw * a.Cpad, 0);
+    for (int f = 0; f < F; ++f)
+        for (int ci = 0; ci < C; ++ci)
+            for (int dy = 0; dy < kh; ++dy)
+                for (int dx = 0; dx < kw; ++dx) {
+                    const size_t dst = a.ur ? static_cast<size_t>(f) * a.Cpad + (dy * kw + dx) * C + ci
+                                            : ((static_cast<size_t>(f) * kh + dy) * kw + dx) * a.Cpad + ci;
+                    r[dst] = w8[static_cast<size_t>(f) * a.Kpad + (ci * kh + dy) * kw + dx];
+                }
+    return r;
 }
 
 // int16 matrix transpose out[c][r] = in[r][c] (label-major <-> component-major), kernels_label.hip

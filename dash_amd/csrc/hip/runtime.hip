@@ -634,12 +634,15 @@ void HipEvaluator::build() {
                         const char* e = std::getenv("DASH_CONV_IMG");
                         return !(e && e[0] == '0');
                     }();
+                    int max_p = 0;
+                    for (int j = 0; j < k_; ++j) max_p = std::max(max_p, crt_[j]);
+                    if (mfma_ && img_ok) conv_unroll_taps(a, max_p);
                     conv_img_geometry(a);
                     if (!(mfma_ && img_ok)) a.band = a.nbands = 0;
+                    DASH_CHECK(!a.ur || a.nbands > 0, "tap-unrolled conv without an LDS band");
                 }
                 a.img_off[0] = 0;
                 for (int j = 0; j < k_; ++j) a.img_off[j + 1] = a.img_off[j] + static_cast<i64>(B_) * crt.n[j];
-                const i64 F16 = (G.F + 15) / 16 * 16;
                 const Array& w = g.arr("w");
                 for (int j = 0; j < k_; ++j) {
                     const int p = crt_[j];
@@ -657,13 +660,7 @@ void HipEvaluator::build() {
                     a.w8[j] = (mfma_ && p <= 255) ? upload(w8.data(), w8.size()) : nullptr;
                     if (a.nbands > 0 && p <= 255) {
                         // [F16][kh][kw][Cpad] centered int8 (im2col order ci*kh*kw + dy*kw + dx -> (dy, dx, ci))
-                        std::vector<int8_t> w8r(static_cast<size_t>(F16) * G.kh * G.kw * a.Cpad, 0);
-                        for (i64 f = 0; f < G.F; ++f)
-                            for (i64 ci = 0; ci < G.C; ++ci)
-                                for (i64 dy = 0; dy < G.kh; ++dy)
-                                    for (i64 dx = 0; dx < G.kw; ++dx)
-                                        w8r[((f * G.kh + dy) * G.kw + dx) * a.Cpad + ci] =
-                                            w8[f * a.Kpad + (ci * G.kh + dy) * G.kw + dx];
+                        const std::vector<int8_t> w8r = conv_w8r(a, w8, static_cast<int>(G.F));
                         a.w8r[j] = upload(w8r.data(), w8r.size());
                     } else {
                         a.w8r[j] = nullptr;

@@ -74,15 +74,17 @@ def test_conv(mfma):
     _check(c, 9, None, xs, mfma=mfma)
 
 
-@pytest.mark.parametrize("W,H,k,s,pad", [(30, 6, 3, 1, 0), (13, 5, 3, 1, 1), (8, 4, 3, 1, 0), (16, 6, 5, 1, 2),
-                                         (21, 7, 2, 2, 0), (11, 5, 3, 2, 1)])
-def test_conv_band_edges(W, H, k, s, pad):
+@pytest.mark.parametrize("W,H,C,k,sw,sh,pad", [(30, 6, 5, 3, 1, 1, 0), (13, 5, 5, 3, 1, 1, 1), (8, 4, 5, 3, 1, 1, 0),
+                                               (16, 6, 5, 5, 1, 1, 2), (21, 7, 5, 2, 2, 2, 0), (11, 5, 5, 3, 2, 2, 1),
+                                               (12, 9, 3, 3, 1, 2, 1), (10, 6, 70, 3, 1, 1, 1)])
+def test_conv_band_edges(W, H, C, k, sw, sh, pad):
     """Band staging of the MFMA conv: rows whose width is not a multiple of 8 (edge items as clamped loads),
-    left/right padding, strides; labels bit-exact against the host evaluator."""
+    left/right padding, strides; few input channels take the tap-unrolled image (C * k * k <= 64 patch bytes as
+    the channels of one 1x1 k-step), C = 70 the channel-chunked image. Labels bit-exact against the host."""
     rng = np.random.default_rng(W * 100 + H)
-    C, F = 5, 6
+    F = 6
     Wt = rng.integers(-5, 6, (F, C, k, k)); b = rng.integers(-5, 6, F)
-    c = d.Circuit([d.Conv2d.from_quantized(Wt, b, W, H, C, F, k, k, s, s, pad_width=pad, pad_height=pad)])
+    c = d.Circuit([d.Conv2d.from_quantized(Wt, b, W, H, C, F, k, k, sw, sh, pad_width=pad, pad_height=pad)])
     xs = [rng.integers(-6, 7, C * H * W) for _ in range(2)]
     _check(c, 7, None, xs)
 
