@@ -706,6 +706,9 @@ __device__ __forceinline__ u128 add_packed(u128 a, u128 b, u128 hmask) {
 #define DASH_MRS_CHUNK 8
 #endif
 constexpr int kMrsChunk = DASH_MRS_CHUNK;
+#ifndef DASH_MRS_M2CH
+#define DASH_MRS_M2CH 16  // components per load batch of the mod-2 key (modes 1, 2)
+#endif
 template <int K>
 __device__ __forceinline__ constexpr int mrs_pair(int l, int j) {  // l < j < K
     return l * (2 * K - l - 1) / 2 + (j - l - 1);
@@ -718,8 +721,11 @@ __device__ __forceinline__ constexpr int mrs_pair(int l, int j) {  // l < j < K
 // MODE 2 (joint rescale + ReLU sign, RescaleMrsPlan::sign_last): MODE 1's
 // order with MODE 0's T target on every row (the mod-2 position's row has only
 // that one) and final row; the mod-2 key's hash and color go to hs / cs.
+#ifndef DASH_CHAIN2_WAVES
+#define DASH_CHAIN2_WAVES 4  // mode 2 (joint rescale + sign) register budget in waves per SIMD
+#endif
 template <int K, int MODE>
-__global__ __launch_bounds__(kAesBlock, DASH_UA_MINBLOCKS) void k_mrs_chain(MrsArgs a, Act x, const ModC* mc,
+__global__ __launch_bounds__(kAesBlock, MODE == 2 ? DASH_CHAIN2_WAVES : DASH_UA_MINBLOCKS) void k_mrs_chain(MrsArgs a, Act x, const ModC* mc,
                                                                           const uint32_t* te0, const uint32_t* rk) {
     AES_PROLOGUE(te0, rk);
     const int b = blockIdx.z;
@@ -731,25 +737,11 @@ __global__ __launch_bounds__(kAesBlock, DASH_UA_MINBLOCKS) void k_mrs_chain(MrsA
         u128* PS = a.ps + static_cast<int64_t>(b) * NP * N + e;
         u128 acc = 0;
 #pragma unroll
-        for (int i = 0; i < K; ++i) {
+        for (int i = 0; i < (MODE >= 1 ? K - 1 : K); ++i) {
             const int r = MODE >= 1 ? (i + 1) % K : i;  // residue converted at position i
             const ModC m = mc[a.crt.p[r]];
             const int n = static_cast<int>(m.n);
             const act_t* L = x.p[r] + static_cast<int64_t>(b) * n * N + e;
-            if (MODE >= 1 && i == K - 1) {
-                // residue 0 (mod 2): compress = bit pack, subtraction = XOR
-                u128 key = compress_cm(L, N, m);
-#pragma unroll
-                for (int l = 0; l < K - 1; ++l) key ^= PS[static_cast<int64_t>(mrs_pair<K>(l, K - 1)) * N];
-                const uint32_t c = static_cast<uint32_t>(key) & 1u;
-                u128 E = 0;
-                if (MODE == 2) E = row0[a.dig_off[K - 1] + c];  // the sign digit's T payload row (one entry)
-                const u128 H = aes_encrypt(aes, key);
-                a.hs[static_cast<int64_t>(b) * N + e] = H;
-                a.cs[static_cast<int64_t>(b) * N + e] = static_cast<uint8_t>(c);
-                if (MODE == 2) acc = add_packed(acc, E - H, a.hmask);
-                break;
-            }
             DigitStream ds[K > 1 ? K - 1 : 1];
 #pragma unroll
             for (int l = 0; l < i; ++l) ds[l].init(PS[static_cast<int64_t>(mrs_pair<K>(l, i)) * N]);
@@ -789,6 +781,21 @@ __global__ __launch_bounds__(kAesBlock, DASH_UA_MINBLOCKS) void k_mrs_chain(MrsA
 #pragma unroll
             for (int t = 0; t < K - 1 - i; ++t) PS[static_cast<int64_t>(mrs_pair<K>(i, i + 1 + t)) * N] = E[t] - H;
             if (MODE != 1) acc = add_packed(acc, E[K - 1 - i] - H, a.hmask);
+        }
+        if (MODE >= 1) {
+            // last position: residue 0 (mod 2): compress = bit pack, subtraction = XOR
+            const ModC m = mc[a.crt.p[0]];
+            const act_t* L = x.p[0] + static_cast<int64_t>(b) * m.n * N + e;
+            u128 key = compress_cm<DASH_MRS_M2CH>(L, N, m);
+#pragma unroll
+            for (int l = 0; l < K - 1; ++l) key ^= PS[static_cast<int64_t>(mrs_pair<K>(l, K - 1)) * N];
+            const uint32_t c = static_cast<uint32_t>(key) & 1u;
+            u128 E = 0;
+            if (MODE == 2) E = row0[a.dig_off[K - 1] + c];  // the sign digit's T payload row (one entry)
+            const u128 H = aes_encrypt(aes, key);
+            a.hs[static_cast<int64_t>(b) * N + e] = H;
+            a.cs[static_cast<int64_t>(b) * N + e] = static_cast<uint8_t>(c);
+            if (MODE == 2) acc = add_packed(acc, E - H, a.hmask);
         }
         if (MODE == 1) continue;
         const uint32_t col = static_cast<uint32_t>(acc) & static_cast<uint32_t>(a.T - 1);
@@ -898,7 +905,10 @@ __global__ __launch_bounds__(kAesBlock, kAesMinBlocks) void k_rescale_mrs_out_ha
 // place), its hash -> the garbler half gate G = g[color(Y_j)] - H(Y_j) (gathered as soon as the first
 // component is known), then relu_j = E + ypr * Y_j - G (k_relu_mult's arithmetic) streamed into y while Y_j
 // is read back from the lines this lane just wrote. The sign's hash / color come from chain MODE 2.
-__global__ __launch_bounds__(kAesBlock, kAesMinBlocks) void k_rescale_relu_out(MrsArgs a, SignArgs sa, Act x, Act y,
+#ifndef DASH_RRO_WAVES
+#define DASH_RRO_WAVES 4  // k_rescale_relu_out register budget (waves per SIMD): 6 spilled 256 B per lane
+#endif
+__global__ __launch_bounds__(kAesBlock, DASH_RRO_WAVES) void k_rescale_relu_out(MrsArgs a, SignArgs sa, Act x, Act y,
                                                                               const u128* gtab, const u128* etab,
                                                                               const ModC* mc, const uint32_t* te0,
                                                                               const uint32_t* rk) {
