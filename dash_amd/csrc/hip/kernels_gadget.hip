@@ -703,7 +703,7 @@ __device__ __forceinline__ u128 add_packed(u128 a, u128 b, u128 hmask) {
 // (a.ps, [B][pair][N], coalesced) and are read back when digit j starts:
 // holding them in registers (up to K(K-1)/2 u128) spilled.
 #ifndef DASH_MRS_CHUNK
-#define DASH_MRS_CHUNK 8
+#define DASH_MRS_CHUNK 4  // 8: mode-2 chain spilled 84 B/lane, 4: 28 (mode 0: 52 -> 0); 24 GCs 13.07 -> 12.96 ms
 #endif
 constexpr int kMrsChunk = DASH_MRS_CHUNK;
 #ifndef DASH_MRS_M2CH
