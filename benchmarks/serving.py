@@ -32,7 +32,7 @@ def main() -> None:
     ap.add_argument("--faults", type=float, default=0.0)
     ap.add_argument("--timeout", type=float, default=120.0)
     ap.add_argument("--rescale", default="mrs", choices=["mrs", "legacy"])
-    ap.add_argument("--relu", default="approx", choices=["mrs", "approx", "joint"])
+    ap.add_argument("--relu", default="joint", choices=["mrs", "approx", "joint"])
     args = ap.parse_args()
 
     from dash_amd.ir.quant import QuantizationMethod

@@ -187,7 +187,7 @@ class InferenceService:
                  backend: str = "hip", device: int = 0, garble_device: Optional[bool] = None, max_retries: int = 2,
                  step_timeout_s: float = 120.0, seed: Optional[bytes] = None, prefetch: bool = True,
                  fault_hook: Optional[Callable[[int, int], bool]] = None, nthreads: int = 0,
-                 rescale: str = "mrs", relu: str = "approx", fused_sign: bool = True):
+                 rescale: str = "mrs", relu: str = "joint", fused_sign: bool = True):
         if backend not in ("hip", "cpu"):
             raise ValueError("backend must be 'hip' or 'cpu'")
         if backend == "hip" and native().hip_device_count() == 0:
