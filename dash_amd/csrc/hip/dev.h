@@ -202,7 +202,7 @@ struct CompressFwd {
 // (the compiler does not hoist loads across a runtime-trip-count loop, nor
 // past a store to the same column): stage kChunk loads first, then consume.
 #ifndef DASH_KCHUNK
-#define DASH_KCHUNK 16
+#define DASH_KCHUNK 8  // 24 GCs: 16 -> 12.96, 8 -> 12.39, 32 -> 19.44 ms per step (profiles/ab/kchunk*.json)
 #endif
 constexpr int kChunk = DASH_KCHUNK;
 
