@@ -1,278 +1,23 @@
 #!/usr/bin/env python
 """Headline benchmark: online garbled inferences/sec for the MiniONN-style
-CIFAR-10 CNN (MODEL_F_MINIONN_POOL_REPL, DASH legacy config: ScaleQuant l=5,
-k=7 CRT base {2..17}, ReLU accuracy 100 % -> MRS {86,7,6,6,5}).
+CIFAR-10 CNN (MODEL_F_MINIONN_POOL_REPL, DASH config: ScaleQuant l=5, k=7 CRT
+base {2..17}, ReLU accuracy 100 %).
 
-Timed region per step (the reference's GPU model benchmark,
-benchmarks/model_benchmarks/sgx/Enclave/Enclave.cpp:177-183):
-    garble_inputs -> H2D -> evaluate -> D2H -> decode_outputs
-for B independent garbled circuits per GPU (one fresh input per GC per step).
-Offline garbling and the table upload are excluded, as in the reference, and
-reported separately. The B GCs are garbled once and re-encoded every step: with
-garbling and upload outside the timed region, a step's work (encode, H2D,
-evaluate, D2H, decode for B inferences) is the same as on fresh GCs
-(benchmarks/serving.py measures the fresh-GC-per-inference service instead).
-Groups are encoded and launched one after the other: the staggered starts
-measured faster (375 inf/s) than encoding the next step ahead and launching
-all groups at once (360). Data: synthetic CIFAR-shaped normalized images, random
-(PyTorch-default) initialised weights.
+    python bench.py --gpus N --steps K --warmup W
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
 
-Multi-GPU: one process per GPU (torchrun), batch data parallel; every rank
-garbles and evaluates its own GCs; decoded logits are all-gathered over RCCL.
+Prints one JSON line (rank 0). The driver, timed region, phases (headline,
+reference constructions, fresh-GC serving) and the multi-rank evidence live in
+dash_amd/benchcore.py, which the multi-rank CPU tests run as well.
 """
 from __future__ import annotations
 
-import argparse
-import hashlib
-import json
 import os
 import sys
-import time
 
-import numpy as np
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
-BASELINE_INF_PER_S = 1000.0 / 1443.0  # RTX 4090, DASH GPU, MiniONN
-
-
-def log(*a):
-    print(f"[bench {time.strftime('%H:%M:%S')}]", *a, file=sys.stderr, flush=True)
-
-
-def main() -> None:
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=5)
-    ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--batch", type=int, default=int(os.environ.get("DASH_BENCH_BATCH", "0")),
-                    help="garbled circuits evaluated together per GPU (0: as many as HBM holds, a multiple of "
-                         "--streams)")
-    ap.add_argument("--sign", default=os.environ.get("DASH_BENCH_SIGN", "fused"), choices=["fused", "reference"],
-                    help="sign-gadget construction: casts folded into the approx/carry projections (fused) or the "
-                         "reference's explicit cast gates; both compute the same function")
-    ap.add_argument("--rescale", default=os.environ.get("DASH_BENCH_RESCALE", "mrs"), choices=["mrs", "legacy"],
-                    help="construction of the DASH rescale ceil(x/2^l): one exact mixed-radix conversion (mrs) or the "
-                         "reference's l sign-gadget halvings (legacy); same function on the signed range")
-    ap.add_argument("--relu", default=os.environ.get("DASH_BENCH_RELU", "joint"), choices=["mrs", "approx", "joint"],
-                    help="sign of the ReLU: taken from the preceding mixed-radix rescale's conversion where a ReLU "
-                         "follows a rescale, else the approximate gadget (joint); exact mixed-radix conversion "
-                         "(mrs); or the reference's approximate sign gadget at 100 %% accuracy (approx)")
-    ap.add_argument("--streams", type=int, default=int(os.environ.get("DASH_BENCH_STREAMS", "4")),
-                    help="independent GC groups per GPU, each on its own HIP stream (overlap latency- and "
-                         "bandwidth-bound phases)")
-    ap.add_argument("--model", default="MODEL_F_MINIONN_POOL_REPL")
-    ap.add_argument("--config", default="DASH", choices=["DASH", "REDASH_OPT", "REDASH_CPM"])
-    ap.add_argument("--no-mfma", action="store_true")
-    ap.add_argument("--profile", action="store_true", help="print per-layer GPU times")
-    ap.add_argument("--threads", type=int, default=0)
-    ap.add_argument("--verify", type=int, default=1)
-    ap.add_argument("--garble-device", type=int, default=int(os.environ.get("DASH_BENCH_GARBLE_DEVICE", "1")),
-                    help="garble the sign-gadget layers on this rank's GPU (byte-identical to the host garbler; "
-                         "keeps the offline phase off the shared host CPUs when 8 ranks garble at once)")
-    args = ap.parse_args()
-
-    import torch
-
-    from dash_amd.garbling import GarbledCircuit
-    from dash_amd.ir.quant import QuantizationMethod
-    from dash_amd.models import BENCH_CONFIGS, build_circuit, canonical, quantized_inputs
-    from dash_amd.native import native
-    from dash_amd.runtime import HipEvaluator
-
-    from dash_amd.parallel import all_gather_array, all_reduce_max, barrier, init_distributed, shutdown
-
-    # one process per GPU (torchrun); backend nccl (= RCCL over xGMI). DASH_DIST_BACKEND=gloo and a
-    # device count smaller than the world size are only for rehearsing the multi-rank path on one GPU.
-    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-    if int(os.environ.get("WORLD_SIZE", "1")) > 1 and torch.cuda.device_count() < int(os.environ["WORLD_SIZE"]):
-        os.environ["LOCAL_RANK"] = str(int(os.environ.get("LOCAL_RANK", "0")) % max(1, torch.cuda.device_count()))
-    ctx = init_distributed(backend=os.environ.get("DASH_DIST_BACKEND") or None, use_gpu=True)
-    world, rank, dist = ctx.world, ctx.rank, ctx.distributed
-    device = torch.cuda.current_device()
-    if args.threads:
-        native().set_num_threads(args.threads)
-
-    model = canonical(args.model)
-    cfg = BENCH_CONFIGS.get(f"{model}/{args.config}") or BENCH_CONFIGS["MODEL_F_MINIONN_POOL_REPL/DASH"]
-    qm, qp = QuantizationMethod(cfg["q_method"]), cfg["q_parameter"]
-    circuit = build_circuit(model, qm, qp, seed=0)  # public model, identical on every rank
-    B = args.batch if args.batch > 0 else 256  # auto: upper bound, sized from HBM after the first GC
-    G = max(1, min(args.streams, B))
-    B -= B % G
-
-    # ---------------- offline: garble B circuits, stream them into HBM
-    t_off = time.perf_counter()
-    assert B % G == 0, "--batch must be a multiple of --streams"
-    per = B // G
-    gcs = []
-    evs = [None] * G
-    garble_s = 0.0
-    upload_s = 0.0
-    free0 = torch.cuda.mem_get_info(device)[0]
-    b = 0
-    def offline_one(b: int):
-        """Garble GC b (on this rank's GPU) and stream it into its evaluator slot."""
-        nonlocal B, per, garble_s, upload_s
-        seed = hashlib.sha256(f"dash-bench/{rank}/{b}/{os.getpid()}".encode()).digest()[:16]
-        t = time.perf_counter()
-        gc = GarbledCircuit(circuit, cfg["crt"], cfg["mrs"], seed=seed, device=device if args.garble_device else None,
-                            fused_sign=args.sign == "fused", rescale=args.rescale, relu=args.relu)
-        garble_s += time.perf_counter() - t
-        if b == 0:
-            # HBM guard: every GC's tables stay resident. Size B from the real device footprint of one GC
-            # (tables + evaluator scratch) plus one GC in flight in the garbler; --batch 0 fills HBM, an explicit
-            # batch shrinks to a multiple of the stream groups if this device cannot hold it.
-            probe = HipEvaluator(template=gc.model, batch=1, device=device, mfma=not args.no_mfma)
-            per_gc = probe.device_bytes() * 1.01
-            del probe
-            fit = int((free0 - gc.table_bytes - 2.5e9) // per_gc)
-            log(f"rank {rank}: {free0 / 1e9:.1f} GB HBM free, {per_gc / 1e9:.2f} GB per GC "
-                f"({gc.table_bytes / 1e9:.2f} GB tables): fits {fit}")
-            if fit < B:
-                B = max(G, fit - fit % G)
-                log(f"rank {rank}: batch {'sized' if args.batch <= 0 else 'reduced'} to {B}")
-            B = int(-all_reduce_max(ctx, -float(B)))  # every rank evaluates the same number of GCs
-            per = B // G
-            evs[0] = HipEvaluator(template=gc.model, batch=per, device=device, mfma=not args.no_mfma,
-                                  profile=args.profile)
-        t = time.perf_counter()
-        g = b // per
-        if evs[g] is None:
-            native().gpu_table_cache_trim()  # the new group's table arena needs the garbler's cached blocks
-            evs[g] = HipEvaluator(template=gc.model, batch=per, device=device, mfma=not args.no_mfma,
-                                  profile=args.profile)
-        evs[g].load(b % per, gc.model)
-        upload_s += time.perf_counter() - t
-        tgb = gc.table_bytes / 1e9
-        gc.model = None  # host copy no longer needed (tables live in HBM)
-        gcs.append(gc)
-        log(f"rank {rank}: garbled+uploaded GC {b + 1}/{B} ({tgb:.2f} GB tables)")
-        return tgb
-
-    b = 0
-    table_gb = 0.0
-    while b < B:
-        try:
-            table_gb = offline_one(b)
-        except RuntimeError as e:
-            # HBM ran out before the estimate said it would (allocator fragmentation near full memory): keep the
-            # complete groups only
-            if "out of memory" not in str(e) or b < per:
-                raise
-            G = b // per
-            B = G * per
-            del evs[G:]
-            del gcs[B:]
-            native().gpu_table_cache_trim()
-            native().hip_clear_last_error()  # the handled OOM must not resurface in the next launch check
-            log(f"rank {rank}: out of HBM at GC {b + 1}: continuing with {G} groups, batch {B}")
-            break
-        b += 1
-    offline_s = time.perf_counter() - t_off
-    native().gpu_table_cache_trim()  # the garbler's recycled table blocks are no longer needed
-    free_b, total_b = torch.cuda.mem_get_info(device)
-    n_inputs = B * (args.steps + args.warmup)
-    inputs = quantized_inputs(model, n_inputs, qm, qp, seed=1000 + rank)
-
-    # group 0 on the current stream, the others on torch pool streams (measured best on MI355X:
-    # 313 inf/s at B=24 vs 295 with one dedicated non-blocking HIP stream per group, which runs all
-    # groups fully concurrently and over-subscribes caches); DASH_BENCH_TORCH_STREAMS=0 -> dedicated
-    if os.environ.get("DASH_BENCH_TORCH_STREAMS", "1") == "1":
-        streams = [torch.cuda.current_stream()] + [torch.cuda.Stream() for _ in range(G - 1)]
-    else:
-        streams = [native().hip_stream_create(0) for _ in range(G)]
-
-    def step(i: int, verify: bool = False):
-        xs = inputs[i * B:(i + 1) * B]
-        # online message #1 in wire form (16-B compressed labels) -> pinned staging -> H2D -> GPU unpack;
-        # the G groups run concurrently on their own streams
-        for g, (ev, st) in enumerate(zip(evs, streams)):
-            for b in range(per):
-                ev.encode_compressed_into(b, gcs[g * per + b], xs[g * per + b])
-            ev.upload_inputs_compressed(st)
-            ev.run(st)
-        dec = []
-        for g, (ev, st) in enumerate(zip(evs, streams)):
-            ev.fetch_outputs(st)  # online message #2 (synchronizes this group's stream)
-            dec += [ev.decode(b, gcs[g * per + b]) for b in range(per)]
-        if verify:
-            for gc, x, y in zip(gcs, xs, dec):
-                ref = gc.plain_q_eval(x)
-                if not np.array_equal(ref, y):
-                    raise RuntimeError(f"garbled output mismatch: {y} vs {ref}")
-        return dec
-
-    verified = False
-    for w in range(args.warmup):
-        step(w, verify=bool(args.verify) and w == 0)
-        verified = verified or bool(args.verify)
-    torch.cuda.synchronize()
-    barrier(ctx)
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    last = None
-    for s in range(args.steps):
-        last = step(args.warmup + s)
-    torch.cuda.synchronize()
-    barrier(ctx)
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
-
-    elapsed = all_reduce_max(ctx, elapsed)  # slowest rank defines the step time
-    # decoded logits of the last step onto every rank (RCCL all-gather over xGMI)
-    gathered = all_gather_array(ctx, np.stack(last))
-    assert gathered.shape[0] == world
-
-    total_inf = world * B * args.steps
-    value = total_inf / elapsed
-    ms_step = 1000.0 * elapsed / args.steps
-    prof = op_ms = None
-    if args.profile:
-        step(0)
-        prof = {k: round(v, 3) for k, v in evs[0].layer_times().items()}
-        op_ms = [[n, round(v, 4)] for n, v in evs[0].op_times()]
-    if rank == 0:
-        out = {
-            "metric": ("online garbled inferences/sec (MiniONN CIFAR-10 CNN)" if model == "MODEL_F_MINIONN_POOL_REPL"
-                       else f"online garbled inferences/sec ({model})"),
-            "value": round(value, 3),
-            "unit": "inferences/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": round(ms_step, 3),
-            "ms_per_inference": round(1000.0 * elapsed / (B * args.steps), 3),
-            "latency_ms_per_batch": round(ms_step, 3),
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": round(value / BASELINE_INF_PER_S, 2),
-            "dtype": "uint8 label components / int8 MFMA (exact modular arithmetic)",
-            "data": "synthetic CIFAR-10-shaped inputs, random-init weights",
-            "config": {
-                "model": model,
-                "scheme": args.config,
-                "crt_base": cfg["crt"] if isinstance(cfg["crt"], list) else native().first_primes(cfg["crt"]),
-                "mrs": cfg["mrs"],
-                "global_batch": world * B,
-                "gcs_per_gpu": B,
-                "streams": G,
-                "sign_construction": args.sign,
-                "rescale_construction": args.rescale,
-                "relu_construction": args.relu,
-                "seq_len": None,
-                "input_shape": [3, 32, 32],
-                "parallelism": f"dp{world}",
-            },
-            "offline": {"garble_s_per_gc": round(garble_s / B, 2), "upload_s_per_gc": round(upload_s / B, 2),
-                        "table_gb_per_gc": round(table_gb, 3), "offline_total_s": round(offline_s, 1)},
-            "hbm_gb": {"used": round((total_b - free_b) / 1e9, 1), "total": round(total_b / 1e9, 1)},
-            "verified_vs_plaintext": verified,
-        }
-        if prof:
-            out["layer_ms"] = prof
-            out["op_ms"] = op_ms
-        print(json.dumps(out), flush=True)
-    shutdown(ctx)
-
+from dash_amd.benchcore import main  # noqa: E402
 
 if __name__ == "__main__":
     main()

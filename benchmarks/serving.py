@@ -44,6 +44,11 @@ def main() -> None:
                                                               crt=8, mrs=100.0)
     qm, qp = QuantizationMethod(cfg["q_method"]), cfg["q_parameter"]
     circuit = build_circuit(model, qm, qp, seed=0)
+    from dash_amd.ir.bases import crt_modulus as _cm, first_primes as _fp
+
+    # range calibration arms the mixed-radix rescale's wrap-band guard (GarbledCircuit refuses a tracked violation)
+    circuit.calibrate(quantized_inputs(model, 32, qm, qp, seed=0),
+                      _cm(cfg["crt"] if isinstance(cfg["crt"], list) else _fp(cfg["crt"])))
     xs = quantized_inputs(model, args.slots * args.requests, qm, qp, seed=11)
     rng = random.Random(5)
     hook = (lambda i, a: a == 0 and rng.random() < args.faults) if args.faults > 0 else None

@@ -125,7 +125,7 @@ def cmd_run_service(args):
     with InferenceService(circuit, crt, mrs, max_modulus=mm, slots_per_group=max(1, cfg.batch), groups=cfg.groups,
                           backend=cfg.backend, device=cfg.device, garble_device=cfg.garble_device,
                           max_retries=cfg.max_retries, step_timeout_s=cfg.step_timeout_s, seed=cfg.seed_bytes(),
-                          nthreads=cfg.nthreads, **cfg.gc_kwargs()) as svc:
+                          nthreads=cfg.nthreads, insecure_fixed_seed=cfg.insecure_fixed_seed, **cfg.gc_kwargs()) as svc:
         ys = svc.infer(xq)
         stats = svc.stats.as_dict()
     preds = [int(np.argmax(y)) for y in ys]

@@ -1,0 +1,540 @@
+"""Headline benchmark engine (bench.py and the multi-rank tests share it).
+
+Metric: online garbled inferences/sec for the MiniONN-style CIFAR-10 CNN
+(MODEL_F_MINIONN_POOL_REPL, DASH config: ScaleQuant l=5, k=7 CRT base {2..17},
+ReLU accuracy 100 % -> MRS {86,7,6,6,5}), BASELINE.json.
+
+Timed region per step (the reference's GPU model benchmark,
+benchmarks/model_benchmarks/sgx/Enclave/Enclave.cpp:177-183):
+    garble_inputs -> H2D -> evaluate -> D2H -> decode_outputs
+for B independent garbled circuits per GPU (one fresh input per GC per step).
+Offline garbling and the table upload are excluded, as in the reference, and
+reported separately. The B GCs of the online phase are garbled once and
+re-encoded every step; a step's work (encode, H2D, evaluate, D2H, decode for B
+inferences) is the same as on fresh GCs. Two further phases run after the
+timed loop and are reported beside the headline, never instead of it:
+
+* ``reference``: the same loop with the reference's gadget constructions
+  (legacy l-fold sign-base-extension rescale rescale_gadget.h:115-242,
+  approximate-sign ReLU garbled_relu.h:119-179, explicit cast gates
+  sign_gadget.h:456-546) -> ``reference_constructions_value``;
+* ``served``: fresh GC per inference (GCs are single use), offline garbling
+  pipelined against online evaluation (dash_amd.serving.InferenceService)
+  -> ``served_inf_per_s``, garbling included.
+
+Multi-GPU: one process per GPU (torchrun), batch data parallel; every rank
+garbles and evaluates its own GCs; the slowest rank defines the step time;
+per-rank records (device, PCI bus id, ms/step, host encode+decode time) are
+all-gathered over the job's process group (RCCL) and printed by rank 0.
+
+``--backend cpu`` runs the identical driver on the native host evaluator
+(tests: gloo, world 2/4, no GPU).
+"""
+from __future__ import annotations
+
+import argparse
+import hashlib
+import json
+import os
+import socket
+import sys
+import time
+from typing import List, Optional
+
+import numpy as np
+
+BASELINE_INF_PER_S = 1000.0 / 1443.0  # RTX 4090, DASH GPU, MiniONN
+
+CONSTRUCTIONS = {
+    # the framework's fastest exact-on-the-guarded-range constructions (headline)
+    "flagship": dict(sign="fused", rescale="mrs", relu="joint"),
+    # the reference's constructions
+    "reference": dict(sign="reference", rescale="legacy", relu="approx"),
+}
+
+
+def log(*a):
+    print(f"[bench {time.strftime('%H:%M:%S')}]", *a, file=sys.stderr, flush=True)
+
+
+def host_thread_budget(requested: int = 0) -> int:
+    """Host worker threads per rank: the rank's share of the visible CPUs
+    (cores / ranks on this node), capped by OMP_NUM_THREADS when set."""
+    if requested > 0:
+        return requested
+    try:
+        ncpu = len(os.sched_getaffinity(0))
+    except AttributeError:  # pragma: no cover - non-Linux
+        ncpu = os.cpu_count() or 1
+    local = max(1, int(os.environ.get("LOCAL_WORLD_SIZE", "1")))
+    t = max(1, ncpu // local)
+    omp = os.environ.get("OMP_NUM_THREADS")
+    if omp and omp.isdigit() and int(omp) > 0:
+        t = min(t, int(omp))
+    return t
+
+
+def parse_args(argv=None) -> argparse.Namespace:
+    ap = argparse.ArgumentParser(description=__doc__.split("\n")[0])
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--batch", type=int, default=int(os.environ.get("DASH_BENCH_BATCH", "0")),
+                    help="GCs evaluated together per GPU (0: as many as HBM holds, a multiple of --streams)")
+    ap.add_argument("--constructions", default=os.environ.get("DASH_BENCH_CONSTRUCTIONS", "flagship"),
+                    choices=sorted(CONSTRUCTIONS), help="gadget constructions of the headline phase")
+    ap.add_argument("--sign", default=None, choices=["fused", "reference"], help="override the sign construction")
+    ap.add_argument("--rescale", default=None, choices=["mrs", "legacy"], help="override the rescale construction")
+    ap.add_argument("--relu", default=None, choices=["mrs", "approx", "joint"], help="override the ReLU sign")
+    ap.add_argument("--streams", type=int, default=int(os.environ.get("DASH_BENCH_STREAMS", "4")),
+                    help="independent GC groups per GPU, each on its own HIP stream")
+    ap.add_argument("--model", default="MODEL_F_MINIONN_POOL_REPL")
+    ap.add_argument("--config", default="DASH", choices=["DASH", "REDASH_OPT", "REDASH_CPM"])
+    ap.add_argument("--backend", default="hip", choices=["hip", "cpu"])
+    ap.add_argument("--no-mfma", action="store_true")
+    ap.add_argument("--profile", action="store_true", help="print per-layer GPU times")
+    ap.add_argument("--threads", type=int, default=0, help="host threads per rank (0: cores / local ranks)")
+    ap.add_argument("--verify", type=int, default=1)
+    ap.add_argument("--garble-device", type=int, default=int(os.environ.get("DASH_BENCH_GARBLE_DEVICE", "1")),
+                    help="garble on this rank's GPU (byte-identical to the host garbler)")
+    ap.add_argument("--phases", default=os.environ.get("DASH_BENCH_PHASES", "main,reference,served"),
+                    help="comma list of main, reference, served (main is always run)")
+    ap.add_argument("--ref-batch", type=int, default=0, help="GCs per GPU of the reference phase (0: auto)")
+    ap.add_argument("--ref-steps", type=int, default=0, help="timed steps of the reference phase (0: --steps)")
+    ap.add_argument("--served-slots", type=int, default=16)
+    ap.add_argument("--served-groups", type=int, default=3)
+    ap.add_argument("--served-requests", type=int, default=8, help="online batches of the served phase")
+    return ap.parse_args(argv)
+
+
+# ----------------------------------------------------------------------------------------- evaluator slots
+class _HipGroup:
+    """``per`` GC slots evaluated together by one HipEvaluator on one stream."""
+
+    def __init__(self, template, per: int, device: int, mfma: bool, profile: bool, stream):
+        from .runtime import HipEvaluator
+
+        self.ev = HipEvaluator(template=template, batch=per, device=device, mfma=mfma, profile=profile)
+        self.stream = stream
+
+    def load(self, b, gc):
+        self.ev.load(b, gc.model)
+        gc.model = None  # tables live in HBM now
+
+    def encode(self, b, gc, x):
+        self.ev.encode_compressed_into(b, gc, x)
+
+    def launch(self):
+        self.ev.upload_inputs_compressed(self.stream)
+        self.ev.run(self.stream)
+
+    def fetch(self):
+        self.ev.fetch_outputs(self.stream)  # online message #2 (synchronizes this group's stream)
+
+    def decode(self, b, gc):
+        return self.ev.decode(b, gc)
+
+
+class _CpuGroup:
+    """Host-evaluator stand-in with the same interface (tests, no GPU)."""
+
+    def __init__(self, template, per: int, threads: int):
+        self.per, self.threads = per, threads
+        self.models = [None] * per
+        self.inputs = [None] * per
+        self.outputs = [None] * per
+
+    def load(self, b, gc):
+        self.models[b] = gc
+
+    def encode(self, b, gc, x):
+        self.inputs[b] = gc.garble_inputs(x)
+
+    def launch(self):
+        for b, gc in enumerate(self.models):
+            self.outputs[b] = gc.cpu_evaluate(self.inputs[b], self.threads)
+
+    def fetch(self):
+        pass
+
+    def decode(self, b, gc):
+        return gc.decode_outputs(self.outputs[b])
+
+
+# ----------------------------------------------------------------------------------------- phases
+class _Bench:
+    def __init__(self, args, ctx):
+        self.args, self.ctx = args, ctx
+        from .ir.quant import QuantizationMethod
+        from .models import BENCH_CONFIGS, build_circuit, canonical
+
+        self.model = canonical(args.model)
+        cfg = BENCH_CONFIGS.get(f"{self.model}/{args.config}") or BENCH_CONFIGS["MODEL_F_MINIONN_POOL_REPL/DASH"]
+        self.cfg = cfg
+        self.qm, self.qp = QuantizationMethod(cfg["q_method"]), cfg["q_parameter"]
+        self.circuit = build_circuit(self.model, self.qm, self.qp, seed=0)  # public model, identical on every rank
+        # range calibration (reference layer.h range tracking): arms the mixed-radix rescale's wrap-band guard
+        # (garbling.resolve_constructions refuses rescale="mrs" when a tracked rescale input enters the band)
+        from .models import quantized_inputs
+
+        self.circuit.calibrate(quantized_inputs(self.model, 32, self.qm, self.qp, seed=0), svc_modulus(cfg["crt"]))
+        self.hip = args.backend == "hip"
+        self.device = ctx.device if (self.hip and ctx.device is not None) else 0
+        if self.hip:
+            import torch
+
+            self.device = torch.cuda.current_device()
+
+    # ---- one GC
+    def garble(self, tag: str, b: int, cons: dict):
+        from .garbling import GarbledCircuit
+
+        seed = hashlib.sha256(f"dash-bench/{tag}/{self.ctx.rank}/{b}/{os.getpid()}".encode()).digest()[:16]
+        dev = self.device if (self.hip and self.args.garble_device) else None
+        return GarbledCircuit(self.circuit, self.cfg["crt"], self.cfg["mrs"], seed=seed, device=dev,
+                              fused_sign=cons["sign"] == "fused", rescale=cons["rescale"], relu=cons["relu"],
+                              nthreads=self.threads)
+
+    # ---- offline: garble B GCs into G groups of evaluator slots
+    def offline(self, tag: str, cons: dict, batch: int):
+        from .parallel import all_reduce_min
+
+        args, ctx = self.args, self.ctx
+        B = batch if batch > 0 else (256 if self.hip else 2)
+        G = max(1, min(args.streams, B))
+        B -= B % G
+        per = B // G
+        gcs: list = []
+        groups: list = [None] * G
+        st = dict(garble_s=0.0, upload_s=0.0, table_gb=0.0)
+        free0 = None
+        if self.hip:
+            import torch
+
+            free0 = torch.cuda.mem_get_info(self.device)[0]
+            streams = [torch.cuda.current_stream()] + [torch.cuda.Stream() for _ in range(G - 1)]
+        else:
+            streams = [None] * G
+        t_off = time.perf_counter()
+
+        def new_group(gc, g, per_):
+            if self.hip:
+                from .native import native
+
+                native().gpu_table_cache_trim()  # the new group's table arena needs the garbler's cached blocks
+                return _HipGroup(gc.model, per_, self.device, not args.no_mfma, args.profile, streams[g])
+            return _CpuGroup(gc.model, per_, self.threads)
+
+        b = 0
+        while b < B:
+            try:
+                t = time.perf_counter()
+                gc = self.garble(tag, b, cons)
+                st["garble_s"] += time.perf_counter() - t
+                if b == 0:
+                    if self.hip:
+                        # HBM guard: every GC's tables stay resident. Size B from the real device footprint of
+                        # one GC (tables + evaluator scratch) plus one GC in flight in the garbler.
+                        from .runtime import HipEvaluator
+
+                        probe = HipEvaluator(template=gc.model, batch=1, device=self.device, mfma=not args.no_mfma)
+                        per_gc = probe.device_bytes() * 1.01
+                        del probe
+                        fit = int((free0 - gc.table_bytes - 2.5e9) // per_gc)
+                        log(f"[{tag}] rank {ctx.rank}: {free0 / 1e9:.1f} GB HBM free, {per_gc / 1e9:.2f} GB per GC "
+                            f"({gc.table_bytes / 1e9:.2f} GB tables): fits {fit}")
+                        if fit < B:
+                            B = max(G, fit - fit % G)
+                            log(f"[{tag}] rank {ctx.rank}: batch {'sized' if batch <= 0 else 'reduced'} to {B}")
+                    B = int(all_reduce_min(ctx, float(B)))  # every rank evaluates the same number of GCs
+                    G = max(1, min(G, B))
+                    B -= B % G
+                    per = B // G
+                    groups = groups[:G]
+                t = time.perf_counter()
+                g = b // per
+                if groups[g] is None:
+                    groups[g] = new_group(gc, g, per)
+                st["table_gb"] = gc.table_bytes / 1e9
+                groups[g].load(b % per, gc)
+                st["upload_s"] += time.perf_counter() - t
+                gcs.append(gc)
+                if b < 3 or (b + 1) % 16 == 0 or b + 1 == B:
+                    log(f"[{tag}] rank {ctx.rank}: garbled+uploaded GC {b + 1}/{B} ({st['table_gb']:.2f} GB tables)")
+            except RuntimeError as e:
+                # HBM ran out before the estimate said it would: keep this rank's complete groups; the
+                # all-reduce below makes every rank agree on the smallest batch
+                if "out of memory" not in str(e) or b < per:
+                    raise
+                from .native import native
+
+                native().gpu_table_cache_trim()
+                native().hip_clear_last_error()  # the handled OOM must not resurface in the next launch check
+                log(f"[{tag}] rank {ctx.rank}: out of HBM at GC {b + 1}")
+                B = b
+                break
+            b += 1
+        # ranks agree on B after the loop too (one rank's out-of-memory fallback shrinks only its own batch)
+        B_all = int(all_reduce_min(ctx, float(B - B % per)))
+        G = B_all // per
+        groups, gcs, streams = groups[:G], gcs[:G * per], streams[:G]
+        B = G * per
+        if self.hip:
+            from .native import native
+
+            native().gpu_table_cache_trim()
+        st["offline_s"] = time.perf_counter() - t_off
+        return gcs, groups, B, G, per, st
+
+    # ---- online: timed steps over the loaded groups
+    def online(self, gcs, groups, B, per, steps, warmup, seed_base, verify):
+        from .models import quantized_inputs
+        from .parallel import all_reduce_max, barrier
+
+        ctx = self.ctx
+        inputs = quantized_inputs(self.model, B * (steps + warmup), self.qm, self.qp, seed=seed_base + ctx.rank)
+        host = [0.0]
+
+        def step(i: int, check: bool = False):
+            xs = inputs[i * B:(i + 1) * B]
+            # online message #1 in wire form (16-B compressed labels) -> pinned staging -> H2D -> GPU unpack;
+            # the G groups run concurrently on their own streams
+            for g, grp in enumerate(groups):
+                t = time.perf_counter()
+                for b in range(per):
+                    grp.encode(b, gcs[g * per + b], xs[g * per + b])
+                host[0] += time.perf_counter() - t
+                grp.launch()
+            dec = []
+            for g, grp in enumerate(groups):
+                grp.fetch()
+                t = time.perf_counter()
+                dec += [grp.decode(b, gcs[g * per + b]) for b in range(per)]
+                host[0] += time.perf_counter() - t
+            if check:
+                for gc, x, y in zip(gcs, xs, dec):
+                    ref = gc.plain_q_eval(x)
+                    if not np.array_equal(ref, y):
+                        raise RuntimeError(f"garbled output mismatch: {y} vs {ref}")
+            return dec
+
+        verified = False
+        for w in range(warmup):
+            step(w, check=bool(verify) and w == 0)
+            verified = verified or bool(verify)
+        self.sync()
+        barrier(ctx)
+        self.sync()
+        host[0] = 0.0
+        t0 = time.perf_counter()
+        last = None
+        for s in range(steps):
+            last = step(warmup + s)
+        self.sync()
+        barrier(ctx)
+        self.sync()
+        local = time.perf_counter() - t0
+        elapsed = all_reduce_max(ctx, local)  # slowest rank defines the step time
+        return dict(elapsed=elapsed, local=local, host_ms=1000.0 * host[0] / max(1, steps), last=last,
+                    verified=verified, step=step)
+
+    def sync(self):
+        if self.hip:
+            import torch
+
+            torch.cuda.synchronize()
+
+    # ---- served: fresh GC per inference, garbling pipelined against evaluation
+    def served(self, cons: dict) -> dict:
+        from .models import quantized_inputs
+        from .parallel import all_reduce_max, barrier
+        from .serving import InferenceService
+
+        a, ctx = self.args, self.ctx
+        slots, groups, reqs = a.served_slots, a.served_groups, a.served_requests
+        xs = quantized_inputs(self.model, slots * reqs, self.qm, self.qp, seed=5000 + ctx.rank)
+        t0 = time.perf_counter()
+        svc = InferenceService(self.circuit, self.cfg["crt"], self.cfg["mrs"],
+                               backend="hip" if self.hip else "cpu", device=self.device, slots_per_group=slots,
+                               groups=groups, garble_device=bool(self.hip and a.garble_device),
+                               rescale=cons["rescale"], relu=cons["relu"], fused_sign=cons["sign"] == "fused",
+                               nthreads=self.threads)
+        fill_s = time.perf_counter() - t0
+        try:
+            barrier(ctx)
+            svc.stats.t_start = time.perf_counter()
+            t1 = time.perf_counter()
+            ok = True
+            for r in range(reqs):
+                batch = xs[r * slots:(r + 1) * slots]
+                y = svc.infer(batch)
+                if r == 0:
+                    M = svc_modulus(self.cfg["crt"])
+                    ok = all(np.array_equal(y[i], self.circuit.plain_q_eval(x, track=False, crt_modulus=M))
+                             for i, x in enumerate(batch))
+            local = time.perf_counter() - t1
+            st = svc.stats.as_dict()
+        finally:
+            svc.close()
+        barrier(ctx)
+        elapsed = all_reduce_max(ctx, local)
+        n = slots * reqs
+        return dict(value=ctx.world * n / elapsed, local_inf_per_s=n / local, pool_fill_s=fill_s,
+                    garble_s_per_gc=st["garble_s_per_gc"], pool_wait_s=st["pool_wait_s"],
+                    batch_latency_ms=st["batch_latency_ms"], verified=ok, slots=slots, groups=groups,
+                    requests=reqs)
+
+    # ---- per-rank evidence
+    def rank_record(self, ms_step: float, inf_s: float, host_ms: float, B: int) -> dict:
+        rec = dict(rank=self.ctx.rank, local_rank=self.ctx.local_rank, host=socket.gethostname(), pid=os.getpid(),
+                   threads=self.threads, gcs=B, ms_per_step=round(ms_step, 3), inf_per_s=round(inf_s, 3),
+                   host_encode_decode_ms_per_step=round(host_ms, 3))
+        if self.hip:
+            from .native import native
+
+            rec["device"] = int(self.device)
+            rec["pci_bus_id"] = native().hip_device_pci_bus_id(int(self.device))
+        else:
+            rec["device"] = "cpu"
+        return rec
+
+
+def svc_modulus(crt) -> int:
+    from .ir.bases import crt_modulus, first_primes
+
+    return crt_modulus(crt if isinstance(crt, list) else first_primes(crt))
+
+
+def run(argv=None) -> Optional[dict]:
+    """Run the benchmark; rank 0 returns (and bench.py prints) the JSON record, other ranks None."""
+    args = parse_args(argv)
+    from .native import native
+    from .parallel import all_gather_array, all_gather_object, init_distributed, shutdown
+
+    hip = args.backend == "hip"
+    if hip:
+        import torch
+
+        # one process per GPU (torchrun); backend nccl (= RCCL over xGMI). DASH_DIST_BACKEND=gloo and a device
+        # count smaller than the world size are only for rehearsing the multi-rank path on one GPU.
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        if int(os.environ.get("WORLD_SIZE", "1")) > 1 and torch.cuda.device_count() < int(os.environ["WORLD_SIZE"]):
+            os.environ["LOCAL_RANK"] = str(int(os.environ.get("LOCAL_RANK", "0")) % max(1, torch.cuda.device_count()))
+    ctx = init_distributed(backend=os.environ.get("DASH_DIST_BACKEND") or None, use_gpu=hip)
+    world, rank = ctx.world, ctx.rank
+    bench = _Bench(args, ctx)
+    bench.threads = host_thread_budget(args.threads)
+    native().set_num_threads(bench.threads)
+    phases = {p.strip() for p in args.phases.split(",") if p.strip()} | {"main"}
+
+    cons = dict(CONSTRUCTIONS[args.constructions])
+    for key in ("sign", "rescale", "relu"):
+        if getattr(args, key):
+            cons[key] = getattr(args, key)
+
+    # ---------------- main (headline) phase
+    gcs, groups, B, G, per, off = bench.offline("main", cons, args.batch)
+    free_b = total_b = None
+    if hip:
+        import torch
+
+        free_b, total_b = torch.cuda.mem_get_info(bench.device)
+    r = bench.online(gcs, groups, B, per, args.steps, args.warmup, 1000, args.verify)
+    elapsed = r["elapsed"]
+    gathered = all_gather_array(ctx, np.stack(r["last"]))  # decoded logits of the last step onto every rank
+    assert gathered.shape[0] == world
+    total_inf = world * B * args.steps
+    value = total_inf / elapsed
+    ms_step = 1000.0 * elapsed / args.steps
+    recs = all_gather_object(ctx, bench.rank_record(1000.0 * r["local"] / args.steps,
+                                                    B * args.steps / r["local"], r["host_ms"], B))
+    prof = op_ms = None
+    if args.profile and hip:
+        r["step"](0)
+        prof = {k: round(v, 3) for k, v in groups[0].ev.layer_times().items()}
+        op_ms = [[n, round(v, 4)] for n, v in groups[0].ev.op_times()]
+    verified = r["verified"]
+    del gcs, groups, r
+
+    # ---------------- reference-constructions phase (same driver, the reference's gadgets)
+    ref = None
+    if "reference" in phases and args.constructions != "reference":
+        rc = CONSTRUCTIONS["reference"]
+        rsteps = args.ref_steps or args.steps
+        g2, grp2, B2, G2, per2, off2 = bench.offline("reference", rc, args.ref_batch)
+        r2 = bench.online(g2, grp2, B2, per2, rsteps, max(1, min(args.warmup, 2)), 3000, args.verify)
+        ref = dict(value=round(world * B2 * rsteps / r2["elapsed"], 3),
+                   ms_per_step=round(1000.0 * r2["elapsed"] / rsteps, 3), gcs_per_gpu=B2, steps=rsteps,
+                   constructions=rc, verified_vs_plaintext=r2["verified"],
+                   offline={"garble_s_per_gc": round(off2["garble_s"] / max(1, B2), 3),
+                            "table_gb_per_gc": round(off2["table_gb"], 3)})
+        del g2, grp2, r2
+
+    # ---------------- served phase (fresh GC per inference, garbling included)
+    served = None
+    if "served" in phases:
+        served = bench.served(cons)
+
+    out = None
+    if rank == 0:
+        out = {
+            "metric": ("online garbled inferences/sec (MiniONN CIFAR-10 CNN)"
+                       if bench.model == "MODEL_F_MINIONN_POOL_REPL" else f"online garbled inferences/sec ({bench.model})"),
+            "value": round(value, 3),
+            "unit": "inferences/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_step, 3),
+            "ms_per_inference": round(1000.0 * elapsed / (B * args.steps), 3),
+            "latency_ms_per_batch": round(ms_step, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": round(value / BASELINE_INF_PER_S, 2),
+            "dtype": "uint8 label components / int8 MFMA (exact modular arithmetic)",
+            "data": f"synthetic {'CIFAR-10' if bench.circuit.input_dims[0] == 3 else 'MNIST'}-shaped inputs, random-init weights",
+            "config": {
+                "model": bench.model,
+                "scheme": args.config,
+                "crt_base": bench.cfg["crt"] if isinstance(bench.cfg["crt"], list) else native().first_primes(bench.cfg["crt"]),
+                "mrs": bench.cfg["mrs"],
+                "global_batch": world * B,
+                "gcs_per_gpu": B,
+                "streams": G,
+                "constructions": args.constructions,
+                "sign_construction": cons["sign"],
+                "rescale_construction": cons["rescale"],
+                "relu_construction": cons["relu"],
+                "seq_len": None,
+                "input_shape": list(bench.circuit.input_dims),
+                "parallelism": f"dp{world}",
+                "backend": args.backend,
+            },
+            "dist_backend": ctx.backend if ctx.distributed else "none",
+            "world_size": world,
+            "threads_per_rank": bench.threads,
+            "ranks": recs,
+            "offline": {"garble_s_per_gc": round(off["garble_s"] / max(1, B), 3),
+                        "upload_s_per_gc": round(off["upload_s"] / max(1, B), 3),
+                        "table_gb_per_gc": round(off["table_gb"], 3), "offline_total_s": round(off["offline_s"], 1)},
+            "verified_vs_plaintext": verified,
+        }
+        if hip:
+            out["hbm_gb"] = {"used": round((total_b - free_b) / 1e9, 1), "total": round(total_b / 1e9, 1)}
+        if ref is not None:
+            out["reference_constructions_value"] = ref["value"]
+            out["reference_constructions"] = ref
+        if served is not None:
+            out["served_inf_per_s"] = round(served["value"], 3)
+            out["served"] = {k: (round(v, 3) if isinstance(v, float) else v) for k, v in served.items() if k != "value"}
+        if prof:
+            out["layer_ms"] = prof
+            out["op_ms"] = op_ms
+    shutdown(ctx)
+    return out
+
+
+def main(argv=None) -> None:
+    out = run(argv)
+    if out is not None:
+        print(json.dumps(out), flush=True)

@@ -47,8 +47,8 @@ class DashConfig:
     crt: Union[int, list, None] = None        # k (first k primes) or explicit base
     mrs: Union[float, list, None] = None      # ReLU accuracy (table lookup) or explicit MRS base
     max_modulus: int = 0
-    rescale: str = "mrs"                      # DASH rescale construction: mrs (one mixed-radix gadget) | legacy
-    relu: str = "approx"                      # ReLU sign: approx (reference gadget) | mrs (exact mixed radix) | joint (from the preceding mixed-radix rescale)
+    rescale: str = "auto"                     # DASH rescale construction: auto (mrs where the base and ranges allow) | mrs (one mixed-radix gadget) | legacy
+    relu: str = "auto"                        # ReLU sign: auto (joint with the mrs rescale, else approx) | approx (reference gadget) | mrs (exact mixed radix) | joint (from the preceding mixed-radix rescale)
     sign: str = "fused"                       # approximate sign gadget: fused casts | reference
     seed: Optional[str] = None                # hex seed for reproducible garbling (tests only)
     insecure_fixed_seed: bool = False         # allow `seed` in the serving engine (reuses labels across restarts)
@@ -78,7 +78,7 @@ class DashConfig:
     # ------------------------------------------------------------ derived
     def gc_kwargs(self) -> dict:
         """GarbledCircuit keyword arguments selecting the gadget constructions."""
-        if self.rescale not in ("mrs", "legacy") or self.relu not in ("approx", "mrs", "joint") or \
+        if self.rescale not in ("auto", "mrs", "legacy") or self.relu not in ("auto", "approx", "mrs", "joint") or \
                 self.sign not in ("fused", "reference"):
             raise ValueError(f"bad gadget construction: rescale={self.rescale} relu={self.relu} sign={self.sign}")
         return dict(rescale=self.rescale, relu=self.relu, fused_sign=self.sign == "fused")

@@ -1289,6 +1289,12 @@ void register_hip_bindings(py::module_& m) {
         if (hipGetDeviceCount(&n) != hipSuccess) return 0;
         return n;
     });
+    // "dddd:bb:dd.f" of a device (multi-GPU bench evidence: which physical GPU each rank ran on)
+    m.def("hip_device_pci_bus_id", [](int device) {
+        char buf[64] = {0};
+        HIPCHECK(hipDeviceGetPCIBusId(buf, static_cast<int>(sizeof(buf)), device));
+        return std::string(buf);
+    });
     py::class_<HipEvaluator, std::shared_ptr<HipEvaluator>>(m, "HipEvaluator")
         .def(py::init([](std::shared_ptr<GarbledModel> tmpl, int B, int device, bool mfma) {
                  return std::make_shared<HipEvaluator>(std::move(tmpl), B, device, mfma);

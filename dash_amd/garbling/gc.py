@@ -26,11 +26,45 @@ from ..native import native
 Labels = list  # list[(modulus, np.ndarray int16 [N, n_p])]
 
 
+def mrs_capable(crt_base: Sequence[int]) -> bool:
+    """The mixed-radix rescale / sign constructions need residue 0 = 2 and odd other residues."""
+    return len(crt_base) >= 2 and int(crt_base[0]) == 2 and all(int(p) % 2 == 1 for p in crt_base[1:])
+
+
+def resolve_constructions(circuit: Circuit, crt_base: Sequence[int], rescale: str, relu: str):
+    """Resolve "auto" gadget constructions and guard the mixed-radix rescale's range.
+
+    rescale="auto" -> "mrs" when the base allows it and the circuit was calibrated
+    (Circuit.calibrate: every DASH rescale has a tracked input range) with no
+    tracked input in the wrap band (Circuit.mrs_rescale_violations); otherwise
+    "legacy", the reference's construction, exact on the whole signed range.
+    An explicit "mrs" on a circuit whose tracked range enters the band raises.
+    relu="auto" -> "joint" with the mixed-radix rescale, else "approx"."""
+    if rescale not in ("auto", "legacy", "mrs"):
+        raise ValueError(f"rescale construction must be 'auto', 'legacy' or 'mrs', got {rescale!r}")
+    if relu not in ("auto", "approx", "mrs", "joint"):
+        raise ValueError(f"relu construction must be 'auto', 'approx', 'mrs' or 'joint', got {relu!r}")
+    M = _crt_mod(crt_base)
+    dash_rescales = circuit._dash_rescales()
+    bad = circuit.mrs_rescale_violations(M) if dash_rescales else []
+    if rescale == "auto":
+        calibrated = bool(dash_rescales) and all(l.input_tracked for l in dash_rescales)
+        rescale = "mrs" if (mrs_capable(crt_base) and calibrated and not bad) else "legacy"
+    elif rescale == "mrs" and bad:
+        i, hi, lim = bad[0]
+        raise ValueError(f"rescale='mrs': layer {i}'s tracked input reaches {hi} >= {lim}, inside the mixed-radix "
+                         f"wrap band below M/2 = {M // 2}; use rescale='legacy' or a larger CRT base "
+                         f"(Circuit.infer_crt_base_size reserves the band)")
+    if relu == "auto":
+        relu = "joint" if rescale == "mrs" and mrs_capable(crt_base) else "approx"
+    return rescale, relu
+
+
 class GarbledCircuit:
     def __init__(self, circuit: Circuit, crt: Union[int, Sequence[int]], mrs: Union[None, float, Sequence[int]] = None,
                  max_modulus: int = 0, seed: Optional[bytes] = None, garble_me: bool = True, nthreads: int = 0,
-                 device: Optional[int] = None, fused_sign: bool = True, rescale: str = "legacy",
-                 relu: str = "approx"):
+                 device: Optional[int] = None, fused_sign: bool = True, rescale: str = "auto",
+                 relu: str = "auto"):
         """fused_sign: sign-gadget construction. True (default): the MRS casts are folded into the approx and
         carry projections (same function, 3.7x fewer gates per sign; gadgets.h SignPlan::fused). False: the
         reference construction with explicit identity casts (sign_gadget.h:456-546).
@@ -38,14 +72,18 @@ class GarbledCircuit:
         rescale: construction of the DASH legacy rescale (divide by 2^l, Rescale(l)). "legacy": l iterations of
         the reference's sign-base-extension gadget (rescale_gadget.h:115-242). "mrs": one exact mixed-radix
         conversion computing the same ceil(x / 2^l) (gadgets.h RescaleMrsPlan; k + 1 hashes per element instead
-        of l sign gadgets); it differs only on the top U - M/2 < 2^l values of the signed range, which wrap.
+        of l sign gadgets); it differs only on the top U - M/2 < 2^l values of the signed range, which wrap, so a
+        circuit whose tracked range enters that band is refused (resolve_constructions) and
+        Circuit.infer_crt_base_size sizes M with the band reserved. "auto" (default, = the benchmark's choice):
+        "mrs" where the CRT base and the tracked ranges allow it, else "legacy".
 
         relu: sign of the ReLU gadget. "approx": the reference's approximate sign gadget (construction per
         fused_sign). "mrs": exact mixed-radix sign with the mod-2 residue converted last (gadgets.h SignMrsPlan;
         k - 1 hashes, 147 instead of 568 table entries per element at k = 7, exact for every x). "joint": a ReLU
         that directly follows a mixed-radix rescale takes its sign from that rescale's conversion (residue 2
         converted last: its digit is the sign; gadgets.h RescaleMrsPlan::sign_last), so it costs only the
-        mixed-modulus half gates; other ReLUs use the approximate gadget. Needs rescale="mrs" to have effect."""
+        mixed-modulus half gates; other ReLUs use the approximate gadget. Needs rescale="mrs" to have effect.
+        "auto" (default): "joint" with the mixed-radix rescale, else "approx"."""
         self.circuit = circuit
         self.crt_base = first_primes(crt) if isinstance(crt, int) else [int(p) for p in crt]
         if mrs is None:
@@ -60,12 +98,7 @@ class GarbledCircuit:
         # device: garble the ReLU / Sign / legacy-rescale layers on this GPU (bit-identical to the CPU garbler)
         self.device = -1 if device is None else int(device)
         self.fused_sign = bool(fused_sign)
-        if rescale not in ("legacy", "mrs"):
-            raise ValueError(f"rescale construction must be 'legacy' or 'mrs', got {rescale!r}")
-        self.rescale = rescale
-        if relu not in ("approx", "mrs", "joint"):
-            raise ValueError(f"relu construction must be 'approx', 'mrs' or 'joint', got {relu!r}")
-        self.relu = relu
+        self.rescale, self.relu = resolve_constructions(circuit, self.crt_base, rescale, relu)
         self._n = native()
         self.garbler = self._n.Garbler(self.crt_base, self.mrs_base, self.seed, int(max_modulus))
         self.model = None

@@ -75,23 +75,61 @@ class Circuit:
         for layer in self.layers:
             layer.reset_ranges()
 
+    def calibrate(self, inputs, crt_modulus: Optional[int] = None, reset: bool = True) -> "Circuit":
+        """Track every layer's quantized value range over `inputs` (the reference's
+        range tracking, layer.h:13-77): feeds CRT sizing and the mixed-radix
+        rescale guard (mrs_rescale_violations, garbling.resolve_constructions)."""
+        if isinstance(inputs, np.ndarray) and inputs.ndim == 1:
+            inputs = [inputs]
+        if reset:
+            self.reset_ranges()
+        for x in inputs:
+            self.plain_q_eval(x, True, crt_modulus)
+        return self
+
     def get_min_plain_q_val(self) -> int:
         return min(l.get_min_plain_q_val() for l in self.layers)
 
     def get_max_plain_q_val(self) -> int:
         return max(l.get_max_plain_q_val() for l in self.layers)
 
-    def required_crt_modulus(self) -> int:
-        return 2 * max(abs(self.get_min_plain_q_val()), abs(self.get_max_plain_q_val()))
+    def required_crt_modulus(self, rescale_margin: bool = True) -> int:
+        """2 * max |tracked value| (circuit.h:159-231). With `rescale_margin`, the
+        input of every DASH rescale (divide by 2^l) also keeps 2^l below M/2, the
+        band in which the single-shot mixed-radix rescale construction wraps
+        (Rescale.mrs_limit): a base sized here is valid for every construction."""
+        need = 2 * max(abs(self.get_min_plain_q_val()), abs(self.get_max_plain_q_val()))
+        if rescale_margin:
+            for l in self._dash_rescales():
+                if l.input_tracked:
+                    need = max(need, 2 * (max(abs(l.in_min_q), abs(l.in_max_q)) + (1 << l.l)))
+        return need
 
-    def infer_crt_base_size(self, inputs, max_k: int = 11, assert_bound: bool = True) -> int:
+    def _dash_rescales(self):
+        return [l for l in self.layers if getattr(l, "use_sign_base_extension", False) and getattr(l, "l", -1) >= 1]
+
+    def mrs_rescale_violations(self, crt_modulus: int) -> list:
+        """DASH rescale layers whose tracked input range reaches the mixed-radix wrap
+        band [Rescale.mrs_limit(M), M/2): (layer index, tracked max, limit). Empty
+        when no layer has been evaluated with range tracking (nothing to check)."""
+        bad = []
+        for i, l in enumerate(self.layers):
+            if l in self._dash_rescales() and l.input_tracked:
+                lim = l.mrs_limit(crt_modulus)
+                if l.in_max_q >= lim:
+                    bad.append((i, int(l.in_max_q), int(lim)))
+        return bad
+
+    def infer_crt_base_size(self, inputs, max_k: int = 11, assert_bound: bool = True,
+                            rescale_margin: bool = True) -> int:
         """Smallest k such that the product of the first k primes covers every
-        tracked intermediate value (circuit.h:159-265)."""
+        tracked intermediate value (circuit.h:159-265), plus the mixed-radix
+        rescale headroom (required_crt_modulus)."""
         if isinstance(inputs, np.ndarray) and inputs.ndim == 1:
             inputs = [inputs]
         for x in inputs:
             self.plain_q_eval(x, True)
-        need = self.required_crt_modulus()
+        need = self.required_crt_modulus(rescale_margin)
         k = 0
         M = 0
         while M < need:

@@ -376,7 +376,28 @@ class Rescale(Layer):
         y = self._apply(x, crt_modulus)
         if track:
             self._track_q(x, y)
+            if x.size:
+                self.in_min_q = min(self.in_min_q, int(x.min()))
+                self.in_max_q = max(self.in_max_q, int(x.max()))
         return y
+
+    def reset_ranges(self):
+        super().reset_ranges()
+        self.in_min_q = Q_MAX  # tracked range of the rescale's input (mixed-radix headroom check)
+        self.in_max_q = Q_MIN
+
+    @property
+    def input_tracked(self) -> bool:
+        return self.in_max_q >= self.in_min_q
+
+    def mrs_limit(self, crt_modulus: int) -> int:
+        """Exclusive upper bound of the inputs on which the single-shot mixed-radix rescale
+        (gadgets.h RescaleMrsPlan) equals the reference's l-fold halving: x + U < M with
+        U = M/2 rounded up to S - 1 mod S, S = 2^l (the top U - M/2 < S values wrap)."""
+        M, S = int(crt_modulus), 1 << self.l
+        h = M // 2
+        U = h + (S - 1 - h % S) % S
+        return M - U
 
     def garble_spec(self):
         if self.use_sign_base_extension:

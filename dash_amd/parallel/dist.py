@@ -128,6 +128,22 @@ def all_reduce_max(ctx: DistContext, v: float) -> float:
     return float(t.item())
 
 
+def all_reduce_min(ctx: DistContext, v: float) -> float:
+    return -all_reduce_max(ctx, -float(v))
+
+
+def all_gather_object(ctx: DistContext, obj) -> list:
+    """Gather one small picklable record per rank (rank order). Records come
+    only from ranks of this job."""
+    if not ctx.distributed:
+        return [obj]
+    import torch.distributed as dist
+
+    out = [None] * ctx.world
+    dist.all_gather_object(out, obj)
+    return out
+
+
 def barrier(ctx: DistContext) -> None:
     if ctx.distributed:
         import torch.distributed as dist
@@ -150,13 +166,20 @@ class BatchDataParallel:
     round and evaluates them on its GPU (`backend="hip"`) or on the CPU
     oracle (`backend="cpu"`); outputs are all-gathered in global order.
 
-    Every round garbles new circuits (GCs are single use)."""
+    Every round garbles new circuits (GCs are single use). With the ``hip``
+    backend they are garbled on the rank's own GPU (byte-identical to the host
+    garbler), so N ranks never compete for the shared host cores; the gadget
+    constructions default to GarbledCircuit's ("auto": the mixed-radix rescale
+    and joint ReLU where the CRT base and tracked ranges allow)."""
 
     def __init__(self, ctx: DistContext, circuit, crt, mrs=None, per_rank: int = 1, backend: str = "hip",
-                 max_modulus: int = 0, seed: Optional[bytes] = None):
+                 max_modulus: int = 0, seed: Optional[bytes] = None, garble_device: Optional[bool] = None,
+                 **gc_kw):
         self.ctx, self.circuit, self.crt, self.mrs = ctx, circuit, crt, mrs
         self.per_rank, self.backend, self.max_modulus = per_rank, backend, max_modulus
         self.seed = seed
+        self.garble_device = (backend == "hip") if garble_device is None else bool(garble_device)
+        self.gc_kw = gc_kw
         self.round = 0
         self.ev = None
 
@@ -174,7 +197,9 @@ class BatchDataParallel:
         ctx = self.ctx
         assert len(inputs) == ctx.world * self.per_rank, "global batch must be world * per_rank"
         mine = inputs[ctx.rank * self.per_rank:(ctx.rank + 1) * self.per_rank]
-        gcs = [GarbledCircuit(self.circuit, self.crt, self.mrs, max_modulus=self.max_modulus, seed=self._seed(b))
+        dev = (ctx.device or 0) if self.garble_device else None
+        gcs = [GarbledCircuit(self.circuit, self.crt, self.mrs, max_modulus=self.max_modulus, seed=self._seed(b),
+                              device=dev, **self.gc_kw)
                for b in range(self.per_rank)]
         self.round += 1
         if self.backend == "hip":

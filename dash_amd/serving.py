@@ -187,9 +187,14 @@ class InferenceService:
                  backend: str = "hip", device: int = 0, garble_device: Optional[bool] = None, max_retries: int = 2,
                  step_timeout_s: float = 120.0, seed: Optional[bytes] = None, prefetch: bool = True,
                  fault_hook: Optional[Callable[[int, int], bool]] = None, nthreads: int = 0,
-                 rescale: str = "mrs", relu: str = "joint", fused_sign: bool = True):
+                 rescale: str = "auto", relu: str = "auto", fused_sign: bool = True,
+                 insecure_fixed_seed: bool = False):
         if backend not in ("hip", "cpu"):
             raise ValueError("backend must be 'hip' or 'cpu'")
+        if seed is not None and not insecure_fixed_seed:
+            # a fixed seed replays the same GC label / offset sequence after every restart, on new inputs
+            raise ValueError("InferenceService(seed=...) reuses garbling randomness across restarts; pass "
+                             "insecure_fixed_seed=True to accept that (tests / reproducible benchmarks only)")
         if backend == "hip" and native().hip_device_count() == 0:
             raise RuntimeError("InferenceService(backend='hip') needs a visible MI355X")
         self.circuit, self.crt, self.mrs, self.max_modulus = circuit, crt, mrs, max_modulus

@@ -349,7 +349,7 @@ def test_rescale_mrs_tables_and_model():
     c = build_circuit("MODEL_B_POOL_REPL", Q.ScaleQuant, 3, seed=1)
     xs = quantized_inputs("MODEL_B_POOL_REPL", 3, Q.ScaleQuant, 3, seed=5)
     new = GarbledCircuit(c, 8, 100.0, seed=SEED, rescale="mrs")
-    old = GarbledCircuit(c, 8, 100.0, seed=SEED)
+    old = GarbledCircuit(c, 8, 100.0, seed=SEED, rescale="legacy")
     assert new.table_bytes < old.table_bytes / 2
     for x in xs:
         y = new.decode_outputs(new.cpu_evaluate(new.garble_inputs(x)))
@@ -387,7 +387,7 @@ def test_relu_mrs_tables_and_model():
     c = build_circuit("MODEL_B_POOL_REPL", Q.ScaleQuant, 3, seed=1)
     xs = quantized_inputs("MODEL_B_POOL_REPL", 3, Q.ScaleQuant, 3, seed=6)
     both = GarbledCircuit(c, 8, 100.0, seed=SEED, rescale="mrs", relu="mrs")
-    resc = GarbledCircuit(c, 8, 100.0, seed=SEED, rescale="mrs")
+    resc = GarbledCircuit(c, 8, 100.0, seed=SEED, rescale="mrs", relu="approx")
     assert both.table_bytes < resc.table_bytes
     for x in xs:
         y = both.decode_outputs(both.cpu_evaluate(both.garble_inputs(x)))
@@ -429,7 +429,7 @@ def test_rescale_relu_joint_model():
     c = build_circuit("MODEL_B_POOL_REPL", Q.ScaleQuant, 3, seed=1)
     xs = quantized_inputs("MODEL_B_POOL_REPL", 3, Q.ScaleQuant, 3, seed=7)
     joint = GarbledCircuit(c, 8, 100.0, seed=SEED, rescale="mrs", relu="joint")
-    resc = GarbledCircuit(c, 8, 100.0, seed=SEED, rescale="mrs")
+    resc = GarbledCircuit(c, 8, 100.0, seed=SEED, rescale="mrs", relu="approx")
     assert joint.table_bytes < resc.table_bytes
     nj = sum(1 for i in range(joint.model.num_layers) if list(joint.model.layer_params(i).get("smode", [])) == [2])
     assert nj >= 1
@@ -440,3 +440,38 @@ def test_rescale_relu_joint_model():
     m2 = native().GarbledModel.deserialize(blob)
     y = joint.decode_outputs(native().cpu_evaluate(m2, joint.garble_inputs(xs[0]), 0))
     np.testing.assert_array_equal(y, joint.plain_q_eval(xs[0]))
+
+
+def test_rescale_mrs_wrap_band_guard():
+    """The mixed-radix rescale wraps on the top U - M/2 values below M/2. M = 2*3*5*7 = 210, l = 2: U = 107, so
+    inputs 103, 104 wrap. A calibrated circuit whose tracked rescale input reaches the band is refused with
+    rescale="mrs", "auto" falls back to the reference construction (exact there), and infer_crt_base_size
+    reserves the band."""
+    crt, l, M = [2, 3, 5, 7], 2, 210
+    band = np.arange(M // 2 - (1 << l), M // 2, dtype=np.int64)  # M/2 - 2^l ... M/2 - 1 = 101..104
+    c = d.Circuit([d.Rescale(l, (band.size,))])
+    assert c.layers[0].mrs_limit(M) == 103
+    # unguarded (never calibrated): the mixed-radix construction really does differ on 103, 104
+    raw = GarbledCircuit(c, crt, 100.0, seed=SEED, rescale="mrs")
+    out = raw.decode_outputs(raw.cpu_evaluate(raw.garble_inputs(band)))
+    ref = c.plain_q_eval(band, False, M)
+    assert np.array_equal(out[:2], ref[:2]) and not np.array_equal(out[2:], ref[2:])
+    # calibrated on the band: refused / auto -> legacy, which matches the reference semantics
+    c.calibrate([band])
+    assert c.mrs_rescale_violations(M) == [(0, 104, 103)]
+    with pytest.raises(ValueError, match="wrap band"):
+        GarbledCircuit(c, crt, 100.0, seed=SEED, rescale="mrs")
+    auto = GarbledCircuit(c, crt, 100.0, seed=SEED)
+    assert auto.rescale == "legacy" and auto.relu == "approx"
+    np.testing.assert_array_equal(auto.decode_outputs(auto.cpu_evaluate(auto.garble_inputs(band))), ref)
+    # CRT sizing reserves 2^l below M/2 for every rescale input: 104 + 4 > 105 -> one more prime than 2*104 needs
+    assert c.required_crt_modulus(rescale_margin=False) == 2 * 104
+    assert c.required_crt_modulus() == 2 * (104 + 4)
+    assert c.infer_crt_base_size([band], rescale_margin=False) == 4
+    assert c.infer_crt_base_size([band]) == 5
+    # below the band: calibrated auto picks the mixed-radix construction and it is exact
+    ok = np.arange(90, 103, dtype=np.int64)
+    c2 = d.Circuit([d.Rescale(l, (ok.size,))]).calibrate([ok])
+    g2 = GarbledCircuit(c2, crt, 100.0, seed=SEED)
+    assert g2.rescale == "mrs" and g2.relu == "joint"
+    np.testing.assert_array_equal(g2.decode_outputs(g2.cpu_evaluate(g2.garble_inputs(ok))), c2.plain_q_eval(ok, False, M))

@@ -316,8 +316,8 @@ def test_gpu_garbler_bit_identical_mrs_rescale(name):
         full = build_circuit("MODEL_F_MINIONN_POOL_REPL", Q.ScaleQuant, 5, seed=0)
         c, k = Circuit(full.layers[:4]), 7  # conv, rescale(l=5), relu, conv
     seed = bytes(range(16))
-    cpu = GarbledCircuit(c, k, 100.0, seed=seed, rescale="mrs")
-    gpu = GarbledCircuit(c, k, 100.0, seed=seed, device=0, rescale="mrs")
+    cpu = GarbledCircuit(c, k, 100.0, seed=seed, rescale="mrs", relu="approx")
+    gpu = GarbledCircuit(c, k, 100.0, seed=seed, device=0, rescale="mrs", relu="approx")
     assert gpu.model.serialize() == cpu.model.serialize()
     assert gpu.decoder.serialize() == cpu.decoder.serialize()
 

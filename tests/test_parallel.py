@@ -52,6 +52,44 @@ def test_batch_dp_gloo(world):
     assert [i for r in res for i in r[2]] == list(range(5))
 
 
+def _bench_worker(rank, world, port, q):
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank), LOCAL_WORLD_SIZE=str(world),
+                      MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    from dash_amd import benchcore
+
+    out = benchcore.run(["--backend", "cpu", "--model", "MODEL_A", "--batch", "2", "--streams", "1", "--steps", "2",
+                         "--warmup", "1", "--phases", "main,served", "--served-slots", "2", "--served-groups", "2",
+                         "--served-requests", "1"])
+    q.put((rank, out))
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_bench_driver_gloo(world):
+    """bench.py's own driver (dash_amd.benchcore) over gloo: the ranks agree on the batch, the JSON carries the
+    backend, world size and one record per rank, and every rank's outputs match the plaintext evaluation."""
+    ctx = tmp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_bench_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=600) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    out = res[0]
+    assert all(res[r] is None for r in range(1, world))
+    assert out["n_gpus"] == world and out["world_size"] == world and out["dist_backend"] == "gloo"
+    assert out["config"]["global_batch"] == 2 * world and out["config"]["parallelism"] == f"dp{world}"
+    assert [r["rank"] for r in out["ranks"]] == list(range(world))
+    assert all(r["gcs"] == 2 and r["ms_per_step"] > 0 and r["host_encode_decode_ms_per_step"] >= 0
+               for r in out["ranks"])
+    assert out["verified_vs_plaintext"] and out["served"]["verified"]
+    assert out["value"] > 0 and out["served_inf_per_s"] > 0
+    # the headline value is the whole-job rate over the slowest rank's time
+    assert abs(out["value"] - world * 2 * 2 / (out["ms_per_step"] * 2 / 1000.0)) / out["value"] < 0.01
+
+
 def test_single_process_context():
     from dash_amd.parallel import all_gather_array, init_distributed
 

@@ -34,7 +34,7 @@ def _ref(c, xs):
 def test_service_cpu_matches_plaintext(small, prefetch):
     c, xs = small
     with InferenceService(c, 8, 100.0, backend="cpu", slots_per_group=2, groups=2, prefetch=prefetch,
-                          seed=b"p" * 16) as svc:
+                          seed=b"p" * 16, insecure_fixed_seed=True) as svc:
         y = svc.infer(xs)          # 7 inputs -> 4 groups of <= 2 (pool cycles, re-garbled in the background)
         y2 = svc.infer(xs[:3])
         st = svc.stats.as_dict()
@@ -57,7 +57,7 @@ def test_service_recovers_from_integrity_failures(small):
         return bad
 
     with InferenceService(c, 8, 100.0, backend="cpu", slots_per_group=3, groups=2, fault_hook=fault,
-                          max_retries=2, seed=b"f" * 16) as svc:
+                          max_retries=2, seed=b"f" * 16, insecure_fixed_seed=True) as svc:
         y = svc.infer(xs)
         st = svc.stats.as_dict()
     np.testing.assert_array_equal(y, _ref(c, xs))
@@ -68,7 +68,7 @@ def test_service_recovers_from_integrity_failures(small):
 def test_service_gives_up_after_max_retries(small):
     c, xs = small
     with InferenceService(c, 8, 100.0, backend="cpu", slots_per_group=2, groups=1, prefetch=False,
-                          fault_hook=lambda i, a: i == 0, max_retries=1, seed=b"g" * 16) as svc:
+                          fault_hook=lambda i, a: i == 0, max_retries=1, seed=b"g" * 16, insecure_fixed_seed=True) as svc:
         with pytest.raises(d.IntegrityError):
             svc.infer(xs[:2])
         assert svc.stats.integrity_failures == 2
@@ -125,7 +125,7 @@ def _timeout_worker(rank, world, port):
 @pytest.mark.gpu
 def test_service_hip_matches_plaintext_and_recovers(small):
     c, xs = small
-    with InferenceService(c, 8, 100.0, backend="hip", slots_per_group=2, groups=2, device=0, seed=b"h" * 16,
+    with InferenceService(c, 8, 100.0, backend="hip", slots_per_group=2, groups=2, device=0, seed=b"h" * 16, insecure_fixed_seed=True,
                           fault_hook=lambda i, a: i == 2 and a == 0, step_timeout_s=60) as svc:
         y = svc.infer(xs)
         st = svc.stats.as_dict()
@@ -189,7 +189,7 @@ def test_timeout_is_not_requeued_and_close_returns(small, monkeypatch):
     import threading
 
     c, xs = small
-    svc = InferenceService(c, 8, 100.0, backend="cpu", slots_per_group=2, groups=2, seed=b"t" * 16)
+    svc = InferenceService(c, 8, 100.0, backend="cpu", slots_per_group=2, groups=2, seed=b"t" * 16, insecure_fixed_seed=True)
     hang = threading.Event()
     refills = []
 
@@ -219,7 +219,7 @@ def test_garbler_failure_wakes_every_waiter(small, monkeypatch):
     """A dead background garbler fails every later infer() promptly instead of blocking on a group that
     will never be refilled."""
     c, xs = small
-    svc = InferenceService(c, 8, 100.0, backend="cpu", slots_per_group=1, groups=3, seed=b"w" * 16)
+    svc = InferenceService(c, 8, 100.0, backend="cpu", slots_per_group=1, groups=3, seed=b"w" * 16, insecure_fixed_seed=True)
 
     def boom():
         raise OSError("garbler died")
