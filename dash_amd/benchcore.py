@@ -118,8 +118,11 @@ class _HipGroup:
         self.stream = stream
 
     def load(self, b, gc):
-        self.ev.load(b, gc.model)
+        self.ev.load(b, gc.model)  # a GC garbled into this slot (sink) only copies its small constants
         gc.model = None  # tables live in HBM now
+
+    def sink(self, b):
+        return self.ev.sink(b)
 
     def encode(self, b, gc, x):
         self.ev.encode_compressed_into(b, gc, x)
@@ -146,6 +149,9 @@ class _CpuGroup:
 
     def load(self, b, gc):
         self.models[b] = gc
+
+    def sink(self, b):
+        return None
 
     def encode(self, b, gc, x):
         self.inputs[b] = gc.garble_inputs(x)
@@ -185,15 +191,15 @@ class _Bench:
 
             self.device = torch.cuda.current_device()
 
-    # ---- one GC
-    def garble(self, tag: str, b: int, cons: dict):
+    # ---- one GC (sink: the evaluator slot the GPU garbler writes the tables into)
+    def garble(self, tag: str, b: int, cons: dict, sink=None):
         from .garbling import GarbledCircuit
 
         seed = hashlib.sha256(f"dash-bench/{tag}/{self.ctx.rank}/{b}/{os.getpid()}".encode()).digest()[:16]
         dev = self.device if (self.hip and self.args.garble_device) else None
         return GarbledCircuit(self.circuit, self.cfg["crt"], self.cfg["mrs"], seed=seed, device=dev,
                               fused_sign=cons["sign"] == "fused", rescale=cons["rescale"], relu=cons["relu"],
-                              nthreads=self.threads)
+                              nthreads=self.threads, sink=sink if dev is not None else None)
 
     # ---- offline: garble B GCs into G groups of evaluator slots
     def offline(self, tag: str, cons: dict, batch: int):
@@ -229,7 +235,8 @@ class _Bench:
         while b < B:
             try:
                 t = time.perf_counter()
-                gc = self.garble(tag, b, cons)
+                grp = groups[b // per] if b > 0 and b // per < len(groups) else None
+                gc = self.garble(tag, b, cons, sink=grp.sink(b % per) if grp is not None else None)
                 st["garble_s"] += time.perf_counter() - t
                 if b == 0:
                     if self.hip:
@@ -250,11 +257,23 @@ class _Bench:
                     G = max(1, min(G, B))
                     B -= B % G
                     per = B // G
-                    groups = groups[:G]
+                    # every group's arena up front (template: this GC), so later GCs garble straight into slots
+                    groups = []
+                    for g in range(G):
+                        try:
+                            groups.append(new_group(gc, g, per))
+                        except RuntimeError as e:  # fragmentation near full HBM: keep the groups that fit
+                            if "out of memory" not in str(e) or g == 0:
+                                raise
+                            from .native import native
+
+                            native().hip_clear_last_error()
+                            log(f"[{tag}] rank {ctx.rank}: HBM holds {g} of {G} groups")
+                            break
+                    G = len(groups)
+                    B = G * per
                 t = time.perf_counter()
                 g = b // per
-                if groups[g] is None:
-                    groups[g] = new_group(gc, g, per)
                 st["table_gb"] = gc.table_bytes / 1e9
                 groups[g].load(b % per, gc)
                 st["upload_s"] += time.perf_counter() - t

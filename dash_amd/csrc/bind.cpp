@@ -253,15 +253,18 @@ PYBIND11_MODULE(_dash_native, m) {
             return l;
         });
 
+    py::class_<TableSink, std::shared_ptr<TableSink>>(m, "TableSink");
     py::class_<Garbler, std::shared_ptr<Garbler>>(m, "Garbler")
         .def(py::init([](std::vector<int> crt, std::vector<int> mrs, py::bytes seed, int max_mod) {
                  return std::make_shared<Garbler>(crt, mrs, std::string(seed), max_mod);
              }),
              py::arg("crt"), py::arg("mrs"), py::arg("seed"), py::arg("max_mod") = 0)
         .def("garble", [](Garbler& g, const py::list& layers, std::vector<i64> in_dims, int nthreads, int device,
-                          bool fused_sign, bool rescale_mrs, bool relu_mrs, bool relu_joint) {
+                          bool fused_sign, bool rescale_mrs, bool relu_mrs, bool relu_joint,
+                          std::shared_ptr<TableSink> sink) {
             auto specs = specs_from_py(layers);
             GarbleOptions o;
+            o.sink = std::move(sink);
             o.nthreads = nthreads;
             o.device = device;
             o.fused_sign = fused_sign;
@@ -276,7 +279,7 @@ PYBIND11_MODULE(_dash_native, m) {
             return std::make_shared<GarbledModel>(std::move(gm));
         }, py::arg("layers"), py::arg("in_dims"), py::arg("nthreads") = 0, py::arg("device") = -1,
            py::arg("fused_sign") = true, py::arg("rescale_mrs") = false,
-           py::arg("relu_mrs") = false, py::arg("relu_joint") = false)
+           py::arg("relu_mrs") = false, py::arg("relu_joint") = false, py::arg("sink") = nullptr)
         .def("layer_ms", [](const Garbler& g) { return g.layer_ms(); })
         .def("encode", [](const Garbler& g, py::array_t<i64, py::array::c_style | py::array::forcecast> x) {
             std::vector<i64> v(x.data(), x.data() + x.size());

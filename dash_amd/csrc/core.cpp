@@ -50,6 +50,7 @@ struct ModTable {
             }
             m.chunk = c;
             m.pchunk = pc;
+            m.prg_m = prg_digits(p);
         }
     }
 };

@@ -51,6 +51,31 @@ inline int nr_comps(i64 p) {
     return static_cast<int>(std::floor(128.0 / std::log2(static_cast<double>(p))));
 }
 
+// Label PRG digits per AES-CTR block. The m least significant base-p digits of a
+// uniform 128-bit block are uniform on Z_p^m up to statistical distance
+// p^m / 2^128, so m is the largest count with p^m <= 2^64 (distance <= 2^-64);
+// for p = 2^b all 128 / b digits (exact). p = 7: 22 digits per block instead of
+// 2 (one 64-bit half per component), i.e. 3 AES per 45-component label, not 23.
+inline int prg_digits(i64 p) {
+    if ((p & (p - 1)) == 0) {
+        int b = 0;
+        while ((i64(1) << b) < p) ++b;
+        return 128 / b;
+    }
+    int m = 0;
+    unsigned __int128 v = 1;
+    while (v * static_cast<unsigned __int128>(p) <= (static_cast<unsigned __int128>(1) << 64)) {
+        v *= static_cast<unsigned __int128>(p);
+        ++m;
+    }
+    return m;
+}
+// AES-CTR blocks of one label
+inline int prg_blocks(i64 p) {
+    const int m = prg_digits(p);
+    return (nr_comps(p) + m - 1) / m;
+}
+
 inline i64 pmod(i64 a, i64 p) {
     i64 r = a % p;
     return r < 0 ? r + p : r;
@@ -89,6 +114,7 @@ struct ModInfo {
     u64 pchunk = 1;   // p^chunk
     bool pow2 = false;
     int bits = 0;     // log2 p when pow2
+    int prg_m = 2;    // label PRG digits per AES block (prg_digits)
 };
 
 const ModInfo& mod_info(int p);
@@ -235,13 +261,28 @@ struct Prg {
         uint8_t z[16] = {0};
         aes_expand(z, key);
     }
+    // n components of a uniform label mod p: block b = AES_seed(stream || ctr + b) gives components
+    // b*m .. b*m + m - 1 as its least significant base-p digits (m = prg_digits(p)); ctr advances by
+    // prg_blocks(p). The GPU garbler (garble_gpu.hip k_draw) produces the same digits.
     inline void label(u64 stream, u64& ctr, int p, int n, comp_t* out) const {
-        for (int j = 0; j < n; j += 2) {
+        const ModInfo& mi = mod_info(p);
+        const int m = mi.prg_m;
+        for (int j = 0; j < n; j += m) {
             u128 blk = (static_cast<u128>(stream) << 64) | ctr++;
-            u128 r = m_to_u128(aes_enc_block(u128_to_m(blk), key));
-            u64 lo = static_cast<u64>(r), hi = static_cast<u64>(r >> 64);
-            out[j] = static_cast<comp_t>(lo % static_cast<u64>(p));
-            if (j + 1 < n) out[j + 1] = static_cast<comp_t>(hi % static_cast<u64>(p));
+            u128 V = m_to_u128(aes_enc_block(u128_to_m(blk), key));
+            const int cnt = std::min(m, n - j);
+            if (mi.pow2) {
+                for (int u = 0; u < cnt; ++u, V >>= mi.bits) out[j + u] = static_cast<comp_t>(static_cast<u64>(V) & (p - 1));
+                continue;
+            }
+            for (int u = 0; u < cnt;) {
+                u64 r = static_cast<u64>(V % mi.pchunk);  // chunk of `chunk` digits
+                V /= mi.pchunk;
+                for (int c = 0; c < mi.chunk && u < cnt; ++c, ++u) {
+                    out[j + u] = static_cast<comp_t>(r % static_cast<u64>(p));
+                    r /= static_cast<u64>(p);
+                }
+            }
         }
     }
 };
@@ -307,6 +348,9 @@ struct Array {
         std::function<void(void* host, const void* dev, size_t n)> fetch;
         std::once_flag once;
         std::shared_ptr<uint8_t> host;
+        // the buffer belongs to someone else (a HIP evaluator's table arena slot the GPU garbler wrote
+        // into): `p` does not own it, and it is valid only while that slot holds this model
+        bool external = false;
     };
 
     DType dtype = DType::u8;

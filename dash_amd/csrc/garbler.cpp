@@ -364,6 +364,14 @@ GarbledModel Garbler::garble(const std::vector<LayerSpec>& layers, const std::ve
 
     std::unique_ptr<GpuGarbler> gpu;
     if (opt.device >= 0) gpu.reset(new GpuGarbler(crt_, mrs_, seed_, R_, Z_, opt.device));
+    // zero-copy offline phase: a GPU-garbled table whose destination the sink knows (an evaluator slot) is
+    // written there directly; the model's array then aliases that buffer
+    size_t cur_layer = 0;
+    auto sinkify = [&](Array& a, const std::string& name) {
+        if (!gpu || !opt.sink || !a.nbytes) return;
+        auto d = opt.sink->dest(cur_layer, name, a.nbytes);
+        if (d) a = Array::on_device(a.dtype, a.shape, std::move(d));
+    };
     // which copy of `cur` is current: GPU layers read and write the device copy,
     // host layers the host copy; a copy is refreshed only when the other side changed it
     bool host_ok = true, dev_ok = false;
@@ -450,6 +458,7 @@ GarbledModel Garbler::garble(const std::vector<LayerSpec>& layers, const std::ve
     for (size_t li = 0; li < layers.size(); ++li) {
         const auto t_layer = std::chrono::steady_clock::now();
         const LayerSpec& spec = layers[li];
+        cur_layer = li;
         const u64 L = li + 1;
         const bool sig_in = sig_next;  // the previous layer (a mixed-radix rescale) produced this ReLU's sign
         sig_next = false;
@@ -612,6 +621,8 @@ GarbledModel Garbler::garble(const std::vector<LayerSpec>& layers, const std::ve
                     // sign from the preceding rescale (RescaleMrsPlan::sign_last): mixed-modulus half gates only
                     Array tg(DType::u128, {Nin, sum_crt}), te(DType::u128, {Nin, static_cast<i64>(k), 3});
                     if (on_gpu) {
+                        sinkify(tg, "mm.g");
+                        sinkify(te, "mm.e");
                         gpu->relu_mult(L, cur, &prefix, tg, te);
                     } else {
                         DASH_CHECK(sig_host.N == Nin, "joint ReLU: sign labels missing");
@@ -639,6 +650,9 @@ GarbledModel Garbler::garble(const std::vector<LayerSpec>& layers, const std::ve
                     Array tab(DType::u128, {Nin, std::max<i64>(sp.n_tab, 1)});
                     Array tg(DType::u128, {Nin, sum_crt}), te(DType::u128, {Nin, static_cast<i64>(k), 3});
                     if (on_gpu) {
+                        sinkify(tab, "mrs");
+                        sinkify(tg, "mm.g");
+                        sinkify(te, "mm.e");
                         gpu->relu_mrs(L, sp, cur, tab, &crt_, &prefix, tg, te);
                     } else {
                         CrtLabels nxt;
@@ -670,6 +684,12 @@ GarbledModel Garbler::garble(const std::vector<LayerSpec>& layers, const std::ve
                 ReluTables t = make_relu_tables(sp, Nin, sum_crt, k);
                 CrtLabels nxt;
                 if (gpu) {
+                    sinkify(t.approx, "s.approx");
+                    sinkify(t.cast1, "s.cast1");
+                    sinkify(t.cast2, "s.cast2");
+                    sinkify(t.sign, "s.sign");
+                    sinkify(t.g, "mm.g");
+                    sinkify(t.e, "mm.e");
                     gpu->sign_layer(L, sp, cur, t.approx, t.cast1, t.cast2, t.sign, &crt_, &prefix, &t.g, &t.e);
                     put_relu_tables(g, "", t);
                     break;
@@ -699,6 +719,10 @@ GarbledModel Garbler::garble(const std::vector<LayerSpec>& layers, const std::ve
                 if (sp.has_cast1()) c1 = Array(DType::u128, {Nin, std::max<i64>(sp.n_cast, 1)});
                 CrtLabels nxt;
                 if (gpu) {
+                    sinkify(ap, "s.approx");
+                    sinkify(c1, "s.cast1");
+                    sinkify(c2, "s.cast2");
+                    sinkify(sg, "s.sign");
                     gpu->sign_layer(L, sp, cur, ap, c1, c2, sg, nullptr, nullptr, nullptr, nullptr);
                 } else {
                     for (int j = 0; j < k; ++j) nxt.emplace_back(crt_[j], Nin);
@@ -731,7 +755,10 @@ GarbledModel Garbler::garble(const std::vector<LayerSpec>& layers, const std::ve
                     const RescaleMrsPlan P(crt_, static_cast<int>(param1(spec.p, "l")), joint_out);
                     Array tab(DType::u128, {Nin, P.n_tab});
                     if (joint_out && !on_gpu) sig_host = Labels(2, Nin);
-                    if (on_gpu) gpu->rescale_mrs(L, P, cur, tab);
+                    if (on_gpu) {
+                        sinkify(tab, "mrs");
+                        gpu->rescale_mrs(L, P, cur, tab);
+                    }
                     else parallel_for(Nin, [&](i64 b0, i64 b1) {
                         std::vector<comp_t*> Lp(k);
                         for (i64 e = b0; e < b1; ++e) {
@@ -782,6 +809,11 @@ GarbledModel Garbler::garble(const std::vector<LayerSpec>& layers, const std::ve
                     }
                     if (on_gpu) {
                         DASH_CHECK(P.sign_be, "gpu garbler: legacy rescale plan without sign base extension");
+                        sinkify(tr, pre + "trans");
+                        sinkify(ap, pre + "s.approx");
+                        sinkify(c1, pre + "s.cast1");
+                        sinkify(c2, pre + "s.cast2");
+                        sinkify(sg, pre + "s.sign");
                         gpu->rescale_legacy_iter(L, static_cast<int>(it), P, cur, up_base, dn, tr, ap, c1, c2, sg);
                     } else parallel_for(Nin, [&](i64 b0, i64 b1) {
                         std::vector<comp_t*> Lp(k);

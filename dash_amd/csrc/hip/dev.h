@@ -33,6 +33,7 @@ struct ModC {
     uint32_t bits;   // log2 q if power of two, else 0
     uint32_t dm;     // digit magic: floor(r / q) = mulhi(r, dm) >> ds for r < D (host_util.h make_modc)
     uint32_t ds;
+    uint32_t pm;     // label PRG digits per AES block (core.h prg_digits)
 };
 
 __device__ __forceinline__ uint64_t mulhi64(uint64_t a, uint64_t b) { return __umul64hi(a, b); }

@@ -38,6 +38,10 @@ using namespace hostutil;
 
 namespace gg {
 
+// The garbling stream of the calling thread (DevCtx::st, set by every GpuGarbler entry point): a
+// non-blocking stream per device, so garbling never synchronizes with evaluation streams.
+thread_local hipStream_t tl_st = nullptr;
+
 constexpr int kW = 128;  // label slot width (max components)
 
 // label reference kinds
@@ -114,16 +118,12 @@ __device__ __forceinline__ u128 aes_keyed(const AesCtx& a, u128 in, const uint32
            ((static_cast<uint64_t>(bswap32(o1)) << 32) | bswap32(o0));
 }
 
-// Prg::label (core.h): two components per AES-CTR block
-__device__ __forceinline__ void prg_label(const AesCtx& a, const uint32_t* rk, uint64_t stream, uint64_t ctr,
-                                          const ModC& m, int16_t* out) {
-    const int n = static_cast<int>(m.n);
-    for (int j = 0; j < n; j += 2) {
-        const u128 blk = (static_cast<u128>(stream) << 64) | (ctr + static_cast<uint64_t>(j >> 1));
-        const u128 r = aes_keyed(a, blk, rk);
-        out[j] = static_cast<int16_t>(modq64(static_cast<uint64_t>(r), m));
-        if (j + 1 < n) out[j + 1] = static_cast<int16_t>(modq64(static_cast<uint64_t>(r >> 64), m));
-    }
+// Prg::label (core.h): block b of a label = AES_seed(stream || ctr + b); its m = ModC::pm least significant
+// base-q digits are components b*m .. b*m + m - 1
+__device__ __forceinline__ void prg_digits(u128 V, const ModC& m, int cnt, int16_t* out) {
+    DigitStream ds;
+    ds.init(V);
+    for (int u = 0; u < cnt; ++u) out[u] = static_cast<int16_t>(ds.next(m));
 }
 
 __device__ __forceinline__ uint64_t stream_of(uint64_t layer, uint64_t slot, uint64_t e, uint64_t mask) {
@@ -144,6 +144,7 @@ struct Gadget {
     int mrs[kMaxMrs]; // MRS base of the sign gadget (per-digit output moduli of the fanned-out approx projections)
     const int16_t* flut;  // F_FAN: payload values [a0 + i * stride + target] (reduced mod the target modulus)
     const int* fan;       // F_FAN: target moduli [a1 + target]
+    const int* fbank;     // F_FAN: [a1 + target] 1 + payload bank row of value 0 (k_payloads), 0: computed inline
 };
 
 // Stage a gadget's small descriptor array (draws / projections) in LDS so the
@@ -158,9 +159,10 @@ __device__ __forceinline__ void lds_stage(T* dst, const T* src, int n) {
     for (int i = threadIdx.x; i < words; i += blockDim.x) d[i] = s[i];
 }
 
-// one thread per (element, AES-CTR block): each block yields two label
-// components of one draw (Prg::label order), so neighbouring lanes write
-// neighbouring components and every lane does exactly one AES.
+// one thread per (element, AES-CTR block): each block yields ModC::pm
+// consecutive components of one draw (Prg::label order), extracted as the
+// base-q digits of the block (DigitStream: one 128-bit long division per
+// chunk of digits), so every lane does exactly one AES.
 __global__ __launch_bounds__(kGB) void k_draw(Ctx c, Gadget g) {
     __shared__ __attribute__((aligned(16))) uint32_t lds_aes[DASH_AES_LDS_WORDS];
     __shared__ Draw sd[kMaxDesc];
@@ -180,17 +182,11 @@ __global__ __launch_bounds__(kGB) void k_draw(Ctx c, Gadget g) {
         }
         const Draw d = sd[lo];
         const ModC m = c.mc[d.q];
-        const int j = 2 * (b - d.ctr);
+        const int j = static_cast<int>(m.pm) * (b - d.ctr);
+        const int cnt = min(static_cast<int>(m.pm), static_cast<int>(m.n) - j);
         const uint64_t stream = stream_of(g.layer, g.sslot, static_cast<uint64_t>(e), g.mask);
         const u128 r = aes_keyed(aes, (static_cast<u128>(stream) << 64) | static_cast<uint64_t>(b), c.rk);
-        const uint32_t v0 = modq64(static_cast<uint64_t>(r), m);
-        int16_t* out = g.S + (e * g.nslots + d.slot) * kW + j;
-        if (j + 1 < static_cast<int>(m.n)) {
-            const uint32_t v1 = modq64(static_cast<uint64_t>(r >> 64), m);
-            *reinterpret_cast<uint32_t*>(out) = v0 | (v1 << 16);
-        } else {
-            out[0] = static_cast<int16_t>(v0);
-        }
+        prg_digits(r, m, cnt, g.S + (e * g.nslots + d.slot) * kW + j);
     }
 }
 
@@ -378,6 +374,7 @@ __device__ __forceinline__ ModC rfl_modc(const ModC& m) {
     r.bits = rflu(m.bits);
     r.dm = rflu(m.dm);
     r.ds = rflu(m.ds);
+    r.pm = rflu(m.pm);
     return r;
 }
 __device__ __forceinline__ Proj rfl_proj(const Proj& p) {
@@ -453,11 +450,18 @@ __global__ __launch_bounds__(kPB) void k_project(Ctx c, Gadget g, In in, Tables 
             const int t = P.stride;
             u128* row = tb.t[P.table] + e * tb.row[P.table] + P.off + static_cast<int64_t>(color) * t;
             for (int d = 0; d < t; ++d) {
-                const int pout = rfl(g.fan[P.a1 + d]);
-                const ModC md = rfl_modc(c.mc[pout]);
                 const uint32_t cm = static_cast<uint32_t>(rfl(g.flut[P.a0 + i * t + d]));
-                const int16_t* ol = g.S + (e * g.nslots + P.out_slot + d) * kW;
-                const u128 pay = proj_payload(ol, c.R + static_cast<int64_t>(pout) * kW, cm, md);
+                const int bk = g.fbank ? rfl(g.fbank[P.a1 + d]) : 0;
+                u128 pay;
+                if (bk) {
+                    // few distinct values (e.g. the rescale's final projection: T = 2^(l+1) entries, p_j values)
+                    pay = g.PB[static_cast<int64_t>(bk - 1 + static_cast<int>(cm)) * N + e];
+                } else {
+                    const int pout = rfl(g.fan[P.a1 + d]);
+                    const ModC md = rfl_modc(c.mc[pout]);
+                    const int16_t* ol = g.S + (e * g.nslots + P.out_slot + d) * kW;
+                    pay = proj_payload(ol, c.R + static_cast<int64_t>(pout) * kW, cm, md);
+                }
                 if (e_raw < N) row[d] = pay + H;
             }
             continue;
@@ -763,20 +767,21 @@ __global__ __launch_bounds__(kGB) void k_rescale_pre(Ctx c, RsArgs a, Tables tb,
         CompressFwd p0, p1;
         p0.init();
         p1.init();
-        for (int q = 0; q < n; q += 2) {
-            const u128 r = aes_keyed(aes, (static_cast<u128>(stream) << 64) | static_cast<uint64_t>(a.ctr[j] + (q >> 1)),
-                                     c.rk);
-#pragma unroll
-            for (int h = 0; h < 2; ++h) {
-                if (q + h >= n) break;
-                const uint32_t o = modq64(static_cast<uint64_t>(h ? r >> 64 : r), mj);
+        const int pm = static_cast<int>(mj.pm);
+        for (int q0 = 0, blk = 0; q0 < n; q0 += pm, ++blk) {
+            DigitStream ds;
+            ds.init(aes_keyed(aes, (static_cast<u128>(stream) << 64) | static_cast<uint64_t>(a.ctr[j] + blk), c.rk));
+            const int cnt = min(pm, n - q0);
+            for (int h = 0; h < cnt; ++h) {
+                const int q = q0 + h;
+                const uint32_t o = ds.next(mj);
                 p0.push(o, mj);
-                p1.push(modq(o + static_cast<uint32_t>(Rp[q + h]), mj), mj);
-                int v = L[q + h] + upj[q + h];
+                p1.push(modq(o + static_cast<uint32_t>(Rp[q]), mj), mj);
+                int v = L[q] + upj[q];
                 if (v >= p) v -= p;
                 v -= static_cast<int>(o);
                 if (v < 0) v += p;
-                L[q + h] = static_cast<int16_t>(modq(static_cast<uint32_t>(v * a.inv[j]), mj));
+                L[q] = static_cast<int16_t>(modq(static_cast<uint32_t>(v * a.inv[j]), mj));
             }
         }
         u128* row = tb.t[6] + e * tb.row[6] + (j - 1) * 2;
@@ -901,7 +906,7 @@ SignLayout sign_layout_fused(const SignPlan& P, int extra_slots) {
     int slot = 0, ctr = 0;
     auto draw = [&](int q) {
         L.draws.push_back({slot, q, ctr});
-        ctr += (nr_comps(q) + 1) / 2;
+        ctr += prg_blocks(q);
         return slot++;
     };
     const int dig0 = slot;
@@ -963,7 +968,7 @@ SignLayout sign_layout(const SignPlan& P, int extra_slots) {
     int slot = 0, ctr = 0;
     auto draw = [&](int q) {
         L.draws.push_back({slot, q, ctr});
-        ctr += (nr_comps(q) + 1) / 2;
+        ctr += prg_blocks(q);
         return slot++;
     };
     const int mrs0 = slot;
@@ -1046,15 +1051,6 @@ SignLayout sign_layout(const SignPlan& P, int extra_slots) {
                                 P.lower, P.upper, R_BANK, 0, 3, 1, static_cast<int64_t>(o) * m0, 0}));
     L.entries = first;
     return L;
-}
-
-template <class T>
-T* dput(const T* h, size_t n, std::vector<void*>& owned) {
-    T* d = nullptr;
-    HIPCHECK(hipMalloc(reinterpret_cast<void**>(&d), std::max<size_t>(1, n) * sizeof(T)));
-    if (n) HIPCHECK(hipMemcpy(d, h, n * sizeof(T), hipMemcpyHostToDevice));
-    owned.push_back(d);
-    return d;
 }
 
 // Structure-only device constants (gadget descriptors, public conv weights):
@@ -1177,11 +1173,12 @@ inline unsigned blocks_for(int64_t n, int bs, int cap = 65536) {
     return static_cast<unsigned>(std::max<int64_t>(1, std::min<int64_t>((n + bs - 1) / bs, cap)));
 }
 
-// a cached device block with RAII return to the cache
+// a cached device block with RAII return to the cache (or a borrowed buffer: never cached or freed)
 struct DevBlock {
     void* p = nullptr;
     size_t bytes = 0;
     int device = 0;
+    bool borrowed = false;
     DevBlock() = default;
     DevBlock(const DevBlock&) = delete;
     DevBlock& operator=(const DevBlock&) = delete;
@@ -1191,6 +1188,7 @@ struct DevBlock {
         p = o.p;
         bytes = o.bytes;
         device = o.device;
+        borrowed = o.borrowed;
         o.p = nullptr;
         return *this;
     }
@@ -1199,10 +1197,18 @@ struct DevBlock {
         release();
         device = dev;
         bytes = std::max<size_t>(16, b);
+        borrowed = false;
         p = cache_get(dev, bytes);
     }
+    void borrow(int dev, void* q, size_t b) {
+        release();
+        device = dev;
+        bytes = b;
+        borrowed = true;
+        p = q;
+    }
     void release() {
-        if (p) cache_put(device, p, bytes);
+        if (p && !borrowed) cache_put(device, p, bytes);
         p = nullptr;
     }
     template <class T>
@@ -1216,17 +1222,30 @@ struct DevTable {
     int64_t row = 0;
     // zero: only for tables whose entries are not all written by the kernels (the ReLU e table's
     // mini entry fills 2 of its 8 int16 slots); every other table is fully covered, since the
-    // colors of a projection's p keys are a permutation of Z_p (R[0] = 1)
-    void alloc(int device, int64_t N, int64_t r, bool zero = false) {
+    // colors of a projection's p keys are a permutation of Z_p (R[0] = 1).
+    // target: the model array this table becomes; when it already names an external device buffer
+    // (GarbleOptions::sink: an evaluator's arena slot) the kernels write there directly.
+    void alloc(int device, int64_t N, int64_t r, const Array& target, bool zero = false) {
         row = r;
-        b.alloc(device, static_cast<size_t>(N) * r * sizeof(u128));
-        if (zero) HIPCHECK(hipMemsetAsync(b.p, 0, b.bytes, nullptr));
+        const size_t bytes = static_cast<size_t>(N) * r * sizeof(u128);
+        if (target.device_resident() && target.dev->external) {
+            DASH_CHECK(target.nbytes == bytes && target.dev->device == device, "gpu garbler: table sink size mismatch");
+            b.borrow(device, const_cast<void*>(target.device_ptr()), bytes);
+        } else {
+            b.alloc(device, bytes);
+        }
+        if (zero) HIPCHECK(hipMemsetAsync(b.p, 0, b.bytes, gg::tl_st));
     }
     u128* p() const { return b.as<u128>(); }
     // hand the buffer to `a` as a device-resident array (kept in HBM; the
     // evaluator on this node copies it device-to-device). Its deleter returns
-    // the block to the cache.
+    // the block to the cache. A borrowed (sink) buffer already is `a`'s.
     void to_array(Array& a, int device) {
+        if (b.borrowed) {
+            DASH_CHECK(a.device_ptr() == b.p, "gpu garbler: sink table rebound");
+            b.p = nullptr;
+            return;
+        }
         DASH_CHECK(a.nbytes <= b.bytes && (a.nbytes == static_cast<size_t>(b.bytes) || a.nbytes < 16),
                    "gpu garbler: table size mismatch");
         auto d = std::make_shared<Array::Device>();
@@ -1245,7 +1264,7 @@ struct DevTable {
 // AES-CTR blocks per element: draws are laid out back to back in counter order
 int draw_blocks(const std::vector<gg::Draw>& d) {
     if (d.empty()) return 0;
-    return d.back().ctr + (nr_comps(d.back().q) + 1) / 2;
+    return d.back().ctr + prg_blocks(d.back().q);
 }
 
 void check_desc(const gg::Gadget& g) {
@@ -1264,15 +1283,15 @@ void run_sign(const gg::Ctx& c, const gg::SignLayout& L, gg::Gadget& g, const gg
     g.nblk = draw_blocks(L.draws);
     for (int d = 0; d < L.ss.t; ++d) g.mrs[d] = L.fan[d];
     check_desc(g);
-    hipLaunchKernelGGL(gg::k_draw, dim3(blocks_for(g.N * g.nblk, gg::kGB, 8192)), dim3(gg::kGB), 0, nullptr, c, g);
-    hipLaunchKernelGGL(gg::k_sign_derive, dim3(blocks_for(g.N, 256)), dim3(256), 0, nullptr, c, g, L.ss);
+    hipLaunchKernelGGL(gg::k_draw, dim3(blocks_for(g.N * g.nblk, gg::kGB, 8192)), dim3(gg::kGB), 0, gg::tl_st, c, g);
+    hipLaunchKernelGGL(gg::k_sign_derive, dim3(blocks_for(g.N, 256)), dim3(256), 0, gg::tl_st, c, g, L.ss);
     if (!L.pays.empty()) {
         DASH_CHECK(g.PB != nullptr, "gpu garbler: payload bank not allocated");
         const gg::PayDesc* pd = gg::dconst(L.pays.data(), L.pays.size());
         const int npd = static_cast<int>(L.pays.size());
-        hipLaunchKernelGGL(gg::k_payloads, dim3(blocks_for(g.N * npd, 256, 16384)), dim3(256), 0, nullptr, c, g, pd, npd);
+        hipLaunchKernelGGL(gg::k_payloads, dim3(blocks_for(g.N * npd, 256, 16384)), dim3(256), 0, gg::tl_st, c, g, pd, npd);
     }
-    hipLaunchKernelGGL(gg::k_project, dim3(blocks_for((g.N + 63) / 64 * 64 * g.entries, gg::kPB, 16384)), dim3(gg::kPB), 0, nullptr, c,
+    hipLaunchKernelGGL(gg::k_project, dim3(blocks_for((g.N + 63) / 64 * 64 * g.entries, gg::kPB, 16384)), dim3(gg::kPB), 0, gg::tl_st, c,
                        g, in, tb);
     HIPCHECK(hipGetLastError());
 }
@@ -1296,18 +1315,107 @@ namespace gg {
 // DASH_GG_SYNC=1 restores per-layer syncs (exact per-layer garbling timers).
 inline void end_layer(std::vector<void*>& tmp) {
     static const bool sync = std::getenv("DASH_GG_SYNC") != nullptr;
-    if (sync || !tmp.empty()) HIPCHECK(hipDeviceSynchronize());
+    if (sync || !tmp.empty()) HIPCHECK(hipStreamSynchronize(tl_st));
     for (void* p : tmp) (void)hipFree(p);
     tmp.clear();
 }
 }  // namespace gg
 
-struct GpuGarbler::Impl {
-    gg::Ctx c{};
-    std::vector<void*> owned;
-    // grow-only gadget scratch (label slots) reused by every layer
+// Per-device garbling context, shared by every GpuGarbler of the process: the non-blocking garbling stream,
+// modulus constants and AES table, the pinned staging ring and the grow-only gadget scratch. A GpuGarbler
+// holds the context's lock for its lifetime (one garbling per device at a time; concurrent GarbledCircuit
+// constructions on one device queue up), so the per-GC setup is a few async copies: no allocation, no
+// device-wide synchronization, nothing that would stall or serialize the evaluator's streams.
+struct DevCtx {
+    std::mutex m;
+    int device = 0;
+    hipStream_t st = nullptr;
+    dev::ModC* mc = nullptr;
+    int mc_max = 0;
+    uint32_t* te0 = nullptr;
+    // pinned staging + device ring for per-GC uploads (R, Z, shift labels), copied asynchronously on st
+    static constexpr size_t kRing = 8u << 20;
+    char* ring_h = nullptr;
+    char* ring_d = nullptr;
+    size_t ring_off = 0;
+    // grow-only gadget scratch (label slots) and payload bank reused by every layer and GC
     int16_t* S = nullptr;
     size_t S_bytes = 0;
+    u128* PB = nullptr;
+    size_t PB_bytes = 0;
+    void init(int dev) {
+        device = dev;
+        HIPCHECK(hipSetDevice(dev));
+        HIPCHECK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+        HIPCHECK(hipHostMalloc(reinterpret_cast<void**>(&ring_h), kRing));
+        HIPCHECK(hipMalloc(reinterpret_cast<void**>(&ring_d), kRing));
+        auto te = make_te0();
+        HIPCHECK(hipMalloc(reinterpret_cast<void**>(&te0), te.size() * sizeof(uint32_t)));
+        HIPCHECK(hipMemcpy(te0, te.data(), te.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
+    }
+    // ModC table covering moduli up to max_mod (grows; rebuilt on the stream, waited for before reuse)
+    const dev::ModC* modc(int max_mod) {
+        if (max_mod > mc_max) {
+            HIPCHECK(hipStreamSynchronize(st));  // earlier kernels may still read the old table
+            if (mc) HIPCHECK(hipFree(mc));
+            std::vector<dev::ModC> h(max_mod + 1);
+            for (int q = 2; q <= max_mod; ++q) h[q] = make_modc(q);
+            HIPCHECK(hipMalloc(reinterpret_cast<void**>(&mc), h.size() * sizeof(dev::ModC)));
+            HIPCHECK(hipMemcpy(mc, h.data(), h.size() * sizeof(dev::ModC), hipMemcpyHostToDevice));
+            mc_max = max_mod;
+        }
+        return mc;
+    }
+    template <class T>
+    const T* stage(const T* h, size_t n) {
+        const size_t bytes = (n * sizeof(T) + 255) / 256 * 256;
+        DASH_CHECK(bytes <= kRing, "gpu garbler: staging ring too small");
+        if (ring_off + bytes > kRing) {  // wrap: earlier copies must have landed before their staging is reused
+            HIPCHECK(hipStreamSynchronize(st));
+            ring_off = 0;
+        }
+        std::memcpy(ring_h + ring_off, h, n * sizeof(T));
+        HIPCHECK(hipMemcpyAsync(ring_d + ring_off, ring_h + ring_off, n * sizeof(T), hipMemcpyHostToDevice, st));
+        const T* d = reinterpret_cast<const T*>(ring_d + ring_off);
+        ring_off += bytes;
+        return d;
+    }
+    int16_t* scratch(size_t bytes) {
+        if (bytes > S_bytes) {
+            HIPCHECK(hipStreamSynchronize(st));
+            if (S) (void)hipFree(S);
+            HIPCHECK(hipMalloc(reinterpret_cast<void**>(&S), bytes));
+            S_bytes = bytes;
+        }
+        return S;
+    }
+    u128* pbank(size_t rows, int64_t N) {
+        const size_t bytes = std::max<size_t>(16, rows * static_cast<size_t>(N) * sizeof(u128));
+        if (bytes > PB_bytes) {
+            HIPCHECK(hipStreamSynchronize(st));
+            if (PB) (void)hipFree(PB);
+            HIPCHECK(hipMalloc(reinterpret_cast<void**>(&PB), bytes));
+            PB_bytes = bytes;
+        }
+        return PB;
+    }
+};
+DevCtx& dev_ctx(int device) {
+    static std::mutex m;
+    static std::map<int, DevCtx*>* ctxs = new std::map<int, DevCtx*>();  // leaked: lives as long as the process
+    std::lock_guard<std::mutex> g(m);
+    auto it = ctxs->find(device);
+    if (it != ctxs->end()) return *it->second;
+    DevCtx* c = new DevCtx();
+    c->init(device);
+    (*ctxs)[device] = c;
+    return *c;
+}
+
+struct GpuGarbler::Impl {
+    DevCtx& dc;
+    std::unique_lock<std::mutex> lock;
+    gg::Ctx c{};
     // device cur: per residue label-major [N][n_j]
     std::vector<DevBlock> cur;
     std::vector<int> cur_mod;
@@ -1319,49 +1427,11 @@ struct GpuGarbler::Impl {
     // sign base labels a sign_last mixed-radix rescale leaves for the next ReLU ([N][kW], relu_mult)
     DevBlock sig;
     int64_t sig_N = 0;
-    // per-GC small uploads (up/down shift labels): pinned staging + device ring, copied asynchronously on the
-    // garbling stream (no queue drain); one garble() uses far less than the ring, which restarts per GpuGarbler
-    static constexpr size_t kRing = 8u << 20;
-    char* ring_h = nullptr;
-    char* ring_d = nullptr;
-    size_t ring_off = 0;
+    explicit Impl(int dev) : dc(dev_ctx(dev)), lock(dc.m), device(dev) {}
     template <class T>
-    const T* stage(const T* h, size_t n) {
-        const size_t bytes = (n * sizeof(T) + 255) / 256 * 256;
-        if (!ring_h) {
-            HIPCHECK(hipHostMalloc(reinterpret_cast<void**>(&ring_h), kRing));
-            HIPCHECK(hipMalloc(reinterpret_cast<void**>(&ring_d), kRing));
-        }
-        if (ring_off + bytes > kRing) {  // wrap: earlier copies must have landed before their staging is reused
-            HIPCHECK(hipStreamSynchronize(nullptr));
-            ring_off = 0;
-        }
-        std::memcpy(ring_h + ring_off, h, n * sizeof(T));
-        HIPCHECK(hipMemcpyAsync(ring_d + ring_off, ring_h + ring_off, n * sizeof(T), hipMemcpyHostToDevice, nullptr));
-        const T* d = reinterpret_cast<const T*>(ring_d + ring_off);
-        ring_off += bytes;
-        return d;
-    }
-    int16_t* scratch(size_t bytes) {
-        if (bytes > S_bytes) {
-            if (S) (void)hipFree(S);
-            HIPCHECK(hipMalloc(reinterpret_cast<void**>(&S), bytes));
-            S_bytes = bytes;
-        }
-        return S;
-    }
-    // grow-only payload bank (k_payloads), same lifetime rules as S
-    u128* PB = nullptr;
-    size_t PB_bytes = 0;
-    u128* pbank(size_t rows, int64_t N) {
-        const size_t bytes = std::max<size_t>(16, rows * static_cast<size_t>(N) * sizeof(u128));
-        if (bytes > PB_bytes) {
-            if (PB) (void)hipFree(PB);
-            HIPCHECK(hipMalloc(reinterpret_cast<void**>(&PB), bytes));
-            PB_bytes = bytes;
-        }
-        return PB;
-    }
+    const T* stage(const T* h, size_t n) { return dc.stage(h, n); }
+    int16_t* scratch(size_t bytes) { return dc.scratch(bytes); }
+    u128* pbank(size_t rows, int64_t N) { return dc.pbank(rows, N); }
     std::vector<DevBlock> alloc_labels(const std::vector<int>& mods, int64_t N) {
         std::vector<DevBlock> v(mods.size());
         for (size_t j = 0; j < mods.size(); ++j)
@@ -1373,23 +1443,23 @@ struct GpuGarbler::Impl {
                    "gpu garbler: device labels out of sync with the host garbler");
         for (size_t j = 0; j < host.size(); ++j) DASH_CHECK(host[j].p == cur_mod[j], "gpu garbler: modulus mismatch");
     }
+    void enter() {
+        HIPCHECK(hipSetDevice(device));
+        gg::tl_st = dc.st;
+    }
     ~Impl() {
-        (void)hipDeviceSynchronize();  // garble() returns with every table written
+        // garble() returns with every table written; blocks released below are reused in stream order
+        (void)hipStreamSynchronize(dc.st);
         cur.clear();
-        for (void* p : owned) (void)hipFree(p);
-        if (S) (void)hipFree(S);
-        if (PB) (void)hipFree(PB);
-        if (ring_h) (void)hipHostFree(ring_h);
-        if (ring_d) (void)hipFree(ring_d);
+        sig = DevBlock();
     }
 };
 
 GpuGarbler::GpuGarbler(const std::vector<int>& crt, const std::vector<int>& mrs, const std::string& seed16,
                        const LabelBank& R, const LabelBank& Z, int device)
-    : impl_(new Impl) {
-    HIPCHECK(hipSetDevice(device));
+    : impl_(new Impl(device)) {
     Impl& I = *impl_;
-    I.device = device;
+    I.enter();
     I.crt = crt;
     I.k = static_cast<int>(crt.size());
     I.max_mod = R.max_mod;
@@ -1399,13 +1469,10 @@ GpuGarbler::GpuGarbler(const std::vector<int>& crt, const std::vector<int>& mrs,
         std::copy(R.lab[p].begin(), R.lab[p].end(), hR.begin() + p * gg::kW);
         std::copy(Z.lab[p].begin(), Z.lab[p].end(), hZ.begin() + p * gg::kW);
     }
-    I.c.R = gg::dput(hR.data(), hR.size(), I.owned);
-    I.c.Z = gg::dput(hZ.data(), hZ.size(), I.owned);
-    std::vector<dev::ModC> mc(R.max_mod + 1);
-    for (int q = 2; q <= R.max_mod; ++q) mc[q] = make_modc(q);
-    I.c.mc = gg::dput(mc.data(), mc.size(), I.owned);
-    auto te = make_te0();
-    I.c.te0 = gg::dput(te.data(), te.size(), I.owned);
+    I.c.R = I.stage(hR.data(), hR.size());
+    I.c.Z = I.stage(hZ.data(), hZ.size());
+    I.c.mc = I.dc.modc(R.max_mod);
+    I.c.te0 = I.dc.te0;
     auto rk = round_key_words(reinterpret_cast<const uint8_t*>(seed16.data()));
     std::copy(rk.begin(), rk.end(), I.c.rk);
     if (!mrs.empty()) {
@@ -1415,17 +1482,17 @@ GpuGarbler::GpuGarbler(const std::vector<int>& crt, const std::vector<int>& mrs,
             I.c.lut_off[j] = static_cast<int>(flat.size());
             flat.insert(flat.end(), lut[j].begin(), lut[j].end());
         }
-        I.c.lut = gg::dput(flat.data(), flat.size(), I.owned);
+        I.c.lut = gg::dconst(flat.data(), flat.size());
     }
 }
 
 GpuGarbler::~GpuGarbler() {
-    if (impl_) (void)hipSetDevice(impl_->device);
+    if (impl_) impl_->enter();
 }
 
 void GpuGarbler::to_device(const CrtLabels& cur) {
     Impl& I = *impl_;
-    HIPCHECK(hipSetDevice(I.device));
+    I.enter();
     DASH_CHECK(!cur.empty(), "gpu garbler: no labels");
     I.cur_mod.clear();
     for (const auto& l : cur) I.cur_mod.push_back(l.p);
@@ -1433,19 +1500,22 @@ void GpuGarbler::to_device(const CrtLabels& cur) {
     I.cur = I.alloc_labels(I.cur_mod, I.cur_N);
     for (size_t j = 0; j < cur.size(); ++j) {
         DASH_CHECK(cur[j].c.size() == static_cast<size_t>(cur[j].N) * cur[j].n, "gpu garbler: host labels are stale");
-        HIPCHECK(hipMemcpy(I.cur[j].p, cur[j].c.data(), cur[j].c.size() * sizeof(int16_t), hipMemcpyHostToDevice));
+        // pageable source: the copy is staged before the call returns, ordered on the garbling stream
+        HIPCHECK(hipMemcpyAsync(I.cur[j].p, cur[j].c.data(), cur[j].c.size() * sizeof(int16_t), hipMemcpyHostToDevice,
+                                gg::tl_st));
     }
 }
 
 void GpuGarbler::to_host(CrtLabels& cur) {
     Impl& I = *impl_;
-    HIPCHECK(hipSetDevice(I.device));
+    I.enter();
     I.check_cur(cur);
-    HIPCHECK(hipDeviceSynchronize());
     for (size_t j = 0; j < cur.size(); ++j) {
         cur[j].c.resize(static_cast<size_t>(cur[j].N) * cur[j].n);
-        HIPCHECK(hipMemcpy(cur[j].c.data(), I.cur[j].p, cur[j].c.size() * sizeof(int16_t), hipMemcpyDeviceToHost));
+        HIPCHECK(hipMemcpyAsync(cur[j].c.data(), I.cur[j].p, cur[j].c.size() * sizeof(int16_t), hipMemcpyDeviceToHost,
+                                gg::tl_st));
     }
+    HIPCHECK(hipStreamSynchronize(gg::tl_st));
 }
 
 // Conv base labels = the evaluator's garbled conv applied to the zero labels:
@@ -1457,7 +1527,7 @@ void GpuGarbler::to_host(CrtLabels& cur) {
 // DASH_GG_CONV=valu selects the label-major VALU kernel (A/B).
 void GpuGarbler::conv(const ConvGeom& G, const std::vector<i64>& w, CrtLabels& cur) {
     Impl& I = *impl_;
-    HIPCHECK(hipSetDevice(I.device));
+    I.enter();
     I.check_cur(cur);
     PhaseTrace tr_("conv");
     const int K = static_cast<int>(G.K());
@@ -1495,7 +1565,7 @@ void GpuGarbler::conv(const ConvGeom& G, const std::vector<i64>& w, CrtLabels& c
             const int64_t threads = G.OH * G.OW * static_cast<int64_t>(g.n);
             DASH_CHECK((threads + 255) / 256 < (int64_t(1) << 31), "gpu garbler: conv grid too large");
             hipLaunchKernelGGL(gg::k_conv_garble, dim3(static_cast<unsigned>((threads + 255) / 256), nch), dim3(256), 0,
-                               nullptr, g, I.cur[j].as<int16_t>(), out[j].as<int16_t>(), dw, dz,
+                               gg::tl_st, g, I.cur[j].as<int16_t>(), out[j].as<int16_t>(), dw, dz,
                                I.c.Z + static_cast<int64_t>(p) * gg::kW);
         }
     } else {
@@ -1516,9 +1586,7 @@ void GpuGarbler::conv(const ConvGeom& G, const std::vector<i64>& w, CrtLabels& c
         a.use_mfma = 1;
         int max_p = 0;
         for (int j = 0; j < a.crt.k; ++j) max_p = std::max(max_p, mods[j]);
-        dev::conv_unroll_taps(a, max_p);
-        dev::conv_img_geometry(a);
-        DASH_CHECK(!a.ur || a.nbands > 0, "gpu garbler: tap-unrolled conv without an LDS band");
+        dev::conv_plan(a, max_p, true);
         a.zero = I.c.Z;  // one GC: zero label component c of residue j at Z[p_j * kW + c]
         a.lab_stride = 0;
         a.img_off[0] = 0;
@@ -1554,17 +1622,26 @@ void GpuGarbler::conv(const ConvGeom& G, const std::vector<i64>& w, CrtLabels& c
         dev::Act x{}, y{};
         x.N = Nin;
         y.N = Nout;
+        dev::TrRes ti{}, to{};
+        ti.k = to.k = a.crt.k;
         for (int j = 0; j < a.crt.k; ++j) {
             DASH_CHECK(mods[j] <= dev::kActMaxModulus, "gpu garbler: conv residue modulus above 255");
             xin[j].alloc(I.device, static_cast<size_t>(Nin) * a.crt.n[j]);
             yout[j].alloc(I.device, static_cast<size_t>(Nout) * a.crt.n[j]);
-            dev::launch_transpose_to_act(I.cur[j].as<int16_t>(), xin[j].as<dev::act_t>(), Nin, a.crt.n[j], nullptr);
+            ti.in[j] = I.cur[j].as<int16_t>();
+            ti.out[j] = xin[j].as<dev::act_t>();
+            ti.rows[j] = Nin;
+            ti.cols[j] = a.crt.n[j];
+            to.in[j] = yout[j].as<dev::act_t>();
+            to.out[j] = out[j].as<int16_t>();
+            to.rows[j] = a.crt.n[j];
+            to.cols[j] = Nout;
             x.p[j] = xin[j].as<dev::act_t>();
             y.p[j] = yout[j].as<dev::act_t>();
         }
-        dev::launch_conv(a, x, y, 1, nullptr);
-        for (int j = 0; j < a.crt.k; ++j)
-            dev::launch_transpose_from_act(yout[j].as<dev::act_t>(), out[j].as<int16_t>(), a.crt.n[j], Nout, nullptr);
+        dev::launch_transpose_to_act_res(ti, gg::tl_st);  // all residues in one launch
+        dev::launch_conv(a, x, y, 1, gg::tl_st);
+        dev::launch_transpose_from_act_res(to, gg::tl_st);
         // xin / yout return to the block cache; later users are ordered behind these kernels on the null stream
     }
     HIPCHECK(hipGetLastError());
@@ -1579,7 +1656,7 @@ void GpuGarbler::sign_layer(uint64_t layer, const SignPlan& sp, CrtLabels& cur, 
                             Array& sg, const std::vector<int>* relu_crt, const std::vector<i64>* prefix, Array* mmg,
                             Array* mme) {
     Impl& I = *impl_;
-    HIPCHECK(hipSetDevice(I.device));
+    I.enter();
     I.check_cur(cur);
     PhaseTrace tr_(relu_crt ? "relu" : "sign");
     const int64_t N = I.cur_N;
@@ -1591,18 +1668,18 @@ void GpuGarbler::sign_layer(uint64_t layer, const SignPlan& sp, CrtLabels& cur, 
     int sk0 = L.nslots - (relu ? 2 * k : 0);
     int16_t* S = I.scratch(static_cast<size_t>(N) * L.nslots * gg::kW * sizeof(int16_t));
     DevTable tA, t1, t2, tS, tG, tE;
-    tA.alloc(I.device, N, ap.shape[1]);
-    if (sp.has_cast1()) t1.alloc(I.device, N, c1.shape[1]);
-    t2.alloc(I.device, N, c2.shape[1]);
-    tS.alloc(I.device, N, sg.shape[1]);
+    tA.alloc(I.device, N, ap.shape[1], ap);
+    if (sp.has_cast1()) t1.alloc(I.device, N, c1.shape[1], c1);
+    t2.alloc(I.device, N, c2.shape[1], c2);
+    tS.alloc(I.device, N, sg.shape[1], sg);
     gg::Tables tb{};
     tb.t[0] = tA.p(); tb.row[0] = tA.row;
     tb.t[1] = t1.p(); tb.row[1] = t1.row;
     tb.t[2] = t2.p(); tb.row[2] = t2.row;
     tb.t[3] = tS.p(); tb.row[3] = tS.row;
     if (relu) {
-        tG.alloc(I.device, N, mmg->shape[1]);
-        tE.alloc(I.device, N, static_cast<int64_t>(k) * 3, true);
+        tG.alloc(I.device, N, mmg->shape[1], *mmg);
+        tE.alloc(I.device, N, static_cast<int64_t>(k) * 3, *mme, true);
         tb.t[4] = tG.p(); tb.row[4] = tG.row;
         tb.t[5] = tE.p(); tb.row[5] = tE.row;
     }
@@ -1632,9 +1709,9 @@ void GpuGarbler::sign_layer(uint64_t layer, const SignPlan& sp, CrtLabels& cur, 
         for (int j = 0; j < k; ++j) {
             const int p = I.crt[j], n = nr_comps(p);
             dr.push_back({sk0 + 2 * j, p, ctr});
-            ctr += (n + 1) / 2;
+            ctr += prg_blocks(p);
             dr.push_back({sk0 + 2 * j + 1, p, ctr});
-            ctr += (n + 1) / 2;
+            ctr += prg_blocks(p);
         }
         for (int j = 0; j < k; ++j) {
             const int p = I.crt[j];
@@ -1659,8 +1736,8 @@ void GpuGarbler::sign_layer(uint64_t layer, const SignPlan& sp, CrtLabels& cur, 
         gm.entries = first;
         gm.nblk = draw_blocks(dr);
         check_desc(gm);
-        hipLaunchKernelGGL(gg::k_draw, dim3(blocks_for(N * gm.nblk, gg::kGB, 8192)), dim3(gg::kGB), 0, nullptr, I.c, gm);
-        hipLaunchKernelGGL(gg::k_project, dim3(blocks_for((N + 63) / 64 * 64 * gm.entries, gg::kPB, 16384)), dim3(gg::kPB), 0, nullptr,
+        hipLaunchKernelGGL(gg::k_draw, dim3(blocks_for(N * gm.nblk, gg::kGB, 8192)), dim3(gg::kGB), 0, gg::tl_st, I.c, gm);
+        hipLaunchKernelGGL(gg::k_project, dim3(blocks_for((N + 63) / 64 * 64 * gm.entries, gg::kPB, 16384)), dim3(gg::kPB), 0, gg::tl_st,
                            I.c, gm, in, tb);
         gg::MiniArgs ma{};
         ma.k = k;
@@ -1670,10 +1747,10 @@ void GpuGarbler::sign_layer(uint64_t layer, const SignPlan& sp, CrtLabels& cur, 
         for (int j = 0; j < k; ++j) ma.out[j] = out[j].as<int16_t>();
         // the sign gadget's payload bank (>= 2 rows, its readers are done: same stream) now holds the two
         // mini-gate key hashes of the sign output
-        hipLaunchKernelGGL(gg::k_bin_keys, dim3(blocks_for(N, gg::kGB, 8192)), dim3(gg::kGB), 0, nullptr, I.c,
+        hipLaunchKernelGGL(gg::k_bin_keys, dim3(blocks_for(N, gg::kGB, 8192)), dim3(gg::kGB), 0, gg::tl_st, I.c,
                            S + static_cast<int64_t>(L.out_slot0) * gg::kW, static_cast<int64_t>(L.nslots) * gg::kW,
                            static_cast<const int16_t*>(nullptr), g.PB, N);
-        hipLaunchKernelGGL(gg::k_relu_finish, dim3(blocks_for(N * k, 256, 8192)), dim3(256), 0, nullptr, I.c, gm, in,
+        hipLaunchKernelGGL(gg::k_relu_finish, dim3(blocks_for(N * k, 256, 8192)), dim3(256), 0, gg::tl_st, I.c, gm, in,
                            tb, ma, static_cast<const u128*>(g.PB));
         tG.to_array(*mmg, I.device);
         tE.to_array(*mme, I.device);
@@ -1686,7 +1763,7 @@ void GpuGarbler::sign_layer(uint64_t layer, const SignPlan& sp, CrtLabels& cur, 
             ga.out[o] = out[o].as<int16_t>();
             ga.n[o] = nr_comps(omods[o]);
         }
-        hipLaunchKernelGGL(gg::k_gather_slots, dim3(blocks_for(N * 128, 256, 4096), ga.k), dim3(256), 0, nullptr, g, ga);
+        hipLaunchKernelGGL(gg::k_gather_slots, dim3(blocks_for(N * 128, 256, 4096), ga.k), dim3(256), 0, gg::tl_st, g, ga);
     }
     HIPCHECK(hipGetLastError());
     gg::end_layer(tmp);
@@ -1705,7 +1782,7 @@ void GpuGarbler::rescale_legacy_iter(uint64_t layer, int it, const RescalePlan& 
                                      const std::vector<std::vector<comp_t>>& down, Array& tr, Array& ap, Array& c1,
                                      Array& c2, Array& sg) {
     Impl& I = *impl_;
-    HIPCHECK(hipSetDevice(I.device));
+    I.enter();
     I.check_cur(cur);
     PhaseTrace tr_("rescale_iter");
     const int64_t N = I.cur_N;
@@ -1730,11 +1807,11 @@ void GpuGarbler::rescale_legacy_iter(uint64_t layer, int it, const RescalePlan& 
     ra.layer = layer;
     ra.sslot = 10 + it;
     DevTable tT, tA, t1, t2, tS;
-    tT.alloc(I.device, N, tr.shape[1]);
-    tA.alloc(I.device, N, ap.shape[1]);
-    if (P.sign.has_cast1()) t1.alloc(I.device, N, c1.shape[1]);
-    t2.alloc(I.device, N, c2.shape[1]);
-    tS.alloc(I.device, N, sg.shape[1]);
+    tT.alloc(I.device, N, tr.shape[1], tr);
+    tA.alloc(I.device, N, ap.shape[1], ap);
+    if (P.sign.has_cast1()) t1.alloc(I.device, N, c1.shape[1], c1);
+    t2.alloc(I.device, N, c2.shape[1], c2);
+    tS.alloc(I.device, N, sg.shape[1], sg);
     gg::Tables tb{};
     tb.t[0] = tA.p(); tb.row[0] = tA.row;
     tb.t[1] = t1.p(); tb.row[1] = t1.row;
@@ -1744,15 +1821,15 @@ void GpuGarbler::rescale_legacy_iter(uint64_t layer, int it, const RescalePlan& 
     tr_.mark("alloc");
     for (int j = 1, ctr = 0; j < k; ++j) {
         ra.ctr[j] = ctr;
-        ctr += (nr_comps(I.crt[j]) + 1) / 2;
+        ctr += prg_blocks(I.crt[j]);
     }
     gg::SignLayout L = gg::sign_layout(P.sign, 0);
     // the payload bank is sized once for both users: rows 0-1 hold the trans key hashes until the sign gadget's
     // k_payloads (later on the same stream) overwrites them
     u128* PB = I.pbank(std::max<size_t>(2, L.pays.size()), N);
-    hipLaunchKernelGGL(gg::k_bin_keys, dim3(blocks_for(N, gg::kGB, 8192)), dim3(gg::kGB), 0, nullptr, I.c, ra.L[0],
+    hipLaunchKernelGGL(gg::k_bin_keys, dim3(blocks_for(N, gg::kGB, 8192)), dim3(gg::kGB), 0, gg::tl_st, I.c, ra.L[0],
                        int64_t(128), ra.up, PB, N);
-    hipLaunchKernelGGL(gg::k_rescale_pre, dim3(blocks_for(N * (k - 1), gg::kGB, 8192)), dim3(gg::kGB), 0, nullptr, I.c,
+    hipLaunchKernelGGL(gg::k_rescale_pre, dim3(blocks_for(N * (k - 1), gg::kGB, 8192)), dim3(gg::kGB), 0, gg::tl_st, I.c,
                        ra, tb, PB, N);
     int16_t* S = I.scratch(static_cast<size_t>(N) * L.nslots * gg::kW * sizeof(int16_t));
     gg::In in{};
@@ -1772,7 +1849,7 @@ void GpuGarbler::rescale_legacy_iter(uint64_t layer, int it, const RescalePlan& 
     g.N = N;
     g.nslots = L.nslots;
     run_sign(I.c, L, g, in, tb, tmp);
-    hipLaunchKernelGGL(gg::k_rescale_post_g, dim3(blocks_for(N * 128, 256, 4096), k), dim3(256), 0, nullptr, I.c, ra,
+    hipLaunchKernelGGL(gg::k_rescale_post_g, dim3(blocks_for(N * 128, 256, 4096), k), dim3(256), 0, gg::tl_st, I.c, ra,
                        g, L.out_slot0);
     HIPCHECK(hipGetLastError());
     gg::end_layer(tmp);
@@ -1800,9 +1877,9 @@ static std::vector<DevBlock> relu_mult_gates(GpuGarbler::Impl& I, const gg::Gadg
     for (int j = 0; j < k; ++j) {
         const int p = I.crt[j], n = nr_comps(p);
         dm.push_back({sk0 + 2 * j, p, c2});
-        c2 += (n + 1) / 2;
+        c2 += prg_blocks(p);
         dm.push_back({sk0 + 2 * j + 1, p, c2});
-        c2 += (n + 1) / 2;
+        c2 += prg_blocks(p);
     }
     for (int j = 0; j < k; ++j) {
         const int p = I.crt[j];
@@ -1827,19 +1904,19 @@ static std::vector<DevBlock> relu_mult_gates(GpuGarbler::Impl& I, const gg::Gadg
     gm.entries = f2;
     gm.nblk = draw_blocks(dm);
     check_desc(gm);
-    hipLaunchKernelGGL(gg::k_draw, dim3(blocks_for(N * gm.nblk, gg::kGB, 8192)), dim3(gg::kGB), 0, nullptr, I.c, gm);
+    hipLaunchKernelGGL(gg::k_draw, dim3(blocks_for(N * gm.nblk, gg::kGB, 8192)), dim3(gg::kGB), 0, gg::tl_st, I.c, gm);
     hipLaunchKernelGGL(gg::k_project, dim3(blocks_for((N + 63) / 64 * 64 * gm.entries, gg::kPB, 16384)),
-                       dim3(gg::kPB), 0, nullptr, I.c, gm, in, tb);
+                       dim3(gg::kPB), 0, gg::tl_st, I.c, gm, in, tb);
     gg::MiniArgs ma{};
     ma.k = k;
     for (int j = 0; j < k; ++j) ma.crt[j] = I.crt[j];
     ma.sig_slot = sig_slot;
     ma.sk_slot0 = sk0;
     for (int j = 0; j < k; ++j) ma.out[j] = out[j].as<int16_t>();
-    hipLaunchKernelGGL(gg::k_bin_keys, dim3(blocks_for(N, gg::kGB, 8192)), dim3(gg::kGB), 0, nullptr, I.c,
+    hipLaunchKernelGGL(gg::k_bin_keys, dim3(blocks_for(N, gg::kGB, 8192)), dim3(gg::kGB), 0, gg::tl_st, I.c,
                        g.S + static_cast<int64_t>(sig_slot) * gg::kW, static_cast<int64_t>(g.nslots) * gg::kW,
                        static_cast<const int16_t*>(nullptr), gm.PB, N);
-    hipLaunchKernelGGL(gg::k_relu_finish, dim3(blocks_for(N * k, 256, 8192)), dim3(256), 0, nullptr, I.c, gm, in,
+    hipLaunchKernelGGL(gg::k_relu_finish, dim3(blocks_for(N * k, 256, 8192)), dim3(256), 0, gg::tl_st, I.c, gm, in,
                        tb, ma, static_cast<const u128*>(gm.PB));
     return out;
 }
@@ -1850,7 +1927,7 @@ static std::vector<DevBlock> relu_mult_gates(GpuGarbler::Impl& I, const gg::Gadg
 void GpuGarbler::relu_mrs(uint64_t layer, const SignMrsPlan& P, CrtLabels& cur, Array& tab,
                           const std::vector<int>* relu_crt, const std::vector<i64>* prefix, Array& mmg, Array& mme) {
     Impl& I = *impl_;
-    HIPCHECK(hipSetDevice(I.device));
+    I.enter();
     I.check_cur(cur);
     PhaseTrace tr_("relu_mrs");
     (void)relu_crt;
@@ -1871,7 +1948,7 @@ void GpuGarbler::relu_mrs(uint64_t layer, const SignMrsPlan& P, CrtLabels& cur, 
             const int r = P.target_res(i, t);
             a.sub[r][a.nsub[r]++] = slot;
             dr.push_back({slot++, P.crt[r], ctr});
-            ctr += (nr_comps(P.crt[r]) + 1) / 2;
+            ctr += prg_blocks(P.crt[r]);
         }
     }
     a.key0 = slot;
@@ -1896,9 +1973,9 @@ void GpuGarbler::relu_mrs(uint64_t layer, const SignMrsPlan& P, CrtLabels& cur, 
     }
     for (int j = 0; j < k; ++j) a.crt[j] = P.crt[j];
     DevTable tT, tG, tE;
-    tT.alloc(I.device, N, tab.shape[1]);
-    tG.alloc(I.device, N, mmg.shape[1]);
-    tE.alloc(I.device, N, static_cast<int64_t>(k) * 3, true);
+    tT.alloc(I.device, N, tab.shape[1], tab);
+    tG.alloc(I.device, N, mmg.shape[1], mmg);
+    tE.alloc(I.device, N, static_cast<int64_t>(k) * 3, mme, true);
     gg::Tables tb{};
     tb.t[0] = tT.p(); tb.row[0] = tT.row;
     tb.t[4] = tG.p(); tb.row[4] = tG.row;
@@ -1926,10 +2003,10 @@ void GpuGarbler::relu_mrs(uint64_t layer, const SignMrsPlan& P, CrtLabels& cur, 
     g.fan = gg::dconst(fan.data(), fan.size());
     check_desc(g);
     std::vector<void*> tmp;
-    hipLaunchKernelGGL(gg::k_draw, dim3(blocks_for(N * g.nblk, gg::kGB, 8192)), dim3(gg::kGB), 0, nullptr, I.c, g);
-    hipLaunchKernelGGL(gg::k_mrs_sign_derive, dim3(blocks_for(N, 256)), dim3(256), 0, nullptr, I.c, g, in, a);
+    hipLaunchKernelGGL(gg::k_draw, dim3(blocks_for(N * g.nblk, gg::kGB, 8192)), dim3(gg::kGB), 0, gg::tl_st, I.c, g);
+    hipLaunchKernelGGL(gg::k_mrs_sign_derive, dim3(blocks_for(N, 256)), dim3(256), 0, gg::tl_st, I.c, g, in, a);
     hipLaunchKernelGGL(gg::k_project, dim3(blocks_for((N + 63) / 64 * 64 * g.entries, gg::kPB, 16384)), dim3(gg::kPB), 0,
-                       nullptr, I.c, g, in, tb);
+                       gg::tl_st, I.c, g, in, tb);
     // mixed-modulus half gates (as sign_layer's ReLU branch, sign label = residue 0's key slot)
     std::vector<DevBlock> out = relu_mult_gates(I, g, in, tb, sig_slot, sk0, *prefix);
     HIPCHECK(hipGetLastError());
@@ -1947,7 +2024,7 @@ void GpuGarbler::relu_mrs(uint64_t layer, const SignMrsPlan& P, CrtLabels& cur, 
 // projections (one per digit, one final).
 void GpuGarbler::rescale_mrs(uint64_t layer, const RescaleMrsPlan& P, CrtLabels& cur, Array& tab) {
     Impl& I = *impl_;
-    HIPCHECK(hipSetDevice(I.device));
+    I.enter();
     I.check_cur(cur);
     PhaseTrace tr_("rescale_mrs");
     const int64_t N = I.cur_N;
@@ -1955,8 +2032,9 @@ void GpuGarbler::rescale_mrs(uint64_t layer, const RescaleMrsPlan& P, CrtLabels&
     DASH_CHECK(P.k() == k && static_cast<int>(P.T) <= I.max_mod, "gpu garbler: mixed-radix rescale plan mismatch");
     std::vector<gg::Draw> dr;
     std::vector<gg::Proj> pr;
-    std::vector<int> fan;
+    std::vector<int> fan, fbank;
     std::vector<int16_t> flut;
+    std::vector<gg::PayDesc> pays;
     gg::MrsG a{};
     a.k = k;
     a.T = static_cast<int>(P.T);
@@ -1973,13 +2051,13 @@ void GpuGarbler::rescale_mrs(uint64_t layer, const RescaleMrsPlan& P, CrtLabels&
                 a.sub[r][a.nsub[r]++] = slot;
             }
             dr.push_back({slot++, q, ctr});
-            ctr += (nr_comps(q) + 1) / 2;
+            ctr += prg_blocks(q);
         }
     }
     a.fin0 = slot;
     for (int j = 0; j < k; ++j) {
         dr.push_back({slot++, P.crt[j], ctr});
-        ctr += (nr_comps(P.crt[j]) + 1) / 2;
+        ctr += prg_blocks(P.crt[j]);
     }
     a.key0 = slot;
     slot += k;
@@ -2004,6 +2082,12 @@ void GpuGarbler::rescale_mrs(uint64_t layer, const RescaleMrsPlan& P, CrtLabels&
         for (int v = 0; v < P.T; ++v)
             for (int j = 0; j < k; ++j) flut.push_back(static_cast<int16_t>(P.final_fn(j, v)));
         for (int j = 0; j < k; ++j) fan.push_back(P.crt[j]);
+        // T entries but only p_j distinct payloads per target j: payload bank rows fin_j + f * R_{p_j}
+        fbank.assign(fan.size(), 0);
+        for (int j = 0; j < k; ++j) {
+            fbank[a1 + j] = static_cast<int>(pays.size()) + 1;
+            for (int f = 0; f < P.crt[j]; ++f) pays.push_back(gg::PayDesc{a.fin0 + j, P.crt[j], f});
+        }
         gg::Proj p{};
         p.in_kind = gg::S_SLOT; p.in_idx = a.acc; p.pin = static_cast<int>(P.T);
         p.out_slot = a.fin0; p.pout = P.crt[0]; p.fn = gg::F_FAN; p.a0 = a0; p.a1 = a1;
@@ -2017,7 +2101,7 @@ void GpuGarbler::rescale_mrs(uint64_t layer, const RescaleMrsPlan& P, CrtLabels&
         a.L[j] = I.cur[j].as<int16_t>();
     }
     DevTable tT;
-    tT.alloc(I.device, N, P.n_tab);
+    tT.alloc(I.device, N, P.n_tab, tab);
     gg::Tables tb{};
     tb.t[0] = tT.p();
     tb.row[0] = tT.row;
@@ -2026,7 +2110,7 @@ void GpuGarbler::rescale_mrs(uint64_t layer, const RescaleMrsPlan& P, CrtLabels&
     g.sslot = 30;
     g.mask = 0;
     g.S = I.scratch(static_cast<size_t>(N) * nslots * gg::kW * sizeof(int16_t));
-    g.PB = nullptr;
+    g.PB = I.pbank(std::max<size_t>(1, pays.size()), N);
     g.N = N;
     g.nslots = nslots;
     g.draws = gg::dconst(dr.data(), dr.size());
@@ -2037,20 +2121,26 @@ void GpuGarbler::rescale_mrs(uint64_t layer, const RescaleMrsPlan& P, CrtLabels&
     g.nblk = draw_blocks(dr);
     g.flut = gg::dconst(flut.data(), flut.size());
     g.fan = gg::dconst(fan.data(), fan.size());
+    g.fbank = gg::dconst(fbank.data(), fbank.size());
     check_desc(g);
     gg::In in{};
     std::vector<void*> tmp;
-    hipLaunchKernelGGL(gg::k_draw, dim3(blocks_for(N * g.nblk, gg::kGB, 8192)), dim3(gg::kGB), 0, nullptr, I.c, g);
-    hipLaunchKernelGGL(gg::k_mrs_derive, dim3(blocks_for(N, 256)), dim3(256), 0, nullptr, I.c, g, a);
+    hipLaunchKernelGGL(gg::k_draw, dim3(blocks_for(N * g.nblk, gg::kGB, 8192)), dim3(gg::kGB), 0, gg::tl_st, I.c, g);
+    if (!pays.empty()) {
+        const gg::PayDesc* pd = gg::dconst(pays.data(), pays.size());
+        const int npd = static_cast<int>(pays.size());
+        hipLaunchKernelGGL(gg::k_payloads, dim3(blocks_for(N * npd, 256, 16384)), dim3(256), 0, gg::tl_st, I.c, g, pd, npd);
+    }
+    hipLaunchKernelGGL(gg::k_mrs_derive, dim3(blocks_for(N, 256)), dim3(256), 0, gg::tl_st, I.c, g, a);
     hipLaunchKernelGGL(gg::k_project, dim3(blocks_for((N + 63) / 64 * 64 * g.entries, gg::kPB, 16384)), dim3(gg::kPB), 0,
-                       nullptr, I.c, g, in, tb);
+                       gg::tl_st, I.c, g, in, tb);
     if (P.sign_last) {
         // residue 0's key slot is the sign label of the ReLU that follows (relu_mult)
         I.sig.alloc(I.device, static_cast<size_t>(N) * gg::kW * sizeof(int16_t));
         I.sig_N = N;
         HIPCHECK(hipMemcpy2DAsync(I.sig.p, gg::kW * sizeof(int16_t), g.S + static_cast<int64_t>(a.key0) * gg::kW,
                                   static_cast<size_t>(nslots) * gg::kW * sizeof(int16_t), gg::kW * sizeof(int16_t),
-                                  static_cast<size_t>(N), hipMemcpyDeviceToDevice, nullptr));
+                                  static_cast<size_t>(N), hipMemcpyDeviceToDevice, gg::tl_st));
     }
     HIPCHECK(hipGetLastError());
     gg::end_layer(tmp);
@@ -2063,7 +2153,7 @@ void GpuGarbler::rescale_mrs(uint64_t layer, const RescaleMrsPlan& P, CrtLabels&
 // mixed-modulus half gates only; device cur -> next base labels.
 void GpuGarbler::relu_mult(uint64_t layer, CrtLabels& cur, const std::vector<i64>* prefix, Array& mmg, Array& mme) {
     Impl& I = *impl_;
-    HIPCHECK(hipSetDevice(I.device));
+    I.enter();
     I.check_cur(cur);
     PhaseTrace tr_("relu_mult");
     const int64_t N = I.cur_N;
@@ -2071,8 +2161,8 @@ void GpuGarbler::relu_mult(uint64_t layer, CrtLabels& cur, const std::vector<i64
     DASH_CHECK(I.sig.p && I.sig_N == N, "gpu garbler: joint ReLU without a preceding sign-producing rescale");
     const int sig_slot = 0, sk0 = 1, nslots = 1 + 2 * k;
     DevTable tG, tE;
-    tG.alloc(I.device, N, mmg.shape[1]);
-    tE.alloc(I.device, N, static_cast<int64_t>(k) * 3, true);
+    tG.alloc(I.device, N, mmg.shape[1], mmg);
+    tE.alloc(I.device, N, static_cast<int64_t>(k) * 3, mme, true);
     gg::Tables tb{};
     tb.t[4] = tG.p(); tb.row[4] = tG.row;
     tb.t[5] = tE.p(); tb.row[5] = tE.row;
@@ -2090,7 +2180,7 @@ void GpuGarbler::relu_mult(uint64_t layer, CrtLabels& cur, const std::vector<i64
     g.nslots = nslots;
     HIPCHECK(hipMemcpy2DAsync(g.S + static_cast<int64_t>(sig_slot) * gg::kW, static_cast<size_t>(nslots) * gg::kW *
                               sizeof(int16_t), I.sig.p, gg::kW * sizeof(int16_t), gg::kW * sizeof(int16_t),
-                              static_cast<size_t>(N), hipMemcpyDeviceToDevice, nullptr));
+                              static_cast<size_t>(N), hipMemcpyDeviceToDevice, gg::tl_st));
     std::vector<DevBlock> out = relu_mult_gates(I, g, in, tb, sig_slot, sk0, *prefix);
     HIPCHECK(hipGetLastError());
     std::vector<void*> tmp;

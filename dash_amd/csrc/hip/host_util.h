@@ -76,6 +76,7 @@ inline dev::ModC make_modc(int q) {
     dev::ModC m{};
     m.q = q;
     m.n = nr_comps(q);
+    m.pm = static_cast<uint32_t>(prg_digits(q));
     if ((q & (q - 1)) == 0) {
         int b = 0;
         while ((1 << b) < q) ++b;

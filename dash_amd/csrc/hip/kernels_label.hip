@@ -168,6 +168,26 @@ __global__ __launch_bounds__(256) void k_transpose(const Tin* __restrict__ in, T
         if (r < rows && c < cols) out[c * rows + r] = static_cast<Tout>(t[tx][y]);
     }
 }
+template <class Tin, class Tout>
+__global__ __launch_bounds__(256) void k_transpose_res(TrRes a) {
+    __shared__ int16_t t[64][65];
+    const int j = blockIdx.z;
+    const int64_t rows = a.rows[j], cols = a.cols[j];
+    const int64_t c0 = static_cast<int64_t>(blockIdx.x) * 64, r0 = static_cast<int64_t>(blockIdx.y) * 64;
+    if (c0 >= cols || r0 >= rows) return;  // block-uniform: this residue's matrix is smaller than the grid
+    const Tin* __restrict__ in = static_cast<const Tin*>(a.in[j]);
+    Tout* __restrict__ out = static_cast<Tout*>(a.out[j]);
+    const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+    for (int y = ty; y < 64; y += 4) {
+        const int64_t r = r0 + y, c = c0 + tx;
+        if (r < rows && c < cols) t[y][tx] = static_cast<int16_t>(in[r * cols + c]);
+    }
+    __syncthreads();
+    for (int y = ty; y < 64; y += 4) {
+        const int64_t c = c0 + y, r = r0 + tx;
+        if (r < rows && c < cols) out[c * rows + r] = static_cast<Tout>(t[tx][y]);
+    }
+}
 __global__ __launch_bounds__(256) void k_narrow(const int16_t* __restrict__ in, act_t* __restrict__ out, int64_t n) {
     for (int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < n;
          i += static_cast<int64_t>(gridDim.x) * blockDim.x)
@@ -189,6 +209,21 @@ void launch_transpose_to_act(const int16_t* in, act_t* out, int64_t rows, int64_
 }
 void launch_transpose_from_act(const act_t* in, int16_t* out, int64_t rows, int64_t cols, hipStream_t st) {
     hipLaunchKernelGGL((k_transpose<act_t, int16_t>), grid_tr(rows, cols), dim3(256), 0, st, in, out, rows, cols);
+}
+
+static inline dim3 grid_tr_res(const TrRes& a) {
+    int64_t r = 1, c = 1;
+    for (int j = 0; j < a.k; ++j) {
+        r = std::max(r, a.rows[j]);
+        c = std::max(c, a.cols[j]);
+    }
+    return dim3(static_cast<unsigned>((c + 63) / 64), static_cast<unsigned>((r + 63) / 64), static_cast<unsigned>(a.k));
+}
+void launch_transpose_to_act_res(const TrRes& a, hipStream_t st) {
+    hipLaunchKernelGGL((k_transpose_res<int16_t, act_t>), grid_tr_res(a), dim3(256), 0, st, a);
+}
+void launch_transpose_from_act_res(const TrRes& a, hipStream_t st) {
+    hipLaunchKernelGGL((k_transpose_res<act_t, int16_t>), grid_tr_res(a), dim3(256), 0, st, a);
 }
 
 void launch_aes_test(const u128* in, u128* out, int64_t n, const AesGlobals& g, hipStream_t st) {

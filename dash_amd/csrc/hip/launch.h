@@ -215,6 +215,19 @@ inline void conv_unroll_taps(ConvArgs& a, int max_p) {
     a.ph = a.pw = 0;
 }
 
+// Conv kernel geometry for a layer: the tap-unrolled view where it pays (conv_unroll_taps), the LDS band
+// image otherwise; when no band of the unrolled view fits the LDS budget (wide outputs, small
+// DASH_CONV_LDS_KB) the layer falls back to its own geometry (plain band image, or im2col when nbands = 0).
+inline void conv_plan(ConvArgs& a, int max_p, bool unroll) {
+    const ConvArgs own = a;
+    if (unroll) conv_unroll_taps(a, max_p);
+    conv_img_geometry(a);
+    if (a.ur && a.nbands == 0) {
+        a = own;
+        conv_img_geometry(a);
+    }
+}
+
 // MFMA weight image [F16][kh][kw][Cpad] from the centered im2col weights w8 [F][Kpad] (order ci*kh*kw + dy*kw
 // + dx); tap-unrolled layers: [F16][Cpad] with patch channel (dy*kw + dx)*C + ci (the staging's order)
 inline std::vector<int8_t> conv_w8r(const ConvArgs& a, const std::vector<int8_t>& w8, int F) {
@@ -237,6 +250,15 @@ void launch_transpose16(const int16_t* in, int16_t* out, int64_t rows, int64_t c
 void launch_narrow(const int16_t* in, act_t* out, int64_t n, hipStream_t st);  // int16 labels -> byte activations
 void launch_transpose_to_act(const int16_t* in, act_t* out, int64_t rows, int64_t cols, hipStream_t st);
 void launch_transpose_from_act(const act_t* in, int16_t* out, int64_t rows, int64_t cols, hipStream_t st);
+// the same for every residue of a label set in one launch (grid z = residue): matrix j is rows[j] x cols[j]
+struct TrRes {
+    const void* in[kMaxRes];
+    void* out[kMaxRes];
+    int64_t rows[kMaxRes], cols[kMaxRes];
+    int k;
+};
+void launch_transpose_to_act_res(const TrRes& a, hipStream_t st);    // int16 -> bytes
+void launch_transpose_from_act_res(const TrRes& a, hipStream_t st);  // bytes -> int16
 
 }  // namespace dev
 }  // namespace dash

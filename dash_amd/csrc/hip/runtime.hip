@@ -9,6 +9,7 @@
 #include <pybind11/stl.h>
 
 #include <chrono>
+#include <map>
 #include <functional>
 #include <thread>
 
@@ -60,8 +61,32 @@ class HipEvaluator {
                    "model does not garble the evaluator's circuit");
         HIPCHECK(hipSetDevice(dev_));
         for (auto& f : loaders_) f(b, m);
-        HIPCHECK(hipDeviceSynchronize());
+        // the loaders' copies run on the null stream; evaluation and garbling streams are non-blocking, so this
+        // waits for the load only (a device-wide sync would also wait for other groups' evaluations)
+        HIPCHECK(hipStreamSynchronize(nullptr));
         loaded_[b] = 1;
+    }
+    // Zero-copy offline phase (GarbleOptions::sink): slot b's table arenas as GPU-garbler destinations.
+    // A model garbled with this sink already has its tables in slot b, and load(b, m) skips their copies.
+    std::shared_ptr<TableSink> sink(int b) const {
+        DASH_CHECK(b >= 0 && b < B_, "batch slot out of range");
+        auto arena = arena_;
+        const int dev = dev_;
+        auto s = std::make_shared<TableSink>();
+        s->dest = [arena, b, dev](size_t layer, const std::string& name, size_t nbytes) -> std::shared_ptr<Array::Device> {
+            auto it = arena.find({layer, name});
+            if (it == arena.end() || it->second.second != nbytes) return nullptr;
+            auto d = std::make_shared<Array::Device>();
+            d->p = std::shared_ptr<void>(it->second.first + nbytes * b, [](void*) {});  // the evaluator owns it
+            d->device = dev;
+            d->external = true;
+            d->fetch = [dev](void* h, const void* dv, size_t n) {
+                HIPCHECK(hipSetDevice(dev));
+                HIPCHECK(hipMemcpy(h, dv, n, hipMemcpyDeviceToHost));
+            };
+            return d;
+        };
+        return s;
     }
     ~HipEvaluator() {
         if (gexec_) (void)hipGraphExecDestroy(gexec_);
@@ -241,6 +266,7 @@ class HipEvaluator {
     // a model array into device memory: device-to-device (or peer) when the GPU
     // garbler left it in HBM and nobody has fetched (and possibly edited) a host copy
     static void copy_in(uint8_t* dst, const Array& a) {
+        if (a.device_resident() && a.device_ptr() == dst) return;  // garbled straight into this slot (sink)
         if (a.device_resident() && !a.dev->host)
             HIPCHECK(hipMemcpy(dst, a.device_ptr(), a.nbytes, hipMemcpyDefault));
         else
@@ -250,6 +276,7 @@ class HipEvaluator {
     const u128* upload_tables(size_t li, const std::string& name) {
         const size_t nb = tmpl_->layers[li].arr(name).nbytes;
         uint8_t* d = dalloc<uint8_t>(nb * B_);
+        arena_[{li, name}] = {d, nb};
         loaders_.push_back([d, nb, li, name](int b, const GarbledModel& m) {
             const Array& a = m.layers[li].arr(name);
             DASH_CHECK(a.nbytes == nb, "table size mismatch across batch");
@@ -359,6 +386,7 @@ class HipEvaluator {
     size_t tmpl_nlayers_ = 0;
     bool mfma_;
     std::vector<std::function<void(int, const GarbledModel&)>> loaders_;
+    std::map<std::pair<size_t, std::string>, std::pair<uint8_t*, size_t>> arena_;  // (layer, table) -> [B][nb]
     std::vector<int> loaded_;
     int dev_ = 0, B_ = 1, k_ = 0;
     std::vector<int> crt_, out_mod_;
@@ -636,10 +664,8 @@ void HipEvaluator::build() {
                     }();
                     int max_p = 0;
                     for (int j = 0; j < k_; ++j) max_p = std::max(max_p, crt_[j]);
-                    if (mfma_ && img_ok) conv_unroll_taps(a, max_p);
-                    conv_img_geometry(a);
+                    conv_plan(a, max_p, mfma_ && img_ok);
                     if (!(mfma_ && img_ok)) a.band = a.nbands = 0;
-                    DASH_CHECK(!a.ur || a.nbands > 0, "tap-unrolled conv without an LDS band");
                 }
                 a.img_off[0] = 0;
                 for (int j = 0; j < k_; ++j) a.img_off[j + 1] = a.img_off[j] + static_cast<i64>(B_) * crt.n[j];
@@ -1304,6 +1330,7 @@ void register_hip_bindings(py::module_& m) {
             py::gil_scoped_release rel;
             h.load(b, *m);
         })
+        .def("sink", &HipEvaluator::sink, "slot b's table arenas as a GPU-garbler destination (zero-copy load)")
         .def_property_readonly("batch", &HipEvaluator::batch)
         .def("device_bytes", &HipEvaluator::device_bytes)
         .def("table_bytes", &HipEvaluator::table_bytes)

@@ -97,6 +97,13 @@ struct Decoder {
     static Decoder deserialize(const std::string& blob);
 };
 
+// Destination of garbled tables produced on the GPU (zero-copy offline phase): the GPU garbler writes
+// table `name` of layer `layer` straight into the returned device buffer (e.g. a HipEvaluator's arena slot,
+// HipEvaluator::sink) instead of a buffer of its own; null = no destination for that table.
+struct TableSink {
+    std::function<std::shared_ptr<Array::Device>(size_t layer, const std::string& name, size_t nbytes)> dest;
+};
+
 struct GarbleOptions {
     int nthreads = 0;
     int device = -1;  // >= 0: garble ReLU / Sign / legacy rescale layers on this GPU
@@ -106,6 +113,7 @@ struct GarbleOptions {
     // A ReLU right after a mixed-radix rescale takes its sign from that rescale's conversion
     // (gadgets.h RescaleMrsPlan::sign_last); other ReLUs use relu_mrs / the approximate gadget.
     bool relu_joint = false;
+    std::shared_ptr<TableSink> sink;  // GPU-garbled tables go straight to these buffers (device >= 0 only)
 };
 
 class Garbler {

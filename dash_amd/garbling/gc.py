@@ -64,7 +64,7 @@ class GarbledCircuit:
     def __init__(self, circuit: Circuit, crt: Union[int, Sequence[int]], mrs: Union[None, float, Sequence[int]] = None,
                  max_modulus: int = 0, seed: Optional[bytes] = None, garble_me: bool = True, nthreads: int = 0,
                  device: Optional[int] = None, fused_sign: bool = True, rescale: str = "auto",
-                 relu: str = "auto"):
+                 relu: str = "auto", sink=None):
         """fused_sign: sign-gadget construction. True (default): the MRS casts are folded into the approx and
         carry projections (same function, 3.7x fewer gates per sign; gadgets.h SignPlan::fused). False: the
         reference construction with explicit identity casts (sign_gadget.h:456-546).
@@ -83,7 +83,11 @@ class GarbledCircuit:
         that directly follows a mixed-radix rescale takes its sign from that rescale's conversion (residue 2
         converted last: its digit is the sign; gadgets.h RescaleMrsPlan::sign_last), so it costs only the
         mixed-modulus half gates; other ReLUs use the approximate gadget. Needs rescale="mrs" to have effect.
-        "auto" (default): "joint" with the mixed-radix rescale, else "approx"."""
+        "auto" (default): "joint" with the mixed-radix rescale, else "approx".
+
+        sink: with `device`, a HipEvaluator slot destination (HipEvaluator.sink(b)): the GPU garbler writes the
+        garbled tables straight into that slot's HBM arena (zero-copy offline phase; HipEvaluator.load(b, model)
+        then skips them). The model's tables alias the slot and are valid only while it holds this GC."""
         self.circuit = circuit
         self.crt_base = first_primes(crt) if isinstance(crt, int) else [int(p) for p in crt]
         if mrs is None:
@@ -99,6 +103,7 @@ class GarbledCircuit:
         self.device = -1 if device is None else int(device)
         self.fused_sign = bool(fused_sign)
         self.rescale, self.relu = resolve_constructions(circuit, self.crt_base, rescale, relu)
+        self.sink = sink
         self._n = native()
         self.garbler = self._n.Garbler(self.crt_base, self.mrs_base, self.seed, int(max_modulus))
         self.model = None
@@ -113,7 +118,8 @@ class GarbledCircuit:
         t = time.perf_counter()
         self.model = self.garbler.garble(specs, list(self.circuit.input_dims), self.nthreads, self.device,
                                          self.fused_sign, self.rescale == "mrs", self.relu == "mrs",
-                                         self.relu == "joint")
+                                         self.relu == "joint", self.sink if self.device >= 0 else None)
+        self.sink = None  # single use: the slot now holds this GC
         self.garbling_time_s = time.perf_counter() - t
         self.decoder = self.garbler.decoder()
         return self.model

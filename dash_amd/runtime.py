@@ -54,6 +54,12 @@ class HipEvaluator:
     def load(self, b: int, model) -> None:
         self._h.load(b, model)
 
+    def sink(self, b: int):
+        """Slot b as the GPU garbler's table destination: ``GarbledCircuit(..., device=d, sink=ev.sink(b))``
+        writes the tables straight into this evaluator's HBM arena, and ``load(b, gc.model)`` then copies
+        only the small per-GC constants (zero-copy offline phase)."""
+        return self._h.sink(b)
+
     @property
     def batch(self) -> int:
         return self._h.batch

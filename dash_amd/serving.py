@@ -235,14 +235,15 @@ class InferenceService:
             self._worker.start()
 
     # ------------------------------------------------------------ offline
-    def _new_gc(self):
+    def _new_gc(self, sink=None):
         from .garbling import GarbledCircuit
 
         seed = hashlib.sha256(self._seed + self._ctr.to_bytes(8, "little")).digest()[:16]
         self._ctr += 1
         t = time.perf_counter()
         gc = GarbledCircuit(self.circuit, self.crt, self.mrs, max_modulus=self.max_modulus, seed=seed,
-                            nthreads=self.nthreads, device=self.device if self.garble_device else None, **self.gc_kw)
+                            nthreads=self.nthreads, device=self.device if self.garble_device else None,
+                            sink=sink if self.garble_device else None, **self.gc_kw)
         self.stats.garble_s += time.perf_counter() - t
         self.stats.gcs_garbled += 1
         return gc
@@ -268,8 +269,9 @@ class InferenceService:
             if self.backend == "hip":
                 from .runtime import HipEvaluator
 
-                with self._capture_lock:  # GPU garbling + upload: device-wide syncs and allocations
-                    gc = self._new_gc()
+                with self._capture_lock:  # GPU garbling + upload (allocations on the first fill)
+                    # the GPU garbler writes the tables straight into the slot (zero-copy load)
+                    gc = self._new_gc(g.ev.sink(b) if g.ev is not None else None)
                     if g.ev is None:
                         g.ev = HipEvaluator(template=gc.model, batch=g.slots, device=self.device)
                     g.ev.load(b, gc.model)

@@ -1,4 +1,10 @@
-"""Summarise a rocprofv3 kernel-trace database (rocpd SQLite) per kernel."""
+"""Summarise a rocprofv3 kernel-trace database (rocpd SQLite) per kernel.
+
+    python -m dash_amd.utils.profsum DB [TOP] [--dispatches PATTERN N]
+
+--dispatches lists the first N dispatches whose kernel name contains PATTERN in
+launch order (grid size and duration), to attribute one kernel's calls to layers.
+"""
 from __future__ import annotations
 
 import re
@@ -6,16 +12,23 @@ import sqlite3
 import sys
 
 
-def summarize(db: str, top: int = 40) -> str:
+def _rows(db: str):
     c = sqlite3.connect(db)
-    q = """select k.display_name, d.start, d.end from rocpd_kernel_dispatch d
-           join rocpd_info_kernel_symbol k on d.kernel_id = k.id"""
-    rows = c.execute(q).fetchall()
+    cols = {r[1] for r in c.execute("pragma table_info(rocpd_kernel_dispatch)")}
+    grid = "d.grid_size_x" if "grid_size_x" in cols else "0"
+    q = f"""select k.display_name, d.start, d.end, {grid} from rocpd_kernel_dispatch d
+           join rocpd_info_kernel_symbol k on d.kernel_id = k.id order by d.start"""
+    return c.execute(q).fetchall()
+
+
+def _short(name: str) -> str:
+    return re.sub(r"^void ", "", re.sub(r"\(.*", "", name))
+
+
+def summarize(db: str, top: int = 40) -> str:
     agg: dict[str, list] = {}
-    for name, s, e in rows:
-        short = re.sub(r"\(.*", "", name)
-        short = re.sub(r"^void ", "", short)
-        a = agg.setdefault(short, [0, 0.0])
+    for name, s, e, _ in _rows(db):
+        a = agg.setdefault(_short(name), [0, 0.0])
         a[0] += 1
         a[1] += (e - s) / 1e6
     tot = sum(v[1] for v in agg.values()) or 1.0
@@ -26,5 +39,23 @@ def summarize(db: str, top: int = 40) -> str:
     return "\n".join(lines)
 
 
+def dispatches(db: str, pattern: str, n: int) -> str:
+    out = [f"# first {n} dispatches matching {pattern!r} (launch order): grid_x, us"]
+    for name, s, e, g in _rows(db):
+        if pattern in name:
+            out.append(f"{_short(name)[:40]:40s} {g:10d} {(e - s) / 1e3:10.1f}")
+            if len(out) > n:
+                break
+    return "\n".join(out)
+
+
 if __name__ == "__main__":
-    print(summarize(sys.argv[1], int(sys.argv[2]) if len(sys.argv) > 2 else 40))
+    args = sys.argv[1:]
+    extra = ""
+    if "--dispatches" in args:
+        i = args.index("--dispatches")
+        extra = dispatches(args[0], args[i + 1], int(args[i + 2]))
+        args = args[:i]
+    print(summarize(args[0], int(args[1]) if len(args) > 1 else 40))
+    if extra:
+        print(extra)

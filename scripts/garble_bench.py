@@ -27,9 +27,34 @@ def main():
     ap.add_argument("--device", type=int, default=0)
     ap.add_argument("--gpu-only", action="store_true", help="skip the host garbler (profiling)")
     ap.add_argument("--rescale", default="mrs", help="rescale construction (mrs | legacy)")
+    ap.add_argument("--relu", default="joint", help="relu construction (joint | approx | mrs)")
+    ap.add_argument("--sink", type=int, default=0,
+                    help="N > 0: garble N GCs straight into the slots of a 2-slot HipEvaluator (zero-copy load), "
+                         "timing garble + load per GC like the serving engine")
     args = ap.parse_args()
     c = build_circuit(args.model, Q.ScaleQuant, args.l, seed=0)
     seed = bytes(range(16))
+    if args.sink:
+        from dash_amd.runtime import HipEvaluator
+
+        kw = dict(rescale=args.rescale, relu=args.relu)
+        t0 = GarbledCircuit(c, args.k, 100.0, seed=seed, device=args.device, **kw)
+        ev = HipEvaluator(template=t0.model, batch=2, device=args.device)
+        del t0
+        ts = []
+        for r in range(args.sink):
+            t = time.perf_counter()
+            gc = GarbledCircuit(c, args.k, 100.0, seed=bytes([r % 256]) * 16, device=args.device,
+                                sink=ev.sink(r % 2), **kw)
+            tg = time.perf_counter() - t
+            ev.load(r % 2, gc.model)
+            ts.append((tg, time.perf_counter() - t))
+        steady = ts[1:] or ts
+        print(json.dumps({"mode": "gpu_sink", "model": args.model, "gcs": args.sink,
+                          "garble_ms_per_gc": round(1000 * sum(a for a, _ in steady) / len(steady), 2),
+                          "garble_load_ms_per_gc": round(1000 * sum(b for _, b in steady) / len(steady), 2),
+                          "layer_ms": [round(x, 1) for x in gc.garbling_layer_ms()]}), flush=True)
+        return
     blobs = {}
     modes = (("gpu", args.device),) if args.gpu_only else (("gpu", args.device), ("cpu", None))
     for mode, dev in modes:
@@ -37,7 +62,7 @@ def main():
         gc = None
         for _ in range(args.reps):
             t = time.perf_counter()
-            gc = GarbledCircuit(c, args.k, 100.0, seed=seed, device=dev, rescale=args.rescale)
+            gc = GarbledCircuit(c, args.k, 100.0, seed=seed, device=dev, rescale=args.rescale, relu=args.relu)
             times.append(time.perf_counter() - t)
         blobs[mode] = gc.model.serialize()
         print(json.dumps({"mode": mode, "model": args.model, "s_per_gc": round(min(times), 3),

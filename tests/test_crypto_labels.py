@@ -69,3 +69,28 @@ def test_prg_deterministic(native):
     np.testing.assert_array_equal(a, b)
     assert not np.array_equal(a, c)
     assert a.min() >= 0 and a.max() < 17
+
+
+@pytest.mark.parametrize("p", [2, 3, 7, 17, 32, 64, 86, 97, 173])
+def test_prg_label_matches_oracle(native, p):
+    """Prg::label (core.h): block b = AES_seed(stream || ctr + b) (little-endian 128-bit) supplies components
+    b*m .. b*m + m - 1 as its least significant base-p digits, m = largest count with p^m <= 2^64 (all
+    128 / log2 p bits for powers of two). Pure-Python oracle on tests/aes_ref.py."""
+    seed, stream, ctr = bytes(range(3, 19)), 0x1234_5678_9ABC, 41
+    n = native.nr_comps(p)
+    if p & (p - 1) == 0:
+        m = 128 // (p.bit_length() - 1)
+    else:
+        m = 0
+        while p ** (m + 1) <= 2 ** 64:
+            m += 1
+    exp = []
+    b = 0
+    while len(exp) < n:
+        blk = ((stream << 64) | (ctr + b)).to_bytes(16, "little")
+        v = int.from_bytes(encrypt_block(seed, blk), "little")
+        for _ in range(min(m, n - len(exp))):
+            exp.append(v % p)
+            v //= p
+        b += 1
+    np.testing.assert_array_equal(native.prg_label(seed, stream, ctr, p), exp)

@@ -378,3 +378,34 @@ def test_gpu_garbler_bit_identical_joint_relu(name):
     gpu = GarbledCircuit(c, k, 100.0, seed=seed, device=0, rescale="mrs", relu="joint")
     assert gpu.model.serialize() == cpu.model.serialize()
     assert gpu.decoder.serialize() == cpu.decoder.serialize()
+
+
+@pytest.mark.parametrize("rescale,relu", [("mrs", "joint"), ("legacy", "approx")])
+def test_gpu_garble_into_evaluator_slot(rescale, relu):
+    """Zero-copy offline phase: the GPU garbler writes a GC's tables straight into an evaluator slot
+    (HipEvaluator.sink). The slot then holds exactly the host garbler's tables (same seed), load() only adds the
+    per-GC constants, and both slots decode to the plaintext outputs."""
+    from dash_amd.ir.circuit import Circuit
+    from dash_amd.ir.quant import QuantizationMethod as Q
+    from dash_amd.models import build_circuit, quantized_inputs
+    from dash_amd.runtime import HipEvaluator
+
+    full = build_circuit("MODEL_F_MINIONN_POOL_REPL", Q.ScaleQuant, 5, seed=0)
+    c, k = Circuit(full.layers[:5]), 7  # conv, rescale(l=5), relu, conv, rescale
+    xs = quantized_inputs("MODEL_F_MINIONN_POOL_REPL", 2, Q.ScaleQuant, 5, seed=3)
+    kw = dict(rescale=rescale, relu=relu)
+    first = GarbledCircuit(c, k, 100.0, seed=bytes([7]) * 16, device=0, **kw)
+    ev = HipEvaluator(template=first.model, batch=2, device=0)
+    ev.load(0, first.model)
+    seed = bytes(range(16))
+    into = GarbledCircuit(c, k, 100.0, seed=seed, device=0, sink=ev.sink(1), **kw)
+    host = GarbledCircuit(c, k, 100.0, seed=seed, **kw)
+    assert into.model.serialize() == host.model.serialize()  # the host copy is fetched from the slot itself
+    ev.load(1, into.model)
+    for b, gc in enumerate((first, into)):
+        ev.encode_compressed_into(b, gc, xs[b])
+    ev.upload_inputs_compressed()
+    ev.run()
+    ev.fetch_outputs()
+    for b, gc in enumerate((first, into)):
+        np.testing.assert_array_equal(ev.decode(b, gc), gc.plain_q_eval(xs[b]))
