@@ -16,6 +16,7 @@ per-circuit time (runtime / batch) so batching gains are visible.
 
 Usage:
   python benchmarks/micro.py --layers dense,conv2d,approx_relu,sign,rescaling --targets cpu,gpu --runs 3
+  python benchmarks/micro.py --layers dense --targets gpu,gpu_valu --batch 16   # MFMA vs VALU dense
 """
 from __future__ import annotations
 
@@ -69,26 +70,31 @@ def run_cpu(circuit, k, mrs, x):
     return ms, -1.0
 
 
-def run_gpu(circuit, k, mrs, x, batch):
+def run_gpu(circuit, k, mrs, x, batch, mfma=True, reps=10):
+    """Per-GC evaluation time: one untimed run (lazy setup), then the mean of `reps` runs (the same
+    evaluation repeated on the staged inputs; outputs are decoded and checked after the last)."""
     import torch
 
     from dash_amd.runtime import HipEvaluator
 
     m1 = gpu_mem_used()
     gcs = [GarbledCircuit(circuit, k, mrs) for _ in range(batch)]
-    ev = HipEvaluator([g.model for g in gcs])
+    ev = HipEvaluator([g.model for g in gcs], mfma=mfma)
     for b, g in enumerate(gcs):
         ev.encode_compressed_into(b, g, x)
     ev.upload_inputs_compressed()
     torch.cuda.synchronize()
     m2 = gpu_mem_used()
-    t = time.perf_counter()
     ev.run()
     torch.cuda.synchronize()
-    ms = 1000 * (time.perf_counter() - t)
+    t = time.perf_counter()
+    for _ in range(reps):
+        ev.run()
+    torch.cuda.synchronize()
+    ms = 1000 * (time.perf_counter() - t) / reps
     ev.fetch_outputs()
     for b, g in enumerate(gcs):
-        ev.decode(b, g)
+        np.testing.assert_array_equal(ev.decode(b, g), g.plain_q_eval(x))
     del ev
     return ms / batch, (m2 - m1) / batch
 
@@ -140,8 +146,8 @@ def bench(layer, targets, runs, batch, rng, out_dir, date):
                         k, mrs = 8, 100.0
                     if target == "cpu":
                         ms, mem = run_cpu(c, k, mrs, x)
-                    else:
-                        ms, mem = run_gpu(c, k, mrs, x, batch)
+                    else:  # gpu: MFMA kernels where they exist; gpu_valu: the VALU kernels (A/B)
+                        ms, mem = run_gpu(c, k, mrs, x, batch, mfma=target != "gpu_valu")
                     dims_s = "x".join(map(str, dim)) if isinstance(dim, tuple) else str(dim)
                     row = [target.upper(), dims_s, str(k), str(run), f"{ms:f}", f"{mem:f}"]
                     if layer == "rescaling":
@@ -171,12 +177,12 @@ def main():
         ACT_DIMS = [d for d in ACT_DIMS if d <= args.max_dim]
         CONV_DIMS = [d for d in CONV_DIMS if d[0] <= args.max_dim]
     targets = args.targets.split(",")
-    if "gpu" in targets:
+    if any(t.startswith("gpu") for t in targets):
         from dash_amd.runtime import hip_available
 
         if not hip_available():
             print("no GPU visible: running cpu only", file=sys.stderr)
-            targets = [t for t in targets if t != "gpu"]
+            targets = [t for t in targets if not t.startswith("gpu")]
     rng = np.random.default_rng(42)
     date = date_string()
     for layer in args.layers.split(","):

@@ -94,10 +94,17 @@ def quantize_images(cfg, circuit, imgs):
     return [quantize_input(x, qm, cfg.q_parameter, 0.0) for x in imgs]
 
 
-def make_gc(cfg, circuit, relu_acc):
+def make_gc(cfg, circuit, relu_acc, device=None):
+    """Reference constructions (the published numbers' gadgets): legacy rescale, approximate-sign ReLU, explicit
+    casts. device: garble on this GPU (byte-identical to the host garbler)."""
+    kw = dict(device=device, rescale="legacy", relu="approx", fused_sign=False)
     if cfg.crt_base:
-        return GarbledCircuit(circuit, cfg.crt_base, cfg.mrs_base, max_modulus=max(cfg.crt_base))
-    return GarbledCircuit(circuit, cfg.target_crt_base_size, relu_acc)
+        return GarbledCircuit(circuit, cfg.crt_base, cfg.mrs_base, max_modulus=max(cfg.crt_base), **kw)
+    return GarbledCircuit(circuit, cfg.target_crt_base_size, relu_acc, **kw)
+
+
+def scheme_of(cfg: InferConfig) -> str:
+    return config_name(cfg).split("/")[1]
 
 
 def layer_names(circuit):
@@ -116,12 +123,12 @@ def run_cpu(cfg, circuit, xq, labels, relu_acc, rows, dist_g, dist_e):
         pred = int(np.argmax(y))
         preds.append(pred)
         rows.append(["CPU", cfg.model_name, cfg.target_crt_base_size, int(cfg.optimize_bases), ms, relu_acc,
-                     labels[i], pred])
+                     labels[i], pred, scheme_of(cfg)])
         for name, gms, ems in zip(layer_names(circuit), gc.garbling_layer_ms(), ms_layers):
             dist_g.append(["CPU", cfg.model_name, name, cfg.target_crt_base_size, int(cfg.optimize_bases), gms,
-                           relu_acc])
+                           relu_acc, scheme_of(cfg)])
             dist_e.append(["CPU", cfg.model_name, name, cfg.target_crt_base_size, int(cfg.optimize_bases), ems,
-                           relu_acc])
+                           relu_acc, scheme_of(cfg)])
         print(f"  CPU {config_name(cfg)} input {i}: {ms:.1f} ms  pred={pred} label={labels[i]}", flush=True)
     return preds
 
@@ -134,7 +141,7 @@ def run_gpu(cfg, circuit, xq, labels, relu_acc, rows, dist_e):
     preds = []
     ev = None
     for i, x in enumerate(xq):
-        gc = make_gc(cfg, circuit, relu_acc)  # fresh GC per input
+        gc = make_gc(cfg, circuit, relu_acc, device=0)  # fresh GC per input, garbled on the GPU
         if ev is None:
             ev = HipEvaluator(template=gc.model, batch=1, profile=bool(dist_e is not None))
         ev.load(0, gc.model)
@@ -149,11 +156,11 @@ def run_gpu(cfg, circuit, xq, labels, relu_acc, rows, dist_e):
         pred = int(np.argmax(y))
         preds.append(pred)
         rows.append(["GPU", cfg.model_name, cfg.target_crt_base_size, int(cfg.optimize_bases), ms, relu_acc,
-                     labels[i], pred])
+                     labels[i], pred, scheme_of(cfg)])
         if dist_e is not None:
             for name, ems in ev.layer_times().items():
                 dist_e.append(["GPU", cfg.model_name, name, cfg.target_crt_base_size, int(cfg.optimize_bases), ems,
-                               relu_acc])
+                               relu_acc, scheme_of(cfg)])
         print(f"  GPU {config_name(cfg)} input {i}: {ms:.2f} ms  pred={pred} label={labels[i]}", flush=True)
     return preds
 

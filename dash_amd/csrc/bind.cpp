@@ -190,6 +190,57 @@ PYBIND11_MODULE(_dash_native, m) {
     });
     m.def("kind_name", &kind_name);
 
+    // Single gates of the native garbler with caller-chosen labels (wire-compatibility vectors: the tests
+    // rebuild the reference's formulas in a pure-Python oracle and compare table bytes). Tables come back as
+    // uint64 (entries, 2) = (lo, hi) of each 16-byte entry.
+    using I16 = py::array_t<int16_t, py::array::c_style | py::array::forcecast>;
+    auto table_out = [](const std::vector<u128>& t) {
+        py::array_t<uint64_t> out({static_cast<py::ssize_t>(t.size()), static_cast<py::ssize_t>(2)});
+        auto o = out.mutable_unchecked<2>();
+        for (size_t i = 0; i < t.size(); ++i) {
+            o(i, 0) = static_cast<uint64_t>(t[i]);
+            o(i, 1) = static_cast<uint64_t>(t[i] >> 64);
+        }
+        return out;
+    };
+    auto check_label = [](const I16& a, int p, const char* what) {
+        DASH_CHECK(a.size() == nr_comps(p), std::string(what) + ": label length does not match its modulus");
+    };
+    m.def("garble_projection_gate", [=](I16 in0, I16 Rin, int pin, I16 out0, I16 outR, int pout, std::vector<i64> f) {
+        check_label(in0, pin, "in0"); check_label(Rin, pin, "Rin"); check_label(out0, pout, "out0");
+        check_label(outR, pout, "outR");
+        DASH_CHECK(static_cast<int>(f.size()) == pin, "one function value per input value");
+        std::vector<u128> t(pin);
+        garble_proj(in0.data(), Rin.data(), mod_info(pin), out0.data(), outR.data(), mod_info(pout),
+                    [&](int v) { return f[v]; }, t.data());
+        return table_out(t);
+    }, "projection gate T[color(in0 + i Rin)] = compress(out0 + f(i) outR) + H(compress(in0 + i Rin))");
+    m.def("garble_mini_gate", [=](I16 in0, I16 Rin, int pin, std::vector<i64> f) {
+        check_label(in0, pin, "in0"); check_label(Rin, pin, "Rin");
+        DASH_CHECK(static_cast<int>(f.size()) == pin, "one function value per input value");
+        std::vector<u128> t(1, 0);
+        garble_proj_mini(in0.data(), Rin.data(), mod_info(pin), [&](int v) { return f[v]; }, t.data());
+        return table_out(t);
+    }, "mini projection: int16 payloads f(i) + (int16)H at slot color of one 16-byte entry");
+    m.def("garble_mixed_mod_gate", [=](I16 x0, int p, I16 y0, int q, I16 Rp, I16 Rq, py::bytes seed, uint64_t stream) {
+        check_label(x0, p, "x0"); check_label(y0, q, "y0"); check_label(Rp, p, "Rp"); check_label(Rq, q, "Rq");
+        std::string sd = seed;
+        DASH_CHECK(sd.size() == 16, "seed must be 16 bytes");
+        Prg prg(reinterpret_cast<const uint8_t*>(sd.data()));
+        LabelBank R;
+        R.max_mod = std::max(p, q);
+        R.lab.assign(R.max_mod + 1, {});
+        R.lab[p].assign(Rp.data(), Rp.data() + Rp.size());
+        R.lab[q].assign(Rq.data(), Rq.data() + Rq.size());
+        std::vector<u128> g(p), e(q + 1, 0);
+        py::array_t<int16_t> out0(nr_comps(p));
+        u64 ctr = 0;
+        mixed_mult_garble(x0.data(), mod_info(p), y0.data(), mod_info(q), R, prg, stream, ctr, g.data(), e.data(),
+                          out0.mutable_data());
+        return py::make_tuple(table_out(g), table_out(e), out0);
+    }, "mixed-modulus half gate x (mod p) * y (mod q): garbler table [p], evaluator table [q + 1] (q full entries, "
+       "then the mini entry), output base label; sk03 / sk04 drawn from Prg(seed) on `stream`");
+
     py::class_<GarbledModel, std::shared_ptr<GarbledModel>>(m, "GarbledModel")
         .def("serialize", [](const GarbledModel& g) { return py::bytes(g.serialize()); })
         .def_static("deserialize", [](py::bytes b) { return std::make_shared<GarbledModel>(GarbledModel::deserialize(std::string(b))); })

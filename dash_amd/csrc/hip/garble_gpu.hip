@@ -87,9 +87,28 @@ struct Ctx {
     const uint32_t* te0;
 };
 
-// input labels: per residue a label-major array [N][n_j]
+// Chunked component-major labels (all device labels of the GPU garbler): the
+// components of an element are grouped in chunks of 8 (16 bytes); chunk c8 of
+// element e of a label set of N elements sits at base + (c8 * N + e) * 8. A
+// wave of lanes walking consecutive elements reads a chunk with one coalesced
+// 16-byte load per lane (1 KiB contiguous per wave), and a lane gets 8
+// components per load instruction. A single uniform label row (R_p, Z_p) is
+// the same view with chunk stride 8 (components contiguous).
+constexpr int kCh = 8;
+__host__ __device__ constexpr int64_t chunks_of(int n) { return (n + kCh - 1) / kCh; }
+
+// strided label view: component q at p[(q >> 3) * cs + (q & 7)], chunk c8 (16-B aligned) at p + c8 * cs
+struct LRef {
+    const int16_t* p;
+    int64_t cs;
+};
+__host__ __device__ __forceinline__ LRef row_ref(const int16_t* row) { return LRef{row, kCh}; }
+
+// input labels, per residue: element e's view is {p + e * es, cs}: chunked sets have es = 8,
+// cs = 8 N; es = 0, cs = 8 broadcasts one label row to every element (the legacy rescale's Z_2 residue)
 struct In {
     const int16_t* p[kMaxRes];
+    int64_t es[kMaxRes], cs[kMaxRes];
     int n[kMaxRes];
 };
 
@@ -118,14 +137,6 @@ __device__ __forceinline__ u128 aes_keyed(const AesCtx& a, u128 in, const uint32
            ((static_cast<uint64_t>(bswap32(o1)) << 32) | bswap32(o0));
 }
 
-// Prg::label (core.h): block b of a label = AES_seed(stream || ctr + b); its m = ModC::pm least significant
-// base-q digits are components b*m .. b*m + m - 1
-__device__ __forceinline__ void prg_digits(u128 V, const ModC& m, int cnt, int16_t* out) {
-    DigitStream ds;
-    ds.init(V);
-    for (int u = 0; u < cnt; ++u) out[u] = static_cast<int16_t>(ds.next(m));
-}
-
 __device__ __forceinline__ uint64_t stream_of(uint64_t layer, uint64_t slot, uint64_t e, uint64_t mask) {
     return ((layer << 44) ^ (slot << 36) ^ e) ^ mask;
 }
@@ -138,7 +149,7 @@ struct Gadget {
     int64_t entries;  // per element
     int nblk;         // AES-CTR blocks drawn per element (sum over draws)
     uint64_t layer, sslot, mask;  // PRG stream of this gadget: stream_of(layer, sslot, e, mask)
-    int16_t* S;       // scratch [N][nslots][kW]
+    int16_t* S;       // scratch: slot s is a chunked label set of kW components ([kW / 8][N][8]) at S + s * kW * N
     u128* PB;         // payload bank [row][N] (PayDesc rows)
     int64_t N;
     int mrs[kMaxMrs]; // MRS base of the sign gadget (per-digit output moduli of the fanned-out approx projections)
@@ -146,6 +157,38 @@ struct Gadget {
     const int* fan;       // F_FAN: target moduli [a1 + target]
     const int* fbank;     // F_FAN: [a1 + target] 1 + payload bank row of value 0 (k_payloads), 0: computed inline
 };
+
+// slot s as a chunked label set, and element e's view of it
+__host__ __device__ __forceinline__ int16_t* slot_base(const Gadget& g, int s) {
+    return g.S + static_cast<int64_t>(s) * kW * g.N;
+}
+__device__ __forceinline__ LRef slot_ref(const Gadget& g, int s, int64_t e) {
+    return LRef{slot_base(g, s) + e * kCh, g.N * kCh};
+}
+
+typedef uint32_t u32x4a __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ u32x4a ld_chunk(LRef a, int c8) { return *reinterpret_cast<const u32x4a*>(a.p + c8 * a.cs); }
+__device__ __forceinline__ void st_chunk(int16_t* p, const u32x4a& v) { *reinterpret_cast<u32x4a*>(p) = v; }
+__device__ __forceinline__ void unpack8(const u32x4a& v, uint32_t (&d)[8]) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        d[2 * u] = v[u] & 0xffffu;
+        d[2 * u + 1] = v[u] >> 16;
+    }
+}
+__device__ __forceinline__ u32x4a pack8(const uint32_t (&d)[8]) {
+    u32x4a v;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) v[u] = d[2 * u] | (d[2 * u + 1] << 16);
+    return v;
+}
+__device__ __forceinline__ void add8(uint32_t (&acc)[8], const u32x4a& v) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        acc[2 * u] += v[u] & 0xffffu;
+        acc[2 * u + 1] += v[u] >> 16;
+    }
+}
 
 // Stage a gadget's small descriptor array (draws / projections) in LDS so the
 // per-thread binary search costs LDS, not dependent global round trips.
@@ -159,21 +202,24 @@ __device__ __forceinline__ void lds_stage(T* dst, const T* src, int n) {
     for (int i = threadIdx.x; i < words; i += blockDim.x) d[i] = s[i];
 }
 
-// one thread per (element, AES-CTR block): each block yields ModC::pm
-// consecutive components of one draw (Prg::label order), extracted as the
-// base-q digits of the block (DigitStream: one 128-bit long division per
-// chunk of digits), so every lane does exactly one AES.
+// One thread per (AES-CTR block, element), block-major: the lanes of a wave are
+// consecutive elements drawing the same block, so the binary search is (mostly)
+// wave-uniform and the stores land in neighbouring chunks. Block b of a draw
+// yields ModC::pm consecutive components (Prg::label order) as the base-q
+// digits of the block (DigitStream: one 128-bit long division per chunk of
+// digits).
 __global__ __launch_bounds__(kGB) void k_draw(Ctx c, Gadget g) {
     __shared__ __attribute__((aligned(16))) uint32_t lds_aes[DASH_AES_LDS_WORDS];
     __shared__ Draw sd[kMaxDesc];
     lds_stage(sd, g.draws, g.ndraws);
     aes_lds_fill(lds_aes, c.te0);
     const AesCtx aes = aes_ctx(lds_aes, nullptr);
-    const int64_t total = g.N * g.nblk;
+    const int64_t N = g.N;
+    const int64_t total = N * g.nblk;
     for (int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < total;
          i += static_cast<int64_t>(gridDim.x) * blockDim.x) {
-        const int64_t e = i / g.nblk;
-        const int b = static_cast<int>(i - e * g.nblk);
+        const int b = static_cast<int>(i / N);
+        const int64_t e = i - static_cast<int64_t>(b) * N;
         int lo = 0, hi = g.ndraws - 1;
         while (lo < hi) {  // last draw with ctr <= b
             const int mid = (lo + hi + 1) >> 1;
@@ -185,16 +231,22 @@ __global__ __launch_bounds__(kGB) void k_draw(Ctx c, Gadget g) {
         const int j = static_cast<int>(m.pm) * (b - d.ctr);
         const int cnt = min(static_cast<int>(m.pm), static_cast<int>(m.n) - j);
         const uint64_t stream = stream_of(g.layer, g.sslot, static_cast<uint64_t>(e), g.mask);
-        const u128 r = aes_keyed(aes, (static_cast<u128>(stream) << 64) | static_cast<uint64_t>(b), c.rk);
-        prg_digits(r, m, cnt, g.S + (e * g.nslots + d.slot) * kW + j);
+        DigitStream ds;
+        ds.init(aes_keyed(aes, (static_cast<u128>(stream) << 64) | static_cast<uint64_t>(b), c.rk));
+        int16_t* out = slot_base(g, d.slot) + e * kCh;
+        const int64_t cs = N * kCh;
+        for (int u = 0; u < cnt; ++u) {
+            const int q = j + u;
+            out[(q >> 3) * cs + (q & 7)] = static_cast<int16_t>(ds.next(m));
+        }
     }
 }
 
-__device__ __forceinline__ const int16_t* label_ref(const Ctx& c, const Gadget& g, const In& in, int64_t e, int kind,
-                                                    int idx, int q) {
-    if (kind == S_INPUT) return in.p[idx] + e * in.n[idx];
-    if (kind == S_SLOT) return g.S + (e * g.nslots + idx) * kW;
-    return c.Z + static_cast<int64_t>(q) * kW;
+__device__ __forceinline__ LRef label_ref(const Ctx& c, const Gadget& g, const In& in, int64_t e, int kind, int idx,
+                                          int q) {
+    if (kind == S_INPUT) return LRef{in.p[idx] + e * in.es[idx], in.cs[idx]};
+    if (kind == S_SLOT) return slot_ref(g, idx, e);
+    return row_ref(c.Z + static_cast<int64_t>(q) * kW);
 }
 
 // sign derive: sum2[q] = sum_{j<=k} bases[q][j]; sum = carry_final + sum_j mrs[j][0]
@@ -206,133 +258,91 @@ struct SignSlots {
     int dmod[kMaxMrs];      // fused: modulus of digit d's labels (SignPlan::digit_mod)
 };
 
-// One thread per element; slot rows are kW-aligned (256 B), so components
-// move 8 at a time (16-B loads/stores; lanes read rows of different elements,
-// and per-component loads were L1 tag-rate bound). Rows are kW wide, so the
-// 8-wide tail past n stays inside the row and is never stored.
-typedef uint32_t u32x4a __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ u32x4a ld8a(const int16_t* p) { return *reinterpret_cast<const u32x4a*>(p); }
-__device__ __forceinline__ void add8(uint32_t (&acc)[8], const u32x4a& v) {
+// dst = sum of `cnt` source slots (src0 + i * step) [+ one extra label ex] mod m; 8 components per step
+__device__ __forceinline__ void slot_sum(const Gadget& g, int64_t e, int dst, int src0, int step, int cnt, LRef ex,
+                                         bool has_ex, const ModC& m) {
+    const int n = static_cast<int>(m.n);
+    const LRef d = slot_ref(g, dst, e);
+    for (int c8 = 0; c8 < chunks_of(n); ++c8) {
+        uint32_t acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        if (has_ex) add8(acc, ld_chunk(ex, c8));
+        for (int i = 0; i < cnt; ++i) add8(acc, ld_chunk(slot_ref(g, src0 + i * step, e), c8));
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-        acc[2 * u] += v[u] & 0xffffu;
-        acc[2 * u + 1] += v[u] >> 16;
-    }
-}
-__device__ __forceinline__ void st8a(int16_t* p, const uint32_t (&acc)[8], const ModC& m, int valid) {
-    if (valid >= 8) {
-        u32x4a o;
-#pragma unroll
-        for (int u = 0; u < 4; ++u) o[u] = modq(acc[2 * u], m) | (modq(acc[2 * u + 1], m) << 16);
-        *reinterpret_cast<u32x4a*>(p) = o;
-    } else {
-        for (int u = 0; u < valid; ++u) p[u] = static_cast<int16_t>(modq(acc[u], m));
+        for (int u = 0; u < 8; ++u) acc[u] = modq(acc[u], m);
+        st_chunk(const_cast<int16_t*>(d.p) + c8 * d.cs, pack8(acc));  // chunks past n stay inside the slot
     }
 }
 
 __global__ __launch_bounds__(256) void k_sign_derive(Ctx c, Gadget g, SignSlots s) {
     const int64_t e = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
     if (e >= g.N) return;
-    int16_t* S = g.S + e * g.nslots * kW;
     const int k = s.k, t = s.t;
+    const LRef none{nullptr, 0};
     if (s.fused) {
         // digit q (d = t-1-q): sum_j approx[j][d] (+ carry of the previous digit, none for q = 0);
         // MSD: sum_j approx[j][0] + last carry (none when t = 1)
         for (int q = 0; q <= t - 1; ++q) {
             const int d = t - 1 - q;
             const ModC Mo = c.mc[s.dmod[d]];
-            const int n = static_cast<int>(Mo.n);
-            int16_t* dst = S + (d == 0 ? s.sum_slot : s.sum2_slot0 + q) * kW;
-            for (int i0 = 0; i0 < n; i0 += 8) {
-                uint32_t acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-                if (q > 0) add8(acc, ld8a(S + (s.newc_slot0 + q - 1) * kW + i0));
-                for (int j = 0; j < k; ++j) add8(acc, ld8a(S + (s.mrs_slot0 + j * t + d) * kW + i0));
-                st8a(dst + i0, acc, Mo, n - i0);
-            }
+            const int dst = d == 0 ? s.sum_slot : s.sum2_slot0 + q;
+            slot_sum(g, e, dst, s.mrs_slot0 + d, t, k, q > 0 ? slot_ref(g, s.newc_slot0 + q - 1, e) : none, q > 0, Mo);
         }
         return;
     }
     for (int q = 0; q + 1 < t; ++q) {
         const int d = t - 1 - q;
-        const int mo = (k + 1) * s.mrs[d];
-        const ModC Mo = c.mc[mo];
-        const int n = static_cast<int>(Mo.n);
-        int16_t* dst = S + (s.sum2_slot0 + q) * kW;
-        const int16_t* b0 = S + (s.bases_slot0 + q * s.stride_q) * kW;
-        for (int i0 = 0; i0 < n; i0 += 8) {
-            uint32_t acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-            for (int j = 0; j <= k; ++j) add8(acc, ld8a(b0 + j * kW + i0));
-            st8a(dst + i0, acc, Mo, n - i0);
-        }
+        const ModC Mo = c.mc[(k + 1) * s.mrs[d]];
+        slot_sum(g, e, s.sum2_slot0 + q, s.bases_slot0 + q * s.stride_q, 1, k + 1, none, false, Mo);
     }
     const int m0 = s.mrs[0];
     const ModC M0 = c.mc[m0];
-    const int n0 = static_cast<int>(M0.n);
-    const int16_t* carry = t >= 2 ? S + (s.newc_slot0 + (t - 2) * s.stride_q) * kW : c.Z + static_cast<int64_t>(m0) * kW;
-    int16_t* sum = S + s.sum_slot * kW;
-    for (int i0 = 0; i0 < n0; i0 += 8) {
-        uint32_t acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-        add8(acc, ld8a(carry + i0));
-        for (int j = 0; j < k; ++j) add8(acc, ld8a(S + (s.mrs_slot0 + j * t) * kW + i0));
-        st8a(sum + i0, acc, M0, n0 - i0);
-    }
+    const LRef carry = t >= 2 ? slot_ref(g, s.newc_slot0 + (t - 2) * s.stride_q, e)
+                              : row_ref(c.Z + static_cast<int64_t>(m0) * kW);
+    slot_sum(g, e, s.sum_slot, s.mrs_slot0, t, k, carry, true, M0);
 }
 
-// Label rows are contiguous int16 runs (label-major inputs, kW-wide slots).
-// In the element-tiled k_project the 64 lanes of a wave read 64 different
-// rows, so every load instruction costs up to 64 L1 tag lookups: rows are read
-// 8 components (16 B) per load (global_load_dwordx4; gfx950 allows the 2-byte
-// aligned addresses of packed input rows), never past the row end (the tail
-// is read per component), two chunks in flight per step.
-constexpr int kPC = 16;  // components staged per step by the per-component loaders
-typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-struct __attribute__((packed, aligned(2))) Row8 {
-    u32x4 v;
-};
-__device__ __forceinline__ u32x4 ld_row8(const int16_t* p) {
-    Row8 t;
-    __builtin_memcpy(&t, p, 16);
-    return t.v;
-}
-__device__ __forceinline__ uint32_t lane16(const u32x4& v, int u) {  // component u (0..7), zero-extended
-    const uint32_t w = v[u >> 1];
-    return (u & 1) ? (w >> 16) : (w & 0xffffu);
-}
-
-// digits (a_c + f * b_c) mod m of two label rows a, b (components in [0, m)), pushed into cf
-__device__ __forceinline__ void push_row(CompressFwd& cf, const int16_t* a, const int16_t* b, uint32_t f,
-                                         const ModC& m) {
+// digits (a_q + f * b_q) mod m of two labels (components in [0, m)) pushed into cf, 8 per chunk load;
+// two chunks in flight per step
+__device__ __forceinline__ void push_row(CompressFwd& cf, LRef a, LRef b, uint32_t f, const ModC& m) {
     const int n = static_cast<int>(m.n);
-    int q0 = 0;
-    for (; q0 + 16 <= n; q0 += 16) {
-        const u32x4 a0 = ld_row8(a + q0), a1 = ld_row8(a + q0 + 8);
-        const u32x4 b0 = ld_row8(b + q0), b1 = ld_row8(b + q0 + 8);
+    const int nc = static_cast<int>(chunks_of(n));
+    int c8 = 0;
+    for (; c8 + 2 <= nc; c8 += 2) {
+        uint32_t a0[8], a1[8], b0[8], b1[8];
+        unpack8(ld_chunk(a, c8), a0);
+        unpack8(ld_chunk(a, c8 + 1), a1);
+        unpack8(ld_chunk(b, c8), b0);
+        unpack8(ld_chunk(b, c8 + 1), b1);
+        const int q0 = c8 * 8;
 #pragma unroll
-        for (int u = 0; u < 8; ++u) cf.push(modq(lane16(a0, u) + f * lane16(b0, u), m), m);
+        for (int u = 0; u < 8; ++u)
+            if (q0 + u < n) cf.push(modq(a0[u] + f * b0[u], m), m);
 #pragma unroll
-        for (int u = 0; u < 8; ++u) cf.push(modq(lane16(a1, u) + f * lane16(b1, u), m), m);
+        for (int u = 0; u < 8; ++u)
+            if (q0 + 8 + u < n) cf.push(modq(a1[u] + f * b1[u], m), m);
     }
-    if (q0 + 8 <= n) {
-        const u32x4 a0 = ld_row8(a + q0), b0 = ld_row8(b + q0);
+    if (c8 < nc) {
+        uint32_t a0[8], b0[8];
+        unpack8(ld_chunk(a, c8), a0);
+        unpack8(ld_chunk(b, c8), b0);
+        const int q0 = c8 * 8;
 #pragma unroll
-        for (int u = 0; u < 8; ++u) cf.push(modq(lane16(a0, u) + f * lane16(b0, u), m), m);
-        q0 += 8;
+        for (int u = 0; u < 8; ++u)
+            if (q0 + u < n) cf.push(modq(a0[u] + f * b0[u], m), m);
     }
-    for (; q0 < n; ++q0)
-        cf.push(modq(static_cast<uint32_t>(static_cast<uint16_t>(a[q0])) + f * static_cast<uint16_t>(b[q0]), m), m);
 }
 
 // key = x + i*R (mod m), compressed from the least significant digit
-__device__ __forceinline__ u128 proj_key(const int16_t* x, const int16_t* R, int i, const ModC& m, uint32_t& color) {
+__device__ __forceinline__ u128 proj_key(LRef x, LRef R, int i, const ModC& m, uint32_t& color) {
     CompressFwd kc;
     kc.init();
     push_row(kc, x, R, static_cast<uint32_t>(i), m);
-    color = modq(static_cast<uint32_t>(x[0] + i * R[0]), m);
+    color = modq(static_cast<uint32_t>(static_cast<uint16_t>(x.p[0]) + i * static_cast<uint16_t>(R.p[0])), m);
     return kc.finish();
 }
 
 // payload = o + f*R (mod m), o, f, R in [0, m)
-__device__ __forceinline__ u128 proj_payload(const int16_t* o, const int16_t* R, uint32_t f, const ModC& m) {
+__device__ __forceinline__ u128 proj_payload(LRef o, LRef R, uint32_t f, const ModC& m) {
     CompressFwd pc;
     pc.init();
     push_row(pc, o, R, f, m);
@@ -340,14 +350,14 @@ __device__ __forceinline__ u128 proj_payload(const int16_t* o, const int16_t* R,
 }
 
 // one thread per (element, table entry). Element-tiled order: the 64 lanes of
-// a wavefront are 64 elements of one tile, all on the SAME table entry r, so
-// the projection descriptor, i, the label widths (loop trip counts), the
-// moduli and the function are wave-uniform. They are moved to SGPRs
-// explicitly (readfirstlane): the digit loops then branch on scalar
+// a wavefront are 64 consecutive elements of one tile, all on the SAME table
+// entry r, so the projection descriptor, i, the label widths (loop trip
+// counts), the moduli and the function are wave-uniform. They are moved to
+// SGPRs explicitly (readfirstlane): the digit loops then branch on scalar
 // conditions instead of exec masks, and the compressor's running power of the
-// modulus (PW, pt, digit counters) is scalar work issued beside the vector
-// digits. Consecutive waves walk the entries of the same 64 elements, so their
-// label rows stay cached.
+// modulus is scalar work issued beside the vector digits. Labels are chunked
+// component-major: one coalesced 16-byte load per lane covers 8 components;
+// consecutive waves walk the entries of the same 64 elements.
 constexpr int kTile = 64;
 #ifndef DASH_GG_PB
 #define DASH_GG_PB 512
@@ -426,9 +436,9 @@ __global__ __launch_bounds__(kPB) void k_project(Ctx c, Gadget g, In in, Tables 
         // the last tile's spare lanes recompute element N-1 (uniform control flow) and skip the store
         const int64_t e_raw = tile * kTile + lane;
         const int64_t e = e_raw < N ? e_raw : N - 1;
-        const int16_t* inl = label_ref(c, g, in, e, P.in_kind, P.in_idx, P.pin);
+        const LRef inl = label_ref(c, g, in, e, P.in_kind, P.in_idx, P.pin);
         uint32_t color;
-        const u128 H = aes_encrypt(aes, proj_key(inl, c.R + static_cast<int64_t>(P.pin) * kW, i, mi, color));
+        const u128 H = aes_encrypt(aes, proj_key(inl, row_ref(c.R + static_cast<int64_t>(P.pin) * kW), i, mi, color));
         if (P.fn == F_LUT) {
             // approx fan-out: digit d's entry at off + color*t + d, payload mrs0_slot + d + lut[j][i][d] * R_{m_d}
             const int t = P.stride;
@@ -439,8 +449,8 @@ __global__ __launch_bounds__(kPB) void k_project(Ctx c, Gadget g, In in, Tables 
                 int64_t f = c.lut[c.lut_off[P.a0] + i * t + d];
                 int64_t cm = f % pout;
                 if (cm < 0) cm += pout;
-                const int16_t* ol = g.S + (e * g.nslots + P.out_slot + d) * kW;
-                const u128 pay = proj_payload(ol, c.R + static_cast<int64_t>(pout) * kW, static_cast<uint32_t>(cm), md);
+                const u128 pay = proj_payload(slot_ref(g, P.out_slot + d, e), row_ref(c.R + static_cast<int64_t>(pout) * kW),
+                                              static_cast<uint32_t>(cm), md);
                 if (e_raw < N) row[d] = pay + H;
             }
             continue;
@@ -459,8 +469,8 @@ __global__ __launch_bounds__(kPB) void k_project(Ctx c, Gadget g, In in, Tables 
                 } else {
                     const int pout = rfl(g.fan[P.a1 + d]);
                     const ModC md = rfl_modc(c.mc[pout]);
-                    const int16_t* ol = g.S + (e * g.nslots + P.out_slot + d) * kW;
-                    pay = proj_payload(ol, c.R + static_cast<int64_t>(pout) * kW, cm, md);
+                    pay = proj_payload(slot_ref(g, P.out_slot + d, e), row_ref(c.R + static_cast<int64_t>(pout) * kW), cm,
+                                       md);
                 }
                 if (e_raw < N) row[d] = pay + H;
             }
@@ -479,32 +489,23 @@ __global__ __launch_bounds__(kPB) void k_project(Ctx c, Gadget g, In in, Tables 
             case F_DIV: f = i / P.a0; break;
             case F_DIVMOD: f = (i / P.a0) % P.a1; break;
             case F_SIGN: f = i < P.a0 ? P.a2 : P.a1; break;  // a0 = half, a1 = lower, a2 = upper
-            case F_MULR: {
-                const int16_t* x = label_ref(c, g, in, e, S_INPUT, P.a0, 0);
-                f = static_cast<int64_t>(i) * x[0];
-                break;
-            }
-            case F_NEGR: {
-                const int16_t* x = label_ref(c, g, in, e, S_INPUT, P.a0, 0);
-                f = -(static_cast<int64_t>(i) + x[0]);
-                break;
-            }
+            case F_MULR: f = static_cast<int64_t>(i) * in.p[P.a0][e * in.es[P.a0]]; break;
+            case F_NEGR: f = -(static_cast<int64_t>(i) + in.p[P.a0][e * in.es[P.a0]]); break;
             default: f = i;
         }
         int64_t cm = f % P.pout;
         if (cm < 0) cm += P.pout;
-        const int16_t* ol = g.S + (e * g.nslots + P.out_slot) * kW;
-        const int16_t* oR = P.outr_kind == R_BANK ? c.R + static_cast<int64_t>(P.pout) * kW
-                                                  : label_ref(c, g, in, e, S_INPUT, P.outr_idx, 0);
-        const u128 pay = proj_payload(ol, oR, static_cast<uint32_t>(cm), mo);
+        const LRef oR = P.outr_kind == R_BANK ? row_ref(c.R + static_cast<int64_t>(P.pout) * kW)
+                                              : label_ref(c, g, in, e, S_INPUT, P.outr_idx, 0);
+        const u128 pay = proj_payload(slot_ref(g, P.out_slot, e), oR, static_cast<uint32_t>(cm), mo);
         if (e_raw < N) tb.t[P.table][e * tb.row[P.table] + P.off + static_cast<int64_t>(color) * P.stride] = pay + H;
     }
 }
 
 // Mixed-radix rescale (gadgets.h RescaleMrsPlan), garbler side of the free
-// operations, one thread per element: key base labels K_i = L_i - sum_{l<i}
-// P_{l,i}, the mod-T accumulator r = sum_i P_{i,T}, then the output base labels
-// (in place) Y_0 = F_0, Y_j = S^-1 L_j + F_j.
+// operations, one thread per element, 8 components per load: key base labels
+// K_i = L_i - sum_{l<i} P_{l,i}, the mod-T accumulator r = sum_i P_{i,T}, then
+// the output base labels (in place) Y_0 = F_0, Y_j = S^-1 L_j + F_j.
 struct MrsG {
     int k, T;
     int crt[kMaxRes], sinv[kMaxRes];
@@ -512,89 +513,52 @@ struct MrsG {
     int sub[kMaxRes][kMaxRes];  // digit-target slots subtracted from residue j's key
     int tslot[kMaxRes];         // slot of digit i's T target
     int key0, acc, fin0;
-    int16_t* L[kMaxRes];  // label-major [N][n_j], updated in place
+    int16_t* L[kMaxRes];  // chunked [n_j / 8][N][8], updated in place
 };
-// 8 components per step: slot rows are kW-aligned (16-B loads/stores), the
-// label-major input rows [N][n_j] are read 16 B at a time at 2-B alignment
-// (unaligned global loads) except the row tail, which goes per component so
-// the last element never reads past its array.
-__device__ __forceinline__ void unpack8(const u32x4a& v, uint32_t (&d)[8]) {
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-        d[2 * u] = v[u] & 0xffffu;
-        d[2 * u + 1] = v[u] >> 16;
-    }
-}
-__device__ __forceinline__ u32x4a pack8(const uint32_t (&d)[8]) {
-    u32x4a v;
-#pragma unroll
-    for (int u = 0; u < 4; ++u) v[u] = d[2 * u] | (d[2 * u + 1] << 16);
-    return v;
-}
 
 __global__ __launch_bounds__(256) void k_mrs_derive(Ctx c, Gadget g, MrsG a) {
     const int64_t e = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
     if (e >= g.N) return;
-    int16_t* S = g.S + e * g.nslots * kW;
+    const int64_t cs = g.N * kCh;
     const int k = a.k;
     for (int j = 0; j < k; ++j) {
         const int p = a.crt[j];
         const ModC m = c.mc[p];
-        const int n = static_cast<int>(m.n);
-        int16_t* Lj = a.L[j] + e * n;
-        int16_t* K = S + (a.key0 + j) * kW;
-        const int16_t* F = S + (a.fin0 + j) * kW;
-        for (int q0 = 0; q0 < n; q0 += 8) {
-            const int cnt = n - q0 < 8 ? n - q0 : 8;
+        const int nc = static_cast<int>(chunks_of(static_cast<int>(m.n))), ns = a.nsub[j];
+        int16_t* Lj = a.L[j] + e * kCh;
+        const LRef K = slot_ref(g, a.key0 + j, e), F = slot_ref(g, a.fin0 + j, e);
+        for (int c8 = 0; c8 < nc; ++c8) {
             uint32_t x[8];
-            if (cnt == 8) {
-                unpack8(*reinterpret_cast<const u32x4a*>(Lj + q0), x);
-            } else {
-#pragma unroll
-                for (int u = 0; u < 8; ++u) x[u] = u < cnt ? static_cast<uint16_t>(Lj[q0 + u]) : 0u;
-            }
+            unpack8(*reinterpret_cast<const u32x4a*>(Lj + c8 * cs), x);
             // key: L_j - sum of the digit payload labels aimed at residue j
             uint32_t kv[8];
 #pragma unroll
-            for (int u = 0; u < 8; ++u) kv[u] = x[u] + static_cast<uint32_t>(p) * static_cast<uint32_t>(a.nsub[j]);
-            for (int l = 0; l < a.nsub[j]; ++l) {
+            for (int u = 0; u < 8; ++u) kv[u] = x[u] + static_cast<uint32_t>(p) * static_cast<uint32_t>(ns);
+            for (int l = 0; l < ns; ++l) {
                 uint32_t sv[8];
-                unpack8(ld8a(S + a.sub[j][l] * kW + q0), sv);
+                unpack8(ld_chunk(slot_ref(g, a.sub[j][l], e), c8), sv);
 #pragma unroll
                 for (int u = 0; u < 8; ++u) kv[u] -= sv[u];
             }
 #pragma unroll
             for (int u = 0; u < 8; ++u) kv[u] = modq(kv[u], m);
-            *reinterpret_cast<u32x4a*>(K + q0) = pack8(kv);  // slot rows are kW wide: the tail stays inside
-            // output base label (in place): Y_0 = F_0, Y_j = S^-1 L_j + F_j
+            st_chunk(const_cast<int16_t*>(K.p) + c8 * K.cs, pack8(kv));
+            // output base label (in place): Y_0 = F_0, Y_j = S^-1 L_j + F_j (chunk padding stays in the block)
             uint32_t fv[8], y[8];
-            unpack8(ld8a(F + q0), fv);
+            unpack8(ld_chunk(F, c8), fv);
 #pragma unroll
             for (int u = 0; u < 8; ++u) y[u] = j == 0 ? fv[u] : modq(x[u] * static_cast<uint32_t>(a.sinv[j]) + fv[u], m);
-            if (cnt == 8) {
-                *reinterpret_cast<u32x4a*>(Lj + q0) = pack8(y);
-            } else {
-#pragma unroll
-                for (int u = 0; u < 8; ++u)
-                    if (u < cnt) Lj[q0 + u] = static_cast<int16_t>(y[u]);
-            }
+            st_chunk(Lj + c8 * cs, pack8(y));
         }
     }
-    {
-        const int nT = static_cast<int>(c.mc[a.T].n);
-        int16_t* A = S + a.acc * kW;
-        for (int q0 = 0; q0 < nT; q0 += 8) {
-            uint32_t av[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-            for (int l = 0; l < k; ++l) {
-                uint32_t sv[8];
-                unpack8(ld8a(S + a.tslot[l] * kW + q0), sv);
+    const int ncT = static_cast<int>(chunks_of(static_cast<int>(c.mc[a.T].n)));
+    const LRef A = slot_ref(g, a.acc, e);
+    for (int c8 = 0; c8 < ncT; ++c8) {
+        uint32_t av[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        for (int l = 0; l < k; ++l) add8(av, ld_chunk(slot_ref(g, a.tslot[l], e), c8));
 #pragma unroll
-                for (int u = 0; u < 8; ++u) av[u] += sv[u];
-            }
-#pragma unroll
-            for (int u = 0; u < 8; ++u) av[u] &= static_cast<uint32_t>(a.T - 1);
-            *reinterpret_cast<u32x4a*>(A + q0) = pack8(av);
-        }
+        for (int u = 0; u < 8; ++u) av[u] &= static_cast<uint32_t>(a.T - 1);
+        st_chunk(const_cast<int16_t*>(A.p) + c8 * A.cs, pack8(av));
     }
 }
 
@@ -610,18 +574,26 @@ struct MrsSG {
 __global__ __launch_bounds__(256) void k_mrs_sign_derive(Ctx c, Gadget g, In in, MrsSG a) {
     const int64_t e = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
     if (e >= g.N) return;
-    int16_t* S = g.S + e * g.nslots * kW;
     for (int r = 0; r < a.k; ++r) {
-        const int p = a.crt[r], n = in.n[r];
-        const int16_t* x = in.p[r] + e * n;
-        int16_t* K = S + (a.key0 + r) * kW;
-        for (int q = 0; q < n; ++q) {
-            int v = x[q];
-            for (int u = 0; u < a.nsub[r]; ++u) {
-                v -= S[a.sub[r][u] * kW + q];
-                if (v < 0) v += p;
+        const int p = a.crt[r];
+        const ModC m = c.mc[p];
+        const int nc = static_cast<int>(chunks_of(in.n[r])), ns = a.nsub[r];
+        const LRef x{in.p[r] + e * in.es[r], in.cs[r]};
+        const LRef K = slot_ref(g, a.key0 + r, e);
+        for (int c8 = 0; c8 < nc; ++c8) {
+            uint32_t kv[8];
+            unpack8(ld_chunk(x, c8), kv);
+#pragma unroll
+            for (int u = 0; u < 8; ++u) kv[u] += static_cast<uint32_t>(p) * static_cast<uint32_t>(ns);
+            for (int l = 0; l < ns; ++l) {
+                uint32_t sv[8];
+                unpack8(ld_chunk(slot_ref(g, a.sub[r][l], e), c8), sv);
+#pragma unroll
+                for (int u = 0; u < 8; ++u) kv[u] -= sv[u];
             }
-            K[q] = static_cast<int16_t>(v);
+#pragma unroll
+            for (int u = 0; u < 8; ++u) kv[u] = modq(kv[u], m);
+            st_chunk(const_cast<int16_t*>(K.p) + c8 * K.cs, pack8(kv));
         }
     }
 }
@@ -634,45 +606,49 @@ __global__ __launch_bounds__(256) void k_payloads(Ctx c, Gadget g, const PayDesc
         const int r = static_cast<int>(x / g.N);
         const int64_t e = x - static_cast<int64_t>(r) * g.N;
         const PayDesc d = pd[r];
-        const int16_t* ol = g.S + (e * g.nslots + d.out_slot) * kW;
-        g.PB[x] = proj_payload(ol, c.R + static_cast<int64_t>(d.pout) * kW, static_cast<uint32_t>(d.f), c.mc[d.pout]);
+        g.PB[x] = proj_payload(slot_ref(g, d.out_slot, e), row_ref(c.R + static_cast<int64_t>(d.pout) * kW),
+                               static_cast<uint32_t>(d.f), c.mc[d.pout]);
     }
 }
 
 // ReLU mixed-mod half gates beyond the g/e projections: mini gate payloads
 // (16-bit, e[q]) and the output base labels out0[j] = sk04 - sk03.
+// Grid (elements, residue j): per thread the two mini entries of (e, j) and
+// the chunks of out0[j].
 struct MiniArgs {
     int k;
     int crt[kMaxRes];
     int sig_slot, sk_slot0;  // sk03_j = sk_slot0 + 2j, sk04_j = +1
-    int16_t* out[kMaxRes];   // next base labels [N][n_j]
+    int16_t* out[kMaxRes];   // next base labels, chunked
 };
 
 __global__ __launch_bounds__(256) void k_relu_finish(Ctx c, Gadget g, In in, Tables tb, MiniArgs m, const u128* hk) {
-    const int64_t total = g.N * m.k;
-    for (int64_t gi = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; gi < total;
-         gi += static_cast<int64_t>(gridDim.x) * blockDim.x) {
-        const int64_t e = gi / m.k;
-        const int j = static_cast<int>(gi % m.k);
-        const int p = m.crt[j];
-        const int16_t* x = in.p[j] + e * in.n[j];
-        const int16_t* sig = g.S + (e * g.nslots + m.sig_slot) * kW;
-        const int16_t* R2 = c.R + 2 * kW;
-        const int r = x[0];
+    const int j = blockIdx.y;
+    const int64_t N = g.N;
+    const int p = m.crt[j], nc = static_cast<int>(chunks_of(in.n[j]));
+    const ModC mp = c.mc[p];
+    const int16_t* R2 = c.R + 2 * kW;
+    for (int64_t e = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; e < N;
+         e += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+        const int r = in.p[j][e * in.es[j]];
+        const int sig0 = slot_ref(g, m.sig_slot, e).p[0];
         // mini gate y -> (y + r) mod p, 16-bit payload at t16[color] of entry e[k][2]; key hashes: k_bin_keys
         int16_t* t16 = reinterpret_cast<int16_t*>(tb.t[5] + (e * m.k + j) * 3 + 2);
         for (int i = 0; i < 2; ++i) {
-            const uint32_t color = static_cast<uint32_t>(sig[0] + i * R2[0]) & 1u;
-            const u128 H = hk[i * g.N + e];
+            const uint32_t color = static_cast<uint32_t>(sig0 + i * R2[0]) & 1u;
+            const u128 H = hk[i * N + e];
             const int fv = (i + r) % p;
             t16[color] = static_cast<int16_t>(static_cast<int16_t>(fv) + static_cast<int16_t>(static_cast<uint16_t>(H)));
         }
-        const int16_t* s3 = g.S + (e * g.nslots + m.sk_slot0 + 2 * j) * kW;
-        const int16_t* s4 = s3 + kW;
-        int16_t* o = m.out[j] + e * in.n[j];
-        for (int q = 0; q < in.n[j]; ++q) {
-            int v = s4[q] - s3[q];
-            o[q] = static_cast<int16_t>(v < 0 ? v + p : v);
+        const LRef s3 = slot_ref(g, m.sk_slot0 + 2 * j, e), s4 = slot_ref(g, m.sk_slot0 + 2 * j + 1, e);
+        int16_t* o = m.out[j] + e * kCh;
+        for (int c8 = 0; c8 < nc; ++c8) {
+            uint32_t a[8], b[8];
+            unpack8(ld_chunk(s4, c8), a);
+            unpack8(ld_chunk(s3, c8), b);
+#pragma unroll
+            for (int u = 0; u < 8; ++u) a[u] = modq(a[u] + static_cast<uint32_t>(p) - b[u], mp);
+            st_chunk(o + c8 * N * kCh, pack8(a));
         }
     }
 }
@@ -684,61 +660,57 @@ struct RsArgs {
     int crt[kMaxRes];
     int inv[kMaxRes];
     int ctr[kMaxRes];          // first trans-label AES-CTR block of residue j
-    int16_t* L[kMaxRes];       // [N][n_j], updated in place
+    int16_t* L[kMaxRes];       // chunked, updated in place
     const int16_t* up;         // [k][kW]
     const int16_t* down;       // [k][kW]
     uint64_t layer, sslot;     // trans stream = stream_of(layer, sslot, e, 0)
 };
 
-// 8 mod-2 components (0/1 in the low bit of each 16-bit half) -> 8 bits
+// Keys x + i*R_2 (i = 0, 1) of a mod-2 label x [+ add], hashed once per
+// element (hk[i][N]). Both users need the same two hashes for all k residues:
+// the legacy rescale's trans projections of L_0 + up_0 and the ReLU mini
+// gates of the sign output. A mod-2 label compresses to its component bits,
+// so the key is a bit pack and key 1 is key 0 XOR the bits of R_2. x is a
+// chunked label set (16 chunks of 8 components), add a uniform row.
 __device__ __forceinline__ uint32_t bits8(const u32x4a& v) {
     uint32_t b = 0;
 #pragma unroll
     for (int u = 0; u < 4; ++u) b |= ((v[u] & 1u) | ((v[u] >> 15) & 2u)) << (2 * u);
     return b;
 }
-
-// Keys x + i*R_2 (i = 0, 1) of a mod-2 label x = row(e) [+ add], hashed once
-// per element (hk[i][N]). Both users need the same two hashes for all k
-// residues: the legacy rescale's trans projections of L_0 + up_0 and the ReLU
-// mini gates of the sign output. A mod-2 label compresses to its component
-// bits, so the key is a bit pack and key 1 is key 0 XOR the bits of R_2.
-__global__ __launch_bounds__(kGB) void k_bin_keys(Ctx c, const int16_t* rows, int64_t stride, const int16_t* add,
-                                                  u128* hk, int64_t N) {
+__global__ __launch_bounds__(kGB) void k_bin_keys(Ctx c, const int16_t* x, const int16_t* add, u128* hk, int64_t N) {
     __shared__ __attribute__((aligned(16))) uint32_t lds_aes[DASH_AES_LDS_WORDS];
     aes_lds_fill(lds_aes, c.te0);
     const AesCtx aes = aes_ctx(lds_aes, nullptr);
-    const int16_t* R2 = c.R + 2 * kW;
+    const LRef R2 = row_ref(c.R + 2 * kW);
+    uint32_t rb[4] = {0, 0, 0, 0}, ab[4] = {0, 0, 0, 0};
+#pragma unroll
+    for (int c8 = 0; c8 < 16; ++c8) {
+        rb[c8 >> 2] |= bits8(ld_chunk(R2, c8)) << (8 * (c8 & 3));
+        if (add) ab[c8 >> 2] |= bits8(ld_chunk(row_ref(add), c8)) << (8 * (c8 & 3));
+    }
+    const u128 rbits = (static_cast<u128>((static_cast<uint64_t>(rb[3]) << 32) | rb[2]) << 64) |
+                       ((static_cast<uint64_t>(rb[1]) << 32) | rb[0]);
+    const u128 abits = (static_cast<u128>((static_cast<uint64_t>(ab[3]) << 32) | ab[2]) << 64) |
+                       ((static_cast<uint64_t>(ab[1]) << 32) | ab[0]);
     for (int64_t e = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; e < N;
          e += static_cast<int64_t>(gridDim.x) * blockDim.x) {
-        const int16_t* L0 = rows + e * stride;
-        uint32_t k0[4] = {0, 0, 0, 0}, r[4] = {0, 0, 0, 0};
+        const LRef xe{x + e * kCh, N * kCh};
+        uint32_t k0[4] = {0, 0, 0, 0};
 #pragma unroll
-        for (int q0 = 0; q0 < 128; q0 += 8) {
-            const u32x4a la = ld8a(L0 + q0), ra = ld8a(R2 + q0);
-            u32x4a s = la;
-            if (add) {
-                const u32x4a ua = ld8a(add + q0);
-#pragma unroll
-                for (int u = 0; u < 4; ++u) s[u] = la[u] + ua[u];  // halves <= 2: no carry between them
-            }
-            k0[q0 >> 5] |= bits8(s) << (q0 & 31);
-            r[q0 >> 5] |= bits8(ra) << (q0 & 31);
-        }
-        const u128 key0 = (static_cast<u128>((static_cast<uint64_t>(k0[3]) << 32) | k0[2]) << 64) |
-                          ((static_cast<uint64_t>(k0[1]) << 32) | k0[0]);
-        const u128 rb = (static_cast<u128>((static_cast<uint64_t>(r[3]) << 32) | r[2]) << 64) |
-                        ((static_cast<uint64_t>(r[1]) << 32) | r[0]);
+        for (int c8 = 0; c8 < 16; ++c8) k0[c8 >> 2] |= bits8(ld_chunk(xe, c8)) << (8 * (c8 & 3));
+        const u128 key0 = ((static_cast<u128>((static_cast<uint64_t>(k0[3]) << 32) | k0[2]) << 64) |
+                           ((static_cast<uint64_t>(k0[1]) << 32) | k0[0])) ^ abits;  // mod-2 add = XOR of the bits
         u128 h0, h1;
-        aes_encrypt2(aes, key0, key0 ^ rb, h0, h1);
+        aes_encrypt2(aes, key0, key0 ^ rbits, h0, h1);
         hk[e] = h0;
         hk[N + e] = h1;
     }
 }
 
-// One thread per (element, residue j >= 1): the trans projection of the
-// mod-2 residue into residue j plus the in-place update of L_j. The trans
-// output label is drawn one AES-CTR block (two components) at a time and
+// One thread per (element, residue j >= 1) (grid y = j - 1): the trans
+// projection of the mod-2 residue into residue j plus the in-place update of
+// L_j. The trans output label is drawn one AES-CTR block at a time and
 // consumed at once (no per-thread label array, no scratch). L_0 is not
 // written here: the sign gadget reads Z_2 for residue 0 directly (In with a
 // zero element stride) and k_rescale_post_g overwrites L_0 afterwards.
@@ -746,28 +718,25 @@ __global__ __launch_bounds__(kGB) void k_rescale_pre(Ctx c, RsArgs a, Tables tb,
     __shared__ __attribute__((aligned(16))) uint32_t lds_aes[DASH_AES_LDS_WORDS];
     aes_lds_fill(lds_aes, c.te0);
     const AesCtx aes = aes_ctx(lds_aes, nullptr);
-    const int km = a.k - 1;
-    const ModC m2 = c.mc[2];
+    const int j = 1 + static_cast<int>(blockIdx.y);
+    const int p = a.crt[j];
+    const ModC mj = c.mc[p];
+    const int n = static_cast<int>(mj.n), pm = static_cast<int>(mj.pm);
     const int16_t* R2 = c.R + 2 * kW;
-    for (int64_t gi = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; gi < N * km;
-         gi += static_cast<int64_t>(gridDim.x) * blockDim.x) {
-        const int64_t e = gi / km;
-        const int j = 1 + static_cast<int>(gi - e * km);
-        const int p = a.crt[j];
-        const ModC mj = c.mc[p];
-        const int n = static_cast<int>(mj.n);
-        // hashes of the two trans rows' keys (L_0 + up_0) + i*R_2: k_rescale_keys
-        const int16_t* L0 = a.L[0] + e * m2.n;
-        const uint32_t color0 = static_cast<uint32_t>(L0[0] + a.up[0]) & 1u;
+    const int16_t* Rp = c.R + static_cast<int64_t>(p) * kW;
+    const int16_t* upj = a.up + j * kW;
+    const int64_t cs = N * kCh;
+    for (int64_t e = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; e < N;
+         e += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+        // hashes of the two trans rows' keys (L_0 + up_0) + i*R_2: k_bin_keys
+        const int l00 = a.L[0][e * kCh];
+        const uint32_t color0 = static_cast<uint32_t>(l00 + a.up[0]) & 1u;
         const u128 H0 = hk[e], H1 = hk[N + e];
         const uint64_t stream = stream_of(a.layer, a.sslot, static_cast<uint64_t>(e), 0);
-        const int16_t* Rp = c.R + static_cast<int64_t>(p) * kW;
-        const int16_t* upj = a.up + j * kW;
-        int16_t* L = a.L[j] + e * n;
+        int16_t* L = a.L[j] + e * kCh;
         CompressFwd p0, p1;
         p0.init();
         p1.init();
-        const int pm = static_cast<int>(mj.pm);
         for (int q0 = 0, blk = 0; q0 < n; q0 += pm, ++blk) {
             DigitStream ds;
             ds.init(aes_keyed(aes, (static_cast<u128>(stream) << 64) | static_cast<uint64_t>(a.ctr[j] + blk), c.rk));
@@ -777,97 +746,36 @@ __global__ __launch_bounds__(kGB) void k_rescale_pre(Ctx c, RsArgs a, Tables tb,
                 const uint32_t o = ds.next(mj);
                 p0.push(o, mj);
                 p1.push(modq(o + static_cast<uint32_t>(Rp[q]), mj), mj);
-                int v = L[q] + upj[q];
+                int16_t& Lq = L[(q >> 3) * cs + (q & 7)];
+                int v = Lq + upj[q];
                 if (v >= p) v -= p;
                 v -= static_cast<int>(o);
                 if (v < 0) v += p;
-                L[q] = static_cast<int16_t>(modq(static_cast<uint32_t>(v * a.inv[j]), mj));
+                Lq = static_cast<int16_t>(modq(static_cast<uint32_t>(v * a.inv[j]), mj));
             }
         }
         u128* row = tb.t[6] + e * tb.row[6] + (j - 1) * 2;
-        const uint32_t color1 = static_cast<uint32_t>(L0[0] + a.up[0] + R2[0]) & 1u;
+        const uint32_t color1 = static_cast<uint32_t>(l00 + a.up[0] + R2[0]) & 1u;
         row[color0] = p0.finish() + H0;
         row[color1] = p1.finish() + H1;
     }
 }
 
 // After the sign gadget: L_0 = sign output; L -= down. Elementwise over
-// (residue j = blockIdx.y, element-component e*n_j + q).
+// (residue j = blockIdx.y, chunked index (c8 * N + e) * 8 + u).
 __global__ __launch_bounds__(256) void k_rescale_post_g(Ctx c, RsArgs a, Gadget g, int sig_slot) {
     const int j = blockIdx.y;
-    const int p = a.crt[j], n = static_cast<int>(c.mc[p].n);
+    const int p = a.crt[j];
+    const int64_t nc = chunks_of(static_cast<int>(c.mc[p].n));
     const int16_t* dn = a.down + j * kW;
     int16_t* L = a.L[j];
-    for (int64_t x = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; x < g.N * n;
+    const int64_t N = g.N;
+    const int16_t* sig = slot_base(g, sig_slot);
+    for (int64_t x = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; x < N * nc * kCh;
          x += static_cast<int64_t>(gridDim.x) * blockDim.x) {
-        const int64_t e = x / n;
-        const int q = static_cast<int>(x - e * n);
-        int v = (j == 0 ? g.S[(e * g.nslots + sig_slot) * kW + q] : L[x]) - dn[q];
+        const int q = static_cast<int>(x / (N * kCh)) * kCh + static_cast<int>(x & (kCh - 1));
+        const int v = (j == 0 ? sig[x] : L[x]) - dn[q];
         L[x] = static_cast<int16_t>(v < 0 ? v + p : v);
-    }
-}
-
-// Conv base labels (garbler side of the free linear layer, garbler.cpp K_CONV):
-// y[o][c] = (sum_{k: w[f][k] != 0} w[f][k] * x_k[c] + zc[f] * Z[c]) mod p with
-// x_k the input label under tap k (Z for padding taps). One thread per
-// (output position, component); kFT filters per thread so every input
-// component load feeds kFT MACs. Weights are laid out [f-chunk][K][kFT] and
-// indexed uniformly across the block, so they arrive as scalar loads.
-constexpr int kFT = 16;
-struct ConvG {
-    int C, H, W, F, kh, kw, sh, sw, ph, pw, OH, OW, K, n, p;
-};
-__global__ __launch_bounds__(256) void k_conv_garble(ConvG g, const int16_t* __restrict__ X, int16_t* __restrict__ Y,
-                                                     const int32_t* __restrict__ w, const int32_t* __restrict__ zc,
-                                                     const int16_t* __restrict__ Zp) {
-    const int f0 = blockIdx.y * kFT;
-    const int npos = g.OH * g.OW;
-    const int64_t t = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-    if (t >= static_cast<int64_t>(npos) * g.n) return;
-    const int pos = static_cast<int>(t / g.n), c = static_cast<int>(t - static_cast<int64_t>(pos) * g.n);
-    const int oy = pos / g.OW, ox = pos - oy * g.OW;
-    const int32_t* wc = w + static_cast<int64_t>(blockIdx.y) * g.K * kFT;
-    const int zv = Zp[c];
-    uint32_t acc[kFT];
-#pragma unroll
-    for (int f = 0; f < kFT; ++f) acc[f] = 0;
-    int k = 0;
-    for (int ci = 0; ci < g.C; ++ci)
-        for (int dy = 0; dy < g.kh; ++dy) {
-            const int iy = oy * g.sh - g.ph + dy;
-            for (int dx = 0; dx < g.kw; ++dx, ++k) {
-                const int ix = ox * g.sw - g.pw + dx;
-                const bool in = iy >= 0 && iy < g.H && ix >= 0 && ix < g.W;
-                const uint32_t xv = static_cast<uint32_t>(
-                    in ? X[(static_cast<int64_t>(ci * g.H + iy) * g.W + ix) * g.n + c] : zv);
-                const int32_t* wk = wc + k * kFT;
-#pragma unroll
-                // w, x < p < 2^24: full-rate v_mad_u32_u24 (a 32-bit product is a quarter-rate v_mul_lo_u32)
-                for (int f = 0; f < kFT; ++f) acc[f] = __umul24(static_cast<uint32_t>(wk[f]), xv) + acc[f];
-            }
-        }
-#pragma unroll
-    for (int f = 0; f < kFT; ++f) {
-        if (f0 + f >= g.F) break;
-        const uint32_t v = (acc[f] + static_cast<uint32_t>(zc[f0 + f]) * static_cast<uint32_t>(zv)) % static_cast<uint32_t>(g.p);
-        Y[(static_cast<int64_t>(f0 + f) * npos + pos) * g.n + c] = static_cast<int16_t>(v);
-    }
-}
-
-// Sign layer outputs: slot out_slot0 + o of every element -> label-major out[o]
-struct GatherArgs {
-    int16_t* out[kMaxRes];
-    int n[kMaxRes];
-    int k, slot0;
-};
-__global__ __launch_bounds__(256) void k_gather_slots(Gadget g, GatherArgs a) {
-    const int o = blockIdx.y;
-    const int n = a.n[o];
-    for (int64_t x = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; x < g.N * n;
-         x += static_cast<int64_t>(gridDim.x) * blockDim.x) {
-        const int64_t e = x / n;
-        const int q = static_cast<int>(x - e * n);
-        a.out[o][x] = g.S[(e * g.nslots + a.slot0 + o) * kW + q];
     }
 }
 
@@ -1435,7 +1343,7 @@ struct GpuGarbler::Impl {
     std::vector<DevBlock> alloc_labels(const std::vector<int>& mods, int64_t N) {
         std::vector<DevBlock> v(mods.size());
         for (size_t j = 0; j < mods.size(); ++j)
-            v[j].alloc(device, static_cast<size_t>(N) * nr_comps(mods[j]) * sizeof(int16_t));
+            v[j].alloc(device, static_cast<size_t>(N) * gg::chunks_of(nr_comps(mods[j])) * gg::kCh * sizeof(int16_t));
         return v;
     }
     void check_cur(const CrtLabels& host) const {
@@ -1490,6 +1398,8 @@ GpuGarbler::~GpuGarbler() {
     if (impl_) impl_->enter();
 }
 
+// Device labels are chunked component-major (gg::kCh): host label-major rows are transposed on the host
+// around the (rare) host<->device hand-offs.
 void GpuGarbler::to_device(const CrtLabels& cur) {
     Impl& I = *impl_;
     I.enter();
@@ -1498,11 +1408,16 @@ void GpuGarbler::to_device(const CrtLabels& cur) {
     for (const auto& l : cur) I.cur_mod.push_back(l.p);
     I.cur_N = cur[0].N;
     I.cur = I.alloc_labels(I.cur_mod, I.cur_N);
+    std::vector<int16_t> t;
     for (size_t j = 0; j < cur.size(); ++j) {
-        DASH_CHECK(cur[j].c.size() == static_cast<size_t>(cur[j].N) * cur[j].n, "gpu garbler: host labels are stale");
-        // pageable source: the copy is staged before the call returns, ordered on the garbling stream
-        HIPCHECK(hipMemcpyAsync(I.cur[j].p, cur[j].c.data(), cur[j].c.size() * sizeof(int16_t), hipMemcpyHostToDevice,
-                                gg::tl_st));
+        const Labels& L = cur[j];
+        DASH_CHECK(L.c.size() == static_cast<size_t>(L.N) * L.n, "gpu garbler: host labels are stale");
+        t.assign(static_cast<size_t>(gg::chunks_of(L.n)) * gg::kCh * L.N, 0);
+        for (i64 e = 0; e < L.N; ++e)
+            for (int q = 0; q < L.n; ++q)
+                t[((static_cast<size_t>(q >> 3)) * L.N + e) * gg::kCh + (q & 7)] = L.c[static_cast<size_t>(e) * L.n + q];
+        // pageable source: staged before the call returns, ordered on the garbling stream
+        HIPCHECK(hipMemcpyAsync(I.cur[j].p, t.data(), t.size() * sizeof(int16_t), hipMemcpyHostToDevice, gg::tl_st));
     }
 }
 
@@ -1510,21 +1425,60 @@ void GpuGarbler::to_host(CrtLabels& cur) {
     Impl& I = *impl_;
     I.enter();
     I.check_cur(cur);
+    std::vector<std::vector<int16_t>> t(cur.size());
     for (size_t j = 0; j < cur.size(); ++j) {
-        cur[j].c.resize(static_cast<size_t>(cur[j].N) * cur[j].n);
-        HIPCHECK(hipMemcpyAsync(cur[j].c.data(), I.cur[j].p, cur[j].c.size() * sizeof(int16_t), hipMemcpyDeviceToHost,
+        t[j].resize(static_cast<size_t>(cur[j].N) * gg::chunks_of(cur[j].n) * gg::kCh);
+        HIPCHECK(hipMemcpyAsync(t[j].data(), I.cur[j].p, t[j].size() * sizeof(int16_t), hipMemcpyDeviceToHost,
                                 gg::tl_st));
     }
     HIPCHECK(hipStreamSynchronize(gg::tl_st));
+    for (size_t j = 0; j < cur.size(); ++j) {
+        Labels& L = cur[j];
+        L.c.resize(static_cast<size_t>(L.N) * L.n);
+        for (i64 e = 0; e < L.N; ++e)
+            for (int q = 0; q < L.n; ++q)
+                L.c[static_cast<size_t>(e) * L.n + q] = t[j][((static_cast<size_t>(q >> 3)) * L.N + e) * gg::kCh + (q & 7)];
+    }
 }
+
+namespace {
+// 64-bit mix hash of a weight vector (public conv weights: the per-layer MFMA setup is cached by content)
+uint64_t weights_hash(const std::vector<i64>& w) {
+    uint64_t h = 0x9e3779b97f4a7c15ull ^ w.size();
+    for (i64 v : w) {
+        h ^= static_cast<uint64_t>(v) + 0x9e3779b97f4a7c15ull + (h << 6) + (h >> 2);
+        h *= 0xff51afd7ed558ccdull;
+    }
+    return h;
+}
+struct ConvPlanKey {
+    int dev;
+    uint64_t wh;
+    std::vector<i64> geom;
+    std::vector<int> mods;
+    bool operator<(const ConvPlanKey& o) const {
+        return std::tie(dev, wh, geom, mods) < std::tie(o.dev, o.wh, o.geom, o.mods);
+    }
+};
+// prepared MFMA conv arguments (weights images, zero counts, zero bias rows in device memory), per process
+std::map<ConvPlanKey, dev::ConvArgs>& conv_plans() {
+    static auto* m = new std::map<ConvPlanKey, dev::ConvArgs>();  // leaked: device buffers live as long as the process
+    return *m;
+}
+std::mutex& conv_plans_mutex() {
+    static std::mutex m;
+    return m;
+}
+}  // namespace
 
 // Conv base labels = the evaluator's garbled conv applied to the zero labels:
 // y = W x + (#zero weights + 1) Z (the +1 is the bias label's Z_p, the bias
-// itself being public). The labels are transposed to the evaluator's
-// component-major layout and run through the same int8 MFMA implicit-GEMM
-// kernel (launch_conv: k_conv_img, one launch for all residues); public
-// weights, zero counts and the all-zero bias rows are cached per process.
-// DASH_GG_CONV=valu selects the label-major VALU kernel (A/B).
+// itself being public), through the same int8 MFMA implicit-GEMM kernel
+// (launch_conv, one launch for all residues). The garbler's chunked labels
+// are unchunked into the kernel's component-major byte activations and its
+// output chunked back (one launch each for all residues). The public per-layer setup
+// (centered int8 weight images, zero counts, all-zero bias rows) is built
+// once per process and looked up by a hash of the weights.
 void GpuGarbler::conv(const ConvGeom& G, const std::vector<i64>& w, CrtLabels& cur) {
     Impl& I = *impl_;
     I.enter();
@@ -1538,113 +1492,93 @@ void GpuGarbler::conv(const ConvGeom& G, const std::vector<i64>& w, CrtLabels& c
     std::vector<int> mods = I.cur_mod;
     const int64_t Nin = I.cur_N, Nout = G.out_size();
     std::vector<DevBlock> out = I.alloc_labels(mods, Nout);
-    std::vector<void*> tmp;
-    static const bool valu = [] {
-        const char* e = std::getenv("DASH_GG_CONV");
-        return e && std::string(e) == "valu";
-    }();
-    if (valu) {
-        const int nch = (F + gg::kFT - 1) / gg::kFT;
-        for (size_t j = 0; j < mods.size(); ++j) {
-            const int p = mods[j];
-            std::vector<int32_t> wp(static_cast<size_t>(nch) * K * gg::kFT, 0), zc(static_cast<size_t>(nch) * gg::kFT, 0);
-            for (int f = 0; f < F; ++f) {
-                int z = 1;
-                for (int kk = 0; kk < K; ++kk) {
-                    const int v = static_cast<int>(w[static_cast<size_t>(f) * K + kk] % p);
-                    if (v == 0) ++z;
-                    wp[(static_cast<size_t>(f / gg::kFT) * K + kk) * gg::kFT + f % gg::kFT] = v;
-                }
-                zc[f] = z;
+    dev::ConvArgs a{};
+    {
+        ConvPlanKey key{I.device, weights_hash(w), {G.C, G.H, G.W, G.F, G.kh, G.kw, G.sh, G.sw, G.ph, G.pw}, mods};
+        std::lock_guard<std::mutex> lk(conv_plans_mutex());
+        auto it = conv_plans().find(key);
+        if (it != conv_plans().end()) {
+            a = it->second;
+        } else {
+            a.crt.k = static_cast<int>(mods.size());
+            for (int j = 0; j < a.crt.k; ++j) {
+                a.crt.p[j] = mods[j];
+                a.crt.n[j] = nr_comps(mods[j]);
+                a.crt.prefix[j] = a.crt.sum;
+                a.crt.sum += mods[j];
             }
-            gg::ConvG g{static_cast<int>(G.C), static_cast<int>(G.H), static_cast<int>(G.W), F, static_cast<int>(G.kh),
-                        static_cast<int>(G.kw), static_cast<int>(G.sh), static_cast<int>(G.sw), static_cast<int>(G.ph),
-                        static_cast<int>(G.pw), static_cast<int>(G.OH), static_cast<int>(G.OW), K, nr_comps(p), p};
-            const int32_t* dw = gg::dconst(wp.data(), wp.size());
-            const int32_t* dz = gg::dconst(zc.data(), zc.size());
-            const int64_t threads = G.OH * G.OW * static_cast<int64_t>(g.n);
-            DASH_CHECK((threads + 255) / 256 < (int64_t(1) << 31), "gpu garbler: conv grid too large");
-            hipLaunchKernelGGL(gg::k_conv_garble, dim3(static_cast<unsigned>((threads + 255) / 256), nch), dim3(256), 0,
-                               gg::tl_st, g, I.cur[j].as<int16_t>(), out[j].as<int16_t>(), dw, dz,
-                               I.c.Z + static_cast<int64_t>(p) * gg::kW);
-        }
-    } else {
-        dev::ConvArgs a{};
-        a.crt.k = static_cast<int>(mods.size());
-        for (int j = 0; j < a.crt.k; ++j) {
-            a.crt.p[j] = mods[j];
-            a.crt.n[j] = nr_comps(mods[j]);
-            a.crt.prefix[j] = a.crt.sum;
-            a.crt.sum += mods[j];
-        }
-        a.C = static_cast<int>(G.C); a.H = static_cast<int>(G.H); a.W = static_cast<int>(G.W);
-        a.F = F; a.kh = static_cast<int>(G.kh); a.kw = static_cast<int>(G.kw);
-        a.sh = static_cast<int>(G.sh); a.sw = static_cast<int>(G.sw);
-        a.ph = static_cast<int>(G.ph); a.pw = static_cast<int>(G.pw);
-        a.OH = static_cast<int>(G.OH); a.OW = static_cast<int>(G.OW);
-        a.Kpad = (K + 63) / 64 * 64;
-        a.use_mfma = 1;
-        int max_p = 0;
-        for (int j = 0; j < a.crt.k; ++j) max_p = std::max(max_p, mods[j]);
-        dev::conv_plan(a, max_p, true);
-        a.zero = I.c.Z;  // one GC: zero label component c of residue j at Z[p_j * kW + c]
-        a.lab_stride = 0;
-        a.img_off[0] = 0;
-        for (int j = 0; j < a.crt.k; ++j) {
-            const int p = mods[j], n = a.crt.n[j];
-            a.lab_off[j] = p * gg::kW;
-            a.img_off[j + 1] = a.img_off[j] + n;
-            std::vector<int16_t> wm(static_cast<size_t>(F) * K);
-            std::vector<int8_t> w8(static_cast<size_t>(F) * a.Kpad, 0);
-            std::vector<int32_t> zc(F, 1);
-            for (int f = 0; f < F; ++f)
-                for (int q = 0; q < K; ++q) {
-                    const int v = static_cast<int>(w[static_cast<size_t>(f) * K + q] % p);
-                    wm[static_cast<size_t>(f) * K + q] = static_cast<int16_t>(v);
-                    if (v == 0) ++zc[f];
-                    w8[static_cast<size_t>(f) * a.Kpad + q] = static_cast<int8_t>(v > p / 2 ? v - p : v);
+            a.C = static_cast<int>(G.C); a.H = static_cast<int>(G.H); a.W = static_cast<int>(G.W);
+            a.F = F; a.kh = static_cast<int>(G.kh); a.kw = static_cast<int>(G.kw);
+            a.sh = static_cast<int>(G.sh); a.sw = static_cast<int>(G.sw);
+            a.ph = static_cast<int>(G.ph); a.pw = static_cast<int>(G.pw);
+            a.OH = static_cast<int>(G.OH); a.OW = static_cast<int>(G.OW);
+            a.Kpad = (K + 63) / 64 * 64;
+            a.use_mfma = 1;
+            int max_p = 0;
+            for (int j = 0; j < a.crt.k; ++j) max_p = std::max(max_p, mods[j]);
+            dev::conv_plan(a, max_p, true);
+            a.lab_stride = 0;
+            a.img_off[0] = 0;
+            for (int j = 0; j < a.crt.k; ++j) {
+                const int p = mods[j], n = a.crt.n[j];
+                DASH_CHECK(p <= dev::kActMaxModulus, "gpu garbler: conv residue modulus above 255");
+                a.lab_off[j] = p * gg::kW;
+                a.img_off[j + 1] = a.img_off[j] + n;
+                std::vector<int16_t> wm(static_cast<size_t>(F) * K);
+                std::vector<int8_t> w8(static_cast<size_t>(F) * a.Kpad, 0);
+                std::vector<int32_t> zc(F, 1);
+                for (int f = 0; f < F; ++f)
+                    for (int q = 0; q < K; ++q) {
+                        const int v = static_cast<int>(w[static_cast<size_t>(f) * K + q] % p);
+                        wm[static_cast<size_t>(f) * K + q] = static_cast<int16_t>(v);
+                        if (v == 0) ++zc[f];
+                        w8[static_cast<size_t>(f) * a.Kpad + q] = static_cast<int8_t>(v > p / 2 ? v - p : v);
+                    }
+                a.w[j] = gg::dconst(wm.data(), wm.size());
+                a.zc[j] = gg::dconst(zc.data(), zc.size());
+                std::vector<int16_t> zb(static_cast<size_t>(F) * n, 0);
+                a.bias[j] = gg::dconst(zb.data(), zb.size());
+                a.w8[j] = nullptr;
+                a.w8r[j] = nullptr;
+                if (a.nbands > 0) {
+                    const std::vector<int8_t> w8r = dev::conv_w8r(a, w8, F);
+                    a.w8r[j] = gg::dconst(w8r.data(), w8r.size());
+                } else {
+                    a.w8[j] = gg::dconst(w8.data(), w8.size());
                 }
-            a.w[j] = gg::dconst(wm.data(), wm.size());
-            a.zc[j] = gg::dconst(zc.data(), zc.size());
-            std::vector<int16_t> zb(static_cast<size_t>(F) * n, 0);
-            a.bias[j] = gg::dconst(zb.data(), zb.size());
-            a.w8[j] = nullptr;
-            a.w8r[j] = nullptr;
-            if (p <= 255 && a.nbands > 0) {
-                const std::vector<int8_t> w8r = dev::conv_w8r(a, w8, F);
-                a.w8r[j] = gg::dconst(w8r.data(), w8r.size());
-            } else if (p <= 255) {
-                a.w8[j] = gg::dconst(w8.data(), w8.size());
             }
+            conv_plans().emplace(std::move(key), a);
         }
-        // label-major int16 [N][n] <-> the evaluator's component-major byte activations [n][N]
-        std::vector<DevBlock> xin(mods.size()), yout(mods.size());
-        dev::Act x{}, y{};
-        x.N = Nin;
-        y.N = Nout;
-        dev::TrRes ti{}, to{};
-        ti.k = to.k = a.crt.k;
-        for (int j = 0; j < a.crt.k; ++j) {
-            DASH_CHECK(mods[j] <= dev::kActMaxModulus, "gpu garbler: conv residue modulus above 255");
-            xin[j].alloc(I.device, static_cast<size_t>(Nin) * a.crt.n[j]);
-            yout[j].alloc(I.device, static_cast<size_t>(Nout) * a.crt.n[j]);
-            ti.in[j] = I.cur[j].as<int16_t>();
-            ti.out[j] = xin[j].as<dev::act_t>();
-            ti.rows[j] = Nin;
-            ti.cols[j] = a.crt.n[j];
-            to.in[j] = yout[j].as<dev::act_t>();
-            to.out[j] = out[j].as<int16_t>();
-            to.rows[j] = a.crt.n[j];
-            to.cols[j] = Nout;
-            x.p[j] = xin[j].as<dev::act_t>();
-            y.p[j] = yout[j].as<dev::act_t>();
-        }
-        dev::launch_transpose_to_act_res(ti, gg::tl_st);  // all residues in one launch
-        dev::launch_conv(a, x, y, 1, gg::tl_st);
-        dev::launch_transpose_from_act_res(to, gg::tl_st);
-        // xin / yout return to the block cache; later users are ordered behind these kernels on the null stream
     }
+    a.zero = I.c.Z;  // this GC's zero labels: component c of residue j at Z[p_j * kW + c]
+    // chunked int16 labels <-> the kernel's component-major byte activations
+    std::vector<DevBlock> xin(mods.size()), yout(mods.size());
+    dev::Act x{}, y{};
+    x.N = Nin;
+    y.N = Nout;
+    dev::TrRes ti{}, to{};
+    ti.k = to.k = a.crt.k;
+    for (int j = 0; j < a.crt.k; ++j) {
+        const int n = a.crt.n[j];
+        xin[j].alloc(I.device, static_cast<size_t>(Nin) * n);
+        yout[j].alloc(I.device, static_cast<size_t>(Nout) * n);
+        ti.in[j] = I.cur[j].as<int16_t>();
+        ti.out[j] = xin[j].as<dev::act_t>();
+        ti.rows[j] = n;
+        ti.cols[j] = Nin;
+        to.in[j] = yout[j].as<dev::act_t>();
+        to.out[j] = out[j].as<int16_t>();
+        to.rows[j] = n;
+        to.cols[j] = Nout;
+        x.p[j] = xin[j].as<dev::act_t>();
+        y.p[j] = yout[j].as<dev::act_t>();
+    }
+    dev::launch_unchunk_to_act_res(ti, gg::tl_st);  // all residues in one launch
+    dev::launch_conv(a, x, y, 1, gg::tl_st);
+    dev::launch_chunk_from_act_res(to, gg::tl_st);
+    // xin / yout return to the block cache; later users are ordered behind these kernels on the stream
     HIPCHECK(hipGetLastError());
+    std::vector<void*> tmp;
     gg::end_layer(tmp);
     tr_.mark("kernels");
     I.cur = std::move(out);
@@ -1688,6 +1622,8 @@ void GpuGarbler::sign_layer(uint64_t layer, const SignPlan& sp, CrtLabels& cur, 
     for (int j = 0; j < k; ++j) {
         in.p[j] = I.cur[j].as<int16_t>();
         in.n[j] = nr_comps(I.crt[j]);
+        in.es[j] = gg::kCh;  // chunked component-major
+        in.cs[j] = N * gg::kCh;
     }
     gg::Gadget g{};
     g.layer = layer;
@@ -1748,22 +1684,18 @@ void GpuGarbler::sign_layer(uint64_t layer, const SignPlan& sp, CrtLabels& cur, 
         // the sign gadget's payload bank (>= 2 rows, its readers are done: same stream) now holds the two
         // mini-gate key hashes of the sign output
         hipLaunchKernelGGL(gg::k_bin_keys, dim3(blocks_for(N, gg::kGB, 8192)), dim3(gg::kGB), 0, gg::tl_st, I.c,
-                           S + static_cast<int64_t>(L.out_slot0) * gg::kW, static_cast<int64_t>(L.nslots) * gg::kW,
+                           static_cast<const int16_t*>(gg::slot_base(g, L.out_slot0)),
                            static_cast<const int16_t*>(nullptr), g.PB, N);
-        hipLaunchKernelGGL(gg::k_relu_finish, dim3(blocks_for(N * k, 256, 8192)), dim3(256), 0, gg::tl_st, I.c, gm, in,
+        hipLaunchKernelGGL(gg::k_relu_finish, dim3(blocks_for(N, 256, 4096), k), dim3(256), 0, gg::tl_st, I.c, gm, in,
                            tb, ma, static_cast<const u128*>(g.PB));
         tG.to_array(*mmg, I.device);
         tE.to_array(*mme, I.device);
     } else {
-        // sign layer outputs: out0[o] slots (one per output residue) -> label-major device labels
-        gg::GatherArgs ga{};
-        ga.k = static_cast<int>(omods.size());
-        ga.slot0 = L.out_slot0;
-        for (int o = 0; o < ga.k; ++o) {
-            ga.out[o] = out[o].as<int16_t>();
-            ga.n[o] = nr_comps(omods[o]);
-        }
-        hipLaunchKernelGGL(gg::k_gather_slots, dim3(blocks_for(N * 128, 256, 4096), ga.k), dim3(256), 0, gg::tl_st, g, ga);
+        // sign layer outputs: out0[o] slots (one per output residue) are already component-major [n][N] blocks
+        for (size_t o = 0; o < omods.size(); ++o)
+            HIPCHECK(hipMemcpyAsync(out[o].p, gg::slot_base(g, L.out_slot0 + static_cast<int>(o)),
+                                    static_cast<size_t>(gg::chunks_of(nr_comps(omods[o]))) * gg::kCh * N * sizeof(int16_t),
+                                    hipMemcpyDeviceToDevice, gg::tl_st));
     }
     HIPCHECK(hipGetLastError());
     gg::end_layer(tmp);
@@ -1827,19 +1759,22 @@ void GpuGarbler::rescale_legacy_iter(uint64_t layer, int it, const RescalePlan& 
     // the payload bank is sized once for both users: rows 0-1 hold the trans key hashes until the sign gadget's
     // k_payloads (later on the same stream) overwrites them
     u128* PB = I.pbank(std::max<size_t>(2, L.pays.size()), N);
-    hipLaunchKernelGGL(gg::k_bin_keys, dim3(blocks_for(N, gg::kGB, 8192)), dim3(gg::kGB), 0, gg::tl_st, I.c, ra.L[0],
-                       int64_t(128), ra.up, PB, N);
-    hipLaunchKernelGGL(gg::k_rescale_pre, dim3(blocks_for(N * (k - 1), gg::kGB, 8192)), dim3(gg::kGB), 0, gg::tl_st, I.c,
+    hipLaunchKernelGGL(gg::k_bin_keys, dim3(blocks_for(N, gg::kGB, 8192)), dim3(gg::kGB), 0, gg::tl_st, I.c,
+                       static_cast<const int16_t*>(ra.L[0]), ra.up, PB, N);
+    hipLaunchKernelGGL(gg::k_rescale_pre, dim3(blocks_for(N, gg::kGB, 2048), k - 1), dim3(gg::kGB), 0, gg::tl_st, I.c,
                        ra, tb, PB, N);
     int16_t* S = I.scratch(static_cast<size_t>(N) * L.nslots * gg::kW * sizeof(int16_t));
     gg::In in{};
     for (int j = 0; j < k; ++j) {
         in.p[j] = I.cur[j].as<int16_t>();
         in.n[j] = nr_comps(I.crt[j]);
+        in.es[j] = gg::kCh;  // chunked component-major
+        in.cs[j] = N * gg::kCh;
     }
     DASH_CHECK(I.crt[0] == 2, "gpu garbler: legacy rescale needs residue 0 = 2");
-    in.p[0] = I.c.Z + 2 * gg::kW;  // residue 0 is Z_2 for every element (zero stride)
-    in.n[0] = 0;
+    in.p[0] = I.c.Z + 2 * gg::kW;  // residue 0 is Z_2 for every element (zero element stride)
+    in.es[0] = 0;
+    in.cs[0] = gg::kCh;
     gg::Gadget g{};
     g.layer = layer;
     g.sslot = 10 + it;
@@ -1914,9 +1849,9 @@ static std::vector<DevBlock> relu_mult_gates(GpuGarbler::Impl& I, const gg::Gadg
     ma.sk_slot0 = sk0;
     for (int j = 0; j < k; ++j) ma.out[j] = out[j].as<int16_t>();
     hipLaunchKernelGGL(gg::k_bin_keys, dim3(blocks_for(N, gg::kGB, 8192)), dim3(gg::kGB), 0, gg::tl_st, I.c,
-                       g.S + static_cast<int64_t>(sig_slot) * gg::kW, static_cast<int64_t>(g.nslots) * gg::kW,
-                       static_cast<const int16_t*>(nullptr), gm.PB, N);
-    hipLaunchKernelGGL(gg::k_relu_finish, dim3(blocks_for(N * k, 256, 8192)), dim3(256), 0, gg::tl_st, I.c, gm, in,
+                       static_cast<const int16_t*>(gg::slot_base(g, sig_slot)), static_cast<const int16_t*>(nullptr),
+                       gm.PB, N);
+    hipLaunchKernelGGL(gg::k_relu_finish, dim3(blocks_for(N, 256, 4096), k), dim3(256), 0, gg::tl_st, I.c, gm, in,
                        tb, ma, static_cast<const u128*>(gm.PB));
     return out;
 }
@@ -1984,6 +1919,8 @@ void GpuGarbler::relu_mrs(uint64_t layer, const SignMrsPlan& P, CrtLabels& cur, 
     for (int j = 0; j < k; ++j) {
         in.p[j] = I.cur[j].as<int16_t>();
         in.n[j] = nr_comps(I.crt[j]);
+        in.es[j] = gg::kCh;  // chunked component-major
+        in.cs[j] = N * gg::kCh;
     }
     gg::Gadget g{};
     g.layer = layer;
@@ -2138,9 +2075,9 @@ void GpuGarbler::rescale_mrs(uint64_t layer, const RescaleMrsPlan& P, CrtLabels&
         // residue 0's key slot is the sign label of the ReLU that follows (relu_mult)
         I.sig.alloc(I.device, static_cast<size_t>(N) * gg::kW * sizeof(int16_t));
         I.sig_N = N;
-        HIPCHECK(hipMemcpy2DAsync(I.sig.p, gg::kW * sizeof(int16_t), g.S + static_cast<int64_t>(a.key0) * gg::kW,
-                                  static_cast<size_t>(nslots) * gg::kW * sizeof(int16_t), gg::kW * sizeof(int16_t),
-                                  static_cast<size_t>(N), hipMemcpyDeviceToDevice, gg::tl_st));
+        // the mod-2 key slot is a contiguous component-major block [128][N]
+        HIPCHECK(hipMemcpyAsync(I.sig.p, gg::slot_base(g, a.key0), static_cast<size_t>(N) * gg::kW * sizeof(int16_t),
+                                hipMemcpyDeviceToDevice, gg::tl_st));
     }
     HIPCHECK(hipGetLastError());
     gg::end_layer(tmp);
@@ -2170,6 +2107,8 @@ void GpuGarbler::relu_mult(uint64_t layer, CrtLabels& cur, const std::vector<i64
     for (int j = 0; j < k; ++j) {
         in.p[j] = I.cur[j].as<int16_t>();
         in.n[j] = nr_comps(I.crt[j]);
+        in.es[j] = gg::kCh;  // chunked component-major
+        in.cs[j] = N * gg::kCh;
     }
     gg::Gadget g{};
     g.layer = layer;
@@ -2178,9 +2117,8 @@ void GpuGarbler::relu_mult(uint64_t layer, CrtLabels& cur, const std::vector<i64
     g.S = I.scratch(static_cast<size_t>(N) * nslots * gg::kW * sizeof(int16_t));
     g.N = N;
     g.nslots = nslots;
-    HIPCHECK(hipMemcpy2DAsync(g.S + static_cast<int64_t>(sig_slot) * gg::kW, static_cast<size_t>(nslots) * gg::kW *
-                              sizeof(int16_t), I.sig.p, gg::kW * sizeof(int16_t), gg::kW * sizeof(int16_t),
-                              static_cast<size_t>(N), hipMemcpyDeviceToDevice, gg::tl_st));
+    HIPCHECK(hipMemcpyAsync(gg::slot_base(g, sig_slot), I.sig.p, static_cast<size_t>(N) * gg::kW * sizeof(int16_t),
+                            hipMemcpyDeviceToDevice, gg::tl_st));
     std::vector<DevBlock> out = relu_mult_gates(I, g, in, tb, sig_slot, sk0, *prefix);
     HIPCHECK(hipGetLastError());
     std::vector<void*> tmp;

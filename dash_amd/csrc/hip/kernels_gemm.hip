@@ -12,7 +12,11 @@
 //     with the zero-count and bias-label adds. n runs over (GC, component,
 //     output position) of one residue, so every residue is one large GEMM.
 #include <cstdlib>
+#include <map>
+#include <mutex>
+#include <vector>
 
+#include "host_util.h"
 #include "launch.h"
 
 namespace dash {
@@ -641,45 +645,139 @@ __global__ __launch_bounds__(256) void k_conv_img2(ConvArgs a, Act x, Act y, int
 }
 
 // ---------------------------------------------------------------------------
+// Dense on MFMA: per residue j one GEMM Y[col][o] = W[o][:] . X[col][:] with
+// columns col = (gc, component) of the input labels (each column is K
+// contiguous bytes, component-major activations), both operands centered
+// int8 (products mod p unchanged), int32 accumulation, then the mod-p
+// epilogue with the (#zero weights) * Z_p term and the bias label.
+// Block 256 = 4 waves; tile 64 outputs x 64 columns; wave w owns outputs
+// [16w, 16w + 16) and 4 column tiles of 16. Operands come straight from
+// global memory (16 B per lane per k-step: W rows stay L2-resident, X columns
+// are read once), no LDS. Grid (col tiles, O tiles, residues).
+__device__ __forceinline__ uint32_t center4p(uint32_t w, int p) {
+    // each byte v in [0, p): v > p/2 -> v - p (two's complement byte)
+    const int half = p / 2;
+    uint32_t r = 0;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        int v = static_cast<int>((w >> (8 * u)) & 0xffu);
+        v = v > half ? v - p : v;
+        r |= (static_cast<uint32_t>(v) & 0xffu) << (8 * u);
+    }
+    return r;
+}
+
+__global__ __launch_bounds__(256) void k_dense_mfma(DenseArgs a, Act x, Act y, int B) {
+    const int j = blockIdx.z;
+    const int p = a.crt.p[j], n = a.crt.n[j];
+    const int64_t ncols = static_cast<int64_t>(B) * n;
+    const int64_t col0 = static_cast<int64_t>(blockIdx.x) * 64;
+    if (col0 >= ncols) return;  // block-uniform: this residue has fewer columns than the grid
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const int o0 = blockIdx.y * 64 + wave * 16;
+    const int K = static_cast<int>(a.K), O = static_cast<int>(a.O);
+    const int8_t* W8 = a.w8[j];
+    const act_t* X = x.p[j];
+    const int kq = (lane >> 4) * 16;  // this lane's 16-byte k slice of each 64-wide step
+    const int orow = min(o0 + (lane & 15), O - 1);  // rows past O read a valid row; their results are dropped
+    int64_t cols[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) cols[t] = min(col0 + t * 16 + (lane & 15), ncols - 1);
+    v4i acc[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) acc[t] = v4i{0, 0, 0, 0};
+    typedef uint32_t u32x4d __attribute__((ext_vector_type(4)));
+    for (int k0 = 0; k0 < a.Kpad; k0 += 64) {
+        const v2l av = *reinterpret_cast<const v2l*>(W8 + static_cast<int64_t>(orow) * a.Kpad + k0 + kq);
+        const int kk = k0 + kq;
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            // 16 consecutive k of column cols[t]; bytes at k >= K meet zero weights (the activation buffers have
+            // 64 B of slack past the last column, so the over-read stays in bounds)
+            const u32x4d raw = *reinterpret_cast<const u32x4d*>(X + cols[t] * K + kk);
+            u32x4d c;
+#pragma unroll
+            for (int u = 0; u < 4; ++u) c[u] = center4p(raw[u], p);
+            v2l bv;
+            __builtin_memcpy(&bv, &c, 16);
+            acc[t] = __builtin_amdgcn_mfma_i32_16x16x64_i8(av, bv, acc[t], 0, 0, 0);
+        }
+    }
+    // epilogue: C/D map col = lane & 15, row = (lane >> 4) * 4 + r
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+        const int64_t col = col0 + t * 16 + (lane & 15);
+        if (col >= ncols) continue;
+        const int b = static_cast<int>(col / n), c = static_cast<int>(col - static_cast<int64_t>(b) * n);
+        const int32_t zv = a.zero[static_cast<int64_t>(b) * a.lab_stride + a.lab_off[j] + c];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int o = o0 + (lane >> 4) * 4 + r;
+            if (o >= O) continue;
+            const int32_t bv = a.bias[j][(static_cast<int64_t>(b) * O + o) * n + c];
+            y.p[j][col * O + o] = static_cast<act_t>(mod_p(acc[t][r] % p + a.zc[j][o] * zv + bv, p));
+        }
+    }
+}
+
 namespace {
 struct ZTab {
     int* dj = nullptr;
     int* dc = nullptr;
     int sumn = 0;
-    CrtInfo key{};
 };
-ZTab& ztab_for(const CrtInfo& crt, hipStream_t st) {
-    static thread_local ZTab t;
-    bool same = t.dj && t.key.k == crt.k;
-    for (int j = 0; same && j < crt.k; ++j) same = t.key.n[j] == crt.n[j];
-    if (!same) {
-        if (t.dj) {
-            (void)hipFree(t.dj);
-            (void)hipFree(t.dc);
+// process-wide, keyed by the label widths; built by prepare_zmap at evaluator construction (never inside a
+// hipGraph capture: allocation and synchronous copies are not capturable)
+std::mutex& ztab_mutex() {
+    static std::mutex m;
+    return m;
+}
+std::map<std::vector<int>, ZTab>& ztabs() {
+    static auto* t = new std::map<std::vector<int>, ZTab>();  // leaked: device tables live as long as the process
+    return *t;
+}
+std::vector<int> ztab_key(const CrtInfo& crt) { return std::vector<int>(crt.n, crt.n + crt.k); }
+}  // namespace
+
+void prepare_zmap(const CrtInfo& crt) {
+    std::lock_guard<std::mutex> g(ztab_mutex());
+    auto key = ztab_key(crt);
+    if (ztabs().count(key)) return;
+    ZTab t;
+    for (int j = 0; j < crt.k; ++j) t.sumn += crt.n[j];
+    std::vector<int> hj(t.sumn), hc(t.sumn);
+    int q = 0;
+    for (int j = 0; j < crt.k; ++j)
+        for (int c = 0; c < crt.n[j]; ++c, ++q) {
+            hj[q] = j;
+            hc[q] = c;
         }
-        int sumn = 0;
-        for (int j = 0; j < crt.k; ++j) sumn += crt.n[j];
-        std::vector<int> hj(sumn), hc(sumn);
-        int q = 0;
-        for (int j = 0; j < crt.k; ++j)
-            for (int c = 0; c < crt.n[j]; ++c, ++q) {
-                hj[q] = j;
-                hc[q] = c;
-            }
-        (void)hipMalloc(&t.dj, sumn * sizeof(int));
-        (void)hipMalloc(&t.dc, sumn * sizeof(int));
-        (void)hipMemcpy(t.dj, hj.data(), sumn * sizeof(int), hipMemcpyHostToDevice);
-        (void)hipMemcpy(t.dc, hc.data(), sumn * sizeof(int), hipMemcpyHostToDevice);
-        t.sumn = sumn;
-        t.key = crt;
-    }
-    (void)st;
-    return t;
+    HIPCHECK(hipMalloc(&t.dj, t.sumn * sizeof(int)));
+    HIPCHECK(hipMalloc(&t.dc, t.sumn * sizeof(int)));
+    HIPCHECK(hipMemcpy(t.dj, hj.data(), t.sumn * sizeof(int), hipMemcpyHostToDevice));
+    HIPCHECK(hipMemcpy(t.dc, hc.data(), t.sumn * sizeof(int), hipMemcpyHostToDevice));
+    ztabs().emplace(std::move(key), t);
+}
+
+namespace {
+const ZTab& ztab_for(const CrtInfo& crt) {
+    std::lock_guard<std::mutex> g(ztab_mutex());
+    auto it = ztabs().find(ztab_key(crt));
+    DASH_CHECK(it != ztabs().end(), "prepare_zmap was not called for this CRT base");
+    return it->second;
 }
 }  // namespace
 
 void launch_dense(const DenseArgs& a, const Act& x, const Act& y, int B, hipStream_t st) {
-    ZTab& z = ztab_for(a.crt, st);
+    if (a.w8[0]) {
+        int maxn = 0;
+        for (int j = 0; j < a.crt.k; ++j) maxn = max(maxn, a.crt.n[j]);
+        dim3 g(static_cast<unsigned>((static_cast<int64_t>(B) * maxn + 63) / 64), static_cast<unsigned>((a.O + 63) / 64),
+               static_cast<unsigned>(a.crt.k));
+        hipLaunchKernelGGL(k_dense_mfma, g, dim3(256), 0, st, a, x, y, B);
+        return;
+    }
+    const ZTab& z = ztab_for(a.crt);
     dim3 g(static_cast<unsigned>((a.O + 255) / 256), 1, static_cast<unsigned>(B * z.sumn));
     hipLaunchKernelGGL(k_dense, g, dim3(256), 0, st, a, x, y, z.dj, z.dc, z.sumn);
 }
@@ -724,7 +822,7 @@ void launch_conv(const ConvArgs& a, const Act& x, const Act& y, int B, hipStream
         for (int j = 0; j < a.crt.k; ++j) rest |= (a.w8[j] == nullptr);
         if (!rest) return;
     }
-    ZTab& z = ztab_for(a.crt, st);
+    const ZTab& z = ztab_for(a.crt);
     dim3 g(static_cast<unsigned>((a.OH * a.OW + 255) / 256), static_cast<unsigned>(a.F), static_cast<unsigned>(B * z.sumn));
     hipLaunchKernelGGL(k_conv_valu, g, dim3(256), 0, st, a, x, y, z.dj, z.dc, z.sumn);
 }

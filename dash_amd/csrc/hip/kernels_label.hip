@@ -188,6 +188,32 @@ __global__ __launch_bounds__(256) void k_transpose_res(TrRes a) {
         if (r < rows && c < cols) out[c * rows + r] = static_cast<Tout>(t[tx][y]);
     }
 }
+// grid (blocks, residue): out[j][x] = in[j][x], x < rows[j] * cols[j]; 4 components per lane-iteration
+template <class Tin, class Tout>
+__global__ __launch_bounds__(256) void k_cast_res(TrRes a) {
+    const int j = blockIdx.y;
+    const int64_t n = a.rows[j] * a.cols[j];
+    const Tin* __restrict__ in = static_cast<const Tin*>(a.in[j]);
+    Tout* __restrict__ out = static_cast<Tout*>(a.out[j]);
+    for (int64_t x = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; x < n;
+         x += static_cast<int64_t>(gridDim.x) * blockDim.x)
+        out[x] = static_cast<Tout>(in[x]);
+}
+// grid (blocks, residue) over the component-major index x = q * N + e
+template <bool TO_ACT>
+__global__ __launch_bounds__(256) void k_chunk_res(TrRes a) {
+    const int j = blockIdx.y;
+    const int64_t N = a.cols[j], n = a.rows[j] * N;
+    for (int64_t x = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; x < n;
+         x += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+        const int64_t q = x / N, e = x - q * N;
+        const int64_t cx = ((q >> 3) * N + e) * 8 + (q & 7);
+        if (TO_ACT)
+            static_cast<act_t*>(a.out[j])[x] = static_cast<act_t>(static_cast<const int16_t*>(a.in[j])[cx]);
+        else
+            static_cast<int16_t*>(a.out[j])[cx] = static_cast<int16_t>(static_cast<const act_t*>(a.in[j])[x]);
+    }
+}
 __global__ __launch_bounds__(256) void k_narrow(const int16_t* __restrict__ in, act_t* __restrict__ out, int64_t n) {
     for (int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < n;
          i += static_cast<int64_t>(gridDim.x) * blockDim.x)
@@ -224,6 +250,25 @@ void launch_transpose_to_act_res(const TrRes& a, hipStream_t st) {
 }
 void launch_transpose_from_act_res(const TrRes& a, hipStream_t st) {
     hipLaunchKernelGGL((k_transpose_res<act_t, int16_t>), grid_tr_res(a), dim3(256), 0, st, a);
+}
+
+static inline dim3 grid_cast_res(const TrRes& a) {
+    int64_t mx = 1;
+    for (int j = 0; j < a.k; ++j) mx = std::max(mx, a.rows[j] * a.cols[j]);
+    return dim3(static_cast<unsigned>(std::min<int64_t>((mx + 255) / 256, 4096)), static_cast<unsigned>(a.k));
+}
+void launch_cast_to_act_res(const TrRes& a, hipStream_t st) {
+    hipLaunchKernelGGL((k_cast_res<int16_t, act_t>), grid_cast_res(a), dim3(256), 0, st, a);
+}
+void launch_cast_from_act_res(const TrRes& a, hipStream_t st) {
+    hipLaunchKernelGGL((k_cast_res<act_t, int16_t>), grid_cast_res(a), dim3(256), 0, st, a);
+}
+
+void launch_unchunk_to_act_res(const TrRes& a, hipStream_t st) {
+    hipLaunchKernelGGL(k_chunk_res<true>, grid_cast_res(a), dim3(256), 0, st, a);
+}
+void launch_chunk_from_act_res(const TrRes& a, hipStream_t st) {
+    hipLaunchKernelGGL(k_chunk_res<false>, grid_cast_res(a), dim3(256), 0, st, a);
 }
 
 void launch_aes_test(const u128* in, u128* out, int64_t n, const AesGlobals& g, hipStream_t st) {

@@ -70,8 +70,15 @@ struct DenseArgs {
     int lab_stride;
     int lab_off[kMaxRes];
     const int32_t* src;            // [K] input remap (channel_tf) or null
+    // MFMA path (all p <= 255): centered int8 weights [O][Kpad] with the channel_tf remap folded into the
+    // column order (w8[o][src(i)] = w[o][i]), zero-padded to Kpad = 64 * ceil(K / 64); null: VALU kernel
+    const int8_t* w8[kMaxRes];
+    int Kpad;
 };
 void launch_dense(const DenseArgs& a, const Act& x, const Act& y, int B, hipStream_t st);
+// builds the process-wide (residue, component) lookup the VALU dense / conv kernels index blocks with, outside
+// any stream capture (HipEvaluator construction calls it)
+void prepare_zmap(const CrtInfo& crt);
 
 struct ConvArgs {
     CrtInfo crt;
@@ -259,6 +266,13 @@ struct TrRes {
 };
 void launch_transpose_to_act_res(const TrRes& a, hipStream_t st);    // int16 -> bytes
 void launch_transpose_from_act_res(const TrRes& a, hipStream_t st);  // bytes -> int16
+// elementwise casts of rows[j] * cols[j] contiguous components per residue (layouts already match)
+void launch_cast_to_act_res(const TrRes& a, hipStream_t st);    // int16 -> bytes
+void launch_cast_from_act_res(const TrRes& a, hipStream_t st);  // bytes -> int16
+// the GPU garbler's chunked labels (component q of element e at ((q / 8) * N + e) * 8 + q % 8; rows[j] = n_j,
+// cols[j] = N) <-> component-major bytes [n][N]
+void launch_unchunk_to_act_res(const TrRes& a, hipStream_t st);
+void launch_chunk_from_act_res(const TrRes& a, hipStream_t st);
 
 }  // namespace dev
 }  // namespace dash

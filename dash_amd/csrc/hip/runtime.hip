@@ -455,6 +455,7 @@ void HipEvaluator::build() {
         lab_stride_ += nr_comps(crt_[j]);
     }
     d_lab_off_ = upload(lab_off_, k_);
+    prepare_zmap(crt_info(crt_));  // VALU dense / conv block lookup, built here (not under a graph capture)
     zero_rows_ = upload_const_rows([&](int j) { return "Z." + std::to_string(crt_[j]); });
     // compressed zero labels + colors for every modulus (carry init)
     zstride_ = maxmod + 1;
@@ -530,7 +531,8 @@ void HipEvaluator::build() {
     for (int bi = 0; bi < 4; ++bi) {
         bufs_[bi].N = 0;
         for (int j = 0; j < k_; ++j) {
-            const size_t count = static_cast<size_t>(B_) * widest[j] * cap;
+            // + 64 B: the MFMA dense kernel reads whole 16-byte k slices past the last column's end
+            const size_t count = static_cast<size_t>(B_) * widest[j] * cap + 64;
             bufs_[bi].p[j] = dalloc<act_t>(count);
             // defined contents before any input is staged (serving primes the hipGraph with an unencoded run)
             HIPCHECK(hipMemset(bufs_[bi].p[j], 0, count * sizeof(act_t)));
@@ -626,6 +628,23 @@ void HipEvaluator::build() {
                     a.w[j] = upload(wt.data(), wt.size());
                     a.zc[j] = upload(zc.data(), zc.size());
                     a.bias[j] = upload_i16_rows(li, arr_name("bias.", j, ""));
+                }
+                // MFMA path: centered int8 weights [O][Kpad], channel_tf folded into the column order
+                a.Kpad = static_cast<int>((a.K + 63) / 64 * 64);
+                bool mfma_ok = mfma_ && a.K < (1 << 17);  // 127 * 127 * K fits the int32 accumulator
+                for (int j = 0; j < k_; ++j) mfma_ok = mfma_ok && crt_[j] <= 255;
+                for (int j = 0; j < k_; ++j) {
+                    a.w8[j] = nullptr;
+                    if (!mfma_ok) continue;
+                    const int p = crt_[j];
+                    std::vector<int8_t> w8(static_cast<size_t>(a.O) * a.Kpad, 0);
+                    for (i64 o = 0; o < a.O; ++o)
+                        for (i64 i = 0; i < a.K; ++i) {
+                            const int v = static_cast<int>(w.ptr<i64>()[o * a.K + i] % p);
+                            const i64 s = ch > 0 ? dense_src(i, a.K, ch) : i;
+                            w8[static_cast<size_t>(o) * a.Kpad + s] = static_cast<int8_t>(v > p / 2 ? v - p : v);
+                        }
+                    a.w8[j] = upload(w8.data(), w8.size());
                 }
                 a.zero = zero_rows_;
                 a.lab_stride = lab_stride_;
