@@ -63,6 +63,8 @@ struct Proj {
     int64_t off;                 // entry offset inside the element's table row
     int64_t first;               // first global entry index of this projection
     int pay1;                    // 1 + payload bank row of f-index 0 (F_SIGN, F_DIV, F_DIVMOD); 0: computed inline
+    int pad_;
+    int64_t first_out;           // first global output (entry x target) index (k_emit; set by gg::project)
 };
 
 // A projection whose function takes few distinct values (sign: 2, carry: k+1)
@@ -156,6 +158,9 @@ struct Gadget {
     const int16_t* flut;  // F_FAN: payload values [a0 + i * stride + target] (reduced mod the target modulus)
     const int* fan;       // F_FAN: target moduli [a1 + target]
     const int* fbank;     // F_FAN: [a1 + target] 1 + payload bank row of value 0 (k_payloads), 0: computed inline
+    int64_t outputs;      // per element: table entries written (sum over projections of entries x targets)
+    u128* HC;             // [entries][N] key hashes (k_hash -> k_emit)
+    uint8_t* CC;          // [entries][N] key colors
 };
 
 // slot s as a chunked label set, and element e's view of it
@@ -273,6 +278,8 @@ __device__ __forceinline__ void slot_sum(const Gadget& g, int64_t e, int dst, in
     }
 }
 
+// grid (elements, t): y = q is one digit sum (the fused sums read the previous carry, which the carry
+// projections of k_project produce later, so every q is independent here)
 __global__ __launch_bounds__(256) void k_sign_derive(Ctx c, Gadget g, SignSlots s) {
     const int64_t e = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
     if (e >= g.N) return;
@@ -281,7 +288,8 @@ __global__ __launch_bounds__(256) void k_sign_derive(Ctx c, Gadget g, SignSlots 
     if (s.fused) {
         // digit q (d = t-1-q): sum_j approx[j][d] (+ carry of the previous digit, none for q = 0);
         // MSD: sum_j approx[j][0] + last carry (none when t = 1)
-        for (int q = 0; q <= t - 1; ++q) {
+        {
+            const int q = blockIdx.y;
             const int d = t - 1 - q;
             const ModC Mo = c.mc[s.dmod[d]];
             const int dst = d == 0 ? s.sum_slot : s.sum2_slot0 + q;
@@ -289,10 +297,12 @@ __global__ __launch_bounds__(256) void k_sign_derive(Ctx c, Gadget g, SignSlots 
         }
         return;
     }
-    for (int q = 0; q + 1 < t; ++q) {
+    const int q = blockIdx.y;
+    if (q + 1 < t) {
         const int d = t - 1 - q;
         const ModC Mo = c.mc[(k + 1) * s.mrs[d]];
         slot_sum(g, e, s.sum2_slot0 + q, s.bases_slot0 + q * s.stride_q, 1, k + 1, none, false, Mo);
+        return;
     }
     const int m0 = s.mrs[0];
     const ModC M0 = c.mc[m0];
@@ -301,27 +311,32 @@ __global__ __launch_bounds__(256) void k_sign_derive(Ctx c, Gadget g, SignSlots 
     slot_sum(g, e, s.sum_slot, s.mrs_slot0, t, k, carry, true, M0);
 }
 
-// digits (a_q + f * b_q) mod m of two labels (components in [0, m)) pushed into cf, 8 per chunk load;
-// two chunks in flight per step
-__device__ __forceinline__ void push_row(CompressFwd& cf, LRef a, LRef b, uint32_t f, const ModC& m) {
+// digits (a_q + f * b_q) mod m of a per-lane label a and a wave-uniform row b (R_q: components in [0, m)),
+// pushed into cf, 8 per chunk load. The row's chunk is moved to SGPRs (readfirstlane of a uniform load), so it
+// costs no vector registers and its unpacking is scalar work.
+__device__ __forceinline__ void push_row(CompressFwd& cf, LRef a, const int16_t* b, uint32_t f, const ModC& m) {
     const int n = static_cast<int>(m.n);
     const int nc = static_cast<int>(chunks_of(n));
-    int c8 = 0;
-    for (; c8 + 2 <= nc; c8 += 2) {
-        uint32_t a0[8], a1[8], b0[8], b1[8];
-        unpack8(ld_chunk(a, c8), a0);
-        unpack8(ld_chunk(a, c8 + 1), a1);
-        unpack8(ld_chunk(b, c8), b0);
-        unpack8(ld_chunk(b, c8 + 1), b1);
+    for (int c8 = 0; c8 < nc; ++c8) {
+        const u32x4a av = ld_chunk(a, c8);
+        const u32x4a bv = *reinterpret_cast<const u32x4a*>(b + c8 * kCh);
+        uint32_t bs[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) bs[u] = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(bv[u])));
         const int q0 = c8 * 8;
 #pragma unroll
-        for (int u = 0; u < 8; ++u)
-            if (q0 + u < n) cf.push(modq(a0[u] + f * b0[u], m), m);
-#pragma unroll
-        for (int u = 0; u < 8; ++u)
-            if (q0 + 8 + u < n) cf.push(modq(a1[u] + f * b1[u], m), m);
+        for (int u = 0; u < 8; ++u) {
+            const uint32_t x = (u & 1) ? (av[u >> 1] >> 16) : (av[u >> 1] & 0xffffu);
+            const uint32_t y = (u & 1) ? (bs[u >> 1] >> 16) : (bs[u >> 1] & 0xffffu);
+            if (q0 + u < n) cf.push(modq(x + f * y, m), m);
+        }
     }
-    if (c8 < nc) {
+}
+// the same with a per-lane offset label b (the evaluator half gate's offset is the input label x0)
+__device__ __forceinline__ void push_row2(CompressFwd& cf, LRef a, LRef b, uint32_t f, const ModC& m) {
+    const int n = static_cast<int>(m.n);
+    const int nc = static_cast<int>(chunks_of(n));
+    for (int c8 = 0; c8 < nc; ++c8) {
         uint32_t a0[8], b0[8];
         unpack8(ld_chunk(a, c8), a0);
         unpack8(ld_chunk(b, c8), b0);
@@ -332,17 +347,17 @@ __device__ __forceinline__ void push_row(CompressFwd& cf, LRef a, LRef b, uint32
     }
 }
 
-// key = x + i*R (mod m), compressed from the least significant digit
-__device__ __forceinline__ u128 proj_key(LRef x, LRef R, int i, const ModC& m, uint32_t& color) {
+// key = x + i*R (mod m), compressed from the least significant digit (R: uniform row)
+__device__ __forceinline__ u128 proj_key(LRef x, const int16_t* R, int i, const ModC& m, uint32_t& color) {
     CompressFwd kc;
     kc.init();
     push_row(kc, x, R, static_cast<uint32_t>(i), m);
-    color = modq(static_cast<uint32_t>(static_cast<uint16_t>(x.p[0]) + i * static_cast<uint16_t>(R.p[0])), m);
+    color = modq(static_cast<uint32_t>(static_cast<uint16_t>(x.p[0]) + i * static_cast<uint16_t>(R[0])), m);
     return kc.finish();
 }
 
-// payload = o + f*R (mod m), o, f, R in [0, m)
-__device__ __forceinline__ u128 proj_payload(LRef o, LRef R, uint32_t f, const ModC& m) {
+// payload = o + f*R (mod m), o, f, R in [0, m) (R: uniform row)
+__device__ __forceinline__ u128 proj_payload(LRef o, const int16_t* R, uint32_t f, const ModC& m) {
     CompressFwd pc;
     pc.init();
     push_row(pc, o, R, f, m);
@@ -405,10 +420,32 @@ __device__ __forceinline__ Proj rfl_proj(const Proj& p) {
     r.off = rfl64(p.off);
     r.first = rfl64(p.first);
     r.pay1 = rfl(p.pay1);
+    r.first_out = rfl64(p.first_out);
     return r;
 }
 
-__global__ __launch_bounds__(kPB) void k_project(Ctx c, Gadget g, In in, Tables tb) {
+// Projections in two passes, so no lane carries a long dependent chain (key
+// loads -> compress -> AES -> payload loads -> compress -> store):
+//   k_hash  one lane per (element, table entry): key = x + i*R, H(compress(key)),
+//           color -> HC / CC [entry][N];
+//   k_emit  one lane per (element, entry, target): payload (inline, or from the
+//           payload bank) + H -> the entry's table slot.
+// Element-tiled order: the 64 lanes of a wavefront are 64 consecutive elements
+// of one tile, all on the SAME work item, so the projection descriptor, i, the
+// label widths (loop trip counts), the moduli and the function are
+// wave-uniform and moved to SGPRs (readfirstlane); labels are chunked
+// component-major, so one coalesced 16-byte load per lane covers 8 components.
+__device__ __forceinline__ int find_proj(const Proj* sp, int n, int64_t r, bool by_out) {
+    int lo = 0, hi = n - 1;
+    while (lo < hi) {  // last projection with first (first_out) <= r (uniform search)
+        const int mid = (lo + hi + 1) >> 1;
+        if (rfl64(by_out ? sp[mid].first_out : sp[mid].first) <= r) lo = mid;
+        else hi = mid - 1;
+    }
+    return lo;
+}
+
+__global__ __launch_bounds__(kPB) void k_hash(Ctx c, Gadget g, In in) {
     __shared__ __attribute__((aligned(16))) uint32_t lds_aes[DASH_AES_LDS_WORDS];
     __shared__ Proj sp[kMaxDesc];
     lds_stage(sp, g.projs, g.nprojs);
@@ -424,81 +461,98 @@ __global__ __launch_bounds__(kPB) void k_project(Ctx c, Gadget g, In in, Tables 
     for (int64_t w = w0; w < nw; w += wstep) {
         const int64_t tile = w / g.entries;
         const int64_t r = w - tile * g.entries;
-        int lo = 0, hi = g.nprojs - 1;
-        while (lo < hi) {  // last projection with first <= r (uniform search)
-            const int mid = (lo + hi + 1) >> 1;
-            if (rfl64(sp[mid].first) <= r) lo = mid;
-            else hi = mid - 1;
-        }
-        const Proj P = rfl_proj(sp[lo]);
+        const Proj P = rfl_proj(sp[find_proj(sp, g.nprojs, r, false)]);
         const int i = static_cast<int>(r - P.first);
-        const ModC mi = rfl_modc(c.mc[P.pin]), mo = rfl_modc(c.mc[P.pout]);
+        const ModC mi = rfl_modc(c.mc[P.pin]);
         // the last tile's spare lanes recompute element N-1 (uniform control flow) and skip the store
         const int64_t e_raw = tile * kTile + lane;
         const int64_t e = e_raw < N ? e_raw : N - 1;
-        const LRef inl = label_ref(c, g, in, e, P.in_kind, P.in_idx, P.pin);
         uint32_t color;
-        const u128 H = aes_encrypt(aes, proj_key(inl, row_ref(c.R + static_cast<int64_t>(P.pin) * kW), i, mi, color));
+        const u128 H = aes_encrypt(aes, proj_key(label_ref(c, g, in, e, P.in_kind, P.in_idx, P.pin),
+                                                 c.R + static_cast<int64_t>(P.pin) * kW, i, mi, color));
+        if (e_raw < N) {
+            g.HC[r * N + e] = H;
+            g.CC[r * N + e] = static_cast<uint8_t>(color);
+        }
+    }
+}
+
+__global__ __launch_bounds__(256) void k_emit(Ctx c, Gadget g, In in, Tables tb) {
+    __shared__ Proj sp[kMaxDesc];
+    lds_stage(sp, g.projs, g.nprojs);
+    __syncthreads();
+    const int64_t N = g.N;
+    const int64_t tiles = (N + kTile - 1) / kTile;
+    const int64_t nw = tiles * g.outputs;  // wave work items (tile, output)
+    const int lane = static_cast<int>(threadIdx.x) & (kTile - 1);
+    const int64_t wpb = blockDim.x / kTile;
+    const int64_t w0 = static_cast<int64_t>(blockIdx.x) * wpb + rfl(static_cast<int>(threadIdx.x) / kTile);
+    const int64_t wstep = static_cast<int64_t>(gridDim.x) * wpb;
+    for (int64_t w = w0; w < nw; w += wstep) {
+        const int64_t tile = w / g.outputs;
+        const int64_t o = w - tile * g.outputs;
+        const Proj P = rfl_proj(sp[find_proj(sp, g.nprojs, o, true)]);
+        const bool fan = P.fn == F_LUT || P.fn == F_FAN;
+        const int t = fan ? P.stride : 1;
+        const int local = static_cast<int>(o - P.first_out);
+        const int i = local / t, d = local - i * t;
+        const int64_t r = P.first + i;
+        const int64_t e_raw = tile * kTile + lane;
+        const int64_t e = e_raw < N ? e_raw : N - 1;
+        const u128 H = g.HC[r * N + e];
+        const uint32_t color = g.CC[r * N + e];
+        u128 pay;
         if (P.fn == F_LUT) {
-            // approx fan-out: digit d's entry at off + color*t + d, payload mrs0_slot + d + lut[j][i][d] * R_{m_d}
-            const int t = P.stride;
-            u128* row = tb.t[P.table] + e * tb.row[P.table] + P.off + static_cast<int64_t>(color) * t;
-            for (int d = 0; d < t; ++d) {
-                const int pout = rfl(g.mrs[d]);
-                const ModC md = rfl_modc(c.mc[pout]);
-                int64_t f = c.lut[c.lut_off[P.a0] + i * t + d];
-                int64_t cm = f % pout;
-                if (cm < 0) cm += pout;
-                const u128 pay = proj_payload(slot_ref(g, P.out_slot + d, e), row_ref(c.R + static_cast<int64_t>(pout) * kW),
-                                              static_cast<uint32_t>(cm), md);
-                if (e_raw < N) row[d] = pay + H;
-            }
-            continue;
-        }
-        if (P.fn == F_FAN) {
+            // approx fan-out: digit d's payload mrs0_slot + d + lut[j][i][d] * R_{m_d}
+            const int pout = rfl(g.mrs[d]);
+            int64_t cm = c.lut[c.lut_off[P.a0] + i * t + d] % pout;
+            if (cm < 0) cm += pout;
+            pay = proj_payload(slot_ref(g, P.out_slot + d, e), c.R + static_cast<int64_t>(pout) * kW,
+                               static_cast<uint32_t>(cm), rfl_modc(c.mc[pout]));
+        } else if (P.fn == F_FAN) {
             // generic fan-out: target d writes slot out_slot + d, modulus fan[a1 + d], value flut[a0 + i * t + d]
-            const int t = P.stride;
-            u128* row = tb.t[P.table] + e * tb.row[P.table] + P.off + static_cast<int64_t>(color) * t;
-            for (int d = 0; d < t; ++d) {
-                const uint32_t cm = static_cast<uint32_t>(rfl(g.flut[P.a0 + i * t + d]));
-                const int bk = g.fbank ? rfl(g.fbank[P.a1 + d]) : 0;
-                u128 pay;
-                if (bk) {
-                    // few distinct values (e.g. the rescale's final projection: T = 2^(l+1) entries, p_j values)
-                    pay = g.PB[static_cast<int64_t>(bk - 1 + static_cast<int>(cm)) * N + e];
-                } else {
-                    const int pout = rfl(g.fan[P.a1 + d]);
-                    const ModC md = rfl_modc(c.mc[pout]);
-                    pay = proj_payload(slot_ref(g, P.out_slot + d, e), row_ref(c.R + static_cast<int64_t>(pout) * kW), cm,
-                                       md);
-                }
-                if (e_raw < N) row[d] = pay + H;
+            const uint32_t cm = static_cast<uint32_t>(rfl(g.flut[P.a0 + i * t + d]));
+            const int bk = g.fbank ? rfl(g.fbank[P.a1 + d]) : 0;
+            if (bk) {
+                // few distinct values (e.g. the rescale's final projection: T = 2^(l+1) entries, p_j values)
+                pay = g.PB[static_cast<int64_t>(bk - 1 + static_cast<int>(cm)) * N + e];
+            } else {
+                const int pout = rfl(g.fan[P.a1 + d]);
+                pay = proj_payload(slot_ref(g, P.out_slot + d, e), c.R + static_cast<int64_t>(pout) * kW, cm,
+                                   rfl_modc(c.mc[pout]));
             }
-            continue;
-        }
-        if (P.pay1 > 0) {
+        } else if (P.pay1 > 0) {
             // few distinct payloads: precomputed per element by k_payloads
             const int idx = P.fn == F_SIGN ? (i < P.a0 ? 1 : 0) : i / P.a0;  // F_SIGN: 0 lower / 1 upper; F_DIV(MOD): i / m
-            const u128 pay = g.PB[static_cast<int64_t>(P.pay1 - 1 + idx) * N + e];
-            if (e_raw < N) tb.t[P.table][e * tb.row[P.table] + P.off + static_cast<int64_t>(color) * P.stride] = pay + H;
-            continue;
+            pay = g.PB[static_cast<int64_t>(P.pay1 - 1 + idx) * N + e];
+        } else {
+            int64_t f;
+            switch (P.fn) {
+                case F_DIV: f = i / P.a0; break;
+                case F_DIVMOD: f = (i / P.a0) % P.a1; break;
+                case F_SIGN: f = i < P.a0 ? P.a2 : P.a1; break;  // a0 = half, a1 = lower, a2 = upper
+                case F_MULR: f = static_cast<int64_t>(i) * in.p[P.a0][e * in.es[P.a0]]; break;
+                case F_NEGR: f = -(static_cast<int64_t>(i) + in.p[P.a0][e * in.es[P.a0]]); break;
+                default: f = i;
+            }
+            int64_t cm = f % P.pout;
+            if (cm < 0) cm += P.pout;
+            const ModC mo = rfl_modc(c.mc[P.pout]);
+            if (P.outr_kind == R_BANK) {
+                pay = proj_payload(slot_ref(g, P.out_slot, e), c.R + static_cast<int64_t>(P.pout) * kW,
+                                   static_cast<uint32_t>(cm), mo);
+            } else {
+                CompressFwd pc;
+                pc.init();
+                push_row2(pc, slot_ref(g, P.out_slot, e), label_ref(c, g, in, e, S_INPUT, P.outr_idx, 0),
+                          static_cast<uint32_t>(cm), mo);
+                pay = pc.finish();
+            }
         }
-        // function value
-        int64_t f;
-        switch (P.fn) {
-            case F_DIV: f = i / P.a0; break;
-            case F_DIVMOD: f = (i / P.a0) % P.a1; break;
-            case F_SIGN: f = i < P.a0 ? P.a2 : P.a1; break;  // a0 = half, a1 = lower, a2 = upper
-            case F_MULR: f = static_cast<int64_t>(i) * in.p[P.a0][e * in.es[P.a0]]; break;
-            case F_NEGR: f = -(static_cast<int64_t>(i) + in.p[P.a0][e * in.es[P.a0]]); break;
-            default: f = i;
+        if (e_raw < N) {
+            const int64_t slot = fan ? static_cast<int64_t>(color) * t + d : static_cast<int64_t>(color) * P.stride;
+            tb.t[P.table][e * tb.row[P.table] + P.off + slot] = pay + H;
         }
-        int64_t cm = f % P.pout;
-        if (cm < 0) cm += P.pout;
-        const LRef oR = P.outr_kind == R_BANK ? row_ref(c.R + static_cast<int64_t>(P.pout) * kW)
-                                              : label_ref(c, g, in, e, S_INPUT, P.outr_idx, 0);
-        const u128 pay = proj_payload(slot_ref(g, P.out_slot, e), oR, static_cast<uint32_t>(cm), mo);
-        if (e_raw < N) tb.t[P.table][e * tb.row[P.table] + P.off + static_cast<int64_t>(color) * P.stride] = pay + H;
     }
 }
 
@@ -516,12 +570,15 @@ struct MrsG {
     int16_t* L[kMaxRes];  // chunked [n_j / 8][N][8], updated in place
 };
 
+// grid (elements, k + 1): y = j < k derives residue j, y = k the accumulator
 __global__ __launch_bounds__(256) void k_mrs_derive(Ctx c, Gadget g, MrsG a) {
     const int64_t e = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
     if (e >= g.N) return;
     const int64_t cs = g.N * kCh;
     const int k = a.k;
-    for (int j = 0; j < k; ++j) {
+    const int y = blockIdx.y;
+    if (y < k) {
+        const int j = y;
         const int p = a.crt[j];
         const ModC m = c.mc[p];
         const int nc = static_cast<int>(chunks_of(static_cast<int>(m.n))), ns = a.nsub[j];
@@ -544,12 +601,13 @@ __global__ __launch_bounds__(256) void k_mrs_derive(Ctx c, Gadget g, MrsG a) {
             for (int u = 0; u < 8; ++u) kv[u] = modq(kv[u], m);
             st_chunk(const_cast<int16_t*>(K.p) + c8 * K.cs, pack8(kv));
             // output base label (in place): Y_0 = F_0, Y_j = S^-1 L_j + F_j (chunk padding stays in the block)
-            uint32_t fv[8], y[8];
+            uint32_t fv[8], yv[8];
             unpack8(ld_chunk(F, c8), fv);
 #pragma unroll
-            for (int u = 0; u < 8; ++u) y[u] = j == 0 ? fv[u] : modq(x[u] * static_cast<uint32_t>(a.sinv[j]) + fv[u], m);
-            st_chunk(Lj + c8 * cs, pack8(y));
+            for (int u = 0; u < 8; ++u) yv[u] = j == 0 ? fv[u] : modq(x[u] * static_cast<uint32_t>(a.sinv[j]) + fv[u], m);
+            st_chunk(Lj + c8 * cs, pack8(yv));
         }
+        return;
     }
     const int ncT = static_cast<int>(chunks_of(static_cast<int>(c.mc[a.T].n)));
     const LRef A = slot_ref(g, a.acc, e);
@@ -571,10 +629,12 @@ struct MrsSG {
     int sub[kMaxRes][kMaxRes];  // slots subtracted from residue r's key
     int key0;                   // key slot of residue r = key0 + r
 };
+// grid (elements, residue r)
 __global__ __launch_bounds__(256) void k_mrs_sign_derive(Ctx c, Gadget g, In in, MrsSG a) {
     const int64_t e = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
     if (e >= g.N) return;
-    for (int r = 0; r < a.k; ++r) {
+    {
+        const int r = blockIdx.y;
         const int p = a.crt[r];
         const ModC m = c.mc[p];
         const int nc = static_cast<int>(chunks_of(in.n[r])), ns = a.nsub[r];
@@ -606,8 +666,12 @@ __global__ __launch_bounds__(256) void k_payloads(Ctx c, Gadget g, const PayDesc
         const int r = static_cast<int>(x / g.N);
         const int64_t e = x - static_cast<int64_t>(r) * g.N;
         const PayDesc d = pd[r];
-        g.PB[x] = proj_payload(slot_ref(g, d.out_slot, e), row_ref(c.R + static_cast<int64_t>(d.pout) * kW),
-                               static_cast<uint32_t>(d.f), c.mc[d.pout]);
+        // a wave may straddle two rows (N is not a multiple of 64): the offset row is per lane here
+        CompressFwd pc;
+        pc.init();
+        push_row2(pc, slot_ref(g, d.out_slot, e), row_ref(c.R + static_cast<int64_t>(d.pout) * kW),
+                  static_cast<uint32_t>(d.f), c.mc[d.pout]);
+        g.PB[x] = pc.finish();
     }
 }
 
@@ -1020,7 +1084,9 @@ struct PhaseTrace {
 namespace {
 struct BlockCache {
     std::mutex m;
-    std::multimap<std::pair<int, size_t>, void*> free;
+    // (device, stream, bytes): a block is reused only on the stream that released it (stream-ordered reuse;
+    // two garbling contexts never hand each other a block their queued kernels may still touch)
+    std::multimap<std::tuple<int, hipStream_t, size_t>, void*> free;
     size_t cached = 0;
     size_t cap = static_cast<size_t>(std::getenv("DASH_GG_CACHE_GB") ? std::atof(std::getenv("DASH_GG_CACHE_GB")) * 1e9
                                                                       : 16e9);
@@ -1030,11 +1096,11 @@ BlockCache& block_cache() {
     return *c;
 }
 
-void* cache_get(int device, size_t bytes) {
+void* cache_get(int device, hipStream_t st, size_t bytes) {
     BlockCache& c = block_cache();
     {
         std::lock_guard<std::mutex> g(c.m);
-        auto it = c.free.find({device, bytes});
+        auto it = c.free.find(std::make_tuple(device, st, bytes));
         if (it != c.free.end()) {
             void* p = it->second;
             c.free.erase(it);
@@ -1047,13 +1113,13 @@ void* cache_get(int device, size_t bytes) {
     return p;
 }
 
-void cache_put(int device, void* p, size_t bytes) {
+void cache_put(int device, hipStream_t st, void* p, size_t bytes) {
     if (!p) return;
     BlockCache& c = block_cache();
     {
         std::lock_guard<std::mutex> g(c.m);
         if (c.cached + bytes <= c.cap) {
-            c.free.emplace(std::make_pair(device, bytes), p);
+            c.free.emplace(std::make_tuple(device, st, bytes), p);
             c.cached += bytes;
             return;
         }
@@ -1087,6 +1153,7 @@ struct DevBlock {
     size_t bytes = 0;
     int device = 0;
     bool borrowed = false;
+    hipStream_t st = nullptr;  // the garbling stream that allocated (and last used) the block
     DevBlock() = default;
     DevBlock(const DevBlock&) = delete;
     DevBlock& operator=(const DevBlock&) = delete;
@@ -1097,6 +1164,7 @@ struct DevBlock {
         bytes = o.bytes;
         device = o.device;
         borrowed = o.borrowed;
+        st = o.st;
         o.p = nullptr;
         return *this;
     }
@@ -1106,7 +1174,8 @@ struct DevBlock {
         device = dev;
         bytes = std::max<size_t>(16, b);
         borrowed = false;
-        p = cache_get(dev, bytes);
+        st = gg::tl_st;
+        p = cache_get(dev, st, bytes);
     }
     void borrow(int dev, void* q, size_t b) {
         release();
@@ -1116,7 +1185,7 @@ struct DevBlock {
         p = q;
     }
     void release() {
-        if (p && !borrowed) cache_put(device, p, bytes);
+        if (p && !borrowed) cache_put(device, st, p, bytes);
         p = nullptr;
     }
     template <class T>
@@ -1158,7 +1227,8 @@ struct DevTable {
                    "gpu garbler: table size mismatch");
         auto d = std::make_shared<Array::Device>();
         const size_t bytes = b.bytes;
-        d->p = std::shared_ptr<void>(b.p, [device, bytes](void* x) { cache_put(device, x, bytes); });
+        const hipStream_t st = b.st;
+        d->p = std::shared_ptr<void>(b.p, [device, st, bytes](void* x) { cache_put(device, st, x, bytes); });
         b.p = nullptr;
         d->device = device;
         d->fetch = [device](void* h, const void* dv, size_t n) {
@@ -1181,6 +1251,31 @@ void check_desc(const gg::Gadget& g) {
 }
 
 // run the three sign-gadget passes for N elements with input labels `in`
+// key-hash scratch of the calling thread's garbling context (DevCtx, grow-only): [entries][N] hashes + colors
+std::pair<u128*, uint8_t*> hc_scratch(size_t entries, int64_t N);
+
+// The projections of a gadget: output indices (entry x target) assigned, descriptors staged, then k_hash and
+// k_emit on the garbling stream. g.draws / labels / payload bank must be ready (same stream).
+void project(const gg::Ctx& c, gg::Gadget& g, const gg::In& in, const gg::Tables& tb, std::vector<gg::Proj> pr) {
+    int64_t outs = 0;
+    for (auto& p : pr) {
+        p.first_out = outs;
+        const bool fan = p.fn == gg::F_LUT || p.fn == gg::F_FAN;
+        outs += static_cast<int64_t>(p.pin) * (fan ? p.stride : 1);
+    }
+    g.projs = gg::dconst(pr.data(), pr.size());
+    g.nprojs = static_cast<int>(pr.size());
+    g.outputs = outs;
+    auto hc = hc_scratch(static_cast<size_t>(g.entries), g.N);
+    g.HC = hc.first;
+    g.CC = hc.second;
+    check_desc(g);
+    const int64_t lanes = (g.N + gg::kTile - 1) / gg::kTile * gg::kTile;
+    hipLaunchKernelGGL(gg::k_hash, dim3(blocks_for(lanes * g.entries, gg::kPB, 16384)), dim3(gg::kPB), 0, gg::tl_st, c, g,
+                       in);
+    hipLaunchKernelGGL(gg::k_emit, dim3(blocks_for(lanes * g.outputs, 256, 16384)), dim3(256), 0, gg::tl_st, c, g, in, tb);
+}
+
 void run_sign(const gg::Ctx& c, const gg::SignLayout& L, gg::Gadget& g, const gg::In& in, const gg::Tables& tb,
               std::vector<void*>& tmp) {
     g.draws = gg::dconst(L.draws.data(), L.draws.size());
@@ -1192,15 +1287,14 @@ void run_sign(const gg::Ctx& c, const gg::SignLayout& L, gg::Gadget& g, const gg
     for (int d = 0; d < L.ss.t; ++d) g.mrs[d] = L.fan[d];
     check_desc(g);
     hipLaunchKernelGGL(gg::k_draw, dim3(blocks_for(g.N * g.nblk, gg::kGB, 8192)), dim3(gg::kGB), 0, gg::tl_st, c, g);
-    hipLaunchKernelGGL(gg::k_sign_derive, dim3(blocks_for(g.N, 256)), dim3(256), 0, gg::tl_st, c, g, L.ss);
+    hipLaunchKernelGGL(gg::k_sign_derive, dim3(blocks_for(g.N, 256), L.ss.t), dim3(256), 0, gg::tl_st, c, g, L.ss);
     if (!L.pays.empty()) {
         DASH_CHECK(g.PB != nullptr, "gpu garbler: payload bank not allocated");
         const gg::PayDesc* pd = gg::dconst(L.pays.data(), L.pays.size());
         const int npd = static_cast<int>(L.pays.size());
         hipLaunchKernelGGL(gg::k_payloads, dim3(blocks_for(g.N * npd, 256, 16384)), dim3(256), 0, gg::tl_st, c, g, pd, npd);
     }
-    hipLaunchKernelGGL(gg::k_project, dim3(blocks_for((g.N + 63) / 64 * 64 * g.entries, gg::kPB, 16384)), dim3(gg::kPB), 0, gg::tl_st, c,
-                       g, in, tb);
+    project(c, g, in, tb, L.projs);
     HIPCHECK(hipGetLastError());
 }
 
@@ -1307,22 +1401,68 @@ struct DevCtx {
         }
         return PB;
     }
+    // key hashes / colors between k_hash and k_emit
+    u128* HC = nullptr;
+    uint8_t* CC = nullptr;
+    size_t HC_n = 0;
+    std::pair<u128*, uint8_t*> hc(size_t entries, int64_t N) {
+        const size_t n = std::max<size_t>(1, entries * static_cast<size_t>(N));
+        if (n > HC_n) {
+            HIPCHECK(hipStreamSynchronize(st));
+            if (HC) (void)hipFree(HC);
+            if (CC) (void)hipFree(CC);
+            HIPCHECK(hipMalloc(reinterpret_cast<void**>(&HC), n * sizeof(u128)));
+            HIPCHECK(hipMalloc(reinterpret_cast<void**>(&CC), n));
+            HC_n = n;
+        }
+        return {HC, CC};
+    }
 };
-DevCtx& dev_ctx(int device) {
+thread_local DevCtx* tl_dc = nullptr;  // the calling thread's garbling context (set by Impl::enter)
+namespace {  // the same (translation-unit) anonymous namespace as its declaration above run_sign
+std::pair<u128*, uint8_t*> hc_scratch(size_t entries, int64_t N) {
+    DASH_CHECK(tl_dc != nullptr, "gpu garbler: no garbling context on this thread");
+    return tl_dc->hc(entries, N);
+}
+}  // namespace
+// A free garbling context of the device, locked for the caller: up to DASH_GG_CONTEXTS (default 2) per
+// device, so two garblings (two threads, e.g. the serving engine's refill workers) run on two streams at
+// once and fill each other's launch gaps; a third waits for the first context to free up.
+std::unique_lock<std::mutex> acquire_ctx(int device, DevCtx*& out) {
     static std::mutex m;
-    static std::map<int, DevCtx*>* ctxs = new std::map<int, DevCtx*>();  // leaked: lives as long as the process
-    std::lock_guard<std::mutex> g(m);
-    auto it = ctxs->find(device);
-    if (it != ctxs->end()) return *it->second;
-    DevCtx* c = new DevCtx();
-    c->init(device);
-    (*ctxs)[device] = c;
-    return *c;
+    static auto* pools = new std::map<int, std::vector<DevCtx*>>();  // leaked: lives as long as the process
+    static const size_t cap = [] {
+        const char* e = std::getenv("DASH_GG_CONTEXTS");
+        return static_cast<size_t>(std::max(1, e ? std::atoi(e) : 2));
+    }();
+    DevCtx* first = nullptr;
+    {
+        std::lock_guard<std::mutex> g(m);
+        auto& pool = (*pools)[device];
+        for (DevCtx* c : pool) {
+            std::unique_lock<std::mutex> l(c->m, std::try_to_lock);
+            if (l.owns_lock()) {
+                out = c;
+                return l;
+            }
+        }
+        if (pool.size() < cap) {
+            DevCtx* c = new DevCtx();
+            c->init(device);
+            pool.push_back(c);
+            out = c;
+            return std::unique_lock<std::mutex>(c->m);
+        }
+        first = pool.front();
+    }
+    out = first;
+    return std::unique_lock<std::mutex>(first->m);  // every context busy: queue on the first one
 }
 
 struct GpuGarbler::Impl {
-    DevCtx& dc;
+    DevCtx* dcp = nullptr;
     std::unique_lock<std::mutex> lock;
+    DevCtx& dc;
     gg::Ctx c{};
     // device cur: per residue label-major [N][n_j]
     std::vector<DevBlock> cur;
@@ -1335,7 +1475,7 @@ struct GpuGarbler::Impl {
     // sign base labels a sign_last mixed-radix rescale leaves for the next ReLU ([N][kW], relu_mult)
     DevBlock sig;
     int64_t sig_N = 0;
-    explicit Impl(int dev) : dc(dev_ctx(dev)), lock(dc.m), device(dev) {}
+    explicit Impl(int dev) : lock(acquire_ctx(dev, dcp)), dc(*dcp), device(dev) {}
     template <class T>
     const T* stage(const T* h, size_t n) { return dc.stage(h, n); }
     int16_t* scratch(size_t bytes) { return dc.scratch(bytes); }
@@ -1354,6 +1494,7 @@ struct GpuGarbler::Impl {
     void enter() {
         HIPCHECK(hipSetDevice(device));
         gg::tl_st = dc.st;
+        tl_dc = &dc;
     }
     ~Impl() {
         // garble() returns with every table written; blocks released below are reused in stream order
@@ -1673,8 +1814,7 @@ void GpuGarbler::sign_layer(uint64_t layer, const SignPlan& sp, CrtLabels& cur, 
         gm.nblk = draw_blocks(dr);
         check_desc(gm);
         hipLaunchKernelGGL(gg::k_draw, dim3(blocks_for(N * gm.nblk, gg::kGB, 8192)), dim3(gg::kGB), 0, gg::tl_st, I.c, gm);
-        hipLaunchKernelGGL(gg::k_project, dim3(blocks_for((N + 63) / 64 * 64 * gm.entries, gg::kPB, 16384)), dim3(gg::kPB), 0, gg::tl_st,
-                           I.c, gm, in, tb);
+        project(I.c, gm, in, tb, pr);
         gg::MiniArgs ma{};
         ma.k = k;
         for (int j = 0; j < k; ++j) ma.crt[j] = I.crt[j];
@@ -1840,8 +1980,7 @@ static std::vector<DevBlock> relu_mult_gates(GpuGarbler::Impl& I, const gg::Gadg
     gm.nblk = draw_blocks(dm);
     check_desc(gm);
     hipLaunchKernelGGL(gg::k_draw, dim3(blocks_for(N * gm.nblk, gg::kGB, 8192)), dim3(gg::kGB), 0, gg::tl_st, I.c, gm);
-    hipLaunchKernelGGL(gg::k_project, dim3(blocks_for((N + 63) / 64 * 64 * gm.entries, gg::kPB, 16384)),
-                       dim3(gg::kPB), 0, gg::tl_st, I.c, gm, in, tb);
+    project(I.c, gm, in, tb, pm);
     gg::MiniArgs ma{};
     ma.k = k;
     for (int j = 0; j < k; ++j) ma.crt[j] = I.crt[j];
@@ -1941,9 +2080,8 @@ void GpuGarbler::relu_mrs(uint64_t layer, const SignMrsPlan& P, CrtLabels& cur, 
     check_desc(g);
     std::vector<void*> tmp;
     hipLaunchKernelGGL(gg::k_draw, dim3(blocks_for(N * g.nblk, gg::kGB, 8192)), dim3(gg::kGB), 0, gg::tl_st, I.c, g);
-    hipLaunchKernelGGL(gg::k_mrs_sign_derive, dim3(blocks_for(N, 256)), dim3(256), 0, gg::tl_st, I.c, g, in, a);
-    hipLaunchKernelGGL(gg::k_project, dim3(blocks_for((N + 63) / 64 * 64 * g.entries, gg::kPB, 16384)), dim3(gg::kPB), 0,
-                       gg::tl_st, I.c, g, in, tb);
+    hipLaunchKernelGGL(gg::k_mrs_sign_derive, dim3(blocks_for(N, 256), k), dim3(256), 0, gg::tl_st, I.c, g, in, a);
+    project(I.c, g, in, tb, pr);
     // mixed-modulus half gates (as sign_layer's ReLU branch, sign label = residue 0's key slot)
     std::vector<DevBlock> out = relu_mult_gates(I, g, in, tb, sig_slot, sk0, *prefix);
     HIPCHECK(hipGetLastError());
@@ -2068,9 +2206,8 @@ void GpuGarbler::rescale_mrs(uint64_t layer, const RescaleMrsPlan& P, CrtLabels&
         const int npd = static_cast<int>(pays.size());
         hipLaunchKernelGGL(gg::k_payloads, dim3(blocks_for(N * npd, 256, 16384)), dim3(256), 0, gg::tl_st, I.c, g, pd, npd);
     }
-    hipLaunchKernelGGL(gg::k_mrs_derive, dim3(blocks_for(N, 256)), dim3(256), 0, gg::tl_st, I.c, g, a);
-    hipLaunchKernelGGL(gg::k_project, dim3(blocks_for((N + 63) / 64 * 64 * g.entries, gg::kPB, 16384)), dim3(gg::kPB), 0,
-                       gg::tl_st, I.c, g, in, tb);
+    hipLaunchKernelGGL(gg::k_mrs_derive, dim3(blocks_for(N, 256), k + 1), dim3(256), 0, gg::tl_st, I.c, g, a);
+    project(I.c, g, in, tb, pr);
     if (P.sign_last) {
         // residue 0's key slot is the sign label of the ReLU that follows (relu_mult)
         I.sig.alloc(I.device, static_cast<size_t>(N) * gg::kW * sizeof(int16_t));

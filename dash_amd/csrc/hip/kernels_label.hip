@@ -271,6 +271,22 @@ void launch_chunk_from_act_res(const TrRes& a, hipStream_t st) {
     hipLaunchKernelGGL(k_chunk_res<false>, grid_cast_res(a), dim3(256), 0, st, a);
 }
 
+// one block per descriptor; 4-byte words where source, destination and size allow, bytes otherwise
+__global__ __launch_bounds__(256) void k_scatter(const ScatterDesc* d, const uint8_t* src, int b) {
+    const ScatterDesc c = d[blockIdx.x];
+    const uint8_t* s = src + c.off;
+    uint8_t* t = c.dst0 + static_cast<size_t>(b) * c.stride;
+    if (((reinterpret_cast<uintptr_t>(t) | reinterpret_cast<uintptr_t>(s) | c.bytes) & 3) == 0) {
+        for (size_t i = threadIdx.x; i < c.bytes / 4; i += blockDim.x)
+            reinterpret_cast<uint32_t*>(t)[i] = reinterpret_cast<const uint32_t*>(s)[i];
+    } else {
+        for (size_t i = threadIdx.x; i < c.bytes; i += blockDim.x) t[i] = s[i];
+    }
+}
+void launch_scatter(const ScatterDesc* d, int n, const uint8_t* src, int b, hipStream_t st) {
+    hipLaunchKernelGGL(k_scatter, dim3(static_cast<unsigned>(n)), dim3(256), 0, st, d, src, b);
+}
+
 void launch_aes_test(const u128* in, u128* out, int64_t n, const AesGlobals& g, hipStream_t st) {
     const unsigned nb = static_cast<unsigned>(std::min<int64_t>((n + 511) / 512, 2048));
     hipLaunchKernelGGL(k_aes_test, dim3(nb), dim3(512), 0, st, in, out, n, g.te0, g.rk);

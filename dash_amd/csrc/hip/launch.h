@@ -269,6 +269,13 @@ void launch_transpose_from_act_res(const TrRes& a, hipStream_t st);  // bytes ->
 // elementwise casts of rows[j] * cols[j] contiguous components per residue (layouts already match)
 void launch_cast_to_act_res(const TrRes& a, hipStream_t st);    // int16 -> bytes
 void launch_cast_from_act_res(const TrRes& a, hipStream_t st);  // bytes -> int16
+// per-slot constant scatter (HipEvaluator::load): block i copies `bytes` from src + off to dst0 + b * stride
+struct ScatterDesc {
+    size_t off;
+    uint8_t* dst0;
+    size_t stride, bytes;
+};
+void launch_scatter(const ScatterDesc* d, int n, const uint8_t* src, int b, hipStream_t st);
 // the GPU garbler's chunked labels (component q of element e at ((q / 8) * N + e) * 8 + q % 8; rows[j] = n_j,
 // cols[j] = N) <-> component-major bytes [n][N]
 void launch_unchunk_to_act_res(const TrRes& a, hipStream_t st);

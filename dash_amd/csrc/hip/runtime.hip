@@ -60,10 +60,18 @@ class HipEvaluator {
                        m.h.in_dims == tmpl_h_.in_dims,
                    "model does not garble the evaluator's circuit");
         HIPCHECK(hipSetDevice(dev_));
+        if (!load_st_) HIPCHECK(hipStreamCreateWithFlags(&load_st_, hipStreamNonBlocking));
+        // per-GC small constants (bias labels, zero / shift labels, ...): filled into one pinned staging block,
+        // one H2D copy and one scatter kernel to their slot-b destinations, instead of ~100 small copies
+        if (!small_.empty()) {
+            for (const auto& c : small_) c.fill(m, small_h_ + c.off);
+            HIPCHECK(hipMemcpyAsync(small_d_, small_h_, small_bytes_, hipMemcpyHostToDevice, load_st_));
+            launch_scatter(small_desc_, static_cast<int>(small_.size()), small_d_, b, load_st_);
+        }
+        // tables (a GC garbled into this slot through sink() needs none of these copies)
         for (auto& f : loaders_) f(b, m);
-        // the loaders' copies run on the null stream; evaluation and garbling streams are non-blocking, so this
-        // waits for the load only (a device-wide sync would also wait for other groups' evaluations)
-        HIPCHECK(hipStreamSynchronize(nullptr));
+        // evaluation and garbling streams are non-blocking: this waits for this load only
+        HIPCHECK(hipStreamSynchronize(load_st_));
         loaded_[b] = 1;
     }
     // Zero-copy offline phase (GarbleOptions::sink): slot b's table arenas as GPU-garbler destinations.
@@ -89,6 +97,7 @@ class HipEvaluator {
         return s;
     }
     ~HipEvaluator() {
+        if (load_st_) (void)hipStreamDestroy(load_st_);
         if (gexec_) (void)hipGraphExecDestroy(gexec_);
         for (void* p : allocs_) (void)hipFree(p);
         for (void* p : host_allocs_) (void)hipHostFree(p);
@@ -265,22 +274,43 @@ class HipEvaluator {
     }
     // a model array into device memory: device-to-device (or peer) when the GPU
     // garbler left it in HBM and nobody has fetched (and possibly edited) a host copy
-    static void copy_in(uint8_t* dst, const Array& a) {
+    static void copy_in(uint8_t* dst, const Array& a, hipStream_t st) {
         if (a.device_resident() && a.device_ptr() == dst) return;  // garbled straight into this slot (sink)
         if (a.device_resident() && !a.dev->host)
-            HIPCHECK(hipMemcpy(dst, a.device_ptr(), a.nbytes, hipMemcpyDefault));
-        else
-            HIPCHECK(hipMemcpy(dst, a.ptr<uint8_t>(), a.nbytes, hipMemcpyHostToDevice));
+            HIPCHECK(hipMemcpyAsync(dst, a.device_ptr(), a.nbytes, hipMemcpyDefault, st));
+        else  // pageable host source: staged before the call returns
+            HIPCHECK(hipMemcpyAsync(dst, a.ptr<uint8_t>(), a.nbytes, hipMemcpyHostToDevice, st));
+    }
+    // a per-GC small constant of `bytes` at dst0 + b * stride for slot b, filled on the host by `fill`
+    void add_small(uint8_t* dst0, size_t stride, size_t bytes, std::function<void(const GarbledModel&, uint8_t*)> fill) {
+        SmallLoad c;
+        c.off = small_bytes_;
+        c.dst0 = dst0;
+        c.stride = stride;
+        c.bytes = bytes;
+        c.fill = std::move(fill);
+        small_bytes_ += (bytes + 15) / 16 * 16;
+        small_.push_back(std::move(c));
+    }
+    // after build(): staging buffers and the device descriptor table of the small constants
+    void finish_small() {
+        if (small_.empty()) return;
+        HIPCHECK(hipHostMalloc(reinterpret_cast<void**>(&small_h_), small_bytes_));
+        host_allocs_.push_back(small_h_);
+        small_d_ = dalloc<uint8_t>(small_bytes_);
+        std::vector<ScatterDesc> d;
+        for (const auto& c : small_) d.push_back(ScatterDesc{c.off, c.dst0, c.stride, c.bytes});
+        small_desc_ = upload(d.data(), d.size());
     }
     // one device buffer holding array `name` of layer li of every GC slot
     const u128* upload_tables(size_t li, const std::string& name) {
         const size_t nb = tmpl_->layers[li].arr(name).nbytes;
         uint8_t* d = dalloc<uint8_t>(nb * B_);
         arena_[{li, name}] = {d, nb};
-        loaders_.push_back([d, nb, li, name](int b, const GarbledModel& m) {
+        loaders_.push_back([this, d, nb, li, name](int b, const GarbledModel& m) {
             const Array& a = m.layers[li].arr(name);
             DASH_CHECK(a.nbytes == nb, "table size mismatch across batch");
-            copy_in(d + nb * b, a);
+            copy_in(d + nb * b, a, load_st_);
         });
         table_bytes_ += nb * B_;
         return reinterpret_cast<const u128*>(d);
@@ -288,8 +318,10 @@ class HipEvaluator {
     const int16_t* upload_i16_rows(size_t li, const std::string& name) {
         const size_t nb = tmpl_->layers[li].arr(name).nbytes;
         uint8_t* d = dalloc<uint8_t>(nb * B_);
-        loaders_.push_back([d, nb, li, name](int b, const GarbledModel& m) {
-            copy_in(d + nb * b, m.layers[li].arr(name));
+        add_small(d, nb, nb, [nb, li, name](const GarbledModel& m, uint8_t* h) {
+            const Array& a = m.layers[li].arr(name);
+            DASH_CHECK(a.nbytes == nb, "bias rows size mismatch across batch");
+            std::memcpy(h, a.ptr<uint8_t>(), nb);
         });
         return reinterpret_cast<const int16_t*>(d);
     }
@@ -300,14 +332,15 @@ class HipEvaluator {
         for (int j = 0; j < k_; ++j) names.push_back(name_of(j));
         const int ls = lab_stride_, k = k_;
         std::vector<int> off(lab_off_, lab_off_ + k_), crt = crt_;
-        loaders_.push_back([d, names, ls, k, off, crt](int b, const GarbledModel& m) {
-            std::vector<int16_t> h(ls);
+        add_small(reinterpret_cast<uint8_t*>(d), sizeof(int16_t) * ls, sizeof(int16_t) * ls,
+                  [names, ls, k, off, crt](const GarbledModel& m, uint8_t* hb) {
+            int16_t* h = reinterpret_cast<int16_t*>(hb);
+            std::fill(h, h + ls, int16_t(0));
             for (int j = 0; j < k; ++j) {
                 auto it = m.consts.find(names[j]);
                 DASH_CHECK(it != m.consts.end(), "missing model constant " + names[j]);
                 std::memcpy(&h[off[j]], it->second.ptr<int16_t>(), sizeof(int16_t) * nr_comps(crt[j]));
             }
-            HIPCHECK(hipMemcpy(d + static_cast<size_t>(b) * ls, h.data(), sizeof(int16_t) * ls, hipMemcpyHostToDevice));
         });
         return d;
     }
@@ -386,6 +419,18 @@ class HipEvaluator {
     size_t tmpl_nlayers_ = 0;
     bool mfma_;
     std::vector<std::function<void(int, const GarbledModel&)>> loaders_;
+    struct SmallLoad {
+        size_t off = 0;
+        uint8_t* dst0 = nullptr;
+        size_t stride = 0, bytes = 0;
+        std::function<void(const GarbledModel&, uint8_t*)> fill;
+    };
+    std::vector<SmallLoad> small_;
+    size_t small_bytes_ = 0;
+    uint8_t* small_h_ = nullptr;
+    uint8_t* small_d_ = nullptr;
+    const ScatterDesc* small_desc_ = nullptr;
+    hipStream_t load_st_ = nullptr;
     std::map<std::pair<size_t, std::string>, std::pair<uint8_t*, size_t>> arena_;  // (layer, table) -> [B][nb]
     std::vector<int> loaded_;
     int dev_ = 0, B_ = 1, k_ = 0;
@@ -467,9 +512,12 @@ void HipEvaluator::build() {
         zh_ = dzh;
         zcol_ = dzcol;
         const int zs = zstride_;
-        loaders_.push_back([dzc, dzh, dzcol, zs, maxmod](int b, const GarbledModel& m) {
-            std::vector<u128> zc(zs, 0), zh(zs, 0);
-            std::vector<uint16_t> zcol(zs, 0);
+        // compressed zero labels, their hashes and colors: one fill writes all three staging blocks (the zc
+        // block's fill computes them; the two followers' fills are no-ops on the same pass)
+        auto zfill = [zs, maxmod](const GarbledModel& m, u128* zc, u128* zh, uint16_t* zcol) {
+            std::fill(zc, zc + zs, u128(0));
+            std::fill(zh, zh + zs, u128(0));
+            std::fill(zcol, zcol + zs, uint16_t(0));
             LabelBank Z = m.zero_bank();
             for (int q = 2; q <= maxmod; ++q) {
                 if (Z.lab[q].empty()) continue;
@@ -477,10 +525,16 @@ void HipEvaluator::build() {
                 zh[q] = hash(zc[q]);
                 zcol[q] = static_cast<uint16_t>(Z.lab[q][0]);
             }
-            HIPCHECK(hipMemcpy(dzc + static_cast<size_t>(b) * zs, zc.data(), sizeof(u128) * zs, hipMemcpyHostToDevice));
-            HIPCHECK(hipMemcpy(dzh + static_cast<size_t>(b) * zs, zh.data(), sizeof(u128) * zs, hipMemcpyHostToDevice));
-            HIPCHECK(hipMemcpy(dzcol + static_cast<size_t>(b) * zs, zcol.data(), sizeof(uint16_t) * zs, hipMemcpyHostToDevice));
+        };
+        const size_t zcb = sizeof(u128) * zs, zcolb = sizeof(uint16_t) * zs;
+        const size_t zoff = small_bytes_;  // the three blocks are staged back to back (16-B rounded)
+        const size_t zhoff = zoff + (zcb + 15) / 16 * 16, zcoloff = zhoff + (zcb + 15) / 16 * 16;
+        add_small(reinterpret_cast<uint8_t*>(dzc), zcb, zcb, [zfill, zoff, zhoff, zcoloff](const GarbledModel& m, uint8_t* h) {
+            zfill(m, reinterpret_cast<u128*>(h), reinterpret_cast<u128*>(h + (zhoff - zoff)),
+                  reinterpret_cast<uint16_t*>(h + (zcoloff - zoff)));
         });
+        add_small(reinterpret_cast<uint8_t*>(dzh), zcb, zcb, [](const GarbledModel&, uint8_t*) {});
+        add_small(reinterpret_cast<uint8_t*>(dzcol), zcolb, zcolb, [](const GarbledModel&, uint8_t*) {});
     }
     bool any_rescale = false;
     for (auto& l : m0.layers) any_rescale |= (l.kind == K_RESCALE && l.param("mode", 0) != 2);  // mode 2: no shift labels
@@ -1160,6 +1214,7 @@ void HipEvaluator::build() {
         host_allocs_.push_back(p);
         out_stage_.push_back(p);
     }
+    finish_small();
     HIPCHECK(hipDeviceSynchronize());
 }
 
@@ -1182,19 +1237,24 @@ void HipEvaluator::plan_rescale_legacy(size_t li, i64 iters, i64 N, const CrtInf
         u128* ddu = dalloc<u128>(B_);
         const int k = k_;
         std::vector<int> off(lab_off_, lab_off_ + k_), crtv = crt_;
-        loaders_.push_back([dd, ddu, ls, k, off, crtv](int b, const GarbledModel& m) {
-            std::vector<int16_t> h(ls);
-            u128 pk = 0;
+        add_small(reinterpret_cast<uint8_t*>(dd), sizeof(int16_t) * ls, sizeof(int16_t) * ls,
+                  [ls, k, off, crtv](const GarbledModel& m, uint8_t* hb) {
+            int16_t* h = reinterpret_cast<int16_t*>(hb);
+            std::fill(h, h + ls, int16_t(0));
             for (int j = 0; j < k; ++j) {
                 const int p = crtv[j], n = nr_comps(p);
                 const int16_t* up = m.consts.at("up." + std::to_string(j)).ptr<int16_t>();
                 const int16_t* dn = m.consts.at("down.2." + std::to_string(j)).ptr<int16_t>();
                 for (int c = 0; c < n; ++c) h[off[j] + c] = static_cast<int16_t>(pmod(up[c] - dn[c], p));
-                if (j == 0)
-                    for (int c = 0; c < n; ++c) pk |= static_cast<u128>((up[c] ^ dn[c]) & 1) << c;
             }
-            HIPCHECK(hipMemcpy(dd + static_cast<size_t>(b) * ls, h.data(), sizeof(int16_t) * ls, hipMemcpyHostToDevice));
-            HIPCHECK(hipMemcpy(ddu + b, &pk, sizeof(u128), hipMemcpyHostToDevice));
+        });
+        add_small(reinterpret_cast<uint8_t*>(ddu), sizeof(u128), sizeof(u128), [](const GarbledModel& m, uint8_t* hb) {
+            u128 pk = 0;
+            const int n = nr_comps(2);
+            const int16_t* up = m.consts.at("up.0").ptr<int16_t>();
+            const int16_t* dn = m.consts.at("down.2.0").ptr<int16_t>();
+            for (int c = 0; c < n; ++c) pk |= static_cast<u128>((up[c] ^ dn[c]) & 1) << c;
+            std::memcpy(hb, &pk, sizeof(u128));
         });
         delta = dd;
         du = ddu;

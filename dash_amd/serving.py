@@ -168,6 +168,8 @@ class _Group:
         self.ready = threading.Event()
         self.stream = None
         self.runs = 0           # evaluations so far (run 2 captures the hipGraph)
+        self.lock = threading.Lock()
+        self.pending = 0        # spent slots still being refilled
 
 
 class InferenceService:
@@ -188,7 +190,7 @@ class InferenceService:
                  step_timeout_s: float = 120.0, seed: Optional[bytes] = None, prefetch: bool = True,
                  fault_hook: Optional[Callable[[int, int], bool]] = None, nthreads: int = 0,
                  rescale: str = "auto", relu: str = "auto", fused_sign: bool = True,
-                 insecure_fixed_seed: bool = False):
+                 insecure_fixed_seed: bool = False, garble_workers: Optional[int] = None):
         if backend not in ("hip", "cpu"):
             raise ValueError("backend must be 'hip' or 'cpu'")
         if seed is not None and not insecure_fixed_seed:
@@ -210,13 +212,18 @@ class InferenceService:
         self.stats = ServiceStats()
         self.healthy = True
         self.groups = [_Group(g, slots_per_group) for g in range(groups)]
+        # background refill workers: with the GPU garbler two GCs garble at once on two streams of the device
+        # (gpu_garbler.h DevCtx pool), filling each other's kernel-launch gaps
+        self.garble_workers = max(1, int(garble_workers if garble_workers is not None else
+                                         (2 if self.garble_device else 1)))
+        self._ctr_lock = threading.Lock()
         self._next_group = 0
         self._err: Optional[BaseException] = None
         # hipGraph capture (a group's 2nd run) must not overlap the garbler thread's device-wide syncs and
         # allocations, which would invalidate the capture; replays and eager runs need no lock
         self._capture_lock = threading.Lock()
         self._infer_lock = threading.Lock()
-        self._q: "queue.Queue[Optional[_Group]]" = queue.Queue()
+        self._q: "queue.Queue" = queue.Queue()  # (group, slot) refill items; None stops a worker
         if backend == "hip":
             import torch
 
@@ -229,23 +236,31 @@ class InferenceService:
             self._refill(g)
         if backend == "hip":
             self._prime_graphs()
-        self._worker = None
+        self._workers: List[threading.Thread] = []
         if prefetch:
-            self._worker = threading.Thread(target=self._garbler_loop, name="dash-garbler", daemon=True)
-            self._worker.start()
+            for w in range(self.garble_workers):
+                t = threading.Thread(target=self._garbler_loop, name=f"dash-garbler-{w}", daemon=True)
+                t.start()
+                self._workers.append(t)
+
+    @property
+    def _worker(self):  # the first refill worker (None without prefetch)
+        return self._workers[0] if self._workers else None
 
     # ------------------------------------------------------------ offline
     def _new_gc(self, sink=None):
         from .garbling import GarbledCircuit
 
-        seed = hashlib.sha256(self._seed + self._ctr.to_bytes(8, "little")).digest()[:16]
-        self._ctr += 1
+        with self._ctr_lock:
+            seed = hashlib.sha256(self._seed + self._ctr.to_bytes(8, "little")).digest()[:16]
+            self._ctr += 1
         t = time.perf_counter()
         gc = GarbledCircuit(self.circuit, self.crt, self.mrs, max_modulus=self.max_modulus, seed=seed,
                             nthreads=self.nthreads, device=self.device if self.garble_device else None,
                             sink=sink if self.garble_device else None, **self.gc_kw)
-        self.stats.garble_s += time.perf_counter() - t
-        self.stats.gcs_garbled += 1
+        with self._ctr_lock:
+            self.stats.garble_s += time.perf_counter() - t
+            self.stats.gcs_garbled += 1
         return gc
 
     def _prime_graphs(self) -> None:
@@ -262,32 +277,44 @@ class InferenceService:
             g.runs = 2
             wait_stream(g.stream, self.step_timeout_s, f"group {g.idx} graph capture")
 
-    def _refill(self, g: _Group) -> None:
-        for b in range(g.slots):
-            if g.gcs[b] is not None:  # never encoded: still fresh
-                continue
-            if self.backend == "hip":
-                from .runtime import HipEvaluator
+    def _refill_slot(self, g: _Group, b: int) -> None:
+        if self.backend == "hip":
+            from .runtime import HipEvaluator
 
-                with self._capture_lock:  # GPU garbling + upload (allocations on the first fill)
-                    # the GPU garbler writes the tables straight into the slot (zero-copy load)
-                    gc = self._new_gc(g.ev.sink(b) if g.ev is not None else None)
+            if g.ev is None:
+                with self._capture_lock:  # first fill: evaluator allocation and its device-wide setup
+                    gc = self._new_gc()
                     if g.ev is None:
                         g.ev = HipEvaluator(template=gc.model, batch=g.slots, device=self.device)
-                    g.ev.load(b, gc.model)
-                gc.model = None  # tables live in HBM now
             else:
-                gc = self._new_gc()
-            g.gcs[b] = gc
-        g.ready.set()  # the GPU garbler's recycled table blocks stay cached for the next refill
+                # the GPU garbler writes the tables straight into the slot (zero-copy load) on its own stream:
+                # no device-wide synchronization, so refills overlap the other groups' evaluations
+                gc = self._new_gc(g.ev.sink(b))
+            g.ev.load(b, gc.model)
+            gc.model = None  # tables live in HBM now
+        else:
+            gc = self._new_gc()
+        g.gcs[b] = gc
+
+    def _refill(self, g: _Group) -> None:
+        for b in range(g.slots):
+            if g.gcs[b] is None:  # a non-None GC was never encoded: still fresh
+                self._refill_slot(g, b)
+        g.ready.set()
 
     def _garbler_loop(self) -> None:
         while True:
-            g = self._q.get()
-            if g is None or not self.healthy:
+            item = self._q.get()
+            if item is None or not self.healthy:
                 return
+            g, b = item
             try:
-                self._refill(g)
+                self._refill_slot(g, b)
+                with g.lock:
+                    g.pending -= 1
+                    done = g.pending == 0
+                if done:
+                    g.ready.set()
             except BaseException as e:  # surfaced by the next infer()
                 self._err = e
                 self.healthy = False
@@ -318,9 +345,12 @@ class InferenceService:
             g.gcs[b] = None
         g.ready.clear()
         # an unhealthy service (hung GPU step or dead garbler) never refills: the refill would block on the
-        # hung kernel (device-wide syncs in the GPU garbler and in HipEvaluator.load)
-        if self._worker is not None and self.healthy:
-            self._q.put(g)
+        # hung kernel
+        if self._workers and self.healthy:
+            with g.lock:
+                g.pending = used
+            for b in range(used):  # one item per spent slot: the workers garble a group's slots in parallel
+                self._q.put((g, b))
 
     # ------------------------------------------------------------- online
     def _run_group(self, g: _Group, xs: Sequence[np.ndarray], idx: Sequence[int], attempts: Sequence[int]):
@@ -408,15 +438,17 @@ class InferenceService:
         pool: freeing device memory or destroying streams would block on the
         hung kernel. The garbler thread is a daemon, so the process can still
         exit (non-zero) and the supervisor restarts the rank."""
-        if self._worker is not None:
+        if self._workers:
             while True:  # drop pending refills: the pool is going away
                 try:
                     self._q.get_nowait()
                 except queue.Empty:
                     break
-            self._q.put(None)
-            self._worker.join(timeout=join_timeout_s if self.healthy else 1.0)
-            self._worker = None
+            for _ in self._workers:
+                self._q.put(None)
+            for t in self._workers:
+                t.join(timeout=join_timeout_s if self.healthy else 1.0)
+            self._workers = []
         if not self.healthy:
             self._abandoned = (self.groups, getattr(self, "_streams", []))  # never freed, see above
             self.groups, self._streams = [], []

@@ -11,7 +11,8 @@ import os
 import sys
 import time
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+# DASH_PKG_ROOT: import dash_amd from another tree (A/B builds, scripts/ab_variant.sh)
+sys.path.insert(0, os.environ.get("DASH_PKG_ROOT") or os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 from dash_amd.garbling import GarbledCircuit  # noqa: E402
 from dash_amd.ir.quant import QuantizationMethod as Q  # noqa: E402

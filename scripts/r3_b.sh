@@ -18,3 +18,5 @@ rm -rf gpurun_out/$T/ggkt
 head -24 gpurun_out/$T/gg_kt_summary.txt
 timeout -k 10 600 python bench.py --steps 10 --warmup 3 > gpurun_out/$T/bench.json 2> gpurun_out/$T/bench.err || { tail -20 gpurun_out/$T/bench.err; exit 1; }
 cat gpurun_out/$T/bench.json
+timeout -k 10 300 python benchmarks/serving.py --slots 16 --groups 3 --requests 12 --faults 0.05 > gpurun_out/$T/serve.json 2> gpurun_out/$T/serve.err || { tail -20 gpurun_out/$T/serve.err; exit 1; }
+cat gpurun_out/$T/serve.json
