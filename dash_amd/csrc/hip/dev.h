@@ -273,8 +273,9 @@ __device__ __forceinline__ uint32_t u128_mod(u128 P, const ModC& m) {
 #endif
 #define DASH_AES_LDS_BYTES (2048 * DASH_AES_COPIES)
 #define DASH_AES_LDS_WORDS (DASH_AES_LDS_BYTES / 4)
-constexpr uint32_t kAesRow = 8 * DASH_AES_COPIES;  // bytes per table row: Te0 copies, then Te2 copies
-constexpr uint32_t kAesT2 = 4 * DASH_AES_COPIES;   // offset of the Te2 copies inside a row
+// Image size for C copies (the garbler's AES-bound kernels use the conflict-free 32-copy image, 64 KiB)
+template <int C>
+constexpr int aes_lds_words() { return 512 * C; }
 
 __device__ constexpr uint32_t kAesRk[44] = {
     0x00010203u, 0x04050607u, 0x08090a0bu, 0x0c0d0e0fu, 0xd6aa74fdu, 0xd2af72fau, 0xdaa678f1u, 0xd6ab76feu,
@@ -284,31 +285,33 @@ __device__ constexpr uint32_t kAesRk[44] = {
     0x47438735u, 0xa41c65b9u, 0xe016baf4u, 0xaebf7ad2u, 0x549932d1u, 0xf0855768u, 0x1093ed9cu, 0xbe2c974eu,
     0x13111d7fu, 0xe3944a17u, 0xf307a78bu, 0x4d2b30c5u};
 
-struct AesCtx {
+// LDS image of C copies: row x = C words of Te0[x], then C words of Te2[x] (8 * C bytes per row)
+template <int C>
+struct AesT {
+    static constexpr uint32_t kRow = 8 * C;  // bytes per table row
+    static constexpr uint32_t kT2 = 4 * C;   // offset of the Te2 copies inside a row
     const char* T;  // LDS image base
-    uint32_t lo;    // 4 * (lane mod 32)
+    uint32_t lo;    // 4 * (lane mod C)
 };
+using AesCtx = AesT<DASH_AES_COPIES>;
 
 __device__ __forceinline__ uint32_t ror32(uint32_t x, int r) { return (x >> r) | (x << (32 - r)); }
 __device__ __forceinline__ uint32_t rol32c(uint32_t x, int r) { return (x << r) | (x >> (32 - r)); }
 __device__ __forceinline__ uint32_t bswap32(uint32_t x) { return __builtin_bswap32(x); }
 
-// byte offset of row byte_I(s), lane copy: D = {0, 0, s.byte[I], lo.byte[0]}
-template <int I>
+// byte offset of row byte_I(s), lane copy (C = 32: D = {0, 0, s.byte[I], lo.byte[0]}, one v_perm_b32)
+template <int I, int C>
 __device__ __forceinline__ uint32_t aes_off(uint32_t s, uint32_t lo) {
-#if DASH_AES_COPIES == 32
-    return __builtin_amdgcn_perm(s, lo, 0x0c0c0000u | ((4u + I) << 8));
-#else
-    return (((s >> (8 * I)) & 0xffu) * kAesRow) | lo;
-#endif
+    if constexpr (C == 32) return __builtin_amdgcn_perm(s, lo, 0x0c0c0000u | ((4u + I) << 8));
+    else return (((s >> (8 * I)) & 0xffu) * AesT<C>::kRow) | lo;
 }
-template <int I>
-__device__ __forceinline__ uint32_t aes_t0(const AesCtx& a, uint32_t s) {
-    return *reinterpret_cast<const uint32_t*>(a.T + aes_off<I>(s, a.lo));
+template <int I, int C>
+__device__ __forceinline__ uint32_t aes_t0(const AesT<C>& a, uint32_t s) {
+    return *reinterpret_cast<const uint32_t*>(a.T + aes_off<I, C>(s, a.lo));
 }
-template <int I>
-__device__ __forceinline__ uint32_t aes_t2(const AesCtx& a, uint32_t s) {
-    return *reinterpret_cast<const uint32_t*>(a.T + aes_off<I>(s, a.lo) + kAesT2);
+template <int I, int C>
+__device__ __forceinline__ uint32_t aes_t2(const AesT<C>& a, uint32_t s) {
+    return *reinterpret_cast<const uint32_t*>(a.T + aes_off<I, C>(s, a.lo) + AesT<C>::kT2);
 }
 // three-input XOR in one VALU op (v_bitop3_b32, truth table 0x96)
 __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
@@ -317,30 +320,35 @@ __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
     return d;
 }
 // one output column of a middle round: Te0[s0.b3]^Te1[s1.b2]^Te2[s2.b1]^Te3[s3.b0]^rk
-__device__ __forceinline__ uint32_t aes_col(const AesCtx& a, uint32_t s0, uint32_t s1, uint32_t s2, uint32_t s3,
+template <int C>
+__device__ __forceinline__ uint32_t aes_col(const AesT<C>& a, uint32_t s0, uint32_t s1, uint32_t s2, uint32_t s3,
                                             uint32_t rk) {
-    const uint32_t u = xor3(aes_t0<2>(a, s1), aes_t2<0>(a, s3), rol32c(rk, 8));
-    return xor3(aes_t0<3>(a, s0), aes_t2<1>(a, s2), ror32(u, 8));
+    const uint32_t u = xor3(aes_t0<2, C>(a, s1), aes_t2<0, C>(a, s3), rol32c(rk, 8));
+    return xor3(aes_t0<3, C>(a, s0), aes_t2<1, C>(a, s2), ror32(u, 8));
 }
 // final round column: S-box bytes sit at Te2.b3, Te0.b2, Te0.b1, Te2.b0
-__device__ __forceinline__ uint32_t aes_last(const AesCtx& a, uint32_t s0, uint32_t s1, uint32_t s2, uint32_t s3,
+template <int C>
+__device__ __forceinline__ uint32_t aes_last(const AesT<C>& a, uint32_t s0, uint32_t s1, uint32_t s2, uint32_t s3,
                                              uint32_t rk) {
-    const uint32_t x1 = __builtin_amdgcn_perm(aes_t2<3>(a, s0), aes_t0<2>(a, s1), 0x07020c0cu);
-    const uint32_t x2 = __builtin_amdgcn_perm(aes_t0<1>(a, s2), aes_t2<0>(a, s3), 0x0c0c0500u);
+    const uint32_t x1 = __builtin_amdgcn_perm(aes_t2<3, C>(a, s0), aes_t0<2, C>(a, s1), 0x07020c0cu);
+    const uint32_t x2 = __builtin_amdgcn_perm(aes_t0<1, C>(a, s2), aes_t2<0, C>(a, s3), 0x0c0c0500u);
     return xor3(x1, x2, rk);
 }
 
 #ifdef DASH_FAKE_AES
 // A/B experiment only (bound analysis): a cheap stand-in mixing function in place of AES.
-__device__ __forceinline__ u128 aes_encrypt(const AesCtx&, u128 in) {
+template <int C>
+__device__ __forceinline__ u128 aes_encrypt(const AesT<C>&, u128 in) {
     return (in ^ (in >> 61)) * static_cast<u128>(0x9e3779b97f4a7c15ull);
 }
-__device__ __forceinline__ void aes_encrypt2(const AesCtx& a, u128 inA, u128 inB, u128& outA, u128& outB) {
+template <int C>
+__device__ __forceinline__ void aes_encrypt2(const AesT<C>& a, u128 inA, u128 inB, u128& outA, u128& outB) {
     outA = aes_encrypt(a, inA);
     outB = aes_encrypt(a, inB);
 }
 #else
-__device__ __forceinline__ u128 aes_encrypt(const AesCtx& a, u128 in) {
+template <int C>
+__device__ __forceinline__ u128 aes_encrypt(const AesT<C>& a, u128 in) {
     uint32_t s0 = bswap32(static_cast<uint32_t>(in)) ^ kAesRk[0];
     uint32_t s1 = bswap32(static_cast<uint32_t>(in >> 32)) ^ kAesRk[1];
     uint32_t s2 = bswap32(static_cast<uint32_t>(in >> 64)) ^ kAesRk[2];
@@ -366,7 +374,8 @@ __device__ __forceinline__ u128 aes_encrypt(const AesCtx& a, u128 in) {
 
 // Two independent blocks with interleaved rounds: doubles the LDS-read ILP of
 // a latency-bound lane (the serial sign chain).
-__device__ __forceinline__ void aes_encrypt2(const AesCtx& a, u128 inA, u128 inB, u128& outA, u128& outB) {
+template <int C>
+__device__ __forceinline__ void aes_encrypt2(const AesT<C>& a, u128 inA, u128 inB, u128& outA, u128& outB) {
     uint32_t a0 = bswap32(static_cast<uint32_t>(inA)) ^ kAesRk[0], a1 = bswap32(static_cast<uint32_t>(inA >> 32)) ^ kAesRk[1];
     uint32_t a2 = bswap32(static_cast<uint32_t>(inA >> 64)) ^ kAesRk[2], a3 = bswap32(static_cast<uint32_t>(inA >> 96)) ^ kAesRk[3];
     uint32_t b0 = bswap32(static_cast<uint32_t>(inB)) ^ kAesRk[0], b1 = bswap32(static_cast<uint32_t>(inB >> 32)) ^ kAesRk[1];
@@ -404,24 +413,26 @@ struct AesGlobals {
 };
 
 // Fill the LDS image; all threads of the block participate.
+template <int C = DASH_AES_COPIES>
 __device__ __forceinline__ void aes_lds_fill(uint32_t* lds, const uint32_t* te0) {
     // 16-B LDS stores: the 4 words of an aligned quad share the table entry
-    // (i >> 6) and the rotation (i & 32), so every block's 64 KiB image costs
-    // a quarter of the loads and LDS writes of a word-wise fill
+    // and the rotation, so every block's image costs a quarter of the loads
+    // and LDS writes of a word-wise fill
     const int nt = blockDim.x * blockDim.y;
-    for (int i4 = threadIdx.x + threadIdx.y * blockDim.x; i4 < DASH_AES_LDS_WORDS / 4; i4 += nt) {
+    for (int i4 = threadIdx.x + threadIdx.y * blockDim.x; i4 < aes_lds_words<C>() / 4; i4 += nt) {
         const int i = 4 * i4;
-        const uint32_t v = te0[i / (2 * DASH_AES_COPIES)];
-        const uint32_t w = (i % (2 * DASH_AES_COPIES) >= DASH_AES_COPIES) ? ror32(v, 16) : v;
+        const uint32_t v = te0[i / (2 * C)];
+        const uint32_t w = (i % (2 * C) >= C) ? ror32(v, 16) : v;
         reinterpret_cast<uint4*>(lds)[i4] = make_uint4(w, w, w, w);
     }
     __syncthreads();
 }
 
-__device__ __forceinline__ AesCtx aes_ctx(const uint32_t* lds, const uint32_t* /*rk*/) {
-    AesCtx a;
+template <int C = DASH_AES_COPIES>
+__device__ __forceinline__ AesT<C> aes_ctx(const uint32_t* lds, const uint32_t* /*rk*/) {
+    AesT<C> a;
     a.T = reinterpret_cast<const char*>(lds);
-    a.lo = (__lane_id() % DASH_AES_COPIES) << 2;
+    a.lo = (__lane_id() % C) << 2;
     return a;
 }
 

@@ -18,6 +18,7 @@
 #include <cstring>
 #include <chrono>
 #include <cstdio>
+#include <cstdint>
 #include <cstdlib>
 #include <map>
 #include <tuple>
@@ -62,16 +63,7 @@ struct Proj {
     int table, stride;           // table id, entry stride
     int64_t off;                 // entry offset inside the element's table row
     int64_t first;               // first global entry index of this projection
-    int pay1;                    // 1 + payload bank row of f-index 0 (F_SIGN, F_DIV, F_DIVMOD); 0: computed inline
-    int pad_;
-    int64_t first_out;           // first global output (entry x target) index (k_emit; set by gg::project)
-};
-
-// A projection whose function takes few distinct values (sign: 2, carry: k+1)
-// has few distinct payloads o + f*R: they are computed once per element into a
-// payload bank (row-major [row][N], coalesced) instead of once per table entry.
-struct PayDesc {
-    int out_slot, pout, f;  // payload = slot label + f * R_pout (f already reduced mod pout)
+    int pay1;                    // unused by the kernels (k_emit's bank indices: EProj::pay1)
 };
 
 struct Tables {
@@ -83,8 +75,6 @@ struct Ctx {
     const int16_t* R;    // [max_mod + 1][kW]
     const int16_t* Z;    // [max_mod + 1][kW]
     const ModC* mc;      // [max_mod + 1]
-    const int16_t* lut;  // approx lookup [k][p][t] flattened, offsets lut_off[j]
-    int lut_off[kMaxRes];
     uint32_t rk[44];     // PRG (seed) round keys
     const uint32_t* te0;
 };
@@ -115,7 +105,13 @@ struct In {
 };
 
 // ------------------------------------------------------------------ device
-__device__ __forceinline__ u128 aes_keyed(const AesCtx& a, u128 in, const uint32_t* rk) {
+// AES-bound garbling kernels use the conflict-free 32-copy LDS image (dev.h AesT)
+constexpr int kGAes = 32;
+using GAes = AesT<kGAes>;
+constexpr int kGAesWords = aes_lds_words<kGAes>();
+
+template <int C>
+__device__ __forceinline__ u128 aes_keyed(const AesT<C>& a, u128 in, const uint32_t* rk) {
     uint32_t s0 = bswap32(static_cast<uint32_t>(in)) ^ rk[0];
     uint32_t s1 = bswap32(static_cast<uint32_t>(in >> 32)) ^ rk[1];
     uint32_t s2 = bswap32(static_cast<uint32_t>(in >> 64)) ^ rk[2];
@@ -152,15 +148,12 @@ struct Gadget {
     int nblk;         // AES-CTR blocks drawn per element (sum over draws)
     uint64_t layer, sslot, mask;  // PRG stream of this gadget: stream_of(layer, sslot, e, mask)
     int16_t* S;       // scratch: slot s is a chunked label set of kW components ([kW / 8][N][8]) at S + s * kW * N
-    u128* PB;         // payload bank [row][N] (PayDesc rows)
+    u128* PB;         // key-hash scratch of the binary (mod-2) mini gates: [2][N] (k_bin_keys)
     int64_t N;
     int mrs[kMaxMrs]; // MRS base of the sign gadget (per-digit output moduli of the fanned-out approx projections)
-    const int16_t* flut;  // F_FAN: payload values [a0 + i * stride + target] (reduced mod the target modulus)
-    const int* fan;       // F_FAN: target moduli [a1 + target]
-    const int* fbank;     // F_FAN: [a1 + target] 1 + payload bank row of value 0 (k_payloads), 0: computed inline
-    int64_t outputs;      // per element: table entries written (sum over projections of entries x targets)
-    u128* HC;             // [entries][N] key hashes (k_hash -> k_emit)
-    uint8_t* CC;          // [entries][N] key colors
+    u128* BK;             // [bank rows][N] payloads (k_bank -> k_emit)
+    u128* HC;             // [entries][N] key hashes (k_hash -> k_emit), entry = first + color
+    uint16_t* CC;         // [entries][N] the entry index i of that color
 };
 
 // slot s as a chunked label set, and element e's view of it
@@ -197,7 +190,7 @@ __device__ __forceinline__ void add8(uint32_t (&acc)[8], const u32x4a& v) {
 
 // Stage a gadget's small descriptor array (draws / projections) in LDS so the
 // per-thread binary search costs LDS, not dependent global round trips.
-constexpr int kMaxDesc = 224;  // 224 x 72-B Proj (16 KiB) beside the AES image (dev.h)
+constexpr int kMaxDesc = 224;  // 224 x 80-B Proj (17.5 KiB) beside the AES image (dev.h)
 constexpr int kGB = 512;        // threads per block of the AES-bound garbling kernels
 template <class T>
 __device__ __forceinline__ void lds_stage(T* dst, const T* src, int n) {
@@ -207,42 +200,114 @@ __device__ __forceinline__ void lds_stage(T* dst, const T* src, int n) {
     for (int i = threadIdx.x; i < words; i += blockDim.x) d[i] = s[i];
 }
 
-// One thread per (AES-CTR block, element), block-major: the lanes of a wave are
-// consecutive elements drawing the same block, so the binary search is (mostly)
-// wave-uniform and the stores land in neighbouring chunks. Block b of a draw
-// yields ModC::pm consecutive components (Prg::label order) as the base-q
-// digits of the block (DigitStream: one 128-bit long division per chunk of
-// digits).
+constexpr int kTile = 64;
+#ifndef DASH_GG_PB
+#define DASH_GG_PB 512
+#endif
+constexpr int kPB = DASH_GG_PB;  // threads per k_project block (A/B knob)
+
+__device__ __forceinline__ int rfl(int x) { return __builtin_amdgcn_readfirstlane(x); }
+__device__ __forceinline__ uint32_t rflu(uint32_t x) {
+    return static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(x)));
+}
+__device__ __forceinline__ int64_t rfl64(int64_t x) {
+    const uint64_t u = static_cast<uint64_t>(x);
+    const uint64_t lo = rflu(static_cast<uint32_t>(u)), hi = rflu(static_cast<uint32_t>(u >> 32));
+    return static_cast<int64_t>(lo | (hi << 32));
+}
+__device__ __forceinline__ ModC rfl_modc(const ModC& m) {
+    ModC r;
+    r.q = rflu(m.q);
+    r.n = rflu(m.n);
+    r.c = rflu(m.c);
+    r.D = rflu(m.D);
+    r.mD = static_cast<uint64_t>(rfl64(static_cast<int64_t>(m.mD)));
+    r.mq = rflu(m.mq);
+    r.bits = rflu(m.bits);
+    r.dm = rflu(m.dm);
+    r.ds = rflu(m.ds);
+    r.pm = rflu(m.pm);
+    return r;
+}
+__device__ __forceinline__ Proj rfl_proj(const Proj& p) {
+    Proj r;
+    r.in_kind = rfl(p.in_kind);
+    r.in_idx = rfl(p.in_idx);
+    r.pin = rfl(p.pin);
+    r.out_slot = rfl(p.out_slot);
+    r.pout = rfl(p.pout);
+    r.fn = rfl(p.fn);
+    r.a0 = rfl(p.a0);
+    r.a1 = rfl(p.a1);
+    r.a2 = rfl(p.a2);
+    r.outr_kind = rfl(p.outr_kind);
+    r.outr_idx = rfl(p.outr_idx);
+    r.table = rfl(p.table);
+    r.stride = rfl(p.stride);
+    r.off = rfl64(p.off);
+    r.first = rfl64(p.first);
+    r.pay1 = rfl(p.pay1);
+    return r;
+}
+
+// One thread per (draw, element), draw-major: the 64 lanes of a wave are
+// consecutive elements of one draw (uniform modulus, width and counter), each
+// producing its whole label: AES-CTR blocks ctr, ctr+1, ... of its stream,
+// ModC::pm consecutive components (Prg::label order) per block as the base-q
+// digits of the block (DigitStream). Components are gathered 8 at a time in a
+// 128-bit shift register and stored as 16-byte chunks: one coalesced KiB per
+// wave per chunk, and chunk padding past n is written as zeros.
+template <int C>
 __global__ __launch_bounds__(kGB) void k_draw(Ctx c, Gadget g) {
-    __shared__ __attribute__((aligned(16))) uint32_t lds_aes[DASH_AES_LDS_WORDS];
-    __shared__ Draw sd[kMaxDesc];
-    lds_stage(sd, g.draws, g.ndraws);
-    aes_lds_fill(lds_aes, c.te0);
-    const AesCtx aes = aes_ctx(lds_aes, nullptr);
+    __shared__ __attribute__((aligned(16))) uint32_t lds_aes[aes_lds_words<C>()];
+    aes_lds_fill<C>(lds_aes, c.te0);
+    const AesT<C> aes = aes_ctx<C>(lds_aes, nullptr);
     const int64_t N = g.N;
-    const int64_t total = N * g.nblk;
-    for (int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < total;
-         i += static_cast<int64_t>(gridDim.x) * blockDim.x) {
-        const int b = static_cast<int>(i / N);
-        const int64_t e = i - static_cast<int64_t>(b) * N;
-        int lo = 0, hi = g.ndraws - 1;
-        while (lo < hi) {  // last draw with ctr <= b
-            const int mid = (lo + hi + 1) >> 1;
-            if (sd[mid].ctr <= b) lo = mid;
-            else hi = mid - 1;
-        }
-        const Draw d = sd[lo];
-        const ModC m = c.mc[d.q];
-        const int j = static_cast<int>(m.pm) * (b - d.ctr);
-        const int cnt = min(static_cast<int>(m.pm), static_cast<int>(m.n) - j);
+    const int64_t tiles = (N + kTile - 1) / kTile;
+    const int64_t nw = tiles * g.ndraws;
+    const int lane = static_cast<int>(threadIdx.x) & (kTile - 1);
+    const int64_t wpb = kGB / kTile;
+    const int64_t w0 = static_cast<int64_t>(blockIdx.x) * wpb + rfl(static_cast<int>(threadIdx.x) / kTile);
+    const int64_t wstep = static_cast<int64_t>(gridDim.x) * wpb;
+    const int64_t cs = N * kCh;
+    for (int64_t w = w0; w < nw; w += wstep) {
+        const int di = static_cast<int>(w / tiles);
+        const int64_t tile = w - static_cast<int64_t>(di) * tiles;
+        const int64_t e = tile * kTile + lane;
+        const Draw d{rfl(g.draws[di].slot), rfl(g.draws[di].q), rfl(g.draws[di].ctr)};
+        const ModC m = rfl_modc(c.mc[d.q]);
+        const int n = static_cast<int>(m.n), pm = static_cast<int>(m.pm);
+        if (e >= N) continue;
         const uint64_t stream = stream_of(g.layer, g.sslot, static_cast<uint64_t>(e), g.mask);
-        DigitStream ds;
-        ds.init(aes_keyed(aes, (static_cast<u128>(stream) << 64) | static_cast<uint64_t>(b), c.rk));
         int16_t* out = slot_base(g, d.slot) + e * kCh;
-        const int64_t cs = N * kCh;
-        for (int u = 0; u < cnt; ++u) {
-            const int q = j + u;
-            out[(q >> 3) * cs + (q & 7)] = static_cast<int16_t>(ds.next(m));
+        DigitStream ds;
+        u128 acc = 0;  // pending components, the oldest in the low 16 bits once 8 are in
+        int blk = 0, left = 0;
+        for (int q = 0; q < n; ++q) {
+            if (left == 0) {
+                ds.init(aes_keyed(aes, (static_cast<u128>(stream) << 64) | static_cast<uint64_t>(d.ctr + blk), c.rk));
+                ++blk;
+                left = pm;
+            }
+            acc = (acc >> 16) | (static_cast<u128>(ds.next(m)) << 112);
+            --left;
+            if ((q & 7) == 7) {
+                u32x4a v;
+                v[0] = static_cast<uint32_t>(acc);
+                v[1] = static_cast<uint32_t>(acc >> 32);
+                v[2] = static_cast<uint32_t>(acc >> 64);
+                v[3] = static_cast<uint32_t>(acc >> 96);
+                st_chunk(out + (q >> 3) * cs, v);
+            }
+        }
+        if (n & 7) {  // last partial chunk: shift the pending components down, zeros above
+            const u128 last = acc >> (16 * (8 - (n & 7)));
+            u32x4a v;
+            v[0] = static_cast<uint32_t>(last);
+            v[1] = static_cast<uint32_t>(last >> 32);
+            v[2] = static_cast<uint32_t>(last >> 64);
+            v[3] = static_cast<uint32_t>(last >> 96);
+            st_chunk(out + (n >> 3) * cs, v);
         }
     }
 }
@@ -311,57 +376,44 @@ __global__ __launch_bounds__(256) void k_sign_derive(Ctx c, Gadget g, SignSlots 
     slot_sum(g, e, s.sum_slot, s.mrs_slot0, t, k, carry, true, M0);
 }
 
-// digits (a_q + f * b_q) mod m of a per-lane label a and a wave-uniform row b (R_q: components in [0, m)),
-// pushed into cf, 8 per chunk load. The row's chunk is moved to SGPRs (readfirstlane of a uniform load), so it
-// costs no vector registers and its unpacking is scalar work.
-__device__ __forceinline__ void push_row(CompressFwd& cf, LRef a, const int16_t* b, uint32_t f, const ModC& m) {
+// Digits (a_q + f * b_q) mod m, q < m.n, of a per-lane label a and an offset label b, pushed into cf. Chunks
+// are loaded kLd at a time (one memory round trip per 8 kLd components instead of one per 8). BU: b is a
+// wave-uniform row (R_q), moved to SGPRs (readfirstlane), so it costs no vector registers. KEY: f is the key
+// index i = (col - a_0) mod m, computed from the first loaded chunk (R[0] = 1: the key's color is col).
+constexpr int kLd = 4;
+template <bool BU, bool KEY>
+__device__ __forceinline__ void push_lin(CompressFwd& cf, LRef a, LRef b, uint32_t& f, const ModC& m, uint32_t col = 0) {
     const int n = static_cast<int>(m.n);
     const int nc = static_cast<int>(chunks_of(n));
-    for (int c8 = 0; c8 < nc; ++c8) {
-        const u32x4a av = ld_chunk(a, c8);
-        const u32x4a bv = *reinterpret_cast<const u32x4a*>(b + c8 * kCh);
-        uint32_t bs[4];
+    for (int c0 = 0; c0 < nc; c0 += kLd) {
+        u32x4a av[kLd], bv[kLd];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) bs[u] = static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(bv[u])));
-        const int q0 = c8 * 8;
+        for (int h = 0; h < kLd; ++h) {
+            if (c0 + h < nc) {
+                av[h] = ld_chunk(a, c0 + h);
+                bv[h] = ld_chunk(b, c0 + h);
+            }
+        }
+        if (KEY && c0 == 0) {
+            const uint32_t x0 = av[0][0] & 0xffffu;
+            f = col + m.q - x0;
+            if (f >= m.q) f -= m.q;
+        }
 #pragma unroll
-        for (int u = 0; u < 8; ++u) {
-            const uint32_t x = (u & 1) ? (av[u >> 1] >> 16) : (av[u >> 1] & 0xffffu);
-            const uint32_t y = (u & 1) ? (bs[u >> 1] >> 16) : (bs[u >> 1] & 0xffffu);
-            if (q0 + u < n) cf.push(modq(x + f * y, m), m);
+        for (int h = 0; h < kLd; ++h) {
+            if (c0 + h >= nc) break;
+            uint32_t bs[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) bs[u] = BU ? rflu(bv[h][u]) : bv[h][u];
+            const int q0 = (c0 + h) * 8;
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const uint32_t x = (u & 1) ? (av[h][u >> 1] >> 16) : (av[h][u >> 1] & 0xffffu);
+                const uint32_t y = (u & 1) ? (bs[u >> 1] >> 16) : (bs[u >> 1] & 0xffffu);
+                if (q0 + u < n) cf.push(modq(x + f * y, m), m);
+            }
         }
     }
-}
-// the same with a per-lane offset label b (the evaluator half gate's offset is the input label x0)
-__device__ __forceinline__ void push_row2(CompressFwd& cf, LRef a, LRef b, uint32_t f, const ModC& m) {
-    const int n = static_cast<int>(m.n);
-    const int nc = static_cast<int>(chunks_of(n));
-    for (int c8 = 0; c8 < nc; ++c8) {
-        uint32_t a0[8], b0[8];
-        unpack8(ld_chunk(a, c8), a0);
-        unpack8(ld_chunk(b, c8), b0);
-        const int q0 = c8 * 8;
-#pragma unroll
-        for (int u = 0; u < 8; ++u)
-            if (q0 + u < n) cf.push(modq(a0[u] + f * b0[u], m), m);
-    }
-}
-
-// key = x + i*R (mod m), compressed from the least significant digit (R: uniform row)
-__device__ __forceinline__ u128 proj_key(LRef x, const int16_t* R, int i, const ModC& m, uint32_t& color) {
-    CompressFwd kc;
-    kc.init();
-    push_row(kc, x, R, static_cast<uint32_t>(i), m);
-    color = modq(static_cast<uint32_t>(static_cast<uint16_t>(x.p[0]) + i * static_cast<uint16_t>(R[0])), m);
-    return kc.finish();
-}
-
-// payload = o + f*R (mod m), o, f, R in [0, m) (R: uniform row)
-__device__ __forceinline__ u128 proj_payload(LRef o, const int16_t* R, uint32_t f, const ModC& m) {
-    CompressFwd pc;
-    pc.init();
-    push_row(pc, o, R, f, m);
-    return pc.finish();
 }
 
 // one thread per (element, table entry). Element-tiled order: the 64 lanes of
@@ -373,84 +425,40 @@ __device__ __forceinline__ u128 proj_payload(LRef o, const int16_t* R, uint32_t 
 // modulus is scalar work issued beside the vector digits. Labels are chunked
 // component-major: one coalesced 16-byte load per lane covers 8 components;
 // consecutive waves walk the entries of the same 64 elements.
-constexpr int kTile = 64;
-#ifndef DASH_GG_PB
-#define DASH_GG_PB 512
-#endif
-constexpr int kPB = DASH_GG_PB;  // threads per k_project block (A/B knob)
-
-__device__ __forceinline__ int rfl(int x) { return __builtin_amdgcn_readfirstlane(x); }
-__device__ __forceinline__ uint32_t rflu(uint32_t x) {
-    return static_cast<uint32_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(x)));
-}
-__device__ __forceinline__ int64_t rfl64(int64_t x) {
-    const uint64_t u = static_cast<uint64_t>(x);
-    const uint64_t lo = rflu(static_cast<uint32_t>(u)), hi = rflu(static_cast<uint32_t>(u >> 32));
-    return static_cast<int64_t>(lo | (hi << 32));
-}
-__device__ __forceinline__ ModC rfl_modc(const ModC& m) {
-    ModC r;
-    r.q = rflu(m.q);
-    r.n = rflu(m.n);
-    r.c = rflu(m.c);
-    r.D = rflu(m.D);
-    r.mD = static_cast<uint64_t>(rfl64(static_cast<int64_t>(m.mD)));
-    r.mq = rflu(m.mq);
-    r.bits = rflu(m.bits);
-    r.dm = rflu(m.dm);
-    r.ds = rflu(m.ds);
-    r.pm = rflu(m.pm);
-    return r;
-}
-__device__ __forceinline__ Proj rfl_proj(const Proj& p) {
-    Proj r;
-    r.in_kind = rfl(p.in_kind);
-    r.in_idx = rfl(p.in_idx);
-    r.pin = rfl(p.pin);
-    r.out_slot = rfl(p.out_slot);
-    r.pout = rfl(p.pout);
-    r.fn = rfl(p.fn);
-    r.a0 = rfl(p.a0);
-    r.a1 = rfl(p.a1);
-    r.a2 = rfl(p.a2);
-    r.outr_kind = rfl(p.outr_kind);
-    r.outr_idx = rfl(p.outr_idx);
-    r.table = rfl(p.table);
-    r.stride = rfl(p.stride);
-    r.off = rfl64(p.off);
-    r.first = rfl64(p.first);
-    r.pay1 = rfl(p.pay1);
-    r.first_out = rfl64(p.first_out);
-    return r;
-}
-
 // Projections in two passes, so no lane carries a long dependent chain (key
 // loads -> compress -> AES -> payload loads -> compress -> store):
-//   k_hash  one lane per (element, table entry): key = x + i*R, H(compress(key)),
-//           color -> HC / CC [entry][N];
-//   k_emit  one lane per (element, entry, target): payload (inline, or from the
-//           payload bank) + H -> the entry's table slot.
+//   k_hash  one lane per (element, color c of a projection): the entry i whose
+//           key x + i*R has color c (R[0] = 1: i = c - x[0] mod p), its hash
+//           H(compress(key)) and i -> HC / CC [first + c][N];
+//   k_emit  one block per (table, 64-element tile, segment of kSeg table
+//           positions): every lane computes the entry of one element at one
+//           position (payload o + f(i)*R, inline or from the payload bank, + H)
+//           into an LDS image of the tile's row segments, which is then written
+//           out as 64 contiguous runs of kSeg x 16 bytes.
+// Table rows are element-major ([N][row]) and permuted by color, so a wave of
+// consecutive elements at one position writes 64 lines 16 bytes each; the LDS
+// image turns that into full-line stores.
 // Element-tiled order: the 64 lanes of a wavefront are 64 consecutive elements
-// of one tile, all on the SAME work item, so the projection descriptor, i, the
+// of one tile, all on the SAME work item, so the projection descriptor, the
 // label widths (loop trip counts), the moduli and the function are
 // wave-uniform and moved to SGPRs (readfirstlane); labels are chunked
 // component-major, so one coalesced 16-byte load per lane covers 8 components.
-__device__ __forceinline__ int find_proj(const Proj* sp, int n, int64_t r, bool by_out) {
+__device__ __forceinline__ int find_proj(const Proj* sp, int n, int64_t r) {
     int lo = 0, hi = n - 1;
-    while (lo < hi) {  // last projection with first (first_out) <= r (uniform search)
+    while (lo < hi) {  // last projection with first <= r (uniform search)
         const int mid = (lo + hi + 1) >> 1;
-        if (rfl64(by_out ? sp[mid].first_out : sp[mid].first) <= r) lo = mid;
+        if (rfl64(sp[mid].first) <= r) lo = mid;
         else hi = mid - 1;
     }
     return lo;
 }
 
+template <int C>
 __global__ __launch_bounds__(kPB) void k_hash(Ctx c, Gadget g, In in) {
-    __shared__ __attribute__((aligned(16))) uint32_t lds_aes[DASH_AES_LDS_WORDS];
-    __shared__ Proj sp[kMaxDesc];
-    lds_stage(sp, g.projs, g.nprojs);
-    aes_lds_fill(lds_aes, c.te0);
-    const AesCtx aes = aes_ctx(lds_aes, nullptr);
+    __shared__ __attribute__((aligned(16))) uint32_t lds_aes[aes_lds_words<C>()];
+    aes_lds_fill<C>(lds_aes, c.te0);
+    const AesT<C> aes = aes_ctx<C>(lds_aes, nullptr);
+    const Proj* sp = g.projs;  // wave-uniform reads (scalar / broadcast loads)
     const int64_t N = g.N;
     const int64_t tiles = (N + kTile - 1) / kTile;
     const int64_t nw = tiles * g.entries;  // wave work items (tile, entry)
@@ -461,98 +469,275 @@ __global__ __launch_bounds__(kPB) void k_hash(Ctx c, Gadget g, In in) {
     for (int64_t w = w0; w < nw; w += wstep) {
         const int64_t tile = w / g.entries;
         const int64_t r = w - tile * g.entries;
-        const Proj P = rfl_proj(sp[find_proj(sp, g.nprojs, r, false)]);
-        const int i = static_cast<int>(r - P.first);
+        const Proj P = rfl_proj(sp[find_proj(sp, g.nprojs, r)]);
+        const uint32_t col = static_cast<uint32_t>(r - P.first);
         const ModC mi = rfl_modc(c.mc[P.pin]);
         // the last tile's spare lanes recompute element N-1 (uniform control flow) and skip the store
         const int64_t e_raw = tile * kTile + lane;
         const int64_t e = e_raw < N ? e_raw : N - 1;
-        uint32_t color;
-        const u128 H = aes_encrypt(aes, proj_key(label_ref(c, g, in, e, P.in_kind, P.in_idx, P.pin),
-                                                 c.R + static_cast<int64_t>(P.pin) * kW, i, mi, color));
+        const LRef x = label_ref(c, g, in, e, P.in_kind, P.in_idx, P.pin);
+        uint32_t i = 0;
+        CompressFwd kc;
+        kc.init();
+        push_lin<true, true>(kc, x, row_ref(c.R + static_cast<int64_t>(P.pin) * kW), i, mi, col);
+        const u128 H = aes_encrypt(aes, kc.finish());
         if (e_raw < N) {
             g.HC[r * N + e] = H;
-            g.CC[r * N + e] = static_cast<uint8_t>(color);
+            g.CC[r * N + e] = static_cast<uint16_t>(i);
         }
     }
 }
 
-__global__ __launch_bounds__(256) void k_emit(Ctx c, Gadget g, In in, Tables tb) {
-    __shared__ Proj sp[kMaxDesc];
-    lds_stage(sp, g.projs, g.nprojs);
-    __syncthreads();
+// Key hashes, one wave per (64-element tile, hash job), a job = up to kHJ consecutive colors of one
+// projection: the input label comes from HBM once, the job's later colors re-read it from the CU's L1
+// (a wave's label is <= 16 KiB), and the waves of a block are few jobs, not few entries. (Holding the label
+// in registers instead spilled: 8 chunks x 16 B per lane plus the unrolled compress exceed 128 VGPRs.)
+constexpr int kHJ = 8;  // colors per hash job
+struct HashJob {
+    int proj, c0;
+};
+template <int C>
+__global__ __launch_bounds__(kPB, 4) void k_hash_jobs(Ctx c, Gadget g, In in, const HashJob* jobs, int njobs) {
+    __shared__ __attribute__((aligned(16))) uint32_t lds_aes[aes_lds_words<C>()];
+    aes_lds_fill<C>(lds_aes, c.te0);
+    const AesT<C> aes = aes_ctx<C>(lds_aes, nullptr);
     const int64_t N = g.N;
     const int64_t tiles = (N + kTile - 1) / kTile;
-    const int64_t nw = tiles * g.outputs;  // wave work items (tile, output)
+    const int64_t nw = tiles * njobs;
     const int lane = static_cast<int>(threadIdx.x) & (kTile - 1);
-    const int64_t wpb = blockDim.x / kTile;
+    const int64_t wpb = kPB / kTile;
     const int64_t w0 = static_cast<int64_t>(blockIdx.x) * wpb + rfl(static_cast<int>(threadIdx.x) / kTile);
     const int64_t wstep = static_cast<int64_t>(gridDim.x) * wpb;
     for (int64_t w = w0; w < nw; w += wstep) {
-        const int64_t tile = w / g.outputs;
-        const int64_t o = w - tile * g.outputs;
-        const Proj P = rfl_proj(sp[find_proj(sp, g.nprojs, o, true)]);
-        const bool fan = P.fn == F_LUT || P.fn == F_FAN;
-        const int t = fan ? P.stride : 1;
-        const int local = static_cast<int>(o - P.first_out);
-        const int i = local / t, d = local - i * t;
-        const int64_t r = P.first + i;
+        const int64_t tile = w / njobs;
+        const int jb = static_cast<int>(w - tile * njobs);
+        const int pi = rfl(jobs[jb].proj), c0 = rfl(jobs[jb].c0);
+        const Proj P = rfl_proj(g.projs[pi]);
+        const ModC mi = rfl_modc(c.mc[P.pin]);
+        const uint32_t p = static_cast<uint32_t>(P.pin);
+        const int c1 = min(P.pin, c0 + kHJ);
         const int64_t e_raw = tile * kTile + lane;
         const int64_t e = e_raw < N ? e_raw : N - 1;
-        const u128 H = g.HC[r * N + e];
-        const uint32_t color = g.CC[r * N + e];
-        u128 pay;
-        if (P.fn == F_LUT) {
-            // approx fan-out: digit d's payload mrs0_slot + d + lut[j][i][d] * R_{m_d}
-            const int pout = rfl(g.mrs[d]);
-            int64_t cm = c.lut[c.lut_off[P.a0] + i * t + d] % pout;
-            if (cm < 0) cm += pout;
-            pay = proj_payload(slot_ref(g, P.out_slot + d, e), c.R + static_cast<int64_t>(pout) * kW,
-                               static_cast<uint32_t>(cm), rfl_modc(c.mc[pout]));
-        } else if (P.fn == F_FAN) {
-            // generic fan-out: target d writes slot out_slot + d, modulus fan[a1 + d], value flut[a0 + i * t + d]
-            const uint32_t cm = static_cast<uint32_t>(rfl(g.flut[P.a0 + i * t + d]));
-            const int bk = g.fbank ? rfl(g.fbank[P.a1 + d]) : 0;
-            if (bk) {
-                // few distinct values (e.g. the rescale's final projection: T = 2^(l+1) entries, p_j values)
-                pay = g.PB[static_cast<int64_t>(bk - 1 + static_cast<int>(cm)) * N + e];
-            } else {
-                const int pout = rfl(g.fan[P.a1 + d]);
-                pay = proj_payload(slot_ref(g, P.out_slot + d, e), c.R + static_cast<int64_t>(pout) * kW, cm,
-                                   rfl_modc(c.mc[pout]));
-            }
-        } else if (P.pay1 > 0) {
-            // few distinct payloads: precomputed per element by k_payloads
-            const int idx = P.fn == F_SIGN ? (i < P.a0 ? 1 : 0) : i / P.a0;  // F_SIGN: 0 lower / 1 upper; F_DIV(MOD): i / m
-            pay = g.PB[static_cast<int64_t>(P.pay1 - 1 + idx) * N + e];
-        } else {
-            int64_t f;
-            switch (P.fn) {
-                case F_DIV: f = i / P.a0; break;
-                case F_DIVMOD: f = (i / P.a0) % P.a1; break;
-                case F_SIGN: f = i < P.a0 ? P.a2 : P.a1; break;  // a0 = half, a1 = lower, a2 = upper
-                case F_MULR: f = static_cast<int64_t>(i) * in.p[P.a0][e * in.es[P.a0]]; break;
-                case F_NEGR: f = -(static_cast<int64_t>(i) + in.p[P.a0][e * in.es[P.a0]]); break;
-                default: f = i;
-            }
-            int64_t cm = f % P.pout;
-            if (cm < 0) cm += P.pout;
-            const ModC mo = rfl_modc(c.mc[P.pout]);
-            if (P.outr_kind == R_BANK) {
-                pay = proj_payload(slot_ref(g, P.out_slot, e), c.R + static_cast<int64_t>(P.pout) * kW,
-                                   static_cast<uint32_t>(cm), mo);
-            } else {
-                CompressFwd pc;
-                pc.init();
-                push_row2(pc, slot_ref(g, P.out_slot, e), label_ref(c, g, in, e, S_INPUT, P.outr_idx, 0),
-                          static_cast<uint32_t>(cm), mo);
-                pay = pc.finish();
+        const LRef x = label_ref(c, g, in, e, P.in_kind, P.in_idx, P.pin);
+        const int16_t* R = c.R + static_cast<int64_t>(P.pin) * kW;
+        for (int col = c0; col < c1; ++col) {
+            uint32_t i = 0;
+            CompressFwd kc;
+            kc.init();
+            push_lin<true, true>(kc, x, row_ref(R), i, mi, static_cast<uint32_t>(col));
+            const u128 H = aes_encrypt(aes, kc.finish());
+            if (e_raw < N) {
+                g.HC[(P.first + col) * N + e] = H;
+                g.CC[(P.first + col) * N + e] = static_cast<uint16_t>(i);
             }
         }
-        if (e_raw < N) {
-            const int64_t slot = fan ? static_cast<int64_t>(color) * t + d : static_cast<int64_t>(color) * P.stride;
-            tb.t[P.table][e * tb.row[P.table] + P.off + slot] = pay + H;
+    }
+}
+
+// LDS AES image copies of the AES-bound kernels (A/B knob DASH_GG_AES_COPIES = 16 | 32): 32 copies are
+// bank-conflict free (64 KiB: 2 blocks per CU), 16 copies halve the image (2-way conflicts, more blocks)
+inline int gg_aes_copies() {
+    static const int v = [] {
+        const char* e = std::getenv("DASH_GG_AES_COPIES");
+        return e && std::atoi(e) == 16 ? 16 : 32;
+    }();
+    return v;
+}
+inline auto draw_kernel() { return gg_aes_copies() == 16 ? k_draw<16> : k_draw<32>; }
+inline auto hash_kernel() { return gg_aes_copies() == 16 ? k_hash<16> : k_hash<32>; }
+inline auto hash_jobs_kernel() { return gg_aes_copies() == 16 ? k_hash_jobs<16> : k_hash_jobs<32>; }
+// DASH_GG_HASH=entry: one wave per (tile, entry) (k_hash); default: per (tile, hash job) (k_hash_jobs)
+inline bool gg_hash_jobs() {
+    static const bool v = [] {
+        const char* e = std::getenv("DASH_GG_HASH");
+        return !(e && std::string(e) == "entry");
+    }();
+    return v;
+}
+
+// ---- k_emit: table rows assembled per tile of elements in LDS
+// A table entry is T[color] = payload + H, payload = o + v * R (mod pout) with
+// v = f(i, d) taking few distinct values per (projection, target d), so every
+// distinct payload of an element is computed once into a bank row, and an
+// entry is two LDS lookups and an add. A k_emit block owns a scope (a
+// contiguous range of table positions covering whole projections) for te
+// consecutive elements:
+//   1a  stage the scope's key hashes and entry indices (HC / CC rows, coalesced)
+//   1b  compute the scope's bank payloads (lanes: consecutive elements of a bank row)
+//   2   one lane per (element, position): bank row of (i, d) + H -> the table,
+//       te contiguous runs of span x 16 bytes (full-line stores)
+constexpr uint32_t kHole = 0xffffffffu;  // position map: no projection writes here
+constexpr int kEB = 256;                 // k_emit threads
+struct BankRow {
+    int slot, pout, v, res;  // payload = slot label + v * (res < 0 ? R_pout : input label of residue res) mod pout
+};
+struct EProj {
+    int first;  // first key-hash entry (HC / CC row)
+    int pay1;   // element-independent f: bix base (bank row of (i, d) at bix[pay1 + i * t + d]);
+                // F_MULR / F_NEGR: scope-relative bank row of v = 0 (rows v = 0 .. pout - 1)
+    int fn, t, res, pout;
+};
+struct Scope {
+    int table, tsh;  // table id; te = 1 << tsh elements per block
+    int a, span;     // table positions [a, a + span)
+    int r0, ne;      // key-hash entries [r0, r0 + ne)
+    int b0, nb;      // bank rows [b0, b0 + nb)
+    int bx0, nbx;    // bank indices [bx0, bx0 + nbx) of its element-independent projections
+    int64_t blk0;    // first block of the scope
+};
+struct Emit {
+    const Scope* sc;
+    int nsc, nep;
+    int64_t blocks;
+    const uint32_t* map;  // table t's positions at map + map_off[t]: projection << 24 | color << 12 | target
+    int64_t map_off[8];
+    const uint16_t* bix;
+    const BankRow* rows;
+    const EProj* ep;
+};
+
+// Bank payloads: one wave per (64-element tile, bank row), lanes = consecutive elements (the row's slot,
+// modulus and offset kind are wave-uniform): BK[row][N] = slot label + v * offset (mod pout), compressed.
+__global__ __launch_bounds__(256) void k_bank(Ctx c, Gadget g, In in, const BankRow* rows, int nrows) {
+    const int64_t N = g.N;
+    const int64_t tiles = (N + kTile - 1) / kTile;
+    const int64_t nw = tiles * nrows;
+    const int lane = static_cast<int>(threadIdx.x) & (kTile - 1);
+    const int64_t wpb = 256 / kTile;
+    const int64_t w0 = static_cast<int64_t>(blockIdx.x) * wpb + rfl(static_cast<int>(threadIdx.x) / kTile);
+    const int64_t wstep = static_cast<int64_t>(gridDim.x) * wpb;
+    for (int64_t w = w0; w < nw; w += wstep) {
+        // tile-major: the rows of one slot label (a target's values) run in neighbouring waves, so the label's
+        // re-reads hit L2 (row-major order re-fetched it from HBM for every value)
+        const int64_t tile = w / nrows;
+        const int row = static_cast<int>(w - tile * nrows);
+        const int slot = rfl(rows[row].slot), pout = rfl(rows[row].pout), res = rfl(rows[row].res);
+        uint32_t f = rflu(static_cast<uint32_t>(rows[row].v));
+        const ModC mo = rfl_modc(c.mc[pout]);
+        const int64_t e_raw = tile * kTile + lane;
+        const int64_t e = e_raw < N ? e_raw : N - 1;
+        CompressFwd pc;
+        pc.init();
+        if (res < 0) push_lin<true, false>(pc, slot_ref(g, slot, e), row_ref(c.R + static_cast<int64_t>(pout) * kW), f, mo);
+        else push_lin<false, false>(pc, slot_ref(g, slot, e), LRef{in.p[res] + e * in.es[res], in.cs[res]}, f, mo);
+        if (e_raw < N) g.BK[static_cast<int64_t>(row) * N + e] = pc.finish();
+    }
+}
+
+__global__ __launch_bounds__(kEB) void k_emit(Ctx c, Gadget g, In in, Tables tb, Emit em) {
+    extern __shared__ __attribute__((aligned(16))) uint32_t dyn[];
+    __shared__ EProj sep[kMaxDesc];
+    lds_stage(sep, em.ep, em.nep);
+    __syncthreads();
+    const int64_t N = g.N;
+    for (int64_t b = blockIdx.x; b < em.blocks; b += gridDim.x) {
+        int lo = 0, hi = em.nsc - 1;
+        while (lo < hi) {  // last scope with blk0 <= b (uniform)
+            const int mid = (lo + hi + 1) >> 1;
+            if (rfl64(em.sc[mid].blk0) <= b) lo = mid;
+            else hi = mid - 1;
         }
+        const Scope S = em.sc[lo];
+        const int tsh = rfl(S.tsh), te = 1 << tsh;
+        const int64_t e0 = (b - rfl64(S.blk0)) << tsh;
+        const int ne = rfl(S.ne), nb = rfl(S.nb), r0 = rfl(S.r0), span = rfl(S.span), a = rfl(S.a);
+        // LDS rows of te + 1 entries: rows of different hashes / payloads start 4 banks apart, so the lanes of
+        // a ds_read_b128 group (consecutive positions: different rows, one element) hit distinct banks
+        const int te1 = te + 1;
+        const int bx0 = rfl(S.bx0), nbx = rfl(S.nbx);
+        u128* HCL = reinterpret_cast<u128*>(dyn);
+        u128* PBL = HCL + ne * te1;
+        uint16_t* CCL = reinterpret_cast<uint16_t*>(PBL + nb * te1);
+        uint32_t* MAP = reinterpret_cast<uint32_t*>(CCL + ((ne * te1 + 1) & ~1));
+        uint16_t* BIX = reinterpret_cast<uint16_t*>(MAP + span);
+        const int table = rfl(S.table);
+        // 1: the tile's key hashes, entry indices and bank payloads (coalesced rows of te elements, kUn loads in
+        // flight per thread), the scope's position map and bank indices
+        constexpr int kUn = 4;
+        const int b0 = rfl(S.b0);
+        const int nh = ne << tsh, nall = (ne + nb) << tsh;
+        for (int x0 = threadIdx.x; x0 < nall; x0 += kUn * kEB) {
+            u128 hv[kUn];
+            uint16_t cv[kUn];
+#pragma unroll
+            for (int u = 0; u < kUn; ++u) {
+                const int x = x0 + u * kEB;
+                if (x >= nall) continue;
+                const int rr = x >> tsh;
+                const int64_t e = min(e0 + (x & (te - 1)), N - 1);
+                if (x < nh) {
+                    hv[u] = g.HC[(r0 + rr) * N + e];
+                    cv[u] = g.CC[(r0 + rr) * N + e];
+                } else {
+                    hv[u] = g.BK[(b0 + rr - ne) * N + e];
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < kUn; ++u) {
+                const int x = x0 + u * kEB;
+                if (x >= nall) continue;
+                const int rr = x >> tsh, el = x & (te - 1);
+                if (x < nh) {
+                    HCL[rr * te1 + el] = hv[u];
+                    CCL[rr * te1 + el] = cv[u];
+                } else {
+                    PBL[(rr - ne) * te1 + el] = hv[u];
+                }
+            }
+        }
+        const uint32_t* gmap = em.map + em.map_off[table] + a;
+        for (int x = threadIdx.x; x < span; x += kEB) MAP[x] = gmap[x];
+        for (int x = threadIdx.x; x < nbx; x += kEB) BIX[x] = em.bix[bx0 + x];
+        __syncthreads();
+        // 2: entries, position-fastest (contiguous per element), kUn independent LDS-only chains per thread
+        u128* T = tb.t[table];
+        const int64_t row = tb.row[table];
+        const int total = span * te;
+        const float inv_span = 1.0f / static_cast<float>(span);
+        for (int x0 = threadIdx.x; x0 < total; x0 += kUn * kEB) {
+            uint32_t mm[kUn];
+            int el[kUn], pp[kUn];
+#pragma unroll
+            for (int u = 0; u < kUn; ++u) {
+                const int x = x0 + u * kEB;
+                int q = static_cast<int>(static_cast<float>(x) * inv_span);
+                if (q * span > x) --q;
+                else if ((q + 1) * span <= x) ++q;
+                el[u] = q;
+                pp[u] = x - q * span;
+                mm[u] = (x < total && e0 + q < N) ? MAP[pp[u]] : kHole;
+            }
+            u128 v[kUn];
+#pragma unroll
+            for (int u = 0; u < kUn; ++u) {
+                if (mm[u] == kHole) continue;
+                const EProj P = sep[mm[u] >> 24];
+                const int rr = P.first + static_cast<int>((mm[u] >> 12) & 0xfffu) - r0;
+                const int i = CCL[rr * te1 + el[u]];
+                int br;
+                if (P.fn == F_MULR || P.fn == F_NEGR) {
+                    const int64_t e = e0 + el[u];
+                    const int xr = in.p[P.res][e * in.es[P.res]];
+                    int w = P.fn == F_MULR ? (i * xr) % P.pout : -(i + xr) % P.pout;
+                    if (w < 0) w += P.pout;
+                    br = P.pay1 + w;
+                } else {
+                    br = BIX[P.pay1 - bx0 + i * P.t + static_cast<int>(mm[u] & 0xfffu)];
+                }
+                v[u] = PBL[br * te1 + el[u]] + HCL[rr * te1 + el[u]];
+            }
+#pragma unroll
+            for (int u = 0; u < kUn; ++u) {
+                if (mm[u] == kHole) continue;
+                u32x4a w;
+                w[0] = static_cast<uint32_t>(v[u]);
+                w[1] = static_cast<uint32_t>(v[u] >> 32);
+                w[2] = static_cast<uint32_t>(v[u] >> 64);
+                w[3] = static_cast<uint32_t>(v[u] >> 96);
+                *reinterpret_cast<u32x4a*>(T + (e0 + el[u]) * row + a + pp[u]) = w;
+            }
+        }
+        __syncthreads();
     }
 }
 
@@ -560,6 +745,7 @@ __global__ __launch_bounds__(256) void k_emit(Ctx c, Gadget g, In in, Tables tb)
 // operations, one thread per element, 8 components per load: key base labels
 // K_i = L_i - sum_{l<i} P_{l,i}, the mod-T accumulator r = sum_i P_{i,T}, then
 // the output base labels (in place) Y_0 = F_0, Y_j = S^-1 L_j + F_j.
+constexpr int kMaxY = 160;  // (residue, chunk) work items: sum of chunks_of(n_j) over residues + accumulator
 struct MrsG {
     int k, T;
     int crt[kMaxRes], sinv[kMaxRes];
@@ -568,56 +754,70 @@ struct MrsG {
     int tslot[kMaxRes];         // slot of digit i's T target
     int key0, acc, fin0;
     int16_t* L[kMaxRes];  // chunked [n_j / 8][N][8], updated in place
+    int yj[kMaxY], yc[kMaxY];  // k_mrs_derive grid y -> (residue j (k: accumulator), chunk)
 };
 
-// grid (elements, k + 1): y = j < k derives residue j, y = k the accumulator
+// grid (elements, work items y): item y = (residue j, chunk c8), j = k the accumulator; one chunk per thread,
+// so all of a thread's loads are one memory round trip (a chunk loop paid one per chunk)
 __global__ __launch_bounds__(256) void k_mrs_derive(Ctx c, Gadget g, MrsG a) {
     const int64_t e = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
     if (e >= g.N) return;
     const int64_t cs = g.N * kCh;
     const int k = a.k;
-    const int y = blockIdx.y;
-    if (y < k) {
-        const int j = y;
+    const int j = a.yj[blockIdx.y], c8 = a.yc[blockIdx.y];
+    if (j < k) {
         const int p = a.crt[j];
         const ModC m = c.mc[p];
-        const int nc = static_cast<int>(chunks_of(static_cast<int>(m.n))), ns = a.nsub[j];
+        const int ns = a.nsub[j];
         int16_t* Lj = a.L[j] + e * kCh;
         const LRef K = slot_ref(g, a.key0 + j, e), F = slot_ref(g, a.fin0 + j, e);
-        for (int c8 = 0; c8 < nc; ++c8) {
-            uint32_t x[8];
-            unpack8(*reinterpret_cast<const u32x4a*>(Lj + c8 * cs), x);
-            // key: L_j - sum of the digit payload labels aimed at residue j
-            uint32_t kv[8];
+        const u32x4a xv = *reinterpret_cast<const u32x4a*>(Lj + c8 * cs);
+        const u32x4a fvv = ld_chunk(F, c8);
+        uint32_t x[8];
+        unpack8(xv, x);
+        // key: L_j - sum of the digit payload labels aimed at residue j (loads batched kLd at a time)
+        uint32_t kv[8];
 #pragma unroll
-            for (int u = 0; u < 8; ++u) kv[u] = x[u] + static_cast<uint32_t>(p) * static_cast<uint32_t>(ns);
-            for (int l = 0; l < ns; ++l) {
-                uint32_t sv[8];
-                unpack8(ld_chunk(slot_ref(g, a.sub[j][l], e), c8), sv);
+        for (int u = 0; u < 8; ++u) kv[u] = x[u] + static_cast<uint32_t>(p) * static_cast<uint32_t>(ns);
+        for (int l0 = 0; l0 < ns; l0 += kLd) {
+            u32x4a sv[kLd];
 #pragma unroll
-                for (int u = 0; u < 8; ++u) kv[u] -= sv[u];
+            for (int h = 0; h < kLd; ++h)
+                if (l0 + h < ns) sv[h] = ld_chunk(slot_ref(g, a.sub[j][l0 + h], e), c8);
+#pragma unroll
+            for (int h = 0; h < kLd; ++h) {
+                if (l0 + h >= ns) break;
+                uint32_t t[8];
+                unpack8(sv[h], t);
+#pragma unroll
+                for (int u = 0; u < 8; ++u) kv[u] -= t[u];
             }
-#pragma unroll
-            for (int u = 0; u < 8; ++u) kv[u] = modq(kv[u], m);
-            st_chunk(const_cast<int16_t*>(K.p) + c8 * K.cs, pack8(kv));
-            // output base label (in place): Y_0 = F_0, Y_j = S^-1 L_j + F_j (chunk padding stays in the block)
-            uint32_t fv[8], yv[8];
-            unpack8(ld_chunk(F, c8), fv);
-#pragma unroll
-            for (int u = 0; u < 8; ++u) yv[u] = j == 0 ? fv[u] : modq(x[u] * static_cast<uint32_t>(a.sinv[j]) + fv[u], m);
-            st_chunk(Lj + c8 * cs, pack8(yv));
         }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) kv[u] = modq(kv[u], m);
+        st_chunk(const_cast<int16_t*>(K.p) + c8 * K.cs, pack8(kv));
+        // output base label (in place): Y_0 = F_0, Y_j = S^-1 L_j + F_j (chunk padding stays in the block)
+        uint32_t fv[8], yv[8];
+        unpack8(fvv, fv);
+#pragma unroll
+        for (int u = 0; u < 8; ++u) yv[u] = j == 0 ? fv[u] : modq(x[u] * static_cast<uint32_t>(a.sinv[j]) + fv[u], m);
+        st_chunk(Lj + c8 * cs, pack8(yv));
         return;
     }
-    const int ncT = static_cast<int>(chunks_of(static_cast<int>(c.mc[a.T].n)));
     const LRef A = slot_ref(g, a.acc, e);
-    for (int c8 = 0; c8 < ncT; ++c8) {
-        uint32_t av[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-        for (int l = 0; l < k; ++l) add8(av, ld_chunk(slot_ref(g, a.tslot[l], e), c8));
+    uint32_t av[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (int l0 = 0; l0 < k; l0 += kLd) {
+        u32x4a tv[kLd];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) av[u] &= static_cast<uint32_t>(a.T - 1);
-        st_chunk(const_cast<int16_t*>(A.p) + c8 * A.cs, pack8(av));
+        for (int h = 0; h < kLd; ++h)
+            if (l0 + h < k) tv[h] = ld_chunk(slot_ref(g, a.tslot[l0 + h], e), c8);
+#pragma unroll
+        for (int h = 0; h < kLd; ++h)
+            if (l0 + h < k) add8(av, tv[h]);
     }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) av[u] &= static_cast<uint32_t>(a.T - 1);
+    st_chunk(const_cast<int16_t*>(A.p) + c8 * A.cs, pack8(av));
 }
 
 // Mixed-radix sign (gadgets.h SignMrsPlan): key base labels
@@ -655,23 +855,6 @@ __global__ __launch_bounds__(256) void k_mrs_sign_derive(Ctx c, Gadget g, In in,
             for (int u = 0; u < 8; ++u) kv[u] = modq(kv[u], m);
             st_chunk(const_cast<int16_t*>(K.p) + c8 * K.cs, pack8(kv));
         }
-    }
-}
-
-// Payload bank: one thread per (row, element), rows = PayDesc entries.
-__global__ __launch_bounds__(256) void k_payloads(Ctx c, Gadget g, const PayDesc* pd, int npd) {
-    const int64_t total = g.N * npd;
-    for (int64_t x = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; x < total;
-         x += static_cast<int64_t>(gridDim.x) * blockDim.x) {
-        const int r = static_cast<int>(x / g.N);
-        const int64_t e = x - static_cast<int64_t>(r) * g.N;
-        const PayDesc d = pd[r];
-        // a wave may straddle two rows (N is not a multiple of 64): the offset row is per lane here
-        CompressFwd pc;
-        pc.init();
-        push_row2(pc, slot_ref(g, d.out_slot, e), row_ref(c.R + static_cast<int64_t>(d.pout) * kW),
-                  static_cast<uint32_t>(d.f), c.mc[d.pout]);
-        g.PB[x] = pc.finish();
     }
 }
 
@@ -743,9 +926,9 @@ __device__ __forceinline__ uint32_t bits8(const u32x4a& v) {
     return b;
 }
 __global__ __launch_bounds__(kGB) void k_bin_keys(Ctx c, const int16_t* x, const int16_t* add, u128* hk, int64_t N) {
-    __shared__ __attribute__((aligned(16))) uint32_t lds_aes[DASH_AES_LDS_WORDS];
-    aes_lds_fill(lds_aes, c.te0);
-    const AesCtx aes = aes_ctx(lds_aes, nullptr);
+    __shared__ __attribute__((aligned(16))) uint32_t lds_aes[kGAesWords];
+    aes_lds_fill<kGAes>(lds_aes, c.te0);
+    const GAes aes = aes_ctx<kGAes>(lds_aes, nullptr);
     const LRef R2 = row_ref(c.R + 2 * kW);
     uint32_t rb[4] = {0, 0, 0, 0}, ab[4] = {0, 0, 0, 0};
 #pragma unroll
@@ -779,9 +962,9 @@ __global__ __launch_bounds__(kGB) void k_bin_keys(Ctx c, const int16_t* x, const
 // written here: the sign gadget reads Z_2 for residue 0 directly (In with a
 // zero element stride) and k_rescale_post_g overwrites L_0 afterwards.
 __global__ __launch_bounds__(kGB) void k_rescale_pre(Ctx c, RsArgs a, Tables tb, const u128* hk, int64_t N) {
-    __shared__ __attribute__((aligned(16))) uint32_t lds_aes[DASH_AES_LDS_WORDS];
-    aes_lds_fill(lds_aes, c.te0);
-    const AesCtx aes = aes_ctx(lds_aes, nullptr);
+    __shared__ __attribute__((aligned(16))) uint32_t lds_aes[kGAesWords];
+    aes_lds_fill<kGAes>(lds_aes, c.te0);
+    const GAes aes = aes_ctx<kGAes>(lds_aes, nullptr);
     const int j = 1 + static_cast<int>(blockIdx.y);
     const int p = a.crt[j];
     const ModC mj = c.mc[p];
@@ -847,29 +1030,12 @@ __global__ __launch_bounds__(256) void k_rescale_post_g(Ctx c, RsArgs a, Gadget 
 struct SignLayout {
     std::vector<Draw> draws;
     std::vector<Proj> projs;
-    std::vector<PayDesc> pays;
     int fan[kMaxMrs] = {};  // output modulus of the approx fan-out per digit
     SignSlots ss{};
     int nslots = 0;
     int out_slot0 = 0;
     int64_t entries = 0;
 };
-
-// Route projection p's payloads through the payload bank: row idx < nidx holds
-// out_slot + f(idx) * R_pout.
-template <class F>
-Proj banked(SignLayout& L, Proj p, int nidx, F&& f) {
-    p.pay1 = static_cast<int>(L.pays.size()) + 1;
-    for (int idx = 0; idx < nidx; ++idx) {
-        int64_t cm = static_cast<int64_t>(f(idx)) % p.pout;
-        if (cm < 0) cm += p.pout;
-        L.pays.push_back(PayDesc{p.out_slot, p.pout, static_cast<int>(cm)});
-    }
-    return p;
-}
-inline Proj banked_sign(SignLayout& L, const Proj& p) {  // F_SIGN: row 0 = lower (a1), row 1 = upper (a2)
-    return banked(L, p, 2, [&](int idx) { return idx ? p.a2 : p.a1; });
-}
 
 // Fused construction (gadgets.cpp sign_garble_fused): digit labels, carries, outputs.
 SignLayout sign_layout_fused(const SignPlan& P, int extra_slots) {
@@ -921,13 +1087,13 @@ SignLayout sign_layout_fused(const SignPlan& P, int extra_slots) {
         const int mo = P.digit_mod(d);
         const Proj cp{S_SLOT, sum2_0 + q, mo, newc0 + q, P.carry_mod(d), F_DIVMOD, P.mrs[d], P.mrs[d - 1], 0, R_BANK, 0,
                       2, 1, c2, 0};
-        add(banked(L, cp, (mo + cp.a0 - 1) / cp.a0, [&](int idx) { return idx % cp.a1; }));
+        add(cp);
         c2 += mo;
     }
     const int m0 = P.mrs[0];
     for (size_t o = 0; o < P.out_mod.size(); ++o)
-        add(banked_sign(L, Proj{S_SLOT, sum_slot, m0, L.out_slot0 + static_cast<int>(o), P.out_mod[o], F_SIGN, m0 / 2,
-                                P.lower, P.upper, R_BANK, 0, 3, 1, static_cast<int64_t>(o) * m0, 0}));
+        add(Proj{S_SLOT, sum_slot, m0, L.out_slot0 + static_cast<int>(o), P.out_mod[o], F_SIGN, m0 / 2, P.lower, P.upper,
+                 R_BANK, 0, 3, 1, static_cast<int64_t>(o) * m0, 0});
     L.entries = first;
     return L;
 }
@@ -1012,15 +1178,14 @@ SignLayout sign_layout(const SignPlan& P, int extra_slots) {
             c1 += m;
             add(p);
         }
-        add(banked(L, Proj{S_SLOT, sum2_0 + q, mo, bases0 + q * stride_q + (k + 1), P.mrs[d - 1], F_DIV, m, 0, 0, R_BANK,
-                           0, 2, 1, c2, 0},
-                   (mo + m - 1) / m, [](int idx) { return idx; }));
+        add(Proj{S_SLOT, sum2_0 + q, mo, bases0 + q * stride_q + (k + 1), P.mrs[d - 1], F_DIV, m, 0, 0, R_BANK, 0, 2, 1,
+                 c2, 0});
         c2 += mo;
     }
     const int m0 = P.mrs[0];
     for (size_t o = 0; o < P.out_mod.size(); ++o)
-        add(banked_sign(L, Proj{S_SLOT, sum_slot, m0, L.out_slot0 + static_cast<int>(o), P.out_mod[o], F_SIGN, m0 / 2,
-                                P.lower, P.upper, R_BANK, 0, 3, 1, static_cast<int64_t>(o) * m0, 0}));
+        add(Proj{S_SLOT, sum_slot, m0, L.out_slot0 + static_cast<int>(o), P.out_mod[o], F_SIGN, m0 / 2, P.lower, P.upper,
+                 R_BANK, 0, 3, 1, static_cast<int64_t>(o) * m0, 0});
     L.entries = first;
     return L;
 }
@@ -1239,6 +1404,12 @@ struct DevTable {
     }
 };
 
+// k_draw grid: one lane per (draw, element), elements padded to whole waves
+unsigned draw_grid(const gg::Gadget& g) {
+    const int64_t lanes = (g.N + gg::kTile - 1) / gg::kTile * gg::kTile * g.ndraws;
+    return blocks_for(lanes, gg::kGB, 16384);
+}
+
 // AES-CTR blocks per element: draws are laid out back to back in counter order
 int draw_blocks(const std::vector<gg::Draw>& d) {
     if (d.empty()) return 0;
@@ -1252,32 +1423,223 @@ void check_desc(const gg::Gadget& g) {
 
 // run the three sign-gadget passes for N elements with input labels `in`
 // key-hash scratch of the calling thread's garbling context (DevCtx, grow-only): [entries][N] hashes + colors
-std::pair<u128*, uint8_t*> hc_scratch(size_t entries, int64_t N);
+std::pair<u128*, uint16_t*> hc_scratch(size_t entries, int64_t N);
+u128* bank_scratch(size_t rows, int64_t N);
 
-// The projections of a gadget: output indices (entry x target) assigned, descriptors staged, then k_hash and
-// k_emit on the garbling stream. g.draws / labels / payload bank must be ready (same stream).
-void project(const gg::Ctx& c, gg::Gadget& g, const gg::In& in, const gg::Tables& tb, std::vector<gg::Proj> pr) {
-    int64_t outs = 0;
-    for (auto& p : pr) {
-        p.first_out = outs;
-        const bool fan = p.fn == gg::F_LUT || p.fn == gg::F_FAN;
-        outs += static_cast<int64_t>(p.pin) * (fan ? p.stride : 1);
+// Host-side function data of a projection set (the value f(i, d) of every entry): k_emit reads bank rows
+// and bank indices built from it here, so none of it is needed on the device.
+struct ProjFns {
+    const std::vector<int16_t>* flut = nullptr;  // F_FAN values [a0 + i * t + d]
+    const std::vector<int>* fan = nullptr;       // F_FAN target moduli [a1 + d]
+    const std::vector<int16_t>* lut = nullptr;   // F_LUT approx lookup, residue j's [p][t] at lut_off[j]
+    const int* lut_off = nullptr;
+};
+
+constexpr size_t kEmitLds = 48 << 10;  // k_emit dynamic LDS budget per block
+
+// The projections of a gadget: k_hash (one key hash per (element, color)), then k_emit over scopes. Host
+// preparation, cached by content per gadget structure (dconst): the per-table position maps, the scopes
+// (contiguous position ranges covering whole projections, te elements per block within the LDS budget),
+// the deduplicated bank rows of every scope and the (i, d) -> bank row index of every projection.
+// g.draws / label slots must be ready (same stream).
+void project(const gg::Ctx& c, gg::Gadget& g, const gg::In& in, const gg::Tables& tb, const std::vector<gg::Proj>& pr,
+             const ProjFns& fx = ProjFns()) {
+    DASH_CHECK(!pr.empty() && pr.size() <= 255, "gpu garbler: projection count outside [1, 255]");
+    const int np = static_cast<int>(pr.size());
+    auto is_fan = [](const gg::Proj& p) { return p.fn == gg::F_LUT || p.fn == gg::F_FAN; };
+    auto elem_dep = [](const gg::Proj& p) { return p.fn == gg::F_MULR || p.fn == gg::F_NEGR; };
+    auto targets = [&](const gg::Proj& p) { return is_fan(p) ? p.stride : 1; };
+    auto extent = [&](const gg::Proj& p) {
+        return is_fan(p) ? static_cast<int64_t>(p.pin) * p.stride : static_cast<int64_t>(p.pin - 1) * p.stride + 1;
+    };
+    auto pout_of = [&](const gg::Proj& p, int d) {
+        if (p.fn == gg::F_LUT) return g.mrs[d];
+        if (p.fn == gg::F_FAN) return (*fx.fan)[p.a1 + d];
+        return p.pout;
+    };
+    auto value = [&](const gg::Proj& p, int i, int d) -> int {  // f(i, d) mod pout, element-independent f
+        const int t = targets(p), po = pout_of(p, d);
+        int64_t f;
+        switch (p.fn) {
+            case gg::F_LUT: f = (*fx.lut)[fx.lut_off[p.a0] + i * t + d]; break;
+            case gg::F_FAN: f = (*fx.flut)[p.a0 + i * t + d]; break;
+            case gg::F_DIV: f = i / p.a0; break;
+            case gg::F_DIVMOD: f = (i / p.a0) % p.a1; break;
+            case gg::F_SIGN: f = i < p.a0 ? p.a2 : p.a1; break;
+            default: f = i;
+        }
+        f %= po;
+        return static_cast<int>(f < 0 ? f + po : f);
+    };
+    for (const auto& p : pr) {
+        DASH_CHECK(p.pin >= 2 && p.pin <= 4096 && targets(p) < 4096, "gpu garbler: projection shape out of range");
+        DASH_CHECK(p.table >= 0 && p.table < 8 && tb.t[p.table] != nullptr && tb.row[p.table] > 0,
+                   "gpu garbler: projection into an unallocated table");
+        DASH_CHECK(p.fn != gg::F_LUT || (fx.lut && fx.lut_off), "gpu garbler: F_LUT projection without its lookup");
+        DASH_CHECK(p.fn != gg::F_FAN || (fx.flut && fx.fan), "gpu garbler: F_FAN projection without its values");
+    }
+    gg::Emit em{};
+    // position maps
+    std::vector<uint32_t> map;
+    for (int t = 0; t < 8; ++t) {
+        bool used = false;
+        for (const auto& p : pr) used |= p.table == t;
+        if (!used) continue;
+        const int64_t row = tb.row[t];
+        const size_t m0 = map.size();
+        em.map_off[t] = static_cast<int64_t>(m0);
+        map.resize(m0 + static_cast<size_t>(row), gg::kHole);
+        for (int pi = 0; pi < np; ++pi) {
+            const auto& p = pr[pi];
+            if (p.table != t) continue;
+            const int nt = targets(p);
+            for (int col = 0; col < p.pin; ++col)
+                for (int d = 0; d < nt; ++d) {
+                    const int64_t pos = p.off + (is_fan(p) ? static_cast<int64_t>(col) * nt + d : static_cast<int64_t>(col) * p.stride);
+                    DASH_CHECK(pos >= 0 && pos < row && map[m0 + pos] == gg::kHole,
+                               "gpu garbler: projection table positions overlap or overflow the row");
+                    map[m0 + pos] = (static_cast<uint32_t>(pi) << 24) | (static_cast<uint32_t>(col) << 12) |
+                                    static_cast<uint32_t>(d);
+                }
+        }
+    }
+    // scopes: projections by (table, offset); overlapping spans must share a scope, adjacent ones are grouped
+    // while the group stays small (te >= 8)
+    std::vector<int> order(np);
+    for (int i = 0; i < np; ++i) order[i] = i;
+    std::sort(order.begin(), order.end(), [&](int x, int y) {
+        return std::tie(pr[x].table, pr[x].off) < std::tie(pr[y].table, pr[y].off);
+    });
+    auto elem_bytes = [&](int64_t ne, int64_t nb) { return ne * (16 + 2) + nb * 16; };
+    auto rows_bound = [&](const gg::Proj& p) {  // bank rows upper bound
+        int64_t n = 0;
+        for (int d = 0; d < targets(p); ++d) n += std::min<int64_t>(elem_dep(p) ? pout_of(p, d) : p.pin, pout_of(p, d));
+        return n;
+    };
+    std::vector<std::vector<int>> groups;
+    {
+        int64_t gend = -1, gne = 0, gnb = 0;
+        int gt = -1;
+        for (int pi : order) {
+            const auto& p = pr[pi];
+            const bool overlap = p.table == gt && p.off < gend;
+            const bool near = p.table == gt && p.off <= gend + 8 &&
+                              elem_bytes(gne + p.pin, gnb + rows_bound(p)) * 9 <= static_cast<int64_t>(kEmitLds);
+            if (groups.empty() || !(overlap || near)) {
+                groups.push_back({});
+                gend = -1;
+                gne = gnb = 0;
+                gt = p.table;
+            }
+            groups.back().push_back(pi);
+            gend = std::max(gend, p.off + extent(p));
+            gne += p.pin;
+            gnb += rows_bound(p);
+        }
+    }
+    std::vector<gg::EProj> ep(np);
+    std::vector<uint16_t> bix;
+    std::vector<gg::BankRow> rows;
+    std::vector<gg::Scope> sc;
+    size_t lds_max = 0;
+    const auto N = g.N;
+    for (const auto& grp : groups) {
+        gg::Scope S{};
+        S.table = pr[grp[0]].table;
+        int64_t a = INT64_MAX, end = 0, r0 = INT64_MAX, r1 = 0;
+        for (int pi : grp) {
+            a = std::min(a, pr[pi].off);
+            end = std::max(end, pr[pi].off + extent(pr[pi]));
+            r0 = std::min(r0, pr[pi].first);
+            r1 = std::max(r1, pr[pi].first + pr[pi].pin);
+        }
+        S.a = static_cast<int>(a);
+        S.span = static_cast<int>(end - a);
+        S.r0 = static_cast<int>(r0);
+        S.ne = static_cast<int>(r1 - r0);
+        S.b0 = static_cast<int>(rows.size());
+        S.bx0 = static_cast<int>(bix.size());
+        std::map<std::tuple<int, int, int, int>, int> dedup;
+        auto row_of = [&](int slot, int po, int v, int res) {
+            auto key = std::make_tuple(slot, po, v, res);
+            auto it = dedup.find(key);
+            if (it != dedup.end()) return it->second;
+            const int r = static_cast<int>(rows.size()) - S.b0;
+            rows.push_back(gg::BankRow{slot, po, v, res});
+            dedup.emplace(key, r);
+            return r;
+        };
+        for (int pi : grp) {
+            const auto& p = pr[pi];
+            gg::EProj& E = ep[pi];
+            E.first = static_cast<int>(p.first);
+            E.fn = p.fn;
+            E.t = targets(p);
+            E.res = elem_dep(p) ? p.a0 : -1;
+            E.pout = p.pout;
+            const int res = p.outr_kind == gg::R_INPUT ? p.outr_idx : -1;
+            if (elem_dep(p)) {
+                E.pay1 = static_cast<int>(rows.size()) - S.b0;
+                for (int v = 0; v < p.pout; ++v) rows.push_back(gg::BankRow{p.out_slot, p.pout, v, res});
+            } else {
+                E.pay1 = static_cast<int>(bix.size());
+                for (int i = 0; i < p.pin; ++i)
+                    for (int d = 0; d < E.t; ++d) {
+                        const int r = row_of(is_fan(p) ? p.out_slot + d : p.out_slot, pout_of(p, d), value(p, i, d), res);
+                        DASH_CHECK(r < 65536, "gpu garbler: bank row index overflow");
+                        bix.push_back(static_cast<uint16_t>(r));
+                    }
+            }
+        }
+        S.nb = static_cast<int>(rows.size()) - S.b0;
+        S.nbx = static_cast<int>(bix.size()) - S.bx0;
+        const size_t per = static_cast<size_t>(elem_bytes(S.ne, S.nb));
+        const size_t fixed = static_cast<size_t>(S.span) * 4 + static_cast<size_t>(S.nbx) * 2 + 16;
+        auto lds_of = [&](int sh) { return ((1u << sh) + 1) * per + fixed; };
+        int tsh = 5;
+        while (tsh > 0 && lds_of(tsh) > kEmitLds) --tsh;
+        DASH_CHECK(lds_of(tsh) <= (64u << 10) - sizeof(gg::EProj) * gg::kMaxDesc, "gpu garbler: projection scope exceeds LDS");
+        S.tsh = tsh;
+        lds_max = std::max(lds_max, lds_of(tsh));
+        S.blk0 = em.blocks;
+        em.blocks += (N + (1 << tsh) - 1) >> tsh;
+        sc.push_back(S);
     }
     g.projs = gg::dconst(pr.data(), pr.size());
-    g.nprojs = static_cast<int>(pr.size());
-    g.outputs = outs;
+    g.nprojs = np;
+    em.map = gg::dconst(map.data(), map.size());
+    em.bix = gg::dconst(bix.data(), bix.size());
+    em.rows = gg::dconst(rows.data(), rows.size());
+    em.ep = gg::dconst(ep.data(), ep.size());
+    em.nep = np;
+    em.sc = gg::dconst(sc.data(), sc.size());
+    em.nsc = static_cast<int>(sc.size());
     auto hc = hc_scratch(static_cast<size_t>(g.entries), g.N);
     g.HC = hc.first;
     g.CC = hc.second;
+    g.BK = bank_scratch(rows.size(), g.N);
     check_desc(g);
     const int64_t lanes = (g.N + gg::kTile - 1) / gg::kTile * gg::kTile;
-    hipLaunchKernelGGL(gg::k_hash, dim3(blocks_for(lanes * g.entries, gg::kPB, 16384)), dim3(gg::kPB), 0, gg::tl_st, c, g,
-                       in);
-    hipLaunchKernelGGL(gg::k_emit, dim3(blocks_for(lanes * g.outputs, 256, 16384)), dim3(256), 0, gg::tl_st, c, g, in, tb);
+    if (!rows.empty())
+        hipLaunchKernelGGL(gg::k_bank, dim3(blocks_for(lanes * static_cast<int64_t>(rows.size()), 256, 32768)), dim3(256), 0,
+                           gg::tl_st, c, g, in, em.rows, static_cast<int>(rows.size()));
+    if (gg::gg_hash_jobs()) {
+        std::vector<gg::HashJob> hj;
+        for (int pi = 0; pi < np; ++pi)
+            for (int c0 = 0; c0 < pr[pi].pin; c0 += gg::kHJ) hj.push_back(gg::HashJob{pi, c0});
+        const gg::HashJob* dj = gg::dconst(hj.data(), hj.size());
+        hipLaunchKernelGGL(gg::hash_jobs_kernel(), dim3(blocks_for(lanes * static_cast<int64_t>(hj.size()), gg::kPB, 16384)),
+                           dim3(gg::kPB), 0, gg::tl_st, c, g, in, dj, static_cast<int>(hj.size()));
+    } else {
+        hipLaunchKernelGGL(gg::hash_kernel(), dim3(blocks_for(lanes * g.entries, gg::kPB, 16384)), dim3(gg::kPB), 0,
+                           gg::tl_st, c, g, in);
+    }
+    hipLaunchKernelGGL(gg::k_emit, dim3(static_cast<unsigned>(std::min<int64_t>(em.blocks, 65536))), dim3(gg::kEB),
+                       lds_max, gg::tl_st, c, g, in, tb, em);
 }
 
 void run_sign(const gg::Ctx& c, const gg::SignLayout& L, gg::Gadget& g, const gg::In& in, const gg::Tables& tb,
-              std::vector<void*>& tmp) {
+              const ProjFns& fx) {
     g.draws = gg::dconst(L.draws.data(), L.draws.size());
     g.ndraws = static_cast<int>(L.draws.size());
     g.projs = gg::dconst(L.projs.data(), L.projs.size());
@@ -1286,15 +1648,9 @@ void run_sign(const gg::Ctx& c, const gg::SignLayout& L, gg::Gadget& g, const gg
     g.nblk = draw_blocks(L.draws);
     for (int d = 0; d < L.ss.t; ++d) g.mrs[d] = L.fan[d];
     check_desc(g);
-    hipLaunchKernelGGL(gg::k_draw, dim3(blocks_for(g.N * g.nblk, gg::kGB, 8192)), dim3(gg::kGB), 0, gg::tl_st, c, g);
+    hipLaunchKernelGGL(gg::draw_kernel(), dim3(draw_grid(g)), dim3(gg::kGB), 0, gg::tl_st, c, g);
     hipLaunchKernelGGL(gg::k_sign_derive, dim3(blocks_for(g.N, 256), L.ss.t), dim3(256), 0, gg::tl_st, c, g, L.ss);
-    if (!L.pays.empty()) {
-        DASH_CHECK(g.PB != nullptr, "gpu garbler: payload bank not allocated");
-        const gg::PayDesc* pd = gg::dconst(L.pays.data(), L.pays.size());
-        const int npd = static_cast<int>(L.pays.size());
-        hipLaunchKernelGGL(gg::k_payloads, dim3(blocks_for(g.N * npd, 256, 16384)), dim3(256), 0, gg::tl_st, c, g, pd, npd);
-    }
-    project(c, g, in, tb, L.projs);
+    project(c, g, in, tb, L.projs, fx);
     HIPCHECK(hipGetLastError());
 }
 
@@ -1401,18 +1757,31 @@ struct DevCtx {
         }
         return PB;
     }
+    // bank payloads between k_bank and k_emit
+    u128* BK = nullptr;
+    size_t BK_n = 0;
+    u128* bank(size_t rows, int64_t N) {
+        const size_t n = std::max<size_t>(1, rows * static_cast<size_t>(N));
+        if (n > BK_n) {
+            HIPCHECK(hipStreamSynchronize(st));
+            if (BK) (void)hipFree(BK);
+            HIPCHECK(hipMalloc(reinterpret_cast<void**>(&BK), n * sizeof(u128)));
+            BK_n = n;
+        }
+        return BK;
+    }
     // key hashes / colors between k_hash and k_emit
     u128* HC = nullptr;
-    uint8_t* CC = nullptr;
+    uint16_t* CC = nullptr;
     size_t HC_n = 0;
-    std::pair<u128*, uint8_t*> hc(size_t entries, int64_t N) {
+    std::pair<u128*, uint16_t*> hc(size_t entries, int64_t N) {
         const size_t n = std::max<size_t>(1, entries * static_cast<size_t>(N));
         if (n > HC_n) {
             HIPCHECK(hipStreamSynchronize(st));
             if (HC) (void)hipFree(HC);
             if (CC) (void)hipFree(CC);
             HIPCHECK(hipMalloc(reinterpret_cast<void**>(&HC), n * sizeof(u128)));
-            HIPCHECK(hipMalloc(reinterpret_cast<void**>(&CC), n));
+            HIPCHECK(hipMalloc(reinterpret_cast<void**>(&CC), n * sizeof(uint16_t)));
             HC_n = n;
         }
         return {HC, CC};
@@ -1420,9 +1789,13 @@ struct DevCtx {
 };
 thread_local DevCtx* tl_dc = nullptr;  // the calling thread's garbling context (set by Impl::enter)
 namespace {  // the same (translation-unit) anonymous namespace as its declaration above run_sign
-std::pair<u128*, uint8_t*> hc_scratch(size_t entries, int64_t N) {
+std::pair<u128*, uint16_t*> hc_scratch(size_t entries, int64_t N) {
     DASH_CHECK(tl_dc != nullptr, "gpu garbler: no garbling context on this thread");
     return tl_dc->hc(entries, N);
+}
+u128* bank_scratch(size_t rows, int64_t N) {
+    DASH_CHECK(tl_dc != nullptr, "gpu garbler: no garbling context on this thread");
+    return tl_dc->bank(rows, N);
 }
 }  // namespace
 // A free garbling context of the device, locked for the caller: up to DASH_GG_CONTEXTS (default 2) per
@@ -1472,6 +1845,10 @@ struct GpuGarbler::Impl {
     std::vector<int> crt;
     int k = 0;
     int device = 0;
+    // approx-sign lookup (gen_approx_lookup: residue j's [p][t] at lut_off[j]) for the F_LUT bank rows
+    std::vector<int16_t> lut;
+    int lut_off[kMaxRes] = {};
+    ProjFns lut_fns() const { return ProjFns{nullptr, nullptr, &lut, lut_off}; }
     // sign base labels a sign_last mixed-radix rescale leaves for the next ReLU ([N][kW], relu_mult)
     DevBlock sig;
     int64_t sig_N = 0;
@@ -1526,12 +1903,10 @@ GpuGarbler::GpuGarbler(const std::vector<int>& crt, const std::vector<int>& mrs,
     std::copy(rk.begin(), rk.end(), I.c.rk);
     if (!mrs.empty()) {
         auto lut = gen_approx_lookup(crt, mrs);
-        std::vector<int16_t> flat;
         for (int j = 0; j < I.k; ++j) {
-            I.c.lut_off[j] = static_cast<int>(flat.size());
-            flat.insert(flat.end(), lut[j].begin(), lut[j].end());
+            I.lut_off[j] = static_cast<int>(I.lut.size());
+            I.lut.insert(I.lut.end(), lut[j].begin(), lut[j].end());
         }
-        I.c.lut = gg::dconst(flat.data(), flat.size());
     }
 }
 
@@ -1771,10 +2146,10 @@ void GpuGarbler::sign_layer(uint64_t layer, const SignPlan& sp, CrtLabels& cur, 
     g.sslot = 1;
     g.mask = 0;
     g.S = S;
-    g.PB = I.pbank(std::max<size_t>(2, L.pays.size()), N);
+    g.PB = I.pbank(2, N);
     g.N = N;
     g.nslots = L.nslots;
-    run_sign(I.c, L, g, in, tb, tmp);
+    run_sign(I.c, L, g, in, tb, I.lut_fns());
     std::vector<int> omods = relu ? I.crt : sp.out_mod;
     std::vector<DevBlock> out = I.alloc_labels(omods, N);
     if (relu) {
@@ -1813,7 +2188,7 @@ void GpuGarbler::sign_layer(uint64_t layer, const SignPlan& sp, CrtLabels& cur, 
         gm.entries = first;
         gm.nblk = draw_blocks(dr);
         check_desc(gm);
-        hipLaunchKernelGGL(gg::k_draw, dim3(blocks_for(N * gm.nblk, gg::kGB, 8192)), dim3(gg::kGB), 0, gg::tl_st, I.c, gm);
+        hipLaunchKernelGGL(gg::draw_kernel(), dim3(draw_grid(gm)), dim3(gg::kGB), 0, gg::tl_st, I.c, gm);
         project(I.c, gm, in, tb, pr);
         gg::MiniArgs ma{};
         ma.k = k;
@@ -1896,9 +2271,8 @@ void GpuGarbler::rescale_legacy_iter(uint64_t layer, int it, const RescalePlan& 
         ctr += prg_blocks(I.crt[j]);
     }
     gg::SignLayout L = gg::sign_layout(P.sign, 0);
-    // the payload bank is sized once for both users: rows 0-1 hold the trans key hashes until the sign gadget's
-    // k_payloads (later on the same stream) overwrites them
-    u128* PB = I.pbank(std::max<size_t>(2, L.pays.size()), N);
+    // rows 0-1: the trans key hashes (k_bin_keys -> k_rescale_pre)
+    u128* PB = I.pbank(2, N);
     hipLaunchKernelGGL(gg::k_bin_keys, dim3(blocks_for(N, gg::kGB, 8192)), dim3(gg::kGB), 0, gg::tl_st, I.c,
                        static_cast<const int16_t*>(ra.L[0]), ra.up, PB, N);
     hipLaunchKernelGGL(gg::k_rescale_pre, dim3(blocks_for(N, gg::kGB, 2048), k - 1), dim3(gg::kGB), 0, gg::tl_st, I.c,
@@ -1920,10 +2294,10 @@ void GpuGarbler::rescale_legacy_iter(uint64_t layer, int it, const RescalePlan& 
     g.sslot = 10 + it;
     g.mask = 1ull << 43;  // nested sign stream (rescale_garble_elem)
     g.S = S;
-    g.PB = I.pbank(std::max<size_t>(2, L.pays.size()), N);
+    g.PB = I.pbank(2, N);
     g.N = N;
     g.nslots = L.nslots;
-    run_sign(I.c, L, g, in, tb, tmp);
+    run_sign(I.c, L, g, in, tb, I.lut_fns());
     hipLaunchKernelGGL(gg::k_rescale_post_g, dim3(blocks_for(N * 128, 256, 4096), k), dim3(256), 0, gg::tl_st, I.c, ra,
                        g, L.out_slot0);
     HIPCHECK(hipGetLastError());
@@ -1979,7 +2353,7 @@ static std::vector<DevBlock> relu_mult_gates(GpuGarbler::Impl& I, const gg::Gadg
     gm.entries = f2;
     gm.nblk = draw_blocks(dm);
     check_desc(gm);
-    hipLaunchKernelGGL(gg::k_draw, dim3(blocks_for(N * gm.nblk, gg::kGB, 8192)), dim3(gg::kGB), 0, gg::tl_st, I.c, gm);
+    hipLaunchKernelGGL(gg::draw_kernel(), dim3(draw_grid(gm)), dim3(gg::kGB), 0, gg::tl_st, I.c, gm);
     project(I.c, gm, in, tb, pm);
     gg::MiniArgs ma{};
     ma.k = k;
@@ -2075,13 +2449,12 @@ void GpuGarbler::relu_mrs(uint64_t layer, const SignMrsPlan& P, CrtLabels& cur, 
     g.nprojs = static_cast<int>(pr.size());
     g.entries = first;
     g.nblk = draw_blocks(dr);
-    g.flut = gg::dconst(flut.data(), flut.size());
-    g.fan = gg::dconst(fan.data(), fan.size());
+
     check_desc(g);
     std::vector<void*> tmp;
-    hipLaunchKernelGGL(gg::k_draw, dim3(blocks_for(N * g.nblk, gg::kGB, 8192)), dim3(gg::kGB), 0, gg::tl_st, I.c, g);
+    hipLaunchKernelGGL(gg::draw_kernel(), dim3(draw_grid(g)), dim3(gg::kGB), 0, gg::tl_st, I.c, g);
     hipLaunchKernelGGL(gg::k_mrs_sign_derive, dim3(blocks_for(N, 256), k), dim3(256), 0, gg::tl_st, I.c, g, in, a);
-    project(I.c, g, in, tb, pr);
+    project(I.c, g, in, tb, pr, ProjFns{&flut, &fan});
     // mixed-modulus half gates (as sign_layer's ReLU branch, sign label = residue 0's key slot)
     std::vector<DevBlock> out = relu_mult_gates(I, g, in, tb, sig_slot, sk0, *prefix);
     HIPCHECK(hipGetLastError());
@@ -2107,9 +2480,8 @@ void GpuGarbler::rescale_mrs(uint64_t layer, const RescaleMrsPlan& P, CrtLabels&
     DASH_CHECK(P.k() == k && static_cast<int>(P.T) <= I.max_mod, "gpu garbler: mixed-radix rescale plan mismatch");
     std::vector<gg::Draw> dr;
     std::vector<gg::Proj> pr;
-    std::vector<int> fan, fbank;
+    std::vector<int> fan;
     std::vector<int16_t> flut;
-    std::vector<gg::PayDesc> pays;
     gg::MrsG a{};
     a.k = k;
     a.T = static_cast<int>(P.T);
@@ -2157,12 +2529,7 @@ void GpuGarbler::rescale_mrs(uint64_t layer, const RescaleMrsPlan& P, CrtLabels&
         for (int v = 0; v < P.T; ++v)
             for (int j = 0; j < k; ++j) flut.push_back(static_cast<int16_t>(P.final_fn(j, v)));
         for (int j = 0; j < k; ++j) fan.push_back(P.crt[j]);
-        // T entries but only p_j distinct payloads per target j: payload bank rows fin_j + f * R_{p_j}
-        fbank.assign(fan.size(), 0);
-        for (int j = 0; j < k; ++j) {
-            fbank[a1 + j] = static_cast<int>(pays.size()) + 1;
-            for (int f = 0; f < P.crt[j]; ++f) pays.push_back(gg::PayDesc{a.fin0 + j, P.crt[j], f});
-        }
+        // T entries but only p_j distinct payloads per target j (k_emit's bank rows)
         gg::Proj p{};
         p.in_kind = gg::S_SLOT; p.in_idx = a.acc; p.pin = static_cast<int>(P.T);
         p.out_slot = a.fin0; p.pout = P.crt[0]; p.fn = gg::F_FAN; p.a0 = a0; p.a1 = a1;
@@ -2185,7 +2552,7 @@ void GpuGarbler::rescale_mrs(uint64_t layer, const RescaleMrsPlan& P, CrtLabels&
     g.sslot = 30;
     g.mask = 0;
     g.S = I.scratch(static_cast<size_t>(N) * nslots * gg::kW * sizeof(int16_t));
-    g.PB = I.pbank(std::max<size_t>(1, pays.size()), N);
+    g.PB = nullptr;
     g.N = N;
     g.nslots = nslots;
     g.draws = gg::dconst(dr.data(), dr.size());
@@ -2194,20 +2561,22 @@ void GpuGarbler::rescale_mrs(uint64_t layer, const RescaleMrsPlan& P, CrtLabels&
     g.nprojs = static_cast<int>(pr.size());
     g.entries = first;
     g.nblk = draw_blocks(dr);
-    g.flut = gg::dconst(flut.data(), flut.size());
-    g.fan = gg::dconst(fan.data(), fan.size());
-    g.fbank = gg::dconst(fbank.data(), fbank.size());
+
     check_desc(g);
     gg::In in{};
     std::vector<void*> tmp;
-    hipLaunchKernelGGL(gg::k_draw, dim3(blocks_for(N * g.nblk, gg::kGB, 8192)), dim3(gg::kGB), 0, gg::tl_st, I.c, g);
-    if (!pays.empty()) {
-        const gg::PayDesc* pd = gg::dconst(pays.data(), pays.size());
-        const int npd = static_cast<int>(pays.size());
-        hipLaunchKernelGGL(gg::k_payloads, dim3(blocks_for(N * npd, 256, 16384)), dim3(256), 0, gg::tl_st, I.c, g, pd, npd);
+    hipLaunchKernelGGL(gg::draw_kernel(), dim3(draw_grid(g)), dim3(gg::kGB), 0, gg::tl_st, I.c, g);
+    int ny = 0;
+    for (int j = 0; j <= k; ++j) {
+        const int nc = static_cast<int>(gg::chunks_of(nr_comps(j < k ? P.crt[j] : static_cast<int>(P.T))));
+        for (int c8 = 0; c8 < nc; ++c8) {
+            DASH_CHECK(ny < gg::kMaxY, "gpu garbler: mixed-radix derive work items");
+            a.yj[ny] = j;
+            a.yc[ny++] = c8;
+        }
     }
-    hipLaunchKernelGGL(gg::k_mrs_derive, dim3(blocks_for(N, 256), k + 1), dim3(256), 0, gg::tl_st, I.c, g, a);
-    project(I.c, g, in, tb, pr);
+    hipLaunchKernelGGL(gg::k_mrs_derive, dim3(blocks_for(N, 256), ny), dim3(256), 0, gg::tl_st, I.c, g, a);
+    project(I.c, g, in, tb, pr, ProjFns{&flut, &fan});
     if (P.sign_last) {
         // residue 0's key slot is the sign label of the ReLU that follows (relu_mult)
         I.sig.alloc(I.device, static_cast<size_t>(N) * gg::kW * sizeof(int16_t));

@@ -46,6 +46,12 @@ def main(paths):
         if c.get("SQ_WAVES"):
             d["valu_insts/wave"] = c.get("SQ_INSTS_VALU", 0) / c["SQ_WAVES"]
             d["vmem_rd/wave"] = c.get("SQ_INSTS_VMEM_RD", 0) / c["SQ_WAVES"]
+            for ctr, name in (("SQ_INSTS_VMEM_WR", "vmem_wr/wave"), ("SQ_INSTS_LDS", "lds/wave"),
+                              ("SQ_INSTS_SALU", "salu/wave")):
+                if ctr in c:
+                    d[name] = c[ctr] / c["SQ_WAVES"]
+        if c.get("SQ_ACTIVE_INST_LDS"):
+            d["lds_conf%"] = 100 * c.get("SQ_LDS_BANK_CONFLICT", 0) / c["SQ_ACTIVE_INST_LDS"]
         for ctr, name in (("FETCH_SIZE", "fetch"), ("WRITE_SIZE", "write")):
             if ctr in c and ms_by_pass:
                 pms = ms_by_pass.get(cpass[k][ctr], ms)  # time of the pass that collected this counter
@@ -54,7 +60,7 @@ def main(paths):
         rows.append(d)
     rows.sort(key=lambda r: -r["ms"])
     cols = ["kernel", "ms", "dispatch", "valu%", "active%", "wait%", "stall%", "valu_insts/wave", "vmem_rd/wave",
-            "fetch_GB", "fetch_TB/s", "write_GB", "write_TB/s"]
+            "vmem_wr/wave", "lds/wave", "salu/wave", "lds_conf%", "fetch_GB", "fetch_TB/s", "write_GB", "write_TB/s"]
     print(" ".join(f"{c:>14s}" if c != "kernel" else f"{c:40s}" for c in cols))
     for r in rows[:25]:
         out = []

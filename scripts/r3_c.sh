@@ -10,7 +10,7 @@ mkdir -p $OUT
 DASH_GG_TRACE=1 timeout -k 10 200 python -u scripts/garble_bench.py --sink 6 > $OUT/trace.json 2> $OUT/trace.err || { tail -20 $OUT/trace.err; exit 1; }
 tail -30 $OUT/trace.err
 cd /tmp
-RX="k_project|k_mrs_derive|k_draw|k_relu_finish|k_payloads|k_transpose"
+RX="k_hash|k_emit|k_draw|k_bank"
 N=0
 run() {
   timeout -s KILL 120 rocprofv3 --kernel-trace --kernel-include-regex "$RX" --pmc "$@" --output-format csv -d "$ROOT/$OUT/p$N" -o run -- python3 "$ROOT/scripts/garble_bench.py" --sink 3 > "$ROOT/$OUT/p$N.log" 2>&1 || { tail -5 "$ROOT/$OUT/p$N.log"; exit 1; }
