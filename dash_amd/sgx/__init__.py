@@ -19,10 +19,17 @@ boundary:
     predictions        <--- return (pipe) ----
 
 The host never sees R_p or the decoder; the enclave never touches the GPU.
+
+Trust mechanisms (attest.py): the enclave process hardens itself (non-dumpable,
+memory locked), the host verifies its quote (measurement of the garbler build
+and circuit configuration, fresh nonce) before handing over inputs, and the
+garbler's master secret + GC counter can be sealed to that measurement and
+resumed by a later enclave of the same build.
 """
 from __future__ import annotations
 
 import multiprocessing as mp
+import os
 import socket
 import threading
 from typing import Optional, Sequence
@@ -30,38 +37,91 @@ from typing import Optional, Sequence
 import numpy as np
 
 
-def _enclave_main(conn, sock_fd_port, circuit, crt, mrs, max_modulus, batch):
-    from ..net.protocol import GarblerClient
+def _config(circuit, crt, mrs, max_modulus) -> dict:
+    from .attest import circuit_digest
 
-    host, port = sock_fd_port
-    client = GarblerClient(host, port, circuit, crt, mrs, batch=batch, max_modulus=max_modulus)
+    return {"crt": crt if isinstance(crt, int) else [int(p) for p in crt],
+            "mrs": mrs if mrs is None or isinstance(mrs, (int, float)) else [int(m) for m in mrs],
+            "max_modulus": int(max_modulus), "circuit": circuit_digest(circuit)}
+
+
+def _enclave_main(conn, sock_fd_port, circuit, crt, mrs, max_modulus, batch, sealed, key_file):
+    import hashlib
+    import json
+    import secrets
+
+    from ..net.protocol import GarblerClient
+    from . import attest
+
+    if key_file:
+        os.environ["DASH_PLATFORM_KEY_FILE"] = key_file
+    hard = attest.harden(lock_memory=False)  # mlockall(MCL_FUTURE) makes later allocations fail at the limit
+    cfg = _config(circuit, crt, mrs, max_modulus)
+    meas = attest.measure(cfg)
+    report = hashlib.sha256(b"dash_amd garbler v1" + json.dumps(cfg, sort_keys=True).encode()).digest()
     try:
+        if sealed is not None:
+            # resume: master secret + GC counter, so no per-GC seed is ever reused across restarts
+            state, _ = attest.unseal(sealed, meas)
+            master, ctr = state[:32], int.from_bytes(state[32:40], "little")
+        else:
+            master, ctr = secrets.token_bytes(32), 0
+    except Exception as e:
+        conn.send(("error", repr(e), None))
+        conn.close()
+        return
+    # ready before connecting: the host starts its evaluator server only after this message, and the client's
+    # HELO waits for that server
+    conn.send(("ready", hard, None))
+    host, port = sock_fd_port
+    client = None
+    try:
+        client = GarblerClient(host, port, circuit, crt, mrs, batch=batch, max_modulus=max_modulus, seed=master)
+        client._ctr = ctr
         while True:
             msg = conn.recv()
             if msg is None:
                 break
-            xs = msg
-            outs = []
-            for s in range(0, len(xs), batch):
-                client.offline()
-                outs += client.infer(xs[s:s + batch])
-            conn.send(("ok", np.stack(outs), dict(client.stats, online_s=list(client.stats["online_s"]))))
+            op, arg = msg
+            if op == "attest":
+                conn.send(("ok", attest.make_quote(meas, report, arg), None))
+            elif op == "seal":
+                state = master + client._ctr.to_bytes(8, "little")
+                conn.send(("ok", attest.seal(state, meas, aad=b"dash_amd garbler state"), None))
+            elif op == "infer":
+                xs = arg
+                outs = []
+                for s in range(0, len(xs), batch):
+                    client.offline()
+                    outs += client.infer(xs[s:s + batch])
+                conn.send(("ok", np.stack(outs), dict(client.stats, online_s=list(client.stats["online_s"]))))
+            else:
+                conn.send(("error", f"unknown ecall {op!r}", None))
     except Exception as e:  # report to the host instead of dying silently
         conn.send(("error", repr(e), None))
     finally:
-        client.close()
+        if client is not None:
+            client.close()
         conn.close()
 
 
 class GarblerEnclave:
-    """Host-side handle of a trusted garbler process."""
+    """Host-side handle of a trusted garbler process.
+
+    attest: verify the enclave's quote (fresh nonce, expected measurement of this garbler build and circuit
+    configuration) before any input is handed over; AttestationError otherwise.
+    sealed_state: a blob from seal_state() of an earlier enclave of the same build and configuration: the
+    garbler resumes its master secret and GC counter (no per-GC seed reuse across restarts)."""
 
     def __init__(self, circuit, crt, mrs=None, max_modulus: int = 0, batch: int = 1, backend: str = "hip",
-                 device: int = 0):
+                 device: int = 0, attest: bool = True, sealed_state: Optional[bytes] = None,
+                 platform_key_file: Optional[str] = None):
         from ..net.channel import Channel
         from ..net.protocol import EvaluatorServer
+        from . import attest as at
 
         self.batch = batch
+        self._key_file = platform_key_file
         lst = socket.socket(socket.AF_INET, socket.SOCK_STREAM)
         lst.bind(("127.0.0.1", 0))
         lst.listen(1)
@@ -69,23 +129,62 @@ class GarblerEnclave:
         ctx = mp.get_context("spawn")
         self._conn, child = ctx.Pipe()
         self._proc = ctx.Process(target=_enclave_main,
-                                 args=(child, ("127.0.0.1", port), circuit, crt, mrs, max_modulus, batch),
+                                 args=(child, ("127.0.0.1", port), circuit, crt, mrs, max_modulus, batch,
+                                       sealed_state, platform_key_file),
                                  daemon=True)
         self._proc.start()
+        status, info, _ = self._conn.recv()
+        if status != "ready":
+            self._proc.join(timeout=30)
+            lst.close()
+            raise at.SealError(f"garbler enclave failed to start: {info}")
+        self.hardening = info
         conn, _ = lst.accept()
         lst.close()
         self._server = EvaluatorServer(backend, device)
         self._thread = threading.Thread(target=self._server.serve, args=(Channel(conn),), daemon=True)
         self._thread.start()
         self.last_stats: Optional[dict] = None
+        self.quote: Optional[dict] = None
+        self._cfg = _config(circuit, crt, mrs, max_modulus)
+        if attest:
+            try:
+                self.attest()
+            except Exception:
+                self.close()
+                raise
+
+    def _ecall(self, op, arg=None):
+        self._conn.send((op, arg))
+        status, out, stats = self._conn.recv()
+        if status != "ok":
+            raise RuntimeError(f"garbler enclave failed: {out}")
+        return out, stats
+
+    def attest(self, nonce: Optional[bytes] = None) -> dict:
+        """Challenge the enclave with a fresh nonce and verify its quote against the measurement this host
+        expects for the garbler build + circuit configuration."""
+        import os as _os
+
+        from . import attest as at
+
+        if self._key_file:
+            _os.environ.setdefault("DASH_PLATFORM_KEY_FILE", self._key_file)
+        nonce = nonce or _os.urandom(16)
+        quote, _ = self._ecall("attest", nonce)
+        at.verify_quote(quote, at.measure(self._cfg), nonce)
+        self.quote = quote
+        return quote
+
+    def seal_state(self) -> bytes:
+        """The garbler's master secret and GC counter, sealed to this build + configuration."""
+        blob, _ = self._ecall("seal")
+        return blob
 
     def ann_infer(self, inputs: Sequence[np.ndarray]) -> np.ndarray:
         """ecall: quantized inputs -> decoded outputs [n, n_out] (n multiple of batch)."""
         assert len(inputs) % self.batch == 0, "number of inputs must be a multiple of the batch"
-        self._conn.send([np.asarray(x, dtype=np.int64) for x in inputs])
-        status, out, stats = self._conn.recv()
-        if status != "ok":
-            raise RuntimeError(f"garbler enclave failed: {out}")
+        out, stats = self._ecall("infer", [np.asarray(x, dtype=np.int64) for x in inputs])
         self.last_stats = stats
         return out
 
