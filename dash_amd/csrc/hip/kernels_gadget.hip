@@ -92,6 +92,52 @@ static inline int aes_bs(int64_t n, int y, int z) {
     const AesCtx aes = aes_ctx(lds_aes, rk)
 
 // ---------------------------------------------------------------------------
+// LDS staging of component-major byte labels (rows of N bytes, N % 16 == 0): a block owning BS consecutive
+// elements moves rows [c0, c0 + cnt) of its tile between HBM and an LDS image S[c][BS] with 16-byte
+// accesses, U of them in flight per thread. Lanes then walk their own element's components in LDS. A lane
+// streaming its own column from HBM moves one byte per lane per load (64 B per wave instruction) with a
+// few loads in flight: the streaming kernels sat at 0.2-1.5 TB/s, 65-70 % of cycles waiting (r03 roofline).
+template <int BS, int U>
+__device__ __forceinline__ void lds_stage_rows(uint8_t* S, const act_t* L, int64_t N, int64_t e0, int c0, int cnt) {
+    constexpr int W = BS / 16;  // 16-byte units per row
+    const int units = cnt * W;
+    for (int x0 = threadIdx.x; x0 < units; x0 += U * BS) {
+        uint4 v[U];
+#pragma unroll
+        for (int h = 0; h < U; ++h) {
+            const int x = x0 + h * BS;
+            const int64_t e = e0 + 16 * (x % W);
+            if (x < units && e < N) v[h] = *reinterpret_cast<const uint4*>(L + static_cast<int64_t>(c0 + x / W) * N + e);
+        }
+#pragma unroll
+        for (int h = 0; h < U; ++h) {
+            const int x = x0 + h * BS;
+            if (x < units) *reinterpret_cast<uint4*>(S + (x / W) * BS + 16 * (x % W)) = v[h];
+        }
+    }
+}
+template <int BS>
+__device__ __forceinline__ void lds_store_rows(act_t* L, const uint8_t* S, int64_t N, int64_t e0, int c0, int cnt) {
+    constexpr int W = BS / 16;
+    const int units = cnt * W;
+    for (int x = threadIdx.x; x < units; x += BS) {
+        const int64_t e = e0 + 16 * (x % W);
+        if (e < N)
+            *reinterpret_cast<uint4*>(L + static_cast<int64_t>(c0 + x / W) * N + e) =
+                *reinterpret_cast<const uint4*>(S + (x / W) * BS + 16 * (x % W));
+    }
+}
+// the staged kernels where the shape allows (whole 16-byte rows, at least one full block); A/B knob
+// DASH_MRS_STAGE=0 keeps the per-lane forms
+static inline bool stage_ok(int64_t N, int bs) {
+    static const bool on = [] {
+        const char* e = std::getenv("DASH_MRS_STAGE");
+        return !(e && e[0] == '0');
+    }();
+    return on && N % 16 == 0 && N >= bs;
+}
+
+// ---------------------------------------------------------------------------
 // Phase A tail: the casts Z_{m_d} -> Z_{(k+1) m_d} of residue j's approx
 // labels for every digit d >= 1. They do not depend on the carry, so they run
 // here, in the lane that just produced the approx labels (still in registers):
@@ -443,6 +489,55 @@ __global__ __launch_bounds__(256) void k_relu_mult(SignArgs a, Act x, Act y, con
             }
 #pragma unroll
         for (int u = 0; u < kChunk; ++u) cur[u] = nxt[u];
+    }
+}
+
+// k_relu_mult with the label staged in LDS (stage_ok): a block = (256-element tile, residue j, GC b); the
+// per-element gathers go out first, the block's x_j rows come in as 16-byte loads, each lane rewrites its
+// column in place and the block stores the y_j rows back as 16-byte stores.
+constexpr int kRmBS = 256;
+__global__ __launch_bounds__(kRmBS) void k_relu_mult_s(SignArgs a, Act x, Act y, const u128* gtab, const u128* etab,
+                                                       const ModC* mc) {
+    __shared__ __attribute__((aligned(16))) uint8_t stg[128 * kRmBS];
+    const int j = blockIdx.y, b = blockIdx.z;
+    const int64_t N = a.N;
+    const int tid = static_cast<int>(threadIdx.x);
+    const int k = a.crt.k;
+    const int p = a.crt.p[j];
+    const ModC m = mc[p];
+    const int n = static_cast<int>(m.n);
+    const act_t* X = x.p[j] + static_cast<int64_t>(b) * n * N;
+    act_t* Y = y.p[j] + static_cast<int64_t>(b) * n * N;
+    for (int64_t e0 = static_cast<int64_t>(blockIdx.x) * kRmBS; e0 < N; e0 += static_cast<int64_t>(gridDim.x) * kRmBS) {
+        const int64_t e = min(e0 + tid, N - 1);
+        const int64_t bke = (static_cast<int64_t>(b) * k + j) * N + e;
+        const int64_t be = static_cast<int64_t>(b) * N + e;
+        const u128 Hx = a.hx[bke];
+        const uint32_t colx = a.colx[bke];
+        const u128 HS = a.hs[be];
+        const uint32_t cS = a.cs[be];
+        const u128* E3 = etab + (be * k + j) * 3;
+        const u128 Graw = gtab[be * a.crt.sum + a.crt.prefix[j] + colx];
+        const u128 Eraw = E3[cS];
+        const u128 mini = E3[2];
+        __syncthreads();  // the previous tile's stores have read the image
+        lds_stage_rows<kRmBS, 4>(stg, X, N, e0, 0, n);
+        __syncthreads();
+        const u128 G = Graw - Hx, E = Eraw - HS;
+        const int16_t t16 = static_cast<int16_t>(static_cast<uint16_t>(mini >> (16 * cS)));
+        const int16_t ypr16 = static_cast<int16_t>(t16 - static_cast<int16_t>(static_cast<uint16_t>(HS)));
+        const uint32_t ypr = modq(static_cast<uint32_t>(static_cast<int32_t>(ypr16) + (p << 15)), m);
+        DigitStream sg, se;
+        sg.init(G);
+        se.init(E);
+        for (int c = 0; c < n; ++c) {
+            const uint32_t g = sg.next(m);
+            const uint32_t ev = se.next(m);
+            uint8_t& v = stg[c * kRmBS + tid];
+            v = static_cast<uint8_t>(modq(ev + ypr * static_cast<uint32_t>(v) + static_cast<uint32_t>(p) - g, m));
+        }
+        __syncthreads();
+        lds_store_rows<kRmBS>(Y, stg, N, e0, 0, n);
     }
 }
 
@@ -809,6 +904,128 @@ __global__ __launch_bounds__(kAesBlock, MODE == 2 ? DASH_CHAIN2_WAVES : DASH_UA_
     }
 }
 
+// LDS-staged chain (N % 16 == 0, N >= kMrsBS): a block owns kMrsBS consecutive elements and walks the
+// positions in lockstep; residue r's label bytes for the block are brought into LDS by the whole block,
+// kMrsCap components per pass, as 16-byte loads that are all in flight at once, and each lane then reads its
+// components from LDS. The per-lane form (k_mrs_chain) loaded one byte per lane per component, kMrsChunk
+// at a time: ~n / 4 dependent HBM round trips per position, 65 % of its cycles waiting (r03 roofline:
+// 0.87 TB/s fetched). Outputs, payload scratch and table gathers are per lane as before.
+constexpr int kMrsBS = 512;   // elements (lanes) per block
+constexpr int kMrsCap = 64;   // components staged per pass (kMrsCap * kMrsBS = 32 KiB beside the AES image)
+#ifndef DASH_STAGE_U
+#define DASH_STAGE_U 2  // 16-byte loads in flight per thread while staging (4 pushed the chain into spills)
+#endif
+constexpr int kStageU = DASH_STAGE_U;
+#ifndef DASH_STAGE_RD
+#define DASH_STAGE_RD 4  // LDS component reads batched per lane
+#endif
+constexpr int kStageRd = DASH_STAGE_RD;
+template <int K, int MODE>
+__global__ __launch_bounds__(kMrsBS, MODE == 2 ? DASH_CHAIN2_WAVES : DASH_UA_MINBLOCKS) void k_mrs_chain_s(
+    MrsArgs a, Act x, const ModC* mc, const uint32_t* te0, const uint32_t* rk) {
+    AES_PROLOGUE(te0, rk);
+    __shared__ __attribute__((aligned(16))) uint8_t stg[kMrsCap * kMrsBS];
+    const int b = blockIdx.z;
+    const int64_t N = a.N;
+    constexpr int NP = K * (K - 1) / 2 > 0 ? K * (K - 1) / 2 : 1;
+    const int tid = static_cast<int>(threadIdx.x);
+    for (int64_t e0 = static_cast<int64_t>(blockIdx.x) * kMrsBS; e0 < N; e0 += static_cast<int64_t>(gridDim.x) * kMrsBS) {
+        const bool valid = e0 + tid < N;
+        const int64_t e = valid ? e0 + tid : N - 1;  // spare lanes shadow a real element, store nothing
+        const u128* row0 = a.tab + (static_cast<int64_t>(b) * N + e) * a.n_tab;
+        u128* PS = a.ps + static_cast<int64_t>(b) * NP * N + e;
+        u128 acc = 0;
+#pragma unroll
+        for (int i = 0; i < (MODE >= 1 ? K - 1 : K); ++i) {
+            const int r = MODE >= 1 ? (i + 1) % K : i;
+            const ModC m = mc[a.crt.p[r]];
+            const int n = static_cast<int>(m.n);
+            const act_t* L = x.p[r] + static_cast<int64_t>(b) * n * N;
+            DigitStream ds[K > 1 ? K - 1 : 1];
+#pragma unroll
+            for (int l = 0; l < i; ++l) ds[l].init(PS[static_cast<int64_t>(mrs_pair<K>(l, i)) * N]);
+            CompressFwd cf;
+            cf.init();
+            uint32_t col = 0;
+            for (int c0 = 0; c0 < n; c0 += kMrsCap) {
+                const int cnt = min(kMrsCap, n - c0);
+                __syncthreads();
+                lds_stage_rows<kMrsBS, kStageU>(stg, L, N, e0, c0, cnt);
+                __syncthreads();
+                for (int c = 0; c < cnt; c += kStageRd) {
+                    uint32_t v[kStageRd];
+#pragma unroll
+                    for (int u = 0; u < kStageRd; ++u)
+                        if (c + u < cnt) v[u] = stg[(c + u) * kMrsBS + tid];
+#pragma unroll
+                    for (int u = 0; u < kStageRd; ++u)
+                        if (c + u < cnt) {
+                            uint32_t d = v[u];
+#pragma unroll
+                            for (int l = 0; l < i; ++l) {
+                                const uint32_t s = ds[l].next(m);
+                                d = d >= s ? d - s : d + m.q - s;
+                            }
+                            if (c0 + c + u == 0) col = d;
+                            cf.push(d, m);
+                        }
+                }
+            }
+            constexpr int kExtra = MODE == 1 ? 0 : 1;
+            const int nt = K - 1 - i + kExtra;
+            const u128* row = row0 + a.dig_off[i] + static_cast<int64_t>(col) * nt;
+            u128 E[K];
+#pragma unroll
+            for (int t = 0; t < nt; ++t) E[t] = row[t];
+            const u128 H = aes_encrypt(aes, cf.finish());
+            if (valid) {
+#pragma unroll
+                for (int t = 0; t < K - 1 - i; ++t) PS[static_cast<int64_t>(mrs_pair<K>(i, i + 1 + t)) * N] = E[t] - H;
+            }
+            if (MODE != 1) acc = add_packed(acc, E[K - 1 - i] - H, a.hmask);
+        }
+        if (MODE >= 1) {
+            const ModC m = mc[a.crt.p[0]];
+            const int n = static_cast<int>(m.n);
+            const act_t* L = x.p[0] + static_cast<int64_t>(b) * n * N;
+            CompressFwd cf;
+            cf.init();
+            for (int c0 = 0; c0 < n; c0 += kMrsCap) {
+                const int cnt = min(kMrsCap, n - c0);
+                __syncthreads();
+                lds_stage_rows<kMrsBS, kStageU>(stg, L, N, e0, c0, cnt);
+                __syncthreads();
+                for (int c = 0; c < cnt; ++c) cf.push(stg[c * kMrsBS + tid], m);
+            }
+            u128 key = cf.finish();
+#pragma unroll
+            for (int l = 0; l < K - 1; ++l) key ^= PS[static_cast<int64_t>(mrs_pair<K>(l, K - 1)) * N];
+            const uint32_t c = static_cast<uint32_t>(key) & 1u;
+            u128 E = 0;
+            if (MODE == 2) E = row0[a.dig_off[K - 1] + c];
+            const u128 H = aes_encrypt(aes, key);
+            if (valid) {
+                a.hs[static_cast<int64_t>(b) * N + e] = H;
+                a.cs[static_cast<int64_t>(b) * N + e] = static_cast<uint8_t>(c);
+            }
+            if (MODE == 2) acc = add_packed(acc, E - H, a.hmask);
+        }
+        if (MODE == 1) continue;
+        const uint32_t colf = static_cast<uint32_t>(acc) & static_cast<uint32_t>(a.T - 1);
+        const u128* row = row0 + a.fin_off + static_cast<int64_t>(colf) * K;
+        u128 F[K];
+#pragma unroll
+        for (int j = 0; j < K; ++j) F[j] = row[j];
+        const u128 H = aes_encrypt(aes, acc);
+        if (valid) {
+#pragma unroll
+            for (int j = 0; j < K; ++j) a.pf[(static_cast<int64_t>(b) * K + j) * N + e] = F[j] - H;
+        }
+    }
+}
+
+static inline bool mrs_staged(int64_t N) { return stage_ok(N, kMrsBS); }
+
 // Output: Y_0 = pf_0 (mod 2), Y_j = S^-1 L_j + pf_j (mod p_j), in place. grid (ceil(N/256), k, B)
 __global__ __launch_bounds__(256) void k_rescale_mrs_out(MrsArgs a, Act x, const ModC* mc) {
     const int j = blockIdx.y, b = blockIdx.z;
@@ -898,6 +1115,57 @@ __global__ __launch_bounds__(kAesBlock, kAesMinBlocks) void k_rescale_mrs_out_ha
         }
         a.colx[bke] = static_cast<uint16_t>(c0);
         a.hx[bke] = aes_encrypt(aes, cf.finish());
+    }
+}
+
+// k_rescale_mrs_out_hash with the label staged in LDS (stage_ok): a block = (512-element tile, residue j,
+// GC b) walks the label kOhCap components per pass: stage the rows, each lane rewrites its column in place,
+// store the rows back (residue 0 only writes the decompressed payload).
+constexpr int kOhBS = 512;
+constexpr int kOhCap = 32;  // 16 KiB image beside the 32 KiB AES image: three blocks per CU
+__global__ __launch_bounds__(kOhBS, kAesMinBlocks) void k_rescale_mrs_out_hash_s(MrsArgs a, Act x, const ModC* mc,
+                                                                               const uint32_t* te0, const uint32_t* rk) {
+    AES_PROLOGUE(te0, rk);
+    __shared__ __attribute__((aligned(16))) uint8_t stg[kOhCap * kOhBS];
+    const int j = blockIdx.y, b = blockIdx.z;
+    const int64_t N = a.N;
+    const int k = a.crt.k;
+    const ModC m = mc[a.crt.p[j]];
+    const int n = static_cast<int>(m.n);
+    const int tid = static_cast<int>(threadIdx.x);
+    act_t* L = x.p[j] + static_cast<int64_t>(b) * n * N;
+    const uint32_t inv = static_cast<uint32_t>(a.sinv[j]);
+    for (int64_t e0 = static_cast<int64_t>(blockIdx.x) * kOhBS; e0 < N; e0 += static_cast<int64_t>(gridDim.x) * kOhBS) {
+        const bool valid = e0 + tid < N;
+        const int64_t bke = (static_cast<int64_t>(b) * k + j) * N + (valid ? e0 + tid : N - 1);
+        const u128 P = a.pf[bke];
+        DigitStream s;
+        s.init(P);
+        CompressFwd cf;
+        cf.init();
+        uint32_t c0 = 0;
+        for (int q0 = 0; q0 < n; q0 += kOhCap) {
+            const int cnt = min(kOhCap, n - q0);
+            __syncthreads();  // the previous pass's stores have read the image
+            if (j != 0) {
+                lds_stage_rows<kOhBS, 2>(stg, L, N, e0, q0, cnt);
+                __syncthreads();
+            }
+            for (int c = 0; c < cnt; ++c) {
+                uint8_t& w = stg[c * kOhBS + tid];
+                const uint32_t v = j == 0 ? s.next(m) : modq(static_cast<uint32_t>(w) * inv + s.next(m), m);
+                if (q0 + c == 0) c0 = v;
+                w = static_cast<uint8_t>(v);
+                if (j != 0) cf.push(v, m);
+            }
+            __syncthreads();
+            lds_store_rows<kOhBS>(L, stg, N, e0, q0, cnt);
+        }
+        const u128 H = aes_encrypt(aes, j == 0 ? P : cf.finish());
+        if (valid) {
+            a.colx[bke] = static_cast<uint16_t>(c0);
+            a.hx[bke] = H;
+        }
     }
 }
 
@@ -1029,10 +1297,15 @@ void launch_relu_mrs(const MrsArgs& a, const SignArgs& sa, const Act& x, const A
                      const u128* etab, int B, const ModC* mc, const AesGlobals& g, hipStream_t st) {
     hipLaunchKernelGGL(k_label_hash, AES_LAUNCH(a.N, a.crt.k, B), kAesLds, st, x, a.crt, a.N,
                        sa.hx, sa.colx, mc, g.te0, g.rk);
-    const dim3 gc = grid_aes(a.N, aes_bs(a.N, 1, B), 1, B), bc(aes_bs(a.N, 1, B));
+    const bool stg = mrs_staged(a.N);
+    const dim3 gc = stg ? grid_aes(a.N, kMrsBS, 1, B) : grid_aes(a.N, aes_bs(a.N, 1, B), 1, B);
+    const dim3 bc(stg ? kMrsBS : aes_bs(a.N, 1, B));
     switch (a.crt.k) {
 #define DASH_MRS_K(KK) \
-        case KK: hipLaunchKernelGGL((k_mrs_chain<KK, 1>), gc, bc, kAesLds, st, a, x, mc, g.te0, g.rk); break;
+        case KK: \
+            if (stg) hipLaunchKernelGGL((k_mrs_chain_s<KK, 1>), gc, bc, 0, st, a, x, mc, g.te0, g.rk); \
+            else hipLaunchKernelGGL((k_mrs_chain<KK, 1>), gc, bc, kAesLds, st, a, x, mc, g.te0, g.rk); \
+            break;
         DASH_MRS_K(2) DASH_MRS_K(3) DASH_MRS_K(4) DASH_MRS_K(5) DASH_MRS_K(6) DASH_MRS_K(7) DASH_MRS_K(8)
         DASH_MRS_K(9) DASH_MRS_K(10) DASH_MRS_K(11) DASH_MRS_K(12)
 #undef DASH_MRS_K
@@ -1052,11 +1325,15 @@ void launch_relu_joint(const SignArgs& sa, const Act& x, const Act& y, const u12
 
 void launch_rescale_mrs(const MrsArgs& a, const Act& x, int B, const ModC* mc, const AesGlobals& g, hipStream_t st,
                         bool chain_only) {
-    const dim3 gc = grid_aes(a.N, aes_bs(a.N, 1, B), 1, B), bc(aes_bs(a.N, 1, B));
+    const bool stg = mrs_staged(a.N);
+    const dim3 gc = stg ? grid_aes(a.N, kMrsBS, 1, B) : grid_aes(a.N, aes_bs(a.N, 1, B), 1, B);
+    const dim3 bc(stg ? kMrsBS : aes_bs(a.N, 1, B));
     switch (a.crt.k) {
 #define DASH_MRS_K(KK) \
         case KK: \
-            if (a.mode == 2) hipLaunchKernelGGL((k_mrs_chain<KK, 2>), gc, bc, kAesLds, st, a, x, mc, g.te0, g.rk); \
+            if (stg && a.mode == 2) hipLaunchKernelGGL((k_mrs_chain_s<KK, 2>), gc, bc, 0, st, a, x, mc, g.te0, g.rk); \
+            else if (stg) hipLaunchKernelGGL((k_mrs_chain_s<KK, 0>), gc, bc, 0, st, a, x, mc, g.te0, g.rk); \
+            else if (a.mode == 2) hipLaunchKernelGGL((k_mrs_chain<KK, 2>), gc, bc, kAesLds, st, a, x, mc, g.te0, g.rk); \
             else hipLaunchKernelGGL((k_mrs_chain<KK, 0>), gc, bc, kAesLds, st, a, x, mc, g.te0, g.rk); \
             break;
         DASH_MRS_K(2) DASH_MRS_K(3) DASH_MRS_K(4) DASH_MRS_K(5) DASH_MRS_K(6) DASH_MRS_K(7) DASH_MRS_K(8)
@@ -1065,7 +1342,10 @@ void launch_rescale_mrs(const MrsArgs& a, const Act& x, int B, const ModC* mc, c
         default: std::fprintf(stderr, "dash: mixed-radix rescale supports 2..12 CRT residues\n"); std::abort();
     }
     if (chain_only) return;  // the joint ReLU's k_rescale_relu_out writes the outputs
-    if (a.mode == 2)
+    if (a.mode == 2 && stage_ok(a.N, kOhBS))
+        hipLaunchKernelGGL(k_rescale_mrs_out_hash_s, grid_aes(a.N, kOhBS, a.crt.k, B), dim3(kOhBS), 0, st, a, x, mc,
+                           g.te0, g.rk);
+    else if (a.mode == 2)
         hipLaunchKernelGGL(k_rescale_mrs_out_hash, AES_LAUNCH(a.N, a.crt.k, B), kAesLds, st, a, x, mc, g.te0, g.rk);
     else
         hipLaunchKernelGGL(k_rescale_mrs_out, dim3(static_cast<unsigned>((a.N + 255) / 256), a.crt.k, B), dim3(256), 0,
@@ -1255,6 +1535,12 @@ void launch_unpack(const u128* P, int nres, const Act& out, const CrtInfo& mods,
 }
 void launch_relu_mult(const SignArgs& a, const Act& x, const Act& y, const u128* gtab, const u128* etab,
                       const ModC* mc, hipStream_t st) {
+    if (stage_ok(a.N, kRmBS) && x.p[0] != y.p[0]) {
+        const unsigned nx = static_cast<unsigned>(std::min<int64_t>((a.N + kRmBS - 1) / kRmBS,
+                                                                   std::max(1, 16 * num_cus() / (a.crt.k * a.B))));
+        hipLaunchKernelGGL(k_relu_mult_s, dim3(nx, a.crt.k, a.B), dim3(kRmBS), 0, st, a, x, y, gtab, etab, mc);
+        return;
+    }
     hipLaunchKernelGGL(k_relu_mult, grid_for(a.N, 256, a.crt.k, a.B), dim3(256), 0, st, a, x, y, gtab, etab, mc);
 }
 void launch_rescale_hash(const Act& x, int fi, int s, const int16_t* up, int up_stride, int add_up, int64_t N, int B,

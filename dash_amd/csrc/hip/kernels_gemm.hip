@@ -386,16 +386,15 @@ __global__ __launch_bounds__(256) void k_conv_img2(ConvArgs a, Act x, Act y, int
         static_cast<uint32_t>(p) * (static_cast<uint32_t>(a.Kpad * half) * xmax / static_cast<uint32_t>(p) + 1);
     // col -> (output row in band, column): multiply-high by ceil(2^32 / OW) is exact for col < 2^23
     const uint32_t owm = a.OW > 1 ? 0xffffffffu / static_cast<uint32_t>(a.OW) + 1u : 0u;
-    // per-lane epilogue constants of its 4 filter rows, loaded once (a dependent global load per output
-    // inside the column loop cost a round trip per 64-column chunk); combined after the barrier
-    uint32_t zq[4] = {0u, 0u, 0u, 0u}, bq[4] = {0u, 0u, 0u, 0u};
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-        const int f = fw + (lane >> 4) * 4 + r;
-        if (f < a.F) {
-            zq[r] = static_cast<uint32_t>(zcp[f]);
-            bq[r] = static_cast<uint16_t>(bias[(static_cast<int64_t>(b) * a.F + f) * n + c]);
-        }
+    // Transposed product: the MFMA runs with the image as A and the filters as B, so a lane's 4 accumulator
+    // rows are 4 consecutive output positions of ONE filter (fw + lane % 16): the epilogue stores them as one
+    // dword (4 output bytes) instead of 4 byte stores, and needs one filter's constants per lane. Loaded
+    // once (a dependent global load per output inside the column loop cost a round trip per 64 columns).
+    const int fl = fw + (lane & 15);
+    uint32_t zq = 0u, bq = 0u;
+    if (fl < a.F) {
+        zq = static_cast<uint32_t>(zcp[fl]);
+        bq = static_cast<uint16_t>(bias[(static_cast<int64_t>(b) * a.F + fl) * n + c]);
     }
     // stage the band: item = (4 channels, 8 columns, row), channel groups fastest across lanes (the
     // channel-last dword stores of a lane group then cover consecutive banks); 4 x 8-B loads -> 8 dwords.
@@ -563,10 +562,10 @@ __global__ __launch_bounds__(256) void k_conv_img2(ConvArgs a, Act x, Act y, int
     if (fw >= a.F) return;  // wave-uniform; no barrier follows
     const int ncol = (oy1 - oy0) * a.OW;
     const int npos = a.OH * a.OW;
-    uint32_t addc[4];
-#pragma unroll
-    for (int r = 0; r < 4; ++r) addc[r] = off + zq[r] * static_cast<uint32_t>(zv) + bq[r];
+    const uint32_t addc = off + zq * static_cast<uint32_t>(zv) + bq;
     act_t* Y = y.p[j] + (static_cast<int64_t>(b) * n + c) * a.F * npos;
+    // dword stores need 4-byte aligned filter rows and band starts
+    const bool dw = (npos & 3) == 0 && ((oy0 * a.OW) & 3) == 0;
     const uint32_t mq = a.mq[j];
     // tap offsets of the A-in-VGPR path, once per block (the k-step loop then only adds)
     int toff[AREG ? KSC : 1];
@@ -608,7 +607,7 @@ __global__ __launch_bounds__(256) void k_conv_img2(ConvArgs a, Act x, Act y, int
                 }
                 __builtin_amdgcn_sched_barrier(0);  // keep the reads ahead (the scheduler otherwise sinks them)
 #pragma unroll
-                for (int t = 0; t < 4; ++t) acc[t] = __builtin_amdgcn_mfma_i32_16x16x64_i8(av[s], bcur[t], acc[t], 0, 0, 0);
+                for (int t = 0; t < 4; ++t) acc[t] = __builtin_amdgcn_mfma_i32_16x16x64_i8(bcur[t], av[s], acc[t], 0, 0, 0);
                 __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
                 for (int t = 0; t < 4; ++t) bcur[t] = bnxt[t];
@@ -622,23 +621,32 @@ __global__ __launch_bounds__(256) void k_conv_img2(ConvArgs a, Act x, Act y, int
 #pragma unroll
                         for (int t = 0; t < 4; ++t) {
                             const v2l bv = *reinterpret_cast<const v2l*>(img + base[t] + offs);
-                            acc[t] = __builtin_amdgcn_mfma_i32_16x16x64_i8(av1, bv, acc[t], 0, 0, 0);
+                            acc[t] = __builtin_amdgcn_mfma_i32_16x16x64_i8(bv, av1, acc[t], 0, 0, 0);
                         }
                     }
         }
+        if (fl < a.F) {
 #pragma unroll
-        for (int t = 0; t < 4; ++t) {
-            if (!ok[t]) continue;
-            const int pos = oy0 * a.OW + col0 + t * 16 + (lane & 15);  // band rows are whole output rows
+            for (int t = 0; t < 4; ++t) {
+                // rows r = 0..3: positions col0 + 16 t + 4 (lane / 16) + r of filter fl (band rows are whole output rows)
+                const int cb = col0 + t * 16 + (lane >> 4) * 4;
+                const int pos = oy0 * a.OW + cb;
+                uint32_t o[4];
 #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int f = fw + (lane >> 4) * 4 + r;
-                if (f >= a.F) continue;
-                const uint32_t v = static_cast<uint32_t>(acc[t][r]) + addc[r];
+                for (int r = 0; r < 4; ++r) o[r] = modq_conv(static_cast<uint32_t>(acc[t][r]) + addc, static_cast<uint32_t>(p), mq);
+                act_t* yr = Y + static_cast<int64_t>(fl) * npos + pos;
 #ifdef DASH_FAKE_CONV_NOSTORE
-                if (v == 0xdeadbeefu)  // A/B bound analysis only: never true, keeps the math
+                if (o[0] == 0xdeadbeefu)  // A/B bound analysis only: never true, keeps the math
 #endif
-                Y[static_cast<int64_t>(f) * npos + pos] = static_cast<act_t>(modq_conv(v, static_cast<uint32_t>(p), mq));
+                {
+                    if (dw && cb + 3 < ncol) {
+                        *reinterpret_cast<uint32_t*>(yr) = o[0] | (o[1] << 8) | (o[2] << 16) | (o[3] << 24);
+                    } else {
+#pragma unroll
+                        for (int r = 0; r < 4; ++r)
+                            if (cb + r < ncol) yr[r] = static_cast<act_t>(o[r]);
+                    }
+                }
             }
         }
     }

@@ -29,8 +29,8 @@ using namespace hostutil;
 // ---------------------------------------------------------------------------
 class HipEvaluator {
    public:
-    HipEvaluator(std::shared_ptr<GarbledModel> tmpl, int B, int device, bool use_mfma)
-        : tmpl_(std::move(tmpl)), mfma_(use_mfma) {
+    HipEvaluator(std::shared_ptr<GarbledModel> tmpl, int B, int device, bool use_mfma, bool stream_tables = false)
+        : tmpl_(std::move(tmpl)), mfma_(use_mfma), stream_(stream_tables) {
         DASH_CHECK(tmpl_ && B >= 1, "HipEvaluator needs a template model and B >= 1");
         int ndev = 0;
         if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0)
@@ -97,6 +97,11 @@ class HipEvaluator {
         return s;
     }
     ~HipEvaluator() {
+        if (copy_st_) (void)hipStreamSynchronize(copy_st_);
+        for (auto e : ready_) (void)hipEventDestroy(e);
+        for (auto e : done_) (void)hipEventDestroy(e);
+        if (run_end_) (void)hipEventDestroy(run_end_);
+        if (copy_st_) (void)hipStreamDestroy(copy_st_);
         if (load_st_) (void)hipStreamDestroy(load_st_);
         if (gexec_) (void)hipGraphExecDestroy(gexec_);
         for (void* p : allocs_) (void)hipFree(p);
@@ -104,6 +109,7 @@ class HipEvaluator {
     }
 
     int batch() const { return B_; }
+    bool streams_tables() const { return stream_; }
     size_t device_bytes() const { return dev_bytes_; }
     size_t table_bytes() const { return table_bytes_; }
 
@@ -305,6 +311,7 @@ class HipEvaluator {
     // one device buffer holding array `name` of layer li of every GC slot
     const u128* upload_tables(size_t li, const std::string& name) {
         const size_t nb = tmpl_->layers[li].arr(name).nbytes;
+        if (stream_) return stream_table(li, name, nb);
         uint8_t* d = dalloc<uint8_t>(nb * B_);
         arena_[{li, name}] = {d, nb};
         loaders_.push_back([this, d, nb, li, name](int b, const GarbledModel& m) {
@@ -314,6 +321,72 @@ class HipEvaluator {
         });
         table_bytes_ += nb * B_;
         return reinterpret_cast<const u128*>(d);
+    }
+    // Streamed tables (stream_tables): every GC's copy of the array lives in pinned host memory; the layer's
+    // tables of all B slots are copied into one of three rotating HBM windows on a copy stream one layer
+    // ahead of their use (stage_layer), so the device holds at most three layers of tables. For models (or
+    // batches) whose tables exceed the HBM pool; the reference uploads every table at load (sign_gadget.h
+    // cuda_move, 708-734). Three windows because a joint rescale's op runs in the next layer, reading its
+    // own layer's tables: layer x's window is reused by layer x + 3 only after layer x + 1 has finished.
+    const u128* stream_table(size_t li, const std::string& name, size_t nb) {
+        const size_t span = (nb * B_ + 255) / 256 * 256;
+        DASH_CHECK(woff_[li] + span <= win_bytes_, "streamed tables: layer window overflow");
+        uint8_t* d = win_[li % 3] + woff_[li];
+        woff_[li] += span;
+        uint8_t* h = nullptr;
+        HIPCHECK(hipHostMalloc(reinterpret_cast<void**>(&h), std::max<size_t>(16, nb * B_)));
+        host_allocs_.push_back(h);
+        stabs_[li].push_back(StreamTab{d, h, nb});
+        loaders_.push_back([h, nb, li, name](int b, const GarbledModel& m) {
+            const Array& a = m.layers[li].arr(name);
+            DASH_CHECK(a.nbytes == nb, "table size mismatch across batch");
+            if (a.device_resident() && !a.dev->host)
+                HIPCHECK(hipMemcpy(h + nb * b, a.device_ptr(), nb, hipMemcpyDeviceToHost));
+            else
+                std::memcpy(h + nb * b, a.ptr<uint8_t>(), nb);
+        });
+        table_bytes_ += nb * B_;
+        return reinterpret_cast<const u128*>(d);
+    }
+    // Op at the start of layer li's ops: layer li - 2 is done (its window may be refilled), layer li + 1's
+    // tables go up on the copy stream (layer 0's too, at li = 0), and the evaluation waits for layer li's.
+    void stage_layer(size_t li, hipStream_t st) {
+        if (li >= 2) HIPCHECK(hipEventRecord(done_[li - 2], st));
+        auto issue = [&](size_t x) {
+            if (x >= stabs_.size() || stabs_[x].empty()) return;
+            if (x >= 3) HIPCHECK(hipStreamWaitEvent(copy_st_, done_[x - 3], 0));
+            else if (run_end_recorded_) HIPCHECK(hipStreamWaitEvent(copy_st_, run_end_, 0));  // the previous run's
+            for (const auto& t : stabs_[x])
+                HIPCHECK(hipMemcpyAsync(t.d, t.h, t.nb * B_, hipMemcpyHostToDevice, copy_st_));
+            HIPCHECK(hipEventRecord(ready_[x], copy_st_));
+        };
+        if (li == 0) issue(0);
+        issue(li + 1);
+        if (!stabs_[li].empty()) HIPCHECK(hipStreamWaitEvent(st, ready_[li], 0));
+    }
+    void stage_end(hipStream_t st) {
+        HIPCHECK(hipEventRecord(run_end_, st));
+        run_end_recorded_ = true;
+    }
+    void init_streaming(const GarbledModel& m0) {
+        const size_t L = m0.layers.size();
+        size_t most = 256;
+        for (const auto& l : m0.layers) {
+            size_t s = 0;
+            for (const auto& kv : l.a) s += (kv.second.nbytes * B_ + 255) / 256 * 256;
+            most = std::max(most, s);
+        }
+        win_bytes_ = most;
+        for (auto& w : win_) w = dalloc<uint8_t>(win_bytes_);
+        woff_.assign(L, 0);
+        stabs_.assign(L, {});
+        ready_.resize(L);
+        done_.resize(L);
+        for (auto& e : ready_) HIPCHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        for (auto& e : done_) HIPCHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        HIPCHECK(hipEventCreateWithFlags(&run_end_, hipEventDisableTiming));
+        HIPCHECK(hipStreamCreateWithFlags(&copy_st_, hipStreamNonBlocking));
+        use_graph_ = false;  // the copy stream's waits on the previous run are issued per run
     }
     const int16_t* upload_i16_rows(size_t li, const std::string& name) {
         const size_t nb = tmpl_->layers[li].arr(name).nbytes;
@@ -418,6 +491,21 @@ class HipEvaluator {
     ModelHeader tmpl_h_;
     size_t tmpl_nlayers_ = 0;
     bool mfma_;
+    // streamed tables (stream_table / stage_layer)
+    bool stream_ = false;
+    struct StreamTab {
+        uint8_t* d;  // window address of slot 0 ([B][nb])
+        uint8_t* h;  // pinned host copy ([B][nb])
+        size_t nb;
+    };
+    uint8_t* win_[3] = {};
+    size_t win_bytes_ = 0;
+    std::vector<size_t> woff_;
+    std::vector<std::vector<StreamTab>> stabs_;
+    hipStream_t copy_st_ = nullptr;
+    std::vector<hipEvent_t> ready_, done_;
+    hipEvent_t run_end_ = nullptr;
+    bool run_end_recorded_ = false;
     std::vector<std::function<void(int, const GarbledModel&)>> loaders_;
     struct SmallLoad {
         size_t off = 0;
@@ -637,9 +725,11 @@ void HipEvaluator::build() {
         saved_mods[slot] = md;
     };
     save_if_needed(0, cur, N, mods);
+    if (stream_) init_streaming(m0);
 
     for (size_t li = 0; li < m0.layers.size(); ++li) {
         const GLayer& g = m0.layers[li];
+        if (stream_) add_op("stage", [this, li](hipStream_t st) { stage_layer(li, st); });
         const int nxt = (cur + 1) % 2;
         const std::string lname = std::string(kind_name(g.kind)) + "#" + std::to_string(li);
         if (g.p.count("in_src")) {
@@ -1205,6 +1295,7 @@ void HipEvaluator::build() {
         }
         save_if_needed(li + 1, cur, N, mods);
     }
+    if (stream_) add_op("stage_end", [this](hipStream_t st) { stage_end(st); });
     final_ = act_of(cur);
     Nout_ = N;
     out_mod_ = mods;
@@ -1401,10 +1492,12 @@ void register_hip_bindings(py::module_& m) {
         return std::string(buf);
     });
     py::class_<HipEvaluator, std::shared_ptr<HipEvaluator>>(m, "HipEvaluator")
-        .def(py::init([](std::shared_ptr<GarbledModel> tmpl, int B, int device, bool mfma) {
-                 return std::make_shared<HipEvaluator>(std::move(tmpl), B, device, mfma);
+        .def(py::init([](std::shared_ptr<GarbledModel> tmpl, int B, int device, bool mfma, bool stream_tables) {
+                 return std::make_shared<HipEvaluator>(std::move(tmpl), B, device, mfma, stream_tables);
              }),
-             py::arg("template"), py::arg("batch"), py::arg("device") = 0, py::arg("mfma") = true)
+             py::arg("template"), py::arg("batch"), py::arg("device") = 0, py::arg("mfma") = true,
+             py::arg("stream_tables") = false)
+        .def_property_readonly("streams_tables", &HipEvaluator::streams_tables)
         .def("load", [](HipEvaluator& h, int b, std::shared_ptr<GarbledModel> m) {
             py::gil_scoped_release rel;
             h.load(b, *m);

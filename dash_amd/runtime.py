@@ -32,10 +32,14 @@ def _stream_handle(stream) -> int:
 
 class HipEvaluator:
     def __init__(self, models: Sequence = (), device: int = 0, mfma: bool = True, profile: bool = False,
-                 template=None, batch: Optional[int] = None):
+                 template=None, batch: Optional[int] = None, stream_tables: bool = False):
         """Either pass all `models` (uploaded immediately), or a `template`
         model plus a `batch` size and stream models in with `load(b, m)` so
-        that host memory never holds more than one garbled model."""
+        that host memory never holds more than one garbled model.
+
+        stream_tables: keep the garbled tables in pinned host memory and copy each layer's tables into
+        one of three rotating HBM windows one layer ahead of its use (for models or batches whose tables
+        exceed the device's HBM; the tables then cross PCIe on every run)."""
         n = native()
         if n.hip_device_count() == 0:
             raise RuntimeError("dash_amd: no HIP device visible; HipEvaluator needs an MI355X (gfx950)")
@@ -45,7 +49,7 @@ class HipEvaluator:
                 raise ValueError("need models or a template")
             template = models[0]
         B = batch if batch is not None else len(models)
-        self._h = n.HipEvaluator(template, B, device, mfma)
+        self._h = n.HipEvaluator(template, B, device, mfma, stream_tables)
         for b, m in enumerate(models):
             self._h.load(b, m)
         if profile:
@@ -63,6 +67,10 @@ class HipEvaluator:
     @property
     def batch(self) -> int:
         return self._h.batch
+
+    @property
+    def streams_tables(self) -> bool:
+        return self._h.streams_tables
 
     def device_bytes(self) -> int:
         return self._h.device_bytes()
