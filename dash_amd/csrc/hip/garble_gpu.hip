@@ -534,91 +534,6 @@ __global__ __launch_bounds__(kPB, 4) void k_hash_jobs(Ctx c, Gadget g, In in, co
     }
 }
 
-// Key hashes by (projection, 64-element tile): a block stages the tile's input label chunks and the R_pin row
-// in LDS once (every load in flight at once), then its waves take the projection's colors two at a time
-// (two independent compress chains and one paired AES per lane). k_hash_jobs re-read the label from L1/L2
-// for every color, kLd chunks per round trip; here the colors' inner loops touch LDS only.
-template <int C>
-__global__ __launch_bounds__(kPB) void k_hash_g(Ctx c, Gadget g, In in) {
-    __shared__ __attribute__((aligned(16))) uint32_t lds_aes[aes_lds_words<C>()];
-    extern __shared__ __attribute__((aligned(16))) uint32_t dyn[];
-    aes_lds_fill<C>(lds_aes, c.te0);
-    const AesT<C> aes = aes_ctx<C>(lds_aes, nullptr);
-    u32x4a* A = reinterpret_cast<u32x4a*>(dyn);  // [chunk][64] input label chunks, then the R row's chunks
-    const int64_t N = g.N;
-    const int64_t tiles = (N + kTile - 1) / kTile;
-    const int np = g.nprojs;
-    const int64_t nw = tiles * np;
-    const int lane = static_cast<int>(threadIdx.x) & (kTile - 1);
-    const int wave = rfl(static_cast<int>(threadIdx.x) / kTile);
-    constexpr int kWv = kPB / kTile;
-    for (int64_t w = blockIdx.x; w < nw; w += gridDim.x) {
-        const int64_t tile = w / np;
-        const int pi = static_cast<int>(w - tile * np);
-        const Proj P = rfl_proj(g.projs[pi]);
-        const ModC mi = rfl_modc(c.mc[P.pin]);
-        const int n = static_cast<int>(mi.n), nc = static_cast<int>(chunks_of(n));
-        const uint32_t p = static_cast<uint32_t>(P.pin);
-        u32x4a* Rl = A + nc * kTile;
-        const int64_t e0 = tile * kTile;
-        {
-            constexpr int kU = 4;
-            const int tot = nc * kTile;
-            for (int x0 = threadIdx.x; x0 < tot; x0 += kU * kPB) {
-                u32x4a v[kU];
-#pragma unroll
-                for (int u = 0; u < kU; ++u) {
-                    const int x = x0 + u * kPB;
-                    if (x >= tot) continue;
-                    const int64_t e = min(e0 + (x & (kTile - 1)), N - 1);
-                    v[u] = ld_chunk(label_ref(c, g, in, e, P.in_kind, P.in_idx, P.pin), x >> 6);
-                }
-#pragma unroll
-                for (int u = 0; u < kU; ++u)
-                    if (x0 + u * kPB < tot) A[x0 + u * kPB] = v[u];
-            }
-            for (int x = threadIdx.x; x < nc; x += kPB) Rl[x] = ld_chunk(row_ref(c.R + static_cast<int64_t>(P.pin) * kW), x);
-        }
-        __syncthreads();
-        const int64_t e = e0 + lane;
-        const uint32_t x0 = A[lane][0] & 0xffffu;  // R[0] = 1: key i has color x0 + i
-        for (int col = 2 * wave; col < P.pin; col += 2 * kWv) {
-            const bool two = col + 1 < P.pin;
-            uint32_t i0 = static_cast<uint32_t>(col) + p - x0;
-            if (i0 >= p) i0 -= p;
-            uint32_t i1 = i0 + 1 == p ? 0 : i0 + 1;
-            CompressFwd k0, k1;
-            k0.init();
-            k1.init();
-            for (int c8 = 0; c8 < nc; ++c8) {
-                const u32x4a av = A[c8 * kTile + lane];
-                const u32x4a rv = Rl[c8];
-                const int q0 = c8 * 8;
-#pragma unroll
-                for (int u = 0; u < 8; ++u) {
-                    const uint32_t xv = (u & 1) ? (av[u >> 1] >> 16) : (av[u >> 1] & 0xffffu);
-                    const uint32_t y = (u & 1) ? (rv[u >> 1] >> 16) : (rv[u >> 1] & 0xffffu);
-                    if (q0 + u < n) {
-                        k0.push(modq(xv + i0 * y, mi), mi);
-                        k1.push(modq(xv + i1 * y, mi), mi);
-                    }
-                }
-            }
-            u128 H0, H1;
-            aes_encrypt2(aes, k0.finish(), k1.finish(), H0, H1);
-            if (e < N) {
-                g.HC[(P.first + col) * N + e] = H0;
-                g.CC[(P.first + col) * N + e] = static_cast<uint16_t>(i0);
-                if (two) {
-                    g.HC[(P.first + col + 1) * N + e] = H1;
-                    g.CC[(P.first + col + 1) * N + e] = static_cast<uint16_t>(i1);
-                }
-            }
-        }
-        __syncthreads();
-    }
-}
-
 // LDS AES image copies of the AES-bound kernels (A/B knob DASH_GG_AES_COPIES = 16 | 32): 32 copies are
 // bank-conflict free (64 KiB: 2 blocks per CU), 16 copies halve the image (2-way conflicts, more blocks)
 inline int gg_aes_copies() {
@@ -631,14 +546,13 @@ inline int gg_aes_copies() {
 inline auto draw_kernel() { return gg_aes_copies() == 16 ? k_draw<16> : k_draw<32>; }
 inline auto hash_kernel() { return gg_aes_copies() == 16 ? k_hash<16> : k_hash<32>; }
 inline auto hash_jobs_kernel() { return gg_aes_copies() == 16 ? k_hash_jobs<16> : k_hash_jobs<32>; }
-// DASH_GG_HASH=entry: one wave per (tile, entry) (k_hash); jobs: per (tile, hash job) (k_hash_jobs);
-// default: one block per (tile, projection), label staged in LDS (k_hash_g)
-inline int gg_hash_mode() {
-    static const int v = [] {
+// DASH_GG_HASH=entry: one wave per (tile, entry) (k_hash); default: per (tile, hash job) (k_hash_jobs).
+// (A block per (tile, projection) with the label staged in LDS was slower, 9.8 -> 17.6 ms per 4 GCs: most
+// projections have 3-17 colors, so most of a block's waves idled at its barriers; profiles/ab/README.md.)
+inline bool gg_hash_jobs() {
+    static const bool v = [] {
         const char* e = std::getenv("DASH_GG_HASH");
-        if (e && std::string(e) == "entry") return 0;
-        if (e && std::string(e) == "jobs") return 1;
-        return 2;
+        return !(e && std::string(e) == "entry");
     }();
     return v;
 }
@@ -710,105 +624,6 @@ __global__ __launch_bounds__(256) void k_bank(Ctx c, Gadget g, In in, const Bank
         else push_lin<false, false>(pc, slot_ref(g, slot, e), LRef{in.p[res] + e * in.es[res], in.cs[res]}, f, mo);
         if (e_raw < N) g.BK[static_cast<int64_t>(row) * N + e] = pc.finish();
     }
-}
-
-// Bank payloads by label group: the rows of a scope that share a slot label, output modulus and offset label
-// (the values v of one fan-out target, of one F_MULR / F_NEGR projection) are one group. A block owns
-// (group, 64-element tile): its 256 threads load the tile's slot label (and the input offset label) into LDS
-// with every chunk load in flight at once, then each wave computes the compressed payload of one value v at
-// a time from LDS. A label is read from HBM once per group instead of once per row: with one wave per row
-// the rows of a group ran in blocks spread over the 8 XCDs, so the re-reads missed their XCD's L2.
-struct BankGroup {
-    int slot, pout, res;  // payload = slot label + v * (res < 0 ? R_pout : input label of residue res) mod pout
-    int first, count;     // its (row, v) items
-};
-struct BankItem {
-    int row, v;
-};
-constexpr int kBGT = 256;  // k_bank_g threads
-__global__ __launch_bounds__(kBGT) void k_bank_g(Ctx c, Gadget g, In in, const BankGroup* grp, const BankItem* items,
-                                                int ngrp) {
-    extern __shared__ __attribute__((aligned(16))) uint32_t dyn[];
-    u32x4a* A = reinterpret_cast<u32x4a*>(dyn);  // [chunk][64] slot label chunks of the tile
-    const int64_t N = g.N;
-    const int64_t tiles = (N + kTile - 1) / kTile;
-    const int64_t nw = tiles * ngrp;
-    const int lane = static_cast<int>(threadIdx.x) & (kTile - 1);
-    const int wave = rfl(static_cast<int>(threadIdx.x) / kTile);
-    for (int64_t w = blockIdx.x; w < nw; w += gridDim.x) {
-        const int64_t tile = w / ngrp;
-        const int gi = static_cast<int>(w - tile * ngrp);
-        const int slot = rfl(grp[gi].slot), pout = rfl(grp[gi].pout), res = rfl(grp[gi].res);
-        const int first = rfl(grp[gi].first), count = rfl(grp[gi].count);
-        const ModC mo = rfl_modc(c.mc[pout]);
-        const int n = static_cast<int>(mo.n), nc = static_cast<int>(chunks_of(n));
-        u32x4a* B = A + nc * kTile;  // [chunk][64] input offset label chunks (res >= 0), else the R_pout row
-        const int64_t e0 = tile * kTile;
-        if (res < 0)
-            for (int x = threadIdx.x; x < nc; x += kBGT) B[x] = ld_chunk(row_ref(c.R + static_cast<int64_t>(pout) * kW), x);
-        {
-            constexpr int kU = 4;  // chunk loads in flight per thread
-            const int tot = nc * kTile * (res >= 0 ? 2 : 1);
-            for (int x0 = threadIdx.x; x0 < tot; x0 += kU * kBGT) {
-                u32x4a v[kU];
-#pragma unroll
-                for (int u = 0; u < kU; ++u) {
-                    const int x = x0 + u * kBGT;
-                    if (x >= tot) continue;
-                    const int half = x >= nc * kTile, xx = half ? x - nc * kTile : x;
-                    const int c8 = xx >> 6;
-                    const int64_t e = min(e0 + (xx & (kTile - 1)), N - 1);
-                    v[u] = half ? ld_chunk(LRef{in.p[res] + e * in.es[res], in.cs[res]}, c8)
-                                : ld_chunk(slot_ref(g, slot, e), c8);
-                }
-#pragma unroll
-                for (int u = 0; u < kU; ++u)
-                    if (x0 + u * kBGT < tot) A[x0 + u * kBGT] = v[u];
-            }
-        }
-        __syncthreads();
-        // two values per wave at a time: two independent compress chains (the push recurrences are serial)
-        const int64_t e = e0 + lane;
-        const int bl = res < 0 ? 0 : lane;  // the R row is one broadcast chunk per c8
-        const int bstride = res < 0 ? 1 : kTile;
-        for (int it = 2 * wave; it < count; it += 2 * (kBGT / kTile)) {
-            const bool two = it + 1 < count;
-            const int row0 = rfl(items[first + it].row);
-            const uint32_t f0 = rflu(static_cast<uint32_t>(items[first + it].v));
-            const int row1 = two ? rfl(items[first + it + 1].row) : row0;
-            const uint32_t f1 = two ? rflu(static_cast<uint32_t>(items[first + it + 1].v)) : f0;
-            CompressFwd p0, p1;
-            p0.init();
-            p1.init();
-            for (int c8 = 0; c8 < nc; ++c8) {
-                const u32x4a av = A[c8 * kTile + lane];
-                const u32x4a bv = B[c8 * bstride + bl];
-                const int q0 = c8 * 8;
-#pragma unroll
-                for (int u = 0; u < 8; ++u) {
-                    const uint32_t x = (u & 1) ? (av[u >> 1] >> 16) : (av[u >> 1] & 0xffffu);
-                    const uint32_t y = (u & 1) ? (bv[u >> 1] >> 16) : (bv[u >> 1] & 0xffffu);
-                    if (q0 + u < n) {
-                        p0.push(modq(x + f0 * y, mo), mo);
-                        p1.push(modq(x + f1 * y, mo), mo);
-                    }
-                }
-            }
-            if (e < N) {
-                g.BK[static_cast<int64_t>(row0) * N + e] = p0.finish();
-                if (two) g.BK[static_cast<int64_t>(row1) * N + e] = p1.finish();
-            }
-        }
-        __syncthreads();
-    }
-}
-// DASH_GG_BANK=row: one wave per (tile, bank row) (k_bank, A/B); default: per (tile, label group) (k_bank_g)
-inline bool gg_bank_groups() {
-    static const bool v = [] {
-        const char* e = std::getenv("DASH_GG_BANK");
-        return !(e && std::string(e) == "row");
-    }();
-    return v;
 }
 
 __global__ __launch_bounds__(kEB) void k_emit(Ctx c, Gadget g, In in, Tables tb, Emit em) {
@@ -1622,7 +1437,16 @@ struct ProjFns {
     const int* lut_off = nullptr;
 };
 
-constexpr size_t kEmitLds = 48 << 10;  // k_emit dynamic LDS budget per block
+// k_emit dynamic LDS budget per block (A/B knob DASH_GG_EMIT_LDS_KB): smaller scopes per block, more
+// resident blocks per CU to overlap one block's staging loads with another's table stores
+inline size_t emit_lds_budget() {
+    static const size_t v = [] {
+        const char* e = std::getenv("DASH_GG_EMIT_LDS_KB");
+        const int kb = e ? std::atoi(e) : 48;
+        return static_cast<size_t>(std::min(56, std::max(8, kb))) << 10;
+    }();
+    return v;
+}
 
 // The projections of a gadget: k_hash (one key hash per (element, color)), then k_emit over scopes. Host
 // preparation, cached by content per gadget structure (dconst): the per-table position maps, the scopes
@@ -1711,7 +1535,7 @@ void project(const gg::Ctx& c, gg::Gadget& g, const gg::In& in, const gg::Tables
             const auto& p = pr[pi];
             const bool overlap = p.table == gt && p.off < gend;
             const bool near = p.table == gt && p.off <= gend + 8 &&
-                              elem_bytes(gne + p.pin, gnb + rows_bound(p)) * 9 <= static_cast<int64_t>(kEmitLds);
+                              elem_bytes(gne + p.pin, gnb + rows_bound(p)) * 9 <= static_cast<int64_t>(emit_lds_budget());
             if (groups.empty() || !(overlap || near)) {
                 groups.push_back({});
                 gend = -1;
@@ -1784,7 +1608,7 @@ void project(const gg::Ctx& c, gg::Gadget& g, const gg::In& in, const gg::Tables
         const size_t fixed = static_cast<size_t>(S.span) * 4 + static_cast<size_t>(S.nbx) * 2 + 16;
         auto lds_of = [&](int sh) { return ((1u << sh) + 1) * per + fixed; };
         int tsh = 5;
-        while (tsh > 0 && lds_of(tsh) > kEmitLds) --tsh;
+        while (tsh > 0 && lds_of(tsh) > emit_lds_budget()) --tsh;
         DASH_CHECK(lds_of(tsh) <= (64u << 10) - sizeof(gg::EProj) * gg::kMaxDesc, "gpu garbler: projection scope exceeds LDS");
         S.tsh = tsh;
         lds_max = std::max(lds_max, lds_of(tsh));
@@ -1807,53 +1631,13 @@ void project(const gg::Ctx& c, gg::Gadget& g, const gg::In& in, const gg::Tables
     g.BK = bank_scratch(rows.size(), g.N);
     check_desc(g);
     const int64_t lanes = (g.N + gg::kTile - 1) / gg::kTile * gg::kTile;
-    if (!rows.empty() && gg::gg_bank_groups()) {
-        // label groups: the rows sharing (slot, pout, res), in first-row order
-        std::map<std::tuple<int, int, int>, int> gid;
-        std::vector<std::vector<gg::BankItem>> gitems;
-        std::vector<gg::BankGroup> grp;
-        for (int r = 0; r < static_cast<int>(rows.size()); ++r) {
-            const auto& br = rows[r];
-            auto key = std::make_tuple(br.slot, br.pout, br.res);
-            auto it = gid.find(key);
-            if (it == gid.end()) {
-                it = gid.emplace(key, static_cast<int>(grp.size())).first;
-                grp.push_back(gg::BankGroup{br.slot, br.pout, br.res, 0, 0});
-                gitems.emplace_back();
-            }
-            gitems[it->second].push_back(gg::BankItem{r, br.v});
-        }
-        std::vector<gg::BankItem> items;
-        size_t lds = 16;
-        for (size_t i = 0; i < grp.size(); ++i) {
-            grp[i].first = static_cast<int>(items.size());
-            grp[i].count = static_cast<int>(gitems[i].size());
-            items.insert(items.end(), gitems[i].begin(), gitems[i].end());
-            // slot label chunks of the tile, then the input label's (res >= 0) or the R_pout row's
-            const size_t nc = static_cast<size_t>(gg::chunks_of(nr_comps(grp[i].pout)));
-            lds = std::max(lds, (nc * gg::kTile + (grp[i].res >= 0 ? nc * gg::kTile : nc)) * 16);
-        }
-        DASH_CHECK(lds <= (64u << 10), "gpu garbler: bank group label exceeds LDS");
-        const int64_t nwork = (g.N + gg::kTile - 1) / gg::kTile * static_cast<int64_t>(grp.size());
-        hipLaunchKernelGGL(gg::k_bank_g, dim3(static_cast<unsigned>(std::min<int64_t>(nwork, 65536))), dim3(gg::kBGT),
-                           lds, gg::tl_st, c, g, in, gg::dconst(grp.data(), grp.size()),
-                           gg::dconst(items.data(), items.size()), static_cast<int>(grp.size()));
-    } else if (!rows.empty()) {
+    // (one block per label group with the label staged in LDS measured no faster, 7.2 -> 7.6-8.2 ms per 4 GCs:
+    // the payload compress chains, not the label reads, bound this kernel; profiles/ab/README.md)
+    if (!rows.empty()) {
         hipLaunchKernelGGL(gg::k_bank, dim3(blocks_for(lanes * static_cast<int64_t>(rows.size()), 256, 32768)), dim3(256), 0,
                            gg::tl_st, c, g, in, em.rows, static_cast<int>(rows.size()));
     }
-    if (gg::gg_hash_mode() == 2) {
-        size_t lds = 16;
-        for (const auto& p : pr) {
-            const size_t nc = static_cast<size_t>(gg::chunks_of(nr_comps(p.pin)));
-            lds = std::max(lds, (nc * gg::kTile + nc) * 16);
-        }
-        // the 32-copy AES image (64 KiB) while two blocks still fit a CU's 160 KiB, else the 16-copy one
-        const bool c32 = (64u << 10) + lds <= (80u << 10) && gg::gg_aes_copies() == 32;
-        const int64_t nwork = (g.N + gg::kTile - 1) / gg::kTile * static_cast<int64_t>(np);
-        hipLaunchKernelGGL(c32 ? gg::k_hash_g<32> : gg::k_hash_g<16>, dim3(static_cast<unsigned>(std::min<int64_t>(nwork, 65536))),
-                           dim3(gg::kPB), lds, gg::tl_st, c, g, in);
-    } else if (gg::gg_hash_mode() == 1) {
+    if (gg::gg_hash_jobs()) {
         std::vector<gg::HashJob> hj;
         for (int pi = 0; pi < np; ++pi)
             for (int c0 = 0; c0 < pr[pi].pin; c0 += gg::kHJ) hj.push_back(gg::HashJob{pi, c0});
@@ -2080,8 +1864,11 @@ struct GpuGarbler::Impl {
     int lut_off[kMaxRes] = {};
     ProjFns lut_fns() const { return ProjFns{nullptr, nullptr, &lut, lut_off}; }
     // sign base labels a sign_last mixed-radix rescale leaves for the next ReLU ([N][kW], relu_mult)
-    DevBlock sig;
+    // the sign label a sign_last mixed-radix rescale leaves in its scratch slot sig_slot (scratch at sig_S)
+    // for the next ReLU's relu_mult, which reuses that scratch in place (no copy out and back)
+    int sig_slot = -1;
     int64_t sig_N = 0;
+    const int16_t* sig_S = nullptr;
     explicit Impl(int dev) : lock(acquire_ctx(dev, dcp)), dc(*dcp), device(dev) {}
     template <class T>
     const T* stage(const T* h, size_t n) { return dc.stage(h, n); }
@@ -2107,7 +1894,6 @@ struct GpuGarbler::Impl {
         // garble() returns with every table written; blocks released below are reused in stream order
         (void)hipStreamSynchronize(dc.st);
         cur.clear();
-        sig = DevBlock();
     }
 };
 
@@ -2809,11 +2595,9 @@ void GpuGarbler::rescale_mrs(uint64_t layer, const RescaleMrsPlan& P, CrtLabels&
     project(I.c, g, in, tb, pr, ProjFns{&flut, &fan});
     if (P.sign_last) {
         // residue 0's key slot is the sign label of the ReLU that follows (relu_mult)
-        I.sig.alloc(I.device, static_cast<size_t>(N) * gg::kW * sizeof(int16_t));
+        I.sig_slot = a.key0;
         I.sig_N = N;
-        // the mod-2 key slot is a contiguous component-major block [128][N]
-        HIPCHECK(hipMemcpyAsync(I.sig.p, gg::slot_base(g, a.key0), static_cast<size_t>(N) * gg::kW * sizeof(int16_t),
-                                hipMemcpyDeviceToDevice, gg::tl_st));
+        I.sig_S = g.S;
     }
     HIPCHECK(hipGetLastError());
     gg::end_layer(tmp);
@@ -2822,7 +2606,7 @@ void GpuGarbler::rescale_mrs(uint64_t layer, const RescaleMrsPlan& P, CrtLabels&
     set_stale(cur, I.cur_mod, N);
 }
 
-// ReLU whose sign came out of the preceding mixed-radix rescale (RescaleMrsPlan::sign_last, I.sig): the
+// ReLU whose sign came out of the preceding mixed-radix rescale (RescaleMrsPlan::sign_last, I.sig_slot): the
 // mixed-modulus half gates only; device cur -> next base labels.
 void GpuGarbler::relu_mult(uint64_t layer, CrtLabels& cur, const std::vector<i64>* prefix, Array& mmg, Array& mme) {
     Impl& I = *impl_;
@@ -2831,8 +2615,11 @@ void GpuGarbler::relu_mult(uint64_t layer, CrtLabels& cur, const std::vector<i64
     PhaseTrace tr_("relu_mult");
     const int64_t N = I.cur_N;
     const int k = I.k;
-    DASH_CHECK(I.sig.p && I.sig_N == N, "gpu garbler: joint ReLU without a preceding sign-producing rescale");
-    const int sig_slot = 0, sk0 = 1, nslots = 1 + 2 * k;
+    DASH_CHECK(I.sig_slot >= 2 * k && I.sig_N == N, "gpu garbler: joint ReLU without a preceding sign-producing rescale");
+    // the rescale's scratch in place: the sign label stays in its slot, the mixed-multiply output labels take
+    // slots 0 .. 2k - 1 (the rescale's digit-target labels, dead by now); no slot above the sign is needed,
+    // so the grow-only scratch is not reallocated
+    const int sig_slot = I.sig_slot, sk0 = 0, nslots = sig_slot + 1;
     DevTable tG, tE;
     tG.alloc(I.device, N, mmg.shape[1], mmg);
     tE.alloc(I.device, N, static_cast<int64_t>(k) * 3, mme, true);
@@ -2851,10 +2638,9 @@ void GpuGarbler::relu_mult(uint64_t layer, CrtLabels& cur, const std::vector<i64
     g.sslot = 2;
     g.mask = 0;
     g.S = I.scratch(static_cast<size_t>(N) * nslots * gg::kW * sizeof(int16_t));
+    DASH_CHECK(g.S == I.sig_S, "gpu garbler: garbling scratch moved between the rescale and its joint ReLU");
     g.N = N;
     g.nslots = nslots;
-    HIPCHECK(hipMemcpyAsync(gg::slot_base(g, sig_slot), I.sig.p, static_cast<size_t>(N) * gg::kW * sizeof(int16_t),
-                            hipMemcpyDeviceToDevice, gg::tl_st));
     std::vector<DevBlock> out = relu_mult_gates(I, g, in, tb, sig_slot, sk0, *prefix);
     HIPCHECK(hipGetLastError());
     std::vector<void*> tmp;
@@ -2863,8 +2649,9 @@ void GpuGarbler::relu_mult(uint64_t layer, CrtLabels& cur, const std::vector<i64
     tG.to_array(mmg, I.device);
     tE.to_array(mme, I.device);
     I.cur = std::move(out);
-    I.sig = DevBlock();
+    I.sig_slot = -1;
     I.sig_N = 0;
+    I.sig_S = nullptr;
     set_stale(cur, I.crt, N);
 }
 
