@@ -534,6 +534,14 @@ __global__ __launch_bounds__(kPB, 4) void k_hash_jobs(Ctx c, Gadget g, In in, co
     }
 }
 
+// the 8 low bits (mod-2 components) of a chunk, component q at bit q
+__device__ __forceinline__ uint32_t bits8(const u32x4a& v) {
+    uint32_t b = 0;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) b |= ((v[u] & 1u) | ((v[u] >> 15) & 2u)) << (2 * u);
+    return b;
+}
+
 // LDS AES image copies of the AES-bound kernels (A/B knob DASH_GG_AES_COPIES = 16 | 32): 32 copies are
 // bank-conflict free (64 KiB: 2 blocks per CU), 16 copies halve the image (2-way conflicts, more blocks)
 inline int gg_aes_copies() {
@@ -547,8 +555,10 @@ inline auto draw_kernel() { return gg_aes_copies() == 16 ? k_draw<16> : k_draw<3
 inline auto hash_kernel() { return gg_aes_copies() == 16 ? k_hash<16> : k_hash<32>; }
 inline auto hash_jobs_kernel() { return gg_aes_copies() == 16 ? k_hash_jobs<16> : k_hash_jobs<32>; }
 // DASH_GG_HASH=entry: one wave per (tile, entry) (k_hash); default: per (tile, hash job) (k_hash_jobs).
-// (A block per (tile, projection) with the label staged in LDS was slower, 9.8 -> 17.6 ms per 4 GCs: most
-// projections have 3-17 colors, so most of a block's waves idled at its barriers; profiles/ab/README.md.)
+// Rejected (profiles/ab/README.md): a block per (tile, projection) with the label staged in LDS (9.8 -> 17.6 ms
+// per 4 GCs: most projections have 3-17 colors, most of the block's waves idled at its barriers), and a wave per
+// (tile, projection) stepping packed-byte keys x + i*R incrementally (22.1 ms: fewer, longer serial work items
+// and the unrolled compress's uniform constants spilled 146 SGPRs).
 inline bool gg_hash_jobs() {
     static const bool v = [] {
         const char* e = std::getenv("DASH_GG_HASH");
@@ -921,12 +931,6 @@ struct RsArgs {
 // gates of the sign output. A mod-2 label compresses to its component bits,
 // so the key is a bit pack and key 1 is key 0 XOR the bits of R_2. x is a
 // chunked label set (16 chunks of 8 components), add a uniform row.
-__device__ __forceinline__ uint32_t bits8(const u32x4a& v) {
-    uint32_t b = 0;
-#pragma unroll
-    for (int u = 0; u < 4; ++u) b |= ((v[u] & 1u) | ((v[u] >> 15) & 2u)) << (2 * u);
-    return b;
-}
 __global__ __launch_bounds__(kGB) void k_bin_keys(Ctx c, const int16_t* x, const int16_t* add, u128* hk, int64_t N) {
     __shared__ __attribute__((aligned(16))) uint32_t lds_aes[kGAesWords];
     aes_lds_fill<kGAes>(lds_aes, c.te0);
@@ -1631,8 +1635,8 @@ void project(const gg::Ctx& c, gg::Gadget& g, const gg::In& in, const gg::Tables
     g.BK = bank_scratch(rows.size(), g.N);
     check_desc(g);
     const int64_t lanes = (g.N + gg::kTile - 1) / gg::kTile * gg::kTile;
-    // (one block per label group with the label staged in LDS measured no faster, 7.2 -> 7.6-8.2 ms per 4 GCs:
-    // the payload compress chains, not the label reads, bound this kernel; profiles/ab/README.md)
+    // (rejected, profiles/ab/README.md: one block per label group with the label staged in LDS, 7.2 -> 7.6-8.2 ms
+    // per 4 GCs, and one wave per group stepping packed-byte payloads o + v*off incrementally, 10.7 ms)
     if (!rows.empty()) {
         hipLaunchKernelGGL(gg::k_bank, dim3(blocks_for(lanes * static_cast<int64_t>(rows.size()), 256, 32768)), dim3(256), 0,
                            gg::tl_st, c, g, in, em.rows, static_cast<int>(rows.size()));

@@ -1024,7 +1024,11 @@ __global__ __launch_bounds__(kMrsBS, MODE == 2 ? DASH_CHAIN2_WAVES : DASH_UA_MIN
     }
 }
 
-static inline bool mrs_staged(int64_t N) { return stage_ok(N, kMrsBS); }
+// the staged chain holds two 512-lane blocks per CU: below two blocks per CU (batch-1 latency) the per-lane form,
+// whose block size shrinks to spread a small launch over every CU, is faster
+static inline bool mrs_staged(int64_t N, int B) {
+    return stage_ok(N, kMrsBS) && (N + kMrsBS - 1) / kMrsBS * B >= 2 * num_cus();
+}
 
 // Output: Y_0 = pf_0 (mod 2), Y_j = S^-1 L_j + pf_j (mod p_j), in place. grid (ceil(N/256), k, B)
 __global__ __launch_bounds__(256) void k_rescale_mrs_out(MrsArgs a, Act x, const ModC* mc) {
@@ -1297,7 +1301,7 @@ void launch_relu_mrs(const MrsArgs& a, const SignArgs& sa, const Act& x, const A
                      const u128* etab, int B, const ModC* mc, const AesGlobals& g, hipStream_t st) {
     hipLaunchKernelGGL(k_label_hash, AES_LAUNCH(a.N, a.crt.k, B), kAesLds, st, x, a.crt, a.N,
                        sa.hx, sa.colx, mc, g.te0, g.rk);
-    const bool stg = mrs_staged(a.N);
+    const bool stg = mrs_staged(a.N, B);
     const dim3 gc = stg ? grid_aes(a.N, kMrsBS, 1, B) : grid_aes(a.N, aes_bs(a.N, 1, B), 1, B);
     const dim3 bc(stg ? kMrsBS : aes_bs(a.N, 1, B));
     switch (a.crt.k) {
@@ -1325,7 +1329,7 @@ void launch_relu_joint(const SignArgs& sa, const Act& x, const Act& y, const u12
 
 void launch_rescale_mrs(const MrsArgs& a, const Act& x, int B, const ModC* mc, const AesGlobals& g, hipStream_t st,
                         bool chain_only) {
-    const bool stg = mrs_staged(a.N);
+    const bool stg = mrs_staged(a.N, B);
     const dim3 gc = stg ? grid_aes(a.N, kMrsBS, 1, B) : grid_aes(a.N, aes_bs(a.N, 1, B), 1, B);
     const dim3 bc(stg ? kMrsBS : aes_bs(a.N, 1, B));
     switch (a.crt.k) {
