@@ -33,6 +33,9 @@ def main() -> None:
     ap.add_argument("--timeout", type=float, default=120.0)
     ap.add_argument("--rescale", default="mrs", choices=["mrs", "legacy"])
     ap.add_argument("--relu", default="joint", choices=["mrs", "approx", "joint"])
+    ap.add_argument("--garble-workers", type=int, default=None,
+                    help="refill workers (GPU garbler: concurrent garblings, one garbling context each, "
+                         "DASH_GG_CONTEXTS caps the contexts per device)")
     args = ap.parse_args()
 
     from dash_amd.ir.quant import QuantizationMethod
@@ -55,7 +58,7 @@ def main() -> None:
     t0 = time.perf_counter()
     svc = InferenceService(circuit, cfg["crt"], cfg["mrs"], backend=args.backend, slots_per_group=args.slots,
                            groups=args.groups, fault_hook=hook, step_timeout_s=args.timeout, rescale=args.rescale,
-                           relu=args.relu)
+                           relu=args.relu, garble_workers=args.garble_workers)
     fill_s = time.perf_counter() - t0
     svc.stats.t_start = time.perf_counter()
     from dash_amd.ir.bases import crt_modulus, first_primes
@@ -70,11 +73,12 @@ def main() -> None:
             ok = all((y[i] == circuit.plain_q_eval(x, track=False, crt_modulus=M)).all() for i, x in enumerate(batch))
     st = svc.stats.as_dict()
     online_ms = sum(svc.stats.latencies_ms)
+    workers = svc.garble_workers
     svc.close()
     print(json.dumps({
         "metric": f"served garbled inferences/s incl. garbling ({model})", "backend": args.backend,
         "rescale": args.rescale, "relu": args.relu,
-        "slots": args.slots, "groups": args.groups, "pool_fill_s": round(fill_s, 2),
+        "slots": args.slots, "groups": args.groups, "garble_workers": workers, "pool_fill_s": round(fill_s, 2),
         "online_only_inf_per_s": round(st["inferences"] / (online_ms / 1000.0), 2) if online_ms else None,
         **st, "ok": ok}), flush=True)
 
