@@ -1816,15 +1816,15 @@ u128* bank_scratch(size_t rows, int64_t N) {
     return tl_dc->bank(rows, N);
 }
 }  // namespace
-// A free garbling context of the device, locked for the caller: up to DASH_GG_CONTEXTS (default 2) per
-// device, so two garblings (two threads, e.g. the serving engine's refill workers) run on two streams at
-// once and fill each other's launch gaps; a third waits for the first context to free up.
+// A free garbling context of the device, locked for the caller: up to DASH_GG_CONTEXTS (default 4) per
+// device, so that many garblings (threads, e.g. the serving engine's refill workers) run on their own streams
+// at once and fill each other's launch gaps and latency stalls; one more waits for the first context.
 std::unique_lock<std::mutex> acquire_ctx(int device, DevCtx*& out) {
     static std::mutex m;
     static auto* pools = new std::map<int, std::vector<DevCtx*>>();  // leaked: lives as long as the process
     static const size_t cap = [] {
         const char* e = std::getenv("DASH_GG_CONTEXTS");
-        return static_cast<size_t>(std::max(1, e ? std::atoi(e) : 2));
+        return static_cast<size_t>(std::max(1, e ? std::atoi(e) : 4));
     }();
     DevCtx* first = nullptr;
     {

@@ -212,10 +212,11 @@ class InferenceService:
         self.stats = ServiceStats()
         self.healthy = True
         self.groups = [_Group(g, slots_per_group) for g in range(groups)]
-        # background refill workers: with the GPU garbler two GCs garble at once on two streams of the device
-        # (gpu_garbler.h DevCtx pool), filling each other's kernel-launch gaps
+        # background refill workers: with the GPU garbler four GCs garble at once on four streams of the device
+        # (garble_gpu.hip DevCtx pool), filling each other's kernel-launch gaps and latency stalls
+        # (served inf/s with 5 % faults, 2 / 3 / 4 workers: 88 / 104 / 110, profiles/r03_serving_workers_*.json)
         self.garble_workers = max(1, int(garble_workers if garble_workers is not None else
-                                         (2 if self.garble_device else 1)))
+                                         (4 if self.garble_device else 1)))
         self._ctr_lock = threading.Lock()
         self._next_group = 0
         self._err: Optional[BaseException] = None
