@@ -596,14 +596,18 @@ __global__ __launch_bounds__(256) void k_conv_img2(ConvArgs a, Act x, Act y, int
             // B operands one k-step ahead: the 4 LDS reads of step s+1 are in flight while step s's 4 MFMAs
             // run (one read ahead left each MFMA waiting out most of an LDS round trip)
             v2l bcur[4], bnxt[4];
+#ifdef DASH_FAKE_CONV_NOLDSB  // A/B bound analysis only: B operands from registers, no LDS reads (wrong results)
+#define DASH_CONV_LDB(off) v2l{static_cast<long>(base[t] + (off)), static_cast<long>(lane)}
+#else
+#define DASH_CONV_LDB(off) *reinterpret_cast<const v2l*>(img + base[t] + (off))
+#endif
 #pragma unroll
-            for (int t = 0; t < 4; ++t) bcur[t] = *reinterpret_cast<const v2l*>(img + base[t] + toff[0]);
+            for (int t = 0; t < 4; ++t) bcur[t] = DASH_CONV_LDB(toff[0]);
 #pragma unroll
             for (int s = 0; s < (AREG ? KSC : 1); ++s) {
                 if (s + 1 < (AREG ? KSC : 1)) {
 #pragma unroll
-                    for (int t = 0; t < 4; ++t)
-                        bnxt[t] = *reinterpret_cast<const v2l*>(img + base[t] + toff[(s + 1 < KSC) ? s + 1 : s]);
+                    for (int t = 0; t < 4; ++t) bnxt[t] = DASH_CONV_LDB(toff[(s + 1 < KSC) ? s + 1 : s]);
                 }
                 __builtin_amdgcn_sched_barrier(0);  // keep the reads ahead (the scheduler otherwise sinks them)
 #pragma unroll
