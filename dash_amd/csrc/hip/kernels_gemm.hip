@@ -332,6 +332,11 @@ __device__ __forceinline__ uint32_t modq_conv(uint32_t x, uint32_t q, uint32_t m
 #ifndef DASH_CONV_ITEMS
 #define DASH_CONV_ITEMS 2
 #endif
+#ifndef DASH_CONV_FW
+#define DASH_CONV_FW 16  // filters per wave in the MFMA phase (A/B knob: 32 feeds two MFMAs per B read, measured slower)
+#endif
+constexpr int kConvFW = DASH_CONV_FW;
+static_assert(kConvFW == 16 || kConvFW == 32, "conv: 16 or 32 filters per wave");
 #ifndef DASH_CONV_CLAMP
 #define DASH_CONV_CLAMP 1  // edge items of the band staging as clamped 8-B loads (0: byte-wise, A/B)
 #endif
@@ -362,16 +367,28 @@ __global__ __launch_bounds__(256) void k_conv_img2(ConvArgs a, Act x, Act y, int
     const int zc8 = zv > half ? zv - p : zv;
     const int tid = threadIdx.x;
     const int wave = tid >> 6, lane = tid & 63;
-    const int fw = f0 + wave * 16;
+    // Wave tiling of the block's 64 filters x 64 columns per column chunk: kConvFW filters (NG groups of 16) x
+    // 16 NT columns per wave; every B operand (image) fragment read from LDS feeds NG MFMAs. 32 filters per wave
+    // (half the B reads) measured slower, 2.40 -> 2.69 ms of conv per 24-GC step (132 VGPRs, 3 waves per SIMD),
+    // and a build without any B reads from LDS ran no faster (2.43 ms): the conv is not LDS-read bound
+    // (profiles/ab/README.md, round 3).
+    constexpr int NG = kConvFW / 16, NT = 4 / NG, WF = 64 / kConvFW;
+    const int wave_f = wave % WF, wave_c = wave / WF;
+    const int fw = f0 + wave_f * kConvFW;  // first filter of the wave (group g: fw + 16 g)
     const int KK = a.kh * a.kw, CC = a.Cpad / 64, KS = KK * CC;
-    const int8_t* Wr = a.w8r[j] + static_cast<int64_t>(fw + (lane & 15)) * (KK * a.Cpad) + (lane >> 4) * 16;
+    const int8_t* Wr[NG];
+#pragma unroll
+    for (int g = 0; g < NG; ++g)
+        Wr[g] = a.w8r[j] + static_cast<int64_t>(fw + 16 * g + (lane & 15)) * (KK * a.Cpad) + (lane >> 4) * 16;
     // A operand into VGPRs while the band is staged (padded filter rows exist up to F16)
-    v2l av[AREG ? KSC : 1];
-    if (AREG && fw < a.F) {
+    v2l av[NG][AREG ? KSC : 1];
+#pragma unroll
+    for (int g = 0; g < NG; ++g) {
+        const bool gin = fw + 16 * g < a.F;
 #pragma unroll
         for (int s = 0; s < (AREG ? KSC : 1); ++s) {
             const int kk = s / CC, cc = s - kk * CC;
-            av[s] = *reinterpret_cast<const v2l*>(Wr + kk * a.Cpad + cc * 64);
+            av[g][s] = (AREG && gin) ? *reinterpret_cast<const v2l*>(Wr[g] + kk * a.Cpad + cc * 64) : v2l{0, 0};
         }
     }
     // epilogue constants first: their global loads are in flight with the A operand and the band staging
@@ -390,11 +407,15 @@ __global__ __launch_bounds__(256) void k_conv_img2(ConvArgs a, Act x, Act y, int
     // rows are 4 consecutive output positions of ONE filter (fw + lane % 16): the epilogue stores them as one
     // dword (4 output bytes) instead of 4 byte stores, and needs one filter's constants per lane. Loaded
     // once (a dependent global load per output inside the column loop cost a round trip per 64 columns).
-    const int fl = fw + (lane & 15);
-    uint32_t zq = 0u, bq = 0u;
-    if (fl < a.F) {
-        zq = static_cast<uint32_t>(zcp[fl]);
-        bq = static_cast<uint16_t>(bias[(static_cast<int64_t>(b) * a.F + fl) * n + c]);
+    uint32_t zq[NG], bq[NG];
+#pragma unroll
+    for (int g = 0; g < NG; ++g) {
+        const int fl = fw + 16 * g + (lane & 15);
+        zq[g] = bq[g] = 0u;
+        if (fl < a.F) {
+            zq[g] = static_cast<uint32_t>(zcp[fl]);
+            bq[g] = static_cast<uint16_t>(bias[(static_cast<int64_t>(b) * a.F + fl) * n + c]);
+        }
     }
     // stage the band: item = (4 channels, 8 columns, row), channel groups fastest across lanes (the
     // channel-last dword stores of a lane group then cover consecutive banks); 4 x 8-B loads -> 8 dwords.
@@ -562,7 +583,9 @@ __global__ __launch_bounds__(256) void k_conv_img2(ConvArgs a, Act x, Act y, int
     if (fw >= a.F) return;  // wave-uniform; no barrier follows
     const int ncol = (oy1 - oy0) * a.OW;
     const int npos = a.OH * a.OW;
-    const uint32_t addc = off + zq * static_cast<uint32_t>(zv) + bq;
+    uint32_t addc[NG];
+#pragma unroll
+    for (int g = 0; g < NG; ++g) addc[g] = off + zq[g] * static_cast<uint32_t>(zv) + bq[g];
     act_t* Y = y.p[j] + (static_cast<int64_t>(b) * n + c) * a.F * npos;
     // dword stores need 4-byte aligned filter rows and band starts
     const bool dw = (npos & 3) == 0 && ((oy0 * a.OW) & 3) == 0;
@@ -577,67 +600,81 @@ __global__ __launch_bounds__(256) void k_conv_img2(ConvArgs a, Act x, Act y, int
             toff[s] = dy * R + dx * S + cc * 64;
         }
     }
-    for (int col0 = 0; col0 < ncol; col0 += 64) {
-        v4i acc[4];
-        int base[4];
-        bool ok[4];
+    for (int colw = wave_c * 16 * NT; colw < ncol; colw += 64) {
+        v4i acc[NG][NT];
+        int base[NT];
 #pragma unroll
-        for (int t = 0; t < 4; ++t) {
-            acc[t] = v4i{0, 0, 0, 0};
-            const int col = col0 + t * 16 + (lane & 15);
-            ok[t] = col < ncol;
+        for (int t = 0; t < NT; ++t) {
+#pragma unroll
+            for (int g = 0; g < NG; ++g) acc[g][t] = v4i{0, 0, 0, 0};
+            const int col = colw + t * 16 + (lane & 15);
             // columns past the band read column 0's operands (valid LDS); their results are never stored
-            const int cl = ok[t] ? col : 0;
+            const int cl = col < ncol ? col : 0;
             const int oyl = a.OW > 1 ? static_cast<int>(__umulhi(static_cast<uint32_t>(cl), owm)) : cl;
             const int ox = cl - oyl * a.OW;
             base[t] = (oyl * a.sh) * R + (ox * a.sw) * S + (lane >> 4) * 16;
         }
         if (AREG) {
-            // B operands one k-step ahead: the 4 LDS reads of step s+1 are in flight while step s's 4 MFMAs
-            // run (one read ahead left each MFMA waiting out most of an LDS round trip)
-            v2l bcur[4], bnxt[4];
+            // B operands one k-step ahead: the LDS reads of step s+1 are in flight while step s's MFMAs run
+            // (one read ahead left each MFMA waiting out most of an LDS round trip)
+            v2l bcur[NT], bnxt[NT];
 #ifdef DASH_FAKE_CONV_NOLDSB  // A/B bound analysis only: B operands from registers, no LDS reads (wrong results)
 #define DASH_CONV_LDB(off) v2l{static_cast<long>(base[t] + (off)), static_cast<long>(lane)}
 #else
 #define DASH_CONV_LDB(off) *reinterpret_cast<const v2l*>(img + base[t] + (off))
 #endif
 #pragma unroll
-            for (int t = 0; t < 4; ++t) bcur[t] = DASH_CONV_LDB(toff[0]);
+            for (int t = 0; t < NT; ++t) bcur[t] = DASH_CONV_LDB(toff[0]);
 #pragma unroll
             for (int s = 0; s < (AREG ? KSC : 1); ++s) {
                 if (s + 1 < (AREG ? KSC : 1)) {
 #pragma unroll
-                    for (int t = 0; t < 4; ++t) bnxt[t] = DASH_CONV_LDB(toff[(s + 1 < KSC) ? s + 1 : s]);
+                    for (int t = 0; t < NT; ++t) bnxt[t] = DASH_CONV_LDB(toff[(s + 1 < KSC) ? s + 1 : s]);
                 }
                 __builtin_amdgcn_sched_barrier(0);  // keep the reads ahead (the scheduler otherwise sinks them)
 #pragma unroll
-                for (int t = 0; t < 4; ++t) acc[t] = __builtin_amdgcn_mfma_i32_16x16x64_i8(bcur[t], av[s], acc[t], 0, 0, 0);
+                for (int t = 0; t < NT; ++t)
+#pragma unroll
+                    for (int g = 0; g < NG; ++g)
+                        acc[g][t] = __builtin_amdgcn_mfma_i32_16x16x64_i8(bcur[t], av[g][s], acc[g][t], 0, 0, 0);
                 __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-                for (int t = 0; t < 4; ++t) bcur[t] = bnxt[t];
+                for (int t = 0; t < NT; ++t) bcur[t] = bnxt[t];
             }
+#undef DASH_CONV_LDB
         } else {
             for (int dy = 0; dy < a.kh; ++dy)
                 for (int dx = 0; dx < a.kw; ++dx)
                     for (int cc = 0; cc < CC; ++cc) {
-                        const v2l av1 = *reinterpret_cast<const v2l*>(Wr + (dy * a.kw + dx) * a.Cpad + cc * 64);
+                        v2l av1[NG];
+#pragma unroll
+                        for (int g = 0; g < NG; ++g)
+                            av1[g] = fw + 16 * g < a.F ? *reinterpret_cast<const v2l*>(Wr[g] + (dy * a.kw + dx) * a.Cpad + cc * 64)
+                                                       : v2l{0, 0};
                         const int offs = dy * R + dx * S + cc * 64;
 #pragma unroll
-                        for (int t = 0; t < 4; ++t) {
+                        for (int t = 0; t < NT; ++t) {
                             const v2l bv = *reinterpret_cast<const v2l*>(img + base[t] + offs);
-                            acc[t] = __builtin_amdgcn_mfma_i32_16x16x64_i8(bv, av1, acc[t], 0, 0, 0);
+#pragma unroll
+                            for (int g = 0; g < NG; ++g)
+                                acc[g][t] = __builtin_amdgcn_mfma_i32_16x16x64_i8(bv, av1[g], acc[g][t], 0, 0, 0);
                         }
                     }
         }
-        if (fl < a.F) {
 #pragma unroll
-            for (int t = 0; t < 4; ++t) {
-                // rows r = 0..3: positions col0 + 16 t + 4 (lane / 16) + r of filter fl (band rows are whole output rows)
-                const int cb = col0 + t * 16 + (lane >> 4) * 4;
+        for (int g = 0; g < NG; ++g) {
+            const int fl = fw + 16 * g + (lane & 15);
+            if (fl >= a.F) continue;
+#pragma unroll
+            for (int t = 0; t < NT; ++t) {
+                // rows r = 0..3: positions colw + 16 t + 4 (lane / 16) + r of filter fl (band rows are whole output rows)
+                const int cb = colw + t * 16 + (lane >> 4) * 4;
+                if (cb >= ncol) continue;
                 const int pos = oy0 * a.OW + cb;
                 uint32_t o[4];
 #pragma unroll
-                for (int r = 0; r < 4; ++r) o[r] = modq_conv(static_cast<uint32_t>(acc[t][r]) + addc, static_cast<uint32_t>(p), mq);
+                for (int r = 0; r < 4; ++r)
+                    o[r] = modq_conv(static_cast<uint32_t>(acc[g][t][r]) + addc[g], static_cast<uint32_t>(p), mq);
                 act_t* yr = Y + static_cast<int64_t>(fl) * npos + pos;
 #ifdef DASH_FAKE_CONV_NOSTORE
                 if (o[0] == 0xdeadbeefu)  // A/B bound analysis only: never true, keeps the math
