@@ -1756,6 +1756,19 @@ struct DevCtx {
         ring_off += bytes;
         return d;
     }
+    // pinned host buffer of the label hand-offs (to_device / to_host): DMA copies instead of the runtime's
+    // chunked pageable staging (dozens of blit kernels per GC); grow-only, reused once the stream has drained
+    char* pin_h = nullptr;
+    size_t pin_bytes = 0;
+    char* pinned(size_t bytes) {
+        if (bytes > pin_bytes) {
+            HIPCHECK(hipStreamSynchronize(st));
+            if (pin_h) (void)hipHostFree(pin_h);
+            HIPCHECK(hipHostMalloc(reinterpret_cast<void**>(&pin_h), bytes));
+            pin_bytes = bytes;
+        }
+        return pin_h;
+    }
     int16_t* scratch(size_t bytes) {
         if (bytes > S_bytes) {
             HIPCHECK(hipStreamSynchronize(st));
@@ -1944,16 +1957,21 @@ void GpuGarbler::to_device(const CrtLabels& cur) {
     for (const auto& l : cur) I.cur_mod.push_back(l.p);
     I.cur_N = cur[0].N;
     I.cur = I.alloc_labels(I.cur_mod, I.cur_N);
-    std::vector<int16_t> t;
+    // every residue transposed into one pinned block (the stream is idle: the previous hand-off synchronized
+    // or the context was just acquired), one DMA copy per residue
+    size_t total = 0;
+    for (const auto& L : cur) total += static_cast<size_t>(gg::chunks_of(L.n)) * gg::kCh * L.N;
+    int16_t* t = reinterpret_cast<int16_t*>(I.dc.pinned(std::max<size_t>(16, total * sizeof(int16_t))));
     for (size_t j = 0; j < cur.size(); ++j) {
         const Labels& L = cur[j];
         DASH_CHECK(L.c.size() == static_cast<size_t>(L.N) * L.n, "gpu garbler: host labels are stale");
-        t.assign(static_cast<size_t>(gg::chunks_of(L.n)) * gg::kCh * L.N, 0);
+        const size_t cnt = static_cast<size_t>(gg::chunks_of(L.n)) * gg::kCh * L.N;
+        std::fill(t, t + cnt, int16_t(0));
         for (i64 e = 0; e < L.N; ++e)
             for (int q = 0; q < L.n; ++q)
                 t[((static_cast<size_t>(q >> 3)) * L.N + e) * gg::kCh + (q & 7)] = L.c[static_cast<size_t>(e) * L.n + q];
-        // pageable source: staged before the call returns, ordered on the garbling stream
-        HIPCHECK(hipMemcpyAsync(I.cur[j].p, t.data(), t.size() * sizeof(int16_t), hipMemcpyHostToDevice, gg::tl_st));
+        HIPCHECK(hipMemcpyAsync(I.cur[j].p, t, cnt * sizeof(int16_t), hipMemcpyHostToDevice, gg::tl_st));
+        t += cnt;
     }
 }
 
@@ -1961,19 +1979,25 @@ void GpuGarbler::to_host(CrtLabels& cur) {
     Impl& I = *impl_;
     I.enter();
     I.check_cur(cur);
-    std::vector<std::vector<int16_t>> t(cur.size());
+    size_t total = 0;
+    for (const auto& L : cur) total += static_cast<size_t>(L.N) * gg::chunks_of(L.n) * gg::kCh;
+    // pinned(): a growth synchronizes the stream before the old block is freed (an earlier to_device's copies)
+    int16_t* t0 = reinterpret_cast<int16_t*>(I.dc.pinned(std::max<size_t>(16, total * sizeof(int16_t))));
+    int16_t* t = t0;
     for (size_t j = 0; j < cur.size(); ++j) {
-        t[j].resize(static_cast<size_t>(cur[j].N) * gg::chunks_of(cur[j].n) * gg::kCh);
-        HIPCHECK(hipMemcpyAsync(t[j].data(), I.cur[j].p, t[j].size() * sizeof(int16_t), hipMemcpyDeviceToHost,
-                                gg::tl_st));
+        const size_t cnt = static_cast<size_t>(cur[j].N) * gg::chunks_of(cur[j].n) * gg::kCh;
+        HIPCHECK(hipMemcpyAsync(t, I.cur[j].p, cnt * sizeof(int16_t), hipMemcpyDeviceToHost, gg::tl_st));
+        t += cnt;
     }
     HIPCHECK(hipStreamSynchronize(gg::tl_st));
+    t = t0;
     for (size_t j = 0; j < cur.size(); ++j) {
         Labels& L = cur[j];
         L.c.resize(static_cast<size_t>(L.N) * L.n);
         for (i64 e = 0; e < L.N; ++e)
             for (int q = 0; q < L.n; ++q)
-                L.c[static_cast<size_t>(e) * L.n + q] = t[j][((static_cast<size_t>(q >> 3)) * L.N + e) * gg::kCh + (q & 7)];
+                L.c[static_cast<size_t>(e) * L.n + q] = t[((static_cast<size_t>(q >> 3)) * L.N + e) * gg::kCh + (q & 7)];
+        t += static_cast<size_t>(L.N) * gg::chunks_of(L.n) * gg::kCh;
     }
 }
 

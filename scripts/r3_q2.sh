@@ -8,7 +8,7 @@ ROOT=$(pwd)
 mkdir -p gpurun_out/$T
 timeout -k 10 400 python -u -m pytest tests/test_gpu_parity.py tests/test_wire_compat.py -m gpu -x -q --timeout 200 --timeout-method thread > gpurun_out/$T/gpu_tests.log 2>&1 || { tail -40 gpurun_out/$T/gpu_tests.log; exit 1; }
 tail -1 gpurun_out/$T/gpu_tests.log
-for V in "default default" "jobs default" "default row" "jobs row"; do
+for V in ${VARIANTS:-"default default"}; do
   set -- $V
   timeout -k 10 300 env DASH_GG_HASH=$1 DASH_GG_BANK=$2 python -u scripts/garble_bench.py --sink 12 > gpurun_out/$T/gg_sink_$1_$2.json 2> gpurun_out/$T/gg_sink_$1_$2.err || { tail -20 gpurun_out/$T/gg_sink_$1_$2.err; exit 1; }
   echo "hash=$1 bank=$2 $(cut -c1-120 gpurun_out/$T/gg_sink_$1_$2.json)"
