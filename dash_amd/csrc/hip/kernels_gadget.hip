@@ -955,8 +955,8 @@ __global__ __launch_bounds__(kMrsBS, MODE == 2 ? DASH_CHAIN2_WAVES : DASH_UA_MIN
                 for (int c = 0; c < cnt; c += kStageRd) {
                     uint32_t v[kStageRd];
 #pragma unroll
-                    for (int u = 0; u < kStageRd; ++u)
-                        if (c + u < cnt) v[u] = stg[(c + u) * kMrsBS + tid];
+                    for (int u = 0; u < kStageRd; ++u)  // spare lanes (e >= N) read no staged bytes: digit 0
+                        if (c + u < cnt) v[u] = valid ? stg[(c + u) * kMrsBS + tid] : 0u;
 #pragma unroll
                     for (int u = 0; u < kStageRd; ++u)
                         if (c + u < cnt) {
@@ -995,7 +995,7 @@ __global__ __launch_bounds__(kMrsBS, MODE == 2 ? DASH_CHAIN2_WAVES : DASH_UA_MIN
                 __syncthreads();
                 lds_stage_rows<kMrsBS, kStageU>(stg, L, N, e0, c0, cnt);
                 __syncthreads();
-                for (int c = 0; c < cnt; ++c) cf.push(stg[c * kMrsBS + tid], m);
+                for (int c = 0; c < cnt; ++c) cf.push(valid ? stg[c * kMrsBS + tid] : 0u, m);
             }
             u128 key = cf.finish();
 #pragma unroll
