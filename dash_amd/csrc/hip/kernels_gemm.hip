@@ -587,8 +587,10 @@ __global__ __launch_bounds__(256) void k_conv_img2(ConvArgs a, Act x, Act y, int
 #pragma unroll
     for (int g = 0; g < NG; ++g) addc[g] = off + zq[g] * static_cast<uint32_t>(zv) + bq[g];
     act_t* Y = y.p[j] + (static_cast<int64_t>(b) * n + c) * a.F * npos;
-    // dword stores need 4-byte aligned filter rows and band starts
+    // dword stores need 4-byte aligned filter rows and band starts, the transposed 16-byte stores 16-byte ones
     const bool dw = (npos & 3) == 0 && ((oy0 * a.OW) & 3) == 0;
+    const bool dw16 = (npos & 15) == 0 && ((oy0 * a.OW) & 15) == 0 &&
+                      ((reinterpret_cast<uintptr_t>(Y) & 15) == 0);
     const uint32_t mq = a.mq[j];
     // tap offsets of the A-in-VGPR path, once per block (the k-step loop then only adds)
     int toff[AREG ? KSC : 1];
@@ -664,6 +666,40 @@ __global__ __launch_bounds__(256) void k_conv_img2(ConvArgs a, Act x, Act y, int
 #pragma unroll
         for (int g = 0; g < NG; ++g) {
             const int fl = fw + 16 * g + (lane & 15);
+            if (NT == 4 && dw16 && colw + 64 <= ncol) {
+                // whole 64-column chunk: lane (f, h) holds positions 16 t + 4 h + 0..3 of tile t as one dword; a
+                // 4x4 transpose over (t, h) with v_permlane32_swap / v_permlane16_swap gives it positions
+                // 16 h + 0..15, stored as one 16-byte store per lane (64 contiguous bytes per filter row)
+                uint32_t d[4];
+#pragma unroll
+                for (int t = 0; t < 4; ++t) {
+                    uint32_t w = 0;
+#pragma unroll
+                    for (int r = 0; r < 4; ++r)
+                        w |= modq_conv(static_cast<uint32_t>(acc[g][t][r]) + addc[g], static_cast<uint32_t>(p), mq) << (8 * r);
+                    d[t] = w;
+                }
+                auto r02 = __builtin_amdgcn_permlane32_swap(d[0], d[2], false, false);
+                d[0] = r02[0];
+                d[2] = r02[1];
+                auto r13 = __builtin_amdgcn_permlane32_swap(d[1], d[3], false, false);
+                d[1] = r13[0];
+                d[3] = r13[1];
+                auto r01 = __builtin_amdgcn_permlane16_swap(d[0], d[1], false, false);
+                d[0] = r01[0];
+                d[1] = r01[1];
+                auto r23 = __builtin_amdgcn_permlane16_swap(d[2], d[3], false, false);
+                d[2] = r23[0];
+                d[3] = r23[1];
+                if (fl < a.F) {
+                    act_t* yr = Y + static_cast<int64_t>(fl) * npos + oy0 * a.OW + colw + 16 * (lane >> 4);
+#ifdef DASH_FAKE_CONV_NOSTORE
+                    if (d[0] == 0xdeadbeefu)  // A/B bound analysis only
+#endif
+                    *reinterpret_cast<uint4*>(yr) = make_uint4(d[0], d[1], d[2], d[3]);
+                }
+                continue;
+            }
             if (fl >= a.F) continue;
 #pragma unroll
             for (int t = 0; t < NT; ++t) {
