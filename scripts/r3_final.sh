@@ -14,11 +14,9 @@ timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smok
 tail -1 $OUT/smoke.log
 timeout -k 10 600 python bench.py --steps 20 --warmup 3 > $OUT/bench.json 2> $OUT/bench.err || { tail -20 $OUT/bench.err; exit 1; }
 cat $OUT/bench.json
-DASH_BENCH_ROLLING=0 timeout -k 10 300 python bench.py --steps 20 --warmup 3 --phases main > $OUT/bench_perstep.json 2> $OUT/bench_perstep.err || { tail -20 $OUT/bench_perstep.err; exit 1; }
-python -c "import json,sys; d=json.load(open(sys.argv[1])); print('per-step loop', d['value'], d['ms_per_step'], d['verified_vs_plaintext'])" $OUT/bench_perstep.json
 timeout -k 10 300 python bench.py --steps 20 --warmup 3 --batch 1 --phases main > $OUT/b1.json 2> $OUT/b1.err || { tail -20 $OUT/b1.err; exit 1; }
 python -c "import json,sys; d=json.load(open(sys.argv[1])); print('b1', d['value'], d['ms_per_step'], d['verified_vs_plaintext'])" $OUT/b1.json
-WORKERS="${WORKERS:-2 3 4}" bash scripts/r3_serve.sh $T || exit 1
+WORKERS="${WORKERS:-4}" bash scripts/r3_serve.sh $T || exit 1
 cd /tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$ROOT/$OUT/kt" -o run -- python3 "$ROOT/bench.py" --steps 5 --warmup 2 --phases main > "$ROOT/$OUT/kt.log" 2>&1 || { tail -5 "$ROOT/$OUT/kt.log"; exit 1; }
 cd "$ROOT"
