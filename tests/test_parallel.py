@@ -1,4 +1,4 @@
-"""Batch-DP over torch.distributed with the gloo backend, world_size 2 (CPU).
+"""Batch-DP over torch.distributed with the gloo backend, world_size 2, 4 and 8 (CPU).
 The same code path runs with nccl (RCCL) on GPUs (bench.py, --gpus N)."""
 import os
 import socket
@@ -33,7 +33,7 @@ def _worker(rank, world, port, q):
     shutdown(ctx)
 
 
-@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("world", [2, 4, 8])
 def test_batch_dp_gloo(world):
     ctx = tmp.get_context("spawn")
     q = ctx.Queue()
@@ -63,7 +63,7 @@ def _bench_worker(rank, world, port, q):
     q.put((rank, out))
 
 
-@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("world", [2, 4, 8])
 def test_bench_driver_gloo(world):
     """bench.py's own driver (dash_amd.benchcore) over gloo: the ranks agree on the batch, the JSON carries the
     backend, world size and one record per rank, and every rank's outputs match the plaintext evaluation."""
