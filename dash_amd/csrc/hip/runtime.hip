@@ -10,6 +10,7 @@
 
 #include <chrono>
 #include <map>
+#include <mutex>
 #include <functional>
 #include <thread>
 
@@ -56,6 +57,10 @@ class HipEvaluator {
     // Upload garbled model `m` (same circuit as the template) into batch slot b.
     void load(int b, const GarbledModel& m) {
         DASH_CHECK(b >= 0 && b < B_, "batch slot out of range");
+        // one load at a time: the per-GC constants go through ONE pinned staging block, device block and load
+        // stream shared by all slots (the serving engine's refill workers load different slots of one evaluator
+        // concurrently; unserialized, one slot's constants could land in another's)
+        std::lock_guard<std::mutex> load_guard(load_mu_);
         DASH_CHECK(m.h.crt == tmpl_h_.crt && m.h.mrs == tmpl_h_.mrs && m.layers.size() == tmpl_nlayers_ &&
                        m.h.in_dims == tmpl_h_.in_dims,
                    "model does not garble the evaluator's circuit");
@@ -519,6 +524,7 @@ class HipEvaluator {
     uint8_t* small_d_ = nullptr;
     const ScatterDesc* small_desc_ = nullptr;
     hipStream_t load_st_ = nullptr;
+    std::mutex load_mu_;  // load(): the staging blocks and load stream above are shared by every slot
     std::map<std::pair<size_t, std::string>, std::pair<uint8_t*, size_t>> arena_;  // (layer, table) -> [B][nb]
     std::vector<int> loaded_;
     int dev_ = 0, B_ = 1, k_ = 0;
