@@ -88,7 +88,7 @@ def parse_args(argv=None) -> argparse.Namespace:
     ap.add_argument("--sign", default=None, choices=["fused", "reference"], help="override the sign construction")
     ap.add_argument("--rescale", default=None, choices=["mrs", "legacy"], help="override the rescale construction")
     ap.add_argument("--relu", default=None, choices=["mrs", "approx", "joint"], help="override the ReLU sign")
-    ap.add_argument("--streams", type=int, default=int(os.environ.get("DASH_BENCH_STREAMS", "12")),
+    ap.add_argument("--streams", type=int, default=int(os.environ.get("DASH_BENCH_STREAMS", "8")),
                     help="independent GC groups per GPU, each on its own HIP stream")
     ap.add_argument("--model", default="MODEL_F_MINIONN_POOL_REPL")
     ap.add_argument("--config", default="DASH", choices=["DASH", "REDASH_OPT", "REDASH_CPM"])
