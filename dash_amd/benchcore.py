@@ -78,7 +78,13 @@ def host_thread_budget(requested: int = 0) -> int:
 
 def parse_args(argv=None) -> argparse.Namespace:
     ap = argparse.ArgumentParser(description=__doc__.split("\n")[0])
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=1,
+                    help="ranks (one per GPU). Without a launcher (WORLD_SIZE unset) bench.py starts N fresh ranks "
+                         "itself; with one, WORLD_SIZE must equal N")
+    ap.add_argument("--rehearse-shared-device", action="store_true",
+                    default=os.environ.get("DASH_BENCH_REHEARSAL", "") == "1",
+                    help="allow more ranks than visible GPUs (ranks share devices over gloo). A rehearsal of the "
+                         "multi-rank path, never a scaling measurement; the record says so")
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--batch", type=int, default=int(os.environ.get("DASH_BENCH_BATCH", "0")),
@@ -99,14 +105,87 @@ def parse_args(argv=None) -> argparse.Namespace:
     ap.add_argument("--verify", type=int, default=1)
     ap.add_argument("--garble-device", type=int, default=int(os.environ.get("DASH_BENCH_GARBLE_DEVICE", "1")),
                     help="garble on this rank's GPU (byte-identical to the host garbler)")
-    ap.add_argument("--phases", default=os.environ.get("DASH_BENCH_PHASES", "main,reference,served"),
-                    help="comma list of main, reference, served (main is always run)")
+    ap.add_argument("--phases", default=os.environ.get("DASH_BENCH_PHASES", "main,threads,latency,reference,served"),
+                    help="comma list of main, threads, latency, reference, served (main is always run)")
+    ap.add_argument("--thread-sweep", default="4,8",
+                    help="host thread budgets of the threads phase (headline loop re-timed at each)")
+    ap.add_argument("--latency-gcs", type=int, default=8, help="fresh GCs timed one by one in the latency phase")
     ap.add_argument("--ref-batch", type=int, default=0, help="GCs per GPU of the reference phase (0: auto)")
     ap.add_argument("--ref-steps", type=int, default=0, help="timed steps of the reference phase (0: --steps)")
     ap.add_argument("--served-slots", type=int, default=16)
     ap.add_argument("--served-groups", type=int, default=3)
-    ap.add_argument("--served-requests", type=int, default=8, help="online batches of the served phase")
+    ap.add_argument("--served-requests", type=int, default=64, help="online batches of the served phase")
+    ap.add_argument("--served-min-s", type=float, default=10.0,
+                    help="the served phase keeps issuing requests until it has run this long (steady state)")
     return ap.parse_args(argv)
+
+
+# ----------------------------------------------------------------------------------------- rank launcher
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def visible_gpus() -> int:
+    """Visible GPU count without initialising HIP in this process (a parent that starts ranks must not)."""
+    import torch
+
+    return int(torch.cuda.device_count())
+
+
+def spawn_ranks(args, argv: List[str]) -> int:
+    """``bench.py --gpus N`` with no launcher: start N fresh rank processes (torch.distributed.run, one per GPU,
+    rendezvous on 127.0.0.1) and forward rank 0's JSON line. This parent never makes a HIP call and never
+    execs; it exits with the launcher's code (non-zero when any rank failed). The reference is single-device
+    (benchmarks/model_benchmarks/non_sgx/main.cpp:27-92); batch DP over the node is this framework's scale-out."""
+    import subprocess
+
+    n = args.gpus
+    if args.backend == "hip":
+        avail = visible_gpus()
+        if avail < n and not args.rehearse_shared_device:
+            log(f"--gpus {n} requested but only {avail} GPU(s) visible: refusing (a scaling run needs one GPU per "
+                f"rank; --rehearse-shared-device runs the multi-rank path on shared devices, clearly labelled)")
+            return 2
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ)
+    env["PYTHONPATH"] = root + (os.pathsep + env["PYTHONPATH"] if env.get("PYTHONPATH") else "")
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    if args.rehearse_shared_device:
+        env["DASH_BENCH_REHEARSAL"] = "1"
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.join(root, "bench.py"), *argv]
+    log(f"starting {n} ranks: {' '.join(cmd[1:6])} ...")
+    proc = subprocess.Popen(cmd, stdout=subprocess.PIPE, env=env, text=True)
+    record = None
+    for line in proc.stdout:
+        if line.lstrip().startswith("{") and '"metric"' in line:
+            record = line.strip()
+        else:
+            sys.stderr.write(line)
+    rc = proc.wait()
+    if record is not None:
+        print(record, flush=True)
+    if rc == 0 and record is None:
+        log("ranks exited 0 but rank 0 printed no record")
+        return 1
+    return rc
+
+
+def check_world(args, ctx, recs: list, rehearsal: bool) -> None:
+    """Rank 0's guard before it prints: the job really is N ranks, over RCCL, on N distinct GPUs."""
+    if ctx.world != args.gpus:
+        raise RuntimeError(f"--gpus {args.gpus} but the job has {ctx.world} rank(s)")
+    if args.backend != "hip" or ctx.world == 1 or rehearsal:
+        return
+    if ctx.backend != "nccl":
+        raise RuntimeError(f"multi-GPU bench must run over nccl (RCCL), got {ctx.backend}")
+    buses = {r.get("pci_bus_id") for r in recs}
+    if len(buses) != ctx.world:
+        raise RuntimeError(f"{ctx.world} ranks but {len(buses)} distinct GPU(s) (PCI bus ids {sorted(buses)})")
 
 
 # ----------------------------------------------------------------------------------------- evaluator slots
@@ -373,7 +452,7 @@ class _Bench:
 
         a, ctx = self.args, self.ctx
         slots, groups, reqs = a.served_slots, a.served_groups, a.served_requests
-        xs = quantized_inputs(self.model, slots * reqs, self.qm, self.qp, seed=5000 + ctx.rank)
+        pool = quantized_inputs(self.model, slots * 8, self.qm, self.qp, seed=5000 + ctx.rank)
         t0 = time.perf_counter()
         svc = InferenceService(self.circuit, self.cfg["crt"], self.cfg["mrs"],
                                backend="hip" if self.hip else "cpu", device=self.device, slots_per_group=slots,
@@ -386,24 +465,80 @@ class _Bench:
             svc.stats.t_start = time.perf_counter()
             t1 = time.perf_counter()
             ok = True
-            for r in range(reqs):
-                batch = xs[r * slots:(r + 1) * slots]
+            M = svc_modulus(self.cfg["crt"])
+            r = 0
+            # steady state: at least `reqs` requests AND at least served_min_s seconds (the pool's initial fill
+            # is drained within the first few requests; after that every inference waits on fresh garbling)
+            while True:
+                k = r % 8
+                batch = pool[k * slots:(k + 1) * slots]
                 y = svc.infer(batch)
-                if r == 0:
-                    M = svc_modulus(self.cfg["crt"])
-                    ok = all(np.array_equal(y[i], self.circuit.plain_q_eval(x, track=False, crt_modulus=M))
-                             for i, x in enumerate(batch))
+                if r < 8:
+                    ok = ok and all(np.array_equal(y[i], self.circuit.plain_q_eval(x, track=False, crt_modulus=M))
+                                    for i, x in enumerate(batch))
+                r += 1
+                # every rank stops after the same number of requests (agreed by rank 0's clock)
+                if r >= reqs:
+                    done = all_reduce_max(ctx, float(time.perf_counter() - t1 >= a.served_min_s))
+                    if done > 0:
+                        break
             local = time.perf_counter() - t1
             st = svc.stats.as_dict()
         finally:
             svc.close()
         barrier(ctx)
         elapsed = all_reduce_max(ctx, local)
-        n = slots * reqs
+        n = slots * r
         return dict(value=ctx.world * n / elapsed, local_inf_per_s=n / local, pool_fill_s=fill_s,
                     garble_s_per_gc=st["garble_s_per_gc"], pool_wait_s=st["pool_wait_s"],
                     batch_latency_ms=st["batch_latency_ms"], verified=ok, slots=slots, groups=groups,
-                    requests=reqs)
+                    requests=r, duration_s=round(local, 2),
+                    note=("one-process simulation: garbler and evaluator share this rank's process and GPU (the "
+                          "reference's non-SGX benches do the same); benchmarks/two_party.py measures the split"))
+
+    # ---- batch-1 latency on fresh GCs (the reference's timed region, one image at a time)
+    def latency(self, cons: dict) -> dict:
+        """garble_inputs -> H2D -> evaluate -> D2H -> decode for one inference on a fresh GC each
+        (benchmarks/model_benchmarks/sgx/Enclave/Enclave.cpp:177-183); garbling and the table upload are
+        outside the timed region, as there."""
+        from .models import quantized_inputs
+
+        n = max(2, self.args.latency_gcs)
+        xs = quantized_inputs(self.model, n, self.qm, self.qp, seed=7000 + self.ctx.rank)
+        ev, grp, times, ok = None, None, [], True
+        for i in range(n + 1):  # one untimed warm-up GC (first launch, graph build)
+            if self.hip:
+                if grp is None:
+                    gc = self.garble("lat", i, cons)
+                    from .native import native
+
+                    native().gpu_table_cache_trim()
+                    grp = _HipGroup(gc.model, 1, self.device, not self.args.no_mfma, False, None)
+                else:
+                    gc = self.garble("lat", i, cons, sink=grp.sink(0))
+            else:
+                gc = self.garble("lat", i, cons)
+                grp = grp or _CpuGroup(gc.model, 1, self.threads)
+            grp.load(0, gc)
+            x = xs[max(0, i - 1)]
+            self.sync()
+            t = time.perf_counter()
+            grp.encode(0, gc, x)
+            grp.launch()
+            grp.fetch()
+            y = grp.decode(0, gc)
+            dt = time.perf_counter() - t
+            if i > 0:
+                times.append(1000.0 * dt)
+                ok = ok and bool(np.array_equal(y, gc.plain_q_eval(x)))
+        del grp
+        if self.hip:
+            from .native import native
+
+            native().gpu_table_cache_trim()
+        ts = sorted(times)
+        return dict(latency_b1_ms=round(float(np.median(ts)), 3), min_ms=round(ts[0], 3), max_ms=round(ts[-1], 3),
+                    gcs=n, fresh_gc_per_inference=True, verified=ok)
 
     # ---- per-rank evidence
     def rank_record(self, ms_step: float, inf_s: float, host_ms: float, B: int) -> dict:
@@ -427,21 +562,34 @@ def svc_modulus(crt) -> int:
 
 
 def run(argv=None) -> Optional[dict]:
-    """Run the benchmark; rank 0 returns (and bench.py prints) the JSON record, other ranks None."""
+    """Run the benchmark in this process (one rank); rank 0 returns (and bench.py prints) the JSON record,
+    other ranks None."""
     args = parse_args(argv)
     from .native import native
     from .parallel import all_gather_array, all_gather_object, init_distributed, shutdown
 
     hip = args.backend == "hip"
+    rehearsal = bool(args.rehearse_shared_device)
+    world_env = int(os.environ.get("WORLD_SIZE", "1"))
+    if world_env != args.gpus:
+        raise RuntimeError(f"--gpus {args.gpus} but WORLD_SIZE={world_env}: start the bench with "
+                           f"'python bench.py --gpus N' (it launches the ranks) or under torchrun with N ranks")
     if hip:
-        import torch
-
-        # one process per GPU (torchrun); backend nccl (= RCCL over xGMI). DASH_DIST_BACKEND=gloo and a device
-        # count smaller than the world size are only for rehearsing the multi-rank path on one GPU.
+        # one process per GPU; backend nccl (= RCCL over xGMI). More ranks than GPUs only as a labelled rehearsal
+        # (ranks share devices over gloo; RCCL refuses two ranks on one device).
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        if int(os.environ.get("WORLD_SIZE", "1")) > 1 and torch.cuda.device_count() < int(os.environ["WORLD_SIZE"]):
-            os.environ["LOCAL_RANK"] = str(int(os.environ.get("LOCAL_RANK", "0")) % max(1, torch.cuda.device_count()))
-    ctx = init_distributed(backend=os.environ.get("DASH_DIST_BACKEND") or None, use_gpu=hip)
+        ndev = visible_gpus()
+        if world_env > ndev:
+            if not rehearsal:
+                raise RuntimeError(f"{world_env} ranks but {ndev} visible GPU(s); pass --rehearse-shared-device "
+                                   f"for a (labelled) shared-device rehearsal")
+            os.environ["LOCAL_RANK"] = str(int(os.environ.get("LOCAL_RANK", "0")) % max(1, ndev))
+    backend = os.environ.get("DASH_DIST_BACKEND") or None
+    if rehearsal and world_env > 1 and backend is None:
+        backend = "gloo"
+    if backend not in (None, "nccl") and hip and world_env > 1 and not rehearsal:
+        raise RuntimeError(f"DASH_DIST_BACKEND={backend}: a GPU scaling run uses nccl (RCCL)")
+    ctx = init_distributed(backend=backend, use_gpu=hip)
     world, rank = ctx.world, ctx.rank
     bench = _Bench(args, ctx)
     bench.threads = host_thread_budget(args.threads)
@@ -455,6 +603,7 @@ def run(argv=None) -> Optional[dict]:
 
     # ---------------- main (headline) phase
     gcs, groups, B, G, per, off = bench.offline("main", cons, args.batch)
+    resolved = gcs[0].effective_constructions()
     free_b = total_b = None
     if hip:
         import torch
@@ -475,7 +624,23 @@ def run(argv=None) -> Optional[dict]:
         prof = {k: round(v, 3) for k, v in groups[0].ev.layer_times().items()}
         op_ms = [[n, round(v, 4)] for n, v in groups[0].ev.op_times()]
     verified = r["verified"]
+
+    # ---------------- threads phase: the same loop at smaller host thread budgets (an 8-rank node gives each
+    # rank cores / 8); the step time must not depend on the host encode/decode
+    threads = None
+    if "threads" in phases:
+        threads = {str(bench.threads): dict(ms_per_step=round(ms_step, 3), host_encode_decode_ms_per_step=round(
+            r["host_ms"], 3))}
+        for t in sorted({int(v) for v in args.thread_sweep.split(",") if v.strip()} - {bench.threads}):
+            native().set_num_threads(t)
+            rt = bench.online(gcs, groups, B, per, args.steps, 1, 2000 + t, 0)
+            threads[str(t)] = dict(ms_per_step=round(1000.0 * rt["elapsed"] / args.steps, 3),
+                                   host_encode_decode_ms_per_step=round(all_reduce_max_(ctx, rt["host_ms"]), 3))
+        native().set_num_threads(bench.threads)
     del gcs, groups, r
+
+    # ---------------- latency phase: batch 1, fresh GC per inference (the reference's metric)
+    lat = bench.latency(cons) if "latency" in phases else None
 
     # ---------------- reference-constructions phase (same driver, the reference's gadgets)
     ref = None
@@ -486,7 +651,8 @@ def run(argv=None) -> Optional[dict]:
         r2 = bench.online(g2, grp2, B2, per2, rsteps, max(1, min(args.warmup, 2)), 3000, args.verify)
         ref = dict(value=round(world * B2 * rsteps / r2["elapsed"], 3),
                    ms_per_step=round(1000.0 * r2["elapsed"] / rsteps, 3), gcs_per_gpu=B2, steps=rsteps,
-                   constructions=rc, verified_vs_plaintext=r2["verified"],
+                   constructions=g2[0].effective_constructions(), verified_vs_plaintext=r2["verified"],
+                   gc_reuse=True,
                    offline={"garble_s_per_gc": round(off2["garble_s"] / max(1, B2), 3),
                             "table_gb_per_gc": round(off2["table_gb"], 3)})
         del g2, grp2, r2
@@ -498,6 +664,7 @@ def run(argv=None) -> Optional[dict]:
 
     out = None
     if rank == 0:
+        check_world(args, ctx, recs, rehearsal)
         out = {
             "metric": ("online garbled inferences/sec (MiniONN CIFAR-10 CNN)"
                        if bench.model == "MODEL_F_MINIONN_POOL_REPL" else f"online garbled inferences/sec ({bench.model})"),
@@ -523,16 +690,21 @@ def run(argv=None) -> Optional[dict]:
                 "gcs_per_gpu": B,
                 "streams": G,
                 "constructions": args.constructions,
-                "sign_construction": cons["sign"],
-                "rescale_construction": cons["rescale"],
-                "relu_construction": cons["relu"],
+                "requested_constructions": cons,
+                "sign_construction": resolved["sign"],
+                "rescale_construction": resolved["rescale"],
+                "relu_construction": resolved["relu"],
                 "seq_len": None,
                 "input_shape": list(bench.circuit.input_dims),
                 "parallelism": f"dp{world}",
                 "backend": args.backend,
             },
+            # the headline's GCs are garbled once and re-encoded every step: an online-phase rate (a step's
+            # work equals that of fresh GCs); served_inf_per_s is the protocol-valid fresh-GC rate
+            "gc_reuse": True,
             "dist_backend": ctx.backend if ctx.distributed else "none",
             "world_size": world,
+            "rehearsal_shared_device": rehearsal and world > 1,
             "threads_per_rank": bench.threads,
             "ranks": recs,
             "offline": {"garble_s_per_gc": round(off["garble_s"] / max(1, B), 3),
@@ -542,6 +714,11 @@ def run(argv=None) -> Optional[dict]:
         }
         if hip:
             out["hbm_gb"] = {"used": round((total_b - free_b) / 1e9, 1), "total": round(total_b / 1e9, 1)}
+        if threads is not None:
+            out["host_thread_sweep"] = threads
+        if lat is not None:
+            out["latency_b1_ms"] = lat["latency_b1_ms"]
+            out["latency_b1"] = lat
         if ref is not None:
             out["reference_constructions_value"] = ref["value"]
             out["reference_constructions"] = ref
@@ -555,7 +732,21 @@ def run(argv=None) -> Optional[dict]:
     return out
 
 
+def all_reduce_max_(ctx, v: float) -> float:
+    from .parallel import all_reduce_max
+
+    return all_reduce_max(ctx, v)
+
+
 def main(argv=None) -> None:
+    argv = list(sys.argv[1:] if argv is None else argv)
+    args = parse_args(argv)
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(args, argv))  # parent: starts the ranks, never touches the GPU
     out = run(argv)
     if out is not None:
         print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()

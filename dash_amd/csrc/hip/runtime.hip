@@ -8,6 +8,7 @@
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
+#include <atomic>
 #include <chrono>
 #include <map>
 #include <mutex>
@@ -85,15 +86,20 @@ class HipEvaluator {
         DASH_CHECK(b >= 0 && b < B_, "batch slot out of range");
         auto arena = arena_;
         const int dev = dev_;
+        auto alive = alive_;
         auto s = std::make_shared<TableSink>();
-        s->dest = [arena, b, dev](size_t layer, const std::string& name, size_t nbytes) -> std::shared_ptr<Array::Device> {
+        s->dest = [arena, b, dev, alive](size_t layer, const std::string& name, size_t nbytes) -> std::shared_ptr<Array::Device> {
             auto it = arena.find({layer, name});
             if (it == arena.end() || it->second.second != nbytes) return nullptr;
             auto d = std::make_shared<Array::Device>();
             d->p = std::shared_ptr<void>(it->second.first + nbytes * b, [](void*) {});  // the evaluator owns it
             d->device = dev;
             d->external = true;
-            d->fetch = [dev](void* h, const void* dv, size_t n) {
+            // the arena belongs to the evaluator: a model that outlives it must not read freed HBM
+            d->fetch = [dev, alive](void* h, const void* dv, size_t n) {
+                if (!alive->load())
+                    throw std::runtime_error("dash: garbled tables live in a destroyed HipEvaluator's slot (sink); "
+                                             "the model is no longer readable");
                 HIPCHECK(hipSetDevice(dev));
                 HIPCHECK(hipMemcpy(h, dv, n, hipMemcpyDeviceToHost));
             };
@@ -102,6 +108,7 @@ class HipEvaluator {
         return s;
     }
     ~HipEvaluator() {
+        alive_->store(false);  // orphans every sink-backed model array (fetch raises instead of reading freed HBM)
         if (copy_st_) (void)hipStreamSynchronize(copy_st_);
         for (auto e : ready_) (void)hipEventDestroy(e);
         for (auto e : done_) (void)hipEventDestroy(e);
@@ -267,6 +274,7 @@ class HipEvaluator {
     }
 
    private:
+    std::shared_ptr<std::atomic<bool>> alive_ = std::make_shared<std::atomic<bool>>(true);
     // ------------------------------------------------------------ helpers
     template <typename T>
     T* dalloc(size_t count) {

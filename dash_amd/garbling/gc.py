@@ -35,9 +35,13 @@ def resolve_constructions(circuit: Circuit, crt_base: Sequence[int], rescale: st
     """Resolve "auto" gadget constructions and guard the mixed-radix rescale's range.
 
     rescale="auto" -> "mrs" when the base allows it and the circuit was calibrated
-    (Circuit.calibrate: every DASH rescale has a tracked input range) with no
-    tracked input in the wrap band (Circuit.mrs_rescale_violations); otherwise
-    "legacy", the reference's construction, exact on the whole signed range.
+    (Circuit.calibrate: every DASH rescale has a tracked input range) with every
+    tracked input at least one further 2^l band below the wrap band
+    (Circuit.mrs_rescale_violations(headroom=True)); otherwise "legacy", the
+    reference's construction, exact on the whole signed range. "auto" therefore
+    depends on how well the calibration samples cover the inputs served later:
+    an input beyond the calibrated range by more than 2^l that lands in the
+    band (< 2^l values just below M/2, i.e. next to a CRT overflow) would wrap.
     An explicit "mrs" on a circuit whose tracked range enters the band raises.
     relu="auto" -> "joint" with the mixed-radix rescale, else "approx"."""
     if rescale not in ("auto", "legacy", "mrs"):
@@ -49,7 +53,8 @@ def resolve_constructions(circuit: Circuit, crt_base: Sequence[int], rescale: st
     bad = circuit.mrs_rescale_violations(M) if dash_rescales else []
     if rescale == "auto":
         calibrated = bool(dash_rescales) and all(l.input_tracked for l in dash_rescales)
-        rescale = "mrs" if (mrs_capable(crt_base) and calibrated and not bad) else "legacy"
+        tight = circuit.mrs_rescale_violations(M, headroom=True) if dash_rescales else []
+        rescale = "mrs" if (mrs_capable(crt_base) and calibrated and not bad and not tight) else "legacy"
     elif rescale == "mrs" and bad:
         i, hi, lim = bad[0]
         raise ValueError(f"rescale='mrs': layer {i}'s tracked input reaches {hi} >= {lim}, inside the mixed-radix "
@@ -168,6 +173,35 @@ class GarbledCircuit:
         return HipEvaluator([self.model], **kw)
 
     # -------------------------------------------------------------- helpers
+    def effective_constructions(self) -> dict:
+        """The gadget constructions this GC actually contains (not the requested ones): the mixed-radix
+        rescale applies only to DASH Rescale(l) layers (ReDash Rescale({s}) layers use the base-extension
+        gadget), and a joint ReLU only to a ReLU directly after such a rescale (garbler.cpp joint_out)."""
+        from ..ir.layers import Kind
+
+        specs = self.circuit.garble_specs()
+        dash = [i for i, (k, p) in enumerate(specs) if k == Kind.RESCALE and p.get("mode") == 0]
+        redash = [i for i, (k, p) in enumerate(specs) if k == Kind.RESCALE and p.get("mode") == 1]
+        relus = [i for i, (k, p) in enumerate(specs) if k == Kind.RELU]
+        mrs = self.rescale == "mrs" and bool(dash)
+        parts = []
+        if dash:
+            parts.append("mrs" if mrs else "legacy")
+        if redash:
+            parts.append("redash-base-extension")
+        rescale = "+".join(parts) if parts else "none"
+        joint = [i for i in relus if mrs and self.relu == "joint" and i - 1 in dash and "in_src" not in specs[i][1]]
+        other = "mrs" if self.relu == "mrs" else "approx"
+        if not relus:
+            relu = "none"
+        elif len(joint) == len(relus):
+            relu = "joint"
+        elif joint:
+            relu = f"joint({len(joint)})+{other}({len(relus) - len(joint)})"
+        else:
+            relu = other
+        return dict(sign="fused" if self.fused_sign else "reference", rescale=rescale, relu=relu)
+
     @property
     def table_bytes(self) -> int:
         return self.model.table_bytes()

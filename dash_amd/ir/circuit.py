@@ -108,7 +108,7 @@ class Circuit:
     def _dash_rescales(self):
         return [l for l in self.layers if getattr(l, "use_sign_base_extension", False) and getattr(l, "l", -1) >= 1]
 
-    def mrs_rescale_violations(self, crt_modulus: int) -> list:
+    def mrs_rescale_violations(self, crt_modulus: int, headroom: bool = False) -> list:
         """DASH rescale layers whose tracked input range reaches the mixed-radix wrap
         band [Rescale.mrs_limit(M), M/2): (layer index, tracked max, limit). Empty
         when no layer has been evaluated with range tracking (nothing to check)."""
@@ -116,7 +116,9 @@ class Circuit:
         for i, l in enumerate(self.layers):
             if l in self._dash_rescales() and l.input_tracked:
                 lim = l.mrs_limit(crt_modulus)
-                if l.in_max_q >= lim:
+                # headroom: one further 2^l band above the tracked maximum must stay below the limit (the
+                # tracked range comes from calibration samples; "auto" keeps a margin for unseen inputs)
+                if l.in_max_q + ((1 << l.l) if headroom else 0) >= lim:
                     bad.append((i, int(l.in_max_q), int(lim)))
         return bad
 

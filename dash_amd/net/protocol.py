@@ -37,6 +37,7 @@ class EvaluatorServer:
         assert backend in ("cpu", "hip")
         self.backend, self.device, self.nthreads = backend, device, nthreads
         self.tamper = tamper  # fault injection: flip one output bit (tests)
+        self.input_digests: list = []  # sha256 of every online message #1 received (seed-reuse audits, tests)
         self._reset()
 
     def _reset(self):
@@ -92,6 +93,9 @@ class EvaluatorServer:
         n = native()
         if nb != self.batch or len(self.models) != self.batch:
             raise ValueError(f"online round needs all {self.batch} slots garbled (have {sorted(self.models)})")
+        import hashlib
+
+        self.input_digests.append(hashlib.sha256(bytes(buf)).hexdigest())
         raw = np.frombuffer(buf, dtype=np.uint64)
         per = raw.size // nb
         outs = []

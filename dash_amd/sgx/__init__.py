@@ -53,20 +53,23 @@ def _enclave_main(conn, sock_fd_port, circuit, crt, mrs, max_modulus, batch, sea
     from ..net.protocol import GarblerClient
     from . import attest
 
-    if key_file:
-        os.environ["DASH_PLATFORM_KEY_FILE"] = key_file
-    hard = attest.harden(lock_memory=False)  # mlockall(MCL_FUTURE) makes later allocations fail at the limit
-    cfg = _config(circuit, crt, mrs, max_modulus)
-    meas = attest.measure(cfg)
-    report = hashlib.sha256(b"dash_amd garbler v1" + json.dumps(cfg, sort_keys=True).encode()).digest()
     try:
+        if key_file:
+            os.environ["DASH_PLATFORM_KEY_FILE"] = key_file
+        hard = attest.harden(lock_memory=False)  # mlockall(MCL_FUTURE) makes later allocations fail at the limit
+        cfg = _config(circuit, crt, mrs, max_modulus)
+        meas = attest.measure(cfg)
+        report = hashlib.sha256(b"dash_amd garbler v1" + json.dumps(cfg, sort_keys=True).encode()).digest()
         if sealed is not None:
-            # resume: master secret + GC counter, so no per-GC seed is ever reused across restarts
+            # resume: the sealed master secret is re-keyed with fresh enclave randomness, so a replayed or
+            # duplicated blob (the host controls which blob it hands back) can never reproduce a per-GC seed;
+            # the counter only continues the numbering
             state, _ = attest.unseal(sealed, meas)
-            master, ctr = state[:32], int.from_bytes(state[32:40], "little")
+            master = hashlib.sha256(b"dash_amd resume" + state[:32] + secrets.token_bytes(32)).digest()
+            ctr = int.from_bytes(state[32:40], "little")
         else:
             master, ctr = secrets.token_bytes(32), 0
-    except Exception as e:
+    except BaseException as e:  # every failure before 'ready' reaches the host instead of a silent death
         conn.send(("error", repr(e), None))
         conn.close()
         return
@@ -111,11 +114,14 @@ class GarblerEnclave:
     attest: verify the enclave's quote (fresh nonce, expected measurement of this garbler build and circuit
     configuration) before any input is handed over; AttestationError otherwise.
     sealed_state: a blob from seal_state() of an earlier enclave of the same build and configuration: the
-    garbler resumes its master secret and GC counter (no per-GC seed reuse across restarts)."""
+    garbler resumes from it with its master secret re-keyed by fresh enclave randomness, so no per-GC seed is
+    reused even when the host replays one blob to several enclaves.
+
+    start_timeout_s: the enclave must report ready (and connect back) within this time, else SealError."""
 
     def __init__(self, circuit, crt, mrs=None, max_modulus: int = 0, batch: int = 1, backend: str = "hip",
                  device: int = 0, attest: bool = True, sealed_state: Optional[bytes] = None,
-                 platform_key_file: Optional[str] = None):
+                 platform_key_file: Optional[str] = None, start_timeout_s: float = 120.0):
         from ..net.channel import Channel
         from ..net.protocol import EvaluatorServer
         from . import attest as at
@@ -133,13 +139,31 @@ class GarblerEnclave:
                                        sealed_state, platform_key_file),
                                  daemon=True)
         self._proc.start()
-        status, info, _ = self._conn.recv()
-        if status != "ready":
-            self._proc.join(timeout=30)
+        child.close()  # the child's end lives in the child only: a dead child reads as EOF here
+
+        def _fail(why: str):
             lst.close()
-            raise at.SealError(f"garbler enclave failed to start: {info}")
+            if self._proc.is_alive():
+                self._proc.terminate()
+            self._proc.join(timeout=30)
+            raise at.SealError(f"garbler enclave failed to start: {why}")
+
+        try:
+            if not self._conn.poll(start_timeout_s):
+                _fail(f"no ready message within {start_timeout_s:.0f} s (alive={self._proc.is_alive()})")
+            status, info, _ = self._conn.recv()
+        except EOFError:
+            _fail(f"enclave process exited (code {self._proc.exitcode})")
+        if status != "ready":
+            _fail(str(info))
         self.hardening = info
-        conn, _ = lst.accept()
+        lst.settimeout(start_timeout_s)
+        try:
+            conn, _ = lst.accept()
+        except OSError:  # timeout: the enclave's client never connected; its reason is on the pipe
+            why = self._conn.recv()[1] if self._conn.poll(1.0) else "no connection"
+            _fail(f"garbler did not connect: {why}")
+        conn.settimeout(None)
         lst.close()
         self._server = EvaluatorServer(backend, device)
         self._thread = threading.Thread(target=self._server.serve, args=(Channel(conn),), daemon=True)

@@ -35,11 +35,30 @@ def test_enclave_ann_infer_attested_cpu(keyfile):
     with GarblerEnclave(c, 7, 100.0, batch=2, backend="cpu", platform_key_file=keyfile, sealed_state=blob) as enc2:
         out2 = enc2.ann_infer(xs[:2])
     np.testing.assert_array_equal(out2, out[:2])
+    # resuming one blob twice (a replay by the untrusted host) must not repeat any GC seed: the same inputs
+    # are encoded under different labels
+    with GarblerEnclave(c, 7, 100.0, batch=2, backend="cpu", platform_key_file=keyfile, sealed_state=blob) as enc3:
+        out3 = enc3.ann_infer(xs[:2])
+    np.testing.assert_array_equal(out3, out[:2])
+    assert enc2._server.input_digests and enc3._server.input_digests
+    assert enc2._server.input_digests[0] != enc3._server.input_digests[0]
     # a modified blob is refused at start
     bad = bytearray(blob)
     bad[-40] ^= 1
     with pytest.raises(at.SealError):
         GarblerEnclave(c, 7, 100.0, batch=2, backend="cpu", platform_key_file=keyfile, sealed_state=bytes(bad))
+
+
+def test_enclave_start_failure_does_not_block(keyfile, monkeypatch):
+    """An enclave that dies before 'ready' (here: an unsealable blob makes it exit) is reported, not waited on."""
+    import time
+
+    c = build_circuit("MODEL_A")
+    t = time.perf_counter()
+    with pytest.raises(at.SealError):
+        GarblerEnclave(c, 7, 100.0, batch=2, backend="cpu", platform_key_file=keyfile, sealed_state=b"x" * 64,
+                       start_timeout_s=60)
+    assert time.perf_counter() - t < 60
 
 
 def test_quote_checks(keyfile):

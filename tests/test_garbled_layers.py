@@ -469,8 +469,15 @@ def test_rescale_mrs_wrap_band_guard():
     assert c.required_crt_modulus() == 2 * (104 + 4)
     assert c.infer_crt_base_size([band], rescale_margin=False) == 4
     assert c.infer_crt_base_size([band]) == 5
-    # below the band: calibrated auto picks the mixed-radix construction and it is exact
-    ok = np.arange(90, 103, dtype=np.int64)
+    # just below the band without a further 2^l of headroom: explicit "mrs" is exact, "auto" stays legacy
+    near = np.arange(99, 103, dtype=np.int64)
+    c1 = d.Circuit([d.Rescale(l, (near.size,))]).calibrate([near])
+    assert GarbledCircuit(c1, crt, 100.0, seed=SEED, garble_me=False).rescale == "legacy"
+    g1 = GarbledCircuit(c1, crt, 100.0, seed=SEED, rescale="mrs")
+    np.testing.assert_array_equal(g1.decode_outputs(g1.cpu_evaluate(g1.garble_inputs(near))),
+                                  c1.plain_q_eval(near, False, M))
+    # well below the band: calibrated auto picks the mixed-radix construction and it is exact
+    ok = np.arange(90, 99, dtype=np.int64)
     c2 = d.Circuit([d.Rescale(l, (ok.size,))]).calibrate([ok])
     g2 = GarbledCircuit(c2, crt, 100.0, seed=SEED)
     assert g2.rescale == "mrs" and g2.relu == "joint"

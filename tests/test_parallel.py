@@ -57,9 +57,9 @@ def _bench_worker(rank, world, port, q):
                       MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     from dash_amd import benchcore
 
-    out = benchcore.run(["--backend", "cpu", "--model", "MODEL_A", "--batch", "2", "--streams", "1", "--steps", "2",
-                         "--warmup", "1", "--phases", "main,served", "--served-slots", "2", "--served-groups", "2",
-                         "--served-requests", "1"])
+    out = benchcore.run(["--backend", "cpu", "--gpus", str(world), "--model", "MODEL_A", "--batch", "2", "--streams",
+                         "1", "--steps", "2", "--warmup", "1", "--phases", "main,served", "--served-slots", "2",
+                         "--served-groups", "2", "--served-requests", "1", "--served-min-s", "0"])
     q.put((rank, out))
 
 
@@ -112,3 +112,54 @@ def test_batch_dp_hip_single_rank():
         out = dp.infer(xs)
         ref = GarbledCircuit(c, 7, 100.0, garble_me=False)
         np.testing.assert_array_equal(out, np.stack([ref.plain_q_eval(x) for x in xs]))
+
+
+def _run_bench_cli(args, timeout=600):
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "LOCAL_WORLD_SIZE")}
+    return subprocess.run([sys.executable, os.path.join(root, "bench.py"), *args], capture_output=True, text=True,
+                          timeout=timeout, env=env, cwd=root)
+
+
+def test_bench_cli_spawns_ranks():
+    """`python bench.py --gpus 4` with no launcher starts 4 fresh ranks itself (no torchrun by the caller) and
+    prints rank 0's record with world size 4 and one record per rank."""
+    import json
+
+    p = _run_bench_cli(["--backend", "cpu", "--gpus", "4", "--model", "MODEL_A", "--batch", "2", "--streams", "1",
+                        "--steps", "2", "--warmup", "1", "--phases", "main,latency", "--latency-gcs", "2"])
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [l for l in p.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, p.stdout
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 4 and out["world_size"] == 4 and out["dist_backend"] == "gloo"
+    assert [r["rank"] for r in out["ranks"]] == [0, 1, 2, 3]
+    assert len({r["pid"] for r in out["ranks"]}) == 4
+    assert out["gc_reuse"] is True and out["latency_b1"]["verified"] and out["latency_b1_ms"] > 0
+    assert out["config"]["rescale_construction"] in ("mrs", "legacy", "none")
+
+
+def test_bench_cli_refuses_world_mismatch():
+    """Under a launcher, --gpus must equal WORLD_SIZE (a 1-rank job never reports itself as N GPUs)."""
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    p = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--backend", "cpu", "--gpus", "2",
+                        "--model", "MODEL_A", "--batch", "2", "--steps", "1", "--phases", "main"],
+                       capture_output=True, text=True, timeout=300, env=env, cwd=root)
+    assert p.returncode != 0 and "WORLD_SIZE" in p.stderr
+
+
+def test_bench_cli_refuses_missing_gpus():
+    """--gpus N on a host with fewer visible GPUs fails loudly unless the shared-device rehearsal is asked for."""
+    import torch
+
+    if torch.cuda.device_count() >= 2:
+        pytest.skip("host has 2+ GPUs")
+    p = _run_bench_cli(["--gpus", "2", "--steps", "1"], timeout=300)
+    assert p.returncode == 2 and "refusing" in p.stderr

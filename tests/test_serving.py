@@ -134,6 +134,40 @@ def test_service_hip_matches_plaintext_and_recovers(small):
 
 
 @pytest.mark.gpu
+def test_service_hip_concurrent_refill_no_spurious_failures(small):
+    """Regression (HipEvaluator.load serialization, runtime.hip load_mu_): 4 refill workers loading slots of the
+    same evaluators concurrently, no injected faults -> no integrity failure, no retry, exact outputs."""
+    c, xs = small
+    xs4 = [xs[i % len(xs)] for i in range(24)]
+    with InferenceService(c, 8, 100.0, backend="hip", slots_per_group=4, groups=2, device=0, garble_workers=4,
+                          seed=b"c" * 16, insecure_fixed_seed=True, step_timeout_s=60) as svc:
+        ys = [svc.infer(xs4[i:i + 8]) for i in range(0, 24, 8)]
+        st = svc.stats.as_dict()
+    np.testing.assert_array_equal(np.concatenate(ys), _ref(c, xs4))
+    assert st["integrity_failures"] == 0 and st["retries"] == 0 and st["timeouts"] == 0
+
+
+@pytest.mark.gpu
+def test_sink_model_orphaned_by_evaluator_raises(small):
+    """A GC garbled into an evaluator slot (sink) aliases that evaluator's HBM: after the evaluator is gone its
+    tables must refuse a host read instead of reading freed memory."""
+    import gc as pygc
+
+    from dash_amd.garbling import GarbledCircuit
+    from dash_amd.runtime import HipEvaluator
+
+    c, xs = small
+    g0 = GarbledCircuit(c, 8, 100.0, seed=b"s" * 16, device=0)
+    ev = HipEvaluator(template=g0.model, batch=1, device=0)
+    g1 = GarbledCircuit(c, 8, 100.0, seed=b"t" * 16, device=0, sink=ev.sink(0))
+    ev.load(0, g1.model)
+    del ev
+    pygc.collect()
+    with pytest.raises(RuntimeError, match="destroyed HipEvaluator"):
+        g1.model.serialize()
+
+
+@pytest.mark.gpu
 def test_hip_stream_wait_bounded():
     from dash_amd.native import native
 
