@@ -634,13 +634,18 @@ def run(argv=None) -> Optional[dict]:
         for t in sorted({int(v) for v in args.thread_sweep.split(",") if v.strip()} - {bench.threads}):
             native().set_num_threads(t)
             rt = bench.online(gcs, groups, B, per, args.steps, 1, 2000 + t, 0)
+            rt.pop("step")  # the closure holds the groups (all of the phase's HBM)
             threads[str(t)] = dict(ms_per_step=round(1000.0 * rt["elapsed"] / args.steps, 3),
                                    host_encode_decode_ms_per_step=round(all_reduce_max_(ctx, rt["host_ms"]), 3))
         native().set_num_threads(bench.threads)
+        log(f"[threads] {threads}")
+    r.pop("step")
     del gcs, groups, r
 
     # ---------------- latency phase: batch 1, fresh GC per inference (the reference's metric)
     lat = bench.latency(cons) if "latency" in phases else None
+    if lat is not None:
+        log(f"[latency] {lat}")
 
     # ---------------- reference-constructions phase (same driver, the reference's gadgets)
     ref = None

@@ -244,6 +244,22 @@ PYBIND11_MODULE(_dash_native, m) {
     py::class_<GarbledModel, std::shared_ptr<GarbledModel>>(m, "GarbledModel")
         .def("serialize", [](const GarbledModel& g) { return py::bytes(g.serialize()); })
         .def_static("deserialize", [](py::bytes b) { return std::make_shared<GarbledModel>(GarbledModel::deserialize(std::string(b))); })
+        .def("serialized_size", &GarbledModel::serialized_size)
+        .def("serialize_into", [](const GarbledModel& g, py::buffer b) {
+            py::buffer_info bi = b.request(true);
+            DASH_CHECK(bi.itemsize == 1 || bi.ndim == 1, "serialize_into needs a writable byte buffer");
+            const size_t cap = static_cast<size_t>(bi.size) * static_cast<size_t>(bi.itemsize);
+            py::gil_scoped_release nogil;
+            return g.serialize_to(static_cast<uint8_t*>(bi.ptr), cap);
+        }, "write the offline message into a writable buffer (>= serialized_size() bytes) -> bytes written; "
+           "device-resident tables are fetched straight into it")
+        .def_static("deserialize_buffer", [](py::buffer b) {
+            py::buffer_info bi = b.request();
+            const size_t n = static_cast<size_t>(bi.size) * static_cast<size_t>(bi.itemsize);
+            const uint8_t* p = static_cast<const uint8_t*>(bi.ptr);
+            py::gil_scoped_release nogil;
+            return std::make_shared<GarbledModel>(GarbledModel::deserialize(p, n));
+        }, "parse an offline message from any byte buffer (no intermediate copy)")
         .def_property_readonly("crt", [](const GarbledModel& g) { return g.h.crt; })
         .def_property_readonly("mrs", [](const GarbledModel& g) { return g.h.mrs; })
         .def_property_readonly("in_dims", [](const GarbledModel& g) { return g.h.in_dims; })

@@ -440,7 +440,14 @@ GarbledModel Garbler::garble(const std::vector<LayerSpec>& layers, const std::ve
     std::vector<int> cur_mod = crt_;
     std::vector<i64> dims = in_dims;
     if (keep[0]) {
-        saved[0] = cur;
+        // with a GPU garbler, outputs read again later (residual adds, in_src) are kept as device copies
+        if (gpu) {
+            gpu->to_device(cur);
+            dev_ok = true;
+            gpu->save(0);
+        } else {
+            saved[0] = cur;
+        }
         saved_mod[0] = cur_mod;
         saved_dims[0] = dims;
     }
@@ -467,9 +474,15 @@ GarbledModel Garbler::garble(const std::vector<LayerSpec>& layers, const std::ve
             if (it != spec.p.end() && !it->second.empty()) {
                 const i64 s = it->second[0];
                 DASH_CHECK(s >= -1 && s < static_cast<i64>(li), "in_src must name an earlier layer");
-                cur = saved[s + 1];
-                host_ok = true;
-                dev_ok = false;
+                if (gpu) {
+                    gpu->restore(static_cast<size_t>(s + 1), cur);
+                    host_ok = false;
+                    dev_ok = true;
+                } else {
+                    cur = saved[s + 1];
+                    host_ok = true;
+                    dev_ok = false;
+                }
                 cur_mod = saved_mod[s + 1];
                 dims = saved_dims[s + 1];
             }
@@ -491,8 +504,12 @@ GarbledModel Garbler::garble(const std::vector<LayerSpec>& layers, const std::ve
         const bool relu_mrs = opt.relu_mrs && spec.kind == K_RELU;
         const bool joint_out = mrs_rescale && opt.relu_joint && li + 1 < layers.size() &&
                                layers[li + 1].kind == K_RELU && param1(layers[li + 1].p, "in_src", -2) == -2;
+        // every layer kind but the test-only projection / mult layers garbles on the device when a GPU garbler
+        // is present (the legacy rescale's sign base extension needs residue 0 = 2)
         const bool on_gpu = gpu && (spec.kind == K_CONV || spec.kind == K_RELU || spec.kind == K_SIGN ||
-                                    (spec.kind == K_RESCALE && param1(spec.p, "mode", 0) == 0 && crt_[0] == 2));
+                                    spec.kind == K_DENSE || spec.kind == K_SUMPOOL || spec.kind == K_ADD ||
+                                    spec.kind == K_MAXPOOL || spec.kind == K_MAX || spec.kind == K_BASEEXT ||
+                                    (spec.kind == K_RESCALE && (param1(spec.p, "mode", 0) != 0 || crt_[0] == 2)));
         const bool passthru = spec.kind == K_FLATTEN;
         if (on_gpu && !dev_ok) {
             gpu->to_device(cur);
@@ -527,6 +544,7 @@ GarbledModel Garbler::garble(const std::vector<LayerSpec>& layers, const std::ve
                     for (i64 o = 0; o < out; ++o)
                         lab_affine(bias.ptr<comp_t>() + o * mi.n, Zp, pmod(pmod(b[o], M_), p), R_.get(p), mi.n, p);
                     g.a[arr_name("bias.", j, "")] = bias;
+                    if (on_gpu) continue;
                     const Labels& I = cur[j];
                     parallel_for(out, [&](i64 b0, i64 b1) {
                         std::vector<i64> acc(mi.n);
@@ -549,7 +567,8 @@ GarbledModel Garbler::garble(const std::vector<LayerSpec>& layers, const std::ve
                     }, nt);
                     nxt.push_back(std::move(O));
                 }
-                cur = std::move(nxt);
+                if (on_gpu) gpu->dense(in, out, ch, std::vector<i64>(wa.ptr<i64>(), wa.ptr<i64>() + wa.count()), cur);
+                else cur = std::move(nxt);
                 dims = {out};
                 break;
             }
@@ -807,8 +826,11 @@ GarbledModel Garbler::garble(const std::vector<LayerSpec>& layers, const std::ve
                     } else {
                         be = Array(DType::u128, {Nin, P.n_be});
                     }
-                    if (on_gpu) {
-                        DASH_CHECK(P.sign_be, "gpu garbler: legacy rescale plan without sign base extension");
+                    if (on_gpu && !P.sign_be) {
+                        sinkify(tr, pre + "trans");
+                        sinkify(be, pre + "be");
+                        gpu->rescale_redash(L, static_cast<int>(it), P, cur, up_base, dn, tr, be);
+                    } else if (on_gpu) {
                         sinkify(tr, pre + "trans");
                         sinkify(ap, pre + "s.approx");
                         sinkify(c1, pre + "s.cast1");
@@ -869,6 +891,25 @@ GarbledModel Garbler::garble(const std::vector<LayerSpec>& layers, const std::ve
                 }
                 MaxTree T(K);
                 SignPlan sp(crt_, mrs_, {2}, 0, 1, fused);
+                if (on_gpu) {
+                    gpu->maxpool_begin(win, cur);
+                    for (size_t lv = 0; lv < T.ops.size(); ++lv) {
+                        ReluTables t = make_relu_tables(sp, Nout * T.ops[lv], sum_crt, k);
+                        const std::string pre = arr_name("lv", static_cast<int>(lv), ".");
+                        sinkify(t.approx, pre + "s.approx");
+                        sinkify(t.cast1, pre + "s.cast1");
+                        sinkify(t.cast2, pre + "s.cast2");
+                        sinkify(t.sign, pre + "s.sign");
+                        sinkify(t.g, pre + "mm.g");
+                        sinkify(t.e, pre + "mm.e");
+                        gpu->maxpool_level(L, static_cast<int>(lv), T.ops[lv], sp, prefix, t.approx, t.cast1, t.cast2,
+                                           t.sign, t.g, t.e);
+                        put_relu_tables(g, pre, t);
+                    }
+                    gpu->maxpool_end(cur);
+                    g.p["levels"] = {static_cast<i64>(T.ops.size())};
+                    break;
+                }
                 // value slots: vals[j] holds Nout x cnt labels (slot-major per output)
                 std::vector<Labels> vals;
                 for (int j = 0; j < k; ++j) {
@@ -924,6 +965,11 @@ GarbledModel Garbler::garble(const std::vector<LayerSpec>& layers, const std::ve
                 DASH_CHECK(is_crt(), "sum pool needs CRT-base labels");
                 PoolGeom G(spec.p);
                 DASH_CHECK(G.C * G.H * G.W == Nin, "sumpool input size mismatch");
+                if (on_gpu) {
+                    gpu->sumpool(G, cur);
+                    dims = {G.C, G.OH, G.OW};
+                    break;
+                }
                 CrtLabels nxt;
                 std::vector<i64> w;
                 for (int j = 0; j < k; ++j) {
@@ -942,6 +988,10 @@ GarbledModel Garbler::garble(const std::vector<LayerSpec>& layers, const std::ve
             case K_ADD: {
                 const i64 src = param1(spec.p, "src");
                 DASH_CHECK(src >= -1 && src < static_cast<i64>(li), "add: bad source layer");
+                if (on_gpu) {
+                    gpu->add_saved(static_cast<size_t>(src + 1), cur);
+                    break;
+                }
                 const CrtLabels& other = saved[src + 1];
                 DASH_CHECK(!other.empty() && other[0].N == Nin, "add: operand size mismatch");
                 for (int j = 0; j < k; ++j)
@@ -1037,6 +1087,12 @@ GarbledModel Garbler::garble(const std::vector<LayerSpec>& layers, const std::ve
                 for (auto v : paramv(spec.p, "extra")) ext.push_back(static_cast<int>(v));
                 BEPlan P(crt_, ext);
                 Array be(DType::u128, {Nin, P.n_tab});
+                if (on_gpu) {
+                    sinkify(be, "be");
+                    gpu->base_ext(L, P, cur, be);
+                    g.a["be"] = be;
+                    break;
+                }
                 parallel_for(Nin, [&](i64 b0, i64 b1) {
                     std::vector<comp_t*> Lp(k);
                     for (i64 e = b0; e < b1; ++e) {
@@ -1056,11 +1112,15 @@ GarbledModel Garbler::garble(const std::vector<LayerSpec>& layers, const std::ve
         if (on_gpu) host_ok = false;
         else if (!passthru) dev_ok = false;
         if (keep[li + 1]) {
-            if (!host_ok) {
-                gpu->to_host(cur);
-                host_ok = true;
+            if (gpu) {
+                if (!dev_ok) {
+                    gpu->to_device(cur);
+                    dev_ok = true;
+                }
+                gpu->save(li + 1);
+            } else {
+                saved[li + 1] = cur;
             }
-            saved[li + 1] = cur;
             saved_mod[li + 1] = cur_mod;
             saved_dims[li + 1] = dims;
         }

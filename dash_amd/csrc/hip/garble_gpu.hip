@@ -1032,6 +1032,161 @@ __global__ __launch_bounds__(256) void k_rescale_post_g(Ctx c, RsArgs a, Gadget 
     }
 }
 
+// ---------------------------------------------------------------------------
+// Label algebra of the remaining layer kinds (dense, sum / max pooling, residual
+// add, ReDash rescale, base extension). All labels are chunked component-major
+// (kCh), so each thread moves one 16-byte chunk (8 components) of one element.
+
+// dst = ca a + cb b + cr r (mod p), any operand optional. A label set has element stride 8 and chunk stride
+// 8 N; a uniform row (R_p, Z_p, a shift label) element stride 0 and chunk stride 8. Chunk padding past n stays 0
+// when the operands' padding is 0 (draws, rows and every kernel here keep it 0).
+struct LinJob {
+    int16_t* dst;
+    const int16_t* a;
+    const int16_t* b;
+    const int16_t* r;
+    int64_t aes, acs, bes, bcs;
+    int p, nc;
+    int ca, cb, cr;
+};
+constexpr int kMaxLin = 24;
+struct LinArgs {
+    LinJob j[kMaxLin];
+    int n;
+    int64_t N;
+};
+__global__ __launch_bounds__(256) void k_lin(Ctx c, LinArgs a) {
+    const LinJob J = a.j[blockIdx.y];
+    const ModC m = c.mc[J.p];
+    const int64_t N = a.N, total = N * J.nc;
+    const uint32_t ca = J.ca, cb = J.cb, cr = J.cr;
+    for (int64_t x = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; x < total;
+         x += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+        const int c8 = static_cast<int>(x / N);
+        const int64_t e = x - static_cast<int64_t>(c8) * N;
+        uint32_t acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, t[8];
+        if (J.a) {
+            unpack8(*reinterpret_cast<const u32x4a*>(J.a + e * J.aes + c8 * J.acs), t);
+#pragma unroll
+            for (int u = 0; u < 8; ++u) acc[u] += ca * t[u];
+        }
+        if (J.b) {
+            unpack8(*reinterpret_cast<const u32x4a*>(J.b + e * J.bes + c8 * J.bcs), t);
+#pragma unroll
+            for (int u = 0; u < 8; ++u) acc[u] += cb * t[u];
+        }
+        if (J.r) {
+            unpack8(*reinterpret_cast<const u32x4a*>(J.r + c8 * kCh), t);
+#pragma unroll
+            for (int u = 0; u < 8; ++u) acc[u] += cr * t[u];
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) acc[u] = modq(acc[u], m);
+        st_chunk(J.dst + (static_cast<int64_t>(c8) * N + e) * kCh, pack8(acc));
+    }
+}
+
+// Gathered sums: dst[e] (+)= sum_t cf[t] src[map[e K + t]] (mod p); map entries < 0 are skipped. Max-pool
+// window gathers, pair differences and recombination, sum-pool windows.
+constexpr int kMaxTerms = 16;
+struct GsJob {
+    int16_t* dst;
+    const int16_t* src;
+    int p, nc;
+    int cf[kMaxTerms];
+};
+struct GsArgs {
+    GsJob j[kMaxRes];
+    int n, K, acc;
+    int64_t N, Nsrc;
+    const int32_t* map;
+};
+__global__ __launch_bounds__(256) void k_gsum(Ctx c, GsArgs a) {
+    const GsJob& J = a.j[blockIdx.y];
+    const ModC m = c.mc[J.p];
+    const int64_t N = a.N, total = N * J.nc;
+    for (int64_t x = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; x < total;
+         x += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+        const int c8 = static_cast<int>(x / N);
+        const int64_t e = x - static_cast<int64_t>(c8) * N;
+        int16_t* d = J.dst + (static_cast<int64_t>(c8) * N + e) * kCh;
+        uint32_t acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, t[8];
+        if (a.acc) unpack8(*reinterpret_cast<const u32x4a*>(d), acc);
+        for (int s = 0; s < a.K; ++s) {
+            const int32_t src = a.map[e * a.K + s];
+            if (src < 0) continue;
+            unpack8(*reinterpret_cast<const u32x4a*>(J.src + (static_cast<int64_t>(c8) * a.Nsrc + src) * kCh), t);
+            const uint32_t f = static_cast<uint32_t>(J.cf[s]);
+#pragma unroll
+            for (int u = 0; u < 8; ++u) acc[u] += f * t[u];
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) acc[u] = modq(acc[u], m);
+        st_chunk(d, pack8(acc));
+    }
+}
+
+// Dense base labels y_o = sum_i w_oi x_i + zc_o Z_p (mod p), weights reduced mod p and transposed ([in][out],
+// rows already in the channel_tf source order), zc_o = 1 + #(w_oi = 0 mod p) (the reference's zero-weight Z
+// quirk, and the bias label's Z). Block: 64 outputs x 4 input groups for one (chunk, residue); the groups'
+// partial sums meet in LDS.
+struct DnJob {
+    int16_t* dst;
+    const int16_t* x;
+    const int16_t* wt;
+    const int32_t* zc;
+    int p, nc;
+};
+struct DnArgs {
+    DnJob j[kMaxRes];
+    int n, in, out, otiles;
+};
+__global__ __launch_bounds__(256) void k_gdense(Ctx c, DnArgs a) {
+    __shared__ uint32_t part[3][64][9];
+    const DnJob J = a.j[blockIdx.y];
+    const int c8 = static_cast<int>(blockIdx.x) / a.otiles;
+    if (c8 >= J.nc) return;
+    const int o = (static_cast<int>(blockIdx.x) - c8 * a.otiles) * 64 + (threadIdx.x & 63);
+    const int grp = threadIdx.x >> 6;
+    const ModC m = c.mc[J.p];
+    const int64_t xcs = static_cast<int64_t>(a.in) * kCh;
+    uint32_t acc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, t[8];
+    if (o < a.out) {
+        int since = 0;
+        for (int i = grp; i < a.in; i += 4) {
+            const uint32_t w = static_cast<uint16_t>(J.wt[static_cast<int64_t>(i) * a.out + o]);
+            if (w) {
+                unpack8(*reinterpret_cast<const u32x4a*>(J.x + c8 * xcs + static_cast<int64_t>(i) * kCh), t);
+#pragma unroll
+                for (int u = 0; u < 8; ++u) acc[u] += w * t[u];
+            }
+            if (++since == 256) {  // w, x < p <= 2048: 256 products stay below 2^30 on top of a residue
+                since = 0;
+#pragma unroll
+                for (int u = 0; u < 8; ++u) acc[u] = modq(acc[u], m);
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) acc[u] = modq(acc[u], m);
+    }
+    if (grp > 0) {
+#pragma unroll
+        for (int u = 0; u < 8; ++u) part[grp - 1][threadIdx.x & 63][u] = acc[u];
+    }
+    __syncthreads();
+    if (grp == 0 && o < a.out) {
+        unpack8(*reinterpret_cast<const u32x4a*>(c.Z + static_cast<int64_t>(J.p) * kW + c8 * kCh), t);
+        const uint32_t zc = static_cast<uint32_t>(J.zc[o]);
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            uint32_t v = acc[u] + part[0][o & 63][u] + part[1][o & 63][u] + part[2][o & 63][u];
+            v = modq(v, m) + modq(zc, m) * t[u];
+            acc[u] = modq(v, m);
+        }
+        st_chunk(J.dst + (static_cast<int64_t>(c8) * a.out + o) * kCh, pack8(acc));
+    }
+}
+
 // ------------------------------------------------------------------- host
 struct SignLayout {
     std::vector<Draw> draws;
@@ -1886,6 +2041,16 @@ struct GpuGarbler::Impl {
     int sig_slot = -1;
     int64_t sig_N = 0;
     const int16_t* sig_S = nullptr;
+    // device copies of layer outputs that a later residual add or in_src layer reads (index = layer + 1)
+    struct Saved {
+        std::vector<DevBlock> L;
+        std::vector<int> mods;
+        int64_t N = 0;
+    };
+    std::map<size_t, Saved> saved;
+    // max pool in progress: value slots [Nout][cnt] (output-major) of the current tree level
+    std::vector<DevBlock> mp_V;
+    int64_t mp_Nout = 0, mp_cnt = 0;
     explicit Impl(int dev) : lock(acquire_ctx(dev, dcp)), dc(*dcp), device(dev) {}
     template <class T>
     const T* stage(const T* h, size_t n) { return dc.stage(h, n); }
@@ -2146,17 +2311,16 @@ void GpuGarbler::conv(const ConvGeom& G, const std::vector<i64>& w, CrtLabels& c
     set_stale(cur, mods, I.cur_N);
 }
 
-void GpuGarbler::sign_layer(uint64_t layer, const SignPlan& sp, CrtLabels& cur, Array& ap, Array& c1, Array& c2,
-                            Array& sg, const std::vector<int>* relu_crt, const std::vector<i64>* prefix, Array* mmg,
-                            Array* mme) {
-    Impl& I = *impl_;
-    I.enter();
-    I.check_cur(cur);
-    PhaseTrace tr_(relu_crt ? "relu" : "sign");
-    const int64_t N = I.cur_N;
+// Sign gadget (+ the ReLU's mixed-modulus half gates when prefix/mmg/mme are set) over N elements whose input
+// labels are `in`: PRG streams (layer, sslot_s) for the sign and (layer, sslot_m) for the half gates. Returns
+// the output base labels (out_mod of the plan, or the CRT base for a ReLU). Shared by Sign, ReLU and every
+// level of a max pool (relu_garble_elem with its own stream slots).
+static std::vector<DevBlock> sign_core(GpuGarbler::Impl& I, uint64_t layer, uint64_t sslot_s, uint64_t sslot_m,
+                                       const SignPlan& sp, const gg::In& in, int64_t N, Array& ap, Array& c1,
+                                       Array& c2, Array& sg, const std::vector<i64>* prefix, Array* mmg, Array* mme,
+                                       std::vector<int>& omods) {
     const int k = I.k;
-    std::vector<void*> tmp;
-    const bool relu = relu_crt != nullptr;
+    const bool relu = prefix != nullptr;
     // relu: 2 slots per residue for the mixed-mult output labels sk03/sk04
     gg::SignLayout L = gg::sign_layout(sp, relu ? 2 * k : 0);
     int sk0 = L.nslots - (relu ? 2 * k : 0);
@@ -2177,33 +2341,25 @@ void GpuGarbler::sign_layer(uint64_t layer, const SignPlan& sp, CrtLabels& cur, 
         tb.t[4] = tG.p(); tb.row[4] = tG.row;
         tb.t[5] = tE.p(); tb.row[5] = tE.row;
     }
-    tr_.mark("alloc");
-    gg::In in{};
-    for (int j = 0; j < k; ++j) {
-        in.p[j] = I.cur[j].as<int16_t>();
-        in.n[j] = nr_comps(I.crt[j]);
-        in.es[j] = gg::kCh;  // chunked component-major
-        in.cs[j] = N * gg::kCh;
-    }
     gg::Gadget g{};
     g.layer = layer;
-    g.sslot = 1;
+    g.sslot = sslot_s;
     g.mask = 0;
     g.S = S;
     g.PB = I.pbank(2, N);
     g.N = N;
     g.nslots = L.nslots;
     run_sign(I.c, L, g, in, tb, I.lut_fns());
-    std::vector<int> omods = relu ? I.crt : sp.out_mod;
+    omods = relu ? I.crt : sp.out_mod;
     std::vector<DevBlock> out = I.alloc_labels(omods, N);
     if (relu) {
-        // mixed-mult draws (stream slot 2, counters run over the residues) and the g/e projections
+        // mixed-mult draws (stream slot sslot_m, counters run over the residues) and the g/e projections
         std::vector<gg::Draw> dr;
         std::vector<gg::Proj> pr;
         int ctr = 0;
         int64_t first = 0;
         for (int j = 0; j < k; ++j) {
-            const int p = I.crt[j], n = nr_comps(p);
+            const int p = I.crt[j];
             dr.push_back({sk0 + 2 * j, p, ctr});
             ctr += prg_blocks(p);
             dr.push_back({sk0 + 2 * j + 1, p, ctr});
@@ -2224,7 +2380,7 @@ void GpuGarbler::sign_layer(uint64_t layer, const SignPlan& sp, CrtLabels& cur, 
         }
         // the e table row is [k][3]: projection entries land at j*3 + color
         gg::Gadget gm = g;
-        gm.sslot = 2;
+        gm.sslot = sslot_m;
         gm.draws = gg::dconst(dr.data(), dr.size());
         gm.ndraws = static_cast<int>(dr.size());
         gm.projs = gg::dconst(pr.data(), pr.size());
@@ -2257,12 +2413,39 @@ void GpuGarbler::sign_layer(uint64_t layer, const SignPlan& sp, CrtLabels& cur, 
                                     hipMemcpyDeviceToDevice, gg::tl_st));
     }
     HIPCHECK(hipGetLastError());
-    gg::end_layer(tmp);
-    tr_.mark("kernels");
     tA.to_array(ap, I.device);
     if (sp.has_cast1()) t1.to_array(c1, I.device);
     t2.to_array(c2, I.device);
     tS.to_array(sg, I.device);
+    return out;
+}
+
+// chunked label set of N elements as a projection / derive input
+static gg::In labels_in(const std::vector<DevBlock>& L, const std::vector<int>& mods, int64_t N) {
+    gg::In in{};
+    for (size_t j = 0; j < L.size(); ++j) {
+        in.p[j] = L[j].as<int16_t>();
+        in.n[j] = nr_comps(mods[j]);
+        in.es[j] = gg::kCh;
+        in.cs[j] = N * gg::kCh;
+    }
+    return in;
+}
+
+void GpuGarbler::sign_layer(uint64_t layer, const SignPlan& sp, CrtLabels& cur, Array& ap, Array& c1, Array& c2,
+                            Array& sg, const std::vector<int>* relu_crt, const std::vector<i64>* prefix, Array* mmg,
+                            Array* mme) {
+    Impl& I = *impl_;
+    I.enter();
+    I.check_cur(cur);
+    PhaseTrace tr_(relu_crt ? "relu" : "sign");
+    const int64_t N = I.cur_N;
+    std::vector<void*> tmp;
+    std::vector<int> omods;
+    std::vector<DevBlock> out = sign_core(I, layer, 1, 2, sp, labels_in(I.cur, I.crt, N), N, ap, c1, c2, sg,
+                                          relu_crt ? prefix : nullptr, mmg, mme, omods);
+    gg::end_layer(tmp);
+    tr_.mark("kernels");
     I.cur = std::move(out);
     I.cur_mod = omods;
     set_stale(cur, omods, N);
@@ -2681,6 +2864,538 @@ void GpuGarbler::relu_mult(uint64_t layer, CrtLabels& cur, const std::vector<i64
     I.sig_N = 0;
     I.sig_S = nullptr;
     set_stale(cur, I.crt, N);
+}
+
+// ===========================================================================
+// Remaining layer kinds on the device: dense, sum pool, residual add (device
+// copies of saved outputs), max pool / max (trees of ReLU gadgets), ReDash
+// rescale (trans projections + base extension) and the base-extension layer.
+// Each is byte-identical to the host garbler (garbler.cpp; tests compare the
+// serialized models), so a GC of any zoo model is garbled without host round
+// trips of its labels.
+namespace {
+
+size_t label_bytes(int p, int64_t N) {
+    return static_cast<size_t>(N) * gg::chunks_of(nr_comps(p)) * gg::kCh * sizeof(int16_t);
+}
+
+gg::LinJob lin_job(int16_t* dst, int p) {
+    gg::LinJob j{};
+    j.dst = dst;
+    j.p = p;
+    j.nc = static_cast<int>(gg::chunks_of(nr_comps(p)));
+    return j;
+}
+// operands: a / b label sets of N elements (element stride 8, chunk stride 8 N), r a uniform row
+void lin_a(gg::LinJob& j, const int16_t* a, int64_t N, int64_t coef) {
+    j.a = a;
+    j.aes = gg::kCh;
+    j.acs = N * gg::kCh;
+    j.ca = static_cast<int>(pmod(coef, j.p));
+}
+void lin_b(gg::LinJob& j, const int16_t* b, int64_t N, int64_t coef) {
+    j.b = b;
+    j.bes = gg::kCh;
+    j.bcs = N * gg::kCh;
+    j.cb = static_cast<int>(pmod(coef, j.p));
+}
+void lin_r(gg::LinJob& j, const int16_t* r, int64_t coef) {
+    j.r = r;
+    j.cr = static_cast<int>(pmod(coef, j.p));
+}
+
+void launch_lin(const gg::Ctx& c, const std::vector<gg::LinJob>& jobs, int64_t N) {
+    for (size_t s0 = 0; s0 < jobs.size(); s0 += gg::kMaxLin) {
+        gg::LinArgs a{};
+        a.n = static_cast<int>(std::min<size_t>(gg::kMaxLin, jobs.size() - s0));
+        a.N = N;
+        int ncmax = 1;
+        for (int i = 0; i < a.n; ++i) {
+            a.j[i] = jobs[s0 + i];
+            ncmax = std::max(ncmax, a.j[i].nc);
+        }
+        hipLaunchKernelGGL(gg::k_lin, dim3(blocks_for(N * ncmax, 256, 8192), a.n), dim3(256), 0, gg::tl_st, c, a);
+    }
+}
+
+// dst[e] (+)= sum_t cf_j[t] src[map[e K + t]] for every residue j (cf of residue j: coef(p_j, t))
+template <class Coef>
+void launch_gsum(const gg::Ctx& c, const std::vector<DevBlock>& dst, const std::vector<DevBlock>& src,
+                 const std::vector<int>& mods, int64_t N, int64_t Nsrc, const int32_t* map, int K, bool acc,
+                 Coef coef) {
+    DASH_CHECK(K >= 1 && K <= gg::kMaxTerms && mods.size() <= static_cast<size_t>(kMaxRes),
+               "gpu garbler: gathered sum shape");
+    gg::GsArgs a{};
+    a.n = static_cast<int>(mods.size());
+    a.K = K;
+    a.acc = acc ? 1 : 0;
+    a.N = N;
+    a.Nsrc = Nsrc;
+    a.map = map;
+    int ncmax = 1;
+    for (int j = 0; j < a.n; ++j) {
+        a.j[j].dst = dst[j].as<int16_t>();
+        a.j[j].src = src[j].as<int16_t>();
+        a.j[j].p = mods[j];
+        a.j[j].nc = static_cast<int>(gg::chunks_of(nr_comps(mods[j])));
+        for (int t = 0; t < K; ++t) a.j[j].cf[t] = static_cast<int>(pmod(coef(mods[j], t), mods[j]));
+        ncmax = std::max(ncmax, a.j[j].nc);
+    }
+    hipLaunchKernelGGL(gg::k_gsum, dim3(blocks_for(N * ncmax, 256, 8192), a.n), dim3(256), 0, gg::tl_st, c, a);
+}
+
+struct DensePlanKey {
+    int dev;
+    uint64_t wh;
+    std::vector<i64> geom;
+    std::vector<int> mods;
+    bool operator<(const DensePlanKey& o) const {
+        return std::tie(dev, wh, geom, mods) < std::tie(o.dev, o.wh, o.geom, o.mods);
+    }
+};
+struct DensePlan {
+    const int16_t* wt[kMaxRes];
+    const int32_t* zc[kMaxRes];
+};
+std::map<DensePlanKey, DensePlan>& dense_plans() {
+    static auto* m = new std::map<DensePlanKey, DensePlan>();  // leaked: device buffers live as long as the process
+    return *m;
+}
+std::mutex& dense_plans_mutex() {
+    static std::mutex m;
+    return m;
+}
+
+// residue labels (chunked) and a working-copy area for the base-extension stages of one gadget
+struct BeStage {
+    std::vector<std::vector<int>> slot;  // [i][j]: drawn output label of stage i's projection to target i+j+1
+};
+
+// BEPlan draws in be_garble_elem's PRG order, appended to dr (slots from `slot`, counters from `ctr`)
+BeStage be_draws(const BEPlan& P, std::vector<gg::Draw>& dr, int& slot, int& ctr) {
+    BeStage st;
+    const int E = static_cast<int>(P.moduli.size());
+    st.slot.resize(P.nonext);
+    for (int i = 0; i < P.nonext; ++i)
+        for (int j = 0; j < E - i - 1; ++j) {
+            const int q = P.swapped[i + j + 1];
+            st.slot[i].push_back(slot);
+            dr.push_back({slot++, q, ctr});
+            ctr += prg_blocks(q);
+        }
+    return st;
+}
+
+// be_garble_elem on the device: working copies lw (slots lw0 + position in the swapped order) of the labels
+// Lp (residue i of P.moduli); per non-extended stage i the identity projections of lw[i] into every later
+// modulus (table `table`, entries in be_garble_elem's order), then lw[t] = (lw[t] - out) inv; the extended
+// residues come back scaled by -invv. Draws (st) must be done.
+void be_run(GpuGarbler::Impl& I, gg::Gadget& g, const BEPlan& P, const std::vector<int16_t*>& Lp, const BeStage& st,
+            int lw0, gg::Tables& tb, int table) {
+    const int E = static_cast<int>(P.moduli.size());
+    const int64_t N = g.N;
+    std::vector<gg::LinJob> jobs;
+    for (int i = 0; i < E; ++i) {
+        gg::LinJob j = lin_job(gg::slot_base(g, lw0 + P.pos_of[i]), P.moduli[i]);
+        lin_a(j, Lp[i], N, 1);
+        jobs.push_back(j);
+    }
+    launch_lin(I.c, jobs, N);
+    int64_t off = 0;
+    gg::In none{};
+    for (int i = 0; i < P.nonext; ++i) {
+        std::vector<gg::Proj> pr;
+        int64_t first = 0;
+        for (int j = 0; j < E - i - 1; ++j) {
+            const int tg = i + j + 1;
+            gg::Proj p{gg::S_SLOT, lw0 + i, P.swapped[i], st.slot[i][j], P.swapped[tg], gg::F_IDENT, 0, 0, 0,
+                       gg::R_BANK, 0, table, 1, off, first};
+            off += P.swapped[i];
+            first += P.swapped[i];
+            pr.push_back(p);
+        }
+        g.entries = first;
+        project(I.c, g, none, tb, pr);
+        jobs.clear();
+        for (int j = 0; j < E - i - 1; ++j) {
+            const int tg = i + j + 1, q = P.swapped[tg];
+            const i64 inv = P.inv_partial[i][j];
+            gg::LinJob J = lin_job(gg::slot_base(g, lw0 + tg), q);
+            lin_a(J, gg::slot_base(g, lw0 + tg), N, inv);
+            lin_b(J, gg::slot_base(g, st.slot[i][j]), N, -inv);
+            jobs.push_back(J);
+        }
+        launch_lin(I.c, jobs, N);
+    }
+    jobs.clear();
+    for (size_t x = 0; x < P.extra.size(); ++x) {
+        const int bi = P.extra_idx[x];
+        gg::LinJob J = lin_job(Lp[bi], P.moduli[bi]);
+        lin_a(J, gg::slot_base(g, lw0 + P.pos_of[bi]), N, -P.invv[x]);
+        jobs.push_back(J);
+    }
+    launch_lin(I.c, jobs, N);
+}
+
+}  // namespace
+
+void GpuGarbler::save(size_t idx) {
+    Impl& I = *impl_;
+    I.enter();
+    Impl::Saved sv;
+    sv.mods = I.cur_mod;
+    sv.N = I.cur_N;
+    sv.L = I.alloc_labels(sv.mods, sv.N);
+    for (size_t j = 0; j < sv.mods.size(); ++j)
+        HIPCHECK(hipMemcpyAsync(sv.L[j].p, I.cur[j].p, label_bytes(sv.mods[j], sv.N), hipMemcpyDeviceToDevice, gg::tl_st));
+    I.saved[idx] = std::move(sv);
+}
+
+bool GpuGarbler::has_saved(size_t idx) const { return impl_->saved.count(idx) != 0; }
+
+void GpuGarbler::restore(size_t idx, CrtLabels& cur) {
+    Impl& I = *impl_;
+    I.enter();
+    auto it = I.saved.find(idx);
+    DASH_CHECK(it != I.saved.end(), "gpu garbler: no device copy of that layer output");
+    const Impl::Saved& sv = it->second;
+    I.cur = I.alloc_labels(sv.mods, sv.N);
+    for (size_t j = 0; j < sv.mods.size(); ++j)
+        HIPCHECK(hipMemcpyAsync(I.cur[j].p, sv.L[j].p, label_bytes(sv.mods[j], sv.N), hipMemcpyDeviceToDevice, gg::tl_st));
+    I.cur_mod = sv.mods;
+    I.cur_N = sv.N;
+    set_stale(cur, I.cur_mod, I.cur_N);
+}
+
+// residual add: cur += saved output (free addition of base labels, garbler.cpp K_ADD)
+void GpuGarbler::add_saved(size_t idx, CrtLabels& cur) {
+    Impl& I = *impl_;
+    I.enter();
+    I.check_cur(cur);
+    auto it = I.saved.find(idx);
+    DASH_CHECK(it != I.saved.end() && it->second.N == I.cur_N && it->second.mods == I.cur_mod,
+               "gpu garbler: add operand missing or of another shape");
+    std::vector<gg::LinJob> jobs;
+    for (size_t j = 0; j < I.cur_mod.size(); ++j) {
+        gg::LinJob J = lin_job(I.cur[j].as<int16_t>(), I.cur_mod[j]);
+        lin_a(J, I.cur[j].as<int16_t>(), I.cur_N, 1);
+        lin_b(J, it->second.L[j].as<int16_t>(), I.cur_N, 1);
+        jobs.push_back(J);
+    }
+    launch_lin(I.c, jobs, I.cur_N);
+    HIPCHECK(hipGetLastError());
+}
+
+// dense base labels (garbler.cpp K_DENSE): y_o = sum_{w != 0 mod p} w x_src(i) + (1 + #zero weights) Z_p
+void GpuGarbler::dense(i64 in, i64 out, i64 ch, const std::vector<i64>& w, CrtLabels& cur) {
+    Impl& I = *impl_;
+    I.enter();
+    I.check_cur(cur);
+    PhaseTrace tr_("dense");
+    DASH_CHECK(I.cur_N == in && static_cast<i64>(w.size()) == in * out, "gpu garbler: dense shape");
+    const int k = static_cast<int>(I.cur_mod.size());
+    DensePlan plan{};
+    {
+        DensePlanKey key{I.device, weights_hash(w), {in, out, ch}, I.cur_mod};
+        std::lock_guard<std::mutex> lk(dense_plans_mutex());
+        auto it = dense_plans().find(key);
+        if (it != dense_plans().end()) {
+            plan = it->second;
+        } else {
+            for (int j = 0; j < k; ++j) {
+                const int p = I.cur_mod[j];
+                DASH_CHECK(p <= 2048, "gpu garbler: dense residue modulus above 2048");
+                std::vector<int16_t> wt(static_cast<size_t>(in) * out);
+                std::vector<int32_t> zc(out, 1);
+                for (i64 o = 0; o < out; ++o)
+                    for (i64 i = 0; i < in; ++i) {
+                        const int v = static_cast<int>(w[static_cast<size_t>(o * in + i)] % p);
+                        if (v == 0) ++zc[o];
+                        wt[static_cast<size_t>(dense_src(i, in, ch)) * out + o] = static_cast<int16_t>(v);
+                    }
+                plan.wt[j] = gg::dconst(wt.data(), wt.size());
+                plan.zc[j] = gg::dconst(zc.data(), zc.size());
+            }
+            dense_plans().emplace(std::move(key), plan);
+        }
+    }
+    std::vector<DevBlock> y = I.alloc_labels(I.cur_mod, out);
+    gg::DnArgs a{};
+    a.n = k;
+    a.in = static_cast<int>(in);
+    a.out = static_cast<int>(out);
+    a.otiles = static_cast<int>((out + 63) / 64);
+    int ncmax = 1;
+    for (int j = 0; j < k; ++j) {
+        a.j[j] = gg::DnJob{y[j].as<int16_t>(), I.cur[j].as<int16_t>(), plan.wt[j], plan.zc[j], I.cur_mod[j],
+                           static_cast<int>(gg::chunks_of(nr_comps(I.cur_mod[j])))};
+        ncmax = std::max(ncmax, a.j[j].nc);
+    }
+    hipLaunchKernelGGL(gg::k_gdense, dim3(a.otiles * ncmax, k), dim3(256), 0, gg::tl_st, I.c, a);
+    HIPCHECK(hipGetLastError());
+    tr_.mark("kernels");
+    I.cur = std::move(y);
+    I.cur_N = out;
+    set_stale(cur, I.cur_mod, out);
+}
+
+// sum pool (garbler.cpp K_SUMPOOL): window sums of base labels
+void GpuGarbler::sumpool(const PoolGeom& G, CrtLabels& cur) {
+    Impl& I = *impl_;
+    I.enter();
+    I.check_cur(cur);
+    DASH_CHECK(G.C * G.H * G.W == I.cur_N, "gpu garbler: sum pool input size");
+    const int64_t Nout = G.out_size();
+    const int K = static_cast<int>(G.kh * G.kw);
+    std::vector<int32_t> map(static_cast<size_t>(Nout) * K);
+    std::vector<i64> win;
+    for (int64_t o = 0; o < Nout; ++o) {
+        G.window(o, win);
+        for (int s = 0; s < K; ++s) map[static_cast<size_t>(o) * K + s] = static_cast<int32_t>(win[s]);
+    }
+    std::vector<DevBlock> y = I.alloc_labels(I.cur_mod, Nout);
+    // windows of more than kMaxTerms values: accumulate term groups (the map is re-cut per group)
+    for (int t0 = 0; t0 < K; t0 += gg::kMaxTerms) {
+        const int Kt = std::min(gg::kMaxTerms, K - t0);
+        std::vector<int32_t> mt(static_cast<size_t>(Nout) * Kt);
+        for (int64_t o = 0; o < Nout; ++o)
+            for (int t = 0; t < Kt; ++t) mt[static_cast<size_t>(o) * Kt + t] = map[static_cast<size_t>(o) * K + t0 + t];
+        launch_gsum(I.c, y, I.cur, I.cur_mod, Nout, I.cur_N, gg::dconst(mt.data(), mt.size()), Kt, t0 > 0,
+                    [](int, int) { return 1; });
+    }
+    HIPCHECK(hipGetLastError());
+    I.cur = std::move(y);
+    I.cur_N = Nout;
+    set_stale(cur, I.cur_mod, Nout);
+}
+
+// max pool / max (garbler.cpp K_MAXPOOL / K_MAX): the window values, then per tree level the pair differences,
+// a ReLU gadget (streams 20 + 2 lv / 21 + 2 lv), and max = relu(b - a) + a, the odd value carried
+void GpuGarbler::maxpool_begin(const std::vector<std::vector<i64>>& win, CrtLabels& cur) {
+    Impl& I = *impl_;
+    I.enter();
+    I.check_cur(cur);
+    const int64_t Nout = static_cast<int64_t>(win.size());
+    DASH_CHECK(Nout > 0, "gpu garbler: empty max pool");
+    const int64_t K = static_cast<int64_t>(win[0].size());
+    std::vector<int32_t> map(static_cast<size_t>(Nout * K));
+    for (int64_t o = 0; o < Nout; ++o) {
+        DASH_CHECK(static_cast<int64_t>(win[o].size()) == K, "gpu garbler: ragged max pool windows");
+        for (int64_t s = 0; s < K; ++s) map[static_cast<size_t>(o * K + s)] = static_cast<int32_t>(win[o][s]);
+    }
+    I.mp_V = I.alloc_labels(I.cur_mod, Nout * K);
+    launch_gsum(I.c, I.mp_V, I.cur, I.cur_mod, Nout * K, I.cur_N, gg::dconst(map.data(), map.size()), 1, false,
+                [](int, int) { return 1; });
+    I.mp_Nout = Nout;
+    I.mp_cnt = K;
+}
+
+void GpuGarbler::maxpool_level(uint64_t layer, int lv, i64 ops, const SignPlan& sp, const std::vector<i64>& prefix,
+                               Array& ap, Array& c1, Array& c2, Array& sg, Array& mmg, Array& mme) {
+    Impl& I = *impl_;
+    I.enter();
+    PhaseTrace tr_("maxpool_level");
+    const int64_t Nout = I.mp_Nout, cnt = I.mp_cnt, cnt1 = ops + cnt % 2, Nd = Nout * ops;
+    DASH_CHECK(ops >= 1 && 2 * ops <= cnt, "gpu garbler: max tree level shape");
+    // pair differences D[o ops + q] = V[o cnt + 2q + 1] - V[o cnt + 2q]
+    std::vector<int32_t> dm(static_cast<size_t>(Nd) * 2), am(static_cast<size_t>(Nout * cnt1)),
+        ym(static_cast<size_t>(Nout * cnt1));
+    for (int64_t o = 0; o < Nout; ++o) {
+        for (int64_t q = 0; q < ops; ++q) {
+            dm[static_cast<size_t>((o * ops + q) * 2)] = static_cast<int32_t>(o * cnt + 2 * q + 1);
+            dm[static_cast<size_t>((o * ops + q) * 2 + 1)] = static_cast<int32_t>(o * cnt + 2 * q);
+        }
+        for (int64_t q = 0; q < cnt1; ++q) {
+            am[static_cast<size_t>(o * cnt1 + q)] = static_cast<int32_t>(q < ops ? o * cnt + 2 * q : o * cnt + cnt - 1);
+            ym[static_cast<size_t>(o * cnt1 + q)] = q < ops ? static_cast<int32_t>(o * ops + q) : -1;
+        }
+    }
+    std::vector<DevBlock> D = I.alloc_labels(I.crt, Nd);
+    launch_gsum(I.c, D, I.mp_V, I.crt, Nd, Nout * cnt, gg::dconst(dm.data(), dm.size()), 2, false,
+                [](int p, int t) { return t == 0 ? 1 : p - 1; });
+    std::vector<int> omods;
+    std::vector<DevBlock> Y = sign_core(I, layer, 20 + 2 * lv, 21 + 2 * lv, sp, labels_in(D, I.crt, Nd), Nd, ap, c1, c2,
+                                        sg, &prefix, &mmg, &mme, omods);
+    std::vector<DevBlock> nv = I.alloc_labels(I.crt, Nout * cnt1);
+    launch_gsum(I.c, nv, I.mp_V, I.crt, Nout * cnt1, Nout * cnt, gg::dconst(am.data(), am.size()), 1, false,
+                [](int, int) { return 1; });
+    launch_gsum(I.c, nv, Y, I.crt, Nout * cnt1, Nd, gg::dconst(ym.data(), ym.size()), 1, true,
+                [](int, int) { return 1; });
+    HIPCHECK(hipGetLastError());
+    tr_.mark("kernels");
+    I.mp_V = std::move(nv);
+    I.mp_cnt = cnt1;
+}
+
+void GpuGarbler::maxpool_end(CrtLabels& cur) {
+    Impl& I = *impl_;
+    I.enter();
+    DASH_CHECK(I.mp_cnt == 1, "gpu garbler: max tree not reduced to one value");
+    I.cur = std::move(I.mp_V);
+    I.cur_N = I.mp_Nout;
+    I.cur_mod = I.crt;
+    I.mp_Nout = I.mp_cnt = 0;
+    set_stale(cur, I.cur_mod, I.cur_N);
+}
+
+// ReDash rescale iteration (rescale_garble_elem with a base-extension plan): L += up; per factor the identity
+// projections of L[fi] into every active residue (trans table), L_j = (L_j - out) s^-1; L[fi] = Z; base
+// extension of the factors' residues (be table); L -= down. One PRG stream (layer, 10 + it), counters in
+// rescale_garble_elem's order.
+void GpuGarbler::rescale_redash(uint64_t layer, int it, const RescalePlan& P, CrtLabels& cur,
+                                const std::vector<std::vector<comp_t>>& up,
+                                const std::vector<std::vector<comp_t>>& down, Array& tr, Array& be) {
+    Impl& I = *impl_;
+    I.enter();
+    I.check_cur(cur);
+    PhaseTrace tr_("rescale_redash");
+    DASH_CHECK(!P.sign_be && I.cur_mod == I.crt, "gpu garbler: ReDash rescale plan mismatch");
+    const int64_t N = I.cur_N;
+    const int k = I.k;
+    std::vector<int16_t> hup(k * gg::kW, 0), hdn(k * gg::kW, 0);
+    for (int j = 0; j < k; ++j) {
+        std::copy(up[j].begin(), up[j].end(), hup.begin() + j * gg::kW);
+        std::copy(down[j].begin(), down[j].end(), hdn.begin() + j * gg::kW);
+    }
+    const int16_t* dup = I.stage(hup.data(), hup.size());
+    const int16_t* ddn = I.stage(hdn.data(), hdn.size());
+    // draws: trans outputs (factor, active residue), then the base extension's
+    std::vector<gg::Draw> dr;
+    int slot = 0, ctr = 0;
+    std::vector<std::vector<int>> ts(P.factors.size());
+    for (size_t f = 0; f < P.factors.size(); ++f)
+        for (int j : P.active[f]) {
+            ts[f].push_back(slot);
+            dr.push_back({slot++, P.crt[j], ctr});
+            ctr += prg_blocks(P.crt[j]);
+        }
+    BeStage st = be_draws(P.be, dr, slot, ctr);
+    const int lw0 = slot;
+    slot += k;
+    const int nslots = slot;
+    DevTable tT, tB;
+    tT.alloc(I.device, N, tr.shape[1], tr);
+    tB.alloc(I.device, N, be.shape[1], be);
+    gg::Tables tb{};
+    tb.t[6] = tT.p(); tb.row[6] = tT.row;
+    tb.t[7] = tB.p(); tb.row[7] = tB.row;
+    gg::Gadget g{};
+    g.layer = layer;
+    g.sslot = 10 + it;
+    g.mask = 0;
+    g.S = I.scratch(static_cast<size_t>(N) * nslots * gg::kW * sizeof(int16_t));
+    g.N = N;
+    g.nslots = nslots;
+    g.draws = gg::dconst(dr.data(), dr.size());
+    g.ndraws = static_cast<int>(dr.size());
+    g.nblk = draw_blocks(dr);
+    check_desc(g);
+    hipLaunchKernelGGL(gg::draw_kernel(), dim3(draw_grid(g)), dim3(gg::kGB), 0, gg::tl_st, I.c, g);
+    std::vector<int16_t*> L(k);
+    for (int j = 0; j < k; ++j) L[j] = I.cur[j].as<int16_t>();
+    std::vector<gg::LinJob> jobs;
+    for (int j = 0; j < k; ++j) {
+        gg::LinJob J = lin_job(L[j], I.crt[j]);
+        lin_a(J, L[j], N, 1);
+        lin_r(J, dup + j * gg::kW, 1);
+        jobs.push_back(J);
+    }
+    launch_lin(I.c, jobs, N);
+    const gg::In in = labels_in(I.cur, I.crt, N);
+    int64_t off = 0;
+    for (size_t f = 0; f < P.factors.size(); ++f) {
+        const int s = P.factors[f], fi = P.factor_idx[f];
+        std::vector<gg::Proj> pr;
+        int64_t first = 0;
+        for (size_t a = 0; a < P.active[f].size(); ++a) {
+            const int j = P.active[f][a];
+            pr.push_back(gg::Proj{gg::S_INPUT, fi, s, ts[f][a], P.crt[j], gg::F_IDENT, 0, 0, 0, gg::R_BANK, 0, 6, 1,
+                                  off, first});
+            off += s;
+            first += s;
+        }
+        g.entries = first;
+        project(I.c, g, in, tb, pr);
+        jobs.clear();
+        for (size_t a = 0; a < P.active[f].size(); ++a) {
+            const int j = P.active[f][a];
+            gg::LinJob J = lin_job(L[j], P.crt[j]);
+            lin_a(J, L[j], N, P.inv[f][a]);
+            lin_b(J, gg::slot_base(g, ts[f][a]), N, -P.inv[f][a]);
+            jobs.push_back(J);
+        }
+        launch_lin(I.c, jobs, N);
+    }
+    jobs.clear();
+    for (int fi : P.factor_idx) {
+        gg::LinJob J = lin_job(L[fi], P.crt[fi]);
+        lin_r(J, I.c.Z + static_cast<int64_t>(P.crt[fi]) * gg::kW, 1);
+        jobs.push_back(J);
+    }
+    launch_lin(I.c, jobs, N);
+    be_run(I, g, P.be, L, st, lw0, tb, 7);
+    jobs.clear();
+    for (int j = 0; j < k; ++j) {
+        gg::LinJob J = lin_job(L[j], I.crt[j]);
+        lin_a(J, L[j], N, 1);
+        lin_r(J, ddn + j * gg::kW, -1);
+        jobs.push_back(J);
+    }
+    launch_lin(I.c, jobs, N);
+    HIPCHECK(hipGetLastError());
+    std::vector<void*> tmp;
+    gg::end_layer(tmp);
+    tr_.mark("kernels");
+    tT.to_array(tr, I.device);
+    tB.to_array(be, I.device);
+    set_stale(cur, I.cur_mod, N);
+}
+
+// base-extension layer (garbler.cpp K_BASEEXT): the extra residues start from Z, then be_garble_elem on
+// stream (layer, 1), counters from 0
+void GpuGarbler::base_ext(uint64_t layer, const BEPlan& P, CrtLabels& cur, Array& be) {
+    Impl& I = *impl_;
+    I.enter();
+    I.check_cur(cur);
+    DASH_CHECK(P.moduli == I.cur_mod, "gpu garbler: base extension plan mismatch");
+    const int64_t N = I.cur_N;
+    const int E = static_cast<int>(P.moduli.size());
+    std::vector<gg::Draw> dr;
+    int slot = 0, ctr = 0;
+    BeStage st = be_draws(P, dr, slot, ctr);
+    const int lw0 = slot;
+    slot += E;
+    DevTable tB;
+    tB.alloc(I.device, N, be.shape[1], be);
+    gg::Tables tb{};
+    tb.t[7] = tB.p(); tb.row[7] = tB.row;
+    gg::Gadget g{};
+    g.layer = layer;
+    g.sslot = 1;
+    g.mask = 0;
+    g.S = I.scratch(static_cast<size_t>(N) * slot * gg::kW * sizeof(int16_t));
+    g.N = N;
+    g.nslots = slot;
+    g.draws = gg::dconst(dr.data(), dr.size());
+    g.ndraws = static_cast<int>(dr.size());
+    g.nblk = draw_blocks(dr);
+    check_desc(g);
+    if (!dr.empty()) hipLaunchKernelGGL(gg::draw_kernel(), dim3(draw_grid(g)), dim3(gg::kGB), 0, gg::tl_st, I.c, g);
+    std::vector<int16_t*> L(E);
+    for (int j = 0; j < E; ++j) L[j] = I.cur[j].as<int16_t>();
+    std::vector<gg::LinJob> jobs;
+    for (int xi : P.extra_idx) {
+        gg::LinJob J = lin_job(L[xi], P.moduli[xi]);
+        lin_r(J, I.c.Z + static_cast<int64_t>(P.moduli[xi]) * gg::kW, 1);
+        jobs.push_back(J);
+    }
+    launch_lin(I.c, jobs, N);
+    be_run(I, g, P, L, st, lw0, tb, 7);
+    HIPCHECK(hipGetLastError());
+    std::vector<void*> tmp;
+    gg::end_layer(tmp);
+    tB.to_array(be, I.device);
+    set_stale(cur, I.cur_mod, N);
 }
 
 }  // namespace dash

@@ -47,6 +47,29 @@ class GpuGarbler {
     // gates only; device cur -> next
     void relu_mult(uint64_t layer, CrtLabels& cur, const std::vector<i64>* prefix, Array& mmg, Array& mme);
 
+    // dense base labels y_o = sum_{w != 0 mod p} w x_src(i) + (1 + #zero weights) Z_p (w reduced mod M, [out][in],
+    // src = dense_src(i, in, channel_tf))
+    void dense(i64 in, i64 out, i64 channel_tf, const std::vector<i64>& w, CrtLabels& cur);
+    // window sums of the device cur
+    void sumpool(const PoolGeom& G, CrtLabels& cur);
+    // device copies of layer outputs a later residual add / in_src layer reads (idx = layer index + 1)
+    void save(size_t idx);
+    bool has_saved(size_t idx) const;
+    void restore(size_t idx, CrtLabels& cur);
+    void add_saved(size_t idx, CrtLabels& cur);
+    // max pool / max: window values, one ReLU-gadget tree level per call (relu_garble_elem on streams
+    // 20 + 2 lv / 21 + 2 lv), then the reduced values become cur
+    void maxpool_begin(const std::vector<std::vector<i64>>& win, CrtLabels& cur);
+    void maxpool_level(uint64_t layer, int lv, i64 ops, const SignPlan& sp, const std::vector<i64>& prefix, Array& ap,
+                       Array& c1, Array& c2, Array& sg, Array& mmg, Array& mme);
+    void maxpool_end(CrtLabels& cur);
+    // ReDash rescale iteration (base-extension plan) on the device cur, in place
+    void rescale_redash(uint64_t layer, int it, const RescalePlan& P, CrtLabels& cur,
+                        const std::vector<std::vector<comp_t>>& up, const std::vector<std::vector<comp_t>>& down,
+                        Array& tr, Array& be);
+    // base-extension layer on the device cur, in place
+    void base_ext(uint64_t layer, const BEPlan& P, CrtLabels& cur, Array& be);
+
     struct Impl;
 
    private:

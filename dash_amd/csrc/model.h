@@ -77,7 +77,11 @@ struct GarbledModel {
     std::vector<GLayer> layers;
 
     std::string serialize() const;
+    // the offline message written straight into a caller buffer (device tables fetched into place)
+    size_t serialized_size() const;
+    size_t serialize_to(uint8_t* out, size_t cap) const;
     static GarbledModel deserialize(const std::string& blob);
+    static GarbledModel deserialize(const uint8_t* blob, size_t nbytes);
     size_t table_bytes() const;  // bytes of garbled tables (u128 arrays)
     size_t total_bytes() const;
     LabelBank zero_bank() const;

@@ -8,9 +8,20 @@ namespace {
 constexpr char kModelMagic[8] = {'D', 'A', 'M', 'D', 'G', 'C', '0', '1'};
 constexpr char kDecMagic[8] = {'D', 'A', 'M', 'D', 'D', 'E', 'C', '1'};
 
+// Writer over an output byte range (or a size count when out == nullptr): the offline message is written
+// once, straight into the caller's buffer (a send buffer), and a device-resident array (GPU garbler tables)
+// is fetched from HBM directly into its place, with no intermediate host copy.
 struct W {
-    std::string s;
-    void raw(const void* p, size_t n) { s.append(static_cast<const char*>(p), n); }
+    uint8_t* out = nullptr;
+    size_t cap = 0;
+    size_t off = 0;
+    void raw(const void* p, size_t n) {
+        if (out) {
+            DASH_CHECK(off + n <= cap, "serialize: output buffer too small");
+            std::memcpy(out + off, p, n);
+        }
+        off += n;
+    }
     void u32(uint32_t v) { raw(&v, 4); }
     void i64v(i64 v) { raw(&v, 8); }
     void str(const std::string& x) {
@@ -30,18 +41,28 @@ struct W {
         raw(&dt, 1);
         ivec(a.shape);
         i64v(static_cast<i64>(a.nbytes));
-        raw(a.ptr<uint8_t>(), a.nbytes);
+        if (out && a.device_resident() && !a.dev->host) {
+            DASH_CHECK(off + a.nbytes <= cap, "serialize: output buffer too small");
+            a.dev->fetch(out + off, a.device_ptr(), a.nbytes);
+            off += a.nbytes;
+        } else if (out) {
+            raw(a.ptr<uint8_t>(), a.nbytes);
+        } else {
+            off += a.nbytes;
+        }
     }
 };
 
 struct Rd {
-    const std::string& s;
+    const uint8_t* s;
+    size_t n;
     size_t off = 0;
-    explicit Rd(const std::string& x) : s(x) {}
-    void raw(void* p, size_t n) {
-        DASH_CHECK(off + n <= s.size(), "truncated blob");
-        std::memcpy(p, s.data() + off, n);
-        off += n;
+    Rd(const uint8_t* p, size_t len) : s(p), n(len) {}
+    explicit Rd(const std::string& x) : s(reinterpret_cast<const uint8_t*>(x.data())), n(x.size()) {}
+    void raw(void* p, size_t k) {
+        DASH_CHECK(off + k <= n, "truncated blob");
+        std::memcpy(p, s + off, k);
+        off += k;
     }
     uint32_t u32() {
         uint32_t v;
@@ -54,15 +75,16 @@ struct Rd {
         return v;
     }
     std::string str() {
-        uint32_t n = u32();
-        DASH_CHECK(off + n <= s.size(), "truncated blob");
-        std::string r = s.substr(off, n);
-        off += n;
+        uint32_t k = u32();
+        DASH_CHECK(off + k <= n, "truncated blob");
+        std::string r(reinterpret_cast<const char*>(s + off), k);
+        off += k;
         return r;
     }
     std::vector<i64> ivec() {
-        uint32_t n = u32();
-        std::vector<i64> v(n);
+        uint32_t k = u32();
+        DASH_CHECK(static_cast<size_t>(k) * 8 <= n - off, "truncated blob");
+        std::vector<i64> v(k);
         for (auto& x : v) x = i64v();
         return v;
     }
@@ -75,6 +97,12 @@ struct Rd {
         raw(&dt, 1);
         DASH_CHECK(dt <= 4, "bad dtype");
         auto shape = ivec();
+        size_t cnt = 1;
+        for (auto d : shape) {
+            DASH_CHECK(d >= 0 && (d == 0 || cnt <= n / static_cast<size_t>(d)), "bad array shape");
+            cnt *= static_cast<size_t>(d);
+        }
+        DASH_CHECK(n - off >= 8 && cnt * dtype_size(static_cast<DType>(dt)) <= n - off - 8, "array larger than the blob");
         Array a(static_cast<DType>(dt), shape);
         i64 nb = i64v();
         DASH_CHECK(static_cast<size_t>(nb) == a.nbytes, "array size mismatch");
@@ -84,8 +112,11 @@ struct Rd {
 };
 }  // namespace
 
-std::string GarbledModel::serialize() const {
-    W w;
+namespace {
+void write_model(const GarbledModel& m, W& w) {
+    const auto& h = m.h;
+    const auto& consts = m.consts;
+    const auto& layers = m.layers;
     w.raw(kModelMagic, 8);
     w.u32(3u);
     w.u32(static_cast<uint32_t>(h.sign_fused));
@@ -114,11 +145,35 @@ std::string GarbledModel::serialize() const {
             w.arr(kv.second);
         }
     }
-    return std::move(w.s);
+}
+}  // namespace
+
+size_t GarbledModel::serialized_size() const {
+    W w;
+    write_model(*this, w);
+    return w.off;
+}
+
+size_t GarbledModel::serialize_to(uint8_t* out, size_t cap) const {
+    W w;
+    w.out = out;
+    w.cap = cap;
+    write_model(*this, w);
+    return w.off;
+}
+
+std::string GarbledModel::serialize() const {
+    std::string s(serialized_size(), '\0');
+    serialize_to(reinterpret_cast<uint8_t*>(&s[0]), s.size());
+    return s;
 }
 
 GarbledModel GarbledModel::deserialize(const std::string& blob) {
-    Rd r(blob);
+    return deserialize(reinterpret_cast<const uint8_t*>(blob.data()), blob.size());
+}
+
+GarbledModel GarbledModel::deserialize(const uint8_t* blob, size_t nbytes) {
+    Rd r(blob, nbytes);
     char mg[8];
     r.raw(mg, 8);
     DASH_CHECK(std::memcmp(mg, kModelMagic, 8) == 0, "not a garbled model blob");
@@ -155,18 +210,26 @@ GarbledModel GarbledModel::deserialize(const std::string& blob) {
         }
         m.layers.push_back(std::move(g));
     }
-    DASH_CHECK(r.off == blob.size(), "trailing bytes after garbled model");
+    DASH_CHECK(r.off == nbytes, "trailing bytes after garbled model");
     return m;
 }
 
 std::string Decoder::serialize() const {
+    auto put = [this](W& w) {
+        w.raw(kDecMagic, 8);
+        w.ivec32(moduli);
+        w.i64v(n_out);
+        w.u32(static_cast<uint32_t>(dec.size()));
+        for (const auto& a : dec) w.arr(a);
+    };
+    W sz;
+    put(sz);
+    std::string s(sz.off, '\0');
     W w;
-    w.raw(kDecMagic, 8);
-    w.ivec32(moduli);
-    w.i64v(n_out);
-    w.u32(static_cast<uint32_t>(dec.size()));
-    for (const auto& a : dec) w.arr(a);
-    return std::move(w.s);
+    w.out = reinterpret_cast<uint8_t*>(&s[0]);
+    w.cap = s.size();
+    put(w);
+    return s;
 }
 
 Decoder Decoder::deserialize(const std::string& blob) {

@@ -66,7 +66,7 @@ class EvaluatorServer:
                         slot = flags
                         if not 0 <= slot < self.batch:
                             raise ValueError(f"slot {slot} out of range")
-                        m = n.GarbledModel.deserialize(bytes(buf))
+                        m = n.GarbledModel.deserialize_buffer(buf)  # parsed in place, no bytes() copy
                         del buf
                         if self.backend == "hip":
                             from ..runtime import HipEvaluator
@@ -136,12 +136,19 @@ def serve_once(sock, backend: str = "cpu", device: int = 0, tamper: bool = False
 
 class GarblerClient:
     """Garbler party: owns the circuit, garbles fresh GCs (offline), encodes
-    inputs and decodes outputs (online)."""
+    inputs and decodes outputs (online).
+
+    device: garble on this GPU (the garbler's own device; byte-identical to the host garbler), else on the
+    host CPU. pipeline: garble GC b + 1 while GC b is serialized onto the wire and loaded by the evaluator
+    (a bounded producer thread; the evaluator's ACKs are collected after the last model instead of after each
+    one). gc_kw: GarbledCircuit construction options (rescale / relu / fused_sign)."""
 
     def __init__(self, host: str, port: int, circuit, crt, mrs=None, batch: int = 1, max_modulus: int = 0,
-                 seed: Optional[bytes] = None, timeout: float = 600.0):
+                 seed: Optional[bytes] = None, timeout: float = 600.0, device: Optional[int] = None,
+                 pipeline: bool = True, **gc_kw):
         self.circuit, self.crt, self.mrs = circuit, crt, mrs
         self.batch, self.max_modulus = batch, max_modulus
+        self.device, self.pipeline, self.gc_kw = device, pipeline, gc_kw
         self._seed = seed
         self._ctr = 0
         self.ch = connect(host, port, timeout=timeout)
@@ -149,7 +156,9 @@ class GarblerClient:
         _, _, buf = self.ch.recv(b"HELO")
         self.server_info = json.loads(buf.decode())
         self.gcs: list = []
-        self.stats = {"offline_bytes": 0, "online_bytes": 0, "garble_s": 0.0, "offline_s": 0.0, "online_s": []}
+        self._bufs: list = []
+        self.stats = {"offline_bytes": 0, "online_bytes": 0, "garble_s": 0.0, "serialize_s": 0.0, "offline_s": 0.0,
+                      "online_s": [], "gcs": 0}
 
     def _next_seed(self) -> Optional[bytes]:
         if self._seed is None:
@@ -159,21 +168,75 @@ class GarblerClient:
         self._ctr += 1
         return hashlib.sha256(self._seed + self._ctr.to_bytes(8, "little")).digest()[:16]
 
+    def _garble_one(self, seed):
+        """One fresh GC and its offline message (a reused send buffer); the garbler keeps only the encoder and
+        decoder secrets."""
+        from ..garbling import GarbledCircuit
+
+        t = time.perf_counter()
+        gc = GarbledCircuit(self.circuit, self.crt, self.mrs, max_modulus=self.max_modulus, seed=seed,
+                            device=self.device, **self.gc_kw)
+        t1 = time.perf_counter()
+        n = gc.model.serialized_size()
+        try:
+            buf = self._bufs.pop()  # a buffer whose send has completed (appended by the sending thread)
+        except IndexError:
+            buf = None
+        if buf is None or buf.size < n:
+            buf = np.empty(n, dtype=np.uint8)
+        gc.model.serialize_into(buf)
+        gc.model = None
+        t2 = time.perf_counter()
+        return gc, buf, n, t1 - t, t2 - t1
+
     def offline(self) -> None:
         """Garble `batch` fresh circuits and ship them (offline phase)."""
-        from ..garbling import GarbledCircuit
+        import queue
+        import threading
 
         t0 = time.perf_counter()
         sent0 = self.ch.bytes_sent
+        seeds = [self._next_seed() for _ in range(self.batch)]
         self.gcs = []
-        for b in range(self.batch):
-            t = time.perf_counter()
-            gc = GarbledCircuit(self.circuit, self.crt, self.mrs, max_modulus=self.max_modulus, seed=self._next_seed())
-            self.stats["garble_s"] += time.perf_counter() - t
-            self.ch.send(b"MODL", gc.model.serialize(), flags=b)
-            self.ch.recv(b"ACK_")
-            gc.model = None  # the garbler keeps only encoder + decoder secrets
-            self.gcs.append(gc)
+        if not self.pipeline or self.batch == 1:
+            for b in range(self.batch):
+                gc, buf, n, tg, ts = self._garble_one(seeds[b])
+                self.stats["garble_s"] += tg
+                self.stats["serialize_s"] += ts
+                self.ch.send(b"MODL", memoryview(buf)[:n], flags=b)
+                self.ch.recv(b"ACK_")
+                self._bufs.append(buf)
+                self.gcs.append(gc)
+        else:
+            q: "queue.Queue" = queue.Queue(maxsize=2)  # at most two models in flight beside the one on the wire
+            err: list = []
+
+            def produce():
+                try:
+                    for b in range(self.batch):
+                        q.put(self._garble_one(seeds[b]))
+                except BaseException as e:  # surfaced on the sending thread
+                    err.append(e)
+                    q.put(None)
+
+            th = threading.Thread(target=produce, name="dash-garbler", daemon=True)
+            th.start()
+            try:
+                for b in range(self.batch):
+                    item = q.get()
+                    if item is None:
+                        raise err[0]
+                    gc, buf, n, tg, ts = item
+                    self.stats["garble_s"] += tg
+                    self.stats["serialize_s"] += ts
+                    self.ch.send(b"MODL", memoryview(buf)[:n], flags=b)
+                    self._bufs.append(buf)
+                    self.gcs.append(gc)
+                for _ in range(self.batch):  # the evaluator acknowledges every load, in order
+                    self.ch.recv(b"ACK_")
+            finally:
+                th.join()
+        self.stats["gcs"] += self.batch
         self.stats["offline_bytes"] += self.ch.bytes_sent - sent0
         self.stats["offline_s"] += time.perf_counter() - t0
 

@@ -45,7 +45,8 @@ def _config(circuit, crt, mrs, max_modulus) -> dict:
             "max_modulus": int(max_modulus), "circuit": circuit_digest(circuit)}
 
 
-def _enclave_main(conn, sock_fd_port, circuit, crt, mrs, max_modulus, batch, sealed, key_file):
+def _enclave_main(conn, sock_fd_port, circuit, crt, mrs, max_modulus, batch, sealed, key_file, garble_device=None,
+                  client_kw=None):
     import hashlib
     import json
     import secrets
@@ -79,7 +80,8 @@ def _enclave_main(conn, sock_fd_port, circuit, crt, mrs, max_modulus, batch, sea
     host, port = sock_fd_port
     client = None
     try:
-        client = GarblerClient(host, port, circuit, crt, mrs, batch=batch, max_modulus=max_modulus, seed=master)
+        client = GarblerClient(host, port, circuit, crt, mrs, batch=batch, max_modulus=max_modulus, seed=master,
+                               device=garble_device, **(client_kw or {}))
         client._ctr = ctr
         while True:
             msg = conn.recv()
@@ -117,11 +119,15 @@ class GarblerEnclave:
     garbler resumes from it with its master secret re-keyed by fresh enclave randomness, so no per-GC seed is
     reused even when the host replays one blob to several enclaves.
 
-    start_timeout_s: the enclave must report ready (and connect back) within this time, else SealError."""
+    start_timeout_s: the enclave must report ready (and connect back) within this time, else SealError.
+    garble_device: the trusted garbler garbles on this GPU (its own device in a deployment whose accelerator is
+    inside the trust boundary, e.g. a confidential-computing GPU); None garbles on the enclave's CPU, as the
+    reference's SGX enclave does. client_kw: GarblerClient options (pipeline, rescale / relu constructions)."""
 
     def __init__(self, circuit, crt, mrs=None, max_modulus: int = 0, batch: int = 1, backend: str = "hip",
                  device: int = 0, attest: bool = True, sealed_state: Optional[bytes] = None,
-                 platform_key_file: Optional[str] = None, start_timeout_s: float = 120.0):
+                 platform_key_file: Optional[str] = None, start_timeout_s: float = 120.0,
+                 garble_device: Optional[int] = None, client_kw: Optional[dict] = None):
         from ..net.channel import Channel
         from ..net.protocol import EvaluatorServer
         from . import attest as at
@@ -136,7 +142,7 @@ class GarblerEnclave:
         self._conn, child = ctx.Pipe()
         self._proc = ctx.Process(target=_enclave_main,
                                  args=(child, ("127.0.0.1", port), circuit, crt, mrs, max_modulus, batch,
-                                       sealed_state, platform_key_file),
+                                       sealed_state, platform_key_file, garble_device, client_kw),
                                  daemon=True)
         self._proc.start()
         child.close()  # the child's end lives in the child only: a dead child reads as EOF here

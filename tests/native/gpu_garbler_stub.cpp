@@ -34,6 +34,23 @@ void GpuGarbler::relu_mrs(uint64_t, const SignMrsPlan&, CrtLabels&, Array&, cons
     no_gpu();
 }
 void GpuGarbler::relu_mult(uint64_t, CrtLabels&, const std::vector<i64>*, Array&, Array&) { no_gpu(); }
+void GpuGarbler::dense(i64, i64, i64, const std::vector<i64>&, CrtLabels&) { no_gpu(); }
+void GpuGarbler::sumpool(const PoolGeom&, CrtLabels&) { no_gpu(); }
+void GpuGarbler::save(size_t) { no_gpu(); }
+bool GpuGarbler::has_saved(size_t) const { return false; }
+void GpuGarbler::restore(size_t, CrtLabels&) { no_gpu(); }
+void GpuGarbler::add_saved(size_t, CrtLabels&) { no_gpu(); }
+void GpuGarbler::maxpool_begin(const std::vector<std::vector<i64>>&, CrtLabels&) { no_gpu(); }
+void GpuGarbler::maxpool_level(uint64_t, int, i64, const SignPlan&, const std::vector<i64>&, Array&, Array&, Array&,
+                               Array&, Array&, Array&) {
+    no_gpu();
+}
+void GpuGarbler::maxpool_end(CrtLabels&) { no_gpu(); }
+void GpuGarbler::rescale_redash(uint64_t, int, const RescalePlan&, CrtLabels&, const std::vector<std::vector<comp_t>>&,
+                                const std::vector<std::vector<comp_t>>&, Array&, Array&) {
+    no_gpu();
+}
+void GpuGarbler::base_ext(uint64_t, const BEPlan&, CrtLabels&, Array&) { no_gpu(); }
 void gpu_table_cache_trim() {}
 size_t gpu_table_cache_bytes() { return 0; }
 

@@ -409,3 +409,73 @@ def test_gpu_garble_into_evaluator_slot(rescale, relu):
     ev.fetch_outputs()
     for b, gc in enumerate((first, into)):
         np.testing.assert_array_equal(ev.decode(b, gc), gc.plain_q_eval(xs[b]))
+
+
+def _dense_layer(rng, fin, fout, channel_tf=0):
+    return d.Dense(rng.integers(-4, 5, (fout, fin)), rng.integers(-6, 6, fout), q_const=1.0, channel_tf=channel_tf)
+
+
+def _gpu_vs_host(c, crt, mrs, **kw):
+    seed = bytes(range(16))
+    cpu = GarbledCircuit(c, crt, mrs, seed=seed, **kw)
+    gpu = GarbledCircuit(c, crt, mrs, seed=seed, device=0, **kw)
+    assert gpu.model.serialize() == cpu.model.serialize()
+    assert gpu.decoder.serialize() == cpu.decoder.serialize()
+    return gpu
+
+
+@pytest.mark.parametrize("name", ["dense", "dense_tf", "dense_zero_weights", "model_a", "lenet5", "sumpool",
+                                  "maxpool_odd", "max", "shortcut", "redash_head", "redash_rescale2",
+                                  "base_ext"])
+def test_gpu_garbler_bit_identical_all_kinds(name):
+    """Round 4: dense, sum / max pooling, residual add + in_src, the ReDash rescale (trans projections + base
+    extension) and the base-extension layer garble on the device, byte-identical to the host garbler."""
+    from dash_amd.ir.quant import QuantizationMethod as Q
+    from dash_amd.models import BENCH_CONFIGS, build_circuit
+
+    rng = np.random.default_rng(11)
+    crt, mrs, kw = 8, 100.0, {}
+    if name == "dense":
+        c = d.Circuit([_dense_layer(rng, 300, 70)])
+    elif name == "dense_tf":
+        c = d.Circuit([_dense_layer(rng, 96, 33, channel_tf=3)])
+    elif name == "dense_zero_weights":
+        lay = _dense_layer(rng, 64, 20)
+        lay.q_weights[:, ::3] = 0  # zero (and multiple-of-p) weights take the Z-label quirk
+        lay.q_weights[:, 1::7] = 2 * 3 * 5
+        c = d.Circuit([lay])
+    elif name == "model_a":
+        c = build_circuit("MODEL_A")
+    elif name == "lenet5":
+        c, crt = build_circuit("LENET5", Q.ScaleQuant, 3, seed=1), 8
+    elif name == "sumpool":
+        c = d.Circuit([d.SumPool2d(8, 8, 3, 4, 4), d.Relu((3, 2, 2))])
+    elif name == "maxpool_odd":
+        c = d.Circuit([d.MaxPool2d(9, 9, 2, 3, 3)])  # 9-value windows: levels with an odd carry
+    elif name == "max":
+        c = d.Circuit([d.Max((7,))])
+    elif name == "shortcut":
+        from tests.test_garbled_layers import _shortcut_block
+
+        c, xs = _shortcut_block()
+        crt = c.infer_crt_base_size(xs)
+    elif name == "redash_head":
+        cfg = BENCH_CONFIGS["MODEL_F_MINIONN_POOL_REPL/REDASH_OPT"]
+        full = build_circuit("MODEL_F_MINIONN_POOL_REPL", cfg["q_method"], cfg["q_parameter"], seed=0)
+        c, crt, mrs = d.Circuit(full.layers[:4]), cfg["crt"], cfg["mrs"]  # conv, rescale({32}), relu, conv
+    elif name == "redash_rescale2":
+        c, crt, mrs = d.Circuit([d.Rescale([32], (200,))]), [32, 3, 5, 7, 11, 13, 17], [10, 9, 9, 8, 7, 7, 6]
+    else:
+        c, crt, mrs = d.Circuit([d.BaseExtension((50,), [32])]), [32, 97, 107], [22, 19, 15, 13]
+    g = _gpu_vs_host(c, crt, mrs, **kw)
+    if name in ("dense", "model_a", "maxpool_odd", "shortcut", "redash_head"):
+        from dash_amd.runtime import HipEvaluator
+
+        xs = [np.random.default_rng(5 + i).integers(-20, 20, c.input_size) for i in range(2)]
+        ev = HipEvaluator(template=g.model, batch=1, device=0)
+        ev.load(0, g.model)
+        ev.encode_compressed_into(0, g, xs[0])
+        ev.upload_inputs_compressed()
+        ev.run()
+        ev.fetch_outputs()
+        np.testing.assert_array_equal(ev.decode(0, g), g.plain_q_eval(xs[0]))

@@ -115,3 +115,37 @@ def test_two_party_hip_server_in_thread():
                 np.testing.assert_array_equal(y, _plain(c, x))
     th.join(timeout=60)
     s.close()
+
+
+def test_two_party_benchmark_cpu():
+    """benchmarks/two_party.py over both splits (TCP client/server processes, attested enclave process) on the
+    host evaluator: one JSON record per split, verified against the plaintext model, offline bytes counted."""
+    import os
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, os.path.join(root, "benchmarks"))  # importable by name in the spawned server too
+    import two_party as tp
+    recs = tp.main(["--backend", "cpu", "--models", "MODEL_A/SIMPLE", "--batch", "2", "--rounds", "1"])
+    assert [r["split"] for r in recs] == ["tcp", "enclave"]
+    for r in recs:
+        assert r["verified"] and r["offline_gb_per_gc"] > 0 and r["served_inf_per_s"] > 0
+        assert r["online_bytes_per_inference"] > 0 and r["online_round_ms"] > 0
+
+
+def test_pipelined_offline_matches_serial():
+    """The pipelined offline phase (garbling overlapped with shipping, ACKs collected last) ships the same
+    models as the serial one: same seeds -> identical outputs and offline byte counts."""
+    c = build_circuit("MODEL_A")
+    xs = quantized_inputs("MODEL_A", 3)
+    res = []
+    for pipe in (False, True):
+        p, port = _start()
+        try:
+            with GarblerClient("127.0.0.1", port, c, 7, 100.0, batch=3, seed=b"p" * 16, pipeline=pipe) as cl:
+                cl.offline()
+                res.append((np.stack(cl.infer(xs)), cl.stats["offline_bytes"]))
+        finally:
+            p.join(timeout=60)
+    np.testing.assert_array_equal(res[0][0], res[1][0])
+    assert res[0][1] == res[1][1]
