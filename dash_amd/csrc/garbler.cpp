@@ -222,11 +222,14 @@ void Garbler::encode_cm(const i64* x, i64 N, const std::vector<comp_t*>& dst, in
     }, nthreads);
 }
 
-// Builds the input codebook on first use (bounded to 256 MiB; larger inputs use the per-label path).
+// Builds the input codebook on the second encode (bounded to 256 MiB; larger inputs use the per-label path).
+// A GC is single use in the protocol, and its one encode is cheaper per label (k labels per input) than the
+// codebook (sum of p_j labels per input); only a reused GC (benchmarks) amortizes the table.
 const Garbler::InputCodebook* Garbler::input_codebook() const {
     InputCodebook& cb = *codebook_;
     std::lock_guard<std::mutex> g(cb.m);
     if (cb.built) return cb.tab.empty() ? nullptr : &cb;
+    if (++cb.uses < 2) return nullptr;
     cb.built = true;
     if (in_base_.empty()) return nullptr;
     const int k = static_cast<int>(crt_.size());

@@ -77,6 +77,9 @@ struct Ctx {
     const ModC* mc;      // [max_mod + 1]
     uint32_t rk[44];     // PRG (seed) round keys
     const uint32_t* te0;
+    // multiples of this GC's offsets, per modulus p (null until a projection of that modulus needs them):
+    // iR[p] = [p][4 * chunks(n_p)] words, row i = the components i * R_p[q] mod p packed two per word
+    const uint32_t* const* iR;
 };
 
 // Chunked component-major labels (all device labels of the GPU garbler): the
@@ -534,6 +537,159 @@ __global__ __launch_bounds__(kPB, 4) void k_hash_jobs(Ctx c, Gadget g, In in, co
     }
 }
 
+// ---- uniform-offset compression: compress(x + a) for a per-lane label x and a wave-uniform row a
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ u16x2 as_u16x2(uint32_t w) { return __builtin_bit_cast(u16x2, w); }
+__device__ __forceinline__ uint32_t as_u32(u16x2 v) { return __builtin_bit_cast(uint32_t, v); }
+
+// C * d + v for d, v < 2^24 (four 32-bit limbs, carries by 64-bit adds)
+__device__ __forceinline__ u128 mad128_24(u128 C, uint32_t d, uint32_t v) {
+    const uint64_t lo = static_cast<uint64_t>(C), hi = static_cast<uint64_t>(C >> 64);
+    const uint64_t l0 = static_cast<uint64_t>(static_cast<uint32_t>(lo)) * d + v;
+    const uint64_t l1 = static_cast<uint64_t>(static_cast<uint32_t>(lo >> 32)) * d + (l0 >> 32);
+    const uint64_t h0 = static_cast<uint64_t>(static_cast<uint32_t>(hi)) * d + (l1 >> 32);
+    const uint64_t h1 = static_cast<uint64_t>(static_cast<uint32_t>(hi >> 32)) * d + (h0 >> 32);
+    return (static_cast<u128>((h1 << 32) | static_cast<uint32_t>(h0)) << 64) |
+           ((l1 << 32) | static_cast<uint32_t>(l0));
+}
+
+// Digits d_q = (x_q + a_q) mod q (q < n; padding components count as 0) of a per-lane chunked label x and a
+// uniform row a (a_q < q, two components
+// per word, chunk c8 at words 4 c8 .. 4 c8 + 3; same-address broadcast loads), compressed as sum_q d_q q^q by
+// Horner's rule from the top chunk: two digits per packed 16-bit add / subtract / min, one 24-bit multiply-add
+// (or shift-or for a power of two) per digit, a 128-bit merge per group of digits below 2^24 (the group
+// bookkeeping is scalar). d0 = digit 0 (the color when a_0 = i and x's color is x_0).
+template <bool PW2>
+__device__ __forceinline__ u128 compress_xa_t(LRef x, const uint32_t* a, const ModC& m, uint32_t& d0) {
+    const int nc = static_cast<int>(chunks_of(static_cast<int>(m.n)));
+    const uint32_t q = m.q, b = m.bits;
+    int g = 1;  // digits per group: q^g <= 2^24 (power of two: 24 / b bits)
+    uint32_t D = q;
+    if (PW2) {
+        g = static_cast<int>(24 / b);
+        D = 1u << (b * g);
+    } else {
+        while (static_cast<uint64_t>(D) * q <= (1u << 24)) {
+            D *= q;
+            ++g;
+        }
+    }
+    const u16x2 qq = {static_cast<unsigned short>(q), static_cast<unsigned short>(q)};
+    const u16x2 msk = {static_cast<unsigned short>(q - 1), static_cast<unsigned short>(q - 1)};
+    u128 C = 0;
+    uint32_t v = 0;
+    int r = (8 * nc - 1) % g;  // digits after the current one in its group (groups are aligned at digit 0)
+    uint32_t dlow = 0;
+    // kLd chunks of x and of the row in flight per round trip, consumed from the most significant chunk
+    for (int c0 = nc - 1; c0 >= 0; c0 -= kLd) {
+        u32x4a xv[kLd], av[kLd];
+#pragma unroll
+        for (int h = 0; h < kLd; ++h) {
+            if (c0 - h >= 0) {
+                xv[h] = ld_chunk(x, c0 - h);
+                av[h] = *reinterpret_cast<const u32x4a*>(a + 4 * (c0 - h));
+            }
+        }
+#pragma unroll
+        for (int h = 0; h < kLd; ++h) {
+            if (c0 - h < 0) break;
+            uint32_t t[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const u16x2 sm = as_u16x2(xv[h][u]) + as_u16x2(av[h][u]);
+                t[u] = PW2 ? as_u32(sm & msk) : as_u32(__builtin_elementwise_min(sm, sm - qq));
+            }
+            const int qb = 8 * (c0 - h);  // first component of this chunk
+#pragma unroll
+            for (int k = 7; k >= 0; --k) {
+                // chunk padding (components >= n) is not guaranteed zero in reused label blocks: digit 0
+                const uint32_t d = qb + k >= static_cast<int>(m.n) ? 0u
+                                   : ((k & 1) ? (t[k >> 1] >> 16) : (t[k >> 1] & 0xffffu));
+                v = PW2 ? ((v << b) | d) : __umul24(v, q) + d;
+                if (r == 0) {
+                    C = mad128_24(C, D, v);
+                    v = 0;
+                    r = g - 1;
+                } else {
+                    --r;
+                }
+            }
+            dlow = t[0] & 0xffffu;
+        }
+    }
+    d0 = dlow;
+    return C;
+}
+__device__ __forceinline__ u128 compress_xa(LRef x, const uint32_t* a, const ModC& m, uint32_t& d0) {
+    return m.bits ? compress_xa_t<true>(x, a, m, d0) : compress_xa_t<false>(x, a, m, d0);
+}
+
+// Key hashes with the entry index i uniform across the wave (one wave per (64-element tile, hash job), a job =
+// up to kHJ consecutive i of one projection): key = x + i R_pin, i.e. digits x_q + (i R_q mod p) with the
+// multiple row iR[pin][i] read from scalar memory; the key's color (digit 0, R_0 = 1) places the hash:
+// HC / CC[first + color][e] = H, i.
+template <int C>
+__global__ __launch_bounds__(kPB, 4) void k_hash_iu(Ctx c, Gadget g, In in, const HashJob* jobs, int njobs) {
+    __shared__ __attribute__((aligned(16))) uint32_t lds_aes[aes_lds_words<C>()];
+    aes_lds_fill<C>(lds_aes, c.te0);
+    const AesT<C> aes = aes_ctx<C>(lds_aes, nullptr);
+    const int64_t N = g.N;
+    const int64_t tiles = (N + kTile - 1) / kTile;
+    const int64_t nw = tiles * njobs;
+    const int lane = static_cast<int>(threadIdx.x) & (kTile - 1);
+    const int64_t wpb = kPB / kTile;
+    const int64_t w0 = static_cast<int64_t>(blockIdx.x) * wpb + rfl(static_cast<int>(threadIdx.x) / kTile);
+    const int64_t wstep = static_cast<int64_t>(gridDim.x) * wpb;
+    for (int64_t w = w0; w < nw; w += wstep) {
+        const int64_t tile = w / njobs;
+        const int jb = static_cast<int>(w - tile * njobs);
+        const int pi = rfl(jobs[jb].proj), c0 = rfl(jobs[jb].c0);
+        const Proj P = rfl_proj(g.projs[pi]);
+        const ModC mi = rfl_modc(c.mc[P.pin]);
+        const int c1 = min(P.pin, c0 + kHJ);
+        const int64_t e_raw = tile * kTile + lane;
+        const int64_t e = e_raw < N ? e_raw : N - 1;
+        const LRef x = label_ref(c, g, in, e, P.in_kind, P.in_idx, P.pin);
+        const int words = 4 * static_cast<int>(chunks_of(static_cast<int>(mi.n)));
+        const uint32_t* rows = c.iR[P.pin];
+        for (int i = c0; i < c1; ++i) {
+            uint32_t col;
+            const u128 key = compress_xa(x, rows + static_cast<int64_t>(i) * words, mi, col);
+            const u128 H = aes_encrypt(aes, key);
+            if (e_raw < N) {
+                g.HC[(P.first + col) * N + e] = H;
+                g.CC[(P.first + col) * N + e] = static_cast<uint16_t>(i);
+            }
+        }
+    }
+}
+
+// the multiple rows iR[p] of this GC's offsets (k_hash_iu, k_bank_iu): dst[i][w] = (i R_2w mod p) |
+// (i R_2w+1 mod p) << 16 for the components of chunks(n_p) chunks (padding components are 0)
+struct IrJob {
+    uint32_t* dst;
+    int p, words;
+};
+constexpr int kMaxIr = 32;
+struct IrArgs {
+    IrJob j[kMaxIr];
+    int n;
+};
+__global__ __launch_bounds__(256) void k_iR(Ctx c, IrArgs a) {
+    const IrJob J = a.j[blockIdx.y];
+    const ModC m = c.mc[J.p];
+    const int16_t* R = c.R + static_cast<int64_t>(J.p) * kW;
+    const int64_t total = static_cast<int64_t>(J.p) * J.words;
+    for (int64_t x = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; x < total;
+         x += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+        const uint32_t i = static_cast<uint32_t>(x / J.words);
+        const int wd = static_cast<int>(x - static_cast<int64_t>(i) * J.words);
+        const uint32_t r0 = modq(i * static_cast<uint32_t>(R[2 * wd]), m);
+        const uint32_t r1 = modq(i * static_cast<uint32_t>(R[2 * wd + 1]), m);
+        J.dst[x] = r0 | (r1 << 16);
+    }
+}
+
 // the 8 low bits (mod-2 components) of a chunk, component q at bit q
 __device__ __forceinline__ uint32_t bits8(const u32x4a& v) {
     uint32_t b = 0;
@@ -554,6 +710,16 @@ inline int gg_aes_copies() {
 inline auto draw_kernel() { return gg_aes_copies() == 16 ? k_draw<16> : k_draw<32>; }
 inline auto hash_kernel() { return gg_aes_copies() == 16 ? k_hash<16> : k_hash<32>; }
 inline auto hash_jobs_kernel() { return gg_aes_copies() == 16 ? k_hash_jobs<16> : k_hash_jobs<32>; }
+inline auto hash_iu_kernel() { return gg_aes_copies() == 16 ? k_hash_iu<16> : k_hash_iu<32>; }
+// DASH_GG_KEYS (A/B knob): 2 (default) = uniform-i key hashes and bank payloads from the offsets' multiple rows
+// (compress_xa); 1 = multiple rows for the bank payloads only; 0 = the round-3 per-lane forms
+inline int gg_hash_mode() {
+    static const int v = [] {
+        const char* e = std::getenv("DASH_GG_KEYS");
+        return e ? std::atoi(e) : 2;
+    }();
+    return v;
+}
 // DASH_GG_HASH=entry: one wave per (tile, entry) (k_hash); default: per (tile, hash job) (k_hash_jobs).
 // Rejected (profiles/ab/README.md): a block per (tile, projection) with the label staged in LDS (9.8 -> 17.6 ms
 // per 4 GCs: most projections have 3-17 colors, most of the block's waves idled at its barriers), and a wave per
@@ -628,11 +794,20 @@ __global__ __launch_bounds__(256) void k_bank(Ctx c, Gadget g, In in, const Bank
         const ModC mo = rfl_modc(c.mc[pout]);
         const int64_t e_raw = tile * kTile + lane;
         const int64_t e = e_raw < N ? e_raw : N - 1;
-        CompressFwd pc;
-        pc.init();
-        if (res < 0) push_lin<true, false>(pc, slot_ref(g, slot, e), row_ref(c.R + static_cast<int64_t>(pout) * kW), f, mo);
-        else push_lin<false, false>(pc, slot_ref(g, slot, e), LRef{in.p[res] + e * in.es[res], in.cs[res]}, f, mo);
-        if (e_raw < N) g.BK[static_cast<int64_t>(row) * N + e] = pc.finish();
+        u128 P;
+        if (res < 0 && c.iR != nullptr && c.iR[pout] != nullptr) {
+            // uniform offset v R_pout: its multiple row from scalar memory (compress_xa)
+            const int words = 4 * static_cast<int>(chunks_of(static_cast<int>(mo.n)));
+            uint32_t d0;
+            P = compress_xa(slot_ref(g, slot, e), c.iR[pout] + static_cast<int64_t>(f) * words, mo, d0);
+        } else {
+            CompressFwd pc;
+            pc.init();
+            if (res < 0) push_lin<true, false>(pc, slot_ref(g, slot, e), row_ref(c.R + static_cast<int64_t>(pout) * kW), f, mo);
+            else push_lin<false, false>(pc, slot_ref(g, slot, e), LRef{in.p[res] + e * in.es[res], in.cs[res]}, f, mo);
+            P = pc.finish();
+        }
+        if (e_raw < N) g.BK[static_cast<int64_t>(row) * N + e] = P;
     }
 }
 
@@ -1586,6 +1761,7 @@ void check_desc(const gg::Gadget& g) {
 // key-hash scratch of the calling thread's garbling context (DevCtx, grow-only): [entries][N] hashes + colors
 std::pair<u128*, uint16_t*> hc_scratch(size_t entries, int64_t N);
 u128* bank_scratch(size_t rows, int64_t N);
+const uint32_t* const* ensure_iR(const gg::Ctx& c, const std::vector<int>& mods);
 
 // Host-side function data of a projection set (the value f(i, d) of every entry): k_emit reads bank rows
 // and bank indices built from it here, so none of it is needed on the device.
@@ -1790,13 +1966,35 @@ void project(const gg::Ctx& c, gg::Gadget& g, const gg::In& in, const gg::Tables
     g.BK = bank_scratch(rows.size(), g.N);
     check_desc(g);
     const int64_t lanes = (g.N + gg::kTile - 1) / gg::kTile * gg::kTile;
+    // multiple rows of the projections' input moduli (uniform-i key hashes) and of the bank rows' R offsets
+    gg::Ctx cc = c;
+    bool iu = gg::gg_hash_mode() == 2;
+    {
+        std::vector<int> mods;
+        for (const auto& p : pr) {
+            mods.push_back(p.pin);
+            if (p.pin >= 32768) iu = false;
+        }
+        for (const auto& r : rows)
+            if (r.res < 0) mods.push_back(r.pout);
+        std::sort(mods.begin(), mods.end());
+        mods.erase(std::unique(mods.begin(), mods.end()), mods.end());
+        if (gg::gg_hash_mode() != 0) cc.iR = ensure_iR(c, mods);
+    }
     // (rejected, profiles/ab/README.md: one block per label group with the label staged in LDS, 7.2 -> 7.6-8.2 ms
     // per 4 GCs, and one wave per group stepping packed-byte payloads o + v*off incrementally, 10.7 ms)
     if (!rows.empty()) {
         hipLaunchKernelGGL(gg::k_bank, dim3(blocks_for(lanes * static_cast<int64_t>(rows.size()), 256, 32768)), dim3(256), 0,
-                           gg::tl_st, c, g, in, em.rows, static_cast<int>(rows.size()));
+                           gg::tl_st, cc, g, in, em.rows, static_cast<int>(rows.size()));
     }
-    if (gg::gg_hash_jobs()) {
+    if (iu) {
+        std::vector<gg::HashJob> hj;
+        for (int pi = 0; pi < np; ++pi)
+            for (int c0 = 0; c0 < pr[pi].pin; c0 += gg::kHJ) hj.push_back(gg::HashJob{pi, c0});
+        const gg::HashJob* dj = gg::dconst(hj.data(), hj.size());
+        hipLaunchKernelGGL(gg::hash_iu_kernel(), dim3(blocks_for(lanes * static_cast<int64_t>(hj.size()), gg::kPB, 16384)),
+                           dim3(gg::kPB), 0, gg::tl_st, cc, g, in, dj, static_cast<int>(hj.size()));
+    } else if (gg::gg_hash_jobs()) {
         std::vector<gg::HashJob> hj;
         for (int pi = 0; pi < np; ++pi)
             for (int c0 = 0; c0 < pr[pi].pin; c0 += gg::kHJ) hj.push_back(gg::HashJob{pi, c0});
@@ -1956,6 +2154,12 @@ struct DevCtx {
         }
         return BK;
     }
+    // multiple rows iR[p] of the current GC's offsets (k_iR): per-modulus grow-only buffers, valid for the
+    // garbling generation that computed them (a new GpuGarbler = new offsets R = new generation)
+    uint64_t iR_gen = 0;
+    std::map<int, std::pair<uint32_t*, uint64_t>> iR_buf;  // p -> (buffer, generation)
+    const uint32_t* const* iR_dev = nullptr;                // staged pointer table of the current generation
+    bool iR_dirty = true;
     // key hashes / colors between k_hash and k_emit
     u128* HC = nullptr;
     uint16_t* CC = nullptr;
@@ -1982,6 +2186,43 @@ std::pair<u128*, uint16_t*> hc_scratch(size_t entries, int64_t N) {
 u128* bank_scratch(size_t rows, int64_t N) {
     DASH_CHECK(tl_dc != nullptr, "gpu garbler: no garbling context on this thread");
     return tl_dc->bank(rows, N);
+}
+// the iR pointer table with rows for every modulus of `mods` (k_iR launches for those missing in this
+// generation); moduli >= 32768 get none (their users keep the generic per-lane form)
+const uint32_t* const* ensure_iR(const gg::Ctx& c, const std::vector<int>& mods) {
+    DASH_CHECK(tl_dc != nullptr, "gpu garbler: no garbling context on this thread");
+    DevCtx& d = *tl_dc;
+    gg::IrArgs a{};
+    auto flush = [&]() {
+        if (!a.n) return;
+        int64_t mx = 1;
+        for (int i = 0; i < a.n; ++i) mx = std::max<int64_t>(mx, static_cast<int64_t>(a.j[i].p) * a.j[i].words);
+        hipLaunchKernelGGL(gg::k_iR, dim3(blocks_for(mx, 256, 1024), a.n), dim3(256), 0, gg::tl_st, c, a);
+        a.n = 0;
+    };
+    for (int p : mods) {
+        if (p < 2 || p >= 32768 || p > d.mc_max) continue;
+        auto& slot = d.iR_buf[p];
+        if (slot.first && slot.second == d.iR_gen) continue;
+        const int words = 4 * static_cast<int>(gg::chunks_of(nr_comps(p)));
+        if (!slot.first) {
+            HIPCHECK(hipStreamSynchronize(gg::tl_st));  // no kernel of this context may still hold the stage ring
+            HIPCHECK(hipMalloc(reinterpret_cast<void**>(&slot.first), static_cast<size_t>(p) * words * sizeof(uint32_t)));
+        }
+        slot.second = d.iR_gen;
+        d.iR_dirty = true;
+        a.j[a.n++] = gg::IrJob{slot.first, p, words};
+        if (a.n == gg::kMaxIr) flush();
+    }
+    flush();
+    if (d.iR_dirty) {
+        std::vector<const uint32_t*> tab(static_cast<size_t>(d.mc_max) + 1, nullptr);
+        for (const auto& kv : d.iR_buf)
+            if (kv.second.second == d.iR_gen && kv.first <= d.mc_max) tab[kv.first] = kv.second.first;
+        d.iR_dev = d.stage(tab.data(), tab.size());
+        d.iR_dirty = false;
+    }
+    return d.iR_dev;
 }
 }  // namespace
 // A free garbling context of the device, locked for the caller: up to DASH_GG_CONTEXTS (default 4) per
@@ -2097,6 +2338,9 @@ GpuGarbler::GpuGarbler(const std::vector<int>& crt, const std::vector<int>& mrs,
     I.c.Z = I.stage(hZ.data(), hZ.size());
     I.c.mc = I.dc.modc(R.max_mod);
     I.c.te0 = I.dc.te0;
+    ++I.dc.iR_gen;  // this GC's offsets R: every multiple row is recomputed on first use
+    I.dc.iR_dirty = true;
+    I.c.iR = nullptr;
     auto rk = round_key_words(reinterpret_cast<const uint8_t*>(seed16.data()));
     std::copy(rk.begin(), rk.end(), I.c.rk);
     if (!mrs.empty()) {

@@ -156,6 +156,7 @@ class Garbler {
     struct InputCodebook {
         std::mutex m;
         bool built = false;
+        int uses = 0;           // encodes so far: a GC encoded once (the protocol's case) never builds the table
         std::vector<u128> tab;  // residue j at off[j]: [N][p_j]
         std::vector<i64> off;
     };
