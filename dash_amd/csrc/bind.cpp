@@ -241,6 +241,16 @@ PYBIND11_MODULE(_dash_native, m) {
     }, "mixed-modulus half gate x (mod p) * y (mod q): garbler table [p], evaluator table [q + 1] (q full entries, "
        "then the mini entry), output base label; sk03 / sk04 drawn from Prg(seed) on `stream`");
 
+    py::class_<GarbleSpecs, std::shared_ptr<GarbleSpecs>>(m, "GarbleSpecs",
+        "a circuit's layer specs converted once; its public weights are reduced mod M once per CRT modulus and "
+        "shared by every GC garbled from it")
+        .def(py::init([](const py::list& layers) {
+            auto s = std::make_shared<GarbleSpecs>();
+            s->layers = specs_from_py(layers);
+            return s;
+        }))
+        .def_property_readonly("num_layers", [](const GarbleSpecs& s) { return s.layers.size(); });
+
     py::class_<GarbledModel, std::shared_ptr<GarbledModel>>(m, "GarbledModel")
         .def("serialize", [](const GarbledModel& g) { return py::bytes(g.serialize()); })
         .def_static("deserialize", [](py::bytes b) { return std::make_shared<GarbledModel>(GarbledModel::deserialize(std::string(b))); })
@@ -326,6 +336,27 @@ PYBIND11_MODULE(_dash_native, m) {
                  return std::make_shared<Garbler>(crt, mrs, std::string(seed), max_mod);
              }),
              py::arg("crt"), py::arg("mrs"), py::arg("seed"), py::arg("max_mod") = 0)
+        .def("garble", [](Garbler& g, std::shared_ptr<GarbleSpecs> specs, std::vector<i64> in_dims, int nthreads,
+                          int device, bool fused_sign, bool rescale_mrs, bool relu_mrs, bool relu_joint,
+                          std::shared_ptr<TableSink> sink) {
+            GarbleOptions o;
+            o.sink = std::move(sink);
+            o.nthreads = nthreads;
+            o.device = device;
+            o.fused_sign = fused_sign;
+            o.rescale_mrs = rescale_mrs;
+            o.relu_mrs = relu_mrs;
+            o.relu_joint = relu_joint;
+            o.cache = specs.get();
+            GarbledModel gm;
+            {
+                py::gil_scoped_release rel;
+                gm = g.garble(specs->layers, in_dims, o);
+            }
+            return std::make_shared<GarbledModel>(std::move(gm));
+        }, py::arg("layers"), py::arg("in_dims"), py::arg("nthreads") = 0, py::arg("device") = -1,
+           py::arg("fused_sign") = true, py::arg("rescale_mrs") = false,
+           py::arg("relu_mrs") = false, py::arg("relu_joint") = false, py::arg("sink") = nullptr)
         .def("garble", [](Garbler& g, const py::list& layers, std::vector<i64> in_dims, int nthreads, int device,
                           bool fused_sign, bool rescale_mrs, bool relu_mrs, bool relu_joint,
                           std::shared_ptr<TableSink> sink) {

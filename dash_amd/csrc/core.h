@@ -288,6 +288,16 @@ struct Prg {
 };
 
 // Stream identifiers: distinct (layer, slot, element) triples never collide.
+// 64-bit mix hash of an int64 array (public weights: GPU plan cache keys)
+inline uint64_t hash_i64(const i64* w, size_t n) {
+    uint64_t h = 0x9e3779b97f4a7c15ull ^ n;
+    for (size_t i = 0; i < n; ++i) {
+        h ^= static_cast<uint64_t>(w[i]) + 0x9e3779b97f4a7c15ull + (h << 6) + (h >> 2);
+        h *= 0xff51afd7ed558ccdull;
+    }
+    return h;
+}
+
 inline u64 stream_id(u64 layer, u64 slot, u64 elem) {
     return (layer << 44) ^ (slot << 36) ^ elem;
 }

@@ -375,6 +375,28 @@ GarbledModel Garbler::garble(const std::vector<LayerSpec>& layers, const std::ve
         auto d = opt.sink->dest(cur_layer, name, a.nbytes);
         if (d) a = Array::on_device(a.dtype, a.shape, std::move(d));
     };
+    // a layer's public weights reduced mod M, and their content hash (the GPU plan key): computed once per specs
+    // object (GarbleOptions::cache) and shared by every GC garbled from it
+    auto reduced_weights = [&](size_t li, const std::vector<i64>& w, std::vector<i64> shape) {
+        if (opt.cache) {
+            std::lock_guard<std::mutex> lk(opt.cache->m);
+            auto it = opt.cache->wcache.find({li, M_});
+            if (it != opt.cache->wcache.end() && it->second.w.count() == w.size())
+                return std::make_pair(it->second.w, it->second.hash);
+        }
+        Array wa(DType::i64, std::move(shape));
+        DASH_CHECK(wa.count() == w.size(), "weight shape");
+        i64* d = wa.ptr<i64>();
+        parallel_for(static_cast<i64>(w.size()), [&](i64 b0, i64 b1) {
+            for (i64 i = b0; i < b1; ++i) d[i] = pmod(w[i], M_);
+        }, nt);
+        const uint64_t h = hash_i64(d, w.size());
+        if (opt.cache) {
+            std::lock_guard<std::mutex> lk(opt.cache->m);
+            opt.cache->wcache[{li, M_}] = GarbleSpecs::Weights{wa, h};
+        }
+        return std::make_pair(wa, h);
+    };
     // which copy of `cur` is current: GPU layers read and write the device copy,
     // host layers the host copy; a copy is refreshed only when the other side changed it
     bool host_ok = true, dev_ok = false;
@@ -534,8 +556,8 @@ GarbledModel Garbler::garble(const std::vector<LayerSpec>& layers, const std::ve
                 const auto& w = paramv(spec.p, "w");
                 const auto& b = paramv(spec.p, "b");
                 DASH_CHECK(static_cast<i64>(w.size()) == in * out && static_cast<i64>(b.size()) == out, "dense weight shape");
-                Array wa(DType::i64, {out, in});
-                for (i64 i = 0; i < in * out; ++i) wa.ptr<i64>()[i] = pmod(w[i], M_);
+                const auto rw = reduced_weights(li, w, {out, in});
+                const Array& wa = rw.first;
                 g.a["w"] = wa;
                 CrtLabels nxt;
                 for (int j = 0; j < k; ++j) {
@@ -570,7 +592,7 @@ GarbledModel Garbler::garble(const std::vector<LayerSpec>& layers, const std::ve
                     }, nt);
                     nxt.push_back(std::move(O));
                 }
-                if (on_gpu) gpu->dense(in, out, ch, std::vector<i64>(wa.ptr<i64>(), wa.ptr<i64>() + wa.count()), cur);
+                if (on_gpu) gpu->dense(in, out, ch, wa.ptr<i64>(), wa.count(), rw.second, cur);
                 else cur = std::move(nxt);
                 dims = {out};
                 break;
@@ -582,8 +604,8 @@ GarbledModel Garbler::garble(const std::vector<LayerSpec>& layers, const std::ve
                 const auto& w = paramv(spec.p, "w");
                 const auto& b = paramv(spec.p, "b");
                 DASH_CHECK(static_cast<i64>(w.size()) == G.F * G.K() && static_cast<i64>(b.size()) == G.F, "conv weight shape");
-                Array wa(DType::i64, {G.F, G.C, G.kh, G.kw});
-                for (size_t i = 0; i < w.size(); ++i) wa.ptr<i64>()[i] = pmod(w[i], M_);
+                const auto rw = reduced_weights(li, w, {G.F, G.C, G.kh, G.kw});
+                const Array& wa = rw.first;
                 g.a["w"] = wa;
                 CrtLabels nxt;
                 for (int j = 0; j < k; ++j) {
@@ -596,7 +618,7 @@ GarbledModel Garbler::garble(const std::vector<LayerSpec>& layers, const std::ve
                     g.a[arr_name("bias.", j, "")] = bias;
                 }
                 if (gpu) {
-                    gpu->conv(G, std::vector<i64>(wa.ptr<i64>(), wa.ptr<i64>() + wa.count()), cur);
+                    gpu->conv(G, wa.ptr<i64>(), wa.count(), rw.second, cur);
                     dims = {G.F, G.OH, G.OW};
                     break;
                 }

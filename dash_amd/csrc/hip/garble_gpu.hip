@@ -2411,15 +2411,6 @@ void GpuGarbler::to_host(CrtLabels& cur) {
 }
 
 namespace {
-// 64-bit mix hash of a weight vector (public conv weights: the per-layer MFMA setup is cached by content)
-uint64_t weights_hash(const std::vector<i64>& w) {
-    uint64_t h = 0x9e3779b97f4a7c15ull ^ w.size();
-    for (i64 v : w) {
-        h ^= static_cast<uint64_t>(v) + 0x9e3779b97f4a7c15ull + (h << 6) + (h >> 2);
-        h *= 0xff51afd7ed558ccdull;
-    }
-    return h;
-}
 struct ConvPlanKey {
     int dev;
     uint64_t wh;
@@ -2448,14 +2439,14 @@ std::mutex& conv_plans_mutex() {
 // output chunked back (one launch each for all residues). The public per-layer setup
 // (centered int8 weight images, zero counts, all-zero bias rows) is built
 // once per process and looked up by a hash of the weights.
-void GpuGarbler::conv(const ConvGeom& G, const std::vector<i64>& w, CrtLabels& cur) {
+void GpuGarbler::conv(const ConvGeom& G, const i64* w, size_t nw, uint64_t wh, CrtLabels& cur) {
     Impl& I = *impl_;
     I.enter();
     I.check_cur(cur);
     PhaseTrace tr_("conv");
     const int K = static_cast<int>(G.K());
     const int F = static_cast<int>(G.F);
-    DASH_CHECK(static_cast<i64>(w.size()) == G.F * G.K(), "gpu garbler: conv weight shape");
+    DASH_CHECK(static_cast<i64>(nw) == G.F * G.K(), "gpu garbler: conv weight shape");
     DASH_CHECK(G.C * G.H * G.W == I.cur_N, "gpu garbler: conv input size mismatch");
     DASH_CHECK(static_cast<int>(I.cur_mod.size()) <= kMaxRes, "gpu garbler: too many residues");
     std::vector<int> mods = I.cur_mod;
@@ -2463,7 +2454,7 @@ void GpuGarbler::conv(const ConvGeom& G, const std::vector<i64>& w, CrtLabels& c
     std::vector<DevBlock> out = I.alloc_labels(mods, Nout);
     dev::ConvArgs a{};
     {
-        ConvPlanKey key{I.device, weights_hash(w), {G.C, G.H, G.W, G.F, G.kh, G.kw, G.sh, G.sw, G.ph, G.pw}, mods};
+        ConvPlanKey key{I.device, wh, {G.C, G.H, G.W, G.F, G.kh, G.kw, G.sh, G.sw, G.ph, G.pw}, mods};
         std::lock_guard<std::mutex> lk(conv_plans_mutex());
         auto it = conv_plans().find(key);
         if (it != conv_plans().end()) {
@@ -3331,16 +3322,16 @@ void GpuGarbler::add_saved(size_t idx, CrtLabels& cur) {
 }
 
 // dense base labels (garbler.cpp K_DENSE): y_o = sum_{w != 0 mod p} w x_src(i) + (1 + #zero weights) Z_p
-void GpuGarbler::dense(i64 in, i64 out, i64 ch, const std::vector<i64>& w, CrtLabels& cur) {
+void GpuGarbler::dense(i64 in, i64 out, i64 ch, const i64* w, size_t nw, uint64_t wh, CrtLabels& cur) {
     Impl& I = *impl_;
     I.enter();
     I.check_cur(cur);
     PhaseTrace tr_("dense");
-    DASH_CHECK(I.cur_N == in && static_cast<i64>(w.size()) == in * out, "gpu garbler: dense shape");
+    DASH_CHECK(I.cur_N == in && static_cast<i64>(nw) == in * out, "gpu garbler: dense shape");
     const int k = static_cast<int>(I.cur_mod.size());
     DensePlan plan{};
     {
-        DensePlanKey key{I.device, weights_hash(w), {in, out, ch}, I.cur_mod};
+        DensePlanKey key{I.device, wh, {in, out, ch}, I.cur_mod};
         std::lock_guard<std::mutex> lk(dense_plans_mutex());
         auto it = dense_plans().find(key);
         if (it != dense_plans().end()) {

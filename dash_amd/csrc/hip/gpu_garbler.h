@@ -26,8 +26,8 @@ class GpuGarbler {
     void to_device(const CrtLabels& cur);
     void to_host(CrtLabels& cur);
     // conv base labels: y = sum_{w != 0 mod p} w*x + (1 + #zero weights)*Z_p (padding reads Z_p);
-    // w are the weights reduced mod M ([F][C][kh][kw])
-    void conv(const ConvGeom& G, const std::vector<i64>& w, CrtLabels& cur);
+    // w are the weights reduced mod M ([F][C][kh][kw]), wh their hash_i64 (plan cache key)
+    void conv(const ConvGeom& G, const i64* w, size_t nw, uint64_t wh, CrtLabels& cur);
     // ReLU (relu_crt/prefix/mmg/mme set) or Sign layer: tables; device cur -> next base labels
     void sign_layer(uint64_t layer, const SignPlan& sp, CrtLabels& cur, Array& ap, Array& c1, Array& c2, Array& sg,
                     const std::vector<int>* relu_crt, const std::vector<i64>* prefix, Array* mmg, Array* mme);
@@ -49,7 +49,7 @@ class GpuGarbler {
 
     // dense base labels y_o = sum_{w != 0 mod p} w x_src(i) + (1 + #zero weights) Z_p (w reduced mod M, [out][in],
     // src = dense_src(i, in, channel_tf))
-    void dense(i64 in, i64 out, i64 channel_tf, const std::vector<i64>& w, CrtLabels& cur);
+    void dense(i64 in, i64 out, i64 channel_tf, const i64* w, size_t nw, uint64_t wh, CrtLabels& cur);
     // window sums of the device cur
     void sumpool(const PoolGeom& G, CrtLabels& cur);
     // device copies of layer outputs a later residual add / in_src layer reads (idx = layer index + 1)

@@ -108,6 +108,19 @@ struct TableSink {
     std::function<std::shared_ptr<Array::Device>(size_t layer, const std::string& name, size_t nbytes)> dest;
 };
 
+// A circuit's layer specs converted once, plus the public weights reduced mod M (and their content hash, the
+// GPU plan key) shared by every GC garbled from them: per-GC host work no longer scales with the weight count
+// (VGG-16: 15 M weights were copied, reduced and hashed for every GC).
+struct GarbleSpecs {
+    std::vector<LayerSpec> layers;
+    struct Weights {
+        Array w;            // int64 [out][in] / [F][C][kh][kw], reduced mod M
+        uint64_t hash = 0;  // hash_i64 of w
+    };
+    std::mutex m;
+    std::map<std::pair<size_t, i64>, Weights> wcache;  // (layer, M)
+};
+
 struct GarbleOptions {
     int nthreads = 0;
     int device = -1;  // >= 0: garble ReLU / Sign / legacy rescale layers on this GPU
@@ -118,6 +131,7 @@ struct GarbleOptions {
     // (gadgets.h RescaleMrsPlan::sign_last); other ReLUs use relu_mrs / the approximate gadget.
     bool relu_joint = false;
     std::shared_ptr<TableSink> sink;  // GPU-garbled tables go straight to these buffers (device >= 0 only)
+    GarbleSpecs* cache = nullptr;     // reduced-weight cache of the specs being garbled (optional)
 };
 
 class Garbler {

@@ -119,7 +119,7 @@ class GarbledCircuit:
 
     # -------------------------------------------------------------- offline
     def garble(self):
-        specs = self.circuit.garble_specs()
+        specs = self.circuit.garble_specs_native()
         t = time.perf_counter()
         self.model = self.garbler.garble(specs, list(self.circuit.input_dims), self.nthreads, self.device,
                                          self.fused_sign, self.rescale == "mrs", self.relu == "mrs",

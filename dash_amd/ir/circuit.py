@@ -144,6 +144,7 @@ class Circuit:
         return max(k, 1)
 
     def quantize(self, q_const: float):
+        self._native_specs = None
         for layer in self.layers:
             layer.quantize(q_const)
 
@@ -181,6 +182,26 @@ class Circuit:
                 last_q, q = q, q - step
             self.quantize(q)
         return q
+
+    def __getstate__(self):
+        # the cached native specs are process-local (circuits are pickled to other ranks / processes)
+        st = dict(self.__dict__)
+        st.pop("_native_specs", None)
+        return st
+
+    def garble_specs_native(self):
+        """The layer specs as a native GarbleSpecs, built once and reused while the layers' quantized parameters
+        are unchanged (a fingerprint of the layer list and its weight arrays' identity; quantize() drops it):
+        the garbler then reduces and hashes the public weights once, not per GC."""
+        from ..native import native
+
+        fp = tuple((id(l), l.kind, id(getattr(l, "q_weights", None)), id(getattr(l, "q_biases", None)),
+                    getattr(l, "in_src", None)) for l in self.layers)
+        cache = getattr(self, "_native_specs", None)
+        if cache is None or cache[0] != fp:
+            cache = (fp, native().GarbleSpecs(self.garble_specs()))
+            self._native_specs = cache
+        return cache[1]
 
     def garble_specs(self) -> list:
         specs = []

@@ -17,7 +17,7 @@ GpuGarbler::GpuGarbler(const std::vector<int>&, const std::vector<int>&, const s
 GpuGarbler::~GpuGarbler() = default;
 void GpuGarbler::to_device(const CrtLabels&) { no_gpu(); }
 void GpuGarbler::to_host(CrtLabels&) { no_gpu(); }
-void GpuGarbler::conv(const ConvGeom&, const std::vector<i64>&, CrtLabels&) { no_gpu(); }
+void GpuGarbler::conv(const ConvGeom&, const i64*, size_t, uint64_t, CrtLabels&) { no_gpu(); }
 void GpuGarbler::sign_layer(uint64_t, const SignPlan&, CrtLabels&, Array&, Array&, Array&, Array&,
                             const std::vector<int>*, const std::vector<i64>*, Array*, Array*) {
     no_gpu();
@@ -34,7 +34,7 @@ void GpuGarbler::relu_mrs(uint64_t, const SignMrsPlan&, CrtLabels&, Array&, cons
     no_gpu();
 }
 void GpuGarbler::relu_mult(uint64_t, CrtLabels&, const std::vector<i64>*, Array&, Array&) { no_gpu(); }
-void GpuGarbler::dense(i64, i64, i64, const std::vector<i64>&, CrtLabels&) { no_gpu(); }
+void GpuGarbler::dense(i64, i64, i64, const i64*, size_t, uint64_t, CrtLabels&) { no_gpu(); }
 void GpuGarbler::sumpool(const PoolGeom&, CrtLabels&) { no_gpu(); }
 void GpuGarbler::save(size_t) { no_gpu(); }
 bool GpuGarbler::has_saved(size_t) const { return false; }

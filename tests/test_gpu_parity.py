@@ -443,6 +443,7 @@ def test_gpu_garbler_bit_identical_all_kinds(name):
 
     rng = np.random.default_rng(11)
     crt, mrs, kw = 8, 100.0, {}
+    xs = [np.random.default_rng(5 + i).integers(-20, 20, 1) for i in range(2)]  # replaced per circuit below
     if name == "dense":
         c = d.Circuit([_dense_layer(rng, 300, 70)])
     elif name == "dense_tf":
@@ -466,11 +467,14 @@ def test_gpu_garbler_bit_identical_all_kinds(name):
         from tests.test_garbled_layers import _shortcut_block
 
         c, xs = _shortcut_block()
-        crt = c.infer_crt_base_size(xs)
+        crt = c.infer_crt_base_size(xs)  # sized for these inputs
     elif name == "redash_head":
+        from dash_amd.models import quantized_inputs
+
         cfg = BENCH_CONFIGS["MODEL_F_MINIONN_POOL_REPL/REDASH_OPT"]
         full = build_circuit("MODEL_F_MINIONN_POOL_REPL", cfg["q_method"], cfg["q_parameter"], seed=0)
         c, crt, mrs = d.Circuit(full.layers[:4]), cfg["crt"], cfg["mrs"]  # conv, rescale({32}), relu, conv
+        xs = quantized_inputs("MODEL_F_MINIONN_POOL_REPL", 2, cfg["q_method"], cfg["q_parameter"], seed=3)
     elif name == "redash_rescale2":
         c, crt, mrs = d.Circuit([d.Rescale([32], (200,))]), [32, 3, 5, 7, 11, 13, 17], [10, 9, 9, 8, 7, 7, 6]
     else:
@@ -479,7 +483,8 @@ def test_gpu_garbler_bit_identical_all_kinds(name):
     if name in ("dense", "model_a", "maxpool_odd", "shortcut", "redash_head"):
         from dash_amd.runtime import HipEvaluator
 
-        xs = [np.random.default_rng(5 + i).integers(-20, 20, c.input_size) for i in range(2)]
+        if xs[0].size != c.input_size:
+            xs = [np.random.default_rng(5 + i).integers(-20, 20, c.input_size) for i in range(2)]
         ev = HipEvaluator(template=g.model, batch=1, device=0)
         ev.load(0, g.model)
         ev.encode_compressed_into(0, g, xs[0])
