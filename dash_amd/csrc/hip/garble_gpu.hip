@@ -138,6 +138,39 @@ __device__ __forceinline__ u128 aes_keyed(const AesT<C>& a, u128 in, const uint3
            ((static_cast<uint64_t>(bswap32(o1)) << 32) | bswap32(o0));
 }
 
+// two independent blocks under the PRG key, rounds interleaved (twice the LDS-read ILP of one lane)
+template <int C>
+__device__ __forceinline__ void aes_keyed2(const AesT<C>& a, u128 inA, u128 inB, const uint32_t* rk, u128& outA,
+                                           u128& outB) {
+    uint32_t a0 = bswap32(static_cast<uint32_t>(inA)) ^ rk[0], a1 = bswap32(static_cast<uint32_t>(inA >> 32)) ^ rk[1];
+    uint32_t a2 = bswap32(static_cast<uint32_t>(inA >> 64)) ^ rk[2], a3 = bswap32(static_cast<uint32_t>(inA >> 96)) ^ rk[3];
+    uint32_t b0 = bswap32(static_cast<uint32_t>(inB)) ^ rk[0], b1 = bswap32(static_cast<uint32_t>(inB >> 32)) ^ rk[1];
+    uint32_t b2 = bswap32(static_cast<uint32_t>(inB >> 64)) ^ rk[2], b3 = bswap32(static_cast<uint32_t>(inB >> 96)) ^ rk[3];
+#pragma unroll
+    for (int r = 1; r < 10; ++r) {
+        const uint32_t ta0 = aes_col(a, a0, a1, a2, a3, rk[4 * r + 0]);
+        const uint32_t tb0 = aes_col(a, b0, b1, b2, b3, rk[4 * r + 0]);
+        const uint32_t ta1 = aes_col(a, a1, a2, a3, a0, rk[4 * r + 1]);
+        const uint32_t tb1 = aes_col(a, b1, b2, b3, b0, rk[4 * r + 1]);
+        const uint32_t ta2 = aes_col(a, a2, a3, a0, a1, rk[4 * r + 2]);
+        const uint32_t tb2 = aes_col(a, b2, b3, b0, b1, rk[4 * r + 2]);
+        const uint32_t ta3 = aes_col(a, a3, a0, a1, a2, rk[4 * r + 3]);
+        const uint32_t tb3 = aes_col(a, b3, b0, b1, b2, rk[4 * r + 3]);
+        a0 = ta0; a1 = ta1; a2 = ta2; a3 = ta3;
+        b0 = tb0; b1 = tb1; b2 = tb2; b3 = tb3;
+    }
+    auto fin = [&](uint32_t s0, uint32_t s1, uint32_t s2, uint32_t s3) -> u128 {
+        const uint32_t o0 = aes_last(a, s0, s1, s2, s3, rk[40]);
+        const uint32_t o1 = aes_last(a, s1, s2, s3, s0, rk[41]);
+        const uint32_t o2 = aes_last(a, s2, s3, s0, s1, rk[42]);
+        const uint32_t o3 = aes_last(a, s3, s0, s1, s2, rk[43]);
+        return (static_cast<u128>((static_cast<uint64_t>(bswap32(o3)) << 32) | bswap32(o2)) << 64) |
+               ((static_cast<uint64_t>(bswap32(o1)) << 32) | bswap32(o0));
+    };
+    outA = fin(a0, a1, a2, a3);
+    outB = fin(b0, b1, b2, b3);
+}
+
 __device__ __forceinline__ uint64_t stream_of(uint64_t layer, uint64_t slot, uint64_t e, uint64_t mask) {
     return ((layer << 44) ^ (slot << 36) ^ e) ^ mask;
 }
@@ -260,6 +293,10 @@ __device__ __forceinline__ Proj rfl_proj(const Proj& p) {
 // digits of the block (DigitStream). Components are gathered 8 at a time in a
 // 128-bit shift register and stored as 16-byte chunks: one coalesced KiB per
 // wave per chunk, and chunk padding past n is written as zeros.
+#ifndef DASH_GG_DRAW_PAIRS
+#define DASH_GG_DRAW_PAIRS 1  // A/B knob: a label's AES-CTR blocks computed up front, two interleaved (0: one by one)
+#endif
+constexpr bool kDrawPairs = DASH_GG_DRAW_PAIRS != 0;
 template <int C>
 __global__ __launch_bounds__(kGB) void k_draw(Ctx c, Gadget g) {
     __shared__ __attribute__((aligned(16))) uint32_t lds_aes[aes_lds_words<C>()];
@@ -286,9 +323,20 @@ __global__ __launch_bounds__(kGB) void k_draw(Ctx c, Gadget g) {
         DigitStream ds;
         u128 acc = 0;  // pending components, the oldest in the low 16 bits once 8 are in
         int blk = 0, left = 0;
+        // the label's AES-CTR blocks up front (<= 3: q^pm <= 2^64 and q^n <= 2^128), two interleaved at a time
+        const int nb = (n + pm - 1) / pm;
+        const u128 base = static_cast<u128>(stream) << 64;
+        u128 B[3];
+        if (kDrawPairs && nb >= 2) {
+            aes_keyed2(aes, base | static_cast<uint64_t>(d.ctr), base | static_cast<uint64_t>(d.ctr + 1), c.rk, B[0], B[1]);
+            if (nb >= 3) B[2] = aes_keyed(aes, base | static_cast<uint64_t>(d.ctr + 2), c.rk);
+        } else if (kDrawPairs) {
+            B[0] = aes_keyed(aes, base | static_cast<uint64_t>(d.ctr), c.rk);
+        }
         for (int q = 0; q < n; ++q) {
             if (left == 0) {
-                ds.init(aes_keyed(aes, (static_cast<u128>(stream) << 64) | static_cast<uint64_t>(d.ctr + blk), c.rk));
+                if (kDrawPairs && nb <= 3) ds.init(blk == 0 ? B[0] : (blk == 1 ? B[1] : B[2]));
+                else ds.init(aes_keyed(aes, base | static_cast<uint64_t>(d.ctr + blk), c.rk));
                 ++blk;
                 left = pm;
             }
@@ -624,6 +672,87 @@ __device__ __forceinline__ u128 compress_xa(LRef x, const uint32_t* a, const Mod
     return m.bits ? compress_xa_t<true>(x, a, m, d0) : compress_xa_t<false>(x, a, m, d0);
 }
 
+// Two keys of one label x with two uniform rows a1, a2 (two entry indices): x is read once, and the two
+// Horner chains (and the two AES blocks that follow) are independent work for the same lane.
+template <bool PW2>
+__device__ __forceinline__ void compress_xa2_t(LRef x, const uint32_t* a1, const uint32_t* a2, const ModC& m, u128& C1,
+                                               u128& C2, uint32_t& d01, uint32_t& d02) {
+    const int nc = static_cast<int>(chunks_of(static_cast<int>(m.n)));
+    const uint32_t q = m.q, b = m.bits;
+    int g = 1;
+    uint32_t D = q;
+    if (PW2) {
+        g = static_cast<int>(24 / b);
+        D = 1u << (b * g);
+    } else {
+        while (static_cast<uint64_t>(D) * q <= (1u << 24)) {
+            D *= q;
+            ++g;
+        }
+    }
+    const u16x2 qq = {static_cast<unsigned short>(q), static_cast<unsigned short>(q)};
+    const u16x2 msk = {static_cast<unsigned short>(q - 1), static_cast<unsigned short>(q - 1)};
+    C1 = 0;
+    C2 = 0;
+    uint32_t v1 = 0, v2 = 0;
+    int r = (8 * nc - 1) % g;
+    uint32_t l1 = 0, l2 = 0;
+    constexpr int kL2 = 2;  // chunks in flight per round trip (x plus two rows each)
+    for (int c0 = nc - 1; c0 >= 0; c0 -= kL2) {
+        u32x4a xv[kL2], av[kL2], bv[kL2];
+#pragma unroll
+        for (int h = 0; h < kL2; ++h) {
+            if (c0 - h >= 0) {
+                xv[h] = ld_chunk(x, c0 - h);
+                av[h] = *reinterpret_cast<const u32x4a*>(a1 + 4 * (c0 - h));
+                bv[h] = *reinterpret_cast<const u32x4a*>(a2 + 4 * (c0 - h));
+            }
+        }
+#pragma unroll
+        for (int h = 0; h < kL2; ++h) {
+            if (c0 - h < 0) break;
+            uint32_t t1[4], t2[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const u16x2 s1 = as_u16x2(xv[h][u]) + as_u16x2(av[h][u]);
+                const u16x2 s2 = as_u16x2(xv[h][u]) + as_u16x2(bv[h][u]);
+                t1[u] = PW2 ? as_u32(s1 & msk) : as_u32(__builtin_elementwise_min(s1, s1 - qq));
+                t2[u] = PW2 ? as_u32(s2 & msk) : as_u32(__builtin_elementwise_min(s2, s2 - qq));
+            }
+            const int qb = 8 * (c0 - h);
+#pragma unroll
+            for (int k = 7; k >= 0; --k) {
+                const bool pad = qb + k >= static_cast<int>(m.n);
+                const uint32_t e1 = pad ? 0u : ((k & 1) ? (t1[k >> 1] >> 16) : (t1[k >> 1] & 0xffffu));
+                const uint32_t e2 = pad ? 0u : ((k & 1) ? (t2[k >> 1] >> 16) : (t2[k >> 1] & 0xffffu));
+                v1 = PW2 ? ((v1 << b) | e1) : __umul24(v1, q) + e1;
+                v2 = PW2 ? ((v2 << b) | e2) : __umul24(v2, q) + e2;
+                if (r == 0) {
+                    C1 = mad128_24(C1, D, v1);
+                    C2 = mad128_24(C2, D, v2);
+                    v1 = v2 = 0;
+                    r = g - 1;
+                } else {
+                    --r;
+                }
+            }
+            l1 = t1[0] & 0xffffu;
+            l2 = t2[0] & 0xffffu;
+        }
+    }
+    d01 = l1;
+    d02 = l2;
+}
+__device__ __forceinline__ void compress_xa2(LRef x, const uint32_t* a1, const uint32_t* a2, const ModC& m, u128& C1,
+                                             u128& C2, uint32_t& d01, uint32_t& d02) {
+    if (m.bits) compress_xa2_t<true>(x, a1, a2, m, C1, C2, d01, d02);
+    else compress_xa2_t<false>(x, a1, a2, m, C1, C2, d01, d02);
+}
+
+#ifndef DASH_GG_HASH_PAIRS
+#define DASH_GG_HASH_PAIRS 1  // A/B knob: two entry indices per k_hash_iu step (0: one)
+#endif
+constexpr bool kHashPairs = DASH_GG_HASH_PAIRS != 0;
 // Key hashes with the entry index i uniform across the wave (one wave per (64-element tile, hash job), a job =
 // up to kHJ consecutive i of one projection): key = x + i R_pin, i.e. digits x_q + (i R_q mod p) with the
 // multiple row iR[pin][i] read from scalar memory; the key's color (digit 0, R_0 = 1) places the hash:
@@ -652,7 +781,24 @@ __global__ __launch_bounds__(kPB, 4) void k_hash_iu(Ctx c, Gadget g, In in, cons
         const LRef x = label_ref(c, g, in, e, P.in_kind, P.in_idx, P.pin);
         const int words = 4 * static_cast<int>(chunks_of(static_cast<int>(mi.n)));
         const uint32_t* rows = c.iR[P.pin];
-        for (int i = c0; i < c1; ++i) {
+        int i = c0;
+        if (kHashPairs) {
+            // two entry indices per step: one pass over x, two interleaved AES blocks (twice the LDS-read ILP)
+            for (; i + 1 < c1; i += 2) {
+                u128 k1, k2, H1, H2;
+                uint32_t col1, col2;
+                compress_xa2(x, rows + static_cast<int64_t>(i) * words, rows + static_cast<int64_t>(i + 1) * words, mi,
+                             k1, k2, col1, col2);
+                aes_encrypt2(aes, k1, k2, H1, H2);
+                if (e_raw < N) {
+                    g.HC[(P.first + col1) * N + e] = H1;
+                    g.CC[(P.first + col1) * N + e] = static_cast<uint16_t>(i);
+                    g.HC[(P.first + col2) * N + e] = H2;
+                    g.CC[(P.first + col2) * N + e] = static_cast<uint16_t>(i + 1);
+                }
+            }
+        }
+        for (; i < c1; ++i) {
             uint32_t col;
             const u128 key = compress_xa(x, rows + static_cast<int64_t>(i) * words, mi, col);
             const u128 H = aes_encrypt(aes, key);
@@ -776,10 +922,35 @@ struct Emit {
 
 // Bank payloads: one wave per (64-element tile, bank row), lanes = consecutive elements (the row's slot,
 // modulus and offset kind are wave-uniform): BK[row][N] = slot label + v * offset (mod pout), compressed.
-__global__ __launch_bounds__(256) void k_bank(Ctx c, Gadget g, In in, const BankRow* rows, int nrows) {
+__device__ __forceinline__ u128 bank_payload(const Ctx& c, const Gadget& g, const In& in, const BankRow* rows, int row,
+                                             int64_t e) {
+    const int slot = rfl(rows[row].slot), pout = rfl(rows[row].pout), res = rfl(rows[row].res);
+    uint32_t f = rflu(static_cast<uint32_t>(rows[row].v));
+    const ModC mo = rfl_modc(c.mc[pout]);
+    if (res < 0 && c.iR != nullptr && c.iR[pout] != nullptr) {
+        // uniform offset v R_pout: its multiple row (compress_xa)
+        const int words = 4 * static_cast<int>(chunks_of(static_cast<int>(mo.n)));
+        uint32_t d0;
+        return compress_xa(slot_ref(g, slot, e), c.iR[pout] + static_cast<int64_t>(f) * words, mo, d0);
+    }
+    CompressFwd pc;
+    pc.init();
+    if (res < 0) push_lin<true, false>(pc, slot_ref(g, slot, e), row_ref(c.R + static_cast<int64_t>(pout) * kW), f, mo);
+    else push_lin<false, false>(pc, slot_ref(g, slot, e), LRef{in.p[res] + e * in.es[res], in.cs[res]}, f, mo);
+    return pc.finish();
+}
+
+// Bank payloads: one wave per (64-element tile, bank job), lanes = consecutive elements (the rows' slot,
+// modulus and offset kind are wave-uniform): BK[row][N] = slot label + v * offset (mod pout), compressed. A job
+// is one row or two rows of the same slot label and R offset (two values v): the label is read once for both.
+struct BankJob {
+    int r0, r1;  // r1 < 0: a single row
+};
+__global__ __launch_bounds__(256) void k_bank(Ctx c, Gadget g, In in, const BankRow* rows, const BankJob* jobs,
+                                              int njobs) {
     const int64_t N = g.N;
     const int64_t tiles = (N + kTile - 1) / kTile;
-    const int64_t nw = tiles * nrows;
+    const int64_t nw = tiles * njobs;
     const int lane = static_cast<int>(threadIdx.x) & (kTile - 1);
     const int64_t wpb = 256 / kTile;
     const int64_t w0 = static_cast<int64_t>(blockIdx.x) * wpb + rfl(static_cast<int>(threadIdx.x) / kTile);
@@ -787,27 +958,29 @@ __global__ __launch_bounds__(256) void k_bank(Ctx c, Gadget g, In in, const Bank
     for (int64_t w = w0; w < nw; w += wstep) {
         // tile-major: the rows of one slot label (a target's values) run in neighbouring waves, so the label's
         // re-reads hit L2 (row-major order re-fetched it from HBM for every value)
-        const int64_t tile = w / nrows;
-        const int row = static_cast<int>(w - tile * nrows);
-        const int slot = rfl(rows[row].slot), pout = rfl(rows[row].pout), res = rfl(rows[row].res);
-        uint32_t f = rflu(static_cast<uint32_t>(rows[row].v));
-        const ModC mo = rfl_modc(c.mc[pout]);
+        const int64_t tile = w / njobs;
+        const int jb = static_cast<int>(w - tile * njobs);
+        const int r0 = rfl(jobs[jb].r0), r1 = rfl(jobs[jb].r1);
         const int64_t e_raw = tile * kTile + lane;
         const int64_t e = e_raw < N ? e_raw : N - 1;
-        u128 P;
-        if (res < 0 && c.iR != nullptr && c.iR[pout] != nullptr) {
-            // uniform offset v R_pout: its multiple row from scalar memory (compress_xa)
+        if (r1 >= 0) {  // (host-checked: same slot, same modulus, R offsets, multiple rows present)
+            const int slot = rfl(rows[r0].slot), pout = rfl(rows[r0].pout);
+            const uint32_t f0 = rflu(static_cast<uint32_t>(rows[r0].v)), f1 = rflu(static_cast<uint32_t>(rows[r1].v));
+            const ModC mo = rfl_modc(c.mc[pout]);
             const int words = 4 * static_cast<int>(chunks_of(static_cast<int>(mo.n)));
-            uint32_t d0;
-            P = compress_xa(slot_ref(g, slot, e), c.iR[pout] + static_cast<int64_t>(f) * words, mo, d0);
+            const uint32_t* rp = c.iR[pout];
+            u128 P0, P1;
+            uint32_t d0, d1;
+            compress_xa2(slot_ref(g, slot, e), rp + static_cast<int64_t>(f0) * words, rp + static_cast<int64_t>(f1) * words,
+                         mo, P0, P1, d0, d1);
+            if (e_raw < N) {
+                g.BK[static_cast<int64_t>(r0) * N + e] = P0;
+                g.BK[static_cast<int64_t>(r1) * N + e] = P1;
+            }
         } else {
-            CompressFwd pc;
-            pc.init();
-            if (res < 0) push_lin<true, false>(pc, slot_ref(g, slot, e), row_ref(c.R + static_cast<int64_t>(pout) * kW), f, mo);
-            else push_lin<false, false>(pc, slot_ref(g, slot, e), LRef{in.p[res] + e * in.es[res], in.cs[res]}, f, mo);
-            P = pc.finish();
+            const u128 P = bank_payload(c, g, in, rows, r0, e);
+            if (e_raw < N) g.BK[static_cast<int64_t>(r0) * N + e] = P;
         }
-        if (e_raw < N) g.BK[static_cast<int64_t>(row) * N + e] = P;
     }
 }
 
@@ -1984,8 +2157,24 @@ void project(const gg::Ctx& c, gg::Gadget& g, const gg::In& in, const gg::Tables
     // (rejected, profiles/ab/README.md: one block per label group with the label staged in LDS, 7.2 -> 7.6-8.2 ms
     // per 4 GCs, and one wave per group stepping packed-byte payloads o + v*off incrementally, 10.7 ms)
     if (!rows.empty()) {
-        hipLaunchKernelGGL(gg::k_bank, dim3(blocks_for(lanes * static_cast<int64_t>(rows.size()), 256, 32768)), dim3(256), 0,
-                           gg::tl_st, cc, g, in, em.rows, static_cast<int>(rows.size()));
+        // bank jobs: neighbouring rows of one slot label with R offsets pair up (one label read, two payloads)
+        std::vector<gg::BankJob> bj;
+        const bool pairs = gg::gg_hash_mode() == 2;
+        for (size_t r = 0; r < rows.size(); ++r) {
+            const auto& a = rows[r];
+            if (pairs && r + 1 < rows.size()) {
+                const auto& b = rows[r + 1];
+                if (a.res < 0 && b.res < 0 && a.slot == b.slot && a.pout == b.pout && a.pout < 32768) {
+                    bj.push_back(gg::BankJob{static_cast<int>(r), static_cast<int>(r + 1)});
+                    ++r;
+                    continue;
+                }
+            }
+            bj.push_back(gg::BankJob{static_cast<int>(r), -1});
+        }
+        const gg::BankJob* dbj = gg::dconst(bj.data(), bj.size());
+        hipLaunchKernelGGL(gg::k_bank, dim3(blocks_for(lanes * static_cast<int64_t>(bj.size()), 256, 32768)), dim3(256), 0,
+                           gg::tl_st, cc, g, in, em.rows, dbj, static_cast<int>(bj.size()));
     }
     if (iu) {
         std::vector<gg::HashJob> hj;
