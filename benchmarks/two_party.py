@@ -19,6 +19,12 @@ by the evaluator. Per (model config, split) one JSON line:
   online_bytes_per_inference, served_inf_per_s (fresh GC per inference, offline + online wall time),
   verified (decoded == plaintext).
 
+The offline message travels over the TCP channel (``--transport tcp``, any host) or through a ring of shared-memory
+segments of this host (``shm``, the same-host split of the reference's enclave: the channel then carries only the
+segment names and the evaluator's acknowledgements). The circuit is range-calibrated first, so the default
+("auto") constructions are the headline's (mixed-radix rescale, joint ReLU) where the ranges allow; the record
+names the resolved ones.
+
 On a one-GPU lease both parties share device 0: the numbers are a performance rehearsal of the split, not a
 trust-valid deployment (the record says so). The ``--splits`` list may name either or both.
 
@@ -28,6 +34,7 @@ trust-valid deployment (the record says so). The ``--splits`` list may name eith
 from __future__ import annotations
 
 import argparse
+import itertools
 import json
 import multiprocessing as mp
 import os
@@ -84,7 +91,8 @@ def run_tcp(circuit, cfg, xs, args) -> dict:
     ok = True
     try:
         with GarblerClient("127.0.0.1", port, circuit, crt, mrs, batch=args.batch, max_modulus=mm,
-                           seed=os.urandom(16), device=dev, pipeline=not args.no_pipeline) as cl:
+                           seed=os.urandom(16), device=dev, pipeline=not args.no_pipeline,
+                           transport=args._transport) as cl:
             for r in range(args.rounds + 1):  # round 0 warms up (evaluator build, graph capture)
                 batch = xs[(r % 4) * args.batch:(r % 4 + 1) * args.batch]
                 t0 = time.perf_counter()
@@ -127,7 +135,7 @@ def run_enclave(circuit, cfg, xs, args) -> dict:
         at.platform_key(key)
         with GarblerEnclave(circuit, crt, mrs, max_modulus=mm, batch=args.batch, backend=args.backend,
                             device=args.device, platform_key_file=key, garble_device=dev,
-                            client_kw={"pipeline": not args.no_pipeline}) as enc:
+                            client_kw={"pipeline": not args.no_pipeline, "transport": args._transport}) as enc:
             warm = xs[:args.batch]
             y0 = enc.ann_infer(warm)
             ok = all(np.array_equal(y, _plain(circuit, crt, mrs, x)) for x, y in zip(warm, y0))
@@ -159,6 +167,8 @@ def main(argv=None):
     ap.add_argument("--batch", type=int, default=4, help="GCs per offline/online round")
     ap.add_argument("--rounds", type=int, default=4, help="timed rounds (after one warm-up round)")
     ap.add_argument("--no-pipeline", action="store_true")
+    ap.add_argument("--transport", default="tcp,shm",
+                    help="offline-message transports to measure per split: tcp (any host) and/or shm (same host)")
     ap.add_argument("--out", default=None, help="also append the JSON lines to this file")
     args = ap.parse_args(argv)
     if args.backend == "cpu":
@@ -171,10 +181,21 @@ def main(argv=None):
         circuit = load_circuit(cfg, None)
         imgs = synthetic_inputs(cfg.model_name, 4 * args.batch, seed=3)
         xs = quantize_images(cfg, circuit, imgs)
-        for split in args.splits.split(","):
+        # range calibration (as the headline bench): lets the "auto" constructions pick the mixed-radix
+        # rescale + joint ReLU where the tracked ranges allow (GarbledCircuit defaults)
+        cal = quantize_images(cfg, circuit, synthetic_inputs(cfg.model_name, 32, seed=0))
+        crt0, _, _ = _gc_args(cfg)
+        from dash_amd.garbling.gc import GarbledCircuit as _GC
+
+        M = _GC(circuit, crt0, _gc_args(cfg)[1], garble_me=False).crt_modulus
+        circuit.calibrate(cal, M)
+        cons = _GC(circuit, crt0, _gc_args(cfg)[1], garble_me=False).effective_constructions()
+        for split, tr in itertools.product(args.splits.split(","), args.transport.split(",")):
+            args._transport = tr
             t = time.perf_counter()
             r = (run_tcp if split == "tcp" else run_enclave)(circuit, cfg, xs, args)
-            rec = dict(bench="two_party", model=name, split=split, backend=args.backend,
+            rec = dict(bench="two_party", model=name, split=split, transport=tr, constructions=cons,
+                       backend=args.backend,
                        garbler=("gpu%d" % args.garble_device) if args.garble_device >= 0 else "cpu",
                        evaluator=f"{args.backend}{args.device if args.backend == 'hip' else ''}", batch=args.batch,
                        rounds=args.rounds, pipeline=not args.no_pipeline,

@@ -3,6 +3,9 @@
 Messages (tags):
   HELO  client -> server  JSON {"version", "batch"};   server -> client JSON {"backend", "device"}
   MODL  client -> server  flags = slot, payload = GarbledModel.serialize()      (offline)
+  MODS  client -> server  flags = slot, payload = JSON {"name", "size"}: the same offline message in a shared
+                          memory segment of the garbler's ring (same-host split; the evaluator ACKs once it has
+                          loaded it, after which the garbler reuses the segment)
   INPT  client -> server  flags = n, payload = n x (k, N, 2) uint64 compressed input labels   (online #1)
   OUTP  server -> client  payload = n x (k, n_out, 2) uint64 compressed output labels          (online #2)
   BYE_  either side
@@ -18,6 +21,7 @@ per inference is exactly input_size*k*16 B + n_out*k*16 B plus framing, the
 from __future__ import annotations
 
 import json
+import os
 import time
 from typing import Optional, Sequence
 
@@ -45,6 +49,32 @@ class EvaluatorServer:
         self.ev = None
         self.batch = 1
         self.rounds = 0
+        self._close_shm()
+
+    def _close_shm(self):
+        for mm in getattr(self, "_shm", {}).values():
+            try:
+                mm.close()
+            except (OSError, BufferError):
+                pass
+        self._shm: dict = {}
+
+    def _segment(self, name: str):
+        """Read-only map of the garbler's POSIX shared-memory segment (its owner creates and unlinks it; mapped
+        directly so that no resource tracker of this process claims it)."""
+        mm = self._shm.get(name)
+        if mm is None:
+            import mmap
+
+            if "/" in name.strip("/") or not name.strip("/"):
+                raise ValueError("bad shared-memory segment name")
+            fd = os.open("/dev/shm/" + name.strip("/"), os.O_RDONLY)
+            try:
+                mm = mmap.mmap(fd, 0, prot=mmap.PROT_READ)
+            finally:
+                os.close(fd)
+            self._shm[name] = mm
+        return mm
 
     def serve(self, ch: Channel) -> None:
         n = native()
@@ -62,11 +92,23 @@ class EvaluatorServer:
                         self._reset()
                         self.batch = int(hello.get("batch", 1))
                         ch.send(b"HELO", json.dumps({"backend": self.backend, "device": self.device}).encode())
-                    elif tag == b"MODL":
+                    elif tag in (b"MODL", b"MODS"):
                         slot = flags
                         if not 0 <= slot < self.batch:
                             raise ValueError(f"slot {slot} out of range")
-                        m = n.GarbledModel.deserialize_buffer(buf)  # parsed in place, no bytes() copy
+                        if tag == b"MODL":
+                            m = n.GarbledModel.deserialize_buffer(buf)  # parsed in place, no bytes() copy
+                        else:
+                            ref = json.loads(buf.decode())
+                            seg = self._segment(str(ref["name"]))
+                            size = int(ref["size"])
+                            if not 0 < size <= len(seg):
+                                raise ValueError("shared-memory model size out of range")
+                            view = memoryview(seg)[:size]
+                            try:
+                                m = n.GarbledModel.deserialize_buffer(view)
+                            finally:
+                                view.release()
                         del buf
                         if self.backend == "hip":
                             from ..runtime import HipEvaluator
@@ -81,12 +123,14 @@ class EvaluatorServer:
                     elif tag == b"INPT":
                         ch.send(b"OUTP", self._round(flags, buf))
                     elif tag == b"BYE_":
+                        self._close_shm()
                         return
                     else:
                         raise ValueError(f"unknown message {tag!r}")
                 except Exception as e:  # report every failure to the peer, keep serving
                     ch.send(b"ERR!", f"{type(e).__name__}: {e}".encode())
         finally:
+            self._close_shm()
             ch.close()
 
     def _round(self, nb: int, buf: bytearray) -> bytes:
@@ -145,10 +189,17 @@ class GarblerClient:
 
     def __init__(self, host: str, port: int, circuit, crt, mrs=None, batch: int = 1, max_modulus: int = 0,
                  seed: Optional[bytes] = None, timeout: float = 600.0, device: Optional[int] = None,
-                 pipeline: bool = True, **gc_kw):
+                 pipeline: bool = True, transport: str = "tcp", **gc_kw):
+        """transport: "tcp" ships the offline message over the channel (any host); "shm" writes it into a ring
+        of shared-memory segments of this host and sends only their names (same-host split, e.g. the trusted
+        garbler beside its evaluator); online messages always use the channel."""
+        if transport not in ("tcp", "shm"):
+            raise ValueError("transport must be 'tcp' or 'shm'")
         self.circuit, self.crt, self.mrs = circuit, crt, mrs
         self.batch, self.max_modulus = batch, max_modulus
         self.device, self.pipeline, self.gc_kw = device, pipeline, gc_kw
+        self.transport = transport
+        self._ring: list = []  # shared-memory segments (shm transport)
         self._seed = seed
         self._ctr = 0
         self.ch = connect(host, port, timeout=timeout)
@@ -189,11 +240,118 @@ class GarblerClient:
         t2 = time.perf_counter()
         return gc, buf, n, t1 - t, t2 - t1
 
+    # ---- shared-memory ring (transport="shm")
+    _RING = 3
+
+    def _ring_ensure(self, size: int) -> None:
+        from multiprocessing import shared_memory
+
+        if self._ring and self._ring[0].size >= size:
+            return
+        self._ring_close()
+        self._ring = [shared_memory.SharedMemory(create=True, size=size) for _ in range(self._RING)]
+
+    def _ring_close(self) -> None:
+        for seg in self._ring:
+            try:
+                seg.close()
+                seg.unlink()
+            except (OSError, BufferError):
+                pass
+        self._ring = []
+
+    def _offline_shm(self, seeds) -> None:
+        """Offline phase through the shared-memory ring: the producer garbles GC b + 1 and serializes it into a
+        free segment while GC b's segment is being loaded by the evaluator; a segment is reused after its ACK."""
+        import collections
+        import queue
+        import threading
+
+        first = self._garble_gc(seeds[0])
+        n = first.model.serialized_size()
+        self._ring_ensure(n)
+        free: "queue.Queue" = queue.Queue()
+        for i in range(len(self._ring)):
+            free.put(i)
+        ready: "queue.Queue" = queue.Queue()
+        err: list = []
+
+        def produce():
+            try:
+                for b in range(self.batch):
+                    gc = first if b == 0 else self._garble_gc(seeds[b])
+                    i = free.get()
+                    if i < 0:  # the sending side gave up
+                        return
+                    t = time.perf_counter()
+                    got = gc.model.serialize_into(np.ndarray((self._ring[i].size,), np.uint8, buffer=self._ring[i].buf))
+                    gc.model = None
+                    self.stats["serialize_s"] += time.perf_counter() - t
+                    ready.put((gc, i, got))
+            except BaseException as e:  # surfaced on the sending thread
+                err.append(e)
+                ready.put(None)
+
+        if not self.pipeline:  # one GC at a time: garble, serialize into segment 0, ship, wait for its ACK
+            for b in range(self.batch):
+                gc = first if b == 0 else self._garble_gc(seeds[b])
+                t = time.perf_counter()
+                got = gc.model.serialize_into(np.ndarray((self._ring[0].size,), np.uint8, buffer=self._ring[0].buf))
+                gc.model = None
+                self.stats["serialize_s"] += time.perf_counter() - t
+                self.ch.send(b"MODS", json.dumps({"name": self._ring[0].name, "size": got}).encode(), flags=b)
+                self.stats["offline_bytes"] += got
+                self.ch.recv(b"ACK_")
+                self.gcs.append(gc)
+            return
+        th = threading.Thread(target=produce, name="dash-garbler", daemon=True)
+        th.start()
+        pending: "collections.deque" = collections.deque()
+        try:
+            for b in range(self.batch):
+                item = ready.get()
+                if item is None:
+                    raise err[0]
+                gc, i, got = item
+                self.ch.send(b"MODS", json.dumps({"name": self._ring[i].name, "size": got}).encode(), flags=b)
+                self.stats["offline_bytes"] += got  # the offline message (in the segment) + its frame below
+                pending.append(i)
+                self.gcs.append(gc)
+                if len(pending) >= len(self._ring):
+                    self.ch.recv(b"ACK_")
+                    free.put(pending.popleft())
+            while pending:
+                self.ch.recv(b"ACK_")
+                free.put(pending.popleft())
+        finally:
+            for _ in range(len(self._ring)):  # unblock a producer waiting for a segment if sending failed
+                free.put(-1)
+            th.join()
+
+    def _garble_gc(self, seed):
+        from ..garbling import GarbledCircuit
+
+        t = time.perf_counter()
+        gc = GarbledCircuit(self.circuit, self.crt, self.mrs, max_modulus=self.max_modulus, seed=seed,
+                            device=self.device, **self.gc_kw)
+        self.stats["garble_s"] += time.perf_counter() - t
+        return gc
+
     def offline(self) -> None:
         """Garble `batch` fresh circuits and ship them (offline phase)."""
         import queue
         import threading
 
+        if self.transport == "shm":
+            t0 = time.perf_counter()
+            sent0 = self.ch.bytes_sent
+            seeds = [self._next_seed() for _ in range(self.batch)]
+            self.gcs = []
+            self._offline_shm(seeds)
+            self.stats["gcs"] += self.batch
+            self.stats["offline_bytes"] += self.ch.bytes_sent - sent0
+            self.stats["offline_s"] += time.perf_counter() - t0
+            return
         t0 = time.perf_counter()
         sent0 = self.ch.bytes_sent
         seeds = [self._next_seed() for _ in range(self.batch)]
@@ -267,6 +425,7 @@ class GarblerClient:
         except OSError:
             pass
         self.ch.close()
+        self._ring_close()
 
     def __enter__(self):
         return self

@@ -198,11 +198,12 @@ class GarblerEnclave:
 
         from . import attest as at
 
-        if self._key_file:
-            _os.environ.setdefault("DASH_PLATFORM_KEY_FILE", self._key_file)
+        # this enclave's platform key (explicit file, else the process default): an environment variable left by
+        # an earlier enclave of this process must not pick another platform's key
+        key = at.platform_key(self._key_file) if self._key_file else None
         nonce = nonce or _os.urandom(16)
         quote, _ = self._ecall("attest", nonce)
-        at.verify_quote(quote, at.measure(self._cfg), nonce)
+        at.verify_quote(quote, at.measure(self._cfg), nonce, key=key)
         self.quote = quote
         return quote
 

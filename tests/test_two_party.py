@@ -126,11 +126,35 @@ def test_two_party_benchmark_cpu():
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     sys.path.insert(0, os.path.join(root, "benchmarks"))  # importable by name in the spawned server too
     import two_party as tp
-    recs = tp.main(["--backend", "cpu", "--models", "MODEL_A/SIMPLE", "--batch", "2", "--rounds", "1"])
-    assert [r["split"] for r in recs] == ["tcp", "enclave"]
+    recs = tp.main(["--backend", "cpu", "--models", "MODEL_A/SIMPLE", "--batch", "2", "--rounds", "1",
+                    "--transport", "tcp,shm"])
+    assert [(r["split"], r["transport"]) for r in recs] == [("tcp", "tcp"), ("tcp", "shm"), ("enclave", "tcp"),
+                                                            ("enclave", "shm")]
     for r in recs:
         assert r["verified"] and r["offline_gb_per_gc"] > 0 and r["served_inf_per_s"] > 0
         assert r["online_bytes_per_inference"] > 0 and r["online_round_ms"] > 0
+
+
+def test_shm_transport_matches_tcp():
+    """The same-host shared-memory offline transport ships the same models: same seeds -> identical outputs,
+    serial and pipelined (the ring of 3 segments is reused after each ACK across 2 rounds of 4 GCs)."""
+    c = build_circuit("MODEL_A")
+    xs = quantized_inputs("MODEL_A", 4)
+    res = []
+    for transport, pipe in (("tcp", False), ("shm", False), ("shm", True)):
+        p, port = _start()
+        try:
+            with GarblerClient("127.0.0.1", port, c, 7, 100.0, batch=4, seed=b"s" * 16, pipeline=pipe,
+                               transport=transport) as cl:
+                outs = []
+                for _ in range(2):
+                    cl.offline()
+                    outs.append(np.stack(cl.infer(xs)))
+                res.append(np.stack(outs))
+        finally:
+            p.join(timeout=60)
+    np.testing.assert_array_equal(res[0], res[1])
+    np.testing.assert_array_equal(res[0], res[2])
 
 
 def test_pipelined_offline_matches_serial():
