@@ -790,11 +790,11 @@ __global__ __launch_bounds__(kPB, 4) void k_hash_iu(Ctx c, Gadget g, In in, cons
                 compress_xa2(x, rows + static_cast<int64_t>(i) * words, rows + static_cast<int64_t>(i + 1) * words, mi,
                              k1, k2, col1, col2);
                 aes_encrypt2(aes, k1, k2, H1, H2);
-                if (e_raw < N) {
-                    g.HC[(P.first + col1) * N + e] = H1;
-                    g.CC[(P.first + col1) * N + e] = static_cast<uint16_t>(i);
-                    g.HC[(P.first + col2) * N + e] = H2;
-                    g.CC[(P.first + col2) * N + e] = static_cast<uint16_t>(i + 1);
+                if (e_raw < N) {  // rows by entry index (coalesced); CC = color - i (k_emit inverts in LDS)
+                    g.HC[(P.first + i) * N + e] = H1;
+                    g.CC[(P.first + i) * N + e] = static_cast<uint16_t>(static_cast<int>(col1) - i);
+                    g.HC[(P.first + i + 1) * N + e] = H2;
+                    g.CC[(P.first + i + 1) * N + e] = static_cast<uint16_t>(static_cast<int>(col2) - (i + 1));
                 }
             }
         }
@@ -803,8 +803,8 @@ __global__ __launch_bounds__(kPB, 4) void k_hash_iu(Ctx c, Gadget g, In in, cons
             const u128 key = compress_xa(x, rows + static_cast<int64_t>(i) * words, mi, col);
             const u128 H = aes_encrypt(aes, key);
             if (e_raw < N) {
-                g.HC[(P.first + col) * N + e] = H;
-                g.CC[(P.first + col) * N + e] = static_cast<uint16_t>(i);
+                g.HC[(P.first + i) * N + e] = H;
+                g.CC[(P.first + i) * N + e] = static_cast<uint16_t>(static_cast<int>(col) - i);
             }
         }
     }
@@ -910,6 +910,7 @@ struct Scope {
     int64_t blk0;    // first block of the scope
 };
 struct Emit {
+    int by_i;  // key hashes stored by entry index i with CC = color - i (k_hash_iu); else by color with CC = i
     const Scope* sc;
     int nsc, nep;
     int64_t blocks;
@@ -1008,7 +1009,9 @@ __global__ __launch_bounds__(kEB) void k_emit(Ctx c, Gadget g, In in, Tables tb,
         u128* HCL = reinterpret_cast<u128*>(dyn);
         u128* PBL = HCL + ne * te1;
         uint16_t* CCL = reinterpret_cast<uint16_t*>(PBL + nb * te1);
-        uint32_t* MAP = reinterpret_cast<uint32_t*>(CCL + ((ne * te1 + 1) & ~1));
+        // by_i: IDX[color row][el] = the row of the entry index with that color (the inverse of CCL's deltas)
+        uint16_t* IDX = CCL + ((ne * te1 + 1) & ~1);
+        uint32_t* MAP = reinterpret_cast<uint32_t*>(IDX + (em.by_i ? ((ne * te1 + 1) & ~1) : 0));
         uint16_t* BIX = reinterpret_cast<uint16_t*>(MAP + span);
         const int table = rfl(S.table);
         // 1: the tile's key hashes, entry indices and bank payloads (coalesced rows of te elements, kUn loads in
@@ -1049,6 +1052,16 @@ __global__ __launch_bounds__(kEB) void k_emit(Ctx c, Gadget g, In in, Tables tb,
         for (int x = threadIdx.x; x < span; x += kEB) MAP[x] = gmap[x];
         for (int x = threadIdx.x; x < nbx; x += kEB) BIX[x] = em.bix[bx0 + x];
         __syncthreads();
+        if (em.by_i) {
+            // the colors of a projection's keys are a permutation of its entry indices: invert in LDS,
+            // IDX[row of color c][el] = row of the entry index whose key has color c (delta = c - i)
+            for (int x = threadIdx.x; x < nh; x += kEB) {
+                const int rr = x >> tsh, el = x & (te - 1);
+                const int delta = static_cast<int16_t>(CCL[rr * te1 + el]);
+                IDX[(rr + delta) * te1 + el] = static_cast<uint16_t>(rr);
+            }
+            __syncthreads();
+        }
         // 2: entries, position-fastest (contiguous per element), kUn independent LDS-only chains per thread
         u128* T = tb.t[table];
         const int64_t row = tb.row[table];
@@ -1072,8 +1085,14 @@ __global__ __launch_bounds__(kEB) void k_emit(Ctx c, Gadget g, In in, Tables tb,
             for (int u = 0; u < kUn; ++u) {
                 if (mm[u] == kHole) continue;
                 const EProj P = sep[mm[u] >> 24];
-                const int rr = P.first + static_cast<int>((mm[u] >> 12) & 0xfffu) - r0;
-                const int i = CCL[rr * te1 + el[u]];
+                int rr = P.first + static_cast<int>((mm[u] >> 12) & 0xfffu) - r0;  // the color's row
+                int i;
+                if (em.by_i) {
+                    rr = IDX[rr * te1 + el[u]];  // the entry index's row
+                    i = rr - (P.first - r0);
+                } else {
+                    i = CCL[rr * te1 + el[u]];
+                }
                 int br;
                 if (P.fn == F_MULR || P.fn == F_NEGR) {
                     const int64_t e = e0 + el[u];
@@ -1998,6 +2017,7 @@ void project(const gg::Ctx& c, gg::Gadget& g, const gg::In& in, const gg::Tables
         DASH_CHECK(p.fn != gg::F_FAN || (fx.flut && fx.fan), "gpu garbler: F_FAN projection without its values");
     }
     gg::Emit em{};
+    em.by_i = 0;
     // position maps
     std::vector<uint32_t> map;
     for (int t = 0; t < 8; ++t) {
@@ -2029,7 +2049,10 @@ void project(const gg::Ctx& c, gg::Gadget& g, const gg::In& in, const gg::Tables
     std::sort(order.begin(), order.end(), [&](int x, int y) {
         return std::tie(pr[x].table, pr[x].off) < std::tie(pr[y].table, pr[y].off);
     });
-    auto elem_bytes = [&](int64_t ne, int64_t nb) { return ne * (16 + 2) + nb * 16; };
+    const bool by_i = gg::gg_hash_mode() == 2 && !std::any_of(pr.begin(), pr.end(), [](const gg::Proj& p) {
+        return p.pin >= 32768;
+    });
+    auto elem_bytes = [&](int64_t ne, int64_t nb) { return ne * (16 + 2 + (by_i ? 2 : 0)) + nb * 16; };
     auto rows_bound = [&](const gg::Proj& p) {  // bank rows upper bound
         int64_t n = 0;
         for (int d = 0; d < targets(p); ++d) n += std::min<int64_t>(elem_dep(p) ? pout_of(p, d) : p.pin, pout_of(p, d));
@@ -2141,13 +2164,11 @@ void project(const gg::Ctx& c, gg::Gadget& g, const gg::In& in, const gg::Tables
     const int64_t lanes = (g.N + gg::kTile - 1) / gg::kTile * gg::kTile;
     // multiple rows of the projections' input moduli (uniform-i key hashes) and of the bank rows' R offsets
     gg::Ctx cc = c;
-    bool iu = gg::gg_hash_mode() == 2;
+    const bool iu = by_i;  // k_hash_iu writes the by-index layout k_emit then inverts
+    em.by_i = by_i ? 1 : 0;
     {
         std::vector<int> mods;
-        for (const auto& p : pr) {
-            mods.push_back(p.pin);
-            if (p.pin >= 32768) iu = false;
-        }
+        for (const auto& p : pr) mods.push_back(p.pin);
         for (const auto& r : rows)
             if (r.res < 0) mods.push_back(r.pout);
         std::sort(mods.begin(), mods.end());
