@@ -12,6 +12,7 @@
 //            fully in registers, no device malloc (reference uses new[]).
 //   phase C  one lane per (GC, residue, element): ReLU mixed-mod multiply, no
 //            AES at all (hashes come from phases A/B).
+#include <cmath>
 #include <cstdio>
 #include <cstdlib>
 
@@ -1024,6 +1025,203 @@ __global__ __launch_bounds__(kMrsBS, MODE == 2 ? DASH_CHAIN2_WAVES : DASH_UA_MIN
     }
 }
 
+// Latency form of the staged chain (small launches: batch 1). The per-lane form streams each position's label
+// from HBM (n / kMrsChunk dependent round trips per position) and passes the pair payloads P_{l,i} between
+// positions through HBM; at batch 1 a launch is one wave per SIMD, so every one of those round trips is
+// exposed (~0.17 ms per rescale whatever N is). Here a block owns kMrsWBS consecutive elements:
+//  * the label rows of EVERY residue come into LDS once, in one loop over all rows with kWaveU 16-byte loads in
+//    flight per thread, before the chain starts;
+//  * the positions read their components from LDS with no barrier;
+//  * the K(K-1)/2 pair payloads stay in registers (one wave per SIMD: the whole 512-VGPR file is the lane's).
+constexpr int kMrsWBS = 256;
+constexpr int kWaveU = 8;
+// one position of k_mrs_chain_w, I a compile-time constant (the pair payloads PS stay in registers)
+template <int K, int MODE, int I>
+__device__ __forceinline__ void chain_w_pos(const MrsArgs& a, const AesCtx& aes, const ModC* mc, const uint8_t* wst,
+                                            const int* roff, int tid, bool valid, const u128* row0, u128* PS,
+                                            u128& acc) {
+    constexpr int kLast = MODE >= 1 ? K - 1 : K;
+    if constexpr (I < kLast) {
+        constexpr int r = MODE >= 1 ? (I + 1) % K : I;
+        const ModC m = mc[a.crt.p[r]];
+        const int n = static_cast<int>(m.n);
+        const uint8_t* Ls = wst + roff[r] * kMrsWBS + tid;
+        uint32_t col = 0;
+        u128 key;
+        if (m.bits) {  // power-of-two modulus (uniform branch): per-digit streams
+            DigitStream ds[I > 0 ? I : 1];
+#pragma unroll
+            for (int l = 0; l < I; ++l) ds[l].init(PS[mrs_pair<K>(l, I)]);
+            CompressFwd cf;
+            cf.init();
+            for (int c = 0; c < n; ++c) {
+                uint32_t d = valid ? Ls[c * kMrsWBS] : 0u;
+#pragma unroll
+                for (int l = 0; l < I; ++l) {
+                    const uint32_t s = ds[l].next(m);
+                    d = d >= s ? d - s : d + m.q - s;
+                }
+                if (c == 0) col = d;
+                cf.push(d, m);
+            }
+            key = cf.finish();
+        } else {
+            // chunk-major walk: every stream shares the modulus, so one divmod per stream per chunk of m.c
+            // digits, then the chunk's digits with a wave-uniform trip count, one compress flush per chunk
+            // (the same digits and compress as DigitStream / CompressFwd, without their per-digit bookkeeping)
+            u128 Q[I > 0 ? I : 1];
+#pragma unroll
+            for (int l = 0; l < I; ++l) Q[l] = PS[mrs_pair<K>(l, I)];
+            u128 C = 0, PW = 1;
+            for (int c0 = 0; c0 < n; c0 += static_cast<int>(m.c)) {
+                uint32_t rr[I > 0 ? I : 1];
+#pragma unroll
+                for (int l = 0; l < I; ++l) rr[l] = divmod128(Q[l], m.D, m.mD);
+                const int cnt = min(static_cast<int>(m.c), n - c0);
+                uint32_t v = 0, pt = 1;
+                for (int t = 0; t < cnt; ++t) {
+                    uint32_t d = valid ? Ls[(c0 + t) * kMrsWBS] : 0u;
+#pragma unroll
+                    for (int l = 0; l < I; ++l) {
+                        const uint32_t quot = __umulhi(rr[l], m.dm) >> m.ds;
+                        const uint32_t sd = (rr[l] - __umul24(quot, m.q)) & 0xFFFFFFu;
+                        rr[l] = quot;
+                        d = d >= sd ? d - sd : d + m.q - sd;
+                    }
+                    if (c0 + t == 0) col = d;
+                    v += d * pt;
+                    pt *= m.q;
+                }
+                C += PW * static_cast<u128>(v);
+                PW *= static_cast<u128>(m.D);
+            }
+            key = C;
+        }
+        constexpr int kExtra = MODE == 1 ? 0 : 1;
+        constexpr int nt = K - 1 - I + kExtra;
+        const u128* row = row0 + a.dig_off[I] + static_cast<int64_t>(col) * nt;
+        u128 E[nt > 0 ? nt : 1];
+#pragma unroll
+        for (int t = 0; t < nt; ++t) E[t] = row[t];
+        const u128 H = aes_encrypt(aes, key);
+#pragma unroll
+        for (int t = 0; t < K - 1 - I; ++t) PS[mrs_pair<K>(I, I + 1 + t)] = E[t] - H;
+        if constexpr (MODE != 1) acc = add_packed(acc, E[K - 1 - I] - H, a.hmask);
+        chain_w_pos<K, MODE, I + 1>(a, aes, mc, wst, roff, tid, valid, row0, PS, acc);
+    }
+}
+
+template <int K, int MODE>
+__global__ __launch_bounds__(kMrsWBS, 1) void k_mrs_chain_w(MrsArgs a, Act x, const ModC* mc, const uint32_t* te0,
+                                                            const uint32_t* rk) {
+    AES_PROLOGUE(te0, rk);
+    extern __shared__ __attribute__((aligned(16))) uint8_t wst[];  // row g (residue r, component c) at g * kMrsWBS
+    const int b = blockIdx.z;
+    const int64_t N = a.N;
+    constexpr int NP = K * (K - 1) / 2 > 0 ? K * (K - 1) / 2 : 1;
+    const int tid = static_cast<int>(threadIdx.x);
+    int roff[K + 1];
+    const act_t* src[K];
+    roff[0] = 0;
+#pragma unroll
+    for (int r = 0; r < K; ++r) {
+        const int n = static_cast<int>(mc[a.crt.p[r]].n);
+        roff[r + 1] = roff[r] + n;
+        src[r] = x.p[r] + static_cast<int64_t>(b) * n * N;
+    }
+    const int units = roff[K] * (kMrsWBS / 16);
+    for (int64_t e0 = static_cast<int64_t>(blockIdx.x) * kMrsWBS; e0 < N; e0 += static_cast<int64_t>(gridDim.x) * kMrsWBS) {
+        __syncthreads();  // the previous tile's readers are done
+        for (int x0 = tid; x0 < units; x0 += kWaveU * kMrsWBS) {
+            uint4 v[kWaveU];
+#pragma unroll
+            for (int h = 0; h < kWaveU; ++h) {
+                const int xu = x0 + h * kMrsWBS;
+                const int g = xu >> 4;
+                const int64_t e = e0 + 16 * (xu & 15);
+                const act_t* row = src[0] + static_cast<int64_t>(g) * N;
+#pragma unroll
+                for (int r = 1; r < K; ++r)
+                    if (g >= roff[r]) row = src[r] + static_cast<int64_t>(g - roff[r]) * N;
+                if (xu < units && e < N) v[h] = *reinterpret_cast<const uint4*>(row + e);
+            }
+#pragma unroll
+            for (int h = 0; h < kWaveU; ++h) {
+                const int xu = x0 + h * kMrsWBS;
+                if (xu < units) *reinterpret_cast<uint4*>(wst + (xu >> 4) * kMrsWBS + 16 * (xu & 15)) = v[h];
+            }
+        }
+        __syncthreads();
+        const bool valid = e0 + tid < N;
+        const int64_t e = valid ? e0 + tid : N - 1;  // spare lanes shadow a real element, store nothing
+        const u128* row0 = a.tab + (static_cast<int64_t>(b) * N + e) * a.n_tab;
+        u128 PS[NP];
+        u128 acc = 0;
+        chain_w_pos<K, MODE, 0>(a, aes, mc, wst, roff, tid, valid, row0, PS, acc);
+        if (MODE >= 1) {
+            const ModC m = mc[a.crt.p[0]];
+            const int n = static_cast<int>(m.n);
+            const uint8_t* Ls = wst + tid;
+            CompressFwd cf;
+            cf.init();
+            for (int c = 0; c < n; ++c) cf.push(valid ? Ls[c * kMrsWBS] : 0u, m);
+            u128 key = cf.finish();
+#pragma unroll
+            for (int l = 0; l < K - 1; ++l) key ^= PS[mrs_pair<K>(l, K - 1)];
+            const uint32_t cb = static_cast<uint32_t>(key) & 1u;
+            u128 E = 0;
+            if (MODE == 2) E = row0[a.dig_off[K - 1] + cb];
+            const u128 H = aes_encrypt(aes, key);
+            if (valid) {
+                a.hs[static_cast<int64_t>(b) * N + e] = H;
+                a.cs[static_cast<int64_t>(b) * N + e] = static_cast<uint8_t>(cb);
+            }
+            if (MODE == 2) acc = add_packed(acc, E - H, a.hmask);
+        }
+        if (MODE == 1) continue;
+        const uint32_t colf = static_cast<uint32_t>(acc) & static_cast<uint32_t>(a.T - 1);
+        const u128* row = row0 + a.fin_off + static_cast<int64_t>(colf) * K;
+        u128 F[K];
+#pragma unroll
+        for (int j = 0; j < K; ++j) F[j] = row[j];
+        const u128 H = aes_encrypt(aes, acc);
+        if (valid) {
+#pragma unroll
+            for (int j = 0; j < K; ++j) a.pf[(static_cast<int64_t>(b) * K + j) * N + e] = F[j] - H;
+        }
+    }
+}
+
+// dynamic LDS of k_mrs_chain_w (every residue's rows for kMrsWBS elements), 0 when the form does not apply
+static inline size_t mrs_wave_lds(const MrsArgs& a, int B) {
+    static const bool on = [] {
+        const char* e = std::getenv("DASH_MRS_WAVE");
+        return !(e && e[0] == '0');
+    }();
+    // only launches of at most one block per CU: above that the per-lane form keeps more waves resident (24 GCs,
+    // MiniONN: 11.29 ms per step per-lane vs 11.56 with this form on every small-block launch)
+    if (!on || a.N % 16 != 0 || (a.N + kMrsWBS - 1) / kMrsWBS * B > num_cus()) return 0;
+    size_t sum = 0;
+    for (int r = 0; r < a.crt.k; ++r) sum += static_cast<size_t>(std::floor(128.0 / std::log2(static_cast<double>(a.crt.p[r]))));  // core.h nr_comps
+    const size_t bytes = sum * kMrsWBS;
+    if (bytes + static_cast<size_t>(DASH_AES_LDS_BYTES) > (160u << 10)) return 0;
+    return bytes;
+}
+
+// launches k_mrs_chain_w<K, MODE> with wl bytes of dynamic LDS (the per-kernel limit is raised once)
+template <int K, int MODE>
+static void launch_chain_w(const MrsArgs& a, const Act& x, int B, size_t wl, const ModC* mc, const AesGlobals& g,
+                           hipStream_t st) {
+    static const bool raised = [] {
+        return hipFuncSetAttribute(reinterpret_cast<const void*>(&k_mrs_chain_w<K, MODE>),
+                                   hipFuncAttributeMaxDynamicSharedMemorySize,
+                                   (160 << 10) - DASH_AES_LDS_BYTES) == hipSuccess;
+    }();
+    (void)raised;
+    const dim3 gw(static_cast<unsigned>((a.N + kMrsWBS - 1) / kMrsWBS), 1, B);
+    hipLaunchKernelGGL((k_mrs_chain_w<K, MODE>), gw, dim3(kMrsWBS), wl, st, a, x, mc, g.te0, g.rk);
+}
+
 // the staged chain holds two 512-lane blocks per CU: below two blocks per CU (batch-1 latency) the per-lane form,
 // whose block size shrinks to spread a small launch over every CU, is faster
 static inline bool mrs_staged(int64_t N, int B) {
@@ -1274,8 +1472,90 @@ __global__ __launch_bounds__(kAesBlock, DASH_RRO_WAVES) void k_rescale_relu_out(
     }
 }
 
+// k_rescale_relu_out with the label staged in LDS (stage_ok, small batches): a block = (256-element tile,
+// residue j, GC b) brings x_j's rows in once as 16-byte loads, each lane rescales its column in place and
+// hashes it, the block stores the rescaled rows (x in place), then each lane rewrites its column into the
+// ReLU output, stored as rows again. The per-lane form streams the label twice with one byte per lane per
+// load, n / kChunk dependent round trips per pass. Measured at batch 1 (MiniONN): 90 us per op vs 76 for the
+// per-lane form and ~50 + ~50 for the staged output-hash and ReLU-multiply kernels, whose 2.24 ms per step
+// beat 2.30 here (64 KiB of LDS per block: two blocks per CU), so the planner only fuses unstaged shapes and
+// this form runs under DASH_JOINT_FUSE=1 (A/B).
+constexpr int kRroBS = 256;
+__global__ __launch_bounds__(kRroBS) void k_rescale_relu_out_s(MrsArgs a, SignArgs sa, Act x, Act y, const u128* gtab,
+                                                                const u128* etab, const ModC* mc, const uint32_t* te0,
+                                                                const uint32_t* rk) {
+    AES_PROLOGUE(te0, rk);
+    __shared__ __attribute__((aligned(16))) uint8_t stg[128 * kRroBS];
+    const int j = blockIdx.y, b = blockIdx.z;
+    const int64_t N = a.N;
+    const int k = a.crt.k;
+    const int p = a.crt.p[j];
+    const ModC m = mc[p];
+    const int n = static_cast<int>(m.n);
+    const int tid = static_cast<int>(threadIdx.x);
+    const uint32_t inv = static_cast<uint32_t>(a.sinv[j]);
+    act_t* L = x.p[j] + static_cast<int64_t>(b) * n * N;
+    act_t* Y = y.p[j] + static_cast<int64_t>(b) * n * N;
+    for (int64_t e0 = static_cast<int64_t>(blockIdx.x) * kRroBS; e0 < N; e0 += static_cast<int64_t>(gridDim.x) * kRroBS) {
+        const int64_t e = min(e0 + tid, N - 1);  // spare lanes shadow a real element; the row stores skip them
+        const int64_t be = static_cast<int64_t>(b) * N + e;
+        const int64_t bke = (static_cast<int64_t>(b) * k + j) * N + e;
+        const u128 HS = a.hs[be];
+        const uint32_t cS = a.cs[be];
+        const u128* E3 = etab + (be * k + j) * 3;
+        const u128 Eraw = E3[cS];
+        const u128 mini = E3[2];
+        const u128* grow = gtab + be * sa.crt.sum + sa.crt.prefix[j];
+        const u128 P = a.pf[bke];
+        __syncthreads();  // the previous tile's row stores have read the image
+        if (j != 0) lds_stage_rows<kRroBS, 4>(stg, L, N, e0, 0, n);
+        __syncthreads();
+        DigitStream s;
+        s.init(P);
+        CompressFwd cf;
+        cf.init();
+        u128 Graw = 0;
+        for (int c = 0; c < n; ++c) {
+            uint8_t& w = stg[c * kRroBS + tid];
+            const uint32_t v = j == 0 ? s.next(m) : modq(static_cast<uint32_t>(w) * inv + s.next(m), m);
+            if (c == 0) Graw = grow[v];
+            w = static_cast<uint8_t>(v);
+            if (j != 0) cf.push(v, m);
+        }
+        const u128 key = j == 0 ? P : cf.finish();
+        __syncthreads();
+        lds_store_rows<kRroBS>(L, stg, N, e0, 0, n);  // Y_j, the rescaled label
+        const u128 G = Graw - aes_encrypt(aes, key);
+        const u128 E = Eraw - HS;
+        const int16_t t16 = static_cast<int16_t>(static_cast<uint16_t>(mini >> (16 * cS)));
+        const int16_t ypr16 = static_cast<int16_t>(t16 - static_cast<int16_t>(static_cast<uint16_t>(HS)));
+        const uint32_t ypr = modq(static_cast<uint32_t>(static_cast<int32_t>(ypr16) + (p << 15)), m);
+        DigitStream sg, se;
+        sg.init(G);
+        se.init(E);
+        __syncthreads();  // the row stores have read Y_j
+        for (int c = 0; c < n; ++c) {
+            const uint32_t g = sg.next(m);
+            const uint32_t ev = se.next(m);
+            uint8_t& w = stg[c * kRroBS + tid];
+            w = static_cast<uint8_t>(modq(ev + ypr * static_cast<uint32_t>(w) + static_cast<uint32_t>(p) - g, m));
+        }
+        __syncthreads();
+        lds_store_rows<kRroBS>(Y, stg, N, e0, 0, n);
+    }
+}
+
 void launch_rescale_relu_out(const MrsArgs& a, const SignArgs& sa, const Act& x, const Act& y, const u128* gtab,
                              const u128* etab, int B, const ModC* mc, const AesGlobals& g, hipStream_t st) {
+    static const bool rro_stage = [] {  // DASH_RRO_STAGE=0: the per-lane form (A/B)
+        const char* e = std::getenv("DASH_RRO_STAGE");
+        return !(e && e[0] == '0');
+    }();
+    if (rro_stage && stage_ok(a.N, kRroBS)) {
+        hipLaunchKernelGGL(k_rescale_relu_out_s, dim3(static_cast<unsigned>((a.N + kRroBS - 1) / kRroBS), a.crt.k, B),
+                           dim3(kRroBS), 0, st, a, sa, x, y, gtab, etab, mc, g.te0, g.rk);
+        return;
+    }
     hipLaunchKernelGGL(k_rescale_relu_out, AES_LAUNCH(a.N, a.crt.k, B), kAesLds, st, a, sa, x, y, gtab, etab, mc,
                        g.te0, g.rk);
 }
@@ -1302,12 +1582,14 @@ void launch_relu_mrs(const MrsArgs& a, const SignArgs& sa, const Act& x, const A
     hipLaunchKernelGGL(k_label_hash, AES_LAUNCH(a.N, a.crt.k, B), kAesLds, st, x, a.crt, a.N,
                        sa.hx, sa.colx, mc, g.te0, g.rk);
     const bool stg = mrs_staged(a.N, B);
+    const size_t wl = stg ? 0 : mrs_wave_lds(a, B);
     const dim3 gc = stg ? grid_aes(a.N, kMrsBS, 1, B) : grid_aes(a.N, aes_bs(a.N, 1, B), 1, B);
     const dim3 bc(stg ? kMrsBS : aes_bs(a.N, 1, B));
     switch (a.crt.k) {
 #define DASH_MRS_K(KK) \
         case KK: \
-            if (stg) hipLaunchKernelGGL((k_mrs_chain_s<KK, 1>), gc, bc, 0, st, a, x, mc, g.te0, g.rk); \
+            if (wl) launch_chain_w<KK, 1>(a, x, B, wl, mc, g, st); \
+            else if (stg) hipLaunchKernelGGL((k_mrs_chain_s<KK, 1>), gc, bc, 0, st, a, x, mc, g.te0, g.rk); \
             else hipLaunchKernelGGL((k_mrs_chain<KK, 1>), gc, bc, kAesLds, st, a, x, mc, g.te0, g.rk); \
             break;
         DASH_MRS_K(2) DASH_MRS_K(3) DASH_MRS_K(4) DASH_MRS_K(5) DASH_MRS_K(6) DASH_MRS_K(7) DASH_MRS_K(8)
@@ -1330,12 +1612,15 @@ void launch_relu_joint(const SignArgs& sa, const Act& x, const Act& y, const u12
 void launch_rescale_mrs(const MrsArgs& a, const Act& x, int B, const ModC* mc, const AesGlobals& g, hipStream_t st,
                         bool chain_only) {
     const bool stg = mrs_staged(a.N, B);
+    const size_t wl = stg ? 0 : mrs_wave_lds(a, B);
     const dim3 gc = stg ? grid_aes(a.N, kMrsBS, 1, B) : grid_aes(a.N, aes_bs(a.N, 1, B), 1, B);
     const dim3 bc(stg ? kMrsBS : aes_bs(a.N, 1, B));
     switch (a.crt.k) {
 #define DASH_MRS_K(KK) \
         case KK: \
-            if (stg && a.mode == 2) hipLaunchKernelGGL((k_mrs_chain_s<KK, 2>), gc, bc, 0, st, a, x, mc, g.te0, g.rk); \
+            if (wl && a.mode == 2) launch_chain_w<KK, 2>(a, x, B, wl, mc, g, st); \
+            else if (wl) launch_chain_w<KK, 0>(a, x, B, wl, mc, g, st); \
+            else if (stg && a.mode == 2) hipLaunchKernelGGL((k_mrs_chain_s<KK, 2>), gc, bc, 0, st, a, x, mc, g.te0, g.rk); \
             else if (stg) hipLaunchKernelGGL((k_mrs_chain_s<KK, 0>), gc, bc, 0, st, a, x, mc, g.te0, g.rk); \
             else if (a.mode == 2) hipLaunchKernelGGL((k_mrs_chain<KK, 2>), gc, bc, kAesLds, st, a, x, mc, g.te0, g.rk); \
             else hipLaunchKernelGGL((k_mrs_chain<KK, 0>), gc, bc, kAesLds, st, a, x, mc, g.te0, g.rk); \

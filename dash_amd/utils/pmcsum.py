@@ -50,6 +50,12 @@ def main(paths):
                               ("SQ_INSTS_SALU", "salu/wave")):
                 if ctr in c:
                     d[name] = c[ctr] / c["SQ_WAVES"]
+            for ctr, name in (("SQ_ACTIVE_INST_LDS", "lds_act%"), ("SQ_ACTIVE_INST_SCA", "salu_act%"),
+                              ("SQ_INST_CYCLES_VMEM", "vmem_cyc%"), ("SQ_WAIT_INST_LDS", "wait_lds%")):
+                if ctr in c:
+                    d[name] = 100 * c[ctr] / wc
+        if c.get("SQ_WAVES") and "SQ_IFETCH" in c:
+            d["ifetch/wave"] = c["SQ_IFETCH"] / c["SQ_WAVES"]
         if c.get("SQ_ACTIVE_INST_LDS"):
             d["lds_conf%"] = 100 * c.get("SQ_LDS_BANK_CONFLICT", 0) / c["SQ_ACTIVE_INST_LDS"]
         for ctr, name in (("FETCH_SIZE", "fetch"), ("WRITE_SIZE", "write")):
@@ -60,7 +66,9 @@ def main(paths):
         rows.append(d)
     rows.sort(key=lambda r: -r["ms"])
     cols = ["kernel", "ms", "dispatch", "valu%", "active%", "wait%", "stall%", "valu_insts/wave", "vmem_rd/wave",
-            "vmem_wr/wave", "lds/wave", "salu/wave", "lds_conf%", "fetch_GB", "fetch_TB/s", "write_GB", "write_TB/s"]
+            "vmem_wr/wave", "lds/wave", "salu/wave", "lds_conf%", "lds_act%", "salu_act%", "vmem_cyc%", "wait_lds%",
+            "ifetch/wave", "fetch_GB", "fetch_TB/s", "write_GB", "write_TB/s"]
+    cols = [c for c in cols if c == "kernel" or any(c in r for r in rows)]
     print(" ".join(f"{c:>14s}" if c != "kernel" else f"{c:40s}" for c in cols))
     for r in rows[:25]:
         out = []

@@ -5,7 +5,7 @@ OUT=${1:-gpurun_out/pmcg3}
 ROOT=$(pwd)
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
-RX="k_hash_jobs|k_bank|k_emit|k_draw|k_mrs_derive|k_relu_finish|k_conv|k_rescale|k_bin_keys|k_sign_derive|k_mrs_sign"
+RX="k_hash_iu|k_hash_jobs|k_bank|k_emit|k_draw|k_mrs_derive|k_relu_finish|k_conv|k_chunk_res|k_bin_keys"
 timeout -s KILL 150 rocprofv3 --kernel-trace --stats --kernel-include-regex "$RX" -d "$ROOT/$OUT/kt" -o run -- python3 "$ROOT/scripts/garble_bench.py" --reps 4 --gpu-only > "$ROOT/$OUT/kt.log" 2>&1
 run() {
   timeout -s KILL 150 rocprofv3 --kernel-trace --kernel-include-regex "$RX" --pmc "$@" --output-format csv -d "$ROOT/$OUT/p$N" -o run -- python3 "$ROOT/scripts/garble_bench.py" --reps 2 --gpu-only > "$ROOT/$OUT/p$N.log" 2>&1
