@@ -143,6 +143,21 @@ struct DigitStream {
     }
 };
 
+// Chunk-major digit extraction (callers that walk whole chunks of m.c digits with a wave-uniform trip count):
+// r = divmod128(Q, m.D, m.mD) starts a chunk, chunk_digit(r, m) returns its next digit. The same digits as
+// DigitStream::next without the per-digit chunk bookkeeping.
+__device__ __forceinline__ uint32_t chunk_digit(uint32_t& r, const ModC& m) {
+#if DASH_DIGIT_MAGIC
+    const uint32_t quot = __umulhi(r, m.dm) >> m.ds;
+    const uint32_t d = (r - __umul24(quot, m.q)) & 0xFFFFFFu;
+    r = quot;
+#else
+    uint32_t d;
+    r = div32_q(r, m.q, m.mq, d);
+#endif
+    return d;
+}
+
 // top digit needs a final reduction (matches host decompress for any payload)
 __device__ __forceinline__ uint32_t reduce_top(uint32_t d, const ModC& m) { return d % m.q; }
 

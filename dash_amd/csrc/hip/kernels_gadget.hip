@@ -528,14 +528,28 @@ __global__ __launch_bounds__(kRmBS) void k_relu_mult_s(SignArgs a, Act x, Act y,
         const int16_t t16 = static_cast<int16_t>(static_cast<uint16_t>(mini >> (16 * cS)));
         const int16_t ypr16 = static_cast<int16_t>(t16 - static_cast<int16_t>(static_cast<uint16_t>(HS)));
         const uint32_t ypr = modq(static_cast<uint32_t>(static_cast<int32_t>(ypr16) + (p << 15)), m);
-        DigitStream sg, se;
-        sg.init(G);
-        se.init(E);
-        for (int c = 0; c < n; ++c) {
-            const uint32_t g = sg.next(m);
-            const uint32_t ev = se.next(m);
-            uint8_t& v = stg[c * kRmBS + tid];
-            v = static_cast<uint8_t>(modq(ev + ypr * static_cast<uint32_t>(v) + static_cast<uint32_t>(p) - g, m));
+        if (m.bits) {
+            DigitStream sg, se;
+            sg.init(G);
+            se.init(E);
+            for (int c = 0; c < n; ++c) {
+                const uint32_t g = sg.next(m);
+                const uint32_t ev = se.next(m);
+                uint8_t& v = stg[c * kRmBS + tid];
+                v = static_cast<uint8_t>(modq(ev + ypr * static_cast<uint32_t>(v) + static_cast<uint32_t>(p) - g, m));
+            }
+        } else {  // chunk-major (chunk_digit): one divmod per stream per chunk, uniform digit loops
+            u128 QG = G, QE = E;
+            for (int c0 = 0; c0 < n; c0 += static_cast<int>(m.c)) {
+                uint32_t rg = divmod128(QG, m.D, m.mD), re = divmod128(QE, m.D, m.mD);
+                const int cnt = min(static_cast<int>(m.c), n - c0);
+                for (int t = 0; t < cnt; ++t) {
+                    const uint32_t g = chunk_digit(rg, m);
+                    const uint32_t ev = chunk_digit(re, m);
+                    uint8_t& v = stg[(c0 + t) * kRmBS + tid];
+                    v = static_cast<uint8_t>(modq(ev + ypr * static_cast<uint32_t>(v) + static_cast<uint32_t>(p) - g, m));
+                }
+            }
         }
         __syncthreads();
         lds_store_rows<kRmBS>(Y, stg, N, e0, 0, n);
@@ -921,6 +935,98 @@ constexpr int kStageU = DASH_STAGE_U;
 #define DASH_STAGE_RD 4  // LDS component reads batched per lane
 #endif
 constexpr int kStageRd = DASH_STAGE_RD;
+// one position of k_mrs_chain_s, I a compile-time constant (constant stream counts and pair indices)
+template <int K, int MODE, int I>
+__device__ __forceinline__ void chain_s_pos(const MrsArgs& a, const AesCtx& aes, const ModC* mc, const Act& x,
+                                            uint8_t* stg, int b, int64_t N, int64_t e0, int tid, bool valid,
+                                            const u128* row0, u128* PS, u128& acc) {
+    constexpr int kLast = MODE >= 1 ? K - 1 : K;
+    if constexpr (I < kLast) {
+        constexpr int i = I;
+        {
+            constexpr int r = MODE >= 1 ? (i + 1) % K : i;
+            const ModC m = mc[a.crt.p[r]];
+            const int n = static_cast<int>(m.n);
+            const act_t* L = x.p[r] + static_cast<int64_t>(b) * n * N;
+            uint32_t col = 0;
+            u128 key;
+            if (m.bits) {  // power-of-two modulus (uniform branch): per-digit streams
+                DigitStream ds[K > 1 ? K - 1 : 1];
+#pragma unroll
+                for (int l = 0; l < i; ++l) ds[l].init(PS[static_cast<int64_t>(mrs_pair<K>(l, i)) * N]);
+                CompressFwd cf;
+                cf.init();
+                for (int c0 = 0; c0 < n; c0 += kMrsCap) {
+                    const int cnt = min(kMrsCap, n - c0);
+                    __syncthreads();
+                    lds_stage_rows<kMrsBS, kStageU>(stg, L, N, e0, c0, cnt);
+                    __syncthreads();
+                    for (int c = 0; c < cnt; ++c) {
+                        uint32_t d = valid ? stg[c * kMrsBS + tid] : 0u;  // spare lanes read no staged bytes
+#pragma unroll
+                        for (int l = 0; l < i; ++l) {
+                            const uint32_t s = ds[l].next(m);
+                            d = d >= s ? d - s : d + m.q - s;
+                        }
+                        if (c0 + c == 0) col = d;
+                        cf.push(d, m);
+                    }
+                }
+                key = cf.finish();
+            } else {
+                // chunk-major walk (as k_mrs_chain_w): passes of whole chunks, one divmod per stream per chunk of
+                // m.c digits, wave-uniform digit loops, one compress flush per chunk
+                u128 Q[K > 1 ? K - 1 : 1];
+#pragma unroll
+                for (int l = 0; l < i; ++l) Q[l] = PS[static_cast<int64_t>(mrs_pair<K>(l, i)) * N];
+                u128 C = 0, PW = 1;
+                const int mcn = static_cast<int>(m.c);
+                const int pass = kMrsCap / mcn * mcn;
+                for (int p0 = 0; p0 < n; p0 += pass) {
+                    const int pcnt = min(pass, n - p0);
+                    __syncthreads();
+                    lds_stage_rows<kMrsBS, kStageU>(stg, L, N, e0, p0, pcnt);
+                    __syncthreads();
+                    for (int c0 = 0; c0 < pcnt; c0 += mcn) {
+                        uint32_t rr[K > 1 ? K - 1 : 1];
+#pragma unroll
+                        for (int l = 0; l < i; ++l) rr[l] = divmod128(Q[l], m.D, m.mD);
+                        const int cnt = min(mcn, pcnt - c0);
+                        uint32_t v = 0, pt = 1;
+                        for (int t = 0; t < cnt; ++t) {
+                            uint32_t d = valid ? stg[(c0 + t) * kMrsBS + tid] : 0u;
+#pragma unroll
+                            for (int l = 0; l < i; ++l) {
+                                const uint32_t sd = chunk_digit(rr[l], m);
+                                d = d >= sd ? d - sd : d + m.q - sd;
+                            }
+                            if (p0 + c0 + t == 0) col = d;
+                            v += d * pt;
+                            pt *= m.q;
+                        }
+                        C += PW * static_cast<u128>(v);
+                        PW *= static_cast<u128>(m.D);
+                    }
+                }
+                key = C;
+            }
+            constexpr int kExtra = MODE == 1 ? 0 : 1;
+            const int nt = K - 1 - i + kExtra;
+            const u128* row = row0 + a.dig_off[i] + static_cast<int64_t>(col) * nt;
+            u128 E[K];
+#pragma unroll
+            for (int t = 0; t < nt; ++t) E[t] = row[t];
+            const u128 H = aes_encrypt(aes, key);
+            if (valid) {
+#pragma unroll
+                for (int t = 0; t < K - 1 - i; ++t) PS[static_cast<int64_t>(mrs_pair<K>(i, i + 1 + t)) * N] = E[t] - H;
+            }
+            if constexpr (MODE != 1) acc = add_packed(acc, E[K - 1 - i] - H, a.hmask);
+        }
+        chain_s_pos<K, MODE, I + 1>(a, aes, mc, x, stg, b, N, e0, tid, valid, row0, PS, acc);
+    }
+}
+
 template <int K, int MODE>
 __global__ __launch_bounds__(kMrsBS, MODE == 2 ? DASH_CHAIN2_WAVES : DASH_UA_MINBLOCKS) void k_mrs_chain_s(
     MrsArgs a, Act x, const ModC* mc, const uint32_t* te0, const uint32_t* rk) {
@@ -936,55 +1042,7 @@ __global__ __launch_bounds__(kMrsBS, MODE == 2 ? DASH_CHAIN2_WAVES : DASH_UA_MIN
         const u128* row0 = a.tab + (static_cast<int64_t>(b) * N + e) * a.n_tab;
         u128* PS = a.ps + static_cast<int64_t>(b) * NP * N + e;
         u128 acc = 0;
-#pragma unroll
-        for (int i = 0; i < (MODE >= 1 ? K - 1 : K); ++i) {
-            const int r = MODE >= 1 ? (i + 1) % K : i;
-            const ModC m = mc[a.crt.p[r]];
-            const int n = static_cast<int>(m.n);
-            const act_t* L = x.p[r] + static_cast<int64_t>(b) * n * N;
-            DigitStream ds[K > 1 ? K - 1 : 1];
-#pragma unroll
-            for (int l = 0; l < i; ++l) ds[l].init(PS[static_cast<int64_t>(mrs_pair<K>(l, i)) * N]);
-            CompressFwd cf;
-            cf.init();
-            uint32_t col = 0;
-            for (int c0 = 0; c0 < n; c0 += kMrsCap) {
-                const int cnt = min(kMrsCap, n - c0);
-                __syncthreads();
-                lds_stage_rows<kMrsBS, kStageU>(stg, L, N, e0, c0, cnt);
-                __syncthreads();
-                for (int c = 0; c < cnt; c += kStageRd) {
-                    uint32_t v[kStageRd];
-#pragma unroll
-                    for (int u = 0; u < kStageRd; ++u)  // spare lanes (e >= N) read no staged bytes: digit 0
-                        if (c + u < cnt) v[u] = valid ? stg[(c + u) * kMrsBS + tid] : 0u;
-#pragma unroll
-                    for (int u = 0; u < kStageRd; ++u)
-                        if (c + u < cnt) {
-                            uint32_t d = v[u];
-#pragma unroll
-                            for (int l = 0; l < i; ++l) {
-                                const uint32_t s = ds[l].next(m);
-                                d = d >= s ? d - s : d + m.q - s;
-                            }
-                            if (c0 + c + u == 0) col = d;
-                            cf.push(d, m);
-                        }
-                }
-            }
-            constexpr int kExtra = MODE == 1 ? 0 : 1;
-            const int nt = K - 1 - i + kExtra;
-            const u128* row = row0 + a.dig_off[i] + static_cast<int64_t>(col) * nt;
-            u128 E[K];
-#pragma unroll
-            for (int t = 0; t < nt; ++t) E[t] = row[t];
-            const u128 H = aes_encrypt(aes, cf.finish());
-            if (valid) {
-#pragma unroll
-                for (int t = 0; t < K - 1 - i; ++t) PS[static_cast<int64_t>(mrs_pair<K>(i, i + 1 + t)) * N] = E[t] - H;
-            }
-            if (MODE != 1) acc = add_packed(acc, E[K - 1 - i] - H, a.hmask);
-        }
+        chain_s_pos<K, MODE, 0>(a, aes, mc, x, stg, b, N, e0, tid, valid, row0, PS, acc);
         if (MODE >= 1) {
             const ModC m = mc[a.crt.p[0]];
             const int n = static_cast<int>(m.n);
@@ -1083,9 +1141,7 @@ __device__ __forceinline__ void chain_w_pos(const MrsArgs& a, const AesCtx& aes,
                     uint32_t d = valid ? Ls[(c0 + t) * kMrsWBS] : 0u;
 #pragma unroll
                     for (int l = 0; l < I; ++l) {
-                        const uint32_t quot = __umulhi(rr[l], m.dm) >> m.ds;
-                        const uint32_t sd = (rr[l] - __umul24(quot, m.q)) & 0xFFFFFFu;
-                        rr[l] = quot;
+                        const uint32_t sd = chunk_digit(rr[l], m);
                         d = d >= sd ? d - sd : d + m.q - sd;
                     }
                     if (c0 + t == 0) col = d;
@@ -1324,7 +1380,7 @@ __global__ __launch_bounds__(kAesBlock, kAesMinBlocks) void k_rescale_mrs_out_ha
 // GC b) walks the label kOhCap components per pass: stage the rows, each lane rewrites its column in place,
 // store the rows back (residue 0 only writes the decompressed payload).
 constexpr int kOhBS = 512;
-constexpr int kOhCap = 32;  // 16 KiB image beside the 32 KiB AES image: three blocks per CU
+constexpr int kOhCap = 40;  // 20 KiB image beside the 32 KiB AES image: three blocks per CU
 __global__ __launch_bounds__(kOhBS, kAesMinBlocks) void k_rescale_mrs_out_hash_s(MrsArgs a, Act x, const ModC* mc,
                                                                                const uint32_t* te0, const uint32_t* rk) {
     AES_PROLOGUE(te0, rk);
@@ -1345,25 +1401,47 @@ __global__ __launch_bounds__(kOhBS, kAesMinBlocks) void k_rescale_mrs_out_hash_s
         s.init(P);
         CompressFwd cf;
         cf.init();
+        u128 Q = P, C = 0, PW = 1;  // chunk-major state (non-power-of-two moduli)
         uint32_t c0 = 0;
-        for (int q0 = 0; q0 < n; q0 += kOhCap) {
-            const int cnt = min(kOhCap, n - q0);
+        // passes of whole chunks of m.c digits for the chunk-major walk
+        const int pass = m.bits ? kOhCap : kOhCap / static_cast<int>(m.c) * static_cast<int>(m.c);
+        for (int q0 = 0; q0 < n; q0 += pass) {
+            const int cnt = min(pass, n - q0);
             __syncthreads();  // the previous pass's stores have read the image
             if (j != 0) {
                 lds_stage_rows<kOhBS, 2>(stg, L, N, e0, q0, cnt);
                 __syncthreads();
             }
-            for (int c = 0; c < cnt; ++c) {
-                uint8_t& w = stg[c * kOhBS + tid];
-                const uint32_t v = j == 0 ? s.next(m) : modq(static_cast<uint32_t>(w) * inv + s.next(m), m);
-                if (q0 + c == 0) c0 = v;
-                w = static_cast<uint8_t>(v);
-                if (j != 0) cf.push(v, m);
+            if (m.bits) {
+                for (int c = 0; c < cnt; ++c) {
+                    uint8_t& w = stg[c * kOhBS + tid];
+                    const uint32_t v = j == 0 ? s.next(m) : modq(static_cast<uint32_t>(w) * inv + s.next(m), m);
+                    if (q0 + c == 0) c0 = v;
+                    w = static_cast<uint8_t>(v);
+                    if (j != 0) cf.push(v, m);
+                }
+            } else {  // chunk-major (chunk_digit): one divmod per chunk, uniform digit loops, one flush per chunk
+                for (int k0 = 0; k0 < cnt; k0 += static_cast<int>(m.c)) {
+                    uint32_t r = divmod128(Q, m.D, m.mD);
+                    const int kc = min(static_cast<int>(m.c), cnt - k0);
+                    uint32_t acc = 0, pt = 1;
+                    for (int t = 0; t < kc; ++t) {
+                        uint8_t& w = stg[(k0 + t) * kOhBS + tid];
+                        const uint32_t dd = chunk_digit(r, m);
+                        const uint32_t v = j == 0 ? dd : modq(static_cast<uint32_t>(w) * inv + dd, m);
+                        if (q0 + k0 + t == 0) c0 = v;
+                        w = static_cast<uint8_t>(v);
+                        acc += v * pt;
+                        pt *= m.q;
+                    }
+                    C += PW * static_cast<u128>(acc);
+                    PW *= static_cast<u128>(m.D);
+                }
             }
             __syncthreads();
             lds_store_rows<kOhBS>(L, stg, N, e0, q0, cnt);
         }
-        const u128 H = aes_encrypt(aes, j == 0 ? P : cf.finish());
+        const u128 H = aes_encrypt(aes, j == 0 ? P : (m.bits ? cf.finish() : C));
         if (valid) {
             a.colx[bke] = static_cast<uint16_t>(c0);
             a.hx[bke] = H;

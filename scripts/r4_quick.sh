@@ -10,3 +10,7 @@ for b in ${BATCHES:-1 24}; do
   timeout -k 10 300 python scripts/ab_online.py --batch $b --steps 20 --relu joint --detail > $OUT/ops_b$b.json 2> $OUT/ops_b$b.err || { tail -5 $OUT/ops_b$b.err; exit 1; }
   echo "b$b $(head -c 200 $OUT/ops_b$b.json)"
 done
+if [ -n "$BENCH" ]; then
+  timeout -k 10 400 python bench.py --phases $BENCH --steps 10 --warmup 3 > $OUT/bench.json 2> $OUT/bench.err || { tail -5 $OUT/bench.err; exit 1; }
+  head -c 600 $OUT/bench.json; echo
+fi
