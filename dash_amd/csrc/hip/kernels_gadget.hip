@@ -1188,6 +1188,31 @@ __global__ __launch_bounds__(kMrsWBS, 1) void k_mrs_chain_w(MrsArgs a, Act x, co
     const int units = roff[K] * (kMrsWBS / 16);
     for (int64_t e0 = static_cast<int64_t>(blockIdx.x) * kMrsWBS; e0 < N; e0 += static_cast<int64_t>(gridDim.x) * kMrsWBS) {
         __syncthreads();  // the previous tile's readers are done
+        if (N % 16 != 0) {
+            // rows not 16-byte aligned (tiny layers, e.g. a 10-logit head): each lane stages its own column, one
+            // byte per row, kWaveBU loads in flight (unit xu = row * kMrsWBS + tid, its LDS offset)
+            constexpr int kWaveBU = 32;
+            const int bunits = roff[K] * kMrsWBS;
+            const int64_t e = e0 + tid;
+            for (int x0 = tid; x0 < bunits; x0 += kWaveBU * kMrsWBS) {
+                uint32_t v[kWaveBU];
+#pragma unroll
+                for (int h = 0; h < kWaveBU; ++h) {
+                    const int xu = x0 + h * kMrsWBS;
+                    const int g = xu / kMrsWBS;
+                    const act_t* row = src[0] + static_cast<int64_t>(g) * N;
+#pragma unroll
+                    for (int r = 1; r < K; ++r)
+                        if (g >= roff[r]) row = src[r] + static_cast<int64_t>(g - roff[r]) * N;
+                    v[h] = (xu < bunits && e < N) ? static_cast<uint32_t>(row[e]) : 0u;
+                }
+#pragma unroll
+                for (int h = 0; h < kWaveBU; ++h) {
+                    const int xu = x0 + h * kMrsWBS;
+                    if (xu < bunits) wst[xu] = static_cast<uint8_t>(v[h]);
+                }
+            }
+        } else
         for (int x0 = tid; x0 < units; x0 += kWaveU * kMrsWBS) {
             uint4 v[kWaveU];
 #pragma unroll
@@ -1256,7 +1281,8 @@ static inline size_t mrs_wave_lds(const MrsArgs& a, int B) {
     }();
     // only launches of at most one block per CU: above that the per-lane form keeps more waves resident (24 GCs,
     // MiniONN: 11.29 ms per step per-lane vs 11.56 with this form on every small-block launch)
-    if (!on || a.N % 16 != 0 || (a.N + kMrsWBS - 1) / kMrsWBS * B > num_cus()) return 0;
+    // (rows that are not 16-byte aligned: byte-wise staging, only for single-block layers)
+    if (!on || (a.N % 16 != 0 && a.N > kMrsWBS) || (a.N + kMrsWBS - 1) / kMrsWBS * B > num_cus()) return 0;
     size_t sum = 0;
     for (int r = 0; r < a.crt.k; ++r) sum += static_cast<size_t>(std::floor(128.0 / std::log2(static_cast<double>(a.crt.p[r]))));  // core.h nr_comps
     const size_t bytes = sum * kMrsWBS;
