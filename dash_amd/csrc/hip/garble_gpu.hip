@@ -333,15 +333,8 @@ __global__ __launch_bounds__(kGB) void k_draw(Ctx c, Gadget g) {
         } else if (kDrawPairs) {
             B[0] = aes_keyed(aes, base | static_cast<uint64_t>(d.ctr), c.rk);
         }
-        for (int q = 0; q < n; ++q) {
-            if (left == 0) {
-                if (kDrawPairs && nb <= 3) ds.init(blk == 0 ? B[0] : (blk == 1 ? B[1] : B[2]));
-                else ds.init(aes_keyed(aes, base | static_cast<uint64_t>(d.ctr + blk), c.rk));
-                ++blk;
-                left = pm;
-            }
-            acc = (acc >> 16) | (static_cast<u128>(ds.next(m)) << 112);
-            --left;
+        auto push = [&](int q, uint32_t dg) {
+            acc = (acc >> 16) | (static_cast<u128>(dg) << 112);
             if ((q & 7) == 7) {
                 u32x4a v;
                 v[0] = static_cast<uint32_t>(acc);
@@ -349,6 +342,32 @@ __global__ __launch_bounds__(kGB) void k_draw(Ctx c, Gadget g) {
                 v[2] = static_cast<uint32_t>(acc >> 64);
                 v[3] = static_cast<uint32_t>(acc >> 96);
                 st_chunk(out + (q >> 3) * cs, v);
+            }
+        };
+        if (m.bits) {
+            for (int q = 0; q < n; ++q) {
+                if (left == 0) {
+                    if (kDrawPairs && nb <= 3) ds.init(blk == 0 ? B[0] : (blk == 1 ? B[1] : B[2]));
+                    else ds.init(aes_keyed(aes, base | static_cast<uint64_t>(d.ctr + blk), c.rk));
+                    ++blk;
+                    left = pm;
+                }
+                push(q, ds.next(m));
+                --left;
+            }
+        } else {
+            // chunk-major (dev.h chunk_digit): per block, one divmod per chunk of m.c digits and a uniform digit
+            // loop (the digits DigitStream::next yields)
+            int q = 0;
+            for (int bi = 0; bi < nb; ++bi) {
+                u128 Q = (kDrawPairs && nb <= 3) ? (bi == 0 ? B[0] : (bi == 1 ? B[1] : B[2]))
+                                                 : aes_keyed(aes, base | static_cast<uint64_t>(d.ctr + bi), c.rk);
+                const int bcnt = min(pm, n - bi * pm);
+                for (int k0 = 0; k0 < bcnt; k0 += static_cast<int>(m.c)) {
+                    uint32_t r = divmod128(Q, m.D, m.mD);
+                    const int kc = min(static_cast<int>(m.c), bcnt - k0);
+                    for (int t = 0; t < kc; ++t, ++q) push(q, chunk_digit(r, m));
+                }
             }
         }
         if (n & 7) {  // last partial chunk: shift the pending components down, zeros above
