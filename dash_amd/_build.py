@@ -50,7 +50,8 @@ def _host_cmd(src: Path, obj: Path, debug: bool) -> list[str]:
         cxx = "g++"
     opt = ["-O1", "-g"] if debug else ["-O3"]
     return [cxx, "-std=c++17", "-fPIC", "-fvisibility=hidden", "-maes", "-msse4.2", "-mavx2", "-mpclmul",
-            *opt, "-Wall", "-Wno-unused-function", *_includes(), "-c", str(src), "-o", str(obj)]
+            *opt, "-Wall", "-Wno-unused-function", *_includes(), "-MMD", "-MF", str(obj) + ".d", "-c", str(src),
+            "-o", str(obj)]
 
 
 def _hip_cmd(src: Path, obj: Path, debug: bool) -> list[str]:
@@ -58,7 +59,23 @@ def _hip_cmd(src: Path, obj: Path, debug: bool) -> list[str]:
     opt = ["-O1", "-g"] if debug else ["-O3"]
     extra = os.environ.get("DASH_HIP_FLAGS", "").split()  # e.g. -DDASH_AES_BLOCK=512 for A/B builds
     return [hipcc, "-std=c++17", "-fPIC", "-fvisibility=hidden", f"--offload-arch={ARCH}", "-maes", "-msse4.2",
-            *opt, "-Wno-unused-result", *extra, *_includes(), "-c", "-x", "hip", str(src), "-o", str(obj)]
+            *opt, "-Wno-unused-result", *extra, *_includes(), "-MMD", "-MF", str(obj) + ".d", "-c", "-x", "hip",
+            str(src), "-o", str(obj)]
+
+
+def _dep_headers(obj: Path) -> list[Path] | None:
+    """In-tree headers the object was compiled from (the compiler's -MMD file), or None without one."""
+    d = Path(str(obj) + ".d")
+    if not d.exists():
+        return None
+    text = d.read_text().replace("\\\n", " ")
+    _, _, deps = text.partition(":")
+    out = []
+    for tok in deps.split():
+        p = Path(tok)
+        if p.suffix in (".h", ".cuh", ".hpp") and str(p).startswith(str(CSRC)):
+            out.append(p)
+    return out
 
 
 def _deps_newer(obj: Path, src: Path) -> bool:
@@ -67,8 +84,11 @@ def _deps_newer(obj: Path, src: Path) -> bool:
     t = obj.stat().st_mtime
     if src.stat().st_mtime > t:
         return True
-    for h in list(CSRC.glob("*.h")) + list(CSRC.glob("hip/*.h")) + list(CSRC.glob("hip/*.cuh")):
-        if h.stat().st_mtime > t:
+    hdrs = _dep_headers(obj)
+    if hdrs is None:  # no dependency file yet: any in-tree header may be included
+        hdrs = list(CSRC.glob("*.h")) + list(CSRC.glob("hip/*.h")) + list(CSRC.glob("hip/*.cuh"))
+    for h in hdrs:
+        if not h.exists() or h.stat().st_mtime > t:
             return True
     return False
 

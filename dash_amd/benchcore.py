@@ -130,10 +130,15 @@ def _free_port() -> int:
 
 
 def visible_gpus() -> int:
-    """Visible GPU count without initialising HIP in this process (a parent that starts ranks must not)."""
-    import torch
+    """Visible GPU count without initialising HIP in this process (a parent that starts ranks must not).
 
-    return int(torch.cuda.device_count())
+    Read from the KFD topology in sysfs (parallel/dist.py kfd_gpus), filtered by the *_VISIBLE_DEVICES
+    variables: torch.cuda.device_count() falls back to hipGetDeviceCount when amdsmi is missing, which would
+    initialise the HIP runtime here. Raises when the topology cannot be read (no silent guess)."""
+    from .parallel.dist import kfd_gpus, visible_indices
+
+    gpus = kfd_gpus()
+    return len(visible_indices(len(gpus)))
 
 
 def spawn_ranks(args, argv: List[str]) -> int:

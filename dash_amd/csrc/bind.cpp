@@ -116,6 +116,13 @@ const u128* u128_data(const py::array_t<uint64_t, py::array::c_style | py::array
 
 class IntegrityError : public std::exception {};
 
+// serialize_into / deserialize_buffer read or write bi.size bytes straight from bi.ptr: only a 1-D, C-contiguous
+// byte buffer describes that memory (a strided or negative-stride view would send the copy past the view)
+void check_contig_bytes(const py::buffer_info& bi, const char* who) {
+    DASH_CHECK(bi.itemsize == 1 && bi.ndim == 1 && (bi.shape[0] <= 1 || bi.strides[0] == 1),
+               std::string(who) + " needs a 1-D C-contiguous byte buffer");
+}
+
 }  // namespace
 
 PYBIND11_MODULE(_dash_native, m) {
@@ -141,6 +148,20 @@ PYBIND11_MODULE(_dash_native, m) {
     m.def("set_num_threads", &set_default_threads);
     m.def("get_num_threads", &default_threads);
     m.def("aes_hash", [](py::int_ x) { return u128_to_py(hash(py_to_u128(x))); }, "fixed-key AES-128 of a 128-bit int");
+    m.def("chacha_block", [](std::vector<uint32_t> state, int rounds) {
+        DASH_CHECK(state.size() == 16, "ChaCha state is 16 words");
+        std::vector<uint32_t> out(16);
+        chacha_core(state.data(), out.data(), rounds);
+        return out;
+    }, "ChaCha block function (rounds rounds, feed-forward) of a 16-word state");
+    m.def("hard_pads", [](py::int_ key, uint64_t gate, uint32_t sub, uint32_t blk) {
+        u128 p[4];
+        hard_block(py_to_u128(key), gate, sub, blk, p);
+        py::list out;
+        for (auto v : p) out.append(u128_to_py(v));
+        return out;
+    }, "the four hardened-encoding pads of block blk of key K under tweak (gate, sub)");
+    m.def("stream_id", &stream_id);
     m.def("aes_hash_array", [](py::array_t<uint64_t, py::array::c_style | py::array::forcecast> a) {
         DASH_CHECK(a.ndim() == 2 && a.shape(1) == 2, "expected (n, 2) uint64 array");
         py::array_t<uint64_t> out({a.shape(0), static_cast<py::ssize_t>(2)});
@@ -257,15 +278,16 @@ PYBIND11_MODULE(_dash_native, m) {
         .def("serialized_size", &GarbledModel::serialized_size)
         .def("serialize_into", [](const GarbledModel& g, py::buffer b) {
             py::buffer_info bi = b.request(true);
-            DASH_CHECK(bi.itemsize == 1 || bi.ndim == 1, "serialize_into needs a writable byte buffer");
-            const size_t cap = static_cast<size_t>(bi.size) * static_cast<size_t>(bi.itemsize);
+            check_contig_bytes(bi, "serialize_into");
+            const size_t cap = static_cast<size_t>(bi.size);
             py::gil_scoped_release nogil;
             return g.serialize_to(static_cast<uint8_t*>(bi.ptr), cap);
         }, "write the offline message into a writable buffer (>= serialized_size() bytes) -> bytes written; "
            "device-resident tables are fetched straight into it")
         .def_static("deserialize_buffer", [](py::buffer b) {
             py::buffer_info bi = b.request();
-            const size_t n = static_cast<size_t>(bi.size) * static_cast<size_t>(bi.itemsize);
+            check_contig_bytes(bi, "deserialize_buffer");
+            const size_t n = static_cast<size_t>(bi.size);
             const uint8_t* p = static_cast<const uint8_t*>(bi.ptr);
             py::gil_scoped_release nogil;
             return std::make_shared<GarbledModel>(GarbledModel::deserialize(p, n));
@@ -277,6 +299,15 @@ PYBIND11_MODULE(_dash_native, m) {
         .def_property_readonly("out_moduli", [](const GarbledModel& g) { return g.h.out_moduli; })
         .def_property_readonly("max_mod", [](const GarbledModel& g) { return g.h.max_mod; })
         .def_property_readonly("sign_fused", [](const GarbledModel& g) { return g.h.sign_fused != 0; })
+        .def_property_readonly("hardened", [](const GarbledModel& g) { return g.h.hardened != 0; })
+        .def("const_names", [](const GarbledModel& g) {
+            std::vector<std::string> v;
+            for (const auto& kv : g.consts) v.push_back(kv.first);
+            return v;
+        }, "names of the evaluator-visible constant labels the offline message ships (none when hardened)")
+        .def("const_array", [](std::shared_ptr<GarbledModel> g, const std::string& name) {
+            return array_view(g->consts.at(name), py::cast(g));
+        })
         .def_property_readonly("num_layers", [](const GarbledModel& g) { return g.layers.size(); })
         .def("table_bytes", &GarbledModel::table_bytes)
         .def("total_bytes", &GarbledModel::total_bytes)
@@ -338,8 +369,9 @@ PYBIND11_MODULE(_dash_native, m) {
              py::arg("crt"), py::arg("mrs"), py::arg("seed"), py::arg("max_mod") = 0)
         .def("garble", [](Garbler& g, std::shared_ptr<GarbleSpecs> specs, std::vector<i64> in_dims, int nthreads,
                           int device, bool fused_sign, bool rescale_mrs, bool relu_mrs, bool relu_joint,
-                          std::shared_ptr<TableSink> sink) {
+                          std::shared_ptr<TableSink> sink, bool hardened) {
             GarbleOptions o;
+            o.hardened = hardened;
             o.sink = std::move(sink);
             o.nthreads = nthreads;
             o.device = device;
@@ -356,12 +388,14 @@ PYBIND11_MODULE(_dash_native, m) {
             return std::make_shared<GarbledModel>(std::move(gm));
         }, py::arg("layers"), py::arg("in_dims"), py::arg("nthreads") = 0, py::arg("device") = -1,
            py::arg("fused_sign") = true, py::arg("rescale_mrs") = false,
-           py::arg("relu_mrs") = false, py::arg("relu_joint") = false, py::arg("sink") = nullptr)
+           py::arg("relu_mrs") = false, py::arg("relu_joint") = false, py::arg("sink") = nullptr,
+           py::arg("hardened") = false)
         .def("garble", [](Garbler& g, const py::list& layers, std::vector<i64> in_dims, int nthreads, int device,
                           bool fused_sign, bool rescale_mrs, bool relu_mrs, bool relu_joint,
-                          std::shared_ptr<TableSink> sink) {
+                          std::shared_ptr<TableSink> sink, bool hardened) {
             auto specs = specs_from_py(layers);
             GarbleOptions o;
+            o.hardened = hardened;
             o.sink = std::move(sink);
             o.nthreads = nthreads;
             o.device = device;
@@ -377,7 +411,8 @@ PYBIND11_MODULE(_dash_native, m) {
             return std::make_shared<GarbledModel>(std::move(gm));
         }, py::arg("layers"), py::arg("in_dims"), py::arg("nthreads") = 0, py::arg("device") = -1,
            py::arg("fused_sign") = true, py::arg("rescale_mrs") = false,
-           py::arg("relu_mrs") = false, py::arg("relu_joint") = false, py::arg("sink") = nullptr)
+           py::arg("relu_mrs") = false, py::arg("relu_joint") = false, py::arg("sink") = nullptr,
+           py::arg("hardened") = false)
         .def("layer_ms", [](const Garbler& g) { return g.layer_ms(); })
         .def("encode", [](const Garbler& g, py::array_t<i64, py::array::c_style | py::array::forcecast> x) {
             std::vector<i64> v(x.data(), x.data() + x.size());

@@ -250,6 +250,109 @@ inline u128 hash(u128 x) { return m_to_u128(aes_enc_block(u128_to_m(x), fixed_ke
 void hash_batch(const u128* in, u128* out, size_t n);
 
 // ----------------------------------------------------------------------------
+// Hardened-encoding hash (docs/SECURITY.md): a tweakable hash of a compressed
+// key label K, H(K, gate, sub, blk) = the ChaCha12 block function (feed-forward
+// included) on the state
+//   [sigma0..3][K (4 words, LE)][gate lo, gate hi, sub, "HARD"][blk, 0, 0, 0]
+// whose 512-bit output is four 128-bit pads (pad q = words 4q..4q+3, LE). The
+// table entry of slot s of a projection row is masked by pad (s mod 4) of
+// block s / 4, and (gate, sub) is unique per row within a GC, so no two
+// entries of a GC share a pad: unlike the reference's fixed-key AES H(K), a
+// key that feeds several outputs (fan-out rows, a ReLU's k half gates, a
+// half gate's mini table) gets an independent pad per output.
+// ----------------------------------------------------------------------------
+constexpr int kChaRounds = 12;
+constexpr uint32_t kHardTag = 0x44524148u;  // "HARD"
+
+inline uint32_t rotl32(uint32_t x, int r) { return (x << r) | (x >> (32 - r)); }
+
+// ChaCha block function with `rounds` rounds (even) and feed-forward; in/out 16 words
+inline void chacha_core(const uint32_t in[16], uint32_t out[16], int rounds) {
+    uint32_t x[16];
+    for (int i = 0; i < 16; ++i) x[i] = in[i];
+    auto qr = [&x](int a, int b, int c, int d) {
+        x[a] += x[b]; x[d] = rotl32(x[d] ^ x[a], 16);
+        x[c] += x[d]; x[b] = rotl32(x[b] ^ x[c], 12);
+        x[a] += x[b]; x[d] = rotl32(x[d] ^ x[a], 8);
+        x[c] += x[d]; x[b] = rotl32(x[b] ^ x[c], 7);
+    };
+    for (int r = 0; r < rounds; r += 2) {
+        qr(0, 4, 8, 12); qr(1, 5, 9, 13); qr(2, 6, 10, 14); qr(3, 7, 11, 15);
+        qr(0, 5, 10, 15); qr(1, 6, 11, 12); qr(2, 7, 8, 13); qr(3, 4, 9, 14);
+    }
+    for (int i = 0; i < 16; ++i) out[i] = x[i] + in[i];
+}
+
+// The four pads of block `blk` of key K under tweak (gate, sub)
+inline void hard_block(u128 K, u64 gate, uint32_t sub, uint32_t blk, u128 pads[4]) {
+    uint32_t s[16] = {0x61707865u, 0x3320646eu, 0x79622d32u, 0x6b206574u,
+                      static_cast<uint32_t>(K), static_cast<uint32_t>(K >> 32), static_cast<uint32_t>(K >> 64),
+                      static_cast<uint32_t>(K >> 96), static_cast<uint32_t>(gate), static_cast<uint32_t>(gate >> 32),
+                      sub, kHardTag, blk, 0u, 0u, 0u};
+    uint32_t o[16];
+    chacha_core(s, o, kChaRounds);
+    for (int q = 0; q < 4; ++q)
+        pads[q] = (static_cast<u128>((static_cast<u64>(o[4 * q + 3]) << 32) | o[4 * q + 2]) << 64) |
+                  ((static_cast<u64>(o[4 * q + 1]) << 32) | o[4 * q]);
+}
+
+// pad of slot s
+inline u128 hard_pad(u128 K, u64 gate, uint32_t sub, int s) {
+    u128 p[4];
+    hard_block(K, gate, sub, static_cast<uint32_t>(s) >> 2, p);
+    return p[s & 3];
+}
+
+// The pads of one (key, tweak) row, one block computed at a time as slots are asked for
+struct PadRow {
+    u128 K = 0;
+    u64 gate = 0;
+    uint32_t sub = 0;
+    int blk = -1;
+    u128 p[4];
+    PadRow() = default;
+    PadRow(u128 k, u64 g, uint32_t s) : K(k), gate(g), sub(s) {}
+    u128 get(int s) {
+        if ((s >> 2) != blk) {
+            blk = s >> 2;
+            hard_block(K, gate, sub, static_cast<uint32_t>(blk), p);
+        }
+        return p[s & 3];
+    }
+};
+
+// Tweak kinds (the high 16 bits of `sub`; the low bits index the row inside the gadget)
+enum TweakKind : uint32_t {
+    TW_APPROX = 1,  // sign gadget: residue j's approx row (slots: digits)
+    TW_CAST1 = 2,   // reference casts (non-hardened only)
+    TW_CAST2 = 3,   // sign gadget: digit d's carry projection
+    TW_SIGN = 4,    // sign gadget: MSD -> outputs (slots: output moduli)
+    TW_MMG = 5,     // mixed / generalized half gate, garbler half (key x_j)
+    TW_MMY = 6,     // mixed half gate, evaluator half + mini (key y; slots: residues, then the packed minis)
+    TW_MRS = 7,     // mixed-radix rescale rows (i < k: digit rows; i = k: final row)
+    TW_SMRS = 8,    // mixed-radix sign rows
+    TW_BE = 9,      // base extension rows
+    TW_TRANS = 10,  // ReDash rescale: factor residue -> active residues
+    TW_PROJ = 11,   // projection layer
+    TW_GME = 12,    // generalized half gate, evaluator half (key y_j)
+    TW_MMT = 13,    // mixed-mult layer: the residue-j mod transform (key x_2e+1)
+};
+inline uint32_t tw_sub(TweakKind k, uint32_t idx) { return (static_cast<uint32_t>(k) << 16) | (idx & 0xffffu); }
+
+// A table mask: the reference's H(K) (hard == false) or the hardened pad of slot `slot`
+struct Mask {
+    bool hard = false;
+    u64 gate = 0;
+    uint32_t sub = 0;
+    int slot = 0;
+    Mask with_slot(int s) const {
+        Mask m = *this;
+        m.slot = s;
+        return m;
+    }
+};
+
+// ----------------------------------------------------------------------------
 // Deterministic label PRG: AES-128-CTR keyed with the garbler seed.
 // block(stream, ctr) = AES_k(stream << 64 | ctr); each block yields two
 // 64-bit samples; component = sample mod p (bias <= p / 2^64).

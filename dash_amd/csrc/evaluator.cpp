@@ -9,6 +9,10 @@ LabelBank GarbledModel::zero_bank() const {
     LabelBank Z;
     Z.max_mod = h.max_mod;
     Z.lab.assign(h.max_mod + 1, {});
+    if (h.hardened) {  // public zero wires have label 0 (docs/SECURITY.md)
+        for (int p = 2; p <= h.max_mod; ++p) Z.lab[p].assign(nr_comps(p), 0);
+        return Z;
+    }
     for (const auto& kv : consts) {
         if (kv.first.rfind("Z.", 0) != 0) continue;
         int p = std::stoi(kv.first.substr(2));
@@ -45,19 +49,27 @@ struct ReluTabs {
           sg(&g.arr(pre + "s.sign")), ga(&g.arr(pre + "mm.g")), ea(&g.arr(pre + "mm.e")) {}
 };
 
+// s_gate / m_gate: the sign and mixed-mult gadgets' PRG streams (the hardened tweaks' gates)
 void relu_eval_elem(const SignPlan& sp, const LabelBank& Z, const std::vector<int>& crt,
                     const std::vector<i64>& prefix, const comp_t* const* x, const ReluTabs& T, i64 e,
-                    comp_t* const* out) {
+                    comp_t* const* out, bool hard, u64 s_gate, u64 m_gate) {
     const int k = static_cast<int>(crt.size());
     comp_t sig[128];
     comp_t* outs[1] = {sig};
     sign_eval_elem(sp, Z, x, T.ap->ptr<u128>() + e * T.ap->shape[1],
                    T.c1 ? T.c1->ptr<u128>() + e * T.c1->shape[1] : nullptr,
-                   T.c2->ptr<u128>() + e * T.c2->shape[1], T.sg->ptr<u128>() + e * T.sg->shape[1], outs);
+                   T.c2->ptr<u128>() + e * T.c2->shape[1], T.sg->ptr<u128>() + e * T.sg->shape[1], outs, hard, s_gate);
     const ModInfo& m2 = mod_info(2);
     for (int j = 0; j < k; ++j)
         mixed_mult_eval(x[j], mod_info(crt[j]), sig, m2, T.ga->ptr<u128>() + e * T.ga->shape[1] + prefix[j],
-                        T.ea->ptr<u128>() + (e * k + j) * 3, out[j]);
+                        T.ea->ptr<u128>() + (e * k + j) * 3, out[j], MMTw{hard, m_gate, j, k, true});
+}
+
+// a layer array that the hardened encoding does not ship (bias labels): all-zero rows of the same shape
+const comp_t* zeros_or(const GLayer& g, const std::string& name, bool hard, size_t n, std::vector<comp_t>& buf) {
+    if (!hard) return g.arr(name).ptr<comp_t>();
+    buf.assign(n, 0);
+    return buf.data();
 }
 
 }  // namespace
@@ -68,6 +80,7 @@ CrtLabels cpu_evaluate(const GarbledModel& m, const CrtLabels& inputs, int nt, s
     DASH_CHECK(static_cast<int>(inputs.size()) == k, "input residue count mismatch");
     const LabelBank Z = m.zero_bank();
     const bool fused = m.h.sign_fused != 0;
+    const bool hard = m.h.hardened != 0;
     std::vector<i64> prefix(k);
     i64 sum_crt = 0;
     for (int j = 0; j < k; ++j) {
@@ -83,7 +96,9 @@ CrtLabels cpu_evaluate(const GarbledModel& m, const CrtLabels& inputs, int nt, s
 
     CrtLabels cur = inputs;
     if (keep[0]) saved[0] = cur;
+    std::vector<comp_t> zero_const(128, 0);
     auto get_const = [&](const std::string& name) -> const comp_t* {
+        if (hard) return zero_const.data();  // shift labels: public constants, label 0
         auto it = m.consts.find(name);
         DASH_CHECK(it != m.consts.end(), "missing model constant " + name);
         return it->second.ptr<comp_t>();
@@ -94,6 +109,7 @@ CrtLabels cpu_evaluate(const GarbledModel& m, const CrtLabels& inputs, int nt, s
     for (size_t li = 0; li < m.layers.size(); ++li) {
         const auto t_layer = std::chrono::steady_clock::now();
         const GLayer& g = m.layers[li];
+        const u64 L = li + 1;  // the garbler's layer index (stream ids / hardened tweak gates)
         if (g.p.count("in_src")) cur = saved[g.param("in_src") + 1];
         const i64 Nin = cur[0].N;
         switch (g.kind) {
@@ -108,7 +124,8 @@ CrtLabels cpu_evaluate(const GarbledModel& m, const CrtLabels& inputs, int nt, s
                     const int p = crt[j];
                     const ModInfo& mi = mod_info(p);
                     const comp_t* Zp = Z.get(p);
-                    const comp_t* bias = g.arr(arr_name("bias.", j, "")).ptr<comp_t>();
+                    std::vector<comp_t> zb;
+                    const comp_t* bias = zeros_or(g, arr_name("bias.", j, ""), hard, static_cast<size_t>(out) * mi.n, zb);
                     Labels O(p, out);
                     const Labels& I = cur[j];
                     parallel_for(out, [&](i64 b0, i64 b1) {
@@ -145,7 +162,8 @@ CrtLabels cpu_evaluate(const GarbledModel& m, const CrtLabels& inputs, int nt, s
                     const int p = crt[j];
                     const ModInfo& mi = mod_info(p);
                     const comp_t* Zp = Z.get(p);
-                    const comp_t* bias = g.arr(arr_name("bias.", j, "")).ptr<comp_t>();
+                    std::vector<comp_t> zb;
+                    const comp_t* bias = zeros_or(g, arr_name("bias.", j, ""), hard, static_cast<size_t>(G.F) * mi.n, zb);
                     // weights reduced mod p once
                     std::vector<int32_t> wm(static_cast<size_t>(G.F * G.K()));
                     std::vector<i64> zc(G.F, 0);
@@ -197,7 +215,8 @@ CrtLabels cpu_evaluate(const GarbledModel& m, const CrtLabels& inputs, int nt, s
                             for (int j = 0; j < k; ++j)
                                 mixed_mult_eval(cur[j].at(e), mod_info(crt[j]), sig_joint.at(e), m2,
                                                 tg.ptr<u128>() + e * tg.shape[1] + prefix[j],
-                                                te.ptr<u128>() + (e * k + j) * 3, nxt[j].at(e));
+                                                te.ptr<u128>() + (e * k + j) * 3, nxt[j].at(e),
+                                                MMTw{hard, stream_id(L, 2, e), j, k, true});
                     }, nt);
                     cur = std::move(nxt);
                     sig_joint = Labels();
@@ -216,10 +235,12 @@ CrtLabels cpu_evaluate(const GarbledModel& m, const CrtLabels& inputs, int nt, s
                         const ModInfo& m2 = mod_info(2);
                         for (i64 e = b0; e < b1; ++e) {
                             for (int j = 0; j < k; ++j) x[j] = cur[j].at(e);
-                            sign_mrs_eval_elem(sp, x.data(), tab.ptr<u128>() + e * tab.shape[1], sig);
+                            sign_mrs_eval_elem(sp, x.data(), tab.ptr<u128>() + e * tab.shape[1], sig, hard,
+                                               stream_id(L, 1, e));
                             for (int j = 0; j < k; ++j)
                                 mixed_mult_eval(x[j], mod_info(crt[j]), sig, m2, tg.ptr<u128>() + e * tg.shape[1] + prefix[j],
-                                                te.ptr<u128>() + (e * k + j) * 3, nxt[j].at(e));
+                                                te.ptr<u128>() + (e * k + j) * 3, nxt[j].at(e),
+                                                MMTw{hard, stream_id(L, 2, e), j, k, true});
                         }
                     }, nt);
                     cur = std::move(nxt);
@@ -237,7 +258,8 @@ CrtLabels cpu_evaluate(const GarbledModel& m, const CrtLabels& inputs, int nt, s
                             x[j] = cur[j].at(e);
                             y[j] = nxt[j].at(e);
                         }
-                        relu_eval_elem(sp, Z, crt, prefix, x.data(), T, e, y.data());
+                        relu_eval_elem(sp, Z, crt, prefix, x.data(), T, e, y.data(), hard, stream_id(L, 1, e),
+                                       stream_id(L, 2, e));
                     }
                 }, nt);
                 cur = std::move(nxt);
@@ -261,7 +283,8 @@ CrtLabels cpu_evaluate(const GarbledModel& m, const CrtLabels& inputs, int nt, s
                         }
                         sign_eval_elem(sp, Z, x.data(), ap.ptr<u128>() + e * ap.shape[1],
                                        c1 ? c1->ptr<u128>() + e * c1->shape[1] : nullptr,
-                                       c2.ptr<u128>() + e * c2.shape[1], sg.ptr<u128>() + e * sg.shape[1], y.data());
+                                       c2.ptr<u128>() + e * c2.shape[1], sg.ptr<u128>() + e * sg.shape[1], y.data(),
+                                       hard, stream_id(L, 1, e));
                     }
                 }, nt);
                 cur = std::move(nxt);
@@ -280,7 +303,7 @@ CrtLabels cpu_evaluate(const GarbledModel& m, const CrtLabels& inputs, int nt, s
                         for (i64 e = b0; e < b1; ++e) {
                             for (int j = 0; j < k; ++j) Lp[j] = cur[j].at(e);
                             rescale_mrs_eval_elem(P, Lp.data(), tab.ptr<u128>() + e * P.n_tab,
-                                                  so ? sig_joint.at(e) : nullptr);
+                                                  so ? sig_joint.at(e) : nullptr, hard, stream_id(L, 30, e));
                         }
                     }, nt);
                     break;
@@ -321,10 +344,11 @@ CrtLabels cpu_evaluate(const GarbledModel& m, const CrtLabels& inputs, int nt, s
                                                   ap->ptr<u128>() + e * ap->shape[1],
                                                   c1 ? c1->ptr<u128>() + e * c1->shape[1] : nullptr,
                                                   c2->ptr<u128>() + e * c2->shape[1], sg->ptr<u128>() + e * sg->shape[1],
-                                                  nullptr);
+                                                  nullptr, hard, stream_id(L, 10 + it, e));
                             else
                                 rescale_eval_elem(P, Z, Lp.data(), up.data(), dn.data(), tr.ptr<u128>() + e * P.n_trans,
-                                                  nullptr, nullptr, nullptr, nullptr, be->ptr<u128>() + e * P.n_be);
+                                                  nullptr, nullptr, nullptr, nullptr, be->ptr<u128>() + e * P.n_be, hard,
+                                                  stream_id(L, 10 + it, e));
                         }
                     }, nt);
                 }
@@ -375,7 +399,8 @@ CrtLabels cpu_evaluate(const GarbledModel& m, const CrtLabels& inputs, int nt, s
                                 x[j] = diff[j].data();
                                 y[j] = nv[j].at(o * cnt1 + q);
                             }
-                            relu_eval_elem(sp, Z, crt, prefix, x.data(), T, e, y.data());
+                            relu_eval_elem(sp, Z, crt, prefix, x.data(), T, e, y.data(), hard,
+                                           stream_id(L, 20 + 2 * lv, e), stream_id(L, 21 + 2 * lv, e));
                             for (int j = 0; j < k; ++j) lab_add(y[j], vals[j].at(o * cnt + 2 * q), vals[j].n, vals[j].p);
                         }
                     }, nt);
@@ -427,7 +452,8 @@ CrtLabels cpu_evaluate(const GarbledModel& m, const CrtLabels& inputs, int nt, s
                         for (int j = 0; j < k; ++j) {
                             const ModInfo& mi = mod_info(static_cast<int>(inm[j]));
                             eval_proj(cur[j].at(e), mi, g.arr(arr_name("t.", j, "")).ptr<u128>() + e * mi.p,
-                                      mod_info(static_cast<int>(outm[j])), nxt[j].at(e));
+                                      mod_info(static_cast<int>(outm[j])), nxt[j].at(e), 1,
+                                      Mask{hard, stream_id(L, 1, e), tw_sub(TW_PROJ, j), 0});
                         }
                 }, nt);
                 cur = std::move(nxt);
@@ -444,7 +470,7 @@ CrtLabels cpu_evaluate(const GarbledModel& m, const CrtLabels& inputs, int nt, s
                         for (int j = 0; j < k; ++j)
                             gen_mult_eval(cur[j].at(2 * e), cur[j].at(2 * e + 1), mod_info(crt[j]),
                                           ga.ptr<u128>() + e * sum_crt + prefix[j], ea.ptr<u128>() + e * sum_crt + prefix[j],
-                                          nxt[j].at(e));
+                                          nxt[j].at(e), hard, stream_id(L, 1, e), j);
                 }, nt);
                 cur = std::move(nxt);
                 break;
@@ -463,9 +489,11 @@ CrtLabels cpu_evaluate(const GarbledModel& m, const CrtLabels& inputs, int nt, s
                     for (i64 e = b0; e < b1; ++e)
                         for (int j = 0; j < k; ++j) {
                             const ModInfo& mp = mod_info(crt[j]);
-                            eval_proj(cur[j].at(2 * e + 1), mp, ta.ptr<u128>() + e * sum_crt + prefix[j], mq, t0.data());
+                            eval_proj(cur[j].at(2 * e + 1), mp, ta.ptr<u128>() + e * sum_crt + prefix[j], mq, t0.data(),
+                                      1, Mask{hard, stream_id(L, 1, e), tw_sub(TW_MMT, j), 0});
                             mixed_mult_eval(cur[j].at(2 * e), mp, t0.data(), mq, ga.ptr<u128>() + e * sum_crt + prefix[j],
-                                            ea.ptr<u128>() + (e * k + j) * (q + 1), nxt[j].at(e));
+                                            ea.ptr<u128>() + (e * k + j) * (q + 1), nxt[j].at(e),
+                                            MMTw{hard, stream_id(L, 1, e), j, k, false});
                         }
                 }, nt);
                 cur = std::move(nxt);
@@ -481,7 +509,7 @@ CrtLabels cpu_evaluate(const GarbledModel& m, const CrtLabels& inputs, int nt, s
                     for (i64 e = b0; e < b1; ++e) {
                         for (int j = 0; j < k; ++j) Lp[j] = cur[j].at(e);
                         for (int xi : P.extra_idx) std::memcpy(Lp[xi], Z.get(crt[xi]), sizeof(comp_t) * nr_comps(crt[xi]));
-                        be_eval_elem(P, Lp.data(), be.ptr<u128>() + e * P.n_tab);
+                        be_eval_elem(P, Lp.data(), be.ptr<u128>() + e * P.n_tab, hard, stream_id(L, 1, e));
                     }
                 }, nt);
                 break;

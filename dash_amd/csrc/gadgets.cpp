@@ -102,7 +102,7 @@ namespace {
 // k*t digit labels (residue-major, modulus digit_mod(d)), then per digit
 // d = t-1..1 the carry label (modulus carry_mod(d)), then the outputs.
 void sign_garble_fused(const SignPlan& P, const LabelBank& R, const Prg& prg, u64 stream, const comp_t* const* in0,
-                       u128* approx, u128* cast2, u128* sign, comp_t* const* out0) {
+                       u128* approx, u128* cast2, u128* sign, comp_t* const* out0, bool hard) {
     const int k = static_cast<int>(P.crt.size()), t = static_cast<int>(P.mrs.size());
     const int W = P.max_n;
     comp_t* base = sign_scratch().get(static_cast<size_t>(W) * (k * t + 3));
@@ -117,12 +117,12 @@ void sign_garble_fused(const SignPlan& P, const LabelBank& R, const Prg& prg, u6
     for (int j = 0; j < k; ++j) {
         const ModInfo& mi = mod_info(P.crt[j]);
         const auto& lut = P.lookup[j];
-        proj_keys(in0[j], R.get(mi.p), mi, K);
+        proj_keys(in0[j], R.get(mi.p), mi, K, hard);
         for (int d = 0; d < t; ++d) {
             const ModInfo& mo = mod_info(P.digit_mod(d));
             garble_proj_keys(K, dig + static_cast<size_t>(W) * (j * t + d), R.get(mo.p), mo,
                              [&](int v) { return static_cast<i64>(lut[static_cast<size_t>(v) * t + d]); },
-                             approx + t * P.crt_prefix[j] + d, t);
+                             approx + t * P.crt_prefix[j] + d, t, Mask{hard, stream, tw_sub(TW_APPROX, j), d});
         }
     }
     bool have_carry = false;
@@ -136,7 +136,8 @@ void sign_garble_fused(const SignPlan& P, const LabelBank& R, const Prg& prg, u6
         const ModInfo& mn = mod_info(P.carry_mod(d));
         draw(prg, stream, ctr, mn.p, newc);
         garble_proj(sum, R.get(mo.p), mo, newc, R.get(mn.p), mn,
-                    [m, mprev](int v) { return static_cast<i64>((v / m) % mprev); }, cast2 + c2);
+                    [m, mprev](int v) { return static_cast<i64>((v / m) % mprev); }, cast2 + c2, 1,
+                    Mask{hard, stream, tw_sub(TW_CAST2, d), 0});
         c2 += mo.p;
         std::memcpy(carry, newc, sizeof(comp_t) * mn.n);
         have_carry = true;
@@ -151,12 +152,13 @@ void sign_garble_fused(const SignPlan& P, const LabelBank& R, const Prg& prg, u6
         draw(prg, stream, ctr, mo.p, out0[o]);
         const int lo = P.lower, up = P.upper;
         garble_proj(sum, R.get(m0.p), m0, out0[o], R.get(mo.p), mo,
-                    [half, lo, up](int v) { return static_cast<i64>(v < half ? up : lo); }, sign + o * m0.p);
+                    [half, lo, up](int v) { return static_cast<i64>(v < half ? up : lo); }, sign + o * m0.p, 1,
+                    Mask{hard, stream, tw_sub(TW_SIGN, 0), static_cast<int>(o)});
     }
 }
 
 void sign_eval_fused(const SignPlan& P, const comp_t* const* in, const u128* approx, const u128* cast2,
-                     const u128* sign, comp_t* const* out) {
+                     const u128* sign, comp_t* const* out, bool hard, u64 gate) {
     const int k = static_cast<int>(P.crt.size()), t = static_cast<int>(P.mrs.size());
     const int W = P.max_n;
     comp_t* base = sign_scratch().get(static_cast<size_t>(W) * (k * t + 3));
@@ -166,6 +168,13 @@ void sign_eval_fused(const SignPlan& P, const comp_t* const* in, const u128* app
     comp_t* newc = sum + W;
     for (int j = 0; j < k; ++j) {
         const ModInfo& mi = mod_info(P.crt[j]);
+        if (hard) {  // one key, t slots of the row's pads
+            PadRow pr(compress(in[j], mi), gate, tw_sub(TW_APPROX, j));
+            const u128* row = approx + t * P.crt_prefix[j] + static_cast<i64>(color_of(in[j], mi.p)) * t;
+            for (int d = 0; d < t; ++d)
+                decompress(row[d] - pr.get(d), dig + static_cast<size_t>(W) * (j * t + d), mod_info(P.digit_mod(d)));
+            continue;
+        }
         for (int d = 0; d < t; ++d)
             eval_proj(in[j], mi, approx + t * P.crt_prefix[j] + d, mod_info(P.digit_mod(d)),
                       dig + static_cast<size_t>(W) * (j * t + d), t);
@@ -178,7 +187,7 @@ void sign_eval_fused(const SignPlan& P, const comp_t* const* in, const u128* app
         else std::memcpy(sum, dig + static_cast<size_t>(W) * d, sizeof(comp_t) * mo.n);
         for (int j = have_carry ? 0 : 1; j < k; ++j) lab_add(sum, dig + static_cast<size_t>(W) * (j * t + d), mo.n, mo.p);
         const ModInfo& mn = mod_info(P.carry_mod(d));
-        eval_proj(sum, mo, cast2 + c2, mn, newc);
+        eval_proj(sum, mo, cast2 + c2, mn, newc, 1, Mask{hard, gate, tw_sub(TW_CAST2, d), 0});
         c2 += mo.p;
         std::memcpy(carry, newc, sizeof(comp_t) * mn.n);
         have_carry = true;
@@ -187,18 +196,26 @@ void sign_eval_fused(const SignPlan& P, const comp_t* const* in, const u128* app
     if (have_carry) std::memcpy(sum, carry, sizeof(comp_t) * m0.n);
     else std::memcpy(sum, dig, sizeof(comp_t) * m0.n);
     for (int j = have_carry ? 0 : 1; j < k; ++j) lab_add(sum, dig + static_cast<size_t>(W) * (j * t), m0.n, m0.p);
-    for (size_t o = 0; o < P.out_mod.size(); ++o)
-        eval_proj(sum, m0, sign + o * m0.p, mod_info(P.out_mod[o]), out[o]);
+    PadRow pr(compress(sum, m0), gate, tw_sub(TW_SIGN, 0));
+    for (size_t o = 0; o < P.out_mod.size(); ++o) {
+        if (hard)
+            decompress(sign[o * m0.p + color_of(sum, m0.p)] - pr.get(static_cast<int>(o)), out[o],
+                       mod_info(P.out_mod[o]));
+        else
+            eval_proj(sum, m0, sign + o * m0.p, mod_info(P.out_mod[o]), out[o]);
+    }
 }
 }  // namespace
 
 void sign_garble_elem(const SignPlan& P, const LabelBank& R, const LabelBank& Z, const Prg& prg, u64 stream,
                       const comp_t* const* in0, u128* approx, u128* cast1, u128* cast2, u128* sign,
-                      comp_t* const* out0) {
+                      comp_t* const* out0, bool hard) {
     if (P.fused) {
-        sign_garble_fused(P, R, prg, stream, in0, approx, cast2, sign, out0);
+        sign_garble_fused(P, R, prg, stream, in0, approx, cast2, sign, out0, hard);
         return;
     }
+    DASH_CHECK(!hard, "the hardened encoding needs the fused sign construction (the reference casts key a "
+                      "projection with the public zero label)");
     const int k = static_cast<int>(P.crt.size()), t = static_cast<int>(P.mrs.size());
     const int W = P.max_n;
     comp_t* base = sign_scratch().get(static_cast<size_t>(W) * (k * t + (k + 1) + 4));
@@ -267,11 +284,12 @@ void sign_garble_elem(const SignPlan& P, const LabelBank& R, const LabelBank& Z,
 }
 
 void sign_eval_elem(const SignPlan& P, const LabelBank& Z, const comp_t* const* in, const u128* approx,
-                    const u128* cast1, const u128* cast2, const u128* sign, comp_t* const* out) {
+                    const u128* cast1, const u128* cast2, const u128* sign, comp_t* const* out, bool hard, u64 gate) {
     if (P.fused) {
-        sign_eval_fused(P, in, approx, cast2, sign, out);
+        sign_eval_fused(P, in, approx, cast2, sign, out, hard, gate);
         return;
     }
+    DASH_CHECK(!hard, "the hardened encoding needs the fused sign construction");
     const int k = static_cast<int>(P.crt.size()), t = static_cast<int>(P.mrs.size());
     const int W = P.max_n;
     comp_t* base = sign_scratch().get(static_cast<size_t>(W) * (k * t + (k + 1) + 4));
@@ -318,7 +336,7 @@ void sign_eval_elem(const SignPlan& P, const LabelBank& Z, const comp_t* const* 
 
 // ---------------------------------------------------------------------------
 void mixed_mult_garble(const comp_t* x0, const ModInfo& mp, const comp_t* y0, const ModInfo& mq, const LabelBank& R,
-                       const Prg& prg, u64 stream, u64& ctr, u128* g, u128* e, comp_t* out0) {
+                       const Prg& prg, u64 stream, u64& ctr, u128* g, u128* e, comp_t* out0, const MMTw& tw) {
     const int p = mp.p, q = mq.p;
     comp_t* sk03 = misc_scratch().get(2 * mp.n);
     comp_t* sk04 = sk03 + mp.n;
@@ -326,43 +344,46 @@ void mixed_mult_garble(const comp_t* x0, const ModInfo& mp, const comp_t* y0, co
     draw(prg, stream, ctr, p, sk03);
     draw(prg, stream, ctr, p, sk04);
     // garbler half gate: x -> x*r
-    garble_proj(x0, R.get(p), mp, sk03, R.get(p), mp, [r](int v) { return static_cast<i64>(v) * r; }, g);
+    garble_proj(x0, R.get(p), mp, sk03, R.get(p), mp, [r](int v) { return static_cast<i64>(v) * r; }, g, 1, tw.g());
     // evaluator half gate: y -> -(y + r), payload offset is x0
-    garble_proj(y0, R.get(q), mq, sk04, x0, mp, [r, p](int v) { return pmod(-(v + r), p); }, e);
+    garble_proj(y0, R.get(q), mq, sk04, x0, mp, [r, p](int v) { return pmod(-(v + r), p); }, e, 1, tw.e());
     // mini gate: y -> (y + r) mod p
-    garble_proj_mini(y0, R.get(q), mq, [r, p](int v) { return pmod(v + r, p); }, e + q);
+    garble_proj_mini(y0, R.get(q), mq, [r, p](int v) { return pmod(v + r, p); }, e + q, tw.mini(), tw.lane());
     std::memcpy(out0, sk04, sizeof(comp_t) * mp.n);
     lab_sub(out0, sk03, mp.n, p);
 }
 
 void mixed_mult_eval(const comp_t* x, const ModInfo& mp, const comp_t* y, const ModInfo& mq, const u128* g,
-                     const u128* e, comp_t* out) {
+                     const u128* e, comp_t* out, const MMTw& tw) {
     comp_t* gl = misc_scratch().get(mp.n);
-    eval_proj(x, mp, g, mp, gl);
-    eval_proj(y, mq, e, mp, out);
-    const i64 ypr = pmod(eval_proj_mini(y, mq, e + mq.p), mp.p);
+    eval_proj(x, mp, g, mp, gl, 1, tw.g());
+    eval_proj(y, mq, e, mp, out, 1, tw.e());
+    const i64 ypr = pmod(eval_proj_mini(y, mq, e + mq.p, tw.mini(), tw.lane()), mp.p);
     lab_axpy(out, ypr, x, mp.n, mp.p);
     lab_sub(out, gl, mp.n, mp.p);
 }
 
 void gen_mult_garble(const comp_t* x0, const comp_t* y0, const ModInfo& mp, const LabelBank& R, const Prg& prg,
-                     u64 stream, u64& ctr, u128* g, u128* e, comp_t* out0) {
+                     u64 stream, u64& ctr, u128* g, u128* e, comp_t* out0, bool hard, int j) {
     const int p = mp.p;
     comp_t* sk03 = misc_scratch().get(2 * mp.n);
     comp_t* sk04 = sk03 + mp.n;
     const i64 r = y0[0];
     draw(prg, stream, ctr, p, sk03);
     draw(prg, stream, ctr, p, sk04);
-    garble_proj(x0, R.get(p), mp, sk03, R.get(p), mp, [r](int v) { return static_cast<i64>(v) * r; }, g);
-    garble_proj(y0, R.get(p), mp, sk04, x0, mp, [r, p](int v) { return pmod(-(v + r), p); }, e);
+    garble_proj(x0, R.get(p), mp, sk03, R.get(p), mp, [r](int v) { return static_cast<i64>(v) * r; }, g, 1,
+                Mask{hard, stream, tw_sub(TW_MMG, j), 0});
+    garble_proj(y0, R.get(p), mp, sk04, x0, mp, [r, p](int v) { return pmod(-(v + r), p); }, e, 1,
+                Mask{hard, stream, tw_sub(TW_GME, j), 0});
     std::memcpy(out0, sk04, sizeof(comp_t) * mp.n);
     lab_sub(out0, sk03, mp.n, p);
 }
 
-void gen_mult_eval(const comp_t* x, const comp_t* y, const ModInfo& mp, const u128* g, const u128* e, comp_t* out) {
+void gen_mult_eval(const comp_t* x, const comp_t* y, const ModInfo& mp, const u128* g, const u128* e, comp_t* out,
+                   bool hard, u64 gate, int j) {
     comp_t* gl = misc_scratch().get(mp.n);
-    eval_proj(x, mp, g, mp, gl);
-    eval_proj(y, mp, e, mp, out);
+    eval_proj(x, mp, g, mp, gl, 1, Mask{hard, gate, tw_sub(TW_MMG, j), 0});
+    eval_proj(y, mp, e, mp, out, 1, Mask{hard, gate, tw_sub(TW_GME, j), 0});
     lab_axpy(out, color_of(y, mp.p), x, mp.n, mp.p);
     lab_sub(out, gl, mp.n, mp.p);
 }
@@ -401,7 +422,7 @@ BEPlan::BEPlan(const std::vector<int>& mod, const std::vector<int>& ext) : modul
 }
 
 void be_garble_elem(const BEPlan& P, const LabelBank& R, const Prg& prg, u64 stream, u64& ctr, comp_t* const* L,
-                    u128* tab) {
+                    u128* tab, bool hard) {
     const int E = static_cast<int>(P.moduli.size());
     // l_w: working copies in swapped order; only the extra residues are
     // written back (non-extended residues stay untouched, as in the reference)
@@ -420,7 +441,7 @@ void be_garble_elem(const BEPlan& P, const LabelBank& R, const Prg& prg, u64 str
             const ModInfo& mo = mod_info(P.swapped[tg]);
             draw(prg, stream, ctr, mo.p, out0);
             garble_proj(lw[i], R.get(mi.p), mi, out0, R.get(mo.p), mo, [](int v) { return static_cast<i64>(v); },
-                        tab + off);
+                        tab + off, 1, Mask{hard, stream, tw_sub(TW_BE, i), j});
             off += mi.p;
             lab_sub(lw[tg], out0, mo.n, mo.p);
             lab_scale(lw[tg], P.inv_partial[i][j], mo.n, mo.p);
@@ -433,7 +454,7 @@ void be_garble_elem(const BEPlan& P, const LabelBank& R, const Prg& prg, u64 str
     }
 }
 
-void be_eval_elem(const BEPlan& P, comp_t* const* L, const u128* tab) {
+void be_eval_elem(const BEPlan& P, comp_t* const* L, const u128* tab, bool hard, u64 gate) {
     const int E = static_cast<int>(P.moduli.size());
     comp_t* work = be_scratch().get(static_cast<size_t>(128) * E);
     std::vector<comp_t*> lw(E);
@@ -448,7 +469,7 @@ void be_eval_elem(const BEPlan& P, comp_t* const* L, const u128* tab) {
         for (int j = 0; j < E - i - 1; ++j) {
             const int tg = i + j + 1;
             const ModInfo& mo = mod_info(P.swapped[tg]);
-            eval_proj(lw[i], mi, tab + off, mo, pr);
+            eval_proj(lw[i], mi, tab + off, mo, pr, 1, Mask{hard, gate, tw_sub(TW_BE, i), j});
             off += mi.p;
             lab_sub(lw[tg], pr, mo.n, mo.p);
             lab_scale(lw[tg], P.inv_partial[i][j], mo.n, mo.p);
@@ -497,8 +518,10 @@ RescalePlan::RescalePlan(const std::vector<int>& crt_, const std::vector<int>& m
 
 void rescale_garble_elem(const RescalePlan& P, const LabelBank& R, const LabelBank& Z, const Prg& prg, u64 stream,
                          comp_t* const* L, const comp_t* const* up_base, const comp_t* const* down_base, u128* trans,
-                         u128* s_approx, u128* s_cast1, u128* s_cast2, u128* s_sign, u128* be) {
+                         u128* s_approx, u128* s_cast1, u128* s_cast2, u128* s_sign, u128* be, bool hard) {
     const int k = static_cast<int>(P.crt.size());
+    DASH_CHECK(!hard || !P.sign_be, "the hardened encoding has no legacy (sign base extension) rescale: its sign "
+                                    "gadget keys a projection with the public zero label; use the mixed-radix rescale");
     for (int j = 0; j < k; ++j) lab_add(L[j], up_base[j], nr_comps(P.crt[j]), P.crt[j]);
     comp_t* out0 = rescale_scratch().get(128);
     u64 ctr = 0;
@@ -512,7 +535,7 @@ void rescale_garble_elem(const RescalePlan& P, const LabelBank& R, const LabelBa
             const ModInfo& mj = mod_info(P.crt[j]);
             draw(prg, stream, ctr, mj.p, out0);
             garble_proj(L[fi], R.get(s), ms, out0, R.get(mj.p), mj, [](int v) { return static_cast<i64>(v); },
-                        trans + off);
+                        trans + off, 1, Mask{hard, stream, tw_sub(TW_TRANS, static_cast<uint32_t>(f)), static_cast<int>(a)});
             off += s;
             lab_sub(L[j], out0, mj.n, mj.p);
             lab_scale(L[j], P.inv[f][a], mj.n, mj.p);
@@ -525,15 +548,16 @@ void rescale_garble_elem(const RescalePlan& P, const LabelBank& R, const LabelBa
         sign_garble_elem(P.sign, R, Z, prg, stream ^ (1ull << 43), L, s_approx, s_cast1, s_cast2, s_sign, outs);
         std::memcpy(L[0], sig, sizeof(comp_t) * nr_comps(2));
     } else {
-        be_garble_elem(P.be, R, prg, stream, ctr, L, be);
+        be_garble_elem(P.be, R, prg, stream, ctr, L, be, hard);
     }
     for (int j = 0; j < k; ++j) lab_sub(L[j], down_base[j], nr_comps(P.crt[j]), P.crt[j]);
 }
 
 void rescale_eval_elem(const RescalePlan& P, const LabelBank& Z, comp_t* const* L, const comp_t* const* up,
                        const comp_t* const* down, const u128* trans, const u128* s_approx, const u128* s_cast1,
-                       const u128* s_cast2, const u128* s_sign, const u128* be) {
+                       const u128* s_cast2, const u128* s_sign, const u128* be, bool hard, u64 gate) {
     const int k = static_cast<int>(P.crt.size());
+    DASH_CHECK(!hard || !P.sign_be, "the hardened encoding has no legacy (sign base extension) rescale");
     for (int j = 0; j < k; ++j) lab_add(L[j], up[j], nr_comps(P.crt[j]), P.crt[j]);
     comp_t* pr = rescale_scratch().get(128);
     i64 off = 0;
@@ -544,7 +568,8 @@ void rescale_eval_elem(const RescalePlan& P, const LabelBank& Z, comp_t* const* 
         for (size_t a = 0; a < P.active[f].size(); ++a) {
             const int j = P.active[f][a];
             const ModInfo& mj = mod_info(P.crt[j]);
-            eval_proj(L[fi], ms, trans + off, mj, pr);
+            eval_proj(L[fi], ms, trans + off, mj, pr, 1,
+                      Mask{hard, gate, tw_sub(TW_TRANS, static_cast<uint32_t>(f)), static_cast<int>(a)});
             off += s;
             lab_sub(L[j], pr, mj.n, mj.p);
             lab_scale(L[j], P.inv[f][a], mj.n, mj.p);
@@ -557,7 +582,7 @@ void rescale_eval_elem(const RescalePlan& P, const LabelBank& Z, comp_t* const* 
         sign_eval_elem(P.sign, Z, L, s_approx, s_cast1, s_cast2, s_sign, outs);
         std::memcpy(L[0], sig, sizeof(comp_t) * nr_comps(2));
     } else {
-        be_eval_elem(P.be, L, be);
+        be_eval_elem(P.be, L, be, hard, gate);
     }
     for (int j = 0; j < k; ++j) lab_sub(L[j], down[j], nr_comps(P.crt[j]), P.crt[j]);
 }
@@ -617,7 +642,7 @@ i64 RescaleMrsPlan::final_fn(int j, i64 v) const {
 }
 
 void rescale_mrs_garble_elem(const RescaleMrsPlan& P, const LabelBank& R, const Prg& prg, u64 stream,
-                             comp_t* const* L, u128* tab, comp_t* sig) {
+                             comp_t* const* L, u128* tab, comp_t* sig, bool hard) {
     const int k = P.k();
     constexpr int W = 128;
     // draws, PRG counter order: digit i's target labels (t = 0..k-1-i), then the k final output labels
@@ -659,18 +684,19 @@ void rescale_mrs_garble_elem(const RescaleMrsPlan& P, const LabelBank& R, const 
     s = 0;
     for (int i = 0; i < k; ++i) {
         const ModInfo& mi = mod_info(P.crt[P.ord[i]]);
-        proj_keys(key[P.ord[i]], R.get(mi.p), mi, K);
+        proj_keys(key[P.ord[i]], R.get(mi.p), mi, K, hard);
         const int nt = P.targets(i);
         for (int t = 0; t < nt; ++t, ++s) {
             const ModInfo& mo = mod_info(P.target_mod(i, t));
             garble_proj_keys(K, dig[s], R.get(mo.p), mo, [&](int v) { return P.digit_fn(i, t, v); },
-                             tab + P.dig_off[i] + t, nt);
+                             tab + P.dig_off[i] + t, nt, Mask{hard, stream, tw_sub(TW_MRS, i), t});
         }
     }
-    proj_keys(acc, R.get(mT.p), mT, K);
+    proj_keys(acc, R.get(mT.p), mT, K, hard);
     for (int j = 0; j < k; ++j) {
         const ModInfo& mo = mod_info(P.crt[j]);
-        garble_proj_keys(K, fin[j], R.get(mo.p), mo, [&](int v) { return P.final_fn(j, v); }, tab + P.fin_off + j, k);
+        garble_proj_keys(K, fin[j], R.get(mo.p), mo, [&](int v) { return P.final_fn(j, v); }, tab + P.fin_off + j, k,
+                         Mask{hard, stream, tw_sub(TW_MRS, k), j});
     }
     // output base labels: Y_j = S^-1 L_j + fin_j (j >= 1), Y_0 = fin_0
     std::memcpy(L[0], fin[0], sizeof(comp_t) * nr_comps(2));
@@ -681,7 +707,8 @@ void rescale_mrs_garble_elem(const RescaleMrsPlan& P, const LabelBank& R, const 
     }
 }
 
-void rescale_mrs_eval_elem(const RescaleMrsPlan& P, comp_t* const* L, const u128* tab, comp_t* sig) {
+void rescale_mrs_eval_elem(const RescaleMrsPlan& P, comp_t* const* L, const u128* tab, comp_t* sig, bool hard,
+                           u64 gate) {
     const int k = P.k();
     constexpr int W = 128;
     comp_t* buf = rescale_scratch().get(static_cast<size_t>(W) * (k + 2));
@@ -697,23 +724,27 @@ void rescale_mrs_eval_elem(const RescaleMrsPlan& P, comp_t* const* L, const u128
     for (int i = 0; i < k; ++i) {
         const int r0 = P.ord[i];
         const ModInfo& mi = mod_info(P.crt[r0]);
-        const u128 h = hash(compress(key[r0], mi));
+        const u128 kc = compress(key[r0], mi);
+        const u128 h = hard ? 0 : hash(kc);
+        PadRow pads(kc, gate, tw_sub(TW_MRS, i));
         const int nt = P.targets(i);
         const u128* row = tab + P.dig_off[i] + static_cast<i64>(color_of(key[r0], mi.p)) * nt;
         for (int t = 0; t < nt; ++t) {
             const ModInfo& mo = mod_info(P.target_mod(i, t));
-            decompress(row[t] - h, pr, mo);
+            decompress(row[t] - (hard ? pads.get(t) : h), pr, mo);
             if (t == nt - 1) lab_add(acc, pr, mo.n, mo.p);
             else lab_sub(key[P.target_res(i, t)], pr, mo.n, mo.p);
         }
     }
     if (P.sign_last && sig) std::memcpy(sig, key[0], sizeof(comp_t) * nr_comps(2));
-    const u128 h = hash(compress(acc, mT));
+    const u128 kc = compress(acc, mT);
+    const u128 h = hard ? 0 : hash(kc);
+    PadRow pads(kc, gate, tw_sub(TW_MRS, k));
     const u128* row = tab + P.fin_off + static_cast<i64>(color_of(acc, mT.p)) * k;
-    decompress(row[0] - h, L[0], mod_info(2));
+    decompress(row[0] - (hard ? pads.get(0) : h), L[0], mod_info(2));
     for (int j = 1; j < k; ++j) {
         const ModInfo& mo = mod_info(P.crt[j]);
-        decompress(row[j] - h, pr, mo);
+        decompress(row[j] - (hard ? pads.get(j) : h), pr, mo);
         lab_scale(L[j], P.Sinv[j], mo.n, mo.p);
         lab_add(L[j], pr, mo.n, mo.p);
     }
@@ -754,7 +785,7 @@ i64 SignMrsPlan::digit_fn(int i, int t, i64 v) const {
 }
 
 void sign_mrs_garble_elem(const SignMrsPlan& P, const LabelBank& R, const Prg& prg, u64 stream,
-                          const comp_t* const* x0, u128* tab, comp_t* sig0) {
+                          const comp_t* const* x0, u128* tab, comp_t* sig0, bool hard) {
     const int k = P.k();
     constexpr int W = 128;
     int nd = 0;
@@ -782,18 +813,19 @@ void sign_mrs_garble_elem(const SignMrsPlan& P, const LabelBank& R, const Prg& p
     s = 0;
     for (int i = 0; i + 1 < k; ++i) {
         const ModInfo& mi = mod_info(P.crt[P.ord[i]]);
-        proj_keys(key[P.ord[i]], R.get(mi.p), mi, K);
+        proj_keys(key[P.ord[i]], R.get(mi.p), mi, K, hard);
         const int nt = P.targets(i);
         for (int t = 0; t < nt; ++t, ++s) {
             const ModInfo& mo = mod_info(P.crt[P.target_res(i, t)]);
             garble_proj_keys(K, dig[s], R.get(mo.p), mo, [&](int v) { return P.digit_fn(i, t, v); },
-                             tab + P.dig_off[i] + t, nt);
+                             tab + P.dig_off[i] + t, nt, Mask{hard, stream, tw_sub(TW_SMRS, i), t});
         }
     }
     std::memcpy(sig0, key[P.ord[k - 1]], sizeof(comp_t) * nr_comps(2));
 }
 
-void sign_mrs_eval_elem(const SignMrsPlan& P, const comp_t* const* x, const u128* tab, comp_t* sig) {
+void sign_mrs_eval_elem(const SignMrsPlan& P, const comp_t* const* x, const u128* tab, comp_t* sig, bool hard,
+                        u64 gate) {
     const int k = P.k();
     constexpr int W = 128;
     comp_t* buf = sign_scratch().get(static_cast<size_t>(W) * (k + 1));
@@ -806,13 +838,15 @@ void sign_mrs_eval_elem(const SignMrsPlan& P, const comp_t* const* x, const u128
     for (int i = 0; i + 1 < k; ++i) {
         const int r0 = P.ord[i];
         const ModInfo& mi = mod_info(P.crt[r0]);
-        const u128 h = hash(compress(key[r0], mi));
+        const u128 kc = compress(key[r0], mi);
+        const u128 h = hard ? 0 : hash(kc);
+        PadRow pads(kc, gate, tw_sub(TW_SMRS, i));
         const int nt = P.targets(i);
         const u128* row = tab + P.dig_off[i] + static_cast<i64>(color_of(key[r0], mi.p)) * nt;
         for (int t = 0; t < nt; ++t) {
             const int r = P.target_res(i, t);
             const ModInfo& mo = mod_info(P.crt[r]);
-            decompress(row[t] - h, pr, mo);
+            decompress(row[t] - (hard ? pads.get(t) : h), pr, mo);
             lab_sub(key[r], pr, mo.n, mo.p);
         }
     }

@@ -47,31 +47,45 @@ ProjScratch& proj_scratch();
 // Colors and hashes of the p keys in0 + i*Rin of one input label; shared by
 // every projection of that label (the approx step projects one residue label
 // into all t MRS digits: one key schedule instead of t).
+// The keys of one projection row: kc[i] = compress(in0 + i*Rin), hc[i] = H(kc[i]) (reference masks), and
+// per key the hardened pads of the row's tweak, one block at a time (pads of a fan-out row's slots)
 struct ProjKeys {
     std::vector<comp_t> key;
     std::vector<u128> kc, hc;
     std::vector<int> colors;
+    std::vector<PadRow> pads;
+    bool hard = false;
+    // mask of key i for mask m (m.hard: pad m.slot of (kc[i], m.gate, m.sub))
+    u128 mask(int i, const Mask& m) {
+        if (!m.hard) return hc[i];
+        PadRow& r = pads[i];
+        if (r.gate != m.gate || r.sub != m.sub || r.blk < 0) r = PadRow(kc[i], m.gate, m.sub);
+        return r.get(m.slot);
+    }
 };
-inline void proj_keys(const comp_t* in0, const comp_t* Rin, const ModInfo& mi, ProjKeys& K) {
+// hard: skip the reference hashes (hardened rows use the pads only)
+inline void proj_keys(const comp_t* in0, const comp_t* Rin, const ModInfo& mi, ProjKeys& K, bool hard = false) {
     const int pin = mi.p, nin = mi.n;
     K.key.assign(in0, in0 + nin);
     K.kc.resize(pin);
     K.hc.resize(pin);
     K.colors.resize(pin);
+    K.hard = hard;
     for (int i = 0; i < pin; ++i) {
         K.kc[i] = compress(K.key.data(), mi);
         K.colors[i] = K.key[0];
         lab_add(K.key.data(), Rin, nin, pin);
     }
-    hash_batch(K.kc.data(), K.hc.data(), pin);
+    if (hard) K.pads.assign(pin, PadRow());
+    else hash_batch(K.kc.data(), K.hc.data(), pin);
 }
 
-// table[color(in0 + i*Rin) * stride] = compress(out0 + f(i)*outR) + H(compress(in0 + i*Rin))
+// table[color(in0 + i*Rin) * stride] = compress(out0 + f(i)*outR) + mask(compress(in0 + i*Rin))
 template <class F>
-inline void garble_proj_keys(const ProjKeys& K, const comp_t* out0, const comp_t* outR, const ModInfo& mo, F&& f,
-                             u128* table, int stride = 1) {
+inline void garble_proj_keys(ProjKeys& K, const comp_t* out0, const comp_t* outR, const ModInfo& mo, F&& f,
+                             u128* table, int stride = 1, const Mask& mk = Mask()) {
     ProjScratch& s = proj_scratch();
-    const int pin = static_cast<int>(K.hc.size());
+    const int pin = static_cast<int>(K.kc.size());
     s.payc.resize(mo.p);
     s.have.assign(mo.p, 0);
     s.tmp.resize(mo.n);
@@ -82,7 +96,7 @@ inline void garble_proj_keys(const ProjKeys& K, const comp_t* out0, const comp_t
             s.payc[c] = compress(s.tmp.data(), mo);
             s.have[c] = 1;
         }
-        table[static_cast<i64>(K.colors[i]) * stride] = s.payc[c] + K.hc[i];
+        table[static_cast<i64>(K.colors[i]) * stride] = s.payc[c] + K.mask(i, mk);
     }
 }
 
@@ -90,21 +104,27 @@ ProjKeys& proj_keys_scratch();
 
 template <class F>
 inline void garble_proj(const comp_t* in0, const comp_t* Rin, const ModInfo& mi, const comp_t* out0,
-                        const comp_t* outR, const ModInfo& mo, F&& f, u128* table, int stride = 1) {
+                        const comp_t* outR, const ModInfo& mo, F&& f, u128* table, int stride = 1,
+                        const Mask& mk = Mask()) {
     ProjKeys& K = proj_keys_scratch();
-    proj_keys(in0, Rin, mi, K);
-    garble_proj_keys(K, out0, outR, mo, std::forward<F>(f), table, stride);
+    proj_keys(in0, Rin, mi, K, mk.hard);
+    garble_proj_keys(K, out0, outR, mo, std::forward<F>(f), table, stride, mk);
 }
 
+// Mini projection: 16-bit payloads t16[color] = f(i) + mask16. Reference: the low 16 bits of H(K), the same
+// hash the key's full-entry projection uses (projection_gate_mini.h); hardened: lane `lane` (16 bits) of the
+// pad of mk.slot, a slot no full entry of the row uses.
 template <class F>
-inline void garble_proj_mini(const comp_t* in0, const comp_t* Rin, const ModInfo& mi, F&& f, u128* entry) {
+inline void garble_proj_mini(const comp_t* in0, const comp_t* Rin, const ModInfo& mi, F&& f, u128* entry,
+                             const Mask& mk = Mask(), int lane = 0) {
     ProjScratch& s = proj_scratch();
     const int pin = mi.p, nin = mi.n;
     DASH_CHECK(pin <= 8, "mini projection supports input moduli <= 8");
     s.key.assign(in0, in0 + nin);
     int16_t* t16 = reinterpret_cast<int16_t*>(entry);
     for (int i = 0; i < pin; ++i) {
-        u128 h = hash(compress(s.key.data(), mi));
+        const u128 kc = compress(s.key.data(), mi);
+        const u128 h = mk.hard ? (hard_pad(kc, mk.gate, mk.sub, mk.slot) >> (16 * lane)) : hash(kc);
         int color = s.key[0];
         t16[color] = static_cast<int16_t>(static_cast<int16_t>(f(i)) + static_cast<int16_t>(static_cast<uint16_t>(h)));
         lab_add(s.key.data(), Rin, nin, pin);
@@ -113,15 +133,18 @@ inline void garble_proj_mini(const comp_t* in0, const comp_t* Rin, const ModInfo
 
 inline int color_of(const comp_t* L, int p) { return static_cast<int>(static_cast<uint16_t>(L[0]) % static_cast<unsigned>(p)); }
 
-// out = decompress(T[color(in) * stride] - H(compress(in)))
+// out = decompress(T[color(in) * stride] - mask(compress(in)))
 inline void eval_proj(const comp_t* in, const ModInfo& mi, const u128* table, const ModInfo& mo, comp_t* out,
-                      int stride = 1) {
-    u128 h = hash(compress(in, mi));
+                      int stride = 1, const Mask& mk = Mask()) {
+    const u128 kc = compress(in, mi);
+    const u128 h = mk.hard ? hard_pad(kc, mk.gate, mk.sub, mk.slot) : hash(kc);
     decompress(table[static_cast<i64>(color_of(in, mi.p)) * stride] - h, out, mo);
 }
 
-inline int16_t eval_proj_mini(const comp_t* in, const ModInfo& mi, const u128* entry) {
-    u128 h = hash(compress(in, mi));
+inline int16_t eval_proj_mini(const comp_t* in, const ModInfo& mi, const u128* entry, const Mask& mk = Mask(),
+                              int lane = 0) {
+    const u128 kc = compress(in, mi);
+    const u128 h = mk.hard ? (hard_pad(kc, mk.gate, mk.sub, mk.slot) >> (16 * lane)) : hash(kc);
     const int16_t* t16 = reinterpret_cast<const int16_t*>(entry);
     return static_cast<int16_t>(t16[color_of(in, mi.p)] - static_cast<int16_t>(static_cast<uint16_t>(h)));
 }
@@ -168,24 +191,43 @@ std::vector<std::vector<int16_t>> gen_approx_lookup(const std::vector<int>& crt,
 
 // Garbler: in0[j] = base label of residue j (mod crt[j]); out0[o] receives the
 // output base label for out_mod[o].
+// hard: hardened masks (core.h Mask) with gate = the gadget's PRG stream `stream` (the evaluator passes the
+// same value as `gate`); the hardened encoding needs the fused construction (no constant-keyed carry cast)
 void sign_garble_elem(const SignPlan& P, const LabelBank& R, const LabelBank& Z, const Prg& prg, u64 stream,
                       const comp_t* const* in0, u128* approx, u128* cast1, u128* cast2, u128* sign,
-                      comp_t* const* out0);
+                      comp_t* const* out0, bool hard = false);
 void sign_eval_elem(const SignPlan& P, const LabelBank& Z, const comp_t* const* in, const u128* approx,
-                    const u128* cast1, const u128* cast2, const u128* sign, comp_t* const* out);
+                    const u128* cast1, const u128* cast2, const u128* sign, comp_t* const* out, bool hard = false,
+                    u64 gate = 0);
 
 // ---------------------------------------------------------------------------
 // Mixed-modulus half gate x (mod p) * y (mod q), q <= 8. Tables: g[p], e[q+1].
 // ---------------------------------------------------------------------------
+// Hardened tweaks of one mixed half gate (gate = the gadget's PRG stream): the garbler half's key x_j is row
+// (TW_MMG, j); the evaluator half's key y is row (TW_MMY, 0) shared by the k residues of a ReLU (shared_y:
+// residue j's entry at slot j, its mini at lane j % 8 of slot k + j / 8), or row (TW_MMY, j) of its own
+// (entry at slot 0, mini at lane 0 of slot 1)
+struct MMTw {
+    bool hard = false;
+    u64 gate = 0;
+    int j = 0, k = 1;
+    bool shared_y = true;
+    Mask g() const { return Mask{hard, gate, tw_sub(TW_MMG, j), 0}; }
+    Mask e() const { return Mask{hard, gate, tw_sub(TW_MMY, shared_y ? 0 : j), shared_y ? j : 0}; }
+    Mask mini() const { return Mask{hard, gate, tw_sub(TW_MMY, shared_y ? 0 : j), shared_y ? k + j / 8 : 1}; }
+    int lane() const { return shared_y ? j % 8 : 0; }
+};
 void mixed_mult_garble(const comp_t* x0, const ModInfo& mp, const comp_t* y0, const ModInfo& mq,
-                       const LabelBank& R, const Prg& prg, u64 stream, u64& ctr, u128* g, u128* e, comp_t* out0);
+                       const LabelBank& R, const Prg& prg, u64 stream, u64& ctr, u128* g, u128* e, comp_t* out0,
+                       const MMTw& tw = MMTw());
 void mixed_mult_eval(const comp_t* x, const ModInfo& mp, const comp_t* y, const ModInfo& mq, const u128* g,
-                     const u128* e, comp_t* out);
+                     const u128* e, comp_t* out, const MMTw& tw = MMTw());
 
 // Generalized half gate x * y, both mod p. Tables g[p], e[p].
 void gen_mult_garble(const comp_t* x0, const comp_t* y0, const ModInfo& mp, const LabelBank& R, const Prg& prg,
-                     u64 stream, u64& ctr, u128* g, u128* e, comp_t* out0);
-void gen_mult_eval(const comp_t* x, const comp_t* y, const ModInfo& mp, const u128* g, const u128* e, comp_t* out);
+                     u64 stream, u64& ctr, u128* g, u128* e, comp_t* out0, bool hard = false, int j = 0);
+void gen_mult_eval(const comp_t* x, const comp_t* y, const ModInfo& mp, const u128* g, const u128* e, comp_t* out,
+                   bool hard = false, u64 gate = 0, int j = 0);
 
 // ---------------------------------------------------------------------------
 // Base extension (ReDash MRS conversion) per element
@@ -205,8 +247,8 @@ struct BEPlan {
 };
 // L[j] are labels (mod moduli[j]) of one element, updated in place.
 void be_garble_elem(const BEPlan& P, const LabelBank& R, const Prg& prg, u64 stream, u64& ctr, comp_t* const* L,
-                    u128* tab);
-void be_eval_elem(const BEPlan& P, comp_t* const* L, const u128* tab);
+                    u128* tab, bool hard = false);
+void be_eval_elem(const BEPlan& P, comp_t* const* L, const u128* tab, bool hard = false, u64 gate = 0);
 
 // ---------------------------------------------------------------------------
 // Rescale gadget (one iteration) per element.
@@ -233,10 +275,10 @@ struct RescalePlan {
 // (offset-free) shift base labels.
 void rescale_garble_elem(const RescalePlan& P, const LabelBank& R, const LabelBank& Z, const Prg& prg, u64 stream,
                          comp_t* const* L, const comp_t* const* up_base, const comp_t* const* down_base, u128* trans,
-                         u128* s_approx, u128* s_cast1, u128* s_cast2, u128* s_sign, u128* be);
+                         u128* s_approx, u128* s_cast1, u128* s_cast2, u128* s_sign, u128* be, bool hard = false);
 void rescale_eval_elem(const RescalePlan& P, const LabelBank& Z, comp_t* const* L, const comp_t* const* up,
                        const comp_t* const* down, const u128* trans, const u128* s_approx, const u128* s_cast1,
-                       const u128* s_cast2, const u128* s_sign, const u128* be);
+                       const u128* s_cast2, const u128* s_sign, const u128* be, bool hard = false, u64 gate = 0);
 
 // ---------------------------------------------------------------------------
 // Single-shot mixed-radix rescale (the DASH legacy function, new construction)
@@ -299,8 +341,9 @@ struct RescaleMrsPlan {
 // L[j] (one element's labels mod crt[j]) are replaced by the rescaled labels;
 // with sign_last, sig (nullable) receives the mod-2 label of a_{k-1}.
 void rescale_mrs_garble_elem(const RescaleMrsPlan& P, const LabelBank& R, const Prg& prg, u64 stream,
-                             comp_t* const* L, u128* tab, comp_t* sig = nullptr);
-void rescale_mrs_eval_elem(const RescaleMrsPlan& P, comp_t* const* L, const u128* tab, comp_t* sig = nullptr);
+                             comp_t* const* L, u128* tab, comp_t* sig = nullptr, bool hard = false);
+void rescale_mrs_eval_elem(const RescaleMrsPlan& P, comp_t* const* L, const u128* tab, comp_t* sig = nullptr,
+                           bool hard = false, u64 gate = 0);
 
 // ---------------------------------------------------------------------------
 // Exact sign by mixed-radix conversion (a construction of the ReLU/Sign
@@ -331,7 +374,8 @@ struct SignMrsPlan {
 };
 // sign01 base label (mod 2) of one element with residue base labels x0; tables at tab
 void sign_mrs_garble_elem(const SignMrsPlan& P, const LabelBank& R, const Prg& prg, u64 stream,
-                          const comp_t* const* x0, u128* tab, comp_t* sig0);
-void sign_mrs_eval_elem(const SignMrsPlan& P, const comp_t* const* x, const u128* tab, comp_t* sig);
+                          const comp_t* const* x0, u128* tab, comp_t* sig0, bool hard = false);
+void sign_mrs_eval_elem(const SignMrsPlan& P, const comp_t* const* x, const u128* tab, comp_t* sig, bool hard = false,
+                        u64 gate = 0);
 
 }  // namespace dash

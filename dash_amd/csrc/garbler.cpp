@@ -112,6 +112,16 @@ int required_max_modulus(const std::vector<int>& crt, const std::vector<int>& mr
 // ---------------------------------------------------------------------------
 namespace {
 
+// (-v mod M) of every value (the hardened encoding folds public constants c into garbler bases as -c R)
+std::vector<i64> neg_mod(const std::vector<i64>& v, i64 M) {
+    std::vector<i64> r(v.size());
+    for (size_t i = 0; i < v.size(); ++i) r[i] = pmod(-pmod(v[i], M), M);
+    return r;
+}
+
+// whether the GPU garbler produces hardened gadget tables (else hardened gadget layers garble on the host)
+bool gpu_hardened() { return false; }
+
 struct ReluTables {
     Array approx, cast1, cast2, sign, g, e;
 };
@@ -139,20 +149,20 @@ void put_relu_tables(GLayer& g, const std::string& pre, ReluTables& t) {
 // ReLU of one element: x (k residue labels) -> out (k residue labels).
 void relu_garble_elem(const SignPlan& sp, const LabelBank& R, const LabelBank& Z, const Prg& prg, u64 s_stream,
                       u64 m_stream, const std::vector<int>& crt, const std::vector<i64>& prefix,
-                      const comp_t* const* x0, ReluTables& t, i64 e, comp_t* const* out0) {
+                      const comp_t* const* x0, ReluTables& t, i64 e, comp_t* const* out0, bool hard) {
     const int k = static_cast<int>(crt.size());
     comp_t sig[128];
     comp_t* outs[1] = {sig};
     sign_garble_elem(sp, R, Z, prg, s_stream, x0, t.approx.ptr<u128>() + e * sp.n_approx,
                      sp.has_cast1() ? t.cast1.ptr<u128>() + e * t.cast1.shape[1] : nullptr,
                      t.cast2.ptr<u128>() + e * t.cast2.shape[1],
-                     t.sign.ptr<u128>() + e * sp.n_sign, outs);
+                     t.sign.ptr<u128>() + e * sp.n_sign, outs, hard);
     u64 ctr = 0;
     const ModInfo& m2 = mod_info(2);
     for (int j = 0; j < k; ++j) {
         const ModInfo& mp = mod_info(crt[j]);
         mixed_mult_garble(x0[j], mp, sig, m2, R, prg, m_stream, ctr, t.g.ptr<u128>() + e * t.g.shape[1] + prefix[j],
-                          t.e.ptr<u128>() + (e * k + j) * 3, out0[j]);
+                          t.e.ptr<u128>() + (e * k + j) * 3, out0[j], MMTw{hard, m_stream, j, k, true});
     }
 }
 
@@ -342,7 +352,18 @@ GarbledModel Garbler::garble(const std::vector<LayerSpec>& layers, const std::ve
     max_mod_ = std::max(max_mod_, need);
     GarbledModel m;
     const bool fused = opt.fused_sign;
+    const bool hard = opt.hardened;
     m.h.sign_fused = fused ? 1 : 0;
+    m.h.hardened = hard ? 1 : 0;
+    if (hard) {
+        // the hardened encoding keys no projection with a public label (docs/SECURITY.md): the reference's
+        // cast construction (zero-label carry) and the legacy rescale (zero-label residue 0 -> sign gadget) do
+        DASH_CHECK(fused, "the hardened encoding needs the fused sign construction");
+        for (const auto& l : layers)
+            DASH_CHECK(!(l.kind == K_RESCALE && param1(l.p, "mode", 0) == 0 && !opt.rescale_mrs),
+                       "the hardened encoding has no legacy (sign base extension) rescale; use the mixed-radix "
+                       "rescale (rescale_mrs)");
+    }
     m.h.crt = crt_;
     m.h.mrs = mrs_;
     m.h.in_dims = in_dims;
@@ -359,6 +380,7 @@ GarbledModel Garbler::garble(const std::vector<LayerSpec>& layers, const std::ve
         u64 c1 = 0, c2 = 0;
         prg_.label(stream_id(kGlobalLayer, 1, p), c1, p, n, R_.lab[p].data());
         R_.lab[p][0] = 1;
+        if (hard) continue;  // public zero wires have label 0 (nothing shipped)
         prg_.label(stream_id(kGlobalLayer, 2, p), c2, p, n, Z_.lab[p].data());
         Array z(DType::i16, {n});
         std::memcpy(z.ptr<comp_t>(), Z_.lab[p].data(), sizeof(comp_t) * n);
@@ -424,6 +446,11 @@ GarbledModel Garbler::garble(const std::vector<LayerSpec>& layers, const std::ve
             for (int j = 0; j < k; ++j) {
                 const int p = crt_[j], n = nr_comps(p);
                 up_base[j].resize(n);
+                if (hard) {  // the constant wire's base is -(M/2) R, so its label is 0 (not shipped)
+                    std::vector<comp_t> zero(n, 0);
+                    lab_affine(up_base[j].data(), zero.data(), -pmod(M_ / 2, p), R_.get(p), n, p);
+                    continue;
+                }
                 u64 c = 0;
                 prg_.label(stream_id(kGlobalLayer, 110, j), c, p, n, up_base[j].data());
                 Array a(DType::i16, {n});
@@ -440,6 +467,11 @@ GarbledModel Garbler::garble(const std::vector<LayerSpec>& layers, const std::ve
         for (int j = 0; j < k; ++j) {
             const int p = crt_[j], n = nr_comps(p);
             v[j].resize(n);
+            if (hard) {  // base -c R: label 0
+                std::vector<comp_t> zero(n, 0);
+                lab_affine(v[j].data(), zero.data(), -pmod(M_ / (2 * sprod), p), R_.get(p), n, p);
+                continue;
+            }
             u64 c = 0;
             prg_.label(stream_id(kGlobalLayer, 111, (static_cast<u64>(sprod) << 8) | j), c, p, n, v[j].data());
             Array a(DType::i16, {n});
@@ -531,10 +563,11 @@ GarbledModel Garbler::garble(const std::vector<LayerSpec>& layers, const std::ve
                                layers[li + 1].kind == K_RELU && param1(layers[li + 1].p, "in_src", -2) == -2;
         // every layer kind but the test-only projection / mult layers garbles on the device when a GPU garbler
         // is present (the legacy rescale's sign base extension needs residue 0 = 2)
-        const bool on_gpu = gpu && (spec.kind == K_CONV || spec.kind == K_RELU || spec.kind == K_SIGN ||
-                                    spec.kind == K_DENSE || spec.kind == K_SUMPOOL || spec.kind == K_ADD ||
+        const bool lin_kind = spec.kind == K_CONV || spec.kind == K_DENSE || spec.kind == K_SUMPOOL || spec.kind == K_ADD;
+        const bool on_gpu = gpu && (lin_kind || ((!hard || gpu_hardened()) &&
+                                    (spec.kind == K_RELU || spec.kind == K_SIGN ||
                                     spec.kind == K_MAXPOOL || spec.kind == K_MAX || spec.kind == K_BASEEXT ||
-                                    (spec.kind == K_RESCALE && (param1(spec.p, "mode", 0) != 0 || crt_[0] == 2)));
+                                    (spec.kind == K_RESCALE && (param1(spec.p, "mode", 0) != 0 || crt_[0] == 2)))));
         const bool passthru = spec.kind == K_FLATTEN;
         if (on_gpu && !dev_ok) {
             gpu->to_device(cur);
@@ -564,18 +597,28 @@ GarbledModel Garbler::garble(const std::vector<LayerSpec>& layers, const std::ve
                     const int p = crt_[j];
                     const ModInfo& mi = mod_info(p);
                     Labels O(p, out);
-                    Array bias(DType::i16, {out, mi.n});
                     const comp_t* Zp = Z_.get(p);
-                    for (i64 o = 0; o < out; ++o)
-                        lab_affine(bias.ptr<comp_t>() + o * mi.n, Zp, pmod(pmod(b[o], M_), p), R_.get(p), mi.n, p);
-                    g.a[arr_name("bias.", j, "")] = bias;
+                    // garbler-side base of each bias wire: Z_p (its label Z_p + b R is shipped) or, hardened,
+                    // -b R (label 0, not shipped)
+                    std::vector<comp_t> bbase(static_cast<size_t>(out) * mi.n);
+                    if (hard) {
+                        for (i64 o = 0; o < out; ++o)
+                            lab_affine(bbase.data() + o * mi.n, Zp, -pmod(pmod(b[o], M_), p), R_.get(p), mi.n, p);
+                    } else {
+                        Array bias(DType::i16, {out, mi.n});
+                        for (i64 o = 0; o < out; ++o) {
+                            lab_affine(bias.ptr<comp_t>() + o * mi.n, Zp, pmod(pmod(b[o], M_), p), R_.get(p), mi.n, p);
+                            std::memcpy(bbase.data() + o * mi.n, Zp, sizeof(comp_t) * mi.n);
+                        }
+                        g.a[arr_name("bias.", j, "")] = bias;
+                    }
                     if (on_gpu) continue;
                     const Labels& I = cur[j];
                     parallel_for(out, [&](i64 b0, i64 b1) {
                         std::vector<i64> acc(mi.n);
                         for (i64 o = b0; o < b1; ++o) {
                             std::fill(acc.begin(), acc.end(), 0);
-                            i64 zc = 1;  // garbler adds Z in place of the bias label
+                            i64 zc = 0;
                             const i64* wr = wa.ptr<i64>() + o * in;
                             for (i64 i = 0; i < in; ++i) {
                                 const i64 wv = wr[i] % p;
@@ -587,13 +630,18 @@ GarbledModel Garbler::garble(const std::vector<LayerSpec>& layers, const std::ve
                                 for (int c = 0; c < mi.n; ++c) acc[c] += wv * x[c];
                             }
                             comp_t* y = O.at(o);
-                            for (int c = 0; c < mi.n; ++c) y[c] = static_cast<comp_t>((acc[c] + zc * Zp[c]) % p);
+                            const comp_t* bb = bbase.data() + o * mi.n;
+                            for (int c = 0; c < mi.n; ++c) y[c] = static_cast<comp_t>((acc[c] + zc * Zp[c] + bb[c]) % p);
                         }
                     }, nt);
                     nxt.push_back(std::move(O));
                 }
-                if (on_gpu) gpu->dense(in, out, ch, wa.ptr<i64>(), wa.count(), rw.second, cur);
-                else cur = std::move(nxt);
+                if (on_gpu) {
+                    gpu->dense(in, out, ch, wa.ptr<i64>(), wa.count(), rw.second, cur);
+                    if (hard) gpu->fold_constants(neg_mod(b, M_), 1, cur);
+                } else {
+                    cur = std::move(nxt);
+                }
                 dims = {out};
                 break;
             }
@@ -608,7 +656,7 @@ GarbledModel Garbler::garble(const std::vector<LayerSpec>& layers, const std::ve
                 const Array& wa = rw.first;
                 g.a["w"] = wa;
                 CrtLabels nxt;
-                for (int j = 0; j < k; ++j) {
+                for (int j = 0; j < k && !hard; ++j) {
                     const int p = crt_[j];
                     const ModInfo& mi = mod_info(p);
                     const comp_t* Zp = Z_.get(p);
@@ -617,8 +665,9 @@ GarbledModel Garbler::garble(const std::vector<LayerSpec>& layers, const std::ve
                         lab_affine(bias.ptr<comp_t>() + f * mi.n, Zp, pmod(pmod(b[f], M_), p), R_.get(p), mi.n, p);
                     g.a[arr_name("bias.", j, "")] = bias;
                 }
-                if (gpu) {
+                if (on_gpu) {
                     gpu->conv(G, wa.ptr<i64>(), wa.count(), rw.second, cur);
+                    if (hard) gpu->fold_constants(neg_mod(b, M_), G.OH * G.OW, cur);
                     dims = {G.F, G.OH, G.OW};
                     break;
                 }
@@ -633,7 +682,9 @@ GarbledModel Garbler::garble(const std::vector<LayerSpec>& layers, const std::ve
                         for (i64 o = b0; o < b1; ++o) {
                             const i64 f = o / (G.OH * G.OW), r = o % (G.OH * G.OW), oy = r / G.OW, ox = r % G.OW;
                             std::fill(acc.begin(), acc.end(), 0);
-                            i64 zc = 1;
+                            // bias wire: base Z_p (reference) or -b R (hardened, label 0)
+                            i64 zc = hard ? 0 : 1;
+                            const i64 bneg = hard ? pmod(-pmod(b[f], M_), p) : 0;
                             const i64* wf = wa.ptr<i64>() + f * G.K();
                             for (i64 c = 0; c < G.C; ++c)
                                 for (i64 dy = 0; dy < G.kh; ++dy)
@@ -650,7 +701,9 @@ GarbledModel Garbler::garble(const std::vector<LayerSpec>& layers, const std::ve
                                         for (int cc = 0; cc < mi.n; ++cc) acc[cc] += wv * x[cc];
                                     }
                             comp_t* y = O.at(o);
-                            for (int cc = 0; cc < mi.n; ++cc) y[cc] = static_cast<comp_t>((acc[cc] + zc * Zp[cc]) % p);
+                            const comp_t* Rp = R_.get(p);
+                            for (int cc = 0; cc < mi.n; ++cc)
+                                y[cc] = static_cast<comp_t>((acc[cc] + zc * Zp[cc] + bneg * Rp[cc]) % p);
                         }
                     }, nt);
                     nxt.push_back(std::move(O));
@@ -679,7 +732,8 @@ GarbledModel Garbler::garble(const std::vector<LayerSpec>& layers, const std::ve
                                 for (int j = 0; j < k; ++j)
                                     mixed_mult_garble(cur[j].at(e), mod_info(crt_[j]), sig_host.at(e), m2, R_, prg_,
                                                       stream_id(L, 2, e), ctr, tg.ptr<u128>() + e * sum_crt + prefix[j],
-                                                      te.ptr<u128>() + (e * k + j) * 3, nxt[j].at(e));
+                                                      te.ptr<u128>() + (e * k + j) * 3, nxt[j].at(e),
+                                                      MMTw{hard, stream_id(L, 2, e), j, k, true});
                             }
                         }, nt);
                         cur = std::move(nxt);
@@ -708,12 +762,13 @@ GarbledModel Garbler::garble(const std::vector<LayerSpec>& layers, const std::ve
                             for (i64 e = b0; e < b1; ++e) {
                                 for (int j = 0; j < k; ++j) x[j] = cur[j].at(e);
                                 sign_mrs_garble_elem(sp, R_, prg_, stream_id(L, 1, e), x.data(),
-                                                     tab.ptr<u128>() + e * tab.shape[1], sig);
+                                                     tab.ptr<u128>() + e * tab.shape[1], sig, hard);
                                 u64 ctr = 0;
                                 for (int j = 0; j < k; ++j)
                                     mixed_mult_garble(x[j], mod_info(crt_[j]), sig, m2, R_, prg_, stream_id(L, 2, e), ctr,
                                                       tg.ptr<u128>() + e * sum_crt + prefix[j],
-                                                      te.ptr<u128>() + (e * k + j) * 3, nxt[j].at(e));
+                                                      te.ptr<u128>() + (e * k + j) * 3, nxt[j].at(e),
+                                                      MMTw{hard, stream_id(L, 2, e), j, k, true});
                             }
                         }, nt);
                         cur = std::move(nxt);
@@ -727,7 +782,7 @@ GarbledModel Garbler::garble(const std::vector<LayerSpec>& layers, const std::ve
                 SignPlan sp(crt_, mrs_, {2}, 0, 1, fused);
                 ReluTables t = make_relu_tables(sp, Nin, sum_crt, k);
                 CrtLabels nxt;
-                if (gpu) {
+                if (on_gpu) {
                     sinkify(t.approx, "s.approx");
                     sinkify(t.cast1, "s.cast1");
                     sinkify(t.cast2, "s.cast2");
@@ -748,7 +803,7 @@ GarbledModel Garbler::garble(const std::vector<LayerSpec>& layers, const std::ve
                             y[j] = nxt[j].at(e);
                         }
                         relu_garble_elem(sp, R_, Z_, prg_, stream_id(L, 1, e), stream_id(L, 2, e), crt_, prefix,
-                                         x.data(), t, e, y.data());
+                                         x.data(), t, e, y.data(), hard);
                     }
                 }, nt);
                 put_relu_tables(g, "", t);
@@ -762,7 +817,7 @@ GarbledModel Garbler::garble(const std::vector<LayerSpec>& layers, const std::ve
                     sg(DType::u128, {Nin, sp.n_sign});
                 if (sp.has_cast1()) c1 = Array(DType::u128, {Nin, std::max<i64>(sp.n_cast, 1)});
                 CrtLabels nxt;
-                if (gpu) {
+                if (on_gpu) {
                     sinkify(ap, "s.approx");
                     sinkify(c1, "s.cast1");
                     sinkify(c2, "s.cast2");
@@ -771,7 +826,7 @@ GarbledModel Garbler::garble(const std::vector<LayerSpec>& layers, const std::ve
                 } else {
                     for (int j = 0; j < k; ++j) nxt.emplace_back(crt_[j], Nin);
                 }
-                if (!gpu) parallel_for(Nin, [&](i64 b0, i64 b1) {
+                if (!on_gpu) parallel_for(Nin, [&](i64 b0, i64 b1) {
                     std::vector<const comp_t*> x(k);
                     std::vector<comp_t*> y(k);
                     for (i64 e = b0; e < b1; ++e) {
@@ -782,14 +837,14 @@ GarbledModel Garbler::garble(const std::vector<LayerSpec>& layers, const std::ve
                         sign_garble_elem(sp, R_, Z_, prg_, stream_id(L, 1, e), x.data(),
                                          ap.ptr<u128>() + e * sp.n_approx,
                                          sp.has_cast1() ? c1.ptr<u128>() + e * c1.shape[1] : nullptr,
-                                         c2.ptr<u128>() + e * c2.shape[1], sg.ptr<u128>() + e * sp.n_sign, y.data());
+                                         c2.ptr<u128>() + e * c2.shape[1], sg.ptr<u128>() + e * sp.n_sign, y.data(), hard);
                     }
                 }, nt);
                 g.a["s.approx"] = ap;
                 if (sp.has_cast1()) g.a["s.cast1"] = c1;
                 g.a["s.cast2"] = c2;
                 g.a["s.sign"] = sg;
-                if (!gpu) cur = std::move(nxt);
+                if (!on_gpu) cur = std::move(nxt);
                 break;
             }
             case K_RESCALE: {
@@ -809,7 +864,7 @@ GarbledModel Garbler::garble(const std::vector<LayerSpec>& layers, const std::ve
                             for (int j = 0; j < k; ++j) Lp[j] = cur[j].at(e);
                             rescale_mrs_garble_elem(P, R_, prg_, stream_id(L, 30, e), Lp.data(),
                                                     tab.ptr<u128>() + e * P.n_tab,
-                                                    joint_out ? sig_host.at(e) : nullptr);
+                                                    joint_out ? sig_host.at(e) : nullptr, hard);
                         }
                     }, nt);
                     g.a["mrs"] = tab;
@@ -872,11 +927,11 @@ GarbledModel Garbler::garble(const std::vector<LayerSpec>& layers, const std::ve
                                                     ap.ptr<u128>() + e * ap.shape[1],
                                                     P.sign.has_cast1() ? c1.ptr<u128>() + e * c1.shape[1] : nullptr,
                                                     c2.ptr<u128>() + e * c2.shape[1], sg.ptr<u128>() + e * sg.shape[1],
-                                                    nullptr);
+                                                    nullptr, hard);
                             } else {
                                 rescale_garble_elem(P, R_, Z_, prg_, stream_id(L, 10 + it, e), Lp.data(), upp.data(),
                                                     dnp.data(), tr.ptr<u128>() + e * P.n_trans, nullptr, nullptr,
-                                                    nullptr, nullptr, be.ptr<u128>() + e * P.n_be);
+                                                    nullptr, nullptr, be.ptr<u128>() + e * P.n_be, hard);
                             }
                         }
                     }, nt);
@@ -964,7 +1019,7 @@ GarbledModel Garbler::garble(const std::vector<LayerSpec>& layers, const std::ve
                                 y[j] = nv[j].at(o * cnt1 + q);
                             }
                             relu_garble_elem(sp, R_, Z_, prg_, stream_id(L, 20 + 2 * lv, e), stream_id(L, 21 + 2 * lv, e),
-                                             crt_, prefix, x.data(), t, e, y.data());
+                                             crt_, prefix, x.data(), t, e, y.data(), hard);
                             for (int j = 0; j < k; ++j)
                                 lab_add(y[j], vals[j].at(o * cnt + 2 * q), vals[j].n, vals[j].p);
                         }
@@ -1043,7 +1098,8 @@ GarbledModel Garbler::garble(const std::vector<LayerSpec>& layers, const std::ve
                             const auto& fn = paramv(spec.p, ("fn." + std::to_string(j)).c_str());
                             prg_.label(stream_id(L, 1, e), ctr, mo.p, mo.n, nxt[j].at(e));
                             garble_proj(cur[j].at(e), R_.get(mi.p), mi, nxt[j].at(e), R_.get(mo.p), mo,
-                                        [&fn](int v) { return fn[v]; }, tabs[j].ptr<u128>() + e * mi.p);
+                                        [&fn](int v) { return fn[v]; }, tabs[j].ptr<u128>() + e * mi.p, 1,
+                                        Mask{hard, stream_id(L, 1, e), tw_sub(TW_PROJ, j), 0});
                         }
                     }
                 }, nt);
@@ -1066,7 +1122,7 @@ GarbledModel Garbler::garble(const std::vector<LayerSpec>& layers, const std::ve
                         for (int j = 0; j < k; ++j)
                             gen_mult_garble(cur[j].at(2 * e), cur[j].at(2 * e + 1), mod_info(crt_[j]), R_, prg_,
                                             stream_id(L, 1, e), ctr, ga.ptr<u128>() + e * sum_crt + prefix[j],
-                                            ea.ptr<u128>() + e * sum_crt + prefix[j], nxt[j].at(e));
+                                            ea.ptr<u128>() + e * sum_crt + prefix[j], nxt[j].at(e), hard, j);
                     }
                 }, nt);
                 g.a["g"] = ga;
@@ -1092,10 +1148,12 @@ GarbledModel Garbler::garble(const std::vector<LayerSpec>& layers, const std::ve
                             const ModInfo& mp = mod_info(crt_[j]);
                             prg_.label(stream_id(L, 1, e), ctr, q, mq.n, t0.data());
                             garble_proj(cur[j].at(2 * e + 1), R_.get(mp.p), mp, t0.data(), R_.get(q), mq,
-                                        [](int v) { return static_cast<i64>(v); }, ta.ptr<u128>() + e * sum_crt + prefix[j]);
+                                        [](int v) { return static_cast<i64>(v); }, ta.ptr<u128>() + e * sum_crt + prefix[j],
+                                        1, Mask{hard, stream_id(L, 1, e), tw_sub(TW_MMT, j), 0});
                             mixed_mult_garble(cur[j].at(2 * e), mp, t0.data(), mq, R_, prg_, stream_id(L, 1, e), ctr,
                                               ga.ptr<u128>() + e * sum_crt + prefix[j],
-                                              ea.ptr<u128>() + (e * k + j) * (q + 1), nxt[j].at(e));
+                                              ea.ptr<u128>() + (e * k + j) * (q + 1), nxt[j].at(e),
+                                              MMTw{hard, stream_id(L, 1, e), j, k, false});
                         }
                     }
                 }, nt);
@@ -1125,7 +1183,8 @@ GarbledModel Garbler::garble(const std::vector<LayerSpec>& layers, const std::ve
                         for (int xi : P.extra_idx)
                             std::memcpy(Lp[xi], Z_.get(crt_[xi]), sizeof(comp_t) * nr_comps(crt_[xi]));
                         u64 ctr = 0;
-                        be_garble_elem(P, R_, prg_, stream_id(L, 1, e), ctr, Lp.data(), be.ptr<u128>() + e * P.n_tab);
+                        be_garble_elem(P, R_, prg_, stream_id(L, 1, e), ctr, Lp.data(), be.ptr<u128>() + e * P.n_tab,
+                                       hard);
                     }
                 }, nt);
                 g.a["be"] = be;

@@ -1512,6 +1512,38 @@ __global__ __launch_bounds__(256) void k_gsum(Ctx c, GsArgs a) {
     }
 }
 
+// Hardened encoding (garbler.cpp): public constants c_g (one per group of `group` consecutive elements, e.g.
+// a conv filter's bias) folded into the base labels, y_e += c_{e / group} R_p (mod p), so the constant wires
+// need no evaluator-visible label. Grid (element x chunk work, residue j).
+struct FoldJob {
+    int16_t* dst;
+    const int32_t* c;  // [groups] constants reduced mod p
+    int p, nc;
+};
+struct FoldArgs {
+    FoldJob j[kMaxRes];
+    int64_t N, group;
+};
+__global__ __launch_bounds__(256) void k_fold(Ctx c, FoldArgs a) {
+    const FoldJob& J = a.j[blockIdx.y];
+    const ModC m = c.mc[J.p];
+    const int16_t* Rp = c.R + static_cast<int64_t>(J.p) * kW;
+    const int64_t N = a.N, total = N * J.nc;
+    for (int64_t x = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; x < total;
+         x += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+        const int c8 = static_cast<int>(x / N);
+        const int64_t e = x - static_cast<int64_t>(c8) * N;
+        int16_t* d = J.dst + (static_cast<int64_t>(c8) * N + e) * kCh;
+        const uint32_t f = static_cast<uint32_t>(J.c[e / a.group]);
+        uint32_t acc[8], t[8];
+        unpack8(*reinterpret_cast<const u32x4a*>(d), acc);
+        unpack8(*reinterpret_cast<const u32x4a*>(Rp + c8 * kCh), t);
+#pragma unroll
+        for (int u = 0; u < 8; ++u) acc[u] = modq(acc[u] + f * t[u], m);
+        st_chunk(d, pack8(acc));
+    }
+}
+
 // Dense base labels y_o = sum_i w_oi x_i + zc_o Z_p (mod p), weights reduced mod p and transposed ([in][out],
 // rows already in the channel_tf source order), zc_o = 1 + #(w_oi = 0 mod p) (the reference's zero-weight Z
 // quirk, and the bias label's Z). Block: 64 outputs x 4 input groups for one (chunk, residue); the groups'
@@ -3601,6 +3633,32 @@ void GpuGarbler::dense(i64 in, i64 out, i64 ch, const i64* w, size_t nw, uint64_
     I.cur = std::move(y);
     I.cur_N = out;
     set_stale(cur, I.cur_mod, out);
+}
+
+// hardened encoding: y_e += (c[e / group] mod p_j) R_pj on the device cur (c: one public constant per group,
+// already negated / reduced mod M by the caller)
+void GpuGarbler::fold_constants(const std::vector<i64>& c, i64 group, CrtLabels& cur) {
+    Impl& I = *impl_;
+    I.enter();
+    I.check_cur(cur);
+    DASH_CHECK(group >= 1 && static_cast<i64>(c.size()) * group == I.cur_N, "gpu garbler: constant fold shape");
+    gg::FoldArgs a{};
+    a.N = I.cur_N;
+    a.group = group;
+    int ncmax = 1;
+    const int k = static_cast<int>(I.cur_mod.size());
+    for (int j = 0; j < k; ++j) {
+        const int p = I.cur_mod[j];
+        std::vector<int32_t> cj(c.size());
+        for (size_t g = 0; g < c.size(); ++g) cj[g] = static_cast<int32_t>(pmod(c[g], p));
+        a.j[j] = gg::FoldJob{I.cur[j].as<int16_t>(), gg::dconst(cj.data(), cj.size()), p,
+                             static_cast<int>(gg::chunks_of(nr_comps(p)))};
+        ncmax = std::max(ncmax, a.j[j].nc);
+    }
+    const int64_t work = I.cur_N * ncmax;
+    const int blocks = static_cast<int>(std::min<int64_t>((work + 255) / 256, 4096));
+    hipLaunchKernelGGL(gg::k_fold, dim3(blocks, k), dim3(256), 0, gg::tl_st, I.c, a);
+    HIPCHECK(hipGetLastError());
 }
 
 // sum pool (garbler.cpp K_SUMPOOL): window sums of base labels

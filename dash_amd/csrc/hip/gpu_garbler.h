@@ -50,6 +50,8 @@ class GpuGarbler {
     // dense base labels y_o = sum_{w != 0 mod p} w x_src(i) + (1 + #zero weights) Z_p (w reduced mod M, [out][in],
     // src = dense_src(i, in, channel_tf))
     void dense(i64 in, i64 out, i64 channel_tf, const i64* w, size_t nw, uint64_t wh, CrtLabels& cur);
+    // hardened encoding: cur_e += (c[e / group] mod p) R_p (public constants folded into the base labels)
+    void fold_constants(const std::vector<i64>& c, i64 group, CrtLabels& cur);
     // window sums of the device cur
     void sumpool(const PoolGeom& G, CrtLabels& cur);
     // device copies of layer outputs a later residual add / in_src layer reads (idx = layer index + 1)

@@ -63,8 +63,12 @@ struct GLayer {
 };
 
 struct ModelHeader {
-    int version = 3;  // 2: approx tables interleaved [color][digit]; 3: + sign construction flag
+    int version = 4;  // 2: approx tables interleaved [color][digit]; 3: + sign construction flag; 4: + hardened
     int sign_fused = 0;  // 1: sign gadgets use the fused-cast construction (SignPlan::fused)
+    // 1: hardened encoding (docs/SECURITY.md): no evaluator-visible constant labels (public-constant wires have
+    // label 0: Z_p, bias, shift and padding labels are not shipped) and every table entry is masked by its own
+    // tweaked pad (core.h hard_block) instead of the reference's shared H(K)
+    int hardened = 0;
     std::vector<int> crt, mrs;
     std::vector<i64> in_dims, out_dims;
     std::vector<int> out_moduli;  // moduli of the output residues
@@ -130,6 +134,7 @@ struct GarbleOptions {
     // A ReLU right after a mixed-radix rescale takes its sign from that rescale's conversion
     // (gadgets.h RescaleMrsPlan::sign_last); other ReLUs use relu_mrs / the approximate gadget.
     bool relu_joint = false;
+    bool hardened = false;  // ModelHeader::hardened
     std::shared_ptr<TableSink> sink;  // GPU-garbled tables go straight to these buffers (device >= 0 only)
     GarbleSpecs* cache = nullptr;     // reduced-weight cache of the specs being garbled (optional)
 };

@@ -118,8 +118,9 @@ void write_model(const GarbledModel& m, W& w) {
     const auto& consts = m.consts;
     const auto& layers = m.layers;
     w.raw(kModelMagic, 8);
-    w.u32(3u);
+    w.u32(4u);
     w.u32(static_cast<uint32_t>(h.sign_fused));
+    w.u32(static_cast<uint32_t>(h.hardened));
     w.ivec32(h.crt);
     w.ivec32(h.mrs);
     w.ivec(h.in_dims);
@@ -179,10 +180,12 @@ GarbledModel GarbledModel::deserialize(const uint8_t* blob, size_t nbytes) {
     DASH_CHECK(std::memcmp(mg, kModelMagic, 8) == 0, "not a garbled model blob");
     GarbledModel m;
     m.h.version = static_cast<int>(r.u32());
-    DASH_CHECK(m.h.version == 2 || m.h.version == 3, "unsupported garbled model version (expected 2 or 3)");
+    DASH_CHECK(m.h.version >= 2 && m.h.version <= 4, "unsupported garbled model version (expected 2..4)");
     m.h.sign_fused = m.h.version >= 3 ? static_cast<int>(r.u32()) : 0;
     DASH_CHECK(m.h.sign_fused == 0 || m.h.sign_fused == 1, "bad sign construction flag");
-    m.h.version = 3;
+    m.h.hardened = m.h.version >= 4 ? static_cast<int>(r.u32()) : 0;
+    DASH_CHECK(m.h.hardened == 0 || m.h.hardened == 1, "bad hardened flag");
+    m.h.version = 4;
     m.h.crt = r.ivec32();
     m.h.mrs = r.ivec32();
     m.h.in_dims = r.ivec();

@@ -65,11 +65,18 @@ def resolve_constructions(circuit: Circuit, crt_base: Sequence[int], rescale: st
     return rescale, relu
 
 
+def hardened_supported(circuit: Circuit, fused_sign: bool, rescale: str) -> bool:
+    """The hardened encoding keys no projection with a public label: the reference sign construction's zero
+    carry and the legacy rescale's zero residue 0 (fed to a sign gadget) do, so it needs the fused sign and,
+    when the circuit has DASH Rescale(l) layers, the mixed-radix rescale."""
+    return bool(fused_sign) and (rescale == "mrs" or not circuit._dash_rescales())
+
+
 class GarbledCircuit:
     def __init__(self, circuit: Circuit, crt: Union[int, Sequence[int]], mrs: Union[None, float, Sequence[int]] = None,
                  max_modulus: int = 0, seed: Optional[bytes] = None, garble_me: bool = True, nthreads: int = 0,
                  device: Optional[int] = None, fused_sign: bool = True, rescale: str = "auto",
-                 relu: str = "auto", sink=None):
+                 relu: str = "auto", sink=None, hardened: Optional[bool] = None):
         """fused_sign: sign-gadget construction. True (default): the MRS casts are folded into the approx and
         carry projections (same function, 3.7x fewer gates per sign; gadgets.h SignPlan::fused). False: the
         reference construction with explicit identity casts (sign_gadget.h:456-546).
@@ -92,7 +99,14 @@ class GarbledCircuit:
 
         sink: with `device`, a HipEvaluator slot destination (HipEvaluator.sink(b)): the GPU garbler writes the
         garbled tables straight into that slot's HBM arena (zero-copy offline phase; HipEvaluator.load(b, model)
-        then skips them). The model's tables alias the slot and are valid only while it holds this GC."""
+        then skips them). The model's tables alias the slot and are valid only while it holds this GC.
+
+        hardened: the offline-message encoding (docs/SECURITY.md). True: no evaluator-visible constant labels
+        (public-constant wires have label 0 and their constants are folded into the garbler's base labels) and
+        every table entry masked by its own tweaked pad, closing the reference encoding's R_p recovery from
+        Z_p / bias labels and its shared-hash leaks (mixed half gate mini tables, repeated MRS digit moduli).
+        Needs the fused sign and no legacy rescale. False: the reference's wire-compatible encoding. None
+        (default): hardened whenever the resolved constructions allow it."""
         self.circuit = circuit
         self.crt_base = first_primes(crt) if isinstance(crt, int) else [int(p) for p in crt]
         if mrs is None:
@@ -108,6 +122,19 @@ class GarbledCircuit:
         self.device = -1 if device is None else int(device)
         self.fused_sign = bool(fused_sign)
         self.rescale, self.relu = resolve_constructions(circuit, self.crt_base, rescale, relu)
+        supported = hardened_supported(circuit, self.fused_sign, self.rescale)
+        # the mixed-radix constructions are this framework's own (not wire-compatible with anything): they only
+        # exist in the hardened encoding, whose kernels they use
+        needs = self.rescale == "mrs" or self.relu in ("mrs", "joint")
+        if hardened is None:
+            hardened = supported
+        if hardened and not supported:
+            raise ValueError("hardened=True needs the fused sign construction and no legacy DASH rescale "
+                             "(rescale='mrs'); the reference constructions use the wire-compatible encoding")
+        if needs and not hardened:
+            raise ValueError("the mixed-radix constructions (rescale='mrs', relu='mrs' / 'joint') use the hardened "
+                             "encoding only (fused sign; hardened=None or True)")
+        self.hardened = bool(hardened)
         self.sink = sink
         self._n = native()
         self.garbler = self._n.Garbler(self.crt_base, self.mrs_base, self.seed, int(max_modulus))
@@ -123,7 +150,8 @@ class GarbledCircuit:
         t = time.perf_counter()
         self.model = self.garbler.garble(specs, list(self.circuit.input_dims), self.nthreads, self.device,
                                          self.fused_sign, self.rescale == "mrs", self.relu == "mrs",
-                                         self.relu == "joint", self.sink if self.device >= 0 else None)
+                                         self.relu == "joint", self.sink if self.device >= 0 else None,
+                                         self.hardened)
         self.sink = None  # single use: the slot now holds this GC
         self.garbling_time_s = time.perf_counter() - t
         self.decoder = self.garbler.decoder()
@@ -200,7 +228,8 @@ class GarbledCircuit:
             relu = f"joint({len(joint)})+{other}({len(relus) - len(joint)})"
         else:
             relu = other
-        return dict(sign="fused" if self.fused_sign else "reference", rescale=rescale, relu=relu)
+        return dict(sign="fused" if self.fused_sign else "reference", rescale=rescale, relu=relu,
+                    encoding="hardened" if self.hardened else "reference")
 
     @property
     def table_bytes(self) -> int:

@@ -190,17 +190,37 @@ class Circuit:
         return st
 
     def garble_specs_native(self):
-        """The layer specs as a native GarbleSpecs, built once and reused while the layers' quantized parameters
-        are unchanged (a fingerprint of the layer list and its weight arrays' identity; quantize() drops it):
-        the garbler then reduces and hashes the public weights once, not per GC."""
+        """The layer specs as a native GarbleSpecs, built once and reused while the layers' garbling parameters
+        are unchanged: the garbler then reduces and hashes the public weights once, not per GC.
+
+        The cache key is every scalar / list parameter of every layer spec plus the identity of its weight and
+        bias arrays. Those arrays are made read-only when the specs are built, so an in-place edit
+        (``l.q_weights[...] = v``) raises instead of silently garbling stale weights; assigning a new array (what
+        quantize() does) changes the key. A writable array at call time (re-enabled by the caller) rebuilds."""
         from ..native import native
 
-        fp = tuple((id(l), l.kind, id(getattr(l, "q_weights", None)), id(getattr(l, "q_biases", None)),
-                    getattr(l, "in_src", None)) for l in self.layers)
+        specs = self.garble_specs()
+
+        def norm(v):
+            if isinstance(v, np.ndarray):
+                return ("arr", id(v.base if v.base is not None else v), v.shape, str(v.dtype))
+            if isinstance(v, (list, tuple)):
+                return tuple(norm(x) for x in v)
+            return v
+
+        arrays = [a for l in self.layers for a in (getattr(l, "q_weights", None), getattr(l, "q_biases", None))
+                  if isinstance(a, np.ndarray)]
+        fp = tuple((int(k), tuple(sorted((n, norm(v)) for n, v in p.items()))) for k, p in specs)
+        fp = (fp, tuple(id(a) for a in arrays))
         cache = getattr(self, "_native_specs", None)
-        if cache is None or cache[0] != fp:
-            cache = (fp, native().GarbleSpecs(self.garble_specs()))
+        if cache is None or cache[0] != fp or any(a.flags.writeable for a in arrays):
+            cache = (fp, native().GarbleSpecs(specs))
             self._native_specs = cache
+            for a in arrays:
+                try:
+                    a.setflags(write=False)
+                except ValueError:  # a view of memory we do not own: the identity key still covers reassignment
+                    pass
         return cache[1]
 
     def garble_specs(self) -> list:

@@ -249,7 +249,28 @@ class GarblerClient:
         if self._ring and self._ring[0].size >= size:
             return
         self._ring_close()
-        self._ring = [shared_memory.SharedMemory(create=True, size=size) for _ in range(self._RING)]
+        # tmpfs accepts an ftruncate past its free space and then SIGBUSes the writer (the native serializer
+        # runs without the GIL, so the garbler process dies instead of raising): check the space up front
+        need = self._RING * size
+        try:
+            st = os.statvfs("/dev/shm")
+            free = st.f_bavail * st.f_frsize
+        except OSError:
+            free = None
+        if free is not None and free < need:
+            raise RuntimeError(f"transport='shm' needs {need / 2**30:.2f} GiB in /dev/shm for {self._RING} ring "
+                               f"segments but only {free / 2**30:.2f} GiB are free; use transport='tcp'")
+        self._ring = []
+        try:
+            for _ in range(self._RING):
+                seg = shared_memory.SharedMemory(create=True, size=size)
+                self._ring.append(seg)
+                if hasattr(os, "posix_fallocate"):  # reserve the pages now: a full tmpfs fails here, not in a write
+                    os.posix_fallocate(seg._fd, 0, size)
+        except OSError as e:
+            self._ring_close()
+            raise RuntimeError(f"transport='shm': cannot reserve {size} bytes in /dev/shm ({e}); "
+                               "use transport='tcp'") from e
 
     def _ring_close(self) -> None:
         for seg in self._ring:
@@ -368,14 +389,27 @@ class GarblerClient:
         else:
             q: "queue.Queue" = queue.Queue(maxsize=2)  # at most two models in flight beside the one on the wire
             err: list = []
+            stop = threading.Event()
+
+            def put(item) -> bool:
+                # bounded put that gives up once the sending side has stopped (a failed send must not leave the
+                # producer blocked on a full queue forever)
+                while not stop.is_set():
+                    try:
+                        q.put(item, timeout=0.1)
+                        return True
+                    except queue.Full:
+                        continue
+                return False
 
             def produce():
                 try:
                     for b in range(self.batch):
-                        q.put(self._garble_one(seeds[b]))
+                        if stop.is_set() or not put(self._garble_one(seeds[b])):
+                            return
                 except BaseException as e:  # surfaced on the sending thread
                     err.append(e)
-                    q.put(None)
+                    put(None)
 
             th = threading.Thread(target=produce, name="dash-garbler", daemon=True)
             th.start()
@@ -393,6 +427,12 @@ class GarblerClient:
                 for _ in range(self.batch):  # the evaluator acknowledges every load, in order
                     self.ch.recv(b"ACK_")
             finally:
+                stop.set()
+                while True:  # drain: a producer blocked in put() sees the stop flag within 0.1 s
+                    try:
+                        q.get_nowait()
+                    except queue.Empty:
+                        break
                 th.join()
         self.stats["gcs"] += self.batch
         self.stats["offline_bytes"] += self.ch.bytes_sent - sent0

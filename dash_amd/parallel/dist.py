@@ -22,6 +22,100 @@ from typing import Optional, Sequence
 import numpy as np
 
 
+KFD_TOPOLOGY = "/sys/class/kfd/kfd/topology/nodes"
+
+
+def kfd_gpus(root: str = KFD_TOPOLOGY) -> list:
+    """GPU agents of the KFD topology, in KFD node order (the order HIP enumerates devices), read from sysfs
+    without touching the HIP runtime. Each entry: {"node", "pci" (dddd:bb:dd.f), "gfx"}. Raises when the
+    topology is missing: callers must not guess a device count."""
+    if not os.path.isdir(root):
+        raise RuntimeError(f"KFD topology {root} not readable: cannot count GPUs without initialising HIP")
+    out = []
+    for name in sorted(os.listdir(root), key=lambda s: int(s) if s.isdigit() else 1 << 30):
+        if not name.isdigit():
+            continue
+        props = {}
+        try:
+            with open(os.path.join(root, name, "properties")) as f:
+                for line in f:
+                    parts = line.split()
+                    if len(parts) == 2 and parts[1].lstrip("-").isdigit():
+                        props[parts[0]] = int(parts[1])
+        except OSError:
+            continue
+        if props.get("simd_count", 0) <= 0 or props.get("gfx_target_version", 0) == 0:
+            continue  # CPU agent
+        loc, dom = props.get("location_id", 0), props.get("domain", 0)
+        pci = f"{dom:04x}:{(loc >> 8) & 0xff:02x}:{(loc >> 3) & 0x1f:02x}.{loc & 7:x}"
+        out.append({"node": int(name), "pci": pci, "gfx": props.get("gfx_target_version", 0)})
+    return out
+
+
+def visible_indices(n: int, env: Optional[dict] = None) -> list:
+    """Indices (into the KFD GPU list) a HIP process started with `env` would see: ROCR_VISIBLE_DEVICES
+    filters first, then HIP_VISIBLE_DEVICES / CUDA_VISIBLE_DEVICES index into what remains."""
+    env = os.environ if env is None else env
+    idx = list(range(n))
+    for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        v = env.get(var)
+        if v is None:
+            continue
+        v = v.strip()
+        if v == "":
+            return []
+        sel = []
+        for tok in v.split(","):
+            tok = tok.strip()
+            if tok.isdigit() and int(tok) < len(idx):
+                sel.append(idx[int(tok)])
+            else:
+                break  # HIP stops at the first invalid entry
+        idx = sel
+    return idx
+
+
+def gpu_local_cpus(local_rank: int) -> Optional[set]:
+    """CPUs of the NUMA node closest to the GPU a rank with this LOCAL_RANK uses (PCI local_cpulist), or None
+    when unknown. Sysfs only: safe before the first HIP call."""
+    try:
+        gpus = kfd_gpus()
+    except RuntimeError:
+        return None
+    vis = visible_indices(len(gpus))
+    if local_rank >= len(vis):
+        return None
+    path = f"/sys/bus/pci/devices/{gpus[vis[local_rank]]['pci']}/local_cpulist"
+    try:
+        with open(path) as f:
+            spec = f.read().strip()
+    except OSError:
+        return None
+    cpus = set()
+    for part in spec.split(","):
+        if "-" in part:
+            a, b = part.split("-")
+            cpus.update(range(int(a), int(b) + 1))
+        elif part:
+            cpus.add(int(part))
+    return cpus or None
+
+
+def bind_rank_affinity(local_rank: int) -> Optional[list]:
+    """Pin this process to the CPUs local to its GPU (intersected with the CPUs it may use) before HIP starts,
+    so host encode / decode / garbling threads of 8 ranks do not cross NUMA nodes. Returns the CPU list set, or
+    None when the topology is unknown or the intersection is empty (affinity unchanged)."""
+    cpus = gpu_local_cpus(local_rank)
+    if not cpus or not hasattr(os, "sched_setaffinity"):
+        return None
+    allowed = os.sched_getaffinity(0)
+    mine = sorted(cpus & allowed)
+    if not mine:
+        return None
+    os.sched_setaffinity(0, mine)
+    return mine
+
+
 @dataclass
 class DistContext:
     rank: int = 0
@@ -54,6 +148,8 @@ def init_distributed(backend: Optional[str] = None, use_gpu: Optional[bool] = No
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1 and os.environ.get("DASH_NUMA_BIND", "1") != "0":
+        bind_rank_affinity(local)  # sysfs only, before torch.cuda touches HIP
     if use_gpu is None:
         use_gpu = torch.cuda.is_available()
     dev = None
