@@ -150,7 +150,13 @@ def spawn_ranks(args, argv: List[str]) -> int:
 
     n = args.gpus
     if args.backend == "hip":
-        avail = visible_gpus()
+        try:
+            avail = visible_gpus()
+        except RuntimeError as e:
+            if not args.rehearse_shared_device:
+                log(f"--gpus {n}: {e}; refusing")
+                return 2
+            avail = 0
         if avail < n and not args.rehearse_shared_device:
             log(f"--gpus {n} requested but only {avail} GPU(s) visible: refusing (a scaling run needs one GPU per "
                 f"rank; --rehearse-shared-device runs the multi-rank path on shared devices, clearly labelled)")

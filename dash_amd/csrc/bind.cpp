@@ -477,6 +477,25 @@ PYBIND11_MODULE(_dash_native, m) {
         }
         return labels_to_py(out);
     }, py::arg("model"), py::arg("labels"), py::arg("nthreads") = 0);
+    m.def("cpu_evaluate_trace", [](std::shared_ptr<GarbledModel> gm, const py::list& labels, int nthreads) {
+        auto in = labels_from_py(labels);
+        EvalTrace tr;
+        CrtLabels out;
+        {
+            py::gil_scoped_release rel;
+            out = cpu_evaluate(*gm, in, nthreads, nullptr, &tr);
+        }
+        py::dict relu;
+        for (const auto& kv : tr.relu_sign) {
+            const Labels& S = kv.second;
+            py::array_t<int16_t> sa({static_cast<py::ssize_t>(S.N), static_cast<py::ssize_t>(S.n)});
+            std::memcpy(sa.mutable_data(), S.c.data(), S.c.size() * sizeof(comp_t));
+            relu[py::int_(kv.first)] = py::make_tuple(labels_to_py(tr.relu_in.at(kv.first)), sa);
+        }
+        return py::make_tuple(labels_to_py(out), relu);
+    }, py::arg("model"), py::arg("labels"), py::arg("nthreads") = 0,
+       "host evaluation that also returns, per ReLU layer, (input labels, sign labels): the evaluator's own "
+       "intermediate values (security tests)");
     m.def("cpu_evaluate_timed", [](std::shared_ptr<GarbledModel> gm, const py::list& labels, int nthreads) {
         CrtLabels in = labels_from_py(labels);
         CrtLabels out;

@@ -52,7 +52,7 @@ struct ReluTabs {
 // s_gate / m_gate: the sign and mixed-mult gadgets' PRG streams (the hardened tweaks' gates)
 void relu_eval_elem(const SignPlan& sp, const LabelBank& Z, const std::vector<int>& crt,
                     const std::vector<i64>& prefix, const comp_t* const* x, const ReluTabs& T, i64 e,
-                    comp_t* const* out, bool hard, u64 s_gate, u64 m_gate) {
+                    comp_t* const* out, bool hard, u64 s_gate, u64 m_gate, comp_t* sig_out = nullptr) {
     const int k = static_cast<int>(crt.size());
     comp_t sig[128];
     comp_t* outs[1] = {sig};
@@ -60,6 +60,7 @@ void relu_eval_elem(const SignPlan& sp, const LabelBank& Z, const std::vector<in
                    T.c1 ? T.c1->ptr<u128>() + e * T.c1->shape[1] : nullptr,
                    T.c2->ptr<u128>() + e * T.c2->shape[1], T.sg->ptr<u128>() + e * T.sg->shape[1], outs, hard, s_gate);
     const ModInfo& m2 = mod_info(2);
+    if (sig_out) std::memcpy(sig_out, sig, sizeof(comp_t) * m2.n);
     for (int j = 0; j < k; ++j)
         mixed_mult_eval(x[j], mod_info(crt[j]), sig, m2, T.ga->ptr<u128>() + e * T.ga->shape[1] + prefix[j],
                         T.ea->ptr<u128>() + (e * k + j) * 3, out[j], MMTw{hard, m_gate, j, k, true});
@@ -74,7 +75,8 @@ const comp_t* zeros_or(const GLayer& g, const std::string& name, bool hard, size
 
 }  // namespace
 
-CrtLabels cpu_evaluate(const GarbledModel& m, const CrtLabels& inputs, int nt, std::vector<double>* layer_ms) {
+CrtLabels cpu_evaluate(const GarbledModel& m, const CrtLabels& inputs, int nt, std::vector<double>* layer_ms,
+                       EvalTrace* trace) {
     const std::vector<int>& crt = m.h.crt;
     const int k = static_cast<int>(crt.size());
     DASH_CHECK(static_cast<int>(inputs.size()) == k, "input residue count mismatch");
@@ -203,8 +205,10 @@ CrtLabels cpu_evaluate(const GarbledModel& m, const CrtLabels& inputs, int nt, s
                 break;
             }
             case K_RELU: {
+                if (trace) trace->relu_in[li] = cur;
                 if (g.param("smode", 0) == 2) {  // sign from the preceding rescale (RescaleMrsPlan::sign_last)
                     DASH_CHECK(sig_joint.N == Nin, "joint ReLU without a preceding sign-producing rescale");
+                    if (trace) trace->relu_sign[li] = sig_joint;
                     const Array& tg = g.arr("mm.g");
                     const Array& te = g.arr("mm.e");
                     CrtLabels nxt;
@@ -229,6 +233,7 @@ CrtLabels cpu_evaluate(const GarbledModel& m, const CrtLabels& inputs, int nt, s
                     const Array& te = g.arr("mm.e");
                     CrtLabels nxt;
                     for (int j = 0; j < k; ++j) nxt.emplace_back(crt[j], Nin);
+                    Labels sigs(2, trace ? Nin : 0);
                     parallel_for(Nin, [&](i64 b0, i64 b1) {
                         std::vector<const comp_t*> x(k);
                         comp_t sig[128];
@@ -237,12 +242,14 @@ CrtLabels cpu_evaluate(const GarbledModel& m, const CrtLabels& inputs, int nt, s
                             for (int j = 0; j < k; ++j) x[j] = cur[j].at(e);
                             sign_mrs_eval_elem(sp, x.data(), tab.ptr<u128>() + e * tab.shape[1], sig, hard,
                                                stream_id(L, 1, e));
+                            if (trace) std::memcpy(sigs.at(e), sig, sizeof(comp_t) * m2.n);
                             for (int j = 0; j < k; ++j)
                                 mixed_mult_eval(x[j], mod_info(crt[j]), sig, m2, tg.ptr<u128>() + e * tg.shape[1] + prefix[j],
                                                 te.ptr<u128>() + (e * k + j) * 3, nxt[j].at(e),
                                                 MMTw{hard, stream_id(L, 2, e), j, k, true});
                         }
                     }, nt);
+                    if (trace) trace->relu_sign[li] = std::move(sigs);
                     cur = std::move(nxt);
                     break;
                 }
@@ -250,6 +257,7 @@ CrtLabels cpu_evaluate(const GarbledModel& m, const CrtLabels& inputs, int nt, s
                 const ReluTabs T(g, "");
                 CrtLabels nxt;
                 for (int j = 0; j < k; ++j) nxt.emplace_back(crt[j], Nin);
+                Labels sigs(2, trace ? Nin : 0);
                 parallel_for(Nin, [&](i64 b0, i64 b1) {
                     std::vector<const comp_t*> x(k);
                     std::vector<comp_t*> y(k);
@@ -259,9 +267,10 @@ CrtLabels cpu_evaluate(const GarbledModel& m, const CrtLabels& inputs, int nt, s
                             y[j] = nxt[j].at(e);
                         }
                         relu_eval_elem(sp, Z, crt, prefix, x.data(), T, e, y.data(), hard, stream_id(L, 1, e),
-                                       stream_id(L, 2, e));
+                                       stream_id(L, 2, e), trace ? sigs.at(e) : nullptr);
                     }
                 }, nt);
+                if (trace) trace->relu_sign[li] = std::move(sigs);
                 cur = std::move(nxt);
                 break;
             }

@@ -183,9 +183,17 @@ class Garbler {
     const InputCodebook* input_codebook() const;
 };
 
+// Evaluator-side intermediate values (labels the evaluator computes anyway), per ReLU layer: its input labels
+// and the sign labels (mod 2) its half gates are keyed by. Used by the security tests (tests/test_security.py),
+// which attack the offline message from exactly this view.
+struct EvalTrace {
+    std::map<size_t, CrtLabels> relu_in;
+    std::map<size_t, Labels> relu_sign;
+};
+
 // Host (oracle) evaluator: bit-exact reference for the HIP evaluator.
 CrtLabels cpu_evaluate(const GarbledModel& m, const CrtLabels& inputs, int nthreads = 0,
-                       std::vector<double>* layer_ms = nullptr);
+                       std::vector<double>* layer_ms = nullptr, EvalTrace* trace = nullptr);
 
 // Wire-form helpers: compressed labels [k][N] <-> CrtLabels
 std::vector<u128> compress_labels(const CrtLabels& L, int nthreads = 0);
