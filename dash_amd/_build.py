@@ -26,8 +26,10 @@ ROCM = Path(os.environ.get("ROCM_PATH", "/opt/rocm"))
 ARCH = os.environ.get("DASH_GPU_ARCH", "gfx950")
 
 HOST_SOURCES = ["core.cpp", "gadgets.cpp", "garbler.cpp", "evaluator.cpp", "serialize.cpp", "onnx.cpp", "dataloader.cpp", "bind.cpp"]
-HIP_SOURCES = ["hip/runtime.hip", "hip/kernels_label.hip", "hip/kernels_gemm.hip", "hip/kernels_gadget.hip",
-               "hip/garble_gpu.hip"]
+# kernels_mrs_a.hip (K = 7, the headline) first: the longest units start first in the parallel build
+HIP_SOURCES = ["hip/kernels_mrs_a.hip", "hip/kernels_gadget.hip", "hip/garble_gpu.hip", "hip/runtime.hip",
+               "hip/kernels_mrs_b.hip", "hip/kernels_mrs_c.hip", "hip/kernels_mrs_d.hip", "hip/kernels_mrs_e.hip",
+               "hip/kernels_mrs_f.hip", "hip/kernels_label.hip", "hip/kernels_gemm.hip"]
 
 
 def ext_suffix() -> str:

@@ -421,6 +421,87 @@ __device__ __forceinline__ void aes_encrypt2(const AesT<C>& a, u128 inA, u128 in
 }
 #endif  // DASH_FAKE_AES
 
+// ---------------------------------------------------------------------------
+// Hardened-encoding pads (core.h hard_block): ChaCha12 on
+//   [sigma][K (4 words)][gate lo, gate hi, sub, "HARD"][blk, 0, 0, 0]
+// with feed-forward; pad q of the block = words 4q..4q+3. Pure VALU (adds, xors, 32-bit rotates as
+// v_alignbit): no LDS image, unlike the T-table AES, so hardened kernels leave the LDS to staging.
+#ifndef DASH_CHA_ROUNDS
+#define DASH_CHA_ROUNDS 12  // must equal core.h kChaRounds (part of the hardened encoding)
+#endif
+__device__ __forceinline__ uint32_t rotl(uint32_t x, int r) { return __builtin_rotateleft32(x, r); }
+#define DASH_QR(a, b, c, d)                 \
+    a += b; d = rotl(d ^ a, 16);            \
+    c += d; b = rotl(b ^ c, 12);            \
+    a += b; d = rotl(d ^ a, 8);             \
+    c += d; b = rotl(b ^ c, 7);
+__device__ __forceinline__ void hard_block(u128 K, uint64_t gate, uint32_t sub, uint32_t blk, u128 (&out)[4]) {
+    const uint32_t k0 = static_cast<uint32_t>(K), k1 = static_cast<uint32_t>(K >> 32);
+    const uint32_t k2 = static_cast<uint32_t>(K >> 64), k3 = static_cast<uint32_t>(K >> 96);
+    const uint32_t g0 = static_cast<uint32_t>(gate), g1 = static_cast<uint32_t>(gate >> 32);
+    uint32_t x0 = 0x61707865u, x1 = 0x3320646eu, x2 = 0x79622d32u, x3 = 0x6b206574u;
+    uint32_t x4 = k0, x5 = k1, x6 = k2, x7 = k3, x8 = g0, x9 = g1, x10 = sub, x11 = 0x44524148u;
+    uint32_t x12 = blk, x13 = 0, x14 = 0, x15 = 0;
+#pragma unroll
+    for (int r = 0; r < DASH_CHA_ROUNDS; r += 2) {
+        DASH_QR(x0, x4, x8, x12) DASH_QR(x1, x5, x9, x13) DASH_QR(x2, x6, x10, x14) DASH_QR(x3, x7, x11, x15)
+        DASH_QR(x0, x5, x10, x15) DASH_QR(x1, x6, x11, x12) DASH_QR(x2, x7, x8, x13) DASH_QR(x3, x4, x9, x14)
+    }
+    x0 += 0x61707865u; x1 += 0x3320646eu; x2 += 0x79622d32u; x3 += 0x6b206574u;
+    x4 += k0; x5 += k1; x6 += k2; x7 += k3; x8 += g0; x9 += g1; x10 += sub; x11 += 0x44524148u;
+    x12 += blk;
+    auto pk = [](uint32_t a, uint32_t b, uint32_t c, uint32_t d) -> u128 {
+        return (static_cast<u128>((static_cast<uint64_t>(d) << 32) | c) << 64) | ((static_cast<uint64_t>(b) << 32) | a);
+    };
+    out[0] = pk(x0, x1, x2, x3);
+    out[1] = pk(x4, x5, x6, x7);
+    out[2] = pk(x8, x9, x10, x11);
+    out[3] = pk(x12, x13, x14, x15);
+}
+#undef DASH_QR
+
+// Tweak kinds (core.h TweakKind) and the sub word of row `idx`
+constexpr uint32_t kTwApprox = 1, kTwCast2 = 3, kTwSign = 4, kTwMmg = 5, kTwMmy = 6, kTwMrs = 7, kTwSmrs = 8,
+                   kTwBe = 9, kTwTrans = 10, kTwProj = 11, kTwGme = 12, kTwMmt = 13;
+__device__ __forceinline__ constexpr uint32_t tw_sub(uint32_t kind, uint32_t idx) { return (kind << 16) | (idx & 0xffffu); }
+// gate of element e of a gadget whose PRG streams are stream_id(L, slot, e) (core.h): base = stream_id(L, slot, 0)
+__host__ __device__ __forceinline__ constexpr uint64_t gate_base(uint64_t layer, uint64_t slot) {
+    return (layer << 44) ^ (slot << 36);
+}
+
+// E[t] -= pad t of (K, gate, sub) for t < NT (fan-out row of NT entries, blocks of four pads)
+template <int NT>
+__device__ __forceinline__ void hard_unmask(u128 (&E)[NT], u128 K, uint64_t gate, uint32_t sub) {
+#pragma unroll
+    for (int b = 0; b < (NT + 3) / 4; ++b) {
+        u128 p[4];
+        hard_block(K, gate, sub, static_cast<uint32_t>(b), p);
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+            if (4 * b + q < NT) E[4 * b + q] -= p[q];
+    }
+}
+// runtime row length nt <= NT
+template <int NT>
+__device__ __forceinline__ void hard_unmask_n(u128 (&E)[NT], int nt, u128 K, uint64_t gate, uint32_t sub) {
+#pragma unroll
+    for (int b = 0; b < (NT + 3) / 4; ++b) {
+        if (4 * b >= nt) break;
+        u128 p[4];
+        hard_block(K, gate, sub, static_cast<uint32_t>(b), p);
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+            if (4 * b + q < nt) E[4 * b + q] -= p[q];
+    }
+}
+// single pad of slot s
+__device__ __forceinline__ u128 hard_pad(u128 K, uint64_t gate, uint32_t sub, int s) {
+    u128 p[4];
+    hard_block(K, gate, sub, static_cast<uint32_t>(s) >> 2, p);
+    const int q = s & 3;
+    return q == 0 ? p[0] : (q == 1 ? p[1] : (q == 2 ? p[2] : p[3]));
+}
+
 // Global tables: Te0 (256 words); rk kept for the launch ABI (round keys are literals).
 struct AesGlobals {
     const uint32_t* te0;

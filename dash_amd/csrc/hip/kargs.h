@@ -59,6 +59,12 @@ struct SignArgs {
     int16_t* csum;       // [B][t][kCsumComps][N] per-digit sums of the k cast labels (phase B1)
     int64_t c1off[kMaxMrs];  // offset of digit d's block ((k+1) m_d entries) in a cast1 row
     int fused;           // SignPlan::fused: approx outputs are already cast, carries come out cast (no cast1)
+    // hardened encoding (dev.h hard_block): hx holds the ReLU garbler half gates' pads, ys the sign label's
+    // evaluator-half pads [B][ny][N] (slots 0..k-1 the residues' entries, k.. the packed mini lanes)
+    int hard;
+    uint64_t sgate0, mgate0;  // gate bases of the sign gadget / the mixed-mult gadget (dev.h gate_base)
+    int ny;
+    u128* ys;
 };
 constexpr int kCsumComps = 64;
 
@@ -78,6 +84,9 @@ struct RescaleArgs {
     const int16_t* zero;   // [B][sum n] zero labels of the CRT moduli
     int lab_stride;        // sum_j n_j
     int lab_off[kMaxRes];  // offset of residue j inside up/zero rows
+    int hard;              // hardened encoding: trans pads (TW_TRANS, factor) instead of H
+    uint64_t gate0;
+    int factor;            // index of this factor (the trans row's tweak)
 };
 
 // Single-shot mixed-radix rescale (gadgets.h RescaleMrsPlan)
@@ -99,6 +108,11 @@ struct MrsArgs {
     uint8_t* cs;                   // modes 1, 2: [B][N] its color
     u128* hx;                      // mode 2: [B][k][N] H(compress(Y_j)) of the outputs (the next ReLU's keys)
     uint16_t* colx;                // mode 2: [B][k][N] their colors
+    // hardened encoding (the only one of the mixed-radix constructions): row pads instead of H
+    uint64_t gate0;   // this gadget's gate base (rescale: stream slot 30, sign: slot 1)
+    uint64_t rgate0;  // modes 1, 2: the ReLU mixed-mult gadget's gate base (its y-row / g-row pads)
+    int ny;           // y-row pad slots per element (k entries + packed minis)
+    u128* ys;         // modes 1, 2: [B][ny][N] the sign label's y-row pads
 };
 
 struct BEArgs {
@@ -113,6 +127,8 @@ struct BEArgs {
     int64_t N, n_tab;
     const u128* tab;         // [B][N][n_tab]
     int16_t* work;
+    int hard;
+    uint64_t gate0;
 };
 
 struct ProjArgs {
@@ -120,6 +136,8 @@ struct ProjArgs {
     int pin[kMaxRes], pout[kMaxRes];
     const u128* tab[kMaxRes];  // [B][N][pin_j]
     int64_t N;
+    int hard;
+    uint64_t gate0;
 };
 
 struct MultArgs {
@@ -129,6 +147,8 @@ struct MultArgs {
     const u128* t;  // [B][No][sum]   (mixed only)
     const u128* g;  // [B][No][sum]
     const u128* e;  // same: [B][No][sum]; mixed: [B][No][k][q+1]
+    int hard;
+    uint64_t gate0;
 };
 
 }  // namespace dev

@@ -16,127 +16,11 @@
 #include <cstdio>
 #include <cstdlib>
 
-#include "kargs.h"
-#include "launch.h"
+#include "gadget_common.h"
 
 namespace dash {
 namespace dev {
 
-constexpr size_t kAesLds = 0;  // AES image is static LDS
-
-// AES kernels hold the LDS image (dev.h: 32 KiB at 16 copies) per block; the
-// second launch bound is the minimum number of waves per SIMD, so it sets the
-// register budget: 4 -> 128 VGPRs, 6 -> 80, 8 -> 64. Measured on MiniONN,
-// 24 GCs, one stream (ms per step, scripts/ab_online.py): 64 KiB image at 4
-// waves/SIMD 20.9; 32 KiB image at 6 waves/SIMD 19.7 (the mixed-radix chain
-// 7.4 -> 6.9 ms, approx phase 4.5 -> 4.1); at 8 waves/SIMD the chain spills
-// (9.3 ms). The approx phase has its own knob (8 waves: 4.0-4.3 ms, within the
-// box-to-box noise of 6) and the chain its own (DASH_UA_MINBLOCKS, 4 waves).
-// The 2-way bank conflicts of 16 copies cost less than the extra resident
-// waves buy: these kernels wait on HBM, AES is ~3 % of their time.
-#ifndef DASH_AES_BLOCK
-#define DASH_AES_BLOCK 512
-#endif
-constexpr int kAesBlock = DASH_AES_BLOCK;
-#ifndef DASH_AES_MINBLOCKS
-#define DASH_AES_MINBLOCKS 6
-#endif
-constexpr int kAesMinBlocks = DASH_AES_MINBLOCKS;  // minimum waves per SIMD (register budget)
-#ifndef DASH_SA_MINBLOCKS
-#define DASH_SA_MINBLOCKS 6
-#endif
-constexpr int kSignApproxMinWaves = DASH_SA_MINBLOCKS;
-#ifndef DASH_SA_CHUNK
-#define DASH_SA_CHUNK 16
-#endif
-constexpr int kSignApproxChunk = DASH_SA_CHUNK;  // label loads in flight per lane in the approx phase
-
-// AES kernels stride over their elements so the LDS image is filled once per
-// resident block: resident blocks per CU (register budget: waves per SIMD x 4
-// SIMDs x 64 lanes / block size; LDS: 160 KiB / image), x4 for tail balance.
-static int num_cus() {
-    static int cus = [] {
-        int dev = 0, n = 256;
-        if (hipGetDevice(&dev) == hipSuccess) hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
-        return n;
-    }();
-    return cus;
-}
-static int aes_block_cap(int bs) {
-    const int waves = std::max(kAesMinBlocks, kSignApproxMinWaves);
-    const int resident = std::max(1, std::min(waves * 256 / bs, 160 * 1024 / DASH_AES_LDS_BYTES));
-    return 4 * resident * num_cus();
-}
-static inline dim3 grid_aes(int64_t n, int bs, int y, int z) {
-    int64_t nx = (n + bs - 1) / bs;
-    const int64_t capx = std::max<int64_t>(1, aes_block_cap(bs) / (static_cast<int64_t>(y) * z));
-    return dim3(static_cast<unsigned>(std::min(nx, capx)), y, z);
-}
-// Block size of an AES kernel over n x y x z lanes: kAesBlock when the launch
-// fills every CU at that size, else halved (down to one wave) until it does.
-// Small launches (batch-1 latency, the late small layers) then spread over all
-// CUs with few waves per SIMD, and their lanes are serial chains: a wave that
-// has its SIMD to itself finishes sooner.
-static inline int aes_bs(int64_t n, int y, int z) {
-    const int64_t lanes = n * y * z;
-    int bs = kAesBlock;
-    while (bs > 64 && lanes < static_cast<int64_t>(bs) * num_cus()) bs >>= 1;
-    return bs;
-}
-#define AES_LAUNCH(n, y, z) grid_aes((n), aes_bs((n), (y), (z)), (y), (z)), dim3(aes_bs((n), (y), (z)))
-
-// static (not dynamic) LDS: its address is a link-time constant, so the
-// table base folds into the ds_read offset field
-#define AES_PROLOGUE(tab, rk)                    \
-    __shared__ __attribute__((aligned(16))) uint32_t lds_aes[DASH_AES_LDS_WORDS]; \
-    aes_lds_fill(lds_aes, tab);                   \
-    const AesCtx aes = aes_ctx(lds_aes, rk)
-
-// ---------------------------------------------------------------------------
-// LDS staging of component-major byte labels (rows of N bytes, N % 16 == 0): a block owning BS consecutive
-// elements moves rows [c0, c0 + cnt) of its tile between HBM and an LDS image S[c][BS] with 16-byte
-// accesses, U of them in flight per thread. Lanes then walk their own element's components in LDS. A lane
-// streaming its own column from HBM moves one byte per lane per load (64 B per wave instruction) with a
-// few loads in flight: the streaming kernels sat at 0.2-1.5 TB/s, 65-70 % of cycles waiting (r03 roofline).
-template <int BS, int U>
-__device__ __forceinline__ void lds_stage_rows(uint8_t* S, const act_t* L, int64_t N, int64_t e0, int c0, int cnt) {
-    constexpr int W = BS / 16;  // 16-byte units per row
-    const int units = cnt * W;
-    for (int x0 = threadIdx.x; x0 < units; x0 += U * BS) {
-        uint4 v[U];
-#pragma unroll
-        for (int h = 0; h < U; ++h) {
-            const int x = x0 + h * BS;
-            const int64_t e = e0 + 16 * (x % W);
-            if (x < units && e < N) v[h] = *reinterpret_cast<const uint4*>(L + static_cast<int64_t>(c0 + x / W) * N + e);
-        }
-#pragma unroll
-        for (int h = 0; h < U; ++h) {
-            const int x = x0 + h * BS;
-            if (x < units) *reinterpret_cast<uint4*>(S + (x / W) * BS + 16 * (x % W)) = v[h];
-        }
-    }
-}
-template <int BS>
-__device__ __forceinline__ void lds_store_rows(act_t* L, const uint8_t* S, int64_t N, int64_t e0, int c0, int cnt) {
-    constexpr int W = BS / 16;
-    const int units = cnt * W;
-    for (int x = threadIdx.x; x < units; x += BS) {
-        const int64_t e = e0 + 16 * (x % W);
-        if (e < N)
-            *reinterpret_cast<uint4*>(L + static_cast<int64_t>(c0 + x / W) * N + e) =
-                *reinterpret_cast<const uint4*>(S + (x / W) * BS + 16 * (x % W));
-    }
-}
-// the staged kernels where the shape allows (whole 16-byte rows, at least one full block); A/B knob
-// DASH_MRS_STAGE=0 keeps the per-lane forms
-static inline bool stage_ok(int64_t N, int bs) {
-    static const bool on = [] {
-        const char* e = std::getenv("DASH_MRS_STAGE");
-        return !(e && e[0] == '0');
-    }();
-    return on && N % 16 == 0 && N >= bs;
-}
 
 // ---------------------------------------------------------------------------
 // Phase A tail: the casts Z_{m_d} -> Z_{(k+1) m_d} of residue j's approx
@@ -212,8 +96,28 @@ __global__ __launch_bounds__(kAesBlock, kSignApproxMinWaves) void k_sign_approx(
         for (int d = 0; d < TM; ++d)
             if (d < a.t) P[d] = T[col * a.t + d];
         const u128 C = compress_cm<kSignApproxChunk>(L, N, m);
-        const u128 H = aes_encrypt(aes, C);
         const int64_t bke = (static_cast<int64_t>(b) * a.crt.k + j) * N + e;
+        if (a.hard) {
+            // hardened (fused only): digit d's entry under pad d of (C, sign gate, (TW_APPROX, j)); the ReLU's garbler
+            // half gate keyed by the same label gets its own pad (mixed-mult gate, (TW_MMG, j))
+            const uint64_t sg = a.sgate0 ^ static_cast<uint64_t>(e);
+            u128* out = a.mrsP + (static_cast<int64_t>(b) * a.crt.k + j) * a.t * N + e;
+            for (int blk = 0; 4 * blk < a.t; ++blk) {
+                u128 pd[4];
+                hard_block(C, sg, tw_sub(kTwApprox, j), static_cast<uint32_t>(blk), pd);
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const int d = 4 * blk + q;
+                    if (d < a.t) out[static_cast<int64_t>(d) * N] = T[col * a.t + d] - pd[q];
+                }
+            }
+            if (a.hx) {
+                a.hx[bke] = hard_pad(C, a.mgate0 ^ static_cast<uint64_t>(e), tw_sub(kTwMmg, j), 0);
+                a.colx[bke] = static_cast<uint16_t>(col);
+            }
+            continue;
+        }
+        const u128 H = aes_encrypt(aes, C);
         if (a.hx) {
             a.hx[bke] = H;
             a.colx[bke] = static_cast<uint16_t>(col);
@@ -388,7 +292,8 @@ __global__ __launch_bounds__(kAesBlock, kAesMinBlocks) void k_sign_chain_fused(S
                 }
             const u128 key2 = cf.finish();
             const u128 T2e = T2[c2 + col2];
-            carry = T2e - aes_encrypt(aes, key2);
+            carry = T2e - (a.hard ? hard_pad(key2, a.sgate0 ^ static_cast<uint64_t>(e), tw_sub(kTwCast2, d), 0)
+                                  : aes_encrypt(aes, key2));
             c2 += mo;
         }
         const int m0 = a.mrs[0];
@@ -413,12 +318,24 @@ __global__ __launch_bounds__(kAesBlock, kAesMinBlocks) void k_sign_chain_fused(S
         const u128 key = cf.finish();
         const u128* TS = a.sign + (static_cast<int64_t>(b) * N + e) * a.n_sign;
         const u128 TS0 = TS[col];
-        const u128 H = aes_encrypt(aes, key);
+        const u128 H = a.hard ? 0 : aes_encrypt(aes, key);
+        const uint64_t sg = a.sgate0 ^ static_cast<uint64_t>(e);
         for (int o = 0; o < a.nout; ++o) {
-            const u128 P = (o == 0 ? TS0 : TS[o * m0 + col]) - H;
+            const u128 P = (o == 0 ? TS0 : TS[o * m0 + col]) - (a.hard ? hard_pad(key, sg, tw_sub(kTwSign, 0), o) : H);
             a.outP[(static_cast<int64_t>(b) * a.nout + o) * N + e] = P;
             if (a.relu && o == 0) {
-                a.hs[static_cast<int64_t>(b) * N + e] = aes_encrypt(aes, P);
+                if (a.hard) {  // the sign label's y-row pads (ReLU evaluator half gates + minis)
+                    const uint64_t mg = a.mgate0 ^ static_cast<uint64_t>(e);
+                    for (int blk = 0; 4 * blk < a.ny; ++blk) {
+                        u128 pd[4];
+                        hard_block(P, mg, tw_sub(kTwMmy, 0), static_cast<uint32_t>(blk), pd);
+#pragma unroll
+                        for (int q = 0; q < 4; ++q)
+                            if (4 * blk + q < a.ny) a.ys[(static_cast<int64_t>(b) * a.ny + 4 * blk + q) * N + e] = pd[q];
+                    }
+                } else {
+                    a.hs[static_cast<int64_t>(b) * N + e] = aes_encrypt(aes, P);
+                }
                 a.cs[static_cast<int64_t>(b) * N + e] = static_cast<uint8_t>(static_cast<uint32_t>(P) & 1u);
             }
         }
@@ -453,15 +370,18 @@ __global__ __launch_bounds__(256) void k_relu_mult(SignArgs a, Act x, Act y, con
     const int64_t bke = (static_cast<int64_t>(b) * k + j) * N + e;
     const u128 Hx = a.hx[bke];
     const uint32_t colx = a.colx[bke];
-    const u128 HS = a.hs[static_cast<int64_t>(b) * N + e];
     const uint32_t cS = a.cs[static_cast<int64_t>(b) * N + e];
     const int64_t be = static_cast<int64_t>(b) * N + e;
+    // reference: one H(sign label) masks all k entries and minis; hardened: entry j under y-row pad j, mini j
+    // under lane j % 8 of pad k + j / 8 (MMTw, gadgets.h)
+    const u128 HS = a.hard ? a.ys[(static_cast<int64_t>(b) * a.ny + j) * N + e] : a.hs[be];
+    const u128 HM = a.hard ? (a.ys[(static_cast<int64_t>(b) * a.ny + k + j / 8) * N + e] >> (16 * (j % 8))) : HS;
     const u128 G = gtab[be * a.crt.sum + a.crt.prefix[j] + colx] - Hx;
     const u128* E3 = etab + (be * k + j) * 3;
     const u128 E = E3[cS] - HS;
     const u128 mini = E3[2];
     const int16_t t16 = static_cast<int16_t>(static_cast<uint16_t>(mini >> (16 * cS)));
-    const int16_t ypr16 = static_cast<int16_t>(t16 - static_cast<int16_t>(static_cast<uint16_t>(HS)));
+    const int16_t ypr16 = static_cast<int16_t>(t16 - static_cast<int16_t>(static_cast<uint16_t>(HM)));
     const uint32_t ypr = modq(static_cast<uint32_t>(static_cast<int32_t>(ypr16) + (p << 15)), m);  // p*2^15 > |ypr16|
     const act_t* X = x.p[j] + static_cast<int64_t>(b) * m.n * N + e;
     act_t* Y = y.p[j] + static_cast<int64_t>(b) * m.n * N + e;
@@ -515,7 +435,8 @@ __global__ __launch_bounds__(kRmBS) void k_relu_mult_s(SignArgs a, Act x, Act y,
         const int64_t be = static_cast<int64_t>(b) * N + e;
         const u128 Hx = a.hx[bke];
         const uint32_t colx = a.colx[bke];
-        const u128 HS = a.hs[be];
+        const u128 HS = a.hard ? a.ys[(static_cast<int64_t>(b) * a.ny + j) * N + e] : a.hs[be];
+        const u128 HM = a.hard ? (a.ys[(static_cast<int64_t>(b) * a.ny + k + j / 8) * N + e] >> (16 * (j % 8))) : HS;
         const uint32_t cS = a.cs[be];
         const u128* E3 = etab + (be * k + j) * 3;
         const u128 Graw = gtab[be * a.crt.sum + a.crt.prefix[j] + colx];
@@ -526,7 +447,7 @@ __global__ __launch_bounds__(kRmBS) void k_relu_mult_s(SignArgs a, Act x, Act y,
         __syncthreads();
         const u128 G = Graw - Hx, E = Eraw - HS;
         const int16_t t16 = static_cast<int16_t>(static_cast<uint16_t>(mini >> (16 * cS)));
-        const int16_t ypr16 = static_cast<int16_t>(t16 - static_cast<int16_t>(static_cast<uint16_t>(HS)));
+        const int16_t ypr16 = static_cast<int16_t>(t16 - static_cast<int16_t>(static_cast<uint16_t>(HM)));
         const uint32_t ypr = modq(static_cast<uint32_t>(static_cast<int32_t>(ypr16) + (p << 15)), m);
         if (m.bits) {
             DigitStream sg, se;
@@ -561,7 +482,8 @@ __global__ __launch_bounds__(kRmBS) void k_relu_mult_s(SignArgs a, Act x, Act y,
 // the upshift). grid (ceil(N/256), 1, B)
 __global__ __launch_bounds__(kAesBlock, kAesMinBlocks) void k_rescale_hash(Act x, int fi, int s, const int16_t* up, int up_stride,
                                                       int add_up, int64_t N, u128* h0, uint16_t* col0,
-                                                      const ModC* mc, const uint32_t* te0, const uint32_t* rk) {
+                                                      const ModC* mc, const uint32_t* te0, const uint32_t* rk,
+                                                      int hard) {
     AES_PROLOGUE(te0, rk);
     const int b = blockIdx.z;
     for (int64_t e = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; e < N;
@@ -591,7 +513,8 @@ __global__ __launch_bounds__(kAesBlock, kAesMinBlocks) void k_rescale_hash(Act x
                 cf.push(d, m);
             }
     }
-    h0[static_cast<int64_t>(b) * N + e] = aes_encrypt(aes, cf.finish());
+    // hardened: the key itself (each active residue's update lane derives its own pad, k_rescale_update)
+    h0[static_cast<int64_t>(b) * N + e] = hard ? cf.finish() : aes_encrypt(aes, cf.finish());
     col0[static_cast<int64_t>(b) * N + e] = static_cast<uint16_t>(c0);
     }
 }
@@ -614,7 +537,9 @@ __global__ __launch_bounds__(256) void k_rescale_update(RescaleArgs a, Act x, co
     }
     if (!a.active[j]) return;  // residue of an earlier factor (already zero)
     const int64_t be = static_cast<int64_t>(b) * N + e;
-    const u128 P = a.trans[be * a.n_trans + a.off + static_cast<int64_t>(a.aidx[j]) * a.s + a.col0[be]] - a.h0[be];
+    const u128 mask = a.hard ? hard_pad(a.h0[be], a.gate0 ^ static_cast<uint64_t>(e), tw_sub(kTwTrans, a.factor), a.aidx[j])
+                             : a.h0[be];
+    const u128 P = a.trans[be * a.n_trans + a.off + static_cast<int64_t>(a.aidx[j]) * a.s + a.col0[be]] - mask;
     DigitStream s;
     s.init(P);
     const int32_t inv = a.inv[j];
@@ -705,9 +630,6 @@ __global__ __launch_bounds__(kAesBlock, kAesMinBlocks) void k_rescale_hash_sign(
 #endif
 // the mixed-radix chain keeps K-1 digit streams live: at 6 waves/SIMD (80 VGPRs) it spills 240 B per
 // lane; 4 waves/SIMD with 128 VGPRs measured faster (6.36 vs 7.04 ms per 24-GC MiniONN step)
-#ifndef DASH_UA_MINBLOCKS
-#define DASH_UA_MINBLOCKS 4
-#endif
 constexpr int kChunkUA = DASH_UA_CHUNK;
 template <int TM>
 __global__ __launch_bounds__(kAesBlock, DASH_UA_MINBLOCKS) void k_rescale_update_approx(RescaleArgs r, SignArgs a, Act x, const int16_t* delta,
@@ -793,522 +715,7 @@ void launch_rescale_update_approx(const RescaleArgs& r, const SignArgs& a, const
                            delta, zh, mc, g.te0, g.rk);
 }
 
-// ---------------------------------------------------------------------------
-// Single-shot mixed-radix rescale (gadgets.h RescaleMrsPlan): the serial part
-// runs one lane per (GC, element), K (the CRT size) is a template parameter so
-// the payload matrix P[l][j] (digit l -> later residue j) lives in registers
-// with static indices. Digit i's key is residue i's label minus the payloads
-// of the earlier digits, streamed from HBM, compressed and hashed; its row
-// ([color][K - i] contiguous entries) is gathered while the AES runs. The
-// power-of-two label r = x_u mod 2S is accumulated packed (per-field adds, no
-// decompress), its hash selects the final row; the K final payloads go to
-// a.pf for the elementwise output kernel.
-__device__ __forceinline__ u128 add_packed(u128 a, u128 b, u128 hmask) {
-    return ((a & ~hmask) + (b & ~hmask)) ^ ((a ^ b) & hmask);
-}
 
-// Digit i's key streams residue i's label in chunks of kMrsChunk components,
-// the next chunk's loads issued before the current one is consumed. The
-// payloads P_{l,j} of digit l for later residues j go to a per-lane scratch
-// (a.ps, [B][pair][N], coalesced) and are read back when digit j starts:
-// holding them in registers (up to K(K-1)/2 u128) spilled.
-#ifndef DASH_MRS_CHUNK
-#define DASH_MRS_CHUNK 4  // 8: mode-2 chain spilled 84 B/lane, 4: 28 (mode 0: 52 -> 0); 24 GCs 13.07 -> 12.96 ms
-#endif
-constexpr int kMrsChunk = DASH_MRS_CHUNK;
-#ifndef DASH_MRS_M2CH
-#define DASH_MRS_M2CH 16  // components per load batch of the mod-2 key (modes 1, 2)
-#endif
-template <int K>
-__device__ __forceinline__ constexpr int mrs_pair(int l, int j) {  // l < j < K
-    return l * (2 * K - l - 1) / 2 + (j - l - 1);
-}
-
-// MODE 1 (exact sign, gadgets.h SignMrsPlan): positions convert residues
-// 1..K-1, the last position is residue 0 (mod 2): its key is the bit pack of
-// L_0 XOR the K-1 payloads aimed at it (mod-2 subtraction), i.e. the sign
-// label itself; only its hash and color are produced (the ReLU multiply).
-// MODE 2 (joint rescale + ReLU sign, RescaleMrsPlan::sign_last): MODE 1's
-// order with MODE 0's T target on every row (the mod-2 position's row has only
-// that one) and final row; the mod-2 key's hash and color go to hs / cs.
-#ifndef DASH_CHAIN2_WAVES
-#define DASH_CHAIN2_WAVES 4  // mode 2 (joint rescale + sign) register budget in waves per SIMD
-#endif
-template <int K, int MODE>
-__global__ __launch_bounds__(kAesBlock, MODE == 2 ? DASH_CHAIN2_WAVES : DASH_UA_MINBLOCKS) void k_mrs_chain(MrsArgs a, Act x, const ModC* mc,
-                                                                          const uint32_t* te0, const uint32_t* rk) {
-    AES_PROLOGUE(te0, rk);
-    const int b = blockIdx.z;
-    const int64_t N = a.N;
-    constexpr int NP = K * (K - 1) / 2 > 0 ? K * (K - 1) / 2 : 1;
-    for (int64_t e = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; e < N;
-         e += static_cast<int64_t>(gridDim.x) * blockDim.x) {
-        const u128* row0 = a.tab + (static_cast<int64_t>(b) * N + e) * a.n_tab;
-        u128* PS = a.ps + static_cast<int64_t>(b) * NP * N + e;
-        u128 acc = 0;
-#pragma unroll
-        for (int i = 0; i < (MODE >= 1 ? K - 1 : K); ++i) {
-            const int r = MODE >= 1 ? (i + 1) % K : i;  // residue converted at position i
-            const ModC m = mc[a.crt.p[r]];
-            const int n = static_cast<int>(m.n);
-            const act_t* L = x.p[r] + static_cast<int64_t>(b) * n * N + e;
-            DigitStream ds[K > 1 ? K - 1 : 1];
-#pragma unroll
-            for (int l = 0; l < i; ++l) ds[l].init(PS[static_cast<int64_t>(mrs_pair<K>(l, i)) * N]);
-            CompressFwd cf;
-            cf.init();
-            uint32_t col = 0;
-            uint16_t cur[kMrsChunk], nxt[kMrsChunk];
-#pragma unroll
-            for (int u = 0; u < kMrsChunk; ++u)
-                if (u < n) cur[u] = static_cast<uint16_t>(L[static_cast<int64_t>(u) * N]);
-            for (int c0 = 0; c0 < n; c0 += kMrsChunk) {
-#pragma unroll
-                for (int u = 0; u < kMrsChunk; ++u)
-                    if (c0 + kMrsChunk + u < n) nxt[u] = static_cast<uint16_t>(L[static_cast<int64_t>(c0 + kMrsChunk + u) * N]);
-#pragma unroll
-                for (int u = 0; u < kMrsChunk; ++u)
-                    if (c0 + u < n) {
-                        uint32_t d = cur[u];
-#pragma unroll
-                        for (int l = 0; l < i; ++l) {
-                            const uint32_t s = ds[l].next(m);
-                            d = d >= s ? d - s : d + m.q - s;
-                        }
-                        if (c0 + u == 0) col = d;
-                        cf.push(d, m);
-                    }
-#pragma unroll
-                for (int u = 0; u < kMrsChunk; ++u) cur[u] = nxt[u];
-            }
-            constexpr int kExtra = MODE == 1 ? 0 : 1;        // rescale rows end with the T target
-            const int nt = K - 1 - i + kExtra;
-            const u128* row = row0 + a.dig_off[i] + static_cast<int64_t>(col) * nt;
-            u128 E[K];
-#pragma unroll
-            for (int t = 0; t < nt; ++t) E[t] = row[t];
-            const u128 H = aes_encrypt(aes, cf.finish());
-#pragma unroll
-            for (int t = 0; t < K - 1 - i; ++t) PS[static_cast<int64_t>(mrs_pair<K>(i, i + 1 + t)) * N] = E[t] - H;
-            if (MODE != 1) acc = add_packed(acc, E[K - 1 - i] - H, a.hmask);
-        }
-        if (MODE >= 1) {
-            // last position: residue 0 (mod 2): compress = bit pack, subtraction = XOR
-            const ModC m = mc[a.crt.p[0]];
-            const act_t* L = x.p[0] + static_cast<int64_t>(b) * m.n * N + e;
-            u128 key = compress_cm<DASH_MRS_M2CH>(L, N, m);
-#pragma unroll
-            for (int l = 0; l < K - 1; ++l) key ^= PS[static_cast<int64_t>(mrs_pair<K>(l, K - 1)) * N];
-            const uint32_t c = static_cast<uint32_t>(key) & 1u;
-            u128 E = 0;
-            if (MODE == 2) E = row0[a.dig_off[K - 1] + c];  // the sign digit's T payload row (one entry)
-            const u128 H = aes_encrypt(aes, key);
-            a.hs[static_cast<int64_t>(b) * N + e] = H;
-            a.cs[static_cast<int64_t>(b) * N + e] = static_cast<uint8_t>(c);
-            if (MODE == 2) acc = add_packed(acc, E - H, a.hmask);
-        }
-        if (MODE == 1) continue;
-        const uint32_t col = static_cast<uint32_t>(acc) & static_cast<uint32_t>(a.T - 1);
-        const u128* row = row0 + a.fin_off + static_cast<int64_t>(col) * K;
-        u128 F[K];
-#pragma unroll
-        for (int j = 0; j < K; ++j) F[j] = row[j];
-        const u128 H = aes_encrypt(aes, acc);
-#pragma unroll
-        for (int j = 0; j < K; ++j) a.pf[(static_cast<int64_t>(b) * K + j) * N + e] = F[j] - H;
-    }
-}
-
-// LDS-staged chain (N % 16 == 0, N >= kMrsBS): a block owns kMrsBS consecutive elements and walks the
-// positions in lockstep; residue r's label bytes for the block are brought into LDS by the whole block,
-// kMrsCap components per pass, as 16-byte loads that are all in flight at once, and each lane then reads its
-// components from LDS. The per-lane form (k_mrs_chain) loaded one byte per lane per component, kMrsChunk
-// at a time: ~n / 4 dependent HBM round trips per position, 65 % of its cycles waiting (r03 roofline:
-// 0.87 TB/s fetched). Outputs, payload scratch and table gathers are per lane as before.
-constexpr int kMrsBS = 512;   // elements (lanes) per block
-constexpr int kMrsCap = 64;   // components staged per pass (kMrsCap * kMrsBS = 32 KiB beside the AES image)
-#ifndef DASH_STAGE_U
-#define DASH_STAGE_U 2  // 16-byte loads in flight per thread while staging (4 pushed the chain into spills)
-#endif
-constexpr int kStageU = DASH_STAGE_U;
-#ifndef DASH_STAGE_RD
-#define DASH_STAGE_RD 4  // LDS component reads batched per lane
-#endif
-constexpr int kStageRd = DASH_STAGE_RD;
-// one position of k_mrs_chain_s, I a compile-time constant (constant stream counts and pair indices)
-template <int K, int MODE, int I>
-__device__ __forceinline__ void chain_s_pos(const MrsArgs& a, const AesCtx& aes, const ModC* mc, const Act& x,
-                                            uint8_t* stg, int b, int64_t N, int64_t e0, int tid, bool valid,
-                                            const u128* row0, u128* PS, u128& acc) {
-    constexpr int kLast = MODE >= 1 ? K - 1 : K;
-    if constexpr (I < kLast) {
-        constexpr int i = I;
-        {
-            constexpr int r = MODE >= 1 ? (i + 1) % K : i;
-            const ModC m = mc[a.crt.p[r]];
-            const int n = static_cast<int>(m.n);
-            const act_t* L = x.p[r] + static_cast<int64_t>(b) * n * N;
-            uint32_t col = 0;
-            u128 key;
-            if (m.bits) {  // power-of-two modulus (uniform branch): per-digit streams
-                DigitStream ds[K > 1 ? K - 1 : 1];
-#pragma unroll
-                for (int l = 0; l < i; ++l) ds[l].init(PS[static_cast<int64_t>(mrs_pair<K>(l, i)) * N]);
-                CompressFwd cf;
-                cf.init();
-                for (int c0 = 0; c0 < n; c0 += kMrsCap) {
-                    const int cnt = min(kMrsCap, n - c0);
-                    __syncthreads();
-                    lds_stage_rows<kMrsBS, kStageU>(stg, L, N, e0, c0, cnt);
-                    __syncthreads();
-                    for (int c = 0; c < cnt; ++c) {
-                        uint32_t d = valid ? stg[c * kMrsBS + tid] : 0u;  // spare lanes read no staged bytes
-#pragma unroll
-                        for (int l = 0; l < i; ++l) {
-                            const uint32_t s = ds[l].next(m);
-                            d = d >= s ? d - s : d + m.q - s;
-                        }
-                        if (c0 + c == 0) col = d;
-                        cf.push(d, m);
-                    }
-                }
-                key = cf.finish();
-            } else {
-                // chunk-major walk (as k_mrs_chain_w): passes of whole chunks, one divmod per stream per chunk of
-                // m.c digits, wave-uniform digit loops, one compress flush per chunk
-                u128 Q[K > 1 ? K - 1 : 1];
-#pragma unroll
-                for (int l = 0; l < i; ++l) Q[l] = PS[static_cast<int64_t>(mrs_pair<K>(l, i)) * N];
-                u128 C = 0, PW = 1;
-                const int mcn = static_cast<int>(m.c);
-                const int pass = kMrsCap / mcn * mcn;
-                for (int p0 = 0; p0 < n; p0 += pass) {
-                    const int pcnt = min(pass, n - p0);
-                    __syncthreads();
-                    lds_stage_rows<kMrsBS, kStageU>(stg, L, N, e0, p0, pcnt);
-                    __syncthreads();
-                    for (int c0 = 0; c0 < pcnt; c0 += mcn) {
-                        uint32_t rr[K > 1 ? K - 1 : 1];
-#pragma unroll
-                        for (int l = 0; l < i; ++l) rr[l] = divmod128(Q[l], m.D, m.mD);
-                        const int cnt = min(mcn, pcnt - c0);
-                        uint32_t v = 0, pt = 1;
-                        for (int t = 0; t < cnt; ++t) {
-                            uint32_t d = valid ? stg[(c0 + t) * kMrsBS + tid] : 0u;
-#pragma unroll
-                            for (int l = 0; l < i; ++l) {
-                                const uint32_t sd = chunk_digit(rr[l], m);
-                                d = d >= sd ? d - sd : d + m.q - sd;
-                            }
-                            if (p0 + c0 + t == 0) col = d;
-                            v += d * pt;
-                            pt *= m.q;
-                        }
-                        C += PW * static_cast<u128>(v);
-                        PW *= static_cast<u128>(m.D);
-                    }
-                }
-                key = C;
-            }
-            constexpr int kExtra = MODE == 1 ? 0 : 1;
-            const int nt = K - 1 - i + kExtra;
-            const u128* row = row0 + a.dig_off[i] + static_cast<int64_t>(col) * nt;
-            u128 E[K];
-#pragma unroll
-            for (int t = 0; t < nt; ++t) E[t] = row[t];
-            const u128 H = aes_encrypt(aes, key);
-            if (valid) {
-#pragma unroll
-                for (int t = 0; t < K - 1 - i; ++t) PS[static_cast<int64_t>(mrs_pair<K>(i, i + 1 + t)) * N] = E[t] - H;
-            }
-            if constexpr (MODE != 1) acc = add_packed(acc, E[K - 1 - i] - H, a.hmask);
-        }
-        chain_s_pos<K, MODE, I + 1>(a, aes, mc, x, stg, b, N, e0, tid, valid, row0, PS, acc);
-    }
-}
-
-template <int K, int MODE>
-__global__ __launch_bounds__(kMrsBS, MODE == 2 ? DASH_CHAIN2_WAVES : DASH_UA_MINBLOCKS) void k_mrs_chain_s(
-    MrsArgs a, Act x, const ModC* mc, const uint32_t* te0, const uint32_t* rk) {
-    AES_PROLOGUE(te0, rk);
-    __shared__ __attribute__((aligned(16))) uint8_t stg[kMrsCap * kMrsBS];
-    const int b = blockIdx.z;
-    const int64_t N = a.N;
-    constexpr int NP = K * (K - 1) / 2 > 0 ? K * (K - 1) / 2 : 1;
-    const int tid = static_cast<int>(threadIdx.x);
-    for (int64_t e0 = static_cast<int64_t>(blockIdx.x) * kMrsBS; e0 < N; e0 += static_cast<int64_t>(gridDim.x) * kMrsBS) {
-        const bool valid = e0 + tid < N;
-        const int64_t e = valid ? e0 + tid : N - 1;  // spare lanes shadow a real element, store nothing
-        const u128* row0 = a.tab + (static_cast<int64_t>(b) * N + e) * a.n_tab;
-        u128* PS = a.ps + static_cast<int64_t>(b) * NP * N + e;
-        u128 acc = 0;
-        chain_s_pos<K, MODE, 0>(a, aes, mc, x, stg, b, N, e0, tid, valid, row0, PS, acc);
-        if (MODE >= 1) {
-            const ModC m = mc[a.crt.p[0]];
-            const int n = static_cast<int>(m.n);
-            const act_t* L = x.p[0] + static_cast<int64_t>(b) * n * N;
-            CompressFwd cf;
-            cf.init();
-            for (int c0 = 0; c0 < n; c0 += kMrsCap) {
-                const int cnt = min(kMrsCap, n - c0);
-                __syncthreads();
-                lds_stage_rows<kMrsBS, kStageU>(stg, L, N, e0, c0, cnt);
-                __syncthreads();
-                for (int c = 0; c < cnt; ++c) cf.push(valid ? stg[c * kMrsBS + tid] : 0u, m);
-            }
-            u128 key = cf.finish();
-#pragma unroll
-            for (int l = 0; l < K - 1; ++l) key ^= PS[static_cast<int64_t>(mrs_pair<K>(l, K - 1)) * N];
-            const uint32_t c = static_cast<uint32_t>(key) & 1u;
-            u128 E = 0;
-            if (MODE == 2) E = row0[a.dig_off[K - 1] + c];
-            const u128 H = aes_encrypt(aes, key);
-            if (valid) {
-                a.hs[static_cast<int64_t>(b) * N + e] = H;
-                a.cs[static_cast<int64_t>(b) * N + e] = static_cast<uint8_t>(c);
-            }
-            if (MODE == 2) acc = add_packed(acc, E - H, a.hmask);
-        }
-        if (MODE == 1) continue;
-        const uint32_t colf = static_cast<uint32_t>(acc) & static_cast<uint32_t>(a.T - 1);
-        const u128* row = row0 + a.fin_off + static_cast<int64_t>(colf) * K;
-        u128 F[K];
-#pragma unroll
-        for (int j = 0; j < K; ++j) F[j] = row[j];
-        const u128 H = aes_encrypt(aes, acc);
-        if (valid) {
-#pragma unroll
-            for (int j = 0; j < K; ++j) a.pf[(static_cast<int64_t>(b) * K + j) * N + e] = F[j] - H;
-        }
-    }
-}
-
-// Latency form of the staged chain (small launches: batch 1). The per-lane form streams each position's label
-// from HBM (n / kMrsChunk dependent round trips per position) and passes the pair payloads P_{l,i} between
-// positions through HBM; at batch 1 a launch is one wave per SIMD, so every one of those round trips is
-// exposed (~0.17 ms per rescale whatever N is). Here a block owns kMrsWBS consecutive elements:
-//  * the label rows of EVERY residue come into LDS once, in one loop over all rows with kWaveU 16-byte loads in
-//    flight per thread, before the chain starts;
-//  * the positions read their components from LDS with no barrier;
-//  * the K(K-1)/2 pair payloads stay in registers (one wave per SIMD: the whole 512-VGPR file is the lane's).
-constexpr int kMrsWBS = 256;
-constexpr int kWaveU = 8;
-// one position of k_mrs_chain_w, I a compile-time constant (the pair payloads PS stay in registers)
-template <int K, int MODE, int I>
-__device__ __forceinline__ void chain_w_pos(const MrsArgs& a, const AesCtx& aes, const ModC* mc, const uint8_t* wst,
-                                            const int* roff, int tid, bool valid, const u128* row0, u128* PS,
-                                            u128& acc) {
-    constexpr int kLast = MODE >= 1 ? K - 1 : K;
-    if constexpr (I < kLast) {
-        constexpr int r = MODE >= 1 ? (I + 1) % K : I;
-        const ModC m = mc[a.crt.p[r]];
-        const int n = static_cast<int>(m.n);
-        const uint8_t* Ls = wst + roff[r] * kMrsWBS + tid;
-        uint32_t col = 0;
-        u128 key;
-        if (m.bits) {  // power-of-two modulus (uniform branch): per-digit streams
-            DigitStream ds[I > 0 ? I : 1];
-#pragma unroll
-            for (int l = 0; l < I; ++l) ds[l].init(PS[mrs_pair<K>(l, I)]);
-            CompressFwd cf;
-            cf.init();
-            for (int c = 0; c < n; ++c) {
-                uint32_t d = valid ? Ls[c * kMrsWBS] : 0u;
-#pragma unroll
-                for (int l = 0; l < I; ++l) {
-                    const uint32_t s = ds[l].next(m);
-                    d = d >= s ? d - s : d + m.q - s;
-                }
-                if (c == 0) col = d;
-                cf.push(d, m);
-            }
-            key = cf.finish();
-        } else {
-            // chunk-major walk: every stream shares the modulus, so one divmod per stream per chunk of m.c
-            // digits, then the chunk's digits with a wave-uniform trip count, one compress flush per chunk
-            // (the same digits and compress as DigitStream / CompressFwd, without their per-digit bookkeeping)
-            u128 Q[I > 0 ? I : 1];
-#pragma unroll
-            for (int l = 0; l < I; ++l) Q[l] = PS[mrs_pair<K>(l, I)];
-            u128 C = 0, PW = 1;
-            for (int c0 = 0; c0 < n; c0 += static_cast<int>(m.c)) {
-                uint32_t rr[I > 0 ? I : 1];
-#pragma unroll
-                for (int l = 0; l < I; ++l) rr[l] = divmod128(Q[l], m.D, m.mD);
-                const int cnt = min(static_cast<int>(m.c), n - c0);
-                uint32_t v = 0, pt = 1;
-                for (int t = 0; t < cnt; ++t) {
-                    uint32_t d = valid ? Ls[(c0 + t) * kMrsWBS] : 0u;
-#pragma unroll
-                    for (int l = 0; l < I; ++l) {
-                        const uint32_t sd = chunk_digit(rr[l], m);
-                        d = d >= sd ? d - sd : d + m.q - sd;
-                    }
-                    if (c0 + t == 0) col = d;
-                    v += d * pt;
-                    pt *= m.q;
-                }
-                C += PW * static_cast<u128>(v);
-                PW *= static_cast<u128>(m.D);
-            }
-            key = C;
-        }
-        constexpr int kExtra = MODE == 1 ? 0 : 1;
-        constexpr int nt = K - 1 - I + kExtra;
-        const u128* row = row0 + a.dig_off[I] + static_cast<int64_t>(col) * nt;
-        u128 E[nt > 0 ? nt : 1];
-#pragma unroll
-        for (int t = 0; t < nt; ++t) E[t] = row[t];
-        const u128 H = aes_encrypt(aes, key);
-#pragma unroll
-        for (int t = 0; t < K - 1 - I; ++t) PS[mrs_pair<K>(I, I + 1 + t)] = E[t] - H;
-        if constexpr (MODE != 1) acc = add_packed(acc, E[K - 1 - I] - H, a.hmask);
-        chain_w_pos<K, MODE, I + 1>(a, aes, mc, wst, roff, tid, valid, row0, PS, acc);
-    }
-}
-
-template <int K, int MODE>
-__global__ __launch_bounds__(kMrsWBS, 1) void k_mrs_chain_w(MrsArgs a, Act x, const ModC* mc, const uint32_t* te0,
-                                                            const uint32_t* rk) {
-    AES_PROLOGUE(te0, rk);
-    extern __shared__ __attribute__((aligned(16))) uint8_t wst[];  // row g (residue r, component c) at g * kMrsWBS
-    const int b = blockIdx.z;
-    const int64_t N = a.N;
-    constexpr int NP = K * (K - 1) / 2 > 0 ? K * (K - 1) / 2 : 1;
-    const int tid = static_cast<int>(threadIdx.x);
-    int roff[K + 1];
-    const act_t* src[K];
-    roff[0] = 0;
-#pragma unroll
-    for (int r = 0; r < K; ++r) {
-        const int n = static_cast<int>(mc[a.crt.p[r]].n);
-        roff[r + 1] = roff[r] + n;
-        src[r] = x.p[r] + static_cast<int64_t>(b) * n * N;
-    }
-    const int units = roff[K] * (kMrsWBS / 16);
-    for (int64_t e0 = static_cast<int64_t>(blockIdx.x) * kMrsWBS; e0 < N; e0 += static_cast<int64_t>(gridDim.x) * kMrsWBS) {
-        __syncthreads();  // the previous tile's readers are done
-        if (N % 16 != 0) {
-            // rows not 16-byte aligned (tiny layers, e.g. a 10-logit head): each lane stages its own column, one
-            // byte per row, kWaveBU loads in flight (unit xu = row * kMrsWBS + tid, its LDS offset)
-            constexpr int kWaveBU = 32;
-            const int bunits = roff[K] * kMrsWBS;
-            const int64_t e = e0 + tid;
-            for (int x0 = tid; x0 < bunits; x0 += kWaveBU * kMrsWBS) {
-                uint32_t v[kWaveBU];
-#pragma unroll
-                for (int h = 0; h < kWaveBU; ++h) {
-                    const int xu = x0 + h * kMrsWBS;
-                    const int g = xu / kMrsWBS;
-                    const act_t* row = src[0] + static_cast<int64_t>(g) * N;
-#pragma unroll
-                    for (int r = 1; r < K; ++r)
-                        if (g >= roff[r]) row = src[r] + static_cast<int64_t>(g - roff[r]) * N;
-                    v[h] = (xu < bunits && e < N) ? static_cast<uint32_t>(row[e]) : 0u;
-                }
-#pragma unroll
-                for (int h = 0; h < kWaveBU; ++h) {
-                    const int xu = x0 + h * kMrsWBS;
-                    if (xu < bunits) wst[xu] = static_cast<uint8_t>(v[h]);
-                }
-            }
-        } else
-        for (int x0 = tid; x0 < units; x0 += kWaveU * kMrsWBS) {
-            uint4 v[kWaveU];
-#pragma unroll
-            for (int h = 0; h < kWaveU; ++h) {
-                const int xu = x0 + h * kMrsWBS;
-                const int g = xu >> 4;
-                const int64_t e = e0 + 16 * (xu & 15);
-                const act_t* row = src[0] + static_cast<int64_t>(g) * N;
-#pragma unroll
-                for (int r = 1; r < K; ++r)
-                    if (g >= roff[r]) row = src[r] + static_cast<int64_t>(g - roff[r]) * N;
-                if (xu < units && e < N) v[h] = *reinterpret_cast<const uint4*>(row + e);
-            }
-#pragma unroll
-            for (int h = 0; h < kWaveU; ++h) {
-                const int xu = x0 + h * kMrsWBS;
-                if (xu < units) *reinterpret_cast<uint4*>(wst + (xu >> 4) * kMrsWBS + 16 * (xu & 15)) = v[h];
-            }
-        }
-        __syncthreads();
-        const bool valid = e0 + tid < N;
-        const int64_t e = valid ? e0 + tid : N - 1;  // spare lanes shadow a real element, store nothing
-        const u128* row0 = a.tab + (static_cast<int64_t>(b) * N + e) * a.n_tab;
-        u128 PS[NP];
-        u128 acc = 0;
-        chain_w_pos<K, MODE, 0>(a, aes, mc, wst, roff, tid, valid, row0, PS, acc);
-        if (MODE >= 1) {
-            const ModC m = mc[a.crt.p[0]];
-            const int n = static_cast<int>(m.n);
-            const uint8_t* Ls = wst + tid;
-            CompressFwd cf;
-            cf.init();
-            for (int c = 0; c < n; ++c) cf.push(valid ? Ls[c * kMrsWBS] : 0u, m);
-            u128 key = cf.finish();
-#pragma unroll
-            for (int l = 0; l < K - 1; ++l) key ^= PS[mrs_pair<K>(l, K - 1)];
-            const uint32_t cb = static_cast<uint32_t>(key) & 1u;
-            u128 E = 0;
-            if (MODE == 2) E = row0[a.dig_off[K - 1] + cb];
-            const u128 H = aes_encrypt(aes, key);
-            if (valid) {
-                a.hs[static_cast<int64_t>(b) * N + e] = H;
-                a.cs[static_cast<int64_t>(b) * N + e] = static_cast<uint8_t>(cb);
-            }
-            if (MODE == 2) acc = add_packed(acc, E - H, a.hmask);
-        }
-        if (MODE == 1) continue;
-        const uint32_t colf = static_cast<uint32_t>(acc) & static_cast<uint32_t>(a.T - 1);
-        const u128* row = row0 + a.fin_off + static_cast<int64_t>(colf) * K;
-        u128 F[K];
-#pragma unroll
-        for (int j = 0; j < K; ++j) F[j] = row[j];
-        const u128 H = aes_encrypt(aes, acc);
-        if (valid) {
-#pragma unroll
-            for (int j = 0; j < K; ++j) a.pf[(static_cast<int64_t>(b) * K + j) * N + e] = F[j] - H;
-        }
-    }
-}
-
-// dynamic LDS of k_mrs_chain_w (every residue's rows for kMrsWBS elements), 0 when the form does not apply
-static inline size_t mrs_wave_lds(const MrsArgs& a, int B) {
-    static const bool on = [] {
-        const char* e = std::getenv("DASH_MRS_WAVE");
-        return !(e && e[0] == '0');
-    }();
-    // only launches of at most one block per CU: above that the per-lane form keeps more waves resident (24 GCs,
-    // MiniONN: 11.29 ms per step per-lane vs 11.56 with this form on every small-block launch)
-    // (rows that are not 16-byte aligned: byte-wise staging, only for single-block layers)
-    if (!on || (a.N % 16 != 0 && a.N > kMrsWBS) || (a.N + kMrsWBS - 1) / kMrsWBS * B > num_cus()) return 0;
-    size_t sum = 0;
-    for (int r = 0; r < a.crt.k; ++r) sum += static_cast<size_t>(std::floor(128.0 / std::log2(static_cast<double>(a.crt.p[r]))));  // core.h nr_comps
-    const size_t bytes = sum * kMrsWBS;
-    if (bytes + static_cast<size_t>(DASH_AES_LDS_BYTES) > (160u << 10)) return 0;
-    return bytes;
-}
-
-// launches k_mrs_chain_w<K, MODE> with wl bytes of dynamic LDS (the per-kernel limit is raised once)
-template <int K, int MODE>
-static void launch_chain_w(const MrsArgs& a, const Act& x, int B, size_t wl, const ModC* mc, const AesGlobals& g,
-                           hipStream_t st) {
-    static const bool raised = [] {
-        return hipFuncSetAttribute(reinterpret_cast<const void*>(&k_mrs_chain_w<K, MODE>),
-                                   hipFuncAttributeMaxDynamicSharedMemorySize,
-                                   (160 << 10) - DASH_AES_LDS_BYTES) == hipSuccess;
-    }();
-    (void)raised;
-    const dim3 gw(static_cast<unsigned>((a.N + kMrsWBS - 1) / kMrsWBS), 1, B);
-    hipLaunchKernelGGL((k_mrs_chain_w<K, MODE>), gw, dim3(kMrsWBS), wl, st, a, x, mc, g.te0, g.rk);
-}
-
-// the staged chain holds two 512-lane blocks per CU: below two blocks per CU (batch-1 latency) the per-lane form,
-// whose block size shrinks to spread a small launch over every CU, is faster
-static inline bool mrs_staged(int64_t N, int B) {
-    return stage_ok(N, kMrsBS) && (N + kMrsBS - 1) / kMrsBS * B >= 2 * num_cus();
-}
 
 // Output: Y_0 = pf_0 (mod 2), Y_j = S^-1 L_j + pf_j (mod p_j), in place. grid (ceil(N/256), k, B)
 __global__ __launch_bounds__(256) void k_rescale_mrs_out(MrsArgs a, Act x, const ModC* mc) {
@@ -1350,7 +757,8 @@ __global__ __launch_bounds__(256) void k_rescale_mrs_out(MrsArgs a, Act x, const
 __global__ __launch_bounds__(kAesBlock, kAesMinBlocks) void k_rescale_mrs_out_hash(MrsArgs a, Act x, const ModC* mc,
                                                                                   const uint32_t* te0,
                                                                                   const uint32_t* rk) {
-    AES_PROLOGUE(te0, rk);
+    (void)te0;
+    (void)rk;
     const int j = blockIdx.y, b = blockIdx.z;
     const int64_t N = a.N;
     const int k = a.crt.k;
@@ -1371,7 +779,7 @@ __global__ __launch_bounds__(kAesBlock, kAesMinBlocks) void k_rescale_mrs_out_ha
                 L[static_cast<int64_t>(c) * N] = static_cast<act_t>(v);
             }
             a.colx[bke] = static_cast<uint16_t>(c0);
-            a.hx[bke] = aes_encrypt(aes, P);
+            a.hx[bke] = hard_pad(P, a.rgate0 ^ static_cast<uint64_t>(e), tw_sub(kTwMmg, 0), 0);  // next ReLU g row
             continue;
         }
         const uint32_t inv = static_cast<uint32_t>(a.sinv[j]);
@@ -1398,7 +806,7 @@ __global__ __launch_bounds__(kAesBlock, kAesMinBlocks) void k_rescale_mrs_out_ha
             for (int u = 0; u < kChunk; ++u) cur[u] = nxt[u];
         }
         a.colx[bke] = static_cast<uint16_t>(c0);
-        a.hx[bke] = aes_encrypt(aes, cf.finish());
+        a.hx[bke] = hard_pad(cf.finish(), a.rgate0 ^ static_cast<uint64_t>(e), tw_sub(kTwMmg, j), 0);
     }
 }
 
@@ -1409,7 +817,8 @@ constexpr int kOhBS = 512;
 constexpr int kOhCap = 40;  // 20 KiB image beside the 32 KiB AES image: three blocks per CU
 __global__ __launch_bounds__(kOhBS, kAesMinBlocks) void k_rescale_mrs_out_hash_s(MrsArgs a, Act x, const ModC* mc,
                                                                                const uint32_t* te0, const uint32_t* rk) {
-    AES_PROLOGUE(te0, rk);
+    (void)te0;
+    (void)rk;
     __shared__ __attribute__((aligned(16))) uint8_t stg[kOhCap * kOhBS];
     const int j = blockIdx.y, b = blockIdx.z;
     const int64_t N = a.N;
@@ -1467,7 +876,8 @@ __global__ __launch_bounds__(kOhBS, kAesMinBlocks) void k_rescale_mrs_out_hash_s
             __syncthreads();
             lds_store_rows<kOhBS>(L, stg, N, e0, q0, cnt);
         }
-        const u128 H = aes_encrypt(aes, j == 0 ? P : (m.bits ? cf.finish() : C));
+        const u128 H = hard_pad(j == 0 ? P : (m.bits ? cf.finish() : C),
+                                a.rgate0 ^ static_cast<uint64_t>(valid ? e0 + tid : N - 1), tw_sub(kTwMmg, j), 0);
         if (valid) {
             a.colx[bke] = static_cast<uint16_t>(c0);
             a.hx[bke] = H;
@@ -1486,7 +896,8 @@ __global__ __launch_bounds__(kAesBlock, DASH_RRO_WAVES) void k_rescale_relu_out(
                                                                               const u128* gtab, const u128* etab,
                                                                               const ModC* mc, const uint32_t* te0,
                                                                               const uint32_t* rk) {
-    AES_PROLOGUE(te0, rk);
+    (void)te0;
+    (void)rk;
     const int j = blockIdx.y, b = blockIdx.z;
     const int64_t N = a.N;
     const int k = a.crt.k;
@@ -1500,7 +911,9 @@ __global__ __launch_bounds__(kAesBlock, DASH_RRO_WAVES) void k_rescale_relu_out(
         const int64_t bke = (static_cast<int64_t>(b) * k + j) * N + e;
         act_t* L = x.p[j] + static_cast<int64_t>(b) * n * N + e;
         act_t* Y = y.p[j] + static_cast<int64_t>(b) * n * N + e;
-        const u128 HS = a.hs[be];
+        // hardened y-row pads (chain MODE 2 store_ypads): entry j, mini lane j % 8 of slot k + j / 8
+        const u128 HS = a.ys[(static_cast<int64_t>(b) * a.ny + j) * N + e];
+        const u128 HM = a.ys[(static_cast<int64_t>(b) * a.ny + k + j / 8) * N + e] >> (16 * (j % 8));
         const uint32_t cS = a.cs[be];
         const u128* E3 = etab + (be * k + j) * 3;
         const u128 Eraw = E3[cS];
@@ -1546,10 +959,10 @@ __global__ __launch_bounds__(kAesBlock, DASH_RRO_WAVES) void k_rescale_relu_out(
             }
             key = cf.finish();
         }
-        const u128 G = Graw - aes_encrypt(aes, key);
+        const u128 G = Graw - hard_pad(key, a.rgate0 ^ static_cast<uint64_t>(e), tw_sub(kTwMmg, j), 0);
         const u128 E = Eraw - HS;
         const int16_t t16 = static_cast<int16_t>(static_cast<uint16_t>(mini >> (16 * cS)));
-        const int16_t ypr16 = static_cast<int16_t>(t16 - static_cast<int16_t>(static_cast<uint16_t>(HS)));
+        const int16_t ypr16 = static_cast<int16_t>(t16 - static_cast<int16_t>(static_cast<uint16_t>(HM)));
         const uint32_t ypr = modq(static_cast<uint32_t>(static_cast<int32_t>(ypr16) + (p << 15)), m);
         DigitStream sg, se;
         sg.init(G);
@@ -1588,7 +1001,8 @@ constexpr int kRroBS = 256;
 __global__ __launch_bounds__(kRroBS) void k_rescale_relu_out_s(MrsArgs a, SignArgs sa, Act x, Act y, const u128* gtab,
                                                                 const u128* etab, const ModC* mc, const uint32_t* te0,
                                                                 const uint32_t* rk) {
-    AES_PROLOGUE(te0, rk);
+    (void)te0;
+    (void)rk;
     __shared__ __attribute__((aligned(16))) uint8_t stg[128 * kRroBS];
     const int j = blockIdx.y, b = blockIdx.z;
     const int64_t N = a.N;
@@ -1604,7 +1018,8 @@ __global__ __launch_bounds__(kRroBS) void k_rescale_relu_out_s(MrsArgs a, SignAr
         const int64_t e = min(e0 + tid, N - 1);  // spare lanes shadow a real element; the row stores skip them
         const int64_t be = static_cast<int64_t>(b) * N + e;
         const int64_t bke = (static_cast<int64_t>(b) * k + j) * N + e;
-        const u128 HS = a.hs[be];
+        const u128 HS = a.ys[(static_cast<int64_t>(b) * a.ny + j) * N + e];
+        const u128 HM = a.ys[(static_cast<int64_t>(b) * a.ny + k + j / 8) * N + e] >> (16 * (j % 8));
         const uint32_t cS = a.cs[be];
         const u128* E3 = etab + (be * k + j) * 3;
         const u128 Eraw = E3[cS];
@@ -1629,10 +1044,10 @@ __global__ __launch_bounds__(kRroBS) void k_rescale_relu_out_s(MrsArgs a, SignAr
         const u128 key = j == 0 ? P : cf.finish();
         __syncthreads();
         lds_store_rows<kRroBS>(L, stg, N, e0, 0, n);  // Y_j, the rescaled label
-        const u128 G = Graw - aes_encrypt(aes, key);
+        const u128 G = Graw - hard_pad(key, a.rgate0 ^ static_cast<uint64_t>(e), tw_sub(kTwMmg, j), 0);
         const u128 E = Eraw - HS;
         const int16_t t16 = static_cast<int16_t>(static_cast<uint16_t>(mini >> (16 * cS)));
-        const int16_t ypr16 = static_cast<int16_t>(t16 - static_cast<int16_t>(static_cast<uint16_t>(HS)));
+        const int16_t ypr16 = static_cast<int16_t>(t16 - static_cast<int16_t>(static_cast<uint16_t>(HM)));
         const uint32_t ypr = modq(static_cast<uint32_t>(static_cast<int32_t>(ypr16) + (p << 15)), m);
         DigitStream sg, se;
         sg.init(G);
@@ -1668,7 +1083,8 @@ void launch_rescale_relu_out(const MrsArgs& a, const SignArgs& sa, const Act& x,
 // the approximate path gets them from k_sign_approx). grid (x, k, B)
 __global__ __launch_bounds__(kAesBlock, kAesMinBlocks) void k_label_hash(Act x, CrtInfo crt, int64_t N, u128* hx,
                                                                         uint16_t* colx, const ModC* mc,
-                                                                        const uint32_t* te0, const uint32_t* rk) {
+                                                                        const uint32_t* te0, const uint32_t* rk,
+                                                                        int hard, uint64_t mgate0) {
     AES_PROLOGUE(te0, rk);
     const int j = blockIdx.y, b = blockIdx.z;
     for (int64_t e = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; e < N;
@@ -1677,30 +1093,35 @@ __global__ __launch_bounds__(kAesBlock, kAesMinBlocks) void k_label_hash(Act x, 
         const act_t* L = x.p[j] + static_cast<int64_t>(b) * m.n * N + e;
         const int64_t bke = (static_cast<int64_t>(b) * crt.k + j) * N + e;
         colx[bke] = static_cast<uint16_t>(static_cast<uint16_t>(L[0]) % m.q);
-        hx[bke] = aes_encrypt(aes, compress_cm(L, N, m));
+        const u128 C = compress_cm(L, N, m);
+        hx[bke] = hard ? hard_pad(C, mgate0 ^ static_cast<uint64_t>(e), tw_sub(kTwMmg, j), 0) : aes_encrypt(aes, C);
+    }
+}
+
+// the chain launch of CRT size a.crt.k (per-K units kernels_mrs_*.hip, mrs_chain.h)
+static void dispatch_mrs_chain(const MrsArgs& a, const Act& x, int B, const ModC* mc, const AesGlobals& g,
+                               hipStream_t st) {
+    switch (a.crt.k) {
+        case 2: launch_mrs_chain_k<2>(a, x, B, mc, g, st); break;
+        case 3: launch_mrs_chain_k<3>(a, x, B, mc, g, st); break;
+        case 4: launch_mrs_chain_k<4>(a, x, B, mc, g, st); break;
+        case 5: launch_mrs_chain_k<5>(a, x, B, mc, g, st); break;
+        case 6: launch_mrs_chain_k<6>(a, x, B, mc, g, st); break;
+        case 7: launch_mrs_chain_k<7>(a, x, B, mc, g, st); break;
+        case 8: launch_mrs_chain_k<8>(a, x, B, mc, g, st); break;
+        case 9: launch_mrs_chain_k<9>(a, x, B, mc, g, st); break;
+        case 10: launch_mrs_chain_k<10>(a, x, B, mc, g, st); break;
+        case 11: launch_mrs_chain_k<11>(a, x, B, mc, g, st); break;
+        case 12: launch_mrs_chain_k<12>(a, x, B, mc, g, st); break;
+        default: std::fprintf(stderr, "dash: mixed-radix chains support 2..12 CRT residues\n"); std::abort();
     }
 }
 
 void launch_relu_mrs(const MrsArgs& a, const SignArgs& sa, const Act& x, const Act& y, const u128* gtab,
                      const u128* etab, int B, const ModC* mc, const AesGlobals& g, hipStream_t st) {
     hipLaunchKernelGGL(k_label_hash, AES_LAUNCH(a.N, a.crt.k, B), kAesLds, st, x, a.crt, a.N,
-                       sa.hx, sa.colx, mc, g.te0, g.rk);
-    const bool stg = mrs_staged(a.N, B);
-    const size_t wl = stg ? 0 : mrs_wave_lds(a, B);
-    const dim3 gc = stg ? grid_aes(a.N, kMrsBS, 1, B) : grid_aes(a.N, aes_bs(a.N, 1, B), 1, B);
-    const dim3 bc(stg ? kMrsBS : aes_bs(a.N, 1, B));
-    switch (a.crt.k) {
-#define DASH_MRS_K(KK) \
-        case KK: \
-            if (wl) launch_chain_w<KK, 1>(a, x, B, wl, mc, g, st); \
-            else if (stg) hipLaunchKernelGGL((k_mrs_chain_s<KK, 1>), gc, bc, 0, st, a, x, mc, g.te0, g.rk); \
-            else hipLaunchKernelGGL((k_mrs_chain<KK, 1>), gc, bc, kAesLds, st, a, x, mc, g.te0, g.rk); \
-            break;
-        DASH_MRS_K(2) DASH_MRS_K(3) DASH_MRS_K(4) DASH_MRS_K(5) DASH_MRS_K(6) DASH_MRS_K(7) DASH_MRS_K(8)
-        DASH_MRS_K(9) DASH_MRS_K(10) DASH_MRS_K(11) DASH_MRS_K(12)
-#undef DASH_MRS_K
-        default: std::fprintf(stderr, "dash: mixed-radix sign supports 2..12 CRT residues\n"); std::abort();
-    }
+                       sa.hx, sa.colx, mc, g.te0, g.rk, sa.hard, sa.mgate0);
+    dispatch_mrs_chain(a, x, B, mc, g, st);
     launch_relu_mult(sa, x, y, gtab, etab, mc, st);
 }
 
@@ -1715,25 +1136,7 @@ void launch_relu_joint(const SignArgs& sa, const Act& x, const Act& y, const u12
 
 void launch_rescale_mrs(const MrsArgs& a, const Act& x, int B, const ModC* mc, const AesGlobals& g, hipStream_t st,
                         bool chain_only) {
-    const bool stg = mrs_staged(a.N, B);
-    const size_t wl = stg ? 0 : mrs_wave_lds(a, B);
-    const dim3 gc = stg ? grid_aes(a.N, kMrsBS, 1, B) : grid_aes(a.N, aes_bs(a.N, 1, B), 1, B);
-    const dim3 bc(stg ? kMrsBS : aes_bs(a.N, 1, B));
-    switch (a.crt.k) {
-#define DASH_MRS_K(KK) \
-        case KK: \
-            if (wl && a.mode == 2) launch_chain_w<KK, 2>(a, x, B, wl, mc, g, st); \
-            else if (wl) launch_chain_w<KK, 0>(a, x, B, wl, mc, g, st); \
-            else if (stg && a.mode == 2) hipLaunchKernelGGL((k_mrs_chain_s<KK, 2>), gc, bc, 0, st, a, x, mc, g.te0, g.rk); \
-            else if (stg) hipLaunchKernelGGL((k_mrs_chain_s<KK, 0>), gc, bc, 0, st, a, x, mc, g.te0, g.rk); \
-            else if (a.mode == 2) hipLaunchKernelGGL((k_mrs_chain<KK, 2>), gc, bc, kAesLds, st, a, x, mc, g.te0, g.rk); \
-            else hipLaunchKernelGGL((k_mrs_chain<KK, 0>), gc, bc, kAesLds, st, a, x, mc, g.te0, g.rk); \
-            break;
-        DASH_MRS_K(2) DASH_MRS_K(3) DASH_MRS_K(4) DASH_MRS_K(5) DASH_MRS_K(6) DASH_MRS_K(7) DASH_MRS_K(8)
-        DASH_MRS_K(9) DASH_MRS_K(10) DASH_MRS_K(11) DASH_MRS_K(12)
-#undef DASH_MRS_K
-        default: std::fprintf(stderr, "dash: mixed-radix rescale supports 2..12 CRT residues\n"); std::abort();
-    }
+    dispatch_mrs_chain(a, x, B, mc, g, st);
     if (chain_only) return;  // the joint ReLU's k_rescale_relu_out writes the outputs
     if (a.mode == 2 && stage_ok(a.N, kOhBS))
         hipLaunchKernelGGL(k_rescale_mrs_out_hash_s, grid_aes(a.N, kOhBS, a.crt.k, B), dim3(kOhBS), 0, st, a, x, mc,
@@ -1769,13 +1172,14 @@ __global__ __launch_bounds__(256) void k_base_ext(BEArgs a, Act x, const ModC* m
     for (int i = 0; i < a.nonext; ++i) {
         const ModC mi = mc[a.swapped[i]];
         const int16_t* li = W(i);
-        const u128 H = aes_encrypt(aes, compress_cm(li, N, mi));
+        const u128 C = compress_cm(li, N, mi);
+        const u128 H = a.hard ? 0 : aes_encrypt(aes, C);
         const uint32_t col = static_cast<uint16_t>(li[0]);
         for (int j = 0; j < E - i - 1; ++j) {
             const int tg = i + j + 1;
             const int q = a.swapped[tg];
             const ModC mo = mc[q];
-            const u128 P = T[off + col] - H;
+            const u128 P = T[off + col] - (a.hard ? hard_pad(C, a.gate0 ^ static_cast<uint64_t>(e), tw_sub(kTwBe, i), j) : H);
             off += mi.q;
             DigitStream s;
             s.init(P);
@@ -1811,7 +1215,8 @@ __global__ __launch_bounds__(kAesBlock, kAesMinBlocks) void k_proj(ProjArgs a, A
          e += static_cast<int64_t>(gridDim.x) * blockDim.x) {
     const ModC mi = mc[a.pin[j]], mo = mc[a.pout[j]];
     const act_t* L = x.p[j] + static_cast<int64_t>(b) * mi.n * N + e;
-    const u128 H = aes_encrypt(aes, compress_cm(L, N, mi));
+    const u128 C = compress_cm(L, N, mi);
+    const u128 H = a.hard ? hard_pad(C, a.gate0 ^ static_cast<uint64_t>(e), tw_sub(kTwProj, j), 0) : aes_encrypt(aes, C);
     const uint32_t col = static_cast<uint16_t>(L[0]) % mi.q;
     const u128 P = a.tab[j][(static_cast<int64_t>(b) * N + e) * mi.q + col] - H;
     DigitStream s;
@@ -1835,27 +1240,39 @@ __global__ __launch_bounds__(kAesBlock, kAesMinBlocks) void k_mult(MultArgs a, A
     const act_t* X = x.p[j] + static_cast<int64_t>(b) * m.n * Ni + 2 * o;
     const act_t* Yv = X + 1;
     const int64_t bo = static_cast<int64_t>(b) * No + o;
-    const u128 Hx = aes_encrypt(aes, compress_cm(X, Ni, m));
+    const uint64_t gt = a.gate0 ^ static_cast<uint64_t>(o);
+    const u128 Cx = compress_cm(X, Ni, m);
+    const u128 Hx = a.hard ? hard_pad(Cx, gt, tw_sub(kTwMmg, j), 0) : aes_encrypt(aes, Cx);
     const uint32_t colx = static_cast<uint16_t>(X[0]) % p;
     const u128 G = a.g[bo * a.crt.sum + a.crt.prefix[j] + colx] - Hx;
     u128 E;
     int32_t ypr;
     if (a.q == 0) {
-        const u128 Hy = aes_encrypt(aes, compress_cm(Yv, Ni, m));
+        const u128 Cy = compress_cm(Yv, Ni, m);
+        const u128 Hy = a.hard ? hard_pad(Cy, gt, tw_sub(kTwGme, j), 0) : aes_encrypt(aes, Cy);
         const uint32_t coly = static_cast<uint16_t>(Yv[0]) % p;
         E = a.e[bo * a.crt.sum + a.crt.prefix[j] + coly] - Hy;
         ypr = static_cast<int32_t>(coly);
     } else {
         const ModC mq = mc[a.q];
-        const u128 Hy = aes_encrypt(aes, compress_cm(Yv, Ni, m));
+        const u128 Cy = compress_cm(Yv, Ni, m);
+        const u128 Hy = a.hard ? hard_pad(Cy, gt, tw_sub(kTwMmt, j), 0) : aes_encrypt(aes, Cy);
         const uint32_t coly = static_cast<uint16_t>(Yv[0]) % p;
         const u128 Pt = a.t[bo * a.crt.sum + a.crt.prefix[j] + coly] - Hy;  // compressed label mod q
-        const u128 Ht = aes_encrypt(aes, Pt);
+        u128 Ht, Hm;
+        if (a.hard) {  // own row (TW_MMY, j): entry slot 0, mini lane 0 of slot 1
+            u128 pd[4];
+            hard_block(Pt, gt, tw_sub(kTwMmy, j), 0, pd);
+            Ht = pd[0];
+            Hm = pd[1];
+        } else {
+            Ht = Hm = aes_encrypt(aes, Pt);
+        }
         const uint32_t colt = u128_mod(Pt, mq);
         const u128* E3 = a.e + (bo * a.crt.k + j) * (a.q + 1);
         E = E3[colt] - Ht;
         const int16_t t16 = static_cast<int16_t>(static_cast<uint16_t>(E3[a.q] >> (16 * colt)));
-        ypr = static_cast<int16_t>(t16 - static_cast<int16_t>(static_cast<uint16_t>(Ht)));
+        ypr = static_cast<int16_t>(t16 - static_cast<int16_t>(static_cast<uint16_t>(Hm)));
         ypr %= p;
         if (ypr < 0) ypr += p;
     }
@@ -1937,9 +1354,9 @@ void launch_relu_mult(const SignArgs& a, const Act& x, const Act& y, const u128*
     hipLaunchKernelGGL(k_relu_mult, grid_for(a.N, 256, a.crt.k, a.B), dim3(256), 0, st, a, x, y, gtab, etab, mc);
 }
 void launch_rescale_hash(const Act& x, int fi, int s, const int16_t* up, int up_stride, int add_up, int64_t N, int B,
-                         u128* h0, uint16_t* col0, const ModC* mc, const AesGlobals& g, hipStream_t st) {
+                         u128* h0, uint16_t* col0, const ModC* mc, const AesGlobals& g, hipStream_t st, int hard) {
     hipLaunchKernelGGL(k_rescale_hash, AES_LAUNCH(N, 1, B), kAesLds, st, x, fi, s, up, up_stride,
-                       add_up, N, h0, col0, mc, g.te0, g.rk);
+                       add_up, N, h0, col0, mc, g.te0, g.rk, hard);
 }
 void launch_rescale_update(const RescaleArgs& a, const Act& x, int B, const ModC* mc, hipStream_t st) {
     hipLaunchKernelGGL(k_rescale_update, grid_for(a.N, 256, a.crt.k, B), dim3(256), 0, st, a, x, mc);

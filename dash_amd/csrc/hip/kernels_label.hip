@@ -87,6 +87,18 @@ __global__ __launch_bounds__(512) void k_aes_test(const u128* in, u128* out, int
         out[i] = aes_encrypt(aes, in[i]);
 }
 
+// hardened pads (dev.h hard_block) of n keys: out[4 i + q] = pad q of block blk[i] of (key[i], gate[i], sub[i])
+__global__ __launch_bounds__(256) void k_hard_test(const u128* key, const uint64_t* gate, const uint32_t* sub,
+                                                   const uint32_t* blk, u128* out, int64_t n) {
+    for (int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < n;
+         i += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+        u128 p[4];
+        hard_block(key[i], gate[i], sub[i], blk[i], p);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) out[4 * i + q] = p[q];
+    }
+}
+
 // Throughput probe: every lane runs `iters` x 2 chained encryptions.
 __global__ __launch_bounds__(512) void k_aes_bench(u128* out, int iters, const uint32_t* te0) {
     __shared__ __attribute__((aligned(16))) uint32_t lds_aes[DASH_AES_LDS_WORDS];
@@ -293,6 +305,11 @@ void launch_aes_test(const u128* in, u128* out, int64_t n, const AesGlobals& g, 
 }
 void launch_aes_bench(u128* out, int blocks, int iters, const AesGlobals& g, hipStream_t st) {
     hipLaunchKernelGGL(k_aes_bench, dim3(blocks), dim3(512), 0, st, out, iters, g.te0);
+}
+void launch_hard_test(const u128* key, const uint64_t* gate, const uint32_t* sub, const uint32_t* blk, u128* out,
+                      int64_t n, hipStream_t st) {
+    hipLaunchKernelGGL(k_hard_test, dim3(static_cast<unsigned>(std::min<int64_t>((n + 255) / 256, 1024))), dim3(256), 0,
+                       st, key, gate, sub, blk, out, n);
 }
 void launch_codec_test(const int16_t* labels, int64_t N, int q, const ModC* mc, u128* comp, int16_t* decomp,
                        hipStream_t st) {

@@ -22,7 +22,7 @@ void launch_unpack(const u128* P, int nres, const Act& out, const CrtInfo& mods,
 void launch_relu_mult(const SignArgs& a, const Act& x, const Act& y, const u128* gtab, const u128* etab,
                       const ModC* mc, hipStream_t st);
 void launch_rescale_hash(const Act& x, int fi, int s, const int16_t* up, int up_stride, int add_up, int64_t N, int B,
-                         u128* h0, uint16_t* col0, const ModC* mc, const AesGlobals& g, hipStream_t st);
+                         u128* h0, uint16_t* col0, const ModC* mc, const AesGlobals& g, hipStream_t st, int hard = 0);
 void launch_rescale_update(const RescaleArgs& a, const Act& x, int B, const ModC* mc, hipStream_t st);
 void launch_rescale_post(const Act& x, const CrtInfo& crt, int64_t N, int B, const u128* signP, const int16_t* down,
                          int lab_stride, const int* lab_off, const ModC* mc, hipStream_t st);
@@ -32,6 +32,9 @@ void launch_rescale_update_approx(const RescaleArgs& r, const SignArgs& a, const
                                   const u128* zh, int B, const ModC* mc, const AesGlobals& g, hipStream_t st);
 void launch_rescale_mrs(const MrsArgs& a, const Act& x, int B, const ModC* mc, const AesGlobals& g, hipStream_t st,
                         bool chain_only = false);
+// mixed-radix chain of K residues (mrs_chain.h; instantiated per K in kernels_mrs_*.hip)
+template <int K>
+void launch_mrs_chain_k(const MrsArgs& a, const Act& x, int B, const ModC* mc, const AesGlobals& g, hipStream_t st);
 void launch_rescale_relu_out(const MrsArgs& a, const SignArgs& sa, const Act& x, const Act& y, const u128* gtab,
                              const u128* etab, int B, const ModC* mc, const AesGlobals& g, hipStream_t st);
 void launch_relu_joint(const SignArgs& sa, const Act& x, const Act& y, const u128* gtab, const u128* etab, int B,
@@ -56,6 +59,8 @@ void launch_window_sum(const Act& in, int64_t Nin, const Act& out, int64_t Nout,
                        const CrtInfo& crt, int B, hipStream_t st);
 void launch_aes_bench(u128* out, int blocks, int iters, const AesGlobals& g, hipStream_t st);
 void launch_aes_test(const u128* in, u128* out, int64_t n, const AesGlobals& g, hipStream_t st);
+void launch_hard_test(const u128* key, const uint64_t* gate, const uint32_t* sub, const uint32_t* blk, u128* out,
+                      int64_t n, hipStream_t st);
 void launch_codec_test(const int16_t* labels, int64_t N, int q, const ModC* mc, u128* comp, int16_t* decomp,
                        hipStream_t st);
 

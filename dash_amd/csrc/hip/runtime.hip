@@ -63,8 +63,8 @@ class HipEvaluator {
         // concurrently; unserialized, one slot's constants could land in another's)
         std::lock_guard<std::mutex> load_guard(load_mu_);
         DASH_CHECK(m.h.crt == tmpl_h_.crt && m.h.mrs == tmpl_h_.mrs && m.layers.size() == tmpl_nlayers_ &&
-                       m.h.in_dims == tmpl_h_.in_dims,
-                   "model does not garble the evaluator's circuit");
+                       m.h.in_dims == tmpl_h_.in_dims && m.h.hardened == tmpl_h_.hardened,
+                   "model does not garble the evaluator's circuit (or uses another encoding)");
         HIPCHECK(hipSetDevice(dev_));
         if (!load_st_) HIPCHECK(hipStreamCreateWithFlags(&load_st_, hipStreamNonBlocking));
         // per-GC small constants (bias labels, zero / shift labels, ...): filled into one pinned staging block,
@@ -401,6 +401,12 @@ class HipEvaluator {
         HIPCHECK(hipStreamCreateWithFlags(&copy_st_, hipStreamNonBlocking));
         use_graph_ = false;  // the copy stream's waits on the previous run are issued per run
     }
+    // all-zero device rows (the hardened encoding ships no constant labels: public-constant wires have label 0)
+    const int16_t* zero_i16(size_t count) {
+        int16_t* d = dalloc<int16_t>(count);
+        HIPCHECK(hipMemset(d, 0, std::max<size_t>(count * sizeof(int16_t), 64)));
+        return d;
+    }
     const int16_t* upload_i16_rows(size_t li, const std::string& name) {
         const size_t nb = tmpl_->layers[li].arr(name).nbytes;
         uint8_t* d = dalloc<uint8_t>(nb * B_);
@@ -413,6 +419,7 @@ class HipEvaluator {
     }
     // per-GC concatenated residue labels from model consts ("up.j", "down.s.j", "Z.p")
     const int16_t* upload_const_rows(const std::function<std::string(int)>& name_of) {
+        if (hard_) return zero_i16(static_cast<size_t>(B_) * lab_stride_);
         int16_t* d = dalloc<int16_t>(static_cast<size_t>(B_) * lab_stride_);
         std::vector<std::string> names;
         for (int j = 0; j < k_; ++j) names.push_back(name_of(j));
@@ -450,8 +457,14 @@ class HipEvaluator {
     }
 
     // sign gadget phases over `x` (N elements); results in sign scratch
-    SignArgs make_sign(size_t li, const std::string& pre, const SignPlan& sp, i64 N, int relu) {
+    SignArgs make_sign(size_t li, const std::string& pre, const SignPlan& sp, i64 N, int relu, uint64_t sgate0 = 0,
+                       uint64_t mgate0 = 0) {
         SignArgs a{};
+        a.hard = hard_ ? 1 : 0;
+        a.sgate0 = sgate0;
+        a.mgate0 = mgate0;
+        a.ny = ny_;
+        a.ys = ys_;
         a.crt = crt_info(crt_);
         a.t = static_cast<int>(sp.mrs.size());
         DASH_CHECK(a.t <= kMaxMrs, "MRS base too long for the GPU path");
@@ -502,6 +515,9 @@ class HipEvaluator {
 
     std::shared_ptr<GarbledModel> tmpl_;  // build() only
     ModelHeader tmpl_h_;
+    bool hard_ = false;     // the template's hardened flag (ModelHeader::hardened); every loaded GC must match
+    int ny_ = 0;            // y-row pad slots of a ReLU's sign label: k entries + ceil(k / 8) mini pads
+    u128* ys_ = nullptr;    // [B][ny][maxSignN] y-row pads (hardened ReLU sign labels)
     size_t tmpl_nlayers_ = 0;
     bool mfma_;
     // streamed tables (stream_table / stage_layer)
@@ -588,6 +604,8 @@ class HipEvaluator {
 
 void HipEvaluator::build() {
     const GarbledModel& m0 = *tmpl_;
+    hard_ = m0.h.hardened != 0;
+    ny_ = k_ + (k_ + 7) / 8;
     // ---- global constants
     const int maxmod = m0.h.max_mod;
     std::vector<ModC> mc(maxmod + 1);
@@ -702,6 +720,7 @@ void HipEvaluator::build() {
     outP_ = dalloc<u128>(static_cast<size_t>(B_) * k_ * maxSignN);
     maxSignN_ = maxSignN;
     hs_ = dalloc<u128>(static_cast<size_t>(B_) * maxSignN);
+    if (hard_) ys_ = dalloc<u128>(static_cast<size_t>(B_) * ny_ * maxSignN);
     cs_ = dalloc<uint8_t>(static_cast<size_t>(B_) * maxSignN);
     h0_ = dalloc<u128>(static_cast<size_t>(B_) * maxN);
     col0_ = dalloc<uint16_t>(static_cast<size_t>(B_) * maxN);
@@ -785,7 +804,8 @@ void HipEvaluator::build() {
                         }
                     a.w[j] = upload(wt.data(), wt.size());
                     a.zc[j] = upload(zc.data(), zc.size());
-                    a.bias[j] = upload_i16_rows(li, arr_name("bias.", j, ""));
+                    a.bias[j] = hard_ ? zero_i16(static_cast<size_t>(B_) * a.O * nr_comps(p))
+                                      : upload_i16_rows(li, arr_name("bias.", j, ""));
                 }
                 // MFMA path: centered int8 weights [O][Kpad], channel_tf folded into the column order
                 a.Kpad = static_cast<int>((a.K + 63) / 64 * 64);
@@ -869,7 +889,8 @@ void HipEvaluator::build() {
                         a.w8r[j] = nullptr;
                     }
                     a.zc[j] = upload(zc.data(), zc.size());
-                    a.bias[j] = upload_i16_rows(li, arr_name("bias.", j, ""));
+                    a.bias[j] = hard_ ? zero_i16(static_cast<size_t>(B_) * G.F * nr_comps(p))
+                                      : upload_i16_rows(li, arr_name("bias.", j, ""));
                 }
                 a.zero = zero_rows_;
                 a.lab_stride = lab_stride_;
@@ -894,6 +915,10 @@ void HipEvaluator::build() {
                     sa.colx = colx_;
                     sa.hs = hs_;
                     sa.cs = cs_;
+                    sa.hard = hard_ ? 1 : 0;
+                    sa.mgate0 = gate_base(li + 1, 2);
+                    sa.ny = ny_;
+                    sa.ys = ys_;
                     const u128* gt = upload_tables(li, "mm.g");
                     const u128* et = upload_tables(li, "mm.e");
                     Act x = act_of(cur), y = act_of(nxt);
@@ -927,6 +952,11 @@ void HipEvaluator::build() {
                     a.mode = 1;
                     a.hs = hs_;
                     a.cs = cs_;
+                    DASH_CHECK(hard_, "the mixed-radix sign exists in the hardened encoding only");
+                    a.gate0 = gate_base(li + 1, 1);
+                    a.rgate0 = gate_base(li + 1, 2);
+                    a.ny = ny_;
+                    a.ys = ys_;
                     SignArgs sa{};
                     sa.crt = crt;
                     sa.N = N;
@@ -935,6 +965,10 @@ void HipEvaluator::build() {
                     sa.colx = colx_;
                     sa.hs = hs_;
                     sa.cs = cs_;
+                    sa.hard = 1;
+                    sa.mgate0 = gate_base(li + 1, 2);
+                    sa.ny = ny_;
+                    sa.ys = ys_;
                     const u128* gt = upload_tables(li, "mm.g");
                     const u128* et = upload_tables(li, "mm.e");
                     Act x = act_of(cur), y = act_of(nxt);
@@ -948,7 +982,7 @@ void HipEvaluator::build() {
                     break;
                 }
                 SignPlan sp(crt_, m0.h.mrs, {2}, 0, 1, m0.h.sign_fused != 0);
-                SignArgs a = make_sign(li, "", sp, N, 1);
+                SignArgs a = make_sign(li, "", sp, N, 1, gate_base(li + 1, 1), gate_base(li + 1, 2));
                 const u128* gt = upload_tables(li, "mm.g");
                 const u128* et = upload_tables(li, "mm.e");
                 Act x = act_of(cur), y = act_of(nxt);
@@ -963,7 +997,7 @@ void HipEvaluator::build() {
             }
             case K_SIGN: {
                 SignPlan sp(crt_, m0.h.mrs, crt_, -1, 1, m0.h.sign_fused != 0);
-                SignArgs a = make_sign(li, "", sp, N, 0);
+                SignArgs a = make_sign(li, "", sp, N, 0, gate_base(li + 1, 1), 0);
                 Act x = act_of(cur), y = act_of(nxt);
                 const ModC* mc = mc_;
                 const AesGlobals ag = aes_;
@@ -1006,6 +1040,11 @@ void HipEvaluator::build() {
                     a.cs = cs_;
                     a.hx = hx_;
                     a.colx = colx_;
+                    DASH_CHECK(hard_, "the mixed-radix rescale exists in the hardened encoding only");
+                    a.gate0 = gate_base(li + 1, 30);
+                    a.rgate0 = so ? gate_base(li + 2, 2) : 0;  // the joint ReLU (next layer)'s half gates
+                    a.ny = ny_;
+                    a.ys = ys_;
                     Act x = act_of(cur);
                     const ModC* mc = mc_;
                     const AesGlobals ag = aes_;
@@ -1060,8 +1099,9 @@ void HipEvaluator::build() {
                         u128* h0 = h0_;
                         uint16_t* col0 = col0_;
                         const int ls = lab_stride_;
-                        add_op(lname + ".hash", [x, fi, s, up, ls, add_up, NN, B, h0, col0, mc, ag](hipStream_t st) {
-                            launch_rescale_hash(x, fi, s, up, ls, add_up, NN, B, h0, col0, mc, ag, st);
+                        const int hd = hard_ ? 1 : 0;
+                        add_op(lname + ".hash", [x, fi, s, up, ls, add_up, NN, B, h0, col0, mc, ag, hd](hipStream_t st) {
+                            launch_rescale_hash(x, fi, s, up, ls, add_up, NN, B, h0, col0, mc, ag, st, hd);
                         });
                         RescaleArgs ra{};
                         ra.crt = crt;
@@ -1085,6 +1125,9 @@ void HipEvaluator::build() {
                         ra.zero = zero_rows_;
                         ra.lab_stride = lab_stride_;
                         for (int j = 0; j < k_; ++j) ra.lab_off[j] = lab_off_[j];
+                        ra.hard = hard_ ? 1 : 0;
+                        ra.gate0 = gate_base(li + 1, 10 + it);
+                        ra.factor = static_cast<int>(f);
                         add_op(lname + ".update", [ra, x, B, mc](hipStream_t st) { launch_rescale_update(ra, x, B, mc, st); });
                     }
                     const u128* signP = nullptr;
@@ -1120,6 +1163,8 @@ void HipEvaluator::build() {
                         ba.tab = upload_tables(li, pre + "be");
                         if (!be_work_) be_work_ = dalloc<int16_t>(static_cast<size_t>(B_) * k_ * 128 * maxN);
                         ba.work = be_work_;
+                        ba.hard = hard_ ? 1 : 0;
+                        ba.gate0 = gate_base(li + 1, 10 + it);
                         add_op(lname + ".be", [ba, x, B, mc, ag](hipStream_t st) { launch_base_ext(ba, x, B, mc, ag, st); });
                     }
                     const int16_t* down = upload_const_rows(
@@ -1165,7 +1210,8 @@ void HipEvaluator::build() {
                 for (size_t lv = 0; lv < T.ops.size(); ++lv) {
                     const int ops = T.ops[lv], cnt = T.cnt[lv], cnt1 = T.cnt[lv + 1];
                     const std::string pre = arr_name("lv", static_cast<int>(lv), ".");
-                    SignArgs a = make_sign(li, pre, sp, Nout * ops, 1);
+                    SignArgs a = make_sign(li, pre, sp, Nout * ops, 1, gate_base(li + 1, 20 + 2 * lv),
+                                           gate_base(li + 1, 21 + 2 * lv));
                     const u128* gt = upload_tables(li, pre + "mm.g");
                     const u128* et = upload_tables(li, pre + "mm.e");
                     Act V = act_of(va), D = act_of(cur), Rr = act_of(nxt), NV = act_of(vb);
@@ -1230,6 +1276,8 @@ void HipEvaluator::build() {
                 ProjArgs a{};
                 a.k = k_;
                 a.N = N;
+                a.hard = hard_ ? 1 : 0;
+                a.gate0 = gate_base(li + 1, 1);
                 for (int j = 0; j < k_; ++j) {
                     a.pin[j] = static_cast<int>(inm[j]);
                     a.pout[j] = static_cast<int>(outm[j]);
@@ -1249,6 +1297,8 @@ void HipEvaluator::build() {
                 MultArgs a{};
                 a.crt = crt;
                 a.No = N / 2;
+                a.hard = hard_ ? 1 : 0;
+                a.gate0 = gate_base(li + 1, 1);
                 a.q = g.kind == K_MMULT ? static_cast<int>(g.param("q")) : 0;
                 if (a.q) a.t = upload_tables(li, "t");
                 a.g = upload_tables(li, "g");
@@ -1303,6 +1353,8 @@ void HipEvaluator::build() {
                 ba.tab = upload_tables(li, "be");
                 if (!be_work_) be_work_ = dalloc<int16_t>(static_cast<size_t>(B_) * k_ * 128 * maxN);
                 ba.work = be_work_;
+                ba.hard = hard_ ? 1 : 0;
+                ba.gate0 = gate_base(li + 1, 1);
                 add_op(lname, [ba, x, B, mc, ag](hipStream_t st) { launch_base_ext(ba, x, B, mc, ag, st); });
                 break;
             }
@@ -1606,6 +1658,31 @@ void register_hip_bindings(py::module_& m) {
         (void)hipFree(dte); (void)hipFree(drk); (void)hipFree(din); (void)hipFree(dout);
         return out;
     });
+    m.def("hip_hard_pads", [](py::array_t<uint64_t, py::array::c_style | py::array::forcecast> keys,
+                              py::array_t<uint64_t, py::array::c_style | py::array::forcecast> gates,
+                              py::array_t<uint32_t, py::array::c_style | py::array::forcecast> subs,
+                              py::array_t<uint32_t, py::array::c_style | py::array::forcecast> blks) {
+        DASH_CHECK(keys.ndim() == 2 && keys.shape(1) == 2, "keys: (n, 2) uint64");
+        const int64_t n = keys.shape(0);
+        DASH_CHECK(gates.size() == n && subs.size() == n && blks.size() == n, "one gate / sub / block per key");
+        u128 *dk, *dout;
+        uint64_t* dg;
+        uint32_t *ds, *db;
+        HIPCHECK(hipMalloc(&dk, n * 16 + 16));
+        HIPCHECK(hipMalloc(&dout, n * 64 + 64));
+        HIPCHECK(hipMalloc(&dg, n * 8 + 8));
+        HIPCHECK(hipMalloc(&ds, n * 4 + 4));
+        HIPCHECK(hipMalloc(&db, n * 4 + 4));
+        HIPCHECK(hipMemcpy(dk, keys.data(), n * 16, hipMemcpyHostToDevice));
+        HIPCHECK(hipMemcpy(dg, gates.data(), n * 8, hipMemcpyHostToDevice));
+        HIPCHECK(hipMemcpy(ds, subs.data(), n * 4, hipMemcpyHostToDevice));
+        HIPCHECK(hipMemcpy(db, blks.data(), n * 4, hipMemcpyHostToDevice));
+        launch_hard_test(dk, dg, ds, db, dout, n, nullptr);
+        py::array_t<uint64_t> out({static_cast<py::ssize_t>(n), static_cast<py::ssize_t>(4), static_cast<py::ssize_t>(2)});
+        HIPCHECK(hipMemcpy(out.mutable_data(), dout, n * 64, hipMemcpyDeviceToHost));
+        (void)hipFree(dk); (void)hipFree(dout); (void)hipFree(dg); (void)hipFree(ds); (void)hipFree(db);
+        return out;
+    }, "hardened-encoding pads computed on the GPU (dev.h hard_block), (n, 4, 2) uint64");
     m.def("hip_aes_bench", [](int blocks, int iters) {
         // returns (ms, AES blocks per second)
         auto te = make_te0();

@@ -36,6 +36,7 @@ void GpuGarbler::relu_mrs(uint64_t, const SignMrsPlan&, CrtLabels&, Array&, cons
 void GpuGarbler::relu_mult(uint64_t, CrtLabels&, const std::vector<i64>*, Array&, Array&) { no_gpu(); }
 void GpuGarbler::dense(i64, i64, i64, const i64*, size_t, uint64_t, CrtLabels&) { no_gpu(); }
 void GpuGarbler::sumpool(const PoolGeom&, CrtLabels&) { no_gpu(); }
+void GpuGarbler::fold_constants(const std::vector<i64>&, i64, CrtLabels&) { no_gpu(); }
 void GpuGarbler::save(size_t) { no_gpu(); }
 bool GpuGarbler::has_saved(size_t) const { return false; }
 void GpuGarbler::restore(size_t, CrtLabels&) { no_gpu(); }

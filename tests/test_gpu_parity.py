@@ -25,8 +25,9 @@ def _same(a: bytes, b: bytes) -> bool:
 FUSED = pytest.mark.parametrize("fused", [True, False], ids=["fused", "refcasts"])
 
 
-def _check(circuit, crt, mrs, xs, mfma=True, plain=True, fused=True, rescale="legacy", relu="approx"):
-    gcs = [GarbledCircuit(circuit, crt, mrs, seed=bytes([i + 1]) * 16, fused_sign=fused, rescale=rescale, relu=relu)
+def _check(circuit, crt, mrs, xs, mfma=True, plain=True, fused=True, rescale="legacy", relu="approx", hardened=None):
+    gcs = [GarbledCircuit(circuit, crt, mrs, seed=bytes([i + 1]) * 16, fused_sign=fused, rescale=rescale, relu=relu,
+                          hardened=hardened)
            for i in range(len(xs))]
     enc = [g.garble_inputs(x) for g, x in zip(gcs, xs)]
     cpu = [g.cpu_evaluate(e) for g, e in zip(gcs, enc)]
@@ -48,6 +49,32 @@ def test_aes_parity(native):
     rng = np.random.default_rng(0)
     a = rng.integers(0, 2**63, size=(1000, 2), dtype=np.uint64)
     np.testing.assert_array_equal(native.hip_aes_hash_array(a), native.aes_hash_array(a))
+
+
+def test_hard_pad_parity(native):
+    """Hardened-encoding pads: the GPU's ChaCha12 (dev.h hard_block) == the host's (core.h), every word."""
+    rng = np.random.default_rng(7)
+    n = 600
+    keys = rng.integers(0, 2**63, size=(n, 2), dtype=np.uint64) * np.uint64(2) + np.uint64(1)
+    gates = rng.integers(0, 2**62, size=n, dtype=np.uint64)
+    subs = rng.integers(0, 2**31, size=n, dtype=np.uint64).astype(np.uint32)
+    blks = rng.integers(0, 4, size=n, dtype=np.uint64).astype(np.uint32)
+    dev = native.hip_hard_pads(keys, gates, subs, blks)
+    for i in range(0, n, 37):
+        K = int(keys[i, 0]) | (int(keys[i, 1]) << 64)
+        host = native.hard_pads(K, int(gates[i]), int(subs[i]), int(blks[i]))
+        for q in range(4):
+            assert (int(dev[i, q, 0]) | (int(dev[i, q, 1]) << 64)) == host[q]
+
+
+@pytest.mark.parametrize("hardened", [True, False], ids=["hardened", "reference"])
+def test_dense_relu_encodings(hardened):
+    """Both offline-message encodings through the HIP evaluator: labels bit-exact vs the host oracle."""
+    rng = np.random.default_rng(11)
+    W1 = rng.integers(-8, 9, (24, 30)); b1 = rng.integers(-8, 9, 24)
+    c = d.Circuit([d.Dense.from_quantized(W1, b1), d.Relu((24,)), d.Dense.from_quantized(W1[:6, :24], b1[:6])])
+    xs = [rng.integers(-20, 20, 30) for _ in range(3)]
+    _check(c, 7, 100.0, xs, hardened=hardened)
 
 
 @pytest.mark.parametrize("q", [2, 3, 5, 7, 11, 13, 17, 19, 23, 32, 56, 86, 97, 107, 167, 173])
