@@ -120,7 +120,13 @@ std::vector<i64> neg_mod(const std::vector<i64>& v, i64 M) {
 }
 
 // whether the GPU garbler produces hardened gadget tables (else hardened gadget layers garble on the host)
-bool gpu_hardened() { return false; }
+bool gpu_hardened() {
+    static const bool on = [] {
+        const char* e = std::getenv("DASH_GG_HARD");  // 0: hardened gadget layers on the host garbler (A/B)
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
 
 struct ReluTables {
     Array approx, cast1, cast2, sign, g, e;
@@ -388,7 +394,7 @@ GarbledModel Garbler::garble(const std::vector<LayerSpec>& layers, const std::ve
     }
 
     std::unique_ptr<GpuGarbler> gpu;
-    if (opt.device >= 0) gpu.reset(new GpuGarbler(crt_, mrs_, seed_, R_, Z_, opt.device));
+    if (opt.device >= 0) gpu.reset(new GpuGarbler(crt_, mrs_, seed_, R_, Z_, opt.device, hard));
     // zero-copy offline phase: a GPU-garbled table whose destination the sink knows (an evaluator slot) is
     // written there directly; the model's array then aliases that buffer
     size_t cur_layer = 0;

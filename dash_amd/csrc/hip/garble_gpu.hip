@@ -64,6 +64,10 @@ struct Proj {
     int64_t off;                 // entry offset inside the element's table row
     int64_t first;               // first global entry index of this projection
     int pay1;                    // unused by the kernels (k_emit's bank indices: EProj::pay1)
+    // hardened encoding (core.h Mask): the row's tweak sub word and the pad slot of its first target (fan-out
+    // rows F_LUT / F_FAN use slot hslot + d for target d); the gate is the gadget's PRG stream
+    uint32_t hsub = 0;
+    int hslot = 0;
 };
 
 struct Tables {
@@ -80,6 +84,7 @@ struct Ctx {
     // multiples of this GC's offsets, per modulus p (null until a projection of that modulus needs them):
     // iR[p] = [p][4 * chunks(n_p)] words, row i = the components i * R_p[q] mod p packed two per word
     const uint32_t* const* iR;
+    int hard;  // hardened encoding: HC holds the compressed keys, k_emit / k_relu_finish derive tweaked pads
 };
 
 // Chunked component-major labels (all device labels of the GPU garbler): the
@@ -283,6 +288,8 @@ __device__ __forceinline__ Proj rfl_proj(const Proj& p) {
     r.off = rfl64(p.off);
     r.first = rfl64(p.first);
     r.pay1 = rfl(p.pay1);
+    r.hsub = rflu(p.hsub);
+    r.hslot = rfl(p.hslot);
     return r;
 }
 
@@ -550,7 +557,7 @@ __global__ __launch_bounds__(kPB) void k_hash(Ctx c, Gadget g, In in) {
         CompressFwd kc;
         kc.init();
         push_lin<true, true>(kc, x, row_ref(c.R + static_cast<int64_t>(P.pin) * kW), i, mi, col);
-        const u128 H = aes_encrypt(aes, kc.finish());
+        const u128 H = c.hard ? kc.finish() : aes_encrypt(aes, kc.finish());
         if (e_raw < N) {
             g.HC[r * N + e] = H;
             g.CC[r * N + e] = static_cast<uint16_t>(i);
@@ -595,7 +602,7 @@ __global__ __launch_bounds__(kPB, 4) void k_hash_jobs(Ctx c, Gadget g, In in, co
             CompressFwd kc;
             kc.init();
             push_lin<true, true>(kc, x, row_ref(R), i, mi, static_cast<uint32_t>(col));
-            const u128 H = aes_encrypt(aes, kc.finish());
+            const u128 H = c.hard ? kc.finish() : aes_encrypt(aes, kc.finish());
             if (e_raw < N) {
                 g.HC[(P.first + col) * N + e] = H;
                 g.CC[(P.first + col) * N + e] = static_cast<uint16_t>(i);
@@ -808,7 +815,12 @@ __global__ __launch_bounds__(kPB, 4) void k_hash_iu(Ctx c, Gadget g, In in, cons
                 uint32_t col1, col2;
                 compress_xa2(x, rows + static_cast<int64_t>(i) * words, rows + static_cast<int64_t>(i + 1) * words, mi,
                              k1, k2, col1, col2);
-                aes_encrypt2(aes, k1, k2, H1, H2);
+                if (c.hard) {  // hardened: the keys themselves (k_emit derives each entry's tweaked pad)
+                    H1 = k1;
+                    H2 = k2;
+                } else {
+                    aes_encrypt2(aes, k1, k2, H1, H2);
+                }
                 if (e_raw < N) {  // rows by entry index (coalesced); CC = color - i (k_emit inverts in LDS)
                     g.HC[(P.first + i) * N + e] = H1;
                     g.CC[(P.first + i) * N + e] = static_cast<uint16_t>(static_cast<int>(col1) - i);
@@ -820,7 +832,7 @@ __global__ __launch_bounds__(kPB, 4) void k_hash_iu(Ctx c, Gadget g, In in, cons
         for (; i < c1; ++i) {
             uint32_t col;
             const u128 key = compress_xa(x, rows + static_cast<int64_t>(i) * words, mi, col);
-            const u128 H = aes_encrypt(aes, key);
+            const u128 H = c.hard ? key : aes_encrypt(aes, key);
             if (e_raw < N) {
                 g.HC[(P.first + i) * N + e] = H;
                 g.CC[(P.first + i) * N + e] = static_cast<uint16_t>(static_cast<int>(col) - i);
@@ -915,6 +927,8 @@ struct BankRow {
     int slot, pout, v, res;  // payload = slot label + v * (res < 0 ? R_pout : input label of residue res) mod pout
 };
 struct EProj {
+    uint32_t hsub;  // hardened tweak (Proj::hsub / hslot)
+    int hslot;
     int first;  // first key-hash entry (HC / CC row)
     int pay1;   // element-independent f: bix base (bank row of (i, d) at bix[pay1 + i * t + d]);
                 // F_MULR / F_NEGR: scope-relative bank row of v = 0 (rows v = 0 .. pout - 1)
@@ -1122,7 +1136,13 @@ __global__ __launch_bounds__(kEB) void k_emit(Ctx c, Gadget g, In in, Tables tb,
                 } else {
                     br = BIX[P.pay1 - bx0 + i * P.t + static_cast<int>(mm[u] & 0xfffu)];
                 }
-                v[u] = PBL[br * te1 + el[u]] + HCL[rr * te1 + el[u]];
+                if (c.hard) {
+                    const uint64_t gate = stream_of(g.layer, g.sslot, static_cast<uint64_t>(e0 + el[u]), g.mask);
+                    const int slot = P.hslot + ((P.fn == F_LUT || P.fn == F_FAN) ? static_cast<int>(mm[u] & 0xfffu) : 0);
+                    v[u] = PBL[br * te1 + el[u]] + hard_pad(HCL[rr * te1 + el[u]], gate, P.hsub, slot);
+                } else {
+                    v[u] = PBL[br * te1 + el[u]] + HCL[rr * te1 + el[u]];
+                }
             }
 #pragma unroll
             for (int u = 0; u < kUn; ++u) {
@@ -1281,7 +1301,10 @@ __global__ __launch_bounds__(256) void k_relu_finish(Ctx c, Gadget g, In in, Tab
         int16_t* t16 = reinterpret_cast<int16_t*>(tb.t[5] + (e * m.k + j) * 3 + 2);
         for (int i = 0; i < 2; ++i) {
             const uint32_t color = static_cast<uint32_t>(sig0 + i * R2[0]) & 1u;
-            const u128 H = hk[i * N + e];
+            // hardened: lane j % 8 of pad k + j / 8 of the sign label's y row (MMTw, gadgets.h)
+            const u128 H = c.hard ? (hard_pad(hk[i * N + e], stream_of(g.layer, g.sslot, static_cast<uint64_t>(e), g.mask),
+                                              tw_sub(kTwMmy, 0), m.k + j / 8) >> (16 * (j % 8)))
+                                  : hk[i * N + e];
             const int fv = (i + r) % p;
             t16[color] = static_cast<int16_t>(static_cast<int16_t>(fv) + static_cast<int16_t>(static_cast<uint16_t>(H)));
         }
@@ -1341,7 +1364,12 @@ __global__ __launch_bounds__(kGB) void k_bin_keys(Ctx c, const int16_t* x, const
         const u128 key0 = ((static_cast<u128>((static_cast<uint64_t>(k0[3]) << 32) | k0[2]) << 64) |
                            ((static_cast<uint64_t>(k0[1]) << 32) | k0[0])) ^ abits;  // mod-2 add = XOR of the bits
         u128 h0, h1;
-        aes_encrypt2(aes, key0, key0 ^ rbits, h0, h1);
+        if (c.hard) {  // hardened: the keys (k_relu_finish derives the mini pads)
+            h0 = key0;
+            h1 = key0 ^ rbits;
+        } else {
+            aes_encrypt2(aes, key0, key0 ^ rbits, h0, h1);
+        }
         hk[e] = h0;
         hk[N + e] = h1;
     }
@@ -1657,22 +1685,29 @@ SignLayout sign_layout_fused(const SignPlan& P, int extra_slots) {
         first += p.pin;
         L.projs.push_back(p);
     };
-    for (int j = 0; j < k; ++j)
-        add(Proj{S_INPUT, j, P.crt[j], dig0 + j * t, P.mrs[0], F_LUT, j, 0, t, R_BANK, 0, 0, t,
-                 t * P.crt_prefix[j], 0});
+    for (int j = 0; j < k; ++j) {
+        Proj ap{S_INPUT, j, P.crt[j], dig0 + j * t, P.mrs[0], F_LUT, j, 0, t, R_BANK, 0, 0, t, t * P.crt_prefix[j], 0};
+        ap.hsub = tw_sub(kTwApprox, static_cast<uint32_t>(j));  // slots = digits
+        add(ap);
+    }
     int64_t c2 = 0;
     for (int q = 0; q + 1 < t; ++q) {
         const int d = t - 1 - q;
         const int mo = P.digit_mod(d);
-        const Proj cp{S_SLOT, sum2_0 + q, mo, newc0 + q, P.carry_mod(d), F_DIVMOD, P.mrs[d], P.mrs[d - 1], 0, R_BANK, 0,
-                      2, 1, c2, 0};
+        Proj cp{S_SLOT, sum2_0 + q, mo, newc0 + q, P.carry_mod(d), F_DIVMOD, P.mrs[d], P.mrs[d - 1], 0, R_BANK, 0,
+                2, 1, c2, 0};
+        cp.hsub = tw_sub(kTwCast2, static_cast<uint32_t>(d));
         add(cp);
         c2 += mo;
     }
     const int m0 = P.mrs[0];
-    for (size_t o = 0; o < P.out_mod.size(); ++o)
-        add(Proj{S_SLOT, sum_slot, m0, L.out_slot0 + static_cast<int>(o), P.out_mod[o], F_SIGN, m0 / 2, P.lower, P.upper,
-                 R_BANK, 0, 3, 1, static_cast<int64_t>(o) * m0, 0});
+    for (size_t o = 0; o < P.out_mod.size(); ++o) {
+        Proj sp{S_SLOT, sum_slot, m0, L.out_slot0 + static_cast<int>(o), P.out_mod[o], F_SIGN, m0 / 2, P.lower, P.upper,
+                R_BANK, 0, 3, 1, static_cast<int64_t>(o) * m0, 0};
+        sp.hsub = tw_sub(kTwSign, 0);
+        sp.hslot = static_cast<int>(o);
+        add(sp);
+    }
     L.entries = first;
     return L;
 }
@@ -2166,6 +2201,8 @@ void project(const gg::Ctx& c, gg::Gadget& g, const gg::In& in, const gg::Tables
             const auto& p = pr[pi];
             gg::EProj& E = ep[pi];
             E.first = static_cast<int>(p.first);
+            E.hsub = p.hsub;
+            E.hslot = p.hslot;
             E.fn = p.fn;
             E.t = targets(p);
             E.res = elem_dep(p) ? p.a0 : -1;
@@ -2582,10 +2619,11 @@ struct GpuGarbler::Impl {
 };
 
 GpuGarbler::GpuGarbler(const std::vector<int>& crt, const std::vector<int>& mrs, const std::string& seed16,
-                       const LabelBank& R, const LabelBank& Z, int device)
+                       const LabelBank& R, const LabelBank& Z, int device, bool hardened)
     : impl_(new Impl(device)) {
     Impl& I = *impl_;
     I.enter();
+    I.c.hard = hardened ? 1 : 0;
     I.crt = crt;
     I.k = static_cast<int>(crt.size());
     I.max_mod = R.max_mod;
@@ -2864,6 +2902,7 @@ static std::vector<DevBlock> sign_core(GpuGarbler::Impl& I, uint64_t layer, uint
         for (int j = 0; j < k; ++j) {
             const int p = I.crt[j];
             gg::Proj a{gg::S_INPUT, j, p, sk0 + 2 * j, p, gg::F_MULR, j, 0, 0, gg::R_BANK, 0, 4, 1, (*prefix)[j], first};
+            a.hsub = tw_sub(kTwMmg, static_cast<uint32_t>(j));
             first += p;
             pr.push_back(a);
         }
@@ -2871,6 +2910,8 @@ static std::vector<DevBlock> sign_core(GpuGarbler::Impl& I, uint64_t layer, uint
             const int p = I.crt[j];
             gg::Proj b{gg::S_SLOT, L.out_slot0, 2, sk0 + 2 * j + 1, p, gg::F_NEGR, j, 0, 0, gg::R_INPUT, j, 5, 1,
                        static_cast<int64_t>(j) * 3, first};
+            b.hsub = tw_sub(kTwMmy, 0);  // the sign label's y row, slot j
+            b.hslot = j;
             first += 2;
             pr.push_back(b);
         }
@@ -3056,6 +3097,7 @@ static std::vector<DevBlock> relu_mult_gates(GpuGarbler::Impl& I, const gg::Gadg
     for (int j = 0; j < k; ++j) {
         const int p = I.crt[j];
         gg::Proj q{gg::S_INPUT, j, p, sk0 + 2 * j, p, gg::F_MULR, j, 0, 0, gg::R_BANK, 0, 4, 1, prefix[j], f2};
+        q.hsub = tw_sub(kTwMmg, static_cast<uint32_t>(j));
         f2 += p;
         pm.push_back(q);
     }
@@ -3063,6 +3105,8 @@ static std::vector<DevBlock> relu_mult_gates(GpuGarbler::Impl& I, const gg::Gadg
         const int p = I.crt[j];
         gg::Proj q{gg::S_SLOT, sig_slot, 2, sk0 + 2 * j + 1, p, gg::F_NEGR, j, 0, 0, gg::R_INPUT, j, 5, 1,
                    static_cast<int64_t>(j) * 3, f2};
+        q.hsub = tw_sub(kTwMmy, 0);
+        q.hslot = j;
         f2 += 2;
         pm.push_back(q);
     }
@@ -3139,6 +3183,7 @@ void GpuGarbler::relu_mrs(uint64_t layer, const SignMrsPlan& P, CrtLabels& cur, 
         p.in_kind = gg::S_SLOT; p.in_idx = a.key0 + r0; p.pin = P.crt[r0];
         p.out_slot = dig0[i]; p.pout = P.crt[P.target_res(i, 0)]; p.fn = gg::F_FAN; p.a0 = a0; p.a1 = a1;
         p.outr_kind = gg::R_BANK; p.table = 0; p.stride = nt; p.off = P.dig_off[i]; p.first = first;
+        p.hsub = tw_sub(kTwSmrs, static_cast<uint32_t>(i));
         first += P.crt[r0];
         pr.push_back(p);
     }
@@ -3244,6 +3289,7 @@ void GpuGarbler::rescale_mrs(uint64_t layer, const RescaleMrsPlan& P, CrtLabels&
         p.in_kind = gg::S_SLOT; p.in_idx = a.key0 + r0; p.pin = P.crt[r0];
         p.out_slot = dig0[i]; p.pout = P.target_mod(i, 0); p.fn = gg::F_FAN; p.a0 = a0; p.a1 = a1;
         p.outr_kind = gg::R_BANK; p.table = 0; p.stride = nt; p.off = P.dig_off[i]; p.first = first;
+        p.hsub = tw_sub(kTwMrs, static_cast<uint32_t>(i));
         first += P.crt[r0];
         pr.push_back(p);
     }
@@ -3257,6 +3303,7 @@ void GpuGarbler::rescale_mrs(uint64_t layer, const RescaleMrsPlan& P, CrtLabels&
         p.in_kind = gg::S_SLOT; p.in_idx = a.acc; p.pin = static_cast<int>(P.T);
         p.out_slot = a.fin0; p.pout = P.crt[0]; p.fn = gg::F_FAN; p.a0 = a0; p.a1 = a1;
         p.outr_kind = gg::R_BANK; p.table = 0; p.stride = k; p.off = P.fin_off; p.first = first;
+        p.hsub = tw_sub(kTwMrs, static_cast<uint32_t>(k));
         first += P.T;
         pr.push_back(p);
     }
@@ -3506,6 +3553,8 @@ void be_run(GpuGarbler::Impl& I, gg::Gadget& g, const BEPlan& P, const std::vect
             const int tg = i + j + 1;
             gg::Proj p{gg::S_SLOT, lw0 + i, P.swapped[i], st.slot[i][j], P.swapped[tg], gg::F_IDENT, 0, 0, 0,
                        gg::R_BANK, 0, table, 1, off, first};
+            p.hsub = tw_sub(kTwBe, static_cast<uint32_t>(i));
+            p.hslot = j;
             off += P.swapped[i];
             first += P.swapped[i];
             pr.push_back(p);
@@ -3831,8 +3880,10 @@ void GpuGarbler::rescale_redash(uint64_t layer, int it, const RescalePlan& P, Cr
         int64_t first = 0;
         for (size_t a = 0; a < P.active[f].size(); ++a) {
             const int j = P.active[f][a];
-            pr.push_back(gg::Proj{gg::S_INPUT, fi, s, ts[f][a], P.crt[j], gg::F_IDENT, 0, 0, 0, gg::R_BANK, 0, 6, 1,
-                                  off, first});
+            gg::Proj tp{gg::S_INPUT, fi, s, ts[f][a], P.crt[j], gg::F_IDENT, 0, 0, 0, gg::R_BANK, 0, 6, 1, off, first};
+            tp.hsub = tw_sub(kTwTrans, static_cast<uint32_t>(f));
+            tp.hslot = static_cast<int>(a);
+            pr.push_back(tp);
             off += s;
             first += s;
         }

@@ -20,8 +20,9 @@ namespace dash {
 
 class GpuGarbler {
    public:
+    // hardened: the tables use the hardened encoding's tweaked pads (core.h hard_block) instead of H(K)
     GpuGarbler(const std::vector<int>& crt, const std::vector<int>& mrs, const std::string& seed16, const LabelBank& R,
-               const LabelBank& Z, int device);
+               const LabelBank& Z, int device, bool hardened = false);
     ~GpuGarbler();
     void to_device(const CrtLabels& cur);
     void to_host(CrtLabels& cur);

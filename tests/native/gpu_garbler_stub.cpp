@@ -11,7 +11,7 @@ struct GpuGarbler::Impl {};
 [[noreturn]] static void no_gpu() { throw std::runtime_error("GPU garbler not linked into the host-only build"); }
 
 GpuGarbler::GpuGarbler(const std::vector<int>&, const std::vector<int>&, const std::string&, const LabelBank&,
-                       const LabelBank&, int) {
+                       const LabelBank&, int, bool) {
     no_gpu();
 }
 GpuGarbler::~GpuGarbler() = default;
