@@ -710,6 +710,9 @@ def run(argv=None) -> Optional[dict]:
                 "sign_construction": resolved["sign"],
                 "rescale_construction": resolved["rescale"],
                 "relu_construction": resolved["relu"],
+                # offline-message encoding (docs/SECURITY.md): "hardened" = no constant labels shipped and a
+                # tweaked pad per table entry; "reference" = the reference's wire format
+                "encoding": resolved.get("encoding", "reference"),
                 "seq_len": None,
                 "input_shape": list(bench.circuit.input_dims),
                 "parallelism": f"dp{world}",
@@ -718,6 +721,12 @@ def run(argv=None) -> Optional[dict]:
             # the headline's GCs are garbled once and re-encoded every step: an online-phase rate (a step's
             # work equals that of fresh GCs); served_inf_per_s is the protocol-valid fresh-GC rate
             "gc_reuse": True,
+            "gc_reuse_note": ("the timed steps re-encode fresh inputs under GCs garbled once (a reused GC also "
+                              "builds a per-GC input codebook on its second encode, host_encode_decode_ms_per_step); "
+                              "GCs are single use in the protocol: served_inf_per_s (fresh GC per inference, "
+                              "garbling included) and latency_b1_ms (fresh GC, batch 1) measure that"),
+            "vs_baseline_note": ("value / (1 / 1.443 s): batched throughput over the reference's batch-1 latency; "
+                                 "latency_b1_ms against 1443 ms is the like-for-like comparison"),
             "dist_backend": ctx.backend if ctx.distributed else "none",
             "world_size": world,
             "rehearsal_shared_device": rehearsal and world > 1,
