@@ -556,11 +556,21 @@ class _Bench:
         rec = dict(rank=self.ctx.rank, local_rank=self.ctx.local_rank, host=socket.gethostname(), pid=os.getpid(),
                    threads=self.threads, gcs=B, ms_per_step=round(ms_step, 3), inf_per_s=round(inf_s, 3),
                    host_encode_decode_ms_per_step=round(host_ms, 3))
+        # the GPU this rank owns by LOCAL_RANK, from sysfs (what init_distributed bound it to)
+        from .parallel.dist import rank_gpu
+
+        plan = rank_gpu(self.ctx.local_rank)
+        rec["gpu_plan"] = plan
         if self.hip:
             from .native import native
 
             rec["device"] = int(self.device)
             rec["pci_bus_id"] = native().hip_device_pci_bus_id(int(self.device))
+            if plan is not None:
+                rec["pci_matches_plan"] = rec["pci_bus_id"].lower() == plan["pci"].lower()
+                if not rec["pci_matches_plan"] and os.environ.get("DASH_DEBUG_DEVICE") == "1":
+                    raise RuntimeError(f"rank {self.ctx.rank}: LOCAL_RANK {self.ctx.local_rank} should own "
+                                       f"{plan['pci']} but runs on {rec['pci_bus_id']}")
         else:
             rec["device"] = "cpu"
         return rec

@@ -113,12 +113,6 @@ struct DigitStream {
         left = 0;
     }
     __device__ __forceinline__ uint32_t next(const ModC& m) {
-#ifdef DASH_FAKE_DECOMP
-        // A/B bound analysis only (wrong digits, in range): a 3-op stand-in for the long division
-        const uint32_t f = min(static_cast<uint32_t>(Q) & 15u, m.q - 1);
-        Q = (Q >> 4) | (Q << 124);
-        return f;
-#endif
         if (m.bits) {
             uint32_t d = static_cast<uint32_t>(Q) & (m.q - 1);
             Q >>= m.bits;
@@ -178,10 +172,6 @@ struct CompressFwd {
         sh = 0;
     }
     __device__ __forceinline__ void push(uint32_t d, const ModC& m) {
-#ifdef DASH_FAKE_COMP
-        v = (v << 1) ^ d;  // A/B bound analysis only
-        return;
-#endif
         if (m.bits) {
             v |= d << bp;
             bp += m.bits;
@@ -204,9 +194,6 @@ struct CompressFwd {
         }
     }
     __device__ __forceinline__ u128 finish() {
-#ifdef DASH_FAKE_COMP
-        return static_cast<u128>(v);
-#endif
         if (bp) C |= static_cast<u128>(v) << sh;  // bits path (bp stays 0 otherwise)
         else if (cnt && v) C += PW * static_cast<u128>(v);
         return C;
@@ -350,18 +337,6 @@ __device__ __forceinline__ uint32_t aes_last(const AesT<C>& a, uint32_t s0, uint
     return xor3(x1, x2, rk);
 }
 
-#ifdef DASH_FAKE_AES
-// A/B experiment only (bound analysis): a cheap stand-in mixing function in place of AES.
-template <int C>
-__device__ __forceinline__ u128 aes_encrypt(const AesT<C>&, u128 in) {
-    return (in ^ (in >> 61)) * static_cast<u128>(0x9e3779b97f4a7c15ull);
-}
-template <int C>
-__device__ __forceinline__ void aes_encrypt2(const AesT<C>& a, u128 inA, u128 inB, u128& outA, u128& outB) {
-    outA = aes_encrypt(a, inA);
-    outB = aes_encrypt(a, inB);
-}
-#else
 template <int C>
 __device__ __forceinline__ u128 aes_encrypt(const AesT<C>& a, u128 in) {
     uint32_t s0 = bswap32(static_cast<uint32_t>(in)) ^ kAesRk[0];
@@ -419,16 +394,13 @@ __device__ __forceinline__ void aes_encrypt2(const AesT<C>& a, u128 inA, u128 in
     outA = fin(a0, a1, a2, a3);
     outB = fin(b0, b1, b2, b3);
 }
-#endif  // DASH_FAKE_AES
 
 // ---------------------------------------------------------------------------
 // Hardened-encoding pads (core.h hard_block): ChaCha12 on
 //   [sigma][K (4 words)][gate lo, gate hi, sub, "HARD"][blk, 0, 0, 0]
 // with feed-forward; pad q of the block = words 4q..4q+3. Pure VALU (adds, xors, 32-bit rotates as
 // v_alignbit): no LDS image, unlike the T-table AES, so hardened kernels leave the LDS to staging.
-#ifndef DASH_CHA_ROUNDS
-#define DASH_CHA_ROUNDS 12  // must equal core.h kChaRounds (part of the hardened encoding)
-#endif
+constexpr int kDevChaRounds = 12;  // = core.h kChaRounds: part of the hardened encoding, not a tuning knob
 __device__ __forceinline__ uint32_t rotl(uint32_t x, int r) { return __builtin_rotateleft32(x, r); }
 #define DASH_QR(a, b, c, d)                 \
     a += b; d = rotl(d ^ a, 16);            \
@@ -443,7 +415,7 @@ __device__ __forceinline__ void hard_block(u128 K, uint64_t gate, uint32_t sub, 
     uint32_t x4 = k0, x5 = k1, x6 = k2, x7 = k3, x8 = g0, x9 = g1, x10 = sub, x11 = 0x44524148u;
     uint32_t x12 = blk, x13 = 0, x14 = 0, x15 = 0;
 #pragma unroll
-    for (int r = 0; r < DASH_CHA_ROUNDS; r += 2) {
+    for (int r = 0; r < kDevChaRounds; r += 2) {
         DASH_QR(x0, x4, x8, x12) DASH_QR(x1, x5, x9, x13) DASH_QR(x2, x6, x10, x14) DASH_QR(x3, x7, x11, x15)
         DASH_QR(x0, x5, x10, x15) DASH_QR(x1, x6, x11, x12) DASH_QR(x2, x7, x8, x13) DASH_QR(x3, x4, x9, x14)
     }
@@ -463,7 +435,7 @@ __device__ __forceinline__ void hard_block(u128 K, uint64_t gate, uint32_t sub, 
 // Tweak kinds (core.h TweakKind) and the sub word of row `idx`
 constexpr uint32_t kTwApprox = 1, kTwCast2 = 3, kTwSign = 4, kTwMmg = 5, kTwMmy = 6, kTwMrs = 7, kTwSmrs = 8,
                    kTwBe = 9, kTwTrans = 10, kTwProj = 11, kTwGme = 12, kTwMmt = 13;
-__device__ __forceinline__ constexpr uint32_t tw_sub(uint32_t kind, uint32_t idx) { return (kind << 16) | (idx & 0xffffu); }
+__host__ __device__ __forceinline__ constexpr uint32_t tw_sub(uint32_t kind, uint32_t idx) { return (kind << 16) | (idx & 0xffffu); }
 // gate of element e of a gadget whose PRG streams are stream_id(L, slot, e) (core.h): base = stream_id(L, slot, 0)
 __host__ __device__ __forceinline__ constexpr uint64_t gate_base(uint64_t layer, uint64_t slot) {
     return (layer << 44) ^ (slot << 36);

@@ -2607,7 +2607,7 @@ struct GpuGarbler::Impl {
         for (size_t j = 0; j < host.size(); ++j) DASH_CHECK(host[j].p == cur_mod[j], "gpu garbler: modulus mismatch");
     }
     void enter() {
-        HIPCHECK(hipSetDevice(device));
+        bind_device(device, dc.st, "gpu garbler");  // also on garbling worker threads (one Impl per context)
         gg::tl_st = dc.st;
         tl_dc = &dc;
     }

@@ -25,6 +25,37 @@ namespace dash {
 
 namespace hostutil {
 
+// --------------------------------------------------------- device binding
+// DASH_DEBUG_DEVICE=1: every native entry that launches or allocates checks that the calling thread's current
+// device and the stream it was handed belong to the object's device (a rank or worker thread that never set its
+// device would otherwise launch on device 0 with another device's pointers).
+inline bool debug_device_checks() {
+    static const bool on = [] {
+        const char* e = std::getenv("DASH_DEBUG_DEVICE");
+        return e && e[0] == '1';
+    }();
+    return on;
+}
+inline void check_device(int dev, hipStream_t st, const char* where) {
+    int cur = -1;
+    HIPCHECK(hipGetDevice(&cur));
+    if (cur != dev)
+        throw std::runtime_error(std::string("dash: ") + where + " runs on device " + std::to_string(cur) +
+                                 ", its object lives on device " + std::to_string(dev));
+    if (st) {
+        hipDevice_t sd = -1;
+        HIPCHECK(hipStreamGetDevice(st, &sd));
+        if (static_cast<int>(sd) != dev)
+            throw std::runtime_error(std::string("dash: ") + where + " got a stream of device " +
+                                     std::to_string(sd) + ", its object lives on device " + std::to_string(dev));
+    }
+}
+// Make `dev` current for this thread (cheap: a thread-local store) and, in debug mode, check the stream.
+inline void bind_device(int dev, hipStream_t st, const char* where) {
+    HIPCHECK(hipSetDevice(dev));
+    if (debug_device_checks()) check_device(dev, st, where);
+}
+
 // --------------------------------------------------------------- AES tables
 inline uint8_t gmul(uint8_t a, uint8_t b) {
     uint8_t r = 0;

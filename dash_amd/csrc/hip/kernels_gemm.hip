@@ -509,11 +509,7 @@ __global__ __launch_bounds__(256) void k_conv_img2(ConvArgs a, Act x, Act y, int
             } else if (full) {
                 // one 8-B load of 8 byte components (unaligned: global loads take any address on gfx950)
                 typedef uint32_t u32x2c __attribute__((ext_vector_type(2)));
-#ifdef DASH_FAKE_CONV_NOLOAD
-                const u32x2c t = {static_cast<uint32_t>(ci), static_cast<uint32_t>(ix0)};  // A/B only
-#else
                 const u32x2c t = *reinterpret_cast<const u32x2c*>(row + ix0);
-#endif
                 raw[q][0] = rawx ? t[0] : center4(t[0]);
                 raw[q][1] = rawx ? t[1] : center4(t[1]);
             } else if (DASH_CONV_CLAMP && a.W >= 8) {
@@ -620,11 +616,7 @@ __global__ __launch_bounds__(256) void k_conv_img2(ConvArgs a, Act x, Act y, int
             // B operands one k-step ahead: the LDS reads of step s+1 are in flight while step s's MFMAs run
             // (one read ahead left each MFMA waiting out most of an LDS round trip)
             v2l bcur[NT], bnxt[NT];
-#ifdef DASH_FAKE_CONV_NOLDSB  // A/B bound analysis only: B operands from registers, no LDS reads (wrong results)
-#define DASH_CONV_LDB(off) v2l{static_cast<long>(base[t] + (off)), static_cast<long>(lane)}
-#else
 #define DASH_CONV_LDB(off) *reinterpret_cast<const v2l*>(img + base[t] + (off))
-#endif
 #pragma unroll
             for (int t = 0; t < NT; ++t) bcur[t] = DASH_CONV_LDB(toff[0]);
 #pragma unroll
@@ -693,9 +685,6 @@ __global__ __launch_bounds__(256) void k_conv_img2(ConvArgs a, Act x, Act y, int
                 d[3] = r23[1];
                 if (fl < a.F) {
                     act_t* yr = Y + static_cast<int64_t>(fl) * npos + oy0 * a.OW + colw + 16 * (lane >> 4);
-#ifdef DASH_FAKE_CONV_NOSTORE
-                    if (d[0] == 0xdeadbeefu)  // A/B bound analysis only
-#endif
                     *reinterpret_cast<uint4*>(yr) = make_uint4(d[0], d[1], d[2], d[3]);
                 }
                 continue;
@@ -712,9 +701,6 @@ __global__ __launch_bounds__(256) void k_conv_img2(ConvArgs a, Act x, Act y, int
                 for (int r = 0; r < 4; ++r)
                     o[r] = modq_conv(static_cast<uint32_t>(acc[g][t][r]) + addc[g], static_cast<uint32_t>(p), mq);
                 act_t* yr = Y + static_cast<int64_t>(fl) * npos + pos;
-#ifdef DASH_FAKE_CONV_NOSTORE
-                if (o[0] == 0xdeadbeefu)  // A/B bound analysis only: never true, keeps the math
-#endif
                 {
                     if (dw && cb + 3 < ncol) {
                         *reinterpret_cast<uint32_t*>(yr) = o[0] | (o[1] << 8) | (o[2] << 16) | (o[3] << 24);

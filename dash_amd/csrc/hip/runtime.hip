@@ -65,7 +65,7 @@ class HipEvaluator {
         DASH_CHECK(m.h.crt == tmpl_h_.crt && m.h.mrs == tmpl_h_.mrs && m.layers.size() == tmpl_nlayers_ &&
                        m.h.in_dims == tmpl_h_.in_dims && m.h.hardened == tmpl_h_.hardened,
                    "model does not garble the evaluator's circuit (or uses another encoding)");
-        HIPCHECK(hipSetDevice(dev_));
+        bind_device(dev_, load_st_, "HipEvaluator.load");
         if (!load_st_) HIPCHECK(hipStreamCreateWithFlags(&load_st_, hipStreamNonBlocking));
         // per-GC small constants (bias labels, zero / shift labels, ...): filled into one pinned staging block,
         // one H2D copy and one scatter kernel to their slot-b destinations, instead of ~100 small copies
@@ -152,6 +152,7 @@ class HipEvaluator {
     u128* input_slot_compressed(int b) {
         DASH_CHECK(b >= 0 && b < B_, "batch slot out of range");
         if (!in_comp_stage_) {
+            bind_device(dev_, nullptr, "HipEvaluator.input_slot_compressed");
             const size_t bytes = sizeof(u128) * B_ * k_ * N0_;
             HIPCHECK(hipHostMalloc(reinterpret_cast<void**>(&in_comp_stage_), bytes));
             host_allocs_.push_back(in_comp_stage_);
@@ -162,6 +163,7 @@ class HipEvaluator {
         return in_comp_stage_ + static_cast<i64>(b) * k_ * N0_;
     }
     void upload_inputs_compressed(hipStream_t st) {
+        bind_device(dev_, st, "HipEvaluator.upload_inputs_compressed");
         DASH_CHECK(in_comp_stage_ != nullptr, "no compressed inputs staged");
         HIPCHECK(hipMemcpyAsync(in_comp_dev_, in_comp_stage_, sizeof(u128) * B_ * k_ * N0_, hipMemcpyHostToDevice, st));
         launch_unpack(in_comp_dev_, k_, bufs_[0], crt_info(crt_), mc_, N0_, B_, st);
@@ -180,6 +182,7 @@ class HipEvaluator {
         return r;
     }
     void fetch_outputs(hipStream_t st) {
+        bind_device(dev_, st, "HipEvaluator.fetch_outputs");
         for (int j = 0; j < k_; ++j) {
             const int n = nr_comps(out_mod_[j]);
             HIPCHECK(hipMemcpyAsync(out_stage_[j], final_.p[j], sizeof(act_t) * B_ * n * Nout_, hipMemcpyDeviceToHost, st));
@@ -190,6 +193,7 @@ class HipEvaluator {
     i64 output_size() const { return Nout_; }
     // int16 host staging (the host label format) -> device int16 scratch -> byte activations
     void upload_inputs(hipStream_t st) {
+        bind_device(dev_, st, "HipEvaluator.upload_inputs");
         for (int j = 0; j < k_; ++j) {
             const i64 count = static_cast<i64>(B_) * nr_comps(crt_[j]) * N0_;
             if (!in16_dev_[j]) in16_dev_[j] = dalloc<int16_t>(static_cast<size_t>(count));
@@ -202,6 +206,7 @@ class HipEvaluator {
     // after one eager run (lazy one-time allocations) it is captured into a
     // hipGraph and replayed: one launch per evaluation instead of ~200.
     void run(hipStream_t st) {
+        bind_device(dev_, st, "HipEvaluator.run");
         for (int b = 0; b < B_; ++b) DASH_CHECK(loaded_[b], "batch slot " + std::to_string(b) + " has no garbled model loaded");
         if (profile_ || !use_graph_ || runs_ == 0 || st == nullptr) {
             // roctx ranges per op (layer / gadget phase) for rocprofv3 --marker-trace (DASH_ROCTX=1)
@@ -237,6 +242,7 @@ class HipEvaluator {
     void set_graph(bool on) { use_graph_ = on; }
 
     std::vector<CrtLabels> get_outputs(hipStream_t st) {
+        bind_device(dev_, st, "HipEvaluator.get_outputs");
         std::vector<CrtLabels> out(B_);
         for (int j = 0; j < k_; ++j) {
             const int q = out_mod_[j], n = nr_comps(q);
@@ -258,6 +264,7 @@ class HipEvaluator {
     void set_profile(bool on) {
         profile_ = on;
         if (on && ev_.empty()) {
+            bind_device(dev_, nullptr, "HipEvaluator.set_profile");
             ev_.resize(ops_.size() + 1);
             for (auto& e : ev_) HIPCHECK(hipEventCreate(&e));
         }

@@ -25,10 +25,12 @@ import numpy as np
 KFD_TOPOLOGY = "/sys/class/kfd/kfd/topology/nodes"
 
 
-def kfd_gpus(root: str = KFD_TOPOLOGY) -> list:
+def kfd_gpus(root: Optional[str] = None) -> list:
     """GPU agents of the KFD topology, in KFD node order (the order HIP enumerates devices), read from sysfs
     without touching the HIP runtime. Each entry: {"node", "pci" (dddd:bb:dd.f), "gfx"}. Raises when the
-    topology is missing: callers must not guess a device count."""
+    topology is missing: callers must not guess a device count. ``DASH_KFD_TOPOLOGY`` overrides the sysfs root
+    (tests use a synthetic topology)."""
+    root = root or os.environ.get("DASH_KFD_TOPOLOGY") or KFD_TOPOLOGY
     if not os.path.isdir(root):
         raise RuntimeError(f"KFD topology {root} not readable: cannot count GPUs without initialising HIP")
     out = []
@@ -73,6 +75,21 @@ def visible_indices(n: int, env: Optional[dict] = None) -> list:
                 break  # HIP stops at the first invalid entry
         idx = sel
     return idx
+
+
+def rank_gpu(local_rank: int, env: Optional[dict] = None) -> Optional[dict]:
+    """The GPU a rank with this LOCAL_RANK owns, from sysfs only (no HIP call): HIP device index = LOCAL_RANK
+    within the visible devices, plus the KFD node and PCI address behind it. None when the topology is unknown
+    or LOCAL_RANK is beyond the visible GPUs (a shared-device rehearsal maps ranks modulo the GPU count first)."""
+    try:
+        gpus = kfd_gpus()
+    except RuntimeError:
+        return None
+    vis = visible_indices(len(gpus), env)
+    if not 0 <= local_rank < len(vis):
+        return None
+    g = gpus[vis[local_rank]]
+    return {"device": local_rank, "kfd_node": g["node"], "pci": g["pci"]}
 
 
 def gpu_local_cpus(local_rank: int) -> Optional[set]:

@@ -5,7 +5,8 @@
 Garbles B MiniONN GCs on the GPU, loads them into one evaluator (one stream),
 then times `run` (upload of the encoded inputs + every layer) and prints one
 JSON line with ms per step and the per-op-kind GPU times of a profiled run.
-Outputs are never decoded, so codec stand-ins (-DDASH_FAKE_*) can be timed.
+Outputs are never decoded, so an ab/ tree with a patched (wrong-result) kernel can still be timed;
+such patches live only in the untracked ab/ copies, never in the production sources.
 """
 import argparse
 import json

@@ -52,9 +52,9 @@ def test_batch_dp_gloo(world):
     assert [i for r in res for i in r[2]] == list(range(5))
 
 
-def _bench_worker(rank, world, port, q):
-    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank), LOCAL_WORLD_SIZE=str(world),
-                      MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+def _bench_worker(rank, world, port, q, local_rank=None, env=None):
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank if local_rank is None else local_rank),
+                      LOCAL_WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), **(env or {}))
     from dash_amd import benchcore
 
     out = benchcore.run(["--backend", "cpu", "--gpus", str(world), "--model", "MODEL_A", "--batch", "2", "--streams",
@@ -88,6 +88,66 @@ def test_bench_driver_gloo(world):
     assert out["value"] > 0 and out["served_inf_per_s"] > 0
     # the headline value is the whole-job rate over the slowest rank's time
     assert abs(out["value"] - world * 2 * 2 / (out["ms_per_step"] * 2 / 1000.0)) / out["value"] < 0.01
+
+
+def _fake_kfd(root, n_gpus):
+    """A KFD topology like an MI355X node's: node 0 a CPU agent, nodes 1..n GPUs on distinct PCI buses."""
+    os.makedirs(os.path.join(root, "0"))
+    with open(os.path.join(root, "0", "properties"), "w") as f:
+        f.write("cpu_cores_count 96\nsimd_count 0\ngfx_target_version 0\n")
+    buses = []
+    for i in range(n_gpus):
+        bus = 0x05 + 0x20 * i
+        os.makedirs(os.path.join(root, str(i + 1)))
+        with open(os.path.join(root, str(i + 1), "properties"), "w") as f:
+            f.write(f"simd_count 1024\ngfx_target_version 90500\nlocation_id {bus << 8}\ndomain 0\n")
+        buses.append(f"0000:{bus:02x}:00.0")
+    return buses
+
+
+def test_rank_gpu_follows_local_rank(tmp_path):
+    """LOCAL_RANK (not RANK) picks the GPU, inside the visible set, from sysfs alone."""
+    from dash_amd.parallel.dist import rank_gpu
+
+    buses = _fake_kfd(str(tmp_path / "kfd"), 8)
+    env = {"DASH_KFD_TOPOLOGY": str(tmp_path / "kfd")}
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
+    try:
+        assert rank_gpu(3, {}) == {"device": 3, "kfd_node": 4, "pci": buses[3]}
+        # HIP_VISIBLE_DEVICES=4,5,6,7: device 3 of the rank is the node's 8th GPU
+        assert rank_gpu(3, {"HIP_VISIBLE_DEVICES": "4,5,6,7"})["pci"] == buses[7]
+        assert rank_gpu(4, {"HIP_VISIBLE_DEVICES": "4,5,6,7"}) is None
+    finally:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+
+
+def test_bench_driver_records_local_rank_gpu(tmp_path):
+    """The bench driver over gloo with LOCAL_RANK permuted against RANK (rank r has LOCAL_RANK 3 - r): every
+    rank records the GPU of its LOCAL_RANK (device index, KFD node, PCI address) from a synthetic 4-GPU topology."""
+    buses = _fake_kfd(str(tmp_path / "kfd"), 4)
+    world = 4
+    ctx = tmp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    env = {"DASH_KFD_TOPOLOGY": str(tmp_path / "kfd"), "DASH_NUMA_BIND": "0", "HIP_VISIBLE_DEVICES": "0,1,2,3"}
+    procs = [ctx.Process(target=_bench_worker, args=(r, world, port, q, world - 1 - r, env)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=600) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    recs = res[0]["ranks"]
+    assert [r["rank"] for r in recs] == [0, 1, 2, 3]
+    for r in recs:
+        assert r["local_rank"] == world - 1 - r["rank"]
+        assert r["gpu_plan"] == {"device": r["local_rank"], "kfd_node": r["local_rank"] + 1,
+                                 "pci": buses[r["local_rank"]]}
 
 
 def test_single_process_context():
