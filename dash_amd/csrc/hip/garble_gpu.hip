@@ -940,6 +940,7 @@ struct Scope {
     int r0, ne;      // key-hash entries [r0, r0 + ne)
     int b0, nb;      // bank rows [b0, b0 + nb)
     int bx0, nbx;    // bank indices [bx0, bx0 + nbx) of its element-independent projections
+    int q0, nq;      // hardened: pad quads [q0, q0 + nq) covering the span (Emit::quads)
     int64_t blk0;    // first block of the scope
 };
 struct Emit {
@@ -952,6 +953,9 @@ struct Emit {
     const uint16_t* bix;
     const BankRow* rows;
     const EProj* ep;
+    // hardened: runs of <= 4 consecutive positions of one key whose pads come from ONE ChaCha block (same
+    // projection and color, consecutive fan-out targets, same block of 4 slots), (position - scope a) << 3 | count
+    const uint32_t* quads;
 };
 
 // Bank payloads: one wave per (64-element tile, bank row), lanes = consecutive elements (the row's slot,
@@ -1095,9 +1099,68 @@ __global__ __launch_bounds__(kEB) void k_emit(Ctx c, Gadget g, In in, Tables tb,
             }
             __syncthreads();
         }
-        // 2: entries, position-fastest (contiguous per element), kUn independent LDS-only chains per thread
         u128* T = tb.t[table];
         const int64_t row = tb.row[table];
+        if (c.hard) {
+            // 2 (hardened): one ChaCha block per quad (up to 4 entries of one key: a fan-out row's consecutive
+            // targets share a block), quad-fastest over the tile's elements
+            const int nq = rfl(S.nq);
+            const uint32_t* QD = em.quads + rfl(S.q0);
+            const int totq = nq * te;
+            const float inv_nq = 1.0f / static_cast<float>(nq);
+            for (int x = threadIdx.x; x < totq; x += kEB) {
+                int el = static_cast<int>(static_cast<float>(x) * inv_nq);
+                if (el * nq > x) --el;
+                else if ((el + 1) * nq <= x) ++el;
+                const int q = x - el * nq;
+                const int64_t e = e0 + el;
+                if (e >= N) continue;
+                const uint32_t qd = QD[q];
+                const int p0 = static_cast<int>(qd >> 3), cnt = static_cast<int>(qd & 7u);
+                const uint32_t m0 = MAP[p0];
+                const EProj P = sep[m0 >> 24];
+                int rr = P.first + static_cast<int>((m0 >> 12) & 0xfffu) - r0;  // the color's row
+                int i;
+                if (em.by_i) {
+                    rr = IDX[rr * te1 + el];
+                    i = rr - (P.first - r0);
+                } else {
+                    i = CCL[rr * te1 + el];
+                }
+                const int d0 = static_cast<int>(m0 & 0xfffu);
+                const bool fan = P.fn == F_LUT || P.fn == F_FAN;
+                const int s0 = P.hslot + (fan ? d0 : 0);
+                u128 pad[4];
+                hard_block(HCL[rr * te1 + el], stream_of(g.layer, g.sslot, static_cast<uint64_t>(e), g.mask), P.hsub,
+                           static_cast<uint32_t>(s0) >> 2, pad);
+                u128* dst = T + e * row + a + p0;
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    if (u >= cnt) break;
+                    int br;
+                    if (P.fn == F_MULR || P.fn == F_NEGR) {  // never fan-out: cnt == 1
+                        const int xr = in.p[P.res][e * in.es[P.res]];
+                        int w = P.fn == F_MULR ? (i * xr) % P.pout : -(i + xr) % P.pout;
+                        if (w < 0) w += P.pout;
+                        br = P.pay1 + w;
+                    } else {
+                        br = BIX[P.pay1 - bx0 + i * P.t + d0 + u];
+                    }
+                    const int qq = (s0 + u) & 3;
+                    const u128 h = qq == 0 ? pad[0] : (qq == 1 ? pad[1] : (qq == 2 ? pad[2] : pad[3]));
+                    const u128 v = PBL[br * te1 + el] + h;
+                    u32x4a w;
+                    w[0] = static_cast<uint32_t>(v);
+                    w[1] = static_cast<uint32_t>(v >> 32);
+                    w[2] = static_cast<uint32_t>(v >> 64);
+                    w[3] = static_cast<uint32_t>(v >> 96);
+                    *reinterpret_cast<u32x4a*>(dst + u) = w;
+                }
+            }
+            __syncthreads();
+            continue;
+        }
+        // 2: entries, position-fastest (contiguous per element), kUn independent LDS-only chains per thread
         const int total = span * te;
         const float inv_span = 1.0f / static_cast<float>(span);
         for (int x0 = threadIdx.x; x0 < total; x0 += kUn * kEB) {
@@ -1136,13 +1199,7 @@ __global__ __launch_bounds__(kEB) void k_emit(Ctx c, Gadget g, In in, Tables tb,
                 } else {
                     br = BIX[P.pay1 - bx0 + i * P.t + static_cast<int>(mm[u] & 0xfffu)];
                 }
-                if (c.hard) {
-                    const uint64_t gate = stream_of(g.layer, g.sslot, static_cast<uint64_t>(e0 + el[u]), g.mask);
-                    const int slot = P.hslot + ((P.fn == F_LUT || P.fn == F_FAN) ? static_cast<int>(mm[u] & 0xfffu) : 0);
-                    v[u] = PBL[br * te1 + el[u]] + hard_pad(HCL[rr * te1 + el[u]], gate, P.hsub, slot);
-                } else {
-                    v[u] = PBL[br * te1 + el[u]] + HCL[rr * te1 + el[u]];
-                }
+                v[u] = PBL[br * te1 + el[u]] + HCL[rr * te1 + el[u]];
             }
 #pragma unroll
             for (int u = 0; u < kUn; ++u) {
@@ -2169,6 +2226,7 @@ void project(const gg::Ctx& c, gg::Gadget& g, const gg::In& in, const gg::Tables
     std::vector<uint16_t> bix;
     std::vector<gg::BankRow> rows;
     std::vector<gg::Scope> sc;
+    std::vector<uint32_t> quads;
     size_t lds_max = 0;
     const auto N = g.N;
     for (const auto& grp : groups) {
@@ -2223,6 +2281,32 @@ void project(const gg::Ctx& c, gg::Gadget& g, const gg::In& in, const gg::Tables
         }
         S.nb = static_cast<int>(rows.size()) - S.b0;
         S.nbx = static_cast<int>(bix.size()) - S.bx0;
+        S.q0 = static_cast<int>(quads.size());
+        if (c.hard) {
+            // runs of positions sharing one pad block: same projection and color, consecutive fan-out targets
+            int open = -1;  // index of the run being extended
+            uint32_t pm = 0;
+            for (int64_t pos = a; pos < end; ++pos) {
+                const uint32_t m = map[em.map_off[S.table] + pos];
+                if (m == gg::kHole) {
+                    open = -1;
+                    continue;
+                }
+                const auto& p = pr[m >> 24];
+                const int d = static_cast<int>(m & 0xfffu);
+                const int slot = p.hslot + (is_fan(p) ? d : 0);
+                if (open >= 0 && is_fan(p) && (m >> 12) == (pm >> 12) && d == static_cast<int>(pm & 0xfffu) + 1 &&
+                    (quads[open] & 7u) < 4 && (slot >> 2) == ((slot - 1) >> 2)) {
+                    ++quads[open];
+                } else {
+                    DASH_CHECK(pos - a < (1 << 28), "gpu garbler: table scope too wide for the pad runs");
+                    quads.push_back(static_cast<uint32_t>(pos - a) << 3 | 1u);
+                    open = static_cast<int>(quads.size()) - 1;
+                }
+                pm = m;
+            }
+        }
+        S.nq = static_cast<int>(quads.size()) - S.q0;
         const size_t per = static_cast<size_t>(elem_bytes(S.ne, S.nb));
         const size_t fixed = static_cast<size_t>(S.span) * 4 + static_cast<size_t>(S.nbx) * 2 + 16;
         auto lds_of = [&](int sh) { return ((1u << sh) + 1) * per + fixed; };
@@ -2241,6 +2325,7 @@ void project(const gg::Ctx& c, gg::Gadget& g, const gg::In& in, const gg::Tables
     em.bix = gg::dconst(bix.data(), bix.size());
     em.rows = gg::dconst(rows.data(), rows.size());
     em.ep = gg::dconst(ep.data(), ep.size());
+    em.quads = quads.empty() ? nullptr : gg::dconst(quads.data(), quads.size());
     em.nep = np;
     em.sc = gg::dconst(sc.data(), sc.size());
     em.nsc = static_cast<int>(sc.size());

@@ -1,0 +1,32 @@
+"""Per-kernel summary of rocprofv3 --pmc counter CSVs: python scripts/pmc_summary.py OUT (passes under OUT/*/)."""
+import csv, glob, sys, re
+from collections import defaultdict
+out = sys.argv[1]
+agg = defaultdict(lambda: defaultdict(float))
+ms = defaultdict(float)
+nd = defaultdict(int)
+for f in glob.glob(f"{out}/*/**/*counter_collection.csv", recursive=True):
+    seen = set()
+    pas = f[len(out) + 1:].split("/")[0]
+    for r in csv.DictReader(open(f)):
+        k = re.sub(r"\(.*", "", r["Kernel_Name"])
+        agg[k][r["Counter_Name"]] += float(r["Counter_Value"])
+        key = r["Dispatch_Id"]
+        if key not in seen:
+            seen.add(key)
+            ms[(k, pas)] += (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6
+            nd[(k, pas)] += 1
+for k, c in sorted(agg.items()):
+    print(k)
+    for n, v in sorted(c.items()):
+        print(f"   {n:28s} {v:18.0f}")
+    g = c.get
+    if g("SQ_INSTS_LDS"):
+        print(f"   {'lds_bank_conflict_per_lds':28s} {g('SQ_LDS_BANK_CONFLICT', 0) / max(1, g('SQ_ACTIVE_INST_LDS', 1)):18.3f}")
+    if g("SQ_BUSY_CYCLES"):
+        print(f"   {'mfma_busy_pct':28s} {100 * g('SQ_VALU_MFMA_BUSY_CYCLES', 0) / g('SQ_BUSY_CYCLES'):18.2f}")
+    if g("SQ_WAVE_CYCLES"):
+        print(f"   {'wait_any_pct':28s} {100 * g('SQ_WAIT_ANY', 0) / g('SQ_WAVE_CYCLES'):18.2f}")
+        print(f"   {'wait_lds_pct':28s} {100 * g('SQ_WAIT_INST_LDS', 0) / g('SQ_WAVE_CYCLES'):18.2f}")
+for (k, p), v in sorted(ms.items()):
+    print(f"{k} pass={p} {v:.3f} ms {nd[(k, p)]} dispatches")
