@@ -19,9 +19,11 @@ by the evaluator. Per (model config, split) one JSON line:
   online_bytes_per_inference, served_inf_per_s (fresh GC per inference, offline + online wall time),
   verified (decoded == plaintext).
 
-The offline message travels over the TCP channel (``--transport tcp``, any host) or through a ring of shared-memory
+The offline message travels over the TCP channel (``--transport tcp``, any host), through a ring of shared-memory
 segments of this host (``shm``, the same-host split of the reference's enclave: the channel then carries only the
-segment names and the evaluator's acknowledgements). The circuit is range-calibrated first, so the default
+segment names and the evaluator's acknowledgements), or never leaves device memory (``ipc``: the garbler's GPU
+writes each GC's tables straight into the HIP evaluator's slots through their IPC handles, same device or a peer
+over xGMI; the channel carries the skeleton of each model). The circuit is range-calibrated first, so the default
 ("auto") constructions are the headline's (mixed-radix rescale, joint ReLU) where the ranges allow; the record
 names the resolved ones.
 
@@ -168,7 +170,8 @@ def main(argv=None):
     ap.add_argument("--rounds", type=int, default=4, help="timed rounds (after one warm-up round)")
     ap.add_argument("--no-pipeline", action="store_true")
     ap.add_argument("--transport", default="tcp,shm",
-                    help="offline-message transports to measure per split: tcp (any host) and/or shm (same host)")
+                    help="offline-message transports to measure per split: tcp (any host), shm (same host) and/or "
+                         "ipc (same node, device memory; needs --backend hip and a garble device)")
     ap.add_argument("--out", default=None, help="also append the JSON lines to this file")
     args = ap.parse_args(argv)
     if args.backend == "cpu":
@@ -191,6 +194,10 @@ def main(argv=None):
         circuit.calibrate(cal, M)
         cons = _GC(circuit, crt0, _gc_args(cfg)[1], garble_me=False).effective_constructions()
         for split, tr in itertools.product(args.splits.split(","), args.transport.split(",")):
+            if tr == "ipc" and (args.backend != "hip" or args.garble_device < 0):
+                print(json.dumps({"bench": "two_party", "model": name, "split": split, "transport": tr,
+                                  "skipped": "ipc needs --backend hip and a GPU garbler"}), flush=True)
+                continue
             args._transport = tr
             t = time.perf_counter()
             r = (run_tcp if split == "tcp" else run_enclave)(circuit, cfg, xs, args)

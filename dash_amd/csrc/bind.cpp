@@ -284,6 +284,18 @@ PYBIND11_MODULE(_dash_native, m) {
             return g.serialize_to(static_cast<uint8_t*>(bi.ptr), cap);
         }, "write the offline message into a writable buffer (>= serialized_size() bytes) -> bytes written; "
            "device-resident tables are fetched straight into it")
+        .def("serialize_skeleton", [](const GarbledModel& g, bool all_device) { return py::bytes(g.serialize_skeleton(all_device)); },
+             py::arg("all_device") = false,
+             "the offline message without the tables the garbler wrote into an evaluator slot (device transport); "
+             "all_device: every device-resident array as a placeholder (an evaluator template)")
+        .def_static("deserialize_skeleton", [](py::buffer b) {
+            py::buffer_info bi = b.request();
+            check_contig_bytes(bi, "deserialize_skeleton");
+            const auto* p = static_cast<const uint8_t*>(bi.ptr);
+            const size_t n = static_cast<size_t>(bi.size) * static_cast<size_t>(bi.itemsize);
+            py::gil_scoped_release rel;
+            return std::make_shared<GarbledModel>(GarbledModel::deserialize_skeleton(p, n));
+        })
         .def_static("deserialize_buffer", [](py::buffer b) {
             py::buffer_info bi = b.request();
             check_contig_bytes(bi, "deserialize_buffer");

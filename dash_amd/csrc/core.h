@@ -471,6 +471,9 @@ struct Array {
     std::shared_ptr<uint8_t> buf;
     size_t nbytes = 0;
     std::shared_ptr<Device> dev;
+    // placeholder of a skeleton model (GarbledModel::deserialize_skeleton): the bytes were written straight into
+    // the evaluator's table slot by the garbler (cross-process sink); no host or device payload here
+    bool in_slot = false;
 
     Array() = default;
     Array(DType dt, std::vector<i64> shp) : dtype(dt), shape(std::move(shp)) {
@@ -498,6 +501,7 @@ struct Array {
         return reinterpret_cast<const T*>(host_bytes());
     }
     uint8_t* host_bytes() const {
+        DASH_CHECK(!in_slot, "array bytes live in an evaluator table slot (skeleton model): no host copy");
         if (!device_resident()) return buf.get();
         Device* d = dev.get();
         const size_t n = nbytes;

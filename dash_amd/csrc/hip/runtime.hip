@@ -9,6 +9,8 @@
 #include <pybind11/stl.h>
 
 #include <atomic>
+#include <cstring>
+#include <tuple>
 #include <chrono>
 #include <map>
 #include <mutex>
@@ -27,6 +29,65 @@ namespace dash {
 using namespace dev;
 
 using namespace hostutil;
+
+// ---------------------------------------------------------------------------
+// Garbler side of the same-node device transport: another process's evaluator table arenas opened through their
+// IPC handles (HipEvaluator::ipc_export), handed to the GPU garbler as slot sinks. The garbler's kernels write
+// the tables straight into the evaluator's HBM (its own device, or a peer over xGMI); only the skeleton of each
+// model (constants, shapes) then travels over the channel.
+class IpcTables {
+   public:
+    IpcTables(int device, const std::vector<std::tuple<size_t, std::string, size_t, std::string>>& handles, int B)
+        : dev_(device), B_(B), alive_(std::make_shared<std::atomic<bool>>(true)) {
+        DASH_CHECK(B >= 1, "IpcTables: batch must be >= 1");
+        bind_device(dev_, nullptr, "IpcTables");
+        for (const auto& h : handles) {
+            const std::string& hb = std::get<3>(h);
+            DASH_CHECK(hb.size() == sizeof(hipIpcMemHandle_t), "IpcTables: bad IPC handle size");
+            hipIpcMemHandle_t mh;
+            std::memcpy(&mh, hb.data(), sizeof(mh));
+            void* p = nullptr;
+            HIPCHECK(hipIpcOpenMemHandle(&p, mh, hipIpcMemLazyEnablePeerAccess));
+            opened_.push_back(p);
+            map_[{std::get<0>(h), std::get<1>(h)}] = {static_cast<uint8_t*>(p), std::get<2>(h)};
+        }
+    }
+    ~IpcTables() {
+        alive_->store(false);
+        (void)hipSetDevice(dev_);
+        for (void* p : opened_) (void)hipIpcCloseMemHandle(p);
+    }
+    int tables() const { return static_cast<int>(map_.size()); }
+    std::shared_ptr<TableSink> sink(int b) const {
+        DASH_CHECK(b >= 0 && b < B_, "IpcTables: batch slot out of range");
+        auto map = map_;
+        const int dev = dev_;
+        auto alive = alive_;
+        auto s = std::make_shared<TableSink>();
+        s->dest = [map, b, dev, alive](size_t layer, const std::string& name, size_t nbytes) -> std::shared_ptr<Array::Device> {
+            auto it = map.find({layer, name});
+            if (it == map.end() || it->second.second != nbytes) return nullptr;
+            auto d = std::make_shared<Array::Device>();
+            d->p = std::shared_ptr<void>(it->second.first + nbytes * b, [](void*) {});  // the evaluator owns it
+            d->device = dev;
+            d->external = true;
+            d->fetch = [dev, alive](void* h, const void* dv, size_t n) {
+                if (!alive->load())
+                    throw std::runtime_error("dash: tables live in a closed IPC mapping of the evaluator's slots");
+                HIPCHECK(hipSetDevice(dev));
+                HIPCHECK(hipMemcpy(h, dv, n, hipMemcpyDeviceToHost));
+            };
+            return d;
+        };
+        return s;
+    }
+
+   private:
+    int dev_, B_;
+    std::shared_ptr<std::atomic<bool>> alive_;
+    std::vector<void*> opened_;
+    std::map<std::pair<size_t, std::string>, std::pair<uint8_t*, size_t>> map_;
+};
 
 // ---------------------------------------------------------------------------
 class HipEvaluator {
@@ -106,6 +167,21 @@ class HipEvaluator {
             return d;
         };
         return s;
+    }
+    // Same-node device transport (net/protocol.py, transport "ipc"): an IPC handle per table arena, so a
+    // garbler process can garble straight into this evaluator's slots (IpcTables). Entries: (layer, table,
+    // bytes per slot, handle bytes).
+    std::vector<std::tuple<size_t, std::string, size_t, std::string>> ipc_export() const {
+        bind_device(dev_, nullptr, "HipEvaluator.ipc_export");
+        DASH_CHECK(!stream_, "ipc export needs HBM-resident tables (stream_tables=False)");
+        std::vector<std::tuple<size_t, std::string, size_t, std::string>> out;
+        for (const auto& kv : arena_) {
+            hipIpcMemHandle_t h;
+            HIPCHECK(hipIpcGetMemHandle(&h, kv.second.first));
+            out.emplace_back(kv.first.first, kv.first.second, kv.second.second,
+                             std::string(reinterpret_cast<const char*>(&h), sizeof(h)));
+        }
+        return out;
     }
     ~HipEvaluator() {
         alive_->store(false);  // orphans every sink-backed model array (fetch raises instead of reading freed HBM)
@@ -301,6 +377,7 @@ class HipEvaluator {
     // a model array into device memory: device-to-device (or peer) when the GPU
     // garbler left it in HBM and nobody has fetched (and possibly edited) a host copy
     static void copy_in(uint8_t* dst, const Array& a, hipStream_t st) {
+        if (a.in_slot) return;  // skeleton model: the garbler wrote these bytes into this slot (IPC sink)
         if (a.device_resident() && a.device_ptr() == dst) return;  // garbled straight into this slot (sink)
         if (a.device_resident() && !a.dev->host)
             HIPCHECK(hipMemcpyAsync(dst, a.device_ptr(), a.nbytes, hipMemcpyDefault, st));
@@ -1566,6 +1643,19 @@ void register_hip_bindings(py::module_& m) {
         HIPCHECK(hipDeviceGetPCIBusId(buf, static_cast<int>(sizeof(buf)), device));
         return std::string(buf);
     });
+    py::class_<IpcTables, std::shared_ptr<IpcTables>>(m, "IpcTables")
+        .def(py::init([](int device, const py::list& handles, int B) {
+                 std::vector<std::tuple<size_t, std::string, size_t, std::string>> hs;
+                 for (auto item : handles) {
+                     auto t = item.cast<py::tuple>();
+                     hs.emplace_back(t[0].cast<size_t>(), t[1].cast<std::string>(), t[2].cast<size_t>(),
+                                     t[3].cast<std::string>());
+                 }
+                 return std::make_shared<IpcTables>(device, hs, B);
+             }),
+             py::arg("device"), py::arg("handles"), py::arg("batch"))
+        .def("tables", &IpcTables::tables)
+        .def("sink", &IpcTables::sink, "slot b of the evaluator's table arenas as a GPU-garbler destination");
     py::class_<HipEvaluator, std::shared_ptr<HipEvaluator>>(m, "HipEvaluator")
         .def(py::init([](std::shared_ptr<GarbledModel> tmpl, int B, int device, bool mfma, bool stream_tables) {
                  return std::make_shared<HipEvaluator>(std::move(tmpl), B, device, mfma, stream_tables);
@@ -1578,6 +1668,12 @@ void register_hip_bindings(py::module_& m) {
             h.load(b, *m);
         })
         .def("sink", &HipEvaluator::sink, "slot b's table arenas as a GPU-garbler destination (zero-copy load)")
+        .def("ipc_export", [](const HipEvaluator& h) {
+            py::list out;
+            for (const auto& e : h.ipc_export())
+                out.append(py::make_tuple(std::get<0>(e), std::get<1>(e), std::get<2>(e), py::bytes(std::get<3>(e))));
+            return out;
+        }, "IPC handles of the table arenas: [(layer, table, bytes per slot, handle)] (same-node device transport)")
         .def_property_readonly("batch", &HipEvaluator::batch)
         .def("device_bytes", &HipEvaluator::device_bytes)
         .def("table_bytes", &HipEvaluator::table_bytes)

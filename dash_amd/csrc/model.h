@@ -82,6 +82,10 @@ struct GarbledModel {
 
     std::string serialize() const;
     // the offline message written straight into a caller buffer (device tables fetched into place)
+    // Skeleton form (same-node device transport): arrays written into an evaluator slot through a sink
+    // (Device::external; with all_device, every device-resident array) are sent as shape-only placeholders.
+    std::string serialize_skeleton(bool all_device = false) const;
+    static GarbledModel deserialize_skeleton(const uint8_t* blob, size_t nbytes);
     size_t serialized_size() const;
     size_t serialize_to(uint8_t* out, size_t cap) const;
     static GarbledModel deserialize(const std::string& blob);

@@ -11,10 +11,13 @@ constexpr char kDecMagic[8] = {'D', 'A', 'M', 'D', 'D', 'E', 'C', '1'};
 // Writer over an output byte range (or a size count when out == nullptr): the offline message is written
 // once, straight into the caller's buffer (a send buffer), and a device-resident array (GPU garbler tables)
 // is fetched from HBM directly into its place, with no intermediate host copy.
+constexpr uint8_t kInSlot = 0x80;  // skeleton dtype flag: shape only, the bytes are in the evaluator's slot
+
 struct W {
     uint8_t* out = nullptr;
     size_t cap = 0;
     size_t off = 0;
+    int skeleton = 0;  // 1: external device arrays as placeholders; 2: every device-resident array
     void raw(const void* p, size_t n) {
         if (out) {
             DASH_CHECK(off + n <= cap, "serialize: output buffer too small");
@@ -38,6 +41,13 @@ struct W {
     }
     void arr(const Array& a) {
         uint8_t dt = static_cast<uint8_t>(a.dtype);
+        if (skeleton && a.device_resident() && (skeleton == 2 || a.dev->external)) {
+            dt |= kInSlot;
+            raw(&dt, 1);
+            ivec(a.shape);
+            i64v(static_cast<i64>(a.nbytes));
+            return;
+        }
         raw(&dt, 1);
         ivec(a.shape);
         i64v(static_cast<i64>(a.nbytes));
@@ -92,9 +102,26 @@ struct Rd {
         auto v = ivec();
         return std::vector<int>(v.begin(), v.end());
     }
+    bool skeleton = false;
     Array arr() {
         uint8_t dt;
         raw(&dt, 1);
+        if (skeleton && (dt & kInSlot)) {
+            dt &= static_cast<uint8_t>(~kInSlot);
+            DASH_CHECK(dt <= 4, "bad dtype");
+            Array a;
+            a.dtype = static_cast<DType>(dt);
+            a.shape = ivec();
+            size_t cnt = 1;
+            for (auto d : a.shape) {
+                DASH_CHECK(d >= 0 && (d == 0 || cnt <= (size_t(1) << 50) / static_cast<size_t>(d)), "bad array shape");
+                cnt *= static_cast<size_t>(d);
+            }
+            a.nbytes = cnt * dtype_size(a.dtype);
+            DASH_CHECK(static_cast<size_t>(i64v()) == a.nbytes, "array size mismatch");
+            a.in_slot = true;
+            return a;
+        }
         DASH_CHECK(dt <= 4, "bad dtype");
         auto shape = ivec();
         size_t cnt = 1;
@@ -173,8 +200,36 @@ GarbledModel GarbledModel::deserialize(const std::string& blob) {
     return deserialize(reinterpret_cast<const uint8_t*>(blob.data()), blob.size());
 }
 
+namespace {
+GarbledModel read_model(Rd& r, size_t nbytes);
+}
+
 GarbledModel GarbledModel::deserialize(const uint8_t* blob, size_t nbytes) {
     Rd r(blob, nbytes);
+    return read_model(r, nbytes);
+}
+
+GarbledModel GarbledModel::deserialize_skeleton(const uint8_t* blob, size_t nbytes) {
+    Rd r(blob, nbytes);
+    r.skeleton = true;
+    return read_model(r, nbytes);
+}
+
+std::string GarbledModel::serialize_skeleton(bool all_device) const {
+    W sz;
+    sz.skeleton = all_device ? 2 : 1;
+    write_model(*this, sz);
+    std::string s(sz.off, '\0');
+    W w;
+    w.out = reinterpret_cast<uint8_t*>(&s[0]);
+    w.cap = s.size();
+    w.skeleton = sz.skeleton;
+    write_model(*this, w);
+    return s;
+}
+
+namespace {
+GarbledModel read_model(Rd& r, size_t nbytes) {
     char mg[8];
     r.raw(mg, 8);
     DASH_CHECK(std::memcmp(mg, kModelMagic, 8) == 0, "not a garbled model blob");
@@ -216,6 +271,7 @@ GarbledModel GarbledModel::deserialize(const uint8_t* blob, size_t nbytes) {
     DASH_CHECK(r.off == nbytes, "trailing bytes after garbled model");
     return m;
 }
+}  // namespace
 
 std::string Decoder::serialize() const {
     auto put = [this](W& w) {

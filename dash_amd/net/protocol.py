@@ -6,6 +6,11 @@ Messages (tags):
   MODS  client -> server  flags = slot, payload = JSON {"name", "size"}: the same offline message in a shared
                           memory segment of the garbler's ring (same-host split; the evaluator ACKs once it has
                           loaded it, after which the garbler reuses the segment)
+  TMPL  client -> server  payload = skeleton of one GC (GarbledModel.serialize_skeleton(all_device=True)): the
+                          HIP evaluator is built from it; server -> client IPCH = JSON [[layer, table, bytes per
+                          slot, IPC handle hex], ...] of its table arenas (device transport "ipc")
+  MODX  client -> server  flags = slot, payload = skeleton of a GC whose tables the garbler's GPU wrote straight
+                          into that slot through the IPC handles (same node: same device or a peer over xGMI)
   INPT  client -> server  flags = n, payload = n x (k, N, 2) uint64 compressed input labels   (online #1)
   OUTP  server -> client  payload = n x (k, n_out, 2) uint64 compressed output labels          (online #2)
   BYE_  either side
@@ -92,6 +97,26 @@ class EvaluatorServer:
                         self._reset()
                         self.batch = int(hello.get("batch", 1))
                         ch.send(b"HELO", json.dumps({"backend": self.backend, "device": self.device}).encode())
+                    elif tag == b"TMPL":
+                        if self.backend != "hip":
+                            raise ValueError("the ipc transport needs the HIP evaluator")
+                        from ..runtime import HipEvaluator
+
+                        skel = n.GarbledModel.deserialize_skeleton(buf)
+                        if self.ev is None:
+                            self.ev = HipEvaluator(template=skel, batch=self.batch, device=self.device)
+                        hs = [[int(l), str(t), int(nb), bytes(h).hex()] for l, t, nb, h in self.ev.ipc_export()]
+                        ch.send(b"IPCH", json.dumps(hs).encode())
+                    elif tag == b"MODX":
+                        slot = flags
+                        if not 0 <= slot < self.batch:
+                            raise ValueError(f"slot {slot} out of range")
+                        if self.ev is None:
+                            raise ValueError("MODX before TMPL: the evaluator has no table arenas yet")
+                        self.ev.load(slot, n.GarbledModel.deserialize_skeleton(buf))
+                        del buf
+                        self.models[slot] = True
+                        ch.send(b"ACK_")
                     elif tag in (b"MODL", b"MODS"):
                         slot = flags
                         if not 0 <= slot < self.batch:
@@ -192,14 +217,20 @@ class GarblerClient:
                  pipeline: bool = True, transport: str = "tcp", **gc_kw):
         """transport: "tcp" ships the offline message over the channel (any host); "shm" writes it into a ring
         of shared-memory segments of this host and sends only their names (same-host split, e.g. the trusted
-        garbler beside its evaluator); online messages always use the channel."""
-        if transport not in ("tcp", "shm"):
-            raise ValueError("transport must be 'tcp' or 'shm'")
+        garbler beside its evaluator); "ipc" garbles on this process's GPU straight into the HIP evaluator's
+        table slots through their IPC handles (same node; the garbler's device and the evaluator's may differ,
+        writes then go peer-to-peer over xGMI) and sends only each model's skeleton; online messages always
+        use the channel."""
+        if transport not in ("tcp", "shm", "ipc"):
+            raise ValueError("transport must be 'tcp', 'shm' or 'ipc'")
+        if transport == "ipc" and device is None:
+            raise ValueError("transport='ipc' garbles on a GPU: pass device=")
         self.circuit, self.crt, self.mrs = circuit, crt, mrs
         self.batch, self.max_modulus = batch, max_modulus
         self.device, self.pipeline, self.gc_kw = device, pipeline, gc_kw
         self.transport = transport
         self._ring: list = []  # shared-memory segments (shm transport)
+        self._ipc = None  # the evaluator's table slots, opened (ipc transport)
         self._seed = seed
         self._ctr = 0
         self.ch = connect(host, port, timeout=timeout)
@@ -349,12 +380,34 @@ class GarblerClient:
                 free.put(-1)
             th.join()
 
-    def _garble_gc(self, seed):
+    def _offline_ipc(self, seeds) -> None:
+        """Offline phase over the device transport: GC b is garbled on this process's GPU straight into the
+        evaluator's slot b (opened once from its IPC handles); its skeleton follows on the channel. Slots are
+        distinct, so GC b + 1 is garbled while the evaluator loads GC b's constants; the ACKs are collected last."""
+        if self._ipc is None:
+            tmpl = self._garble_gc(None)  # a template for the evaluator's build (tables stay here, discarded)
+            self.ch.send(b"TMPL", tmpl.model.serialize_skeleton(all_device=True))
+            del tmpl
+            _, _, buf = self.ch.recv(b"IPCH")
+            hs = [(int(l), str(t), int(nb), bytes.fromhex(h)) for l, t, nb, h in json.loads(buf.decode())]
+            self._ipc = native().IpcTables(int(self.device), hs, self.batch)
+        for b in range(self.batch):
+            gc = self._garble_gc(seeds[b], sink=self._ipc.sink(b))
+            t = time.perf_counter()
+            skel = gc.model.serialize_skeleton()
+            gc.model = None
+            self.stats["serialize_s"] += time.perf_counter() - t
+            self.ch.send(b"MODX", skel, flags=b)
+            self.gcs.append(gc)
+        for _ in range(self.batch):
+            self.ch.recv(b"ACK_")
+
+    def _garble_gc(self, seed, sink=None):
         from ..garbling import GarbledCircuit
 
         t = time.perf_counter()
         gc = GarbledCircuit(self.circuit, self.crt, self.mrs, max_modulus=self.max_modulus, seed=seed,
-                            device=self.device, **self.gc_kw)
+                            device=self.device, sink=sink, **self.gc_kw)
         self.stats["garble_s"] += time.perf_counter() - t
         return gc
 
@@ -363,6 +416,16 @@ class GarblerClient:
         import queue
         import threading
 
+        if self.transport == "ipc":
+            t0 = time.perf_counter()
+            sent0 = self.ch.bytes_sent
+            seeds = [self._next_seed() for _ in range(self.batch)]
+            self.gcs = []
+            self._offline_ipc(seeds)
+            self.stats["gcs"] += self.batch
+            self.stats["offline_bytes"] += self.ch.bytes_sent - sent0
+            self.stats["offline_s"] += time.perf_counter() - t0
+            return
         if self.transport == "shm":
             t0 = time.perf_counter()
             sent0 = self.ch.bytes_sent
@@ -466,6 +529,7 @@ class GarblerClient:
             pass
         self.ch.close()
         self._ring_close()
+        self._ipc = None
 
     def __enter__(self):
         return self

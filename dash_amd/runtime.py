@@ -64,6 +64,11 @@ class HipEvaluator:
         only the small per-GC constants (zero-copy offline phase)."""
         return self._h.sink(b)
 
+    def ipc_export(self) -> list:
+        """IPC handles of the table arenas, ``[(layer, table, bytes per slot, handle)]``: a garbler process on the
+        same node opens them (``native().IpcTables``) and garbles straight into this evaluator's slots."""
+        return self._h.ipc_export()
+
     @property
     def batch(self) -> int:
         return self._h.batch

@@ -124,6 +124,19 @@ def test_conv_band_edges(W, H, C, k, sw, sh, pad):
     _check(c, 7, None, xs)
 
 
+@pytest.mark.parametrize("crt", [7, [5, 7, 131]], ids=["base7", "p131_centered"])
+def test_conv_pipeline_many_items(crt):
+    """Persistent double-buffered conv (k_conv_pipe): more (image, band) items than resident blocks, so every block
+    walks several items, prefetching the next one's rows during the current MFMA phase and crossing residue
+    boundaries (weights reloaded); p = 131 takes the centered-operand path. Labels bit-exact against the host."""
+    rng = np.random.default_rng(31)
+    C, F, H, W = 16, 32, 7, 7
+    Wt = rng.integers(-5, 6, (F, C, 3, 3)); b = rng.integers(-5, 6, F)
+    c = d.Circuit([d.Conv2d.from_quantized(Wt, b, W, H, C, F, 3, 3, 1, 1)])
+    xs = [rng.integers(-6, 7, C * H * W) for _ in range(3)]
+    _check(c, crt, None, xs)
+
+
 @FUSED
 def test_sign_edges(fused):
     vals = [0, 1, -1, 55773217, -55773217, 111546434, -111546435]

@@ -173,3 +173,59 @@ def test_pipelined_offline_matches_serial():
             p.join(timeout=60)
     np.testing.assert_array_equal(res[0][0], res[1][0])
     assert res[0][1] == res[1][1]
+
+
+def test_ipc_transport_needs_a_gpu_garbler():
+    """transport='ipc' writes tables from the garbler's GPU into the evaluator's slots: refused without a device."""
+    c = build_circuit("MODEL_A")
+    with pytest.raises(ValueError, match="device"):
+        GarblerClient("127.0.0.1", 1, c, 7, 100.0, transport="ipc")
+
+
+def test_skeleton_of_host_model_is_the_full_message():
+    """A host-garbled model has no slot-resident tables: its skeleton is the whole offline message, and the
+    skeleton reader parses ordinary blobs."""
+    from dash_amd.garbling import GarbledCircuit
+    from dash_amd.native import native
+
+    gc = GarbledCircuit(build_circuit("MODEL_A"), 7, 100.0, seed=b"k" * 16)
+    blob = gc.model.serialize()
+    assert gc.model.serialize_skeleton() == blob
+    assert native().GarbledModel.deserialize_skeleton(blob).serialize() == blob
+
+
+def _ipc_server(port_q):
+    s = listen("127.0.0.1", 0)
+    port_q.put(s.getsockname()[1])
+    serve_once(s, backend="hip", device=0)
+    s.close()
+
+
+@pytest.mark.gpu
+def test_ipc_transport_two_processes():
+    """Device transport: the evaluator (a child process, HIP) exports its table arenas' IPC handles; the garbler
+    (this process, GPU garbler) writes every GC's tables straight into the evaluator's slots and sends skeletons
+    only. Two rounds of 2 fresh GCs decode to the plaintext outputs, and the offline bytes on the channel are a
+    fraction of what four full offline messages would take."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_ipc_server, args=(q,), daemon=True)
+    p.start()
+    port = q.get(timeout=300)
+    c = build_circuit("MODEL_A")
+    xs = quantized_inputs("MODEL_A", 4)
+    try:
+        with GarblerClient("127.0.0.1", port, c, 7, 100.0, batch=2, seed=b"i" * 16, device=0,
+                           transport="ipc") as cl:
+            for r in range(2):
+                cl.offline()
+                outs = cl.infer(xs[2 * r:2 * r + 2])
+                for x, y in zip(xs[2 * r:2 * r + 2], outs):
+                    np.testing.assert_array_equal(y, _plain(c, x))
+            from dash_amd.garbling import GarbledCircuit
+
+            full = len(GarbledCircuit(c, 7, 100.0, seed=b"f" * 16).model.serialize())
+            assert cl.stats["offline_bytes"] < 4 * full  # 5 skeletons (one template) vs 4 full offline messages
+    finally:
+        p.join(timeout=120)
+    assert p.exitcode == 0
