@@ -11,6 +11,7 @@
 //     (products mod p are unchanged), int32 accumulation, mod-p epilogue fused
 //     with the zero-count and bias-label adds. n runs over (GC, component,
 //     output position) of one residue, so every residue is one large GEMM.
+#include <atomic>
 #include <cstdio>
 #include <cstdlib>
 #include <map>
@@ -320,6 +321,13 @@ typedef uint32_t u32x4c __attribute__((ext_vector_type(4)));
 struct __attribute__((packed, aligned(2))) Row8c {
     u32x4c v;
 };
+// x mod q for x < 2^(24 - sh) (launch.h sh24 / m24): q = floor(x / p) exactly from one full-rate 24-bit
+// multiply-high (the 32-bit one is quarter rate), then one 24-bit multiply-add
+__device__ __forceinline__ uint32_t modq_conv24(uint32_t x, int q, uint32_t m, int sh) {
+    uint32_t d;
+    asm("v_mul_hi_u32_u24 %0, %1, %2" : "=v"(d) : "v"(x << sh), "s"(m));
+    return static_cast<uint32_t>(__mul24(static_cast<int>(d), -q) + static_cast<int>(x));
+}
 __device__ __forceinline__ uint32_t modq_conv(uint32_t x, uint32_t q, uint32_t mq) {
     // d = floor(x / q) or one less; the remainder (< 2q < 2^24) from the low 24 bits of x - d * q, so the
     // product can be the full-rate 24-bit multiply
@@ -590,6 +598,12 @@ __global__ __launch_bounds__(256) void k_conv_img2(ConvArgs a, Act x, Act y, int
     const bool dw16 = (npos & 15) == 0 && ((oy0 * a.OW) & 15) == 0 &&
                       ((reinterpret_cast<uintptr_t>(Y) & 15) == 0);
     const uint32_t mq = a.mq[j];
+    const int sh24 = a.sh24[j];
+    const uint32_t m24 = a.m24[j];
+    auto red = [&](int32_t acc, uint32_t add) -> uint32_t {
+        const uint32_t xv = static_cast<uint32_t>(acc) + add;
+        return sh24 >= 0 ? modq_conv24(xv, p, m24, sh24) : modq_conv(xv, static_cast<uint32_t>(p), mq);
+    };
     // tap offsets of the A-in-VGPR path, once per block (the k-step loop then only adds)
     int toff[AREG ? KSC : 1];
     if (AREG) {
@@ -670,7 +684,7 @@ __global__ __launch_bounds__(256) void k_conv_img2(ConvArgs a, Act x, Act y, int
                     uint32_t w = 0;
 #pragma unroll
                     for (int r = 0; r < 4; ++r)
-                        w |= modq_conv(static_cast<uint32_t>(acc[g][t][r]) + addc[g], static_cast<uint32_t>(p), mq) << (8 * r);
+                        w |= red(acc[g][t][r], addc[g]) << (8 * r);
                     d[t] = w;
                 }
                 auto r02 = __builtin_amdgcn_permlane32_swap(d[0], d[2], false, false);
@@ -701,7 +715,7 @@ __global__ __launch_bounds__(256) void k_conv_img2(ConvArgs a, Act x, Act y, int
                 uint32_t o[4];
 #pragma unroll
                 for (int r = 0; r < 4; ++r)
-                    o[r] = modq_conv(static_cast<uint32_t>(acc[g][t][r]) + addc[g], static_cast<uint32_t>(p), mq);
+                    o[r] = red(acc[g][t][r], addc[g]);
                 act_t* yr = Y + static_cast<int64_t>(fl) * npos + pos;
                 {
                     if (dw && cb + 3 < ncol) {
@@ -714,324 +728,6 @@ __global__ __launch_bounds__(256) void k_conv_img2(ConvArgs a, Act x, Act y, int
                 }
             }
         }
-    }
-}
-
-// ---------------------------------------------------------------------------
-// k_conv_pipe: the band-image conv as a persistent, double-buffered pipeline.
-// k_conv_img2 runs one (image, band) per block: the block waits out its band's global loads, then its weight
-// loads, then computes, so with 3 resident blocks per CU the staging latency was exposed (round-5 PMC: 50 % of
-// wave cycles waiting, 10 % MFMA busy). Here a block walks (image, band) items gridDim.x apart:
-//   * the loads of item i + 1 (raw 8-byte row pieces, bias and zero label) are issued before item i's MFMA phase
-//     and committed (centered, transposed, written to the other LDS buffer) after its epilogue, so the global
-//     latency hides behind the block's own compute;
-//   * the wave's A operand (16 filters x KSC k-steps) is reloaded only when the residue changes;
-//   * the accumulators start at the epilogue constant (no add per output) and the mod-p reduction is one
-//     multiply-high, one 24-bit multiply-add and a min when the layer's accumulator bound is below 2^23.
-// Staging items: (4 channels, 8 columns, one input row); edge items are one clamped 8-byte load per channel,
-// shifted and masked at commit time (no divergent byte-wise path for W >= 8).
-template <int KSC, bool UR>
-__global__ __launch_bounds__(256) void k_conv_pipe(ConvArgs a, Act x, Act y, int B) {
-    static_assert(KSC > 0, "k_conv_pipe keeps the A operand in VGPRs");
-    constexpr int kPF = kConvPipeItems;
-    extern __shared__ __attribute__((aligned(16))) int8_t img[];
-    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-    const int fw = blockIdx.y * 64 + wave * 16;  // the wave's 16 filters
-    const int fl = fw + (lane & 15);             // this lane's filter in the transposed product
-    const int nb = a.pnbands, bh = a.pband;
-    const int64_t nitems = a.img_off[a.crt.k] * nb;
-    const int S = a.ldsS, R = a.ldsR, Wp = a.W + 2 * a.pw;
-    const int CC = a.Cpad / 64;
-    const int c4n = a.Cpad / 4, WO = (Wp + 7) / 8;
-    const uint32_t mc4 = c4n > 1 ? 0xffffffffu / static_cast<uint32_t>(c4n) + 1u : 0u;
-    const uint32_t mwo = WO > 1 ? 0xffffffffu / static_cast<uint32_t>(WO) + 1u : 0u;
-    const uint32_t owm = a.OW > 1 ? 0xffffffffu / static_cast<uint32_t>(a.OW) + 1u : 0u;
-    const int HW = UR ? a.uH * a.uW : a.H * a.W;
-    const int Cimg = UR ? a.uC : a.C;  // channels of the stored input image
-    const int Wrow = UR ? a.uW : a.W;  // stored row width
-    const int npos = a.OH * a.OW;
-    int toff[KSC];
-#pragma unroll
-    for (int s = 0; s < KSC; ++s) {
-        const int kk = s / CC, cc = s - kk * CC;
-        const int dy = kk / a.kw, dx = kk - dy * a.kw;
-        toff[s] = dy * R + dx * S + cc * 64;
-    }
-
-    struct It {
-        int j, b, c, oy0, oy1, iy0, items;
-        const act_t* X;
-    };
-    auto decode = [&](int64_t it, It& d) {
-        const int band = static_cast<int>(it % nb);
-        const int64_t gimg = it / nb;
-        int j = 0;
-        while (j + 1 < a.crt.k && gimg >= a.img_off[j + 1]) ++j;
-        const int n = a.crt.n[j];
-        const int64_t r0 = gimg - a.img_off[j];
-        d.j = j;
-        d.b = static_cast<int>(r0 / n);
-        d.c = static_cast<int>(r0 - static_cast<int64_t>(d.b) * n);
-        d.oy0 = band * bh;
-        d.oy1 = min(a.OH, d.oy0 + bh);
-        d.iy0 = d.oy0 * a.sh - a.ph;
-        const int in_rows = (d.oy1 - d.oy0 - 1) * a.sh + a.kh;
-        d.items = in_rows * WO * c4n;
-        d.X = x.p[j] + (static_cast<int64_t>(d.b) * n + d.c) * Cimg * HW;
-    };
-    // item index -> (input row in band, 8-column group, channel group)
-    auto geom = [&](int it, int& yq, int& xo, int& c4) {
-        const int t2 = c4n > 1 ? static_cast<int>(__umulhi(static_cast<uint32_t>(it), mc4)) : it;
-        c4 = it - t2 * c4n;
-        yq = WO > 1 ? static_cast<int>(__umulhi(static_cast<uint32_t>(t2), mwo)) : t2;
-        xo = t2 - yq * WO;
-    };
-    // The row piece of patch channel q of an item, branch-free: the 8-byte load is clamped into the whole
-    // image (C*H*W >= 8 bytes: always a valid address, whatever the row width), `sh` places column ix0 at byte 0,
-    // and bytes outside [lo, hi) (padding, other rows) or channels past C are replaced at commit time.
-    const int CHW = Cimg * HW;
-    auto piece = [&](const It& d, int yq, int xo, int c4, int q, int& s0, int& sh, int& lo, int& hi) {
-        const int cq = c4 * 4 + q;
-        int ci, iy, ix0;
-        if constexpr (UR) {
-            const int tap = cq / a.uC;
-            ci = cq - tap * a.uC;
-            const int dy = tap / a.ukw, dx = tap - dy * a.ukw;
-            iy = (d.iy0 + yq) * a.ush - a.uph + dy;
-            ix0 = xo * 8 - a.upw + dx;
-        } else {
-            ci = cq;
-            iy = d.iy0 + yq;
-            ix0 = xo * 8 - a.pw;
-        }
-        const int Hs = UR ? a.uH : a.H;
-        const bool ok = cq < a.C && iy >= 0 && iy < Hs;
-        const int off = ci * HW + iy * Wrow + ix0;
-        s0 = min(max(off, 0), CHW - 8);
-        sh = off - s0;
-        lo = ok ? max(0, -ix0) : 8;
-        hi = ok ? min(8, Wrow - ix0) : 0;
-    };
-    // prefetched loads of the next item: raw 8-byte pieces, zero label, bias
-    uint64_t raw[kPF][4];
-    int16_t zv_n = 0;
-    uint16_t bq_n = 0;
-    auto issue = [&](const It& d) {
-#pragma unroll
-        for (int u = 0; u < kPF; ++u) {
-            const int it = min(tid + 256 * u, d.items - 1);  // spare lanes repeat the last item (same bytes)
-            int yq, xo, c4;
-            geom(it, yq, xo, c4);
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                int s0, sh, lo, hi;
-                piece(d, yq, xo, c4, q, s0, sh, lo, hi);
-                raw[u][q] = *reinterpret_cast<const uint64_t*>(d.X + s0);
-            }
-        }
-        zv_n = a.zero[static_cast<int64_t>(d.b) * a.lab_stride + a.lab_off[d.j] + d.c];
-        bq_n = static_cast<uint16_t>(a.bias[d.j][(static_cast<int64_t>(d.b) * a.F + min(fl, a.F - 1)) * a.crt.n[d.j] + d.c]);
-    };
-    // shift / mask / center the prefetched pieces, transpose to channel-last dwords, write buffer dst
-    auto commit = [&](const It& d, int8_t* dst, int zv) {
-        const int p = a.crt.p[d.j], half = p / 2;
-        const bool rawx = p < 128;
-        const uint32_t padb = static_cast<uint32_t>(rawx ? zv : (zv > half ? zv - p : zv)) & 0xffu;
-        const uint32_t ck = static_cast<uint32_t>(127 - half) * 0x01010101u;
-        const uint32_t csub = static_cast<uint32_t>(256 - p) * 0x01010101u;
-        auto center4 = [&](uint32_t b) -> uint32_t {
-            const uint32_t hi = (b + ck) & 0x80808080u;
-            const uint32_t msk = (hi - (hi >> 7)) | hi;
-            return ((b + csub) & msk) | (b & ~msk);
-        };
-        const uint64_t padr = static_cast<uint64_t>(padb) * 0x0101010101010101ull;
-#pragma unroll
-        for (int u = 0; u < kPF; ++u) {
-            int it = min(tid + 256 * u, d.items - 1);
-            // recompute the item geometry here instead of keeping issue()'s across the MFMA phase (registers)
-            asm volatile("" : "+v"(it));
-            int yq, xo, c4;
-            geom(it, yq, xo, c4);
-            uint32_t w[4][2];
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                int s0, sh, lo, hi;
-                piece(d, yq, xo, c4, q, s0, sh, lo, hi);
-                uint64_t t = raw[u][q];
-                t = sh >= 8 || sh <= -8 ? 0ull : (sh >= 0 ? t >> (8 * sh) : t << (-8 * sh));
-                const uint64_t msk = hi > lo ? (hi >= 8 ? ~0ull : (1ull << (8 * hi)) - 1ull) & ~((1ull << (8 * lo)) - 1ull) : 0ull;
-                const uint32_t t0 = static_cast<uint32_t>(t), t1 = static_cast<uint32_t>(t >> 32);
-                const uint64_t cv = (static_cast<uint64_t>(rawx ? t1 : center4(t1)) << 32) | (rawx ? t0 : center4(t0));
-                // channels past C stay 0 (their weights are 0); out-of-image bytes take the padding byte
-                const uint64_t v = (c4 * 4 + q >= a.C) ? 0ull : ((cv & msk) | (padr & ~msk));
-                w[q][0] = static_cast<uint32_t>(v);
-                w[q][1] = static_cast<uint32_t>(v >> 32);
-            }
-#pragma unroll
-            for (int h = 0; h < 2; ++h) {
-                const uint32_t ab0 = __builtin_amdgcn_perm(w[1][h], w[0][h], 0x05010400u);
-                const uint32_t ab1 = __builtin_amdgcn_perm(w[1][h], w[0][h], 0x07030602u);
-                const uint32_t cd0 = __builtin_amdgcn_perm(w[3][h], w[2][h], 0x05010400u);
-                const uint32_t cd1 = __builtin_amdgcn_perm(w[3][h], w[2][h], 0x07030602u);
-                const uint32_t col[4] = {__builtin_amdgcn_perm(cd0, ab0, 0x05040100u), __builtin_amdgcn_perm(cd0, ab0, 0x07060302u),
-                                         __builtin_amdgcn_perm(cd1, ab1, 0x05040100u), __builtin_amdgcn_perm(cd1, ab1, 0x07060302u)};
-                int8_t* rowp = dst + yq * R + c4 * 4;
-#pragma unroll
-                for (int t = 0; t < 4; ++t) {
-                    const int xx = xo * 8 + 4 * h + t;
-                    if (xx < Wp) *reinterpret_cast<uint32_t*>(rowp + xx * S) = col[t];
-                }
-            }
-        }
-    };
-    // MFMA phase + epilogue of item d from LDS buffer src. FAST: the exact 24-bit reduction (launch.h sh24 / m24,
-    // three full-rate ops per output); otherwise multiply-high (quarter rate) + 24-bit fix-up.
-    v2l av[KSC];
-    uint32_t zq = 0;
-    int jw = -1;
-    auto load_weights = [&](int j) {
-        if (j == jw) return;  // uniform: once per residue change
-        jw = j;
-        const int8_t* Wr = a.w8r[j] + static_cast<int64_t>(min(fl, ((a.F + 15) & ~15) - 1)) * (a.kh * a.kw * a.Cpad) + (lane >> 4) * 16;
-#pragma unroll
-        for (int s = 0; s < KSC; ++s) {
-            const int kk = s / CC, cc = s - kk * CC;
-            av[s] = *reinterpret_cast<const v2l*>(Wr + kk * a.Cpad + cc * 64);
-        }
-        zq = fl < a.F ? static_cast<uint32_t>(a.zc[j][fl]) : 0u;
-    };
-    auto compute = [&](auto fast_tag, const It& d, const int8_t* src, int zv, uint32_t bq) {
-        constexpr bool FAST = decltype(fast_tag)::value;
-        const int p = a.crt.p[d.j], half = p / 2, n = a.crt.n[d.j];
-        const bool rawx = p < 128;
-        const uint32_t xmax = static_cast<uint32_t>(rawx ? p - 1 : half);
-        const uint32_t bound = static_cast<uint32_t>(a.Kpad * half) * xmax;
-        const uint32_t off = static_cast<uint32_t>(p) * (bound / static_cast<uint32_t>(p) + 1);
-        const uint32_t addc = off + zq * static_cast<uint32_t>(zv) + bq;
-        const uint32_t mq = FAST ? a.m24[d.j] : a.mq[d.j];
-        const int sh = FAST ? a.sh24[d.j] : 0;
-        auto red = [&](int32_t acc) -> uint32_t {
-            const uint32_t xv = static_cast<uint32_t>(acc);
-            if constexpr (FAST) {
-                uint32_t q;  // bits 32..47 of the 24 x 24-bit product (full rate, unlike the 32-bit multiply-high)
-                asm("v_mul_hi_u32_u24 %0, %1, %2" : "=v"(q) : "v"(xv << sh), "s"(mq));
-                return static_cast<uint32_t>(__mul24(static_cast<int>(q), -p) + static_cast<int>(xv));
-            } else {
-                const uint32_t dq = __umulhi(xv, mq);  // floor(x / p) or one less
-                const uint32_t r = (xv - __umul24(dq, static_cast<uint32_t>(p))) & 0xffffffu;
-                return min(r, r - static_cast<uint32_t>(p));  // r - p wraps above r when r < p
-            }
-        };
-        const int ncol = (d.oy1 - d.oy0) * a.OW;
-        act_t* Y = y.p[d.j] + (static_cast<int64_t>(d.b) * n + d.c) * a.F * npos;
-        const bool dw = (npos & 3) == 0 && ((d.oy0 * a.OW) & 3) == 0;
-        const bool dw16 = (npos & 15) == 0 && ((d.oy0 * a.OW) & 15) == 0 && ((reinterpret_cast<uintptr_t>(Y) & 15) == 0);
-        const int32_t ai = static_cast<int32_t>(addc);
-        for (int colw = 0; colw < ncol; colw += 64) {
-            v4i acc[4];
-            int base[4];
-#pragma unroll
-            for (int t = 0; t < 4; ++t) {
-                acc[t] = v4i{ai, ai, ai, ai};
-                const int col = colw + t * 16 + (lane & 15);
-                const int cl = col < ncol ? col : 0;  // columns past the band read column 0 (never stored)
-                const int oyl = a.OW > 1 ? static_cast<int>(__umulhi(static_cast<uint32_t>(cl), owm)) : cl;
-                const int ox = cl - oyl * a.OW;
-                base[t] = (oyl * a.sh) * R + (ox * a.sw) * S + (lane >> 4) * 16;
-            }
-            v2l bcur[4], bnxt[4];
-#pragma unroll
-            for (int t = 0; t < 4; ++t) bcur[t] = *reinterpret_cast<const v2l*>(src + base[t] + toff[0]);
-#pragma unroll
-            for (int s = 0; s < KSC; ++s) {
-                if (s + 1 < KSC) {
-#pragma unroll
-                    for (int t = 0; t < 4; ++t)
-                        bnxt[t] = *reinterpret_cast<const v2l*>(src + base[t] + toff[s + 1 < KSC ? s + 1 : s]);
-                }
-                __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-                for (int t = 0; t < 4; ++t) acc[t] = __builtin_amdgcn_mfma_i32_16x16x64_i8(bcur[t], av[s], acc[t], 0, 0, 0);
-                __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-                for (int t = 0; t < 4; ++t) bcur[t] = bnxt[t];
-            }
-            if (dw16 && colw + 64 <= ncol) {
-                // lane (f, h) holds positions 16 t + 4 h + 0..3 of tile t; a 4x4 transpose over (t, h) with the
-                // permlane swaps gives it positions 16 h + 0..15: one 16-byte store per lane
-                uint32_t dd[4];
-#pragma unroll
-                for (int t = 0; t < 4; ++t)
-                    dd[t] = red(acc[t][0]) | (red(acc[t][1]) << 8) | (red(acc[t][2]) << 16) | (red(acc[t][3]) << 24);
-                auto r02 = __builtin_amdgcn_permlane32_swap(dd[0], dd[2], false, false);
-                auto r13 = __builtin_amdgcn_permlane32_swap(dd[1], dd[3], false, false);
-                dd[0] = r02[0];
-                dd[2] = r02[1];
-                dd[1] = r13[0];
-                dd[3] = r13[1];
-                auto r01 = __builtin_amdgcn_permlane16_swap(dd[0], dd[1], false, false);
-                auto r23 = __builtin_amdgcn_permlane16_swap(dd[2], dd[3], false, false);
-                if (fl < a.F) {
-                    act_t* yr = Y + static_cast<int64_t>(fl) * npos + d.oy0 * a.OW + colw + 16 * (lane >> 4);
-                    *reinterpret_cast<uint4*>(yr) = make_uint4(r01[0], r01[1], r23[0], r23[1]);
-                }
-                continue;
-            }
-            if (fl >= a.F) continue;
-#pragma unroll
-            for (int t = 0; t < 4; ++t) {
-                const int cb = colw + t * 16 + (lane >> 4) * 4;
-                if (cb >= ncol) continue;
-                uint32_t o[4];
-#pragma unroll
-                for (int r = 0; r < 4; ++r) o[r] = red(acc[t][r]);
-                act_t* yr = Y + static_cast<int64_t>(fl) * npos + d.oy0 * a.OW + cb;
-                if (dw && cb + 3 < ncol) {
-                    *reinterpret_cast<uint32_t*>(yr) = o[0] | (o[1] << 8) | (o[2] << 16) | (o[3] << 24);
-                } else {
-#pragma unroll
-                    for (int r = 0; r < 4; ++r)
-                        if (cb + r < ncol) yr[r] = static_cast<act_t>(o[r]);
-                }
-            }
-        }
-    };
-    auto run = [&](const It& d, const int8_t* src, int zv, uint32_t bq) {
-        if (fw >= a.F) return;  // wave-uniform
-        load_weights(d.j);
-        if (a.sh24[d.j] >= 0) compute(std::true_type{}, d, src, zv, bq);
-        else compute(std::false_type{}, d, src, zv, bq);
-    };
-
-    int64_t it = blockIdx.x;
-    if (it >= nitems) return;
-    It cur, nxt;
-    decode(it, cur);
-    issue(cur);
-    int zv_c = zv_n;
-    uint32_t bq_c = bq_n;
-    if (a.w8r[cur.j]) commit(cur, img, zv_c);
-    __syncthreads();
-    int buf = 0;
-    for (;;) {
-        const int64_t in = it + gridDim.x;
-        const bool has = in < nitems;
-        if (has) {
-            decode(in, nxt);
-            if (a.w8r[nxt.j]) issue(nxt);
-        }
-        // residues with p > 255 run on the VALU kernel (uniform skip)
-        if (a.w8r[cur.j]) run(cur, img + buf * a.pbuf, zv_c, bq_c);
-        if (!has) break;
-        if (a.w8r[nxt.j]) {
-            zv_c = zv_n;
-            bq_c = bq_n;
-            commit(nxt, img + (buf ^ 1) * a.pbuf, zv_c);
-        }
-        __syncthreads();
-        buf ^= 1;
-        cur = nxt;
-        it = in;
     }
 }
 
@@ -1184,51 +880,7 @@ void launch_conv(const ConvArgs& a, const Act& x, const Act& y, int B, hipStream
             return e ? std::atoi(e) : 2;
         }();
         const int KS = a.kh * a.kw * (a.Cpad / 64);
-        static const bool pipe = [] {
-            const char* e = std::getenv("DASH_CONV_PIPE");
-            return !(e && e[0] == '0');
-        }();
-        if (pipe && a.pnbands > 0 && (a.ur ? KS == 1 : (KS == 1 || KS == 4 || KS == 9))) {
-            // persistent: as many blocks as stay resident (two LDS buffers each), at most one per item
-            static const int ncu = [] {
-                int dev = 0, n = 0;
-                (void)hipGetDevice(&dev);
-                (void)hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
-                return n > 0 ? n : 256;
-            }();
-            const size_t plds = 2 * static_cast<size_t>(a.pbuf);
-            const void* kfn = a.ur ? reinterpret_cast<const void*>(&k_conv_pipe<1, true>)
-                              : KS == 9 ? reinterpret_cast<const void*>(&k_conv_pipe<9, false>)
-                              : KS == 4 ? reinterpret_cast<const void*>(&k_conv_pipe<4, false>)
-                                        : reinterpret_cast<const void*>(&k_conv_pipe<1, false>);
-            // resident blocks per CU (registers and the two LDS buffers), once per (kernel, buffer size)
-            static std::mutex mu;
-            static std::map<std::pair<const void*, size_t>, int> occ;
-            int per_cu;
-            {
-                std::lock_guard<std::mutex> lk(mu);
-                auto itc = occ.find({kfn, plds});
-                if (itc == occ.end()) {
-                    int nb = 0;
-                    const hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kfn, 256, plds);
-                    if (e != hipSuccess || nb < 1) nb = 1;
-                    if (const char* o = std::getenv("DASH_CONV_PIPE_PERCU")) nb = std::max(1, std::atoi(o));
-                    if (const char* dbg = std::getenv("DASH_CONV_PIPE_DEBUG"))
-                        if (dbg[0] == '1')
-                            std::fprintf(stderr, "[conv_pipe] KS=%d ur=%d lds=%zu occupancy rc=%d blocks/CU=%d band=%d x%d CUs=%d\n",
-                                         KS, a.ur, plds, static_cast<int>(e), nb, a.pband, a.pnbands, ncu);
-                    itc = occ.emplace(std::make_pair(kfn, plds), nb).first;
-                }
-                per_cu = itc->second;
-            }
-            const int64_t items = nimg * a.pnbands;
-            const unsigned gx = static_cast<unsigned>(std::min<int64_t>(items, static_cast<int64_t>(ncu) * per_cu));
-            dim3 gp(gx, static_cast<unsigned>((a.F + 63) / 64), 1);
-            if (a.ur) hipLaunchKernelGGL((k_conv_pipe<1, true>), gp, dim3(256), plds, st, a, x, y, B);
-            else if (KS == 9) hipLaunchKernelGGL((k_conv_pipe<9, false>), gp, dim3(256), plds, st, a, x, y, B);
-            else if (KS == 4) hipLaunchKernelGGL((k_conv_pipe<4, false>), gp, dim3(256), plds, st, a, x, y, B);
-            else hipLaunchKernelGGL((k_conv_pipe<1, false>), gp, dim3(256), plds, st, a, x, y, B);
-        } else if (ver == 1 && a.ldsS == a.Cpad + 16 && a.ldsR == (a.W + 2 * a.pw) * a.ldsS)
+        if (ver == 1 && a.ldsS == a.Cpad + 16 && a.ldsR == (a.W + 2 * a.pw) * a.ldsS)
             hipLaunchKernelGGL(k_conv_img, g, dim3(256), lds, st, a, x, y, B);  // A/B: its fixed layout only
         else if (a.ur && KS == 1)
             hipLaunchKernelGGL((k_conv_img2<1, true>), g, dim3(256), lds, st, a, x, y, B);

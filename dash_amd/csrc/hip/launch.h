@@ -107,9 +107,6 @@ struct ConvArgs {
     uint32_t m24[kMaxRes];
     int sh24[kMaxRes];
     int ldsS = 0, ldsR = 0;        // LDS image: bytes per position and per input row (conv_img_geometry)
-    // persistent double-buffered kernel (k_conv_pipe): band height, bands per image and bytes per LDS buffer;
-    // pnbands = 0: the layer runs the one-band-per-block kernel
-    int pband = 0, pnbands = 0, pbuf = 0;
     // tap-unrolled image (conv_unroll_taps): the band is staged per OUTPUT position with the C*kh*kw patch
     // bytes as its channels, the MFMA phase then runs a 1x1 conv (one k-step instead of kh*kw for C << 64).
     // u* hold the layer's own geometry for the staging; the fields above describe the unrolled view.
@@ -161,37 +158,14 @@ inline int conv_lds_read_cycles(const ConvArgs& a, int S, int R) {
 }
 
 struct ConvGeomPick {
-    int S, R, band, nbands, pband, pnbands, pbuf;
+    int S, R, band, nbands;
 };
-// k_conv_pipe: staging items (4 channels x 8 columns of one input row) per thread it can hold in flight
-constexpr int kConvPipeItems = 4;
-// Band of the persistent pipelined kernel: the tallest band whose staged rows fit one LDS buffer of the budget
-// (two buffers per block) and whose staging items fit kConvPipeItems per thread
-inline void conv_pipe_geometry(ConvArgs& a) {
-    static const int64_t budget = [] {
-        const char* e = std::getenv("DASH_CONV_PIPE_KB");
-        const int64_t kb = e ? std::atoll(e) : 20;
-        return std::max<int64_t>(4, std::min<int64_t>(40, kb)) * 1024;
-    }();
-    a.pband = a.pnbands = a.pbuf = 0;
-    // the staging's 8-byte loads are clamped into the whole input image
-    if ((a.ur ? static_cast<int64_t>(a.uC) * a.uH * a.uW : static_cast<int64_t>(a.C) * a.H * a.W) < 8) return;
-    const int Wp = a.W + 2 * a.pw;
-    const int64_t items_row = static_cast<int64_t>((Wp + 7) / 8) * (a.Cpad / 4);
-    int band = a.OH;
-    auto rows = [&](int b) { return static_cast<int64_t>((b - 1) * a.sh + a.kh); };
-    while (band > 1 && (rows(band) * a.ldsR > budget || rows(band) * items_row > kConvPipeItems * 256)) --band;
-    if (rows(band) * a.ldsR > budget || rows(band) * items_row > kConvPipeItems * 256) return;
-    a.pband = band;
-    a.pnbands = (a.OH + band - 1) / band;
-    a.pbuf = static_cast<int>((rows(band) * a.ldsR + 15) / 16 * 16);
-}
 inline void conv_img_geometry(ConvArgs& a) {
     a.Cpad = (a.C + 63) / 64 * 64;
     for (int j = 0; j < a.crt.k; ++j) {
         const int p = a.crt.p[j];
         a.mq[j] = static_cast<uint32_t>(0x100000000ull / static_cast<uint32_t>(p));
-        // x = acc + epilogue constant < 2 * Kpad * half * xmax + (Kpad + 3) p (k_conv_pipe's bound)
+        // x = acc + epilogue constant < 2 * Kpad * half * xmax + (Kpad + 3) p (the epilogue's bound)
         const int half = p / 2;
         const uint64_t xmax = p < 128 ? static_cast<uint64_t>(p - 1) : static_cast<uint64_t>(half);
         const uint64_t X = 2ull * static_cast<uint64_t>(a.Kpad) * half * xmax + (static_cast<uint64_t>(a.Kpad) + 3) * p;
@@ -223,9 +197,6 @@ inline void conv_img_geometry(ConvArgs& a) {
             a.ldsR = it->second.R;
             a.band = it->second.band;
             a.nbands = it->second.nbands;
-            a.pband = it->second.pband;
-            a.pnbands = it->second.pnbands;
-            a.pbuf = it->second.pbuf;
             return;
         }
     }
@@ -258,9 +229,8 @@ inline void conv_img_geometry(ConvArgs& a) {
             }
         }
     }
-    if (a.nbands > 0) conv_pipe_geometry(a);
     std::lock_guard<std::mutex> lk(mu);
-    memo[key] = ConvGeomPick{a.ldsS, a.ldsR, a.band, a.nbands, a.pband, a.pnbands, a.pbuf};
+    memo[key] = ConvGeomPick{a.ldsS, a.ldsR, a.band, a.nbands};
 }
 
 // Switch a layer to the tap-unrolled image when that cuts the MFMA k-steps (few input channels, e.g. the
