@@ -34,6 +34,9 @@ struct ModC {
     uint32_t dm;     // digit magic: floor(r / q) = mulhi(r, dm) >> ds for r < D (host_util.h make_modc)
     uint32_t ds;
     uint32_t pm;     // label PRG digits per AES block (core.h prg_digits)
+    // division by D with a 32-bit reciprocal (Moller-Granlund 2011, "Improved division by invariant
+    // integers"): Dn = D << sh normalized to [2^31, 2^32), v = floor((2^64 - 1) / Dn) - 2^32
+    uint32_t Dn, v, sh;
 };
 
 __device__ __forceinline__ uint64_t mulhi64(uint64_t a, uint64_t b) { return __umul64hi(a, b); }
@@ -82,6 +85,46 @@ __device__ __forceinline__ uint32_t modq64(uint64_t x, const ModC& m) {
 }
 
 // (Q, r) = divmod(Q, D)
+// One step of the preinverted division: (u1 * 2^32 + u0) / Dn for u1 < Dn; quotient returned, remainder in r.
+// One 32 x 32 -> 64 multiply-add, one 32-bit multiply and two corrections (selects): about half the
+// quarter-rate multiplies of the 64-bit reciprocal form (div64_32).
+__device__ __forceinline__ uint32_t mg_step(uint32_t u1, uint32_t u0, uint32_t Dn, uint32_t v, uint32_t& r) {
+    const uint64_t pr = static_cast<uint64_t>(v) * u1 + u0;
+    uint32_t ql = static_cast<uint32_t>(pr);
+    uint32_t qh = static_cast<uint32_t>(pr >> 32) + u1 + 1u;
+    uint32_t rr = u0 - qh * Dn;
+    if (rr > ql) {
+        --qh;
+        rr += Dn;
+    }
+    if (rr >= Dn) {
+        ++qh;
+        rr -= Dn;
+    }
+    r = rr;
+    return qh;
+}
+// Q / D in place, remainder returned, for D = m.D (odd modulus chunk, D < 2^31 so 1 <= sh <= 31): the
+// numerator is shifted by sh (five limbs, the top one below Dn) and divided by Dn limb by limb.
+__device__ __forceinline__ uint32_t divmod128(u128& Q, const struct ModC& m) {
+    const uint32_t l3 = static_cast<uint32_t>(Q >> 96), l2 = static_cast<uint32_t>(Q >> 64);
+    const uint32_t l1 = static_cast<uint32_t>(Q >> 32), l0 = static_cast<uint32_t>(Q);
+    const uint32_t sh = m.sh, rs = 32u - sh;  // 1 <= sh <= 31
+    const uint32_t u4 = l3 >> rs;
+    const uint32_t u3 = __builtin_amdgcn_alignbit(l3, l2, rs), u2 = __builtin_amdgcn_alignbit(l2, l1, rs);
+    const uint32_t u1 = __builtin_amdgcn_alignbit(l1, l0, rs), u0 = l0 << sh;
+    uint32_t r, q3 = 0, q2 = 0;
+    if (l3 | l2) {
+        q3 = mg_step(u4, u3, m.Dn, m.v, r);
+        q2 = mg_step(r, u2, m.Dn, m.v, r);
+    } else {
+        r = u2;  // Q < 2^64: the shifted top limbs are u2 = l1 >> (32 - sh) < 2^31 <= Dn, no quotient bits
+    }
+    const uint32_t q1 = mg_step(r, u1, m.Dn, m.v, r);
+    const uint32_t q0 = mg_step(r, u0, m.Dn, m.v, r);
+    Q = (static_cast<u128>((static_cast<uint64_t>(q3) << 32) | q2) << 64) | ((static_cast<uint64_t>(q1) << 32) | q0);
+    return r >> sh;
+}
 __device__ __forceinline__ uint32_t divmod128(u128& Q, uint32_t D, uint64_t mD) {
     uint32_t l3 = static_cast<uint32_t>(Q >> 96), l2 = static_cast<uint32_t>(Q >> 64);
     uint32_t l1 = static_cast<uint32_t>(Q >> 32), l0 = static_cast<uint32_t>(Q);
@@ -119,7 +162,7 @@ struct DigitStream {
             return d;
         }
         if (left == 0) {
-            r = divmod128(Q, m.D, m.mD);
+            r = divmod128(Q, m);
             left = m.c;
         }
         // r < D <= 2^31: exact quotient by multiply-high + shift; the digit (< q < 2^24) from the low
@@ -138,7 +181,7 @@ struct DigitStream {
 };
 
 // Chunk-major digit extraction (callers that walk whole chunks of m.c digits with a wave-uniform trip count):
-// r = divmod128(Q, m.D, m.mD) starts a chunk, chunk_digit(r, m) returns its next digit. The same digits as
+// r = divmod128(Q, m) starts a chunk, chunk_digit(r, m) returns its next digit. The same digits as
 // DigitStream::next without the per-digit chunk bookkeeping.
 __device__ __forceinline__ uint32_t chunk_digit(uint32_t& r, const ModC& m) {
 #if DASH_DIGIT_MAGIC
@@ -247,7 +290,7 @@ __device__ __forceinline__ u128 compress_cm(const T* L, long stride, const ModC&
 __device__ __forceinline__ uint32_t u128_mod(u128 P, const ModC& m) {
     if (m.bits) return static_cast<uint32_t>(P) & (m.q - 1);
     u128 Q = P;
-    uint32_t r = divmod128(Q, m.D, m.mD);
+    uint32_t r = divmod128(Q, m);
     uint32_t d;
     div32_q(r, m.q, m.mq, d);
     return d;

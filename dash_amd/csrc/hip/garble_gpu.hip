@@ -268,6 +268,9 @@ __device__ __forceinline__ ModC rfl_modc(const ModC& m) {
     r.dm = rflu(m.dm);
     r.ds = rflu(m.ds);
     r.pm = rflu(m.pm);
+    r.Dn = rflu(m.Dn);
+    r.v = rflu(m.v);
+    r.sh = rflu(m.sh);
     return r;
 }
 __device__ __forceinline__ Proj rfl_proj(const Proj& p) {
@@ -371,7 +374,7 @@ __global__ __launch_bounds__(kGB) void k_draw(Ctx c, Gadget g) {
                                                  : aes_keyed(aes, base | static_cast<uint64_t>(d.ctr + bi), c.rk);
                 const int bcnt = min(pm, n - bi * pm);
                 for (int k0 = 0; k0 < bcnt; k0 += static_cast<int>(m.c)) {
-                    uint32_t r = divmod128(Q, m.D, m.mD);
+                    uint32_t r = divmod128(Q, m);
                     const int kc = min(static_cast<int>(m.c), bcnt - k0);
                     for (int t = 0; t < kc; ++t, ++q) push(q, chunk_digit(r, m));
                 }

@@ -128,6 +128,11 @@ inline dev::ModC make_modc(int q) {
     m.c = c;
     m.D = static_cast<uint32_t>(D);
     m.mD = static_cast<uint64_t>((static_cast<u128>(1) << 64) / D);
+    int bl = 0;
+    while ((D >> bl) != 0) ++bl;
+    m.sh = static_cast<uint32_t>(32 - bl);  // D < 2^31: 1 <= sh
+    m.Dn = static_cast<uint32_t>(D << m.sh);
+    m.v = static_cast<uint32_t>(~0ull / static_cast<uint64_t>(m.Dn) - (1ull << 32));
     m.mq = static_cast<uint32_t>((1ull << 32) / static_cast<uint64_t>(q));
     int s = 0;
     while ((1 << (s + 1)) < q) ++s;  // 2^s < q <= 2^(s+1)

@@ -462,7 +462,7 @@ __global__ __launch_bounds__(kRmBS) void k_relu_mult_s(SignArgs a, Act x, Act y,
         } else {  // chunk-major (chunk_digit): one divmod per stream per chunk, uniform digit loops
             u128 QG = G, QE = E;
             for (int c0 = 0; c0 < n; c0 += static_cast<int>(m.c)) {
-                uint32_t rg = divmod128(QG, m.D, m.mD), re = divmod128(QE, m.D, m.mD);
+                uint32_t rg = divmod128(QG, m), re = divmod128(QE, m);
                 const int cnt = min(static_cast<int>(m.c), n - c0);
                 for (int t = 0; t < cnt; ++t) {
                     const uint32_t g = chunk_digit(rg, m);
@@ -857,7 +857,7 @@ __global__ __launch_bounds__(kOhBS, kAesMinBlocks) void k_rescale_mrs_out_hash_s
                 }
             } else {  // chunk-major (chunk_digit): one divmod per chunk, uniform digit loops, one flush per chunk
                 for (int k0 = 0; k0 < cnt; k0 += static_cast<int>(m.c)) {
-                    uint32_t r = divmod128(Q, m.D, m.mD);
+                    uint32_t r = divmod128(Q, m);
                     const int kc = min(static_cast<int>(m.c), cnt - k0);
                     uint32_t acc = 0, pt = 1;
                     for (int t = 0; t < kc; ++t) {

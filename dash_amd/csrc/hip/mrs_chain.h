@@ -225,7 +225,7 @@ __device__ __forceinline__ void chain_s_pos(const MrsArgs& a, uint64_t gate, con
                     for (int c0 = 0; c0 < pcnt; c0 += mcn) {
                         uint32_t rr[K > 1 ? K - 1 : 1];
 #pragma unroll
-                        for (int l = 0; l < i; ++l) rr[l] = divmod128(Q[l], m.D, m.mD);
+                        for (int l = 0; l < i; ++l) rr[l] = divmod128(Q[l], m);
                         const int cnt = min(mcn, pcnt - c0);
                         uint32_t v = 0, pt = 1;
                         for (int t = 0; t < cnt; ++t) {
@@ -370,7 +370,7 @@ __device__ __forceinline__ void chain_w_pos(const MrsArgs& a, uint64_t gate, con
             for (int c0 = 0; c0 < n; c0 += static_cast<int>(m.c)) {
                 uint32_t rr[I > 0 ? I : 1];
 #pragma unroll
-                for (int l = 0; l < I; ++l) rr[l] = divmod128(Q[l], m.D, m.mD);
+                for (int l = 0; l < I; ++l) rr[l] = divmod128(Q[l], m);
                 const int cnt = min(static_cast<int>(m.c), n - c0);
                 uint32_t v = 0, pt = 1;
                 for (int t = 0; t < cnt; ++t) {
