@@ -457,7 +457,10 @@ __device__ __forceinline__ void hard_block(u128 K, uint64_t gate, uint32_t sub, 
     uint32_t x0 = 0x61707865u, x1 = 0x3320646eu, x2 = 0x79622d32u, x3 = 0x6b206574u;
     uint32_t x4 = k0, x5 = k1, x6 = k2, x7 = k3, x8 = g0, x9 = g1, x10 = sub, x11 = 0x44524148u;
     uint32_t x12 = blk, x13 = 0, x14 = 0, x15 = 0;
-#pragma unroll
+    // NOT unrolled: a kernel inlines this block at every table row it unmasks (the K = 7 chain: ~15 sites), and
+    // fully unrolled each copy was ~9 KiB of code, pushing the chain kernels to 70-95 KiB, beyond the
+    // instruction cache shared by two CUs. The loop costs 3 scalar instructions per double round.
+#pragma unroll 1
     for (int r = 0; r < kDevChaRounds; r += 2) {
         DASH_QR(x0, x4, x8, x12) DASH_QR(x1, x5, x9, x13) DASH_QR(x2, x6, x10, x14) DASH_QR(x3, x7, x11, x15)
         DASH_QR(x0, x5, x10, x15) DASH_QR(x1, x6, x11, x12) DASH_QR(x2, x7, x8, x13) DASH_QR(x3, x4, x9, x14)

@@ -185,6 +185,9 @@ __device__ __forceinline__ void chain_s_pos(const MrsArgs& a, uint64_t gate, con
             const act_t* L = x.p[r] + static_cast<int64_t>(b) * n * N;
             uint32_t col = 0;
             u128 key;
+            constexpr int kExtra = MODE == 1 ? 0 : 1;
+            constexpr int nt = K - 1 - i + kExtra;
+            u128 pf0 = 0, pf1 = 0;  // the row's first and last entries, loaded as soon as the row index is known
             if (m.bits) {  // power-of-two modulus (uniform branch): per-digit streams
                 DigitStream ds[K > 1 ? K - 1 : 1];
 #pragma unroll
@@ -203,7 +206,14 @@ __device__ __forceinline__ void chain_s_pos(const MrsArgs& a, uint64_t gate, con
                             const uint32_t s = ds[l].next(m);
                             d = d >= s ? d - s : d + m.q - s;
                         }
-                        if (c0 + c == 0) col = d;
+                        if (c0 + c == 0) {
+                            col = d;
+                            // the row index is the key's first digit: start the row's first / last entry loads
+                            // now, so the gather overlaps the rest of the digit walk (block-uniform branch)
+                            const u128* rowp = row0 + a.dig_off[i] + static_cast<int64_t>(col) * nt;
+                            pf0 = rowp[0];
+                            pf1 = rowp[nt - 1];
+                        }
                         cf.push(d, m);
                     }
                 }
@@ -235,7 +245,12 @@ __device__ __forceinline__ void chain_s_pos(const MrsArgs& a, uint64_t gate, con
                                 const uint32_t sd = chunk_digit(rr[l], m);
                                 d = d >= sd ? d - sd : d + m.q - sd;
                             }
-                            if (p0 + c0 + t == 0) col = d;
+                            if (p0 + c0 + t == 0) {
+                                col = d;
+                                const u128* rowp = row0 + a.dig_off[i] + static_cast<int64_t>(col) * nt;
+                                pf0 = rowp[0];
+                                pf1 = rowp[nt - 1];
+                            }
                             v += d * pt;
                             pt *= m.q;
                         }
@@ -245,12 +260,12 @@ __device__ __forceinline__ void chain_s_pos(const MrsArgs& a, uint64_t gate, con
                 }
                 key = C;
             }
-            constexpr int kExtra = MODE == 1 ? 0 : 1;
-            const int nt = K - 1 - i + kExtra;
             const u128* row = row0 + a.dig_off[i] + static_cast<int64_t>(col) * nt;
             u128 E[K];
+            E[0] = pf0;
 #pragma unroll
-            for (int t = 0; t < nt; ++t) E[t] = row[t];
+            for (int t = 1; t < nt - 1; ++t) E[t] = row[t];  // the lines were brought in by the early loads
+            if (nt > 1) E[nt - 1] = pf1;
             hard_unmask_n<K>(E, nt, key, gate, mrs_row_sub<MODE>(i));
             if (valid) {
 #pragma unroll
@@ -342,6 +357,9 @@ __device__ __forceinline__ void chain_w_pos(const MrsArgs& a, uint64_t gate, con
         const uint8_t* Ls = wst + roff[r] * kMrsWBS + tid;
         uint32_t col = 0;
         u128 key;
+        constexpr int kExtra = MODE == 1 ? 0 : 1;
+        constexpr int nt = K - 1 - I + kExtra;
+        u128 pf0 = 0, pf1 = 0;  // the row's first and last entries, loaded as soon as the row index is known
         if (m.bits) {  // power-of-two modulus (uniform branch): per-digit streams
             DigitStream ds[I > 0 ? I : 1];
 #pragma unroll
@@ -355,7 +373,13 @@ __device__ __forceinline__ void chain_w_pos(const MrsArgs& a, uint64_t gate, con
                     const uint32_t s = ds[l].next(m);
                     d = d >= s ? d - s : d + m.q - s;
                 }
-                if (c == 0) col = d;
+                if (c == 0) {
+                    col = d;
+                    // the row index is the key's first digit: the gather overlaps the rest of the digit walk
+                    const u128* rowp = row0 + a.dig_off[I] + static_cast<int64_t>(col) * nt;
+                    pf0 = rowp[0];
+                    pf1 = rowp[nt - 1];
+                }
                 cf.push(d, m);
             }
             key = cf.finish();
@@ -380,7 +404,12 @@ __device__ __forceinline__ void chain_w_pos(const MrsArgs& a, uint64_t gate, con
                         const uint32_t sd = chunk_digit(rr[l], m);
                         d = d >= sd ? d - sd : d + m.q - sd;
                     }
-                    if (c0 + t == 0) col = d;
+                    if (c0 + t == 0) {
+                        col = d;
+                        const u128* rowp = row0 + a.dig_off[I] + static_cast<int64_t>(col) * nt;
+                        pf0 = rowp[0];
+                        pf1 = rowp[nt - 1];
+                    }
                     v += d * pt;
                     pt *= m.q;
                 }
@@ -389,12 +418,12 @@ __device__ __forceinline__ void chain_w_pos(const MrsArgs& a, uint64_t gate, con
             }
             key = C;
         }
-        constexpr int kExtra = MODE == 1 ? 0 : 1;
-        constexpr int nt = K - 1 - I + kExtra;
         const u128* row = row0 + a.dig_off[I] + static_cast<int64_t>(col) * nt;
         u128 E[nt > 0 ? nt : 1];
+        E[0] = pf0;
 #pragma unroll
-        for (int t = 0; t < nt; ++t) E[t] = row[t];
+        for (int t = 1; t < nt - 1; ++t) E[t] = row[t];  // the lines were brought in by the early loads
+        if constexpr (nt > 1) E[nt - 1] = pf1;
         if constexpr (nt > 0) hard_unmask<nt>(E, key, gate, mrs_row_sub<MODE>(I));
 #pragma unroll
         for (int t = 0; t < K - 1 - I; ++t) PS[mrs_pair<K>(I, I + 1 + t)] = E[t];
