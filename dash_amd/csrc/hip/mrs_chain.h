@@ -188,7 +188,7 @@ __device__ __forceinline__ void chain_s_pos(const MrsArgs& a, uint64_t gate, con
             constexpr int kExtra = MODE == 1 ? 0 : 1;
             constexpr int nt = K - 1 - i + kExtra;
             u128 pf0 = 0, pf1 = 0;  // the row's first and last entries, loaded as soon as the row index is known
-            if (m.bits) {  // power-of-two modulus (uniform branch): per-digit streams
+            if constexpr (r == 0) {  // residue 0, the base's power of two (mrs_staged checks): per-digit streams
                 DigitStream ds[K > 1 ? K - 1 : 1];
 #pragma unroll
                 for (int l = 0; l < i; ++l) ds[l].init(PS[static_cast<int64_t>(mrs_pair<K>(l, i)) * N]);
@@ -344,7 +344,10 @@ __global__ __launch_bounds__(kMrsBS, MODE == 2 ? DASH_CHAIN2_WAVES : DASH_UA_MIN
 //  * the K(K-1)/2 pair payloads stay in registers (one wave per SIMD: the whole 512-VGPR file is the lane's).
 constexpr int kMrsWBS = 256;
 constexpr int kWaveU = 8;
-// one position of k_mrs_chain_w, I a compile-time constant (the pair payloads PS stay in registers)
+// one position of k_mrs_chain_w, I a compile-time constant (the pair payloads PS stay in registers). The wave
+// form is compiled for bases whose residue 0 is the only power of two (first-primes bases: p_0 = 2, the rest
+// odd; mrs_wave_lds checks it): each position then carries one digit path instead of both, which keeps the
+// kernel's code closer to the instruction cache.
 template <int K, int MODE, int I>
 __device__ __forceinline__ void chain_w_pos(const MrsArgs& a, uint64_t gate, const ModC* mc, const uint8_t* wst,
                                             const int* roff, int tid, bool valid, const u128* row0, u128* PS,
@@ -360,7 +363,7 @@ __device__ __forceinline__ void chain_w_pos(const MrsArgs& a, uint64_t gate, con
         constexpr int kExtra = MODE == 1 ? 0 : 1;
         constexpr int nt = K - 1 - I + kExtra;
         u128 pf0 = 0, pf1 = 0;  // the row's first and last entries, loaded as soon as the row index is known
-        if (m.bits) {  // power-of-two modulus (uniform branch): per-digit streams
+        if constexpr (r == 0) {  // residue 0: the base's power of two (per-digit streams)
             DigitStream ds[I > 0 ? I : 1];
 #pragma unroll
             for (int l = 0; l < I; ++l) ds[l].init(PS[mrs_pair<K>(l, I)]);
@@ -383,7 +386,7 @@ __device__ __forceinline__ void chain_w_pos(const MrsArgs& a, uint64_t gate, con
                 cf.push(d, m);
             }
             key = cf.finish();
-        } else {
+        } else {  // odd residue
             // chunk-major walk: every stream shares the modulus, so one divmod per stream per chunk of m.c
             // digits, then the chunk's digits with a wave-uniform trip count, one compress flush per chunk
             // (the same digits and compress as DigitStream / CompressFwd, without their per-digit bookkeeping)
@@ -539,6 +542,13 @@ __global__ __launch_bounds__(kMrsWBS, 1) void k_mrs_chain_w(MrsArgs a, Act x, co
     }
 }
 
+// bases whose residue 0 is the single power of two: the wave and staged chain forms compile one digit path per position
+static inline bool mrs_odd_base(const CrtInfo& crt) {
+    if ((crt.p[0] & (crt.p[0] - 1)) != 0) return false;
+    for (int r = 1; r < crt.k; ++r)
+        if ((crt.p[r] & 1) == 0) return false;
+    return true;
+}
 // dynamic LDS of k_mrs_chain_w (every residue's rows for kMrsWBS elements), 0 when the form does not apply
 static inline size_t mrs_wave_lds(const MrsArgs& a, int B) {
     static const bool on = [] {
@@ -547,6 +557,8 @@ static inline size_t mrs_wave_lds(const MrsArgs& a, int B) {
     }();
     // only launches of at most one block per CU: above that the per-lane form keeps more waves resident (24 GCs,
     // MiniONN: 11.29 ms per step per-lane vs 11.56 with this form on every small-block launch)
+    // only bases whose residue 0 is the single power of two (the form's positions carry one digit path each)
+    if (!mrs_odd_base(a.crt)) return 0;
     // (rows that are not 16-byte aligned: byte-wise staging, only for single-block layers)
     if (!on || (a.N % 16 != 0 && a.N > kMrsWBS) || (a.N + kMrsWBS - 1) / kMrsWBS * B > num_cus()) return 0;
     size_t sum = 0;
@@ -572,8 +584,8 @@ static void launch_chain_w(const MrsArgs& a, const Act& x, int B, size_t wl, con
 
 // the staged chain holds two 512-lane blocks per CU: below two blocks per CU (batch-1 latency) the per-lane form,
 // whose block size shrinks to spread a small launch over every CU, is faster
-static inline bool mrs_staged(int64_t N, int B) {
-    return stage_ok(N, kMrsBS) && (N + kMrsBS - 1) / kMrsBS * B >= 2 * num_cus();
+static inline bool mrs_staged(const MrsArgs& a, int B) {
+    return mrs_odd_base(a.crt) && stage_ok(a.N, kMrsBS) && (a.N + kMrsBS - 1) / kMrsBS * B >= 2 * num_cus();
 }
 
 
@@ -581,7 +593,7 @@ static inline bool mrs_staged(int64_t N, int B) {
 // latency), the LDS-staged form for large ones, the per-lane form between; a.mode picks rescale / sign / joint.
 template <int K>
 void launch_mrs_chain_k(const MrsArgs& a, const Act& x, int B, const ModC* mc, const AesGlobals& g, hipStream_t st) {
-    const bool stg = mrs_staged(a.N, B);
+    const bool stg = mrs_staged(a, B);
     const size_t wl = stg ? 0 : mrs_wave_lds(a, B);
     const dim3 gc = stg ? grid_aes(a.N, kMrsBS, 1, B) : grid_aes(a.N, aes_bs(a.N, 1, B), 1, B);
     const dim3 bc(stg ? kMrsBS : aes_bs(a.N, 1, B));
