@@ -36,6 +36,18 @@ from ..native import native
 from .channel import Channel, ChannelClosed, connect
 
 VERSION = 1
+# Largest table arena the ipc transport exports: importing a bigger dmabuf-backed allocation
+# (hipIpcOpenMemHandle) never returned on the MI355X lease (MiniONN at batch 4 and 8: 2.2 and 4.5 GB arenas),
+# while 1.1 GB arenas open at once. The server refuses a larger one with a clear error instead of a hang.
+IPC_MAX_ARENA = 2 << 30
+_DEBUG = os.environ.get("DASH_NET_DEBUG") == "1"
+
+
+def _dbg(msg: str) -> None:
+    if _DEBUG:
+        import sys
+
+        print(f"[dash.net {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
 
 
 class EvaluatorServer:
@@ -103,9 +115,17 @@ class EvaluatorServer:
                         from ..runtime import HipEvaluator
 
                         skel = n.GarbledModel.deserialize_skeleton(buf)
+                        _dbg("server: TMPL received, building the evaluator")
                         if self.ev is None:
                             self.ev = HipEvaluator(template=skel, batch=self.batch, device=self.device)
-                        hs = [[int(l), str(t), int(nb), bytes(h).hex()] for l, t, nb, h in self.ev.ipc_export()]
+                        ex = self.ev.ipc_export()
+                        big = max((int(nb) * self.batch for _, _, nb, _ in ex), default=0)
+                        if big >= IPC_MAX_ARENA:
+                            raise ValueError(f"ipc transport: a {big / 2**30:.2f} GiB table arena (batch {self.batch}) is "
+                                             f"above the {IPC_MAX_ARENA >> 30} GiB this transport opens; use a smaller "
+                                             f"batch or transport 'shm'")
+                        hs = [[int(l), str(t), int(nb), bytes(h).hex()] for l, t, nb, h in ex]
+                        _dbg(f"server: exported {len(hs)} table arenas")
                         ch.send(b"IPCH", json.dumps(hs).encode())
                     elif tag == b"MODX":
                         slot = flags
@@ -114,6 +134,7 @@ class EvaluatorServer:
                         if self.ev is None:
                             raise ValueError("MODX before TMPL: the evaluator has no table arenas yet")
                         self.ev.load(slot, n.GarbledModel.deserialize_skeleton(buf))
+                        _dbg(f"server: MODX slot {slot} loaded")
                         del buf
                         self.models[slot] = True
                         ch.send(b"ACK_")
@@ -386,13 +407,17 @@ class GarblerClient:
         distinct, so GC b + 1 is garbled while the evaluator loads GC b's constants; the ACKs are collected last."""
         if self._ipc is None:
             tmpl = self._garble_gc(None)  # a template for the evaluator's build (tables stay here, discarded)
+            _dbg("client: template garbled")
             self.ch.send(b"TMPL", tmpl.model.serialize_skeleton(all_device=True))
             del tmpl
             _, _, buf = self.ch.recv(b"IPCH")
             hs = [(int(l), str(t), int(nb), bytes.fromhex(h)) for l, t, nb, h in json.loads(buf.decode())]
+            _dbg(f"client: {len(hs)} IPC handles received")
             self._ipc = native().IpcTables(int(self.device), hs, self.batch)
+            _dbg("client: handles opened")
         for b in range(self.batch):
             gc = self._garble_gc(seeds[b], sink=self._ipc.sink(b))
+            _dbg(f"client: GC {b} garbled into the evaluator's slot")
             t = time.perf_counter()
             skel = gc.model.serialize_skeleton()
             gc.model = None
