@@ -1142,9 +1142,10 @@ void HipEvaluator::build() {
                         const char* e = std::getenv("DASH_JOINT_FUSE");
                         return e ? std::atoi(e) : -1;
                     }();
-                    // With LDS staging (N % 16 == 0) the two staged kernels beat the fused one at batch 1 too
-                    // (2.24 vs 2.30 ms per step), so the fused form is the default only for unstaged shapes.
-                    const bool fuse = fuse_env >= 0 ? fuse_env == 1 : (B_ <= 2 && N % 16 != 0);
+                    // Round 4 (AES tables) had the two staged kernels ahead at batch 1 for N % 16 == 0; with the
+                    // hardened encoding the fused form wins there too (latency_b1 2.21 -> 2.14 ms) and ties at
+                    // 24 GCs (9.85 vs 9.82 ms per step, profiles/ab/r5_joint_fuse_*.json): on for batch <= 2.
+                    const bool fuse = fuse_env >= 0 ? fuse_env == 1 : B_ <= 2;
                     const bool defer = fuse && so && li + 1 < m0.layers.size() && m0.layers[li + 1].kind == K_RELU &&
                                        m0.layers[li + 1].param("smode", 0) == 2 && !keep[li + 1] &&
                                        !m0.layers[li + 1].p.count("in_src");

@@ -216,6 +216,7 @@ class InferenceService:
         # (garble_gpu.hip DevCtx pool), filling each other's kernel-launch gaps and latency stalls
         # (served inf/s with 5 % faults, 2 / 3 / 4 workers: 88 / 104 / 110, profiles/r03_serving_workers_*.json)
         self.garble_workers = max(1, int(garble_workers if garble_workers is not None else
+                                         int(os.environ.get("DASH_GARBLE_WORKERS", "0")) or
                                          (4 if self.garble_device else 1)))
         self._ctr_lock = threading.Lock()
         self._next_group = 0
