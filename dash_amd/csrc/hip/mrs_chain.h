@@ -542,6 +542,241 @@ __global__ __launch_bounds__(kMrsWBS, 1) void k_mrs_chain_w(MrsArgs a, Act x, co
     }
 }
 
+// ---------------------------------------------------------------------------
+// Quad form of the wave chain (batch-1 latency). At batch 1 a chain launch is one wave per SIMD and every
+// element is a serial walk of K positions (~100 us per launch whatever the layer size, r05 batch-1 trace).
+// Here four lanes share one element:
+//  * position I's I payload streams are dealt to the quad's lanes (stream l to lane l % 4), each lane
+//    decompresses its own, and the per-digit sums are all-reduced over the quad with two DPP adds;
+//  * every lane then has the key digits and compresses the key (the same value in all four lanes);
+//  * the row's entries and their pad blocks are split over the lanes (entries 4g..4g+3 and ChaCha block g on
+//    lane g) and broadcast back with DPP, so the pair payloads stay replicated in every lane's registers;
+//  * the final row likewise: lane g unmasks and stores outputs 4g..4g+3.
+// Four times the lanes of the wave form, and per lane about a quarter of the decompression work.
+constexpr int kMrsQE = 64;            // elements per block
+constexpr int kMrsQBS = 4 * kMrsQE;   // threads per block (quads of consecutive lanes)
+template <int S>
+__device__ __forceinline__ uint32_t quad_bcast(uint32_t v) {  // the value of quad lane S, in every lane of the quad
+    return static_cast<uint32_t>(__builtin_amdgcn_mov_dpp(static_cast<int>(v), S * 0x55, 0xF, 0xF, false));
+}
+template <int S>
+__device__ __forceinline__ u128 quad_bcast128(u128 v) {
+    const uint32_t w0 = quad_bcast<S>(static_cast<uint32_t>(v)), w1 = quad_bcast<S>(static_cast<uint32_t>(v >> 32));
+    const uint32_t w2 = quad_bcast<S>(static_cast<uint32_t>(v >> 64)), w3 = quad_bcast<S>(static_cast<uint32_t>(v >> 96));
+    return (static_cast<u128>((static_cast<uint64_t>(w3) << 32) | w2) << 64) | ((static_cast<uint64_t>(w1) << 32) | w0);
+}
+// sum over the quad of v < q, mod q (every lane gets it): xor-1 then xor-2 partners (quad_perm 1032 / 2301)
+__device__ __forceinline__ uint32_t quad_sum_mod(uint32_t v, uint32_t q) {
+    uint32_t s = v + static_cast<uint32_t>(__builtin_amdgcn_mov_dpp(static_cast<int>(v), 0xB1, 0xF, 0xF, false));
+    s = s >= q ? s - q : s;
+    uint32_t t = s + static_cast<uint32_t>(__builtin_amdgcn_mov_dpp(static_cast<int>(s), 0x4E, 0xF, 0xF, false));
+    return t >= q ? t - q : t;
+}
+template <int K, int MODE, int I>
+__device__ __forceinline__ void chain_q_pos(const MrsArgs& a, uint64_t gate, const ModC* mc, const uint8_t* wst,
+                                            const int* roff, int el, int g, bool valid, const u128* row0, u128* PS,
+                                            u128& acc) {
+    constexpr int kLast = MODE >= 1 ? K - 1 : K;
+    if constexpr (I < kLast) {
+        constexpr int r = MODE >= 1 ? (I + 1) % K : I;
+        const ModC m = mc[a.crt.p[r]];
+        const int n = static_cast<int>(m.n);
+        const uint8_t* Ls = wst + roff[r] * kMrsQE + el;  // the four lanes of a quad read the same byte (broadcast)
+        constexpr int kExtra = MODE == 1 ? 0 : 1;
+        constexpr int nt = K - 1 - I + kExtra;
+        uint32_t col = 0;
+        u128 key;
+        u128 Eo[4] = {0, 0, 0, 0};  // this lane's entries 4g .. 4g + 3 of the row
+        auto fetch_row = [&](uint32_t c) {  // issued as soon as the row index (the key's first digit) is known
+            const u128* rowp = row0 + a.dig_off[I] + static_cast<int64_t>(c) * nt;
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+                if (4 * g + q < nt) Eo[q] = rowp[4 * g + q];
+        };
+        if constexpr (r == 0) {  // residue 0, the base's power of two: mode 0 position 0, no payload streams
+            CompressFwd cf;
+            cf.init();
+            for (int c = 0; c < n; ++c) {
+                const uint32_t d = valid ? Ls[c * kMrsQE] : 0u;
+                if (c == 0) {
+                    col = d;
+                    fetch_row(col);
+                }
+                cf.push(d, m);
+            }
+            key = cf.finish();
+        } else {
+            constexpr int NS = I > 0 ? (I + 3) / 4 : 1;  // streams per lane: l = g + 4 s < I
+            u128 Q[NS];
+#pragma unroll
+            for (int s2 = 0; s2 < NS; ++s2) {
+                Q[s2] = 0;
+#pragma unroll
+                for (int l = 4 * s2; l < 4 * s2 + 4 && l < I; ++l)  // static register indices, selected per lane
+                    if (g == l - 4 * s2) Q[s2] = PS[mrs_pair<K>(l, I)];
+            }
+            u128 C = 0, PW = 1;
+            const int mcn = static_cast<int>(m.c);
+            const uint32_t q = m.q;
+            for (int c0 = 0; c0 < n; c0 += mcn) {
+                uint32_t rr[NS];
+#pragma unroll
+                for (int s2 = 0; s2 < NS; ++s2) rr[s2] = divmod128(Q[s2], m);  // lanes without a stream: Q = 0
+                const int cnt = min(mcn, n - c0);
+                uint32_t v = 0, pt = 1;
+                for (int t = 0; t < cnt; ++t) {
+                    uint32_t sd = 0;
+#pragma unroll
+                    for (int s2 = 0; s2 < NS; ++s2) {
+                        sd += chunk_digit(rr[s2], m);
+                        sd = sd >= q ? sd - q : sd;
+                    }
+                    const uint32_t S = quad_sum_mod(sd, q);  // the digit sum of all I streams
+                    uint32_t d = valid ? Ls[(c0 + t) * kMrsQE] : 0u;
+                    d = d >= S ? d - S : d + q - S;
+                    if (c0 + t == 0) {
+                        col = d;
+                        fetch_row(col);
+                    }
+                    v += d * pt;
+                    pt *= q;
+                }
+                C += PW * static_cast<u128>(v);
+                PW *= static_cast<u128>(m.D);
+            }
+            key = C;
+        }
+        if (4 * g < nt) {  // lane g's pad block (entries 4g .. 4g + 3)
+            u128 pd[4];
+            hard_block(key, gate, mrs_row_sub<MODE>(I), static_cast<uint32_t>(g), pd);
+#pragma unroll
+            for (int qq = 0; qq < 4; ++qq)
+                if (4 * g + qq < nt) Eo[qq] -= pd[qq];
+        }
+        // every lane takes every entry: pair payloads for the later positions, the T target for acc
+        u128 E[nt];
+#pragma unroll
+        for (int t = 0; t < nt; ++t) {
+            if constexpr (true) {
+                const u128 own = Eo[t % 4];
+                E[t] = (t >> 2) == 0 ? quad_bcast128<0>(own) : (t >> 2) == 1 ? quad_bcast128<1>(own)
+                       : (t >> 2) == 2 ? quad_bcast128<2>(own) : quad_bcast128<3>(own);
+            }
+        }
+#pragma unroll
+        for (int t = 0; t < K - 1 - I; ++t) PS[mrs_pair<K>(I, I + 1 + t)] = E[t];
+        if constexpr (MODE != 1) acc = add_packed(acc, E[K - 1 - I], a.hmask);
+        chain_q_pos<K, MODE, I + 1>(a, gate, mc, wst, roff, el, g, valid, row0, PS, acc);
+    }
+}
+
+template <int K, int MODE>
+__global__ __launch_bounds__(kMrsQBS, 2) void k_mrs_chain_q(MrsArgs a, Act x, const ModC* mc) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t wst[];  // row gg (residue r, component c) at gg * kMrsQE
+    const int b = blockIdx.z;
+    const int64_t N = a.N;
+    constexpr int NP = K * (K - 1) / 2 > 0 ? K * (K - 1) / 2 : 1;
+    const int tid = static_cast<int>(threadIdx.x);
+    const int el = tid >> 2, g = tid & 3;
+    int roff[K + 1];
+    const act_t* src[K];
+    roff[0] = 0;
+#pragma unroll
+    for (int r = 0; r < K; ++r) {
+        const int n = static_cast<int>(mc[a.crt.p[r]].n);
+        roff[r + 1] = roff[r] + n;
+        src[r] = x.p[r] + static_cast<int64_t>(b) * n * N;
+    }
+    for (int64_t e0 = static_cast<int64_t>(blockIdx.x) * kMrsQE; e0 < N; e0 += static_cast<int64_t>(gridDim.x) * kMrsQE) {
+        __syncthreads();  // the previous tile's readers are done
+        if (N % 16 == 0) {
+            // 16-byte units: row gg's kMrsQE bytes are kMrsQE / 16 units
+            constexpr int W = kMrsQE / 16;
+            const int units = roff[K] * W;
+            for (int x0 = tid; x0 < units; x0 += 4 * kMrsQBS) {
+                uint4 v[4];
+#pragma unroll
+                for (int h = 0; h < 4; ++h) {
+                    const int xu = x0 + h * kMrsQBS;
+                    const int gg = xu / W;
+                    const int64_t e = e0 + 16 * (xu % W);
+                    const act_t* row = src[0] + static_cast<int64_t>(gg) * N;
+#pragma unroll
+                    for (int r = 1; r < K; ++r)
+                        if (gg >= roff[r]) row = src[r] + static_cast<int64_t>(gg - roff[r]) * N;
+                    if (xu < units && e < N) v[h] = *reinterpret_cast<const uint4*>(row + e);
+                }
+#pragma unroll
+                for (int h = 0; h < 4; ++h) {
+                    const int xu = x0 + h * kMrsQBS;
+                    if (xu < units) *reinterpret_cast<uint4*>(wst + (xu / W) * kMrsQE + 16 * (xu % W)) = v[h];
+                }
+            }
+        } else {
+            const int bunits = roff[K] * kMrsQE;  // one byte per (row, element)
+            for (int xu = tid; xu < bunits; xu += kMrsQBS) {
+                const int gg = xu / kMrsQE;
+                const int64_t e = e0 + xu % kMrsQE;
+                const act_t* row = src[0] + static_cast<int64_t>(gg) * N;
+#pragma unroll
+                for (int r = 1; r < K; ++r)
+                    if (gg >= roff[r]) row = src[r] + static_cast<int64_t>(gg - roff[r]) * N;
+                wst[xu] = e < N ? static_cast<uint8_t>(row[e]) : 0;
+            }
+        }
+        __syncthreads();
+        const bool valid = e0 + el < N;
+        const int64_t e = valid ? e0 + el : N - 1;  // spare quads shadow a real element, store nothing
+        const u128* row0 = a.tab + (static_cast<int64_t>(b) * N + e) * a.n_tab;
+        u128 PS[NP];
+        u128 acc = 0;
+        const uint64_t gate = a.gate0 ^ static_cast<uint64_t>(e);
+        chain_q_pos<K, MODE, 0>(a, gate, mc, wst, roff, el, g, valid, row0, PS, acc);
+        if (MODE >= 1) {
+            // residue 0 (mod 2): bit pack of L_0 XOR the K - 1 payloads aimed at it = the sign label (all lanes)
+            const ModC m = mc[a.crt.p[0]];
+            const int n = static_cast<int>(m.n);
+            const uint8_t* Ls = wst + el;
+            CompressFwd cf;
+            cf.init();
+            for (int c = 0; c < n; ++c) cf.push(valid ? Ls[c * kMrsQE] : 0u, m);
+            u128 key = cf.finish();
+#pragma unroll
+            for (int l = 0; l < K - 1; ++l) key ^= PS[mrs_pair<K>(l, K - 1)];
+            const uint32_t cb = static_cast<uint32_t>(key) & 1u;
+            u128 E = 0;
+            if (MODE == 2) E = row0[a.dig_off[K - 1] + cb] - hard_pad(key, gate, mrs_row_sub<MODE>(K - 1), 0);
+            if (valid) {
+                // the next ReLU's y-row pads: block g on lane g
+                const uint64_t gy = a.rgate0 ^ static_cast<uint64_t>(e);
+                if (4 * g < a.ny) {
+                    u128 pd[4];
+                    hard_block(key, gy, tw_sub(kTwMmy, 0), static_cast<uint32_t>(g), pd);
+#pragma unroll
+                    for (int qq = 0; qq < 4; ++qq)
+                        if (4 * g + qq < a.ny) a.ys[(static_cast<int64_t>(b) * a.ny + 4 * g + qq) * N + e] = pd[qq];
+                }
+                if (g == 0) a.cs[static_cast<int64_t>(b) * N + e] = static_cast<uint8_t>(cb);
+            }
+            if (MODE == 2) acc = add_packed(acc, E, a.hmask);
+        }
+        if (MODE == 1) continue;
+        const uint32_t colf = static_cast<uint32_t>(acc) & static_cast<uint32_t>(a.T - 1);
+        const u128* row = row0 + a.fin_off + static_cast<int64_t>(colf) * K;
+        if (4 * g < K) {  // outputs 4g .. 4g + 3 under pad block g
+            u128 F[4], pd[4];
+#pragma unroll
+            for (int qq = 0; qq < 4; ++qq) F[qq] = 4 * g + qq < K ? row[4 * g + qq] : u128(0);
+            hard_block(acc, gate, mrs_row_sub<0>(K), static_cast<uint32_t>(g), pd);
+            if (valid) {
+#pragma unroll
+                for (int qq = 0; qq < 4; ++qq)
+                    if (4 * g + qq < K) a.pf[(static_cast<int64_t>(b) * K + 4 * g + qq) * N + e] = F[qq] - pd[qq];
+            }
+        }
+    }
+}
+
 // bases whose residue 0 is the single power of two: the wave and staged chain forms compile one digit path per position
 static inline bool mrs_odd_base(const CrtInfo& crt) {
     if ((crt.p[0] & (crt.p[0] - 1)) != 0) return false;
@@ -568,10 +803,25 @@ static inline size_t mrs_wave_lds(const MrsArgs& a, int B) {
     return bytes;
 }
 
-// launches k_mrs_chain_w<K, MODE> with wl bytes of dynamic LDS (the per-kernel limit is raised once)
+// the quad form replaces the wave form where that applies (DASH_MRS_QUAD=0: the wave form, A/B)
+static inline bool mrs_quad_on() {
+    static const bool on = [] {
+        const char* e = std::getenv("DASH_MRS_QUAD");
+        return !(e && e[0] == '0');
+    }();
+    return on;
+}
+// launches k_mrs_chain_w<K, MODE> (or its quad form) with wl bytes of dynamic LDS (the per-kernel limit is raised
+// once)
 template <int K, int MODE>
 static void launch_chain_w(const MrsArgs& a, const Act& x, int B, size_t wl, const ModC* mc, const AesGlobals& g,
                            hipStream_t st) {
+    if (mrs_quad_on()) {
+        const size_t ql = wl / kMrsWBS * kMrsQE;  // every residue's rows for kMrsQE elements
+        const dim3 gq(static_cast<unsigned>((a.N + kMrsQE - 1) / kMrsQE), 1, B);
+        hipLaunchKernelGGL((k_mrs_chain_q<K, MODE>), gq, dim3(kMrsQBS), ql, st, a, x, mc);
+        return;
+    }
     static const bool raised = [] {
         return hipFuncSetAttribute(reinterpret_cast<const void*>(&k_mrs_chain_w<K, MODE>),
                                    hipFuncAttributeMaxDynamicSharedMemorySize,
