@@ -621,17 +621,20 @@ __device__ __forceinline__ void chain_q_pos(const MrsArgs& a, uint64_t gate, con
             for (int c0 = 0; c0 < n; c0 += mcn) {
                 uint32_t rr[NS];
 #pragma unroll
-                for (int s2 = 0; s2 < NS; ++s2) rr[s2] = divmod128(Q[s2], m);  // lanes without a stream: Q = 0
+                for (int s2 = 0; s2 < NS; ++s2) rr[s2] = I > 0 ? divmod128(Q[s2], m) : 0u;  // no stream: Q = 0
                 const int cnt = min(mcn, n - c0);
                 uint32_t v = 0, pt = 1;
                 for (int t = 0; t < cnt; ++t) {
-                    uint32_t sd = 0;
+                    uint32_t S = 0;
+                    if constexpr (I > 0) {
+                        uint32_t sd = 0;
 #pragma unroll
-                    for (int s2 = 0; s2 < NS; ++s2) {
-                        sd += chunk_digit(rr[s2], m);
-                        sd = sd >= q ? sd - q : sd;
+                        for (int s2 = 0; s2 < NS; ++s2) {
+                            sd += chunk_digit(rr[s2], m);
+                            sd = sd >= q ? sd - q : sd;
+                        }
+                        S = quad_sum_mod(sd, q);  // the digit sum of all I streams
                     }
-                    const uint32_t S = quad_sum_mod(sd, q);  // the digit sum of all I streams
                     uint32_t d = valid ? Ls[(c0 + t) * kMrsQE] : 0u;
                     d = d >= S ? d - S : d + q - S;
                     if (c0 + t == 0) {
