@@ -102,6 +102,8 @@ def run_tcp(circuit, cfg, xs, args) -> dict:
                 t1 = time.perf_counter()
                 outs = cl.infer(batch)
                 t2 = time.perf_counter()
+                print(f"[two_party] round {r}: offline {t1 - t0:.3f} s, online {1000 * (t2 - t1):.1f} ms",
+                      file=sys.stderr, flush=True)
                 if r == 0:
                     st0 = dict(cl.stats, online_s=list(cl.stats["online_s"]))
                     ok = all(np.array_equal(y, _plain(circuit, crt, mrs, x)) for x, y in zip(batch, outs))
@@ -186,12 +188,16 @@ def main(argv=None):
         xs = quantize_images(cfg, circuit, imgs)
         # range calibration (as the headline bench): lets the "auto" constructions pick the mixed-radix
         # rescale + joint ReLU where the tracked ranges allow (GarbledCircuit defaults)
+        print(f"[two_party] {name}: calibrating ranges", file=sys.stderr, flush=True)
         cal = quantize_images(cfg, circuit, synthetic_inputs(cfg.model_name, 32, seed=0))
         crt0, _, _ = _gc_args(cfg)
         from dash_amd.garbling.gc import GarbledCircuit as _GC
 
         M = _GC(circuit, crt0, _gc_args(cfg)[1], garble_me=False).crt_modulus
-        circuit.calibrate(cal, M)
+        for i, x in enumerate(cal):  # one image at a time with a heartbeat (a large model takes minutes)
+            circuit.calibrate([x], M, reset=i == 0)
+            if i % 4 == 3:
+                print(f"[two_party] {name}: calibrated {i + 1}/{len(cal)}", file=sys.stderr, flush=True)
         cons = _GC(circuit, crt0, _gc_args(cfg)[1], garble_me=False).effective_constructions()
         for split, tr in itertools.product(args.splits.split(","), args.transport.split(",")):
             if tr == "ipc" and (args.backend != "hip" or args.garble_device < 0):
