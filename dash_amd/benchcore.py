@@ -110,6 +110,10 @@ def parse_args(argv=None) -> argparse.Namespace:
     ap.add_argument("--thread-sweep", default="4,8",
                     help="host thread budgets of the threads phase (headline loop re-timed at each)")
     ap.add_argument("--latency-gcs", type=int, default=8, help="fresh GCs timed one by one in the latency phase")
+    ap.add_argument("--latency-encode", default=os.environ.get("DASH_BENCH_LATENCY_ENCODE", "device"),
+                    choices=["device", "host"],
+                    help="latency phase, online message #1: the garbler's device encoder (GarbledCircuit."
+                         "device_input_encoder) or host-encoded compressed labels + H2D + GPU unpack")
     ap.add_argument("--ref-batch", type=int, default=0, help="GCs per GPU of the reference phase (0: auto)")
     ap.add_argument("--ref-steps", type=int, default=0, help="timed steps of the reference phase (0: --steps)")
     ap.add_argument("--served-slots", type=int, default=16)
@@ -219,8 +223,12 @@ class _HipGroup:
     def encode(self, b, gc, x):
         self.ev.encode_compressed_into(b, gc, x)
 
-    def launch(self):
-        self.ev.upload_inputs_compressed(self.stream)
+    def encode_device(self, b, enc, x):
+        self.ev.encode_device_into(b, enc, x, self.stream)
+
+    def launch(self, upload: bool = True):
+        if upload:
+            self.ev.upload_inputs_compressed(self.stream)
         self.ev.run(self.stream)
 
     def fetch(self):
@@ -516,6 +524,7 @@ class _Bench:
 
         n = max(2, self.args.latency_gcs)
         xs = quantized_inputs(self.model, n, self.qm, self.qp, seed=7000 + self.ctx.rank)
+        dev_enc = self.hip and getattr(self.args, "latency_encode", "device") == "device"
         ev, grp, times, ok = None, None, [], True
         for i in range(n + 1):  # one untimed warm-up GC (first launch, graph build)
             if self.hip:
@@ -531,11 +540,17 @@ class _Bench:
                 gc = self.garble("lat", i, cons)
                 grp = grp or _CpuGroup(gc.model, 1, self.threads)
             grp.load(0, gc)
+            # device encoding: the garbler's input state of this GC goes to the GPU with its tables (offline)
+            enc = gc.device_input_encoder(self.device) if dev_enc else None
             x = xs[max(0, i - 1)]
             self.sync()
             t = time.perf_counter()
-            grp.encode(0, gc, x)
-            grp.launch()
+            if enc is not None:
+                grp.encode_device(0, enc, x)
+                grp.launch(upload=False)
+            else:
+                grp.encode(0, gc, x)
+                grp.launch()
             grp.fetch()
             y = grp.decode(0, gc)
             dt = time.perf_counter() - t
@@ -549,7 +564,8 @@ class _Bench:
             native().gpu_table_cache_trim()
         ts = sorted(times)
         return dict(latency_b1_ms=round(float(np.median(ts)), 3), min_ms=round(ts[0], 3), max_ms=round(ts[-1], 3),
-                    gcs=n, fresh_gc_per_inference=True, verified=ok)
+                    gcs=n, fresh_gc_per_inference=True, verified=ok,
+                    input_encoding="device" if dev_enc else "host")
 
     # ---- per-rank evidence
     def rank_record(self, ms_step: float, inf_s: float, host_ms: float, B: int) -> dict:

@@ -224,6 +224,13 @@ class HipEvaluator {
         return v;
     }
     i64 input_size() const { return N0_; }
+    int device() const { return dev_; }
+    const std::vector<int>& crt() const { return crt_; }
+    // slot b's device input activations of residue j, [n_j][N0] bytes: the target of the garbler's device encoder
+    act_t* input_act(int b, int j) const {
+        DASH_CHECK(b >= 0 && b < B_ && j >= 0 && j < k_, "input slot out of range");
+        return bufs_[0].p[j] + static_cast<i64>(b) * nr_comps(crt_[j]) * N0_;
+    }
     // compressed staging (online message #1 in wire form): [B][k][N0] u128
     u128* input_slot_compressed(int b) {
         DASH_CHECK(b >= 0 && b < B_, "batch slot out of range");
@@ -1557,6 +1564,93 @@ void HipEvaluator::plan_rescale_legacy(size_t li, i64 iters, i64 N, const CrtInf
 }
 
 // ---------------------------------------------------------------------------
+// Garbler side of online message #1 on the device. The garbler's secrets for one GC's inputs (the base labels W0
+// and the offsets R_p) are placed on the evaluator's GPU once, offline; encode_into then writes the encoded input
+// W0 + x R straight into an evaluator slot's input activations (k_encode_in): only the plaintext input (8 B per
+// element) crosses PCIe, and neither side compresses, stages or decompresses a label. This is the in-process form
+// of the same-node device transport (IpcTables): the write target is the evaluator's, the labels are the
+// garbler's, and the evaluator never reads W0 or R.
+class DeviceInputEncoder {
+   public:
+    DeviceInputEncoder(const Garbler& g, int device) : dev_(device), crt_(g.crt()) {
+        const CrtLabels& W0 = g.input_base();
+        DASH_CHECK(!W0.empty() && W0.size() == crt_.size(), "DeviceInputEncoder: garble() must run first");
+        DASH_CHECK(static_cast<int>(crt_.size()) <= kMaxRes, "DeviceInputEncoder: too many residues");
+        bind_device(dev_, nullptr, "DeviceInputEncoder");
+        N_ = W0[0].N;
+        size_t total = 0;
+        for (const Labels& L : W0) {
+            DASH_CHECK(L.p <= kActMaxModulus, "DeviceInputEncoder: modulus above the byte activations");
+            total += static_cast<size_t>(L.n) * (N_ + 1);
+        }
+        std::vector<act_t> h(total);
+        size_t off = 0;
+        a_.k = static_cast<int>(crt_.size());
+        std::vector<size_t> w_off(crt_.size()), r_off(crt_.size());
+        for (size_t j = 0; j < crt_.size(); ++j) {
+            const Labels& L = W0[j];
+            const comp_t* R = g.offsets().get(L.p);
+            a_.p[j] = L.p;
+            a_.n[j] = L.n;
+            w_off[j] = off;
+            for (int c = 0; c < L.n; ++c)
+                for (i64 e = 0; e < N_; ++e) h[off + static_cast<size_t>(c) * N_ + e] = static_cast<act_t>(L.c[e * L.n + c]);
+            off += static_cast<size_t>(L.n) * N_;
+            r_off[j] = off;
+            for (int c = 0; c < L.n; ++c) h[off + c] = static_cast<act_t>(R[c]);
+            off += L.n;
+        }
+        HIPCHECK(hipMalloc(reinterpret_cast<void**>(&w_), total));
+        HIPCHECK(hipMemcpy(w_, h.data(), total, hipMemcpyHostToDevice));
+        for (size_t j = 0; j < crt_.size(); ++j) {
+            a_.w0[j] = w_ + w_off[j];
+            a_.r[j] = w_ + r_off[j];
+        }
+        HIPCHECK(hipHostMalloc(reinterpret_cast<void**>(&x_h_), sizeof(int64_t) * N_));
+        HIPCHECK(hipMalloc(reinterpret_cast<void**>(&x_d_), sizeof(int64_t) * N_));
+        HIPCHECK(hipEventCreateWithFlags(&done_, hipEventDisableTiming));
+    }
+    ~DeviceInputEncoder() {
+        (void)hipSetDevice(dev_);
+        if (pending_) (void)hipEventSynchronize(done_);
+        (void)hipEventDestroy(done_);
+        (void)hipFree(w_);
+        (void)hipFree(x_d_);
+        (void)hipHostFree(x_h_);
+    }
+    DeviceInputEncoder(const DeviceInputEncoder&) = delete;
+    DeviceInputEncoder& operator=(const DeviceInputEncoder&) = delete;
+    i64 input_size() const { return N_; }
+    // x (N plaintext inputs) -> slot b of h, async on st (ordered before h.run on the same stream)
+    void encode_into(HipEvaluator& h, int b, const i64* x, i64 N, hipStream_t st) {
+        DASH_CHECK(N == N_ && h.input_size() == N_, "DeviceInputEncoder: input size mismatch");
+        DASH_CHECK(h.crt() == crt_, "DeviceInputEncoder: the evaluator's CRT base differs from the garbler's");
+        DASH_CHECK(h.device() == dev_, "DeviceInputEncoder: the evaluator lives on another device");
+        bind_device(dev_, st, "DeviceInputEncoder.encode_into");
+        if (pending_) HIPCHECK(hipEventSynchronize(done_));  // the previous H2D has read the pinned staging
+        std::memcpy(x_h_, x, sizeof(int64_t) * N_);
+        HIPCHECK(hipMemcpyAsync(x_d_, x_h_, sizeof(int64_t) * N_, hipMemcpyHostToDevice, st));
+        EncIn a = a_;
+        for (int j = 0; j < a.k; ++j) a.out[j] = h.input_act(b, j);
+        launch_encode_in(a, x_d_, N_, st);
+        HIPCHECK(hipGetLastError());
+        HIPCHECK(hipEventRecord(done_, st));
+        pending_ = true;
+    }
+
+   private:
+    int dev_;
+    std::vector<int> crt_;
+    i64 N_ = 0;
+    EncIn a_{};
+    act_t* w_ = nullptr;
+    int64_t* x_h_ = nullptr;
+    int64_t* x_d_ = nullptr;
+    hipEvent_t done_ = nullptr;
+    bool pending_ = false;
+};
+
+// ---------------------------------------------------------------------------
 namespace {
 py::list labels_to_py2(const CrtLabels& L) {
     py::list out;
@@ -1594,6 +1688,13 @@ void register_hip_bindings(py::module_& m) {
         py::gil_scoped_release rel;
         g.encode_compressed(xp, N, dst);
     });
+    py::class_<DeviceInputEncoder>(m, "DeviceInputEncoder")
+        .def(py::init<const Garbler&, int>(), py::arg("garbler"), py::arg("device"))
+        .def("input_size", &DeviceInputEncoder::input_size)
+        .def("encode_into", [](DeviceInputEncoder& enc, HipEvaluator& h, int b,
+                               py::array_t<i64, py::array::c_style | py::array::forcecast> x, uintptr_t stream) {
+            enc.encode_into(h, b, x.data(), x.size(), as_stream(stream));
+        }, py::arg("evaluator"), py::arg("slot"), py::arg("x"), py::arg("stream") = 0);
     // in-process two-party fast path: the garbler encodes straight into the
     // evaluator's pinned staging slot (the bytes are exactly online message #1)
     m.def("encode_into", [](const Garbler& g, py::array_t<i64, py::array::c_style | py::array::forcecast> x,

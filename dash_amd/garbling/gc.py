@@ -169,6 +169,12 @@ class GarbledCircuit:
         assert x.size == self.circuit.input_size, "input dimension does not match circuit input dimension"
         return self.garbler.encode_cm(x)
 
+    def device_input_encoder(self, device: int):
+        """The garbler's input-encoding state (base labels W0, offsets R) of this GC on GPU `device`, placed once
+        (offline): ``HipEvaluator.encode_device_into(b, enc, x)`` then writes online message #1 for x straight
+        into an evaluator slot on that device (no host label work, only x crosses PCIe)."""
+        return self._n.DeviceInputEncoder(self.garbler, int(device))
+
     def garble_inputs_compressed(self, x: np.ndarray) -> np.ndarray:
         """Online message #1 in wire form: (k, N, 2) uint64, one 16-B compressed label per residue."""
         x = np.asarray(x, dtype=np.int64).reshape(-1)

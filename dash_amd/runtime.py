@@ -100,6 +100,13 @@ class HipEvaluator:
 
         native().encode_into(gc.garbler, np.asarray(x, dtype=np.int64).reshape(-1), self._h, b)
 
+    def encode_device_into(self, b: int, encoder, x, stream=None) -> None:
+        """Online message #1 on the device: the garbler's encoder (GarbledCircuit.device_input_encoder) writes
+        W0 + x R into slot b's input activations, async on `stream` (run() on the same stream follows it)."""
+        import numpy as np
+
+        encoder.encode_into(self._h, b, np.asarray(x, dtype=np.int64).reshape(-1), _stream_handle(stream))
+
     def set_input_compressed(self, b: int, labels) -> None:
         """Stage compressed input labels ((k, N, 2) uint64, GarbledCircuit.garble_inputs_compressed)."""
         self._h.set_input_compressed(b, labels)

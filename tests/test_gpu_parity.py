@@ -318,6 +318,41 @@ def test_graph_replay_matches_eager():
             np.testing.assert_array_equal(ev.decode(b, g), g.plain_q_eval(xs[2 * r + b]))
 
 
+def test_device_input_encoder():
+    """Online message #1 written on the device by the garbler's encoder (k_encode_in) decodes like the host-encoded
+    wire form, across graph replays on a side stream, for a host- and a GPU-garbled GC."""
+    import torch
+
+    from dash_amd.models import build_circuit, quantized_inputs
+    from dash_amd.ir.quant import QuantizationMethod as Q
+
+    c = build_circuit("MODEL_B_POOL_REPL", Q.ScaleQuant, 3, seed=4)
+    xs = quantized_inputs("MODEL_B_POOL_REPL", 6, Q.ScaleQuant, 3)
+    gcs = [GarbledCircuit(c, 8, 100.0, seed=bytes([50]) * 16),
+           GarbledCircuit(c, 8, 100.0, seed=bytes([51]) * 16, device=0)]
+    ev = _hip([g.model for g in gcs])
+    encs = [g.device_input_encoder(0) for g in gcs]
+    assert encs[0].input_size() == c.input_size
+    st = torch.cuda.Stream()
+    for r in range(3):
+        for b, enc in enumerate(encs):
+            ev.encode_device_into(b, enc, xs[2 * r + b], st)
+        ev.run(st)
+        ev.fetch_outputs(st)
+        for b, g in enumerate(gcs):
+            np.testing.assert_array_equal(ev.decode(b, g), g.plain_q_eval(xs[2 * r + b]))
+    # the host wire path on the same slots still agrees (the encoder left no state in the evaluator)
+    for b, g in enumerate(gcs):
+        ev.encode_compressed_into(b, g, xs[b])
+    ev.upload_inputs_compressed(st)
+    ev.run(st)
+    ev.fetch_outputs(st)
+    for b, g in enumerate(gcs):
+        np.testing.assert_array_equal(ev.decode(b, g), g.plain_q_eval(xs[b]))
+    with pytest.raises(Exception, match="size"):
+        ev.encode_device_into(0, encs[0], xs[0][:-1], st)
+
+
 def test_projection_shortcut_in_src():
     from tests.test_garbled_layers import _shortcut_block
 
