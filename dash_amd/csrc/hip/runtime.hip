@@ -1578,45 +1578,59 @@ class DeviceInputEncoder {
         DASH_CHECK(static_cast<int>(crt_.size()) <= kMaxRes, "DeviceInputEncoder: too many residues");
         bind_device(dev_, nullptr, "DeviceInputEncoder");
         N_ = W0[0].N;
-        size_t total = 0;
-        for (const Labels& L : W0) {
-            DASH_CHECK(L.p <= kActMaxModulus, "DeviceInputEncoder: modulus above the byte activations");
-            total += static_cast<size_t>(L.n) * (N_ + 1);
-        }
-        std::vector<act_t> h(total);
-        size_t off = 0;
         a_.k = static_cast<int>(crt_.size());
-        std::vector<size_t> w_off(crt_.size()), r_off(crt_.size());
+        size_t off = 0;
         for (size_t j = 0; j < crt_.size(); ++j) {
             const Labels& L = W0[j];
-            const comp_t* R = g.offsets().get(L.p);
+            DASH_CHECK(L.p <= kActMaxModulus, "DeviceInputEncoder: modulus above the byte activations");
             a_.p[j] = L.p;
             a_.n[j] = L.n;
-            w_off[j] = off;
-            for (int c = 0; c < L.n; ++c)
-                for (i64 e = 0; e < N_; ++e) h[off + static_cast<size_t>(c) * N_ + e] = static_cast<act_t>(L.c[e * L.n + c]);
+            w_off_.push_back(off);
             off += static_cast<size_t>(L.n) * N_;
-            r_off[j] = off;
-            for (int c = 0; c < L.n; ++c) h[off + c] = static_cast<act_t>(R[c]);
+            r_off_.push_back(off);
             off += L.n;
         }
-        HIPCHECK(hipMalloc(reinterpret_cast<void**>(&w_), total));
-        HIPCHECK(hipMemcpy(w_, h.data(), total, hipMemcpyHostToDevice));
+        bytes_ = off;
+        HIPCHECK(hipMalloc(reinterpret_cast<void**>(&w_), bytes_));
+        HIPCHECK(hipHostMalloc(reinterpret_cast<void**>(&w_h_), bytes_));
         for (size_t j = 0; j < crt_.size(); ++j) {
-            a_.w0[j] = w_ + w_off[j];
-            a_.r[j] = w_ + r_off[j];
+            a_.w0[j] = w_ + w_off_[j];
+            a_.r[j] = w_ + r_off_[j];
         }
         HIPCHECK(hipHostMalloc(reinterpret_cast<void**>(&x_h_), sizeof(int64_t) * N_));
         HIPCHECK(hipMalloc(reinterpret_cast<void**>(&x_d_), sizeof(int64_t) * N_));
         HIPCHECK(hipEventCreateWithFlags(&done_, hipEventDisableTiming));
+        HIPCHECK(hipStreamCreateWithFlags(&st_, hipStreamNonBlocking));
+        load(g);
     }
     ~DeviceInputEncoder() {
         (void)hipSetDevice(dev_);
         if (pending_) (void)hipEventSynchronize(done_);
+        (void)hipStreamSynchronize(st_);
+        (void)hipStreamDestroy(st_);
         (void)hipEventDestroy(done_);
         (void)hipFree(w_);
         (void)hipFree(x_d_);
         (void)hipHostFree(x_h_);
+        (void)hipHostFree(w_h_);
+    }
+    // re-arm for another GC of the same circuit and base (a serving slot's next GC): the base labels and offsets
+    // of g replace the current ones (after the last encode has read them), synchronously on a private stream
+    void load(const Garbler& g) {
+        const CrtLabels& W0 = g.input_base();
+        DASH_CHECK(g.crt() == crt_ && !W0.empty() && W0[0].N == N_, "DeviceInputEncoder: another circuit or base");
+        bind_device(dev_, nullptr, "DeviceInputEncoder.load");
+        if (pending_) HIPCHECK(hipEventSynchronize(done_));
+        for (size_t j = 0; j < crt_.size(); ++j) {
+            const Labels& L = W0[j];
+            const comp_t* R = g.offsets().get(L.p);
+            act_t* w = w_h_ + w_off_[j];
+            for (i64 e = 0; e < N_; ++e)
+                for (int c = 0; c < L.n; ++c) w[static_cast<size_t>(c) * N_ + e] = static_cast<act_t>(L.c[e * L.n + c]);
+            for (int c = 0; c < L.n; ++c) w_h_[r_off_[j] + c] = static_cast<act_t>(R[c]);
+        }
+        HIPCHECK(hipMemcpyAsync(w_, w_h_, bytes_, hipMemcpyHostToDevice, st_));
+        HIPCHECK(hipStreamSynchronize(st_));
     }
     DeviceInputEncoder(const DeviceInputEncoder&) = delete;
     DeviceInputEncoder& operator=(const DeviceInputEncoder&) = delete;
@@ -1643,7 +1657,11 @@ class DeviceInputEncoder {
     std::vector<int> crt_;
     i64 N_ = 0;
     EncIn a_{};
+    std::vector<size_t> w_off_, r_off_;
+    size_t bytes_ = 0;
     act_t* w_ = nullptr;
+    act_t* w_h_ = nullptr;
+    hipStream_t st_ = nullptr;
     int64_t* x_h_ = nullptr;
     int64_t* x_d_ = nullptr;
     hipEvent_t done_ = nullptr;
@@ -1691,6 +1709,7 @@ void register_hip_bindings(py::module_& m) {
     py::class_<DeviceInputEncoder>(m, "DeviceInputEncoder")
         .def(py::init<const Garbler&, int>(), py::arg("garbler"), py::arg("device"))
         .def("input_size", &DeviceInputEncoder::input_size)
+        .def("load", &DeviceInputEncoder::load, py::arg("garbler"), py::call_guard<py::gil_scoped_release>())
         .def("encode_into", [](DeviceInputEncoder& enc, HipEvaluator& h, int b,
                                py::array_t<i64, py::array::c_style | py::array::forcecast> x, uintptr_t stream) {
             enc.encode_into(h, b, x.data(), x.size(), as_stream(stream));

@@ -165,6 +165,7 @@ class _Group:
         self.slots = slots
         self.ev = None          # HipEvaluator (hip backend)
         self.gcs: list = [None] * slots
+        self.encs: list = [None] * slots  # per slot the garbler's device input encoder (input_encoding="device")
         self.ready = threading.Event()
         self.stream = None
         self.runs = 0           # evaluations so far (run 2 captures the hipGraph)
@@ -190,7 +191,8 @@ class InferenceService:
                  step_timeout_s: float = 120.0, seed: Optional[bytes] = None, prefetch: bool = True,
                  fault_hook: Optional[Callable[[int, int], bool]] = None, nthreads: int = 0,
                  rescale: str = "auto", relu: str = "auto", fused_sign: bool = True,
-                 insecure_fixed_seed: bool = False, garble_workers: Optional[int] = None):
+                 insecure_fixed_seed: bool = False, garble_workers: Optional[int] = None,
+                 input_encoding: Optional[str] = None):
         if backend not in ("hip", "cpu"):
             raise ValueError("backend must be 'hip' or 'cpu'")
         if seed is not None and not insecure_fixed_seed:
@@ -202,6 +204,12 @@ class InferenceService:
         self.circuit, self.crt, self.mrs, self.max_modulus = circuit, crt, mrs, max_modulus
         self.backend, self.device = backend, device
         self.garble_device = (backend == "hip") if garble_device is None else bool(garble_device)
+        # online message #1: "device" = the garbler's device encoder writes each slot's input labels on the GPU
+        # (GarbledCircuit.device_input_encoder, re-armed per GC); "host" = compressed labels + H2D + GPU unpack
+        enc = input_encoding or os.environ.get("DASH_SERVE_INPUT_ENCODING", "device")
+        if enc not in ("device", "host"):
+            raise ValueError("input_encoding must be 'device' or 'host'")
+        self.device_encode = backend == "hip" and enc == "device"
         self.max_retries, self.step_timeout_s = max_retries, step_timeout_s
         self.fault_hook = fault_hook
         self.nthreads = nthreads
@@ -294,6 +302,11 @@ class InferenceService:
                 gc = self._new_gc(g.ev.sink(b))
             g.ev.load(b, gc.model)
             gc.model = None  # tables live in HBM now
+            if self.device_encode:  # the garbler's input state of this GC to the GPU (offline, with its tables)
+                if g.encs[b] is None:
+                    g.encs[b] = gc.device_input_encoder(self.device)
+                else:
+                    g.encs[b].load(gc.garbler)
         else:
             gc = self._new_gc()
         g.gcs[b] = gc
@@ -363,9 +376,13 @@ class InferenceService:
         t = time.perf_counter()
         if self.backend == "hip":
             ev = g.ev
-            for b in range(len(xs)):  # unused slots are not encoded (see _release)
-                ev.encode_compressed_into(b, g.gcs[b], xs[b])
-            ev.upload_inputs_compressed(g.stream)
+            if self.device_encode:
+                for b in range(len(xs)):  # unused slots are not encoded (see _release)
+                    ev.encode_device_into(b, g.encs[b], xs[b], g.stream)
+            else:
+                for b in range(len(xs)):
+                    ev.encode_compressed_into(b, g.gcs[b], xs[b])
+                ev.upload_inputs_compressed(g.stream)
             ev.run(g.stream)  # graph replay: captured in _prime_graphs
             g.runs += 1
             try:

@@ -123,10 +123,12 @@ def _timeout_worker(rank, world, port):
 
 
 @pytest.mark.gpu
-def test_service_hip_matches_plaintext_and_recovers(small):
+@pytest.mark.parametrize("enc", ["device", "host"])
+def test_service_hip_matches_plaintext_and_recovers(small, enc):
     c, xs = small
     with InferenceService(c, 8, 100.0, backend="hip", slots_per_group=2, groups=2, device=0, seed=b"h" * 16, insecure_fixed_seed=True,
-                          fault_hook=lambda i, a: i == 2 and a == 0, step_timeout_s=60) as svc:
+                          fault_hook=lambda i, a: i == 2 and a == 0, step_timeout_s=60, input_encoding=enc) as svc:
+        assert svc.device_encode == (enc == "device")
         y = svc.infer(xs)
         st = svc.stats.as_dict()
     np.testing.assert_array_equal(y, _ref(c, xs))
