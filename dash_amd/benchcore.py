@@ -110,10 +110,10 @@ def parse_args(argv=None) -> argparse.Namespace:
     ap.add_argument("--thread-sweep", default="4,8",
                     help="host thread budgets of the threads phase (headline loop re-timed at each)")
     ap.add_argument("--latency-gcs", type=int, default=8, help="fresh GCs timed one by one in the latency phase")
-    ap.add_argument("--latency-encode", default=os.environ.get("DASH_BENCH_LATENCY_ENCODE", "device"),
+    ap.add_argument("--input-encoding", default=os.environ.get("DASH_BENCH_INPUT_ENCODING", "device"),
                     choices=["device", "host"],
-                    help="latency phase, online message #1: the garbler's device encoder (GarbledCircuit."
-                         "device_input_encoder) or host-encoded compressed labels + H2D + GPU unpack")
+                    help="online message #1 (hip): the garbler's device encoder (GarbledCircuit.device_input_encoder,"
+                         " one launch per group) or host-encoded compressed labels + H2D + GPU unpack")
     ap.add_argument("--ref-batch", type=int, default=0, help="GCs per GPU of the reference phase (0: auto)")
     ap.add_argument("--ref-steps", type=int, default=0, help="timed steps of the reference phase (0: --steps)")
     ap.add_argument("--served-slots", type=int, default=16)
@@ -205,29 +205,45 @@ def check_world(args, ctx, recs: list, rehearsal: bool) -> None:
 
 # ----------------------------------------------------------------------------------------- evaluator slots
 class _HipGroup:
-    """``per`` GC slots evaluated together by one HipEvaluator on one stream."""
+    """``per`` GC slots evaluated together by one HipEvaluator on one stream.
 
-    def __init__(self, template, per: int, device: int, mfma: bool, profile: bool, stream):
+    Online message #1 (``device_encode``): the garbler's device input encoder of the group (one encoder slot per
+    GC slot, armed when the GC is loaded, offline) writes every slot's input labels with one H2D of the plaintext
+    inputs and one launch; otherwise the host encodes 16-B compressed labels (a reused GC's codebook lookup) that
+    are copied to the GPU and unpacked there."""
+
+    def __init__(self, template, per: int, device: int, mfma: bool, profile: bool, stream, device_encode=False):
         from .runtime import HipEvaluator
 
         self.ev = HipEvaluator(template=template, batch=per, device=device, mfma=mfma, profile=profile)
         self.stream = stream
+        self.per, self.device = per, device
+        self.device_encode = device_encode
+        self.enc = None
 
     def load(self, b, gc):
         self.ev.load(b, gc.model)  # a GC garbled into this slot (sink) only copies its small constants
         gc.model = None  # tables live in HBM now
+        if self.device_encode:  # the garbler's input state of this GC to the GPU (offline, with its tables)
+            if self.enc is None:
+                self.enc = gc.device_input_encoder(self.device, self.per)
+                if b != 0:
+                    self.enc.load(gc.garbler, b)
+            else:
+                self.enc.load(gc.garbler, b)
 
     def sink(self, b):
         return self.ev.sink(b)
 
-    def encode(self, b, gc, x):
-        self.ev.encode_compressed_into(b, gc, x)
+    def encode_batch(self, gcs, xs):
+        if self.device_encode:
+            self.ev.encode_device_into(0, self.enc, np.stack([np.asarray(x).reshape(-1) for x in xs]), self.stream)
+        else:
+            for b, (gc, x) in enumerate(zip(gcs, xs)):
+                self.ev.encode_compressed_into(b, gc, x)
 
-    def encode_device(self, b, enc, x):
-        self.ev.encode_device_into(b, enc, x, self.stream)
-
-    def launch(self, upload: bool = True):
-        if upload:
+    def launch(self):
+        if not self.device_encode:
             self.ev.upload_inputs_compressed(self.stream)
         self.ev.run(self.stream)
 
@@ -253,8 +269,9 @@ class _CpuGroup:
     def sink(self, b):
         return None
 
-    def encode(self, b, gc, x):
-        self.inputs[b] = gc.garble_inputs(x)
+    def encode_batch(self, gcs, xs):
+        for b, (gc, x) in enumerate(zip(gcs, xs)):
+            self.inputs[b] = gc.garble_inputs(x)
 
     def launch(self):
         for b, gc in enumerate(self.models):
@@ -285,6 +302,7 @@ class _Bench:
 
         self.circuit.calibrate(quantized_inputs(self.model, 32, self.qm, self.qp, seed=0), svc_modulus(cfg["crt"]))
         self.hip = args.backend == "hip"
+        self.device_encode = self.hip and getattr(args, "input_encoding", "device") == "device"
         self.device = ctx.device if (self.hip and ctx.device is not None) else 0
         if self.hip:
             import torch
@@ -328,7 +346,8 @@ class _Bench:
                 from .native import native
 
                 native().gpu_table_cache_trim()  # the new group's table arena needs the garbler's cached blocks
-                return _HipGroup(gc.model, per_, self.device, not args.no_mfma, args.profile, streams[g])
+                return _HipGroup(gc.model, per_, self.device, not args.no_mfma, args.profile, streams[g],
+                                 device_encode=self.device_encode)
             return _CpuGroup(gc.model, per_, self.threads)
 
         b = 0
@@ -420,8 +439,7 @@ class _Bench:
             # the G groups run concurrently on their own streams
             for g, grp in enumerate(groups):
                 t = time.perf_counter()
-                for b in range(per):
-                    grp.encode(b, gcs[g * per + b], xs[g * per + b])
+                grp.encode_batch(gcs[g * per:(g + 1) * per], xs[g * per:(g + 1) * per])
                 host[0] += time.perf_counter() - t
                 grp.launch()
             dec = []
@@ -524,7 +542,6 @@ class _Bench:
 
         n = max(2, self.args.latency_gcs)
         xs = quantized_inputs(self.model, n, self.qm, self.qp, seed=7000 + self.ctx.rank)
-        dev_enc = self.hip and getattr(self.args, "latency_encode", "device") == "device"
         ev, grp, times, ok = None, None, [], True
         for i in range(n + 1):  # one untimed warm-up GC (first launch, graph build)
             if self.hip:
@@ -533,24 +550,19 @@ class _Bench:
                     from .native import native
 
                     native().gpu_table_cache_trim()
-                    grp = _HipGroup(gc.model, 1, self.device, not self.args.no_mfma, False, None)
+                    grp = _HipGroup(gc.model, 1, self.device, not self.args.no_mfma, False, None,
+                                    device_encode=self.device_encode)
                 else:
                     gc = self.garble("lat", i, cons, sink=grp.sink(0))
             else:
                 gc = self.garble("lat", i, cons)
                 grp = grp or _CpuGroup(gc.model, 1, self.threads)
             grp.load(0, gc)
-            # device encoding: the garbler's input state of this GC goes to the GPU with its tables (offline)
-            enc = gc.device_input_encoder(self.device) if dev_enc else None
             x = xs[max(0, i - 1)]
             self.sync()
             t = time.perf_counter()
-            if enc is not None:
-                grp.encode_device(0, enc, x)
-                grp.launch(upload=False)
-            else:
-                grp.encode(0, gc, x)
-                grp.launch()
+            grp.encode_batch([gc], [x])
+            grp.launch()
             grp.fetch()
             y = grp.decode(0, gc)
             dt = time.perf_counter() - t
@@ -565,7 +577,7 @@ class _Bench:
         ts = sorted(times)
         return dict(latency_b1_ms=round(float(np.median(ts)), 3), min_ms=round(ts[0], 3), max_ms=round(ts[-1], 3),
                     gcs=n, fresh_gc_per_inference=True, verified=ok,
-                    input_encoding="device" if dev_enc else "host")
+                    input_encoding="device" if self.device_encode else "host")
 
     # ---- per-rank evidence
     def rank_record(self, ms_step: float, inf_s: float, host_ms: float, B: int) -> dict:
@@ -747,10 +759,14 @@ def run(argv=None) -> Optional[dict]:
             # the headline's GCs are garbled once and re-encoded every step: an online-phase rate (a step's
             # work equals that of fresh GCs); served_inf_per_s is the protocol-valid fresh-GC rate
             "gc_reuse": True,
-            "gc_reuse_note": ("the timed steps re-encode fresh inputs under GCs garbled once (a reused GC also "
-                              "builds a per-GC input codebook on its second encode, host_encode_decode_ms_per_step); "
-                              "GCs are single use in the protocol: served_inf_per_s (fresh GC per inference, "
+            "gc_reuse_note": ("the timed steps re-encode fresh inputs under GCs garbled once; "
+                              + ("online message #1 comes from the garbler's device encoder (W0 + x R per label, "
+                                 "the same work for a fresh GC; no codebook)" if bench.device_encode else
+                                 "a reused GC also builds a per-GC input codebook on its second encode "
+                                 "(host_encode_decode_ms_per_step)")
+                              + "; GCs are single use in the protocol: served_inf_per_s (fresh GC per inference, "
                               "garbling included) and latency_b1_ms (fresh GC, batch 1) measure that"),
+            "input_encoding": "device" if bench.device_encode else "host",
             "vs_baseline_note": ("value / (1 / 1.443 s): batched throughput over the reference's batch-1 latency; "
                                  "latency_b1_ms against 1443 ms is the like-for-like comparison"),
             "dist_backend": ctx.backend if ctx.distributed else "none",

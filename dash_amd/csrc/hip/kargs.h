@@ -33,14 +33,16 @@ struct CrtInfo {
     int sum;
 };
 
-// Garbler-side input encoding on the device (k_encode_in): out_j[c][e] = W0_j[c][e] + (x[e] mod p_j) R_j[c] mod p_j
+// Garbler-side input encoding on the device (k_encode_in), per slot s:
+// out_j[s][c][e] = W0_j[s][c][e] + (x[s][e] mod p_j) R_j[s][c] mod p_j
 struct EncIn {
     int k;
     int p[kMaxRes];
     int n[kMaxRes];
     const act_t* w0[kMaxRes];  // [n_j][N] component-major input base labels
     const act_t* r[kMaxRes];   // [n_j] the offset R_{p_j}
-    act_t* out[kMaxRes];       // [n_j][N] an evaluator slot's input activations
+    act_t* out[kMaxRes];       // [n_j][N] an evaluator slot's input activations (slot s + 1 follows n_j N later)
+    int64_t wstride;           // bytes between the encoder slots' W0 / R blocks (grid z = slot)
 };
 
 struct SignArgs {

@@ -237,27 +237,29 @@ void launch_narrow(const int16_t* in, act_t* out, int64_t n, hipStream_t st) {
 }
 
 // Online message #1 encoded on the device by the garbler (core.h lab_affine per component, reference
-// garbled_circuit_interface.h garble_inputs): grid (ceil(N / 256), k), one lane per (element, residue). The n_j
-// components of a label are strided by N (component-major), so every component step is one coalesced byte row.
+// garbled_circuit_interface.h garble_inputs): grid (ceil(N / 256), k, slots), one lane per (element, residue,
+// slot). The n_j components of a label are strided by N (component-major), so every component step is one
+// coalesced byte row.
 __global__ __launch_bounds__(256) void k_encode_in(EncIn a, const int64_t* __restrict__ x, int64_t N) {
-    const int j = blockIdx.y;
+    const int j = blockIdx.y, s = blockIdx.z;
     const int64_t e = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
     if (e >= N) return;
     const int p = a.p[j], n = a.n[j];
-    int64_t v64 = x[e] % p;
+    int64_t v64 = x[static_cast<int64_t>(s) * N + e] % p;
     const uint32_t v = static_cast<uint32_t>(v64 < 0 ? v64 + p : v64);
     const uint32_t up = static_cast<uint32_t>(p);
-    const act_t* __restrict__ w = a.w0[j] + e;
-    const act_t* __restrict__ r = a.r[j];
-    act_t* __restrict__ o = a.out[j] + e;
+    const act_t* __restrict__ w = a.w0[j] + s * a.wstride + e;
+    const act_t* __restrict__ r = a.r[j] + s * a.wstride;
+    act_t* __restrict__ o = a.out[j] + static_cast<int64_t>(s) * n * N + e;
     for (int c = 0; c < n; ++c) {
         const uint32_t t = static_cast<uint32_t>(w[c * N]) + v * static_cast<uint32_t>(r[c]);  // < p + p^2 < 2^17
         o[c * N] = static_cast<act_t>(t % up);
     }
 }
-void launch_encode_in(const EncIn& a, const int64_t* x, int64_t N, hipStream_t st) {
-    hipLaunchKernelGGL(k_encode_in, dim3(static_cast<unsigned>((N + 255) / 256), static_cast<unsigned>(a.k)), dim3(256), 0,
-                       st, a, x, N);
+void launch_encode_in(const EncIn& a, const int64_t* x, int64_t N, int slots, hipStream_t st) {
+    hipLaunchKernelGGL(k_encode_in,
+                       dim3(static_cast<unsigned>((N + 255) / 256), static_cast<unsigned>(a.k), static_cast<unsigned>(slots)),
+                       dim3(256), 0, st, a, x, N);
 }
 
 static inline dim3 grid_tr(int64_t rows, int64_t cols) {

@@ -286,7 +286,7 @@ inline std::vector<int8_t> conv_w8r(const ConvArgs& a, const std::vector<int8_t>
 // int16 matrix transpose out[c][r] = in[r][c] (label-major <-> component-major), kernels_label.hip
 void launch_transpose16(const int16_t* in, int16_t* out, int64_t rows, int64_t cols, hipStream_t st);
 void launch_narrow(const int16_t* in, act_t* out, int64_t n, hipStream_t st);  // int16 labels -> byte activations
-void launch_encode_in(const EncIn& a, const int64_t* x, int64_t N, hipStream_t st);  // garbler: W0 + x R -> slot
+void launch_encode_in(const EncIn& a, const int64_t* x, int64_t N, int slots, hipStream_t st);  // garbler: W0 + x R
 void launch_transpose_to_act(const int16_t* in, act_t* out, int64_t rows, int64_t cols, hipStream_t st);
 void launch_transpose_from_act(const act_t* in, int16_t* out, int64_t rows, int64_t cols, hipStream_t st);
 // the same for every residue of a label set in one launch (grid z = residue): matrix j is rows[j] x cols[j]

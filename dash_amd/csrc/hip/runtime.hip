@@ -1564,16 +1564,18 @@ void HipEvaluator::plan_rescale_legacy(size_t li, i64 iters, i64 N, const CrtInf
 }
 
 // ---------------------------------------------------------------------------
-// Garbler side of online message #1 on the device. The garbler's secrets for one GC's inputs (the base labels W0
-// and the offsets R_p) are placed on the evaluator's GPU once, offline; encode_into then writes the encoded input
+// Garbler side of online message #1 on the device. The garbler's secrets for a GC's inputs (the base labels W0
+// and the offsets R_p) are placed on the evaluator's GPU once, offline; encode then writes the encoded input
 // W0 + x R straight into an evaluator slot's input activations (k_encode_in): only the plaintext input (8 B per
 // element) crosses PCIe, and neither side compresses, stages or decompresses a label. This is the in-process form
 // of the same-node device transport (IpcTables): the write target is the evaluator's, the labels are the
-// garbler's, and the evaluator never reads W0 or R.
+// garbler's, and the evaluator never reads W0 or R. An encoder holds `slots` GCs (one per evaluator slot of a
+// group): encode_all writes all of them with one H2D and one launch.
 class DeviceInputEncoder {
    public:
-    DeviceInputEncoder(const Garbler& g, int device) : dev_(device), crt_(g.crt()) {
+    DeviceInputEncoder(const Garbler& g, int device, int slots) : dev_(device), S_(slots), crt_(g.crt()) {
         const CrtLabels& W0 = g.input_base();
+        DASH_CHECK(S_ >= 1, "DeviceInputEncoder: slots must be >= 1");
         DASH_CHECK(!W0.empty() && W0.size() == crt_.size(), "DeviceInputEncoder: garble() must run first");
         DASH_CHECK(static_cast<int>(crt_.size()) <= kMaxRes, "DeviceInputEncoder: too many residues");
         bind_device(dev_, nullptr, "DeviceInputEncoder");
@@ -1590,18 +1592,20 @@ class DeviceInputEncoder {
             r_off_.push_back(off);
             off += L.n;
         }
-        bytes_ = off;
-        HIPCHECK(hipMalloc(reinterpret_cast<void**>(&w_), bytes_));
+        bytes_ = (off + 15) & ~size_t(15);
+        a_.wstride = static_cast<int64_t>(bytes_);
+        HIPCHECK(hipMalloc(reinterpret_cast<void**>(&w_), bytes_ * S_));
         HIPCHECK(hipHostMalloc(reinterpret_cast<void**>(&w_h_), bytes_));
         for (size_t j = 0; j < crt_.size(); ++j) {
             a_.w0[j] = w_ + w_off_[j];
             a_.r[j] = w_ + r_off_[j];
         }
-        HIPCHECK(hipHostMalloc(reinterpret_cast<void**>(&x_h_), sizeof(int64_t) * N_));
-        HIPCHECK(hipMalloc(reinterpret_cast<void**>(&x_d_), sizeof(int64_t) * N_));
+        HIPCHECK(hipHostMalloc(reinterpret_cast<void**>(&x_h_), sizeof(int64_t) * N_ * S_));
+        HIPCHECK(hipMalloc(reinterpret_cast<void**>(&x_d_), sizeof(int64_t) * N_ * S_));
         HIPCHECK(hipEventCreateWithFlags(&done_, hipEventDisableTiming));
         HIPCHECK(hipStreamCreateWithFlags(&st_, hipStreamNonBlocking));
-        load(g);
+        loaded_.assign(S_, 0);
+        load(g, 0);
     }
     ~DeviceInputEncoder() {
         (void)hipSetDevice(dev_);
@@ -1614,11 +1618,18 @@ class DeviceInputEncoder {
         (void)hipHostFree(x_h_);
         (void)hipHostFree(w_h_);
     }
-    // re-arm for another GC of the same circuit and base (a serving slot's next GC): the base labels and offsets
-    // of g replace the current ones (after the last encode has read them), synchronously on a private stream
-    void load(const Garbler& g) {
+    DeviceInputEncoder(const DeviceInputEncoder&) = delete;
+    DeviceInputEncoder& operator=(const DeviceInputEncoder&) = delete;
+    i64 input_size() const { return N_; }
+    int slots() const { return S_; }
+    // (re-)arm slot s with GC g of the same circuit and base (a serving slot's next GC): its base labels and
+    // offsets replace the slot's current ones once the last encode has read them (synchronous, private stream).
+    // Concurrent loads of different slots serialize on the shared host staging.
+    void load(const Garbler& g, int s) {
         const CrtLabels& W0 = g.input_base();
+        DASH_CHECK(s >= 0 && s < S_, "DeviceInputEncoder: slot out of range");
         DASH_CHECK(g.crt() == crt_ && !W0.empty() && W0[0].N == N_, "DeviceInputEncoder: another circuit or base");
+        std::lock_guard<std::mutex> lk(load_mu_);
         bind_device(dev_, nullptr, "DeviceInputEncoder.load");
         if (pending_) HIPCHECK(hipEventSynchronize(done_));
         for (size_t j = 0; j < crt_.size(); ++j) {
@@ -1629,39 +1640,41 @@ class DeviceInputEncoder {
                 for (int c = 0; c < L.n; ++c) w[static_cast<size_t>(c) * N_ + e] = static_cast<act_t>(L.c[e * L.n + c]);
             for (int c = 0; c < L.n; ++c) w_h_[r_off_[j] + c] = static_cast<act_t>(R[c]);
         }
-        HIPCHECK(hipMemcpyAsync(w_, w_h_, bytes_, hipMemcpyHostToDevice, st_));
+        HIPCHECK(hipMemcpyAsync(w_ + bytes_ * s, w_h_, bytes_, hipMemcpyHostToDevice, st_));
         HIPCHECK(hipStreamSynchronize(st_));
+        loaded_[s] = 1;
     }
-    DeviceInputEncoder(const DeviceInputEncoder&) = delete;
-    DeviceInputEncoder& operator=(const DeviceInputEncoder&) = delete;
-    i64 input_size() const { return N_; }
-    // x (N plaintext inputs) -> slot b of h, async on st (ordered before h.run on the same stream)
-    void encode_into(HipEvaluator& h, int b, const i64* x, i64 N, hipStream_t st) {
+    // slots [0, n) <- x[n][N] into evaluator slots b0 .. b0 + n - 1, async on st (ordered before h.run on st)
+    void encode(HipEvaluator& h, int b0, const i64* x, int n, i64 N, hipStream_t st) {
         DASH_CHECK(N == N_ && h.input_size() == N_, "DeviceInputEncoder: input size mismatch");
+        DASH_CHECK(n >= 1 && n <= S_ && b0 >= 0 && b0 + n <= h.batch(), "DeviceInputEncoder: slot range mismatch");
         DASH_CHECK(h.crt() == crt_, "DeviceInputEncoder: the evaluator's CRT base differs from the garbler's");
         DASH_CHECK(h.device() == dev_, "DeviceInputEncoder: the evaluator lives on another device");
-        bind_device(dev_, st, "DeviceInputEncoder.encode_into");
+        for (int s = 0; s < n; ++s) DASH_CHECK(loaded_[s], "DeviceInputEncoder: slot " + std::to_string(s) + " has no GC");
+        bind_device(dev_, st, "DeviceInputEncoder.encode");
         if (pending_) HIPCHECK(hipEventSynchronize(done_));  // the previous H2D has read the pinned staging
-        std::memcpy(x_h_, x, sizeof(int64_t) * N_);
-        HIPCHECK(hipMemcpyAsync(x_d_, x_h_, sizeof(int64_t) * N_, hipMemcpyHostToDevice, st));
+        std::memcpy(x_h_, x, sizeof(int64_t) * N_ * n);
+        HIPCHECK(hipMemcpyAsync(x_d_, x_h_, sizeof(int64_t) * N_ * n, hipMemcpyHostToDevice, st));
         EncIn a = a_;
-        for (int j = 0; j < a.k; ++j) a.out[j] = h.input_act(b, j);
-        launch_encode_in(a, x_d_, N_, st);
+        for (int j = 0; j < a.k; ++j) a.out[j] = h.input_act(b0, j);
+        launch_encode_in(a, x_d_, N_, n, st);
         HIPCHECK(hipGetLastError());
         HIPCHECK(hipEventRecord(done_, st));
         pending_ = true;
     }
 
    private:
-    int dev_;
+    int dev_, S_;
     std::vector<int> crt_;
     i64 N_ = 0;
     EncIn a_{};
     std::vector<size_t> w_off_, r_off_;
+    std::vector<int> loaded_;
     size_t bytes_ = 0;
     act_t* w_ = nullptr;
     act_t* w_h_ = nullptr;
     hipStream_t st_ = nullptr;
+    std::mutex load_mu_;
     int64_t* x_h_ = nullptr;
     int64_t* x_d_ = nullptr;
     hipEvent_t done_ = nullptr;
@@ -1707,12 +1720,18 @@ void register_hip_bindings(py::module_& m) {
         g.encode_compressed(xp, N, dst);
     });
     py::class_<DeviceInputEncoder>(m, "DeviceInputEncoder")
-        .def(py::init<const Garbler&, int>(), py::arg("garbler"), py::arg("device"))
+        .def(py::init<const Garbler&, int, int>(), py::arg("garbler"), py::arg("device"), py::arg("slots") = 1)
         .def("input_size", &DeviceInputEncoder::input_size)
-        .def("load", &DeviceInputEncoder::load, py::arg("garbler"), py::call_guard<py::gil_scoped_release>())
-        .def("encode_into", [](DeviceInputEncoder& enc, HipEvaluator& h, int b,
+        .def("slots", &DeviceInputEncoder::slots)
+        .def("load", &DeviceInputEncoder::load, py::arg("garbler"), py::arg("slot") = 0,
+             py::call_guard<py::gil_scoped_release>())
+        // x: (N,) for one slot or (n, N) for slots 0 .. n - 1 -> evaluator slots b0 ..
+        .def("encode_into", [](DeviceInputEncoder& enc, HipEvaluator& h, int b0,
                                py::array_t<i64, py::array::c_style | py::array::forcecast> x, uintptr_t stream) {
-            enc.encode_into(h, b, x.data(), x.size(), as_stream(stream));
+            const int n = x.ndim() == 2 ? static_cast<int>(x.shape(0)) : 1;
+            const i64 N = x.ndim() == 2 ? static_cast<i64>(x.shape(1)) : static_cast<i64>(x.size());
+            DASH_CHECK(x.ndim() == 1 || x.ndim() == 2, "DeviceInputEncoder: x must be (N,) or (slots, N)");
+            enc.encode(h, b0, x.data(), n, N, as_stream(stream));
         }, py::arg("evaluator"), py::arg("slot"), py::arg("x"), py::arg("stream") = 0);
     // in-process two-party fast path: the garbler encodes straight into the
     // evaluator's pinned staging slot (the bytes are exactly online message #1)

@@ -169,11 +169,13 @@ class GarbledCircuit:
         assert x.size == self.circuit.input_size, "input dimension does not match circuit input dimension"
         return self.garbler.encode_cm(x)
 
-    def device_input_encoder(self, device: int):
+    def device_input_encoder(self, device: int, slots: int = 1):
         """The garbler's input-encoding state (base labels W0, offsets R) of this GC on GPU `device`, placed once
         (offline): ``HipEvaluator.encode_device_into(b, enc, x)`` then writes online message #1 for x straight
-        into an evaluator slot on that device (no host label work, only x crosses PCIe)."""
-        return self._n.DeviceInputEncoder(self.garbler, int(device))
+        into an evaluator slot on that device (no host label work, only x crosses PCIe). With slots > 1 the
+        encoder holds one GC per slot (this one in slot 0; ``enc.load(gc.garbler, s)`` arms slot s) and encodes
+        a (slots, N) batch of inputs into consecutive evaluator slots with one launch."""
+        return self._n.DeviceInputEncoder(self.garbler, int(device), int(slots))
 
     def garble_inputs_compressed(self, x: np.ndarray) -> np.ndarray:
         """Online message #1 in wire form: (k, N, 2) uint64, one 16-B compressed label per residue."""

@@ -102,10 +102,14 @@ class HipEvaluator:
 
     def encode_device_into(self, b: int, encoder, x, stream=None) -> None:
         """Online message #1 on the device: the garbler's encoder (GarbledCircuit.device_input_encoder) writes
-        W0 + x R into slot b's input activations, async on `stream` (run() on the same stream follows it)."""
+        W0 + x R into slot b's input activations, async on `stream` (run() on the same stream follows it).
+        x of shape (n, ...) with n > 1 rows: encoder slots 0 .. n - 1 into evaluator slots b .. b + n - 1."""
         import numpy as np
 
-        encoder.encode_into(self._h, b, np.asarray(x, dtype=np.int64).reshape(-1), _stream_handle(stream))
+        x = np.asarray(x, dtype=np.int64)
+        N = encoder.input_size()
+        x = x.reshape(-1) if x.size == N else x.reshape(-1, N)
+        encoder.encode_into(self._h, b, x, _stream_handle(stream))
 
     def set_input_compressed(self, b: int, labels) -> None:
         """Stage compressed input labels ((k, N, 2) uint64, GarbledCircuit.garble_inputs_compressed)."""

@@ -165,7 +165,7 @@ class _Group:
         self.slots = slots
         self.ev = None          # HipEvaluator (hip backend)
         self.gcs: list = [None] * slots
-        self.encs: list = [None] * slots  # per slot the garbler's device input encoder (input_encoding="device")
+        self.enc = None         # the garbler's device input encoder, one slot per GC slot (input_encoding="device")
         self.ready = threading.Event()
         self.stream = None
         self.runs = 0           # evaluations so far (run 2 captures the hipGraph)
@@ -303,10 +303,12 @@ class InferenceService:
             g.ev.load(b, gc.model)
             gc.model = None  # tables live in HBM now
             if self.device_encode:  # the garbler's input state of this GC to the GPU (offline, with its tables)
-                if g.encs[b] is None:
-                    g.encs[b] = gc.device_input_encoder(self.device)
+                if g.enc is None:  # (the first, synchronous fill) this GC is armed in encoder slot 0
+                    g.enc = gc.device_input_encoder(self.device, g.slots)
+                    if b != 0:
+                        g.enc.load(gc.garbler, b)
                 else:
-                    g.encs[b].load(gc.garbler)
+                    g.enc.load(gc.garbler, b)
         else:
             gc = self._new_gc()
         g.gcs[b] = gc
@@ -376,9 +378,8 @@ class InferenceService:
         t = time.perf_counter()
         if self.backend == "hip":
             ev = g.ev
-            if self.device_encode:
-                for b in range(len(xs)):  # unused slots are not encoded (see _release)
-                    ev.encode_device_into(b, g.encs[b], xs[b], g.stream)
+            if self.device_encode:  # unused slots are not encoded (see _release)
+                ev.encode_device_into(0, g.enc, np.stack([np.asarray(x).reshape(-1) for x in xs]), g.stream)
             else:
                 for b in range(len(xs)):
                     ev.encode_compressed_into(b, g.gcs[b], xs[b])

@@ -351,6 +351,17 @@ def test_device_input_encoder():
         np.testing.assert_array_equal(ev.decode(b, g), g.plain_q_eval(xs[b]))
     with pytest.raises(Exception, match="size"):
         ev.encode_device_into(0, encs[0], xs[0][:-1], st)
+    # one two-slot encoder (a group's): both slots with one launch; a slot never armed is refused
+    enc2 = gcs[0].device_input_encoder(0, 2)
+    with pytest.raises(Exception, match="no GC"):
+        ev.encode_device_into(0, enc2, np.stack([xs[2], xs[3]]), st)
+    enc2.load(gcs[1].garbler, 1)
+    for r in range(2):
+        ev.encode_device_into(0, enc2, np.stack([xs[2 * r], xs[2 * r + 1]]), st)
+        ev.run(st)
+        ev.fetch_outputs(st)
+        for b, g in enumerate(gcs):
+            np.testing.assert_array_equal(ev.decode(b, g), g.plain_q_eval(xs[2 * r + b]))
 
 
 def test_projection_shortcut_in_src():
