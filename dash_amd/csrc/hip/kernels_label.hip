@@ -237,28 +237,28 @@ void launch_narrow(const int16_t* in, act_t* out, int64_t n, hipStream_t st) {
 }
 
 // Online message #1 encoded on the device by the garbler (core.h lab_affine per component, reference
-// garbled_circuit_interface.h garble_inputs): grid (ceil(N / 256), k, slots), one lane per (element, residue,
-// slot). The n_j components of a label are strided by N (component-major), so every component step is one
-// coalesced byte row.
+// garbled_circuit_interface.h garble_inputs): grid (ceil(n_max N / 256), k, slots), one lane per (component,
+// element) of a residue and slot, elements fastest (coalesced byte rows of the component-major layout). A lane
+// per element looping over its n_j components was a 60 us launch at batch 1 (84 workgroups, r05 timeline).
 __global__ __launch_bounds__(256) void k_encode_in(EncIn a, const int64_t* __restrict__ x, int64_t N) {
     const int j = blockIdx.y, s = blockIdx.z;
-    const int64_t e = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-    if (e >= N) return;
     const int p = a.p[j], n = a.n[j];
+    const uint32_t t = blockIdx.x * 256u + threadIdx.x;
+    const uint32_t N32 = static_cast<uint32_t>(N);
+    const uint32_t c = t / N32, e = t - c * N32;
+    if (c >= static_cast<uint32_t>(n)) return;
     int64_t v64 = x[static_cast<int64_t>(s) * N + e] % p;
     const uint32_t v = static_cast<uint32_t>(v64 < 0 ? v64 + p : v64);
-    const uint32_t up = static_cast<uint32_t>(p);
-    const act_t* __restrict__ w = a.w0[j] + s * a.wstride + e;
-    const act_t* __restrict__ r = a.r[j] + s * a.wstride;
-    act_t* __restrict__ o = a.out[j] + static_cast<int64_t>(s) * n * N + e;
-    for (int c = 0; c < n; ++c) {
-        const uint32_t t = static_cast<uint32_t>(w[c * N]) + v * static_cast<uint32_t>(r[c]);  // < p + p^2 < 2^17
-        o[c * N] = static_cast<act_t>(t % up);
-    }
+    const uint32_t w = a.w0[j][s * a.wstride + static_cast<int64_t>(c) * N + e];
+    const uint32_t r = a.r[j][s * a.wstride + c];
+    a.out[j][(static_cast<int64_t>(s) * n + c) * N + e] = static_cast<act_t>((w + v * r) % static_cast<uint32_t>(p));
 }
 void launch_encode_in(const EncIn& a, const int64_t* x, int64_t N, int slots, hipStream_t st) {
+    int nmx = 1;
+    for (int j = 0; j < a.k; ++j) nmx = std::max(nmx, a.n[j]);
+    const int64_t lanes = static_cast<int64_t>(nmx) * N;  // < 2^32 (host-checked: N n_max fits 32 bits)
     hipLaunchKernelGGL(k_encode_in,
-                       dim3(static_cast<unsigned>((N + 255) / 256), static_cast<unsigned>(a.k), static_cast<unsigned>(slots)),
+                       dim3(static_cast<unsigned>((lanes + 255) / 256), static_cast<unsigned>(a.k), static_cast<unsigned>(slots)),
                        dim3(256), 0, st, a, x, N);
 }
 

@@ -1580,6 +1580,7 @@ class DeviceInputEncoder {
         DASH_CHECK(static_cast<int>(crt_.size()) <= kMaxRes, "DeviceInputEncoder: too many residues");
         bind_device(dev_, nullptr, "DeviceInputEncoder");
         N_ = W0[0].N;
+        DASH_CHECK(N_ * 128 < (i64(1) << 31), "DeviceInputEncoder: input too large for the 32-bit lane index");
         a_.k = static_cast<int>(crt_.size());
         size_t off = 0;
         for (size_t j = 0; j < crt_.size(); ++j) {
