@@ -572,36 +572,21 @@ __device__ __forceinline__ uint32_t quad_sum_mod(uint32_t v, uint32_t q) {
     uint32_t t = s + static_cast<uint32_t>(__builtin_amdgcn_mov_dpp(static_cast<int>(s), 0x4E, 0xF, 0xF, false));
     return t >= q ? t - q : t;
 }
-// The element's digits of one residue in the element-major LDS image (k_mrs_chain_q), read in increasing order:
-// one dword (4 digits) at a time, the next dword in flight while the current one is consumed, so the serial digit
-// walk no longer waits on an LDS read per digit (the component-major image cost one exposed ds_read_u8 each)
-struct QDigits {
-    const uint32_t* p;
-    uint32_t cur, nxt;
-    __device__ __forceinline__ void init(const uint8_t* Ls) {
-        p = reinterpret_cast<const uint32_t*>(Ls);
-        cur = p[0];
-        nxt = p[1];
-    }
-    __device__ __forceinline__ uint32_t get(int c) {
-        if (c > 0 && (c & 3) == 0) {
-            cur = nxt;
-            nxt = p[(c >> 2) + 1];  // may read the next residue's digits or the image's slack: never used
-        }
-        return (cur >> ((c & 3) * 8)) & 0xffu;
-    }
-};
+// byte-wise sum over the quad of four packed values (each byte < 64): every byte of the result < 4 * 64
+__device__ __forceinline__ uint32_t quad_sum_bytes(uint32_t v) {
+    const uint32_t s = v + static_cast<uint32_t>(__builtin_amdgcn_mov_dpp(static_cast<int>(v), 0xB1, 0xF, 0xF, false));
+    return s + static_cast<uint32_t>(__builtin_amdgcn_mov_dpp(static_cast<int>(s), 0x4E, 0xF, 0xF, false));
+}
 template <int K, int MODE, int I>
-__device__ __forceinline__ void chain_q_pos(const MrsArgs& a, uint64_t gate, const ModC* mc, const uint8_t* wel,
-                                            const int* soff, int g, bool valid, const u128* row0, u128* PS,
+__device__ __forceinline__ void chain_q_pos(const MrsArgs& a, uint64_t gate, const ModC* mc, const uint8_t* wst,
+                                            const int* roff, int el, int g, bool valid, const u128* row0, u128* PS,
                                             u128& acc) {
     constexpr int kLast = MODE >= 1 ? K - 1 : K;
     if constexpr (I < kLast) {
         constexpr int r = MODE >= 1 ? (I + 1) % K : I;
         const ModC m = mc[a.crt.p[r]];
         const int n = static_cast<int>(m.n);
-        QDigits dg;  // the four lanes of a quad read the same dwords (broadcast)
-        dg.init(wel + soff[r]);
+        const uint8_t* Ls = wst + roff[r] * kMrsQE + el;  // the four lanes of a quad read the same byte (broadcast)
         constexpr int kExtra = MODE == 1 ? 0 : 1;
         constexpr int nt = K - 1 - I + kExtra;
         uint32_t col = 0;
@@ -617,8 +602,7 @@ __device__ __forceinline__ void chain_q_pos(const MrsArgs& a, uint64_t gate, con
             CompressFwd cf;
             cf.init();
             for (int c = 0; c < n; ++c) {
-                uint32_t d = dg.get(c);
-                if (!valid) d = 0;
+                const uint32_t d = valid ? Ls[c * kMrsQE] : 0u;
                 if (c == 0) {
                     col = d;
                     fetch_row(col);
@@ -645,26 +629,60 @@ __device__ __forceinline__ void chain_q_pos(const MrsArgs& a, uint64_t gate, con
                 for (int s2 = 0; s2 < NS; ++s2) rr[s2] = I > 0 ? divmod128(Q[s2], m) : 0u;  // no stream: Q = 0
                 const int cnt = min(mcn, n - c0);
                 uint32_t v = 0, pt = 1;
-                for (int t = 0; t < cnt; ++t) {
-                    uint32_t S = 0;
-                    if constexpr (I > 0) {
-                        uint32_t sd = 0;
+                if (I > 0 && a.qpack && q <= 63) {
+                    // four digits per quad reduction: the lane's digit sums packed in bytes (each < q), two DPP
+                    // adds leave every byte < 4q <= 252, then each byte is reduced mod q
+                    for (int t0 = 0; t0 < cnt; t0 += 4) {
+                        uint32_t pk = 0;
 #pragma unroll
-                        for (int s2 = 0; s2 < NS; ++s2) {
-                            sd += chunk_digit(rr[s2], m);
-                            sd = sd >= q ? sd - q : sd;
+                        for (int u = 0; u < 4; ++u) {
+                            if (t0 + u >= cnt) break;
+                            uint32_t sd = 0;
+#pragma unroll
+                            for (int s2 = 0; s2 < NS; ++s2) {
+                                sd += chunk_digit(rr[s2], m);
+                                sd = sd >= q ? sd - q : sd;
+                            }
+                            pk |= sd << (8 * u);
                         }
-                        S = quad_sum_mod(sd, q);  // the digit sum of all I streams
+                        pk = quad_sum_bytes(pk);
+#pragma unroll
+                        for (int u = 0; u < 4; ++u) {
+                            if (t0 + u >= cnt) break;
+                            uint32_t S = (pk >> (8 * u)) & 0xffu;
+                            S = S >= 2 * q ? S - 2 * q : S;
+                            S = S >= q ? S - q : S;
+                            uint32_t d = valid ? Ls[(c0 + t0 + u) * kMrsQE] : 0u;
+                            d = d >= S ? d - S : d + q - S;
+                            if (c0 + t0 + u == 0) {
+                                col = d;
+                                fetch_row(col);
+                            }
+                            v += d * pt;
+                            pt *= q;
+                        }
                     }
-                    uint32_t d = dg.get(c0 + t);
-                    if (!valid) d = 0;
-                    d = d >= S ? d - S : d + q - S;
-                    if (c0 + t == 0) {
-                        col = d;
-                        fetch_row(col);
+                } else {
+                    for (int t = 0; t < cnt; ++t) {
+                        uint32_t S = 0;
+                        if constexpr (I > 0) {
+                            uint32_t sd = 0;
+#pragma unroll
+                            for (int s2 = 0; s2 < NS; ++s2) {
+                                sd += chunk_digit(rr[s2], m);
+                                sd = sd >= q ? sd - q : sd;
+                            }
+                            S = quad_sum_mod(sd, q);  // the digit sum of all I streams
+                        }
+                        uint32_t d = valid ? Ls[(c0 + t) * kMrsQE] : 0u;
+                        d = d >= S ? d - S : d + q - S;
+                        if (c0 + t == 0) {
+                            col = d;
+                            fetch_row(col);
+                        }
+                        v += d * pt;
+                        pt *= q;
                     }
-                    v += d * pt;
-                    pt *= q;
                 }
                 C += PW * static_cast<u128>(v);
                 PW *= static_cast<u128>(m.D);
@@ -691,76 +709,62 @@ __device__ __forceinline__ void chain_q_pos(const MrsArgs& a, uint64_t gate, con
 #pragma unroll
         for (int t = 0; t < K - 1 - I; ++t) PS[mrs_pair<K>(I, I + 1 + t)] = E[t];
         if constexpr (MODE != 1) acc = add_packed(acc, E[K - 1 - I], a.hmask);
-        chain_q_pos<K, MODE, I + 1>(a, gate, mc, wel, soff, g, valid, row0, PS, acc);
+        chain_q_pos<K, MODE, I + 1>(a, gate, mc, wst, roff, el, g, valid, row0, PS, acc);
     }
 }
 
-// element-major digit image of k_mrs_chain_q: residue r's digits of element el at el * RS + soff[r] (digit counts
-// padded to whole dwords), RS an odd number of dwords so the 16 quads of a wave read distinct banks
-__host__ __device__ inline int mrs_q_stride(int digits_padded) { return 4 * ((digits_padded / 4) | 1); }
 template <int K, int MODE>
 __global__ __launch_bounds__(kMrsQBS, 2) void k_mrs_chain_q(MrsArgs a, Act x, const ModC* mc) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t wst[];  // [kMrsQE][RS] (+ 16 bytes of slack)
+    extern __shared__ __attribute__((aligned(16))) uint8_t wst[];  // row gg (residue r, component c) at gg * kMrsQE
     const int b = blockIdx.z;
     const int64_t N = a.N;
     constexpr int NP = K * (K - 1) / 2 > 0 ? K * (K - 1) / 2 : 1;
     const int tid = static_cast<int>(threadIdx.x);
     const int el = tid >> 2, g = tid & 3;
-    int soff[K + 1], roff[K + 1];
+    int roff[K + 1];
     const act_t* src[K];
-    soff[0] = roff[0] = 0;
+    roff[0] = 0;
 #pragma unroll
     for (int r = 0; r < K; ++r) {
         const int n = static_cast<int>(mc[a.crt.p[r]].n);
         roff[r + 1] = roff[r] + n;
-        soff[r + 1] = soff[r] + ((n + 3) & ~3);
         src[r] = x.p[r] + static_cast<int64_t>(b) * n * N;
     }
-    const int RS = mrs_q_stride(soff[K]);
     for (int64_t e0 = static_cast<int64_t>(blockIdx.x) * kMrsQE; e0 < N; e0 += static_cast<int64_t>(gridDim.x) * kMrsQE) {
         __syncthreads();  // the previous tile's readers are done
-        // transpose-stage: 16-byte units of a component row (16 consecutive elements, kUn loads in flight per
-        // lane), each unit's bytes written to its 16 elements' rows of the image
-        constexpr int W = kMrsQE / 16;
-        constexpr int kUn = 4;
-        const int units = roff[K] * W;
-        const bool vec = N % 16 == 0;
-        for (int x0 = tid; x0 < units; x0 += kUn * kMrsQBS) {
-            uint4 v[kUn];
-            int dst[kUn];
+        if (N % 16 == 0) {
+            // 16-byte units: row gg's kMrsQE bytes are kMrsQE / 16 units
+            constexpr int W = kMrsQE / 16;
+            const int units = roff[K] * W;
+            for (int x0 = tid; x0 < units; x0 += 4 * kMrsQBS) {
+                uint4 v[4];
 #pragma unroll
-            for (int h = 0; h < kUn; ++h) {
-                const int xu = x0 + h * kMrsQBS;
-                const int gg = xu / W, e16 = 16 * (xu % W);
-                const act_t* row = src[0] + static_cast<int64_t>(gg) * N;
-                int d = soff[0] + gg;
+                for (int h = 0; h < 4; ++h) {
+                    const int xu = x0 + h * kMrsQBS;
+                    const int gg = xu / W;
+                    const int64_t e = e0 + 16 * (xu % W);
+                    const act_t* row = src[0] + static_cast<int64_t>(gg) * N;
 #pragma unroll
-                for (int r = 1; r < K; ++r)
-                    if (gg >= roff[r]) {
-                        row = src[r] + static_cast<int64_t>(gg - roff[r]) * N;
-                        d = soff[r] + gg - roff[r];
-                    }
-                dst[h] = e16 * RS + d;
-                v[h] = make_uint4(0, 0, 0, 0);
-                const int64_t e = e0 + e16;
-                if (xu < units) {
-                    if (vec) {
-                        if (e < N) v[h] = *reinterpret_cast<const uint4*>(row + e);
-                    } else {
-                        uint32_t wv[4] = {0, 0, 0, 0};
+                    for (int r = 1; r < K; ++r)
+                        if (gg >= roff[r]) row = src[r] + static_cast<int64_t>(gg - roff[r]) * N;
+                    if (xu < units && e < N) v[h] = *reinterpret_cast<const uint4*>(row + e);
+                }
 #pragma unroll
-                        for (int i = 0; i < 16; ++i)
-                            if (e + i < N) wv[i >> 2] |= static_cast<uint32_t>(row[e + i]) << (8 * (i & 3));
-                        v[h] = make_uint4(wv[0], wv[1], wv[2], wv[3]);
-                    }
+                for (int h = 0; h < 4; ++h) {
+                    const int xu = x0 + h * kMrsQBS;
+                    if (xu < units) *reinterpret_cast<uint4*>(wst + (xu / W) * kMrsQE + 16 * (xu % W)) = v[h];
                 }
             }
+        } else {
+            const int bunits = roff[K] * kMrsQE;  // one byte per (row, element)
+            for (int xu = tid; xu < bunits; xu += kMrsQBS) {
+                const int gg = xu / kMrsQE;
+                const int64_t e = e0 + xu % kMrsQE;
+                const act_t* row = src[0] + static_cast<int64_t>(gg) * N;
 #pragma unroll
-            for (int h = 0; h < kUn; ++h) {
-                if (x0 + h * kMrsQBS >= units) continue;
-                const uint32_t wv[4] = {v[h].x, v[h].y, v[h].z, v[h].w};
-#pragma unroll
-                for (int i = 0; i < 16; ++i) wst[dst[h] + i * RS] = static_cast<uint8_t>(wv[i >> 2] >> (8 * (i & 3)));
+                for (int r = 1; r < K; ++r)
+                    if (gg >= roff[r]) row = src[r] + static_cast<int64_t>(gg - roff[r]) * N;
+                wst[xu] = e < N ? static_cast<uint8_t>(row[e]) : 0;
             }
         }
         __syncthreads();
@@ -770,20 +774,15 @@ __global__ __launch_bounds__(kMrsQBS, 2) void k_mrs_chain_q(MrsArgs a, Act x, co
         u128 PS[NP];
         u128 acc = 0;
         const uint64_t gate = a.gate0 ^ static_cast<uint64_t>(e);
-        const uint8_t* wel = wst + el * RS;
-        chain_q_pos<K, MODE, 0>(a, gate, mc, wel, soff, g, valid, row0, PS, acc);
+        chain_q_pos<K, MODE, 0>(a, gate, mc, wst, roff, el, g, valid, row0, PS, acc);
         if (MODE >= 1) {
             // residue 0 (mod 2): bit pack of L_0 XOR the K - 1 payloads aimed at it = the sign label (all lanes)
             const ModC m = mc[a.crt.p[0]];
             const int n = static_cast<int>(m.n);
-            QDigits dg;
-            dg.init(wel + soff[0]);
+            const uint8_t* Ls = wst + el;
             CompressFwd cf;
             cf.init();
-            for (int c = 0; c < n; ++c) {
-                const uint32_t d = dg.get(c);
-                cf.push(valid ? d : 0u, m);
-            }
+            for (int c = 0; c < n; ++c) cf.push(valid ? Ls[c * kMrsQE] : 0u, m);
             u128 key = cf.finish();
 #pragma unroll
             for (int l = 0; l < K - 1; ++l) key ^= PS[mrs_pair<K>(l, K - 1)];
@@ -861,11 +860,15 @@ template <int K, int MODE>
 static void launch_chain_w(const MrsArgs& a, const Act& x, int B, size_t wl, const ModC* mc, const AesGlobals& g,
                            hipStream_t st) {
     if (mrs_quad_on()) {
-        int pad = 0;  // element-major image: every residue's digits padded to dwords, odd dword stride, slack
-        for (int r = 0; r < a.crt.k; ++r) pad += (a.crt.n[r] + 3) & ~3;
-        const size_t ql = static_cast<size_t>(mrs_q_stride(pad)) * kMrsQE + 16;
+        static const int qpack = [] {  // A/B knob DASH_MRS_QPACK=0: one quad reduction per digit
+            const char* e = std::getenv("DASH_MRS_QPACK");
+            return e && e[0] == '0' ? 0 : 1;
+        }();
+        MrsArgs aq = a;
+        aq.qpack = qpack;
+        const size_t ql = wl / kMrsWBS * kMrsQE;  // every residue's rows for kMrsQE elements
         const dim3 gq(static_cast<unsigned>((a.N + kMrsQE - 1) / kMrsQE), 1, B);
-        hipLaunchKernelGGL((k_mrs_chain_q<K, MODE>), gq, dim3(kMrsQBS), ql, st, a, x, mc);
+        hipLaunchKernelGGL((k_mrs_chain_q<K, MODE>), gq, dim3(kMrsQBS), ql, st, aq, x, mc);
         return;
     }
     static const bool raised = [] {
