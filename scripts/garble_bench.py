@@ -67,6 +67,8 @@ def main():
             times.append(time.perf_counter() - t)
         blobs[mode] = gc.model.serialize()
         print(json.dumps({"mode": mode, "model": args.model, "s_per_gc": round(min(times), 3),
+                          "ms_per_gc_min": round(1000 * min(times), 2),
+                          "ms_per_gc_median": round(1000 * sorted(times)[len(times) // 2], 2),
                           "layer_ms": [round(x, 1) for x in gc.garbling_layer_ms()]}), flush=True)
     if not args.gpu_only:
         print(json.dumps({"identical": blobs["gpu"] == blobs["cpu"]}), flush=True)
