@@ -577,6 +577,93 @@ __device__ __forceinline__ uint32_t quad_sum_bytes(uint32_t v) {
     const uint32_t s = v + static_cast<uint32_t>(__builtin_amdgcn_mov_dpp(static_cast<int>(v), 0xB1, 0xF, 0xF, false));
     return s + static_cast<uint32_t>(__builtin_amdgcn_mov_dpp(static_cast<int>(s), 0x4E, 0xF, 0xF, false));
 }
+// u128 sum over the quad, every lane gets it (two DPP rounds on the four 32-bit words, carries by the adds)
+template <int CTRL>
+__device__ __forceinline__ u128 dpp128(u128 v) {
+    const uint32_t w0 = static_cast<uint32_t>(__builtin_amdgcn_mov_dpp(static_cast<int>(static_cast<uint32_t>(v)), CTRL, 0xF, 0xF, false));
+    const uint32_t w1 = static_cast<uint32_t>(__builtin_amdgcn_mov_dpp(static_cast<int>(static_cast<uint32_t>(v >> 32)), CTRL, 0xF, 0xF, false));
+    const uint32_t w2 = static_cast<uint32_t>(__builtin_amdgcn_mov_dpp(static_cast<int>(static_cast<uint32_t>(v >> 64)), CTRL, 0xF, 0xF, false));
+    const uint32_t w3 = static_cast<uint32_t>(__builtin_amdgcn_mov_dpp(static_cast<int>(static_cast<uint32_t>(v >> 96)), CTRL, 0xF, 0xF, false));
+    return (static_cast<u128>((static_cast<uint64_t>(w3) << 32) | w2) << 64) | ((static_cast<uint64_t>(w1) << 32) | w0);
+}
+__device__ __forceinline__ u128 quad_sum128(u128 v) {
+    v += dpp128<0xB1>(v);
+    return v + dpp128<0x4E>(v);
+}
+// Chunk-split key (positions with at most kQSplit payload streams): the key's base-q chunks are dealt over the
+// quad, lane g taking chunks 4j + g, so each lane walks a quarter of the digits; every lane runs the streams'
+// chunk divisions (cheap next to the digit walk) and keeps its own chunk's value, and the lanes' partial keys
+// sum over the quad. The stream-split form (below) replicates the whole digit walk on every lane.
+constexpr int kQSplit = 2;
+struct QPow {  // D^1 .. D^4 of a modulus (D = q^c < 2^31): lane g's first chunk weight and the group step
+    u128 d1, d2, d3, d4;
+    __device__ __forceinline__ void init(const ModC& m) {
+        d1 = static_cast<u128>(m.D);
+        d2 = d1 * d1;
+        d3 = d2 * d1;
+        d4 = d2 * d2;
+    }
+    __device__ __forceinline__ u128 first(int g) const {
+        return g == 0 ? static_cast<u128>(1) : (g == 1 ? d1 : (g == 2 ? d2 : d3));
+    }
+};
+template <int NSTR>
+__device__ __forceinline__ u128 quad_key_split(const uint8_t* Ls, const ModC& m, int g, bool valid, u128 (&Q)[NSTR > 0 ? NSTR : 1]) {
+    const int n = static_cast<int>(m.n);
+    if (m.bits) {  // power of two (no streams): lane g packs digits [g * cpl, (g + 1) * cpl) at bit b * t
+        const int cpl = (n + 3) >> 2, b = static_cast<int>(m.bits);
+        u128 P = 0;
+        for (int t = 0; t < cpl; ++t) {
+            const int idx = g * cpl + t;
+            if (valid && idx < n) P |= static_cast<u128>(Ls[idx * kMrsQE]) << (b * idx);
+        }
+        return quad_sum128(P);  // disjoint bit ranges: the sum is the OR
+    }
+    const int c = static_cast<int>(m.c);
+    const uint32_t q = m.q;
+    const int nch = (n + c - 1) / c;
+    QPow pw;
+    pw.init(m);
+    u128 PW = pw.first(g), P = 0;
+    for (int j = 0; 4 * j < nch; ++j) {
+        uint32_t mine[NSTR > 0 ? NSTR : 1];
+        if constexpr (NSTR > 0) {
+#pragma unroll
+            for (int l = 0; l < NSTR; ++l) mine[l] = 0;
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                if (4 * j + u >= nch) break;
+#pragma unroll
+                for (int l = 0; l < NSTR; ++l) {
+                    const uint32_t rr = divmod128(Q[l], m);
+                    mine[l] = u == g ? rr : mine[l];
+                }
+            }
+        }
+        const int i = 4 * j + g;
+        uint32_t v = 0, pt = 1;
+        for (int t = 0; t < c; ++t) {
+            const int idx = i * c + t;
+            uint32_t d = 0;
+            if (valid && idx < n) d = Ls[idx * kMrsQE];
+            if constexpr (NSTR > 0) {
+                uint32_t S = 0;
+#pragma unroll
+                for (int l = 0; l < NSTR; ++l) {
+                    S += chunk_digit(mine[l], m);
+                    S = S >= q ? S - q : S;
+                }
+                d = d >= S ? d - S : d + q - S;
+                if (idx >= n) d = 0;
+            }
+            v += d * pt;
+            pt *= q;
+        }
+        P += PW * static_cast<u128>(v);
+        PW *= pw.d4;
+    }
+    return quad_sum128(P);
+}
 template <int K, int MODE, int I>
 __device__ __forceinline__ void chain_q_pos(const MrsArgs& a, uint64_t gate, const ModC* mc, const uint8_t* wst,
                                             const int* roff, int el, int g, bool valid, const u128* row0, u128* PS,
@@ -598,7 +685,35 @@ __device__ __forceinline__ void chain_q_pos(const MrsArgs& a, uint64_t gate, con
             for (int q = 0; q < 4; ++q)
                 if (4 * g + q < nt) Eo[q] = rowp[4 * g + q];
         };
-        if constexpr (r == 0) {  // residue 0, the base's power of two: mode 0 position 0, no payload streams
+        bool split = false;
+        if constexpr (I <= kQSplit) split = (a.qpack & 2) != 0;  // DASH_MRS_QSPLIT=0: the stream-split walk (A/B)
+        if (split) {
+            // the row index (the key's first digit) first, so the row loads overlap the digit walk
+            u128 Q[I > 0 ? I : 1];
+            uint32_t d0 = valid ? Ls[0] : 0u;
+            if constexpr (I > 0) {
+#pragma unroll
+                for (int l = 0; l < I; ++l) Q[l] = PS[mrs_pair<K>(l, I)];
+                uint32_t S0 = 0;
+                if (m.bits) {
+#pragma unroll
+                    for (int l = 0; l < I; ++l) S0 += static_cast<uint32_t>(Q[l]) & (m.q - 1);
+                    S0 &= m.q - 1;
+                } else {
+#pragma unroll
+                    for (int l = 0; l < I; ++l) {
+                        u128 t = Q[l];
+                        uint32_t c0 = divmod128(t, m);
+                        S0 += chunk_digit(c0, m);
+                        S0 = S0 >= m.q ? S0 - m.q : S0;
+                    }
+                }
+                d0 = d0 >= S0 ? d0 - S0 : d0 + m.q - S0;
+            }
+            col = d0;
+            fetch_row(col);
+            key = quad_key_split<I>(Ls, m, g, valid, Q);
+        } else if constexpr (r == 0) {  // residue 0, the base's power of two: mode 0 position 0, no payload streams
             CompressFwd cf;
             cf.init();
             for (int c = 0; c < n; ++c) {
@@ -629,7 +744,7 @@ __device__ __forceinline__ void chain_q_pos(const MrsArgs& a, uint64_t gate, con
                 for (int s2 = 0; s2 < NS; ++s2) rr[s2] = I > 0 ? divmod128(Q[s2], m) : 0u;  // no stream: Q = 0
                 const int cnt = min(mcn, n - c0);
                 uint32_t v = 0, pt = 1;
-                if (I > 0 && a.qpack && q <= 63) {
+                if (I > 0 && (a.qpack & 1) && q <= 63) {
                     // four digits per quad reduction: the lane's digit sums packed in bytes (each < q), two DPP
                     // adds leave every byte < 4q <= 252, then each byte is reduced mod q
                     for (int t0 = 0; t0 < cnt; t0 += 4) {
@@ -860,9 +975,10 @@ template <int K, int MODE>
 static void launch_chain_w(const MrsArgs& a, const Act& x, int B, size_t wl, const ModC* mc, const AesGlobals& g,
                            hipStream_t st) {
     if (mrs_quad_on()) {
-        static const int qpack = [] {  // A/B knob DASH_MRS_QPACK=0: one quad reduction per digit
+        static const int qpack = [] {  // A/B knobs DASH_MRS_QPACK=0 (one quad reduction per digit), DASH_MRS_QSPLIT=0
             const char* e = std::getenv("DASH_MRS_QPACK");
-            return e && e[0] == '0' ? 0 : 1;
+            const char* f = std::getenv("DASH_MRS_QSPLIT");
+            return (e && e[0] == '0' ? 0 : 1) | (f && f[0] == '0' ? 0 : 2);
         }();
         MrsArgs aq = a;
         aq.qpack = qpack;
