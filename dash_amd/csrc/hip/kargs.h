@@ -125,7 +125,8 @@ struct MrsArgs {
     uint64_t rgate0;  // modes 1, 2: the ReLU mixed-mult gadget's gate base (its y-row / g-row pads)
     int ny;           // y-row pad slots per element (k entries + packed minis)
     u128* ys;         // modes 1, 2: [B][ny][N] the sign label's y-row pads
-    int qpack;        // k_mrs_chain_q: bit 0 four digits per quad reduction (moduli <= 63), bit 1 chunk-split keys
+    int qpack;        // k_mrs_chain_q: bit 0 four digits per quad reduction (moduli <= 63); >> 1: positions
+                      // I < that value take chunk-split keys
 };
 
 struct BEArgs {

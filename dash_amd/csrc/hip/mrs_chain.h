@@ -594,7 +594,7 @@ __device__ __forceinline__ u128 quad_sum128(u128 v) {
 // quad, lane g taking chunks 4j + g, so each lane walks a quarter of the digits; every lane runs the streams'
 // chunk divisions (cheap next to the digit walk) and keeps its own chunk's value, and the lanes' partial keys
 // sum over the quad. The stream-split form (below) replicates the whole digit walk on every lane.
-constexpr int kQSplit = 2;
+constexpr int kQSplit = 3;  // compiled for positions I <= kQSplit; the launch picks the limit (default I <= 2)
 struct QPow {  // D^1 .. D^4 of a modulus (D = q^c < 2^31): lane g's first chunk weight and the group step
     u128 d1, d2, d3, d4;
     __device__ __forceinline__ void init(const ModC& m) {
@@ -685,8 +685,8 @@ __device__ __forceinline__ void chain_q_pos(const MrsArgs& a, uint64_t gate, con
             for (int q = 0; q < 4; ++q)
                 if (4 * g + q < nt) Eo[q] = rowp[4 * g + q];
         };
-        bool split = false;
-        if constexpr (I <= kQSplit) split = (a.qpack & 2) != 0;  // DASH_MRS_QSPLIT=0: the stream-split walk (A/B)
+        bool split = false;  // positions I < (qpack >> 1): chunk-split (DASH_MRS_QSPLIT=-1: the stream-split walk)
+        if constexpr (I <= kQSplit) split = I < (a.qpack >> 1);
         if (split) {
             // the row index (the key's first digit) first, so the row loads overlap the digit walk
             u128 Q[I > 0 ? I : 1];
@@ -977,8 +977,9 @@ static void launch_chain_w(const MrsArgs& a, const Act& x, int B, size_t wl, con
     if (mrs_quad_on()) {
         static const int qpack = [] {  // A/B knobs DASH_MRS_QPACK=0 (one quad reduction per digit), DASH_MRS_QSPLIT=0
             const char* e = std::getenv("DASH_MRS_QPACK");
-            const char* f = std::getenv("DASH_MRS_QSPLIT");
-            return (e && e[0] == '0' ? 0 : 1) | (f && f[0] == '0' ? 0 : 2);
+            const char* f = std::getenv("DASH_MRS_QSPLIT");  // the last chunk-split position (-1: none)
+            const int lim = f ? std::max(-1, std::min(kQSplit, std::atoi(f))) : 2;
+            return (e && e[0] == '0' ? 0 : 1) | ((lim + 1) << 1);
         }();
         MrsArgs aq = a;
         aq.qpack = qpack;
