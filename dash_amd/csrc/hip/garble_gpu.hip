@@ -2111,11 +2111,13 @@ struct ProjFns {
 };
 
 // k_emit dynamic LDS budget per block (A/B knob DASH_GG_EMIT_LDS_KB): smaller scopes per block, more
-// resident blocks per CU to overlap one block's staging loads with another's table stores
+// resident blocks per CU to overlap one block's staging loads with another's table stores. With the hardened
+// encoding's ChaCha pads (VALU-heavy) 24 KiB measured best: garble + load 7.8 / 7.4 / 7.0 ms per MiniONN GC at
+// 48 / 16 / 24 KiB (profiles/ab/README.md, round 5)
 inline size_t emit_lds_budget() {
     static const size_t v = [] {
         const char* e = std::getenv("DASH_GG_EMIT_LDS_KB");
-        const int kb = e ? std::atoi(e) : 48;
+        const int kb = e ? std::atoi(e) : 24;
         return static_cast<size_t>(std::min(56, std::max(8, kb))) << 10;
     }();
     return v;

@@ -594,7 +594,7 @@ __device__ __forceinline__ u128 quad_sum128(u128 v) {
 // quad, lane g taking chunks 4j + g, so each lane walks a quarter of the digits; every lane runs the streams'
 // chunk divisions (cheap next to the digit walk) and keeps its own chunk's value, and the lanes' partial keys
 // sum over the quad. The stream-split form (below) replicates the whole digit walk on every lane.
-constexpr int kQSplit = 3;  // compiled for positions I <= kQSplit; the launch picks the limit (default I <= 2)
+constexpr int kQSplit = 3;  // compiled for positions I <= kQSplit; the launch picks the limit (default all of them)
 struct QPow {  // D^1 .. D^4 of a modulus (D = q^c < 2^31): lane g's first chunk weight and the group step
     u128 d1, d2, d3, d4;
     __device__ __forceinline__ void init(const ModC& m) {
@@ -978,7 +978,7 @@ static void launch_chain_w(const MrsArgs& a, const Act& x, int B, size_t wl, con
         static const int qpack = [] {  // A/B knobs DASH_MRS_QPACK=0 (one quad reduction per digit), DASH_MRS_QSPLIT=0
             const char* e = std::getenv("DASH_MRS_QPACK");
             const char* f = std::getenv("DASH_MRS_QSPLIT");  // the last chunk-split position (-1: none)
-            const int lim = f ? std::max(-1, std::min(kQSplit, std::atoi(f))) : 2;
+            const int lim = f ? std::max(-1, std::min(kQSplit, std::atoi(f))) : 3;
             return (e && e[0] == '0' ? 0 : 1) | ((lim + 1) << 1);
         }();
         MrsArgs aq = a;
