@@ -734,20 +734,23 @@ __global__ __launch_bounds__(256) void k_rescale_mrs_out(MrsArgs a, Act x, const
         return;
     }
     const uint32_t inv = static_cast<uint32_t>(a.sinv[j]);
-    uint16_t cur[kChunk], nxt[kChunk];  // loads of chunk c+1 before the stores of chunk c (as k_relu_mult)
+    // loads of group c+1 before the stores of group c (as k_relu_mult); 16-digit groups: this kernel runs one
+    // short serial walk per lane (batch-1 launches are latency-bound), so fewer, deeper round trips
+    constexpr int kG = 2 * kChunk;
+    uint16_t cur[kG], nxt[kG];
 #pragma unroll
-    for (int u = 0; u < kChunk; ++u)
+    for (int u = 0; u < kG; ++u)
         if (u < n) cur[u] = L[static_cast<int64_t>(u) * N];
-    for (int c0 = 0; c0 < n; c0 += kChunk) {
+    for (int c0 = 0; c0 < n; c0 += kG) {
 #pragma unroll
-        for (int u = 0; u < kChunk; ++u)
-            if (c0 + kChunk + u < n) nxt[u] = L[static_cast<int64_t>(c0 + kChunk + u) * N];
+        for (int u = 0; u < kG; ++u)
+            if (c0 + kG + u < n) nxt[u] = L[static_cast<int64_t>(c0 + kG + u) * N];
 #pragma unroll
-        for (int u = 0; u < kChunk; ++u)
+        for (int u = 0; u < kG; ++u)
             if (c0 + u < n)
                 L[static_cast<int64_t>(c0 + u) * N] = static_cast<act_t>(modq(cur[u] * inv + s.next(m), m));  // < p^2 + p
 #pragma unroll
-        for (int u = 0; u < kChunk; ++u) cur[u] = nxt[u];
+        for (int u = 0; u < kG; ++u) cur[u] = nxt[u];
     }
 }
 
@@ -1034,12 +1037,22 @@ __global__ __launch_bounds__(kRroBS) void k_rescale_relu_out_s(MrsArgs a, SignAr
         CompressFwd cf;
         cf.init();
         u128 Graw = 0;
-        for (int c = 0; c < n; ++c) {
-            uint8_t& w = stg[c * kRroBS + tid];
-            const uint32_t v = j == 0 ? s.next(m) : modq(static_cast<uint32_t>(w) * inv + s.next(m), m);
-            if (c == 0) Graw = grow[v];
-            w = static_cast<uint8_t>(v);
-            if (j != 0) cf.push(v, m);
+        // groups of kRroG digits: the group's LDS reads are issued together (one exposed latency per group instead
+        // of per digit: a digit's write-back may alias the next digit's read, so the compiler cannot hoist it)
+        constexpr int kRroG = 8;
+        for (int c0 = 0; c0 < n; c0 += kRroG) {
+            uint32_t w8[kRroG];
+#pragma unroll
+            for (int u = 0; u < kRroG; ++u) w8[u] = (j != 0 && c0 + u < n) ? stg[(c0 + u) * kRroBS + tid] : 0u;
+#pragma unroll
+            for (int u = 0; u < kRroG; ++u) {
+                const int c = c0 + u;
+                if (c >= n) break;
+                const uint32_t v = j == 0 ? s.next(m) : modq(w8[u] * inv + s.next(m), m);
+                if (c == 0) Graw = grow[v];
+                stg[c * kRroBS + tid] = static_cast<uint8_t>(v);
+                if (j != 0) cf.push(v, m);
+            }
         }
         const u128 key = j == 0 ? P : cf.finish();
         __syncthreads();
@@ -1053,11 +1066,18 @@ __global__ __launch_bounds__(kRroBS) void k_rescale_relu_out_s(MrsArgs a, SignAr
         sg.init(G);
         se.init(E);
         __syncthreads();  // the row stores have read Y_j
-        for (int c = 0; c < n; ++c) {
-            const uint32_t g = sg.next(m);
-            const uint32_t ev = se.next(m);
-            uint8_t& w = stg[c * kRroBS + tid];
-            w = static_cast<uint8_t>(modq(ev + ypr * static_cast<uint32_t>(w) + static_cast<uint32_t>(p) - g, m));
+        for (int c0 = 0; c0 < n; c0 += kRroG) {
+            uint32_t w8[kRroG];
+#pragma unroll
+            for (int u = 0; u < kRroG; ++u) w8[u] = c0 + u < n ? stg[(c0 + u) * kRroBS + tid] : 0u;
+#pragma unroll
+            for (int u = 0; u < kRroG; ++u) {
+                const int c = c0 + u;
+                if (c >= n) break;
+                const uint32_t g = sg.next(m);
+                const uint32_t ev = se.next(m);
+                stg[c * kRroBS + tid] = static_cast<uint8_t>(modq(ev + ypr * w8[u] + static_cast<uint32_t>(p) - g, m));
+            }
         }
         __syncthreads();
         lds_store_rows<kRroBS>(Y, stg, N, e0, 0, n);
