@@ -134,5 +134,31 @@ static inline bool stage_ok(int64_t N, int bs) {
 #define DASH_UA_MINBLOCKS 4
 #endif
 
+// u128 sum over the quad, every lane gets it (two DPP rounds on the four 32-bit words, carries by the adds)
+template <int CTRL>
+__device__ __forceinline__ u128 dpp128(u128 v) {
+    const uint32_t w0 = static_cast<uint32_t>(__builtin_amdgcn_mov_dpp(static_cast<int>(static_cast<uint32_t>(v)), CTRL, 0xF, 0xF, false));
+    const uint32_t w1 = static_cast<uint32_t>(__builtin_amdgcn_mov_dpp(static_cast<int>(static_cast<uint32_t>(v >> 32)), CTRL, 0xF, 0xF, false));
+    const uint32_t w2 = static_cast<uint32_t>(__builtin_amdgcn_mov_dpp(static_cast<int>(static_cast<uint32_t>(v >> 64)), CTRL, 0xF, 0xF, false));
+    const uint32_t w3 = static_cast<uint32_t>(__builtin_amdgcn_mov_dpp(static_cast<int>(static_cast<uint32_t>(v >> 96)), CTRL, 0xF, 0xF, false));
+    return (static_cast<u128>((static_cast<uint64_t>(w3) << 32) | w2) << 64) | ((static_cast<uint64_t>(w1) << 32) | w0);
+}
+__device__ __forceinline__ u128 quad_sum128(u128 v) {
+    v += dpp128<0xB1>(v);
+    return v + dpp128<0x4E>(v);
+}
+struct QPow {  // D^1 .. D^4 of a modulus (D = q^c < 2^31): lane g's first chunk weight and the group step
+    u128 d1, d2, d3, d4;
+    __device__ __forceinline__ void init(const ModC& m) {
+        d1 = static_cast<u128>(m.D);
+        d2 = d1 * d1;
+        d3 = d2 * d1;
+        d4 = d2 * d2;
+    }
+    __device__ __forceinline__ u128 first(int g) const {
+        return g == 0 ? static_cast<u128>(1) : (g == 1 ? d1 : (g == 2 ? d2 : d3));
+    }
+};
+
 }  // namespace dev
 }  // namespace dash

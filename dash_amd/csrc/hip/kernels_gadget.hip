@@ -1084,12 +1084,176 @@ __global__ __launch_bounds__(kRroBS) void k_rescale_relu_out_s(MrsArgs a, SignAr
     }
 }
 
+// Quad form of the joint output (latency-bound launches: batch 1, small layers). Four lanes per (element,
+// residue): the label's base-q chunks are dealt over the quad (lane g takes chunks 4j + g, power-of-two moduli
+// a quarter of the digits each), every lane runs the payload's chunk divisions and keeps its own chunk, the
+// rescaled label's partial keys are summed over the quad. The per-lane forms walk all n digits of three streams
+// serially on one lane (~50 us per launch whatever the layer size at batch 1, r05 timeline).
+constexpr int kRroQE = 64;  // elements per block (256 threads)
+__global__ __launch_bounds__(256) void k_rescale_relu_out_q(MrsArgs a, SignArgs sa, Act x, Act y, const u128* gtab,
+                                                           const u128* etab, const ModC* mc) {
+    __shared__ __attribute__((aligned(16))) uint8_t sL[128 * kRroQE];  // L_j -> Y_j in place
+    __shared__ __attribute__((aligned(16))) uint8_t sO[128 * kRroQE];  // ReLU outputs
+    const int j = blockIdx.y, b = blockIdx.z;
+    const int64_t N = a.N;  // N % 16 == 0 (host-checked)
+    const int k = a.crt.k;
+    const int p = a.crt.p[j];
+    const ModC m = mc[p];
+    const int n = static_cast<int>(m.n);
+    const uint32_t q = m.q;
+    const int tid = static_cast<int>(threadIdx.x);
+    const int el = tid >> 2, g = tid & 3;
+    const uint32_t inv = static_cast<uint32_t>(a.sinv[j]);
+    act_t* L = x.p[j] + static_cast<int64_t>(b) * n * N;
+    act_t* Yo = y.p[j] + static_cast<int64_t>(b) * n * N;
+    for (int64_t e0 = static_cast<int64_t>(blockIdx.x) * kRroQE; e0 < N; e0 += static_cast<int64_t>(gridDim.x) * kRroQE) {
+        const int64_t e = min(e0 + el, N - 1);  // spare quads shadow a real element; the row stores skip them
+        const int64_t be = static_cast<int64_t>(b) * N + e;
+        const int64_t bke = (static_cast<int64_t>(b) * k + j) * N + e;
+        const u128 HS = a.ys[(static_cast<int64_t>(b) * a.ny + j) * N + e];
+        const u128 HM = a.ys[(static_cast<int64_t>(b) * a.ny + k + j / 8) * N + e] >> (16 * (j % 8));
+        const uint32_t cS = a.cs[be];
+        const u128* E3 = etab + (be * k + j) * 3;
+        const u128 mini = E3[2];
+        const u128* grow = gtab + be * sa.crt.sum + sa.crt.prefix[j];
+        const u128 P = a.pf[bke];
+        const u128 Eraw = E3[cS];
+        __syncthreads();  // the previous tile's row stores have read the images
+        if (j != 0) {
+            for (int xu = tid; xu < n * (kRroQE / 16); xu += 256) {
+                const int row = xu / (kRroQE / 16), part = xu % (kRroQE / 16);
+                const int64_t ee = e0 + 16 * part;
+                if (ee < N) *reinterpret_cast<uint4*>(sL + row * kRroQE + 16 * part) =
+                    *reinterpret_cast<const uint4*>(L + static_cast<int64_t>(row) * N + ee);
+            }
+        }
+        __syncthreads();
+        // digit 0 first (every lane): the garbler half gate's row gather overlaps the walk
+        u128 Graw;
+        {
+            uint32_t pd0;
+            if (m.bits) {
+                pd0 = static_cast<uint32_t>(P) & (q - 1);
+            } else {
+                u128 t = P;
+                uint32_t r = divmod128(t, m);
+                pd0 = chunk_digit(r, m);
+            }
+            const uint32_t v0 = j == 0 ? pd0 : modq(static_cast<uint32_t>(sL[el]) * inv + pd0, m);
+            Graw = grow[v0];
+        }
+        // Y_j = S^-1 L_j + P (mod p), residue 0: Y_0 = decompress(P); the lane's digits and its partial key
+        u128 part = 0;
+        const int bb = static_cast<int>(m.bits), cpl = (n + 3) >> 2;
+        QPow pw;
+        if (m.bits) {
+            for (int t = 0; t < cpl; ++t) {
+                const int idx = g * cpl + t;
+                if (idx >= n) break;
+                const uint32_t pd = static_cast<uint32_t>(P >> (bb * idx)) & (q - 1);
+                const uint32_t v = j == 0 ? pd : modq(static_cast<uint32_t>(sL[idx * kRroQE + el]) * inv + pd, m);
+                sL[idx * kRroQE + el] = static_cast<uint8_t>(v);
+                part |= static_cast<u128>(v) << (bb * idx);
+            }
+        } else {
+            pw.init(m);
+            const int c = static_cast<int>(m.c), nch = (n + c - 1) / c;
+            u128 Q = P, PW = pw.first(g);
+            for (int jj = 0; 4 * jj < nch; ++jj) {
+                uint32_t mine = 0;
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    if (4 * jj + u >= nch) break;
+                    const uint32_t r = divmod128(Q, m);
+                    mine = u == g ? r : mine;
+                }
+                const int i = 4 * jj + g;
+                uint32_t cv = 0, pt = 1;
+                for (int t = 0; t < c; ++t) {
+                    const int idx = i * c + t;
+                    const uint32_t pd = chunk_digit(mine, m);
+                    if (idx < n) {
+                        const uint32_t v = j == 0 ? pd : modq(static_cast<uint32_t>(sL[idx * kRroQE + el]) * inv + pd, m);
+                        sL[idx * kRroQE + el] = static_cast<uint8_t>(v);
+                        cv += v * pt;
+                    }
+                    pt *= q;
+                }
+                part += PW * static_cast<u128>(cv);
+                PW *= pw.d4;
+            }
+        }
+        const u128 key = j == 0 ? P : quad_sum128(part);
+        const u128 G = Graw - hard_pad(key, a.rgate0 ^ static_cast<uint64_t>(e), tw_sub(kTwMmg, j), 0);
+        const u128 E = Eraw - HS;
+        const int16_t t16 = static_cast<int16_t>(static_cast<uint16_t>(mini >> (16 * cS)));
+        const int16_t ypr16 = static_cast<int16_t>(t16 - static_cast<int16_t>(static_cast<uint16_t>(HM)));
+        const uint32_t ypr = modq(static_cast<uint32_t>(static_cast<int32_t>(ypr16) + (p << 15)), m);
+        // relu_j = E + ypr Y_j - G, the lane's own digits (k_relu_mult's arithmetic)
+        if (m.bits) {
+            for (int t = 0; t < cpl; ++t) {
+                const int idx = g * cpl + t;
+                if (idx >= n) break;
+                const uint32_t gd = static_cast<uint32_t>(G >> (bb * idx)) & (q - 1);
+                const uint32_t ed = static_cast<uint32_t>(E >> (bb * idx)) & (q - 1);
+                sO[idx * kRroQE + el] =
+                    static_cast<uint8_t>(modq(ed + ypr * static_cast<uint32_t>(sL[idx * kRroQE + el]) + static_cast<uint32_t>(p) - gd, m));
+            }
+        } else {
+            const int c = static_cast<int>(m.c), nch = (n + c - 1) / c;
+            u128 QG = G, QE = E;
+            for (int jj = 0; 4 * jj < nch; ++jj) {
+                uint32_t mg = 0, me = 0;
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    if (4 * jj + u >= nch) break;
+                    const uint32_t rg = divmod128(QG, m);
+                    const uint32_t re = divmod128(QE, m);
+                    mg = u == g ? rg : mg;
+                    me = u == g ? re : me;
+                }
+                const int i = 4 * jj + g;
+                for (int t = 0; t < c; ++t) {
+                    const int idx = i * c + t;
+                    const uint32_t gd = chunk_digit(mg, m);
+                    const uint32_t ed = chunk_digit(me, m);
+                    if (idx < n)
+                        sO[idx * kRroQE + el] = static_cast<uint8_t>(
+                            modq(ed + ypr * static_cast<uint32_t>(sL[idx * kRroQE + el]) + static_cast<uint32_t>(p) - gd, m));
+                }
+            }
+        }
+        __syncthreads();
+        for (int xu = tid; xu < n * (kRroQE / 16); xu += 256) {
+            const int row = xu / (kRroQE / 16), prt = xu % (kRroQE / 16);
+            const int64_t ee = e0 + 16 * prt;
+            if (ee >= N) continue;
+            *reinterpret_cast<uint4*>(L + static_cast<int64_t>(row) * N + ee) =
+                *reinterpret_cast<const uint4*>(sL + row * kRroQE + 16 * prt);
+            *reinterpret_cast<uint4*>(Yo + static_cast<int64_t>(row) * N + ee) =
+                *reinterpret_cast<const uint4*>(sO + row * kRroQE + 16 * prt);
+        }
+    }
+}
+
 void launch_rescale_relu_out(const MrsArgs& a, const SignArgs& sa, const Act& x, const Act& y, const u128* gtab,
                              const u128* etab, int B, const ModC* mc, const AesGlobals& g, hipStream_t st) {
     static const bool rro_stage = [] {  // DASH_RRO_STAGE=0: the per-lane form (A/B)
         const char* e = std::getenv("DASH_RRO_STAGE");
         return !(e && e[0] == '0');
     }();
+    static const bool rro_quad = [] {  // DASH_RRO_QUAD=0: no quad form (A/B)
+        const char* e = std::getenv("DASH_RRO_QUAD");
+        return !(e && e[0] == '0');
+    }();
+    // the quad form where the staged form would not fill the chip (latency-bound: batch 1, small layers)
+    bool fits = rro_quad && a.N % 16 == 0 && (a.N + kRroBS - 1) / kRroBS * a.crt.k * B <= num_cus();
+    for (int j = 0; j < a.crt.k; ++j) fits = fits && a.crt.n[j] <= 128;  // the LDS images hold 128 components
+    if (fits) {
+        hipLaunchKernelGGL(k_rescale_relu_out_q, dim3(static_cast<unsigned>((a.N + kRroQE - 1) / kRroQE), a.crt.k, B),
+                           dim3(256), 0, st, a, sa, x, y, gtab, etab, mc);
+        return;
+    }
     if (rro_stage && stage_ok(a.N, kRroBS)) {
         hipLaunchKernelGGL(k_rescale_relu_out_s, dim3(static_cast<unsigned>((a.N + kRroBS - 1) / kRroBS), a.crt.k, B),
                            dim3(kRroBS), 0, st, a, sa, x, y, gtab, etab, mc, g.te0, g.rk);

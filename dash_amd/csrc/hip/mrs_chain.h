@@ -577,36 +577,11 @@ __device__ __forceinline__ uint32_t quad_sum_bytes(uint32_t v) {
     const uint32_t s = v + static_cast<uint32_t>(__builtin_amdgcn_mov_dpp(static_cast<int>(v), 0xB1, 0xF, 0xF, false));
     return s + static_cast<uint32_t>(__builtin_amdgcn_mov_dpp(static_cast<int>(s), 0x4E, 0xF, 0xF, false));
 }
-// u128 sum over the quad, every lane gets it (two DPP rounds on the four 32-bit words, carries by the adds)
-template <int CTRL>
-__device__ __forceinline__ u128 dpp128(u128 v) {
-    const uint32_t w0 = static_cast<uint32_t>(__builtin_amdgcn_mov_dpp(static_cast<int>(static_cast<uint32_t>(v)), CTRL, 0xF, 0xF, false));
-    const uint32_t w1 = static_cast<uint32_t>(__builtin_amdgcn_mov_dpp(static_cast<int>(static_cast<uint32_t>(v >> 32)), CTRL, 0xF, 0xF, false));
-    const uint32_t w2 = static_cast<uint32_t>(__builtin_amdgcn_mov_dpp(static_cast<int>(static_cast<uint32_t>(v >> 64)), CTRL, 0xF, 0xF, false));
-    const uint32_t w3 = static_cast<uint32_t>(__builtin_amdgcn_mov_dpp(static_cast<int>(static_cast<uint32_t>(v >> 96)), CTRL, 0xF, 0xF, false));
-    return (static_cast<u128>((static_cast<uint64_t>(w3) << 32) | w2) << 64) | ((static_cast<uint64_t>(w1) << 32) | w0);
-}
-__device__ __forceinline__ u128 quad_sum128(u128 v) {
-    v += dpp128<0xB1>(v);
-    return v + dpp128<0x4E>(v);
-}
 // Chunk-split key (positions with at most kQSplit payload streams): the key's base-q chunks are dealt over the
 // quad, lane g taking chunks 4j + g, so each lane walks a quarter of the digits; every lane runs the streams'
 // chunk divisions (cheap next to the digit walk) and keeps its own chunk's value, and the lanes' partial keys
 // sum over the quad. The stream-split form (below) replicates the whole digit walk on every lane.
-constexpr int kQSplit = 3;  // compiled for positions I <= kQSplit; the launch picks the limit (default all of them)
-struct QPow {  // D^1 .. D^4 of a modulus (D = q^c < 2^31): lane g's first chunk weight and the group step
-    u128 d1, d2, d3, d4;
-    __device__ __forceinline__ void init(const ModC& m) {
-        d1 = static_cast<u128>(m.D);
-        d2 = d1 * d1;
-        d3 = d2 * d1;
-        d4 = d2 * d2;
-    }
-    __device__ __forceinline__ u128 first(int g) const {
-        return g == 0 ? static_cast<u128>(1) : (g == 1 ? d1 : (g == 2 ? d2 : d3));
-    }
-};
+constexpr int kQSplit = 5;  // compiled for positions I <= kQSplit; the launch picks the limit (DASH_MRS_QSPLIT)
 template <int NSTR>
 __device__ __forceinline__ u128 quad_key_split(const uint8_t* Ls, const ModC& m, int g, bool valid, u128 (&Q)[NSTR > 0 ? NSTR : 1]) {
     const int n = static_cast<int>(m.n);
