@@ -1090,6 +1090,17 @@ __global__ __launch_bounds__(kRroBS) void k_rescale_relu_out_s(MrsArgs a, SignAr
 // rescaled label's partial keys are summed over the quad. The per-lane forms walk all n digits of three streams
 // serially on one lane (~50 us per launch whatever the layer size at batch 1, r05 timeline).
 constexpr int kRroQE = 64;  // elements per block (256 threads)
+// the quad output forms where a lane-per-element launch would not fill the chip (latency-bound: batch 1, small
+// layers); DASH_RRO_QUAD=0 keeps the lane-per-element forms (A/B)
+static inline bool out_quad_fits(const MrsArgs& a, int B) {
+    static const bool on = [] {
+        const char* e = std::getenv("DASH_RRO_QUAD");
+        return !(e && e[0] == '0');
+    }();
+    bool fits = on && a.N % 16 == 0 && (a.N + 255) / 256 * a.crt.k * B <= num_cus();
+    for (int j = 0; j < a.crt.k; ++j) fits = fits && a.crt.n[j] <= 128;  // the LDS images hold 128 components
+    return fits;
+}
 __global__ __launch_bounds__(256) void k_rescale_relu_out_q(MrsArgs a, SignArgs sa, Act x, Act y, const u128* gtab,
                                                            const u128* etab, const ModC* mc) {
     __shared__ __attribute__((aligned(16))) uint8_t sL[128 * kRroQE];  // L_j -> Y_j in place
@@ -1242,14 +1253,7 @@ void launch_rescale_relu_out(const MrsArgs& a, const SignArgs& sa, const Act& x,
         const char* e = std::getenv("DASH_RRO_STAGE");
         return !(e && e[0] == '0');
     }();
-    static const bool rro_quad = [] {  // DASH_RRO_QUAD=0: no quad form (A/B)
-        const char* e = std::getenv("DASH_RRO_QUAD");
-        return !(e && e[0] == '0');
-    }();
-    // the quad form where the staged form would not fill the chip (latency-bound: batch 1, small layers)
-    bool fits = rro_quad && a.N % 16 == 0 && (a.N + kRroBS - 1) / kRroBS * a.crt.k * B <= num_cus();
-    for (int j = 0; j < a.crt.k; ++j) fits = fits && a.crt.n[j] <= 128;  // the LDS images hold 128 components
-    if (fits) {
+    if (out_quad_fits(a, B)) {
         hipLaunchKernelGGL(k_rescale_relu_out_q, dim3(static_cast<unsigned>((a.N + kRroQE - 1) / kRroQE), a.crt.k, B),
                            dim3(256), 0, st, a, sa, x, y, gtab, etab, mc);
         return;
@@ -1318,6 +1322,75 @@ void launch_relu_joint(const SignArgs& sa, const Act& x, const Act& y, const u12
     launch_relu_mult(sa, x, y, gtab, etab, mc, st);
 }
 
+// Quad form of k_rescale_mrs_out for latency-bound launches (batch 1, small layers): four lanes per (element,
+// residue), the payload's chunks dealt over the quad (as k_rescale_relu_out_q's first pass), rows staged and
+// stored as 16-byte units.
+__global__ __launch_bounds__(256) void k_rescale_mrs_out_q(MrsArgs a, Act x, const ModC* mc) {
+    __shared__ __attribute__((aligned(16))) uint8_t sL[128 * kRroQE];
+    const int j = blockIdx.y, b = blockIdx.z;
+    const int64_t N = a.N;  // N % 16 == 0 (host-checked)
+    const int k = a.crt.k;
+    const ModC m = mc[a.crt.p[j]];
+    const int n = static_cast<int>(m.n);
+    const uint32_t q = m.q;
+    const int tid = static_cast<int>(threadIdx.x);
+    const int el = tid >> 2, g = tid & 3;
+    const uint32_t inv = static_cast<uint32_t>(a.sinv[j]);
+    act_t* L = x.p[j] + static_cast<int64_t>(b) * n * N;
+    for (int64_t e0 = static_cast<int64_t>(blockIdx.x) * kRroQE; e0 < N; e0 += static_cast<int64_t>(gridDim.x) * kRroQE) {
+        const int64_t e = min(e0 + el, N - 1);
+        const u128 P = a.pf[(static_cast<int64_t>(b) * k + j) * N + e];
+        __syncthreads();
+        if (j != 0) {
+            for (int xu = tid; xu < n * (kRroQE / 16); xu += 256) {
+                const int row = xu / (kRroQE / 16), part = xu % (kRroQE / 16);
+                const int64_t ee = e0 + 16 * part;
+                if (ee < N) *reinterpret_cast<uint4*>(sL + row * kRroQE + 16 * part) =
+                    *reinterpret_cast<const uint4*>(L + static_cast<int64_t>(row) * N + ee);
+            }
+        }
+        __syncthreads();
+        if (m.bits) {
+            const int bb = static_cast<int>(m.bits), cpl = (n + 3) >> 2;
+            for (int t = 0; t < cpl; ++t) {
+                const int idx = g * cpl + t;
+                if (idx >= n) break;
+                const uint32_t pd = static_cast<uint32_t>(P >> (bb * idx)) & (q - 1);
+                sL[idx * kRroQE + el] =
+                    static_cast<uint8_t>(j == 0 ? pd : modq(static_cast<uint32_t>(sL[idx * kRroQE + el]) * inv + pd, m));
+            }
+        } else {
+            const int c = static_cast<int>(m.c), nch = (n + c - 1) / c;
+            u128 Q = P;
+            for (int jj = 0; 4 * jj < nch; ++jj) {
+                uint32_t mine = 0;
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    if (4 * jj + u >= nch) break;
+                    const uint32_t r = divmod128(Q, m);
+                    mine = u == g ? r : mine;
+                }
+                const int i = 4 * jj + g;
+                for (int t = 0; t < c; ++t) {
+                    const int idx = i * c + t;
+                    const uint32_t pd = chunk_digit(mine, m);
+                    if (idx < n)
+                        sL[idx * kRroQE + el] = static_cast<uint8_t>(
+                            j == 0 ? pd : modq(static_cast<uint32_t>(sL[idx * kRroQE + el]) * inv + pd, m));  // < p^2 + p
+                }
+            }
+        }
+        __syncthreads();
+        for (int xu = tid; xu < n * (kRroQE / 16); xu += 256) {
+            const int row = xu / (kRroQE / 16), prt = xu % (kRroQE / 16);
+            const int64_t ee = e0 + 16 * prt;
+            if (ee < N)
+                *reinterpret_cast<uint4*>(L + static_cast<int64_t>(row) * N + ee) =
+                    *reinterpret_cast<const uint4*>(sL + row * kRroQE + 16 * prt);
+        }
+    }
+}
+
 void launch_rescale_mrs(const MrsArgs& a, const Act& x, int B, const ModC* mc, const AesGlobals& g, hipStream_t st,
                         bool chain_only) {
     dispatch_mrs_chain(a, x, B, mc, g, st);
@@ -1327,6 +1400,9 @@ void launch_rescale_mrs(const MrsArgs& a, const Act& x, int B, const ModC* mc, c
                            g.te0, g.rk);
     else if (a.mode == 2)
         hipLaunchKernelGGL(k_rescale_mrs_out_hash, AES_LAUNCH(a.N, a.crt.k, B), kAesLds, st, a, x, mc, g.te0, g.rk);
+    else if (out_quad_fits(a, B))
+        hipLaunchKernelGGL(k_rescale_mrs_out_q, dim3(static_cast<unsigned>((a.N + kRroQE - 1) / kRroQE), a.crt.k, B),
+                           dim3(256), 0, st, a, x, mc);
     else
         hipLaunchKernelGGL(k_rescale_mrs_out, dim3(static_cast<unsigned>((a.N + 255) / 256), a.crt.k, B), dim3(256), 0,
                            st, a, x, mc);
