@@ -1090,14 +1090,45 @@ __global__ __launch_bounds__(kRroBS) void k_rescale_relu_out_s(MrsArgs a, SignAr
 // rescaled label's partial keys are summed over the quad. The per-lane forms walk all n digits of three streams
 // serially on one lane (~50 us per launch whatever the layer size at batch 1, r05 timeline).
 constexpr int kRroQE = 64;  // elements per block (256 threads)
+// rows [0, n) of kRroQE elements from e0: 16-byte units when N % 16 == 0, bytes otherwise (tails, tiny layers)
+__device__ __forceinline__ void quad_stage_rows(uint8_t* S, const act_t* L, int64_t N, int64_t e0, int n) {
+    if (N % 16 == 0) {
+        for (int xu = threadIdx.x; xu < n * (kRroQE / 16); xu += blockDim.x) {
+            const int row = xu / (kRroQE / 16), part = xu % (kRroQE / 16);
+            const int64_t ee = e0 + 16 * part;
+            if (ee < N) *reinterpret_cast<uint4*>(S + row * kRroQE + 16 * part) =
+                *reinterpret_cast<const uint4*>(L + static_cast<int64_t>(row) * N + ee);
+        }
+    } else {
+        for (int xb = threadIdx.x; xb < n * kRroQE; xb += blockDim.x) {
+            const int row = xb / kRroQE, c = xb % kRroQE;
+            if (e0 + c < N) S[xb] = L[static_cast<int64_t>(row) * N + e0 + c];
+        }
+    }
+}
+__device__ __forceinline__ void quad_store_rows(act_t* L, const uint8_t* S, int64_t N, int64_t e0, int n) {
+    if (N % 16 == 0) {
+        for (int xu = threadIdx.x; xu < n * (kRroQE / 16); xu += blockDim.x) {
+            const int row = xu / (kRroQE / 16), part = xu % (kRroQE / 16);
+            const int64_t ee = e0 + 16 * part;
+            if (ee < N) *reinterpret_cast<uint4*>(L + static_cast<int64_t>(row) * N + ee) =
+                *reinterpret_cast<const uint4*>(S + row * kRroQE + 16 * part);
+        }
+    } else {
+        for (int xb = threadIdx.x; xb < n * kRroQE; xb += blockDim.x) {
+            const int row = xb / kRroQE, c = xb % kRroQE;
+            if (e0 + c < N) L[static_cast<int64_t>(row) * N + e0 + c] = S[xb];
+        }
+    }
+}
 // the quad output forms where a lane-per-element launch would not fill the chip (latency-bound: batch 1, small
-// layers); DASH_RRO_QUAD=0 keeps the lane-per-element forms (A/B)
+// layers); DASH_RRO_QUAD=0 keeps the lane-per-element forms, =2 takes the quad forms at every size (A/B)
 static inline bool out_quad_fits(const MrsArgs& a, int B) {
-    static const bool on = [] {
+    static const int mode = [] {
         const char* e = std::getenv("DASH_RRO_QUAD");
-        return !(e && e[0] == '0');
+        return e ? std::atoi(e) : 1;
     }();
-    bool fits = on && a.N % 16 == 0 && (a.N + 255) / 256 * a.crt.k * B <= num_cus();
+    bool fits = mode != 0 && (mode == 2 || (a.N + 255) / 256 * a.crt.k * B <= num_cus());
     for (int j = 0; j < a.crt.k; ++j) fits = fits && a.crt.n[j] <= 128;  // the LDS images hold 128 components
     return fits;
 }
@@ -1106,7 +1137,7 @@ __global__ __launch_bounds__(256) void k_rescale_relu_out_q(MrsArgs a, SignArgs 
     __shared__ __attribute__((aligned(16))) uint8_t sL[128 * kRroQE];  // L_j -> Y_j in place
     __shared__ __attribute__((aligned(16))) uint8_t sO[128 * kRroQE];  // ReLU outputs
     const int j = blockIdx.y, b = blockIdx.z;
-    const int64_t N = a.N;  // N % 16 == 0 (host-checked)
+    const int64_t N = a.N;
     const int k = a.crt.k;
     const int p = a.crt.p[j];
     const ModC m = mc[p];
@@ -1130,14 +1161,7 @@ __global__ __launch_bounds__(256) void k_rescale_relu_out_q(MrsArgs a, SignArgs 
         const u128 P = a.pf[bke];
         const u128 Eraw = E3[cS];
         __syncthreads();  // the previous tile's row stores have read the images
-        if (j != 0) {
-            for (int xu = tid; xu < n * (kRroQE / 16); xu += 256) {
-                const int row = xu / (kRroQE / 16), part = xu % (kRroQE / 16);
-                const int64_t ee = e0 + 16 * part;
-                if (ee < N) *reinterpret_cast<uint4*>(sL + row * kRroQE + 16 * part) =
-                    *reinterpret_cast<const uint4*>(L + static_cast<int64_t>(row) * N + ee);
-            }
-        }
+        if (j != 0) quad_stage_rows(sL, L, N, e0, n);
         __syncthreads();
         // digit 0 first (every lane): the garbler half gate's row gather overlaps the walk
         u128 Graw;
@@ -1235,15 +1259,8 @@ __global__ __launch_bounds__(256) void k_rescale_relu_out_q(MrsArgs a, SignArgs 
             }
         }
         __syncthreads();
-        for (int xu = tid; xu < n * (kRroQE / 16); xu += 256) {
-            const int row = xu / (kRroQE / 16), prt = xu % (kRroQE / 16);
-            const int64_t ee = e0 + 16 * prt;
-            if (ee >= N) continue;
-            *reinterpret_cast<uint4*>(L + static_cast<int64_t>(row) * N + ee) =
-                *reinterpret_cast<const uint4*>(sL + row * kRroQE + 16 * prt);
-            *reinterpret_cast<uint4*>(Yo + static_cast<int64_t>(row) * N + ee) =
-                *reinterpret_cast<const uint4*>(sO + row * kRroQE + 16 * prt);
-        }
+        quad_store_rows(L, sL, N, e0, n);
+        quad_store_rows(Yo, sO, N, e0, n);
     }
 }
 
@@ -1328,7 +1345,7 @@ void launch_relu_joint(const SignArgs& sa, const Act& x, const Act& y, const u12
 __global__ __launch_bounds__(256) void k_rescale_mrs_out_q(MrsArgs a, Act x, const ModC* mc) {
     __shared__ __attribute__((aligned(16))) uint8_t sL[128 * kRroQE];
     const int j = blockIdx.y, b = blockIdx.z;
-    const int64_t N = a.N;  // N % 16 == 0 (host-checked)
+    const int64_t N = a.N;
     const int k = a.crt.k;
     const ModC m = mc[a.crt.p[j]];
     const int n = static_cast<int>(m.n);
@@ -1341,14 +1358,7 @@ __global__ __launch_bounds__(256) void k_rescale_mrs_out_q(MrsArgs a, Act x, con
         const int64_t e = min(e0 + el, N - 1);
         const u128 P = a.pf[(static_cast<int64_t>(b) * k + j) * N + e];
         __syncthreads();
-        if (j != 0) {
-            for (int xu = tid; xu < n * (kRroQE / 16); xu += 256) {
-                const int row = xu / (kRroQE / 16), part = xu % (kRroQE / 16);
-                const int64_t ee = e0 + 16 * part;
-                if (ee < N) *reinterpret_cast<uint4*>(sL + row * kRroQE + 16 * part) =
-                    *reinterpret_cast<const uint4*>(L + static_cast<int64_t>(row) * N + ee);
-            }
-        }
+        if (j != 0) quad_stage_rows(sL, L, N, e0, n);
         __syncthreads();
         if (m.bits) {
             const int bb = static_cast<int>(m.bits), cpl = (n + 3) >> 2;
@@ -1381,13 +1391,7 @@ __global__ __launch_bounds__(256) void k_rescale_mrs_out_q(MrsArgs a, Act x, con
             }
         }
         __syncthreads();
-        for (int xu = tid; xu < n * (kRroQE / 16); xu += 256) {
-            const int row = xu / (kRroQE / 16), prt = xu % (kRroQE / 16);
-            const int64_t ee = e0 + 16 * prt;
-            if (ee < N)
-                *reinterpret_cast<uint4*>(L + static_cast<int64_t>(row) * N + ee) =
-                    *reinterpret_cast<const uint4*>(sL + row * kRroQE + 16 * prt);
-        }
+        quad_store_rows(L, sL, N, e0, n);
     }
 }
 
