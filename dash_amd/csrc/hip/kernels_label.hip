@@ -4,6 +4,7 @@
 #include <algorithm>
 
 #include "launch.h"
+#include "fetch.h"
 
 namespace dash {
 namespace dev {
@@ -234,6 +235,31 @@ __global__ __launch_bounds__(256) void k_narrow(const int16_t* __restrict__ in, 
 void launch_narrow(const int16_t* in, act_t* out, int64_t n, hipStream_t st) {
     const unsigned nb = static_cast<unsigned>(std::max<int64_t>(1, std::min<int64_t>((n + 255) / 256, 16384)));
     hipLaunchKernelGGL(k_narrow, dim3(nb), dim3(256), 0, st, in, out, n);
+}
+
+// Output labels of every residue written straight into mapped pinned host memory by one launch, instead of one
+// copy-engine transfer per residue (k = 7 D2H copies were ~35 us of a 1.5 ms batch-1 latency, r05 timeline).
+// grid (blocks, k); 16-byte stores where both sides are 16-byte aligned. The stream synchronize after the launch
+// makes the stores visible to the host (system-scope release at the kernel's end, fenced here as well).
+__global__ __launch_bounds__(256) void k_fetch_res(FetchRes a) {
+    const int j = blockIdx.y;
+    const int64_t nb = a.bytes[j];
+    const uint8_t* s = static_cast<const uint8_t*>(a.in[j]);
+    uint8_t* d = static_cast<uint8_t*>(a.out[j]);
+    const int64_t stride = static_cast<int64_t>(gridDim.x) * 256;
+    const int64_t t0 = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;
+    const bool al = ((reinterpret_cast<uintptr_t>(s) | reinterpret_cast<uintptr_t>(d)) & 15u) == 0;
+    const int64_t n16 = al ? nb / 16 : 0;
+    for (int64_t i = t0; i < n16; i += stride)
+        reinterpret_cast<uint4*>(d)[i] = reinterpret_cast<const uint4*>(s)[i];
+    for (int64_t i = n16 * 16 + t0; i < nb; i += stride) d[i] = s[i];
+    __threadfence_system();
+}
+void launch_fetch_res(const FetchRes& a, hipStream_t st) {
+    int64_t mx = 1;
+    for (int j = 0; j < a.k; ++j) mx = std::max(mx, a.bytes[j]);
+    const unsigned nb = static_cast<unsigned>(std::min<int64_t>((mx / 16 + 255) / 256 + 1, 64));
+    hipLaunchKernelGGL(k_fetch_res, dim3(nb, static_cast<unsigned>(a.k)), dim3(256), 0, st, a);
 }
 
 // Online message #1 encoded on the device by the garbler (core.h lab_affine per component, reference

@@ -20,6 +20,7 @@
 #include "../layers.h"
 #include "host_util.h"
 #include "launch.h"
+#include "fetch.h"
 
 #include <rocprofiler-sdk-roctx/roctx.h>
 
@@ -264,13 +265,34 @@ class HipEvaluator {
         }
         return r;
     }
-    void fetch_outputs(hipStream_t st) {
-        bind_device(dev_, st, "HipEvaluator.fetch_outputs");
+    // every residue's output labels -> out_stage_: one k_fetch_res launch into the mapped pinned buffers for small
+    // outputs (one launch instead of k copy-engine transfers), copies otherwise or with DASH_FETCH_KERNEL=0 (A/B)
+    void stage_outputs(hipStream_t st) {
+        static const bool kern = [] {
+            const char* e = std::getenv("DASH_FETCH_KERNEL");
+            return !(e && e[0] == '0');
+        }();
+        FetchRes f{};
+        f.k = k_;
+        int64_t total = 0;
         for (int j = 0; j < k_; ++j) {
-            const int n = nr_comps(out_mod_[j]);
-            HIPCHECK(hipMemcpyAsync(out_stage_[j], final_.p[j], sizeof(act_t) * B_ * n * Nout_, hipMemcpyDeviceToHost, st));
+            f.in[j] = final_.p[j];
+            f.out[j] = out_stage_dev_[j];
+            f.bytes[j] = static_cast<int64_t>(sizeof(act_t)) * B_ * nr_comps(out_mod_[j]) * Nout_;
+            total += f.bytes[j];
+        }
+        if (kern && total <= (4 << 20) && out_stage_mapped_) {
+            launch_fetch_res(f, st);
+            HIPCHECK(hipGetLastError());
+        } else {
+            for (int j = 0; j < k_; ++j)
+                HIPCHECK(hipMemcpyAsync(out_stage_[j], final_.p[j], f.bytes[j], hipMemcpyDeviceToHost, st));
         }
         HIPCHECK(hipStreamSynchronize(st));
+    }
+    void fetch_outputs(hipStream_t st) {
+        bind_device(dev_, st, "HipEvaluator.fetch_outputs");
+        stage_outputs(st);
     }
     int crt_size() const { return k_; }
     i64 output_size() const { return Nout_; }
@@ -327,11 +349,7 @@ class HipEvaluator {
     std::vector<CrtLabels> get_outputs(hipStream_t st) {
         bind_device(dev_, st, "HipEvaluator.get_outputs");
         std::vector<CrtLabels> out(B_);
-        for (int j = 0; j < k_; ++j) {
-            const int q = out_mod_[j], n = nr_comps(q);
-            HIPCHECK(hipMemcpyAsync(out_stage_[j], final_.p[j], sizeof(act_t) * B_ * n * Nout_, hipMemcpyDeviceToHost, st));
-        }
-        HIPCHECK(hipStreamSynchronize(st));
+        stage_outputs(st);
         for (int b = 0; b < B_; ++b)
             for (int j = 0; j < k_; ++j) {
                 const int q = out_mod_[j];
@@ -656,6 +674,8 @@ class HipEvaluator {
     Act cur_act_{};
     std::vector<int16_t*> in_stage_;
     std::vector<act_t*> out_stage_;
+    std::vector<void*> out_stage_dev_;  // device addresses of the mapped out_stage_ buffers
+    bool out_stage_mapped_ = true;
     int16_t* in16_dev_[kMaxRes] = {};  // device int16 copy of the host-encoded inputs (uncompressed input path)
     u128* in_comp_stage_ = nullptr;
     bool use_graph_ = [] {
@@ -1464,6 +1484,12 @@ void HipEvaluator::build() {
         HIPCHECK(hipHostMalloc(reinterpret_cast<void**>(&p), sizeof(act_t) * B_ * nr_comps(mods[j]) * std::max<i64>(Nout_, 1)));
         host_allocs_.push_back(p);
         out_stage_.push_back(p);
+        void* dp = nullptr;
+        if (hipHostGetDevicePointer(&dp, p, 0) != hipSuccess || !dp) {
+            (void)hipGetLastError();
+            out_stage_mapped_ = false;
+        }
+        out_stage_dev_.push_back(dp);
     }
     finish_small();
     HIPCHECK(hipDeviceSynchronize());
