@@ -615,6 +615,10 @@ __global__ __launch_bounds__(kPB, 4) void k_hash_jobs(Ctx c, Gadget g, In in, co
 }
 
 // ---- uniform-offset compression: compress(x + a) for a per-lane label x and a wave-uniform row a
+#ifndef DASH_GG_ALIGNED_GROUPS
+#define DASH_GG_ALIGNED_GROUPS 1  // A/B knob: chunk-aligned digit groups (compress_xa_g); 0 = runtime groups only
+#endif
+constexpr bool kAlignedGroups = DASH_GG_ALIGNED_GROUPS != 0;
 typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ u16x2 as_u16x2(uint32_t w) { return __builtin_bit_cast(u16x2, w); }
 __device__ __forceinline__ uint32_t as_u32(u16x2 v) { return __builtin_bit_cast(uint32_t, v); }
@@ -697,7 +701,66 @@ __device__ __forceinline__ u128 compress_xa_t(LRef x, const uint32_t* a, const M
     d0 = dlow;
     return C;
 }
+// Chunk-aligned digit groups: G | 8 digits with q^G <= 2^24 (G = 8 for q <= 8, 4 for q <= 64). The groups then
+// start at the chunk boundaries, so after the digit loop is unrolled the flush points are compile-time positions,
+// and only the top chunk can hold padding components (masked once, four ANDs). The digit loop carries no scalar
+// bookkeeping: the runtime-group form above issued more SALU than VALU instructions in k_bank (1.26 G SALU vs
+// 0.99 G VALU per 4 MiniONN GCs, profiles/r05_garble_pmc_hardened_4gc.txt), and the CU's one scalar unit serves
+// all four SIMDs. Same integer as the runtime-group form (exact Horner, any grouping).
+__device__ __forceinline__ void top_chunk_mask(uint32_t (&t)[4], int valid) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+        t[u] &= (2 * u < valid ? 0xffffu : 0u) | (2 * u + 1 < valid ? 0xffff0000u : 0u);
+}
+template <int G>
+__device__ __forceinline__ u128 compress_xa_g(LRef x, const uint32_t* a, const ModC& m, uint32_t& d0) {
+    const int nc = static_cast<int>(chunks_of(static_cast<int>(m.n)));
+    const uint32_t q = m.q;
+    uint32_t D = 1;
+#pragma unroll
+    for (int i = 0; i < G; ++i) D *= q;
+    const u16x2 qq = {static_cast<unsigned short>(q), static_cast<unsigned short>(q)};
+    u128 C = 0;
+    uint32_t dlow = 0;
+    for (int c0 = nc - 1; c0 >= 0; c0 -= kLd) {
+        u32x4a xv[kLd], av[kLd];
+#pragma unroll
+        for (int h = 0; h < kLd; ++h) {
+            if (c0 - h >= 0) {
+                xv[h] = ld_chunk(x, c0 - h);
+                av[h] = *reinterpret_cast<const u32x4a*>(a + 4 * (c0 - h));
+            }
+        }
+#pragma unroll
+        for (int h = 0; h < kLd; ++h) {
+            if (c0 - h < 0) break;
+            uint32_t t[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const u16x2 sm = as_u16x2(xv[h][u]) + as_u16x2(av[h][u]);
+                t[u] = as_u32(__builtin_elementwise_min(sm, sm - qq));
+            }
+            const int valid = static_cast<int>(m.n) - 8 * (c0 - h);
+            if (valid < 8) top_chunk_mask(t, valid);  // uniform: the top chunk only
+            uint32_t v = 0;
+#pragma unroll
+            for (int k = 7; k >= 0; --k) {
+                const uint32_t d = (k & 1) ? (t[k >> 1] >> 16) : (t[k >> 1] & 0xffffu);
+                v = __umul24(v, q) + d;
+                if (k % G == 0) {
+                    C = mad128_24(C, D, v);
+                    v = 0;
+                }
+            }
+            dlow = t[0] & 0xffffu;
+        }
+    }
+    d0 = dlow;
+    return C;
+}
 __device__ __forceinline__ u128 compress_xa(LRef x, const uint32_t* a, const ModC& m, uint32_t& d0) {
+    if (kAlignedGroups && m.q <= 8) return compress_xa_g<8>(x, a, m, d0);
+    if (kAlignedGroups && m.q <= 64) return compress_xa_g<4>(x, a, m, d0);
     return m.bits ? compress_xa_t<true>(x, a, m, d0) : compress_xa_t<false>(x, a, m, d0);
 }
 
@@ -772,9 +835,71 @@ __device__ __forceinline__ void compress_xa2_t(LRef x, const uint32_t* a1, const
     d01 = l1;
     d02 = l2;
 }
+// compress_xa2_t with chunk-aligned groups (compress_xa_g)
+template <int G>
+__device__ __forceinline__ void compress_xa2_g(LRef x, const uint32_t* a1, const uint32_t* a2, const ModC& m, u128& C1,
+                                               u128& C2, uint32_t& d01, uint32_t& d02) {
+    const int nc = static_cast<int>(chunks_of(static_cast<int>(m.n)));
+    const uint32_t q = m.q;
+    uint32_t D = 1;
+#pragma unroll
+    for (int i = 0; i < G; ++i) D *= q;
+    const u16x2 qq = {static_cast<unsigned short>(q), static_cast<unsigned short>(q)};
+    C1 = 0;
+    C2 = 0;
+    uint32_t l1 = 0, l2 = 0;
+    constexpr int kL2 = 2;
+    for (int c0 = nc - 1; c0 >= 0; c0 -= kL2) {
+        u32x4a xv[kL2], av[kL2], bv[kL2];
+#pragma unroll
+        for (int h = 0; h < kL2; ++h) {
+            if (c0 - h >= 0) {
+                xv[h] = ld_chunk(x, c0 - h);
+                av[h] = *reinterpret_cast<const u32x4a*>(a1 + 4 * (c0 - h));
+                bv[h] = *reinterpret_cast<const u32x4a*>(a2 + 4 * (c0 - h));
+            }
+        }
+#pragma unroll
+        for (int h = 0; h < kL2; ++h) {
+            if (c0 - h < 0) break;
+            uint32_t t1[4], t2[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const u16x2 s1 = as_u16x2(xv[h][u]) + as_u16x2(av[h][u]);
+                const u16x2 s2 = as_u16x2(xv[h][u]) + as_u16x2(bv[h][u]);
+                t1[u] = as_u32(__builtin_elementwise_min(s1, s1 - qq));
+                t2[u] = as_u32(__builtin_elementwise_min(s2, s2 - qq));
+            }
+            const int valid = static_cast<int>(m.n) - 8 * (c0 - h);
+            if (valid < 8) {
+                top_chunk_mask(t1, valid);
+                top_chunk_mask(t2, valid);
+            }
+            uint32_t v1 = 0, v2 = 0;
+#pragma unroll
+            for (int k = 7; k >= 0; --k) {
+                const uint32_t e1 = (k & 1) ? (t1[k >> 1] >> 16) : (t1[k >> 1] & 0xffffu);
+                const uint32_t e2 = (k & 1) ? (t2[k >> 1] >> 16) : (t2[k >> 1] & 0xffffu);
+                v1 = __umul24(v1, q) + e1;
+                v2 = __umul24(v2, q) + e2;
+                if (k % G == 0) {
+                    C1 = mad128_24(C1, D, v1);
+                    C2 = mad128_24(C2, D, v2);
+                    v1 = v2 = 0;
+                }
+            }
+            l1 = t1[0] & 0xffffu;
+            l2 = t2[0] & 0xffffu;
+        }
+    }
+    d01 = l1;
+    d02 = l2;
+}
 __device__ __forceinline__ void compress_xa2(LRef x, const uint32_t* a1, const uint32_t* a2, const ModC& m, u128& C1,
                                              u128& C2, uint32_t& d01, uint32_t& d02) {
-    if (m.bits) compress_xa2_t<true>(x, a1, a2, m, C1, C2, d01, d02);
+    if (kAlignedGroups && m.q <= 8) compress_xa2_g<8>(x, a1, a2, m, C1, C2, d01, d02);
+    else if (kAlignedGroups && m.q <= 64) compress_xa2_g<4>(x, a1, a2, m, C1, C2, d01, d02);
+    else if (m.bits) compress_xa2_t<true>(x, a1, a2, m, C1, C2, d01, d02);
     else compress_xa2_t<false>(x, a1, a2, m, C1, C2, d01, d02);
 }
 
