@@ -350,6 +350,9 @@ static_assert(kConvFW == 16 || kConvFW == 32, "conv: 16 or 32 filters per wave")
 #ifndef DASH_CONV_CLAMP
 #define DASH_CONV_CLAMP 1  // edge items of the band staging as clamped 8-B loads (0: byte-wise, A/B)
 #endif
+#ifndef DASH_CONV_BRANCHFREE
+#define DASH_CONV_BRANCHFREE 1  // every staging item as one clamped 8-B load + shift + mask (0: full / edge paths, A/B)
+#endif
 // UR: tap-unrolled band (ConvArgs::ur), a separate instantiation so the channel-chunked staging keeps its
 // registers and code
 template <int KSC, bool UR>
@@ -509,6 +512,35 @@ __global__ __launch_bounds__(256) void k_conv_img2(ConvArgs a, Act x, Act y, int
         const int iy = iy0 + yq;
         const bool rowin = iy >= 0 && iy < a.H;
         const int ix0 = xo * 8 - a.pw;
+        if (DASH_CONV_BRANCHFREE && a.W >= 8) {  // (uniform)
+            // every item (full, edge, padding row, channel past C) as one in-bounds 8-B load at a clamped row /
+            // column / channel, shifted into place and masked: no per-lane path divergence. The branching form
+            // ran both the full and the edge path in most waves (the edge columns of a 32-wide image are 2 of
+            // its 5 eight-column items) and its exec-mask bookkeeping made the conv issue about as many SALU
+            // as VALU instructions (profiles/r05_minionn_b160_headline_pmc.txt)
+            const int iyc = min(max(iy, 0), a.H - 1);
+            const int s0 = min(max(ix0, 0), a.W - 8);
+            const int sh = ix0 - s0;  // > 0: right edge, < 0: left padding
+            const int lo = max(0, -ix0), hi = min(8, a.W - ix0);  // valid bytes [lo, hi)
+            const uint64_t mrow = (rowin && hi > lo)
+                                      ? (hi >= 8 ? ~0ull : (1ull << (8 * hi)) - 1ull) & ~((1ull << (8 * lo)) - 1ull)
+                                      : 0ull;
+            const uint64_t padr = static_cast<uint64_t>(padb) * 0x0101010101010101ull;
+            const act_t* rb = X + static_cast<int64_t>(iyc) * a.W + s0;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int ci = c4 * 4 + q;
+                const bool cin = ci < a.C;
+                uint64_t t = *reinterpret_cast<const uint64_t*>(rb + static_cast<int64_t>(cin ? ci : a.C - 1) * HW);
+                t = sh >= 8 || sh <= -8 ? 0ull : (sh >= 0 ? t >> (8 * sh) : t << (-8 * sh));
+                const uint32_t t0 = static_cast<uint32_t>(t), t1 = static_cast<uint32_t>(t >> 32);
+                const uint64_t c = (static_cast<uint64_t>(rawx ? t1 : center4(t1)) << 32) | (rawx ? t0 : center4(t0));
+                const uint64_t v = cin ? (c & mrow) | (padr & ~mrow) : 0ull;  // channels past C: zero operands
+                raw[q][0] = static_cast<uint32_t>(v);
+                raw[q][1] = static_cast<uint32_t>(v >> 32);
+            }
+            return;
+        }
         const bool full = rowin && ix0 >= 0 && ix0 + 8 <= a.W;
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
