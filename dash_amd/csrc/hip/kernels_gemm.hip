@@ -452,18 +452,22 @@ __global__ __launch_bounds__(256) void k_conv_img2(ConvArgs a, Act x, Act y, int
     // runtime divisions cost ~25 VALU each, 4 per item)
     const uint32_t mc4 = c4n > 1 ? 0xffffffffu / static_cast<uint32_t>(c4n) + 1u : 0u;
     const uint32_t mwo = WO > 1 ? 0xffffffffu / static_cast<uint32_t>(WO) + 1u : 0u;
+    // tap-unrolled staging: cq -> (tap, channel), tap -> (dy, dx) the same way (cq < 2^16)
+    const uint32_t muc = UR && a.uC > 1 ? 0xffffffffu / static_cast<uint32_t>(a.uC) + 1u : 0u;
+    const uint32_t mkw = UR && a.ukw > 1 ? 0xffffffffu / static_cast<uint32_t>(a.ukw) + 1u : 0u;
     // 8 operand bytes of one channel row (tap-unrolled staging): columns ix0 .. ix0 + 7 of `row` (width Wr)
     auto fetch8 = [&](const act_t* row, bool rowin, int ix0, int Wr, uint32_t (&o)[2]) {
         if (Wr >= 8) {
             const int s0 = min(max(ix0, 0), Wr - 8);
             const int sh = ix0 - s0;  // > 0: right edge, < 0: left padding
-            uint64_t t = 0;
-            if (rowin && sh > -8 && sh < 8) t = *reinterpret_cast<const uint64_t*>(row + s0);
+            // `row` is an in-bounds row (the caller clamps it): the load is unconditional, padding rows and
+            // columns are masked (no divergent load, DASH_CONV_BRANCHFREE)
+            uint64_t t = *reinterpret_cast<const uint64_t*>(row + s0);
             t = sh >= 8 || sh <= -8 ? 0ull : (sh >= 0 ? t >> (8 * sh) : t << (-8 * sh));
             const int lo = max(0, -ix0), hi = min(8, Wr - ix0);  // valid bytes [lo, hi)
-            uint64_t msk = 0;
-            if (rowin && hi > lo)
-                msk = (hi >= 8 ? ~0ull : (1ull << (8 * hi)) - 1ull) & ~((1ull << (8 * lo)) - 1ull);
+            const uint64_t msk = (rowin && hi > lo)
+                                     ? (hi >= 8 ? ~0ull : (1ull << (8 * hi)) - 1ull) & ~((1ull << (8 * lo)) - 1ull)
+                                     : 0ull;
             const uint32_t t0 = static_cast<uint32_t>(t), t1 = static_cast<uint32_t>(t >> 32);
             const uint64_t c = (static_cast<uint64_t>(rawx ? t1 : center4(t1)) << 32) | (rawx ? t0 : center4(t0));
             const uint64_t padr = static_cast<uint64_t>(padb) * 0x0101010101010101ull;
@@ -493,19 +497,25 @@ __global__ __launch_bounds__(256) void k_conv_img2(ConvArgs a, Act x, Act y, int
             // tap-unrolled band: channel cq of output position (row iy0 + yq, column xo * 8 + u) is input
             // channel ci at (row * sh - ph + dy, column - pw + dx), cq = (dy * kw + dx) * C + ci (unit column
             // stride: 8 consecutive input columns)
+            // (branch-free: channels past C read channel 0 and are zeroed, rows outside the image read a clamped
+            // row and are masked to padding; tap / channel by multiply-high instead of runtime divisions)
 #pragma unroll
             for (int q = 0; q < 4; ++q) {
                 const int cq = c4 * 4 + q;
-                if (cq >= a.C) {
-                    raw[q][0] = raw[q][1] = 0u;
-                    continue;
-                }
-                const int tap = cq / a.uC, ci = cq - tap * a.uC;
-                const int dy = tap / a.ukw, dx = tap - dy * a.ukw;
+                const bool cin = cq < a.C;
+                const uint32_t cqc = static_cast<uint32_t>(cin ? cq : 0);
+                const int tap = a.uC > 1 ? static_cast<int>(__umulhi(cqc, muc)) : static_cast<int>(cqc);
+                const int ci = static_cast<int>(cqc) - tap * a.uC;
+                const int dy = a.ukw > 1 ? static_cast<int>(__umulhi(static_cast<uint32_t>(tap), mkw)) : tap;
+                const int dx = tap - dy * a.ukw;
                 const int iy = (iy0 + yq) * a.ush - a.uph + dy;
                 const bool rowin = iy >= 0 && iy < a.uH;
-                const act_t* row = X + static_cast<int64_t>(ci) * HW + static_cast<int64_t>(iy) * a.uW;
-                fetch8(row, rowin, xo * 8 - a.upw + dx, a.uW, raw[q]);
+                const int iyc = min(max(iy, 0), a.uH - 1);
+                const act_t* row = X + static_cast<int64_t>(ci) * HW + static_cast<int64_t>(iyc) * a.uW;
+                uint32_t o[2];
+                fetch8(row, rowin, xo * 8 - a.upw + dx, a.uW, o);
+                raw[q][0] = cin ? o[0] : 0u;
+                raw[q][1] = cin ? o[1] : 0u;
             }
             return;
         }
