@@ -642,9 +642,13 @@ __global__ __launch_bounds__(256) void k_conv_img2(ConvArgs a, Act x, Act y, int
     const uint32_t mq = a.mq[j];
     const int sh24 = a.sh24[j];
     const uint32_t m24 = a.m24[j];
-    auto red = [&](int32_t acc, uint32_t add) -> uint32_t {
+    // the reduction form is a compile-time choice inside the column loop, which is instantiated for both and
+    // entered once (a runtime select per reduced value cost a scalar branch per output byte: the epilogue
+    // issued more instructions than the MFMA phase)
+    auto red = [&](auto u24, int32_t acc, uint32_t add) -> uint32_t {
         const uint32_t xv = static_cast<uint32_t>(acc) + add;
-        return sh24 >= 0 ? modq_conv24(xv, p, m24, sh24) : modq_conv(xv, static_cast<uint32_t>(p), mq);
+        if constexpr (decltype(u24)::value) return modq_conv24(xv, p, m24, sh24);
+        else return modq_conv(xv, static_cast<uint32_t>(p), mq);
     };
     // tap offsets of the A-in-VGPR path, once per block (the k-step loop then only adds)
     int toff[AREG ? KSC : 1];
@@ -656,121 +660,125 @@ __global__ __launch_bounds__(256) void k_conv_img2(ConvArgs a, Act x, Act y, int
             toff[s] = dy * R + dx * S + cc * 64;
         }
     }
-    for (int colw = wave_c * 16 * NT; colw < ncol; colw += 64) {
-        v4i acc[NG][NT];
-        int base[NT];
-#pragma unroll
-        for (int t = 0; t < NT; ++t) {
-#pragma unroll
-            for (int g = 0; g < NG; ++g) acc[g][t] = v4i{0, 0, 0, 0};
-            const int col = colw + t * 16 + (lane & 15);
-            // columns past the band read column 0's operands (valid LDS); their results are never stored
-            const int cl = col < ncol ? col : 0;
-            const int oyl = a.OW > 1 ? static_cast<int>(__umulhi(static_cast<uint32_t>(cl), owm)) : cl;
-            const int ox = cl - oyl * a.OW;
-            base[t] = (oyl * a.sh) * R + (ox * a.sw) * S + (lane >> 4) * 16;
-        }
-        if (AREG) {
-            // B operands one k-step ahead: the LDS reads of step s+1 are in flight while step s's MFMAs run
-            // (one read ahead left each MFMA waiting out most of an LDS round trip)
-            v2l bcur[NT], bnxt[NT];
-#define DASH_CONV_LDB(off) *reinterpret_cast<const v2l*>(img + base[t] + (off))
-#pragma unroll
-            for (int t = 0; t < NT; ++t) bcur[t] = DASH_CONV_LDB(toff[0]);
-#pragma unroll
-            for (int s = 0; s < (AREG ? KSC : 1); ++s) {
-                if (s + 1 < (AREG ? KSC : 1)) {
-#pragma unroll
-                    for (int t = 0; t < NT; ++t) bnxt[t] = DASH_CONV_LDB(toff[(s + 1 < KSC) ? s + 1 : s]);
-                }
-                __builtin_amdgcn_sched_barrier(0);  // keep the reads ahead (the scheduler otherwise sinks them)
-#pragma unroll
-                for (int t = 0; t < NT; ++t)
-#pragma unroll
-                    for (int g = 0; g < NG; ++g)
-                        acc[g][t] = __builtin_amdgcn_mfma_i32_16x16x64_i8(bcur[t], av[g][s], acc[g][t], 0, 0, 0);
-                __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-                for (int t = 0; t < NT; ++t) bcur[t] = bnxt[t];
+    auto columns = [&](auto u24) {
+        for (int colw = wave_c * 16 * NT; colw < ncol; colw += 64) {
+            v4i acc[NG][NT];
+            int base[NT];
+    #pragma unroll
+            for (int t = 0; t < NT; ++t) {
+    #pragma unroll
+                for (int g = 0; g < NG; ++g) acc[g][t] = v4i{0, 0, 0, 0};
+                const int col = colw + t * 16 + (lane & 15);
+                // columns past the band read column 0's operands (valid LDS); their results are never stored
+                const int cl = col < ncol ? col : 0;
+                const int oyl = a.OW > 1 ? static_cast<int>(__umulhi(static_cast<uint32_t>(cl), owm)) : cl;
+                const int ox = cl - oyl * a.OW;
+                base[t] = (oyl * a.sh) * R + (ox * a.sw) * S + (lane >> 4) * 16;
             }
-#undef DASH_CONV_LDB
-        } else {
-            for (int dy = 0; dy < a.kh; ++dy)
-                for (int dx = 0; dx < a.kw; ++dx)
-                    for (int cc = 0; cc < CC; ++cc) {
-                        v2l av1[NG];
-#pragma unroll
+            if (AREG) {
+                // B operands one k-step ahead: the LDS reads of step s+1 are in flight while step s's MFMAs run
+                // (one read ahead left each MFMA waiting out most of an LDS round trip)
+                v2l bcur[NT], bnxt[NT];
+    #define DASH_CONV_LDB(off) *reinterpret_cast<const v2l*>(img + base[t] + (off))
+    #pragma unroll
+                for (int t = 0; t < NT; ++t) bcur[t] = DASH_CONV_LDB(toff[0]);
+    #pragma unroll
+                for (int s = 0; s < (AREG ? KSC : 1); ++s) {
+                    if (s + 1 < (AREG ? KSC : 1)) {
+    #pragma unroll
+                        for (int t = 0; t < NT; ++t) bnxt[t] = DASH_CONV_LDB(toff[(s + 1 < KSC) ? s + 1 : s]);
+                    }
+                    __builtin_amdgcn_sched_barrier(0);  // keep the reads ahead (the scheduler otherwise sinks them)
+    #pragma unroll
+                    for (int t = 0; t < NT; ++t)
+    #pragma unroll
                         for (int g = 0; g < NG; ++g)
-                            av1[g] = fw + 16 * g < a.F ? *reinterpret_cast<const v2l*>(Wr[g] + (dy * a.kw + dx) * a.Cpad + cc * 64)
-                                                       : v2l{0, 0};
-                        const int offs = dy * R + dx * S + cc * 64;
-#pragma unroll
-                        for (int t = 0; t < NT; ++t) {
-                            const v2l bv = *reinterpret_cast<const v2l*>(img + base[t] + offs);
-#pragma unroll
+                            acc[g][t] = __builtin_amdgcn_mfma_i32_16x16x64_i8(bcur[t], av[g][s], acc[g][t], 0, 0, 0);
+                    __builtin_amdgcn_sched_barrier(0);
+    #pragma unroll
+                    for (int t = 0; t < NT; ++t) bcur[t] = bnxt[t];
+                }
+    #undef DASH_CONV_LDB
+            } else {
+                for (int dy = 0; dy < a.kh; ++dy)
+                    for (int dx = 0; dx < a.kw; ++dx)
+                        for (int cc = 0; cc < CC; ++cc) {
+                            v2l av1[NG];
+    #pragma unroll
                             for (int g = 0; g < NG; ++g)
-                                acc[g][t] = __builtin_amdgcn_mfma_i32_16x16x64_i8(bv, av1[g], acc[g][t], 0, 0, 0);
+                                av1[g] = fw + 16 * g < a.F ? *reinterpret_cast<const v2l*>(Wr[g] + (dy * a.kw + dx) * a.Cpad + cc * 64)
+                                                           : v2l{0, 0};
+                            const int offs = dy * R + dx * S + cc * 64;
+    #pragma unroll
+                            for (int t = 0; t < NT; ++t) {
+                                const v2l bv = *reinterpret_cast<const v2l*>(img + base[t] + offs);
+    #pragma unroll
+                                for (int g = 0; g < NG; ++g)
+                                    acc[g][t] = __builtin_amdgcn_mfma_i32_16x16x64_i8(bv, av1[g], acc[g][t], 0, 0, 0);
+                            }
+                        }
+            }
+    #pragma unroll
+            for (int g = 0; g < NG; ++g) {
+                const int fl = fw + 16 * g + (lane & 15);
+                if (NT == 4 && dw16 && colw + 64 <= ncol) {
+                    // whole 64-column chunk: lane (f, h) holds positions 16 t + 4 h + 0..3 of tile t as one dword; a
+                    // 4x4 transpose over (t, h) with v_permlane32_swap / v_permlane16_swap gives it positions
+                    // 16 h + 0..15, stored as one 16-byte store per lane (64 contiguous bytes per filter row)
+                    uint32_t d[4];
+    #pragma unroll
+                    for (int t = 0; t < 4; ++t) {
+                        uint32_t w = 0;
+    #pragma unroll
+                        for (int r = 0; r < 4; ++r)
+                            w |= red(u24, acc[g][t][r], addc[g]) << (8 * r);
+                        d[t] = w;
+                    }
+                    auto r02 = __builtin_amdgcn_permlane32_swap(d[0], d[2], false, false);
+                    d[0] = r02[0];
+                    d[2] = r02[1];
+                    auto r13 = __builtin_amdgcn_permlane32_swap(d[1], d[3], false, false);
+                    d[1] = r13[0];
+                    d[3] = r13[1];
+                    auto r01 = __builtin_amdgcn_permlane16_swap(d[0], d[1], false, false);
+                    d[0] = r01[0];
+                    d[1] = r01[1];
+                    auto r23 = __builtin_amdgcn_permlane16_swap(d[2], d[3], false, false);
+                    d[2] = r23[0];
+                    d[3] = r23[1];
+                    if (fl < a.F) {
+                        act_t* yr = Y + static_cast<int64_t>(fl) * npos + oy0 * a.OW + colw + 16 * (lane >> 4);
+                        *reinterpret_cast<uint4*>(yr) = make_uint4(d[0], d[1], d[2], d[3]);
+                    }
+                    continue;
+                }
+                if (fl >= a.F) continue;
+    #pragma unroll
+                for (int t = 0; t < NT; ++t) {
+                    // rows r = 0..3: positions colw + 16 t + 4 (lane / 16) + r of filter fl (band rows are whole output rows)
+                    const int cb = colw + t * 16 + (lane >> 4) * 4;
+                    if (cb >= ncol) continue;
+                    const int pos = oy0 * a.OW + cb;
+                    uint32_t o[4];
+    #pragma unroll
+                    for (int r = 0; r < 4; ++r)
+                        o[r] = red(u24, acc[g][t][r], addc[g]);
+                    act_t* yr = Y + static_cast<int64_t>(fl) * npos + pos;
+                    {
+                        if (dw && cb + 3 < ncol) {
+                            *reinterpret_cast<uint32_t*>(yr) = o[0] | (o[1] << 8) | (o[2] << 16) | (o[3] << 24);
+                        } else {
+    #pragma unroll
+                            for (int r = 0; r < 4; ++r)
+                                if (cb + r < ncol) yr[r] = static_cast<act_t>(o[r]);
                         }
                     }
-        }
-#pragma unroll
-        for (int g = 0; g < NG; ++g) {
-            const int fl = fw + 16 * g + (lane & 15);
-            if (NT == 4 && dw16 && colw + 64 <= ncol) {
-                // whole 64-column chunk: lane (f, h) holds positions 16 t + 4 h + 0..3 of tile t as one dword; a
-                // 4x4 transpose over (t, h) with v_permlane32_swap / v_permlane16_swap gives it positions
-                // 16 h + 0..15, stored as one 16-byte store per lane (64 contiguous bytes per filter row)
-                uint32_t d[4];
-#pragma unroll
-                for (int t = 0; t < 4; ++t) {
-                    uint32_t w = 0;
-#pragma unroll
-                    for (int r = 0; r < 4; ++r)
-                        w |= red(acc[g][t][r], addc[g]) << (8 * r);
-                    d[t] = w;
-                }
-                auto r02 = __builtin_amdgcn_permlane32_swap(d[0], d[2], false, false);
-                d[0] = r02[0];
-                d[2] = r02[1];
-                auto r13 = __builtin_amdgcn_permlane32_swap(d[1], d[3], false, false);
-                d[1] = r13[0];
-                d[3] = r13[1];
-                auto r01 = __builtin_amdgcn_permlane16_swap(d[0], d[1], false, false);
-                d[0] = r01[0];
-                d[1] = r01[1];
-                auto r23 = __builtin_amdgcn_permlane16_swap(d[2], d[3], false, false);
-                d[2] = r23[0];
-                d[3] = r23[1];
-                if (fl < a.F) {
-                    act_t* yr = Y + static_cast<int64_t>(fl) * npos + oy0 * a.OW + colw + 16 * (lane >> 4);
-                    *reinterpret_cast<uint4*>(yr) = make_uint4(d[0], d[1], d[2], d[3]);
-                }
-                continue;
-            }
-            if (fl >= a.F) continue;
-#pragma unroll
-            for (int t = 0; t < NT; ++t) {
-                // rows r = 0..3: positions colw + 16 t + 4 (lane / 16) + r of filter fl (band rows are whole output rows)
-                const int cb = colw + t * 16 + (lane >> 4) * 4;
-                if (cb >= ncol) continue;
-                const int pos = oy0 * a.OW + cb;
-                uint32_t o[4];
-#pragma unroll
-                for (int r = 0; r < 4; ++r)
-                    o[r] = red(acc[g][t][r], addc[g]);
-                act_t* yr = Y + static_cast<int64_t>(fl) * npos + pos;
-                {
-                    if (dw && cb + 3 < ncol) {
-                        *reinterpret_cast<uint32_t*>(yr) = o[0] | (o[1] << 8) | (o[2] << 16) | (o[3] << 24);
-                    } else {
-#pragma unroll
-                        for (int r = 0; r < 4; ++r)
-                            if (cb + r < ncol) yr[r] = static_cast<act_t>(o[r]);
-                    }
                 }
             }
         }
-    }
+    };
+    if (sh24 >= 0) columns(std::true_type{});
+    else columns(std::false_type{});
 }
 
 // ---------------------------------------------------------------------------
