@@ -859,15 +859,17 @@ __global__ __launch_bounds__(kOhBS, kAesMinBlocks) void k_rescale_mrs_out_hash_s
                     if (j != 0) cf.push(v, m);
                 }
             } else {  // chunk-major (chunk_digit): one divmod per chunk, uniform digit loops, one flush per chunk
+                // (digit loop unrolled by 4 and the first digit read back after the pass instead of a compare per
+                // digit: the loop's scalar bookkeeping was ~40 % of the kernel's instructions, r05 headline PMC)
                 for (int k0 = 0; k0 < cnt; k0 += static_cast<int>(m.c)) {
                     uint32_t r = divmod128(Q, m);
                     const int kc = min(static_cast<int>(m.c), cnt - k0);
                     uint32_t acc = 0, pt = 1;
+#pragma unroll 4
                     for (int t = 0; t < kc; ++t) {
                         uint8_t& w = stg[(k0 + t) * kOhBS + tid];
                         const uint32_t dd = chunk_digit(r, m);
                         const uint32_t v = j == 0 ? dd : modq(static_cast<uint32_t>(w) * inv + dd, m);
-                        if (q0 + k0 + t == 0) c0 = v;
                         w = static_cast<uint8_t>(v);
                         acc += v * pt;
                         pt *= m.q;
@@ -875,6 +877,7 @@ __global__ __launch_bounds__(kOhBS, kAesMinBlocks) void k_rescale_mrs_out_hash_s
                     C += PW * static_cast<u128>(acc);
                     PW *= static_cast<u128>(m.D);
                 }
+                if (q0 == 0) c0 = stg[tid];  // digit 0 of the output (this lane's own LDS byte)
             }
             __syncthreads();
             lds_store_rows<kOhBS>(L, stg, N, e0, q0, cnt);

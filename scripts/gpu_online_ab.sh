@@ -10,7 +10,7 @@ mkdir -p "$OUT"
 for i in $(seq 1 "$PAIRS"); do
     for v in "$A" "$B"; do
         n=$(basename "$(realpath "$v")")
-        timeout -k 10 300 python scripts/ab_online.py --root "$v" --batch 24 --steps 5 --relu joint \
+        timeout -k 10 300 python scripts/ab_online.py --root "$v" --batch 24 --steps 5 --relu joint ${DETAIL:+--detail} \
             > "$OUT/online_${n}_$i.json" 2> "$OUT/online_${n}_$i.err" || { tail -20 "$OUT/online_${n}_$i.err"; exit 1; }
         echo "$n $(head -1 "$OUT/online_${n}_$i.json")"
     done
