@@ -2830,6 +2830,7 @@ struct GpuGarbler::Impl {
         // garble() returns with every table written; blocks released below are reused in stream order
         (void)hipStreamSynchronize(dc.st);
         cur.clear();
+        (void)hipGetLastError();  // teardown errors are ignored: do not leave them for a later HIPCHECK
     }
 };
 

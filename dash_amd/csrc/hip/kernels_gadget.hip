@@ -449,7 +449,22 @@ __global__ __launch_bounds__(kRmBS) void k_relu_mult_s(SignArgs a, Act x, Act y,
         const int16_t t16 = static_cast<int16_t>(static_cast<uint16_t>(mini >> (16 * cS)));
         const int16_t ypr16 = static_cast<int16_t>(t16 - static_cast<int16_t>(static_cast<uint16_t>(HM)));
         const uint32_t ypr = modq(static_cast<uint32_t>(static_cast<int32_t>(ypr16) + (p << 15)), m);
-        if (m.bits) {
+        if (m.bits == 1) {
+            // p = 2 (the residue with the most components, 128): the digits of G and E are their bits, and
+            // (e + ypr x + 2 - g) mod 2 = e ^ g ^ (ypr & x): one bit extract and two logic ops per component
+            // instead of two 128-bit digit shifts and a reduction
+#pragma unroll
+            for (int w = 0; w < 4; ++w) {
+                const uint32_t ge = static_cast<uint32_t>(G >> (32 * w)) ^ static_cast<uint32_t>(E >> (32 * w));
+#pragma unroll 8
+                for (int u = 0; u < 32; ++u) {
+                    const int c = 32 * w + u;
+                    if (c >= n) break;
+                    uint8_t& v = stg[c * kRmBS + tid];
+                    v = static_cast<uint8_t>(((ge >> u) & 1u) ^ (static_cast<uint32_t>(v) & ypr));
+                }
+            }
+        } else if (m.bits) {
             DigitStream sg, se;
             sg.init(G);
             se.init(E);

@@ -238,19 +238,30 @@ __device__ __forceinline__ void chain_s_pos(const MrsArgs& a, uint64_t gate, con
                         for (int l = 0; l < i; ++l) rr[l] = divmod128(Q[l], m);
                         const int cnt = min(mcn, pcnt - c0);
                         uint32_t v = 0, pt = 1;
-                        for (int t = 0; t < cnt; ++t) {
+                        auto digit = [&](int t) -> uint32_t {
                             uint32_t d = valid ? stg[(c0 + t) * kMrsBS + tid] : 0u;
 #pragma unroll
                             for (int l = 0; l < i; ++l) {
                                 const uint32_t sd = chunk_digit(rr[l], m);
                                 d = d >= sd ? d - sd : d + m.q - sd;
                             }
-                            if (p0 + c0 + t == 0) {
-                                col = d;
-                                const u128* rowp = row0 + a.dig_off[i] + static_cast<int64_t>(col) * nt;
-                                pf0 = rowp[0];
-                                pf1 = rowp[nt - 1];
-                            }
+                            return d;
+                        };
+                        int t0 = 0;
+                        if (p0 + c0 == 0) {  // (uniform) digit 0 peeled: its row gather starts at once, and the
+                                             // digit loop below carries no per-digit compare
+                            const uint32_t d = digit(0);
+                            col = d;
+                            const u128* rowp = row0 + a.dig_off[i] + static_cast<int64_t>(col) * nt;
+                            pf0 = rowp[0];
+                            pf1 = rowp[nt - 1];
+                            v = d;
+                            pt = m.q;
+                            t0 = 1;
+                        }
+#pragma unroll 2
+                        for (int t = t0; t < cnt; ++t) {
+                            const uint32_t d = digit(t);
                             v += d * pt;
                             pt *= m.q;
                         }

@@ -57,6 +57,7 @@ class IpcTables {
         alive_->store(false);
         (void)hipSetDevice(dev_);
         for (void* p : opened_) (void)hipIpcCloseMemHandle(p);
+        (void)hipGetLastError();  // teardown errors are ignored: do not leave them for a later HIPCHECK
     }
     int tables() const { return static_cast<int>(map_.size()); }
     std::shared_ptr<TableSink> sink(int b) const {
@@ -195,6 +196,7 @@ class HipEvaluator {
         if (gexec_) (void)hipGraphExecDestroy(gexec_);
         for (void* p : allocs_) (void)hipFree(p);
         for (void* p : host_allocs_) (void)hipHostFree(p);
+        (void)hipGetLastError();  // teardown errors are ignored: do not leave them for a later HIPCHECK
     }
 
     int batch() const { return B_; }
@@ -1644,6 +1646,9 @@ class DeviceInputEncoder {
         (void)hipFree(x_d_);
         (void)hipHostFree(x_h_);
         (void)hipHostFree(w_h_);
+        // teardown errors are ignored (e.g. done_'s last stream capturing in another thread): clear the thread's
+        // last error so a later, unrelated HIPCHECK(hipGetLastError()) does not report it
+        (void)hipGetLastError();
     }
     DeviceInputEncoder(const DeviceInputEncoder&) = delete;
     DeviceInputEncoder& operator=(const DeviceInputEncoder&) = delete;
