@@ -1058,7 +1058,22 @@ __global__ __launch_bounds__(kRroBS) void k_rescale_relu_out_s(MrsArgs a, SignAr
         // groups of kRroG digits: the group's LDS reads are issued together (one exposed latency per group instead
         // of per digit: a digit's write-back may alias the next digit's read, so the compiler cannot hoist it)
         constexpr int kRroG = 8;
-        for (int c0 = 0; c0 < n; c0 += kRroG) {
+        if (j == 0 && m.bits == 1) {
+            // p = 2: Y_0's digits are the bits of P. Its 128 components are the longest label, so the residue-0
+            // blocks were the launch's tail when each digit took a 128-bit stream shift
+            Graw = grow[static_cast<uint32_t>(P) & 1u];
+#pragma unroll
+            for (int w = 0; w < 4; ++w) {
+                const uint32_t pw = static_cast<uint32_t>(P >> (32 * w));
+#pragma unroll 8
+                for (int u = 0; u < 32; ++u) {
+                    const int c = 32 * w + u;
+                    if (c >= n) break;
+                    stg[c * kRroBS + tid] = static_cast<uint8_t>((pw >> u) & 1u);
+                }
+            }
+        }
+        for (int c0 = 0; c0 < ((j == 0 && m.bits == 1) ? 0 : n); c0 += kRroG) {
             uint32_t w8[kRroG];
 #pragma unroll
             for (int u = 0; u < kRroG; ++u) w8[u] = (j != 0 && c0 + u < n) ? stg[(c0 + u) * kRroBS + tid] : 0u;
@@ -1084,7 +1099,21 @@ __global__ __launch_bounds__(kRroBS) void k_rescale_relu_out_s(MrsArgs a, SignAr
         sg.init(G);
         se.init(E);
         __syncthreads();  // the row stores have read Y_j
-        for (int c0 = 0; c0 < n; c0 += kRroG) {
+        if (m.bits == 1) {
+            // p = 2: (e + ypr y + 2 - g) mod 2 = e ^ g ^ (ypr & y), the digits of G and E being their bits
+#pragma unroll
+            for (int w = 0; w < 4; ++w) {
+                const uint32_t ge = static_cast<uint32_t>(G >> (32 * w)) ^ static_cast<uint32_t>(E >> (32 * w));
+#pragma unroll 8
+                for (int u = 0; u < 32; ++u) {
+                    const int c = 32 * w + u;
+                    if (c >= n) break;
+                    uint8_t& v = stg[c * kRroBS + tid];
+                    v = static_cast<uint8_t>(((ge >> u) & 1u) ^ (static_cast<uint32_t>(v) & ypr));
+                }
+            }
+        }
+        for (int c0 = 0; c0 < (m.bits == 1 ? 0 : n); c0 += kRroG) {
             uint32_t w8[kRroG];
 #pragma unroll
             for (int u = 0; u < kRroG; ++u) w8[u] = c0 + u < n ? stg[(c0 + u) * kRroBS + tid] : 0u;
@@ -1200,10 +1229,13 @@ __global__ __launch_bounds__(256) void k_rescale_relu_out_q(MrsArgs a, SignArgs 
         const int bb = static_cast<int>(m.bits), cpl = (n + 3) >> 2;
         QPow pw;
         if (m.bits) {
+            // the lane's digits g cpl .. g cpl + cpl - 1 fit one 64-bit window (bb cpl <= 32 + bb): one 128-bit
+            // shift per lane instead of one per digit
+            const uint64_t Pw = static_cast<uint64_t>(P >> (bb * g * cpl));
             for (int t = 0; t < cpl; ++t) {
                 const int idx = g * cpl + t;
                 if (idx >= n) break;
-                const uint32_t pd = static_cast<uint32_t>(P >> (bb * idx)) & (q - 1);
+                const uint32_t pd = static_cast<uint32_t>(Pw >> (bb * t)) & (q - 1);
                 const uint32_t v = j == 0 ? pd : modq(static_cast<uint32_t>(sL[idx * kRroQE + el]) * inv + pd, m);
                 sL[idx * kRroQE + el] = static_cast<uint8_t>(v);
                 part |= static_cast<u128>(v) << (bb * idx);
@@ -1244,11 +1276,12 @@ __global__ __launch_bounds__(256) void k_rescale_relu_out_q(MrsArgs a, SignArgs 
         const uint32_t ypr = modq(static_cast<uint32_t>(static_cast<int32_t>(ypr16) + (p << 15)), m);
         // relu_j = E + ypr Y_j - G, the lane's own digits (k_relu_mult's arithmetic)
         if (m.bits) {
+            const uint64_t Gw = static_cast<uint64_t>(G >> (bb * g * cpl)), Ew = static_cast<uint64_t>(E >> (bb * g * cpl));
             for (int t = 0; t < cpl; ++t) {
                 const int idx = g * cpl + t;
                 if (idx >= n) break;
-                const uint32_t gd = static_cast<uint32_t>(G >> (bb * idx)) & (q - 1);
-                const uint32_t ed = static_cast<uint32_t>(E >> (bb * idx)) & (q - 1);
+                const uint32_t gd = static_cast<uint32_t>(Gw >> (bb * t)) & (q - 1);
+                const uint32_t ed = static_cast<uint32_t>(Ew >> (bb * t)) & (q - 1);
                 sO[idx * kRroQE + el] =
                     static_cast<uint8_t>(modq(ed + ypr * static_cast<uint32_t>(sL[idx * kRroQE + el]) + static_cast<uint32_t>(p) - gd, m));
             }
@@ -1380,10 +1413,11 @@ __global__ __launch_bounds__(256) void k_rescale_mrs_out_q(MrsArgs a, Act x, con
         __syncthreads();
         if (m.bits) {
             const int bb = static_cast<int>(m.bits), cpl = (n + 3) >> 2;
+            const uint64_t Pw = static_cast<uint64_t>(P >> (bb * g * cpl));  // (as k_rescale_relu_out_q)
             for (int t = 0; t < cpl; ++t) {
                 const int idx = g * cpl + t;
                 if (idx >= n) break;
-                const uint32_t pd = static_cast<uint32_t>(P >> (bb * idx)) & (q - 1);
+                const uint32_t pd = static_cast<uint32_t>(Pw >> (bb * t)) & (q - 1);
                 sL[idx * kRroQE + el] =
                     static_cast<uint8_t>(j == 0 ? pd : modq(static_cast<uint32_t>(sL[idx * kRroQE + el]) * inv + pd, m));
             }
