@@ -312,14 +312,25 @@ __global__ __launch_bounds__(kMrsBS, MODE == 2 ? DASH_CHAIN2_WAVES : DASH_UA_MIN
             const act_t* L = x.p[0] + static_cast<int64_t>(b) * n * N;
             CompressFwd cf;
             cf.init();
+            u128 kb = 0;  // mod-2 residue: the components' bits packed 32 at a time (one shift-or each)
             for (int c0 = 0; c0 < n; c0 += kMrsCap) {
                 const int cnt = min(kMrsCap, n - c0);
                 __syncthreads();
                 lds_stage_rows<kMrsBS, kStageU>(stg, L, N, e0, c0, cnt);
                 __syncthreads();
-                for (int c = 0; c < cnt; ++c) cf.push(valid ? stg[c * kMrsBS + tid] : 0u, m);
+                if (m.bits == 1) {
+                    for (int w0 = 0; w0 < cnt; w0 += 32) {
+                        uint32_t w = 0;
+#pragma unroll 8
+                        for (int u = 0; u < 32; ++u)
+                            if (w0 + u < cnt) w |= (valid ? static_cast<uint32_t>(stg[(w0 + u) * kMrsBS + tid]) : 0u) << u;
+                        kb |= static_cast<u128>(w) << (c0 + w0);
+                    }
+                } else {
+                    for (int c = 0; c < cnt; ++c) cf.push(valid ? stg[c * kMrsBS + tid] : 0u, m);
+                }
             }
-            u128 key = cf.finish();
+            u128 key = m.bits == 1 ? kb : cf.finish();
 #pragma unroll
             for (int l = 0; l < K - 1; ++l) key ^= PS[static_cast<int64_t>(mrs_pair<K>(l, K - 1)) * N];
             const uint32_t c = static_cast<uint32_t>(key) & 1u;
@@ -881,10 +892,23 @@ __global__ __launch_bounds__(kMrsQBS, 2) void k_mrs_chain_q(MrsArgs a, Act x, co
             const ModC m = mc[a.crt.p[0]];
             const int n = static_cast<int>(m.n);
             const uint8_t* Ls = wst + el;
-            CompressFwd cf;
-            cf.init();
-            for (int c = 0; c < n; ++c) cf.push(valid ? Ls[c * kMrsQE] : 0u, m);
-            u128 key = cf.finish();
+            u128 key;
+            if (m.bits == 1) {
+                // lane g packs components 32 g .. 32 g + 31 as one word and the quad's words are summed (disjoint
+                // bits): every lane used to walk all 128 components through the compressor
+                uint32_t w = 0;
+#pragma unroll 8
+                for (int u = 0; u < 32; ++u) {
+                    const int c = 32 * g + u;
+                    if (valid && c < n) w |= static_cast<uint32_t>(Ls[c * kMrsQE]) << u;
+                }
+                key = quad_sum128(static_cast<u128>(w) << (32 * g));
+            } else {
+                CompressFwd cf;
+                cf.init();
+                for (int c = 0; c < n; ++c) cf.push(valid ? Ls[c * kMrsQE] : 0u, m);
+                key = cf.finish();
+            }
 #pragma unroll
             for (int l = 0; l < K - 1; ++l) key ^= PS[mrs_pair<K>(l, K - 1)];
             const uint32_t cb = static_cast<uint32_t>(key) & 1u;
