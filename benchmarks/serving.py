@@ -33,6 +33,8 @@ def main() -> None:
     ap.add_argument("--timeout", type=float, default=120.0)
     ap.add_argument("--rescale", default="mrs", choices=["mrs", "legacy"])
     ap.add_argument("--relu", default="joint", choices=["mrs", "approx", "joint"])
+    ap.add_argument("--encoding", default="auto", choices=["auto", "hardened", "reference"],
+                    help="offline-message encoding (reference: wire-compatible, R_p recoverable; docs/SECURITY.md)")
     ap.add_argument("--garble-workers", type=int, default=None,
                     help="refill workers (GPU garbler: concurrent garblings, one garbling context each, "
                          "DASH_GG_CONTEXTS caps the contexts per device)")
@@ -58,7 +60,8 @@ def main() -> None:
     t0 = time.perf_counter()
     svc = InferenceService(circuit, cfg["crt"], cfg["mrs"], backend=args.backend, slots_per_group=args.slots,
                            groups=args.groups, fault_hook=hook, step_timeout_s=args.timeout, rescale=args.rescale,
-                           relu=args.relu, garble_workers=args.garble_workers)
+                           relu=args.relu, garble_workers=args.garble_workers,
+                           hardened={"auto": None, "hardened": True, "reference": False}[args.encoding])
     fill_s = time.perf_counter() - t0
     svc.stats.t_start = time.perf_counter()
     from dash_amd.ir.bases import crt_modulus, first_primes

@@ -123,7 +123,7 @@ def run_tcp(circuit, cfg, xs, args) -> dict:
                 garble_s_per_gc=(st["garble_s"] - st0["garble_s"]) / n_gc,
                 serialize_s_per_gc=(st["serialize_s"] - st0["serialize_s"]) / n_gc,
                 online_round_ms=float(np.median(online)), online_bytes_per_inference=on_b / n_gc,
-                served_inf_per_s=n_gc / tot_s, verified=bool(ok))
+                served_inf_per_s=n_gc / tot_s, verified=bool(ok), encoding=st.get("encoding"))
 
 
 def run_enclave(circuit, cfg, xs, args) -> dict:
@@ -158,7 +158,7 @@ def run_enclave(circuit, cfg, xs, args) -> dict:
                 offline_gbps=off_b / max(off_s, 1e-9) / 1e9, garble_s_per_gc=(st["garble_s"] - st0["garble_s"]) / n_gc,
                 serialize_s_per_gc=(st["serialize_s"] - st0["serialize_s"]) / n_gc,
                 online_round_ms=float(np.median(on)), online_bytes_per_inference=on_b / n_gc,
-                served_inf_per_s=n_gc / tot_s, verified=bool(ok), attested=True)
+                served_inf_per_s=n_gc / tot_s, verified=bool(ok), attested=True, encoding=st.get("encoding"))
 
 
 def main(argv=None):

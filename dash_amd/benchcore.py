@@ -51,7 +51,7 @@ CONSTRUCTIONS = {
     # the framework's fastest exact-on-the-guarded-range constructions (headline)
     "flagship": dict(sign="fused", rescale="mrs", relu="joint"),
     # the reference's constructions
-    "reference": dict(sign="reference", rescale="legacy", relu="approx"),
+    "reference": dict(sign="reference", rescale="legacy", relu="approx", hardened=False),
 }
 
 
@@ -225,10 +225,8 @@ class _HipGroup:
         self.ev.load(b, gc.model)  # a GC garbled into this slot (sink) only copies its small constants
         gc.model = None  # tables live in HBM now
         if self.device_encode:  # the garbler's input state of this GC to the GPU (offline, with its tables)
-            if self.enc is None:
-                self.enc = gc.device_input_encoder(self.device, self.per)
-                if b != 0:
-                    self.enc.load(gc.garbler, b)
+            if self.enc is None:  # arms only slot b; every slot is armed by its own GC
+                self.enc = gc.device_input_encoder(self.device, self.per, slot=b)
             else:
                 self.enc.load(gc.garbler, b)
 
@@ -317,7 +315,8 @@ class _Bench:
         dev = self.device if (self.hip and self.args.garble_device) else None
         return GarbledCircuit(self.circuit, self.cfg["crt"], self.cfg["mrs"], seed=seed, device=dev,
                               fused_sign=cons["sign"] == "fused", rescale=cons["rescale"], relu=cons["relu"],
-                              nthreads=self.threads, sink=sink if dev is not None else None)
+                              hardened=cons.get("hardened"), nthreads=self.threads,
+                              sink=sink if dev is not None else None)
 
     # ---- offline: garble B GCs into G groups of evaluator slots
     def offline(self, tag: str, cons: dict, batch: int):
@@ -495,7 +494,7 @@ class _Bench:
                                backend="hip" if self.hip else "cpu", device=self.device, slots_per_group=slots,
                                groups=groups, garble_device=bool(self.hip and a.garble_device),
                                rescale=cons["rescale"], relu=cons["relu"], fused_sign=cons["sign"] == "fused",
-                               nthreads=self.threads)
+                               hardened=cons.get("hardened"), nthreads=self.threads)
         fill_s = time.perf_counter() - t0
         try:
             barrier(ctx)

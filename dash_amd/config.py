@@ -50,6 +50,7 @@ class DashConfig:
     rescale: str = "auto"                     # DASH rescale construction: auto (mrs where the base and ranges allow) | mrs (one mixed-radix gadget) | legacy
     relu: str = "auto"                        # ReLU sign: auto (joint with the mrs rescale, else approx) | approx (reference gadget) | mrs (exact mixed radix) | joint (from the preceding mixed-radix rescale)
     sign: str = "fused"                       # approximate sign gadget: fused casts | reference
+    encoding: str = "auto"                    # offline-message encoding: auto (hardened where the constructions allow; the serving engine then refuses the reference one) | hardened | reference (wire-compatible, R_p recoverable: docs/SECURITY.md §1.1)
     seed: Optional[str] = None                # hex seed for reproducible garbling (tests only)
     insecure_fixed_seed: bool = False         # allow `seed` in the serving engine (reuses labels across restarts)
     # execution
@@ -81,7 +82,10 @@ class DashConfig:
         if self.rescale not in ("auto", "mrs", "legacy") or self.relu not in ("auto", "approx", "mrs", "joint") or \
                 self.sign not in ("fused", "reference"):
             raise ValueError(f"bad gadget construction: rescale={self.rescale} relu={self.relu} sign={self.sign}")
-        return dict(rescale=self.rescale, relu=self.relu, fused_sign=self.sign == "fused")
+        if self.encoding not in ("auto", "hardened", "reference"):
+            raise ValueError(f"bad encoding {self.encoding!r}: auto | hardened | reference")
+        hardened = {"auto": None, "hardened": True, "reference": False}[self.encoding]
+        return dict(rescale=self.rescale, relu=self.relu, fused_sign=self.sign == "fused", hardened=hardened)
 
     def resolved(self):
         """(q_method, q_parameter, crt, mrs, max_modulus) after applying the scheme."""

@@ -1601,7 +1601,10 @@ void HipEvaluator::plan_rescale_legacy(size_t li, i64 iters, i64 N, const CrtInf
 // group): encode_all writes all of them with one H2D and one launch.
 class DeviceInputEncoder {
    public:
-    DeviceInputEncoder(const Garbler& g, int device, int slots) : dev_(device), S_(slots), crt_(g.crt()) {
+    // g arms encoder slot `slot` (the evaluator slot its tables went to); every other slot stays empty until
+    // load() arms it with its own GC (encode refuses empty slots)
+    DeviceInputEncoder(const Garbler& g, int device, int slots, int slot = 0)
+        : dev_(device), S_(slots), crt_(g.crt()) {
         const CrtLabels& W0 = g.input_base();
         DASH_CHECK(S_ >= 1, "DeviceInputEncoder: slots must be >= 1");
         DASH_CHECK(!W0.empty() && W0.size() == crt_.size(), "DeviceInputEncoder: garble() must run first");
@@ -1634,7 +1637,7 @@ class DeviceInputEncoder {
         HIPCHECK(hipEventCreateWithFlags(&done_, hipEventDisableTiming));
         HIPCHECK(hipStreamCreateWithFlags(&st_, hipStreamNonBlocking));
         loaded_.assign(S_, 0);
-        load(g, 0);
+        load(g, slot);
     }
     ~DeviceInputEncoder() {
         (void)hipSetDevice(dev_);
@@ -1752,7 +1755,8 @@ void register_hip_bindings(py::module_& m) {
         g.encode_compressed(xp, N, dst);
     });
     py::class_<DeviceInputEncoder>(m, "DeviceInputEncoder")
-        .def(py::init<const Garbler&, int, int>(), py::arg("garbler"), py::arg("device"), py::arg("slots") = 1)
+        .def(py::init<const Garbler&, int, int, int>(), py::arg("garbler"), py::arg("device"), py::arg("slots") = 1,
+             py::arg("slot") = 0)
         .def("input_size", &DeviceInputEncoder::input_size)
         .def("slots", &DeviceInputEncoder::slots)
         .def("load", &DeviceInputEncoder::load, py::arg("garbler"), py::arg("slot") = 0,

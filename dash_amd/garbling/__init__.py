@@ -1,2 +1,2 @@
 """Garbling API (GarbledCircuit) on top of the native garbler/evaluator."""
-from .gc import GarbledCircuit, garble  # noqa: F401
+from .gc import GarbledCircuit, ReferenceEncodingWarning, garble  # noqa: F401

@@ -14,6 +14,7 @@ from __future__ import annotations
 
 import os
 import time
+import warnings
 from typing import Optional, Sequence, Union
 
 import numpy as np
@@ -26,13 +27,22 @@ from ..native import native
 Labels = list  # list[(modulus, np.ndarray int16 [N, n_p])]
 
 
+class ReferenceEncodingWarning(UserWarning):
+    """hardened=None resolved to the reference (wire-compatible, R_p-leaking) encoding."""
+
+
 def mrs_capable(crt_base: Sequence[int]) -> bool:
     """The mixed-radix rescale / sign constructions need residue 0 = 2 and odd other residues."""
     return len(crt_base) >= 2 and int(crt_base[0]) == 2 and all(int(p) % 2 == 1 for p in crt_base[1:])
 
 
-def resolve_constructions(circuit: Circuit, crt_base: Sequence[int], rescale: str, relu: str):
+def resolve_constructions(circuit: Circuit, crt_base: Sequence[int], rescale: str, relu: str,
+                          fused_sign: bool = True, hardened: Optional[bool] = None):
     """Resolve "auto" gadget constructions and guard the mixed-radix rescale's range.
+
+    The mixed-radix constructions exist only in the hardened encoding, which needs the fused sign: with
+    fused_sign=False or hardened=False, "auto" resolves to the reference constructions ("legacy" /
+    "approx") instead of picking a construction the requested encoding cannot carry.
 
     rescale="auto" -> "mrs" when the base allows it and the circuit was calibrated
     (Circuit.calibrate: every DASH rescale has a tracked input range) with every
@@ -51,17 +61,18 @@ def resolve_constructions(circuit: Circuit, crt_base: Sequence[int], rescale: st
     M = _crt_mod(crt_base)
     dash_rescales = circuit._dash_rescales()
     bad = circuit.mrs_rescale_violations(M) if dash_rescales else []
+    mrs_ok = mrs_capable(crt_base) and bool(fused_sign) and hardened is not False
     if rescale == "auto":
         calibrated = bool(dash_rescales) and all(l.input_tracked for l in dash_rescales)
         tight = circuit.mrs_rescale_violations(M, headroom=True) if dash_rescales else []
-        rescale = "mrs" if (mrs_capable(crt_base) and calibrated and not bad and not tight) else "legacy"
+        rescale = "mrs" if (mrs_ok and calibrated and not bad and not tight) else "legacy"
     elif rescale == "mrs" and bad:
         i, hi, lim = bad[0]
         raise ValueError(f"rescale='mrs': layer {i}'s tracked input reaches {hi} >= {lim}, inside the mixed-radix "
                          f"wrap band below M/2 = {M // 2}; use rescale='legacy' or a larger CRT base "
                          f"(Circuit.infer_crt_base_size reserves the band)")
     if relu == "auto":
-        relu = "joint" if rescale == "mrs" and mrs_capable(crt_base) else "approx"
+        relu = "joint" if rescale == "mrs" and mrs_ok else "approx"
     return rescale, relu
 
 
@@ -121,13 +132,22 @@ class GarbledCircuit:
         # device: garble the ReLU / Sign / legacy-rescale layers on this GPU (bit-identical to the CPU garbler)
         self.device = -1 if device is None else int(device)
         self.fused_sign = bool(fused_sign)
-        self.rescale, self.relu = resolve_constructions(circuit, self.crt_base, rescale, relu)
+        self.rescale, self.relu = resolve_constructions(circuit, self.crt_base, rescale, relu, self.fused_sign,
+                                                        hardened)
         supported = hardened_supported(circuit, self.fused_sign, self.rescale)
         # the mixed-radix constructions are this framework's own (not wire-compatible with anything): they only
         # exist in the hardened encoding, whose kernels they use
         needs = self.rescale == "mrs" or self.relu in ("mrs", "joint")
         if hardened is None:
             hardened = supported
+            if not supported:
+                # the reference encoding ships public-constant labels that reveal R_p (docs/SECURITY.md §1.1):
+                # never a silent choice
+                warnings.warn("GarbledCircuit: the resolved constructions (sign=%s, rescale=%s) cannot use the "
+                              "hardened encoding; falling back to the reference encoding, whose constant labels "
+                              "reveal the offsets R_p (docs/SECURITY.md §1.1). Pass hardened=False to choose it "
+                              "explicitly." % ("fused" if self.fused_sign else "reference", self.rescale),
+                              ReferenceEncodingWarning, stacklevel=2)
         if hardened and not supported:
             raise ValueError("hardened=True needs the fused sign construction and no legacy DASH rescale "
                              "(rescale='mrs'); the reference constructions use the wire-compatible encoding")
@@ -169,13 +189,14 @@ class GarbledCircuit:
         assert x.size == self.circuit.input_size, "input dimension does not match circuit input dimension"
         return self.garbler.encode_cm(x)
 
-    def device_input_encoder(self, device: int, slots: int = 1):
+    def device_input_encoder(self, device: int, slots: int = 1, slot: int = 0):
         """The garbler's input-encoding state (base labels W0, offsets R) of this GC on GPU `device`, placed once
         (offline): ``HipEvaluator.encode_device_into(b, enc, x)`` then writes online message #1 for x straight
         into an evaluator slot on that device (no host label work, only x crosses PCIe). With slots > 1 the
-        encoder holds one GC per slot (this one in slot 0; ``enc.load(gc.garbler, s)`` arms slot s) and encodes
-        a (slots, N) batch of inputs into consecutive evaluator slots with one launch."""
-        return self._n.DeviceInputEncoder(self.garbler, int(device), int(slots))
+        encoder holds one GC per slot (this one in slot `slot`, the others empty until ``enc.load(gc.garbler,
+        s)`` arms slot s with its own GC) and encodes a (slots, N) batch of inputs into consecutive evaluator
+        slots with one launch."""
+        return self._n.DeviceInputEncoder(self.garbler, int(device), int(slots), int(slot))
 
     def garble_inputs_compressed(self, x: np.ndarray) -> np.ndarray:
         """Online message #1 in wire form: (k, N, 2) uint64, one 16-B compressed label per residue."""

@@ -279,6 +279,7 @@ class GarblerClient:
         t = time.perf_counter()
         gc = GarbledCircuit(self.circuit, self.crt, self.mrs, max_modulus=self.max_modulus, seed=seed,
                             device=self.device, **self.gc_kw)
+        self.stats["encoding"] = "hardened" if gc.hardened else "reference"
         t1 = time.perf_counter()
         n = gc.model.serialized_size()
         try:
@@ -434,6 +435,7 @@ class GarblerClient:
         gc = GarbledCircuit(self.circuit, self.crt, self.mrs, max_modulus=self.max_modulus, seed=seed,
                             device=self.device, sink=sink, **self.gc_kw)
         self.stats["garble_s"] += time.perf_counter() - t
+        self.stats["encoding"] = "hardened" if gc.hardened else "reference"
         return gc
 
     def offline(self) -> None:

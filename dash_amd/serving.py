@@ -138,6 +138,8 @@ class ServiceStats:
     pool_waits_s: float = 0.0
     latencies_ms: Deque[float] = field(default_factory=lambda: deque(maxlen=LATENCY_WINDOW))
     t_start: float = field(default_factory=time.perf_counter)
+    encoding: Optional[str] = None  # offline-message encoding of the served GCs: "hardened" | "reference"
+    input_encoding: Optional[str] = None  # online message #1: "device" (garbler's device encoder) | "host"
 
     def as_dict(self) -> dict:
         lat = np.asarray(self.latencies_ms, dtype=np.float64)
@@ -154,6 +156,7 @@ class ServiceStats:
             # percentiles over the last LATENCY_WINDOW batches
             "batch_latency_ms": {"p50": pct(50), "p90": pct(90), "p99": pct(99), "max": pct(100)},
             "inferences_per_s_wall": round(self.inferences / wall, 3) if wall > 0 else None,
+            "encoding": self.encoding, "input_encoding": self.input_encoding,
         }
 
 
@@ -192,7 +195,7 @@ class InferenceService:
                  fault_hook: Optional[Callable[[int, int], bool]] = None, nthreads: int = 0,
                  rescale: str = "auto", relu: str = "auto", fused_sign: bool = True,
                  insecure_fixed_seed: bool = False, garble_workers: Optional[int] = None,
-                 input_encoding: Optional[str] = None):
+                 input_encoding: Optional[str] = None, hardened: Optional[bool] = None):
         if backend not in ("hip", "cpu"):
             raise ValueError("backend must be 'hip' or 'cpu'")
         if seed is not None and not insecure_fixed_seed:
@@ -214,10 +217,23 @@ class InferenceService:
         self.fault_hook = fault_hook
         self.nthreads = nthreads
         # gadget constructions (GarbledCircuit): the serving default is the fastest measured one
-        self.gc_kw = dict(rescale=rescale, relu=relu, fused_sign=fused_sign)
+        # hardened=None: the hardened encoding whenever the constructions allow it; the reference encoding
+        # (R_p recoverable from its constant labels, docs/SECURITY.md §1.1) only when asked for explicitly
+        if hardened is None:
+            from .garbling.gc import hardened_supported, resolve_constructions
+            from .ir.bases import first_primes
+
+            base = first_primes(crt) if isinstance(crt, int) else [int(p) for p in crt]
+            r, _ = resolve_constructions(circuit, base, rescale, relu, fused_sign, None)
+            if not hardened_supported(circuit, fused_sign, r):
+                raise ValueError("InferenceService: these constructions (fused_sign=%s, rescale=%s) only have the "
+                                 "reference encoding, whose constant labels reveal R_p (docs/SECURITY.md §1.1); pass "
+                                 "hardened=False to serve it anyway" % (fused_sign, r))
+        self.gc_kw = dict(rescale=rescale, relu=relu, fused_sign=fused_sign, hardened=hardened)
         self._seed = seed if seed is not None else os.urandom(16)
         self._ctr = 0
         self.stats = ServiceStats()
+        self.stats.input_encoding = "device" if self.device_encode else ("host" if backend == "hip" else "labels")
         self.healthy = True
         self.groups = [_Group(g, slots_per_group) for g in range(groups)]
         # background refill workers: with the GPU garbler four GCs garble at once on four streams of the device
@@ -303,15 +319,15 @@ class InferenceService:
             g.ev.load(b, gc.model)
             gc.model = None  # tables live in HBM now
             if self.device_encode:  # the garbler's input state of this GC to the GPU (offline, with its tables)
-                if g.enc is None:  # (the first, synchronous fill) this GC is armed in encoder slot 0
-                    g.enc = gc.device_input_encoder(self.device, g.slots)
-                    if b != 0:
-                        g.enc.load(gc.garbler, b)
+                if g.enc is None:  # arms only slot b (this GC's evaluator slot); the others load their own GCs
+                    g.enc = gc.device_input_encoder(self.device, g.slots, slot=b)
                 else:
                     g.enc.load(gc.garbler, b)
         else:
             gc = self._new_gc()
         g.gcs[b] = gc
+        if self.stats.encoding is None:
+            self.stats.encoding = "hardened" if gc.hardened else "reference"
 
     def _refill(self, g: _Group) -> None:
         for b in range(g.slots):

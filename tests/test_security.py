@@ -288,3 +288,57 @@ def test_mrs_constructions_require_hardened():
         GarbledCircuit(c, 6, 100.0, seed=SEED, hardened=False, relu="mrs")
     with pytest.raises(ValueError):
         GarbledCircuit(c, 6, 100.0, seed=SEED, hardened=True, fused_sign=False)
+
+
+def _calibrated_rescale_circuit(rng):
+    """Dense -> Rescale(2) -> ReLU, calibrated: rescale='auto' may pick the mixed-radix construction."""
+    w = rng.integers(-6, 7, size=(16, 12))
+    b = rng.integers(-40, 41, size=16)
+    c = d.Circuit([d.Dense.from_quantized(w, b), d.Rescale(2, (16,)), d.Relu((16,))])
+    from dash_amd.ir.bases import crt_modulus, first_primes
+
+    c.calibrate([rng.integers(-20, 21, size=12) for _ in range(8)], crt_modulus(first_primes(7)))
+    return c
+
+
+def test_auto_constructions_follow_requested_encoding():
+    """'auto' never resolves to a construction the requested sign / encoding cannot carry (the mixed-radix
+    ones exist only in the hardened encoding, which needs the fused sign): it falls back to the reference
+    constructions instead of raising."""
+    rng = np.random.default_rng(11)
+    c = _calibrated_rescale_circuit(rng)
+    gc = GarbledCircuit(c, 7, 100.0, seed=SEED)
+    assert (gc.rescale, gc.relu, gc.hardened) == ("mrs", "joint", True)
+    gc = GarbledCircuit(c, 7, 100.0, seed=SEED, fused_sign=False, hardened=False)
+    assert (gc.rescale, gc.relu, gc.hardened) == ("legacy", "approx", False)
+    gc = GarbledCircuit(c, 7, 100.0, seed=SEED, hardened=False)
+    assert (gc.rescale, gc.relu, gc.hardened) == ("legacy", "approx", False)
+    x = rng.integers(-20, 21, size=12)
+    assert np.array_equal(gc.decode_outputs(gc.cpu_evaluate(gc.garble_inputs(x))), gc.plain_q_eval(x))
+
+
+def test_reference_encoding_fallback_is_never_silent():
+    from dash_amd.garbling import ReferenceEncodingWarning
+    from dash_amd.serving import InferenceService
+
+    rng = np.random.default_rng(12)
+    c = _calibrated_rescale_circuit(rng)
+    with pytest.warns(ReferenceEncodingWarning):
+        gc = GarbledCircuit(c, 7, 100.0, seed=SEED, fused_sign=False)  # hardened=None, reference sign
+    assert not gc.hardened
+    import warnings
+
+    with warnings.catch_warnings():
+        warnings.simplefilter("error", ReferenceEncodingWarning)
+        GarbledCircuit(c, 7, 100.0, seed=SEED, fused_sign=False, hardened=False)  # explicit: no warning
+    # the serving engine refuses the reference encoding unless it is asked for
+    with pytest.raises(ValueError, match="hardened=False"):
+        InferenceService(c, 7, 100.0, backend="cpu", fused_sign=False, prefetch=False)
+    with InferenceService(c, 7, 100.0, backend="cpu", fused_sign=False, hardened=False, prefetch=False,
+                          slots_per_group=1, groups=1) as svc:
+        x = rng.integers(-20, 21, size=12)
+        y = svc.infer([x])
+        assert svc.stats.as_dict()["encoding"] == "reference"
+    with InferenceService(c, 7, 100.0, backend="cpu", prefetch=False, slots_per_group=1, groups=1) as svc:
+        svc.infer([x])
+        assert svc.stats.as_dict()["encoding"] == "hardened"

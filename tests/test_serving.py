@@ -33,7 +33,7 @@ def _ref(c, xs):
 @pytest.mark.parametrize("prefetch", [True, False])
 def test_service_cpu_matches_plaintext(small, prefetch):
     c, xs = small
-    with InferenceService(c, 8, 100.0, backend="cpu", slots_per_group=2, groups=2, prefetch=prefetch,
+    with InferenceService(c, 8, 100.0, hardened=False, backend="cpu", slots_per_group=2, groups=2, prefetch=prefetch,
                           seed=b"p" * 16, insecure_fixed_seed=True) as svc:
         y = svc.infer(xs)          # 7 inputs -> 4 groups of <= 2 (pool cycles, re-garbled in the background)
         y2 = svc.infer(xs[:3])
@@ -56,7 +56,7 @@ def test_service_recovers_from_integrity_failures(small):
             hits.append((i, attempt))
         return bad
 
-    with InferenceService(c, 8, 100.0, backend="cpu", slots_per_group=3, groups=2, fault_hook=fault,
+    with InferenceService(c, 8, 100.0, hardened=False, backend="cpu", slots_per_group=3, groups=2, fault_hook=fault,
                           max_retries=2, seed=b"f" * 16, insecure_fixed_seed=True) as svc:
         y = svc.infer(xs)
         st = svc.stats.as_dict()
@@ -67,7 +67,7 @@ def test_service_recovers_from_integrity_failures(small):
 
 def test_service_gives_up_after_max_retries(small):
     c, xs = small
-    with InferenceService(c, 8, 100.0, backend="cpu", slots_per_group=2, groups=1, prefetch=False,
+    with InferenceService(c, 8, 100.0, hardened=False, backend="cpu", slots_per_group=2, groups=1, prefetch=False,
                           fault_hook=lambda i, a: i == 0, max_retries=1, seed=b"g" * 16, insecure_fixed_seed=True) as svc:
         with pytest.raises(d.IntegrityError):
             svc.infer(xs[:2])
@@ -126,7 +126,7 @@ def _timeout_worker(rank, world, port):
 @pytest.mark.parametrize("enc", ["device", "host"])
 def test_service_hip_matches_plaintext_and_recovers(small, enc):
     c, xs = small
-    with InferenceService(c, 8, 100.0, backend="hip", slots_per_group=2, groups=2, device=0, seed=b"h" * 16, insecure_fixed_seed=True,
+    with InferenceService(c, 8, 100.0, hardened=False, backend="hip", slots_per_group=2, groups=2, device=0, seed=b"h" * 16, insecure_fixed_seed=True,
                           fault_hook=lambda i, a: i == 2 and a == 0, step_timeout_s=60, input_encoding=enc) as svc:
         assert svc.device_encode == (enc == "device")
         y = svc.infer(xs)
@@ -141,7 +141,7 @@ def test_service_hip_concurrent_refill_no_spurious_failures(small):
     same evaluators concurrently, no injected faults -> no integrity failure, no retry, exact outputs."""
     c, xs = small
     xs4 = [xs[i % len(xs)] for i in range(24)]
-    with InferenceService(c, 8, 100.0, backend="hip", slots_per_group=4, groups=2, device=0, garble_workers=4,
+    with InferenceService(c, 8, 100.0, hardened=False, backend="hip", slots_per_group=4, groups=2, device=0, garble_workers=4,
                           seed=b"c" * 16, insecure_fixed_seed=True, step_timeout_s=60) as svc:
         ys = [svc.infer(xs4[i:i + 8]) for i in range(0, 24, 8)]
         st = svc.stats.as_dict()
@@ -225,7 +225,7 @@ def test_timeout_is_not_requeued_and_close_returns(small, monkeypatch):
     import threading
 
     c, xs = small
-    svc = InferenceService(c, 8, 100.0, backend="cpu", slots_per_group=2, groups=2, seed=b"t" * 16, insecure_fixed_seed=True)
+    svc = InferenceService(c, 8, 100.0, hardened=False, backend="cpu", slots_per_group=2, groups=2, seed=b"t" * 16, insecure_fixed_seed=True)
     hang = threading.Event()
     refills = []
 
@@ -255,7 +255,7 @@ def test_garbler_failure_wakes_every_waiter(small, monkeypatch):
     """A dead background garbler fails every later infer() promptly instead of blocking on a group that
     will never be refilled."""
     c, xs = small
-    svc = InferenceService(c, 8, 100.0, backend="cpu", slots_per_group=1, groups=3, seed=b"w" * 16, insecure_fixed_seed=True)
+    svc = InferenceService(c, 8, 100.0, hardened=False, backend="cpu", slots_per_group=1, groups=3, seed=b"w" * 16, insecure_fixed_seed=True)
 
     def boom():
         raise OSError("garbler died")
