@@ -87,7 +87,7 @@ class GarbledCircuit:
     def __init__(self, circuit: Circuit, crt: Union[int, Sequence[int]], mrs: Union[None, float, Sequence[int]] = None,
                  max_modulus: int = 0, seed: Optional[bytes] = None, garble_me: bool = True, nthreads: int = 0,
                  device: Optional[int] = None, fused_sign: bool = True, rescale: str = "auto",
-                 relu: str = "auto", sink=None, hardened: Optional[bool] = None):
+                 relu: str = "auto", sink=None, hardened: Optional[bool] = None, range_guard: str = "auto"):
         """fused_sign: sign-gadget construction. True (default): the MRS casts are folded into the approx and
         carry projections (same function, 3.7x fewer gates per sign; gadgets.h SignPlan::fused). False: the
         reference construction with explicit identity casts (sign_gadget.h:456-546).
@@ -117,7 +117,13 @@ class GarbledCircuit:
         every table entry masked by its own tweaked pad, closing the reference encoding's R_p recovery from
         Z_p / bias labels and its shared-hash leaks (mixed half gate mini tables, repeated MRS digit moduli).
         Needs the fused sign and no legacy rescale. False: the reference's wire-compatible encoding. None
-        (default): hardened whenever the resolved constructions allow it."""
+        (default): hardened whenever the resolved constructions allow it.
+
+        range_guard: the garbler's exact per-input range check (garbling/guard.py): "auto" (default) = on when
+        the GC has the mixed-radix rescale (an input in its wrap band would decode to a valid but wrong label),
+        "on" = always (also catches CRT overflow of the reference constructions), "off". A refused input raises
+        RangeGuardError before it is encoded (host paths) or before its result is released (batched paths:
+        ``guard.submit`` / ``raise_if_bad``)."""
         self.circuit = circuit
         self.crt_base = first_primes(crt) if isinstance(crt, int) else [int(p) for p in crt]
         if mrs is None:
@@ -155,6 +161,10 @@ class GarbledCircuit:
             raise ValueError("the mixed-radix constructions (rescale='mrs', relu='mrs' / 'joint') use the hardened "
                              "encoding only (fused sign; hardened=None or True)")
         self.hardened = bool(hardened)
+        if range_guard not in ("auto", "on", "off"):
+            raise ValueError("range_guard must be 'auto', 'on' or 'off'")
+        self.guard_enabled = range_guard == "on" or (range_guard == "auto" and self.rescale == "mrs"
+                                                      and bool(circuit._dash_rescales()))
         self.sink = sink
         self._n = native()
         self.garbler = self._n.Garbler(self.crt_base, self.mrs_base, self.seed, int(max_modulus))
@@ -178,15 +188,30 @@ class GarbledCircuit:
         return self.model
 
     # --------------------------------------------------------------- online
+    @property
+    def guard(self):
+        """The circuit's exact range guard for this GC's constructions (shared by every GC of the circuit)."""
+        from .guard import guard_for
+
+        return guard_for(self.circuit, self.crt_modulus, self.rescale == "mrs",
+                         self.device if self.device >= 0 else None)
+
+    def check_inputs(self, xs) -> None:
+        """Raise RangeGuardError if a garbled evaluation of any of xs would leave an exact gadget range."""
+        if self.guard_enabled:
+            self.guard.check(xs)
+
     def garble_inputs(self, x: np.ndarray) -> Labels:
         x = np.asarray(x, dtype=np.int64).reshape(-1)
         assert x.size == self.circuit.input_size, "input dimension does not match circuit input dimension"
+        self.check_inputs([x])
         return self.garbler.encode(x)
 
     def garble_inputs_cm(self, x: np.ndarray) -> list:
         """Online message #1 in the GPU wire layout: per residue an int16 (n_p, N) array."""
         x = np.asarray(x, dtype=np.int64).reshape(-1)
         assert x.size == self.circuit.input_size, "input dimension does not match circuit input dimension"
+        self.check_inputs([x])
         return self.garbler.encode_cm(x)
 
     def device_input_encoder(self, device: int, slots: int = 1, slot: int = 0):
@@ -202,6 +227,7 @@ class GarbledCircuit:
         """Online message #1 in wire form: (k, N, 2) uint64, one 16-B compressed label per residue."""
         x = np.asarray(x, dtype=np.int64).reshape(-1)
         assert x.size == self.circuit.input_size, "input dimension does not match circuit input dimension"
+        self.check_inputs([x])
         return self.garbler.encode_compressed(x)
 
     def decode_compressed(self, labels: np.ndarray) -> np.ndarray:

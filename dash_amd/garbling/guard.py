@@ -1,0 +1,256 @@
+"""Exact run-time range guard of the garbler's inputs (the mixed-radix rescale's wrap band, CRT overflow).
+
+The garbled circuit computes every value modulo M = prod(CRT base) and its non-linear gadgets read them as
+signed values in [-M/2, M/2). Two constructions are exact only on a narrower range:
+
+* the mixed-radix rescale (gadgets.h RescaleMrsPlan) adds U = M/2 rounded up to S - 1 mod S (S = 2^l) before
+  its single conversion, so its inputs must stay below ``Rescale.mrs_limit(M)``: the top < 2^l values below
+  M/2 wrap and decode to a wrong but *valid* label (docs/SECURITY.md "mixed-radix wrap band");
+* every gadget input outside [-M/2, M/2) has already wrapped modulo M (CRT overflow) — the reference's own
+  failure mode, which it only guards statically through range calibration (circuit.h:159-265,
+  rescale_gadget.h:115-242 is exact on the whole signed range but not beyond it).
+
+The garbler knows its plaintext input and the public weights, so it can decide exactly, per input, whether
+the garbled result will equal the plaintext one: it evaluates the quantized model and checks the input of
+every non-linear gadget (ReLU, Sign, MaxPool, Rescale) and the outputs. An input that fails is refused with
+``RangeGuardError`` before its result is released (never a silently wrong label).
+
+Exact integer arithmetic on the GPU: the linear layers run as float64 GEMMs (im2col + matmul), exact for
+integers below 2^53 (the largest MiniONN gadget input is ~2^17, weights ~2^6, 576 terms: < 2^30); rescales,
+ReLU and pooling run on int64 tensors. Batches are processed in chunks so the working set stays small next to
+resident garbled tables. Layers without a batched form (test-only Mult / Max) fall back to the per-input
+numpy evaluation (Circuit.plain_q_eval).
+"""
+from __future__ import annotations
+
+from typing import List, Optional, Sequence
+
+import numpy as np
+
+from ..ir import layers as L
+
+
+class RangeGuardError(ValueError):
+    """A garbler input whose garbled evaluation would leave a gadget's exact range (wrap band / overflow)."""
+
+
+def _half(M: int) -> int:
+    return M // 2
+
+
+class RangeGuard:
+    """Per-circuit exact range check. ``mrs=True``: DASH Rescale(l) inputs must stay below the mixed-radix
+    wrap band; every gadget input and output must be a signed CRT value in [-M/2, M/2)."""
+
+    CHUNK = 16  # inputs per GPU pass (im2col working set ~60 MB on the MiniONN CNN)
+
+    def __init__(self, circuit, crt_modulus: int, mrs: bool = True, device: Optional[int] = None):
+        self.circuit, self.M, self.mrs = circuit, int(crt_modulus), bool(mrs)
+        self.device = device
+        self.batched = all(isinstance(l, (L.Conv2d, L.Dense, L.Rescale, L.Relu, L.Sign, L.Flatten, L.MaxPool2d,
+                                          L.SumPool2d, L.Add, L.Projection, L.BaseExtension)) for l in circuit.layers)
+        self._w = None
+        self._stream = None
+
+    # ------------------------------------------------------------------ limits
+    def _limits(self, layer) -> Optional[tuple]:
+        """(lo, hi_exclusive) the layer's input must satisfy, or None (linear / free layers)."""
+        h = _half(self.M)
+        lo, hi = -h, self.M - h
+        if isinstance(layer, L.Rescale):
+            if self.mrs and layer.use_sign_base_extension and layer.l >= 1:
+                hi = min(hi, layer.mrs_limit(self.M))
+            return lo, hi
+        if isinstance(layer, (L.Relu, L.Sign, L.MaxPool2d, L.Max)):
+            return lo, hi
+        return None
+
+    # ------------------------------------------------------------------ exact per-input reference (numpy)
+    def violations_np(self, x) -> list:
+        """[(layer index or 'out', min, max, lo, hi)] of one input, by the numpy plaintext evaluation."""
+        c, M = self.circuit, self.M
+        x = np.asarray(x, dtype=np.int64).reshape(-1)
+        ctx, cur, bad = [x], x, []
+        for i, l in enumerate(c.layers):
+            src = getattr(l, "in_src", None)
+            inp = ctx[src + 1] if src is not None else cur
+            lim = self._limits(l)
+            if lim is not None and inp.size:
+                mn, mx = int(inp.min()), int(inp.max())
+                if mn < lim[0] or mx >= lim[1]:
+                    bad.append((i, mn, mx, lim[0], lim[1]))
+            cur = l.plain_q_eval(inp, False, ctx, M)
+            ctx.append(cur)
+        h = _half(M)
+        if cur.size and (int(cur.min()) < -h or int(cur.max()) >= M - h):
+            bad.append(("out", int(cur.min()), int(cur.max()), -h, M - h))
+        return bad
+
+    # ------------------------------------------------------------------ batched torch path
+    def _tdev(self):
+        import torch
+
+        if self.device is not None and torch.cuda.is_available():
+            return torch.device("cuda", int(self.device))
+        return torch.device("cpu")
+
+    def _weights(self, dev):
+        import torch
+
+        if self._w is None or self._w[0] != dev:
+            ws = []
+            for l in self.circuit.layers:
+                if isinstance(l, L.Conv2d):
+                    ws.append((torch.tensor(np.array(l.q_weights.reshape(l.F, -1)), dtype=torch.float64, device=dev),
+                               torch.tensor(np.array(l.q_biases), dtype=torch.float64, device=dev)))
+                elif isinstance(l, L.Dense):
+                    perm = None
+                    if l.channel_tf:
+                        K, ch = l.in_size, l.channel_tf
+                        i = np.arange(K)
+                        perm = torch.as_tensor(i // ch + (i % ch) * (K // ch), device=dev)
+                    ws.append((torch.tensor(np.array(l.q_weights), dtype=torch.float64, device=dev),
+                               torch.tensor(np.array(l.q_biases), dtype=torch.float64, device=dev), perm))
+                else:
+                    ws.append(None)
+            self._w = (dev, ws)
+        return self._w[1]
+
+    def _bad_batch(self, X, want_out: bool = False):
+        """X: (B, N) int64 tensor -> (B,) bool tensor, True where a gadget input leaves its exact range (and the
+        outputs, with want_out)."""
+        import torch
+        import torch.nn.functional as F
+
+        M, h = self.M, _half(self.M)
+        ws = self._weights(X.device)
+        B = X.shape[0]
+        bad = torch.zeros(B, dtype=torch.bool, device=X.device)
+        ctx, cur = [X], X
+        for i, l in enumerate(self.circuit.layers):
+            src = getattr(l, "in_src", None)
+            inp = ctx[src + 1] if src is not None else cur
+            lim = self._limits(l)
+            if lim is not None:
+                bad |= (inp < lim[0]).any(dim=1) | (inp >= lim[1]).any(dim=1)
+            if isinstance(l, L.Conv2d):
+                W, b = ws[i]
+                cols = F.unfold(inp.to(torch.float64).view(B, l.C, l.H, l.W), (l.kh, l.kw), padding=(l.ph, l.pw),
+                                stride=(l.sh, l.sw))
+                y = torch.matmul(W, cols) + b[:, None]
+                out = y.reshape(B, -1).to(torch.int64)
+            elif isinstance(l, L.Dense):
+                W, b, perm = ws[i]
+                xin = inp if perm is None else inp[:, perm]
+                out = (xin.to(torch.float64) @ W.t() + b).to(torch.int64)
+            elif isinstance(l, L.Rescale):
+                if l.use_sign_base_extension:
+                    out = inp
+                    for _ in range(l.l):
+                        out = torch.div(out + h % 2, 2, rounding_mode="floor")
+                else:
+                    S = int(np.prod(l.s))
+                    out = torch.div(inp + h % S, S, rounding_mode="floor")
+            elif isinstance(l, L.Relu):
+                out = torch.clamp_min(inp, 0)
+            elif isinstance(l, L.Sign):
+                out = torch.where(inp >= 0, 1, -1).to(torch.int64)
+            elif isinstance(l, L.MaxPool2d):
+                v = inp.view(B, l.C, l.H, l.W)
+                out = None
+                for dy in range(l.kh):
+                    for dx in range(l.kw):
+                        w = v[:, :, dy:dy + l.sh * (l.OH - 1) + 1:l.sh, dx:dx + l.sw * (l.OW - 1) + 1:l.sw]
+                        out = w if out is None else torch.maximum(out, w)
+                out = out.reshape(B, -1)
+            elif isinstance(l, L.SumPool2d):
+                v = inp.view(B, l.C, l.H, l.W)
+                out = 0
+                for dy in range(l.kh):
+                    for dx in range(l.kw):
+                        out = out + v[:, :, dy:dy + l.sh * (l.OH - 1) + 1:l.sh, dx:dx + l.sw * (l.OW - 1) + 1:l.sw]
+                out = out.reshape(B, -1)
+            elif isinstance(l, L.Add):
+                out = inp + ctx[l.src + 1]
+            else:  # Flatten, Projection, BaseExtension: value-preserving
+                out = inp.reshape(B, -1)
+            ctx.append(out)
+            cur = out
+        bad |= (cur < -h).any(dim=1) | (cur >= M - h).any(dim=1)
+        return (bad, cur) if want_out else bad
+
+    def outputs(self, xs) -> np.ndarray:
+        """The exact quantized plaintext outputs (Circuit.plain_q_eval with the CRT modulus) of a batch, by the
+        same batched evaluation: the bench's verification oracle for many inputs."""
+        xs = np.asarray(np.stack([np.asarray(x, dtype=np.int64).reshape(-1) for x in xs]))
+        if not self.batched:
+            return np.stack([self.circuit.plain_q_eval(x, False, self.M) for x in xs])
+        import torch
+
+        dev = self._tdev()
+        with torch.no_grad():
+            X = torch.as_tensor(xs).to(dev)
+            outs = [self._bad_batch(X[k:k + self.CHUNK], True)[1] for k in range(0, len(xs), self.CHUNK)]
+            return torch.cat(outs).cpu().numpy()
+
+    # ------------------------------------------------------------------ public API
+    def submit(self, xs) -> "PendingCheck":
+        """Start the check of a batch of inputs; on a GPU it runs on a side stream, overlapping the garbled
+        evaluation launched before. ``PendingCheck.raise_if_bad()`` before releasing the results."""
+        xs = np.asarray(np.stack([np.asarray(x, dtype=np.int64).reshape(-1) for x in xs]))
+        if not self.batched:
+            return PendingCheck(self, xs, None, None)
+        import torch
+
+        dev = self._tdev()
+        if dev.type == "cuda":
+            if self._stream is None:
+                self._stream = torch.cuda.Stream(device=dev)
+            st = self._stream
+            st.wait_stream(torch.cuda.current_stream(dev))  # staging of an earlier submit is free again
+            with torch.cuda.stream(st):
+                X = torch.as_tensor(xs).pin_memory().to(dev, non_blocking=True)
+                flags = torch.cat([self._bad_batch(X[k:k + self.CHUNK]) for k in range(0, len(xs), self.CHUNK)])
+                host = flags.to("cpu", non_blocking=True)
+                ev = torch.cuda.Event()
+                ev.record(st)
+            return PendingCheck(self, xs, host, ev)
+        with torch.no_grad():
+            X = torch.as_tensor(xs)
+            flags = torch.cat([self._bad_batch(X[k:k + self.CHUNK]) for k in range(0, len(xs), self.CHUNK)])
+        return PendingCheck(self, xs, flags, None)
+
+    def check(self, xs) -> None:
+        self.submit(xs).raise_if_bad()
+
+
+class PendingCheck:
+    def __init__(self, guard: RangeGuard, xs: np.ndarray, flags, event):
+        self.guard, self.xs, self.flags, self.event = guard, xs, flags, event
+
+    def bad_indices(self) -> List[int]:
+        if self.flags is None:  # per-input numpy path
+            return [i for i, x in enumerate(self.xs) if self.guard.violations_np(x)]
+        if self.event is not None:
+            self.event.synchronize()
+        return [int(i) for i in np.nonzero(self.flags.numpy())[0]]
+
+    def raise_if_bad(self) -> None:
+        bad = self.bad_indices()
+        if bad:
+            i = bad[0]
+            v = self.guard.violations_np(self.xs[i])
+            raise RangeGuardError(
+                f"range guard: {len(bad)} of {len(self.xs)} input(s) would leave an exact gadget range (first: "
+                f"input {i}, layer/lo/hi violations {v}); the garbled result would be a valid but wrong label. "
+                f"Refused: use rescale='legacy' or a larger CRT base for such inputs")
+
+
+def guard_for(circuit, crt_modulus: int, mrs: bool, device: Optional[int] = None) -> RangeGuard:
+    """The circuit's cached guard (weights staged once per device)."""
+    cache = circuit.__dict__.setdefault("_range_guards", {})
+    key = (int(crt_modulus), bool(mrs), device)
+    g = cache.get(key)
+    if g is None:
+        g = cache[key] = RangeGuard(circuit, crt_modulus, mrs, device)
+    return g

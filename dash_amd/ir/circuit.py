@@ -187,6 +187,7 @@ class Circuit:
         # the cached native specs are process-local (circuits are pickled to other ranks / processes)
         st = dict(self.__dict__)
         st.pop("_native_specs", None)
+        st.pop("_range_guards", None)  # device tensors / streams of the garbler's range guard
         return st
 
     def garble_specs_native(self):

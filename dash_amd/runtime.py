@@ -94,10 +94,13 @@ class HipEvaluator:
         """Stage component-major input labels (GarbledCircuit.garble_inputs_cm) for slot b."""
         self._h.set_input_cm(b, list(arrays))
 
-    def encode_into(self, b: int, gc, x) -> None:
-        """In-process fast path: garbler `gc` encodes x straight into the pinned staging slot b."""
+    def encode_into(self, b: int, gc, x, guarded: bool = False) -> None:
+        """In-process fast path: garbler `gc` encodes x straight into the pinned staging slot b (after the
+        garbler's range guard, unless the caller checked the batch itself: guarded=True)."""
         import numpy as np
 
+        if not guarded:
+            gc.check_inputs([x])
         native().encode_into(gc.garbler, np.asarray(x, dtype=np.int64).reshape(-1), self._h, b)
 
     def encode_device_into(self, b: int, encoder, x, stream=None) -> None:
@@ -115,10 +118,13 @@ class HipEvaluator:
         """Stage compressed input labels ((k, N, 2) uint64, GarbledCircuit.garble_inputs_compressed)."""
         self._h.set_input_compressed(b, labels)
 
-    def encode_compressed_into(self, b: int, gc, x) -> None:
-        """In-process fast path, wire form: the garbler writes 16-B compressed labels into slot b."""
+    def encode_compressed_into(self, b: int, gc, x, guarded: bool = False) -> None:
+        """In-process fast path, wire form: the garbler writes 16-B compressed labels into slot b (after the
+        garbler's range guard, unless the caller checked the batch itself: guarded=True)."""
         import numpy as np
 
+        if not guarded:
+            gc.check_inputs([x])
         native().encode_compressed_into(gc.garbler, np.asarray(x, dtype=np.int64).reshape(-1), self._h, b)
 
     def upload_inputs_compressed(self, stream=None) -> None:

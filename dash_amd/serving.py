@@ -133,6 +133,7 @@ class ServiceStats:
     retries: int = 0
     integrity_failures: int = 0
     timeouts: int = 0
+    range_refusals: int = 0  # batches refused by the garbler's range guard (garbling/guard.py)
     gcs_garbled: int = 0
     garble_s: float = 0.0
     pool_waits_s: float = 0.0
@@ -151,6 +152,7 @@ class ServiceStats:
         return {
             "inferences": self.inferences, "batches": self.batches, "retries": self.retries,
             "integrity_failures": self.integrity_failures, "timeouts": self.timeouts,
+            "range_refusals": self.range_refusals,
             "gcs_garbled": self.gcs_garbled, "garble_s_per_gc": round(self.garble_s / max(1, self.gcs_garbled), 4),
             "pool_wait_s": round(self.pool_waits_s, 3),
             # percentiles over the last LATENCY_WINDOW batches
@@ -398,10 +400,14 @@ class InferenceService:
                 ev.encode_device_into(0, g.enc, np.stack([np.asarray(x).reshape(-1) for x in xs]), g.stream)
             else:
                 for b in range(len(xs)):
-                    ev.encode_compressed_into(b, g.gcs[b], xs[b])
+                    ev.encode_compressed_into(b, g.gcs[b], xs[b], guarded=True)  # batch guard below
                 ev.upload_inputs_compressed(g.stream)
             ev.run(g.stream)  # graph replay: captured in _prime_graphs
             g.runs += 1
+            # the garbler's exact range guard (mixed-radix wrap band, CRT overflow) on a side stream, overlapping
+            # the evaluation: a refused input raises RangeGuardError before any result of the batch is released
+            gc0 = g.gcs[0]
+            pend = gc0.guard.submit(xs) if gc0.guard_enabled else None
             try:
                 wait_stream(g.stream, self.step_timeout_s, f"group {g.idx} evaluation")
             except WatchdogTimeout:
@@ -417,6 +423,12 @@ class InferenceService:
                     out[b] = np.asarray(g.gcs[b].decode_compressed(msg))
                 except IntegrityError:
                     self.stats.integrity_failures += 1
+            if pend is not None:
+                try:
+                    pend.raise_if_bad()
+                except ValueError:
+                    self.stats.range_refusals += 1
+                    raise
         else:
             for b, x in enumerate(xs):
                 gc = g.gcs[b]

@@ -10,7 +10,7 @@ B=${3:-24}
 ROOT=$(pwd)
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
-ARGS="--steps 1 --warmup 0 --batch $B --streams ${STREAMS:-1} --verify 0 --phases main"
+ARGS="--steps 1 --warmup 0 --batch $B --streams ${STREAMS:-1} --verify 0 --phases main ${EXTRA:-}"
 timeout -s KILL 240 rocprofv3 --kernel-trace --kernel-include-regex "$RE" \
     --pmc SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_LDS SQ_INSTS_VALU SQ_INSTS_LDS SQ_VALU_MFMA_BUSY_CYCLES \
     --output-format csv -d "$ROOT/$OUT/a" -o run -- python3 "$ROOT/bench.py" $ARGS > "$ROOT/$OUT/a.log" 2>&1

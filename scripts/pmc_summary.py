@@ -1,6 +1,8 @@
 """Per-kernel summary of rocprofv3 --pmc counter CSVs: python scripts/pmc_summary.py OUT (passes under OUT/*/)."""
 import csv, glob, sys, re
 from collections import defaultdict
+N_SIMD = 256 * 4   # MI355X: 256 CUs x 4 SIMDs
+CLOCK_HZ = 2.4e9   # peak engine clock (MI355X_MICROARCH.md)
 out = sys.argv[1]
 agg = defaultdict(lambda: defaultdict(float))
 ms = defaultdict(float)
@@ -23,8 +25,14 @@ for k, c in sorted(agg.items()):
     g = c.get
     if g("SQ_INSTS_LDS"):
         print(f"   {'lds_bank_conflict_per_lds':28s} {g('SQ_LDS_BANK_CONFLICT', 0) / max(1, g('SQ_ACTIVE_INST_LDS', 1)):18.3f}")
-    if g("SQ_BUSY_CYCLES"):
-        print(f"   {'mfma_busy_pct':28s} {100 * g('SQ_VALU_MFMA_BUSY_CYCLES', 0) / g('SQ_BUSY_CYCLES'):18.2f}")
+    if g("SQ_VALU_MFMA_BUSY_CYCLES") is not None:
+        # SQ_VALU_MFMA_BUSY_CYCLES is summed over every SIMD of the chip (cycles, not quad-cycles), so it is
+        # normalised by the SIMD count times the kernel's elapsed cycles (dispatch time x engine clock). The
+        # round-5 form divided it by SQ_BUSY_CYCLES (one sequencer's busy cycles) and reported up to 352 %.
+        dur_s = sum(v for (kk, _), v in ms.items() if kk == k) / 1e3 / max(1, len({p for (kk, p) in ms if kk == k}))
+        if dur_s > 0:
+            util = g("SQ_VALU_MFMA_BUSY_CYCLES", 0) / (N_SIMD * dur_s * CLOCK_HZ)
+            print(f"   {'mfma_util_pct':28s} {100 * util:18.2f}")
     if g("SQ_WAVE_CYCLES"):
         print(f"   {'wait_any_pct':28s} {100 * g('SQ_WAIT_ANY', 0) / g('SQ_WAVE_CYCLES'):18.2f}")
         print(f"   {'wait_lds_pct':28s} {100 * g('SQ_WAIT_INST_LDS', 0) / g('SQ_WAVE_CYCLES'):18.2f}")

@@ -8,6 +8,6 @@ B=${2:-8}
 ROOT=$(pwd)
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
-timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$ROOT/$OUT" -o run -- python3 "$ROOT/bench.py" --steps 2 --warmup 1 --batch "$B" --phases "${PHASES:-main}" > "$ROOT/$OUT/bench.json" 2> "$ROOT/$OUT/bench.err"
+timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$ROOT/$OUT" -o run -- python3 "$ROOT/bench.py" --steps 2 --warmup 1 --batch "$B" --phases "${PHASES:-main}" ${EXTRA:-} > "$ROOT/$OUT/bench.json" 2> "$ROOT/$OUT/bench.err"
 cd "$ROOT"
 DB=$(find "$OUT" -name "*.db" | head -n 1); python3 -m dash_amd.utils.profsum "$DB" ${AFTER:+--after "$AFTER"} > "$OUT/summary.txt" 2>&1 || true
