@@ -29,7 +29,7 @@ HOST_SOURCES = ["core.cpp", "gadgets.cpp", "garbler.cpp", "evaluator.cpp", "seri
 # kernels_mrs_a.hip (K = 7, the headline) first: the longest units start first in the parallel build
 HIP_SOURCES = ["hip/kernels_mrs_a.hip", "hip/kernels_gadget.hip", "hip/garble_gpu.hip", "hip/runtime.hip",
                "hip/kernels_mrs_b.hip", "hip/kernels_mrs_c.hip", "hip/kernels_mrs_d.hip", "hip/kernels_mrs_e.hip",
-               "hip/kernels_mrs_f.hip", "hip/kernels_label.hip", "hip/kernels_gemm.hip"]
+               "hip/kernels_mrs_f.hip", "hip/kernels_label.hip", "hip/kernels_gemm.hip", "hip/guard.hip"]
 
 
 def ext_suffix() -> str:

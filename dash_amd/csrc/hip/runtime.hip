@@ -1744,7 +1744,10 @@ CrtLabels labels_from_py2(const py::list& l) {
 hipStream_t as_stream(uintptr_t s) { return reinterpret_cast<hipStream_t>(s); }
 }  // namespace
 
+void register_guard_bindings(py::module_& m);  // guard.hip
+
 void register_hip_bindings(py::module_& m) {
+    register_guard_bindings(m);
     m.def("encode_compressed_into", [](const Garbler& g, py::array_t<i64, py::array::c_style | py::array::forcecast> x,
                                        HipEvaluator& h, int b) {
         DASH_CHECK(x.size() == h.input_size(), "input size mismatch");

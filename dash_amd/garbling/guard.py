@@ -15,11 +15,19 @@ the garbled result will equal the plaintext one: it evaluates the quantized mode
 every non-linear gadget (ReLU, Sign, MaxPool, Rescale) and the outputs. An input that fails is refused with
 ``RangeGuardError`` before its result is released (never a silently wrong label).
 
-Exact integer arithmetic on the GPU: the linear layers run as float64 GEMMs (im2col + matmul), exact for
-integers below 2^53 (the largest MiniONN gadget input is ~2^17, weights ~2^6, 576 terms: < 2^30); rescales,
-ReLU and pooling run on int64 tensors. Batches are processed in chunks so the working set stays small next to
-resident garbled tables. Layers without a batched form (test-only Mult / Max) fall back to the per-input
-numpy evaluation (Circuit.plain_q_eval).
+Max pooling is a pairwise tree of max(a, b) = a + relu(b - a): besides its inputs, every difference b - a it
+feeds a ReLU gadget must be a signed value. The guard bounds them all by the window's span: max - min <=
+min(M/2, M - M/2 - 1) (a sufficient condition, exact for the tree's pairs).
+
+Three implementations with one semantics (tests/test_range_guard.py pins them against each other):
+
+* on a GPU, ``DevRangeGuard`` (csrc/hip/guard.hip): one HIP launch per layer over chunks of the batch,
+  int64 activations and 32 x 32 -> 64-bit products, on its own high-priority stream beside the garbled
+  evaluation; inputs whose activations exceed the int32 operand range are re-decided by the numpy model;
+* the batched torch evaluation (float64 GEMMs, exact below 2^53), used on the CPU and as the bench's batched
+  verification oracle (``outputs``);
+* the per-input numpy model (``violations_np``), the exact reference of both and the path of layers without a
+  batched form (test-only Mult / Max).
 """
 from __future__ import annotations
 
@@ -51,6 +59,7 @@ class RangeGuard:
                                           L.SumPool2d, L.Add, L.Projection, L.BaseExtension)) for l in circuit.layers)
         self._w = None
         self._stream = None
+        self._dev = None  # DevRangeGuard (GPU), built on first use
 
     # ------------------------------------------------------------------ limits
     def _limits(self, layer) -> Optional[tuple]:
@@ -64,6 +73,11 @@ class RangeGuard:
         if isinstance(layer, (L.Relu, L.Sign, L.MaxPool2d, L.Max)):
             return lo, hi
         return None
+
+    def span_max(self) -> int:
+        """Largest max - min of a max-pooling window whose pairwise differences are all signed CRT values."""
+        h = _half(self.M)
+        return min(h, self.M - h - 1)
 
     # ------------------------------------------------------------------ exact per-input reference (numpy)
     def violations_np(self, x) -> list:
@@ -79,6 +93,11 @@ class RangeGuard:
                 mn, mx = int(inp.min()), int(inp.max())
                 if mn < lim[0] or mx >= lim[1]:
                     bad.append((i, mn, mx, lim[0], lim[1]))
+            if isinstance(l, L.MaxPool2d) and inp.size:
+                w = np.stack(l._windows(inp))
+                span = int((w.max(axis=0) - w.min(axis=0)).max())
+                if span > self.span_max():
+                    bad.append((i, "span", span, 0, self.span_max()))
             cur = l.plain_q_eval(inp, False, ctx, M)
             ctx.append(cur)
         h = _half(M)
@@ -157,11 +176,13 @@ class RangeGuard:
                 out = torch.where(inp >= 0, 1, -1).to(torch.int64)
             elif isinstance(l, L.MaxPool2d):
                 v = inp.view(B, l.C, l.H, l.W)
-                out = None
+                out = mn = None
                 for dy in range(l.kh):
                     for dx in range(l.kw):
                         w = v[:, :, dy:dy + l.sh * (l.OH - 1) + 1:l.sh, dx:dx + l.sw * (l.OW - 1) + 1:l.sw]
                         out = w if out is None else torch.maximum(out, w)
+                        mn = w if mn is None else torch.minimum(mn, w)
+                bad |= ((out - mn).reshape(B, -1) > self.span_max()).any(dim=1)
                 out = out.reshape(B, -1)
             elif isinstance(l, L.SumPool2d):
                 v = inp.view(B, l.C, l.H, l.W)
@@ -193,13 +214,102 @@ class RangeGuard:
             outs = [self._bad_batch(X[k:k + self.CHUNK], True)[1] for k in range(0, len(xs), self.CHUNK)]
             return torch.cat(outs).cpu().numpy()
 
+    # ------------------------------------------------------------------ native GPU path
+    def native_spec(self) -> dict:
+        """The DevRangeGuard description of the circuit: per layer its kind, input context, activation buffer,
+        geometry, limits and weights; buffers are shared by context values whose lifetimes do not overlap."""
+        c, M, h = self.circuit, self.M, _half(self.M)
+        n = len(c.layers)
+        srcs = []
+        for i, l in enumerate(c.layers):
+            src = getattr(l, "in_src", None)
+            srcs.append(src + 1 if src is not None else i)
+        last_use = {n: n}  # context index -> last layer that reads it (the output: the final check)
+        for i, l in enumerate(c.layers):
+            last_use[srcs[i]] = max(last_use.get(srcs[i], -1), i)
+            if isinstance(l, L.Add):
+                last_use[l.src + 1] = max(last_use.get(l.src + 1, -1), i)
+        ctx_buf, buf_elems, holder = [0], [], []  # holder[b]: context index held by buffer b
+        layers = []
+        for i, l in enumerate(c.layers):
+            free = [b for b, j in enumerate(holder) if j is None or last_use.get(j, -1) < i]
+            out_size, in_size = int(l.out_size), int(l.in_size)
+            if free:
+                b = free[0]
+                buf_elems[b] = max(buf_elems[b], out_size)
+                holder[b] = i + 1
+            else:
+                b = len(holder)
+                holder.append(i + 1)
+                buf_elems.append(out_size)
+            ctx_buf.append(b)
+            d = dict(src=srcs[i], buf=b, in_size=in_size, out_size=out_size)
+            lim = self._limits(l)
+            if lim is not None:
+                d.update(check=True, lo=int(lim[0]), hi=int(lim[1]))
+            if isinstance(l, L.Conv2d):
+                d.update(kind=0, C=l.C, H=l.H, W=l.W, F=l.F, kh=l.kh, kw=l.kw, sh=l.sh, sw=l.sw, ph=l.ph, pw=l.pw,
+                         OH=l.OH, OW=l.OW, w=_i32(l.q_weights.reshape(l.F, -1)), b=np.asarray(l.q_biases, np.int64))
+            elif isinstance(l, L.Dense):
+                perm = None
+                if l.channel_tf:
+                    K, ch = l.in_size, l.channel_tf
+                    k = np.arange(K)
+                    perm = (k // ch + (k % ch) * (K // ch)).astype(np.int32)
+                d.update(kind=1, w=_i32(l.q_weights), b=np.asarray(l.q_biases, np.int64).reshape(-1), perm=perm)
+            elif isinstance(l, L.Rescale):
+                if l.use_sign_base_extension:
+                    d.update(kind=2, l=int(l.l), c=int(h % 2))
+                else:
+                    S = int(np.prod(l.s))
+                    d.update(kind=3, S=S, c=int(h % S))
+            elif isinstance(l, L.Relu):
+                d.update(kind=4)
+            elif isinstance(l, L.Sign):
+                d.update(kind=5)
+            elif isinstance(l, (L.MaxPool2d, L.SumPool2d)):
+                d.update(kind=6 if isinstance(l, L.MaxPool2d) else 7, C=l.C, H=l.H, W=l.W, kh=l.kh, kw=l.kw, sh=l.sh,
+                         sw=l.sw, OH=l.OH, OW=l.OW, span_max=int(self.span_max()))
+            elif isinstance(l, L.Add):
+                d.update(kind=8, add_src=int(l.src + 1))
+            else:  # Flatten, Projection, BaseExtension: value-preserving
+                d.update(kind=9)
+            layers.append(d)
+        return dict(layers=layers, input_size=int(c.input_size), ctx_buf=ctx_buf, buf_elems=buf_elems,
+                    out_lo=-h, out_hi=M - h)
+
+    def _native(self):
+        if self._dev is None:
+            from ..native import native
+
+            spec = self.native_spec()
+            per_input = 8 * sum(spec["buf_elems"])
+            chunk = int(max(1, min(64, (256 << 20) // max(1, per_input))))
+            self._dev = native().DevRangeGuard(int(self.device), spec["layers"], spec["input_size"], spec["ctx_buf"],
+                                               spec["buf_elems"], spec["out_lo"], spec["out_hi"], chunk)
+        return self._dev
+
+    def _native_ok(self) -> bool:
+        if self.device is None or not self.batched:
+            return False
+        try:
+            import torch
+
+            return torch.cuda.is_available()
+        except ImportError:  # pragma: no cover
+            return False
+
     # ------------------------------------------------------------------ public API
     def submit(self, xs) -> "PendingCheck":
-        """Start the check of a batch of inputs; on a GPU it runs on a side stream, overlapping the garbled
-        evaluation launched before. ``PendingCheck.raise_if_bad()`` before releasing the results."""
+        """Start the check of a batch of inputs; on a GPU it runs on its own stream (DevRangeGuard),
+        overlapping the garbled evaluation launched before. ``PendingCheck.raise_if_bad()`` before releasing
+        the results."""
         xs = np.asarray(np.stack([np.asarray(x, dtype=np.int64).reshape(-1) for x in xs]))
         if not self.batched:
             return PendingCheck(self, xs, None, None)
+        if self._native_ok():
+            g = self._native()
+            return PendingCheck(self, xs, None, None, native=(g, g.submit(xs)))
         import torch
 
         dev = self._tdev()
@@ -225,10 +335,22 @@ class RangeGuard:
 
 
 class PendingCheck:
-    def __init__(self, guard: RangeGuard, xs: np.ndarray, flags, event):
+    def __init__(self, guard: RangeGuard, xs: np.ndarray, flags, event, native=None):
         self.guard, self.xs, self.flags, self.event = guard, xs, flags, event
+        self.native = native
+        self._bad = None
 
     def bad_indices(self) -> List[int]:
+        if self._bad is not None:
+            return self._bad
+        if self.native is not None:  # DevRangeGuard: bit 0 violation, bit 1 activations beyond int32 operands
+            g, ticket = self.native
+            f = np.asarray(g.wait(ticket))
+            self.native = None
+            self._bad = [int(i) for i in np.nonzero(f & 1)[0]]
+            self._bad += [int(i) for i in np.nonzero(f == 2)[0] if self.guard.violations_np(self.xs[i])]
+            self._bad.sort()
+            return self._bad
         if self.flags is None:  # per-input numpy path
             return [i for i, x in enumerate(self.xs) if self.guard.violations_np(x)]
         if self.event is not None:
@@ -244,6 +366,13 @@ class PendingCheck:
                 f"range guard: {len(bad)} of {len(self.xs)} input(s) would leave an exact gadget range (first: "
                 f"input {i}, layer/lo/hi violations {v}); the garbled result would be a valid but wrong label. "
                 f"Refused: use rescale='legacy' or a larger CRT base for such inputs")
+
+
+def _i32(a) -> np.ndarray:
+    a = np.asarray(a, dtype=np.int64)
+    if a.size and (a.min() < -(1 << 31) or a.max() >= (1 << 31)):
+        raise ValueError("range guard: weights beyond int32")
+    return a.astype(np.int32)
 
 
 def guard_for(circuit, crt_modulus: int, mrs: bool, device: Optional[int] = None) -> RangeGuard:

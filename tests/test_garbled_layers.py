@@ -333,7 +333,12 @@ def test_rescale_mrs_equals_legacy_function(k, l):
     xt = np.arange(top, M // 2, dtype=np.int64)
     if xt.size:
         ct = d.Circuit([d.Rescale(l, (xt.size,))])
-        gt = GarbledCircuit(ct, k, 100.0, seed=SEED, rescale="mrs")
+        # the garbler's exact range guard refuses the band; with it off, the wrapped values are what decode
+        from dash_amd.garbling.guard import RangeGuardError
+
+        with pytest.raises(RangeGuardError):
+            GarbledCircuit(ct, k, 100.0, seed=SEED, rescale="mrs").garble_inputs(xt)
+        gt = GarbledCircuit(ct, k, 100.0, seed=SEED, rescale="mrs", range_guard="off")
         ot = gt.decode_outputs(gt.cpu_evaluate(gt.garble_inputs(xt)))
         exp = ((xt + U) % M) // S - q
         exp = np.where(exp >= M // 2, exp - M, exp)
@@ -451,8 +456,8 @@ def test_rescale_mrs_wrap_band_guard():
     band = np.arange(M // 2 - (1 << l), M // 2, dtype=np.int64)  # M/2 - 2^l ... M/2 - 1 = 101..104
     c = d.Circuit([d.Rescale(l, (band.size,))])
     assert c.layers[0].mrs_limit(M) == 103
-    # unguarded (never calibrated): the mixed-radix construction really does differ on 103, 104
-    raw = GarbledCircuit(c, crt, 100.0, seed=SEED, rescale="mrs")
+    # unguarded (never calibrated, run-time guard off): the mixed-radix construction really does differ on 103, 104
+    raw = GarbledCircuit(c, crt, 100.0, seed=SEED, rescale="mrs", range_guard="off")
     out = raw.decode_outputs(raw.cpu_evaluate(raw.garble_inputs(band)))
     ref = c.plain_q_eval(band, False, M)
     assert np.array_equal(out[:2], ref[:2]) and not np.array_equal(out[2:], ref[2:])
