@@ -685,6 +685,7 @@ def run(argv=None) -> Optional[dict]:
     # ---------------- main (headline) phase
     gcs, groups, B, G, per, off = bench.offline("main", cons, args.batch)
     resolved = gcs[0].effective_constructions()
+    resolved_guard = gcs[0].guard_enabled
     free_b = total_b = None
     if hip:
         import torch
@@ -836,6 +837,9 @@ def run(argv=None) -> Optional[dict]:
                         "table_gb_per_gc": round(off["table_gb"], 3), "offline_total_s": round(off["offline_s"], 1)},
             "verified_vs_plaintext": verified,
             "verified_last_timed_step": r_last_ok,
+            # the garbler's exact per-input range check (garbling/guard.py, csrc/hip/guard.hip) inside the timed
+            # steps, on its own stream beside the evaluation
+            "range_guard": bool(resolved_guard),
         }
         if hip:
             out["hbm_gb"] = {"used": round((total_b - free_b) / 1e9, 1), "total": round(total_b / 1e9, 1)}

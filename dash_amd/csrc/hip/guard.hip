@@ -27,8 +27,10 @@
 
 #include <algorithm>
 #include <cstdint>
+#include <cstdlib>
 #include <cstring>
 #include <deque>
+#include <map>
 #include <mutex>
 #include <vector>
 
@@ -60,41 +62,61 @@ struct ConvP {
     int* flags;
     int C, H, W, F, kh, kw, sh, sw, ph, pw, OH, OW;
     int64_t in_size, out_size;
+    int64_t asafe;  // I24: operands |x| <= asafe keep every partial sum inside int32 (host bound, see Layer)
 };
-constexpr int kFB = 4;  // filters per lane
-template <bool UNIFORM>
+constexpr int kFB = 8;  // filters per lane (one input load feeds kFB multiply-adds)
+// I24: 24 x 24-bit multiply-adds into int32 accumulators (v_mad_i32_i24, full rate), exact for operands up to
+// the layer's safe bound; a larger operand marks the input uncertain. Otherwise 32 x 32 -> 64-bit products.
+// Lanes = output pixels, padded to whole waves per (input, filter block): the filter block is wave-uniform, so
+// its weights are scalar loads (KS = 3 / 1: the taps unrolled, a channel's taps merged into wide scalar loads).
+template <int KS, bool I24>
 __global__ __launch_bounds__(256) void k_g_conv(ConvP p, int64_t total) {
     const int64_t t = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
     if (t >= total) return;
     const int OHW = p.OH * p.OW;
+    const int OHWp = (OHW + 63) & ~63;
     const int nfb = (p.F + kFB - 1) / kFB;
-    const int pix = static_cast<int>(t % OHW);
-    const int64_t r = t / OHW;
-    int fb = static_cast<int>(r % nfb);
-    int64_t b = r / nfb;
-    if (UNIFORM) {  // OH * OW is a multiple of the wave: the whole wave shares (b, fb)
-        fb = __builtin_amdgcn_readfirstlane(fb);
-        b = static_cast<int64_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(b)));
-    }
+    const int pix = static_cast<int>(t % OHWp);
+    const int64_t r = t / OHWp;
+    const int fb = __builtin_amdgcn_readfirstlane(static_cast<int>(r % nfb));
+    const int64_t b = static_cast<int64_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(r / nfb)));
+    if (pix >= OHW) return;
+    const int kh = KS ? KS : p.kh, kw = KS ? KS : p.kw;
     const int oy = pix / p.OW, ox = pix - oy * p.OW;
     const int f0 = fb * kFB;
-    const int K = p.C * p.kh * p.kw;
+    const int K = p.C * kh * kw;
     const int64_t* xb = p.x + b * p.in_size;
-    int64_t acc[kFB] = {0, 0, 0, 0};
-    bool wide = false;
-    for (int c = 0; c < p.C; ++c) {
-        for (int dy = 0; dy < p.kh; ++dy) {
-            const int iy = oy * p.sh - p.ph + dy;
-            const bool rowok = iy >= 0 && iy < p.H;
-            for (int dx = 0; dx < p.kw; ++dx) {
-                const int ix = ox * p.sw - p.pw + dx;
-                const int64_t xv = (rowok && ix >= 0 && ix < p.W) ? xb[(static_cast<int64_t>(c) * p.H + iy) * p.W + ix] : 0;
-                const int32_t xo = operand(xv, wide);
-                const int k = (c * p.kh + dy) * p.kw + dx;
+    int64_t acc[kFB];
+    int32_t a32[kFB];
 #pragma unroll
-                for (int j = 0; j < kFB; ++j) {
-                    const int f = min(f0 + j, p.F - 1);
-                    acc[j] += static_cast<int64_t>(xo) * p.w[static_cast<int64_t>(f) * K + k];
+    for (int j = 0; j < kFB; ++j) acc[j] = 0, a32[j] = 0;
+    const int32_t* wf[kFB];
+#pragma unroll
+    for (int j = 0; j < kFB; ++j) wf[j] = p.w + static_cast<int64_t>(min(f0 + j, p.F - 1)) * K;
+    bool wide = false;
+    const int iy0 = oy * p.sh - p.ph, ix0 = ox * p.sw - p.pw;
+    for (int c = 0; c < p.C; ++c) {
+        const int64_t* xc = xb + static_cast<int64_t>(c) * p.H * p.W;
+        const int kc = c * kh * kw;
+#pragma unroll
+        for (int dy = 0; dy < kh; ++dy) {
+            const int iy = iy0 + dy;
+            const bool rowok = iy >= 0 && iy < p.H;
+            const int64_t* xr = xc + static_cast<int64_t>(iy) * p.W;
+#pragma unroll
+            for (int dx = 0; dx < kw; ++dx) {
+                const int ix = ix0 + dx;
+                const int64_t xv = (rowok && ix >= 0 && ix < p.W) ? xr[ix] : 0;
+                const int k = kc + dy * kw + dx;
+                if (I24) {
+                    wide |= xv > p.asafe || xv < -p.asafe;
+                    const int32_t xo = static_cast<int32_t>(xv);
+#pragma unroll
+                    for (int j = 0; j < kFB; ++j) a32[j] += __mul24(xo, wf[j][k]);
+                } else {
+                    const int32_t xo = operand(xv, wide);
+#pragma unroll
+                    for (int j = 0; j < kFB; ++j) acc[j] += static_cast<int64_t>(xo) * wf[j][k];
                 }
             }
         }
@@ -104,7 +126,7 @@ __global__ __launch_bounds__(256) void k_g_conv(ConvP p, int64_t total) {
 #pragma unroll
     for (int j = 0; j < kFB; ++j) {
         const int f = f0 + j;
-        if (f < p.F) yb[static_cast<int64_t>(f) * OHW + pix] = acc[j] + p.bias[f];
+        if (f < p.F) yb[static_cast<int64_t>(f) * OHW + pix] = (I24 ? static_cast<int64_t>(a32[j]) : acc[j]) + p.bias[f];
     }
 }
 
@@ -208,6 +230,18 @@ __global__ __launch_bounds__(256) void k_g_out(const int64_t* x, int* flags, int
     if (v < lo || v >= hi) flag(flags, b, kBad);
 }
 
+// flags of a chunk zeroed / copied to the ticket's mapped host flags by kernels: a captured hipMemsetAsync of
+// the flags did not take effect on graph replays (stale flags of an earlier check survived, bench on a full GPU)
+__global__ __launch_bounds__(256) void k_g_zero(int* flags, int64_t n) {
+    const int64_t t = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (t < n) flags[t] = 0;
+}
+__global__ __launch_bounds__(256) void k_g_fetch(const int* flags, int* host, int64_t n) {
+    const int64_t t = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+    if (t < n) host[t] = flags[t];
+    __threadfence_system();
+}
+
 // ------------------------------------------------------------------ host
 struct Layer {
     int kind, src;  // src: context index of the input (0 = circuit input, i + 1 = output of layer i)
@@ -221,8 +255,15 @@ struct Layer {
     int32_t* w = nullptr;
     int64_t* bias = nullptr;
     int32_t* perm = nullptr;
+    // conv: operands |x| <= asafe keep every partial sum inside int32 (asafe * max_f sum_k |w_fk| <= 2^31 - 1;
+    // the bias is added in int64) and inside the 24-bit multiplier; 0 = the 64-bit product form
+    int64_t asafe = 0;
 };
 
+inline int knob(const char* name, int dflt) {
+    const char* e = std::getenv(name);
+    return e ? std::atoi(e) : dflt;
+}
 inline unsigned blocks_of(int64_t total) { return static_cast<unsigned>((total + 255) / 256); }
 
 class DevRangeGuard {
@@ -285,6 +326,21 @@ class DevRangeGuard {
                 DASH_CHECK(w.size() == rows * K && b.size() == rows, "DevRangeGuard: weight / bias shape");
                 L.w = upload(w.data(), w.size());
                 L.bias = upload(b.data(), b.size());
+                if (L.kind == G_CONV) {
+                    int64_t wsum = 1, wmax = 0;
+                    for (int64_t f = 0; f < rows; ++f) {
+                        int64_t s = 0;
+                        for (int64_t k = 0; k < K; ++k) {
+                            const int64_t v = std::abs(static_cast<int64_t>(w.data()[f * K + k]));
+                            s += v;
+                            wmax = std::max(wmax, v);
+                        }
+                        wsum = std::max(wsum, s);
+                    }
+                    const int64_t lim24 = (int64_t(1) << 23) - 1;
+                    L.asafe = wmax <= lim24 ? std::min(lim24, ((int64_t(1) << 31) - 1) / wsum) : 0;
+                    if (knob("DASH_GUARD_I24", 1) == 0) L.asafe = 0;  // A/B: the 64-bit product form
+                }
                 if (L.kind == G_DENSE && d.contains("perm") && !d["perm"].is_none()) {
                     auto pm = d["perm"].cast<py::array_t<int32_t, py::array::c_style | py::array::forcecast>>();
                     DASH_CHECK(pm.size() == L.in_size, "DevRangeGuard: permutation size");
@@ -295,6 +351,8 @@ class DevRangeGuard {
             }
             if (L.kind == G_ADD)
                 DASH_CHECK(L.add_src >= 0 && static_cast<size_t>(L.add_src) < ctx_buf_.size(), "DevRangeGuard: add source");
+            if (L.kind >= G_HALVE && L.kind != G_MAXPOOL && L.kind != G_SUMPOOL)
+                DASH_CHECK(L.in_size == L.out_size, "DevRangeGuard: elementwise layer changes the size");
             layers_.push_back(L);
         }
         DASH_CHECK(!layers_.empty(), "DevRangeGuard: empty circuit");
@@ -340,17 +398,34 @@ class DevRangeGuard {
             HIPCHECK(hipMalloc(reinterpret_cast<void**>(&t.x_d), sizeof(int64_t) * t.cap * N_));
             HIPCHECK(hipMalloc(reinterpret_cast<void**>(&t.flags_d), sizeof(int) * t.cap));
             HIPCHECK(hipHostMalloc(reinterpret_cast<void**>(&t.flags_h), sizeof(int) * t.cap, hipHostMallocMapped));
+            HIPCHECK(hipHostGetDevicePointer(reinterpret_cast<void**>(&t.flags_hd), t.flags_h, 0));
             HIPCHECK(hipEventCreateWithFlags(&t.done, hipEventDisableTiming));
         }
         t.busy = true;
         t.B = B;
         std::memcpy(t.x_h, x, sizeof(int64_t) * B * N_);
-        HIPCHECK(hipMemcpyAsync(t.x_d, t.x_h, sizeof(int64_t) * B * N_, hipMemcpyHostToDevice, st_));
-        HIPCHECK(hipMemsetAsync(t.flags_d, 0, sizeof(int) * B, st_));
-        for (int64_t b0 = 0; b0 < B; b0 += chunk_) run_chunk(t, b0, std::min<int64_t>(chunk_, B - b0));
-        HIPCHECK(hipMemcpyAsync(t.flags_h, t.flags_d, sizeof(int) * B, hipMemcpyDeviceToHost, st_));
+        // the whole check (H2D, one launch per layer and chunk, flags D2H) as one graph per (ticket, batch size):
+        // one launch instead of ~2 per layer, no gaps between the small layer kernels
+        if (knob("DASH_GUARD_GRAPH", 1) == 0) {  // A/B: stream launches
+            enqueue(t, B);
+            HIPCHECK(hipEventRecord(t.done, st_));
+            return id;
+        }
+        auto it = t.graphs.find(B);
+        if (it == t.graphs.end()) {
+            if (t.graphs.size() >= 8) drop_graphs(t);
+            HIPCHECK(hipStreamBeginCapture(st_, hipStreamCaptureModeThreadLocal));
+            enqueue(t, B);
+            hipGraph_t g = nullptr;
+            HIPCHECK(hipStreamEndCapture(st_, &g));
+            hipGraphExec_t ge = nullptr;
+            const hipError_t e = hipGraphInstantiate(&ge, g, nullptr, nullptr, 0);
+            (void)hipGraphDestroy(g);
+            HIPCHECK(e);
+            it = t.graphs.emplace(B, ge).first;
+        }
+        HIPCHECK(hipGraphLaunch(it->second, st_));
         HIPCHECK(hipEventRecord(t.done, st_));
-        HIPCHECK(hipGetLastError());
         return id;
     }
     // the flags of a ticket (blocks until its check has run); the ticket is free again afterwards
@@ -382,11 +457,18 @@ class DevRangeGuard {
         int64_t* x_d = nullptr;
         int* flags_d = nullptr;
         int* flags_h = nullptr;
+        int* flags_hd = nullptr;  // flags_h as seen from the device (mapped)
         hipEvent_t done = nullptr;
         bool busy = false;
+        std::map<int64_t, hipGraphExec_t> graphs;  // batch size -> the captured check
     };
+    static void drop_graphs(Ticket& t) {
+        for (auto& kv : t.graphs) (void)hipGraphExecDestroy(kv.second);
+        t.graphs.clear();
+    }
     void release(Ticket& t) {
         if (t.done) (void)hipEventSynchronize(t.done);
+        drop_graphs(t);
         if (t.x_h) (void)hipHostFree(t.x_h);
         if (t.x_d) (void)hipFree(t.x_d);
         if (t.flags_d) (void)hipFree(t.flags_d);
@@ -401,6 +483,12 @@ class DevRangeGuard {
         if (n) HIPCHECK(hipMemcpy(p, src, sizeof(T) * n, hipMemcpyHostToDevice));
         owned_.push_back(p);
         return p;
+    }
+    void enqueue(const Ticket& t, int64_t B) {
+        HIPCHECK(hipMemcpyAsync(t.x_d, t.x_h, sizeof(int64_t) * B * N_, hipMemcpyHostToDevice, st_));
+        hipLaunchKernelGGL(k_g_zero, dim3(blocks_of(B)), dim3(256), 0, st_, t.flags_d, B);
+        for (int64_t b0 = 0; b0 < B; b0 += chunk_) run_chunk(t, b0, std::min<int64_t>(chunk_, B - b0));
+        hipLaunchKernelGGL(k_g_fetch, dim3(blocks_of(B)), dim3(256), 0, st_, t.flags_d, t.flags_hd, B);
     }
     // context index -> (pointer, per-input stride); index 0 of a chunk is the ticket's input rows
     std::pair<const int64_t*, int64_t> ctx(const Ticket& t, int idx, int64_t b0) const {
@@ -418,12 +506,15 @@ class DevRangeGuard {
             switch (L.kind) {
                 case G_CONV: {
                     ConvP p{in.first, y, L.w, L.bias, flags, L.C, L.H, L.W, L.F, L.kh, L.kw, L.sh, L.sw, L.ph, L.pw,
-                            L.OH, L.OW, in.second, ys};
-                    const int64_t total = B * ((L.F + kFB - 1) / kFB) * static_cast<int64_t>(L.OH) * L.OW;
-                    if ((static_cast<int64_t>(L.OH) * L.OW) % 64 == 0)
-                        hipLaunchKernelGGL(k_g_conv<true>, dim3(blocks_of(total)), dim3(256), 0, st_, p, total);
-                    else
-                        hipLaunchKernelGGL(k_g_conv<false>, dim3(blocks_of(total)), dim3(256), 0, st_, p, total);
+                            L.OH, L.OW, in.second, ys, L.asafe};
+                    const int64_t ohwp = (static_cast<int64_t>(L.OH) * L.OW + 63) & ~int64_t(63);
+                    const int64_t total = B * ((L.F + kFB - 1) / kFB) * ohwp;
+                    const bool i24 = L.asafe > 0;
+                    const int ks = (L.kh == 3 && L.kw == 3) ? 3 : (L.kh == 1 && L.kw == 1) ? 1 : 0;
+                    auto k = ks == 3 ? (i24 ? k_g_conv<3, true> : k_g_conv<3, false>)
+                             : ks == 1 ? (i24 ? k_g_conv<1, true> : k_g_conv<1, false>)
+                                       : (i24 ? k_g_conv<0, true> : k_g_conv<0, false>);
+                    hipLaunchKernelGGL(k, dim3(blocks_of(total)), dim3(256), 0, st_, p, total);
                     break;
                 }
                 case G_DENSE: {
@@ -441,7 +532,6 @@ class DevRangeGuard {
                     break;
                 }
                 default: {
-                    DASH_CHECK(L.in_size == L.out_size, "DevRangeGuard: elementwise layer changes the size");
                     auto in2 = L.kind == G_ADD ? ctx(t, L.add_src, b0) : in;
                     ElemP p{in.first, in2.first, y, flags, L.kind, L.check, L.l, L.lo, L.hi, L.S, L.c,
                             L.out_size, in.second, in2.second, ys};

@@ -161,6 +161,8 @@ class GarbledCircuit:
             raise ValueError("the mixed-radix constructions (rescale='mrs', relu='mrs' / 'joint') use the hardened "
                              "encoding only (fused sign; hardened=None or True)")
         self.hardened = bool(hardened)
+        if range_guard == "auto" and os.environ.get("DASH_RANGE_GUARD") in ("on", "off"):
+            range_guard = os.environ["DASH_RANGE_GUARD"]  # A/B knob (bench records say which was used)
         if range_guard not in ("auto", "on", "off"):
             raise ValueError("range_guard must be 'auto', 'on' or 'off'")
         self.guard_enabled = range_guard == "on" or (range_guard == "auto" and self.rescale == "mrs"

@@ -269,7 +269,7 @@ def test_native_guard_matches_numpy_on_gpu():
     cm = build_circuit("MODEL_F_MINIONN_POOL_REPL", qm, cfg["q_parameter"], seed=0)
     MM = crt_modulus(first_primes(cfg["crt"]))
     xs = list(quantized_inputs("MODEL_F_MINIONN_POOL_REPL", 70, qm, cfg["q_parameter"], seed=3))
-    xs[5] = xs[5] * 40
+    xs[5] = xs[5] * 2000
     xs[66] = xs[66] * 2000
     xs[40] = xs[40] * (1 << 33)  # beyond the int32 operands: decided by the exact host model
     g = RangeGuard(cm, MM, mrs=True, device=0)
@@ -286,3 +286,7 @@ def test_native_guard_matches_numpy_on_gpu():
     # two tickets in flight, waited out of order
     p1, p2 = g.submit(xs[:8]), g.submit(xs[60:70])
     assert p2.bad_indices() == [6] and p1.bad_indices() == [5]
+    # a replayed check (same ticket and batch size) starts from clear flags and reads the new inputs
+    for rep in range(3):
+        assert g.submit(xs[8:16]).bad_indices() == []
+        assert g.submit(xs[:8]).bad_indices() == [5]
