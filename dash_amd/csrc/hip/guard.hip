@@ -54,6 +54,39 @@ __device__ __forceinline__ int32_t operand(int64_t x, bool& wide) {
     return v;
 }
 
+// elementwise layers fused into the epilogue of the layer before them (guard.py native_spec): each checks its
+// input against its gadget range, then applies its function
+struct PostOp {
+    int kind, check, l;
+    int64_t lo, hi, S, c;
+};
+constexpr int kMaxPost = 6;
+struct Post {
+    int n;
+    PostOp op[kMaxPost];
+};
+__device__ __forceinline__ int64_t floordiv(int64_t a, int64_t s) {
+    int64_t q = a / s;
+    if ((a % s != 0) && (a < 0)) --q;
+    return q;
+}
+__device__ __forceinline__ int64_t run_post(const Post& P, int64_t v, bool& bad) {
+    for (int i = 0; i < P.n; ++i) {
+        const PostOp& o = P.op[i];
+        if (o.check && (v < o.lo || v >= o.hi)) bad = true;
+        switch (o.kind) {
+            case G_HALVE:
+                for (int s = 0; s < o.l; ++s) v = (v + o.c) >> 1;  // floor((v + c) / 2), two's complement
+                break;
+            case G_DIV: v = floordiv(v + o.c, o.S); break;
+            case G_RELU: v = v > 0 ? v : 0; break;
+            case G_SIGN: v = v >= 0 ? 1 : -1; break;
+            default: break;
+        }
+    }
+    return v;
+}
+
 struct ConvP {
     const int64_t* x;
     int64_t* y;
@@ -63,13 +96,15 @@ struct ConvP {
     int C, H, W, F, kh, kw, sh, sw, ph, pw, OH, OW;
     int64_t in_size, out_size;
     int64_t asafe;  // I24: operands |x| <= asafe keep every partial sum inside int32 (host bound, see Layer)
+    Post post;
 };
 constexpr int kFB = 8;  // filters per lane (one input load feeds kFB multiply-adds)
 // I24: 24 x 24-bit multiply-adds into int32 accumulators (v_mad_i32_i24, full rate), exact for operands up to
 // the layer's safe bound; a larger operand marks the input uncertain. Otherwise 32 x 32 -> 64-bit products.
 // Lanes = output pixels, padded to whole waves per (input, filter block): the filter block is wave-uniform, so
-// its weights are scalar loads (KS = 3 / 1: the taps unrolled, a channel's taps merged into wide scalar loads).
-template <int KS, bool I24>
+// its weights are scalar loads (KH x KW > 0: the taps unrolled, a channel's taps merged into wide scalar loads).
+// PAD = false: no tap of a valid output pixel leaves the image (no bounds checks).
+template <int KH, int KW, bool I24, bool PAD>
 __global__ __launch_bounds__(256) void k_g_conv(ConvP p, int64_t total) {
     const int64_t t = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
     if (t >= total) return;
@@ -81,7 +116,7 @@ __global__ __launch_bounds__(256) void k_g_conv(ConvP p, int64_t total) {
     const int fb = __builtin_amdgcn_readfirstlane(static_cast<int>(r % nfb));
     const int64_t b = static_cast<int64_t>(__builtin_amdgcn_readfirstlane(static_cast<int>(r / nfb)));
     if (pix >= OHW) return;
-    const int kh = KS ? KS : p.kh, kw = KS ? KS : p.kw;
+    const int kh = KH ? KH : p.kh, kw = KW ? KW : p.kw;
     const int oy = pix / p.OW, ox = pix - oy * p.OW;
     const int f0 = fb * kFB;
     const int K = p.C * kh * kw;
@@ -95,18 +130,20 @@ __global__ __launch_bounds__(256) void k_g_conv(ConvP p, int64_t total) {
     for (int j = 0; j < kFB; ++j) wf[j] = p.w + static_cast<int64_t>(min(f0 + j, p.F - 1)) * K;
     bool wide = false;
     const int iy0 = oy * p.sh - p.ph, ix0 = ox * p.sw - p.pw;
+    const int64_t HW = static_cast<int64_t>(p.H) * p.W;
+#pragma unroll 2
     for (int c = 0; c < p.C; ++c) {
-        const int64_t* xc = xb + static_cast<int64_t>(c) * p.H * p.W;
+        const int64_t* xc = xb + c * HW;
         const int kc = c * kh * kw;
 #pragma unroll
         for (int dy = 0; dy < kh; ++dy) {
             const int iy = iy0 + dy;
-            const bool rowok = iy >= 0 && iy < p.H;
+            const bool rowok = !PAD || (iy >= 0 && iy < p.H);
             const int64_t* xr = xc + static_cast<int64_t>(iy) * p.W;
 #pragma unroll
             for (int dx = 0; dx < kw; ++dx) {
                 const int ix = ix0 + dx;
-                const int64_t xv = (rowok && ix >= 0 && ix < p.W) ? xr[ix] : 0;
+                const int64_t xv = (!PAD || (rowok && ix >= 0 && ix < p.W)) ? xr[ix] : 0;
                 const int k = kc + dy * kw + dx;
                 if (I24) {
                     wide |= xv > p.asafe || xv < -p.asafe;
@@ -123,11 +160,15 @@ __global__ __launch_bounds__(256) void k_g_conv(ConvP p, int64_t total) {
     }
     if (wide) flag(p.flags, b, kUncertain);
     int64_t* yb = p.y + b * p.out_size;
+    bool bad = false;
 #pragma unroll
     for (int j = 0; j < kFB; ++j) {
         const int f = f0 + j;
-        if (f < p.F) yb[static_cast<int64_t>(f) * OHW + pix] = (I24 ? static_cast<int64_t>(a32[j]) : acc[j]) + p.bias[f];
+        if (f < p.F)
+            yb[static_cast<int64_t>(f) * OHW + pix] =
+                run_post(p.post, (I24 ? static_cast<int64_t>(a32[j]) : acc[j]) + p.bias[f], bad);
     }
+    if (bad) flag(p.flags, b, kBad);
 }
 
 struct DenseP {
@@ -138,6 +179,7 @@ struct DenseP {
     const int32_t* perm;  // channel_tf: input element of column k (null: identity)
     int* flags;
     int64_t in, out, in_size, out_size;
+    Post post;
 };
 __global__ __launch_bounds__(256) void k_g_dense(DenseP p, int64_t total) {
     const int64_t t = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
@@ -146,49 +188,34 @@ __global__ __launch_bounds__(256) void k_g_dense(DenseP p, int64_t total) {
     const int64_t* xb = p.x + b * p.in_size;
     const int32_t* wr = p.w + o * p.in;
     int64_t acc = 0;
-    bool wide = false;
+    bool wide = false, bad = false;
     for (int64_t k = 0; k < p.in; ++k) {
         const int64_t xv = xb[p.perm ? p.perm[k] : k];
         acc += static_cast<int64_t>(operand(xv, wide)) * wr[k];
     }
     if (wide) flag(p.flags, b, kUncertain);
-    p.y[b * p.out_size + o] = acc + p.bias[o];
+    p.y[b * p.out_size + o] = run_post(p.post, acc + p.bias[o], bad);
+    if (bad) flag(p.flags, b, kBad);
 }
 
+// a chain of elementwise layers (the head and its fused successors) or a residual add followed by one
 struct ElemP {
     const int64_t* x;
-    const int64_t* x2;  // G_ADD: the residual source
+    const int64_t* x2;  // add: the residual source (null: none)
     int64_t* y;
     int* flags;
-    int kind, check, l;
-    int64_t lo, hi, S, c;  // check range [lo, hi); rescale: divisor S (G_DIV) and offset c
     int64_t n, in_size, in2_size, out_size;
+    Post post;
 };
-__device__ __forceinline__ int64_t floordiv(int64_t a, int64_t s) {
-    int64_t q = a / s;
-    if ((a % s != 0) && (a < 0)) --q;
-    return q;
-}
 __global__ __launch_bounds__(256) void k_g_elem(ElemP p, int64_t total) {
     const int64_t t = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
     if (t >= total) return;
     const int64_t i = t % p.n, b = t / p.n;
-    const int64_t v = p.x[b * p.in_size + i];
-    if (p.check && (v < p.lo || v >= p.hi)) flag(p.flags, b, kBad);
-    int64_t y;
-    switch (p.kind) {
-        case G_HALVE: {
-            y = v;
-            for (int s = 0; s < p.l; ++s) y = (y + p.c) >> 1;  // floor((y + c) / 2), two's complement
-            break;
-        }
-        case G_DIV: y = floordiv(v + p.c, p.S); break;
-        case G_RELU: y = v > 0 ? v : 0; break;
-        case G_SIGN: y = v >= 0 ? 1 : -1; break;
-        case G_ADD: y = v + p.x2[b * p.in2_size + i]; break;
-        default: y = v;
-    }
-    p.y[b * p.out_size + i] = y;
+    int64_t v = p.x[b * p.in_size + i];
+    if (p.x2) v += p.x2[b * p.in2_size + i];
+    bool bad = false;
+    p.y[b * p.out_size + i] = run_post(p.post, v, bad);
+    if (bad) flag(p.flags, b, kBad);
 }
 
 struct PoolP {
@@ -199,6 +226,7 @@ struct PoolP {
     int64_t lo, hi, span_max;
     int C, H, W, kh, kw, sh, sw, OH, OW;
     int64_t in_size, out_size;
+    Post post;
 };
 __global__ __launch_bounds__(256) void k_g_pool(PoolP p, int64_t total) {
     const int64_t t = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
@@ -217,8 +245,9 @@ __global__ __launch_bounds__(256) void k_g_pool(PoolP p, int64_t total) {
             mn = v < mn ? v : mn;
             sum += v;
         }
-    if (p.check && (mn < p.lo || mx >= p.hi || (p.maxp && mx - mn > p.span_max))) flag(p.flags, b, kBad);
-    p.y[b * p.out_size + o] = p.maxp ? mx : sum;
+    bool bad = p.check && (mn < p.lo || mx >= p.hi || (p.maxp && mx - mn > p.span_max));
+    p.y[b * p.out_size + o] = run_post(p.post, p.maxp ? mx : sum, bad);
+    if (bad) flag(p.flags, b, kBad);
 }
 
 __global__ __launch_bounds__(256) void k_g_out(const int64_t* x, int* flags, int64_t lo, int64_t hi, int64_t n,
@@ -258,6 +287,7 @@ struct Layer {
     // conv: operands |x| <= asafe keep every partial sum inside int32 (asafe * max_f sum_k |w_fk| <= 2^31 - 1;
     // the bias is added in int64) and inside the 24-bit multiplier; 0 = the 64-bit product form
     int64_t asafe = 0;
+    Post post{};  // elementwise layers applied to this layer's output (an elementwise head: its own op first)
 };
 
 inline int knob(const char* name, int dflt) {
@@ -298,7 +328,28 @@ class DevRangeGuard {
             L.kh = geti("kh", 0), L.kw = geti("kw", 0), L.sh = geti("sh", 1), L.sw = geti("sw", 1);
             L.ph = geti("ph", 0), L.pw = geti("pw", 0), L.OH = geti("OH", 0), L.OW = geti("OW", 0);
             L.add_src = geti("add_src", -1);
-            DASH_CHECK(L.kind >= G_CONV && L.kind <= G_IDENT, "DevRangeGuard: unknown layer kind");
+            if (d.contains("post")) {
+                py::list ops = d["post"].cast<py::list>();
+                DASH_CHECK(ops.size() <= static_cast<size_t>(kMaxPost), "DevRangeGuard: too many fused layers");
+                for (auto o : ops) {
+                    py::dict od = o.cast<py::dict>();
+                    PostOp& op = L.post.op[L.post.n++];
+                    op.kind = od["kind"].cast<int>();
+                    DASH_CHECK(op.kind >= G_HALVE && op.kind <= G_SIGN || op.kind == G_IDENT,
+                               "DevRangeGuard: fused layer kind");
+                    op.check = od.contains("check") && od["check"].cast<bool>() ? 1 : 0;
+                    op.lo = op.check ? od["lo"].cast<int64_t>() : 0;
+                    op.hi = op.check ? od["hi"].cast<int64_t>() : 0;
+                    op.l = od.contains("l") ? od["l"].cast<int>() : 0;
+                    op.S = od.contains("S") ? od["S"].cast<int64_t>() : 1;
+                    op.c = od.contains("c") ? od["c"].cast<int64_t>() : 0;
+                    DASH_CHECK(op.kind != G_DIV || op.S >= 1, "DevRangeGuard: rescale divisor");
+                    DASH_CHECK(op.l >= 0 && op.l < 63, "DevRangeGuard: rescale halvings");
+                }
+            }
+            DASH_CHECK(L.kind == G_CONV || L.kind == G_DENSE || L.kind == G_MAXPOOL || L.kind == G_SUMPOOL ||
+                           L.kind == G_ADD || L.kind == G_IDENT,
+                       "DevRangeGuard: unknown layer kind (elementwise layers come as fused ops)");
             DASH_CHECK(L.src >= 0 && static_cast<size_t>(L.src) < ctx_buf_.size(), "DevRangeGuard: bad source");
             DASH_CHECK(L.buf >= 0 && static_cast<size_t>(L.buf) < buf_elems_.size(), "DevRangeGuard: bad buffer");
             DASH_CHECK(L.out_size <= buf_elems_[L.buf], "DevRangeGuard: buffer too small");
@@ -351,12 +402,12 @@ class DevRangeGuard {
             }
             if (L.kind == G_ADD)
                 DASH_CHECK(L.add_src >= 0 && static_cast<size_t>(L.add_src) < ctx_buf_.size(), "DevRangeGuard: add source");
-            if (L.kind >= G_HALVE && L.kind != G_MAXPOOL && L.kind != G_SUMPOOL)
+            if (L.kind == G_ADD || L.kind == G_IDENT)
                 DASH_CHECK(L.in_size == L.out_size, "DevRangeGuard: elementwise layer changes the size");
             layers_.push_back(L);
         }
         DASH_CHECK(!layers_.empty(), "DevRangeGuard: empty circuit");
-        DASH_CHECK(ctx_buf_.size() == layers_.size() + 1, "DevRangeGuard: context map size");
+        DASH_CHECK(ctx_buf_.size() >= 2, "DevRangeGuard: context map size");
         // buffers: chunk inputs each
         for (int64_t e : buf_elems_) {
             int64_t* p = nullptr;
@@ -496,6 +547,19 @@ class DevRangeGuard {
         const int buf = ctx_buf_[idx];
         return {bufs_[buf], buf_elems_[buf]};
     }
+    using ConvK = void (*)(ConvP, int64_t);
+    template <int KH, int KW>
+    static ConvK conv_for(bool i24, bool pad) {
+        return i24 ? (pad ? k_g_conv<KH, KW, true, true> : k_g_conv<KH, KW, true, false>)
+                   : (pad ? k_g_conv<KH, KW, false, true> : k_g_conv<KH, KW, false, false>);
+    }
+    static ConvK conv_kernel(const Layer& L) {
+        const bool i24 = L.asafe > 0, pad = L.ph > 0 || L.pw > 0;
+        if (L.kh == 3 && L.kw == 3) return conv_for<3, 3>(i24, pad);
+        if (L.kh == 2 && L.kw == 2) return conv_for<2, 2>(i24, pad);
+        if (L.kh == 1 && L.kw == 1) return conv_for<1, 1>(i24, pad);
+        return conv_for<0, 0>(i24, pad);
+    }
     void run_chunk(const Ticket& t, int64_t b0, int64_t B) {
         int* flags = t.flags_d + b0;
         for (size_t i = 0; i < layers_.size(); ++i) {
@@ -506,19 +570,14 @@ class DevRangeGuard {
             switch (L.kind) {
                 case G_CONV: {
                     ConvP p{in.first, y, L.w, L.bias, flags, L.C, L.H, L.W, L.F, L.kh, L.kw, L.sh, L.sw, L.ph, L.pw,
-                            L.OH, L.OW, in.second, ys, L.asafe};
+                            L.OH, L.OW, in.second, ys, L.asafe, L.post};
                     const int64_t ohwp = (static_cast<int64_t>(L.OH) * L.OW + 63) & ~int64_t(63);
                     const int64_t total = B * ((L.F + kFB - 1) / kFB) * ohwp;
-                    const bool i24 = L.asafe > 0;
-                    const int ks = (L.kh == 3 && L.kw == 3) ? 3 : (L.kh == 1 && L.kw == 1) ? 1 : 0;
-                    auto k = ks == 3 ? (i24 ? k_g_conv<3, true> : k_g_conv<3, false>)
-                             : ks == 1 ? (i24 ? k_g_conv<1, true> : k_g_conv<1, false>)
-                                       : (i24 ? k_g_conv<0, true> : k_g_conv<0, false>);
-                    hipLaunchKernelGGL(k, dim3(blocks_of(total)), dim3(256), 0, st_, p, total);
+                    hipLaunchKernelGGL(conv_kernel(L), dim3(blocks_of(total)), dim3(256), 0, st_, p, total);
                     break;
                 }
                 case G_DENSE: {
-                    DenseP p{in.first, y, L.w, L.bias, L.perm, flags, L.in_size, L.out_size, in.second, ys};
+                    DenseP p{in.first, y, L.w, L.bias, L.perm, flags, L.in_size, L.out_size, in.second, ys, L.post};
                     const int64_t total = B * L.out_size;
                     hipLaunchKernelGGL(k_g_dense, dim3(blocks_of(total)), dim3(256), 0, st_, p, total);
                     break;
@@ -526,15 +585,14 @@ class DevRangeGuard {
                 case G_MAXPOOL:
                 case G_SUMPOOL: {
                     PoolP p{in.first, y, flags, L.kind == G_MAXPOOL, L.check, L.lo, L.hi, L.span_max, L.C, L.H, L.W,
-                            L.kh, L.kw, L.sh, L.sw, L.OH, L.OW, in.second, ys};
+                            L.kh, L.kw, L.sh, L.sw, L.OH, L.OW, in.second, ys, L.post};
                     const int64_t total = B * L.out_size;
                     hipLaunchKernelGGL(k_g_pool, dim3(blocks_of(total)), dim3(256), 0, st_, p, total);
                     break;
                 }
                 default: {
-                    auto in2 = L.kind == G_ADD ? ctx(t, L.add_src, b0) : in;
-                    ElemP p{in.first, in2.first, y, flags, L.kind, L.check, L.l, L.lo, L.hi, L.S, L.c,
-                            L.out_size, in.second, in2.second, ys};
+                    auto in2 = L.kind == G_ADD ? ctx(t, L.add_src, b0) : std::make_pair<const int64_t*, int64_t>(nullptr, 0);
+                    ElemP p{in.first, in2.first, y, flags, L.out_size, in.second, in2.second, ys, L.post};
                     const int64_t total = B * L.out_size;
                     hipLaunchKernelGGL(k_g_elem, dim3(blocks_of(total)), dim3(256), 0, st_, p, total);
                 }

@@ -216,48 +216,30 @@ class RangeGuard:
 
     # ------------------------------------------------------------------ native GPU path
     def native_spec(self) -> dict:
-        """The DevRangeGuard description of the circuit: per layer its kind, input context, activation buffer,
-        geometry, limits and weights; buffers are shared by context values whose lifetimes do not overlap."""
+        """The DevRangeGuard description of the circuit. Elementwise layers (rescale, ReLU, sign, value-preserving)
+        whose input is read by no other layer are fused into the epilogue of the layer before them ("post": each
+        checks its input range, then applies its function); every remaining group is one launch. Activation
+        buffers are shared by values whose lifetimes do not overlap."""
         c, M, h = self.circuit, self.M, _half(self.M)
-        n = len(c.layers)
+        lay = c.layers
+        n = len(lay)
         srcs = []
-        for i, l in enumerate(c.layers):
+        for i, l in enumerate(lay):
             src = getattr(l, "in_src", None)
             srcs.append(src + 1 if src is not None else i)
-        last_use = {n: n}  # context index -> last layer that reads it (the output: the final check)
-        for i, l in enumerate(c.layers):
-            last_use[srcs[i]] = max(last_use.get(srcs[i], -1), i)
+        readers: dict = {}
+        for i, l in enumerate(lay):
+            readers.setdefault(srcs[i], []).append(i)
             if isinstance(l, L.Add):
-                last_use[l.src + 1] = max(last_use.get(l.src + 1, -1), i)
-        ctx_buf, buf_elems, holder = [0], [], []  # holder[b]: context index held by buffer b
-        layers = []
-        for i, l in enumerate(c.layers):
-            free = [b for b, j in enumerate(holder) if j is None or last_use.get(j, -1) < i]
-            out_size, in_size = int(l.out_size), int(l.in_size)
-            if free:
-                b = free[0]
-                buf_elems[b] = max(buf_elems[b], out_size)
-                holder[b] = i + 1
-            else:
-                b = len(holder)
-                holder.append(i + 1)
-                buf_elems.append(out_size)
-            ctx_buf.append(b)
-            d = dict(src=srcs[i], buf=b, in_size=in_size, out_size=out_size)
+                readers.setdefault(l.src + 1, []).append(i)
+        elem = (L.Rescale, L.Relu, L.Sign, L.Flatten, L.Projection, L.BaseExtension)
+
+        def op_of(i):
+            l, d = lay[i], {}
             lim = self._limits(l)
             if lim is not None:
                 d.update(check=True, lo=int(lim[0]), hi=int(lim[1]))
-            if isinstance(l, L.Conv2d):
-                d.update(kind=0, C=l.C, H=l.H, W=l.W, F=l.F, kh=l.kh, kw=l.kw, sh=l.sh, sw=l.sw, ph=l.ph, pw=l.pw,
-                         OH=l.OH, OW=l.OW, w=_i32(l.q_weights.reshape(l.F, -1)), b=np.asarray(l.q_biases, np.int64))
-            elif isinstance(l, L.Dense):
-                perm = None
-                if l.channel_tf:
-                    K, ch = l.in_size, l.channel_tf
-                    k = np.arange(K)
-                    perm = (k // ch + (k % ch) * (K // ch)).astype(np.int32)
-                d.update(kind=1, w=_i32(l.q_weights), b=np.asarray(l.q_biases, np.int64).reshape(-1), perm=perm)
-            elif isinstance(l, L.Rescale):
+            if isinstance(l, L.Rescale):
                 if l.use_sign_base_extension:
                     d.update(kind=2, l=int(l.l), c=int(h % 2))
                 else:
@@ -267,13 +249,69 @@ class RangeGuard:
                 d.update(kind=4)
             elif isinstance(l, L.Sign):
                 d.update(kind=5)
-            elif isinstance(l, (L.MaxPool2d, L.SumPool2d)):
-                d.update(kind=6 if isinstance(l, L.MaxPool2d) else 7, C=l.C, H=l.H, W=l.W, kh=l.kh, kw=l.kw, sh=l.sh,
-                         sw=l.sw, OH=l.OH, OW=l.OW, span_max=int(self.span_max()))
-            elif isinstance(l, L.Add):
-                d.update(kind=8, add_src=int(l.src + 1))
-            else:  # Flatten, Projection, BaseExtension: value-preserving
+            else:
                 d.update(kind=9)
+            return d
+
+        # groups: a head layer and the elementwise layers fused after it
+        groups, i = [], 0
+        while i < n:
+            g, j = [i], i + 1
+            while (j < n and isinstance(lay[j], elem) and srcs[j] == j and readers.get(j) == [j]
+                   and len(g) - (0 if isinstance(lay[i], elem) else 1) < 6):
+                g.append(j)
+                j += 1
+            groups.append(g)
+            i = j
+        # buffers: the output of group k (context index g[-1] + 1) lives until the last group that reads it
+        group_of_ctx = {g[-1] + 1: k for k, g in enumerate(groups)}
+        last_use = {n: len(groups)}
+        for k, g in enumerate(groups):
+            ins = [srcs[g[0]]] + ([lay[g[0]].src + 1] if isinstance(lay[g[0]], L.Add) else [])
+            for ci in ins:
+                assert ci == 0 or ci in group_of_ctx, "range guard: a fused value is read by a later layer"
+                last_use[ci] = max(last_use.get(ci, -1), k)
+        ctx_buf, buf_elems, holder, layers = [0] * (n + 1), [], [], []
+        for k, g in enumerate(groups):
+            head = lay[g[0]]
+            out_ctx = g[-1] + 1
+            out_size = int(lay[g[-1]].out_size)
+            free = [b for b, cj in enumerate(holder) if last_use.get(cj, -1) < k]
+            if free:
+                b = free[0]
+                buf_elems[b] = max(buf_elems[b], out_size)
+                holder[b] = out_ctx
+            else:
+                b = len(holder)
+                holder.append(out_ctx)
+                buf_elems.append(out_size)
+            for j in g:
+                ctx_buf[j + 1] = b
+            d = dict(src=srcs[g[0]], buf=b, in_size=int(head.in_size), out_size=out_size)
+            post = [op_of(j) for j in g[1:]]
+            if isinstance(head, L.Conv2d):
+                d.update(kind=0, C=head.C, H=head.H, W=head.W, F=head.F, kh=head.kh, kw=head.kw, sh=head.sh,
+                         sw=head.sw, ph=head.ph, pw=head.pw, OH=head.OH, OW=head.OW,
+                         w=_i32(head.q_weights.reshape(head.F, -1)), b=np.asarray(head.q_biases, np.int64))
+            elif isinstance(head, L.Dense):
+                perm = None
+                if head.channel_tf:
+                    K, ch = head.in_size, head.channel_tf
+                    kk = np.arange(K)
+                    perm = (kk // ch + (kk % ch) * (K // ch)).astype(np.int32)
+                d.update(kind=1, w=_i32(head.q_weights), b=np.asarray(head.q_biases, np.int64).reshape(-1), perm=perm)
+            elif isinstance(head, (L.MaxPool2d, L.SumPool2d)):
+                d.update(kind=6 if isinstance(head, L.MaxPool2d) else 7, C=head.C, H=head.H, W=head.W, kh=head.kh,
+                         kw=head.kw, sh=head.sh, sw=head.sw, OH=head.OH, OW=head.OW, span_max=int(self.span_max()))
+                lim = self._limits(head)
+                if lim is not None:
+                    d.update(check=True, lo=int(lim[0]), hi=int(lim[1]))
+            elif isinstance(head, L.Add):
+                d.update(kind=8, add_src=int(head.src + 1))
+            else:  # an elementwise head: its own op first
+                d.update(kind=9)
+                post = [op_of(g[0])] + post
+            d["post"] = post
             layers.append(d)
         return dict(layers=layers, input_size=int(c.input_size), ctx_buf=ctx_buf, buf_elems=buf_elems,
                     out_lo=-h, out_hi=M - h)

@@ -150,15 +150,30 @@ def _simulate_spec(spec, xs):
     X = np.asarray(xs, dtype=np.int64)
     B = X.shape[0]
     bufs = [np.full((B, e), 7777777, dtype=np.int64) for e in spec["buf_elems"]]
-    flags = np.zeros(B, dtype=np.int64)
+    flags = np.zeros(B, dtype=bool)
 
     def ctx(i):
         return X if i == 0 else bufs[spec["ctx_buf"][i]]
 
+    def post(ops, y):
+        nonlocal flags
+        for o in ops:
+            if o.get("check"):
+                flags |= ((y < o["lo"]) | (y >= o["hi"])).any(axis=1)
+            k = o["kind"]
+            if k == 2:
+                for _ in range(o["l"]):
+                    y = (y + o["c"]) >> 1
+            elif k == 3:
+                y = (y + o["c"]) // o["S"]
+            elif k == 4:
+                y = np.maximum(y, 0)
+            elif k == 5:
+                y = np.where(y >= 0, 1, -1)
+        return y
+
     for d in spec["layers"]:
         x = ctx(d["src"])[:, :d["in_size"]].copy()
-        if d.get("check"):
-            flags |= ((x < d["lo"]) | (x >= d["hi"])).any(axis=1)
         k = d["kind"]
         if k == 0:
             C, H, W = d["C"], d["H"], d["W"]
@@ -173,21 +188,13 @@ def _simulate_spec(spec, xs):
         elif k == 1:
             xin = x if d.get("perm") is None else x[:, d["perm"]]
             y = xin @ d["w"].astype(np.int64).T + d["b"]
-        elif k == 2:
-            y = x
-            for _ in range(d["l"]):
-                y = (y + d["c"]) >> 1
-        elif k == 3:
-            y = (x + d["c"]) // d["S"]
-        elif k == 4:
-            y = np.maximum(x, 0)
-        elif k == 5:
-            y = np.where(x >= 0, 1, -1)
         elif k in (6, 7):
             v = x.reshape(B, d["C"], d["H"], d["W"])
             ws = [v[:, :, dy:dy + d["sh"] * (d["OH"] - 1) + 1:d["sh"], dx:dx + d["sw"] * (d["OW"] - 1) + 1:d["sw"]]
                   for dy in range(d["kh"]) for dx in range(d["kw"])]
             st = np.stack(ws)
+            if d.get("check"):
+                flags |= ((x < d["lo"]) | (x >= d["hi"])).any(axis=1)
             if k == 6:
                 y = st.max(axis=0)
                 if d.get("check"):
@@ -199,7 +206,7 @@ def _simulate_spec(spec, xs):
             y = x + ctx(d["add_src"])[:, :d["in_size"]]
         else:
             y = x
-        bufs[d["buf"]][:, :d["out_size"]] = y
+        bufs[d["buf"]][:, :d["out_size"]] = post(d.get("post", []), y)
     out = bufs[spec["layers"][-1]["buf"]][:, :spec["layers"][-1]["out_size"]]
     flags |= ((out < spec["out_lo"]) | (out >= spec["out_hi"])).any(axis=1)
     return [int(i) for i in np.nonzero(flags)[0]], out
@@ -236,7 +243,8 @@ def test_native_spec_matches_numpy_model():
             rng = np.random.default_rng(0)
             X = [rng.integers(-20, 21, circ.input_size) for _ in range(6)] + [rng.integers(-900, 900, circ.input_size)]
         spec = g.native_spec()
-        assert len(spec["buf_elems"]) < len(circ.layers)  # values whose lifetimes end share buffers
+        assert len(spec["buf_elems"]) < len(spec["layers"])  # values whose lifetimes end share buffers
+        assert len(spec["layers"]) < len(circ.layers)  # elementwise layers fused into the layer before them
         bad, out = _simulate_spec(spec, X)
         assert bad == [i for i, x in enumerate(X) if g.violations_np(x)]
         for i, x in enumerate(X):
