@@ -147,7 +147,7 @@ def visible_gpus() -> int:
     from .parallel.dist import kfd_gpus, visible_indices
 
     gpus = kfd_gpus()
-    return len(visible_indices(len(gpus)))
+    return len(visible_indices(len(gpus), None, gpus))
 
 
 def spawn_ranks(args, argv: List[str]) -> int:

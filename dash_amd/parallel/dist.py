@@ -50,13 +50,28 @@ def kfd_gpus(root: Optional[str] = None) -> list:
             continue  # CPU agent
         loc, dom = props.get("location_id", 0), props.get("domain", 0)
         pci = f"{dom:04x}:{(loc >> 8) & 0xff:02x}:{(loc >> 3) & 0x1f:02x}.{loc & 7:x}"
-        out.append({"node": int(name), "pci": pci, "gfx": props.get("gfx_target_version", 0)})
-    return out
+        out.append({"node": int(name), "pci": pci, "gfx": props.get("gfx_target_version", 0),
+                    "unique_id": props.get("unique_id"), "render_minor": props.get("drm_render_minor")})
+    return _accessible(out)
 
 
-def visible_indices(n: int, env: Optional[dict] = None) -> list:
+def _accessible(gpus: list) -> list:
+    """The GPUs whose DRM render node this process may open (HIP enumerates only those; sysfs is not namespaced,
+    so a container sees every GPU of the host there). Unfiltered when no render node can be checked at all
+    (no /dev/dri, or no node lists its render minor): never guess a smaller count from missing information."""
+    dri = os.environ.get("DASH_DRI_DIR", "/dev/dri")
+    if not os.path.isdir(dri) or not any(g.get("render_minor") is not None for g in gpus):
+        return gpus
+    ok = [g for g in gpus if g.get("render_minor") is None
+          or os.access(os.path.join(dri, f"renderD{g['render_minor']}"), os.R_OK | os.W_OK)]
+    return ok if ok else gpus
+
+
+def visible_indices(n: int, env: Optional[dict] = None, gpus: Optional[list] = None) -> list:
     """Indices (into the KFD GPU list) a HIP process started with `env` would see: ROCR_VISIBLE_DEVICES
-    filters first, then HIP_VISIBLE_DEVICES / CUDA_VISIBLE_DEVICES index into what remains."""
+    filters first, then HIP_VISIBLE_DEVICES / CUDA_VISIBLE_DEVICES index into what remains. Entries are
+    ordinals or (ROCR_VISIBLE_DEVICES) UUIDs ``GPU-<16 hex digits of the KFD unique_id>``, matched against
+    `gpus` (kfd_gpus entries); an entry that matches nothing ends the list, as in HIP."""
     env = os.environ if env is None else env
     idx = list(range(n))
     for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
@@ -71,6 +86,13 @@ def visible_indices(n: int, env: Optional[dict] = None) -> list:
             tok = tok.strip()
             if tok.isdigit() and int(tok) < len(idx):
                 sel.append(idx[int(tok)])
+            elif tok.upper().startswith("GPU-") and gpus is not None:
+                want = tok[4:].lower()
+                hit = [i for i in idx if gpus[i].get("unique_id") is not None
+                       and f"{gpus[i]['unique_id']:016x}" == want.rjust(16, "0")]
+                if not hit:
+                    break
+                sel.append(hit[0])
             else:
                 break  # HIP stops at the first invalid entry
         idx = sel
@@ -85,7 +107,7 @@ def rank_gpu(local_rank: int, env: Optional[dict] = None) -> Optional[dict]:
         gpus = kfd_gpus()
     except RuntimeError:
         return None
-    vis = visible_indices(len(gpus), env)
+    vis = visible_indices(len(gpus), env, gpus)
     if not 0 <= local_rank < len(vis):
         return None
     g = gpus[vis[local_rank]]
@@ -99,7 +121,7 @@ def gpu_local_cpus(local_rank: int) -> Optional[set]:
         gpus = kfd_gpus()
     except RuntimeError:
         return None
-    vis = visible_indices(len(gpus))
+    vis = visible_indices(len(gpus), None, gpus)
     if local_rank >= len(vis):
         return None
     path = f"/sys/bus/pci/devices/{gpus[vis[local_rank]]['pci']}/local_cpulist"

@@ -90,8 +90,9 @@ def test_bench_driver_gloo(world):
     assert abs(out["value"] - world * 2 * 2 / (out["ms_per_step"] * 2 / 1000.0)) / out["value"] < 0.01
 
 
-def _fake_kfd(root, n_gpus):
-    """A KFD topology like an MI355X node's: node 0 a CPU agent, nodes 1..n GPUs on distinct PCI buses."""
+def _fake_kfd(root, n_gpus, ids=False):
+    """A KFD topology like an MI355X node's: node 0 a CPU agent, nodes 1..n GPUs on distinct PCI buses (ids: with
+    unique_id and drm_render_minor 128 + i)."""
     os.makedirs(os.path.join(root, "0"))
     with open(os.path.join(root, "0", "properties"), "w") as f:
         f.write("cpu_cores_count 96\nsimd_count 0\ngfx_target_version 0\n")
@@ -101,8 +102,34 @@ def _fake_kfd(root, n_gpus):
         os.makedirs(os.path.join(root, str(i + 1)))
         with open(os.path.join(root, str(i + 1), "properties"), "w") as f:
             f.write(f"simd_count 1024\ngfx_target_version 90500\nlocation_id {bus << 8}\ndomain 0\n")
+            if ids:
+                f.write(f"unique_id {0x1234abcd0000 + i}\ndrm_render_minor {128 + i}\n")
         buses.append(f"0000:{bus:02x}:00.0")
     return buses
+
+
+def test_visible_gpus_uuid_and_render_nodes(tmp_path, monkeypatch):
+    """ROCR_VISIBLE_DEVICES may name GPUs by UUID (GPU-<unique_id hex>); sysfs lists every GPU of the host, but
+    only those whose render node this process can open are enumerated by HIP (a container's share)."""
+    from dash_amd.parallel.dist import kfd_gpus, rank_gpu, visible_indices
+
+    buses = _fake_kfd(str(tmp_path / "kfd"), 8, ids=True)
+    monkeypatch.setenv("DASH_KFD_TOPOLOGY", str(tmp_path / "kfd"))
+    dri = tmp_path / "dri"
+    dri.mkdir()
+    monkeypatch.setenv("DASH_DRI_DIR", str(dri))
+    for i in (2, 5):  # this "container" owns GPUs 2 and 5
+        (dri / f"renderD{128 + i}").write_text("")
+    gpus = kfd_gpus()
+    assert [g["pci"] for g in gpus] == [buses[2], buses[5]]
+    uid5 = f"GPU-{0x1234abcd0000 + 5:016x}"
+    assert visible_indices(len(gpus), {"ROCR_VISIBLE_DEVICES": uid5}, gpus) == [1]
+    assert visible_indices(len(gpus), {"ROCR_VISIBLE_DEVICES": f"{uid5},GPU-ffff"}, gpus) == [1]  # stops at a miss
+    assert rank_gpu(0, {"ROCR_VISIBLE_DEVICES": uid5})["pci"] == buses[5]
+    # nothing checkable (no render node accessible): the full list, never a guessed smaller count
+    for f in dri.iterdir():
+        f.unlink()
+    assert len(kfd_gpus()) == 8
 
 
 def test_rank_gpu_follows_local_rank(tmp_path):
