@@ -43,6 +43,9 @@ struct EncIn {
     const act_t* r[kMaxRes];   // [n_j] the offset R_{p_j}
     act_t* out[kMaxRes];       // [n_j][N] an evaluator slot's input activations (slot s + 1 follows n_j N later)
     int64_t wstride;           // bytes between the encoder slots' W0 / R blocks (grid z = slot)
+    // set by launch_encode_in: component prefix of residue j (pre[k] = total) and 1 / p_j
+    int pre[kMaxRes + 1];
+    float inv[kMaxRes];
 };
 
 struct SignArgs {

@@ -263,28 +263,48 @@ void launch_fetch_res(const FetchRes& a, hipStream_t st) {
 }
 
 // Online message #1 encoded on the device by the garbler (core.h lab_affine per component, reference
-// garbled_circuit_interface.h garble_inputs): grid (ceil(n_max N / 256), k, slots), one lane per (component,
-// element) of a residue and slot, elements fastest (coalesced byte rows of the component-major layout). A lane
-// per element looping over its n_j components was a 60 us launch at batch 1 (84 workgroups, r05 timeline).
+// garbled_circuit_interface.h garble_inputs): grid (ceil(sum_j n_j N / 256), 1, slots), one lane per
+// (residue, component, element) of a slot through the component prefix a.pre, elements fastest (coalesced byte
+// rows of the component-major layout), so no lane idles on a residue narrower than the widest (a grid sized by
+// max_j n_j left 54 % of the MiniONN lanes without work). Both reductions (x mod p, (w + v r) mod p) are a
+// float-reciprocal quotient plus one correction, exact below 2^22; an input beyond that takes the 64-bit path.
+__device__ __forceinline__ uint32_t mod_small(int64_t x, uint32_t p, float inv) {
+    if (x > -(int64_t(1) << 22) && x < (int64_t(1) << 22)) {
+        const int32_t xi = static_cast<int32_t>(x);
+        int32_t r = xi - static_cast<int32_t>(floorf(static_cast<float>(xi) * inv)) * static_cast<int32_t>(p);
+        if (r < 0) r += p;
+        if (r >= static_cast<int32_t>(p)) r -= p;
+        return static_cast<uint32_t>(r);
+    }
+    const int64_t r = x % static_cast<int64_t>(p);
+    return static_cast<uint32_t>(r < 0 ? r + p : r);
+}
 __global__ __launch_bounds__(256) void k_encode_in(EncIn a, const int64_t* __restrict__ x, int64_t N) {
-    const int j = blockIdx.y, s = blockIdx.z;
-    const int p = a.p[j], n = a.n[j];
+    const int s = blockIdx.z;
     const uint32_t t = blockIdx.x * 256u + threadIdx.x;
     const uint32_t N32 = static_cast<uint32_t>(N);
-    const uint32_t c = t / N32, e = t - c * N32;
-    if (c >= static_cast<uint32_t>(n)) return;
-    int64_t v64 = x[static_cast<int64_t>(s) * N + e] % p;
-    const uint32_t v = static_cast<uint32_t>(v64 < 0 ? v64 + p : v64);
+    const uint32_t ca = t / N32, e = t - ca * N32;  // component across residues, element
+    if (ca >= static_cast<uint32_t>(a.pre[a.k])) return;
+    int j = 0;
+    while (j + 1 < a.k && static_cast<uint32_t>(a.pre[j + 1]) <= ca) ++j;
+    const uint32_t c = ca - static_cast<uint32_t>(a.pre[j]);
+    const uint32_t p = static_cast<uint32_t>(a.p[j]);
+    const float inv = a.inv[j];
+    const uint32_t v = mod_small(x[static_cast<int64_t>(s) * N + e], p, inv);
     const uint32_t w = a.w0[j][s * a.wstride + static_cast<int64_t>(c) * N + e];
     const uint32_t r = a.r[j][s * a.wstride + c];
-    a.out[j][(static_cast<int64_t>(s) * n + c) * N + e] = static_cast<act_t>((w + v * r) % static_cast<uint32_t>(p));
+    a.out[j][(static_cast<int64_t>(s) * a.n[j] + c) * N + e] = static_cast<act_t>(mod_small(w + v * r, p, inv));
 }
-void launch_encode_in(const EncIn& a, const int64_t* x, int64_t N, int slots, hipStream_t st) {
-    int nmx = 1;
-    for (int j = 0; j < a.k; ++j) nmx = std::max(nmx, a.n[j]);
-    const int64_t lanes = static_cast<int64_t>(nmx) * N;  // < 2^32 (host-checked: N n_max fits 32 bits)
-    hipLaunchKernelGGL(k_encode_in,
-                       dim3(static_cast<unsigned>((lanes + 255) / 256), static_cast<unsigned>(a.k), static_cast<unsigned>(slots)),
+void launch_encode_in(const EncIn& a0, const int64_t* x, int64_t N, int slots, hipStream_t st) {
+    EncIn a = a0;
+    a.pre[0] = 0;
+    for (int j = 0; j < a.k; ++j) {
+        a.pre[j + 1] = a.pre[j] + a.n[j];
+        a.inv[j] = 1.0f / static_cast<float>(a.p[j]);
+    }
+    const int64_t lanes = static_cast<int64_t>(a.pre[a.k]) * N;
+    if (lanes >= (int64_t(1) << 32)) throw std::runtime_error("encode_in: input too large for 32-bit lane indices");
+    hipLaunchKernelGGL(k_encode_in, dim3(static_cast<unsigned>((lanes + 255) / 256), 1, static_cast<unsigned>(slots)),
                        dim3(256), 0, st, a, x, N);
 }
 
