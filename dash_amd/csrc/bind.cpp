@@ -201,16 +201,14 @@ PYBIND11_MODULE(_dash_native, m) {
         return out;
     });
     m.def("gen_approx_lookup", &gen_approx_lookup);
-    m.def("prg_label", [](py::bytes seed, uint64_t stream, uint64_t ctr, int p, bool hardened) {
+    m.def("prg_label", [](py::bytes seed, uint64_t stream, uint64_t ctr, int p) {
         std::string s = seed;
         DASH_CHECK(s.size() == 16, "seed must be 16 bytes");
         Prg prg(reinterpret_cast<const uint8_t*>(s.data()));
-        prg.chacha = hardened;
         py::array_t<int16_t> out(nr_comps(p));
         prg.label(stream, ctr, p, nr_comps(p), out.mutable_data());
         return out;
-    }, py::arg("seed"), py::arg("stream"), py::arg("ctr"), py::arg("p"), py::arg("hardened") = false,
-       "label of Prg(seed) on `stream` from block ctr (hardened: the ChaCha12 label PRG)");
+    });
     m.def("kind_name", &kind_name);
 
     // Single gates of the native garbler with caller-chosen labels (wire-compatibility vectors: the tests

@@ -336,7 +336,6 @@ enum TweakKind : uint32_t {
     TW_PROJ = 11,   // projection layer
     TW_GME = 12,    // generalized half gate, evaluator half (key y_j)
     TW_MMT = 13,    // mixed-mult layer: the residue-j mod transform (key x_2e+1)
-    TW_PRG = 14,    // label PRG of a hardened garbling (key: the garbler seed; Prg::label)
 };
 inline uint32_t tw_sub(TweakKind k, uint32_t idx) { return (static_cast<uint32_t>(k) << 16) | (idx & 0xffffu); }
 
@@ -360,39 +359,20 @@ struct Mask {
 // ----------------------------------------------------------------------------
 struct Prg {
     AesKey key;
-    u128 seed = 0;        // the seed as a little-endian 128-bit key (ChaCha form)
-    bool chacha = false;  // hardened garblings: label blocks from ChaCha12 instead of AES-128
-    explicit Prg(const uint8_t seed16[16]) {
-        aes_expand(seed16, key);
-        std::memcpy(&seed, seed16, 16);
-    }
+    explicit Prg(const uint8_t seed[16]) { aes_expand(seed, key); }
     Prg() {
         uint8_t z[16] = {0};
         aes_expand(z, key);
     }
-    // n components of a uniform label mod p: block b gives components b*m .. b*m + m - 1 as its least
-    // significant base-p digits (m = prg_digits(p)); ctr advances by prg_blocks(p). Block c of `stream` is
-    // AES_seed(stream || c), or with `chacha` (hardened garblings) word group c & 3 of the ChaCha12 block
-    // hard_block(seed, stream, (TW_PRG, 0), c >> 2): four label blocks per ChaCha block, pure integer work on
-    // the GPU (no LDS AES image). The GPU garbler (garble_gpu.hip k_draw / k_draw_hard) produces the same digits.
+    // n components of a uniform label mod p: block b = AES_seed(stream || ctr + b) gives components
+    // b*m .. b*m + m - 1 as its least significant base-p digits (m = prg_digits(p)); ctr advances by
+    // prg_blocks(p). The GPU garbler (garble_gpu.hip k_draw) produces the same digits.
     inline void label(u64 stream, u64& ctr, int p, int n, comp_t* out) const {
         const ModInfo& mi = mod_info(p);
         const int m = mi.prg_m;
-        u128 pads[4];
-        u64 have = ~u64(0);
         for (int j = 0; j < n; j += m) {
-            u128 V;
-            const u64 c = ctr++;
-            if (chacha) {
-                if ((c >> 2) != have) {
-                    have = c >> 2;
-                    hard_block(seed, stream, tw_sub(TW_PRG, 0), static_cast<uint32_t>(have), pads);
-                }
-                V = pads[c & 3];
-            } else {
-                u128 blk = (static_cast<u128>(stream) << 64) | c;
-                V = m_to_u128(aes_enc_block(u128_to_m(blk), key));
-            }
+            u128 blk = (static_cast<u128>(stream) << 64) | ctr++;
+            u128 V = m_to_u128(aes_enc_block(u128_to_m(blk), key));
             const int cnt = std::min(m, n - j);
             if (mi.pow2) {
                 for (int u = 0; u < cnt; ++u, V >>= mi.bits) out[j + u] = static_cast<comp_t>(static_cast<u64>(V) & (p - 1));
@@ -401,7 +381,7 @@ struct Prg {
             for (int u = 0; u < cnt;) {
                 u64 r = static_cast<u64>(V % mi.pchunk);  // chunk of `chunk` digits
                 V /= mi.pchunk;
-                for (int c2 = 0; c2 < mi.chunk && u < cnt; ++c2, ++u) {
+                for (int c = 0; c < mi.chunk && u < cnt; ++c, ++u) {
                     out[j + u] = static_cast<comp_t>(r % static_cast<u64>(p));
                     r /= static_cast<u64>(p);
                 }

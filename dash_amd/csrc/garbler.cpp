@@ -361,7 +361,6 @@ GarbledModel Garbler::garble(const std::vector<LayerSpec>& layers, const std::ve
     const bool hard = opt.hardened;
     m.h.sign_fused = fused ? 1 : 0;
     m.h.hardened = hard ? 1 : 0;
-    prg_.chacha = hard;  // hardened garblings draw every label from the ChaCha12 PRG (core.h Prg::label)
     if (hard) {
         // the hardened encoding keys no projection with a public label (docs/SECURITY.md): the reference's
         // cast construction (zero-label carry) and the legacy rescale (zero-label residue 0 -> sign gadget) do

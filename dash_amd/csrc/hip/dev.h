@@ -480,7 +480,7 @@ __device__ __forceinline__ void hard_block(u128 K, uint64_t gate, uint32_t sub, 
 
 // Tweak kinds (core.h TweakKind) and the sub word of row `idx`
 constexpr uint32_t kTwApprox = 1, kTwCast2 = 3, kTwSign = 4, kTwMmg = 5, kTwMmy = 6, kTwMrs = 7, kTwSmrs = 8,
-                   kTwBe = 9, kTwTrans = 10, kTwProj = 11, kTwGme = 12, kTwMmt = 13, kTwPrg = 14;
+                   kTwBe = 9, kTwTrans = 10, kTwProj = 11, kTwGme = 12, kTwMmt = 13;
 __host__ __device__ __forceinline__ constexpr uint32_t tw_sub(uint32_t kind, uint32_t idx) { return (kind << 16) | (idx & 0xffffu); }
 // gate of element e of a gadget whose PRG streams are stream_id(L, slot, e) (core.h): base = stream_id(L, slot, 0)
 __host__ __device__ __forceinline__ constexpr uint64_t gate_base(uint64_t layer, uint64_t slot) {

@@ -85,7 +85,6 @@ struct Ctx {
     // iR[p] = [p][4 * chunks(n_p)] words, row i = the components i * R_p[q] mod p packed two per word
     const uint32_t* const* iR;
     int hard;  // hardened encoding: HC holds the compressed keys, k_emit / k_relu_finish derive tweaked pads
-    uint64_t seed_lo, seed_hi;  // the garbler seed as a 128-bit key (hardened label PRG, k_draw_hard)
 };
 
 // Chunked component-major labels (all device labels of the GPU garbler): the
@@ -382,95 +381,6 @@ __global__ __launch_bounds__(kGB) void k_draw(Ctx c, Gadget g) {
             }
         }
         if (n & 7) {  // last partial chunk: shift the pending components down, zeros above
-            const u128 last = acc >> (16 * (8 - (n & 7)));
-            u32x4a v;
-            v[0] = static_cast<uint32_t>(last);
-            v[1] = static_cast<uint32_t>(last >> 32);
-            v[2] = static_cast<uint32_t>(last >> 64);
-            v[3] = static_cast<uint32_t>(last >> 96);
-            st_chunk(out + (n >> 3) * cs, v);
-        }
-    }
-}
-
-// k_draw for hardened garblings (core.h Prg::label, chacha): the label's blocks ctr .. ctr + nb - 1 (nb <= 3)
-// are word groups of at most two ChaCha12 blocks hard_block(seed, stream, (TW_PRG, 0), ctr >> 2 ...): VALU only,
-// no LDS AES image, so the kernel runs at full occupancy (the AES form was bound by dependent LDS lookups).
-__device__ __forceinline__ u128 pick8(const u128 (&A)[4], const u128 (&B)[4], int i) {
-    u128 v = A[0];
-#pragma unroll
-    for (int u = 1; u < 4; ++u) v = i == u ? A[u] : v;
-#pragma unroll
-    for (int u = 0; u < 4; ++u) v = i == 4 + u ? B[u] : v;
-    return v;
-}
-__global__ __launch_bounds__(256) void k_draw_hard(Ctx c, Gadget g) {
-    const int64_t N = g.N;
-    const int64_t tiles = (N + kTile - 1) / kTile;
-    const int64_t nw = tiles * g.ndraws;
-    const int lane = static_cast<int>(threadIdx.x) & (kTile - 1);
-    const int64_t wpb = 256 / kTile;
-    const int64_t w0 = static_cast<int64_t>(blockIdx.x) * wpb + rfl(static_cast<int>(threadIdx.x) / kTile);
-    const int64_t wstep = static_cast<int64_t>(gridDim.x) * wpb;
-    const int64_t cs = N * kCh;
-    const u128 seed = (static_cast<u128>(c.seed_hi) << 64) | c.seed_lo;
-    for (int64_t w = w0; w < nw; w += wstep) {
-        const int di = static_cast<int>(w / tiles);
-        const int64_t tile = w - static_cast<int64_t>(di) * tiles;
-        const int64_t e = tile * kTile + lane;
-        const Draw d{rfl(g.draws[di].slot), rfl(g.draws[di].q), rfl(g.draws[di].ctr)};
-        const ModC m = rfl_modc(c.mc[d.q]);
-        const int n = static_cast<int>(m.n), pm = static_cast<int>(m.pm);
-        if (e >= N) continue;
-        const uint64_t stream = stream_of(g.layer, g.sslot, static_cast<uint64_t>(e), g.mask);
-        int16_t* out = slot_base(g, d.slot) + e * kCh;
-        const int nb = (n + pm - 1) / pm;
-        const int c0 = d.ctr & 3;
-        u128 PA[4], PB[4];
-        hard_block(seed, stream, tw_sub(kTwPrg, 0), static_cast<uint32_t>(d.ctr >> 2), PA);
-        if (c0 + nb > 4) {
-            hard_block(seed, stream, tw_sub(kTwPrg, 0), static_cast<uint32_t>(d.ctr >> 2) + 1u, PB);
-        } else {
-#pragma unroll
-            for (int u = 0; u < 4; ++u) PB[u] = 0;
-        }
-        u128 acc = 0;  // pending components, the oldest in the low 16 bits once 8 are in
-        auto push = [&](int q, uint32_t dg) {
-            acc = (acc >> 16) | (static_cast<u128>(dg) << 112);
-            if ((q & 7) == 7) {
-                u32x4a v;
-                v[0] = static_cast<uint32_t>(acc);
-                v[1] = static_cast<uint32_t>(acc >> 32);
-                v[2] = static_cast<uint32_t>(acc >> 64);
-                v[3] = static_cast<uint32_t>(acc >> 96);
-                st_chunk(out + (q >> 3) * cs, v);
-            }
-        };
-        if (m.bits) {
-            DigitStream ds;
-            int blk = 0, left = 0;
-            for (int q = 0; q < n; ++q) {
-                if (left == 0) {
-                    ds.init(pick8(PA, PB, c0 + blk));
-                    ++blk;
-                    left = pm;
-                }
-                push(q, ds.next(m));
-                --left;
-            }
-        } else {
-            int q = 0;
-            for (int bi = 0; bi < nb; ++bi) {
-                u128 Q = pick8(PA, PB, c0 + bi);
-                const int bcnt = min(pm, n - bi * pm);
-                for (int k0 = 0; k0 < bcnt; k0 += static_cast<int>(m.c)) {
-                    uint32_t r = divmod128(Q, m);
-                    const int kc = min(static_cast<int>(m.c), bcnt - k0);
-                    for (int t = 0; t < kc; ++t, ++q) push(q, chunk_digit(r, m));
-                }
-            }
-        }
-        if (n & 7) {
             const u128 last = acc >> (16 * (8 - (n & 7)));
             u32x4a v;
             v[0] = static_cast<uint32_t>(last);
@@ -2299,16 +2209,6 @@ unsigned draw_grid(const gg::Gadget& g) {
     return blocks_for(lanes, gg::kGB, 16384);
 }
 
-// the label draws of a gadget: AES-CTR (reference encoding) or the hardened ChaCha PRG (core.h Prg::label)
-void launch_draw(const gg::Ctx& c, const gg::Gadget& g) {
-    if (c.hard) {
-        const int64_t lanes = (g.N + gg::kTile - 1) / gg::kTile * gg::kTile * g.ndraws;
-        hipLaunchKernelGGL(gg::k_draw_hard, dim3(blocks_for(lanes, 256, 65536)), dim3(256), 0, gg::tl_st, c, g);
-        return;
-    }
-    hipLaunchKernelGGL(gg::draw_kernel(), dim3(draw_grid(g)), dim3(gg::kGB), 0, gg::tl_st, c, g);
-}
-
 // AES-CTR blocks per element: draws are laid out back to back in counter order
 int draw_blocks(const std::vector<gg::Draw>& d) {
     if (d.empty()) return 0;
@@ -2632,7 +2532,7 @@ void run_sign(const gg::Ctx& c, const gg::SignLayout& L, gg::Gadget& g, const gg
     g.nblk = draw_blocks(L.draws);
     for (int d = 0; d < L.ss.t; ++d) g.mrs[d] = L.fan[d];
     check_desc(g);
-    launch_draw(c, g);
+    hipLaunchKernelGGL(gg::draw_kernel(), dim3(draw_grid(g)), dim3(gg::kGB), 0, gg::tl_st, c, g);
     hipLaunchKernelGGL(gg::k_sign_derive, dim3(blocks_for(g.N, 256), L.ss.t), dim3(256), 0, gg::tl_st, c, g, L.ss);
     project(c, g, in, tb, L.projs, fx);
     HIPCHECK(hipGetLastError());
@@ -2958,8 +2858,6 @@ GpuGarbler::GpuGarbler(const std::vector<int>& crt, const std::vector<int>& mrs,
     I.c.iR = nullptr;
     auto rk = round_key_words(reinterpret_cast<const uint8_t*>(seed16.data()));
     std::copy(rk.begin(), rk.end(), I.c.rk);
-    std::memcpy(&I.c.seed_lo, seed16.data(), 8);
-    std::memcpy(&I.c.seed_hi, seed16.data() + 8, 8);
     if (!mrs.empty()) {
         auto lut = gen_approx_lookup(crt, mrs);
         for (int j = 0; j < I.k; ++j) {
@@ -3243,7 +3141,7 @@ static std::vector<DevBlock> sign_core(GpuGarbler::Impl& I, uint64_t layer, uint
         gm.entries = first;
         gm.nblk = draw_blocks(dr);
         check_desc(gm);
-        launch_draw(I.c, gm);
+        hipLaunchKernelGGL(gg::draw_kernel(), dim3(draw_grid(gm)), dim3(gg::kGB), 0, gg::tl_st, I.c, gm);
         project(I.c, gm, in, tb, pr);
         gg::MiniArgs ma{};
         ma.k = k;
@@ -3438,7 +3336,7 @@ static std::vector<DevBlock> relu_mult_gates(GpuGarbler::Impl& I, const gg::Gadg
     gm.entries = f2;
     gm.nblk = draw_blocks(dm);
     check_desc(gm);
-    launch_draw(I.c, gm);
+    hipLaunchKernelGGL(gg::draw_kernel(), dim3(draw_grid(gm)), dim3(gg::kGB), 0, gg::tl_st, I.c, gm);
     project(I.c, gm, in, tb, pm);
     gg::MiniArgs ma{};
     ma.k = k;
@@ -3538,7 +3436,7 @@ void GpuGarbler::relu_mrs(uint64_t layer, const SignMrsPlan& P, CrtLabels& cur, 
 
     check_desc(g);
     std::vector<void*> tmp;
-    launch_draw(I.c, g);
+    hipLaunchKernelGGL(gg::draw_kernel(), dim3(draw_grid(g)), dim3(gg::kGB), 0, gg::tl_st, I.c, g);
     hipLaunchKernelGGL(gg::k_mrs_sign_derive, dim3(blocks_for(N, 256), k), dim3(256), 0, gg::tl_st, I.c, g, in, a);
     project(I.c, g, in, tb, pr, ProjFns{&flut, &fan});
     // mixed-modulus half gates (as sign_layer's ReLU branch, sign label = residue 0's key slot)
@@ -3653,7 +3551,7 @@ void GpuGarbler::rescale_mrs(uint64_t layer, const RescaleMrsPlan& P, CrtLabels&
     check_desc(g);
     gg::In in{};
     std::vector<void*> tmp;
-    launch_draw(I.c, g);
+    hipLaunchKernelGGL(gg::draw_kernel(), dim3(draw_grid(g)), dim3(gg::kGB), 0, gg::tl_st, I.c, g);
     int ny = 0;
     for (int j = 0; j <= k; ++j) {
         const int nc = static_cast<int>(gg::chunks_of(nr_comps(j < k ? P.crt[j] : static_cast<int>(P.T))));
@@ -4179,7 +4077,7 @@ void GpuGarbler::rescale_redash(uint64_t layer, int it, const RescalePlan& P, Cr
     g.ndraws = static_cast<int>(dr.size());
     g.nblk = draw_blocks(dr);
     check_desc(g);
-    launch_draw(I.c, g);
+    hipLaunchKernelGGL(gg::draw_kernel(), dim3(draw_grid(g)), dim3(gg::kGB), 0, gg::tl_st, I.c, g);
     std::vector<int16_t*> L(k);
     for (int j = 0; j < k; ++j) L[j] = I.cur[j].as<int16_t>();
     std::vector<gg::LinJob> jobs;
@@ -4271,7 +4169,7 @@ void GpuGarbler::base_ext(uint64_t layer, const BEPlan& P, CrtLabels& cur, Array
     g.ndraws = static_cast<int>(dr.size());
     g.nblk = draw_blocks(dr);
     check_desc(g);
-    if (!dr.empty()) launch_draw(I.c, g);
+    if (!dr.empty()) hipLaunchKernelGGL(gg::draw_kernel(), dim3(draw_grid(g)), dim3(gg::kGB), 0, gg::tl_st, I.c, g);
     std::vector<int16_t*> L(E);
     for (int j = 0; j < E; ++j) L[j] = I.cur[j].as<int16_t>();
     std::vector<gg::LinJob> jobs;

@@ -94,31 +94,3 @@ def test_prg_label_matches_oracle(native, p):
             v //= p
         b += 1
     np.testing.assert_array_equal(native.prg_label(seed, stream, ctr, p), exp)
-
-
-@pytest.mark.parametrize("p", [2, 3, 7, 17, 32, 86, 173])
-def test_hardened_prg_label_matches_chacha_oracle(native, p):
-    """Hardened garblings draw labels from ChaCha12 (core.h Prg::label, chacha): label block c of `stream` is
-    word group c & 3 of hard_block(seed, stream, (TW_PRG = 14, 0), c >> 2) (the hardened pad function keyed by
-    the seed), digits as in the AES form. The oracle rebuilds it from the ChaCha block function."""
-    seed, stream = bytes(range(3, 19)), 0x1234_5678_9ABC
-    key = int.from_bytes(seed, "little")
-    n = native.nr_comps(p)
-    if p & (p - 1) == 0:
-        m = 128 // (p.bit_length() - 1)
-    else:
-        m = 0
-        while p ** (m + 1) <= 2 ** 64:
-            m += 1
-    for ctr in (0, 3, 41):  # a label's blocks inside one ChaCha block and across two
-        exp, b = [], 0
-        while len(exp) < n:
-            c = ctr + b
-            v = int(native.hard_pads(key, stream, 14 << 16, c >> 2)[c & 3])
-            for _ in range(min(m, n - len(exp))):
-                exp.append(v % p)
-                v //= p
-            b += 1
-        got = native.prg_label(seed, stream, ctr, p, hardened=True)
-        np.testing.assert_array_equal(got, exp)
-        assert not np.array_equal(got, native.prg_label(seed, stream, ctr, p))
