@@ -911,10 +911,12 @@ constexpr bool kHashPairs = DASH_GG_HASH_PAIRS != 0;
 // up to kHJ consecutive i of one projection): key = x + i R_pin, i.e. digits x_q + (i R_q mod p) with the
 // multiple row iR[pin][i] read from scalar memory; the key's color (digit 0, R_0 = 1) places the hash:
 // HC / CC[first + color][e] = H, i.
-template <int C>
-__global__ __launch_bounds__(kPB, 4) void k_hash_iu(Ctx c, Gadget g, In in, const HashJob* jobs, int njobs) {
-    __shared__ __attribute__((aligned(16))) uint32_t lds_aes[aes_lds_words<C>()];
-    aes_lds_fill<C>(lds_aes, c.te0);
+// HARD (hardened encoding): the keys themselves, no AES, so no LDS image either (it capped the kernel at two
+// 512-thread blocks per CU and cost a 64 KiB fill per block): k_hash_iu 2.15 -> 1.74 ms per 4 MiniONN GCs
+template <int C, bool HARD>
+__global__ __launch_bounds__(kPB, HARD ? 5 : 4) void k_hash_iu(Ctx c, Gadget g, In in, const HashJob* jobs, int njobs) {
+    __shared__ __attribute__((aligned(16))) uint32_t lds_aes[HARD ? 4 : aes_lds_words<C>()];
+    if (!HARD) aes_lds_fill<C>(lds_aes, c.te0);
     const AesT<C> aes = aes_ctx<C>(lds_aes, nullptr);
     const int64_t N = g.N;
     const int64_t tiles = (N + kTile - 1) / kTile;
@@ -943,7 +945,7 @@ __global__ __launch_bounds__(kPB, 4) void k_hash_iu(Ctx c, Gadget g, In in, cons
                 uint32_t col1, col2;
                 compress_xa2(x, rows + static_cast<int64_t>(i) * words, rows + static_cast<int64_t>(i + 1) * words, mi,
                              k1, k2, col1, col2);
-                if (c.hard) {  // hardened: the keys themselves (k_emit derives each entry's tweaked pad)
+                if (HARD) {  // hardened: the keys themselves (k_emit derives each entry's tweaked pad)
                     H1 = k1;
                     H2 = k2;
                 } else {
@@ -960,7 +962,7 @@ __global__ __launch_bounds__(kPB, 4) void k_hash_iu(Ctx c, Gadget g, In in, cons
         for (; i < c1; ++i) {
             uint32_t col;
             const u128 key = compress_xa(x, rows + static_cast<int64_t>(i) * words, mi, col);
-            const u128 H = c.hard ? key : aes_encrypt(aes, key);
+            const u128 H = HARD ? key : aes_encrypt(aes, key);
             if (e_raw < N) {
                 g.HC[(P.first + i) * N + e] = H;
                 g.CC[(P.first + i) * N + e] = static_cast<uint16_t>(static_cast<int>(col) - i);
@@ -1015,7 +1017,10 @@ inline int gg_aes_copies() {
 inline auto draw_kernel() { return gg_aes_copies() == 16 ? k_draw<16> : k_draw<32>; }
 inline auto hash_kernel() { return gg_aes_copies() == 16 ? k_hash<16> : k_hash<32>; }
 inline auto hash_jobs_kernel() { return gg_aes_copies() == 16 ? k_hash_jobs<16> : k_hash_jobs<32>; }
-inline auto hash_iu_kernel() { return gg_aes_copies() == 16 ? k_hash_iu<16> : k_hash_iu<32>; }
+inline auto hash_iu_kernel(bool hard) {
+    if (hard) return k_hash_iu<16, true>;
+    return gg_aes_copies() == 16 ? k_hash_iu<16, false> : k_hash_iu<32, false>;
+}
 // DASH_GG_KEYS (A/B knob): 2 (default) = uniform-i key hashes and bank payloads from the offsets' multiple rows
 // (compress_xa); 1 = multiple rows for the bank payloads only; 0 = the round-3 per-lane forms
 inline int gg_hash_mode() {
@@ -1216,6 +1221,14 @@ __global__ __launch_bounds__(kEB) void k_emit(Ctx c, Gadget g, In in, Tables tb,
         const uint32_t* gmap = em.map + em.map_off[table] + a;
         for (int x = threadIdx.x; x < span; x += kEB) MAP[x] = gmap[x];
         for (int x = threadIdx.x; x < nbx; x += kEB) BIX[x] = em.bix[bx0 + x];
+        // hardened: the scope's pad runs too, so a quad's descriptor chain (run -> position map -> projection ->
+        // entry row -> key) is LDS reads only
+        uint32_t* QDL = reinterpret_cast<uint32_t*>(BIX + ((nbx + 1) & ~1));
+        if (c.hard) {
+            const uint32_t* QD = em.quads + rfl(S.q0);
+            const int nq = rfl(S.nq);
+            for (int x = threadIdx.x; x < nq; x += kEB) QDL[x] = QD[x];
+        }
         __syncthreads();
         if (em.by_i) {
             // the colors of a projection's keys are a permutation of its entry indices: invert in LDS,
@@ -1231,9 +1244,10 @@ __global__ __launch_bounds__(kEB) void k_emit(Ctx c, Gadget g, In in, Tables tb,
         const int64_t row = tb.row[table];
         if (c.hard) {
             // 2 (hardened): one ChaCha block per quad (up to 4 entries of one key: a fan-out row's consecutive
-            // targets share a block), quad-fastest over the tile's elements
+            // targets share a block), quad-fastest over the tile's elements. (Rejected, profiles/ab/README.md:
+            // loading the next quad's descriptor chain before this quad's pad block, and a prefetch of the next
+            // tile's staging loads: k_emit unchanged.)
             const int nq = rfl(S.nq);
-            const uint32_t* QD = em.quads + rfl(S.q0);
             const int totq = nq * te;
             const float inv_nq = 1.0f / static_cast<float>(nq);
             for (int x = threadIdx.x; x < totq; x += kEB) {
@@ -1243,7 +1257,7 @@ __global__ __launch_bounds__(kEB) void k_emit(Ctx c, Gadget g, In in, Tables tb,
                 const int q = x - el * nq;
                 const int64_t e = e0 + el;
                 if (e >= N) continue;
-                const uint32_t qd = QD[q];
+                const uint32_t qd = QDL[q];
                 const int p0 = static_cast<int>(qd >> 3), cnt = static_cast<int>(qd & 7u);
                 const uint32_t m0 = MAP[p0];
                 const EProj P = sep[m0 >> 24];
@@ -2438,7 +2452,9 @@ void project(const gg::Ctx& c, gg::Gadget& g, const gg::In& in, const gg::Tables
         }
         S.nq = static_cast<int>(quads.size()) - S.q0;
         const size_t per = static_cast<size_t>(elem_bytes(S.ne, S.nb));
-        const size_t fixed = static_cast<size_t>(S.span) * 4 + static_cast<size_t>(S.nbx) * 2 + 16;
+        // position map, bank indices and (hardened) the pad runs staged in LDS
+        const size_t fixed = static_cast<size_t>(S.span) * 4 + static_cast<size_t>(S.nbx) * 2 + 16 +
+                             (c.hard ? static_cast<size_t>(S.nq) * 4 + 4 : 0);
         auto lds_of = [&](int sh) { return ((1u << sh) + 1) * per + fixed; };
         int tsh = 5;
         while (tsh > 0 && lds_of(tsh) > emit_lds_budget()) --tsh;
@@ -2505,7 +2521,7 @@ void project(const gg::Ctx& c, gg::Gadget& g, const gg::In& in, const gg::Tables
         for (int pi = 0; pi < np; ++pi)
             for (int c0 = 0; c0 < pr[pi].pin; c0 += gg::kHJ) hj.push_back(gg::HashJob{pi, c0});
         const gg::HashJob* dj = gg::dconst(hj.data(), hj.size());
-        hipLaunchKernelGGL(gg::hash_iu_kernel(), dim3(blocks_for(lanes * static_cast<int64_t>(hj.size()), gg::kPB, 16384)),
+        hipLaunchKernelGGL(gg::hash_iu_kernel(cc.hard != 0), dim3(blocks_for(lanes * static_cast<int64_t>(hj.size()), gg::kPB, 16384)),
                            dim3(gg::kPB), 0, gg::tl_st, cc, g, in, dj, static_cast<int>(hj.size()));
     } else if (gg::gg_hash_jobs()) {
         std::vector<gg::HashJob> hj;

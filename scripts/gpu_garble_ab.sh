@@ -21,10 +21,6 @@ for v in "$A" "$B"; do
     n=$(basename "$(realpath "$v")")
     DASH_PKG_ROOT=$(realpath "$v") timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/prof_$n" -o run -- \
         python3 scripts/garble_bench.py --gpu-only --reps 4 > "$OUT/prof_$n.log" 2>&1 || { tail -20 "$OUT/prof_$n.log"; exit 1; }
-    f=$(find "$OUT/prof_$n" -name '*kernel_stats.csv' | head -1)
-    python3 -c "
-import csv,sys
-rows=list(csv.DictReader(open(sys.argv[1])))
-for r in sorted(rows,key=lambda r:-float(r['TotalDurationNs']))[:8]:
-    print('%-40s %6s %10.3f ms' % (r['Name'][:40], r['Calls'], float(r['TotalDurationNs'])/1e6))" "$f"
+    db=$(find "$OUT/prof_$n" -name '*.db' | head -1)
+    python3 -m dash_amd.utils.profsum "$db" 8 || true
 done
