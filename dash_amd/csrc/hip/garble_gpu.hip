@@ -2218,9 +2218,17 @@ struct DevTable {
 };
 
 // k_draw grid: one lane per (draw, element), elements padded to whole waves
+// A/B knob DASH_GG_DRAW_BLOCKS: grid cap of k_draw (grid-stride; every block fills its 32 / 64 KiB LDS AES image)
+inline int draw_block_cap() {
+    static const int v = [] {
+        const char* e = std::getenv("DASH_GG_DRAW_BLOCKS");
+        return e ? std::max(1, std::atoi(e)) : 16384;
+    }();
+    return v;
+}
 unsigned draw_grid(const gg::Gadget& g) {
     const int64_t lanes = (g.N + gg::kTile - 1) / gg::kTile * gg::kTile * g.ndraws;
-    return blocks_for(lanes, gg::kGB, 16384);
+    return blocks_for(lanes, gg::kGB, draw_block_cap());
 }
 
 // AES-CTR blocks per element: draws are laid out back to back in counter order
