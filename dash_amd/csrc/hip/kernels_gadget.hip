@@ -865,7 +865,26 @@ __global__ __launch_bounds__(kOhBS, kAesMinBlocks) void k_rescale_mrs_out_hash_s
                 lds_stage_rows<kOhBS, 2>(stg, L, N, e0, q0, cnt);
                 __syncthreads();
             }
-            if (m.bits) {
+            if (m.bits && cnt * static_cast<int>(m.bits) <= 64) {
+                // power-of-two modulus, the pass's digits in one 64-bit window (residue 0 of the DASH bases: 128
+                // one-bit digits, 40 per pass): a shift-and per digit over a fully unrolled, compile-time loop
+                // instead of a 128-bit stream shift and scalar loop bookkeeping per digit (24-GC step -1.8 %,
+                // profiles/ab/README.md round 6)
+                const uint64_t win = static_cast<uint64_t>(s.Q);
+                const uint32_t b = m.bits, msk = m.q - 1;
+#pragma unroll
+                for (int c = 0; c < kOhCap; ++c) {
+                    if (c < cnt) {
+                        uint8_t& w = stg[c * kOhBS + tid];
+                        const uint32_t d = static_cast<uint32_t>(win >> (c * b)) & msk;
+                        const uint32_t v = j == 0 ? d : modq(static_cast<uint32_t>(w) * inv + d, m);
+                        w = static_cast<uint8_t>(v);
+                        if (j != 0) cf.push(v, m);
+                    }
+                }
+                s.Q >>= cnt * b;
+                if (q0 == 0) c0 = stg[tid];  // digit 0 of the output (this lane's own LDS byte)
+            } else if (m.bits) {
                 for (int c = 0; c < cnt; ++c) {
                     uint8_t& w = stg[c * kOhBS + tid];
                     const uint32_t v = j == 0 ? s.next(m) : modq(static_cast<uint32_t>(w) * inv + s.next(m), m);
