@@ -441,9 +441,6 @@ class _Bench:
 
         def step(i: int, check: bool = False):
             xs = inputs[i * B:(i + 1) * B]
-            # the garbler's exact range guard of the step's inputs (mixed-radix wrap band, CRT overflow): one
-            # batched check on its own stream, overlapping the evaluations; no result is released before it passes
-            pend = guard.submit(xs) if guard is not None else None
             # online message #1 (device encoder, or wire form: 16-B compressed labels -> pinned staging -> H2D ->
             # GPU unpack); the G groups run concurrently on their own streams
             for g, grp in enumerate(groups):
@@ -451,6 +448,10 @@ class _Bench:
                 grp.encode_batch(gcs[g * per:(g + 1) * per], xs[g * per:(g + 1) * per])
                 host[0] += time.perf_counter() - t
                 grp.launch()
+            # the garbler's exact range guard of the step's inputs (mixed-radix wrap band, CRT overflow): one
+            # batched check on its own stream, submitted after the evaluations (its host-side submit is then off
+            # their critical path) and overlapping them; no result is released before it passes
+            pend = guard.submit(xs) if guard is not None else None
             dec = []
             for g, grp in enumerate(groups):
                 grp.fetch()
@@ -588,11 +589,11 @@ class _Bench:
             x = xs[max(0, i - 1)]
             self.sync()
             t = time.perf_counter()
-            # the garbler's range guard on its own stream, queued first and overlapping the evaluation (the cpu
-            # backend guards inside garble_inputs)
-            pend = gc.guard.submit([x]) if (self.hip and gc.guard_enabled) else None
             grp.encode_batch([gc], [x])
             grp.launch()
+            # the garbler's range guard on its own stream, overlapping the evaluation (the cpu backend guards
+            # inside garble_inputs)
+            pend = gc.guard.submit([x]) if (self.hip and gc.guard_enabled) else None
             grp.fetch()
             y = grp.decode(0, gc)
             if pend is not None:
