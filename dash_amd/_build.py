@@ -2,9 +2,10 @@
 
 Compiles the host C++ core (amdclang++) and the HIP kernels for gfx950
 (hipcc --offload-arch=gfx950) into one in-tree extension module
-``dash_amd/_dash_native*.so``. No torch headers are involved, so a full
-rebuild takes well under a minute; incremental rebuilds only recompile
-changed translation units.
+``dash_amd/_dash_native*.so``. No torch headers are involved. A full rebuild
+takes 2.5-4.5 minutes with 8 jobs (the per-K chain units dominate,
+docs/BUILD.md); incremental rebuilds only recompile changed translation
+units.
 
 Usage:  python -m dash_amd._build [--clean] [--jobs N] [--debug]
 """
