@@ -148,6 +148,35 @@ inline u128 compress(const comp_t* L, const ModInfo& m) {
     return C;
 }
 
+// compress() of four labels of one modulus at once: four independent Horner chains interleaved, so the
+// dependent 64-bit multiply-adds of one label overlap those of the other three (the host input encoder's
+// online message #1, Garbler::encode_compressed)
+inline void compress4(const comp_t* const L[4], const ModInfo& m, u128 out[4]) {
+    const int n = m.n;
+    if (m.pow2) {
+        for (int q = 0; q < 4; ++q) out[q] = compress(L[q], m);
+        return;
+    }
+    const u64 p = static_cast<u64>(m.p);
+    int j = n - 1;
+    int first = n % m.chunk;
+    if (first == 0) first = m.chunk;
+    u128 C[4];
+    {
+        u64 v[4] = {0, 0, 0, 0};
+        for (int t = 0; t < first; ++t, --j)
+            for (int q = 0; q < 4; ++q) v[q] = v[q] * p + static_cast<u64>(static_cast<uint16_t>(L[q][j]));
+        for (int q = 0; q < 4; ++q) C[q] = v[q];
+    }
+    while (j >= 0) {
+        u64 v[4] = {0, 0, 0, 0};
+        for (int t = 0; t < m.chunk; ++t, --j)
+            for (int q = 0; q < 4; ++q) v[q] = v[q] * p + static_cast<u64>(static_cast<uint16_t>(L[q][j]));
+        for (int q = 0; q < 4; ++q) C[q] = C[q] * static_cast<u128>(m.pchunk) + v[q];
+    }
+    for (int q = 0; q < 4; ++q) out[q] = C[q];
+}
+
 // Inverse of compress for a valid C (< p^n). For arbitrary C the first n-1
 // digits are the base-p digits and the top digit is reduced mod p.
 inline void decompress(u128 C, comp_t* L, const ModInfo& m) {

@@ -302,20 +302,31 @@ void Garbler::encode_compressed(const i64* x, i64 N, u128* dst, int nthreads) co
         for (int v = 0; v < p; ++v)
             for (int c = 0; c < n; ++c) lut[j][static_cast<size_t>(v) * n + c] = static_cast<int16_t>((v * R[c]) % p);
     }
+    // four labels of one residue per step (compress4: their Horner chains interleave; a fresh GC's first encode
+    // is the batch-1 latency path of the wire form)
     parallel_for(static_cast<i64>(k) * N, [&](i64 r0, i64 r1) {
-        comp_t buf[128];
-        for (i64 r = r0; r < r1; ++r) {
+        comp_t buf[4][128];
+        for (i64 r = r0; r < r1;) {
             const int j = static_cast<int>(r / N);
             const i64 e = r % N;
+            const i64 cnt = std::min<i64>(4, std::min<i64>(r1 - r, N - e));
             const int p = crt_[j];
             const ModInfo& mi = mod_info(p);
-            const comp_t* W0 = in_base_[j].at(e);
-            const int16_t* L = lut[j].data() + static_cast<size_t>(pmod(x[e], p)) * mi.n;
-            for (int c = 0; c < mi.n; ++c) {
-                const int v = W0[c] + L[c];
-                buf[c] = static_cast<comp_t>(v >= p ? v - p : v);
+            for (i64 q = 0; q < cnt; ++q) {
+                const comp_t* W0 = in_base_[j].at(e + q);
+                const int16_t* L = lut[j].data() + static_cast<size_t>(pmod(x[e + q], p)) * mi.n;
+                for (int c = 0; c < mi.n; ++c) {
+                    const int v = W0[c] + L[c];
+                    buf[q][c] = static_cast<comp_t>(v >= p ? v - p : v);
+                }
             }
-            dst[r] = compress(buf, mi);
+            if (cnt == 4) {
+                const comp_t* B[4] = {buf[0], buf[1], buf[2], buf[3]};
+                compress4(B, mi, dst + r);
+            } else {
+                for (i64 q = 0; q < cnt; ++q) dst[r + q] = compress(buf[q], mi);
+            }
+            r += cnt;
         }
     }, nthreads);
 }
