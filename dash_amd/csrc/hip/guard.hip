@@ -414,9 +414,13 @@ class DevRangeGuard {
             HIPCHECK(hipMalloc(reinterpret_cast<void**>(&p), sizeof(int64_t) * e * chunk_));
             bufs_.push_back(p);
         }
+        // stream priority (A/B knob DASH_GUARD_PRIO = 0 low, 1 normal, 2 high): high by default, so the check
+        // never waits behind the evaluation it overlaps
         int lo_pri = 0, hi_pri = 0;
         HIPCHECK(hipDeviceGetStreamPriorityRange(&lo_pri, &hi_pri));
-        HIPCHECK(hipStreamCreateWithPriority(&st_, hipStreamNonBlocking, hi_pri));
+        const int pk = knob("DASH_GUARD_PRIO", 2);
+        const int pri = pk >= 2 ? hi_pri : (pk == 1 ? (lo_pri + hi_pri) / 2 : lo_pri);
+        HIPCHECK(hipStreamCreateWithPriority(&st_, hipStreamNonBlocking, pri));
     }
     ~DevRangeGuard() {
         (void)hipSetDevice(dev_);
