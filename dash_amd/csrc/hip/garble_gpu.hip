@@ -1023,6 +1023,18 @@ inline auto hash_iu_kernel(bool hard) {
 }
 // DASH_GG_KEYS (A/B knob): 2 (default) = uniform-i key hashes and bank payloads from the offsets' multiple rows
 // (compress_xa); 1 = multiple rows for the bank payloads only; 0 = the round-3 per-lane forms
+// DASH_GG_FUSED (A/B knob): 1 = hardened k_emit computes its own keys and bank payloads (no HC / CC / BK round
+// trip); 0 (default) = staged from k_hash_iu / k_bank. Measured and rejected (profiles/ab/README.md, round 6):
+// byte-identical, but k_emit went 5.58 -> 9.22 ms per 4 MiniONN GCs while the k_hash_iu / k_bank time it removed
+// was 2.76 ms (garbler kernels 18.5 -> 19.4 ms): the block's compress phase serialises with its pad and store
+// phases, and a wave spans two key rows of possibly different moduli (te <= 32)
+inline bool gg_emit_fused() {
+    static const bool v = [] {
+        const char* e = std::getenv("DASH_GG_FUSED");
+        return e && std::atoi(e) == 1;
+    }();
+    return v;
+}
 inline int gg_hash_mode() {
     static const int v = [] {
         const char* e = std::getenv("DASH_GG_KEYS");
@@ -1065,8 +1077,13 @@ struct EProj {
     int first;  // first key-hash entry (HC / CC row)
     int pay1;   // element-independent f: bix base (bank row of (i, d) at bix[pay1 + i * t + d]);
                 // F_MULR / F_NEGR: scope-relative bank row of v = 0 (rows v = 0 .. pout - 1)
-    int fn, t, res, pout;
+    int16_t fn, t, res;
+    uint16_t pout;
+    int in_idx;  // the projection's input label (fused key hashes: Emit::fused)
+    int16_t in_kind;
+    uint16_t pin;
 };
+static_assert(sizeof(EProj) == 32, "EProj: 32 B (224 of them are staged in k_emit's LDS)");
 struct Scope {
     int table, tsh;  // table id; te = 1 << tsh elements per block
     int a, span;     // table positions [a, a + span)
@@ -1078,6 +1095,9 @@ struct Scope {
 };
 struct Emit {
     int by_i;  // key hashes stored by entry index i with CC = color - i (k_hash_iu); else by color with CC = i
+    // fused (hardened, every bank row an R-offset row): the block computes its tile's keys and bank payloads
+    // itself (compress_xa over the offsets' multiple rows) instead of loading k_hash_iu's / k_bank's output
+    int fused;
     const Scope* sc;
     int nsc, nep;
     int64_t blocks;
@@ -1189,7 +1209,42 @@ __global__ __launch_bounds__(kEB) void k_emit(Ctx c, Gadget g, In in, Tables tb,
         constexpr int kUn = 4;
         const int b0 = rfl(S.b0);
         const int nh = ne << tsh, nall = (ne + nb) << tsh;
-        for (int x0 = threadIdx.x; x0 < nall; x0 += kUn * kEB) {
+        if (em.fused) {
+            // 1 (fused): item (row, element). A key row r0 + rr is entry index i of the projection holding it: its key
+            // x + i R_pin lands at the row of its color (CCL = i, as k_hash does); a bank row is slot label + v R_pout.
+            // The lanes of a wave are consecutive elements of one or two rows (uniform moduli in the common case).
+            for (int x = threadIdx.x; x < nall; x += kEB) {
+                const int rr = x >> tsh, el = x & (te - 1);
+                const int64_t e = min(e0 + el, N - 1);
+                if (x < nh) {
+                    const int r = r0 + rr;
+                    int lo = 0, hi = em.nep - 1;
+                    while (lo < hi) {  // the projection holding key row r (projections are in `first` order)
+                        const int mid = (lo + hi + 1) >> 1;
+                        if (sep[mid].first <= r) lo = mid;
+                        else hi = mid - 1;
+                    }
+                    const EProj& P = sep[lo];
+                    const int i = r - P.first;
+                    const ModC mi = c.mc[P.pin];
+                    const int words = 4 * static_cast<int>(chunks_of(static_cast<int>(mi.n)));
+                    uint32_t col;
+                    const u128 key = compress_xa(label_ref(c, g, in, e, P.in_kind, P.in_idx, P.pin),
+                                                 c.iR[P.pin] + static_cast<int64_t>(i) * words, mi, col);
+                    const int rc = P.first - r0 + static_cast<int>(col);
+                    HCL[rc * te1 + el] = key;
+                    CCL[rc * te1 + el] = static_cast<uint16_t>(i);
+                } else {
+                    const BankRow B = em.rows[b0 + rr - ne];
+                    const ModC mo = c.mc[B.pout];
+                    const int words = 4 * static_cast<int>(chunks_of(static_cast<int>(mo.n)));
+                    uint32_t d0;
+                    PBL[(rr - ne) * te1 + el] =
+                        compress_xa(slot_ref(g, B.slot, e), c.iR[B.pout] + static_cast<int64_t>(B.v) * words, mo, d0);
+                }
+            }
+        }
+        for (int x0 = threadIdx.x; !em.fused && x0 < nall; x0 += kUn * kEB) {
             u128 hv[kUn];
             uint16_t cv[kUn];
 #pragma unroll
@@ -2344,9 +2399,15 @@ void project(const gg::Ctx& c, gg::Gadget& g, const gg::In& in, const gg::Tables
     std::sort(order.begin(), order.end(), [&](int x, int y) {
         return std::tie(pr[x].table, pr[x].off) < std::tie(pr[y].table, pr[y].off);
     });
-    const bool by_i = gg::gg_hash_mode() == 2 && !std::any_of(pr.begin(), pr.end(), [](const gg::Proj& p) {
+    const bool by_i0 = gg::gg_hash_mode() == 2 && !std::any_of(pr.begin(), pr.end(), [](const gg::Proj& p) {
         return p.pin >= 32768;
     });
+    // fused (hardened, no element-dependent payload offsets): k_emit computes its tile's keys and bank payloads,
+    // no k_hash_iu / k_bank launches and no HC / CC / BK round trip through HBM
+    const bool fused = by_i0 && c.hard && gg::gg_emit_fused() && std::none_of(pr.begin(), pr.end(), [](const gg::Proj& p) {
+        return p.outr_kind == gg::R_INPUT;
+    });
+    const bool by_i = by_i0 && !fused;
     auto elem_bytes = [&](int64_t ne, int64_t nb) { return ne * (16 + 2 + (by_i ? 2 : 0)) + nb * 16; };
     auto rows_bound = [&](const gg::Proj& p) {  // bank rows upper bound
         int64_t n = 0;
@@ -2413,10 +2474,14 @@ void project(const gg::Ctx& c, gg::Gadget& g, const gg::In& in, const gg::Tables
             E.first = static_cast<int>(p.first);
             E.hsub = p.hsub;
             E.hslot = p.hslot;
-            E.fn = p.fn;
-            E.t = targets(p);
-            E.res = elem_dep(p) ? p.a0 : -1;
-            E.pout = p.pout;
+            DASH_CHECK(p.pout > 0 && p.pout < 65536 && p.a0 < 32768, "gpu garbler: projection outside the emit descriptor");
+            E.fn = static_cast<int16_t>(p.fn);
+            E.t = static_cast<int16_t>(targets(p));
+            E.res = static_cast<int16_t>(elem_dep(p) ? p.a0 : -1);
+            E.pout = static_cast<uint16_t>(p.pout);
+            E.in_kind = static_cast<int16_t>(p.in_kind);
+            E.in_idx = p.in_idx;
+            E.pin = static_cast<uint16_t>(p.pin);
             const int res = p.outr_kind == gg::R_INPUT ? p.outr_idx : -1;
             if (elem_dep(p)) {
                 E.pay1 = static_cast<int>(rows.size()) - S.b0;
@@ -2483,16 +2548,19 @@ void project(const gg::Ctx& c, gg::Gadget& g, const gg::In& in, const gg::Tables
     em.nep = np;
     em.sc = gg::dconst(sc.data(), sc.size());
     em.nsc = static_cast<int>(sc.size());
-    auto hc = hc_scratch(static_cast<size_t>(g.entries), g.N);
-    g.HC = hc.first;
-    g.CC = hc.second;
-    g.BK = bank_scratch(rows.size(), g.N);
+    if (!fused) {
+        auto hc = hc_scratch(static_cast<size_t>(g.entries), g.N);
+        g.HC = hc.first;
+        g.CC = hc.second;
+        g.BK = bank_scratch(rows.size(), g.N);
+    }
     check_desc(g);
     const int64_t lanes = (g.N + gg::kTile - 1) / gg::kTile * gg::kTile;
     // multiple rows of the projections' input moduli (uniform-i key hashes) and of the bank rows' R offsets
     gg::Ctx cc = c;
     const bool iu = by_i;  // k_hash_iu writes the by-index layout k_emit then inverts
     em.by_i = by_i ? 1 : 0;
+    em.fused = fused ? 1 : 0;
     {
         std::vector<int> mods;
         for (const auto& p : pr) mods.push_back(p.pin);
@@ -2504,7 +2572,8 @@ void project(const gg::Ctx& c, gg::Gadget& g, const gg::In& in, const gg::Tables
     }
     // (rejected, profiles/ab/README.md: one block per label group with the label staged in LDS, 7.2 -> 7.6-8.2 ms
     // per 4 GCs, and one wave per group stepping packed-byte payloads o + v*off incrementally, 10.7 ms)
-    if (!rows.empty()) {
+    if (fused) DASH_CHECK(cc.iR != nullptr, "gpu garbler: fused emit without the offsets' multiple rows");
+    if (!rows.empty() && !fused) {
         // bank jobs: neighbouring rows of one slot label with R offsets pair up (one label read, two payloads)
         std::vector<gg::BankJob> bj;
         const bool pairs = gg::gg_hash_mode() == 2;
@@ -2524,7 +2593,8 @@ void project(const gg::Ctx& c, gg::Gadget& g, const gg::In& in, const gg::Tables
         hipLaunchKernelGGL(gg::k_bank, dim3(blocks_for(lanes * static_cast<int64_t>(bj.size()), 256, 32768)), dim3(256), 0,
                            gg::tl_st, cc, g, in, em.rows, dbj, static_cast<int>(bj.size()));
     }
-    if (iu) {
+    if (fused) {
+    } else if (iu) {
         std::vector<gg::HashJob> hj;
         for (int pi = 0; pi < np; ++pi)
             for (int c0 = 0; c0 < pr[pi].pin; c0 += gg::kHJ) hj.push_back(gg::HashJob{pi, c0});
@@ -2543,7 +2613,7 @@ void project(const gg::Ctx& c, gg::Gadget& g, const gg::In& in, const gg::Tables
                            gg::tl_st, c, g, in);
     }
     hipLaunchKernelGGL(gg::k_emit, dim3(static_cast<unsigned>(std::min<int64_t>(em.blocks, 65536))), dim3(gg::kEB),
-                       lds_max, gg::tl_st, c, g, in, tb, em);
+                       lds_max, gg::tl_st, fused ? cc : c, g, in, tb, em);
 }
 
 void run_sign(const gg::Ctx& c, const gg::SignLayout& L, gg::Gadget& g, const gg::In& in, const gg::Tables& tb,
