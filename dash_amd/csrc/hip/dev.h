@@ -476,6 +476,46 @@ __device__ __forceinline__ void hard_block(u128 K, uint64_t gate, uint32_t sub, 
     out[2] = pk(x8, x9, x10, x11);
     out[3] = pk(x12, x13, x14, x15);
 }
+// Quad-cooperative block (the four lanes of a quad, all active, the same K / gate / sub / blk in each): lane
+// j = lane & 3 holds state column j (words j, 4 + j, 8 + j, 12 + j). Column rounds are lane-local; a diagonal
+// round rotates rows 1-3 by 1-3 lanes (DPP quad_perm), runs the same quarter round and rotates back. On return
+// x[q] = word j of pad q. A quarter of hard_block's VALU work per lane plus six lane moves per double round: a
+// latency-bound chain whose lanes each ran a whole block per row (batch 1) waits a quarter as long.
+template <int CTRL>
+__device__ __forceinline__ uint32_t qperm(uint32_t v) {
+    return static_cast<uint32_t>(__builtin_amdgcn_mov_dpp(static_cast<int>(v), CTRL, 0xF, 0xF, false));
+}
+constexpr int kQRot1 = 0x39, kQRot2 = 0x4E, kQRot3 = 0x93;  // quad_perm: lane i reads lane (i + 1, 2, 3) & 3
+__device__ __forceinline__ void hard_block_q(u128 K, uint64_t gate, uint32_t sub, uint32_t blk, int j, uint32_t (&x)[4]) {
+    const uint32_t sig = j == 0 ? 0x61707865u : (j == 1 ? 0x3320646eu : (j == 2 ? 0x79622d32u : 0x6b206574u));
+    const uint32_t kj = j == 0 ? static_cast<uint32_t>(K)
+                               : (j == 1 ? static_cast<uint32_t>(K >> 32)
+                                         : (j == 2 ? static_cast<uint32_t>(K >> 64) : static_cast<uint32_t>(K >> 96)));
+    const uint32_t cj = j == 0 ? static_cast<uint32_t>(gate)
+                               : (j == 1 ? static_cast<uint32_t>(gate >> 32) : (j == 2 ? sub : 0x44524148u));
+    const uint32_t dj = j == 0 ? blk : 0u;
+    uint32_t a = sig, b = kj, c = cj, d = dj;
+#pragma unroll 1
+    for (int r = 0; r < kDevChaRounds; r += 2) {
+        DASH_QR(a, b, c, d)
+        b = qperm<kQRot1>(b);
+        c = qperm<kQRot2>(c);
+        d = qperm<kQRot3>(d);
+        DASH_QR(a, b, c, d)
+        b = qperm<kQRot3>(b);
+        c = qperm<kQRot2>(c);
+        d = qperm<kQRot1>(d);
+    }
+    x[0] = a + sig;
+    x[1] = b + kj;
+    x[2] = c + cj;
+    x[3] = d + dj;
+}
+// the 128-bit value whose word j sits in quad lane j, in every lane of the quad
+__device__ __forceinline__ u128 quad_gather128(uint32_t w) {
+    const uint32_t w0 = qperm<0x00>(w), w1 = qperm<0x55>(w), w2 = qperm<0xAA>(w), w3 = qperm<0xFF>(w);
+    return (static_cast<u128>((static_cast<uint64_t>(w3) << 32) | w2) << 64) | ((static_cast<uint64_t>(w1) << 32) | w0);
+}
 #undef DASH_QR
 
 // Tweak kinds (core.h TweakKind) and the sub word of row `idx`

@@ -575,6 +575,10 @@ __global__ __launch_bounds__(kMrsWBS, 1) void k_mrs_chain_w(MrsArgs a, Act x, co
 //    lane g) and broadcast back with DPP, so the pair payloads stay replicated in every lane's registers;
 //  * the final row likewise: lane g unmasks and stores outputs 4g..4g+3.
 // Four times the lanes of the wave form, and per lane about a quarter of the decompression work.
+#ifndef DASH_MRS_QCOOP
+#define DASH_MRS_QCOOP 1  // A/B knob: quad-cooperative pad blocks (dev.h hard_block_q); 0 = block g on lane g
+#endif
+constexpr bool kQCoop = DASH_MRS_QCOOP != 0;
 constexpr int kMrsQE = 64;            // elements per block
 constexpr int kMrsQBS = 4 * kMrsQE;   // threads per block (quads of consecutive lanes)
 template <int S>
@@ -675,12 +679,17 @@ __device__ __forceinline__ void chain_q_pos(const MrsArgs& a, uint64_t gate, con
         constexpr int nt = K - 1 - I + kExtra;
         uint32_t col = 0;
         u128 key;
-        u128 Eo[4] = {0, 0, 0, 0};  // this lane's entries 4g .. 4g + 3 of the row
+        // kQCoop: every lane loads the whole row (the quad's loads share their lines); else this lane's entries
+        // 4g .. 4g + 3
+        constexpr int kNE = kQCoop ? nt : 4;
+        u128 Eo[kNE];
+#pragma unroll
+        for (int t = 0; t < kNE; ++t) Eo[t] = 0;
         auto fetch_row = [&](uint32_t c) {  // issued as soon as the row index (the key's first digit) is known
             const u128* rowp = row0 + a.dig_off[I] + static_cast<int64_t>(c) * nt;
 #pragma unroll
-            for (int q = 0; q < 4; ++q)
-                if (4 * g + q < nt) Eo[q] = rowp[4 * g + q];
+            for (int q = 0; q < kNE; ++q)
+                if (kQCoop || 4 * g + q < nt) Eo[q] = rowp[kQCoop ? q : 4 * g + q];
         };
         bool split = false;  // positions I < (qpack >> 1): chunk-split (DASH_MRS_QSPLIT=-1: the stream-split walk)
         if constexpr (I <= kQSplit) split = I < (a.qpack >> 1);
@@ -801,18 +810,28 @@ __device__ __forceinline__ void chain_q_pos(const MrsArgs& a, uint64_t gate, con
             }
             key = C;
         }
-        if (4 * g < nt) {  // lane g's pad block (entries 4g .. 4g + 3)
-            u128 pd[4];
-            hard_block(key, gate, mrs_row_sub<MODE>(I), static_cast<uint32_t>(g), pd);
-#pragma unroll
-            for (int qq = 0; qq < 4; ++qq)
-                if (4 * g + qq < nt) Eo[qq] -= pd[qq];
-        }
         // every lane takes every entry: pair payloads for the later positions, the T target for acc
         u128 E[nt];
+        if constexpr (kQCoop) {
+            // the quad runs the row's pad blocks together and gathers each pad into every lane
 #pragma unroll
-        for (int t = 0; t < nt; ++t) {
-            if constexpr (true) {
+            for (int bk = 0; bk < (nt + 3) / 4; ++bk) {
+                uint32_t w[4];
+                hard_block_q(key, gate, mrs_row_sub<MODE>(I), static_cast<uint32_t>(bk), g, w);
+#pragma unroll
+                for (int qq = 0; qq < 4; ++qq)
+                    if (4 * bk + qq < nt) E[4 * bk + qq] = Eo[4 * bk + qq] - quad_gather128(w[qq]);
+            }
+        } else {
+            if (4 * g < nt) {  // lane g's pad block (entries 4g .. 4g + 3)
+                u128 pd[4];
+                hard_block(key, gate, mrs_row_sub<MODE>(I), static_cast<uint32_t>(g), pd);
+#pragma unroll
+                for (int qq = 0; qq < 4; ++qq)
+                    if (4 * g + qq < nt) Eo[qq] -= pd[qq];
+            }
+#pragma unroll
+            for (int t = 0; t < nt; ++t) {
                 const u128 own = Eo[t % 4];
                 E[t] = (t >> 2) == 0 ? quad_bcast128<0>(own) : (t >> 2) == 1 ? quad_bcast128<1>(own)
                        : (t >> 2) == 2 ? quad_bcast128<2>(own) : quad_bcast128<3>(own);
@@ -913,8 +932,29 @@ __global__ __launch_bounds__(kMrsQBS, 2) void k_mrs_chain_q(MrsArgs a, Act x, co
             for (int l = 0; l < K - 1; ++l) key ^= PS[mrs_pair<K>(l, K - 1)];
             const uint32_t cb = static_cast<uint32_t>(key) & 1u;
             u128 E = 0;
-            if (MODE == 2) E = row0[a.dig_off[K - 1] + cb] - hard_pad(key, gate, mrs_row_sub<MODE>(K - 1), 0);
-            if (valid) {
+            if (MODE == 2) {
+                if constexpr (kQCoop) {
+                    uint32_t w[4];
+                    hard_block_q(key, gate, mrs_row_sub<MODE>(K - 1), 0u, g, w);
+                    E = row0[a.dig_off[K - 1] + cb] - quad_gather128(w[0]);
+                } else {
+                    E = row0[a.dig_off[K - 1] + cb] - hard_pad(key, gate, mrs_row_sub<MODE>(K - 1), 0);
+                }
+            }
+            if (kQCoop && valid) {
+                // the next ReLU's y-row pads: the quad runs each block, lane j stores word j of its pads
+                const uint64_t gy = a.rgate0 ^ static_cast<uint64_t>(e);
+                for (int bk = 0; 4 * bk < a.ny; ++bk) {
+                    uint32_t w[4];
+                    hard_block_q(key, gy, tw_sub(kTwMmy, 0), static_cast<uint32_t>(bk), g, w);
+#pragma unroll
+                    for (int qq = 0; qq < 4; ++qq)
+                        if (4 * bk + qq < a.ny)
+                            reinterpret_cast<uint32_t*>(a.ys + (static_cast<int64_t>(b) * a.ny + 4 * bk + qq) * N + e)[g] = w[qq];
+                }
+                if (g == 0) a.cs[static_cast<int64_t>(b) * N + e] = static_cast<uint8_t>(cb);
+            }
+            if (!kQCoop && valid) {
                 // the next ReLU's y-row pads: block g on lane g
                 const uint64_t gy = a.rgate0 ^ static_cast<uint64_t>(e);
                 if (4 * g < a.ny) {
@@ -931,7 +971,23 @@ __global__ __launch_bounds__(kMrsQBS, 2) void k_mrs_chain_q(MrsArgs a, Act x, co
         if (MODE == 1) continue;
         const uint32_t colf = static_cast<uint32_t>(acc) & static_cast<uint32_t>(a.T - 1);
         const u128* row = row0 + a.fin_off + static_cast<int64_t>(colf) * K;
-        if (4 * g < K) {  // outputs 4g .. 4g + 3 under pad block g
+        if constexpr (kQCoop) {
+            // output 4 bk + g on lane g under pad g of block bk (the quad runs the block, gathers every pad)
+#pragma unroll
+            for (int bk = 0; bk < (K + 3) / 4; ++bk) {
+                const bool mine = 4 * bk + g < K;
+                const u128 F = mine ? row[4 * bk + g] : u128(0);
+                uint32_t w[4];
+                hard_block_q(acc, gate, mrs_row_sub<0>(K), static_cast<uint32_t>(bk), g, w);
+                u128 pd = 0;
+#pragma unroll
+                for (int qq = 0; qq < 4; ++qq) {
+                    const u128 p = quad_gather128(w[qq]);
+                    pd = qq == g ? p : pd;
+                }
+                if (valid && mine) a.pf[(static_cast<int64_t>(b) * K + 4 * bk + g) * N + e] = F - pd;
+            }
+        } else if (4 * g < K) {  // outputs 4g .. 4g + 3 under pad block g
             u128 F[4], pd[4];
 #pragma unroll
             for (int qq = 0; qq < 4; ++qq) F[qq] = 4 * g + qq < K ? row[4 * g + qq] : u128(0);
