@@ -481,6 +481,10 @@ __device__ __forceinline__ void hard_block(u128 K, uint64_t gate, uint32_t sub, 
 // round rotates rows 1-3 by 1-3 lanes (DPP quad_perm), runs the same quarter round and rotates back. On return
 // x[q] = word j of pad q. A quarter of hard_block's VALU work per lane plus six lane moves per double round: a
 // latency-bound chain whose lanes each ran a whole block per row (batch 1) waits a quarter as long.
+#ifndef DASH_MRS_QCOOP
+#define DASH_MRS_QCOOP 1  // A/B knob: quad-cooperative pad blocks in the quad kernels; 0 = block g on lane g
+#endif
+constexpr bool kQCoop = DASH_MRS_QCOOP != 0;
 template <int CTRL>
 __device__ __forceinline__ uint32_t qperm(uint32_t v) {
     return static_cast<uint32_t>(__builtin_amdgcn_mov_dpp(static_cast<int>(v), CTRL, 0xF, 0xF, false));
@@ -572,12 +576,26 @@ __device__ __forceinline__ void aes_lds_fill(uint32_t* lds, const uint32_t* te0)
     // 16-B LDS stores: the 4 words of an aligned quad share the table entry
     // and the rotation, so every block's image costs a quarter of the loads
     // and LDS writes of a word-wise fill
+    // kU table loads in flight per thread before their stores: a small block (batch-1 launches shrink to one
+    // wave) walks the image in total / nt rounds, and one load round trip per round made the fill a floor of
+    // every small AES launch
+    constexpr int kU = 8;
+    constexpr int total = aes_lds_words<C>() / 4;
     const int nt = blockDim.x * blockDim.y;
-    for (int i4 = threadIdx.x + threadIdx.y * blockDim.x; i4 < aes_lds_words<C>() / 4; i4 += nt) {
-        const int i = 4 * i4;
-        const uint32_t v = te0[i / (2 * C)];
-        const uint32_t w = (i % (2 * C) >= C) ? ror32(v, 16) : v;
-        reinterpret_cast<uint4*>(lds)[i4] = make_uint4(w, w, w, w);
+    for (int i0 = threadIdx.x + threadIdx.y * blockDim.x; i0 < total; i0 += kU * nt) {
+        uint32_t v[kU];
+#pragma unroll
+        for (int u = 0; u < kU; ++u) {
+            const int i4 = i0 + u * nt;
+            v[u] = i4 < total ? te0[(4 * i4) / (2 * C)] : 0u;
+        }
+#pragma unroll
+        for (int u = 0; u < kU; ++u) {
+            const int i4 = i0 + u * nt;
+            if (i4 >= total) break;
+            const uint32_t w = ((4 * i4) % (2 * C) >= C) ? ror32(v[u], 16) : v[u];
+            reinterpret_cast<uint4*>(lds)[i4] = make_uint4(w, w, w, w);
+        }
     }
     __syncthreads();
 }

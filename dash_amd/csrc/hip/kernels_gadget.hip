@@ -999,14 +999,7 @@ __global__ __launch_bounds__(kAesBlock, DASH_RRO_WAVES) void k_rescale_relu_out(
             }
             key = cf.finish();
         }
-        u128 G;
-        if constexpr (kQCoop) {  // the quad runs the pad block together (every lane holds the same key)
-            uint32_t w[4];
-            hard_block_q(key, a.rgate0 ^ static_cast<uint64_t>(e), tw_sub(kTwMmg, j), 0u, g, w);
-            G = Graw - quad_gather128(w[0]);
-        } else {
-            G = Graw - hard_pad(key, a.rgate0 ^ static_cast<uint64_t>(e), tw_sub(kTwMmg, j), 0);
-        }
+        const u128 G = Graw - hard_pad(key, a.rgate0 ^ static_cast<uint64_t>(e), tw_sub(kTwMmg, j), 0);
         const u128 E = Eraw - HS;
         const int16_t t16 = static_cast<int16_t>(static_cast<uint16_t>(mini >> (16 * cS)));
         const int16_t ypr16 = static_cast<int16_t>(t16 - static_cast<int16_t>(static_cast<uint16_t>(HM)));
@@ -1116,14 +1109,7 @@ __global__ __launch_bounds__(kRroBS) void k_rescale_relu_out_s(MrsArgs a, SignAr
         const u128 key = j == 0 ? P : cf.finish();
         __syncthreads();
         lds_store_rows<kRroBS>(L, stg, N, e0, 0, n);  // Y_j, the rescaled label
-        u128 G;
-        if constexpr (kQCoop) {  // the quad runs the pad block together (every lane holds the same key)
-            uint32_t w[4];
-            hard_block_q(key, a.rgate0 ^ static_cast<uint64_t>(e), tw_sub(kTwMmg, j), 0u, g, w);
-            G = Graw - quad_gather128(w[0]);
-        } else {
-            G = Graw - hard_pad(key, a.rgate0 ^ static_cast<uint64_t>(e), tw_sub(kTwMmg, j), 0);
-        }
+        const u128 G = Graw - hard_pad(key, a.rgate0 ^ static_cast<uint64_t>(e), tw_sub(kTwMmg, j), 0);
         const u128 E = Eraw - HS;
         const int16_t t16 = static_cast<int16_t>(static_cast<uint16_t>(mini >> (16 * cS)));
         const int16_t ypr16 = static_cast<int16_t>(t16 - static_cast<int16_t>(static_cast<uint16_t>(HM)));

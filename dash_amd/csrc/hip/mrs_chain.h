@@ -575,10 +575,6 @@ __global__ __launch_bounds__(kMrsWBS, 1) void k_mrs_chain_w(MrsArgs a, Act x, co
 //    lane g) and broadcast back with DPP, so the pair payloads stay replicated in every lane's registers;
 //  * the final row likewise: lane g unmasks and stores outputs 4g..4g+3.
 // Four times the lanes of the wave form, and per lane about a quarter of the decompression work.
-#ifndef DASH_MRS_QCOOP
-#define DASH_MRS_QCOOP 1  // A/B knob: quad-cooperative pad blocks (dev.h hard_block_q); 0 = block g on lane g
-#endif
-constexpr bool kQCoop = DASH_MRS_QCOOP != 0;
 constexpr int kMrsQE = 64;            // elements per block
 constexpr int kMrsQBS = 4 * kMrsQE;   // threads per block (quads of consecutive lanes)
 template <int S>
