@@ -18,3 +18,5 @@ import json; r = json.load(open('$OUT/lat_${n}_$i.json'))
 print('$n', r['latency_b1_ms'], r['latency_b1']['min_ms'], r.get('latency_b1_reference_ms'), r.get('latency_b1_host_encoded_ms'))"
     done
 done
+bash scripts/gpu_b1_ab.sh r06t_rro DASH_RRO_QUAD 1 2 2 || exit 1
+bash scripts/gpu_b1_ab.sh r06t_mq DASH_MRS_QUAD 1 0 1 || exit 1
