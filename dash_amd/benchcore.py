@@ -104,6 +104,9 @@ def parse_args(argv=None) -> argparse.Namespace:
     ap.add_argument("--profile", action="store_true", help="print per-layer GPU times")
     ap.add_argument("--threads", type=int, default=0, help="host threads per rank (0: cores / local ranks)")
     ap.add_argument("--verify", type=int, default=1)
+    ap.add_argument("--pipeline", type=int, default=int(os.environ.get("DASH_BENCH_PIPELINE", "1")),
+                    help="1: a group's next step is encoded and launched as soon as its outputs of the current step "
+                         "are fetched and decoded (the other groups keep the GPU busy meanwhile); 0: step by step")
     ap.add_argument("--garble-device", type=int, default=int(os.environ.get("DASH_BENCH_GARBLE_DEVICE", "1")),
                     help="garble on this rank's GPU (byte-identical to the host garbler)")
     ap.add_argument("--phases",
@@ -464,18 +467,59 @@ class _Bench:
                 self.verify(xs, dec)
             return dec
 
+        def launch_group(g, grp, i):
+            xs = inputs[i * B:(i + 1) * B]
+            t = time.perf_counter()
+            grp.encode_batch(gcs[g * per:(g + 1) * per], xs[g * per:(g + 1) * per])
+            host[0] += time.perf_counter() - t
+            grp.launch()
+
+        def steps_pipelined(first: int, n: int, check_first: bool = False):
+            """Steps first .. first + n - 1 with the groups pipelined across steps: group g's step i + 1 is
+            encoded and launched right after its step-i outputs are fetched and decoded, while the other groups
+            still run step i. Every step's range check still passes before its outputs are released."""
+            for g, grp in enumerate(groups):
+                launch_group(g, grp, first)
+            pend = guard.submit(inputs[first * B:(first + 1) * B]) if guard is not None else None
+            dec = None
+            for i in range(first, first + n):
+                more = i + 1 < first + n
+                dec = []
+                for g, grp in enumerate(groups):
+                    grp.fetch()
+                    t = time.perf_counter()
+                    dec += [grp.decode(b, gcs[g * per + b]) for b in range(per)]
+                    host[0] += time.perf_counter() - t
+                    if more:
+                        launch_group(g, grp, i + 1)
+                nxt = guard.submit(inputs[(i + 1) * B:(i + 2) * B]) if (guard is not None and more) else None
+                if pend is not None:
+                    pend.raise_if_bad()
+                if check_first and i == first:
+                    self.verify(inputs[i * B:(i + 1) * B], dec)
+                pend = nxt
+            return dec
+
+        pipelined = bool(getattr(self.args, "pipeline", 0))
         verified = False
-        for w in range(warmup):
-            step(w, check=bool(verify) and w == 0)
-            verified = verified or bool(verify)
+        if pipelined and warmup > 0:
+            steps_pipelined(0, warmup, check_first=bool(verify))
+            verified = bool(verify)
+        else:
+            for w in range(warmup):
+                step(w, check=bool(verify) and w == 0)
+                verified = verified or bool(verify)
         self.sync()
         barrier(ctx)
         self.sync()
         host[0] = 0.0
         t0 = time.perf_counter()
         last = None
-        for s in range(steps):
-            last = step(warmup + s)
+        if pipelined and steps > 0:
+            last = steps_pipelined(warmup, steps)
+        else:
+            for s in range(steps):
+                last = step(warmup + s)
         self.sync()
         barrier(ctx)
         self.sync()
@@ -809,6 +853,7 @@ def run(argv=None) -> Optional[dict]:
             # the headline's GCs are garbled once and re-encoded every step: an online-phase rate (a step's
             # work equals that of fresh GCs); served_inf_per_s is the protocol-valid fresh-GC rate
             "gc_reuse": True,
+            "pipelined_steps": bool(args.pipeline),
             "gc_reuse_note": ("the timed steps re-encode fresh inputs under GCs garbled once; "
                               + ("online message #1 comes from the garbler's device encoder (W0 + x R per label, "
                                  "the same work for a fresh GC; no codebook)" if bench.device_encode else

@@ -646,7 +646,9 @@ __global__ __launch_bounds__(kAesBlock, kAesMinBlocks) void k_rescale_hash_sign(
 // the mixed-radix chain keeps K-1 digit streams live: at 6 waves/SIMD (80 VGPRs) it spills 240 B per
 // lane; 4 waves/SIMD with 128 VGPRs measured faster (6.36 vs 7.04 ms per 24-GC MiniONN step)
 constexpr int kChunkUA = DASH_UA_CHUNK;
-template <int TM>
+// CH: components per dependent round trip. Latency-bound launches (batch 1, few waves per SIMD) take 16 (the
+// label's n / 4 round trips, 32 for the 128 components of p = 2, were the floor of a small launch)
+template <int TM, int CH>
 __global__ __launch_bounds__(kAesBlock, DASH_UA_MINBLOCKS) void k_rescale_update_approx(RescaleArgs r, SignArgs a, Act x, const int16_t* delta,
                                                                const u128* zh, const ModC* mc, const uint32_t* te0,
                                                                const uint32_t* rk) {
@@ -681,16 +683,16 @@ __global__ __launch_bounds__(kAesBlock, DASH_UA_MINBLOCKS) void k_rescale_update
         const int32_t inv = r.inv[j];
         col = 0;
         const int n = static_cast<int>(m.n);
-        for (int i0 = 0; i0 < n; i0 += kChunkUA) {
-            int16_t lv[kChunkUA], dv[kChunkUA];
+        for (int i0 = 0; i0 < n; i0 += CH) {
+            int16_t lv[CH], dv[CH];
 #pragma unroll
-            for (int u = 0; u < kChunkUA; ++u)
+            for (int u = 0; u < CH; ++u)
                 if (i0 + u < n) {
                     lv[u] = L[(i0 + u) * N];
                     dv[u] = Dl[i0 + u];
                 }
 #pragma unroll
-            for (int u = 0; u < kChunkUA; ++u)
+            for (int u = 0; u < CH; ++u)
                 if (i0 + u < n) {
                     // lv, dv, digit in [0, p): the sum is in [1, 3p), (sum * inv) mod p in one reduction
                     const uint32_t v = modq((static_cast<uint32_t>(lv[u]) + static_cast<uint32_t>(dv[u]) +
@@ -722,12 +724,25 @@ void launch_rescale_hash_sign(const u128* signP, const u128* du, int64_t N, int 
 }
 void launch_rescale_update_approx(const RescaleArgs& r, const SignArgs& a, const Act& x, const int16_t* delta,
                                   const u128* zh, int B, const ModC* mc, const AesGlobals& g, hipStream_t st) {
-    if (a.t <= 5)
-        hipLaunchKernelGGL(k_rescale_update_approx<5>, AES_LAUNCH(r.N, r.crt.k, B), kAesLds, st, r, a, x,
+    // DASH_UA_SMALL=0 keeps the throughput chunk on small launches (A/B)
+    static const bool small_on = [] {
+        const char* e = std::getenv("DASH_UA_SMALL");
+        return !(e && e[0] == '0');
+    }();
+    // at most two waves per SIMD: the lanes are serial chains of round trips
+    const bool small = small_on && r.N * r.crt.k * B <= static_cast<int64_t>(2 * 4 * 64) * num_cus();
+    if (a.t <= 5 && small)
+        hipLaunchKernelGGL((k_rescale_update_approx<5, 16>), AES_LAUNCH(r.N, r.crt.k, B), kAesLds, st, r, a, x,
+                           delta, zh, mc, g.te0, g.rk);
+    else if (a.t <= 5)
+        hipLaunchKernelGGL((k_rescale_update_approx<5, kChunkUA>), AES_LAUNCH(r.N, r.crt.k, B), kAesLds, st, r, a, x,
+                           delta, zh, mc, g.te0, g.rk);
+    else if (small)
+        hipLaunchKernelGGL((k_rescale_update_approx<8, 16>), AES_LAUNCH(r.N, r.crt.k, B), kAesLds, st, r, a, x,
                            delta, zh, mc, g.te0, g.rk);
     else
-        hipLaunchKernelGGL(k_rescale_update_approx<8>, AES_LAUNCH(r.N, r.crt.k, B), kAesLds, st, r, a, x,
-                           delta, zh, mc, g.te0, g.rk);
+        hipLaunchKernelGGL((k_rescale_update_approx<8, kChunkUA>), AES_LAUNCH(r.N, r.crt.k, B), kAesLds, st, r, a,
+                           x, delta, zh, mc, g.te0, g.rk);
 }
 
 
