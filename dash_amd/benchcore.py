@@ -467,12 +467,30 @@ class _Bench:
                 self.verify(xs, dec)
             return dec
 
+        # DASH_BENCH_ORDER=completion: the pipelined loop takes the groups in the order their steps finish
+        # (a HIP event per launch, polled) instead of in index order
+        by_completion = os.environ.get("DASH_BENCH_ORDER", "index") == "completion" and self.hip
+        done_ev = [None] * len(groups)
+
         def launch_group(g, grp, i):
             xs = inputs[i * B:(i + 1) * B]
             t = time.perf_counter()
             grp.encode_batch(gcs[g * per:(g + 1) * per], xs[g * per:(g + 1) * per])
             host[0] += time.perf_counter() - t
             grp.launch()
+            if by_completion:
+                import torch
+
+                done_ev[g] = torch.cuda.Event()
+                done_ev[g].record(grp.stream)
+
+        def group_order():
+            left = list(range(len(groups)))
+            while left:
+                g = next((x for x in left if done_ev[x] is None or done_ev[x].query()), left[0]) if by_completion \
+                    else left[0]
+                left.remove(g)
+                yield g
 
         def steps_pipelined(first: int, n: int, check_first: bool = False):
             """Steps first .. first + n - 1 with the groups pipelined across steps: group g's step i + 1 is
@@ -484,14 +502,16 @@ class _Bench:
             dec = None
             for i in range(first, first + n):
                 more = i + 1 < first + n
-                dec = []
-                for g, grp in enumerate(groups):
+                parts = [None] * len(groups)
+                for g in group_order():
+                    grp = groups[g]
                     grp.fetch()
                     t = time.perf_counter()
-                    dec += [grp.decode(b, gcs[g * per + b]) for b in range(per)]
+                    parts[g] = [grp.decode(b, gcs[g * per + b]) for b in range(per)]
                     host[0] += time.perf_counter() - t
                     if more:
                         launch_group(g, grp, i + 1)
+                dec = [y for part in parts for y in part]
                 nxt = guard.submit(inputs[(i + 1) * B:(i + 2) * B]) if (guard is not None and more) else None
                 if pend is not None:
                     pend.raise_if_bad()
