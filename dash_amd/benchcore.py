@@ -95,8 +95,12 @@ def parse_args(argv=None) -> argparse.Namespace:
     ap.add_argument("--sign", default=None, choices=["fused", "reference"], help="override the sign construction")
     ap.add_argument("--rescale", default=None, choices=["mrs", "legacy"], help="override the rescale construction")
     ap.add_argument("--relu", default=None, choices=["mrs", "approx", "joint"], help="override the ReLU sign")
-    ap.add_argument("--streams", type=int, default=int(os.environ.get("DASH_BENCH_STREAMS", "8")),
+    # 4 groups with the steps pipelined: 3082 / 3073 inf/s against 3007 / 3004 with 8 and 2799 / 2813 with 2
+    # (profiles/ab/r6/r06z_*.json); the reference constructions' 10 GB GCs prefer 2 larger groups
+    ap.add_argument("--streams", type=int, default=int(os.environ.get("DASH_BENCH_STREAMS", "4")),
                     help="independent GC groups per GPU, each on its own HIP stream")
+    ap.add_argument("--ref-streams", type=int, default=int(os.environ.get("DASH_BENCH_REF_STREAMS", "2")),
+                    help="GC groups of the reference-constructions phase")
     ap.add_argument("--model", default="MODEL_F_MINIONN_POOL_REPL")
     ap.add_argument("--config", default="DASH", choices=["DASH", "REDASH_OPT", "REDASH_CPM"])
     ap.add_argument("--backend", default="hip", choices=["hip", "cpu"])
@@ -327,12 +331,12 @@ class _Bench:
                               sink=sink if dev is not None else None)
 
     # ---- offline: garble B GCs into G groups of evaluator slots
-    def offline(self, tag: str, cons: dict, batch: int):
+    def offline(self, tag: str, cons: dict, batch: int, streams: int = 0):
         from .parallel import all_reduce_min
 
         args, ctx = self.args, self.ctx
         B = batch if batch > 0 else (256 if self.hip else 2)
-        G = max(1, min(args.streams, B))
+        G = max(1, min(streams or args.streams, B))
         B -= B % G
         per = B // G
         gcs: list = []
@@ -809,10 +813,10 @@ def run(argv=None) -> Optional[dict]:
     if "reference" in phases and args.constructions != "reference":
         rc = CONSTRUCTIONS["reference"]
         rsteps = args.ref_steps or args.steps
-        g2, grp2, B2, G2, per2, off2 = bench.offline("reference", rc, args.ref_batch)
+        g2, grp2, B2, G2, per2, off2 = bench.offline("reference", rc, args.ref_batch, args.ref_streams)
         r2 = bench.online(g2, grp2, B2, per2, rsteps, max(1, min(args.warmup, 2)), 3000, args.verify)
         ref = dict(value=round(world * B2 * rsteps / r2["elapsed"], 3),
-                   ms_per_step=round(1000.0 * r2["elapsed"] / rsteps, 3), gcs_per_gpu=B2, steps=rsteps,
+                   ms_per_step=round(1000.0 * r2["elapsed"] / rsteps, 3), gcs_per_gpu=B2, streams=G2, steps=rsteps,
                    constructions=g2[0].effective_constructions(), verified_vs_plaintext=r2["verified"],
                    verified_last_timed_step=r2["verified_last_step"],
                    gc_reuse=True,
