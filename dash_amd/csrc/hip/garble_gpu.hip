@@ -2832,7 +2832,7 @@ const uint32_t* const* ensure_iR(const gg::Ctx& c, const std::vector<int>& mods)
     return d.iR_dev;
 }
 }  // namespace
-// A free garbling context of the device, locked for the caller: up to DASH_GG_CONTEXTS (default 4) per
+// A free garbling context of the device, locked for the caller: up to DASH_GG_CONTEXTS (default 8) per
 // device, so that many garblings (threads, e.g. the serving engine's refill workers) run on their own streams
 // at once and fill each other's launch gaps and latency stalls; one more waits for the first context.
 std::unique_lock<std::mutex> acquire_ctx(int device, DevCtx*& out) {
@@ -2840,7 +2840,7 @@ std::unique_lock<std::mutex> acquire_ctx(int device, DevCtx*& out) {
     static auto* pools = new std::map<int, std::vector<DevCtx*>>();  // leaked: lives as long as the process
     static const size_t cap = [] {
         const char* e = std::getenv("DASH_GG_CONTEXTS");
-        return static_cast<size_t>(std::max(1, e ? std::atoi(e) : 4));
+        return static_cast<size_t>(std::max(1, e ? std::atoi(e) : 8));  // = the serving engine's 8 refill workers
     }();
     DevCtx* first = nullptr;
     {

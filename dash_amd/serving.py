@@ -238,12 +238,14 @@ class InferenceService:
         self.stats.input_encoding = "device" if self.device_encode else ("host" if backend == "hip" else "labels")
         self.healthy = True
         self.groups = [_Group(g, slots_per_group) for g in range(groups)]
-        # background refill workers: with the GPU garbler four GCs garble at once on four streams of the device
+        # background refill workers: with the GPU garbler eight GCs garble at once on eight streams of the device
         # (garble_gpu.hip DevCtx pool), filling each other's kernel-launch gaps and latency stalls
-        # (served inf/s with 5 % faults, 2 / 3 / 4 workers: 88 / 104 / 110, profiles/r03_serving_workers_*.json)
+        # (served inf/s with 5 % faults, 2 / 3 / 4 workers: 88 / 104 / 110, profiles/r03_serving_workers_*.json;
+        # round 6, bench served phase, 4 / 6 / 8 / 12 / 16 workers: 172-178 / 181-193 / 190-201 / 188-192 /
+        # 188-190, profiles/ab/r6/r06z{c,d}_*.json)
         self.garble_workers = max(1, int(garble_workers if garble_workers is not None else
                                          int(os.environ.get("DASH_GARBLE_WORKERS", "0")) or
-                                         (4 if self.garble_device else 1)))
+                                         (8 if self.garble_device else 1)))
         self._ctr_lock = threading.Lock()
         self._next_group = 0
         self._err: Optional[BaseException] = None
