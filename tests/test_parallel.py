@@ -250,3 +250,18 @@ def test_bench_cli_refuses_missing_gpus():
         pytest.skip("host has 2+ GPUs")
     p = _run_bench_cli(["--gpus", "2", "--steps", "1"], timeout=300)
     assert p.returncode == 2 and "refusing" in p.stderr
+
+
+@pytest.mark.parametrize("pipeline", [0, 1])
+def test_bench_pipelined_groups_verified(pipeline, monkeypatch):
+    """The online loop with two groups, stepped (0) or with each group's next step launched as soon as its outputs
+    are decoded (1): the first and the last timed step both match the plaintext model."""
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        monkeypatch.delenv(k, raising=False)
+    from dash_amd import benchcore
+
+    out = benchcore.run(["--backend", "cpu", "--gpus", "1", "--model", "MODEL_A", "--batch", "4", "--streams", "2",
+                         "--steps", "3", "--warmup", "2", "--phases", "main", "--pipeline", str(pipeline)])
+    assert out["pipelined_steps"] == bool(pipeline)
+    assert out["config"]["streams"] == 2 and out["config"]["global_batch"] == 4
+    assert out["verified_vs_plaintext"] and out["verified_last_timed_step"]
