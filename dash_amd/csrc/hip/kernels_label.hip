@@ -263,11 +263,13 @@ void launch_fetch_res(const FetchRes& a, hipStream_t st) {
 }
 
 // Online message #1 encoded on the device by the garbler (core.h lab_affine per component, reference
-// garbled_circuit_interface.h garble_inputs): grid (ceil(sum_j n_j N / 256), 1, slots), one lane per
-// (residue, component, element) of a slot through the component prefix a.pre, elements fastest (coalesced byte
-// rows of the component-major layout), so no lane idles on a residue narrower than the widest (a grid sized by
-// max_j n_j left 54 % of the MiniONN lanes without work). Both reductions (x mod p, (w + v r) mod p) are a
-// float-reciprocal quotient plus one correction, exact below 2^22; an input beyond that takes the 64-bit path.
+// garbled_circuit_interface.h garble_inputs): grid (ceil(N / 1024), sum_j n_j, slots). A block owns one
+// (slot, residue, component) row, so the residue lookup, the modulus and the offset component are uniform (scalar
+// loads once per wave); each lane encodes 4 consecutive elements with 4-byte loads and stores of the byte rows.
+// The round-6 form (one lane per (residue, component, element), the residue found per lane) issued three dependent
+// round trips per lane for one byte: 333 us per 20-GC MiniONN launch, 599 us per 41 GCs (r06 headline traces).
+// Both reductions (x mod p, (w + v r) mod p) are a float-reciprocal quotient plus one correction, exact below
+// 2^22; an input beyond that takes the 64-bit path.
 __device__ __forceinline__ uint32_t mod_small(int64_t x, uint32_t p, float inv) {
     if (x > -(int64_t(1) << 22) && x < (int64_t(1) << 22)) {
         const int32_t xi = static_cast<int32_t>(x);
@@ -279,21 +281,36 @@ __device__ __forceinline__ uint32_t mod_small(int64_t x, uint32_t p, float inv) 
     const int64_t r = x % static_cast<int64_t>(p);
     return static_cast<uint32_t>(r < 0 ? r + p : r);
 }
+constexpr int kEncPerLane = 4;
 __global__ __launch_bounds__(256) void k_encode_in(EncIn a, const int64_t* __restrict__ x, int64_t N) {
     const int s = blockIdx.z;
-    const uint32_t t = blockIdx.x * 256u + threadIdx.x;
-    const uint32_t N32 = static_cast<uint32_t>(N);
-    const uint32_t ca = t / N32, e = t - ca * N32;  // component across residues, element
-    if (ca >= static_cast<uint32_t>(a.pre[a.k])) return;
+    const int ca = static_cast<int>(blockIdx.y);  // component across residues (uniform)
     int j = 0;
-    while (j + 1 < a.k && static_cast<uint32_t>(a.pre[j + 1]) <= ca) ++j;
-    const uint32_t c = ca - static_cast<uint32_t>(a.pre[j]);
+    while (j + 1 < a.k && a.pre[j + 1] <= ca) ++j;
+    const int c = ca - a.pre[j];
     const uint32_t p = static_cast<uint32_t>(a.p[j]);
     const float inv = a.inv[j];
-    const uint32_t v = mod_small(x[static_cast<int64_t>(s) * N + e], p, inv);
-    const uint32_t w = a.w0[j][s * a.wstride + static_cast<int64_t>(c) * N + e];
     const uint32_t r = a.r[j][s * a.wstride + c];
-    a.out[j][(static_cast<int64_t>(s) * a.n[j] + c) * N + e] = static_cast<act_t>(mod_small(w + v * r, p, inv));
+    const act_t* w = a.w0[j] + s * a.wstride + static_cast<int64_t>(c) * N;
+    act_t* o = a.out[j] + (static_cast<int64_t>(s) * a.n[j] + c) * N;
+    const int64_t* xs = x + static_cast<int64_t>(s) * N;
+    const bool al = ((reinterpret_cast<uintptr_t>(w) | reinterpret_cast<uintptr_t>(o)) & 3u) == 0;
+    const int64_t step = static_cast<int64_t>(gridDim.x) * 256 * kEncPerLane;
+    for (int64_t e = (static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x) * kEncPerLane; e < N; e += step) {
+        if (al && e + kEncPerLane <= N) {
+            const uint32_t w4 = *reinterpret_cast<const uint32_t*>(w + e);
+            uint32_t o4 = 0;
+#pragma unroll
+            for (int u = 0; u < kEncPerLane; ++u) {
+                const uint32_t v = mod_small(xs[e + u], p, inv);
+                o4 |= mod_small(((w4 >> (8 * u)) & 0xffu) + v * r, p, inv) << (8 * u);
+            }
+            *reinterpret_cast<uint32_t*>(o + e) = o4;
+        } else {
+            for (int64_t f = e; f < e + kEncPerLane && f < N; ++f)
+                o[f] = static_cast<act_t>(mod_small(w[f] + mod_small(xs[f], p, inv) * r, p, inv));
+        }
+    }
 }
 void launch_encode_in(const EncIn& a0, const int64_t* x, int64_t N, int slots, hipStream_t st) {
     EncIn a = a0;
@@ -302,9 +319,10 @@ void launch_encode_in(const EncIn& a0, const int64_t* x, int64_t N, int slots, h
         a.pre[j + 1] = a.pre[j] + a.n[j];
         a.inv[j] = 1.0f / static_cast<float>(a.p[j]);
     }
-    const int64_t lanes = static_cast<int64_t>(a.pre[a.k]) * N;
-    if (lanes >= (int64_t(1) << 32)) throw std::runtime_error("encode_in: input too large for 32-bit lane indices");
-    hipLaunchKernelGGL(k_encode_in, dim3(static_cast<unsigned>((lanes + 255) / 256), 1, static_cast<unsigned>(slots)),
+    if (a.pre[a.k] > 65535 || slots > 65535) throw std::runtime_error("encode_in: grid beyond 65535 rows / slots");
+    const int64_t bx = (N + 256 * kEncPerLane - 1) / (256 * kEncPerLane);
+    hipLaunchKernelGGL(k_encode_in, dim3(static_cast<unsigned>(std::min<int64_t>(bx, 4096)),
+                                         static_cast<unsigned>(a.pre[a.k]), static_cast<unsigned>(slots)),
                        dim3(256), 0, st, a, x, N);
 }
 
