@@ -95,9 +95,10 @@ def parse_args(argv=None) -> argparse.Namespace:
     ap.add_argument("--sign", default=None, choices=["fused", "reference"], help="override the sign construction")
     ap.add_argument("--rescale", default=None, choices=["mrs", "legacy"], help="override the rescale construction")
     ap.add_argument("--relu", default=None, choices=["mrs", "approx", "joint"], help="override the ReLU sign")
-    # 4 groups with the steps pipelined: 3082 / 3073 inf/s against 3007 / 3004 with 8 and 2799 / 2813 with 2
-    # (profiles/ab/r6/r06z_*.json); the reference constructions' 10 GB GCs prefer 2 larger groups
-    ap.add_argument("--streams", type=int, default=int(os.environ.get("DASH_BENCH_STREAMS", "4")),
+    # 3 groups with the steps pipelined: 3230 / 3225 / 3240 / 3229 inf/s (165 GCs) against 3065-3085 with 4, 3158-3174
+    # with 5, 3018-3021 with 6, 3004-3007 with 8 and 2799-2813 with 2, with the box's 4 hardware queues or 8
+    # (profiles/ab/r6/r06z{,p,r}_*.json); the reference constructions' 10 GB GCs take 2 groups
+    ap.add_argument("--streams", type=int, default=int(os.environ.get("DASH_BENCH_STREAMS", "3")),
                     help="independent GC groups per GPU, each on its own HIP stream")
     ap.add_argument("--ref-streams", type=int, default=int(os.environ.get("DASH_BENCH_REF_STREAMS", "2")),
                     help="GC groups of the reference-constructions phase")
