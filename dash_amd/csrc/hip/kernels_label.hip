@@ -263,11 +263,12 @@ void launch_fetch_res(const FetchRes& a, hipStream_t st) {
 }
 
 // Online message #1 encoded on the device by the garbler (core.h lab_affine per component, reference
-// garbled_circuit_interface.h garble_inputs): grid (ceil(N / 1024), sum_j n_j, slots). A block owns one
-// (slot, residue, component) row, so the residue lookup, the modulus and the offset component are uniform (scalar
-// loads once per wave); each lane encodes 4 consecutive elements with 4-byte loads and stores of the byte rows.
-// The round-6 form (one lane per (residue, component, element), the residue found per lane) issued three dependent
-// round trips per lane for one byte: 333 us per 20-GC MiniONN launch, 599 us per 41 GCs (r06 headline traces).
+// garbled_circuit_interface.h garble_inputs): grid (ceil(N / 1024), k, slots). A block owns one (slot, residue)
+// and 1024 elements: the modulus is uniform, each lane reduces its 4 inputs mod p once and walks the residue's
+// component rows with 4-byte loads and stores (independent iterations, unrolled). The first round-6 form (one lane
+// per (residue, component, element), the residue found per lane) issued three dependent round trips per lane for
+// one byte: 333 us per 20-GC MiniONN launch, 599 us per 41 GCs; one row per block: 224 us per 41 GCs; this form:
+// 248 us per 55 GCs (r06 headline traces, profiles/r06_headline_b165_kernels_final.txt).
 // Both reductions (x mod p, (w + v r) mod p) are a float-reciprocal quotient plus one correction, exact below
 // 2^22; an input beyond that takes the 64-bit path.
 __device__ __forceinline__ uint32_t mod_small(int64_t x, uint32_t p, float inv) {
@@ -284,31 +285,53 @@ __device__ __forceinline__ uint32_t mod_small(int64_t x, uint32_t p, float inv) 
 constexpr int kEncPerLane = 4;
 __global__ __launch_bounds__(256) void k_encode_in(EncIn a, const int64_t* __restrict__ x, int64_t N) {
     const int s = blockIdx.z;
-    const int ca = static_cast<int>(blockIdx.y);  // component across residues (uniform)
-    int j = 0;
-    while (j + 1 < a.k && a.pre[j + 1] <= ca) ++j;
-    const int c = ca - a.pre[j];
+    const int j = static_cast<int>(blockIdx.y);  // residue (uniform)
+    const int n = a.n[j];
     const uint32_t p = static_cast<uint32_t>(a.p[j]);
     const float inv = a.inv[j];
-    const uint32_t r = a.r[j][s * a.wstride + c];
-    const act_t* w = a.w0[j] + s * a.wstride + static_cast<int64_t>(c) * N;
-    act_t* o = a.out[j] + (static_cast<int64_t>(s) * a.n[j] + c) * N;
+    const act_t* rr = a.r[j] + s * a.wstride;
+    const act_t* w0 = a.w0[j] + s * a.wstride;
+    act_t* o0 = a.out[j] + static_cast<int64_t>(s) * n * N;
     const int64_t* xs = x + static_cast<int64_t>(s) * N;
-    const bool al = ((reinterpret_cast<uintptr_t>(w) | reinterpret_cast<uintptr_t>(o)) & 3u) == 0;
+    // rows of this residue are 4-byte aligned when N is and the slot bases are (uniform)
+    const bool al = N % kEncPerLane == 0 &&
+                    ((reinterpret_cast<uintptr_t>(w0) | reinterpret_cast<uintptr_t>(o0)) & 3u) == 0;
     const int64_t step = static_cast<int64_t>(gridDim.x) * 256 * kEncPerLane;
     for (int64_t e = (static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x) * kEncPerLane; e < N; e += step) {
-        if (al && e + kEncPerLane <= N) {
-            const uint32_t w4 = *reinterpret_cast<const uint32_t*>(w + e);
-            uint32_t o4 = 0;
+        // x mod p once per element, then every component row of the residue
+        uint32_t v[kEncPerLane];
 #pragma unroll
-            for (int u = 0; u < kEncPerLane; ++u) {
-                const uint32_t v = mod_small(xs[e + u], p, inv);
-                o4 |= mod_small(((w4 >> (8 * u)) & 0xffu) + v * r, p, inv) << (8 * u);
+        for (int u = 0; u < kEncPerLane; ++u) v[u] = e + u < N ? mod_small(xs[e + u], p, inv) : 0u;
+        if (al) {
+            // kEncRows rows' loads issued before any of their stores (the output rows may alias the inputs as far
+            // as the compiler knows, so a plain loop made every row one full round trip)
+            constexpr int kEncRows = 8;
+            for (int c0 = 0; c0 < n; c0 += kEncRows) {
+                uint32_t r8[kEncRows], w8[kEncRows];
+#pragma unroll
+                for (int h = 0; h < kEncRows; ++h) {
+                    const int c = min(c0 + h, n - 1);
+                    r8[h] = rr[c];
+                    w8[h] = *reinterpret_cast<const uint32_t*>(w0 + static_cast<int64_t>(c) * N + e);
+                }
+#pragma unroll
+                for (int h = 0; h < kEncRows; ++h) {
+                    if (c0 + h >= n) break;
+                    uint32_t o4 = 0;
+#pragma unroll
+                    for (int u = 0; u < kEncPerLane; ++u)
+                        o4 |= mod_small(((w8[h] >> (8 * u)) & 0xffu) + v[u] * r8[h], p, inv) << (8 * u);
+                    *reinterpret_cast<uint32_t*>(o0 + static_cast<int64_t>(c0 + h) * N + e) = o4;
+                }
             }
-            *reinterpret_cast<uint32_t*>(o + e) = o4;
         } else {
-            for (int64_t f = e; f < e + kEncPerLane && f < N; ++f)
-                o[f] = static_cast<act_t>(mod_small(w[f] + mod_small(xs[f], p, inv) * r, p, inv));
+            for (int c = 0; c < n; ++c) {
+                const uint32_t r = rr[c];
+                for (int u = 0; u < kEncPerLane && e + u < N; ++u) {
+                    const int64_t f = static_cast<int64_t>(c) * N + e + u;
+                    o0[f] = static_cast<act_t>(mod_small(w0[f] + v[u] * r, p, inv));
+                }
+            }
         }
     }
 }
@@ -319,10 +342,10 @@ void launch_encode_in(const EncIn& a0, const int64_t* x, int64_t N, int slots, h
         a.pre[j + 1] = a.pre[j] + a.n[j];
         a.inv[j] = 1.0f / static_cast<float>(a.p[j]);
     }
-    if (a.pre[a.k] > 65535 || slots > 65535) throw std::runtime_error("encode_in: grid beyond 65535 rows / slots");
+    if (slots > 65535) throw std::runtime_error("encode_in: more than 65535 slots in one launch");
     const int64_t bx = (N + 256 * kEncPerLane - 1) / (256 * kEncPerLane);
-    hipLaunchKernelGGL(k_encode_in, dim3(static_cast<unsigned>(std::min<int64_t>(bx, 4096)),
-                                         static_cast<unsigned>(a.pre[a.k]), static_cast<unsigned>(slots)),
+    hipLaunchKernelGGL(k_encode_in, dim3(static_cast<unsigned>(std::min<int64_t>(bx, 4096)), static_cast<unsigned>(a.k),
+                                         static_cast<unsigned>(slots)),
                        dim3(256), 0, st, a, x, N);
 }
 
