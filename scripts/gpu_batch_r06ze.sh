@@ -2,4 +2,4 @@
 # Final tree validation: GPU tests, smoke, per-model garbling, full bench, two-party.
 set -o pipefail
 export TMPDIR=/tmp
-bash scripts/gpu_round.sh r06zs
+bash scripts/gpu_round.sh r06zu
